@@ -1,0 +1,137 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Megatron-DeepSpeed-style GPT-2 345M pre-training throughput.
+
+Config (BASELINE.json config 2 / SURVEY §6): GPT-2 345M (24 x 1024, 16 heads, seq 1024,
+learned positions, tied embeddings, hidden dropout 0.1), micro-batch 4 per GPU, bf16
+compute with fp32 master weights, AdamW + grad clip 1.0, ZeRO-1 over DP = N GPUs
+(weak scaling: global batch = 4 * N sequences).  Synthetic token data and random-init
+weights (no dataset / checkpoint on the box).
+
+    python bench.py --gpus 1 --steps 20 --warmup 5
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        bench.py --gpus 8 --steps 20 --warmup 5
+
+Rank 0 prints exactly one JSON line (value = whole-job tokens/s, max step time over ranks).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="gpt2-345m")
+    ap.add_argument("--micro-batch-size", type=int, default=4)
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--pp", type=int, default=1)
+    ap.add_argument("--no-graph", action="store_true", help="disable hipGraph step capture")
+    ap.add_argument("--no-overlap", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from mxtrain.models.gpt import GPT_CONFIGS, GPTConfig
+    from mxtrain.parallel import state as pstate
+    from mxtrain.training import GPTTrainer, TrainConfig, synthetic_batch
+
+    ps = pstate.initialize_model_parallel(tp=args.tp, pp=args.pp)
+    world = ps.world_size
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    try:
+        torch.backends.cuda.preferred_blas_library("hipblaslt")
+    except Exception:
+        pass
+    cfg = GPTConfig(**GPT_CONFIGS[args.model])
+    tcfg = TrainConfig(micro_batch_size=args.micro_batch_size,
+                       overlap_grad_reduce=not args.no_overlap, lr_warmup_iters=0)
+    tr = GPTTrainer(cfg, tcfg, ps)
+    gen = torch.Generator().manual_seed(1 + ps.dp_rank)
+    tokens, labels = synthetic_batch(cfg, tr.num_micro, args.micro_batch_size, ps.device, gen)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    use_graph = not args.no_graph
+    graph_err = None
+    for _ in range(args.warmup):
+        tr.train_step(tokens, labels)
+    if use_graph:
+        try:
+            tr.capture(tokens, labels, warmup=1)
+        except Exception as e:  # keep the bench alive; report eager numbers instead
+            graph_err = repr(e)[:300]
+            use_graph = False
+            tr._graph = None
+            print(f"graph capture failed, running eager: {graph_err}", file=sys.stderr)
+    for _ in range(2 if use_graph else 0):
+        tr.train_step(tokens, labels)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loss = None
+    for _ in range(args.steps):
+        loss = tr.train_step(tokens, labels)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    ms = (t1 - t0) * 1000.0 / args.steps
+    if world > 1:
+        t = torch.tensor([ms], dtype=torch.float64, device=ps.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+    tokens_per_step = tr.global_batch * cfg.seq_length
+    value = tokens_per_step / (ms / 1000.0)
+    flops = cfg.flops_per_token() * value
+    if ps.rank == 0:
+        out = {
+            "metric": "tokens/sec Megatron-DeepSpeed GPT-2 345M pretrain (DP+ZeRO-1)",
+            "value": round(value, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random tokens, random-init weights)",
+            "config": {
+                "model": args.model,
+                "global_batch": tr.global_batch,
+                "micro_batch": args.micro_batch_size,
+                "seq_len": cfg.seq_length,
+                "parallelism": f"dp{ps.dp}" + (f"_tp{args.tp}" if args.tp > 1 else "")
+                               + (f"_pp{args.pp}" if args.pp > 1 else "") + "_zero1",
+                "hidden_dropout": cfg.hidden_dropout,
+                "attention_dropout": cfg.attention_dropout,
+                "hipgraph": use_graph,
+            },
+            "tflops_per_gpu": round(flops / world / 1e12, 1),
+            "mfu_bf16_dense_2.5pf": round(flops / world / 2.5e15, 4),
+            "loss": round(float(loss.item()), 4) if loss is not None else None,
+        }
+        if graph_err:
+            out["graph_error"] = graph_err
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,623 @@
+// Flash attention forward + backward for gfx950 (CDNA4), bf16 in/out, fp32 softmax.
+//
+// Replaces the Megatron fused `scaled_upper_triang_masked_softmax` + two batched
+// GEMMs (GPT, causal) and the HF BERT padded-softmax attention the reference runs
+// upstream (containers/megatron-deepspeed/Dockerfile:13, examples/accelerate/
+// bert-glue-mrpc/pretrain.yaml:45).  No S x S matrix is ever
+// materialised.
+//
+// Layout: Q/K/V are read in place from the packed QKV projection output
+// ([tokens, 3, heads, D] with a token stride), O is written [tokens, heads, D], so the
+// model needs no transposes.  lse is base-2: lse2 = max*c + log2(sum), c = scale*log2(e).
+//
+// Forward (one workgroup = 4 waves = 128 query rows of one (batch, head); K/V tiles
+// of 64 keys double-buffered in LDS by register staging, T14):
+//   S^T = K * Q^T with v_mfma_f32_32x32x16_bf16 ("swapped" product: the query is on
+//   the lane, so the row max / row sum are lane-local plus one lane^32 exchange);
+//   O^T = V^T * P^T where the P accumulator registers feed the B operand directly
+//   (cdna_hip_programming.md §3 "accumulator tile as the next MFMA's operand") and V^T
+//   fragments come from ds_read_b64_tr_b16 (T10).  O stays query-on-lane, so the
+//   online-softmax rescale is lane-local.
+// Backward (one workgroup = 4 waves = 128 keys; each wave keeps dK^T/dV^T of its 32
+// keys in accumulators while sweeping 32-row query tiles): S and dP are computed
+// key-on-lane with -lse and -delta preloaded into the accumulators, so P and dS are
+// ready-made B operands of dV^T += dO^T P and dK^T += Q^T dS; dS crosses LDS once for
+// dQ = dS K (v_mfma_f32_16x16x32_bf16), which is summed over key blocks with fp32
+// global atomics (MI355X_MICROARCH.md "Global float atomics") and converted once.
+//
+// Every LDS tile uses a 16-B chunk XOR swizzle chosen so that both the row reads
+// (ds_read_b128 of 32 different rows) and the transposed reads (4 consecutive rows x
+// 32 columns per half-wave) are bank-conflict free (derivation in Swz below).
+#include "common.h"
+
+using namespace mx;
+
+namespace {
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+// Chunk swizzle for a [rows][D] bf16 tile (D*2-byte rows, 16-B chunks).
+//  D=64 (128-B rows, two rows per 256-B bank row): f = x ^ ((x&1)<<2), x = (row>>1)&7
+//    - rows {0-3,12-15,20-27} (one ds_read_b128 lane group) map to distinct slots
+//    - rows R..R+3 (R%4==0) read transposed over 4 chunks land in disjoint chunk quads
+//  D=128 (256-B rows): f = ((row&3)<<2) | ((row>>2)&3)
+template <int D>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (D == 64) {
+    int x = (row >> 1) & 7;
+    return x ^ ((x & 1) << 2);
+  } else {
+    return ((row & 3) << 2) | ((row >> 2) & 3);
+  }
+}
+template <int D>
+__device__ __forceinline__ int toff(int row, int chunk) {
+  return row * (D * 2) + ((chunk ^ swz<D>(row)) << 4);
+}
+// Swizzle for the backward K tile, read only transposed by 8 rows {R..R+3, R+8..R+11}
+// x 2 chunks per half-wave (the 16x16x32 B operand of dQ = dS K).
+template <int D>
+__device__ __forceinline__ int toff_k(int row, int chunk) {
+  int f;
+  if constexpr (D == 64) f = (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2);
+  else f = ((row & 3) << 1) | (((row >> 3) & 1) << 3);
+  return row * (D * 2) + ((chunk ^ f) << 4);
+}
+
+__device__ __forceinline__ bf16x4 tr_read(const char* lds, int byte_off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(lds + byte_off));
+}
+__device__ __forceinline__ bf16x8 cat(bf16x4 a, bf16x4 b) {
+  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+__device__ __forceinline__ bf16x8 pack_acc8(const f32x16& acc, int base) {
+  uint4 u;
+  u.x = pack2(acc[base + 0], acc[base + 1]);
+  u.y = pack2(acc[base + 2], acc[base + 3]);
+  u.z = pack2(acc[base + 4], acc[base + 5]);
+  u.w = pack2(acc[base + 6], acc[base + 7]);
+  return __builtin_bit_cast(bf16x8, u);
+}
+__device__ __forceinline__ bf16x8 ld8(const uint16_t* p) {
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p));
+}
+__device__ __forceinline__ bf16x8 lds8(const char* base, int off) {
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + off));
+}
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ============================================================================ forward
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, int ldq, int ldk, int ldv, uint16_t* __restrict__ o,
+    int ldo, float* __restrict__ lse, int S, int Hq, int Hkv, const int* __restrict__ klen,
+    float c /* scale*log2(e) */) {
+  constexpr int BQ = 128, BK = 64, NKK = D / 16, NDT = D / 32;
+  constexpr int TILE = BK * D * 2;           // bytes of one K (or V) tile
+  constexpr int CPR = D / 8;                 // 16-B chunks per row
+  constexpr int CH = BK * CPR / 256;         // chunks per thread per tile
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5, g = lane >> 4, gi = lane & 15;
+  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;  // heavy blocks first
+  const int hq = blockIdx.y, b = blockIdx.z;
+  const int hk = hq / (Hq / Hkv);
+  const int q0 = qb * BQ;
+  const int qw = q0 + 32 * w;
+  const int kl = klen ? klen[b] : S;
+  const int qrow = qw + r;
+
+  bf16x8 qf[NKK];
+  {
+    const uint16_t* qp = q + (size_t)(b * S + qrow) * ldq + hq * D + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk)
+      qf[kk] = qrow < S ? ld8(qp + 16 * kk) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  int kv_end = kl;
+  if (CAUSAL) kv_end = min(kv_end, min(S, q0 + BQ));
+  const int nt = (kv_end + BK - 1) / BK;
+
+  const uint16_t* kbase = k + (size_t)b * S * ldk + hk * D;
+  const uint16_t* vbase = v + (size_t)b * S * ldv + hk * D;
+  uint4 kreg[CH], vreg[CH];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int ci = tid + 256 * i, row = ci / CPR, ch = ci % CPR, key = t * BK + row;
+      if (key < S) {
+        kreg[i] = *reinterpret_cast<const uint4*>(kbase + (size_t)key * ldk + ch * 8);
+        vreg[i] = *reinterpret_cast<const uint4*>(vbase + (size_t)key * ldv + ch * 8);
+      } else {
+        kreg[i] = make_uint4(0, 0, 0, 0);
+        vreg[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto swrite = [&](int buf) {
+    char* kt = smem + buf * 2 * TILE;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int ci = tid + 256 * i, row = ci / CPR, ch = ci % CPR;
+      *reinterpret_cast<uint4*>(kt + toff<D>(row, ch)) = kreg[i];
+      *reinterpret_cast<uint4*>(kt + TILE + toff<D>(row, ch)) = vreg[i];
+    }
+  };
+
+  float m_i = -INFINITY, l_i = 0.f;
+  f32x16 oacc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) oacc[dt] = f32x16{};
+
+  if (nt > 0) {
+    gload(0);
+    swrite(0);
+  }
+  __syncthreads();
+  for (int j = 0; j < nt; ++j) {
+    if (j + 1 < nt) gload(j + 1);
+    const char* Kt = smem + (j & 1) * 2 * TILE;
+    const char* Vt = Kt + TILE;
+    const int kv0 = j * BK;
+    const bool active = !CAUSAL || kv0 <= qw + 31;
+    if (active) {
+      f32x16 sacc[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        sacc[t] = f32x16{};
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk)
+          sacc[t] = mfma32(lds8(Kt, toff<D>(32 * t + r, 2 * kk + hh)), qf[kk], sacc[t]);
+      }
+      const bool need_mask = (CAUSAL && kv0 + BK - 1 > qw) || (kv0 + BK > kl);
+      if (need_mask) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int key = kv0 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * hh;
+            if (key >= kl || (CAUSAL && key > qrow)) sacc[t][e] = -INFINITY;
+          }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sacc[t][e]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_i, mx);
+      float alpha = 1.f, mc = 0.f;
+      if (m_new != -INFINITY) {
+        alpha = __builtin_amdgcn_exp2f((m_i - m_new) * c);
+        mc = m_new * c;
+      }
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float p = __builtin_amdgcn_exp2f(sacc[t][e] * c - mc);
+          sacc[t][e] = p;
+          rs += p;
+        }
+      l_i = l_i * alpha + rs;
+      m_i = m_new;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) oacc[dt][e] *= alpha;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 pb = pack_acc8(sacc[t], 8 * s);
+          const int row0 = 32 * t + 16 * s + 4 * hh + (gi >> 2);
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) {
+            const int col = 32 * dt + 16 * (g & 1) + 4 * (gi & 3);
+            const int within = (col & 7) * 2;
+            const bf16x4 lo = tr_read(Vt, toff<D>(row0, col >> 3) + within);
+            const bf16x4 hi = tr_read(Vt, toff<D>(row0 + 8, col >> 3) + within);
+            oacc[dt] = mfma32(cat(lo, hi), pb, oacc[dt]);
+          }
+        }
+    }
+    if (j + 1 < nt) swrite((j + 1) & 1);
+    __syncthreads();
+  }
+
+  const float lt = l_i + __shfl_xor(l_i, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (qrow < S) {
+    uint16_t* op = o + (size_t)(b * S + qrow) * ldo + hq * D;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * dt + 8 * g4 + 4 * hh;
+        uint2 u;
+        u.x = pack2(oacc[dt][4 * g4 + 0] * inv, oacc[dt][4 * g4 + 1] * inv);
+        u.y = pack2(oacc[dt][4 * g4 + 2] * inv, oacc[dt][4 * g4 + 3] * inv);
+        *reinterpret_cast<uint2*>(op + d) = u;
+      }
+    if (hh == 0)
+      lse[((size_t)b * Hq + hq) * S + qrow] = lt > 0.f ? m_i * c + __log2f(lt) : INFINITY;
+  }
+}
+
+// ============================================================================ backward
+// delta[b,h,q] = sum_d dO*O  (fp32)
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(
+    const uint16_t* __restrict__ o, int ldo, const uint16_t* __restrict__ dout, int lddo,
+    float* __restrict__ delta, int B, int S, int Hq) {
+  constexpr int LPR = D / 8;  // lanes per (token, head) row
+  const int gid = (blockIdx.x * 256 + threadIdx.x);
+  const int row = gid / LPR, sub = gid % LPR;  // row = (b*S + s)*Hq + h
+  const int nrows = B * S * Hq;
+  float acc = 0.f;
+  if (row < nrows) {
+    const int h = row % Hq, tok = row / Hq;
+    float a[8], bb[8];
+    unpack8(*reinterpret_cast<const uint4*>(o + (size_t)tok * ldo + h * D + sub * 8), a);
+    unpack8(*reinterpret_cast<const uint4*>(dout + (size_t)tok * lddo + h * D + sub * 8), bb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += a[j] * bb[j];
+  }
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (row < nrows && sub == 0) {
+    const int h = row % Hq, tok = row / Hq, bi = tok / S, s = tok % S;
+    delta[((size_t)bi * Hq + h) * S + s] = acc;
+  }
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_bwd_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, int ldq, int ldk, int ldv,
+    const uint16_t* __restrict__ dout, int lddo, const float* __restrict__ lse,
+    const float* __restrict__ delta, float* __restrict__ dq_acc, int lddq,
+    uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, int lddk, int lddv, int S, int Hq,
+    int Hkv, const int* __restrict__ klen, float c, float scale) {
+  constexpr int KB = 128, QT = 32, NKK = D / 16, NDT = D / 32;
+  constexpr int KTILE = KB * D * 2;  // bytes
+  constexpr int QTILE = QT * D * 2;
+  constexpr int CPR = D / 8;
+  constexpr int QCH = QT * CPR / 256;  // chunks per thread for a Q (or dO) tile: 1 or 2
+  constexpr int KCH = KB * CPR / 256;
+  // LDS carve (one array, 16-B aligned offsets)
+  constexpr int OFF_K = 0;
+  constexpr int OFF_Q = OFF_K + KTILE;            // [2][QTILE]
+  constexpr int OFF_DO = OFF_Q + 2 * QTILE;       // [2][QTILE]
+  constexpr int OFF_DS = OFF_DO + 2 * QTILE;      // [KB keys][QT q] bf16, 64-B rows
+  constexpr int OFF_L = OFF_DS + KB * QT * 2;     // [2][QT] float  (-lse2/c)
+  constexpr int OFF_DL = OFF_L + 2 * QT * 4;      // [2][QT] float  (-delta)
+  constexpr int LDS_BYTES = OFF_DL + 2 * QT * 4;
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5, g = lane >> 4, gi = lane & 15;
+  const int k0 = blockIdx.x * KB;
+  const int hk = blockIdx.y, b = blockIdx.z;
+  const int grp = Hq / Hkv;
+  const int kl = klen ? klen[b] : S;
+  const int key = k0 + 32 * w + r;  // this lane's key (column of S / dP)
+
+  // K and V fragments of the wave's 32 keys (B operands of S = Q K^T, dP = dO V^T)
+  bf16x8 kf[NKK], vf[NKK];
+  {
+    const uint16_t* kp = k + (size_t)(b * S + key) * ldk + hk * D + 8 * hh;
+    const uint16_t* vp = v + (size_t)(b * S + key) * ldv + hk * D + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      kf[kk] = key < S ? ld8(kp + 16 * kk) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      vf[kk] = key < S ? ld8(vp + 16 * kk) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  // K tile of the whole block in LDS (transposed reads for dQ)
+#pragma unroll
+  for (int i = 0; i < KCH; ++i) {
+    const int ci = tid + 256 * i, row = ci / CPR, ch = ci % CPR, kk = k0 + row;
+    uint4 val = make_uint4(0, 0, 0, 0);
+    if (kk < S) val = *reinterpret_cast<const uint4*>(k + (size_t)(b * S + kk) * ldk + hk * D + ch * 8);
+    *reinterpret_cast<uint4*>(smem + OFF_K + toff_k<D>(row, ch)) = val;
+  }
+
+  f32x16 dvacc[NDT], dkacc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) { dvacc[dt] = f32x16{}; dkacc[dt] = f32x16{}; }
+
+  const int nqt = (S + QT - 1) / QT;
+  const int qt0 = CAUSAL ? (k0 / QT) : 0;
+  const int per_head = nqt - qt0;
+  const int total = per_head * grp;
+
+  uint4 qreg[QCH], dreg[QCH];
+  float lreg = 0.f, dlreg = 0.f;
+  auto gload = [&](int it) {
+    const int hq = hk * grp + it / per_head;
+    const int qs = (qt0 + it % per_head) * QT;
+#pragma unroll
+    for (int i = 0; i < QCH; ++i) {
+      const int ci = tid + 256 * i, row = ci / CPR, ch = ci % CPR, qq = qs + row;
+      if (qq < S) {
+        qreg[i] = *reinterpret_cast<const uint4*>(q + (size_t)(b * S + qq) * ldq + hq * D + ch * 8);
+        dreg[i] = *reinterpret_cast<const uint4*>(dout + (size_t)(b * S + qq) * lddo + hq * D + ch * 8);
+      } else {
+        qreg[i] = make_uint4(0, 0, 0, 0);
+        dreg[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+    if (tid < QT) {
+      const int qq = qs + tid;
+      const size_t li = ((size_t)b * Hq + hq) * S + qq;
+      lreg = qq < S ? -lse[li] / c : -INFINITY;
+      dlreg = qq < S ? -delta[li] : 0.f;
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < QCH; ++i) {
+      const int ci = tid + 256 * i, row = ci / CPR, ch = ci % CPR;
+      *reinterpret_cast<uint4*>(smem + OFF_Q + buf * QTILE + toff<D>(row, ch)) = qreg[i];
+      *reinterpret_cast<uint4*>(smem + OFF_DO + buf * QTILE + toff<D>(row, ch)) = dreg[i];
+    }
+    if (tid < QT) {
+      reinterpret_cast<float*>(smem + OFF_L)[buf * QT + tid] = lreg;
+      reinterpret_cast<float*>(smem + OFF_DL)[buf * QT + tid] = dlreg;
+    }
+  };
+
+  if (total > 0) {
+    gload(0);
+    swrite(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    const int hq = hk * grp + it / per_head;
+    const int qs = (qt0 + it % per_head) * QT;
+    if (it + 1 < total) gload(it + 1);
+    const int buf = it & 1;
+    const char* Qt = smem + OFF_Q + buf * QTILE;
+    const char* Ot = smem + OFF_DO + buf * QTILE;
+    const float* Ls = reinterpret_cast<const float*>(smem + OFF_L) + buf * QT;
+    const float* DLs = reinterpret_cast<const float*>(smem + OFF_DL) + buf * QT;
+    char* dsimg = smem + OFF_DS;
+    const bool active = !CAUSAL || (qs + QT - 1 >= k0 + 32 * w);
+    if (active) {
+      f32x16 sacc, dpacc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int ql = (e & 3) + 8 * (e >> 2) + 4 * hh;
+        sacc[e] = Ls[ql];
+        dpacc[e] = DLs[ql];
+      }
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        sacc = mfma32(lds8(Qt, toff<D>(r, 2 * kk + hh)), kf[kk], sacc);
+        dpacc = mfma32(lds8(Ot, toff<D>(r, 2 * kk + hh)), vf[kk], dpacc);
+      }
+      // P = exp2(c*(S - lse2/c)); dS = P * (dP - delta)
+      const bool key_ok = key < kl;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int qq = qs + (e & 3) + 8 * (e >> 2) + 4 * hh;
+        float p = __builtin_amdgcn_exp2f(c * sacc[e]);
+        if (!key_ok || (CAUSAL && key > qq)) p = 0.f;
+        sacc[e] = p;
+        dpacc[e] = p * dpacc[e];
+      }
+      // dV^T += dO^T P ;  dK^T += Q^T dS   (A operands by transposed reads)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pb = pack_acc8(sacc, 8 * s);
+        const bf16x8 db = pack_acc8(dpacc, 8 * s);
+        const int row0 = 16 * s + 4 * hh + (gi >> 2);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const int col = 32 * dt + 16 * (g & 1) + 4 * (gi & 3);
+          const int within = (col & 7) * 2;
+          const bf16x8 dot = cat(tr_read(Ot, toff<D>(row0, col >> 3) + within),
+                                 tr_read(Ot, toff<D>(row0 + 8, col >> 3) + within));
+          dvacc[dt] = mfma32(dot, pb, dvacc[dt]);
+          const bf16x8 qtr = cat(tr_read(Qt, toff<D>(row0, col >> 3) + within),
+                                 tr_read(Qt, toff<D>(row0 + 8, col >> 3) + within));
+          dkacc[dt] = mfma32(qtr, db, dkacc[dt]);
+        }
+      }
+      // dS^T image [key][q] (64-B rows, 32-B half swap on key bit 3)
+      const int krow = 32 * w + r;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int ql = 8 * g4 + 4 * hh;
+        uint2 u;
+        u.x = pack2(dpacc[4 * g4 + 0], dpacc[4 * g4 + 1]);
+        u.y = pack2(dpacc[4 * g4 + 2], dpacc[4 * g4 + 3]);
+        *reinterpret_cast<uint2*>(dsimg + krow * 64 + ((ql * 2) ^ (((krow >> 3) & 1) << 5))) = u;
+      }
+    } else {
+      const int krow = 32 * w + r;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int ql = 8 * g4 + 4 * hh;
+        *reinterpret_cast<uint2*>(dsimg + krow * 64 + ((ql * 2) ^ (((krow >> 3) & 1) << 5))) =
+            make_uint2(0, 0);
+      }
+    }
+    __syncthreads();
+    // dQ[q][d] += dS[q][key] K[key][d] over the block's 128 keys (16x16x32 tiles)
+    {
+      constexpr int DTW = D / 32;  // 16-wide d tiles per wave
+      const int qtile = w & 1;
+      f32x4 dq[DTW];
+#pragma unroll
+      for (int i = 0; i < DTW; ++i) dq[i] = f32x4{};
+#pragma unroll
+      for (int ks = 0; ks < KB / 32; ++ks) {
+        const int krow = 32 * ks + 8 * g + (gi >> 2);
+        const int qcol = 16 * qtile + 4 * (gi & 3);
+        const int sw0 = ((krow >> 3) & 1) << 5, sw1 = (((krow + 4) >> 3) & 1) << 5;
+        const bf16x8 a = cat(tr_read(dsimg, krow * 64 + ((qcol * 2) ^ sw0)),
+                             tr_read(dsimg, (krow + 4) * 64 + ((qcol * 2) ^ sw1)));
+#pragma unroll
+        for (int i = 0; i < DTW; ++i) {
+          const int dtile = (w >> 1) * DTW + i;
+          const int dcol = 16 * dtile + 4 * (gi & 3);
+          const int within = (dcol & 7) * 2;
+          const bf16x8 bk = cat(tr_read(smem + OFF_K, toff_k<D>(krow, dcol >> 3) + within),
+                                tr_read(smem + OFF_K, toff_k<D>(krow + 4, dcol >> 3) + within));
+          dq[i] = mfma16(a, bk, dq[i]);
+        }
+      }
+      // C layout 16x16: col = lane&15 (d), row = (lane>>4)*4 + e (q)
+#pragma unroll
+      for (int i = 0; i < DTW; ++i) {
+        const int dtile = (w >> 1) * DTW + i;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int qq = qs + 16 * qtile + 4 * g + e;
+          if (qq < S)
+            atomicAdd(dq_acc + (size_t)(b * S + qq) * lddq + hq * D + 16 * dtile + gi, dq[i][e]);
+        }
+      }
+    }
+    if (it + 1 < total) swrite((it + 1) & 1);
+    __syncthreads();
+  }
+  // write dK (scaled) and dV for this lane's key: rows d = 32dt + 8g4 + 4hh + 0..3
+  if (key < S) {
+    uint16_t* dkp = dk + (size_t)(b * S + key) * lddk + hk * D;
+    uint16_t* dvp = dv + (size_t)(b * S + key) * lddv + hk * D;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * dt + 8 * g4 + 4 * hh;
+        uint2 u;
+        u.x = pack2(dkacc[dt][4 * g4 + 0] * scale, dkacc[dt][4 * g4 + 1] * scale);
+        u.y = pack2(dkacc[dt][4 * g4 + 2] * scale, dkacc[dt][4 * g4 + 3] * scale);
+        *reinterpret_cast<uint2*>(dkp + d) = u;
+        u.x = pack2(dvacc[dt][4 * g4 + 0], dvacc[dt][4 * g4 + 1]);
+        u.y = pack2(dvacc[dt][4 * g4 + 2], dvacc[dt][4 * g4 + 3]);
+        *reinterpret_cast<uint2*>(dvp + d) = u;
+      }
+  }
+}
+
+// dq (bf16, strided into the packed dqkv) = dq_acc * scale
+__global__ __launch_bounds__(256) void dq_convert_kernel(const float* __restrict__ acc,
+                                                         int ldacc, uint16_t* __restrict__ dq,
+                                                         int lddq, int ntok, int width,
+                                                         float scale) {
+  const int64_t v = blockIdx.x * 256ll + threadIdx.x;
+  const int per_row = width / 8;
+  if (v >= (int64_t)ntok * per_row) return;
+  const int t = (int)(v / per_row), c = (int)(v % per_row) * 8;
+  const float4 a = *reinterpret_cast<const float4*>(acc + (size_t)t * ldacc + c);
+  const float4 bq = *reinterpret_cast<const float4*>(acc + (size_t)t * ldacc + c + 4);
+  float f[8] = {a.x * scale, a.y * scale, a.z * scale, a.w * scale,
+                bq.x * scale, bq.y * scale, bq.z * scale, bq.w * scale};
+  *reinterpret_cast<uint4*>(dq + (size_t)t * lddq + c) = pack8(f);
+}
+
+template <int D>
+hipError_t fwd_dispatch(bool causal, dim3 grid, hipStream_t s, const uint16_t* q,
+                        const uint16_t* k, const uint16_t* v, int ldq, int ldk, int ldv,
+                        uint16_t* o, int ldo, float* lse, int S, int Hq, int Hkv,
+                        const int* klen, float c) {
+  if (causal)
+    hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(256), 0, s, q, k, v, ldq, ldk,
+                       ldv, o, ldo, lse, S, Hq, Hkv, klen, c);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), 0, s, q, k, v, ldq, ldk,
+                       ldv, o, ldo, lse, S, Hq, Hkv, klen, c);
+  return hipGetLastError();
+}
+
+template <int D>
+hipError_t bwd_dispatch(bool causal, dim3 grid, hipStream_t s, const uint16_t* q,
+                        const uint16_t* k, const uint16_t* v, int ldq, int ldk, int ldv,
+                        const uint16_t* dout, int lddo, const float* lse, const float* delta,
+                        float* dq_acc, int lddq, uint16_t* dk, uint16_t* dv, int lddk, int lddv,
+                        int S, int Hq, int Hkv, const int* klen, float c, float scale) {
+  if (causal)
+    hipLaunchKernelGGL((attn_bwd_kernel<D, true>), grid, dim3(256), 0, s, q, k, v, ldq, ldk,
+                       ldv, dout, lddo, lse, delta, dq_acc, lddq, dk, dv, lddk, lddv, S, Hq, Hkv,
+                       klen, c, scale);
+  else
+    hipLaunchKernelGGL((attn_bwd_kernel<D, false>), grid, dim3(256), 0, s, q, k, v, ldq, ldk,
+                       ldv, dout, lddo, lse, delta, dq_acc, lddq, dk, dv, lddk, lddv, S, Hq, Hkv,
+                       klen, c, scale);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// Q/K/V/O are bf16 with token strides ld*; head h lives at column h*D.
+// lse: fp32 [B, Hq, S] (base 2).  klen: int32 [B] valid key count or null.
+MX_EXPORT int mx_attn_fwd(const void* q, const void* k, const void* v, int ldq, int ldk,
+                          int ldv, void* o, int ldo, float* lse, int B, int S, int Hq, int Hkv,
+                          int D, int causal, const int* klen, float scale, hipStream_t s) {
+  if (Hq % Hkv) return hipErrorInvalidValue;
+  const float c = scale * 1.4426950408889634f;
+  dim3 grid((S + 127) / 128, Hq, B);
+  if (D == 64)
+    return fwd_dispatch<64>(causal, grid, s, (const uint16_t*)q, (const uint16_t*)k,
+                            (const uint16_t*)v, ldq, ldk, ldv, (uint16_t*)o, ldo, lse, S, Hq,
+                            Hkv, klen, c);
+  if (D == 128)
+    return fwd_dispatch<128>(causal, grid, s, (const uint16_t*)q, (const uint16_t*)k,
+                             (const uint16_t*)v, ldq, ldk, ldv, (uint16_t*)o, ldo, lse, S, Hq,
+                             Hkv, klen, c);
+  return hipErrorInvalidValue;
+}
+
+// dq_acc: fp32 [B*S, Hq*D] zero-initialised workspace; delta: fp32 [B, Hq, S] workspace.
+MX_EXPORT int mx_attn_bwd(const void* q, const void* k, const void* v, int ldq, int ldk,
+                          int ldv, const void* o, int ldo, const void* dout, int lddo,
+                          const float* lse, float* delta, float* dq_acc, void* dq, int lddq,
+                          void* dk, void* dv, int lddk, int lddv, int B, int S, int Hq,
+                          int Hkv, int D, int causal, const int* klen, float scale,
+                          hipStream_t s) {
+  if (Hq % Hkv) return hipErrorInvalidValue;
+  const float c = scale * 1.4426950408889634f;
+  {
+    const int64_t threads = (int64_t)B * S * Hq * (D / 8);
+    if (D == 64)
+      hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, dim3((unsigned)((threads + 255) / 256)),
+                         dim3(256), 0, s, (const uint16_t*)o, ldo, (const uint16_t*)dout, lddo,
+                         delta, B, S, Hq);
+    else if (D == 128)
+      hipLaunchKernelGGL(attn_bwd_pre_kernel<128>, dim3((unsigned)((threads + 255) / 256)),
+                         dim3(256), 0, s, (const uint16_t*)o, ldo, (const uint16_t*)dout, lddo,
+                         delta, B, S, Hq);
+    else
+      return hipErrorInvalidValue;
+  }
+  dim3 grid((S + 127) / 128, Hkv, B);
+  const int lddq_acc = Hq * D;
+  hipError_t e;
+  if (D == 64)
+    e = bwd_dispatch<64>(causal, grid, s, (const uint16_t*)q, (const uint16_t*)k,
+                         (const uint16_t*)v, ldq, ldk, ldv, (const uint16_t*)dout, lddo, lse,
+                         delta, dq_acc, lddq_acc, (uint16_t*)dk, (uint16_t*)dv, lddk, lddv, S,
+                         Hq, Hkv, klen, c, scale);
+  else
+    e = bwd_dispatch<128>(causal, grid, s, (const uint16_t*)q, (const uint16_t*)k,
+                          (const uint16_t*)v, ldq, ldk, ldv, (const uint16_t*)dout, lddo, lse,
+                          delta, dq_acc, lddq_acc, (uint16_t*)dk, (uint16_t*)dv, lddk, lddv, S,
+                          Hq, Hkv, klen, c, scale);
+  if (e != hipSuccess) return e;
+  const int64_t nv = (int64_t)B * S * Hq * D / 8;
+  hipLaunchKernelGGL(dq_convert_kernel, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s,
+                     dq_acc, lddq_acc, (uint16_t*)dq, lddq, B * S, Hq * D, scale);
+  return hipGetLastError();
+}

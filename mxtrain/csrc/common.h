@@ -1,0 +1,101 @@
+// mxtrain HIP kernel library -- shared device helpers (gfx950 / CDNA4 only).
+//
+// Every kernel in csrc/ is exported through a plain C ABI (`extern "C" int mx_*`)
+// that takes raw device pointers plus the caller's hipStream_t, and returns the
+// hipError_t of the launch.  Python binds these with ctypes (mxtrain/ops/_lib.py);
+// there is no torch C++ header in the kernel build, which keeps compiles at a
+// few seconds per file and lets the same .so serve the C++ runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MX_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace mx {
+
+constexpr int kWave = 64;  // CDNA wavefront width (never 32)
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;    // 8 x bf16 = 4 VGPRs
+typedef __attribute__((ext_vector_type(4))) short bf16x4;    // 4 x bf16 = 2 VGPRs
+typedef __attribute__((ext_vector_type(16))) float f32x16;   // 32x32 MFMA accumulator
+typedef __attribute__((ext_vector_type(4))) float f32x4;     // 16x16 MFMA accumulator
+
+__device__ __forceinline__ float bf2f(uint16_t u) {
+  return __uint_as_float(((uint32_t)u) << 16);
+}
+// round-to-nearest-even; hipcc lowers this to v_cvt_pk_bf16_f32 on gfx950 (NaN stays NaN)
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+__device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// unpack 8 bf16 held in a uint4 (16 B) into floats
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  f[0] = lo_bf(v.x); f[1] = hi_bf(v.x);
+  f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
+  f[4] = lo_bf(v.z); f[5] = hi_bf(v.z);
+  f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack2(f[0], f[1]); v.y = pack2(f[2], f[3]);
+  v.z = pack2(f[4], f[5]); v.w = pack2(f[6], f[7]);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Counter-based RNG for dropout: a stateless 32-bit hash of (seed, element index).
+// The mask is regenerated bit-exactly in backward from the same (seed, offset), so
+// nothing but the seed is saved between forward and backward.
+__device__ __forceinline__ uint32_t hash32(uint32_t x, uint32_t seed) {
+  x ^= seed * 0x9E3779B9u;
+  x ^= x >> 16; x *= 0x7feb352du;
+  x ^= x >> 15; x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+// keep-probability test: returns true when the element is kept
+__device__ __forceinline__ bool dropout_keep(uint64_t idx, uint32_t seed, uint32_t thresh) {
+  uint32_t h = hash32((uint32_t)idx ^ (uint32_t)(idx >> 32) * 0x85ebca6bu, seed);
+  return h >= thresh;  // thresh = p * 2^32
+}
+
+// tanh-approximation GeLU (Megatron bias_gelu / HF "gelu_new")
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * x * (1.f + k1 * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float x2 = x * x;
+  float u = k0 * x * (1.f + k1 * x2);
+  float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+}
+
+// bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5 "XCD swizzle
+// must be bijective"): blocks that share an XCD (orig % 8) get contiguous logical ids.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int nx = 8;
+  int q = nwg / nx, r = nwg % nx, x = orig % nx;
+  int base = (x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return base + orig / nx;
+}
+
+}  // namespace mx

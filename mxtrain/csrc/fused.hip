@@ -1,0 +1,314 @@
+// Fused elementwise / reduction kernels of the GPT / BERT training step:
+//   * bias + GeLU (tanh) forward and backward with fused dbias column reduction   (K6)
+//   * token + position embedding gather, deterministic embedding backward          (K11)
+//   * softmax cross-entropy: row statistics + gradient, vocab-parallel capable     (K10)
+// Replaces Megatron `bias_gelu_impl`, `VocabParallelEmbedding` and
+// `vocab_parallel_cross_entropy` (reference pins: containers/megatron-deepspeed/
+// Dockerfile:13).  All bf16 traffic is 16-B vectorised.
+#include "common.h"
+
+using namespace mx;
+
+namespace {
+
+// ---------------------------------------------------------------- bias + GeLU
+__global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ bias,
+    uint16_t* __restrict__ y, int64_t n, int cols) {
+  const int64_t nvec = n / 8;
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nvec;
+       v += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)((v * 8) % cols);
+    float a[8], b[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + v * 8), a);
+    unpack8(*reinterpret_cast<const uint4*>(bias + c), b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = gelu_tanh(a[j] + b[j]);
+    *reinterpret_cast<uint4*>(y + v * 8) = pack8(o);
+  }
+}
+
+// dx = dy * gelu'(x + b); partial[blockIdx.y][c] = sum over the block's rows of dx
+__global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+    const uint16_t* __restrict__ bias, uint16_t* __restrict__ dx, int rows, int cols,
+    int rows_per_block, float* __restrict__ partial) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= cols) return;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  float b[8], acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unpack8(*reinterpret_cast<const uint4*>(bias + c), b);
+  for (int r = r0; r < r1; ++r) {
+    const size_t off = (size_t)r * cols + c;
+    float g[8], a[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(dy + off), g);
+    unpack8(*reinterpret_cast<const uint4*>(x + off), a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = g[j] * gelu_tanh_grad(a[j] + b[j]);
+    uint4 pk = pack8(o);
+    *reinterpret_cast<uint4*>(dx + off) = pk;
+    unpack8(pk, o);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += o[j];
+  }
+  float* p = partial + (size_t)blockIdx.y * cols + c;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) p[j] = acc[j];
+}
+
+__global__ __launch_bounds__(256) void colsum_fold_kernel(const float* __restrict__ partial,
+                                                          int nparts, int cols,
+                                                          uint16_t* __restrict__ out,
+                                                          int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int b = 0; b < nparts; ++b) s += partial[(size_t)b * cols + c];
+  if (accumulate) s += bf2f(out[c]);
+  out[c] = f2bf(s);
+}
+
+// ---------------------------------------------------------------- embedding
+// out[t] = wte[ids[t] - vocab_start] (+ wpe[t % seq]); rows outside the local vocab
+// shard are zero (vocab-parallel embedding; the TP all-reduce sums the shards).
+__global__ __launch_bounds__(256) void embed_fwd_kernel(
+    const int64_t* __restrict__ ids, const uint16_t* __restrict__ wte,
+    const uint16_t* __restrict__ wpe, uint16_t* __restrict__ out, int ntok, int hidden,
+    int seq, int64_t vocab_start, int64_t vocab_end, int pos_offset) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= ntok) return;
+  const int64_t id = ids[t];
+  const bool in = id >= vocab_start && id < vocab_end;
+  const int pos = (t % seq) + pos_offset;
+  for (int c = lane * 8; c < hidden; c += 512) {
+    float a[8], p[8];
+    if (in) unpack8(*reinterpret_cast<const uint4*>(wte + (id - vocab_start) * hidden + c), a);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = 0.f;
+    }
+    if (wpe) {
+      unpack8(*reinterpret_cast<const uint4*>(wpe + (size_t)pos * hidden + c), p);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += p[j];
+    }
+    *reinterpret_cast<uint4*>(out + (size_t)t * hidden + c) = pack8(a);
+  }
+}
+
+// Deterministic scatter-add: ids sorted (sorted_ids, perm = original positions).
+// The first block of each run of equal ids sums the run's rows in fp32 and adds the
+// result to dW[id] once -- no atomics, bitwise reproducible.
+__global__ __launch_bounds__(128) void embed_bwd_kernel(
+    const int64_t* __restrict__ sorted_ids, const int64_t* __restrict__ perm,
+    const uint16_t* __restrict__ dout, uint16_t* __restrict__ dw, int ntok, int hidden,
+    int64_t vocab_start, int64_t vocab_end) {
+  const int i = blockIdx.x;
+  const int64_t id = sorted_ids[i];
+  if (i > 0 && sorted_ids[i - 1] == id) return;
+  if (id < vocab_start || id >= vocab_end) return;
+  int end = i + 1;
+  while (end < ntok && sorted_ids[end] == id) ++end;
+  for (int c = threadIdx.x * 8; c < hidden; c += 128 * 8) {
+    float acc[8];
+    unpack8(*reinterpret_cast<const uint4*>(dw + (id - vocab_start) * hidden + c), acc);
+    for (int k = i; k < end; ++k) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(dout + perm[k] * hidden + c), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+    *reinterpret_cast<uint4*>(dw + (id - vocab_start) * hidden + c) = pack8(acc);
+  }
+}
+
+// dwpe[s] += sum_b dout[b*seq + s]
+__global__ __launch_bounds__(256) void pos_bwd_kernel(const uint16_t* __restrict__ dout,
+                                                      uint16_t* __restrict__ dwpe, int batch,
+                                                      int seq, int hidden) {
+  const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t nvec = (int64_t)seq * hidden / 8;
+  if (v >= nvec) return;
+  float acc[8];
+  unpack8(*reinterpret_cast<const uint4*>(dwpe + v * 8), acc);
+  for (int b = 0; b < batch; ++b) {
+    float x[8];
+    unpack8(*reinterpret_cast<const uint4*>(dout + ((size_t)b * seq * hidden) + v * 8), x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += x[j];
+  }
+  *reinterpret_cast<uint4*>(dwpe + v * 8) = pack8(acc);
+}
+
+// ---------------------------------------------------------------- cross entropy
+// Pass 1: per row (max, sum exp(x - max), x[label] if label in this shard).
+__global__ __launch_bounds__(256) void ce_stats_kernel(
+    const uint16_t* __restrict__ logits, const int64_t* __restrict__ labels, int rows,
+    int vocab, int64_t vocab_start, float* __restrict__ row_max, float* __restrict__ row_sum,
+    float* __restrict__ row_tgt) {
+  __shared__ float sm[8], ss[8];
+  const int row = blockIdx.x;
+  const uint16_t* x = logits + (size_t)row * vocab;
+  float m = -INFINITY, s = 0.f;
+  const int nvec = vocab / 8;
+  for (int v = threadIdx.x; v < nvec; v += 256) {
+    float a[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + v * 8), a);
+    float lm = a[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) lm = fmaxf(lm, a[j]);
+    if (lm > m) { s *= __expf(m - lm); m = lm; }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += __expf(a[j] - m);
+  }
+  for (int c = nvec * 8 + threadIdx.x; c < vocab; c += 256) {  // tail
+    float a = bf2f(x[c]);
+    if (a > m) { s *= __expf(m - a); m = a; }
+    s += __expf(a - m);
+  }
+  // wave combine (m, s)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sm[w] = m; ss[w] = s; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0], S = ss[0];
+    for (int k = 1; k < 4; ++k) {
+      float nm = fmaxf(M, sm[k]);
+      S = (M == -INFINITY ? 0.f : S * __expf(M - nm)) +
+          (sm[k] == -INFINITY ? 0.f : ss[k] * __expf(sm[k] - nm));
+      M = nm;
+    }
+    row_max[row] = M;
+    row_sum[row] = S;
+    const int64_t lab = labels[row] - vocab_start;
+    row_tgt[row] = (lab >= 0 && lab < vocab) ? bf2f(x[lab]) : 0.f;
+  }
+}
+
+// Pass 2: dlogits = (exp(x - lse) - onehot) * scale * (label valid), written in place
+// over the logits (bf16); loss[row] = lse - x[label].
+__global__ __launch_bounds__(256) void ce_grad_kernel(
+    uint16_t* __restrict__ logits, const int64_t* __restrict__ labels, int rows, int vocab,
+    int64_t vocab_start, const float* __restrict__ lse, const float* __restrict__ tgt,
+    float* __restrict__ loss, const float* __restrict__ scale_ptr, float scale,
+    int ignore_index) {
+  const int row = blockIdx.x;
+  uint16_t* x = logits + (size_t)row * vocab;
+  const int64_t glab = labels[row];
+  const bool valid = glab != ignore_index;
+  const float L = lse[row];
+  const float sc = (scale_ptr ? *scale_ptr : scale) * (valid ? 1.f : 0.f);
+  const int64_t lab = glab - vocab_start;
+  const int nvec = vocab / 8;
+  for (int v = threadIdx.x; v < nvec; v += 256) {
+    float a[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + v * 8), a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float p = __expf(a[j] - L);
+      if (v * 8 + j == lab) p -= 1.f;
+      a[j] = p * sc;
+    }
+    *reinterpret_cast<uint4*>(x + v * 8) = pack8(a);
+  }
+  for (int c = nvec * 8 + threadIdx.x; c < vocab; c += 256) {
+    float p = __expf(bf2f(x[c]) - L);
+    if (c == lab) p -= 1.f;
+    x[c] = f2bf(p * sc);
+  }
+  if (threadIdx.x == 0 && loss) loss[row] = valid ? (L - tgt[row]) : 0.f;
+}
+
+__global__ void ce_lse_kernel(const float* __restrict__ m, const float* __restrict__ s,
+                              float* __restrict__ lse, int rows) {
+  int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < rows) lse[r] = m[r] + __logf(s[r]);
+}
+
+}  // namespace
+
+MX_EXPORT int mx_bias_gelu_fwd(const void* x, const void* bias, void* y, int rows, int cols,
+                               hipStream_t s) {
+  const int64_t n = (int64_t)rows * cols;
+  int64_t blocks = (n / 8 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(bias_gelu_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                     (const uint16_t*)x, (const uint16_t*)bias, (uint16_t*)y, n, cols);
+  return hipGetLastError();
+}
+
+MX_EXPORT int mx_bias_gelu_bwd_rows_per_block() { return 16; }
+
+// partial: ceil(rows/16) * cols floats.  dx may alias dy.
+MX_EXPORT int mx_bias_gelu_bwd(const void* dy, const void* x, const void* bias, void* dx,
+                               void* dbias, int accumulate, float* partial, int rows, int cols,
+                               hipStream_t s) {
+  const int rpb = 16;
+  dim3 grid((cols / 8 + 255) / 256, (rows + rpb - 1) / rpb);
+  hipLaunchKernelGGL(bias_gelu_bwd_kernel, grid, dim3(256), 0, s, (const uint16_t*)dy,
+                     (const uint16_t*)x, (const uint16_t*)bias, (uint16_t*)dx, rows, cols, rpb,
+                     partial);
+  if (dbias)
+    hipLaunchKernelGGL(colsum_fold_kernel, dim3((cols + 255) / 256), dim3(256), 0, s, partial,
+                       (int)grid.y, cols, (uint16_t*)dbias, accumulate);
+  return hipGetLastError();
+}
+
+MX_EXPORT int mx_embed_fwd(const int64_t* ids, const void* wte, const void* wpe, void* out,
+                           int ntok, int hidden, int seq, int64_t vocab_start,
+                           int64_t vocab_end, int pos_offset, hipStream_t s) {
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3((ntok + 3) / 4), dim3(256), 0, s, ids,
+                     (const uint16_t*)wte, (const uint16_t*)wpe, (uint16_t*)out, ntok, hidden,
+                     seq, vocab_start, vocab_end, pos_offset);
+  return hipGetLastError();
+}
+
+MX_EXPORT int mx_embed_bwd(const int64_t* sorted_ids, const int64_t* perm, const void* dout,
+                           void* dw, int ntok, int hidden, int64_t vocab_start,
+                           int64_t vocab_end, hipStream_t s) {
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(ntok), dim3(128), 0, s, sorted_ids, perm,
+                     (const uint16_t*)dout, (uint16_t*)dw, ntok, hidden, vocab_start,
+                     vocab_end);
+  return hipGetLastError();
+}
+
+MX_EXPORT int mx_pos_embed_bwd(const void* dout, void* dwpe, int batch, int seq, int hidden,
+                               hipStream_t s) {
+  int64_t nvec = (int64_t)seq * hidden / 8;
+  hipLaunchKernelGGL(pos_bwd_kernel, dim3((unsigned)((nvec + 255) / 256)), dim3(256), 0, s,
+                     (const uint16_t*)dout, (uint16_t*)dwpe, batch, seq, hidden);
+  return hipGetLastError();
+}
+
+MX_EXPORT int mx_ce_stats(const void* logits, const int64_t* labels, int rows, int vocab,
+                          int64_t vocab_start, float* row_max, float* row_sum, float* row_tgt,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(ce_stats_kernel, dim3(rows), dim3(256), 0, s, (const uint16_t*)logits,
+                     labels, rows, vocab, vocab_start, row_max, row_sum, row_tgt);
+  return hipGetLastError();
+}
+
+MX_EXPORT int mx_ce_lse(const float* m, const float* sum, float* lse, int rows,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(ce_lse_kernel, dim3((rows + 255) / 256), dim3(256), 0, s, m, sum, lse,
+                     rows);
+  return hipGetLastError();
+}
+
+MX_EXPORT int mx_ce_grad(void* logits, const int64_t* labels, int rows, int vocab,
+                         int64_t vocab_start, const float* lse, const float* tgt, float* loss,
+                         const float* scale_ptr, float scale, int ignore_index,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(ce_grad_kernel, dim3(rows), dim3(256), 0, s, (uint16_t*)logits, labels,
+                     rows, vocab, vocab_start, lse, tgt, loss, scale_ptr, scale, ignore_index);
+  return hipGetLastError();
+}

@@ -1,0 +1,371 @@
+// Fused LayerNorm / RMSNorm forward+backward and the fused
+// bias-dropout-residual-add + LayerNorm ("BDA-LN") used between GPT sublayers.
+//
+// Replaces Apex `fused_layer_norm_cuda` / Megatron `MixedFusedLayerNorm` and the
+// TorchScript `bias_dropout_add_fused_train` the reference pulls in through the
+// Megatron-DeepSpeed image (containers/megatron-deepspeed/Dockerfile:6-13; SURVEY
+// §2.8 K3, K4, K7).
+//
+// Design (gfx950): one wave64 per row, each lane owns 8 contiguous bf16 per 512
+// columns (16-B vector loads, Guideline 13), statistics in fp32 through wave
+// shuffles only (no LDS, no barriers on the forward path).  Backward keeps the
+// per-column reductions (dgamma, dbeta, dbias) in an LDS fp32 slab per block
+// (conflict-free ds_add_f32: each wave-instruction touches 64 distinct columns),
+// dumps the slab to a [grid][3][cols] partial buffer, and a second tiny kernel
+// folds the partials into the bf16 gradient buffers (optionally accumulating).
+#include "common.h"
+
+using namespace mx;
+
+namespace {
+
+template <int NV, bool RMS, bool HAS_BDA>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(
+    const uint16_t* __restrict__ x,        // [rows, cols]  (GEMM output if HAS_BDA)
+    const uint16_t* __restrict__ bias,     // [cols] or null
+    const uint16_t* __restrict__ residual, // [rows, cols] or null
+    const uint16_t* __restrict__ gamma, const uint16_t* __restrict__ beta,
+    uint16_t* __restrict__ h_out,          // [rows, cols] residual stream out (HAS_BDA)
+    uint16_t* __restrict__ y,              // [rows, cols]
+    float* __restrict__ mean_out, float* __restrict__ rstd_out,
+    int rows, int cols, float eps, uint32_t thresh, float keep_scale,
+    const uint32_t* __restrict__ seed_ptr, uint32_t salt) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const uint32_t seed = HAS_BDA && seed_ptr ? (*seed_ptr + salt) : 0u;
+  const size_t base = (size_t)row * cols;
+  float v[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    if (c < cols) {
+      uint4 raw = *reinterpret_cast<const uint4*>(x + base + c);
+      unpack8(raw, v[i]);
+      if constexpr (HAS_BDA) {
+        float b[8], r[8];
+        if (bias) {
+          unpack8(*reinterpret_cast<const uint4*>(bias + c), b);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) b[j] = 0.f;
+        }
+        if (residual) {
+          unpack8(*reinterpret_cast<const uint4*>(residual + base + c), r);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) r[j] = 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float t = v[i][j] + b[j];
+          if (thresh) t = dropout_keep(base + c + j, seed, thresh) ? t * keep_scale : 0.f;
+          v[i][j] = r[j] + t;
+        }
+        // the residual stream is stored in bf16; normalise the rounded value so that
+        // backward (which re-reads h_out) sees exactly the forward's input
+        uint4 packed = pack8(v[i]);
+        *reinterpret_cast<uint4*>(h_out + base + c) = packed;
+        unpack8(packed, v[i]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  float mean = 0.f;
+  if constexpr (!RMS) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[i][j];
+    mean = wave_sum(s) / (float)cols;
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    if (c < cols) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { float d = v[i][j] - mean; ss += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / (float)cols + eps);
+  if (lane == 0) {
+    if (!RMS) mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    if (c < cols) {
+      float g[8], bt[8], o[8];
+      unpack8(*reinterpret_cast<const uint4*>(gamma + c), g);
+      if (!RMS && beta) {
+        unpack8(*reinterpret_cast<const uint4*>(beta + c), bt);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bt[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + bt[j];
+      *reinterpret_cast<uint4*>(y + base + c) = pack8(o);
+    }
+  }
+}
+
+// Backward.  dh = dres + LN'(dy);  if dx_drop: dx = dh * mask * keep_scale.
+// partial[blk][0][c] = sum dy*xhat, [1] = sum dy, [2] = sum dx.
+template <int NV, bool RMS>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dres,
+    const uint16_t* __restrict__ h, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const uint16_t* __restrict__ gamma,
+    uint16_t* __restrict__ dh_out, uint16_t* __restrict__ dx_drop,
+    float* __restrict__ partial, int rows, int cols, uint32_t thresh, float keep_scale,
+    const uint32_t* __restrict__ seed_ptr, uint32_t salt) {
+  extern __shared__ __attribute__((aligned(16))) float slab[];  // [3][cols]
+  for (int i = threadIdx.x; i < 3 * cols; i += blockDim.x) slab[i] = 0.f;
+  __syncthreads();
+  const uint32_t seed = seed_ptr ? (*seed_ptr + salt) : 0u;
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nw = gridDim.x * 4;
+  float g[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    if (c < cols) unpack8(*reinterpret_cast<const uint4*>(gamma + c), g[i]);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[i][j] = 0.f;
+    }
+  }
+  for (int row = wid; row < rows; row += nw) {
+    const size_t base = (size_t)row * cols;
+    const float mean = RMS ? 0.f : mean_in[row];
+    const float rstd = rstd_in[row];
+    float xh[NV][8], gy[NV][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (lane + 64 * i) * 8;
+      if (c < cols) {
+        float hv[8], d[8];
+        unpack8(*reinterpret_cast<const uint4*>(h + base + c), hv);
+        unpack8(*reinterpret_cast<const uint4*>(dy + base + c), d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[i][j] = (hv[j] - mean) * rstd;
+          gy[i][j] = d[j] * g[i][j];
+          s1 += gy[i][j];
+          s2 += gy[i][j] * xh[i][j];
+          atomicAdd(&slab[c + j], d[j] * xh[i][j]);
+          atomicAdd(&slab[cols + c + j], d[j]);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { xh[i][j] = 0.f; gy[i][j] = 0.f; }
+      }
+    }
+    const float m1 = RMS ? 0.f : wave_sum(s1) / (float)cols;
+    const float m2 = wave_sum(s2) / (float)cols;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (lane + 64 * i) * 8;
+      if (c < cols) {
+        float r[8], o[8];
+        if (dres) unpack8(*reinterpret_cast<const uint4*>(dres + base + c), r);
+        else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) r[j] = 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = r[j] + rstd * (gy[i][j] - m1 - xh[i][j] * m2);
+        *reinterpret_cast<uint4*>(dh_out + base + c) = pack8(o);
+        if (dx_drop) {
+          float dx[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float t = o[j];
+            if (thresh) t = dropout_keep(base + c + j, seed, thresh) ? t * keep_scale : 0.f;
+            dx[j] = t;
+          }
+          uint4 pk = pack8(dx);
+          *reinterpret_cast<uint4*>(dx_drop + base + c) = pk;
+          float dxr[8];
+          unpack8(pk, dxr);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) atomicAdd(&slab[2 * cols + c + j], dxr[j]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  float* out = partial + (size_t)blockIdx.x * 3 * cols;
+  for (int i = threadIdx.x; i < 3 * cols; i += blockDim.x) out[i] = slab[i];
+}
+
+// out_k[c] (+)= sum_b partial[b][k][c]   for k in {0,1,2} with non-null out_k
+__global__ __launch_bounds__(256) void colsum_finalize_kernel(
+    const float* __restrict__ partial, int nparts, int cols, int nvec,
+    uint16_t* __restrict__ o0, uint16_t* __restrict__ o1, uint16_t* __restrict__ o2,
+    int accumulate) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= nvec * cols) return;
+  const int k = idx / cols, c = idx % cols;
+  uint16_t* o = k == 0 ? o0 : (k == 1 ? o1 : o2);
+  if (!o) return;
+  float s = 0.f;
+  for (int b = 0; b < nparts; ++b) s += partial[((size_t)b * nvec + k) * cols + c];
+  if (accumulate) s += bf2f(o[c]);
+  o[c] = f2bf(s);
+}
+
+// Column sum of a bf16 matrix [rows, cols] -> bf16 [cols] (bias gradients of the
+// QKV projection).  Block = 256 threads covers 256*8 columns x a row stripe.
+__global__ __launch_bounds__(256) void colsum_partial_kernel(
+    const uint16_t* __restrict__ x, int rows, int cols, int rows_per_block,
+    float* __restrict__ partial) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  const int r0 = blockIdx.y * rows_per_block;
+  if (c >= cols) return;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int r1 = min(rows, r0 + rows_per_block);
+  for (int r = r0; r < r1; ++r) {
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + (size_t)r * cols + c), v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  }
+  float* o = partial + (size_t)blockIdx.y * cols + c;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = acc[j];
+}
+
+template <bool RMS, bool BDA>
+hipError_t launch_fwd(const void* x, const void* bias, const void* residual,
+                      const void* gamma, const void* beta, void* h_out, void* y,
+                      float* mean, float* rstd, int rows, int cols, float eps,
+                      float p, const uint32_t* seed, uint32_t salt, hipStream_t s) {
+  const int nv = (cols + 511) / 512;
+  const uint32_t thresh = p > 0.f ? (uint32_t)((double)p * 4294967296.0) : 0u;
+  const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  dim3 grid((rows + 3) / 4), block(256);
+#define MX_LN_CASE(N)                                                                  \
+  case N:                                                                              \
+    hipLaunchKernelGGL((ln_fwd_kernel<N, RMS, BDA>), grid, block, 0, s,                \
+                       (const uint16_t*)x, (const uint16_t*)bias,                      \
+                       (const uint16_t*)residual, (const uint16_t*)gamma,              \
+                       (const uint16_t*)beta, (uint16_t*)h_out, (uint16_t*)y, mean,    \
+                       rstd, rows, cols, eps, thresh, ks, seed, salt);                 \
+    break;
+  switch (nv) {
+    MX_LN_CASE(1) MX_LN_CASE(2) MX_LN_CASE(3) MX_LN_CASE(4) MX_LN_CASE(5)
+    MX_LN_CASE(6) MX_LN_CASE(8) MX_LN_CASE(10) MX_LN_CASE(12) MX_LN_CASE(16)
+    default: return hipErrorInvalidValue;
+  }
+#undef MX_LN_CASE
+  return hipGetLastError();
+}
+
+int bwd_grid(int rows) {
+  int g = (rows + 15) / 16;  // >= 4 rows per wave on average
+  if (g > 512) g = 512;
+  if (g < 1) g = 1;
+  return g;
+}
+
+template <bool RMS>
+hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const float* mean,
+                      const float* rstd, const void* gamma, void* dh_out, void* dx_drop,
+                      float* partial, int rows, int cols, float p, const uint32_t* seed,
+                      uint32_t salt, hipStream_t s) {
+  const int nv = (cols + 511) / 512;
+  const uint32_t thresh = p > 0.f ? (uint32_t)((double)p * 4294967296.0) : 0u;
+  const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  dim3 grid(bwd_grid(rows)), block(256);
+  size_t lds = (size_t)3 * cols * sizeof(float);
+#define MX_LNB_CASE(N)                                                                 \
+  case N:                                                                              \
+    hipLaunchKernelGGL((ln_bwd_kernel<N, RMS>), grid, block, lds, s,                   \
+                       (const uint16_t*)dy, (const uint16_t*)dres, (const uint16_t*)h, \
+                       mean, rstd, (const uint16_t*)gamma, (uint16_t*)dh_out,          \
+                       (uint16_t*)dx_drop, partial, rows, cols, thresh, ks, seed,      \
+                       salt);                                                          \
+    break;
+  switch (nv) {
+    MX_LNB_CASE(1) MX_LNB_CASE(2) MX_LNB_CASE(3) MX_LNB_CASE(4) MX_LNB_CASE(5)
+    MX_LNB_CASE(6) MX_LNB_CASE(8) MX_LNB_CASE(10) MX_LNB_CASE(12) MX_LNB_CASE(16)
+    default: return hipErrorInvalidValue;
+  }
+#undef MX_LNB_CASE
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// number of partial slabs the backward kernels write (caller sizes `partial`)
+MX_EXPORT int mx_norm_bwd_nparts(int rows) { return bwd_grid(rows); }
+
+MX_EXPORT int mx_layernorm_fwd(const void* x, const void* gamma, const void* beta, void* y,
+                               float* mean, float* rstd, int rows, int cols, float eps,
+                               hipStream_t s) {
+  return launch_fwd<false, false>(x, nullptr, nullptr, gamma, beta, nullptr, y, mean, rstd,
+                                  rows, cols, eps, 0.f, nullptr, 0, s);
+}
+
+MX_EXPORT int mx_rmsnorm_fwd(const void* x, const void* gamma, void* y, float* rstd,
+                             int rows, int cols, float eps, hipStream_t s) {
+  return launch_fwd<true, false>(x, nullptr, nullptr, gamma, nullptr, nullptr, y, nullptr,
+                                 rstd, rows, cols, eps, 0.f, nullptr, 0, s);
+}
+
+// h_out = residual + dropout(x + bias);  y = LayerNorm(h_out)   (RMS: RMSNorm)
+MX_EXPORT int mx_bda_norm_fwd(const void* x, const void* bias, const void* residual,
+                              const void* gamma, const void* beta, void* h_out, void* y,
+                              float* mean, float* rstd, int rows, int cols, float eps,
+                              float p, const uint32_t* seed, uint32_t salt, int rms,
+                              hipStream_t s) {
+  if (rms)
+    return launch_fwd<true, true>(x, bias, residual, gamma, nullptr, h_out, y, nullptr,
+                                  rstd, rows, cols, eps, p, seed, salt, s);
+  return launch_fwd<false, true>(x, bias, residual, gamma, beta, h_out, y, mean, rstd, rows,
+                                 cols, eps, p, seed, salt, s);
+}
+
+MX_EXPORT int mx_norm_bwd(const void* dy, const void* dres, const void* h, const float* mean,
+                          const float* rstd, const void* gamma, void* dh_out, void* dx_drop,
+                          float* partial, int rows, int cols, float p, const uint32_t* seed,
+                          uint32_t salt, int rms, hipStream_t s) {
+  if (rms)
+    return launch_bwd<true>(dy, dres, h, mean, rstd, gamma, dh_out, dx_drop, partial, rows,
+                            cols, p, seed, salt, s);
+  return launch_bwd<false>(dy, dres, h, mean, rstd, gamma, dh_out, dx_drop, partial, rows,
+                           cols, p, seed, salt, s);
+}
+
+MX_EXPORT int mx_colsum_finalize(const float* partial, int nparts, int cols, int nvec,
+                                 void* o0, void* o1, void* o2, int accumulate,
+                                 hipStream_t s) {
+  int n = nvec * cols;
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s,
+                     partial, nparts, cols, nvec, (uint16_t*)o0, (uint16_t*)o1,
+                     (uint16_t*)o2, accumulate);
+  return hipGetLastError();
+}
+
+// bf16 column sum: `partial` must hold ceil(rows/rows_per_block) * cols floats
+MX_EXPORT int mx_colsum_bf16(const void* x, int rows, int cols, float* partial, void* out,
+                             int accumulate, hipStream_t s) {
+  const int rpb = 64;
+  dim3 grid((cols / 8 + 255) / 256, (rows + rpb - 1) / rpb);
+  hipLaunchKernelGGL(colsum_partial_kernel, grid, dim3(256), 0, s, (const uint16_t*)x, rows,
+                     cols, rpb, partial);
+  int nparts = grid.y;
+  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((cols + 255) / 256), dim3(256), 0, s,
+                     partial, nparts, cols, 1, (uint16_t*)out, (uint16_t*)nullptr,
+                     (uint16_t*)nullptr, accumulate);
+  return hipGetLastError();
+}

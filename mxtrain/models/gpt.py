@@ -1,0 +1,467 @@
+"""Megatron-style GPT (GPT-2 345M / GPT-3 6.7B configs) built on mxtrain's HIP kernels.
+
+Workload parity: Megatron-DeepSpeed `pretrain_gpt.py` GPT model as configured by
+examples/megatron-deepspeed/gpt2_345m/pretrain-ddp-zero1.yaml:39-53 (24 layers, hidden
+1024, 16 heads, seq 1024, learned positions, pre-LN, tied embeddings, GeLU MLP, hidden
+dropout 0.1) and the TP2/PP2 variant (pretrain-ddp-tp-pp-zero1.yaml:39-40).
+
+MI355X-first structure: each transformer layer is ONE autograd Function with a
+hand-scheduled forward and backward:
+
+  fwd: qkv = a Wqkv^T + b (hipBLASLt, bias epilogue) -> flash-attn (HIP, MFMA)
+       -> o = ctx Wo^T -> [h1, m] = BDA-LN(o, bo, h) (HIP: bias+dropout+residual+LN
+       in one pass) -> pre = m W1^T -> f = bias-GeLU(pre) (HIP) -> g = f W2^T
+       -> [h2, a_next] = BDA-LN(g, b2, h1) with the NEXT layer's LN1 (or the final LN)
+  bwd: the mirror image; weight gradients are written straight into the flat bf16
+       gradient buffer with beta=1 GEMMs (Megatron "gradient accumulation fusion"),
+       bias/LN gradients come out of the fused backward kernels' column reductions,
+       and the layer reports completion so its gradient bucket's reduce-scatter can
+       start while earlier layers are still in backward.
+
+Tensor parallelism (Megatron column/row split: QKV+fc1 column-parallel, proj+fc2
+row-parallel, vocab-parallel embedding/CE) and sequence parallelism (LN/dropout on
+token shards with all-gather / reduce-scatter instead of all-reduce) are built in.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+import torch
+
+from .. import ops
+from ..ops import attention as attn_ops
+from ..ops.norm import bda_norm_fwd, colsum, layernorm_fwd, norm_bwd
+from ..ops.fused import (bias_gelu_bwd, bias_gelu_fwd, cross_entropy_fwd_bwd, embed_bwd,
+                         embed_fwd, pos_embed_bwd)
+from ..parallel import collectives as C
+from ..parallel.buffers import ParamSpec
+
+
+@dataclass
+class GPTConfig:
+    num_layers: int = 24
+    hidden_size: int = 1024
+    num_attention_heads: int = 16
+    num_kv_heads: Optional[int] = None
+    ffn_hidden_size: Optional[int] = None
+    vocab_size: int = 50257
+    make_vocab_size_divisible_by: int = 128
+    seq_length: int = 1024
+    max_position_embeddings: int = 1024
+    hidden_dropout: float = 0.1
+    attention_dropout: float = 0.0
+    layernorm_epsilon: float = 1e-5
+    init_method_std: float = 0.02
+    normalization: str = "layernorm"       # layernorm | rmsnorm
+    position_embedding: str = "learned"    # learned | rope
+    tie_embeddings: bool = True
+
+    def __post_init__(self):
+        if self.ffn_hidden_size is None:
+            self.ffn_hidden_size = 4 * self.hidden_size
+        if self.num_kv_heads is None:
+            self.num_kv_heads = self.num_attention_heads
+
+    @property
+    def head_dim(self):
+        return self.hidden_size // self.num_attention_heads
+
+    def padded_vocab(self, tp: int = 1) -> int:
+        m = self.make_vocab_size_divisible_by * tp
+        return (self.vocab_size + m - 1) // m * m
+
+    def num_params(self, tp: int = 1) -> int:
+        h, f, L = self.hidden_size, self.ffn_hidden_size, self.num_layers
+        V = self.padded_vocab(tp)
+        kvh = self.num_kv_heads * self.head_dim
+        per_layer = (2 * h + (h * (h + 2 * kvh) + h + 2 * kvh) + (h * h + h) + 2 * h
+                     + (h * f + f) + (f * h + h))
+        if self.normalization == "rmsnorm":
+            per_layer -= 2 * h
+        n = V * h + L * per_layer + 2 * h
+        if self.position_embedding == "learned":
+            n += self.max_position_embeddings * h
+        if not self.tie_embeddings:
+            n += V * h
+        return n
+
+    def flops_per_token(self) -> float:
+        """Megatron/MFU convention: 6N + 12*L*h*s (fwd+bwd, no recompute)."""
+        return 6.0 * self.num_params() + 12.0 * self.num_layers * self.hidden_size * self.seq_length
+
+
+GPT_CONFIGS = {
+    "gpt2-345m": dict(num_layers=24, hidden_size=1024, num_attention_heads=16, seq_length=1024,
+                      max_position_embeddings=1024),
+    "gpt3-6.7b": dict(num_layers=32, hidden_size=4096, num_attention_heads=32, seq_length=2048,
+                      max_position_embeddings=2048),
+    "gpt-tiny": dict(num_layers=2, hidden_size=128, num_attention_heads=2, seq_length=64,
+                     max_position_embeddings=64, vocab_size=1000),
+}
+
+SALT_EMB = 7
+_NORM_PARAMS = ("ln1_w", "ln1_b")
+
+
+# ============================================================================== specs
+def stage_layer_range(cfg: GPTConfig, pp: int, pp_rank: int):
+    per = cfg.num_layers // pp
+    extra = cfg.num_layers % pp
+    start = pp_rank * per + min(pp_rank, extra)
+    n = per + (1 if pp_rank < extra else 0)
+    return start, start + n
+
+
+def gpt_param_specs(cfg: GPTConfig, tp: int = 1, pp: int = 1, pp_rank: int = 0,
+                    sequence_parallel: bool = False) -> List[ParamSpec]:
+    """Parameter specs for one (tp, pp) stage.  unit = backward-completion unit:
+    0 = embedding (+ layer0.ln1), i+1 = layer i (+ the next layer's ln1 / final LN)."""
+    h = cfg.hidden_size
+    D = cfg.head_dim
+    hl = cfg.num_attention_heads // tp
+    kvl = cfg.num_kv_heads // tp
+    fl = cfg.ffn_hidden_size // tp
+    V = cfg.padded_vocab(tp) // tp
+    std = cfg.init_method_std
+    rms = cfg.normalization == "rmsnorm"
+    sp = sequence_parallel and tp > 1
+    l0, l1 = stage_layer_range(cfg, pp, pp_rank)
+    first, last = pp_rank == 0, pp_rank == pp - 1
+    specs: List[ParamSpec] = []
+
+    def norm(prefix, unit):
+        specs.append(ParamSpec(f"{prefix}_w", (h,), "ones", weight_decay=False, unit=unit,
+                               sp_reduce=sp))
+        if not rms:
+            specs.append(ParamSpec(f"{prefix}_b", (h,), "zeros", weight_decay=False, unit=unit,
+                                   sp_reduce=sp))
+
+    if first:
+        specs.append(ParamSpec("wte", (V, h), std=std, unit=0, tp_duplicated=False,
+                               shared="word_embeddings"))
+        if cfg.position_embedding == "learned":
+            specs.append(ParamSpec("wpe", (cfg.max_position_embeddings, h), std=std, unit=0))
+    for i in range(l0, l1):
+        u = i + 1
+        if i == l0:
+            # the stage's first layer owns its LN1 (computed by embedding or its own Fn)
+            # LN1 of the stage's first layer: computed by EmbedFn (first stage) or NormFn,
+            # finishes backward last on this stage -> unit l0 (== 0 on the first stage)
+            norm(f"layers.{i}.ln1", l0)
+        p = f"layers.{i}."
+        nd = False
+        specs += [
+            ParamSpec(p + "qkv_w", ((hl + 2 * kvl) * D, h), std=std, unit=u, tp_duplicated=nd),
+            ParamSpec(p + "qkv_b", ((hl + 2 * kvl) * D,), "zeros", weight_decay=False, unit=u,
+                      tp_duplicated=nd),
+            ParamSpec(p + "proj_w", (h, hl * D), "scaled_normal", std=std, unit=u,
+                      tp_duplicated=nd),
+            ParamSpec(p + "proj_b", (h,), "zeros", weight_decay=False, unit=u, sp_reduce=sp),
+        ]
+        norm(p + "ln2", u)
+        specs += [
+            ParamSpec(p + "fc1_w", (fl, h), std=std, unit=u, tp_duplicated=nd),
+            ParamSpec(p + "fc1_b", (fl,), "zeros", weight_decay=False, unit=u, tp_duplicated=nd),
+            ParamSpec(p + "fc2_w", (h, fl), "scaled_normal", std=std, unit=u, tp_duplicated=nd),
+            ParamSpec(p + "fc2_b", (h,), "zeros", weight_decay=False, unit=u, sp_reduce=sp),
+        ]
+        if i + 1 < l1:
+            norm(f"layers.{i + 1}.ln1", u)
+        elif last:
+            norm("final_ln", u)
+    if last and (not first or not cfg.tie_embeddings):
+        name = "wte_head" if cfg.tie_embeddings else "lm_head"
+        specs.append(ParamSpec(name, (V, h), std=std, unit=l1, tp_duplicated=False,
+                               shared="word_embeddings" if cfg.tie_embeddings else None))
+    return specs
+
+
+# ============================================================================== runtime
+@dataclass
+class StepRuntime:
+    """Per-model runtime handed to the autograd Functions (non-tensor state)."""
+    cfg: GPTConfig
+    params: Dict[str, torch.Tensor]
+    grads: Dict[str, torch.Tensor]
+    B: int = 1
+    S: int = 1
+    tp_group: Optional[object] = None
+    tp: int = 1
+    tp_rank: int = 0
+    sp: bool = False
+    seed_t: Optional[torch.Tensor] = None
+    training: bool = True
+    vocab_start: int = 0
+    unit_done: Optional[Callable[[int], None]] = None
+    grad_scale: float = 1.0       # loss gradient scale (1 / tokens / microbatches)
+
+    @property
+    def p_drop(self):
+        return self.cfg.hidden_dropout if self.training else 0.0
+
+    @property
+    def rms(self):
+        return self.cfg.normalization == "rmsnorm"
+
+    def norm_params(self, prefix):
+        w = self.params[prefix + "_w"]
+        b = self.params.get(prefix + "_b")
+        return w, b
+
+    def norm_grads(self, prefix):
+        return self.grads[prefix + "_w"], self.grads.get(prefix + "_b")
+
+    def done(self, unit):
+        if self.unit_done is not None:
+            self.unit_done(unit)
+
+    def salt(self, base):
+        return base + (7919 * self.tp_rank if self.sp else 0)
+
+
+def _gather(x, rt):
+    return C.all_gather_dim0(x, rt.tp_group) if rt.sp else x
+
+
+def _reduce(x, rt):
+    """Row-parallel output combine: reduce-scatter under SP, all-reduce under TP."""
+    if rt.tp == 1:
+        return x
+    if rt.sp:
+        return C.reduce_scatter_dim0(x, rt.tp_group)
+    return C.all_reduce_(x, rt.tp_group)
+
+
+def _wgrad(gbuf, dy, x):
+    """gbuf += dy^T x (beta=1 GEMM straight into the flat gradient buffer)."""
+    gbuf.addmm_(dy.t(), x)
+
+
+# ============================================================================== Functions
+class EmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, ids, rt: StepRuntime, first_layer: int):
+        P = rt.params
+        e = embed_fwd(ids, P["wte"], P.get("wpe"), seq=rt.S, vocab_start=rt.vocab_start)
+        if rt.tp > 1:
+            C.all_reduce_(e, rt.tp_group)
+            if rt.sp:
+                e = C.split_dim0(e, rt.tp_group)
+        w, b = rt.norm_params(f"layers.{first_layer}.ln1")
+        h, a, mean, rstd = bda_norm_fwd(e, None, None, w, b, rt.cfg.layernorm_epsilon, rt.p_drop,
+                                        rt.seed_t, rt.salt(SALT_EMB), rt.rms)
+        ctx.saved = (ids, h, mean, rstd)
+        ctx.rt = rt
+        ctx.first_layer = first_layer
+        return h, a
+
+    @staticmethod
+    def backward(ctx, dh, da):
+        rt = ctx.rt
+        ids, h, mean, rstd = ctx.saved
+        w, _ = rt.norm_params(f"layers.{ctx.first_layer}.ln1")
+        gw, gb = rt.norm_grads(f"layers.{ctx.first_layer}.ln1")
+        _, de = norm_bwd(da.contiguous(), dh.contiguous(), h, mean, rstd, w, want_dx=True,
+                         p=rt.p_drop, seed_t=rt.seed_t, salt=rt.salt(SALT_EMB), rms=rt.rms,
+                         dgamma=gw, dbeta=gb, accumulate=True)
+        if rt.sp:
+            de = C.all_gather_dim0(de, rt.tp_group)
+        embed_bwd(ids, de, rt.grads["wte"], rt.vocab_start)
+        if "wpe" in rt.grads:
+            pos_embed_bwd(de, rt.grads["wpe"], rt.B, rt.S)
+        rt.done(0)
+        ctx.saved = None
+        return None, None, None, None
+
+
+class NormFn(torch.autograd.Function):
+    """Stand-alone LN1 for the first layer of a non-first pipeline stage."""
+
+    @staticmethod
+    def forward(ctx, h, rt: StepRuntime, prefix: str, unit: int):
+        w, b = rt.norm_params(prefix)
+        a, mean, rstd = layernorm_fwd(h, w, b, rt.cfg.layernorm_epsilon, rt.rms)
+        ctx.saved = (h, mean, rstd)
+        ctx.rt, ctx.prefix, ctx.unit = rt, prefix, unit
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        rt = ctx.rt
+        h, mean, rstd = ctx.saved
+        w, _ = rt.norm_params(ctx.prefix)
+        gw, gb = rt.norm_grads(ctx.prefix)
+        dh, _ = norm_bwd(da.contiguous(), None, h, mean, rstd, w, rms=rt.rms, dgamma=gw,
+                         dbeta=gb, accumulate=True)
+        ctx.saved = None
+        rt.done(ctx.unit)
+        return dh, None, None, None
+
+
+class GPTLayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, a, rt: StepRuntime, i: int, next_norm: Optional[str]):
+        cfg = rt.cfg
+        P = rt.params
+        p = f"layers.{i}."
+        D = cfg.head_dim
+        hl = cfg.num_attention_heads // rt.tp
+        kvl = cfg.num_kv_heads // rt.tp
+        eps = cfg.layernorm_epsilon
+        a_full = _gather(a, rt)
+        qkv = torch.addmm(P[p + "qkv_b"], a_full, P[p + "qkv_w"].t())
+        q = qkv[:, : hl * D]
+        k = qkv[:, hl * D:(hl + kvl) * D]
+        v = qkv[:, (hl + kvl) * D:]
+        ctx_, lse = attn_ops.attn_fwd(q, k, v, rt.B, rt.S, hl, kvl, D, causal=True)
+        o = _reduce(torch.mm(ctx_, P[p + "proj_w"].t()), rt)
+        w2, b2 = rt.norm_params(p + "ln2")
+        h1, m, mean2, rstd2 = bda_norm_fwd(o, P[p + "proj_b"], h, w2, b2, eps, rt.p_drop, rt.seed_t,
+                                           rt.salt(1000 + 2 * i), rt.rms)
+        m_full = _gather(m, rt)
+        pre = torch.mm(m_full, P[p + "fc1_w"].t())
+        f = bias_gelu_fwd(pre, P[p + "fc1_b"])
+        g = _reduce(torch.mm(f, P[p + "fc2_w"].t()), rt)
+        if next_norm is not None:
+            wn, bn = rt.norm_params(next_norm)
+        else:  # stage boundary: plain bias-dropout-add; normalise into a throwaway
+            wn, bn = P[p + "ln2_w"], P.get(p + "ln2_b")
+        h2, a2, mean_n, rstd_n = bda_norm_fwd(g, P[p + "fc2_b"], h1, wn, bn, eps, rt.p_drop,
+                                              rt.seed_t, rt.salt(1001 + 2 * i), rt.rms)
+        ctx.saved = (a_full, qkv, ctx_, lse, h1, mean2, rstd2, m_full, pre, f, h2, mean_n, rstd_n)
+        ctx.rt, ctx.i, ctx.next_norm = rt, i, next_norm
+        if next_norm is None:
+            return h2, torch.empty(0, device=h2.device, dtype=h2.dtype)
+        return h2, a2
+
+    @staticmethod
+    def backward(ctx, dh2, da2):
+        rt, i = ctx.rt, ctx.i
+        cfg = rt.cfg
+        P, G = rt.params, rt.grads
+        p = f"layers.{i}."
+        D = cfg.head_dim
+        hl = cfg.num_attention_heads // rt.tp
+        kvl = cfg.num_kv_heads // rt.tp
+        (a_full, qkv, ctx_, lse, h1, mean2, rstd2, m_full, pre, f, h2, mean_n, rstd_n) = ctx.saved
+        ctx.saved = None
+        dh2 = dh2.contiguous()
+        # ---- BDA-LN(next) backward
+        if ctx.next_norm is not None:
+            wn, _ = rt.norm_params(ctx.next_norm)
+            gwn, gbn = rt.norm_grads(ctx.next_norm)
+            dh1, dg = norm_bwd(da2.contiguous(), dh2, h2, mean_n, rstd_n, wn, want_dx=True,
+                               p=rt.p_drop, seed_t=rt.seed_t, salt=rt.salt(1001 + 2 * i),
+                               rms=rt.rms, dgamma=gwn, dbeta=gbn, dbias=G[p + "fc2_b"],
+                               accumulate=True)
+        else:
+            wn = P[p + "ln2_w"]
+            zero = torch.zeros_like(dh2)
+            dh1, dg = norm_bwd(zero, dh2, h2, mean_n, rstd_n, wn, want_dx=True, p=rt.p_drop,
+                               seed_t=rt.seed_t, salt=rt.salt(1001 + 2 * i), rms=rt.rms,
+                               dbias=G[p + "fc2_b"], accumulate=True)
+        # ---- MLP backward
+        dg_full = _gather(dg, rt)
+        _wgrad(G[p + "fc2_w"], dg_full, f)
+        df = torch.mm(dg_full, P[p + "fc2_w"])
+        dpre = bias_gelu_bwd(df, pre, P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True,
+                             inplace=True)
+        _wgrad(G[p + "fc1_w"], dpre, m_full)
+        dm = _reduce(torch.mm(dpre, P[p + "fc1_w"]), rt)
+        # ---- BDA-LN2 backward
+        w2, _ = rt.norm_params(p + "ln2")
+        gw2, gb2 = rt.norm_grads(p + "ln2")
+        dh, do_ = norm_bwd(dm, dh1, h1, mean2, rstd2, w2, want_dx=True, p=rt.p_drop,
+                           seed_t=rt.seed_t, salt=rt.salt(1000 + 2 * i), rms=rt.rms, dgamma=gw2,
+                           dbeta=gb2, dbias=G[p + "proj_b"], accumulate=True)
+        # ---- attention backward
+        do_full = _gather(do_, rt)
+        _wgrad(G[p + "proj_w"], do_full, ctx_)
+        dctx = torch.mm(do_full, P[p + "proj_w"])
+        dqkv = torch.empty_like(qkv)
+        q = qkv[:, : hl * D]
+        k = qkv[:, hl * D:(hl + kvl) * D]
+        v = qkv[:, (hl + kvl) * D:]
+        attn_ops.attn_bwd(dctx, q, k, v, ctx_, lse, rt.B, rt.S, hl, kvl, D, causal=True,
+                          dq=dqkv[:, : hl * D], dk=dqkv[:, hl * D:(hl + kvl) * D],
+                          dv=dqkv[:, (hl + kvl) * D:])
+        colsum(dqkv, G[p + "qkv_b"], accumulate=True)
+        _wgrad(G[p + "qkv_w"], dqkv, a_full)
+        da = _reduce(torch.mm(dqkv, P[p + "qkv_w"]), rt)
+        rt.done(i + 1)
+        return dh, da, None, None, None
+
+
+class LMHeadLossFn(torch.autograd.Function):
+    """logits = x W^T (vocab-parallel under TP) -> fused softmax-CE; the gradient is
+    produced in the forward pass (in place over the logits)."""
+
+    @staticmethod
+    def forward(ctx, x, labels, rt: StepRuntime, wname: str):
+        W = rt.params[wname]
+        x_full = _gather(x, rt)
+        logits = torch.mm(x_full, W.t())
+        losses = cross_entropy_fwd_bwd(logits, labels, rt.grad_scale,
+                                       tp_group=rt.tp_group if rt.tp > 1 else None,
+                                       vocab_start=rt.vocab_start)
+        ctx.saved = (x_full, logits)
+        ctx.rt, ctx.wname = rt, wname
+        return losses.sum() * rt.grad_scale
+
+    @staticmethod
+    def backward(ctx, g):
+        rt = ctx.rt
+        x_full, dlogits = ctx.saved
+        ctx.saved = None
+        W = rt.params[ctx.wname]
+        gv = g.reshape(1).to(x_full.dtype)
+        _wgrad(rt.grads[ctx.wname], dlogits, x_full * gv)
+        dx = torch.mm(dlogits, W) * gv
+        dx = _reduce(dx, rt)
+        return dx, None, None, None
+
+
+# ============================================================================== model
+class GPTStage:
+    """The layers of one pipeline stage (all layers when pp == 1)."""
+
+    def __init__(self, cfg: GPTConfig, params, grads, tp=1, tp_rank=0, tp_group=None, pp=1,
+                 pp_rank=0, sequence_parallel=False, seed_t=None):
+        self.cfg = cfg
+        self.l0, self.l1 = stage_layer_range(cfg, pp, pp_rank)
+        self.first, self.last = pp_rank == 0, pp_rank == pp - 1
+        V = cfg.padded_vocab(tp) // tp
+        self.rt = StepRuntime(cfg=cfg, params=params, grads=grads, tp_group=tp_group, tp=tp,
+                              tp_rank=tp_rank, sp=sequence_parallel and tp > 1, seed_t=seed_t,
+                              vocab_start=tp_rank * V)
+        self.anchor = torch.zeros(1, requires_grad=True)
+        if self.last:
+            if cfg.tie_embeddings:
+                self.head_name = "wte" if self.first else "wte_head"
+            else:
+                self.head_name = "lm_head"
+
+    def forward(self, ids=None, hidden=None, labels=None, B=1, S=None):
+        """First stage takes token ids [B*S]; later stages take the hidden state
+        [tokens, h] (requires_grad).  Last stage returns the scalar loss, other stages
+        the hidden state to send downstream."""
+        rt = self.rt
+        rt.B, rt.S = B, S or self.cfg.seq_length
+        if self.first:
+            h, a = EmbedFn.apply(self.anchor, ids, rt, self.l0)
+        else:
+            h = hidden
+            a = NormFn.apply(h, rt, f"layers.{self.l0}.ln1", self.l0)
+        for i in range(self.l0, self.l1):
+            if i + 1 < self.l1:
+                nxt = f"layers.{i + 1}.ln1"
+            elif self.last:
+                nxt = "final_ln"
+            else:
+                nxt = None
+            h, a = GPTLayerFn.apply(h, a, rt, i, nxt)
+        if not self.last:
+            return h
+        return LMHeadLossFn.apply(a, labels, rt, self.head_name)

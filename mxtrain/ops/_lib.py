@@ -1,0 +1,124 @@
+"""ctypes binding of the in-tree HIP kernel library ``mxtrain/lib/libmxkernels.so``.
+
+The library is loaded lazily the first time a GPU op runs.  On a machine with a GPU
+the ops never fall back silently: if the library is missing or fails to load, the op
+raises (set ``MXTRAIN_ALLOW_TORCH_FALLBACK=1`` to opt into the eager-PyTorch
+reference path for debugging).  CPU tensors always use the reference path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libmxkernels.so"))
+
+_lock = threading.Lock()
+_lib = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+I64 = ctypes.c_int64
+F = ctypes.c_float
+U32 = ctypes.c_uint32
+
+# name -> argtypes (every function returns int hipError_t; the stream is the last arg)
+SIGNATURES = {
+    # norm.hip
+    "mx_norm_bwd_nparts": [I],
+    "mx_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],
+    "mx_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
+    "mx_bda_norm_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, F, P, U32, I, P],
+    "mx_norm_bwd": [P, P, P, P, P, P, P, P, P, I, I, F, P, U32, I, P],
+    "mx_colsum_finalize": [P, I, I, I, P, P, P, I, P],
+    "mx_colsum_bf16": [P, I, I, P, P, I, P],
+    # fused.hip
+    "mx_bias_gelu_fwd": [P, P, P, I, I, P],
+    "mx_bias_gelu_bwd_rows_per_block": [],
+    "mx_bias_gelu_bwd": [P, P, P, P, P, I, P, I, I, P],
+    "mx_embed_fwd": [P, P, P, P, I, I, I, I64, I64, I, P],
+    "mx_embed_bwd": [P, P, P, P, I, I, I64, I64, P],
+    "mx_pos_embed_bwd": [P, P, I, I, I, P],
+    "mx_ce_stats": [P, P, I, I, I64, P, P, P, P],
+    "mx_ce_lse": [P, P, P, I, P],
+    "mx_ce_grad": [P, P, I, I, I64, P, P, P, P, F, I, P],
+    # optim.hip
+    "mx_sumsq_nparts": [],
+    "mx_sumsq_bf16": [P, I64, F, P, P, P, I, P],
+    "mx_adamw_step": [P, P, P, P, P, P, I64, P, P, P],
+    # attention.hip
+    "mx_attn_fwd": [P, P, P, I, I, I, P, I, P, I, I, I, I, I, I, P, F, P],
+    "mx_attn_bwd": [P, P, P, I, I, I, P, I, P, I, P, P, P, P, I, P, P, I, I, I, I, I, I, I,
+                    I, P, F, P],
+}
+
+
+def _load():
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"mxtrain HIP kernel library not found at {LIB_PATH}; build it with "
+                "`python -m mxtrain.build` (hipcc --offload-arch=gfx950)")
+        # torch must be imported first so the process-wide HIP runtime is torch's
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def lib():
+    return _load()
+
+
+def available() -> bool:
+    try:
+        _load()
+        return True
+    except Exception:
+        return False
+
+
+def fallback_allowed() -> bool:
+    return os.environ.get("MXTRAIN_ALLOW_TORCH_FALLBACK", "0") == "1"
+
+
+def use_hip(t: torch.Tensor) -> bool:
+    """True when ``t`` lives on the GPU and the HIP kernels must be used."""
+    if not t.is_cuda:
+        return False
+    if fallback_allowed() and not available():
+        return False
+    return True
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def call(name, *args):
+    fn = getattr(_load(), name)
+    err = fn(*args)
+    if err != 0:
+        raise RuntimeError(f"{name} failed with hipError {err}")
+    return err
+
+
+def query(name, *args) -> int:
+    return getattr(_load(), name)(*args)

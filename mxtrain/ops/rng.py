@@ -1,0 +1,54 @@
+"""Counter-based dropout RNG shared by the HIP kernels and the CPU reference.
+
+``keep(idx)`` = hash32(lo(idx) ^ hi(idx)*0x85ebca6b, seed) >= p*2^32, bit-identical to
+``mx::dropout_keep`` in ``csrc/common.h``.  Masks are never stored: backward
+regenerates them from the same (seed, element index).
+
+The seed lives in a 1-element int32 device tensor so a hipGraph-captured step sees a
+fresh value on every replay (``DropoutSeed.advance`` is itself captured).
+"""
+from __future__ import annotations
+
+import torch
+
+M32 = 0xFFFFFFFF
+
+
+def _u32(x: torch.Tensor) -> torch.Tensor:
+    return x & M32
+
+
+def hash32(x: torch.Tensor, seed: int) -> torch.Tensor:
+    x = _u32(x ^ _u32(torch.tensor(seed, dtype=torch.int64) * 0x9E3779B9))
+    x = x ^ (x >> 16)
+    x = _u32(x * 0x7FEB352D)
+    x = x ^ (x >> 15)
+    x = _u32(x * 0x846CA68B)
+    x = x ^ (x >> 16)
+    return x
+
+
+def keep_mask(numel: int, seed: int, p: float, device="cpu", base: int = 0) -> torch.Tensor:
+    """Boolean keep-mask for flat element indices base..base+numel-1."""
+    idx = torch.arange(base, base + numel, dtype=torch.int64, device=device)
+    lo = idx & M32
+    hi = (idx >> 32) & M32
+    x = lo ^ _u32(hi * 0x85EBCA6B)
+    h = hash32(x, seed)
+    thresh = int(p * 4294967296.0) if p > 0 else 0
+    return h >= thresh
+
+
+class DropoutSeed:
+    """Device-resident dropout seed, advanced once per training step."""
+
+    def __init__(self, device, seed: int = 1234):
+        self.t = torch.tensor([seed & 0x7FFFFFFF], dtype=torch.int32, device=device)
+
+    def value(self) -> int:
+        return int(self.t.item())
+
+    def advance(self):
+        # stays on-device (captured into hipGraphs); wraps harmlessly
+        self.t.add_(0x61C88647 & 0x7FFFFFFF)
+        self.t.bitwise_and_(0x7FFFFFFF)

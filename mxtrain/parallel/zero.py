@@ -1,0 +1,236 @@
+"""ZeRO-1 distributed optimizer over the flat bucketed buffers (P1/P2, M2-M5, M10, M11).
+
+Per step:
+  1. backward writes bf16 grads into FlatParams.grad; as soon as every unit of a bucket
+     has finished backward, the bucket is reduce-scattered over the DP group on a
+     dedicated HIP stream (overlapped with the rest of backward);
+  2. grad norm: one fused sum-of-squares over the rank's shard (TP/PP duplicates
+     masked out) + one scalar all-reduce -- no host synchronisation anywhere;
+  3. one fused AdamW launch over the whole fp32 shard, clip coefficient and inf/nan
+     skip computed on device, bf16 params written straight into the all-gather source;
+  4. all-gather of the updated bf16 shards back into FlatParams.data.
+
+DeepSpeed ZeRO-1 equivalent of the reference's ds_config `"zero_optimization":
+{"stage": 1}` (examples/megatron-deepspeed/gpt2_345m/pretrain-ddp-zero1.yaml:33-38).
+With dp == 1 the shard IS the flat buffer (no copies, no collectives).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import optim as optim_ops
+from .buffers import ALIGN, FlatParams
+
+
+class LRSchedule:
+    """Megatron OptimizerParamScheduler subset: linear warmup then cosine/linear/constant
+    decay to min_lr at lr_decay_iters (`--lr-decay-style cosine`, `--lr-warmup-fraction`)."""
+
+    def __init__(self, lr, min_lr=0.0, warmup_iters=0, decay_iters=None, style="cosine"):
+        self.lr, self.min_lr = lr, min_lr
+        self.warmup = warmup_iters
+        self.decay = decay_iters
+        self.style = style
+
+    def __call__(self, it: int) -> float:
+        if self.warmup > 0 and it <= self.warmup:
+            return self.lr * it / self.warmup
+        if self.style == "constant" or self.decay is None:
+            return self.lr
+        if it > self.decay:
+            return self.min_lr
+        r = (it - self.warmup) / max(1, self.decay - self.warmup)
+        if self.style == "linear":
+            c = 1.0 - r
+        else:
+            c = 0.5 * (math.cos(math.pi * r) + 1.0)
+        return self.min_lr + c * (self.lr - self.min_lr)
+
+
+class DistributedOptimizer:
+    def __init__(self, flat: FlatParams, dp_group=None, lr=1.5e-4, betas=(0.9, 0.999), eps=1e-8,
+                 weight_decay=0.01, clip_grad=1.0, overlap: bool = True, tp_rank: int = 0,
+                 tp_group=None, sp_group=None, mp_group=None, embed_group=None,
+                 pp_rank: int = 0, schedule: Optional[LRSchedule] = None):
+        self.flat = flat
+        self.dp_group = dp_group
+        self.world = dist.get_world_size(dp_group) if dp_group is not None else 1
+        self.rank = dist.get_rank(dp_group) if dp_group is not None else 0
+        self.betas, self.eps, self.wd, self.clip = betas, eps, weight_decay, clip_grad
+        self.schedule = schedule or LRSchedule(lr)
+        self.tp_group, self.sp_group, self.mp_group, self.embed_group = (
+            tp_group, sp_group, mp_group, embed_group)
+        dev = flat.device
+        self.device = dev
+        # ---- shard geometry: rank r owns slice r of every bucket
+        self.slices = []  # (bucket, flat_start, shard_off, n)
+        off = 0
+        for b in flat.buckets:
+            n = b.size // self.world
+            assert n % ALIGN == 0
+            self.slices.append((b, b.start + self.rank * n, off, n))
+            off += n
+        self.shard_numel = off
+        if self.world == 1:
+            self.grad_shard = flat.grad
+            self.param_shard = flat.data
+        else:
+            self.grad_shard = torch.zeros(off, dtype=flat.dtype, device=dev)
+            self.param_shard = torch.zeros(off, dtype=flat.dtype, device=dev)
+        self.master = torch.empty(off, dtype=torch.float32, device=dev)
+        self._refresh_master()
+        self.exp_avg = torch.zeros_like(self.master)
+        self.exp_avg_sq = torch.zeros_like(self.master)
+        # weight-decay and grad-norm inclusion flags per 64-element chunk of the shard
+        norm_flags = torch.zeros(flat.numel // ALIGN, dtype=torch.uint8)
+        for s in flat.specs:
+            o = flat.offsets[s.name] // ALIGN
+            n64 = (s.numel + ALIGN - 1) // ALIGN
+            count = True
+            if s.tp_duplicated and tp_rank != 0:
+                count = False
+            if s.name == "wte_head":  # tied copy on the last stage; counted on stage 0
+                count = False
+            norm_flags[o:o + n64] = 1 if count else 0
+        norm_flags = norm_flags.to(dev)
+        self.wd_flags = self._shard_of(flat.wd_flags)
+        self.norm_flags = self._shard_of(norm_flags)
+        self.hyper = torch.zeros(optim_ops.H_N, dtype=torch.float32, device=dev)
+        self.hyper_host = torch.zeros(optim_ops.H_N, dtype=torch.float32,
+                                      pin_memory=dev.type == "cuda")
+        self.normsq = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.step_count = 0
+        # ---- overlap bookkeeping
+        self.overlap = overlap and self.world > 1 and dev.type == "cuda"
+        self.comm_stream = torch.cuda.Stream(device=dev) if self.overlap else None
+        self.units_left: Dict[int, int] = {}
+        self._bucket_units = {b.index: set(b.units) for b in flat.buckets}
+        self._shared_buckets = {flat.unit_to_bucket[s.unit] for s in flat.specs if s.shared}
+        self._sp_names = [s.name for s in flat.specs if s.sp_reduce]
+        self.started = set()
+        self.reset_pending()
+
+    # ------------------------------------------------------------------ helpers
+    def _shard_of(self, per_chunk: torch.Tensor) -> torch.Tensor:
+        parts = [per_chunk[fs // ALIGN:(fs + n) // ALIGN] for (_, fs, _, n) in self.slices]
+        return torch.cat(parts) if len(parts) > 1 else parts[0].clone()
+
+    def _refresh_master(self):
+        for (_, fs, so, n) in self.slices:
+            self.master[so:so + n].copy_(self.flat.data[fs:fs + n].float())
+        if self.world > 1:
+            for (_, fs, so, n) in self.slices:
+                self.param_shard[so:so + n].copy_(self.flat.data[fs:fs + n])
+
+    def reset_pending(self):
+        self.units_left = {b: len(u) for b, u in self._bucket_units.items()}
+        self.started = set()
+
+    # ------------------------------------------------------------------ grad sync
+    def _sp_allreduce(self, bucket):
+        if self.sp_group is None:
+            return
+        for name in self._sp_names:
+            if self.flat.unit_to_bucket[self.flat.spec_by_name[name].unit] == bucket.index:
+                dist.all_reduce(self.flat.grads[name], group=self.sp_group)
+
+    def _start_bucket(self, bi: int):
+        if bi in self.started:
+            return
+        self.started.add(bi)
+        b = self.flat.buckets[bi]
+        if self.world == 1:
+            self._sp_allreduce(b)
+            return
+        (_, _, so, n) = self.slices[bi]
+        if self.overlap:
+            ev = torch.cuda.current_stream(self.device).record_event()
+            with torch.cuda.stream(self.comm_stream):
+                self.comm_stream.wait_event(ev)
+                self._sp_allreduce(b)
+                dist.reduce_scatter_tensor(self.grad_shard[so:so + n],
+                                           self.flat.grad[b.start:b.end], group=self.dp_group)
+        else:
+            self._sp_allreduce(b)
+            dist.reduce_scatter_tensor(self.grad_shard[so:so + n], self.flat.grad[b.start:b.end],
+                                       group=self.dp_group)
+
+    def unit_done(self, unit: int):
+        bi = self.flat.unit_to_bucket.get(unit)
+        if bi is None:
+            return
+        self.units_left[bi] -= 1
+        if self.units_left[bi] == 0 and bi not in self._shared_buckets:
+            self._start_bucket(bi)
+
+    def finish_grads(self):
+        """Complete every bucket's reduction (tied-embedding all-reduce first)."""
+        if self.embed_group is not None and dist.get_world_size(self.embed_group) > 1:
+            for s in self.flat.specs:
+                if s.shared == "word_embeddings":
+                    dist.all_reduce(self.flat.grads[s.name], group=self.embed_group)
+        for bi in range(len(self.flat.buckets)):
+            self._start_bucket(bi)
+        if self.overlap:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+
+    # ------------------------------------------------------------------ step
+    def set_hyper(self, lr: float):
+        t = self.step_count
+        b1, b2 = self.betas
+        h = self.hyper_host
+        h[optim_ops.H_LR] = lr
+        h[optim_ops.H_B1] = b1
+        h[optim_ops.H_B2] = b2
+        h[optim_ops.H_EPS] = self.eps
+        h[optim_ops.H_WD] = self.wd
+        h[optim_ops.H_BC1] = 1.0 - b1 ** t
+        h[optim_ops.H_BC2] = 1.0 - b2 ** t
+        h[optim_ops.H_GS] = 1.0 / self.world
+        h[optim_ops.H_CLIP] = self.clip if self.clip else 0.0
+        self.hyper.copy_(h, non_blocking=True)
+
+    def grad_norm_sq(self) -> torch.Tensor:
+        optim_ops.sumsq_bf16(self.grad_shard, 1.0 / self.world, out=self.normsq,
+                             flags=self.norm_flags)
+        if self.world > 1:
+            dist.all_reduce(self.normsq, group=self.dp_group)
+        if self.mp_group is not None and dist.get_world_size(self.mp_group) > 1:
+            dist.all_reduce(self.normsq, group=self.mp_group)
+        return self.normsq
+
+    def step(self, lr: Optional[float] = None):
+        self.finish_grads()
+        self.step_count += 1
+        self.set_hyper(lr if lr is not None else self.schedule(self.step_count))
+        normsq = self.grad_norm_sq()
+        optim_ops.adamw_step(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
+                             self.param_shard, self.hyper, normsq=normsq, wd_flags=self.wd_flags)
+        if self.world > 1:
+            for (b, fs, so, n) in self.slices:
+                dist.all_gather_into_tensor(self.flat.data[b.start:b.end],
+                                            self.param_shard[so:so + n], group=self.dp_group)
+        self.reset_pending()
+        return normsq
+
+    # ------------------------------------------------------------------ checkpoint
+    def shard_state(self) -> dict:
+        return {"master": self.master, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
+                "step": self.step_count}
+
+    def load_shard_state(self, sd: dict):
+        self.master.copy_(sd["master"])
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        self.step_count = int(sd["step"])
+        # re-materialise bf16 params from the master shard
+        for (b, fs, so, n) in self.slices:
+            self.param_shard[so:so + n].copy_(self.master[so:so + n].to(self.flat.dtype))
+        if self.world > 1:
+            for (b, fs, so, n) in self.slices:
+                dist.all_gather_into_tensor(self.flat.data[b.start:b.end],
+                                            self.param_shard[so:so + n], group=self.dp_group)

@@ -1,0 +1,197 @@
+"""GPT training engine: model stage + flat buffers + ZeRO-1 optimizer + schedules.
+
+This is the in-process replacement of the Megatron-DeepSpeed training loop the
+reference launches (`torchrun pretrain_gpt.py --deepspeed ...`,
+examples/megatron-deepspeed/gpt2_345m/pretrain-ddp-zero1.yaml:72-84):
+one process per MI355X, RCCL process groups for DP/TP/PP, micro-batch accumulation,
+1F1B pipeline schedule (parallel/pipeline.py), optional hipGraph capture of the whole
+step (`capture_graph=True`).
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .models.gpt import GPTConfig, GPTStage, gpt_param_specs
+from .ops.rng import DropoutSeed
+from .parallel import state as pstate
+from .parallel.buffers import FlatParams
+from .parallel.zero import DistributedOptimizer, LRSchedule
+
+
+@dataclass
+class TrainConfig:
+    micro_batch_size: int = 4
+    global_batch_size: Optional[int] = None   # default: micro * dp
+    lr: float = 1.5e-4
+    min_lr: float = 1e-5
+    lr_warmup_iters: int = 0
+    lr_decay_iters: Optional[int] = None
+    lr_decay_style: str = "cosine"
+    weight_decay: float = 0.01
+    adam_beta1: float = 0.9
+    adam_beta2: float = 0.999
+    adam_eps: float = 1e-8
+    clip_grad: float = 1.0
+    seed: int = 1234
+    overlap_grad_reduce: bool = True
+    bucket_numel: int = 40_000_000
+    capture_graph: bool = False
+
+
+class GPTTrainer:
+    def __init__(self, cfg: GPTConfig, tcfg: TrainConfig, ps: Optional[pstate.ParallelState] = None,
+                 dtype: torch.dtype = torch.bfloat16):
+        self.cfg, self.tcfg = cfg, tcfg
+        self.ps = ps = ps or pstate.get()
+        self.device = ps.device
+        self.dtype = dtype
+        gb = tcfg.global_batch_size or tcfg.micro_batch_size * ps.dp
+        assert gb % (tcfg.micro_batch_size * ps.dp) == 0, "global batch must divide mbs*dp"
+        self.num_micro = gb // (tcfg.micro_batch_size * ps.dp)
+        self.global_batch = gb
+        specs = gpt_param_specs(cfg, ps.tp, ps.pp, ps.pp_rank, ps.sequence_parallel)
+        self.flat = FlatParams(specs, self.device, dtype, dp_world=ps.dp,
+                               bucket_numel=tcfg.bucket_numel)
+        gen = torch.Generator().manual_seed(tcfg.seed + 1000 * ps.pp_rank + 100 * ps.tp_rank)
+        self.flat.initialize(gen, cfg.num_layers)
+        self._sync_initial_params()
+        self.seed = DropoutSeed(self.device, tcfg.seed + 7 * ps.dp_rank)
+        self.stage = GPTStage(cfg, self.flat.params, self.flat.grads, tp=ps.tp, tp_rank=ps.tp_rank,
+                              tp_group=ps.tp_group, pp=ps.pp, pp_rank=ps.pp_rank,
+                              sequence_parallel=ps.sequence_parallel, seed_t=self.seed.t)
+        sched = LRSchedule(tcfg.lr, tcfg.min_lr, tcfg.lr_warmup_iters, tcfg.lr_decay_iters,
+                           tcfg.lr_decay_style)
+        self.opt = DistributedOptimizer(
+            self.flat, dp_group=ps.dp_group if ps.dp > 1 else None, lr=tcfg.lr,
+            betas=(tcfg.adam_beta1, tcfg.adam_beta2), eps=tcfg.adam_eps,
+            weight_decay=tcfg.weight_decay, clip_grad=tcfg.clip_grad,
+            overlap=tcfg.overlap_grad_reduce, tp_rank=ps.tp_rank, tp_group=ps.tp_group,
+            sp_group=ps.tp_group if ps.sequence_parallel else None,
+            mp_group=ps.mp_group if ps.tp * ps.pp > 1 else None,
+            embed_group=ps.embed_group if ps.pp > 1 and cfg.tie_embeddings else None,
+            pp_rank=ps.pp_rank, schedule=sched)
+        self.pipeline = None
+        if ps.pp > 1:
+            from .parallel.pipeline import PipelineSchedule
+            self.pipeline = PipelineSchedule(self)
+        self.iteration = 0
+        self._graph = None
+        self._static = None
+
+    # ------------------------------------------------------------------ init
+    def _sync_initial_params(self):
+        ps = self.ps
+        # DP replicas start identical (same generator seed per (pp, tp) already); tied
+        # embedding copy on the last stage starts from the first stage's table.
+        if ps.pp > 1 and self.cfg.tie_embeddings and ps.embed_group is not None:
+            name = "wte" if ps.is_first_stage else ("wte_head" if ps.is_last_stage else None)
+            if name is not None:
+                src = ps.pp_ranks[0]
+                dist.broadcast(self.flat.params[name], src=src, group=ps.embed_group)
+
+    # ------------------------------------------------------------------ step
+    def _micro_forward_backward(self, ids, labels, B, S, last_micro):
+        rt = self.stage.rt
+        rt.unit_done = self.opt.unit_done if last_micro else None
+        loss = self.stage.forward(ids=ids, labels=labels, B=B, S=S)
+        loss.backward()
+        return loss.detach()
+
+    def train_step(self, tokens: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        """tokens/labels: [num_micro, micro_batch, seq] int64 on device.  Returns the
+        mean loss over the step as a device scalar (last stage; 0 elsewhere)."""
+        if self._graph is not None:
+            self._static[0].copy_(tokens)
+            self._static[1].copy_(labels)
+            self.opt.set_hyper(self.opt.schedule(self.opt.step_count + 1))
+            self._graph.replay()
+            self.opt.step_count += 1
+            self.iteration += 1
+            return self._static_loss
+        return self._train_step_eager(tokens, labels)
+
+    def _train_step_eager(self, tokens, labels):
+        nm, B, S = tokens.shape
+        self.flat.zero_grad()
+        self.seed.advance()
+        self.stage.rt.grad_scale = 1.0 / (nm * B * S)
+        if self.pipeline is not None:
+            loss = self.pipeline.run(tokens, labels)
+        else:
+            loss = torch.zeros((), dtype=torch.float32, device=self.device)
+            for m in range(nm):
+                loss = loss + self._micro_forward_backward(tokens[m].reshape(-1),
+                                                           labels[m].reshape(-1), B, S,
+                                                           m == nm - 1)
+        self.opt.step()
+        self.iteration += 1
+        return loss
+
+    def capture(self, tokens, labels, warmup: int = 2):
+        """Capture one whole training step (fwd, bwd, grad reduce, optimizer) into a
+        hipGraph; later steps replay it (no per-kernel launch cost)."""
+        assert self.device.type == "cuda"
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._train_step_eager(tokens, labels)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self._static = (tokens.clone(), labels.clone())
+        g = torch.cuda.CUDAGraph()
+        # the optimizer step counter / hyper-parameters are host-driven: set_hyper copies
+        # from a pinned buffer that the captured memcpy re-reads on every replay
+        step0 = self.opt.step_count
+        with torch.cuda.graph(g, stream=s):
+            loss = self._graph_body()
+        self.opt.step_count = step0
+        self._graph = g
+        self._static_loss = loss
+        return g
+
+    def _graph_body(self):
+        tokens, labels = self._static
+        nm, B, S = tokens.shape
+        self.flat.zero_grad()
+        self.seed.advance()
+        self.stage.rt.grad_scale = 1.0 / (nm * B * S)
+        if self.pipeline is not None:
+            loss = self.pipeline.run(tokens, labels)
+        else:
+            loss = torch.zeros((), dtype=torch.float32, device=self.device)
+            for m in range(nm):
+                loss = loss + self._micro_forward_backward(tokens[m].reshape(-1),
+                                                           labels[m].reshape(-1), B, S,
+                                                           m == nm - 1)
+        # optimizer body without host-side hyper update (done before each replay)
+        o = self.opt
+        o.finish_grads()
+        normsq = o.grad_norm_sq()
+        from .ops import optim as optim_ops
+        optim_ops.adamw_step(o.master, o.exp_avg, o.exp_avg_sq, o.grad_shard, o.param_shard,
+                             o.hyper, normsq=normsq, wd_flags=o.wd_flags)
+        if o.world > 1:
+            for (b, fs, so, n) in o.slices:
+                dist.all_gather_into_tensor(self.flat.data[b.start:b.end],
+                                            o.param_shard[so:so + n], group=o.dp_group)
+        o.reset_pending()
+        return loss
+
+    # ------------------------------------------------------------------ utils
+    def tokens_per_step(self):
+        return self.global_batch * self.cfg.seq_length
+
+
+def synthetic_batch(cfg: GPTConfig, num_micro: int, micro_batch: int, device, generator=None):
+    """Synthetic token stream of the configured shape (no dataset on the box)."""
+    x = torch.randint(0, cfg.vocab_size, (num_micro, micro_batch, cfg.seq_length + 1),
+                      generator=generator, dtype=torch.int64)
+    x = x.to(device)
+    return x[..., :-1].contiguous(), x[..., 1:].contiguous()

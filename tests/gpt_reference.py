@@ -1,0 +1,44 @@
+"""Independent plain-PyTorch GPT used as the autograd oracle for mxtrain's hand-written
+layer backward (fp32, no fusion, torch SDPA math)."""
+import math
+
+import torch
+import torch.nn.functional as F
+
+
+def gelu_tanh(x):
+    return 0.5 * x * (1.0 + torch.tanh(0.7978845608028654 * (x + 0.044715 * x ** 3)))
+
+
+def ref_loss(P, ids, labels, cfg, B, S, head="wte"):
+    h = cfg.hidden_size
+    nh = cfg.num_attention_heads
+    D = h // nh
+    eps = cfg.layernorm_epsilon
+    x = P["wte"][ids]
+    if "wpe" in P:
+        x = x + P["wpe"][torch.arange(B * S) % S]
+
+    def ln(t, pre):
+        if cfg.normalization == "rmsnorm":
+            return t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True) + eps) * P[pre + "_w"]
+        return F.layer_norm(t, (h,), P[pre + "_w"], P[pre + "_b"], eps)
+
+    for i in range(cfg.num_layers):
+        p = f"layers.{i}."
+        a = ln(x, p + "ln1")
+        qkv = a @ P[p + "qkv_w"].t() + P[p + "qkv_b"]
+        q, k, v = qkv.split(h, dim=-1)
+        q = q.view(B, S, nh, D).transpose(1, 2)
+        k = k.view(B, S, nh, D).transpose(1, 2)
+        v = v.view(B, S, nh, D).transpose(1, 2)
+        s = (q @ k.transpose(-1, -2)) / math.sqrt(D)
+        s = s.masked_fill(torch.ones(S, S, dtype=torch.bool).triu(1), float("-inf"))
+        ctx = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * S, h)
+        x = x + ctx @ P[p + "proj_w"].t() + P[p + "proj_b"]
+        m = ln(x, p + "ln2")
+        f = gelu_tanh(m @ P[p + "fc1_w"].t() + P[p + "fc1_b"])
+        x = x + f @ P[p + "fc2_w"].t() + P[p + "fc2_b"]
+    xf = ln(x, "final_ln")
+    logits = xf @ P[head].t()
+    return F.cross_entropy(logits, labels)
