@@ -10,20 +10,24 @@
 // ([tokens, 3, heads, D] with a token stride), O is written [tokens, heads, D], so the
 // model needs no transposes.  lse is base-2: lse2 = max*c + log2(sum), c = scale*log2(e).
 //
-// Forward (one workgroup = 4 waves = 128 query rows of one (batch, head); K/V tiles
-// of 64 keys double-buffered in LDS by register staging, T14):
+// Forward (one workgroup = 8 waves = two 128-row query blocks of one (batch, head) --
+// for causal masks the mirrored pair (i, n-1-i), so every workgroup does identical work
+// and the grid is one workgroup per CU; K/V tiles of 64 keys double-buffered in LDS by
+// register staging, T14, shared by both halves):
 //   S^T = K * Q^T with v_mfma_f32_32x32x16_bf16 ("swapped" product: the query is on
 //   the lane, so the row max / row sum are lane-local plus one lane^32 exchange);
 //   O^T = V^T * P^T where the P accumulator registers feed the B operand directly
 //   (cdna_hip_programming.md §3 "accumulator tile as the next MFMA's operand") and V^T
 //   fragments come from ds_read_b64_tr_b16 (T10).  O stays query-on-lane, so the
 //   online-softmax rescale is lane-local.
-// Backward (one workgroup = 4 waves = 128 keys; each wave keeps dK^T/dV^T of its 32
-// keys in accumulators while sweeping 32-row query tiles): S and dP are computed
-// key-on-lane with -lse and -delta preloaded into the accumulators, so P and dS are
-// ready-made B operands of dV^T += dO^T P and dK^T += Q^T dS; dS crosses LDS once for
-// dQ = dS K (v_mfma_f32_16x16x32_bf16), which is summed over key blocks with fp32
-// global atomics (MI355X_MICROARCH.md "Global float atomics") and converted once.
+// Backward (one workgroup = 8 waves = 256 keys, again a mirrored causal pair of 128-key
+// blocks; each wave keeps dK^T/dV^T of its 32 keys in accumulators while sweeping 32-row
+// query tiles): S and dP are computed key-on-lane with -lse and -delta preloaded into
+// the accumulators, so P and dS are ready-made B operands of dV^T += dO^T P and
+// dK^T += Q^T dS; dS crosses LDS once for dQ = dS K (v_mfma_f32_16x16x32_bf16) over all
+// 256 keys, staged through LDS and summed over key blocks with row-contiguous fp32
+// global atomics (one 256-B wave-instruction per row: the full-rate shape of
+// MI355X_MICROARCH.md "Global float atomics"), converted to bf16 once.
 //
 // Every LDS tile uses a 16-B chunk XOR swizzle chosen so that both the row reads
 // (ds_read_b128 of 32 different rows) and the transposed reads (4 consecutive rows x
@@ -64,6 +68,14 @@ __device__ __forceinline__ int toff_k(int row, int chunk) {
   return row * (D * 2) + ((chunk ^ f) << 4);
 }
 
+// dS^T image [keys][32 q] bf16 (64-B rows): XOR of the 8-B unit with key bits {3, 2, 1^3}
+// makes both the 16-row ds_write_b64 groups and the transposed dQ-operand reads
+// conflict-free (checked by scripts/lds_banks.py).
+__device__ __forceinline__ int ds_off(int krow, int qbytes) {
+  const int f = ((krow >> 3) & 1) | (((krow >> 2) & 1) << 1) | ((((krow >> 1) ^ (krow >> 3)) & 1) << 2);
+  return krow * 64 + ((((qbytes >> 3) ^ f) << 3) | (qbytes & 7));
+}
+
 __device__ __forceinline__ bf16x4 tr_read(const char* lds, int byte_off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(lds + byte_off));
 }
@@ -92,25 +104,43 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 }
 
 // ============================================================================ forward
+// Workgroup = 8 waves = two 128-row query blocks.  Causal: the pair (i, nqb-1-i), so every
+// workgroup does the same number of K/V tiles (light block + its mirrored heavy block)
+// and the grid is exactly one workgroup per CU with no tail; the two halves share every
+// K/V tile staged in LDS.  Non-causal: blocks (2i, 2i+1).
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(
+// waves_per_eu(2,2): one 8-wave workgroup per CU is the design point, so let the
+// scheduler spend the full 256-VGPR budget on read batching instead of occupancy.
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, int ldq, int ldk, int ldv, uint16_t* __restrict__ o,
     int ldo, float* __restrict__ lse, int S, int Hq, int Hkv, const int* __restrict__ klen,
     float c /* scale*log2(e) */) {
-  constexpr int BQ = 128, BK = 64, NKK = D / 16, NDT = D / 32;
+  // 128-key K/V tiles: one tile of compute per wave must cover the HBM latency of the
+  // next tile's register-staged prefetch (64-key tiles left the loop latency-bound)
+  constexpr int BQ = 128, BK = 128, NSUB = BK / 32, NKK = D / 16, NDT = D / 32;
   constexpr int TILE = BK * D * 2;           // bytes of one K (or V) tile
   constexpr int CPR = D / 8;                 // 16-B chunks per row
-  constexpr int CH = BK * CPR / 256;         // chunks per thread per tile
+  constexpr int CH = BK * CPR / 512;         // chunks per thread per tile
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wl = w & 3, half = w >> 2;
   const int r = lane & 31, hh = lane >> 5, g = lane >> 4, gi = lane & 15;
-  const int qb = CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x;  // heavy blocks first
+  const int nqb = (S + BQ - 1) / BQ;
+  const int pair = blockIdx.x;
+  int qb_mine, qb_other;
+  if (CAUSAL) {
+    const int a = pair, bq = nqb - 1 - pair;
+    qb_mine = half ? bq : a;
+    qb_other = half ? a : bq;
+  } else {
+    qb_mine = 2 * pair + half;
+    qb_other = 2 * pair + (half ^ 1);
+  }
+  const bool half_on = qb_mine < nqb && !(CAUSAL && half == 1 && qb_mine == qb_other);
   const int hq = blockIdx.y, b = blockIdx.z;
   const int hk = hq / (Hq / Hkv);
-  const int q0 = qb * BQ;
-  const int qw = q0 + 32 * w;
+  const int qw = qb_mine * BQ + 32 * wl;
   const int kl = klen ? klen[b] : S;
   const int qrow = qw + r;
 
@@ -119,37 +149,48 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
     const uint16_t* qp = q + (size_t)(b * S + qrow) * ldq + hq * D + 8 * hh;
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk)
-      qf[kk] = qrow < S ? ld8(qp + 16 * kk) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      qf[kk] = (half_on && qrow < S) ? ld8(qp + 16 * kk) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
   int kv_end = kl;
-  if (CAUSAL) kv_end = min(kv_end, min(S, q0 + BQ));
+  if (CAUSAL) {
+    const int last_q = (max(qb_mine, qb_other < nqb ? qb_other : 0) + 1) * BQ;
+    kv_end = min(kv_end, min(S, last_q));
+  }
   const int nt = (kv_end + BK - 1) / BK;
 
   const uint16_t* kbase = k + (size_t)b * S * ldk + hk * D;
   const uint16_t* vbase = v + (size_t)b * S * ldv + hk * D;
-  uint4 kreg[CH], vreg[CH];
-  auto gload = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const int ci = tid + 256 * i, row = ci / CPR, ch = ci % CPR, key = t * BK + row;
-      if (key < S) {
-        kreg[i] = *reinterpret_cast<const uint4*>(kbase + (size_t)key * ldk + ch * 8);
-        vreg[i] = *reinterpret_cast<const uint4*>(vbase + (size_t)key * ldv + ch * 8);
-      } else {
-        kreg[i] = make_uint4(0, 0, 0, 0);
-        vreg[i] = make_uint4(0, 0, 0, 0);
-      }
-    }
-  };
-  auto swrite = [&](int buf) {
-    char* kt = smem + buf * 2 * TILE;
-#pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const int ci = tid + 256 * i, row = ci / CPR, ch = ci % CPR;
-      *reinterpret_cast<uint4*>(kt + toff<D>(row, ch)) = kreg[i];
-      *reinterpret_cast<uint4*>(kt + TILE + toff<D>(row, ch)) = vreg[i];
-    }
-  };
+  // Staging: rows past S are clamped to S-1 (their scores are masked to -inf, so the
+  // duplicate rows only need to be finite) -> unconditional 16-B loads, no exec branches.
+  // Staging registers are named scalars (k0..k3 / v0..v3), not arrays: hipcc promoted the
+  // uint4 arrays to LDS / scratch instead of registers.
+  static_assert(CH == 2 || CH == 4, "staging assumes 2 or 4 chunks per thread");
+  uint4 k0, k1, k2, k3, v0, v1, v2, v3;
+  const int srow = tid / CPR, sch = tid % CPR;       // chunk i: row srow + i*512/CPR
+  constexpr int RSTEP = 512 / CPR;
+  const int so0 = toff<D>(srow, sch), so1 = toff<D>(srow + RSTEP, sch);
+  const int so2 = toff<D>(srow + 2 * RSTEP, sch), so3 = toff<D>(srow + 3 * RSTEP, sch);
+#define FWD_LD1(I, T)                                                                    \
+  {                                                                                      \
+    const int key = min((T) * BK + srow + (I) * RSTEP, S - 1);                           \
+    k##I = *reinterpret_cast<const uint4*>(kbase + (size_t)key * ldk + sch * 8);         \
+    v##I = *reinterpret_cast<const uint4*>(vbase + (size_t)key * ldv + sch * 8);         \
+  }
+#define FWD_ST1(I, BUF)                                                                  \
+  {                                                                                      \
+    *reinterpret_cast<uint4*>(smem + (BUF) * 2 * TILE + so##I) = k##I;                   \
+    *reinterpret_cast<uint4*>(smem + (BUF) * 2 * TILE + TILE + so##I) = v##I;            \
+  }
+#define FWD_GLOAD(T)                                                                     \
+  {                                                                                      \
+    FWD_LD1(0, T) FWD_LD1(1, T)                                                          \
+    if constexpr (CH == 4) { FWD_LD1(2, T) FWD_LD1(3, T) }                               \
+  }
+#define FWD_SWRITE(BUF)                                                                  \
+  {                                                                                      \
+    FWD_ST1(0, BUF) FWD_ST1(1, BUF)                                                      \
+    if constexpr (CH == 4) { FWD_ST1(2, BUF) FWD_ST1(3, BUF) }                           \
+  }
 
   float m_i = -INFINITY, l_i = 0.f;
   f32x16 oacc[NDT];
@@ -157,85 +198,111 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(
   for (int dt = 0; dt < NDT; ++dt) oacc[dt] = f32x16{};
 
   if (nt > 0) {
-    gload(0);
-    swrite(0);
+    FWD_GLOAD(0);
+    FWD_SWRITE(0);
   }
   __syncthreads();
   for (int j = 0; j < nt; ++j) {
-    if (j + 1 < nt) gload(j + 1);
     const char* Kt = smem + (j & 1) * 2 * TILE;
     const char* Vt = Kt + TILE;
     const int kv0 = j * BK;
-    const bool active = !CAUSAL || kv0 <= qw + 31;
+    // causal: 32-key subtiles past this wave's last query are skipped outright
+    // (wave-uniform), so a 128-key tile costs only the subtiles it really needs
+    int nsub = NSUB;
+    if (CAUSAL) nsub = min(NSUB, max(0, (qw + 31 - kv0) / 32 + 1));
+    const bool active = half_on && qw < S && nsub > 0;
+    f32x16 sacc[NSUB];
     if (active) {
-      f32x16 sacc[2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        sacc[t] = f32x16{};
+      for (int t = 0; t < NSUB; ++t) {
+        if (t < nsub) {
+          bf16x8 kr[NKK];  // batch the subtile's K fragment reads ahead of its MFMAs
 #pragma unroll
-        for (int kk = 0; kk < NKK; ++kk)
-          sacc[t] = mfma32(lds8(Kt, toff<D>(32 * t + r, 2 * kk + hh)), qf[kk], sacc[t]);
+          for (int kk = 0; kk < NKK; ++kk) kr[kk] = lds8(Kt, toff<D>(32 * t + r, 2 * kk + hh));
+          sacc[t] = f32x16{};
+#pragma unroll
+          for (int kk = 0; kk < NKK; ++kk) sacc[t] = mfma32(kr[kk], qf[kk], sacc[t]);
+        }
       }
-      const bool need_mask = (CAUSAL && kv0 + BK - 1 > qw) || (kv0 + BK > kl);
+    }
+    // T14: the next tile's global loads are issued only after QK^T, so their latency
+    // hides under softmax + PV and no wait lands in front of the first MFMA
+    if (j + 1 < nt) { FWD_GLOAD(j + 1); }
+    if (active) {
+      const bool need_mask = (CAUSAL && kv0 + 32 * nsub - 1 > qw) || (kv0 + BK > kl);
       if (need_mask) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < NSUB; ++t) {
+          if (t < nsub) {
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int key = kv0 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * hh;
-            if (key >= kl || (CAUSAL && key > qrow)) sacc[t][e] = -INFINITY;
+            for (int e = 0; e < 16; ++e) {
+              const int key = kv0 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * hh;
+              const bool dead = key >= kl || (CAUSAL && key > qrow);
+              sacc[t][e] = dead ? -INFINITY : sacc[t][e];
+            }
           }
+        }
       }
       float mx = -INFINITY;
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < NSUB; ++t)
+        if (t < nsub) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sacc[t][e]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_i, mx);
-      float alpha = 1.f, mc = 0.f;
-      if (m_new != -INFINITY) {
-        alpha = __builtin_amdgcn_exp2f((m_i - m_new) * c);
-        mc = m_new * c;
+          for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sacc[t][e]);
+        }
+      mx = xhalf_max(mx);
+      // Exact deferred rescale (T13 with threshold 0): when no row of the wave raised its
+      // running max, alpha == 1 for every lane and the O / l rescale is skipped outright.
+      if (!__all(mx <= m_i)) {
+        const float m_new = fmaxf(m_i, mx);
+        const float alpha = m_new == -INFINITY ? 1.f : __builtin_amdgcn_exp2f((m_i - m_new) * c);
+        l_i *= alpha;
+        m_i = m_new;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) oacc[dt][e] *= alpha;
       }
+      const float mc = m_i == -INFINITY ? 0.f : m_i * c;
       float rs = 0.f;
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < NSUB; ++t)
+        if (t < nsub) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const float p = __builtin_amdgcn_exp2f(sacc[t][e] * c - mc);
-          sacc[t][e] = p;
-          rs += p;
+          for (int e = 0; e < 16; ++e) {
+            const float p = __builtin_amdgcn_exp2f(sacc[t][e] * c - mc);
+            sacc[t][e] = p;
+            rs += p;
+          }
         }
-      l_i = l_i * alpha + rs;
-      m_i = m_new;
+      l_i += rs;
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
+      for (int t = 0; t < NSUB; ++t)
+        if (t < nsub) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) oacc[dt][e] *= alpha;
+          for (int s = 0; s < 2; ++s) {
+            const int row0 = 32 * t + 16 * s + 4 * hh + (gi >> 2);
+            bf16x8 vr[NDT];  // batch the V^T fragment reads ahead of the MFMAs
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+            for (int dt = 0; dt < NDT; ++dt) {
+              const int col = 32 * dt + 16 * (g & 1) + 4 * (gi & 3);
+              const int within = (col & 7) * 2;
+              vr[dt] = cat(tr_read(Vt, toff<D>(row0, col >> 3) + within),
+                           tr_read(Vt, toff<D>(row0 + 8, col >> 3) + within));
+            }
+            const bf16x8 pb = pack_acc8(sacc[t], 8 * s);
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const bf16x8 pb = pack_acc8(sacc[t], 8 * s);
-          const int row0 = 32 * t + 16 * s + 4 * hh + (gi >> 2);
-#pragma unroll
-          for (int dt = 0; dt < NDT; ++dt) {
-            const int col = 32 * dt + 16 * (g & 1) + 4 * (gi & 3);
-            const int within = (col & 7) * 2;
-            const bf16x4 lo = tr_read(Vt, toff<D>(row0, col >> 3) + within);
-            const bf16x4 hi = tr_read(Vt, toff<D>(row0 + 8, col >> 3) + within);
-            oacc[dt] = mfma32(cat(lo, hi), pb, oacc[dt]);
+            for (int dt = 0; dt < NDT; ++dt) oacc[dt] = mfma32(vr[dt], pb, oacc[dt]);
           }
         }
     }
-    if (j + 1 < nt) swrite((j + 1) & 1);
+    if (j + 1 < nt) { FWD_SWRITE((j + 1) & 1); }
     __syncthreads();
   }
 
-  const float lt = l_i + __shfl_xor(l_i, 32, 64);
+  const float lt = xhalf_sum(l_i);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  if (qrow < S) {
+  if (half_on && qrow < S) {
     uint16_t* op = o + (size_t)(b * S + qrow) * ldo + hq * D;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
@@ -279,55 +346,83 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(
   }
 }
 
+// Workgroup = 8 waves = 256 keys: two 128-key blocks, causal pair (i, nkb-1-i) for equal
+// work per workgroup.  Each wave owns 32 keys (dK^T, dV^T in accumulators) and sweeps
+// 32-row query tiles.  Per tile:
+//   phase A  S, dP (key on the lane, -lse / -delta preloaded), P, dS, dV^T += dO^T P,
+//            dK^T += Q^T dS, dS^T -> LDS image                              | barrier
+//   phase B  dQ_tile = dS K over the 256 keys (16x16x32, one 16x16 tile per wave per
+//            16 d-columns) -> fp32 LDS image                                   | barrier
+//   phase C  row-contiguous fp32 atomics of the dQ image (one 256-B wave-instruction
+//            per row, the full-rate atomic shape) + staging of the next Q/dO tile | barrier
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_bwd_kernel(
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, int ldq, int ldk, int ldv,
     const uint16_t* __restrict__ dout, int lddo, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dq_acc, int lddq,
     uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, int lddk, int lddv, int S, int Hq,
     int Hkv, const int* __restrict__ klen, float c, float scale) {
-  constexpr int KB = 128, QT = 32, NKK = D / 16, NDT = D / 32;
-  constexpr int KTILE = KB * D * 2;  // bytes
+  constexpr int KB = 128, KW = 256, QT = 32, NKK = D / 16, NDT = D / 32;
+  constexpr int KTILE = KW * D * 2;  // bytes
   constexpr int QTILE = QT * D * 2;
   constexpr int CPR = D / 8;
-  constexpr int QCH = QT * CPR / 256;  // chunks per thread for a Q (or dO) tile: 1 or 2
-  constexpr int KCH = KB * CPR / 256;
+  constexpr int QCH = (QT * CPR + 511) / 512;  // chunks per thread for a Q (or dO) tile
+  constexpr int KCH = KW * CPR / 512;
+  constexpr int DQT = D / 64;                  // 16x16 dQ tiles per wave (8 waves, 2 q-halves)
   // LDS carve (one array, 16-B aligned offsets)
   constexpr int OFF_K = 0;
   constexpr int OFF_Q = OFF_K + KTILE;            // [2][QTILE]
   constexpr int OFF_DO = OFF_Q + 2 * QTILE;       // [2][QTILE]
-  constexpr int OFF_DS = OFF_DO + 2 * QTILE;      // [KB keys][QT q] bf16, 64-B rows
-  constexpr int OFF_L = OFF_DS + KB * QT * 2;     // [2][QT] float  (-lse2/c)
+  constexpr int OFF_DS = OFF_DO + 2 * QTILE;      // [KW keys][QT q] bf16, 64-B rows
+  constexpr int OFF_DQ = OFF_DS + KW * QT * 2;    // [QT][D+4] fp32
+  constexpr int DQS = D + 4;                      // padded dQ image row (2-way -> 1-way)
+  constexpr int OFF_L = OFF_DQ + QT * DQS * 4;    // [2][QT] float  (-lse2/c)
   constexpr int OFF_DL = OFF_L + 2 * QT * 4;      // [2][QT] float  (-delta)
   constexpr int LDS_BYTES = OFF_DL + 2 * QT * 4;
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wl = w & 3, half = w >> 2;
   const int r = lane & 31, hh = lane >> 5, g = lane >> 4, gi = lane & 15;
-  const int k0 = blockIdx.x * KB;
+  const int nkb = (S + KB - 1) / KB;
+  const int pair = blockIdx.x;
+  int kb_mine, kb_other;
+  if (CAUSAL) {
+    kb_mine = half ? nkb - 1 - pair : pair;
+    kb_other = half ? pair : nkb - 1 - pair;
+  } else {
+    kb_mine = 2 * pair + half;
+    kb_other = 2 * pair + (half ^ 1);
+  }
+  const bool half_on = kb_mine < nkb && !(CAUSAL && half == 1 && kb_mine == kb_other);
   const int hk = blockIdx.y, b = blockIdx.z;
   const int grp = Hq / Hkv;
   const int kl = klen ? klen[b] : S;
-  const int key = k0 + 32 * w + r;  // this lane's key (column of S / dP)
+  const int kw0 = kb_mine * KB + 32 * wl;  // first key of this wave
+  const int key = kw0 + r;                 // this lane's key (column of S / dP)
+  const bool key_ok = half_on && key < kl;
 
-  // K and V fragments of the wave's 32 keys (B operands of S = Q K^T, dP = dO V^T)
   bf16x8 kf[NKK], vf[NKK];
   {
+    const bool in = half_on && key < S;
     const uint16_t* kp = k + (size_t)(b * S + key) * ldk + hk * D + 8 * hh;
     const uint16_t* vp = v + (size_t)(b * S + key) * ldv + hk * D + 8 * hh;
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
-      kf[kk] = key < S ? ld8(kp + 16 * kk) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      vf[kk] = key < S ? ld8(vp + 16 * kk) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      kf[kk] = in ? ld8(kp + 16 * kk) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      vf[kk] = in ? ld8(vp + 16 * kk) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   }
-  // K tile of the whole block in LDS (transposed reads for dQ)
+  // K tile of both key blocks in LDS (rows 0-127: first block of the pair, 128-255: second)
 #pragma unroll
   for (int i = 0; i < KCH; ++i) {
-    const int ci = tid + 256 * i, row = ci / CPR, ch = ci % CPR, kk = k0 + row;
+    const int ci = tid + 512 * i, row = ci / CPR, ch = ci % CPR;
+    const int blk = (row < KB) ? (CAUSAL ? pair : 2 * pair) : (CAUSAL ? nkb - 1 - pair : 2 * pair + 1);
+    const int kk = blk * KB + (row & (KB - 1));
     uint4 val = make_uint4(0, 0, 0, 0);
-    if (kk < S) val = *reinterpret_cast<const uint4*>(k + (size_t)(b * S + kk) * ldk + hk * D + ch * 8);
+    const bool dup = CAUSAL && row >= KB && blk == pair;
+    if (blk < nkb && kk < S && !dup)
+      val = *reinterpret_cast<const uint4*>(k + (size_t)(b * S + kk) * ldk + hk * D + ch * 8);
     *reinterpret_cast<uint4*>(smem + OFF_K + toff_k<D>(row, ch)) = val;
   }
 
@@ -336,43 +431,49 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
   for (int dt = 0; dt < NDT; ++dt) { dvacc[dt] = f32x16{}; dkacc[dt] = f32x16{}; }
 
   const int nqt = (S + QT - 1) / QT;
-  const int qt0 = CAUSAL ? (k0 / QT) : 0;
+  const int first_kb = CAUSAL ? pair : 2 * pair;
+  const int qt0 = CAUSAL ? (first_kb * KB / QT) : 0;
   const int per_head = nqt - qt0;
   const int total = per_head * grp;
 
   uint4 qreg[QCH], dreg[QCH];
   float lreg = 0.f, dlreg = 0.f;
+  int lq = 0;
   auto gload = [&](int it) {
     const int hq = hk * grp + it / per_head;
     const int qs = (qt0 + it % per_head) * QT;
+    // rows past S are clamped (finite duplicates; their P is forced to 0 via lse=-inf)
 #pragma unroll
     for (int i = 0; i < QCH; ++i) {
-      const int ci = tid + 256 * i, row = ci / CPR, ch = ci % CPR, qq = qs + row;
-      if (qq < S) {
+      const int ci = tid + 512 * i, row = ci / CPR, ch = ci % CPR;
+      const int qq = min(qs + row, S - 1);
+      if (row < QT) {
         qreg[i] = *reinterpret_cast<const uint4*>(q + (size_t)(b * S + qq) * ldq + hq * D + ch * 8);
         dreg[i] = *reinterpret_cast<const uint4*>(dout + (size_t)(b * S + qq) * lddo + hq * D + ch * 8);
-      } else {
-        qreg[i] = make_uint4(0, 0, 0, 0);
-        dreg[i] = make_uint4(0, 0, 0, 0);
       }
     }
+    // raw loads only: any arithmetic on a just-loaded value here would make the compiler
+    // wait vmcnt(0) and serialise the whole prefetch; the conversion happens in swrite
     if (tid < QT) {
       const int qq = qs + tid;
-      const size_t li = ((size_t)b * Hq + hq) * S + qq;
-      lreg = qq < S ? -lse[li] / c : -INFINITY;
-      dlreg = qq < S ? -delta[li] : 0.f;
+      const size_t li = ((size_t)b * Hq + hq) * S + min(qq, S - 1);
+      lreg = lse[li];
+      dlreg = delta[li];
+      lq = qq;
     }
   };
   auto swrite = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < QCH; ++i) {
-      const int ci = tid + 256 * i, row = ci / CPR, ch = ci % CPR;
-      *reinterpret_cast<uint4*>(smem + OFF_Q + buf * QTILE + toff<D>(row, ch)) = qreg[i];
-      *reinterpret_cast<uint4*>(smem + OFF_DO + buf * QTILE + toff<D>(row, ch)) = dreg[i];
+      const int ci = tid + 512 * i, row = ci / CPR, ch = ci % CPR;
+      if (row < QT) {
+        *reinterpret_cast<uint4*>(smem + OFF_Q + buf * QTILE + toff<D>(row, ch)) = qreg[i];
+        *reinterpret_cast<uint4*>(smem + OFF_DO + buf * QTILE + toff<D>(row, ch)) = dreg[i];
+      }
     }
     if (tid < QT) {
-      reinterpret_cast<float*>(smem + OFF_L)[buf * QT + tid] = lreg;
-      reinterpret_cast<float*>(smem + OFF_DL)[buf * QT + tid] = dlreg;
+      reinterpret_cast<float*>(smem + OFF_L)[buf * QT + tid] = lq < S ? -lreg / c : -INFINITY;
+      reinterpret_cast<float*>(smem + OFF_DL)[buf * QT + tid] = lq < S ? -dlreg : 0.f;
     }
   };
 
@@ -381,6 +482,9 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
     swrite(0);
   }
   __syncthreads();
+  char* dsimg = smem + OFF_DS;
+  float* dqimg = reinterpret_cast<float*>(smem + OFF_DQ);
+  const int krow = KB * half + 32 * wl + r;  // this lane's row in the dS^T image / K tile
   for (int it = 0; it < total; ++it) {
     const int hq = hk * grp + it / per_head;
     const int qs = (qt0 + it % per_head) * QT;
@@ -390,8 +494,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
     const char* Ot = smem + OFF_DO + buf * QTILE;
     const float* Ls = reinterpret_cast<const float*>(smem + OFF_L) + buf * QT;
     const float* DLs = reinterpret_cast<const float*>(smem + OFF_DL) + buf * QT;
-    char* dsimg = smem + OFF_DS;
-    const bool active = !CAUSAL || (qs + QT - 1 >= k0 + 32 * w);
+    const bool active = half_on && kw0 < S && (!CAUSAL || qs + QT - 1 >= kw0);
+    // ---------------- phase A
     if (active) {
       f32x16 sacc, dpacc;
 #pragma unroll
@@ -400,22 +504,33 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
         sacc[e] = Ls[ql];
         dpacc[e] = DLs[ql];
       }
+      bf16x8 qr[NKK], orr[NKK];  // batch the row reads ahead of the MFMAs
 #pragma unroll
       for (int kk = 0; kk < NKK; ++kk) {
-        sacc = mfma32(lds8(Qt, toff<D>(r, 2 * kk + hh)), kf[kk], sacc);
-        dpacc = mfma32(lds8(Ot, toff<D>(r, 2 * kk + hh)), vf[kk], dpacc);
+        qr[kk] = lds8(Qt, toff<D>(r, 2 * kk + hh));
+        orr[kk] = lds8(Ot, toff<D>(r, 2 * kk + hh));
       }
-      // P = exp2(c*(S - lse2/c)); dS = P * (dP - delta)
-      const bool key_ok = key < kl;
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        sacc = mfma32(qr[kk], kf[kk], sacc);
+        dpacc = mfma32(orr[kk], vf[kk], dpacc);
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) sacc[e] = __builtin_amdgcn_exp2f(c * sacc[e]);
+      // masking only on diagonal / padded tiles (wave-uniform test), as selects
+      if ((CAUSAL && qs < kw0 + 31) || kw0 + 32 > kl) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int qq = qs + (e & 3) + 8 * (e >> 2) + 4 * hh;
+          const bool dead = !key_ok || (CAUSAL && key > qq);
+          sacc[e] = dead ? 0.f : sacc[e];
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int qq = qs + (e & 3) + 8 * (e >> 2) + 4 * hh;
-        float p = __builtin_amdgcn_exp2f(c * sacc[e]);
-        if (!key_ok || (CAUSAL && key > qq)) p = 0.f;
-        sacc[e] = p;
+        const float p = sacc[e];
         dpacc[e] = p * dpacc[e];
       }
-      // dV^T += dO^T P ;  dK^T += Q^T dS   (A operands by transposed reads)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const bf16x8 pb = pack_acc8(sacc, 8 * s);
@@ -433,67 +548,79 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(
           dkacc[dt] = mfma32(qtr, db, dkacc[dt]);
         }
       }
-      // dS^T image [key][q] (64-B rows, 32-B half swap on key bit 3)
-      const int krow = 32 * w + r;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int ql = 8 * g4 + 4 * hh;
         uint2 u;
         u.x = pack2(dpacc[4 * g4 + 0], dpacc[4 * g4 + 1]);
         u.y = pack2(dpacc[4 * g4 + 2], dpacc[4 * g4 + 3]);
-        *reinterpret_cast<uint2*>(dsimg + krow * 64 + ((ql * 2) ^ (((krow >> 3) & 1) << 5))) = u;
+        *reinterpret_cast<uint2*>(dsimg + ds_off(krow, ql * 2)) = u;
       }
     } else {
-      const int krow = 32 * w + r;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int ql = 8 * g4 + 4 * hh;
-        *reinterpret_cast<uint2*>(dsimg + krow * 64 + ((ql * 2) ^ (((krow >> 3) & 1) << 5))) =
-            make_uint2(0, 0);
+        *reinterpret_cast<uint2*>(dsimg + ds_off(krow, ql * 2)) = make_uint2(0, 0);
       }
     }
     __syncthreads();
-    // dQ[q][d] += dS[q][key] K[key][d] over the block's 128 keys (16x16x32 tiles)
+    // ---------------- phase B: dQ[q][d] = sum over 256 keys dS[q][key] K[key][d]
     {
-      constexpr int DTW = D / 32;  // 16-wide d tiles per wave
       const int qtile = w & 1;
-      f32x4 dq[DTW];
+      f32x4 dq[DQT];
 #pragma unroll
-      for (int i = 0; i < DTW; ++i) dq[i] = f32x4{};
+      for (int i = 0; i < DQT; ++i) dq[i] = f32x4{};
 #pragma unroll
-      for (int ks = 0; ks < KB / 32; ++ks) {
-        const int krow = 32 * ks + 8 * g + (gi >> 2);
+      for (int ks = 0; ks < KW / 32; ++ks) {
+        const int kr = 32 * ks + 8 * g + (gi >> 2);
         const int qcol = 16 * qtile + 4 * (gi & 3);
-        const int sw0 = ((krow >> 3) & 1) << 5, sw1 = (((krow + 4) >> 3) & 1) << 5;
-        const bf16x8 a = cat(tr_read(dsimg, krow * 64 + ((qcol * 2) ^ sw0)),
-                             tr_read(dsimg, (krow + 4) * 64 + ((qcol * 2) ^ sw1)));
+        const bf16x8 a = cat(tr_read(dsimg, ds_off(kr, qcol * 2)),
+                             tr_read(dsimg, ds_off(kr + 4, qcol * 2)));
 #pragma unroll
-        for (int i = 0; i < DTW; ++i) {
-          const int dtile = (w >> 1) * DTW + i;
+        for (int i = 0; i < DQT; ++i) {
+          const int dtile = (w >> 1) * DQT + i;
           const int dcol = 16 * dtile + 4 * (gi & 3);
           const int within = (dcol & 7) * 2;
-          const bf16x8 bk = cat(tr_read(smem + OFF_K, toff_k<D>(krow, dcol >> 3) + within),
-                                tr_read(smem + OFF_K, toff_k<D>(krow + 4, dcol >> 3) + within));
+          const bf16x8 bk = cat(tr_read(smem + OFF_K, toff_k<D>(kr, dcol >> 3) + within),
+                                tr_read(smem + OFF_K, toff_k<D>(kr + 4, dcol >> 3) + within));
           dq[i] = mfma16(a, bk, dq[i]);
         }
       }
       // C layout 16x16: col = lane&15 (d), row = (lane>>4)*4 + e (q)
 #pragma unroll
-      for (int i = 0; i < DTW; ++i) {
-        const int dtile = (w >> 1) * DTW + i;
+      for (int i = 0; i < DQT; ++i) {
+        const int dtile = (w >> 1) * DQT + i;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int qq = qs + 16 * qtile + 4 * g + e;
-          if (qq < S)
-            atomicAdd(dq_acc + (size_t)(b * S + qq) * lddq + hq * D + 16 * dtile + gi, dq[i][e]);
+        for (int e = 0; e < 4; ++e) dqimg[(16 * qtile + 4 * g + e) * DQS + 16 * dtile + gi] = dq[i][e];
+      }
+    }
+    __syncthreads();
+    // ---------------- phase C: next-tile staging FIRST (its vmcnt wait must not cover the
+    // atomics), then row-contiguous fp32 atomics that stay in flight across the barrier
+    if (it + 1 < total) swrite((it + 1) & 1);
+    {
+      constexpr int RPW = QT / 8;       // rows per wave
+      constexpr int IPR = D / 64;       // 64-lane instructions per row
+      float vals[RPW][IPR];
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+        for (int ii = 0; ii < IPR; ++ii) vals[rr][ii] = dqimg[(w * RPW + rr) * DQS + 64 * ii + lane];
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) {
+        const int qq = qs + w * RPW + rr;
+        if (qq < S) {
+#pragma unroll
+          for (int ii = 0; ii < IPR; ++ii)
+            atomicAdd(dq_acc + (size_t)(b * S + qq) * lddq + hq * D + 64 * ii + lane,
+                      vals[rr][ii]);
         }
       }
     }
-    if (it + 1 < total) swrite((it + 1) & 1);
     __syncthreads();
   }
   // write dK (scaled) and dV for this lane's key: rows d = 32dt + 8g4 + 4hh + 0..3
-  if (key < S) {
+  if (half_on && key < S) {
     uint16_t* dkp = dk + (size_t)(b * S + key) * lddk + hk * D;
     uint16_t* dvp = dv + (size_t)(b * S + key) * lddv + hk * D;
 #pragma unroll
@@ -534,10 +661,10 @@ hipError_t fwd_dispatch(bool causal, dim3 grid, hipStream_t s, const uint16_t* q
                         uint16_t* o, int ldo, float* lse, int S, int Hq, int Hkv,
                         const int* klen, float c) {
   if (causal)
-    hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(256), 0, s, q, k, v, ldq, ldk,
+    hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(512), 0, s, q, k, v, ldq, ldk,
                        ldv, o, ldo, lse, S, Hq, Hkv, klen, c);
   else
-    hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), 0, s, q, k, v, ldq, ldk,
+    hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(512), 0, s, q, k, v, ldq, ldk,
                        ldv, o, ldo, lse, S, Hq, Hkv, klen, c);
   return hipGetLastError();
 }
@@ -549,11 +676,11 @@ hipError_t bwd_dispatch(bool causal, dim3 grid, hipStream_t s, const uint16_t* q
                         float* dq_acc, int lddq, uint16_t* dk, uint16_t* dv, int lddk, int lddv,
                         int S, int Hq, int Hkv, const int* klen, float c, float scale) {
   if (causal)
-    hipLaunchKernelGGL((attn_bwd_kernel<D, true>), grid, dim3(256), 0, s, q, k, v, ldq, ldk,
+    hipLaunchKernelGGL((attn_bwd_kernel<D, true>), grid, dim3(512), 0, s, q, k, v, ldq, ldk,
                        ldv, dout, lddo, lse, delta, dq_acc, lddq, dk, dv, lddk, lddv, S, Hq, Hkv,
                        klen, c, scale);
   else
-    hipLaunchKernelGGL((attn_bwd_kernel<D, false>), grid, dim3(256), 0, s, q, k, v, ldq, ldk,
+    hipLaunchKernelGGL((attn_bwd_kernel<D, false>), grid, dim3(512), 0, s, q, k, v, ldq, ldk,
                        ldv, dout, lddo, lse, delta, dq_acc, lddq, dk, dv, lddk, lddv, S, Hq, Hkv,
                        klen, c, scale);
   return hipGetLastError();
@@ -568,7 +695,8 @@ MX_EXPORT int mx_attn_fwd(const void* q, const void* k, const void* v, int ldq, 
                           int D, int causal, const int* klen, float scale, hipStream_t s) {
   if (Hq % Hkv) return hipErrorInvalidValue;
   const float c = scale * 1.4426950408889634f;
-  dim3 grid((S + 127) / 128, Hq, B);
+  const int nqb = (S + 127) / 128;
+  dim3 grid((nqb + 1) / 2, Hq, B);
   if (D == 64)
     return fwd_dispatch<64>(causal, grid, s, (const uint16_t*)q, (const uint16_t*)k,
                             (const uint16_t*)v, ldq, ldk, ldv, (uint16_t*)o, ldo, lse, S, Hq,
@@ -602,7 +730,8 @@ MX_EXPORT int mx_attn_bwd(const void* q, const void* k, const void* v, int ldq, 
     else
       return hipErrorInvalidValue;
   }
-  dim3 grid((S + 127) / 128, Hkv, B);
+  const int nkb = (S + 127) / 128;
+  dim3 grid((nkb + 1) / 2, Hkv, B);
   const int lddq_acc = Hq * D;
   hipError_t e;
   if (D == 64)

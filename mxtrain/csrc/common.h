@@ -28,8 +28,22 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(uint16_t, b);
 }
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (a per-element cast + shift/or
+// costs three VALU ops per pair)
 __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
+}
+// reductions across the two 32-lane halves of a wave (lane l <-> l^32) with one
+// v_permlane32_swap instead of ds_bpermute + address arithmetic
+__device__ __forceinline__ float xhalf_max(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 __device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
@@ -48,15 +62,31 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return v;
 }
 
+// Full-wave reductions without the LDS pipe: DPP quad permutes and 16-lane row
+// rotations, then v_permlane16_swap / v_permlane32_swap for the cross-row steps.
+// (__shfl_xor lowers to a chain of 6 dependent ds_bpermute round trips, which made the
+// norm kernels latency-bound: SQ_WAIT_INST_LDS dominated their wave cycles.)
+#define MX_DPP(v, ctrl) \
+  __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), (ctrl), 0xf, 0xf, false))
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
+  v += MX_DPP(v, 0xB1);   // quad_perm [1,0,3,2]
+  v += MX_DPP(v, 0x4E);   // quad_perm [2,3,0,1]
+  v += MX_DPP(v, 0x124);  // row_ror:4
+  v += MX_DPP(v, 0x128);  // row_ror:8   -> every lane holds its 16-lane row sum
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
-  return v;
+  v = fmaxf(v, MX_DPP(v, 0xB1));
+  v = fmaxf(v, MX_DPP(v, 0x4E));
+  v = fmaxf(v, MX_DPP(v, 0x124));
+  v = fmaxf(v, MX_DPP(v, 0x128));
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
 }
 
 // Counter-based RNG for dropout: a stateless 32-bit hash of (seed, element index).
@@ -75,17 +105,22 @@ __device__ __forceinline__ bool dropout_keep(uint64_t idx, uint32_t seed, uint32
   return h >= thresh;  // thresh = p * 2^32
 }
 
+// tanh via one v_exp + one v_rcp (libm tanhf is ~40 VALU ops and made the GeLU
+// kernels VALU-bound); saturates correctly for |u| -> inf.
+__device__ __forceinline__ float fast_tanh(float u) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * u));
+}
 // tanh-approximation GeLU (Megatron bias_gelu / HF "gelu_new")
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float u = k0 * x * (1.f + k1 * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+  return 0.5f * x * (1.f + fast_tanh(u));
 }
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float x2 = x * x;
   float u = k0 * x * (1.f + k1 * x2);
-  float t = tanhf(u);
+  float t = fast_tanh(u);
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
 }
 

@@ -57,18 +57,6 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
   for (int j = 0; j < 8; ++j) p[j] = acc[j];
 }
 
-__global__ __launch_bounds__(256) void colsum_fold_kernel(const float* __restrict__ partial,
-                                                          int nparts, int cols,
-                                                          uint16_t* __restrict__ out,
-                                                          int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
-  float s = 0.f;
-  for (int b = 0; b < nparts; ++b) s += partial[(size_t)b * cols + c];
-  if (accumulate) s += bf2f(out[c]);
-  out[c] = f2bf(s);
-}
-
 // ---------------------------------------------------------------- embedding
 // out[t] = wte[ids[t] - vocab_start] (+ wpe[t % seq]); rows outside the local vocab
 // shard are zero (vocab-parallel embedding; the TP all-reduce sums the shards).
@@ -248,7 +236,12 @@ MX_EXPORT int mx_bias_gelu_fwd(const void* x, const void* bias, void* y, int row
 
 MX_EXPORT int mx_bias_gelu_bwd_rows_per_block() { return 16; }
 
-// partial: ceil(rows/16) * cols floats.  dx may alias dy.
+extern "C" int mx_colsum_finalize(const float* partial, int nparts, int cols, int nvec, void* o0,
+                                  void* o1, void* o2, int accumulate, float* scratch,
+                                  hipStream_t s);
+
+// partial: ceil(rows/16)*cols floats + mx_colreduce_scratch(ceil(rows/16), cols) scratch
+// floats behind it.  dx may alias dy.
 MX_EXPORT int mx_bias_gelu_bwd(const void* dy, const void* x, const void* bias, void* dx,
                                void* dbias, int accumulate, float* partial, int rows, int cols,
                                hipStream_t s) {
@@ -258,8 +251,8 @@ MX_EXPORT int mx_bias_gelu_bwd(const void* dy, const void* x, const void* bias, 
                      (const uint16_t*)x, (const uint16_t*)bias, (uint16_t*)dx, rows, cols, rpb,
                      partial);
   if (dbias)
-    hipLaunchKernelGGL(colsum_fold_kernel, dim3((cols + 255) / 256), dim3(256), 0, s, partial,
-                       (int)grid.y, cols, (uint16_t*)dbias, accumulate);
+    return mx_colsum_finalize(partial, (int)grid.y, cols, 1, dbias, nullptr, nullptr,
+                              accumulate, partial + (size_t)grid.y * cols, s);
   return hipGetLastError();
 }
 

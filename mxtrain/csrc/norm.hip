@@ -9,9 +9,9 @@
 // Design (gfx950): one wave64 per row, each lane owns 8 contiguous bf16 per 512
 // columns (16-B vector loads, Guideline 13), statistics in fp32 through wave
 // shuffles only (no LDS, no barriers on the forward path).  Backward keeps the
-// per-column reductions (dgamma, dbeta, dbias) in an LDS fp32 slab per block
-// (conflict-free ds_add_f32: each wave-instruction touches 64 distinct columns),
-// dumps the slab to a [grid][3][cols] partial buffer, and a second tiny kernel
+// per-column reductions (dgamma, dbeta, dbias) in registers across the rows a wave
+// handles, folds them once per block into an LDS slab, dumps the slab to a
+// [grid][3][cols] partial buffer, and a deterministic two-level column reduction
 // folds the partials into the bf16 gradient buffers (optionally accumulating).
 #include "common.h"
 
@@ -117,7 +117,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
 
 // Backward.  dh = dres + LN'(dy);  if dx_drop: dx = dh * mask * keep_scale.
 // partial[blk][0][c] = sum dy*xhat, [1] = sum dy, [2] = sum dx.
-template <int NV, bool RMS>
+// REG (cols <= 2048): each lane keeps its columns' running sums in registers across all
+// rows it handles; the 4 waves fold them into the block's LDS slab once at the end
+// (4-way LDS atomics, once per column).  Wider rows use per-row LDS atomics.
+template <int NV, bool RMS, bool REG>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dres,
     const uint16_t* __restrict__ h, const float* __restrict__ mean_in,
@@ -132,7 +135,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   const int lane = threadIdx.x & 63;
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int nw = gridDim.x * 4;
-  float g[NV][8];
+  constexpr int NR = REG ? NV : 1;
+  float g[NV][8], ag[NR][8], ab[NR][8], ax[NR][8];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (lane + 64 * i) * 8;
@@ -142,6 +146,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       for (int j = 0; j < 8; ++j) g[i][j] = 0.f;
     }
   }
+#pragma unroll
+  for (int i = 0; i < NR; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { ag[i][j] = 0.f; ab[i][j] = 0.f; ax[i][j] = 0.f; }
   for (int row = wid; row < rows; row += nw) {
     const size_t base = (size_t)row * cols;
     const float mean = RMS ? 0.f : mean_in[row];
@@ -152,17 +160,22 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     for (int i = 0; i < NV; ++i) {
       const int c = (lane + 64 * i) * 8;
       if (c < cols) {
-        float hv[8], d[8];
+        float hv[8], dv[8];
         unpack8(*reinterpret_cast<const uint4*>(h + base + c), hv);
-        unpack8(*reinterpret_cast<const uint4*>(dy + base + c), d);
+        unpack8(*reinterpret_cast<const uint4*>(dy + base + c), dv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[i][j] = (hv[j] - mean) * rstd;
-          gy[i][j] = d[j] * g[i][j];
+          gy[i][j] = dv[j] * g[i][j];
           s1 += gy[i][j];
           s2 += gy[i][j] * xh[i][j];
-          atomicAdd(&slab[c + j], d[j] * xh[i][j]);
-          atomicAdd(&slab[cols + c + j], d[j]);
+          if constexpr (REG) {
+            ag[i][j] += dv[j] * xh[i][j];
+            ab[i][j] += dv[j];
+          } else {
+            atomicAdd(&slab[c + j], dv[j] * xh[i][j]);
+            atomicAdd(&slab[cols + c + j], dv[j]);
+          }
         }
       } else {
 #pragma unroll
@@ -197,7 +210,24 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
           float dxr[8];
           unpack8(pk, dxr);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) atomicAdd(&slab[2 * cols + c + j], dxr[j]);
+          for (int j = 0; j < 8; ++j) {
+            if constexpr (REG) ax[i][j] += dxr[j];
+            else atomicAdd(&slab[2 * cols + c + j], dxr[j]);
+          }
+        }
+      }
+    }
+  }
+  if constexpr (REG) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (lane + 64 * i) * 8;
+      if (c < cols) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          atomicAdd(&slab[c + j], ag[i][j]);
+          atomicAdd(&slab[cols + c + j], ab[i][j]);
+          atomicAdd(&slab[2 * cols + c + j], ax[i][j]);
         }
       }
     }
@@ -207,24 +237,48 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   for (int i = threadIdx.x; i < 3 * cols; i += blockDim.x) out[i] = slab[i];
 }
 
-// out_k[c] (+)= sum_b partial[b][k][c]   for k in {0,1,2} with non-null out_k
-__global__ __launch_bounds__(256) void colsum_finalize_kernel(
-    const float* __restrict__ partial, int nparts, int cols, int nvec,
-    uint16_t* __restrict__ o0, uint16_t* __restrict__ o1, uint16_t* __restrict__ o2,
-    int accumulate) {
+}  // namespace
+
+// Deterministic two-level column reduction of fp32 partials [P][C] (shared by every
+// kernel that produces per-block column partials: LN/BDA backward, bias-GeLU backward,
+// bias column sums):
+//   level 1: groups of 64 partial rows -> [ceil(P/64)][C]  (grid C/256 x P/64)
+//   level 2: fold the groups, write bf16 (optionally adding); flat column c of the
+//            [nvec][cols] layout goes to output k = c / cols.
+namespace {
+__global__ __launch_bounds__(256) void colreduce_l1_kernel(const float* __restrict__ in, int P,
+                                                           int C, float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const int p0 = blockIdx.y * 64, p1 = min(P, p0 + 64);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int p = p0;
+  for (; p + 4 <= p1; p += 4) {
+    s0 += in[(size_t)p * C + c];
+    s1 += in[(size_t)(p + 1) * C + c];
+    s2 += in[(size_t)(p + 2) * C + c];
+    s3 += in[(size_t)(p + 3) * C + c];
+  }
+  for (; p < p1; ++p) s0 += in[(size_t)p * C + c];
+  out[(size_t)blockIdx.y * C + c] = (s0 + s1) + (s2 + s3);
+}
+
+__global__ __launch_bounds__(256) void colreduce_l2_kernel(
+    const float* __restrict__ in, int Q, int cols, int nvec, uint16_t* __restrict__ o0,
+    uint16_t* __restrict__ o1, uint16_t* __restrict__ o2, int accumulate) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= nvec * cols) return;
+  const int C = nvec * cols;
+  if (idx >= C) return;
   const int k = idx / cols, c = idx % cols;
   uint16_t* o = k == 0 ? o0 : (k == 1 ? o1 : o2);
   if (!o) return;
   float s = 0.f;
-  for (int b = 0; b < nparts; ++b) s += partial[((size_t)b * nvec + k) * cols + c];
+  for (int q = 0; q < Q; ++q) s += in[(size_t)q * C + idx];
   if (accumulate) s += bf2f(o[c]);
   o[c] = f2bf(s);
 }
 
-// Column sum of a bf16 matrix [rows, cols] -> bf16 [cols] (bias gradients of the
-// QKV projection).  Block = 256 threads covers 256*8 columns x a row stripe.
+// Column sum of a bf16 matrix [rows, cols] -> fp32 partials [rows/64][cols]
 __global__ __launch_bounds__(256) void colsum_partial_kernel(
     const uint16_t* __restrict__ x, int rows, int cols, int rows_per_block,
     float* __restrict__ partial) {
@@ -271,7 +325,7 @@ hipError_t launch_fwd(const void* x, const void* bias, const void* residual,
 }
 
 int bwd_grid(int rows) {
-  int g = (rows + 15) / 16;  // >= 4 rows per wave on average
+  int g = (rows + 7) / 8;  // 2 rows per wave
   if (g > 512) g = 512;
   if (g < 1) g = 1;
   return g;
@@ -289,7 +343,7 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
   size_t lds = (size_t)3 * cols * sizeof(float);
 #define MX_LNB_CASE(N)                                                                 \
   case N:                                                                              \
-    hipLaunchKernelGGL((ln_bwd_kernel<N, RMS>), grid, block, lds, s,                   \
+    hipLaunchKernelGGL((ln_bwd_kernel<N, RMS, (N <= 4)>), grid, block, lds, s,         \
                        (const uint16_t*)dy, (const uint16_t*)dres, (const uint16_t*)h, \
                        mean, rstd, (const uint16_t*)gamma, (uint16_t*)dh_out,          \
                        (uint16_t*)dx_drop, partial, rows, cols, thresh, ks, seed,      \
@@ -306,8 +360,28 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
 
 }  // namespace
 
-// number of partial slabs the backward kernels write (caller sizes `partial`)
+// number of partial slabs the norm backward writes (caller sizes `partial`)
 MX_EXPORT int mx_norm_bwd_nparts(int rows) { return bwd_grid(rows); }
+// floats of level-1 scratch needed to finalize P partial rows of C columns
+MX_EXPORT int64_t mx_colreduce_scratch(int P, int C) { return (int64_t)((P + 63) / 64) * C; }
+
+// fold fp32 partials [P][nvec*cols] into up to three bf16 outputs (deterministic)
+MX_EXPORT int mx_colsum_finalize(const float* partial, int nparts, int cols, int nvec,
+                                 void* o0, void* o1, void* o2, int accumulate, float* scratch,
+                                 hipStream_t s) {
+  const int C = nvec * cols;
+  const float* src = partial;
+  int Q = nparts;
+  if (nparts > 64) {
+    dim3 g1((C + 255) / 256, (nparts + 63) / 64);
+    hipLaunchKernelGGL(colreduce_l1_kernel, g1, dim3(256), 0, s, partial, nparts, C, scratch);
+    src = scratch;
+    Q = g1.y;
+  }
+  hipLaunchKernelGGL(colreduce_l2_kernel, dim3((C + 255) / 256), dim3(256), 0, s, src, Q, cols,
+                     nvec, (uint16_t*)o0, (uint16_t*)o1, (uint16_t*)o2, accumulate);
+  return hipGetLastError();
+}
 
 MX_EXPORT int mx_layernorm_fwd(const void* x, const void* gamma, const void* beta, void* y,
                                float* mean, float* rstd, int rows, int cols, float eps,
@@ -346,26 +420,15 @@ MX_EXPORT int mx_norm_bwd(const void* dy, const void* dres, const void* h, const
                            cols, p, seed, salt, s);
 }
 
-MX_EXPORT int mx_colsum_finalize(const float* partial, int nparts, int cols, int nvec,
-                                 void* o0, void* o1, void* o2, int accumulate,
-                                 hipStream_t s) {
-  int n = nvec * cols;
-  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s,
-                     partial, nparts, cols, nvec, (uint16_t*)o0, (uint16_t*)o1,
-                     (uint16_t*)o2, accumulate);
-  return hipGetLastError();
-}
-
-// bf16 column sum: `partial` must hold ceil(rows/rows_per_block) * cols floats
+// bf16 column sum: `partial` must hold ceil(rows/64)*cols floats plus
+// mx_colreduce_scratch(ceil(rows/64), cols) floats of scratch behind it
 MX_EXPORT int mx_colsum_bf16(const void* x, int rows, int cols, float* partial, void* out,
                              int accumulate, hipStream_t s) {
-  const int rpb = 64;
+  const int rpb = 16;  // 4x more blocks than 64-row stripes: the loads need the parallelism
   dim3 grid((cols / 8 + 255) / 256, (rows + rpb - 1) / rpb);
   hipLaunchKernelGGL(colsum_partial_kernel, grid, dim3(256), 0, s, (const uint16_t*)x, rows,
                      cols, rpb, partial);
-  int nparts = grid.y;
-  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((cols + 255) / 256), dim3(256), 0, s,
-                     partial, nparts, cols, 1, (uint16_t*)out, (uint16_t*)nullptr,
-                     (uint16_t*)nullptr, accumulate);
-  return hipGetLastError();
+  const int nparts = grid.y;
+  return mx_colsum_finalize(partial, nparts, cols, 1, out, nullptr, nullptr, accumulate,
+                            partial + (size_t)nparts * cols, s);
 }

@@ -33,7 +33,8 @@ SIGNATURES = {
     "mx_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
     "mx_bda_norm_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, F, P, U32, I, P],
     "mx_norm_bwd": [P, P, P, P, P, P, P, P, P, I, I, F, P, U32, I, P],
-    "mx_colsum_finalize": [P, I, I, I, P, P, P, I, P],
+    "mx_colsum_finalize": [P, I, I, I, P, P, P, I, P, P],
+    "mx_colreduce_scratch": [I, I],
     "mx_colsum_bf16": [P, I, I, P, P, I, P],
     # fused.hip
     "mx_bias_gelu_fwd": [P, P, P, I, I, P],
@@ -122,3 +123,9 @@ def call(name, *args):
 
 def query(name, *args) -> int:
     return getattr(_load(), name)(*args)
+
+
+def query64(name, *args) -> int:
+    fn = getattr(_load(), name)
+    fn.restype = ctypes.c_int64
+    return fn(*args)

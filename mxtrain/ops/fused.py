@@ -46,7 +46,9 @@ def bias_gelu_bwd(dy, x, bias, dbias=None, accumulate=False, inplace=False):
         return dx
     dx = dy if inplace else torch.empty_like(dy)
     rpb = _lib.query("mx_bias_gelu_bwd_rows_per_block")
-    partial = torch.empty(((rows + rpb - 1) // rpb) * cols, dtype=torch.float32, device=dy.device)
+    nparts = (rows + rpb - 1) // rpb
+    scratch_n = _lib.query64("mx_colreduce_scratch", nparts, cols)
+    partial = torch.empty(nparts * cols + scratch_n, dtype=torch.float32, device=dy.device)
     _lib.call("mx_bias_gelu_bwd", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(bias), _lib.ptr(dx),
               _lib.ptr(dbias), int(accumulate), _lib.ptr(partial), rows, cols, _lib.stream())
     return dx

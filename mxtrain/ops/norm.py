@@ -120,16 +120,18 @@ def norm_bwd(dy, dres, h, mean, rstd, gamma, want_dx=False, p=0.0, seed_t=None, 
                     buf.copy_(val.to(buf.dtype))
         return dh, dx
     nparts = _lib.query("mx_norm_bwd_nparts", rows)
-    partial = torch.empty(nparts * 3 * cols, dtype=torch.float32, device=dy.device)
+    scratch_n = _lib.query64("mx_colreduce_scratch", nparts, 3 * cols)
+    partial = torch.empty(nparts * 3 * cols + scratch_n, dtype=torch.float32, device=dy.device)
     dh = torch.empty_like(dy)
     dx = torch.empty_like(dy) if want_dx else None
     _lib.call("mx_norm_bwd", _lib.ptr(dy), _lib.ptr(dres), _lib.ptr(h), _lib.ptr(mean),
               _lib.ptr(rstd), _lib.ptr(gamma), _lib.ptr(dh), _lib.ptr(dx), _lib.ptr(partial),
               rows, cols, float(p), _lib.ptr(seed_t), salt, int(rms), _lib.stream())
     if dgamma is not None or dbeta is not None or dbias is not None:
+        scratch = partial[nparts * 3 * cols:]
         _lib.call("mx_colsum_finalize", _lib.ptr(partial), nparts, cols, 3, _lib.ptr(dgamma),
                   _lib.ptr(dbeta), _lib.ptr(dbias if want_dx else None), int(accumulate),
-                  _lib.stream())
+                  _lib.ptr(scratch), _lib.stream())
     return dh, dx
 
 
@@ -142,8 +144,9 @@ def colsum(x, out, accumulate=False):
             v = v + out.float()
         out.copy_(v.to(out.dtype))
         return out
-    nparts = (rows + 63) // 64
-    partial = torch.empty(nparts * cols, dtype=torch.float32, device=x.device)
+    nparts = (rows + 15) // 16
+    scratch_n = _lib.query64("mx_colreduce_scratch", nparts, cols)
+    partial = torch.empty(nparts * cols + scratch_n, dtype=torch.float32, device=x.device)
     _lib.call("mx_colsum_bf16", _lib.ptr(x), rows, cols, _lib.ptr(partial), _lib.ptr(out),
               int(accumulate), _lib.stream())
     return out
