@@ -37,7 +37,9 @@ class _Required(TemplateError):
 
 
 # ============================================================================ lexer
-_ACTION = re.compile(r"\{\{(-\s)?(.*?)(\s-)?\}\}", re.S)
+_ACTION = re.compile(
+    r"\{\{(?P<cl>-\s)?\s*/\*.*?\*/\s*(?P<cr>\s-)?\}\}"      # comment (may contain '}}')
+    r"|\{\{(?P<l>-\s)?(?P<body>.*?)(?P<r>\s-)?\}\}", re.S)
 
 
 def _lex(src: str) -> List[Tuple[str, str]]:
@@ -46,17 +48,16 @@ def _lex(src: str) -> List[Tuple[str, str]]:
     pos = 0
     for m in _ACTION.finditer(src):
         text = src[pos:m.start()]
-        if m.group(1):  # {{- trims preceding whitespace
+        if m.group("l") or m.group("cl"):  # {{- trims preceding whitespace
             text = text.rstrip(" \t\r\n")
         if out and out[-1][0] == "trimnext":
             out.pop()
             text = text.lstrip(" \t\r\n")
         if text:
             out.append(("text", text))
-        body = m.group(2).strip()
-        if not (body.startswith("/*") and body.endswith("*/")):
-            out.append(("action", body))
-        if m.group(3):
+        if m.group("body") is not None:
+            out.append(("action", m.group("body").strip()))
+        if m.group("r") or m.group("cr"):
             out.append(("trimnext", ""))
         pos = m.end()
     text = src[pos:]
@@ -536,7 +537,7 @@ class Engine:
         if name not in self.defines:
             raise TemplateError(f"template {name!r} not defined")
         s = _Scope()
-        s.declare("$", self.root)
+        s.declare("$", dot)  # Go: `$` inside a template is the data it was invoked with
         out: List[str] = []
         self._exec(self.defines[name], dot, s, out)
         return "".join(out)
@@ -633,7 +634,20 @@ class Engine:
                     return x
             return v
 
+        def index(obj, *keys):
+            for k in keys:
+                if obj is None:
+                    return None
+                if isinstance(obj, (list, tuple)):
+                    obj = obj[int(k)] if int(k) < len(obj) else None
+                elif isinstance(obj, dict):
+                    obj = obj.get(k)
+                else:
+                    obj = getattr(obj, str(k), None)
+            return obj
+
         return {
+            "index": index,
             "tpl": self._tpl,
             "include": lambda name, d=None: self.include(name, d),
             "required": required,

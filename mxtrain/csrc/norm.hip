@@ -129,8 +129,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     float* __restrict__ partial, int rows, int cols, uint32_t thresh, float keep_scale,
     const uint32_t* __restrict__ seed_ptr, uint32_t salt) {
   extern __shared__ __attribute__((aligned(16))) float slab[];  // [3][cols]
-  for (int i = threadIdx.x; i < 3 * cols; i += blockDim.x) slab[i] = 0.f;
-  __syncthreads();
+  if constexpr (!REG) {  // REG: [4 waves][3][cols] slabs, fully overwritten -> no zeroing
+    for (int i = threadIdx.x; i < 3 * cols; i += blockDim.x) slab[i] = 0.f;
+    __syncthreads();
+  }
   const uint32_t seed = seed_ptr ? (*seed_ptr + salt) : 0u;
   const int lane = threadIdx.x & 63;
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -218,23 +220,31 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       }
     }
   }
+  float* out = partial + (size_t)blockIdx.x * 3 * cols;
   if constexpr (REG) {
+    // every wave stores its register partials into its OWN slab with plain 16-B LDS
+    // stores (cross-wave ds_add_f32 atomics serialised the issue: SQ_WAIT_INST_LDS was
+    // ~half of all wave cycles), then the block folds the 4 slabs
+    float* my = slab + (threadIdx.x >> 6) * 3 * cols;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (lane + 64 * i) * 8;
       if (c < cols) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          atomicAdd(&slab[c + j], ag[i][j]);
-          atomicAdd(&slab[cols + c + j], ab[i][j]);
-          atomicAdd(&slab[2 * cols + c + j], ax[i][j]);
+        for (int j = 0; j < 8; j += 4) {
+          *reinterpret_cast<float4*>(my + c + j) = make_float4(ag[i][j], ag[i][j + 1], ag[i][j + 2], ag[i][j + 3]);
+          *reinterpret_cast<float4*>(my + cols + c + j) = make_float4(ab[i][j], ab[i][j + 1], ab[i][j + 2], ab[i][j + 3]);
+          *reinterpret_cast<float4*>(my + 2 * cols + c + j) = make_float4(ax[i][j], ax[i][j + 1], ax[i][j + 2], ax[i][j + 3]);
         }
       }
     }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * cols; i += blockDim.x)
+      out[i] = (slab[i] + slab[3 * cols + i]) + (slab[6 * cols + i] + slab[9 * cols + i]);
+  } else {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * cols; i += blockDim.x) out[i] = slab[i];
   }
-  __syncthreads();
-  float* out = partial + (size_t)blockIdx.x * 3 * cols;
-  for (int i = threadIdx.x; i < 3 * cols; i += blockDim.x) out[i] = slab[i];
 }
 
 }  // namespace
@@ -340,7 +350,7 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
   const uint32_t thresh = p > 0.f ? (uint32_t)((double)p * 4294967296.0) : 0u;
   const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
   dim3 grid(bwd_grid(rows)), block(256);
-  size_t lds = (size_t)3 * cols * sizeof(float);
+  const size_t lds = (size_t)(nv <= 4 ? 12 : 3) * cols * sizeof(float);
 #define MX_LNB_CASE(N)                                                                 \
   case N:                                                                              \
     hipLaunchKernelGGL((ln_bwd_kernel<N, RMS, (N <= 4)>), grid, block, lds, s,         \
@@ -420,8 +430,8 @@ MX_EXPORT int mx_norm_bwd(const void* dy, const void* dres, const void* h, const
                            cols, p, seed, salt, s);
 }
 
-// bf16 column sum: `partial` must hold ceil(rows/64)*cols floats plus
-// mx_colreduce_scratch(ceil(rows/64), cols) floats of scratch behind it
+// bf16 column sum: `partial` must hold ceil(rows/16)*cols floats plus
+// mx_colreduce_scratch(ceil(rows/16), cols) floats of scratch behind it
 MX_EXPORT int mx_colsum_bf16(const void* x, int rows, int cols, float* partial, void* out,
                              int accumulate, hipStream_t s) {
   const int rpb = 16;  // 4x more blocks than 64-row stripes: the loads need the parallelism
