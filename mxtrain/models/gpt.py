@@ -178,6 +178,45 @@ def gpt_param_specs(cfg: GPTConfig, tp: int = 1, pp: int = 1, pp_rank: int = 0,
     return specs
 
 
+def shard_gpt_state(global_sd: Dict[str, torch.Tensor], cfg: GPTConfig, tp: int = 1,
+                    tp_rank: int = 0, pp: int = 1, pp_rank: int = 0) -> Dict[str, torch.Tensor]:
+    """Map an unsharded (tp=1, pp=1) GPT state dict onto one (tp_rank, pp_rank) stage:
+    column-parallel weights (qkv, fc1, vocab) split on dim 0, row-parallel weights (proj,
+    fc2) on dim 1, everything else replicated; the tied LM head of a later pipeline stage
+    is a copy of the word embedding.  Used for TP/PP parity tests and checkpoint
+    re-partitioning."""
+    D = cfg.head_dim
+    H, KV = cfg.num_attention_heads, cfg.num_kv_heads
+    hl, kvl = H // tp, KV // tp
+    r = tp_rank
+    out = {}
+    for spec in gpt_param_specs(cfg, tp, pp, pp_rank):
+        name = spec.name
+        src = "wte" if name in ("wte_head",) else name
+        t = global_sd[src]
+        base = name.split(".")[-1]
+        if base in ("wte", "wte_head", "lm_head") or name in ("wte", "wte_head", "lm_head"):
+            V = spec.shape[0]
+            tt = torch.zeros(V * tp, t.shape[1], dtype=t.dtype)
+            tt[: t.shape[0]] = t[: V * tp]
+            t = tt[r * V:(r + 1) * V]
+        elif base in ("qkv_w", "qkv_b"):
+            q = t[: H * D]
+            k = t[H * D:(H + KV) * D]
+            v = t[(H + KV) * D:]
+            t = torch.cat([q[r * hl * D:(r + 1) * hl * D], k[r * kvl * D:(r + 1) * kvl * D],
+                           v[r * kvl * D:(r + 1) * kvl * D]], 0)
+        elif base in ("fc1_w", "fc1_b"):
+            n = t.shape[0] // tp
+            t = t[r * n:(r + 1) * n]
+        elif base in ("proj_w", "fc2_w"):
+            n = t.shape[1] // tp
+            t = t[:, r * n:(r + 1) * n]
+        out[name] = t.clone()
+        assert tuple(out[name].shape) == tuple(spec.shape), (name, out[name].shape, spec.shape)
+    return out
+
+
 # ============================================================================== runtime
 @dataclass
 class StepRuntime:
@@ -244,7 +283,10 @@ class EmbedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, anchor, ids, rt: StepRuntime, first_layer: int):
         P = rt.params
-        e = embed_fwd(ids, P["wte"], P.get("wpe"), seq=rt.S, vocab_start=rt.vocab_start)
+        # vocab-parallel: every TP rank gathers its vocab shard and the shards are summed
+        # by the all-reduce, so the (replicated) position table is added by rank 0 only
+        wpe = P.get("wpe") if rt.tp_rank == 0 else None
+        e = embed_fwd(ids, P["wte"], wpe, seq=rt.S, vocab_start=rt.vocab_start)
         if rt.tp > 1:
             C.all_reduce_(e, rt.tp_group)
             if rt.sp:

@@ -1,0 +1,128 @@
+"""1F1B pipeline-parallel schedule (P4, M9) over point-to-point RCCL send/recv.
+
+Replaces the DeepSpeed PipelineEngine that Megatron-DeepSpeed uses for
+`--pipeline-model-parallel-size 2` (examples/megatron-deepspeed/gpt2_345m/
+pretrain-ddp-tp-pp-zero1.yaml:40).  Stage s runs min(p - s - 1, m) warm-up forwards,
+then alternates one forward / one backward, then drains the remaining backwards.
+Activations travel as one contiguous [tokens, hidden] bf16 tensor per micro-batch
+(a single xGMI p2p transfer); the activation gradient travels back the same way.
+Each stage reports its gradient units to the DP optimizer only during the LAST
+micro-batch's backward, so bucket reduce-scatters overlap the pipeline drain.
+"""
+from __future__ import annotations
+
+from collections import deque
+from typing import TYPE_CHECKING
+
+import torch
+import torch.distributed as dist
+
+if TYPE_CHECKING:  # pragma: no cover
+    from ..training import GPTTrainer
+
+
+class PipelineSchedule:
+    def __init__(self, trainer: "GPTTrainer"):
+        self.tr = trainer
+        self.ps = trainer.ps
+
+    def _act_shape(self, B, S):
+        ps = self.ps
+        tokens = B * S
+        if ps.sequence_parallel:
+            tokens //= ps.tp
+        return (tokens, self.tr.cfg.hidden_size)
+
+    # ---------------------------------------------------------------- p2p primitives
+    # Opposite-direction transfers between a pair of stages are always posted together in
+    # one batch_isend_irecv, so blocking p2p can never deadlock in the steady state.
+    def _buf(self, shape):
+        return torch.empty(shape, dtype=self.tr.dtype, device=self.tr.device)
+
+    def _exchange(self, send_t=None, send_to=None, recv_shape=None, recv_from=None):
+        ops = []
+        rbuf = None
+        if send_t is not None:
+            ops.append(dist.P2POp(dist.isend, send_t.contiguous(), send_to))
+        if recv_shape is not None:
+            rbuf = self._buf(recv_shape)
+            ops.append(dist.P2POp(dist.irecv, rbuf, recv_from))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return rbuf
+
+    def run(self, tokens: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        tr, ps = self.tr, self.ps
+        stage = tr.stage
+        nm, B, S = tokens.shape
+        p, s = ps.pp, ps.pp_rank
+        shape = self._act_shape(B, S)
+        first, last = ps.is_first_stage, ps.is_last_stage
+        prev, nxt = ps.prev_rank(), ps.next_rank()
+        warm = min(p - s - 1, nm)
+        remaining = nm - warm
+        loss_total = torch.zeros((), dtype=torch.float32, device=tr.device)
+        inflight = deque()
+        fwd_i = 0
+        bwd_i = 0
+
+        def fwd(inp):
+            nonlocal fwd_i, loss_total
+            m = fwd_i
+            fwd_i += 1
+            if first:
+                out = stage.forward(ids=tokens[m].reshape(-1), labels=labels[m].reshape(-1), B=B, S=S)
+            else:
+                out = stage.forward(hidden=inp, labels=labels[m].reshape(-1), B=B, S=S)
+            if last:
+                loss_total = loss_total + out.detach()
+            inflight.append((inp, out))
+            return out
+
+        def bwd(out_grad):
+            nonlocal bwd_i
+            inp, out = inflight.popleft()
+            stage.rt.unit_done = tr.opt.unit_done if bwd_i == nm - 1 else None
+            bwd_i += 1
+            if last:
+                out.backward()
+            else:
+                torch.autograd.backward(out, grad_tensors=out_grad)
+            return None if first else inp.grad
+
+        def recv_forward():
+            if first:
+                return None
+            return self._exchange(recv_shape=shape, recv_from=prev).requires_grad_(True)
+
+        # warm-up forwards
+        for _ in range(warm):
+            out = fwd(recv_forward())
+            if not last:
+                self._exchange(send_t=out.detach(), send_to=nxt)
+        # steady state: 1F1B
+        inp = recv_forward() if remaining > 0 else None
+        for i in range(remaining):
+            out = fwd(inp)
+            out_grad = None
+            if not last:
+                out_grad = self._exchange(send_t=out.detach(), send_to=nxt, recv_shape=shape,
+                                          recv_from=nxt)
+            in_grad = bwd(out_grad)
+            if i == remaining - 1:
+                if not first:
+                    self._exchange(send_t=in_grad, send_to=prev)
+            else:
+                if first:
+                    inp = None
+                else:
+                    inp = self._exchange(send_t=in_grad, send_to=prev, recv_shape=shape,
+                                         recv_from=prev).requires_grad_(True)
+        # cool-down backwards
+        for _ in range(warm):
+            out_grad = None if last else self._exchange(recv_shape=shape, recv_from=nxt)
+            in_grad = bwd(out_grad)
+            if not first:
+                self._exchange(send_t=in_grad, send_to=prev)
+        return loss_total

@@ -1,0 +1,161 @@
+"""Distributed parity on CPU (gloo, 2 processes): DP+ZeRO-1, TP (+SP) and PP runs of the
+same GPT must reproduce the single-process loss and parameter updates (fp32, dropout 0).
+
+This is the CPU stand-in for the 8-GPU RCCL runs: every collective the GPU path issues
+(reduce-scatter, all-gather, all-reduce, batched p2p) goes through the same code with the
+gloo backend."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.dist
+
+CFG = dict(num_layers=2, hidden_size=64, num_attention_heads=4, seq_length=16,
+           max_position_embeddings=16, vocab_size=256, hidden_dropout=0.0)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data():
+    g = torch.Generator().manual_seed(7)
+    x = torch.randint(0, CFG["vocab_size"], (2, 2, CFG["seq_length"] + 1), generator=g)
+    return x[..., :-1].contiguous(), x[..., 1:].contiguous()
+
+
+def _reference(steps=2):
+    from mxtrain.models.gpt import GPTConfig
+    from mxtrain.parallel.state import ParallelState
+    from mxtrain.training import GPTTrainer, TrainConfig
+    cfg = GPTConfig(**CFG)
+    tr = GPTTrainer(cfg, TrainConfig(micro_batch_size=2, global_batch_size=4, lr=1e-3,
+                                     overlap_grad_reduce=False), ParallelState(),
+                    dtype=torch.float32)
+    tok, lab = _data()
+    losses = [float(tr.train_step(tok, lab)) for _ in range(steps)]
+    return losses, {n: p.clone() for n, p in tr.flat.params.items()}, tr.flat.state_dict()
+
+
+def _worker(rank, world, port, mode, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.manual_seed(0)
+    from mxtrain.models.gpt import GPTConfig, shard_gpt_state
+    from mxtrain.parallel import state as pstate
+    from mxtrain.training import GPTTrainer, TrainConfig
+    tp = 2 if mode in ("tp", "sp") else 1
+    pp = 2 if mode == "pp" else 1
+    ps = pstate.initialize_model_parallel(tp=tp, pp=pp, sequence_parallel=mode == "sp",
+                                          backend="gloo", device_type="cpu")
+    cfg = GPTConfig(**CFG)
+    # reference init (identical on every rank), then take this rank's shard
+    _, _, init_sd = _ref_init()
+    tcfg = TrainConfig(micro_batch_size=2, global_batch_size=4, lr=1e-3, overlap_grad_reduce=False)
+    tr = GPTTrainer(cfg, tcfg, ps, dtype=torch.float32)
+    local = shard_gpt_state(init_sd, cfg, ps.tp, ps.tp_rank, ps.pp, ps.pp_rank)
+    tr.flat.load_state_dict(local)
+    tr.opt._refresh_master()
+    tok, lab = _data()
+    if mode == "dp":
+        tok, lab = tok[rank:rank + 1], lab[rank:rank + 1]
+    losses = [float(tr.train_step(tok, lab)) for _ in range(2)]
+    # numpy copies: tensors sent through a spawn queue are fd-shared and vanish with the
+    # worker process
+    q.put((rank, mode, losses, {n: p.detach().clone().numpy() for n, p in tr.flat.params.items()},
+           (ps.tp_rank, ps.pp_rank, ps.dp_rank)))
+    pstate.destroy()
+
+
+_REF = {}
+
+
+def _ref_init():
+    if "init" not in _REF:
+        from mxtrain.models.gpt import GPTConfig
+        from mxtrain.parallel.state import ParallelState
+        from mxtrain.training import GPTTrainer, TrainConfig
+        cfg = GPTConfig(**CFG)
+        tr = GPTTrainer(cfg, TrainConfig(micro_batch_size=2, global_batch_size=4),
+                        ParallelState(), dtype=torch.float32)
+        _REF["init"] = (None, None, tr.flat.state_dict())
+    return _REF["init"]
+
+
+def _run(mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res = [(r, m, l, {n: torch.from_numpy(a) for n, a in p.items()}, ids) for r, m, l, p, ids in res]
+    return sorted(res, key=lambda t: t[0])
+
+
+@pytest.fixture(scope="module")
+def reference():
+    # the reference trainer must start from the same init the workers shard
+    from mxtrain.models.gpt import GPTConfig
+    from mxtrain.parallel.state import ParallelState
+    from mxtrain.training import GPTTrainer, TrainConfig
+    cfg = GPTConfig(**CFG)
+    _, _, init_sd = _ref_init()
+    tr = GPTTrainer(cfg, TrainConfig(micro_batch_size=2, global_batch_size=4, lr=1e-3,
+                                     overlap_grad_reduce=False), ParallelState(),
+                    dtype=torch.float32)
+    tr.flat.load_state_dict(init_sd)
+    tr.opt._refresh_master()
+    tok, lab = _data()
+    losses = [float(tr.train_step(tok, lab)) for _ in range(2)]
+    return cfg, losses, tr.flat.state_dict()
+
+
+def _check(mode, reference, loss_ranks):
+    from mxtrain.models.gpt import shard_gpt_state
+    cfg, ref_losses, ref_sd = reference
+    res = _run(mode)
+    for rank, _, losses, params, (tpr, ppr, dpr) in res:
+        if rank in loss_ranks:
+            for a, b in zip(losses, ref_losses):
+                assert abs(a - b) < 2e-5 * max(1.0, abs(b)), (mode, rank, losses, ref_losses)
+        exp = shard_gpt_state(ref_sd, cfg, 2 if mode in ("tp", "sp") else 1, tpr,
+                              2 if mode == "pp" else 1, ppr)
+        for n, t in exp.items():
+            assert torch.allclose(params[n], t, atol=3e-5, rtol=1e-4), (mode, rank, n,
+                                                                        (params[n] - t).abs().max())
+
+
+def test_dp_zero1_matches_single(reference):
+    # DP ranks report their own micro-batch loss; the parameters must match exactly
+    from mxtrain.models.gpt import shard_gpt_state
+    cfg, ref_losses, ref_sd = reference
+    res = _run("dp")
+    mean_first = sum(r[2][0] for r in res) / 2
+    assert abs(mean_first - ref_losses[0]) < 2e-5 * max(1.0, abs(ref_losses[0]))
+    for rank, _, losses, params, _ in res:
+        for n, t in ref_sd.items():
+            assert torch.allclose(params[n], t, atol=3e-5, rtol=1e-4), (rank, n)
+
+
+def test_tp2_matches_single(reference):
+    _check("tp", reference, loss_ranks=(0, 1))
+
+
+def test_tp2_sequence_parallel_matches_single(reference):
+    _check("sp", reference, loss_ranks=(0, 1))
+
+
+def test_pp2_1f1b_matches_single(reference):
+    _check("pp", reference, loss_ranks=(1,))
