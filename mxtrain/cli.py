@@ -1,0 +1,190 @@
+"""`mxtrain` command line -- the helm/kubectl surface of the reference, single node
+(README.md of the reference: `helm install --debug <rel> <chart> -f <values>`,
+`kubectl logs -f`, `helm uninstall`).
+
+    python -m mxtrain install <release> <chart> [-f values.yaml]... [--set k=v]... [--namespace ns] [--wait]
+    python -m mxtrain uninstall <release> [--namespace ns]
+    python -m mxtrain status <release> | list | logs <release> [--pod P] [-f]
+    python -m mxtrain template <release> <chart> [-f ...] [--set ...]     (render only, helm template)
+    python -m mxtrain lint <chart> [-f ...]
+    python -m mxtrain pipeline run <pipeline.yaml>                        (KFP chart pipeline)
+    python -m mxtrain node                                                (topology / GPU ledger)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+from .launch import release as rel
+
+
+def _add_values(p):
+    p.add_argument("-f", "--values", action="append", default=[], help="values YAML file (repeatable)")
+    p.add_argument("--set", action="append", default=[], help="k=v override (repeatable)")
+    p.add_argument("--set-string", action="append", default=[])
+    p.add_argument("-n", "--namespace", default=rel.DEFAULT_NS)
+
+
+def cmd_install(a):
+    st = rel.install(a.chart, a.release, a.namespace, a.values, a.set, a.set_string, wait=a.wait,
+                     timeout=a.timeout)
+    if a.debug:
+        print(open(os.path.join(rel.release_dir(a.release, a.namespace), "manifest.yaml")).read())
+    print(f"NAME: {a.release}\nNAMESPACE: {a.namespace}\nSTATUS: {st.get('phase')}")
+    if a.wait:
+        _print_resources(st)
+        return 0 if st.get("phase") == "Succeeded" else 1
+    return 0
+
+
+def _print_resources(st):
+    for rname, r in (st.get("resources") or {}).items():
+        print(f"  {rname}: {r.get('phase')} (restarts {r.get('restarts', 0)}) {r.get('message', '')}")
+        for pname, p in (r.get("pods") or {}).items():
+            print(f"    pod {pname}: {p.get('phase')} exit={p.get('exit_code')} gpus={p.get('gpus')}")
+
+
+def cmd_uninstall(a):
+    rel.uninstall(a.release, a.namespace)
+    print(f'release "{a.release}" uninstalled')
+    return 0
+
+
+def cmd_status(a):
+    st = rel.read_status(a.release, a.namespace)
+    if a.output == "json":
+        print(json.dumps(st, indent=1))
+    else:
+        print(f"NAME: {st['name']}\nNAMESPACE: {st['namespace']}\nSTATUS: {st.get('phase')}\n"
+              f"MESSAGE: {st.get('message', '')}")
+        _print_resources(st)
+    return 0
+
+
+def cmd_list(a):
+    rows = rel.list_releases(a.namespace if not a.all_namespaces else None)
+    print(f"{'NAME':24s} {'NAMESPACE':28s} {'STATUS':12s} CHART")
+    for st in rows:
+        print(f"{st['name']:24s} {st['namespace']:28s} {st.get('phase', ''):12s} {st.get('chart', '')}")
+    return 0
+
+
+def cmd_logs(a):
+    if not a.follow:
+        sys.stdout.write(rel.logs(a.release, a.namespace, a.pod))
+        return 0
+    d = os.path.join(rel.release_dir(a.release, a.namespace), "logs")
+    offsets = {}
+    while True:
+        if os.path.isdir(d):
+            for fn in sorted(os.listdir(d)):
+                if a.pod and not fn.startswith(a.pod):
+                    continue
+                p = os.path.join(d, fn)
+                with open(p, errors="replace") as f:
+                    f.seek(offsets.get(fn, 0))
+                    chunk = f.read()
+                    offsets[fn] = f.tell()
+                if chunk:
+                    sys.stdout.write(chunk)
+                    sys.stdout.flush()
+        try:
+            if rel.read_status(a.release, a.namespace).get("phase") in ("Succeeded", "Failed", "Terminated"):
+                return 0
+        except FileNotFoundError:
+            return 0
+        time.sleep(0.5)
+
+
+def cmd_template(a):
+    from .chart.render import load_chart, render_chart
+    r = render_chart(load_chart(a.chart), a.release, a.namespace, a.values, a.set, a.set_string)
+    sys.stdout.write(r.text)
+    return 0
+
+
+def cmd_lint(a):
+    from .chart.lint import lint_chart
+    problems = lint_chart(a.chart, a.values, a.set)
+    for p in problems:
+        print(p)
+    failed = any(p.startswith("[ERROR]") for p in problems)
+    print(f"1 chart(s) linted, {int(failed)} chart(s) failed")
+    return 1 if failed else 0
+
+
+def cmd_pipeline(a):
+    from .pipeline import load_pipeline, run_pipeline
+    res = run_pipeline(load_pipeline(a.file))
+    print(res)
+    return 0 if res == "Success" else 1
+
+
+def cmd_node(a):
+    from .runtime.topology import NODE_PROFILES, num_gpus
+    from .runtime.storage import mxtrain_home, pv_root
+    led = os.path.join(mxtrain_home(), "gpu-ledger.json")
+    print(json.dumps({"gpus": num_gpus(), "profile": f"mi355x.{num_gpus()}x", "pv_root": pv_root(),
+                      "ledger": json.load(open(led)) if os.path.exists(led) else {},
+                      "profiles": NODE_PROFILES}, indent=1))
+    return 0
+
+
+def build_parser():
+    p = argparse.ArgumentParser(prog="mxtrain")
+    sp = p.add_subparsers(dest="cmd", required=True)
+    q = sp.add_parser("install")
+    q.add_argument("release")
+    q.add_argument("chart")
+    _add_values(q)
+    q.add_argument("--wait", action="store_true", help="run in the foreground until the jobs finish")
+    q.add_argument("--timeout", type=float, default=None)
+    q.add_argument("--debug", action="store_true")
+    q.set_defaults(fn=cmd_install)
+    q = sp.add_parser("uninstall")
+    q.add_argument("release")
+    q.add_argument("-n", "--namespace", default=rel.DEFAULT_NS)
+    q.set_defaults(fn=cmd_uninstall)
+    q = sp.add_parser("status")
+    q.add_argument("release")
+    q.add_argument("-n", "--namespace", default=rel.DEFAULT_NS)
+    q.add_argument("-o", "--output", default="text")
+    q.set_defaults(fn=cmd_status)
+    q = sp.add_parser("list")
+    q.add_argument("-n", "--namespace", default=rel.DEFAULT_NS)
+    q.add_argument("-A", "--all-namespaces", action="store_true")
+    q.set_defaults(fn=cmd_list)
+    q = sp.add_parser("logs")
+    q.add_argument("release")
+    q.add_argument("--pod", default=None)
+    q.add_argument("-f", "--follow", action="store_true")
+    q.add_argument("-n", "--namespace", default=rel.DEFAULT_NS)
+    q.set_defaults(fn=cmd_logs)
+    q = sp.add_parser("template")
+    q.add_argument("release")
+    q.add_argument("chart")
+    _add_values(q)
+    q.set_defaults(fn=cmd_template)
+    q = sp.add_parser("lint")
+    q.add_argument("chart")
+    _add_values(q)
+    q.set_defaults(fn=cmd_lint)
+    q = sp.add_parser("pipeline")
+    q.add_argument("action", choices=["run"])
+    q.add_argument("file")
+    q.set_defaults(fn=cmd_pipeline)
+    q = sp.add_parser("node")
+    q.set_defaults(fn=cmd_node)
+    return p
+
+
+def main(argv=None):
+    a = build_parser().parse_args(argv)
+    sys.exit(a.fn(a))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,361 @@
+"""Job controllers: PyTorchJob (static + elastic), MPIJob, RayJob, Pod, Deployment.
+
+Single-node replacements of the Kubeflow training-operator, mpi-operator and kuberay
+(SURVEY §2.1 C20/C21/C21b, §3.1-§3.5, §5.3):
+
+* PyTorchJob -- Master + Worker replicas (or Worker-only elastic), every replica gets the
+  training-operator's env contract (PET_NNODES / PET_NPROC_PER_NODE / PET_NODE_RANK /
+  PET_MASTER_ADDR / PET_MASTER_PORT, or PET_RDZV_* for elastic), HOSTNAME
+  `pytorchjob-<rel>-master-0` / `-worker-<i>`, and a disjoint MI355X set (nproc_per_node
+  GPUs) through HIP_VISIBLE_DEVICES.  restartPolicy OnFailure + runPolicy.backoffLimit are
+  honoured as gang restarts; cleanPodPolicy Running stops the survivors when the job ends.
+* MPIJob -- the launcher's `mpirun ... /etc/config/train-script.sh` runs through
+  mxtrain.launch.mpirun (no ssh, no OpenMPI): np ranks on the worker replicas' slots.
+* RayJob -- head group + worker group are realised as a GPU pool; the entrypoint runs as
+  the driver with MXTRAIN_RAY_* env that mxtrain.raylike consumes.
+* Pod / Deployment -- data-prep and testing charts.
+"""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import time
+from typing import Dict, List, Optional
+
+from ..runtime.topology import GPUAllocator, gpus_requested
+from .pods import Pod, build_pod, materialize_configmaps, python_exe
+
+POLL = 0.25
+
+
+def free_port(preferred: Optional[int] = None) -> int:
+    if preferred:
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", int(preferred)))
+            s.close()
+            return int(preferred)
+        except OSError:
+            s.close()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class JobController:
+    kind = "Job"
+
+    def __init__(self, manifest: dict, manifests: List[dict], reldir: str, release: str,
+                 allocator: GPUAllocator, status_cb=None):
+        self.m = manifest
+        self.manifests = manifests
+        self.reldir = reldir
+        self.release = release
+        self.alloc = allocator
+        self.status_cb = status_cb
+        self.pods: List[Pod] = []
+        self.phase = "Pending"
+        self.restarts = 0
+        self.message = ""
+        self.cm_dirs = materialize_configmaps(manifests, reldir)
+        self.gpus: List[int] = []
+        self.mounts: Dict[str, str] = {}
+
+    @property
+    def name(self):
+        return self.m.get("metadata", {}).get("name", self.kind.lower())
+
+    # -- to implement
+    def create_pods(self) -> List[Pod]:
+        raise NotImplementedError
+
+    def done(self) -> Optional[str]:
+        """Return 'Succeeded' / 'Failed' when the job is finished, else None."""
+        raise NotImplementedError
+
+    # -- common machinery
+    def backoff_limit(self) -> int:
+        rp = (self.m.get("spec") or {}).get("runPolicy") or {}
+        return int(rp.get("backoffLimit", 0) or 0)
+
+    def restartable(self, pod: Pod) -> bool:
+        return pod.spec.restart_policy in ("OnFailure", "Always")
+
+    def status(self) -> dict:
+        return {"kind": self.kind, "name": self.name, "phase": self.phase, "restarts": self.restarts,
+                "message": self.message, "gpus": self.gpus, "mounts": self.mounts,
+                "pods": {p.spec.name: p.to_status() for p in self.pods}}
+
+    def _emit(self):
+        if self.status_cb:
+            self.status_cb(self)
+
+    def start(self):
+        self.pods = self.create_pods()
+        for p in self.pods:
+            p.start()
+        self.phase = "Running"
+        self._emit()
+
+    def stop(self):
+        for p in self.pods:
+            p.kill()
+
+    def release_gpus(self):
+        if self.gpus:
+            self.alloc.release(self.gpus)
+            self.gpus = []
+
+    def step(self) -> bool:
+        """One reconcile pass; returns True while the job is active."""
+        for p in self.pods:
+            p.poll()
+        verdict = self.done()
+        if verdict is None:
+            # a failed restartable replica -> gang restart within the backoff budget
+            failed = [p for p in self.pods if p.phase == "Failed"]
+            if failed:
+                if all(self.restartable(p) for p in failed) and self.restarts < self.backoff_limit():
+                    self.restarts += 1
+                    self.message = f"replica {failed[0].spec.name} failed (rc={failed[0].returncode}); restart {self.restarts}"
+                    for p in self.pods:
+                        p.kill()
+                    self._on_restart()
+                    for p in self.pods:
+                        p.restarts = self.restarts
+                        p.start()
+                else:
+                    verdict = "Failed"
+                    self.message = f"replica {failed[0].spec.name} failed (rc={failed[0].returncode})"
+        if verdict is not None:
+            self.phase = verdict
+            # cleanPodPolicy Running: stop replicas that are still alive
+            for p in self.pods:
+                p.kill()
+            self.release_gpus()
+            self._emit()
+            return False
+        self._emit()
+        return True
+
+    def _on_restart(self):
+        pass
+
+
+# ============================================================================ PyTorchJob
+class PyTorchJobController(JobController):
+    kind = "PyTorchJob"
+
+    def _replicas(self):
+        specs = (self.m.get("spec") or {}).get("pytorchReplicaSpecs") or {}
+        out = []
+        for role in ("Master", "Worker"):
+            rs = specs.get(role)
+            if rs:
+                out.append((role, int(rs.get("replicas", 1) or 0), rs))
+        return out
+
+    def _nproc(self, tmpl) -> int:
+        v = (self.m.get("spec") or {}).get("nprocPerNode")
+        c = ((tmpl.get("spec") or {}).get("containers") or [{}])[0]
+        req = gpus_requested(c.get("resources"))
+        if v in (None, "", "auto", "gpu", "None"):
+            return max(req, 1)
+        if v == "cpu":
+            return 1
+        return int(v)
+
+    def create_pods(self):
+        reps = self._replicas()
+        elastic = (self.m.get("spec") or {}).get("elasticPolicy")
+        nnodes = sum(n for _, n, _ in reps)
+        self.master_port = free_port()
+        pods = []
+        node_rank = 0
+        for role, n, rs in reps:
+            tmpl = rs.get("template") or {}
+            nproc = self._nproc(tmpl)
+            for i in range(n):
+                gpus = self.alloc.allocate(nproc) if self.alloc.total > 0 else []
+                self.gpus += gpus
+                env = {"PET_NPROC_PER_NODE": str(nproc), "PET_NODE_RANK": str(node_rank),
+                       "PET_MASTER_ADDR": "127.0.0.1", "PET_MASTER_PORT": str(self.master_port),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(self.master_port),
+                       "WORLD_SIZE": str(nnodes), "RANK": str(node_rank), "PET_NNODES": str(nnodes)}
+                if elastic:
+                    port = free_port(elastic.get("rdzvPort")) if node_rank == 0 else self.rdzv_port
+                    self.rdzv_port = port
+                    mn = elastic.get("minReplicas", nnodes)
+                    mx = elastic.get("maxReplicas", nnodes)
+                    env.update({"PET_NNODES": f"{mn}:{mx}" if mn != mx else str(mn),
+                                "PET_RDZV_BACKEND": str(elastic.get("rdzvBackend", "c10d")),
+                                "PET_RDZV_ENDPOINT": f"127.0.0.1:{port}",
+                                "PET_RDZV_ID": str(elastic.get("rdzvId", self.release)),
+                                "PET_MAX_RESTARTS": str(elastic.get("maxRestarts", 3))})
+                name = f"{self.name}-{role.lower()}-{i}"
+                spec, plan = build_pod(name, tmpl, self.reldir, self.cm_dirs, env, gpus,
+                                       rs.get("restartPolicy", "Never"), role=role, index=i)
+                self.mounts.update(plan.mounts)
+                pods.append(Pod(spec))
+                node_rank += 1
+        return pods
+
+    def done(self):
+        masters = [p for p in self.pods if p.spec.role == "Master"]
+        if masters:
+            if masters[0].phase == "Succeeded":
+                return "Succeeded"
+        elif self.pods and all(p.phase == "Succeeded" for p in self.pods):
+            return "Succeeded"
+        return None
+
+
+# ============================================================================ MPIJob
+class MPIJobController(JobController):
+    kind = "MPIJob"
+
+    def create_pods(self):
+        spec = self.m.get("spec") or {}
+        rs = spec.get("mpiReplicaSpecs") or {}
+        worker = rs.get("Worker") or {}
+        launcher = rs.get("Launcher") or {}
+        nworkers = int(worker.get("replicas", 1) or 1)
+        slots = int(spec.get("slotsPerWorker", 1) or 1)
+        wt = worker.get("template") or {}
+        per_worker_gpus = gpus_requested(((wt.get("spec") or {}).get("containers") or [{}])[0].get("resources"))
+        per_worker_gpus = per_worker_gpus or (slots if self.alloc.total else 0)
+        worker_sets = []
+        for i in range(nworkers):
+            g = self.alloc.allocate(min(per_worker_gpus, slots) if per_worker_gpus else 0) \
+                if self.alloc.total else []
+            self.gpus += g
+            worker_sets.append(g)
+        # resolve the worker pod (env, volumes, mounts) once; ranks inherit it
+        wspec, wplan = build_pod(f"{self.name}-worker-0", wt, self.reldir, self.cm_dirs, {}, [],
+                                 "Never", role="Worker")
+        self.mounts.update(wplan.mounts)
+        wfile = os.path.join(self.reldir, "mpi-workers.json")
+        with open(wfile, "w") as f:
+            json.dump({"workers": [{"name": f"{self.name}-worker-{i}", "gpus": worker_sets[i]}
+                                   for i in range(nworkers)],
+                       "slots": slots, "env": {k: v for k, v in wspec.env.items()
+                                               if k not in os.environ or os.environ[k] != v},
+                       "workdir": wspec.workdir, "mounts": wplan.mounts,
+                       "mount_mode": wplan.mode}, f, indent=1)
+        lt = launcher.get("template") or {}
+        lc = ((lt.get("spec") or {}).get("containers") or [{}])[0]
+        cmd = list(lc.get("command") or []) + list(lc.get("args") or [])
+        if cmd and os.path.basename(cmd[0]) == "mpirun":
+            cmd = [python_exe(), "-m", "mxtrain.launch.mpirun"] + cmd[1:]
+        env = {"MXTRAIN_MPI_WORKERS": wfile, "MXTRAIN_MPI_SLOTS": str(slots)}
+        # the launcher has no PVCs in the reference; resolve paths with the workers' plan
+        lspec, _ = build_pod(f"{self.name}-launcher", lt, self.reldir, self.cm_dirs, env, [],
+                             (lt.get("spec") or {}).get("restartPolicy", "OnFailure"),
+                             command_override=cmd, role="Launcher")
+        lspec.command = [wplan.rewrite(x) for x in lspec.command]
+        for k, v in list(lspec.env.items()):
+            lspec.env[k] = wplan.rewrite(v)
+        return [Pod(lspec)]
+
+    def done(self):
+        p = self.pods[0]
+        if p.phase == "Succeeded":
+            return "Succeeded"
+        return None
+
+
+# ============================================================================ RayJob
+class RayJobController(JobController):
+    kind = "RayJob"
+
+    def create_pods(self):
+        spec = self.m.get("spec") or {}
+        rc = spec.get("rayClusterSpec") or {}
+        head = (rc.get("headGroupSpec") or {}).get("template") or {}
+        groups = rc.get("workerGroupSpecs") or []
+        ngpu = 0
+        nworkers = 0
+        for g in groups:
+            reps = int(g.get("replicas", 1) or 0)
+            c = (((g.get("template") or {}).get("spec") or {}).get("containers") or [{}])[0]
+            ngpu += reps * gpus_requested(c.get("resources"))
+            nworkers += reps
+        gpus = self.alloc.allocate(min(ngpu, self.alloc.total)) if (ngpu and self.alloc.total) else []
+        self.gpus = gpus
+        env = {"MXTRAIN_RAY_NUM_WORKERS": str(max(nworkers, 1)),
+               "MXTRAIN_RAY_GPUS": ",".join(str(x) for x in gpus),
+               "RAY_ADDRESS": "mxtrain://127.0.0.1", "MXTRAIN_RAY_JOB": self.release}
+        rt = spec.get("runtimeEnvYAML")
+        if rt:
+            import yaml
+            renv = yaml.safe_load(rt) or {}
+            for k, v in (renv.get("env_vars") or {}).items():
+                env[k] = str(v)
+            if renv.get("pip"):
+                env["MXTRAIN_RAY_PIP_IGNORED"] = json.dumps(renv.get("pip"))
+        entry = spec.get("entrypoint") or ""
+        cmd = ["bash", "-c", entry] if entry else []
+        pspec, plan = build_pod(f"rayjob-{self.release}-submitter", head, self.reldir, self.cm_dirs,
+                                env, gpus, "Never", command_override=cmd, role="Submitter")
+        # the entrypoint is a shell line; rewrite mount prefixes inside it as well
+        pspec.command = [plan.rewrite(x) for x in pspec.command]
+        self.mounts.update(plan.mounts)
+        return [Pod(pspec)]
+
+    def done(self):
+        return "Succeeded" if self.pods[0].phase == "Succeeded" else None
+
+
+# ============================================================================ Pod / Deployment
+class PodController(JobController):
+    kind = "Pod"
+
+    def create_pods(self):
+        spec = self.m.get("spec") or {}
+        c = (spec.get("containers") or [{}])[0]
+        n = gpus_requested(c.get("resources"))
+        gpus = self.alloc.allocate(n) if (n and self.alloc.total) else []
+        self.gpus = gpus
+        pspec, plan = build_pod(self.name, {"spec": spec}, self.reldir, self.cm_dirs, {}, gpus,
+                                spec.get("restartPolicy", "Always"))
+        self.mounts.update(plan.mounts)
+        return [Pod(pspec)]
+
+    def done(self):
+        p = self.pods[0]
+        return "Succeeded" if p.phase == "Succeeded" else None
+
+
+class DeploymentController(JobController):
+    kind = "Deployment"
+
+    def create_pods(self):
+        spec = self.m.get("spec") or {}
+        tmpl = spec.get("template") or {}
+        n = int(spec.get("replicas", 1) or 1)
+        pods = []
+        for i in range(n):
+            for ci, c in enumerate((tmpl.get("spec") or {}).get("containers") or []):
+                ng = gpus_requested(c.get("resources"))
+                gpus = self.alloc.allocate(ng) if (ng and self.alloc.total) else []
+                self.gpus += gpus
+                pspec, plan = build_pod(f"{self.name}-{i}-{c.get('name', ci)}", tmpl, self.reldir,
+                                        self.cm_dirs, {}, gpus, "Always", container_index=ci)
+                self.mounts.update(plan.mounts)
+                pods.append(Pod(pspec))
+        return pods
+
+    def backoff_limit(self):
+        return 10
+
+    def done(self):
+        return None  # runs until uninstalled
+
+
+CONTROLLERS = {"PyTorchJob": PyTorchJobController, "MPIJob": MPIJobController,
+               "RayJob": RayJobController, "Pod": PodController, "Deployment": DeploymentController}
+PASSIVE_KINDS = {"ConfigMap", "Secret", "Service", "PersistentVolumeClaim", "PersistentVolume",
+                 "StorageClass", "ServiceAccount"}

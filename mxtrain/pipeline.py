@@ -1,0 +1,154 @@
+"""Sequential chart pipeline (replaces the KFP helm-charts component + pipeline;
+SURVEY §2.1 C52/C53, §3.6).
+
+``run_pipeline(chart_configs)`` installs each chart config in order, waits for every job
+resource of the release to finish and always uninstalls it; the first failure stops the
+pipeline and returns "Failure".  The chart-config keys are the reference component's:
+
+    release_name, namespace (default "default"), repo_url, path | chart (+ version, branch),
+    values (dict), timeout, pod_check_secs (300), pod_error_timeout (1800),
+    pod_complete_timeout (7 days)
+
+Differences from the reference, deliberately:
+* the exit code of install/wait is kept when uninstall succeeds (the reference's
+  ``exit_code = uninstall() and exit_code`` masks failures, helm_charts_component.py:38);
+* ``repo_url`` pointing at a remote git host resolves to this checkout (offline node);
+  a local directory or file:// URL is used as is;
+* polling is event-driven (status.json) instead of fixed 60 s sleeps; the *timeouts* keep
+  their meaning: Pending longer than pod_error_timeout or Running longer than
+  pod_complete_timeout fails the config.
+"""
+from __future__ import annotations
+
+import os
+import signal
+import sys
+import tempfile
+import time
+from typing import Dict, List
+
+import yaml
+
+from .launch import release as rel
+from .launch.pods import REPO_ROOT
+
+
+def resolve_chart(cfg: Dict) -> str:
+    repo = cfg.get("repo_url") or REPO_ROOT
+    if repo.startswith("file://"):
+        repo = repo[len("file://"):]
+    if not os.path.isdir(repo):
+        repo = REPO_ROOT        # remote git URL: the node is offline, use this checkout
+    if cfg.get("path"):
+        p = os.path.join(repo, cfg["path"])
+        if os.path.isdir(p):
+            return p
+        raise FileNotFoundError(f"chart path {cfg['path']} not found under {repo}")
+    chart = cfg.get("chart")
+    if not chart:
+        raise ValueError("chart config needs 'path' or 'chart'")
+    for root, dirs, files in os.walk(os.path.join(repo, "charts")):
+        if os.path.basename(root) == chart and "Chart.yaml" in files:
+            return root
+    raise FileNotFoundError(f"chart {chart} not found under {repo}/charts")
+
+
+class ChartHandler:
+    def __init__(self, cfg: Dict, log=print):
+        self.cfg = cfg
+        self.log = log
+        self.name = cfg["release_name"]
+        self.ns = cfg.get("namespace", "default")
+        self._installed = False
+
+    def __call__(self) -> int:
+        prev = {s: signal.signal(s, self._on_signal) for s in (signal.SIGINT, signal.SIGTERM)}
+        exit_code = 1
+        try:
+            exit_code = self.install()
+            if exit_code == 0:
+                exit_code = self.wait()
+        except Exception as e:  # noqa: BLE001 -- reported, counted as failure
+            self.log(f"{type(e).__name__}: {e}")
+            exit_code = 1
+        finally:
+            un = self.uninstall()
+            exit_code = exit_code or un
+            for s, h in prev.items():
+                signal.signal(s, h)
+        return exit_code
+
+    def _on_signal(self, signum, frame):
+        self.uninstall()
+        sys.exit(f"Signal: {signum}")
+
+    def install(self) -> int:
+        chart = resolve_chart(self.cfg)
+        files = []
+        if self.cfg.get("values"):
+            f = tempfile.NamedTemporaryFile("w", prefix="values", suffix=".yaml", delete=False)
+            yaml.safe_dump(self.cfg["values"], f, default_flow_style=False)
+            f.close()
+            files.append(f.name)
+        self.log(f"Install chart: {self.name} <- {chart}")
+        try:
+            rel.install(chart, self.name, self.ns, files)
+        except Exception as e:  # noqa: BLE001
+            self.log(f"Release {self.name} failed: {e}")
+            return 1
+        finally:
+            for f in files:
+                os.unlink(f)
+        self._installed = True
+        self.log(f"Release {self.name} successful")
+        return 0
+
+    def wait(self) -> int:
+        complete_timeout = float(self.cfg.get("pod_complete_timeout", 7 * 24 * 3600))
+        error_timeout = float(self.cfg.get("pod_error_timeout", 1800))
+        check = min(float(self.cfg.get("pod_check_secs", 300)), 1.0)
+        t0 = time.time()
+        while True:
+            try:
+                st = rel.read_status(self.name, self.ns)
+            except FileNotFoundError:
+                return 0     # deleted under us == Succeeded (reference semantics)
+            phase = st.get("phase")
+            if phase == "Succeeded":
+                return 0
+            if phase in ("Failed", "Unknown", "Terminated"):
+                self.log(f"release {self.name}: {phase} {st.get('message', '')}")
+                return 1
+            el = time.time() - t0
+            if phase == "Pending" and el > error_timeout:
+                return 1
+            if phase == "Running" and el > complete_timeout:
+                return 1
+            time.sleep(check)
+
+    def uninstall(self) -> int:
+        if not self._installed:
+            return 0
+        self._installed = False
+        try:
+            rel.uninstall(self.name, self.ns, keep_history=True)
+            self.log(f"Uninstall release: {self.name} successful")
+            return 0
+        except Exception as e:  # noqa: BLE001
+            self.log(f"Uninstall release: {self.name} failed: {e}")
+            return 1
+
+
+def run_pipeline(chart_configs: List[Dict], log=print) -> str:
+    for cfg in chart_configs:
+        if ChartHandler(cfg, log)() > 0:
+            return "Failure"
+    return "Success"
+
+
+def load_pipeline(path: str) -> List[Dict]:
+    with open(path) as f:
+        doc = yaml.safe_load(f)
+    if isinstance(doc, dict):
+        doc = doc.get("chart_configs", [])
+    return list(doc or [])

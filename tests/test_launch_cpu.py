@@ -1,0 +1,228 @@
+"""Launcher plumbing on CPU: chart -> release -> controllers -> replica processes.
+
+Covers the env contracts of the training-operator (PET_* / MASTER_* / HOSTNAME), elastic
+rendezvous env, OnFailure gang restarts within backoffLimit, the MPIJob mpirun emulation
+(OMPI_COMM_WORLD_* env, --output-filename files, --tag-output), the Pod kind
+(data-process), the KFP-style pipeline with the exit-code fix, and PVC path rewriting
+(SURVEY §2.3, §2.4, §3.1-§3.6, §5.3).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import yaml
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHARTS = os.path.join(REPO, "charts", "machine-learning")
+
+
+@pytest.fixture()
+def home(tmp_path, monkeypatch):
+    monkeypatch.setenv("MXTRAIN_HOME", str(tmp_path / "home"))
+    monkeypatch.setenv("MXTRAIN_NUM_GPUS", "0")
+    monkeypatch.setenv("MXTRAIN_PV_LINK", "0")   # never symlink /fsx on the test host
+    return tmp_path
+
+
+def _values(tmp_path, doc, name="v.yaml"):
+    p = tmp_path / name
+    p.write_text(yaml.safe_dump(doc))
+    return str(p)
+
+
+def _install(chart, rel_name, files, sets=(), timeout=120):
+    from mxtrain.launch import release as rel
+    return rel.install(os.path.join(CHARTS, chart), rel_name, value_files=files, sets=list(sets), wait=True,
+                       timeout=timeout)
+
+
+def _log(rel_name, pod):
+    from mxtrain.launch import release as rel
+    return rel.logs(rel_name, pod=pod)
+
+
+ENV_PROBE = ("import os,json; print('ENV', json.dumps({k: os.environ.get(k) for k in "
+             "['HOSTNAME','PET_NNODES','PET_NPROC_PER_NODE','PET_NODE_RANK','PET_MASTER_ADDR','PET_MASTER_PORT',"
+             "'PET_RDZV_ENDPOINT','PET_RDZV_ID','PET_RDZV_BACKEND','HOME','WORLD_SIZE','RANK']}))")
+
+
+def _env_from_log(text):
+    for line in text.splitlines():
+        if line.startswith("ENV "):
+            return json.loads(line[4:])
+    raise AssertionError(f"no ENV line in log:\n{text}")
+
+
+def test_pytorchjob_distributed_env_contract(home):
+    v = _values(home, {
+        "resources": {"nnodes": 3, "nproc_per_node": 2},
+        "pvc": [{"name": "pv-fsx", "mount_path": "/fsx"}, {"name": "pv-efs", "mount_path": "/efs"}],
+        "train": {"env": [{"name": "HOME", "value": "/efs/home/{{ .Release.Name }}"}],
+                  "command": ["python3"], "args": ["-c", f'"{ENV_PROBE}"']}})
+    st = _install("training/pytorchjob-distributed", "envtest", [v])
+    assert st["phase"] == "Succeeded", st
+    pods = st["resources"]["PyTorchJob/pytorchjob-envtest"]["pods"]
+    assert sorted(pods) == ["pytorchjob-envtest-master-0", "pytorchjob-envtest-worker-0", "pytorchjob-envtest-worker-1"]
+    ports = set()
+    for rank, pod in enumerate(sorted(pods)):
+        log = _log("envtest", pod)
+        assert "Training script done" in log
+        env = _env_from_log(log)
+        assert env["HOSTNAME"] == pod
+        assert env["PET_NNODES"] == "3" and env["PET_NPROC_PER_NODE"] == "2"
+        assert env["PET_NODE_RANK"] == str(rank)
+        assert env["PET_MASTER_ADDR"] == "127.0.0.1"
+        ports.add(env["PET_MASTER_PORT"])
+        # /efs is prefix-rewritten to the local PV root, layout below it unchanged
+        assert env["HOME"].endswith(os.path.join("pv", "pv-efs", "home", "envtest"))
+    assert len(ports) == 1
+
+
+def test_pytorchjob_elastic_env_contract(home):
+    v = _values(home, {
+        "resources": {"nnodes": 1, "nproc_per_node": 1},
+        "elastic_policy": {"rdzv_backend": "c10d", "rdzv_port": 0, "min_replicas": 1, "max_replicas": 2},
+        "train": {"command": ["python3"], "args": ["-c", f'"{ENV_PROBE}"']}})
+    st = _install("training/pytorchjob-elastic", "el", [v])
+    assert st["phase"] == "Succeeded", st
+    env = _env_from_log(_log("el", "pytorchjob-el-worker-0"))
+    assert env["PET_RDZV_ID"] == "el"
+    assert env["PET_RDZV_BACKEND"] == "c10d"
+    assert env["PET_RDZV_ENDPOINT"].startswith("127.0.0.1:")
+    assert env["PET_NNODES"] == "1:2"
+
+
+def test_gang_restart_within_backoff(home):
+    marker = home / "attempts"
+    cmd = (f"import os,sys; p='{marker}'; n=int(open(p).read()) if os.path.exists(p) else 0; "
+           f"open(p,'w').write(str(n+1)); sys.exit(0 if n>=2 else 3)")
+    v = _values(home, {"backoff_limit": 5, "resources": {"nnodes": 1},
+                       "train": {"command": ["python3"], "args": ["-c", f'"{cmd}"']}})
+    st = _install("training/pytorchjob-distributed", "rs", [v])
+    assert st["phase"] == "Succeeded", st
+    assert st["resources"]["PyTorchJob/pytorchjob-rs"]["restarts"] == 2
+    # exhausted budget -> Failed
+    marker.unlink()
+    v = _values(home, {"backoff_limit": 1, "resources": {"nnodes": 1},
+                       "train": {"command": ["python3"], "args": ["-c", f'"{cmd}"']}}, "v2.yaml")
+    st = _install("training/pytorchjob-distributed", "rs2", [v])
+    assert st["phase"] == "Failed"
+
+
+def test_failure_masked_by_echo_like_reference(home):
+    # the script contract: `cmd && echo done` is the last command -> exit status is the
+    # training command's (no post_script), so a failing command fails the replica.
+    v = _values(home, {"backoff_limit": 0, "resources": {"nnodes": 1},
+                       "train": {"command": ["false"]}})
+    st = _install("training/pytorchjob-distributed", "fail", [v])
+    assert st["phase"] == "Failed"
+
+
+def test_mpijob_ranks_and_output_files(home):
+    probe = ("import os; print('RANK', os.environ['OMPI_COMM_WORLD_RANK'], os.environ['OMPI_COMM_WORLD_SIZE'], "
+             "os.environ['OMPI_COMM_WORLD_LOCAL_RANK'], os.environ['HOSTNAME'], os.environ['HOME'])")
+    v = _values(home, {
+        "resources": {"gpu_nodes": 2, "gpus_per_node": 2, "gpu_instance_type": "mi355x.8x"},
+        "train": {"command": ["python3"], "args": ["-c", f'"{probe}"']}})
+    st = _install("training/mpijob-horovod-tensorflow-gpu", "mpi", [v])
+    assert st["phase"] == "Succeeded", st
+    log = _log("mpi", "mpijob-mpi-launcher")
+    rows = sorted(line.split("RANK ", 1)[1].split() for line in log.splitlines() if "<stdout>:RANK " in line)
+    assert [r[0] for r in rows] == ["0", "1", "2", "3"]
+    assert all(r[1] == "4" for r in rows)
+    assert [r[3] for r in rows] == ["mpijob-mpi-worker-0"] * 2 + ["mpijob-mpi-worker-1"] * 2
+    assert [r[2] for r in rows] == ["0", "1", "0", "1"]
+    assert "[1,0]<stdout>:" in log and "JOB MAP" in log
+    home_dir = rows[0][4]
+    outs = [d for d in os.listdir(os.path.join(home_dir, "logs")) if d.startswith("mpi-")]
+    assert len(outs) == 1
+    files = os.path.join(home_dir, "logs", outs[0], "1")
+    assert sorted(os.listdir(files)) == ["rank.0", "rank.1", "rank.2", "rank.3"]
+    assert "RANK 2" in open(os.path.join(files, "rank.2", "stdout")).read()
+
+
+def test_mpirun_abort_on_rank_failure(tmp_path):
+    script = tmp_path / "r.sh"
+    script.write_text("#!/bin/bash\nif [ $OMPI_COMM_WORLD_RANK = 1 ]; then exit 7; fi\nsleep 30\n")
+    script.chmod(0o755)
+    env = dict(os.environ, MXTRAIN_MPI_SLOTS="3", PYTHONPATH=REPO)
+    env.pop("MXTRAIN_MPI_WORKERS", None)
+    r = subprocess.run([sys.executable, "-m", "mxtrain.launch.mpirun", "-np", "3", str(script)], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 7
+    assert "Exit code:    7" in r.stderr
+
+
+def test_data_process_pod(home):
+    v = _values(home, {"pvc": [{"name": "pv-fsx", "mount_path": "/fsx"}],
+                       "pre_script": ["mkdir -p /fsx/data/x", "echo hello > /fsx/data/x/f.txt"],
+                       "process": {"command": ["cat"], "args": ["/fsx/data/x/f.txt"]}})
+    st = _install("data-prep/data-process", "dp", [v])
+    assert st["phase"] == "Succeeded", st
+    log = _log("dp", "data-process-dp")
+    assert "hello" in log and "Processing script done" in log
+    assert (home / "home" / "pv" / "pv-fsx" / "data" / "x" / "f.txt").exists()
+
+
+def test_pipeline_stops_on_failure_and_keeps_exit_code(home):
+    from mxtrain.launch import release as rel
+    from mxtrain.pipeline import run_pipeline
+    ok = {"release_name": "p1", "namespace": "default", "path": "charts/machine-learning/data-prep/data-process",
+          "values": {"process": {"command": ["true"]}}}
+    bad = {"release_name": "p2", "namespace": "default", "path": "charts/machine-learning/data-prep/data-process",
+           "values": {"process": {"command": ["false"]}}}
+    never = dict(ok, release_name="p3")
+    logs = []
+    assert run_pipeline([ok, bad, never], log=logs.append) == "Failure"
+    assert rel.read_status("p1", "default")["phase"] == "Uninstalled"
+    assert rel.read_status("p2", "default")["phase"] == "Uninstalled"
+    with pytest.raises(FileNotFoundError):
+        rel.read_status("p3", "default")
+    assert run_pipeline([ok], log=logs.append) == "Success"
+
+
+def test_cli_install_status_uninstall(home):
+    v = _values(home, {"resources": {"nnodes": 1}, "train": {"command": ["sleep"], "args": ["30"]}})
+    env = dict(os.environ, PYTHONPATH=REPO)
+    r = subprocess.run([sys.executable, "-m", "mxtrain", "install", "bg",
+                        os.path.join(CHARTS, "training/pytorchjob-distributed"), "-f", v],
+                       env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    from mxtrain.launch import release as rel
+    import time
+    t0 = time.time()
+    while rel.read_status("bg")["phase"] != "Running" and time.time() - t0 < 30:
+        time.sleep(0.2)
+    assert rel.read_status("bg")["phase"] == "Running"
+    pid = rel.read_status("bg")["resources"]["PyTorchJob/pytorchjob-bg"]["pods"]["pytorchjob-bg-master-0"]["pid"]
+    r = subprocess.run([sys.executable, "-m", "mxtrain", "uninstall", "bg"], env=env, capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    time.sleep(0.5)
+    with pytest.raises(ProcessLookupError):
+        os.kill(pid, 0)
+    assert not os.path.exists(rel.release_dir("bg"))
+
+
+def test_storage_rewrite_keeps_layout(tmp_path, monkeypatch):
+    from mxtrain.runtime.storage import plan_mounts
+    monkeypatch.setenv("MXTRAIN_PV_ROOT", str(tmp_path / "pv"))
+    plan = plan_mounts([{"name": "pv-1", "mountPath": "/fsx"}],
+                       [{"name": "pv-1", "persistentVolumeClaim": {"claimName": "pv-fsx"}}], allow_link=False)
+    s = plan.rewrite("--save /fsx/home/r/checkpoints/0 --x /fsxother /a/fsx/b")
+    assert s == f"--save {tmp_path}/pv/pv-fsx/home/r/checkpoints/0 --x /fsxother /a/fsx/b"
+
+
+def test_gpu_ledger_disjoint(tmp_path):
+    from mxtrain.runtime.topology import NodeLedger
+    a = NodeLedger(str(tmp_path / "l.json"), "a", total=8)
+    b = NodeLedger(str(tmp_path / "l.json"), "b", total=8)
+    ga = a.allocate(4)
+    gb = b.allocate(4)
+    assert not set(ga) & set(gb)
+    with pytest.raises(RuntimeError):
+        b.allocate(1)
+    a.release(ga)
+    assert len(b.allocate(4)) == 4
