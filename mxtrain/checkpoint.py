@@ -1,0 +1,230 @@
+"""Megatron-DeepSpeed checkpoint layout writer/reader.
+
+Directory layout (unchanged from Megatron-DeepSpeed + DeepSpeed ZeRO-1, so
+`/fsx/home/<rel>/checkpoints/<node_rank>/...` trees look the same on MI355X)::
+
+    <save>/latest                                   text: "global_step<N>"
+    <save>/latest_checkpointed_iteration.txt        text: "<N>"
+    <save>/global_step<N>/mp_rank_<MM>_model_states.pt
+    <save>/global_step<N>/zero_pp_rank_<D>_mp_rank_<MM>_optim_states.pt
+
+* ``mp_rank_MM`` = model-parallel rank (pp_rank * tp + tp_rank), written by the DP rank 0
+  replica of that model-parallel slice (DeepSpeed semantics: with per-node save dirs,
+  later nodes hold only their ZeRO shards);
+* ``zero_pp_rank_D`` = data-parallel rank D's optimizer partition (fp32 master,
+  exp_avg, exp_avg_sq of its 1/DP shard).
+
+``module`` uses Megatron state-dict keys (``language_model.embedding.word_embeddings.
+weight``, ``language_model.encoder.layers.<i>.self_attention.query_key_value.weight`` with
+Megatron's per-head [q, k, v] interleave, ...), layer indices local to the stage, as
+Megatron does.  Files contain only tensors / plain Python containers, so they load with
+``torch.load(weights_only=True)``.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import Dict, Optional
+
+import torch
+import torch.distributed as dist
+
+from .models.gpt import GPTConfig, stage_layer_range
+
+DS_VERSION = "0.13.4+mxtrain"
+
+_LAYER_MAP = {
+    "ln1_w": "input_layernorm.weight", "ln1_b": "input_layernorm.bias",
+    "qkv_w": "self_attention.query_key_value.weight", "qkv_b": "self_attention.query_key_value.bias",
+    "proj_w": "self_attention.dense.weight", "proj_b": "self_attention.dense.bias",
+    "ln2_w": "post_attention_layernorm.weight", "ln2_b": "post_attention_layernorm.bias",
+    "fc1_w": "mlp.dense_h_to_4h.weight", "fc1_b": "mlp.dense_h_to_4h.bias",
+    "fc2_w": "mlp.dense_4h_to_h.weight", "fc2_b": "mlp.dense_4h_to_h.bias",
+}
+_LAYER_RMAP = {v: k for k, v in _LAYER_MAP.items()}
+
+
+# ---------------------------------------------------------------------- qkv layout
+def qkv_to_megatron(t: torch.Tensor, hl: int, kvl: int, D: int) -> torch.Tensor:
+    """ours [q(hl*D); k(kvl*D); v(kvl*D)] -> Megatron per-group [q.. k v] interleave."""
+    rest = t.shape[1:]
+    q = t[: hl * D].reshape(kvl, hl // kvl, D, *rest)
+    k = t[hl * D:(hl + kvl) * D].reshape(kvl, 1, D, *rest)
+    v = t[(hl + kvl) * D:].reshape(kvl, 1, D, *rest)
+    return torch.cat([q, k, v], 1).reshape(t.shape)
+
+
+def qkv_from_megatron(t: torch.Tensor, hl: int, kvl: int, D: int) -> torch.Tensor:
+    rest = t.shape[1:]
+    g = t.reshape(kvl, hl // kvl + 2, D, *rest)
+    q = g[:, : hl // kvl].reshape(hl * D, *rest)
+    k = g[:, hl // kvl].reshape(kvl * D, *rest)
+    v = g[:, hl // kvl + 1].reshape(kvl * D, *rest)
+    return torch.cat([q, k, v], 0)
+
+
+# ---------------------------------------------------------------------- name mapping
+def to_megatron_state(params: Dict[str, torch.Tensor], cfg: GPTConfig, tp: int, pp: int,
+                      pp_rank: int) -> Dict[str, torch.Tensor]:
+    l0, _ = stage_layer_range(cfg, pp, pp_rank)
+    hl, kvl, D = cfg.num_attention_heads // tp, cfg.num_kv_heads // tp, cfg.head_dim
+    out = {}
+    for name, t in params.items():
+        t = t.detach().cpu().clone()
+        if name == "wte":
+            out["language_model.embedding.word_embeddings.weight"] = t
+        elif name == "wpe":
+            out["language_model.embedding.position_embeddings.weight"] = t
+        elif name == "wte_head":
+            out["word_embeddings_for_head.weight"] = t
+        elif name == "lm_head":
+            out["language_model.output_layer.weight"] = t
+        elif name.startswith("final_ln"):
+            out["language_model.encoder.final_layernorm." + ("weight" if name.endswith("_w") else "bias")] = t
+        elif name.startswith("layers."):
+            _, i, leaf = name.split(".", 2)
+            if leaf in ("qkv_w", "qkv_b"):
+                t = qkv_to_megatron(t, hl, kvl, D)
+            out[f"language_model.encoder.layers.{int(i) - l0}.{_LAYER_MAP[leaf]}"] = t
+        else:
+            out[name] = t
+    return out
+
+
+def from_megatron_state(sd: Dict[str, torch.Tensor], cfg: GPTConfig, tp: int, pp: int,
+                        pp_rank: int) -> Dict[str, torch.Tensor]:
+    l0, _ = stage_layer_range(cfg, pp, pp_rank)
+    hl, kvl, D = cfg.num_attention_heads // tp, cfg.num_kv_heads // tp, cfg.head_dim
+    out = {}
+    for k, t in sd.items():
+        if k == "language_model.embedding.word_embeddings.weight":
+            out["wte"] = t
+        elif k == "language_model.embedding.position_embeddings.weight":
+            out["wpe"] = t
+        elif k == "word_embeddings_for_head.weight":
+            out["wte_head"] = t
+        elif k == "language_model.output_layer.weight":
+            out["lm_head"] = t
+        elif k.startswith("language_model.encoder.final_layernorm."):
+            out["final_ln_w" if k.endswith("weight") else "final_ln_b"] = t
+        elif k.startswith("language_model.encoder.layers."):
+            rest = k[len("language_model.encoder.layers."):]
+            i, leafm = rest.split(".", 1)
+            leaf = _LAYER_RMAP[leafm]
+            if leaf in ("qkv_w", "qkv_b"):
+                t = qkv_from_megatron(t, hl, kvl, D)
+            out[f"layers.{int(i) + l0}.{leaf}"] = t
+        else:
+            out[k] = t
+    return out
+
+
+# ---------------------------------------------------------------------- save / load
+def _mp_rank(ps) -> int:
+    return ps.pp_rank * ps.tp + ps.tp_rank
+
+
+def _atomic_save(obj, path):
+    tmp = path + f".tmp{os.getpid()}"
+    torch.save(obj, tmp)
+    os.replace(tmp, path)
+
+
+def save_checkpoint(save_dir: str, trainer, iteration: int, consumed_samples: int = 0,
+                    args: Optional[dict] = None, ds_config: Optional[dict] = None,
+                    local_leader: Optional[bool] = None) -> str:
+    """Every rank calls this (collective barrier at the end)."""
+    ps = trainer.ps
+    tag = f"global_step{iteration}"
+    d = os.path.join(save_dir, tag)
+    os.makedirs(d, exist_ok=True)
+    mp = _mp_rank(ps)
+    opt = trainer.opt
+    sched = opt.schedule
+    lr_state = {"max_lr": sched.lr, "min_lr": sched.min_lr, "warmup_steps": sched.warmup,
+                "num_steps": opt.step_count, "decay_steps": sched.decay, "decay_style": sched.style}
+    if ps.dp_rank == 0:
+        module = to_megatron_state(trainer.flat.params, trainer.cfg, ps.tp, ps.pp, ps.pp_rank)
+        state = {
+            "module": module, "buffer_names": [], "optimizer": None, "lr_scheduler": lr_state,
+            "sparse_tensor_module_names": [], "skipped_steps": 0, "global_steps": iteration,
+            "global_samples": consumed_samples, "dp_world_size": ps.dp, "mp_world_size": ps.tp * ps.pp,
+            "ds_config": ds_config or {}, "ds_version": DS_VERSION, "args": args or {},
+            "iteration": iteration, "checkpoint_version": 3.0,
+            "rng_state": [{"torch_rng_state": torch.get_rng_state(),
+                           "mx_dropout_seed": trainer.seed.t.detach().cpu().clone()}],
+            "mx_config": trainer.cfg.__dict__.copy(),
+        }
+        _atomic_save(state, os.path.join(d, f"mp_rank_{mp:02d}_model_states.pt"))
+    optim = {
+        "optimizer_state_dict": {
+            "zero_stage": 1, "loss_scaler": None, "dynamic_loss_scale": False, "overflow": False,
+            "clip_grad": opt.clip, "partition_count": [ps.dp],
+            "base_optimizer_state": {
+                "state": {0: {"step": opt.step_count, "exp_avg": opt.exp_avg.detach().cpu(),
+                              "exp_avg_sq": opt.exp_avg_sq.detach().cpu()}},
+                "param_groups": [{"lr": sched(opt.step_count), "betas": list(opt.betas), "eps": opt.eps,
+                                  "weight_decay": opt.wd, "params": [0]}]},
+            "single_partition_of_fp32_groups": [opt.master.detach().cpu()],
+            "mx_shard_layout": [[int(b.start), int(b.end), int(so), int(n)] for (b, fs, so, n) in opt.slices],
+        },
+        "ds_config": ds_config or {}, "ds_version": DS_VERSION,
+    }
+    _atomic_save(optim, os.path.join(d, f"zero_pp_rank_{ps.dp_rank}_mp_rank_{mp:02d}_optim_states.pt"))
+    if dist.is_initialized():
+        dist.barrier()
+    if local_leader is None:
+        local_leader = int(os.environ.get("LOCAL_RANK", "0")) == 0
+    if local_leader:
+        with open(os.path.join(save_dir, "latest"), "w") as f:
+            f.write(tag)
+        with open(os.path.join(save_dir, "latest_checkpointed_iteration.txt"), "w") as f:
+            f.write(str(iteration))
+    if dist.is_initialized():
+        dist.barrier()
+    return d
+
+
+def latest_iteration(load_dir: str) -> Optional[int]:
+    p = os.path.join(load_dir, "latest_checkpointed_iteration.txt")
+    if os.path.exists(p):
+        return int(open(p).read().strip())
+    p = os.path.join(load_dir, "latest")
+    if os.path.exists(p):
+        return int(open(p).read().strip().replace("global_step", ""))
+    return None
+
+
+def load_checkpoint(load_dir: str, trainer, load_optim: bool = True) -> Optional[dict]:
+    """Restore params (+ optimizer shards) from the newest checkpoint in load_dir.
+    Returns {"iteration", "consumed_samples"} or None if there is none."""
+    it = latest_iteration(load_dir)
+    if it is None:
+        return None
+    ps = trainer.ps
+    d = os.path.join(load_dir, f"global_step{it}")
+    mp = _mp_rank(ps)
+    opt_path = os.path.join(d, f"zero_pp_rank_{ps.dp_rank}_mp_rank_{mp:02d}_optim_states.pt")
+    model_path = os.path.join(d, f"mp_rank_{mp:02d}_model_states.pt")
+    info = {"iteration": it, "consumed_samples": 0}
+    if os.path.exists(model_path):
+        st = torch.load(model_path, map_location="cpu", weights_only=True)
+        sd = from_megatron_state(st["module"], trainer.cfg, ps.tp, ps.pp, ps.pp_rank)
+        trainer.flat.load_state_dict(sd)
+        info["consumed_samples"] = int(st.get("global_samples", 0))
+        trainer.opt._refresh_master()
+    if load_optim and os.path.exists(opt_path):
+        o = torch.load(opt_path, map_location="cpu", weights_only=True)["optimizer_state_dict"]
+        base = o["base_optimizer_state"]["state"][0]
+        trainer.opt.load_shard_state({"master": o["single_partition_of_fp32_groups"][0],
+                                      "exp_avg": base["exp_avg"], "exp_avg_sq": base["exp_avg_sq"],
+                                      "step": base["step"]})
+    elif not os.path.exists(model_path):
+        raise FileNotFoundError(f"no model or optimizer state for mp_rank {mp} / dp_rank {ps.dp_rank} in {d}")
+    if "consumed_samples" not in info or info["consumed_samples"] == 0:
+        info["consumed_samples"] = it * trainer.global_batch
+    trainer.iteration = it
+    # dropout stream continues where it stopped (one advance per optimizer step)
+    trainer.seed.set_step(trainer.tcfg.seed + 7 * ps.dp_rank, trainer.opt.step_count)
+    return info

@@ -48,7 +48,13 @@ class DropoutSeed:
     def value(self) -> int:
         return int(self.t.item())
 
+    INC = 0x61C88647 & 0x7FFFFFFF
+
     def advance(self):
         # stays on-device (captured into hipGraphs); wraps harmlessly
-        self.t.add_(0x61C88647 & 0x7FFFFFFF)
+        self.t.add_(self.INC)
         self.t.bitwise_and_(0x7FFFFFFF)
+
+    def set_step(self, seed: int, steps: int):
+        """State after `steps` advances from `seed` (checkpoint resume)."""
+        self.t.fill_(((seed & 0x7FFFFFFF) + steps * self.INC) % (1 << 31))

@@ -126,3 +126,26 @@ class PipelineSchedule:
             if not first:
                 self._exchange(send_t=in_grad, send_to=prev)
         return loss_total
+
+    @torch.no_grad()
+    def run_forward_only(self, tokens: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        """Evaluation: every micro-batch flows forward through the stages; the last stage
+        returns the summed loss (0 elsewhere)."""
+        tr, ps = self.tr, self.ps
+        stage = tr.stage
+        nm, B, S = tokens.shape
+        shape = self._act_shape(B, S)
+        first, last = ps.is_first_stage, ps.is_last_stage
+        prev, nxt = ps.prev_rank(), ps.next_rank()
+        loss_total = torch.zeros((), dtype=torch.float32, device=tr.device)
+        for m in range(nm):
+            if first:
+                out = stage.forward(ids=tokens[m].reshape(-1), labels=labels[m].reshape(-1), B=B, S=S)
+            else:
+                inp = self._exchange(recv_shape=shape, recv_from=prev)
+                out = stage.forward(hidden=inp, labels=labels[m].reshape(-1), B=B, S=S)
+            if last:
+                loss_total = loss_total + out.detach()
+            else:
+                self._exchange(send_t=out, send_to=nxt)
+        return loss_total

@@ -100,8 +100,13 @@ class DistributedOptimizer:
         self.wd_flags = self._shard_of(flat.wd_flags)
         self.norm_flags = self._shard_of(norm_flags)
         self.hyper = torch.zeros(optim_ops.H_N, dtype=torch.float32, device=dev)
-        self.hyper_host = torch.zeros(optim_ops.H_N, dtype=torch.float32,
-                                      pin_memory=dev.type == "cuda")
+        # ring of pinned staging buffers: the host runs steps ahead of the GPU, so a
+        # buffer is only rewritten once the async copy that last read it has executed
+        self._hyper_ring = [torch.zeros(optim_ops.H_N, dtype=torch.float32, pin_memory=dev.type == "cuda")
+                            for _ in range(4 if dev.type == "cuda" else 1)]
+        self._hyper_events = [None] * len(self._hyper_ring)
+        self._hyper_i = 0
+        self.hyper_host = self._hyper_ring[0]
         self.normsq = torch.zeros(1, dtype=torch.float32, device=dev)
         self.step_count = 0
         # ---- overlap bookkeeping
@@ -182,7 +187,10 @@ class DistributedOptimizer:
     def set_hyper(self, lr: float):
         t = self.step_count
         b1, b2 = self.betas
-        h = self.hyper_host
+        i = self._hyper_i = (self._hyper_i + 1) % len(self._hyper_ring)
+        if self._hyper_events[i] is not None:
+            self._hyper_events[i].synchronize()
+        h = self.hyper_host = self._hyper_ring[i]
         h[optim_ops.H_LR] = lr
         h[optim_ops.H_B1] = b1
         h[optim_ops.H_B2] = b2
@@ -193,6 +201,8 @@ class DistributedOptimizer:
         h[optim_ops.H_GS] = 1.0 / self.world
         h[optim_ops.H_CLIP] = self.clip if self.clip else 0.0
         self.hyper.copy_(h, non_blocking=True)
+        if self.device.type == "cuda" and not torch.cuda.is_current_stream_capturing():
+            self._hyper_events[i] = torch.cuda.current_stream(self.device).record_event()
 
     def grad_norm_sq(self) -> torch.Tensor:
         optim_ops.sumsq_bf16(self.grad_shard, 1.0 / self.world, out=self.normsq,

@@ -109,9 +109,9 @@ class GPTTrainer:
         if self._graph is not None:
             self._static[0].copy_(tokens)
             self._static[1].copy_(labels)
-            self.opt.set_hyper(self.opt.schedule(self.opt.step_count + 1))
+            self.opt.step_count += 1   # bias corrections use the new step, as in eager step()
+            self.opt.set_hyper(self.opt.schedule(self.opt.step_count))
             self._graph.replay()
-            self.opt.step_count += 1
             self.iteration += 1
             return self._static_loss
         return self._train_step_eager(tokens, labels)
@@ -135,13 +135,16 @@ class GPTTrainer:
 
     def capture(self, tokens, labels, warmup: int = 2):
         """Capture one whole training step (fwd, bwd, grad reduce, optimizer) into a
-        hipGraph; later steps replay it (no per-kernel launch cost)."""
+        hipGraph; later steps replay it (no per-kernel launch cost).  The ``warmup``
+        side-stream steps are real training steps on (tokens, labels); the loss of the
+        last one is returned so callers can account for it."""
         assert self.device.type == "cuda"
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
+        last = None
         with torch.cuda.stream(s):
             for _ in range(warmup):
-                self._train_step_eager(tokens, labels)
+                last = self._train_step_eager(tokens, labels)
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self._static = (tokens.clone(), labels.clone())
@@ -154,7 +157,7 @@ class GPTTrainer:
         self.opt.step_count = step0
         self._graph = g
         self._static_loss = loss
-        return g
+        return last
 
     def _graph_body(self):
         tokens, labels = self._static
@@ -183,6 +186,26 @@ class GPTTrainer:
                                             o.param_shard[so:so + n], group=o.dp_group)
         o.reset_pending()
         return loss
+
+    @torch.no_grad()
+    def eval_step(self, tokens: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        """Forward-only loss (dropout off, no gradients, optimizer untouched); mean over
+        the step's tokens on the last stage."""
+        nm, B, S = tokens.shape
+        rt = self.stage.rt
+        rt.training = False
+        rt.unit_done = None
+        rt.grad_scale = 1.0 / (nm * B * S)
+        try:
+            if self.pipeline is not None:
+                return self.pipeline.run_forward_only(tokens, labels)
+            loss = torch.zeros((), dtype=torch.float32, device=self.device)
+            for m in range(nm):
+                loss = loss + self.stage.forward(ids=tokens[m].reshape(-1), labels=labels[m].reshape(-1),
+                                                 B=B, S=S).detach()
+            return loss
+        finally:
+            rt.training = True
 
     # ------------------------------------------------------------------ utils
     def tokens_per_step(self):

@@ -1,0 +1,73 @@
+"""The shipped example values files, end to end on CPU through the launcher (SURVEY §7.3
+minimum slice): data-process(wikicorpus) -> pytorchjob-distributed(pretrain-ddp-zero1)
+with the model shrunk and iterations cut, everything else as in the example file."""
+import os
+import re
+
+import pytest
+import yaml
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EX = os.path.join(REPO, "examples")
+CHARTS = os.path.join(REPO, "charts", "machine-learning")
+
+TINY_GPT = ('  - export GPT_ARGS="--num-layers 2 --hidden-size 64 --num-attention-heads 2 --seq-length 32 '
+            '--max-position-embeddings 32 --micro-batch-size 2 --lr 0.00015 --train-iters 6 --lr-decay-iters 6 '
+            '--lr-decay-style cosine --min-lr 1.0e-5 --weight-decay 1e-2 --lr-warmup-fraction .01 --clip-grad 1.0 --fp16"')
+
+
+def _shrink(path, tmp_path, nproc=2):
+    doc = yaml.safe_load(open(path))
+    pre = []
+    for line in doc.get("pre_script", []):
+        if line.startswith("export GPT_ARGS="):
+            line = TINY_GPT[4:]
+        if line.startswith("export OUTPUT_ARGS="):
+            line = 'export OUTPUT_ARGS="--log-interval 2 --save-interval 3 --eval-interval 3 --eval-iters 1"'
+        line = line.replace('train_micro_batch_size_per_gpu\\": 4', 'train_micro_batch_size_per_gpu\\": 2')
+        line = re.sub(r'"train_micro_batch_size_per_gpu": \d+', '"train_micro_batch_size_per_gpu": 2', line)
+        pre.append(line)
+    doc["pre_script"] = pre
+    for k in ("requests", "limits"):
+        doc.setdefault("resources", {})[k] = {}
+    if "nproc_per_node" in doc["resources"]:
+        doc["resources"]["nproc_per_node"] = nproc
+    out = tmp_path / os.path.basename(path)
+    out.write_text(yaml.safe_dump(doc))
+    return str(out)
+
+
+@pytest.fixture()
+def home(tmp_path, monkeypatch):
+    monkeypatch.setenv("MXTRAIN_HOME", str(tmp_path / "home"))
+    monkeypatch.setenv("MXTRAIN_NUM_GPUS", "0")
+    monkeypatch.setenv("MXTRAIN_PV_LINK", "0")
+    monkeypatch.setenv("NUM_DOCS", "300")
+    return tmp_path
+
+
+def test_wikicorpus_then_pretrain_ddp_zero1(home):
+    from mxtrain.launch import release as rel
+    vals = _shrink(os.path.join(EX, "megatron-deepspeed", "gpt2_345m", "wikicorpus.yaml"), home)
+    st = rel.install(os.path.join(CHARTS, "data-prep", "data-process"), "mds-gpt2-345m", value_files=[vals],
+                     wait=True, timeout=600)
+    log = rel.logs("mds-gpt2-345m")
+    assert st["phase"] == "Succeeded", log
+    data = home / "home" / "pv" / "pv-fsx" / "home" / "mds-gpt2-345m" / "data" / "wikicorpus"
+    assert (data / "gpt2_text_document.bin").exists() and (data / "gpt2-vocab.json").exists()
+    rel.uninstall("mds-gpt2-345m")
+
+    vals = _shrink(os.path.join(EX, "megatron-deepspeed", "gpt2_345m", "pretrain-ddp-zero1.yaml"), home)
+    st = rel.install(os.path.join(CHARTS, "training", "pytorchjob-distributed"), "mds-gpt2-345m",
+                     value_files=[vals], wait=True, timeout=900)
+    log = rel.logs("mds-gpt2-345m")
+    assert st["phase"] == "Succeeded", log
+    assert "Training script done" in log
+    assert "validation loss at iteration 3" in log
+    ck = home / "home" / "pv" / "pv-fsx" / "home" / "mds-gpt2-345m" / "checkpoints" / "0"
+    assert open(ck / "latest").read() == "global_step6"
+    assert sorted(os.listdir(ck / "global_step6")) == [
+        "mp_rank_00_model_states.pt", "zero_pp_rank_0_mp_rank_00_optim_states.pt",
+        "zero_pp_rank_1_mp_rank_00_optim_states.pt"]
+    out_log = home / "home" / "pv" / "pv-efs" / "home" / "mds-gpt2-345m" / "logs" / "0" / "pretrain-ddp-zero1.log"
+    assert "iteration        6/       6" in out_log.read_text()
