@@ -19,6 +19,9 @@ for s in $STEPS; do
     bench)
       timeout -k 10 ${T_BENCH:-400} python bench.py --gpus 1 --steps ${BSTEPS:-20} --warmup ${BWARM:-5} ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1; rc=$?
       tail -5 gpurun_out/bench.log; echo "bench rc=$rc"; ok $rc || exit $rc ;;
+    slice)
+      timeout -k 10 ${T_SLICE:-900} python scripts/gpu_slice.py ${SLICE_ARGS:-} > gpurun_out/slice.log 2>&1; rc=$?
+      tail -20 gpurun_out/slice.log; echo "slice rc=$rc"; ok $rc || exit $rc ;;
     kbench)
       timeout -k 10 300 python scripts/kbench.py ${KBENCH_ARGS:-} > gpurun_out/kbench.log 2>&1; rc=$?
       cat gpurun_out/kbench.log | tail -40; echo "kbench rc=$rc"; ok $rc || exit $rc ;;
