@@ -183,3 +183,36 @@ def layer_norm(x, gamma, beta=None, eps=1e-5):
 
 def rms_norm(x, gamma, eps=1e-6):
     return LayerNormFn.apply(x, gamma, None, eps, True)
+
+
+class BDANormFn(torch.autograd.Function):
+    """y = norm(residual + dropout(x + bias)) with autograd (post-LN transformer blocks,
+    e.g. BERT): one fused HIP pass forward, one fused pass backward producing
+    d(residual), d(x) (dropout mask regenerated from the seed) and the dgamma/dbeta/dbias
+    column sums."""
+
+    @staticmethod
+    def forward(ctx, x, bias, residual, gamma, beta, eps, p, seed_t, salt, rms):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        r2 = residual.reshape(-1, shape[-1]).contiguous() if residual is not None else None
+        h, y, mean, rstd = bda_norm_fwd(x2, bias, r2, gamma, beta, eps, p, seed_t, salt, rms)
+        ctx.save_for_backward(h, mean, rstd, gamma)
+        ctx.meta = (p, seed_t, salt, rms, bias is not None, beta is not None, residual is not None, shape)
+        return y.view(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, mean, rstd, gamma = ctx.saved_tensors
+        p, seed_t, salt, rms, has_bias, has_beta, has_res, shape = ctx.meta
+        dg = torch.empty_like(gamma)
+        db = torch.empty_like(gamma) if has_beta else None
+        dbias = torch.empty_like(gamma) if has_bias else None
+        dh, dx = norm_bwd(dy.reshape(h.shape).contiguous(), None, h, mean, rstd, gamma, want_dx=True, p=p,
+                          seed_t=seed_t, salt=salt, rms=rms, dgamma=dg, dbeta=db, dbias=dbias)
+        return (dx.view(shape), dbias, dh.view(shape) if has_res else None, dg, db,
+                None, None, None, None, None)
+
+
+def bda_norm(x, bias, residual, gamma, beta, eps=1e-5, p=0.0, seed_t=None, salt=0, rms=False):
+    return BDANormFn.apply(x, bias, residual, gamma, beta, eps, p, seed_t, salt, rms)

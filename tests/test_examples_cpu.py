@@ -1,6 +1,7 @@
 """The shipped example values files, end to end on CPU through the launcher (SURVEY §7.3
 minimum slice): data-process(wikicorpus) -> pytorchjob-distributed(pretrain-ddp-zero1)
 with the model shrunk and iterations cut, everything else as in the example file."""
+import json
 import os
 import re
 
@@ -71,3 +72,26 @@ def test_wikicorpus_then_pretrain_ddp_zero1(home):
         "zero_pp_rank_1_mp_rank_00_optim_states.pt"]
     out_log = home / "home" / "pv" / "pv-efs" / "home" / "mds-gpt2-345m" / "logs" / "0" / "pretrain-ddp-zero1.log"
     assert "iteration        6/       6" in out_log.read_text()
+
+
+def test_config1_accelerate_bert_base_mrpc_cpu(home, monkeypatch):
+    """BASELINE config 1: Accelerate BERT-base GLUE MRPC on CPU, world_size=1, through the
+    elastic training chart."""
+    from mxtrain.launch import release as rel
+    monkeypatch.setenv("MAX_TRAIN_STEPS", "3")
+    monkeypatch.setenv("MXTRAIN_CPU_ONLY", "1")
+    vals = os.path.join(EX, "accelerate", "bert-glue-mrpc", "pretrain-cpu.yaml")
+    st = rel.install(os.path.join(CHARTS, "training", "pytorchjob-elastic"), "accel-bert", value_files=[vals],
+                     wait=True, timeout=900)
+    log = rel.logs("accel-bert")
+    assert st["phase"] == "Succeeded", log
+    assert "epoch 0:" in log and "Training script done" in log
+    hd = home / "home" / "pv" / "pv-efs" / "home" / "accel-bert"
+    ck = hd / "checkpoints" / "pytorchjob-accel-bert-worker-0" / "epoch_0"
+    assert (ck / "model.safetensors").exists() and (ck / "optimizer.bin").exists()
+    metrics = hd / "project" / "pytorchjob-accel-bert-worker-0" / "complete_nlp_example" / "metrics.jsonl"
+    rec = [json.loads(x) for x in metrics.read_text().splitlines()]
+    assert rec[0]["epoch"] == 0 and 0.0 <= rec[0]["accuracy"] <= 1.0
+    from safetensors.torch import load_file
+    sd = load_file(str(ck / "model.safetensors"))
+    assert sd["word_embeddings"].shape == (28996, 768) and len([k for k in sd if k.startswith("layers.")]) == 12 * 12
