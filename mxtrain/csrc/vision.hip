@@ -1,0 +1,423 @@
+// Detection kernels for the Mask R-CNN workload: multi-level
+// RoIAlign forward/backward on NHWC bf16 FPN features, bitmask NMS, fused anchor/proposal
+// <-> ground-truth matching, fused box decode + clip.  gfx950 / wave64.
+//
+// Layout choices (MI355X-first):
+//  * features are NHWC (channels_last) bf16, so one RoIAlign sample point reads C
+//    contiguous channels: a 64-lane wave covers 2 x 256 channels with 16-byte loads;
+//  * RoIAlign output is [R, PH, PW, C] -- directly the NHWC input of the mask head convs
+//    and, flattened, the box-head FC input;
+//  * backward scatters with hardware fp32 global atomics (global_atomic_add_f32) into an
+//    fp32 NHWC gradient per level, converted to bf16 by the caller's cast.
+//  * NMS: one 64x64 IoU tile per workgroup-wave produces 64-bit suppression words
+//    (wave64 = one word per lane); the sequential keep pass runs in one wave per problem
+//    with the removed-bitmask distributed one word per lane.
+#include "common.h"
+
+namespace {
+
+using namespace mx;
+
+struct Levels {
+  const uint16_t* f[4];
+  float* g[4];
+  int H[4];
+  int W[4];
+  float scale[4];
+  int n;        // number of levels
+  int lvl_min;  // FPN level of f[0] (2 for P2)
+  float canon;  // canonical box size (224) for level assignment
+  int canon_lvl;
+};
+
+__device__ __forceinline__ int roi_level(const Levels& L, float x1, float y1, float x2, float y2) {
+  if (L.n == 1) return 0;
+  const float area = fmaxf(x2 - x1, 0.f) * fmaxf(y2 - y1, 0.f);
+  const float k = floorf((float)L.canon_lvl + log2f(sqrtf(area) / L.canon + 1e-8f));
+  int lvl = (int)k - L.lvl_min;
+  lvl = lvl < 0 ? 0 : (lvl >= L.n ? L.n - 1 : lvl);
+  return lvl;
+}
+
+struct Bilinear {
+  int o[4];
+  float w[4];
+  bool valid;
+};
+
+__device__ __forceinline__ Bilinear bilinear(float y, float x, int H, int W) {
+  Bilinear b;
+  b.valid = !(y < -1.f || y > (float)H || x < -1.f || x > (float)W);
+  if (!b.valid) {
+    b.o[0] = b.o[1] = b.o[2] = b.o[3] = 0;
+    b.w[0] = b.w[1] = b.w[2] = b.w[3] = 0.f;
+    return b;
+  }
+  y = fmaxf(y, 0.f);
+  x = fmaxf(x, 0.f);
+  int yl = (int)y, xl = (int)x, yh, xh;
+  if (yl >= H - 1) { yh = yl = H - 1; y = (float)yl; } else { yh = yl + 1; }
+  if (xl >= W - 1) { xh = xl = W - 1; x = (float)xl; } else { xh = xl + 1; }
+  const float ly = y - yl, lx = x - xl, hy = 1.f - ly, hx = 1.f - lx;
+  b.o[0] = yl * W + xl; b.o[1] = yl * W + xh; b.o[2] = yh * W + xl; b.o[3] = yh * W + xh;
+  b.w[0] = hy * hx; b.w[1] = hy * lx; b.w[2] = ly * hx; b.w[3] = ly * lx;
+  return b;
+}
+
+// one thread = (roi, bin, 8-channel chunk)
+__global__ __launch_bounds__(256) void roi_align_fwd_kernel(Levels L, const float* __restrict__ rois, int R,
+                                                            int C, int PH, int PW, int sr, int aligned,
+                                                            uint16_t* __restrict__ out) {
+  const int cch = C >> 3;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)R * PH * PW * cch;
+  if (idx >= total) return;
+  const int ch = (int)(idx % cch);
+  const int bin = (int)((idx / cch) % (PH * PW));
+  const int r = (int)(idx / ((long)cch * PH * PW));
+  const float* rr = rois + (size_t)r * 5;
+  const int b = (int)rr[0];
+  const int lv = roi_level(L, rr[1], rr[2], rr[3], rr[4]);
+  const float s = L.scale[lv];
+  const float off = aligned ? 0.5f : 0.f;
+  const float x0 = rr[1] * s - off, y0 = rr[2] * s - off;
+  float rw = rr[3] * s - off - x0, rh = rr[4] * s - off - y0;
+  if (!aligned) { rw = fmaxf(rw, 1.f); rh = fmaxf(rh, 1.f); }
+  const float bw = rw / PW, bh = rh / PH;
+  const int ph = bin / PW, pw = bin % PW;
+  const int H = L.H[lv], W = L.W[lv];
+  const uint16_t* base = L.f[lv] + ((size_t)b * H * W) * C + ch * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int iy = 0; iy < sr; ++iy) {
+    const float y = y0 + ph * bh + (iy + 0.5f) * bh / sr;
+    for (int ix = 0; ix < sr; ++ix) {
+      const float x = x0 + pw * bw + (ix + 0.5f) * bw / sr;
+      const Bilinear bl = bilinear(y, x, H, W);
+      if (!bl.valid) continue;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(base + (size_t)bl.o[k] * C), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += bl.w[k] * v[j];
+      }
+    }
+  }
+  const float inv = 1.f / (float)(sr * sr);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] *= inv;
+  *reinterpret_cast<uint4*>(out + ((size_t)r * PH * PW + bin) * C + ch * 8) = pack8(acc);
+}
+
+__global__ __launch_bounds__(256) void roi_align_bwd_kernel(Levels L, const float* __restrict__ rois, int R,
+                                                            int C, int PH, int PW, int sr, int aligned,
+                                                            const uint16_t* __restrict__ dout) {
+  const int cch = C >> 3;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)R * PH * PW * cch;
+  if (idx >= total) return;
+  const int ch = (int)(idx % cch);
+  const int bin = (int)((idx / cch) % (PH * PW));
+  const int r = (int)(idx / ((long)cch * PH * PW));
+  const float* rr = rois + (size_t)r * 5;
+  const int b = (int)rr[0];
+  const int lv = roi_level(L, rr[1], rr[2], rr[3], rr[4]);
+  const float s = L.scale[lv];
+  const float off = aligned ? 0.5f : 0.f;
+  const float x0 = rr[1] * s - off, y0 = rr[2] * s - off;
+  float rw = rr[3] * s - off - x0, rh = rr[4] * s - off - y0;
+  if (!aligned) { rw = fmaxf(rw, 1.f); rh = fmaxf(rh, 1.f); }
+  const float bw = rw / PW, bh = rh / PH;
+  const int ph = bin / PW, pw = bin % PW;
+  const int H = L.H[lv], W = L.W[lv];
+  float* gbase = L.g[lv] + ((size_t)b * H * W) * C + ch * 8;
+  float go[8];
+  unpack8(*reinterpret_cast<const uint4*>(dout + ((size_t)r * PH * PW + bin) * C + ch * 8), go);
+  const float inv = 1.f / (float)(sr * sr);
+  for (int iy = 0; iy < sr; ++iy) {
+    const float y = y0 + ph * bh + (iy + 0.5f) * bh / sr;
+    for (int ix = 0; ix < sr; ++ix) {
+      const float x = x0 + pw * bw + (ix + 0.5f) * bw / sr;
+      const Bilinear bl = bilinear(y, x, H, W);
+      if (!bl.valid) continue;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float wk = bl.w[k] * inv;
+        if (wk == 0.f) continue;
+        float* g = gbase + (size_t)bl.o[k] * C;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) unsafeAtomicAdd(g + j, wk * go[j]);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ NMS
+__device__ __forceinline__ float iou4(const float4 a, const float4 b) {
+  const float iw = fminf(a.z, b.z) - fmaxf(a.x, b.x);
+  const float ih = fminf(a.w, b.w) - fmaxf(a.y, b.y);
+  if (iw <= 0.f || ih <= 0.f) return 0.f;
+  const float inter = iw * ih;
+  const float ua = (a.z - a.x) * (a.w - a.y) + (b.z - b.x) * (b.w - b.y) - inter;
+  return inter / fmaxf(ua, 1e-12f);
+}
+
+// boxes: [P, N, 4] sorted by score (desc) per problem; counts[P] valid boxes.
+// mask: [P, N, NB] uint64, bit j of word (i, cb) set when box cb*64+j (> i) overlaps i.
+__global__ __launch_bounds__(64) void nms_mask_kernel(const float4* __restrict__ boxes, const int* __restrict__ counts,
+                                                      int N, int NB, float thr,
+                                                      unsigned long long* __restrict__ mask) {
+  const int cb = blockIdx.x, rb = blockIdx.y, p = blockIdx.z;
+  const int n = counts ? counts[p] : N;
+  const int t = threadIdx.x;
+  const int i = rb * 64 + t;
+  if (cb < rb || rb * 64 >= n) return;
+  __shared__ float4 cbox[64];
+  const int j0 = cb * 64;
+  if (j0 + t < n) cbox[t] = boxes[(size_t)p * N + j0 + t];
+  __syncthreads();
+  if (i >= n) return;
+  const float4 bi = boxes[(size_t)p * N + i];
+  unsigned long long bits = 0ull;
+  const int jn = min(64, n - j0);
+  for (int j = 0; j < jn; ++j) {
+    if (j0 + j > i && iou4(bi, cbox[j]) > thr) bits |= (1ull << j);
+  }
+  mask[((size_t)p * N + i) * NB + cb] = bits;
+}
+
+// one wave per problem; lane w owns removed-word w (NB <= 64 -> N <= 4096)
+__global__ __launch_bounds__(64) void nms_keep_kernel(const unsigned long long* __restrict__ mask,
+                                                      const int* __restrict__ counts, int N, int NB,
+                                                      int max_out, int* __restrict__ keep,
+                                                      int* __restrict__ nkeep) {
+  const int p = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int n = counts ? counts[p] : N;
+  // the 64 mask rows of the current chunk are staged in LDS with one coalesced batch of
+  // loads, so the serial pass waits on LDS (~100 cycles) instead of HBM per box
+  __shared__ unsigned long long rows[64 * 64];
+  unsigned long long removed = 0ull;
+  int out = 0;
+  const unsigned long long* m = mask + (size_t)p * N * NB;
+  for (int c0 = 0; c0 < n && out < max_out; c0 += 64) {
+    const int cn = min(64, n - c0);
+    for (int k = lane; k < cn * NB; k += 64) rows[k] = m[(size_t)c0 * NB + k];
+    __syncthreads();
+    const unsigned long long word0 = __shfl(removed, c0 >> 6);
+    unsigned long long word = word0;
+    for (int ii = 0; ii < cn && out < max_out; ++ii) {
+      if ((word >> ii) & 1ull) continue;
+      if (lane == 0) keep[(size_t)p * max_out + out] = c0 + ii;
+      ++out;
+      const unsigned long long rw = lane < NB ? rows[ii * NB + lane] : 0ull;
+      removed |= rw;
+      // suppression of later boxes in this chunk comes from word (c0 >> 6) of the row
+      word |= rows[ii * NB + (c0 >> 6)];
+    }
+    __syncthreads();
+  }
+  if (lane == 0) nkeep[p] = out;
+  for (int k = out + lane; k < max_out; k += 64) keep[(size_t)p * max_out + k] = -1;
+}
+
+// ------------------------------------------------------------------------------ matching
+// per (image, anchor): max IoU over that image's gt boxes and its argmax; per gt: the
+// best IoU over anchors (atomicMax on the float bits -- IoU >= 0).
+__global__ __launch_bounds__(256) void match_kernel(const float4* __restrict__ anchors, int A, int per_image_anchors,
+                                                    const float4* __restrict__ gt, const int* __restrict__ gcount,
+                                                    int G, float* __restrict__ max_iou, int* __restrict__ argmax,
+                                                    unsigned int* __restrict__ gt_best) {
+  __shared__ float4 sg[256];
+  const int b = blockIdx.y;
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ng = gcount[b];
+  const float4 an = a < A ? anchors[(per_image_anchors ? (size_t)b * A : 0) + a] : make_float4(0, 0, 0, 0);
+  float best = -1.f;
+  int bi = -1;
+  for (int g0 = 0; g0 < ng; g0 += 256) {
+    __syncthreads();
+    if (g0 + (int)threadIdx.x < ng) sg[threadIdx.x] = gt[(size_t)b * G + g0 + threadIdx.x];
+    __syncthreads();
+    const int gn = min(256, ng - g0);
+    for (int g = 0; g < gn; ++g) {
+      const float v = a < A ? iou4(an, sg[g]) : 0.f;
+      if (v > best) { best = v; bi = g0 + g; }
+      // per-gt best, reduced within the wave first to cut atomics 64x (all lanes take
+      // part: out-of-range anchors contribute 0)
+      float wv = v;
+      for (int o = 32; o > 0; o >>= 1) wv = fmaxf(wv, __shfl_xor(wv, o));
+      if ((threadIdx.x & 63) == 0 && wv > 0.f) atomicMax(gt_best + (size_t)b * G + g0 + g, __float_as_uint(wv));
+    }
+  }
+  if (a < A) {
+    max_iou[(size_t)b * A + a] = ng > 0 ? best : 0.f;
+    argmax[(size_t)b * A + a] = bi;
+  }
+}
+
+// low-quality matches (Faster R-CNN rule): an anchor whose IoU with some gt equals that
+// gt's best IoU is matched to it even below the positive threshold
+__global__ __launch_bounds__(256) void match_lowq_kernel(const float4* __restrict__ anchors, int A,
+                                                         int per_image_anchors, const float4* __restrict__ gt,
+                                                         const int* __restrict__ gcount, int G,
+                                                         const unsigned int* __restrict__ gt_best,
+                                                         int* __restrict__ lowq) {
+  const int b = blockIdx.y;
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= A) return;
+  const int ng = gcount[b];
+  const float4 an = anchors[(per_image_anchors ? (size_t)b * A : 0) + a];
+  int hit = -1;
+  for (int g = 0; g < ng; ++g) {
+    const float gb = __uint_as_float(gt_best[(size_t)b * G + g]);
+    if (gb > 0.f && iou4(an, gt[(size_t)b * G + g]) >= gb) { hit = g; }
+  }
+  lowq[(size_t)b * A + a] = hit;
+}
+
+// ------------------------------------------------------------------------------ decode
+// boxes = clip(decode(ref, deltas / weights)); dw/dh clamped at log(1000/16)
+__global__ __launch_bounds__(256) void decode_clip_kernel(const float4* __restrict__ ref, const float* __restrict__ deltas,
+                                                          int N, int per_row_ref, float wx, float wy, float ww, float wh,
+                                                          float clamp, const float* __restrict__ img_hw, int rows_per_img,
+                                                          float4* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const float4 r = ref[per_row_ref ? i : 0];
+  const float* d = deltas + (size_t)i * 4;
+  const float w = r.z - r.x, h = r.w - r.y;
+  const float cx = r.x + 0.5f * w, cy = r.y + 0.5f * h;
+  const float dx = d[0] / wx, dy = d[1] / wy;
+  const float dw = fminf(d[2] / ww, clamp), dh = fminf(d[3] / wh, clamp);
+  const float pcx = dx * w + cx, pcy = dy * h + cy;
+  const float pw = __expf(dw) * w, ph = __expf(dh) * h;
+  float4 o = make_float4(pcx - 0.5f * pw, pcy - 0.5f * ph, pcx + 0.5f * pw, pcy + 0.5f * ph);
+  if (img_hw) {
+    const int im = rows_per_img > 0 ? i / rows_per_img : 0;
+    const float H = img_hw[2 * im], W = img_hw[2 * im + 1];
+    o.x = fminf(fmaxf(o.x, 0.f), W); o.z = fminf(fmaxf(o.z, 0.f), W);
+    o.y = fminf(fmaxf(o.y, 0.f), H); o.w = fminf(fmaxf(o.w, 0.f), H);
+  }
+  out[i] = o;
+}
+
+// mask-head targets: bilinear crop of instance masks (uint8, full image) by RoI boxes to
+// M x M (one thread per output pixel; masks are read in place, never replicated per RoI)
+__global__ __launch_bounds__(256) void crop_resize_masks_kernel(const uint8_t* __restrict__ masks, int H, int W,
+                                                                const float4* __restrict__ boxes,
+                                                                const int* __restrict__ gidx, int R, int M,
+                                                                float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * M * M) return;
+  const int r = i / (M * M), py = (i / M) % M, px = i % M;
+  const float4 b = boxes[r];
+  const uint8_t* m = masks + (size_t)gidx[r] * H * W;
+  const float y = b.y + (py + 0.5f) * (b.w - b.y) / M - 0.5f;
+  const float x = b.x + (px + 0.5f) * (b.z - b.x) / M - 0.5f;
+  float v = 0.f;
+  if (!(y < -1.f || y > (float)H || x < -1.f || x > (float)W)) {
+    const float yc = fmaxf(y, 0.f), xc = fmaxf(x, 0.f);
+    int yl = (int)yc, xl = (int)xc, yh, xh;
+    float yy = yc, xx = xc;
+    if (yl >= H - 1) { yh = yl = H - 1; yy = (float)yl; } else { yh = yl + 1; }
+    if (xl >= W - 1) { xh = xl = W - 1; xx = (float)xl; } else { xh = xl + 1; }
+    const float ly = yy - yl, lx = xx - xl;
+    v = (1.f - ly) * ((1.f - lx) * m[yl * W + xl] + lx * m[yl * W + xh]) +
+        ly * ((1.f - lx) * m[yh * W + xl] + lx * m[yh * W + xh]);
+  }
+  out[i] = v;
+}
+
+Levels make_levels(const void* const* feats, float* const* grads, const int* H, const int* W, const float* scales,
+                   int n, int lvl_min, float canon, int canon_lvl) {
+  Levels L;
+  for (int i = 0; i < 4; ++i) {
+    L.f[i] = i < n ? (const uint16_t*)feats[i] : nullptr;
+    L.g[i] = (grads && i < n) ? grads[i] : nullptr;
+    L.H[i] = i < n ? H[i] : 0;
+    L.W[i] = i < n ? W[i] : 0;
+    L.scale[i] = i < n ? scales[i] : 0.f;
+  }
+  L.n = n;
+  L.lvl_min = lvl_min;
+  L.canon = canon;
+  L.canon_lvl = canon_lvl;
+  return L;
+}
+
+}  // namespace
+
+// feats: n (<= 4) NHWC bf16 levels; rois fp32 [R, 5] (batch, x1, y1, x2, y2) in image px.
+MX_EXPORT int mx_roi_align_fwd(const void* const* feats, const int* H, const int* W, const float* scales, int n,
+                               int lvl_min, float canon, int canon_lvl, const float* rois, int R, int C, int PH,
+                               int PW, int sampling, int aligned, void* out, hipStream_t s) {
+  if (n < 1 || n > 4 || (C & 7)) return hipErrorInvalidValue;
+  if (R == 0) return hipSuccess;
+  Levels L = make_levels(feats, nullptr, H, W, scales, n, lvl_min, canon, canon_lvl);
+  const long total = (long)R * PH * PW * (C / 8);
+  hipLaunchKernelGGL(roi_align_fwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, L, rois, R, C, PH,
+                     PW, sampling, aligned, (uint16_t*)out);
+  return hipGetLastError();
+}
+
+// grads: n fp32 NHWC buffers (zeroed by the caller), accumulated with atomics
+MX_EXPORT int mx_roi_align_bwd(float* const* grads, const int* H, const int* W, const float* scales, int n, int lvl_min,
+                               float canon, int canon_lvl, const float* rois, int R, int C, int PH, int PW,
+                               int sampling, int aligned, const void* dout, hipStream_t s) {
+  if (n < 1 || n > 4 || (C & 7)) return hipErrorInvalidValue;
+  if (R == 0) return hipSuccess;
+  Levels L = make_levels(nullptr, grads, H, W, scales, n, lvl_min, canon, canon_lvl);
+  const long total = (long)R * PH * PW * (C / 8);
+  hipLaunchKernelGGL(roi_align_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, L, rois, R, C, PH,
+                     PW, sampling, aligned, (const uint16_t*)dout);
+  return hipGetLastError();
+}
+
+MX_EXPORT int mx_nms_workspace_words(int N) { return (N + 63) / 64; }
+
+// batched NMS over P independent problems (boxes sorted by score desc per problem)
+MX_EXPORT int mx_nms(const float* boxes, const int* counts, int P, int N, float thr, int max_out, void* mask_ws,
+                     int* keep, int* nkeep, hipStream_t s) {
+  const int NB = (N + 63) / 64;
+  if (NB > 64) return hipErrorInvalidValue;
+  if (P == 0 || N == 0) return hipSuccess;
+  hipLaunchKernelGGL(nms_mask_kernel, dim3(NB, NB, P), dim3(64), 0, s, (const float4*)boxes, counts, N, NB, thr,
+                     (unsigned long long*)mask_ws);
+  hipLaunchKernelGGL(nms_keep_kernel, dim3(P), dim3(64), 0, s, (const unsigned long long*)mask_ws, counts, N, NB,
+                     max_out, keep, nkeep);
+  return hipGetLastError();
+}
+
+// anchors [A,4] shared by all B images (per_image_anchors=0) or [B,A,4]; gt [B,G,4]
+MX_EXPORT int mx_match(const float* anchors, int A, int per_image_anchors, const float* gt, const int* gcount, int B,
+                       int G, float* max_iou, int* argmax, unsigned int* gt_best, int* lowq, hipStream_t s) {
+  if (A == 0 || B == 0) return hipSuccess;
+  hipMemsetAsync(gt_best, 0, sizeof(unsigned int) * (size_t)B * (G > 0 ? G : 1), s);
+  dim3 grid((A + 255) / 256, B);
+  hipLaunchKernelGGL(match_kernel, grid, dim3(256), 0, s, (const float4*)anchors, A, per_image_anchors,
+                     (const float4*)gt, gcount, G, max_iou, argmax, gt_best);
+  if (lowq)
+    hipLaunchKernelGGL(match_lowq_kernel, grid, dim3(256), 0, s, (const float4*)anchors, A, per_image_anchors,
+                       (const float4*)gt, gcount, G, (const unsigned int*)gt_best, lowq);
+  return hipGetLastError();
+}
+
+MX_EXPORT int mx_decode_clip(const float* ref, const float* deltas, int N, int per_row_ref, float wx, float wy,
+                             float ww, float wh, float clamp, const float* img_hw, int rows_per_img, float* out,
+                             hipStream_t s) {
+  if (N == 0) return hipSuccess;
+  hipLaunchKernelGGL(decode_clip_kernel, dim3((N + 255) / 256), dim3(256), 0, s, (const float4*)ref, deltas, N,
+                     per_row_ref, wx, wy, ww, wh, clamp, img_hw, rows_per_img, (float4*)out);
+  return hipGetLastError();
+}
+
+// masks uint8 [G, H, W] (0/1), boxes fp32 [R, 4], gidx int32 [R] -> out fp32 [R, M, M]
+MX_EXPORT int mx_crop_resize_masks(const void* masks, int H, int W, const float* boxes, const int* gidx, int R, int M,
+                                   float* out, hipStream_t s) {
+  if (R == 0) return hipSuccess;
+  const int total = R * M * M;
+  hipLaunchKernelGGL(crop_resize_masks_kernel, dim3((total + 255) / 256), dim3(256), 0, s, (const uint8_t*)masks, H, W,
+                     (const float4*)boxes, gidx, R, M, out);
+  return hipGetLastError();
+}

@@ -1,0 +1,411 @@
+"""Mask R-CNN, ResNet-50-FPN (tensorpack `ResNetFPNModel` with MODE_MASK=True MODE_FPN=True,
+as the reference's MPIJob examples train it: examples/maskrcnn/train-maskrcnn-tensorpack.yaml,
+SURVEY §2.11, §3.3).
+
+MI355X-first data flow -- every per-step shape is static, so the whole step runs without
+host synchronisation and can be replayed as a graph:
+
+  images [B, 3, H, W] -> NHWC bf16 -> ResNet-50 (FrozenBN folded into convs, MIOpen NHWC)
+  -> FPN P2..P6 -> RPN head (shared 3x3 conv)
+  -> anchor targets: fused IoU/argmax/low-quality matching kernel (K15), sampling by
+     random-key ranks (no nonzero()/host sync)
+  -> proposals: per-(image, level) top-k, fused decode+clip kernel, one batched bitmask
+     NMS launch over all B x 5 problems (K14)
+  -> RoI sampling (fixed 512/img, fg first) -> multi-level RoIAlign 7x7 (K13, NHWC)
+  -> 2FC box head; mask branch on the 128 fg slots/img: RoIAlign 14x14 -> 4 conv ->
+     deconv -> per-class 28x28 logits; targets cropped from the instance masks in place
+     by a kernel (no per-RoI mask copies).
+
+Losses follow tensorpack: RPN BCE + Huber(1/9), Fast R-CNN CE + Huber(1) on class-specific
+deltas (weights 10,10,5,5), mask sigmoid BCE.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import vision as V
+from .resnet import resnet50
+
+
+@dataclass
+class MaskRCNNConfig:
+    num_classes: int = 81                      # 80 COCO classes + background
+    fpn_channels: int = 256
+    anchor_sizes: Tuple[int, ...] = (32, 64, 128, 256, 512)
+    anchor_ratios: Tuple[float, ...] = (0.5, 1.0, 2.0)
+    anchor_strides: Tuple[int, ...] = (4, 8, 16, 32, 64)
+    rpn_fg_thresh: float = 0.7
+    rpn_bg_thresh: float = 0.3
+    rpn_batch_per_im: int = 256
+    rpn_fg_ratio: float = 0.5
+    rpn_nms_thresh: float = 0.7
+    train_per_level_topk: int = 2000
+    train_post_nms_topk: int = 2000
+    test_per_level_topk: int = 1000
+    test_post_nms_topk: int = 1000
+    frcnn_batch_per_im: int = 512
+    frcnn_fg_ratio: float = 0.25
+    frcnn_fg_thresh: float = 0.5
+    bbox_reg_weights: Tuple[float, ...] = (10.0, 10.0, 5.0, 5.0)
+    fc_dim: int = 1024
+    mask: bool = True
+    mask_size: int = 28
+    mask_head_dim: int = 256
+    result_score_thresh: float = 0.05
+    test_nms_thresh: float = 0.5
+    results_per_im: int = 100
+    pixel_mean: Tuple[float, ...] = (123.675, 116.28, 103.53)
+    pixel_std: Tuple[float, ...] = (58.395, 57.12, 57.375)
+
+
+# ---------------------------------------------------------------------------- anchors
+def level_anchors(stride: int, size: int, ratios, H: int, W: int, device) -> torch.Tensor:
+    """[H*W*len(ratios), 4] anchors centred on stride-grid cells (tensorpack layout:
+    cell-major, ratio-minor)."""
+    base = []
+    for r in ratios:
+        w = size / math.sqrt(r)
+        h = size * math.sqrt(r)
+        base.append([-w / 2, -h / 2, w / 2, h / 2])
+    base = torch.tensor(base, dtype=torch.float32, device=device)
+    ys = (torch.arange(H, device=device, dtype=torch.float32) + 0.5) * stride
+    xs = (torch.arange(W, device=device, dtype=torch.float32) + 0.5) * stride
+    cy, cx = torch.meshgrid(ys, xs, indexing="ij")
+    ctr = torch.stack([cx, cy, cx, cy], -1).reshape(-1, 1, 4)
+    return (ctr + base[None]).reshape(-1, 4)
+
+
+def _rank_select(key: torch.Tensor, want: torch.Tensor, eligible: torch.Tensor) -> torch.Tensor:
+    """Per row: choose up to want[row] random eligible entries (key = random uniform).
+    Vectorised: rank of every entry among the eligible ones of its row, no host sync."""
+    k = torch.where(eligible, key, torch.full_like(key, 2.0))
+    order = k.argsort(dim=-1)
+    rank = torch.empty_like(order)
+    rank.scatter_(-1, order, torch.arange(order.shape[-1], device=key.device).expand_as(order))
+    return eligible & (rank < want[:, None])
+
+
+def huber(x: torch.Tensor, delta: float) -> torch.Tensor:
+    a = x.abs()
+    return torch.where(a < delta, 0.5 * x * x, delta * (a - 0.5 * delta))
+
+
+# ---------------------------------------------------------------------------- modules
+class FPN(nn.Module):
+    def __init__(self, in_channels: Sequence[int], out: int = 256):
+        super().__init__()
+        self.lateral = nn.ModuleList([nn.Conv2d(c, out, 1) for c in in_channels])
+        self.output = nn.ModuleList([nn.Conv2d(out, out, 3, padding=1) for _ in in_channels])
+        for m in list(self.lateral) + list(self.output):
+            nn.init.kaiming_uniform_(m.weight, a=1)
+            nn.init.zeros_(m.bias)
+
+    def forward(self, feats: List[torch.Tensor]) -> List[torch.Tensor]:
+        dt = feats[0].dtype
+        lat = [F.conv2d(f, m.weight.to(dt), m.bias.to(dt)) for f, m in zip(feats, self.lateral)]
+        for i in range(len(lat) - 2, -1, -1):
+            lat[i] = lat[i] + F.interpolate(lat[i + 1], scale_factor=2, mode="nearest")
+        outs = [F.conv2d(x, m.weight.to(dt), m.bias.to(dt), padding=1) for x, m in zip(lat, self.output)]
+        outs.append(F.max_pool2d(outs[-1], 1, 2))   # P6
+        return outs
+
+
+class RPNHead(nn.Module):
+    def __init__(self, c: int, na: int):
+        super().__init__()
+        self.conv = nn.Conv2d(c, c, 3, padding=1)
+        self.cls = nn.Conv2d(c, na, 1)
+        self.box = nn.Conv2d(c, 4 * na, 1)
+        for m in (self.conv, self.cls, self.box):
+            nn.init.normal_(m.weight, std=0.01)
+            nn.init.zeros_(m.bias)
+
+    def forward(self, x):
+        dt = x.dtype
+        t = F.relu(F.conv2d(x, self.conv.weight.to(dt), self.conv.bias.to(dt), padding=1), inplace=True)
+        lg = F.conv2d(t, self.cls.weight.to(dt), self.cls.bias.to(dt))
+        bx = F.conv2d(t, self.box.weight.to(dt), self.box.bias.to(dt))
+        B = x.shape[0]
+        # NHWC flatten -> [B, H*W*A] / [B, H*W*A, 4] (cell-major, anchor-minor)
+        return lg.permute(0, 2, 3, 1).reshape(B, -1), bx.permute(0, 2, 3, 1).reshape(B, -1, 4)
+
+
+class BoxHead(nn.Module):
+    def __init__(self, c: int, fc: int, ncls: int):
+        super().__init__()
+        self.fc1 = nn.Linear(c * 49, fc)
+        self.fc2 = nn.Linear(fc, fc)
+        self.cls = nn.Linear(fc, ncls)
+        self.box = nn.Linear(fc, ncls * 4)
+        for m in (self.fc1, self.fc2):
+            nn.init.kaiming_uniform_(m.weight, a=1)
+            nn.init.zeros_(m.bias)
+        nn.init.normal_(self.cls.weight, std=0.01)
+        nn.init.normal_(self.box.weight, std=0.001)
+        nn.init.zeros_(self.cls.bias)
+        nn.init.zeros_(self.box.bias)
+
+    def forward(self, x):
+        dt = x.dtype
+        x = x.reshape(x.shape[0], -1)
+        x = F.relu(F.linear(x, self.fc1.weight.to(dt), self.fc1.bias.to(dt)), inplace=True)
+        x = F.relu(F.linear(x, self.fc2.weight.to(dt), self.fc2.bias.to(dt)), inplace=True)
+        return (F.linear(x, self.cls.weight.to(dt), self.cls.bias.to(dt)).float(),
+                F.linear(x, self.box.weight.to(dt), self.box.bias.to(dt)).float().view(x.shape[0], -1, 4))
+
+
+class MaskHead(nn.Module):
+    def __init__(self, c: int, dim: int, ncls: int):
+        super().__init__()
+        self.convs = nn.ModuleList([nn.Conv2d(c if i == 0 else dim, dim, 3, padding=1) for i in range(4)])
+        self.deconv = nn.ConvTranspose2d(dim, dim, 2, stride=2)
+        self.pred = nn.Conv2d(dim, ncls, 1)
+        for m in list(self.convs) + [self.deconv]:
+            nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            nn.init.zeros_(m.bias)
+        nn.init.normal_(self.pred.weight, std=0.001)
+        nn.init.zeros_(self.pred.bias)
+
+    def forward(self, x):            # x: [R, 14, 14, C] NHWC -> [R, ncls, 28, 28]
+        dt = x.dtype
+        x = x.permute(0, 3, 1, 2)    # NCHW view of NHWC memory (channels_last)
+        for m in self.convs:
+            x = F.relu(F.conv2d(x, m.weight.to(dt), m.bias.to(dt), padding=1), inplace=True)
+        x = F.relu(F.conv_transpose2d(x, self.deconv.weight.to(dt), self.deconv.bias.to(dt), stride=2), inplace=True)
+        return F.conv2d(x, self.pred.weight.to(dt), self.pred.bias.to(dt))
+
+
+# ---------------------------------------------------------------------------- model
+class MaskRCNN(nn.Module):
+    def __init__(self, cfg: Optional[MaskRCNNConfig] = None):
+        super().__init__()
+        self.cfg = cfg = cfg or MaskRCNNConfig()
+        self.backbone = resnet50(norm="frozen")
+        self.fpn = FPN(self.backbone.out_channels, cfg.fpn_channels)
+        self.rpn = RPNHead(cfg.fpn_channels, len(cfg.anchor_ratios))
+        self.box_head = BoxHead(cfg.fpn_channels, cfg.fc_dim, cfg.num_classes)
+        self.mask_head = MaskHead(cfg.fpn_channels, cfg.mask_head_dim, cfg.num_classes - 1) if cfg.mask else None
+        self.register_buffer("pixel_mean", torch.tensor(cfg.pixel_mean).view(1, 3, 1, 1), persistent=False)
+        self.register_buffer("pixel_std", torch.tensor(cfg.pixel_std).view(1, 3, 1, 1), persistent=False)
+        self._anchor_cache: Dict = {}
+
+    # ------------------------------------------------------------------ helpers
+    def compute_dtype(self, device):
+        return torch.bfloat16 if device.type == "cuda" else torch.float32
+
+    def anchors(self, shapes, device):
+        key = (tuple(shapes), str(device))
+        if key not in self._anchor_cache:
+            cfg = self.cfg
+            lv = [level_anchors(s, z, cfg.anchor_ratios, h, w, device)
+                  for (h, w), s, z in zip(shapes, cfg.anchor_strides, cfg.anchor_sizes)]
+            self._anchor_cache[key] = lv
+        return self._anchor_cache[key]
+
+    def features(self, images: torch.Tensor):
+        dt = self.compute_dtype(images.device)
+        x = ((images.float() - self.pixel_mean) / self.pixel_std).to(dt)
+        x = x.contiguous(memory_format=torch.channels_last)
+        c = self.backbone.forward_features(x)
+        return self.fpn(c)      # P2..P6, NCHW views of channels_last memory
+
+    @staticmethod
+    def _nhwc(p: torch.Tensor) -> torch.Tensor:
+        # channels_last memory viewed as [B, H, W, C] without a copy
+        return p.permute(0, 2, 3, 1).contiguous()
+
+    # ------------------------------------------------------------------ RPN
+    def rpn_targets(self, anchors: torch.Tensor, gt_boxes, gt_count, img_hw):
+        cfg = self.cfg
+        B = gt_boxes.shape[0]
+        mi, am, lq = V.match_boxes(anchors, gt_boxes, gt_count)
+        inside = ((anchors[None, :, 0] >= 0) & (anchors[None, :, 1] >= 0) &
+                  (anchors[None, :, 2] <= img_hw[:, 1:2]) & (anchors[None, :, 3] <= img_hw[:, 0:1]))
+        pos = ((mi >= cfg.rpn_fg_thresh) | (lq >= 0)) & inside
+        neg = (mi < cfg.rpn_bg_thresh) & ~pos & inside
+        g = torch.rand(mi.shape, device=mi.device)
+        nfg_max = int(cfg.rpn_batch_per_im * cfg.rpn_fg_ratio)
+        sel_pos = _rank_select(g, torch.full((B,), nfg_max, device=mi.device), pos)
+        npos = sel_pos.sum(1)
+        sel_neg = _rank_select(g, cfg.rpn_batch_per_im - npos, neg)
+        matched = torch.where(lq >= 0, lq, am).clamp(min=0)
+        tgt_boxes = torch.gather(gt_boxes, 1, matched[..., None].expand(-1, -1, 4))
+        return sel_pos, sel_neg, tgt_boxes
+
+    def rpn_losses(self, logits, deltas, anchors, gt_boxes, gt_count, img_hw):
+        cfg = self.cfg
+        sel_pos, sel_neg, tgt = self.rpn_targets(anchors, gt_boxes, gt_count, img_hw)
+        sel = sel_pos | sel_neg
+        lab = sel_pos.float()
+        nsel = sel.sum().clamp(min=1).float()
+        cls_loss = (F.binary_cross_entropy_with_logits(logits.float(), lab, reduction="none") * sel).sum() / nsel
+        B = logits.shape[0]
+        enc = V.encode_boxes(anchors[None].expand(B, -1, -1).reshape(-1, 4), tgt.reshape(-1, 4)).view(B, -1, 4)
+        box = huber(deltas.float() - enc, 1.0 / 9).sum(-1)
+        box_loss = (box * sel_pos).sum() / (B * cfg.rpn_batch_per_im)
+        return cls_loss, box_loss
+
+    @torch.no_grad()
+    def proposals(self, logits_lv, deltas_lv, anchors_lv, img_hw, training: bool):
+        """Per image top proposals [B, K, 4] (+ scores [B, K]); static K."""
+        cfg = self.cfg
+        B = logits_lv[0].shape[0]
+        pre = cfg.train_per_level_topk if training else cfg.test_per_level_topk
+        post = cfg.train_post_nms_topk if training else cfg.test_post_nms_topk
+        boxes_all, scores_all, counts = [], [], []
+        for lg, dl, an in zip(logits_lv, deltas_lv, anchors_lv):
+            k = min(pre, lg.shape[1])
+            sc, idx = lg.float().topk(k, dim=1)                                # sorted desc
+            d = torch.gather(dl.float(), 1, idx[..., None].expand(-1, -1, 4))
+            ref = an[idx.reshape(-1)]
+            bx = V.decode_boxes(ref, d.reshape(-1, 4), (1.0, 1.0, 1.0, 1.0), img_hw, rows_per_img=k).view(B, k, 4)
+            if k < pre:
+                bx = F.pad(bx, (0, 0, 0, pre - k))
+                sc = F.pad(sc, (0, pre - k), value=-float("inf"))
+            boxes_all.append(bx)
+            scores_all.append(sc)
+            counts.append(k)
+        L = len(boxes_all)
+        boxes = torch.stack(boxes_all, 1).reshape(B * L, pre, 4)               # problem = (image, level)
+        scores = torch.stack(scores_all, 1).reshape(B * L, pre)
+        cnt = torch.tensor(counts, dtype=torch.int32, device=boxes.device).repeat(B)
+        keep, nk = V.batched_nms_sorted(boxes, cnt, cfg.rpn_nms_thresh, pre)
+        valid = keep >= 0
+        ki = keep.clamp(min=0)
+        kb = torch.gather(boxes, 1, ki[..., None].expand(-1, -1, 4))
+        ks = torch.where(valid, torch.gather(scores, 1, ki), torch.full_like(scores, -float("inf")))
+        kb = kb.view(B, L * pre, 4)
+        ks = ks.view(B, L * pre)
+        top = min(post, ks.shape[1])
+        s, i = ks.topk(top, dim=1)
+        b = torch.gather(kb, 1, i[..., None].expand(-1, -1, 4))
+        return b.detach(), s.detach()
+
+    # ------------------------------------------------------------------ RoI sampling
+    @torch.no_grad()
+    def sample_rois(self, props, gt_boxes, gt_labels, gt_count):
+        """Returns rois [B, N, 4] (fg first), labels [B, N] (0 = bg), matched gt [B, N],
+        regression targets [B, N, 4], fg mask [B, N]; N = frcnn_batch_per_im."""
+        cfg = self.cfg
+        B, G = gt_boxes.shape[:2]
+        gvalid = torch.arange(G, device=props.device)[None] < gt_count[:, None]
+        gtb = torch.where(gvalid[..., None], gt_boxes, torch.full_like(gt_boxes, -1e4))  # invalid gt -> far away
+        cand = torch.cat([props, gtb], 1)                                                  # [B, K+G, 4]
+        cvalid = torch.cat([torch.ones(props.shape[:2], dtype=torch.bool, device=props.device), gvalid], 1)
+        mi, am, _ = V.match_boxes(cand, gt_boxes, gt_count, low_quality=False)
+        fg = (mi >= cfg.frcnn_fg_thresh) & cvalid
+        bg = (mi < cfg.frcnn_fg_thresh) & cvalid
+        N = cfg.frcnn_batch_per_im
+        nfg = int(N * cfg.frcnn_fg_ratio)
+        r = torch.rand(mi.shape, device=mi.device)
+        sel_fg = _rank_select(r, torch.full((B,), nfg, device=mi.device), fg)
+        key = torch.where(sel_fg, 2.0 + r, torch.where(bg, 1.0 + r, torch.zeros_like(r)))
+        _, idx = key.topk(N, dim=1)                                                        # fg first, then bg
+        rois = torch.gather(cand, 1, idx[..., None].expand(-1, -1, 4))
+        is_fg = torch.gather(sel_fg, 1, idx)
+        g = torch.gather(am.clamp(min=0), 1, idx)
+        labels = torch.where(is_fg, torch.gather(gt_labels, 1, g), torch.zeros_like(g))
+        mgt = torch.gather(gt_boxes, 1, g[..., None].expand(-1, -1, 4))
+        tgt = V.encode_boxes(rois.reshape(-1, 4), mgt.reshape(-1, 4), cfg.bbox_reg_weights).view(B, N, 4)
+        return rois, labels, g, tgt, is_fg
+
+    @staticmethod
+    def _with_batch(boxes: torch.Tensor) -> torch.Tensor:
+        B, N, _ = boxes.shape
+        bi = torch.arange(B, device=boxes.device, dtype=torch.float32)[:, None, None].expand(B, N, 1)
+        return torch.cat([bi, boxes.float()], -1).reshape(-1, 5)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, images, img_hw, gt_boxes=None, gt_labels=None, gt_count=None, gt_masks=None):
+        """Training: returns dict of losses.  images [B,3,H,W] (padded), img_hw [B,2] real
+        sizes, gt_* padded to G per image, gt_masks uint8 [B, G, H, W]."""
+        cfg = self.cfg
+        P = self.features(images)
+        lv = [self.rpn(p) for p in P]
+        logits_lv = [l for l, _ in lv]
+        deltas_lv = [d for _, d in lv]
+        anchors_lv = self.anchors([(p.shape[2], p.shape[3]) for p in P], images.device)
+        img_hw = img_hw.float()
+        if not self.training:
+            return self.inference(P, logits_lv, deltas_lv, anchors_lv, img_hw)
+        anchors = torch.cat(anchors_lv, 0)
+        rpn_cls, rpn_box = self.rpn_losses(torch.cat(logits_lv, 1), torch.cat(deltas_lv, 1), anchors,
+                                           gt_boxes, gt_count, img_hw)
+        props, _ = self.proposals(logits_lv, deltas_lv, anchors_lv, img_hw, True)
+        rois, labels, gidx, tgt, is_fg = self.sample_rois(props, gt_boxes.float(), gt_labels, gt_count)
+        B, N = labels.shape
+        feats = [self._nhwc(p) for p in P[:4]]
+        scales = [1.0 / s for s in cfg.anchor_strides[:4]]
+        roi_feat = V.roi_align(feats, self._with_batch(rois), (7, 7), scales)
+        cls_logits, box_deltas = self.box_head(roi_feat)
+        lab = labels.reshape(-1)
+        cls_loss = F.cross_entropy(cls_logits, lab)
+        fgm = is_fg.reshape(-1)
+        pick = torch.gather(box_deltas, 1, lab[:, None, None].expand(-1, 1, 4)).squeeze(1)
+        box_loss = (huber(pick - tgt.reshape(-1, 4), 1.0).sum(-1) * fgm).sum() / (B * N)
+        out = {"rpn_cls_loss": rpn_cls, "rpn_box_loss": rpn_box, "fastrcnn_cls_loss": cls_loss,
+               "fastrcnn_box_loss": box_loss}
+        if self.mask_head is not None:
+            nfg = int(N * cfg.frcnn_fg_ratio)
+            fg_rois = rois[:, :nfg]
+            fg_valid = is_fg[:, :nfg].reshape(-1).float()
+            fg_lab = labels[:, :nfg].reshape(-1)
+            mf = V.roi_align(feats, self._with_batch(fg_rois), (14, 14), scales)
+            ml = self.mask_head(mf)                                               # [R, 80, 28, 28]
+            ml = torch.gather(ml, 1, (fg_lab - 1).clamp(min=0)[:, None, None, None].expand(-1, 1, *ml.shape[2:]))
+            ml = ml.squeeze(1).float()
+            G = gt_masks.shape[1]
+            flat_gid = (torch.arange(B, device=images.device)[:, None] * G + gidx[:, :nfg]).reshape(-1)
+            tgt_m = V.crop_resize_masks(gt_masks.reshape(-1, *gt_masks.shape[2:]), fg_rois.reshape(-1, 4), flat_gid,
+                                        cfg.mask_size)
+            tgt_m = (tgt_m >= 0.5).float()
+            bce = F.binary_cross_entropy_with_logits(ml, tgt_m, reduction="none").mean(dim=(1, 2))
+            out["maskrcnn_loss"] = (bce * fg_valid).sum() / fg_valid.sum().clamp(min=1)
+        out["total_loss"] = sum(out.values())
+        return out
+
+    @torch.no_grad()
+    def inference(self, P, logits_lv, deltas_lv, anchors_lv, img_hw):
+        cfg = self.cfg
+        props, _ = self.proposals(logits_lv, deltas_lv, anchors_lv, img_hw, False)
+        B, K, _ = props.shape
+        feats = [self._nhwc(p) for p in P[:4]]
+        scales = [1.0 / s for s in cfg.anchor_strides[:4]]
+        roi_feat = V.roi_align(feats, self._with_batch(props), (7, 7), scales)
+        cls_logits, box_deltas = self.box_head(roi_feat)
+        prob = cls_logits.softmax(-1).view(B, K, -1)[..., 1:]                    # [B, K, C]
+        C = prob.shape[-1]
+        ref = props.reshape(-1, 1, 4).expand(-1, C, 4).reshape(-1, 4)
+        dec = V.decode_boxes(ref, box_deltas[:, 1:].reshape(-1, 4), cfg.bbox_reg_weights, img_hw,
+                             rows_per_img=K * C).view(B, K, C, 4)
+        # per (image, class) NMS problems, boxes sorted by class score
+        sc = prob.permute(0, 2, 1)                                                 # [B, C, K]
+        sc = torch.where(sc >= cfg.result_score_thresh, sc, torch.full_like(sc, -1.0))
+        s_sorted, order = sc.sort(dim=-1, descending=True)
+        bx = dec.permute(0, 2, 1, 3)
+        bx = torch.gather(bx, 2, order[..., None].expand(-1, -1, -1, 4))
+        cnt = (s_sorted >= 0).sum(-1).to(torch.int32).reshape(-1)
+        keep, nk = V.batched_nms_sorted(bx.reshape(B * C, K, 4), cnt, cfg.test_nms_thresh, cfg.results_per_im)
+        valid = keep >= 0
+        ki = keep.clamp(min=0)
+        kb = torch.gather(bx.reshape(B * C, K, 4), 1, ki[..., None].expand(-1, -1, 4)).view(B, C * cfg.results_per_im, 4)
+        ks = torch.where(valid, torch.gather(s_sorted.reshape(B * C, K), 1, ki),
+                         torch.full_like(ki, -1, dtype=torch.float32)).view(B, -1)
+        kl = torch.arange(1, C + 1, device=ks.device)[None, :, None].expand(B, C, cfg.results_per_im).reshape(B, -1)
+        s, i = ks.topk(cfg.results_per_im, dim=1)
+        boxes = torch.gather(kb, 1, i[..., None].expand(-1, -1, 4))
+        labels = torch.gather(kl, 1, i)
+        res = {"boxes": boxes, "scores": s, "labels": labels, "valid": s > 0}
+        if self.mask_head is not None:
+            mf = V.roi_align(feats, self._with_batch(boxes), (14, 14), scales)
+            ml = self.mask_head(mf)
+            ml = torch.gather(ml, 1, (labels.reshape(-1) - 1).clamp(min=0)[:, None, None, None].expand(
+                -1, 1, *ml.shape[2:]))
+            res["masks"] = ml.squeeze(1).float().sigmoid().view(B, cfg.results_per_im, cfg.mask_size, cfg.mask_size)
+        return res

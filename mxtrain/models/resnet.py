@@ -1,0 +1,122 @@
+"""ResNet-50 (torchvision-free) for the Mask R-CNN backbone (FrozenBN) and
+the Ray Train ResNet-50 config (BatchNorm, BASELINE config 5).
+
+MI355X layout: activations are channels_last (NHWC) bf16 so MIOpen runs its NHWC
+implicit-GEMM (MFMA) convolutions and no layout transposes appear between layers;
+parameters stay fp32 masters (cast per forward, AMP style).
+
+``norm="frozen"``  FrozenBatchNorm: a fixed per-channel affine (tensorpack
+                   BACKBONE.NORM=FreezeBN); with random-init weights it is the identity
+                   transform, applied as conv bias so it costs no extra pass.
+``norm="bn"``      trainable BatchNorm2d (ImageNet classification training).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class FrozenBN(nn.Module):
+    def __init__(self, c: int, eps: float = 1e-5):
+        super().__init__()
+        self.register_buffer("weight", torch.ones(c))
+        self.register_buffer("bias", torch.zeros(c))
+        self.register_buffer("running_mean", torch.zeros(c))
+        self.register_buffer("running_var", torch.ones(c))
+        self.eps = eps
+
+    def scale_shift(self):
+        s = self.weight * torch.rsqrt(self.running_var + self.eps)
+        return s, self.bias - self.running_mean * s
+
+
+class ConvNorm(nn.Module):
+    """conv (no bias) + norm (+ ReLU).  FrozenBN is folded into the conv (weight scale +
+    bias) at forward time, so the frozen affine never touches activations separately."""
+
+    def __init__(self, cin, cout, k, stride=1, padding=0, norm="frozen", relu=True, dilation=1):
+        super().__init__()
+        self.conv = nn.Conv2d(cin, cout, k, stride, padding, dilation=dilation, bias=False)
+        nn.init.kaiming_normal_(self.conv.weight, mode="fan_out", nonlinearity="relu")
+        self.norm_kind = norm
+        self.norm = FrozenBN(cout) if norm == "frozen" else nn.BatchNorm2d(cout)
+        self.relu = relu
+
+    def forward(self, x):
+        dt = x.dtype
+        w = self.conv.weight
+        if self.norm_kind == "frozen":
+            s, b = self.norm.scale_shift()
+            y = F.conv2d(x, (w * s[:, None, None, None]).to(dt), b.to(dt), self.conv.stride, self.conv.padding,
+                         self.conv.dilation)
+        else:
+            y = self.norm(F.conv2d(x, w.to(dt), None, self.conv.stride, self.conv.padding, self.conv.dilation))
+        return F.relu(y, inplace=True) if self.relu else y
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, width, stride=1, norm="frozen", stride_in_1x1=True):
+        super().__init__()
+        cout = width * 4
+        s1, s3 = (stride, 1) if stride_in_1x1 else (1, stride)
+        self.conv1 = ConvNorm(cin, width, 1, s1, 0, norm)
+        self.conv2 = ConvNorm(width, width, 3, s3, 1, norm)
+        self.conv3 = ConvNorm(width, cout, 1, 1, 0, norm, relu=False)
+        self.shortcut = ConvNorm(cin, cout, 1, stride, 0, norm, relu=False) if (stride != 1 or cin != cout) else None
+        if norm == "bn":
+            nn.init.zeros_(self.conv3.norm.weight)   # zero-init last BN gamma (standard ResNet recipe)
+
+    def forward(self, x):
+        idt = self.shortcut(x) if self.shortcut is not None else x
+        return F.relu(self.conv3(self.conv2(self.conv1(x))) + idt, inplace=True)
+
+
+class ResNet(nn.Module):
+    def __init__(self, depth: int = 50, norm: str = "frozen", num_classes: Optional[int] = None,
+                 freeze_at: int = 2, stride_in_1x1: bool = True):
+        super().__init__()
+        blocks = {50: (3, 4, 6, 3), 101: (3, 4, 23, 3)}[depth]
+        self.stem = ConvNorm(3, 64, 7, 2, 3, norm)
+        self.freeze_at = freeze_at if norm == "frozen" else 0
+        stages = []
+        cin = 64
+        for i, (n, w) in enumerate(zip(blocks, (64, 128, 256, 512))):
+            layers = []
+            for j in range(n):
+                layers.append(Bottleneck(cin, w, (1 if i == 0 else 2) if j == 0 else 1, norm, stride_in_1x1))
+                cin = w * 4
+            stages.append(nn.Sequential(*layers))
+        self.stages = nn.ModuleList(stages)
+        self.out_channels = [256, 512, 1024, 2048]
+        self.fc = nn.Linear(2048, num_classes) if num_classes else None
+        if self.freeze_at:
+            # tensorpack freezes the stem and res2 (FREEZE_AT=2)
+            for p in self.stem.parameters():
+                p.requires_grad_(False)
+            for p in self.stages[0].parameters():
+                p.requires_grad_(False)
+
+    def forward_features(self, x) -> List[torch.Tensor]:
+        x = self.stem(x)
+        x = F.max_pool2d(x, 3, 2, 1)
+        outs = []
+        for st in self.stages:
+            x = st(x)
+            outs.append(x)
+        return outs   # C2..C5 (strides 4..32)
+
+    def forward(self, x):
+        c = self.forward_features(x)
+        if self.fc is None:
+            return c
+        pooled = c[-1].float().mean(dim=(2, 3))
+        return self.fc(pooled)
+
+
+def resnet50(norm="frozen", num_classes=None, **kw) -> ResNet:
+    return ResNet(50, norm, num_classes, **kw)

@@ -54,6 +54,14 @@ SIGNATURES = {
     "mx_attn_fwd": [P, P, P, I, I, I, P, I, P, I, I, I, I, I, I, P, F, P],
     "mx_attn_bwd": [P, P, P, I, I, I, P, I, P, I, P, P, P, P, I, P, P, I, I, I, I, I, I, I,
                     I, P, F, P],
+    # vision.hip
+    "mx_roi_align_fwd": [P, P, P, P, I, I, F, I, P, I, I, I, I, I, I, P, P],
+    "mx_roi_align_bwd": [P, P, P, P, I, I, F, I, P, I, I, I, I, I, I, P, P],
+    "mx_nms_workspace_words": [I],
+    "mx_nms": [P, P, I, I, F, I, P, P, P, P],
+    "mx_match": [P, I, I, P, P, I, I, P, P, P, P, P],
+    "mx_decode_clip": [P, P, I, I, F, F, F, F, F, P, I, P, P],
+    "mx_crop_resize_masks": [P, I, I, P, P, I, I, P, P],
 }
 
 

@@ -22,6 +22,13 @@ for s in $STEPS; do
     slice)
       timeout -k 10 ${T_SLICE:-900} python scripts/gpu_slice.py ${SLICE_ARGS:-} > gpurun_out/slice.log 2>&1; rc=$?
       tail -20 gpurun_out/slice.log; echo "slice rc=$rc"; ok $rc || exit $rc ;;
+    mrcnn)
+      timeout -k 10 ${T_MRCNN:-600} python scripts/bench_maskrcnn.py ${MRCNN_ARGS:-} > gpurun_out/mrcnn.log 2>&1; rc=$?
+      tail -12 gpurun_out/mrcnn.log; echo "mrcnn rc=$rc"; ok $rc || exit $rc ;;
+    mrprof)
+      cd /tmp && export TMPDIR=/tmp
+      timeout -k 10 ${T_PROF:-500} rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/mrprof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/scripts/bench_maskrcnn.py" --steps 12 --warmup 6 ${MRCNN_ARGS:-} > "$GRAFT_REPO_ROOT/gpurun_out/mrprof.log" 2>&1; rc=$?
+      cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/mrprof.log; echo "mrprof rc=$rc"; ok $rc || exit $rc ;;
     kbench)
       timeout -k 10 300 python scripts/kbench.py ${KBENCH_ARGS:-} > gpurun_out/kbench.log 2>&1; rc=$?
       cat gpurun_out/kbench.log | tail -40; echo "kbench rc=$rc"; ok $rc || exit $rc ;;

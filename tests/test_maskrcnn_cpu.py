@@ -1,0 +1,89 @@
+"""Mask R-CNN workload plumbing on CPU: tensorpack --config parsing and schedule
+derivation, COCO-format synthetic data + loader, COCO AP evaluator, model forward /
+backward / inference shapes, checkpoint + predictor round trip."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_tensorpack_config_overrides_and_schedule():
+    from mxtrain.workloads.maskrcnn import config as C
+    cfg = C.make_config(["MODE_MASK=True", "DATA.TRAIN=[\"coco_train2017\"]", "DATA.VAL=(\"coco_val2017\")",
+                         "TRAIN.LR_SCHEDULE=[240000,320000,360000]", "TRAIN.BASE_LR=0.01", "TRAINER=horovod",
+                         "TRAIN.STEPS_PER_EPOCH=7500", "BACKBONE.NORM=FreezeBN"])
+    C.finalize(cfg, 16)
+    assert cfg.DATA.VAL == ("coco_val2017",) and cfg.TRAINER == "horovod"
+    assert abs(cfg.TRAIN.LR - 0.02) < 1e-9                 # linear scaling from total batch 8 to 16
+    assert cfg.TRAIN.LR_STEPS[0][0] == 120000 and cfg.TRAIN.MAX_EPOCH == 24
+    aws = C.make_config(["TRAIN.BATCH_SIZE_PER_GPU=4", "TRAIN.LR_EPOCH_SCHEDULE=[(16, 0.1), (20, 0.01), (24, None)]",
+                         "TRAIN.BASE_LR=0.0015625", "DATA.TRAIN=[\"train2017\"]"])
+    C.finalize(aws, 16, images_per_epoch=120000)
+    assert abs(aws.TRAIN.LR - 0.1) < 1e-9 and aws.TRAIN.STEPS_PER_EPOCH == 1875 and aws.TRAIN.MAX_EPOCH == 24
+    assert C.lr_at(aws, 17 * 1875) == pytest.approx(0.01)
+
+
+def test_coco_eval_perfect_and_empty():
+    from mxtrain.workloads.maskrcnn.coco_eval import evaluate
+    gts = [{"image_id": 1, "category": 3, "box": np.array([0, 0, 10, 10.])},
+           {"image_id": 1, "category": 5, "box": np.array([20, 20, 40, 50.])}]
+    dets = [dict(g, score=0.9) for g in gts]
+    assert evaluate(dets, gts)["AP"] == pytest.approx(1.0)
+    shifted = [dict(g, score=0.9, box=g["box"] + 100) for g in gts]
+    assert evaluate(shifted, gts)["AP"] == pytest.approx(0.0)
+
+
+@pytest.fixture(scope="module")
+def coco_dir(tmp_path_factory):
+    d = tmp_path_factory.mktemp("coco")
+    from mxtrain.data.coco_synth import write_split
+    write_split(str(d), "train2017", 6, 0, 1)
+    write_split(str(d), "val2017", 3, 1, 1_000_000)
+    write_split(str(d), "test2017", 1, 2, 2_000_000, with_anns=False)
+    os.makedirs(d / "pretrained-models")
+    return str(d)
+
+
+def test_loader_shapes(coco_dir):
+    from mxtrain.data.coco import AspectGroupedSampler, COCODetection, DetectionDataset, collate
+    ds = DetectionDataset(COCODetection(coco_dir, "coco_train2017"), 320, 512)
+    s = AspectGroupedSampler(ds, 2)
+    for b in s:
+        batch = collate([ds[i] for i in b], 320, 512)
+        B, _, H, W = batch["images"].shape
+        assert (H, W) in ((320, 512), (512, 320))
+        assert batch["gt_masks"].shape[:2] == (B, (batch["gt_boxes"].shape[1] + 7) // 8 * 8)
+        n = int(batch["gt_count"][0])
+        x1, y1, x2, y2 = batch["gt_boxes"][0, 0].tolist()
+        m = batch["gt_masks"][0, 0]
+        assert m.sum() > 0 and m[int(y1):int(y2) + 1, int(x1):int(x2) + 1].sum() == m.sum()
+
+
+def test_train_cli_checkpoint_and_predict(coco_dir, tmp_path):
+    env = dict(os.environ, PYTHONPATH=REPO, MXTRAIN_CPU_ONLY="1")
+    logdir = tmp_path / "train_log" / "maskrcnn"
+    common = [f"DATA.BASEDIR={coco_dir}", "PREPROC.TRAIN_SHORT_EDGE_SIZE=[256,256]", "PREPROC.MAX_SIZE=384",
+              "PREPROC.TEST_SHORT_EDGE_SIZE=256", "DATA.NUM_WORKERS=0", "RPN.TRAIN_PER_LEVEL_NMS_TOPK=300",
+              "RPN.TRAIN_POST_NMS_TOPK=300", "RPN.TEST_PER_LEVEL_NMS_TOPK=200", "RPN.TEST_POST_NMS_TOPK=200",
+              "FRCNN.BATCH_PER_IM=64"]
+    r = subprocess.run([sys.executable, os.path.join(REPO, "mxtrain", "workloads", "maskrcnn", "train.py"),
+                        "--logdir", str(logdir), "--mx-max-steps", "2", "--config", "MODE_MASK=True",
+                        "MODE_FPN=True", "TRAINER=horovod", "TRAIN.STEPS_PER_EPOCH=2", "TRAIN.EVAL_PERIOD=1",
+                        "TRAIN.CHECKPOINT_PERIOD=1"] + common, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "Epoch 1 (global_step 2) finished" in r.stdout
+    assert (logdir / "model-2.index").exists() and (logdir / "checkpoint").exists()
+    stats = json.load(open(logdir / "stats.json"))
+    assert stats[-1]["global_step"] == 2 and "mAP(bbox)/IoU=0.5:0.95" in stats[-1]
+    r = subprocess.run([sys.executable, "-m", "mxtrain.predict", "--logdir", str(tmp_path), "--data-dir", coco_dir,
+                        "--score-thresh", "0.0", "--config"] + common, env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert os.path.exists(rec["output"])

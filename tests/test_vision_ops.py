@@ -1,0 +1,144 @@
+"""Detection ops (K13-K15): RoIAlign / NMS / matching / decode.  CPU: the PyTorch
+references against brute-force per-sample loops.  GPU: the HIP kernels against the fp32
+references (forward values, RoIAlign gradients, exact NMS keep lists)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from mxtrain.ops import vision as V
+
+
+def _bilinear_loop(f, y, x):
+    H, W = f.shape[0], f.shape[1]
+    if y < -1 or y > H or x < -1 or x > W:
+        return torch.zeros(f.shape[-1])
+    y, x = max(y, 0.0), max(x, 0.0)
+    yl, xl = int(y), int(x)
+    if yl >= H - 1:
+        yh = yl = H - 1
+        y = float(yl)
+    else:
+        yh = yl + 1
+    if xl >= W - 1:
+        xh = xl = W - 1
+        x = float(xl)
+    else:
+        xh = xl + 1
+    ly, lx = y - yl, x - xl
+    return ((1 - ly) * (1 - lx) * f[yl, xl] + (1 - ly) * lx * f[yl, xh] + ly * (1 - lx) * f[yh, xl] +
+            ly * lx * f[yh, xh])
+
+
+def _roi_align_loop(feat, roi, scale, PH, PW, sr):
+    b, x1, y1, x2, y2 = roi.tolist()
+    f = feat[int(b)]
+    x0, y0 = x1 * scale - 0.5, y1 * scale - 0.5
+    rw, rh = x2 * scale - 0.5 - x0, y2 * scale - 0.5 - y0
+    out = torch.zeros(PH, PW, f.shape[-1])
+    for ph in range(PH):
+        for pw in range(PW):
+            acc = 0
+            for iy in range(sr):
+                for ix in range(sr):
+                    y = y0 + ph * rh / PH + (iy + 0.5) * rh / PH / sr
+                    x = x0 + pw * rw / PW + (ix + 0.5) * rw / PW / sr
+                    acc = acc + _bilinear_loop(f, y, x)
+            out[ph, pw] = acc / (sr * sr)
+    return out
+
+
+def _rand_rois(R, B, H, W, gen):
+    x1 = torch.rand(R, generator=gen) * W * 0.8
+    y1 = torch.rand(R, generator=gen) * H * 0.8
+    w = torch.rand(R, generator=gen) * W * 0.5 + 2
+    h = torch.rand(R, generator=gen) * H * 0.5 + 2
+    b = torch.randint(0, B, (R,), generator=gen).float()
+    return torch.stack([b, x1, y1, x1 + w, y1 + h], 1)
+
+
+def test_roi_align_reference_matches_loop():
+    g = torch.Generator().manual_seed(0)
+    feat = torch.randn(2, 12, 16, 8, generator=g)
+    rois = _rand_rois(5, 2, 48, 64, g)
+    out = V._ref_roi_align([feat], [0.25], rois, 3, 4, 2, True, 2, 224.0, 4)
+    for r in range(5):
+        torch.testing.assert_close(out[r], _roi_align_loop(feat, rois[r], 0.25, 3, 4, 2), rtol=1e-4, atol=1e-5)
+
+
+def test_nms_and_match_reference():
+    g = torch.Generator().manual_seed(1)
+    xy = torch.rand(60, 2, generator=g) * 100
+    boxes = torch.cat([xy, xy + torch.rand(60, 2, generator=g) * 40 + 5], 1)
+    scores = torch.rand(60, generator=g)
+    keep = V.nms(boxes, scores, 0.5)
+    # greedy definition
+    order = scores.argsort(descending=True).tolist()
+    iou = V.box_iou(boxes, boxes)
+    ref, supp = [], set()
+    for i in order:
+        if i in supp:
+            continue
+        ref.append(i)
+        supp |= {j for j in range(60) if iou[i, j] > 0.5}
+    assert keep.tolist() == ref
+    gt = boxes[:7][None]
+    mi, am, lq = V.match_boxes(boxes, gt, torch.tensor([7]))
+    torch.testing.assert_close(mi[0], iou[:, :7].max(1).values)
+    assert (lq[0, :7] >= 0).all()
+
+
+def test_decode_inverts_encode():
+    g = torch.Generator().manual_seed(2)
+    ref = torch.cat([torch.rand(50, 2, generator=g) * 50, torch.rand(50, 2, generator=g) * 50 + 60], 1)
+    gt = torch.cat([torch.rand(50, 2, generator=g) * 50, torch.rand(50, 2, generator=g) * 50 + 60], 1)
+    w = (10.0, 10.0, 5.0, 5.0)
+    torch.testing.assert_close(V.decode_boxes(ref, V.encode_boxes(ref, gt, w), w), gt, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_roi_align_gpu_fwd_bwd():
+    g = torch.Generator().manual_seed(3)
+    B, C = 2, 256
+    shapes = [(200, 336), (100, 168), (50, 84), (25, 42)]
+    scales = [1 / 4, 1 / 8, 1 / 16, 1 / 32]
+    feats = [torch.randn(B, h, w, C, generator=g).bfloat16() for h, w in shapes]
+    rois = _rand_rois(300, B, 800, 1344, g)
+    ref_in = [f.float().requires_grad_(True) for f in feats]
+    ref = V._ref_roi_align(ref_in, scales, rois, 7, 7, 2, True, 2, 224.0, 4)
+    fg = [f.cuda().requires_grad_(True) for f in feats]
+    out = V.roi_align(fg, rois.cuda(), (7, 7), scales)
+    torch.testing.assert_close(out.float().cpu(), ref, rtol=2e-2, atol=2e-2)
+    dout = torch.randn(ref.shape, generator=g)
+    (ref * dout).sum().backward()
+    (out.float() * dout.cuda()).sum().backward()
+    for a, b in zip(fg, ref_in):
+        err = (a.grad.float().cpu() - b.grad).norm() / (b.grad.norm() + 1e-6)
+        assert err < 2e-2, float(err)
+
+
+@pytest.mark.gpu
+def test_nms_match_decode_gpu():
+    g = torch.Generator().manual_seed(4)
+    P, N = 5, 2000
+    xy = torch.rand(P, N, 2, generator=g) * 700
+    boxes = torch.cat([xy, xy + torch.rand(P, N, 2, generator=g) * 120 + 4], 2)
+    counts = torch.tensor([2000, 1500, 64, 1, 0])
+    kg, ng = V.batched_nms_sorted(boxes.cuda(), counts.cuda(), 0.7, 1000)
+    kc, nc = V.batched_nms_sorted(boxes, counts, 0.7, 1000)
+    assert ng.cpu().tolist() == nc.tolist()
+    assert torch.equal(kg.cpu(), kc)
+    anchors = boxes[0]
+    gt = boxes[1:3, :20]
+    gc = torch.tensor([20, 7])
+    a = V.match_boxes(anchors.cuda(), gt.cuda(), gc.cuda())
+    b = V.match_boxes(anchors, gt, gc)
+    torch.testing.assert_close(a[0].cpu(), b[0], rtol=1e-5, atol=1e-6)
+    same = a[0].cpu() > 0
+    assert torch.equal(a[1].cpu()[same], b[1][same])
+    assert torch.equal(a[2].cpu(), b[2])
+    d = torch.randn(N, 4, generator=g)
+    hw = torch.tensor([[800.0, 1344.0]])
+    torch.testing.assert_close(V.decode_boxes(anchors.cuda(), d.cuda(), (10, 10, 5, 5), hw.cuda()).cpu(),
+                               V.decode_boxes(anchors, d, (10, 10, 5, 5), hw), rtol=1e-4, atol=1e-2)
