@@ -333,7 +333,7 @@ Levels make_levels(const void* const* feats, float* const* grads, const int* H, 
                    int n, int lvl_min, float canon, int canon_lvl) {
   Levels L;
   for (int i = 0; i < 4; ++i) {
-    L.f[i] = i < n ? (const uint16_t*)feats[i] : nullptr;
+    L.f[i] = (feats && i < n) ? (const uint16_t*)feats[i] : nullptr;
     L.g[i] = (grads && i < n) ? grads[i] : nullptr;
     L.H[i] = i < n ? H[i] : 0;
     L.W[i] = i < n ? W[i] : 0;

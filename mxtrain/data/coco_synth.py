@@ -117,13 +117,26 @@ def write_split(data_dir: str, split: str, n: int, seed: int, start_id: int, wit
     return images, anns
 
 
-def write_backbone_npz(path: str, seed: int = 0):
+def write_backbone_npz(path: str, seed: int = 0, calib_images=None):
     """Random-init ResNet-50 in tensorpack's variable naming (HWIO conv kernels +
-    FrozenBN statistics), what BACKBONE.WEIGHTS points at."""
-    from ..models.resnet import resnet50
+    FrozenBN statistics), what BACKBONE.WEIGHTS points at.  The frozen statistics are
+    calibrated on a few synthetic images so the random backbone is well conditioned."""
+    from ..models.resnet import calibrate_frozen_bn, resnet50
     import torch
     torch.manual_seed(seed)
     m = resnet50(norm="frozen")
+    if calib_images:
+        from PIL import Image
+        ims = []
+        for p in calib_images[:4]:
+            im = Image.open(p).convert("RGB").resize((320, 256))
+            ims.append(torch.from_numpy(np.asarray(im, dtype=np.float32).copy()).permute(2, 0, 1))
+        x = torch.stack(ims)
+    else:
+        x = torch.rand(2, 3, 256, 320) * 255
+    mean = torch.tensor([123.675, 116.28, 103.53]).view(1, 3, 1, 1)
+    std = torch.tensor([58.395, 57.12, 57.375]).view(1, 3, 1, 1)
+    calibrate_frozen_bn(m, (x - mean) / std)
     from ..workloads.maskrcnn.weights import to_tensorpack_npz
     np.savez(path, **to_tensorpack_npz(m))
 
@@ -140,7 +153,9 @@ def main(argv=None):
     write_split(a.data_dir, "val2017", a.num_val, a.seed + 1, 1_000_000)
     write_split(a.data_dir, "test2017", a.num_test, a.seed + 2, 2_000_000, with_anns=False)
     os.makedirs(os.path.join(a.data_dir, "pretrained-models"), exist_ok=True)
-    write_backbone_npz(os.path.join(a.data_dir, "pretrained-models", "ImageNet-R50-AlignPadding.npz"), a.seed)
+    import glob
+    calib = sorted(glob.glob(os.path.join(a.data_dir, "train2017", "*.jpg")))[:4]
+    write_backbone_npz(os.path.join(a.data_dir, "pretrained-models", "ImageNet-R50-AlignPadding.npz"), a.seed, calib)
     print(f"wrote synthetic COCO-2017 layout to {a.data_dir}: {a.num_train} train / {a.num_val} val / "
           f"{a.num_test} test images")
 

@@ -285,7 +285,8 @@ class RayJobController(JobController):
             nworkers += reps
         gpus = self.alloc.allocate(min(ngpu, self.alloc.total)) if (ngpu and self.alloc.total) else []
         self.gpus = gpus
-        env = {"MXTRAIN_RAY_NUM_WORKERS": str(max(nworkers, 1)),
+        # one Ray Train worker per GPU of the worker group (CPU groups: one per replica)
+        env = {"MXTRAIN_RAY_NUM_WORKERS": str(len(gpus) if gpus else max(nworkers, 1)),
                "MXTRAIN_RAY_GPUS": ",".join(str(x) for x in gpus),
                "RAY_ADDRESS": "mxtrain://127.0.0.1", "MXTRAIN_RAY_JOB": self.release}
         rt = spec.get("runtimeEnvYAML")

@@ -144,7 +144,8 @@ class BoxHead(nn.Module):
         self.cls = nn.Linear(fc, ncls)
         self.box = nn.Linear(fc, ncls * 4)
         for m in (self.fc1, self.fc2):
-            nn.init.kaiming_uniform_(m.weight, a=1)
+            # tensorpack variance_scaling (fan_in, scale 1): std = 1 / sqrt(fan_in)
+            nn.init.normal_(m.weight, std=1.0 / math.sqrt(m.weight.shape[1]))
             nn.init.zeros_(m.bias)
         nn.init.normal_(self.cls.weight, std=0.01)
         nn.init.normal_(self.box.weight, std=0.001)

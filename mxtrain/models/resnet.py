@@ -45,9 +45,20 @@ class ConvNorm(nn.Module):
         self.norm = FrozenBN(cout) if norm == "frozen" else nn.BatchNorm2d(cout)
         self.relu = relu
 
+    calibrating = False
+
     def forward(self, x):
         dt = x.dtype
         w = self.conv.weight
+        if self.norm_kind == "frozen" and ConvNorm.calibrating:
+            # data-dependent init of a random backbone: set the frozen statistics so this
+            # conv's output is zero-mean / unit-variance per channel (LSUV-style)
+            with torch.no_grad():
+                y = F.conv2d(x.float(), w.float(), None, self.conv.stride, self.conv.padding, self.conv.dilation)
+                self.norm.running_mean.copy_(y.mean(dim=(0, 2, 3)))
+                self.norm.running_var.copy_(y.var(dim=(0, 2, 3), unbiased=False) + 1e-5)
+                self.norm.weight.fill_(1.0)
+                self.norm.bias.zero_()
         if self.norm_kind == "frozen":
             s, b = self.norm.scale_shift()
             y = F.conv2d(x, (w * s[:, None, None, None]).to(dt), b.to(dt), self.conv.stride, self.conv.padding,
@@ -116,6 +127,19 @@ class ResNet(nn.Module):
             return c
         pooled = c[-1].float().mean(dim=(2, 3))
         return self.fc(pooled)
+
+
+@torch.no_grad()
+def calibrate_frozen_bn(resnet: ResNet, images: torch.Tensor):
+    """Give a random-init FrozenBN ResNet sane statistics: one forward pass over
+    ``images`` (normalised NCHW) in which every FrozenBN takes the batch statistics of its
+    conv output.  Without this a BN-free random ResNet-50 has activations growing by
+    orders of magnitude through the 16 residual blocks."""
+    ConvNorm.calibrating = True
+    try:
+        resnet.forward_features(images.float())
+    finally:
+        ConvNorm.calibrating = False
 
 
 def resnet50(norm="frozen", num_classes=None, **kw) -> ResNet:

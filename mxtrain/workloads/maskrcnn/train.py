@@ -193,7 +193,9 @@ def main(argv=None):
     C.finalize(cfg, world, args.images_per_epoch)
     if device.type == "cuda" and hasattr(torch.backends.cuda, "preferred_blas_library"):
         torch.backends.cuda.preferred_blas_library("hipblaslt")
-        torch.backends.cudnn.benchmark = True
+    # MIOpen exhaustive find costs minutes on a fresh node (it times naive kernels too);
+    # opt in with MXTRAIN_CONV_BENCHMARK=1 when the find-db is warm
+    torch.backends.cudnn.benchmark = os.environ.get("MXTRAIN_CONV_BENCHMARK", "0") == "1"
     os.makedirs(args.logdir, exist_ok=True)
     log(f"Config: world {world} x {cfg.TRAIN.BATCH_SIZE_PER_GPU} img/GPU, device {device}, "
         f"lr {cfg.TRAIN.LR:.5f}, steps/epoch {cfg.TRAIN.STEPS_PER_EPOCH}, epochs {cfg.TRAIN.MAX_EPOCH}")
@@ -202,9 +204,12 @@ def main(argv=None):
             json.dump(cfg.to_dict(), f, indent=1, default=str)
     torch.manual_seed(1234 + rank)
     model = MaskRCNN(C.model_config(cfg))
+    calibrate = False
     if cfg.BACKBONE.WEIGHTS and os.path.exists(cfg.BACKBONE.WEIGHTS) and not args.load:
         n = load_tensorpack_npz(model.backbone, cfg.BACKBONE.WEIGHTS)
         log(f"Loaded {n} backbone tensors from {cfg.BACKBONE.WEIGHTS}")
+    elif not args.load:
+        calibrate = True   # random-init backbone: calibrate FrozenBN on the first batch
     model.to(device)
     short, max_size = cfg.PREPROC.TRAIN_SHORT, int(cfg.PREPROC.MAX_SIZE)
     coll = functools.partial(collate, short=short, max_size=max_size)
@@ -260,6 +265,12 @@ def main(argv=None):
         step = int(meta.get("global_step", 0))
         start_epoch = int(meta.get("epoch", 0)) + 1
         log(f"Resumed from {ck} at global_step {step}")
+    if calibrate and not ck:
+        from mxtrain.models.resnet import calibrate_frozen_bn
+        b0 = collate([ds[i] for i in range(min(2, len(ds)))], short, max_size)
+        x = (b0["images"].float().to(device) - model.pixel_mean) / model.pixel_std
+        calibrate_frozen_bn(model.backbone, x)
+        log("Calibrated FrozenBN statistics of the random-init backbone")
     hvd.broadcast_parameters(model.state_dict().values())
     dmodel = hvd.DistributedDataParallel(model)
     params = decay + no_decay

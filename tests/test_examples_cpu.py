@@ -95,3 +95,25 @@ def test_config1_accelerate_bert_base_mrpc_cpu(home, monkeypatch):
     from safetensors.torch import load_file
     sd = load_file(str(ck / "model.safetensors"))
     assert sd["word_embeddings"].shape == (28996, 768) and len([k for k in sd if k.startswith("layers.")]) == 12 * 12
+
+
+def test_raytrain_lightning_bert_example_cpu(home, monkeypatch):
+    """raytrain chart -> RayJob controller -> raylike TorchTrainer worker group -> Lightning
+    BERT loop (shrunk through env; CPU)."""
+    import yaml as _y
+    from mxtrain.launch import release as rel
+    monkeypatch.setenv("MXTRAIN_CPU_ONLY", "1")
+    doc = _y.safe_load(open(os.path.join(EX, "ray", "lightning-bert", "fine-tune.yaml")))
+    doc["resources"] = {"requests": {}, "limits": {}, "nnodes": 2, "node_type": None}
+    doc["train"]["args"] = ["$MXTRAIN_WORKLOADS/ray/fine_tune_text_classifier.py", "--model bert-tiny", "--cpu",
+                            "--epochs 1", "--train-size 64", "--eval-size 32", "--storage-path $HOME/ray_results",
+                            "2>&1 | tee $OUTPUT_LOG"]
+    p = home / "ray.yaml"
+    p.write_text(_y.safe_dump(doc))
+    st = rel.install(os.path.join(CHARTS, "training", "raytrain"), "ray-bert", value_files=[str(p)], wait=True,
+                     timeout=900)
+    log = rel.logs("ray-bert")
+    assert st["phase"] == "Succeeded", log
+    assert "starting worker group: 2 workers" in log and "Training result:" in log
+    res = home / "home" / "pv" / "pv-efs" / "home" / "ray-bert" / "ray_results" / "ptl-sent-classification"
+    assert (res / "checkpoint_000000" / "checkpoint.ckpt").exists()
