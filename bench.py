@@ -75,6 +75,15 @@ def main():
             use_graph = False
             tr._graph = None
             print(f"graph capture failed, running eager: {graph_err}", file=sys.stderr)
+        if world > 1:
+            # every rank must take the same path (captured collectives never ran, so a
+            # rank whose capture failed left the communicators untouched)
+            ok = torch.tensor([1 if use_graph else 0], dtype=torch.int32, device=ps.device)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0 and use_graph:
+                use_graph = False
+                tr._graph = None
+                graph_err = graph_err or "capture failed on another rank"
     for _ in range(2 if use_graph else 0):
         tr.train_step(tokens, labels)
     torch.cuda.synchronize()

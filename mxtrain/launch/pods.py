@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import json
 import os
+import re
 import signal
 import stat
 import subprocess
@@ -178,8 +179,9 @@ def build_pod(name: str, pod_template: dict, reldir: str, cm_dirs: Dict[str, str
     plan = plan_mounts(c.get("volumeMounts") or [], spec.get("volumes") or [],
                        extra=_configmap_mounts(spec, cm_dirs, c))
     env = base_env()
-    user_env = {k: plan.rewrite(v) for k, v in container_env(c).items()}
-    env.update(user_env)
+    for k, v in container_env(c).items():
+        # env values may reference earlier variables with $(VAR), as in a pod spec
+        env[k] = plan.rewrite(expand_k8s_vars(v, env))
     env.update(extra_env)
     env["HOSTNAME"] = name
     env["MXTRAIN_POD_NAME"] = name
@@ -190,7 +192,7 @@ def build_pod(name: str, pod_template: dict, reldir: str, cm_dirs: Dict[str, str
         env.setdefault("MXTRAIN_CPU_ONLY", "1")
     cmd = list(command_override if command_override is not None else
                (list(c.get("command") or []) + list(c.get("args") or [])))
-    cmd = [plan.rewrite(str(x)) for x in cmd]
+    cmd = [plan.rewrite(expand_k8s_vars(str(x), env)) for x in cmd]
     # rewrite the materialised scripts too, so hard-coded /fsx paths land on NVMe
     for mp, d in plan.mounts.items():
         if plan.mode.get(mp) == "rewrite" and d.startswith(os.path.join(reldir, "configmaps")):
@@ -206,12 +208,26 @@ def build_pod(name: str, pod_template: dict, reldir: str, cm_dirs: Dict[str, str
         cmd = ["bash"] + cmd
     home = env.get("HOME")
     workdir = c.get("workingDir")
-    workdir = plan.rewrite(workdir) if workdir else None
+    workdir = plan.rewrite(expand_k8s_vars(workdir, env)) if workdir else None
     if not workdir:
         workdir = home if home and (os.path.isdir(home) or _mkdir_ok(home)) else os.path.join(reldir, "pods", name)
     log = os.path.join(reldir, "logs", f"{name}.log")
     return PodSpec(name=name, command=cmd, env=env, workdir=workdir, log_path=log, gpus=gpus,
                    restart_policy=restart_policy, role=role, index=index), plan
+
+
+_K8S_VAR = re.compile(r"\$\$|\$\(([A-Za-z_][A-Za-z0-9_]*)\)")
+
+
+def expand_k8s_vars(s: str, env: Dict[str, str]) -> str:
+    """Kubernetes `$(VAR)` expansion in command/args against the container env; `$$`
+    escapes, unknown references stay verbatim (kubelet semantics)."""
+    def rep(m):
+        if m.group(0) == "$$":
+            return "$"
+        k = m.group(1)
+        return env[k] if k in env else m.group(0)
+    return _K8S_VAR.sub(rep, s)
 
 
 def _mkdir_ok(path: str) -> bool:

@@ -84,6 +84,13 @@ def plan_mounts(volume_mounts: List[dict], volumes: List[dict], extra: Optional[
             plan.mode[mp] = "link" if allow_link and _try_link(mp, host) else "rewrite"
         elif "hostPath" in v:
             hp = v["hostPath"].get("path")
+            if v["hostPath"].get("type") == "DirectoryOrCreate" and not os.path.isdir(hp):
+                try:
+                    os.makedirs(hp, exist_ok=True)
+                except OSError:
+                    # not creatable here (read-only /, non-root): back it by local storage
+                    hp = os.path.join(mxtrain_home(), "hostpath", hp.strip("/").replace("/", "_"))
+                    os.makedirs(hp, exist_ok=True)
             plan.mounts[mp] = hp
             plan.mode[mp] = "same" if os.path.realpath(hp) == os.path.realpath(mp) else "rewrite"
     for mp, host in (extra or {}).items():

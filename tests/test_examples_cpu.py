@@ -117,3 +117,51 @@ def test_raytrain_lightning_bert_example_cpu(home, monkeypatch):
     assert "starting worker group: 2 workers" in log and "Training result:" in log
     res = home / "home" / "pv" / "pv-efs" / "home" / "ray-bert" / "ray_results" / "ptl-sent-classification"
     assert (res / "checkpoint_000000" / "checkpoint.ckpt").exists()
+
+
+SMALL_MRCNN = ["PREPROC.TRAIN_SHORT_EDGE_SIZE=[256,256]", "PREPROC.MAX_SIZE=384", "PREPROC.TEST_SHORT_EDGE_SIZE=256",
+               "DATA.NUM_WORKERS=0", "RPN.TRAIN_PER_LEVEL_NMS_TOPK=300", "RPN.TRAIN_POST_NMS_TOPK=300",
+               "RPN.TEST_PER_LEVEL_NMS_TOPK=200", "RPN.TEST_POST_NMS_TOPK=200", "FRCNN.BATCH_PER_IM=64"]
+
+
+def test_coco_data_then_mpijob_maskrcnn_cpu(home, monkeypatch):
+    """coco-data chart (synthetic COCO on the PVC) -> mpijob chart with the tensorpack
+    example: 2 ranks through the mpirun emulator, horovod-style RCCL/gloo DDP."""
+    import yaml as _y
+    from mxtrain.launch import release as rel
+    monkeypatch.setenv("MXTRAIN_CPU_ONLY", "1")
+    monkeypatch.setenv("MXTRAIN_MAX_STEPS", "2")
+    st = rel.install(os.path.join(CHARTS, "data-prep", "coco-data"), "coco", value_files=[
+        os.path.join(EX, "maskrcnn", "coco-data.yaml")], sets=["synthetic.num_train=6", "synthetic.num_val=2",
+                                                                "synthetic.num_test=1"], wait=True, timeout=600)
+    assert st["phase"] == "Succeeded", rel.logs("coco")
+    data = home / "home" / "pv" / "pv-fsx" / "data" / "coco2017"
+    assert (data / "annotations" / "instances_train2017.json").exists()
+    assert (data / "pretrained-models" / "ImageNet-R50-AlignPadding.npz").exists()
+    doc = _y.safe_load(open(os.path.join(EX, "maskrcnn", "train-maskrcnn-tensorpack.yaml")))
+    doc["resources"] = {"gpu_nodes": 1, "gpus_per_node": 2, "gpu_instance_type": "mi355x.8x"}
+    doc["train"]["args"] = [a.replace("TRAIN.STEPS_PER_EPOCH=15000", "TRAIN.STEPS_PER_EPOCH=2")
+                            for a in doc["train"]["args"]] + SMALL_MRCNN
+    p = home / "mr.yaml"
+    p.write_text(_y.safe_dump(doc))
+    st = rel.install(os.path.join(CHARTS, "training", "mpijob-horovod-tensorflow-gpu"), "maskrcnn-tensorpack",
+                     value_files=[str(p)], wait=True, timeout=900)
+    log = rel.logs("maskrcnn-tensorpack")
+    assert st["phase"] == "Succeeded", log[-4000:]
+    assert "[1,0]<stdout>:" in log and "Epoch 1 (global_step 2) finished" in log
+    assert "Loaded 265 backbone tensors" in log
+    logs = home / "home" / "pv" / "pv-efs" / "home" / "maskrcnn-tensorpack" / "logs"
+    run = [d for d in os.listdir(logs) if d.startswith("maskrcnn-tensorpack-")]
+    assert run and any(f.endswith(".index") for f in os.listdir(logs / run[0]))
+
+
+def test_legacy_maskrcnn_chart_renders_inline_mpirun(home):
+    from mxtrain.chart.render import load_chart, render_chart
+    r = render_chart(load_chart(os.path.join(CHARTS, "training", "maskrcnn")), "mr")
+    job = r.by_kind("MPIJob")[0]
+    args = job["spec"]["mpiReplicaSpecs"]["Launcher"]["template"]["spec"]["containers"][0]["args"]
+    assert args[args.index("-np") + 1] == "8" and "$(MXTRAIN_WORKLOADS)/maskrcnn/train.py" in args
+    assert "TRAINER=horovod" in args and "TRAIN.CHECKPOINT_PERIOD=2" in args
+    r2 = render_chart(load_chart(os.path.join(CHARTS, "training", "maskrcnn-optimized")), "mr")
+    a2 = r2.by_kind("MPIJob")[0]["spec"]["mpiReplicaSpecs"]["Launcher"]["template"]["spec"]["containers"][0]["args"]
+    assert "--images_per_epoch" in a2 and "TRAIN.BATCH_SIZE_PER_GPU=4" in a2 and "PREPROC.PREDEFINED_PADDING=True" in a2
