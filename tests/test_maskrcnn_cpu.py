@@ -87,3 +87,67 @@ def test_train_cli_checkpoint_and_predict(coco_dir, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     rec = json.loads(r.stdout.strip().splitlines()[-1])
     assert os.path.exists(rec["output"])
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_jupyter_chart_viewer_serves_predictions(coco_dir, tmp_path, monkeypatch):
+    """maskrcnn-jupyter chart -> Deployment (prediction + metrics viewers) on the
+    checkpoint of a 1-step training run; basic auth enforced."""
+    import base64
+    import hashlib
+    import shutil
+    import time
+    import urllib.request
+    monkeypatch.setenv("MXTRAIN_HOME", str(tmp_path / "home"))
+    monkeypatch.setenv("MXTRAIN_NUM_GPUS", "0")
+    monkeypatch.setenv("MXTRAIN_PV_LINK", "0")
+    monkeypatch.setenv("MXTRAIN_CPU_ONLY", "1")
+    pv = tmp_path / "home" / "pv" / "pv-fsx"
+    logdir = pv / "logs" / "run1" / "train_log" / "maskrcnn"
+    shutil.copytree(coco_dir, pv / "data" / "coco2017")
+    env = dict(os.environ, PYTHONPATH=REPO)
+    common = [f"DATA.BASEDIR={pv / 'data' / 'coco2017'}", "PREPROC.TRAIN_SHORT_EDGE_SIZE=[256,256]",
+              "PREPROC.MAX_SIZE=384", "DATA.NUM_WORKERS=0", "RPN.TRAIN_PER_LEVEL_NMS_TOPK=300",
+              "RPN.TRAIN_POST_NMS_TOPK=300", "FRCNN.BATCH_PER_IM=64"]
+    r = subprocess.run([sys.executable, os.path.join(REPO, "mxtrain", "workloads", "maskrcnn", "train.py"),
+                        "--logdir", str(logdir), "--mx-max-steps", "1", "--config", "TRAIN.STEPS_PER_EPOCH=1",
+                        "TRAIN.EVAL_PERIOD=100", "DATA.VAL=()"] + common, env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    with open(logdir / "stats.json", "w") as f:
+        json.dump([{"epoch_num": 1, "global_step": 1, "mAP(bbox)/IoU=0.5:0.95": 0.0}], f)
+    from mxtrain.launch import release as rel
+    p1, p2 = _free_port(), _free_port()
+    pw_hash = "{SHA}" + base64.b64encode(hashlib.sha1(b"secret").digest()).decode()
+    rel.install(os.path.join(REPO, "charts", "machine-learning", "testing", "maskrcnn-jupyter"), "viewer",
+                sets=["global.log_dir=logs/run1", f"jupyter.target_port={p1}", f"tensorboard.target_port={p2}"],
+                set_strings=[f"nginx.htpasswd={pw_hash}"])
+    try:
+        auth = {"Authorization": "Basic " + base64.b64encode(b"tensorboard:secret").decode()}
+        deadline = time.time() + 60
+        while True:
+            try:
+                urllib.request.urlopen(urllib.request.Request(f"http://127.0.0.1:{p2}/healthz", headers=auth),
+                                       timeout=2)
+                break
+            except Exception:  # noqa: BLE001
+                assert time.time() < deadline, rel.logs("viewer")
+                time.sleep(0.5)
+        with pytest.raises(urllib.error.HTTPError):
+            urllib.request.urlopen(f"http://127.0.0.1:{p2}/stats.json", timeout=5)
+        stats = json.loads(urllib.request.urlopen(urllib.request.Request(
+            f"http://127.0.0.1:{p2}/stats.json", headers=auth), timeout=10).read())
+        assert stats[0]["global_step"] == 1
+        rec = json.loads(urllib.request.urlopen(urllib.request.Request(
+            f"http://127.0.0.1:{p1}/predict.json", headers=auth), timeout=120).read())
+        assert rec["output"].endswith(".png") and isinstance(rec["boxes"], list)
+    finally:
+        rel.uninstall("viewer")
