@@ -29,9 +29,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="gpt2-345m")
     ap.add_argument("--micro-batch-size", type=int, default=4)
+    ap.add_argument("--global-batch-size", type=int, default=None,
+                    help="default micro-batch x DP (one micro-batch per step); larger values accumulate "
+                         "micro-batches (needed to fill a pipeline)")
+    ap.add_argument("--sequence-parallel", action="store_true")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--pp", type=int, default=1)
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph step capture")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the step in a hipGraph also when N > 1 (default: single GPU only; "
+                         "eager and graph steps measure the same on MI355X, the step is GPU-bound)")
     ap.add_argument("--no-overlap", action="store_true")
     args = ap.parse_args()
 
@@ -43,7 +50,7 @@ def main():
     from mxtrain.parallel import state as pstate
     from mxtrain.training import GPTTrainer, TrainConfig, synthetic_batch
 
-    ps = pstate.initialize_model_parallel(tp=args.tp, pp=args.pp)
+    ps = pstate.initialize_model_parallel(tp=args.tp, pp=args.pp, sequence_parallel=args.sequence_parallel)
     world = ps.world_size
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
@@ -53,7 +60,7 @@ def main():
     except Exception:
         pass
     cfg = GPTConfig(**GPT_CONFIGS[args.model])
-    tcfg = TrainConfig(micro_batch_size=args.micro_batch_size,
+    tcfg = TrainConfig(micro_batch_size=args.micro_batch_size, global_batch_size=args.global_batch_size,
                        overlap_grad_reduce=not args.no_overlap, lr_warmup_iters=0)
     tr = GPTTrainer(cfg, tcfg, ps)
     gen = torch.Generator().manual_seed(1 + ps.dp_rank)
@@ -63,7 +70,7 @@ def main():
         if world > 1:
             dist.barrier()
 
-    use_graph = not args.no_graph
+    use_graph = not args.no_graph and (world == 1 or args.graph)
     graph_err = None
     for _ in range(args.warmup):
         tr.train_step(tokens, labels)
@@ -107,7 +114,8 @@ def main():
     flops = cfg.flops_per_token() * value
     if ps.rank == 0:
         out = {
-            "metric": "tokens/sec Megatron-DeepSpeed GPT-2 345M pretrain (DP+ZeRO-1)",
+            "metric": ("tokens/sec Megatron-DeepSpeed GPT-2 345M pretrain (DP+ZeRO-1)" if args.model == "gpt2-345m"
+                       else f"tokens/sec Megatron-DeepSpeed {args.model} pretrain"),
             "value": round(value, 1),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -125,7 +133,8 @@ def main():
                 "micro_batch": args.micro_batch_size,
                 "seq_len": cfg.seq_length,
                 "parallelism": f"dp{ps.dp}" + (f"_tp{args.tp}" if args.tp > 1 else "")
-                               + (f"_pp{args.pp}" if args.pp > 1 else "") + "_zero1",
+                               + (f"_pp{args.pp}" if args.pp > 1 else "")
+                               + ("_sp" if ps.sequence_parallel else "") + "_zero1",
                 "hidden_dropout": cfg.hidden_dropout,
                 "attention_dropout": cfg.attention_dropout,
                 "hipgraph": use_graph,

@@ -136,6 +136,7 @@ def save_checkpoint(save_dir: str, trainer, iteration: int, consumed_samples: in
                     local_leader: Optional[bool] = None) -> str:
     """Every rank calls this (collective barrier at the end)."""
     ps = trainer.ps
+    trainer.sync_params()
     tag = f"global_step{iteration}"
     d = os.path.join(save_dir, tag)
     os.makedirs(d, exist_ok=True)

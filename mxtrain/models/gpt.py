@@ -234,6 +234,7 @@ class StepRuntime:
     training: bool = True
     vocab_start: int = 0
     unit_done: Optional[Callable[[int], None]] = None
+    before_unit: Optional[Callable[[int], None]] = None   # wait for the unit's params (AG overlap)
     grad_scale: float = 1.0       # loss gradient scale (1 / tokens / microbatches)
 
     @property
@@ -255,6 +256,10 @@ class StepRuntime:
     def done(self, unit):
         if self.unit_done is not None:
             self.unit_done(unit)
+
+    def need(self, unit):
+        if self.before_unit is not None:
+            self.before_unit(unit)
 
     def salt(self, base):
         return base + (7919 * self.tp_rank if self.sp else 0)
@@ -492,9 +497,11 @@ class GPTStage:
         rt = self.rt
         rt.B, rt.S = B, S or self.cfg.seq_length
         if self.first:
+            rt.need(0)
             h, a = EmbedFn.apply(self.anchor, ids, rt, self.l0)
         else:
             h = hidden
+            rt.need(self.l0)
             a = NormFn.apply(h, rt, f"layers.{self.l0}.ln1", self.l0)
         for i in range(self.l0, self.l1):
             if i + 1 < self.l1:
@@ -503,6 +510,7 @@ class GPTStage:
                 nxt = "final_ln"
             else:
                 nxt = None
+            rt.need(i + 1)
             h, a = GPTLayerFn.apply(h, a, rt, i, nxt)
         if not self.last:
             return h

@@ -55,7 +55,8 @@ class DistributedOptimizer:
     def __init__(self, flat: FlatParams, dp_group=None, lr=1.5e-4, betas=(0.9, 0.999), eps=1e-8,
                  weight_decay=0.01, clip_grad=1.0, overlap: bool = True, tp_rank: int = 0,
                  tp_group=None, sp_group=None, mp_group=None, embed_group=None,
-                 pp_rank: int = 0, schedule: Optional[LRSchedule] = None):
+                 pp_rank: int = 0, schedule: Optional[LRSchedule] = None,
+                 overlap_param_gather: Optional[bool] = None):
         self.flat = flat
         self.dp_group = dp_group
         self.world = dist.get_world_size(dp_group) if dp_group is not None else 1
@@ -118,6 +119,13 @@ class DistributedOptimizer:
         self._sp_names = [s.name for s in flat.specs if s.sp_reduce]
         self.started = set()
         self.reset_pending()
+        # ZeRO-1 parameter all-gather deferred to the start of the next step and overlapped
+        # with its forward (bucket by bucket, in forward order); the layers wait on their
+        # bucket's event (StepRuntime.before_unit -> wait_unit)
+        self.overlap_param_gather = (self.overlap if overlap_param_gather is None
+                                     else bool(overlap_param_gather) and self.world > 1)
+        self.gather_pending = False
+        self._gather_events: Dict[int, object] = {}
 
     # ------------------------------------------------------------------ helpers
     def _shard_of(self, per_chunk: torch.Tensor) -> torch.Tensor:
@@ -220,12 +228,54 @@ class DistributedOptimizer:
         normsq = self.grad_norm_sq()
         optim_ops.adamw_step(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
                              self.param_shard, self.hyper, normsq=normsq, wd_flags=self.wd_flags)
-        if self.world > 1:
-            for (b, fs, so, n) in self.slices:
-                dist.all_gather_into_tensor(self.flat.data[b.start:b.end],
-                                            self.param_shard[so:so + n], group=self.dp_group)
+        self.gather_params()
         self.reset_pending()
         return normsq
+
+    # ------------------------------------------------------------------ param all-gather
+    def gather_params(self):
+        """After the update: all-gather the new bf16 shards now, or (overlap mode) mark
+        them pending for begin_param_gather() at the next step's start."""
+        if self.world == 1:
+            return
+        if self.overlap_param_gather:
+            self.gather_pending = True
+            return
+        for (b, fs, so, n) in self.slices:
+            dist.all_gather_into_tensor(self.flat.data[b.start:b.end], self.param_shard[so:so + n],
+                                        group=self.dp_group)
+
+    def begin_param_gather(self):
+        if not self.gather_pending:
+            return
+        self.gather_pending = False
+        cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        ev0 = cur.record_event() if cur is not None else None
+        # buckets are laid out last-layer-first; the forward needs them in reverse order
+        for bi in reversed(range(len(self.slices))):
+            b, fs, so, n = self.slices[bi]
+            if cur is not None:
+                with torch.cuda.stream(self.comm_stream):
+                    self.comm_stream.wait_event(ev0)
+                    dist.all_gather_into_tensor(self.flat.data[b.start:b.end], self.param_shard[so:so + n],
+                                                group=self.dp_group)
+                    self._gather_events[bi] = self.comm_stream.record_event()
+            else:
+                dist.all_gather_into_tensor(self.flat.data[b.start:b.end], self.param_shard[so:so + n],
+                                            group=self.dp_group)
+
+    def wait_unit(self, unit: int):
+        bi = self.flat.unit_to_bucket.get(unit)
+        ev = self._gather_events.pop(bi, None) if bi is not None else None
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+
+    def finish_param_gather(self):
+        """Make every parameter current (before eval / checkpointing / inspection)."""
+        self.begin_param_gather()
+        if self.device.type == "cuda":
+            for bi in list(self._gather_events):
+                torch.cuda.current_stream(self.device).wait_event(self._gather_events.pop(bi))
 
     # ------------------------------------------------------------------ checkpoint
     def shard_state(self) -> dict:

@@ -112,12 +112,16 @@ class GPTTrainer:
             self.opt.step_count += 1   # bias corrections use the new step, as in eager step()
             self.opt.set_hyper(self.opt.schedule(self.opt.step_count))
             self._graph.replay()
+            # the replay left this step's update un-gathered (the next replay's body, or a
+            # sync_params(), gathers it; re-gathering an unchanged shard is idempotent)
+            self.opt.gather_pending = self.opt.overlap_param_gather
             self.iteration += 1
             return self._static_loss
         return self._train_step_eager(tokens, labels)
 
     def _train_step_eager(self, tokens, labels):
         nm, B, S = tokens.shape
+        self._begin_step()
         self.flat.zero_grad()
         self.seed.advance()
         self.stage.rt.grad_scale = 1.0 / (nm * B * S)
@@ -162,6 +166,9 @@ class GPTTrainer:
     def _graph_body(self):
         tokens, labels = self._static
         nm, B, S = tokens.shape
+        # the captured step starts by gathering the shards the previous replay updated
+        self.opt.gather_pending = self.opt.overlap_param_gather
+        self._begin_step()
         self.flat.zero_grad()
         self.seed.advance()
         self.stage.rt.grad_scale = 1.0 / (nm * B * S)
@@ -180,18 +187,27 @@ class GPTTrainer:
         from .ops import optim as optim_ops
         optim_ops.adamw_step(o.master, o.exp_avg, o.exp_avg_sq, o.grad_shard, o.param_shard,
                              o.hyper, normsq=normsq, wd_flags=o.wd_flags)
-        if o.world > 1:
-            for (b, fs, so, n) in o.slices:
-                dist.all_gather_into_tensor(self.flat.data[b.start:b.end],
-                                            o.param_shard[so:so + n], group=o.dp_group)
+        o.gather_params()
+        o.gather_pending = False   # (overlap mode) the next replay's body gathers
+        o._gather_events.clear()
         o.reset_pending()
         return loss
+
+    def _begin_step(self):
+        self.opt.begin_param_gather()
+        self.stage.rt.before_unit = self.opt.wait_unit if self.opt.overlap_param_gather else None
+
+    def sync_params(self):
+        """Complete a deferred parameter all-gather (call before reading parameters)."""
+        self.opt.finish_param_gather()
+        self.stage.rt.before_unit = None
 
     @torch.no_grad()
     def eval_step(self, tokens: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         """Forward-only loss (dropout off, no gradients, optimizer untouched); mean over
         the step's tokens on the last stage."""
         nm, B, S = tokens.shape
+        self.sync_params()
         rt = self.stage.rt
         rt.training = False
         rt.unit_done = None

@@ -51,22 +51,26 @@ def _worker(rank, world, port, mode, q):
     from mxtrain.models.gpt import GPTConfig, shard_gpt_state
     from mxtrain.parallel import state as pstate
     from mxtrain.training import GPTTrainer, TrainConfig
-    tp = 2 if mode in ("tp", "sp") else 1
-    pp = 2 if mode == "pp" else 1
-    ps = pstate.initialize_model_parallel(tp=tp, pp=pp, sequence_parallel=mode == "sp",
+    tp = 2 if mode in ("tp", "sp", "3d", "3dsp") else 1
+    pp = 2 if mode in ("pp", "3d", "3dsp") else 1
+    ps = pstate.initialize_model_parallel(tp=tp, pp=pp, sequence_parallel=mode in ("sp", "3dsp"),
                                           backend="gloo", device_type="cpu")
     cfg = GPTConfig(**CFG)
     # reference init (identical on every rank), then take this rank's shard
     _, _, init_sd = _ref_init()
     tcfg = TrainConfig(micro_batch_size=2, global_batch_size=4, lr=1e-3, overlap_grad_reduce=False)
     tr = GPTTrainer(cfg, tcfg, ps, dtype=torch.float32)
+    if ps.dp > 1:
+        # exercise the deferred (next-step, per-bucket) ZeRO-1 parameter all-gather path
+        tr.opt.overlap_param_gather = True
     local = shard_gpt_state(init_sd, cfg, ps.tp, ps.tp_rank, ps.pp, ps.pp_rank)
     tr.flat.load_state_dict(local)
     tr.opt._refresh_master()
     tok, lab = _data()
-    if mode == "dp":
-        tok, lab = tok[rank:rank + 1], lab[rank:rank + 1]
+    if ps.dp > 1:
+        tok, lab = tok[ps.dp_rank:ps.dp_rank + 1], lab[ps.dp_rank:ps.dp_rank + 1]
     losses = [float(tr.train_step(tok, lab)) for _ in range(2)]
+    tr.sync_params()
     # numpy copies: tensors sent through a spawn queue are fd-shared and vanish with the
     # worker process
     q.put((rank, mode, losses, {n: p.detach().clone().numpy() for n, p in tr.flat.params.items()},
@@ -89,11 +93,11 @@ def _ref_init():
     return _REF["init"]
 
 
-def _run(mode):
+def _run(mode, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]
@@ -159,3 +163,21 @@ def test_tp2_sequence_parallel_matches_single(reference):
 
 def test_pp2_1f1b_matches_single(reference):
     _check("pp", reference, loss_ranks=(1,))
+
+
+@pytest.mark.parametrize("mode", ["3d", "3dsp"])
+def test_tp2_pp2_dp2_matches_single(reference, mode):
+    """BASELINE config 4 topology (TP=2 x PP=2 x DP=2 = 8 ranks, + SP variant) on a tiny
+    GPT: every rank's parameter shard after two ZeRO-1 steps equals the single-process
+    result, and the DP-mean of the last stage's losses equals the reference loss."""
+    from mxtrain.models.gpt import shard_gpt_state
+    cfg, ref_losses, ref_sd = reference
+    res = _run(mode, world=8)
+    last = [r for r in res if r[4][1] == 1 and r[4][0] == 0]           # last stage, tp rank 0
+    assert len(last) == 2
+    mean_first = sum(r[2][0] for r in last) / 2
+    assert abs(mean_first - ref_losses[0]) < 2e-5 * max(1.0, abs(ref_losses[0]))
+    for rank, _, losses, params, (tpr, ppr, dpr) in res:
+        exp = shard_gpt_state(ref_sd, cfg, 2, tpr, 2, ppr)
+        for n, t in exp.items():
+            assert torch.allclose(params[n], t, atol=3e-5, rtol=1e-4), (mode, rank, n, (params[n] - t).abs().max())
