@@ -8,7 +8,8 @@
     python -m mxtrain template <release> <chart> [-f ...] [--set ...]     (render only, helm template)
     python -m mxtrain lint <chart> [-f ...]
     python -m mxtrain pipeline run <pipeline.yaml>                        (KFP chart pipeline)
-    python -m mxtrain node                                                (topology / GPU ledger)
+    python -m mxtrain node [--check]                                      (topology / GPU ledger / acceptance)
+    python -m mxtrain hpo run <experiment.yaml>                           (Katib-style search)
 """
 from __future__ import annotations
 
@@ -123,7 +124,19 @@ def cmd_pipeline(a):
     return 0 if res == "Success" else 1
 
 
+def cmd_hpo(a):
+    from .hpo import load_experiment, run_experiment
+    res = run_experiment(load_experiment(a.file), a.namespace)
+    b = res["best"]
+    print(json.dumps({"condition": res["condition"], "best": b and {"trial": b["trial"], "parameters": b["parameters"],
+                                                                  "metrics": b["metrics"]}}, indent=1))
+    return 0 if res["condition"] == "Succeeded" else 1
+
+
 def cmd_node(a):
+    if a.check:
+        from .runtime.nodecheck import main as nodecheck
+        return nodecheck([] if a.gpus is None else ["--gpus", str(a.gpus)])
     from .runtime.topology import NODE_PROFILES, num_gpus
     from .runtime.storage import mxtrain_home, pv_root
     led = os.path.join(mxtrain_home(), "gpu-ledger.json")
@@ -177,7 +190,14 @@ def build_parser():
     q.add_argument("file")
     q.set_defaults(fn=cmd_pipeline)
     q = sp.add_parser("node")
+    q.add_argument("--check", action="store_true", help="run the node acceptance checks (GPUs, HBM, RCCL, PV)")
+    q.add_argument("--gpus", type=int, default=None)
     q.set_defaults(fn=cmd_node)
+    q = sp.add_parser("hpo")
+    q.add_argument("action", choices=["run"])
+    q.add_argument("file")
+    q.add_argument("-n", "--namespace", default=rel.DEFAULT_NS)
+    q.set_defaults(fn=cmd_hpo)
     return p
 
 

@@ -256,36 +256,40 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 //   level 2: fold the groups, write bf16 (optionally adding); flat column c of the
 //            [nvec][cols] layout goes to output k = c / cols.
 namespace {
-__global__ __launch_bounds__(256) void colreduce_l1_kernel(const float* __restrict__ in, int P,
-                                                           int C, float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  const int p0 = blockIdx.y * 64, p1 = min(P, p0 + 64);
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int p = p0;
-  for (; p + 4 <= p1; p += 4) {
-    s0 += in[(size_t)p * C + c];
-    s1 += in[(size_t)(p + 1) * C + c];
-    s2 += in[(size_t)(p + 2) * C + c];
-    s3 += in[(size_t)(p + 3) * C + c];
-  }
-  for (; p < p1; ++p) s0 += in[(size_t)p * C + c];
-  out[(size_t)blockIdx.y * C + c] = (s0 + s1) + (s2 + s3);
-}
-
-__global__ __launch_bounds__(256) void colreduce_l2_kernel(
-    const float* __restrict__ in, int Q, int cols, int nvec, uint16_t* __restrict__ o0,
-    uint16_t* __restrict__ o1, uint16_t* __restrict__ o2, int accumulate) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+// One-launch deterministic column reduction of fp32 partial rows [P][nvec*cols] into up to
+// three bf16 vectors.  Block = 8 waves over 64 columns (lane = column, 256-B coalesced
+// row reads); wave w sums rows w, w+8, ... with 8 loads in flight, then the 8 wave sums
+// are folded in LDS in a fixed order.  (The previous two-level l1/l2 pair cost two
+// latency-bound launches per norm backward.)
+__global__ __launch_bounds__(512) void colreduce_kernel(const float* __restrict__ in, int P, int cols, int nvec,
+                                                        uint16_t* __restrict__ o0, uint16_t* __restrict__ o1,
+                                                        uint16_t* __restrict__ o2, int accumulate) {
+  __shared__ float part[8][64];
   const int C = nvec * cols;
-  if (idx >= C) return;
-  const int k = idx / cols, c = idx % cols;
-  uint16_t* o = k == 0 ? o0 : (k == 1 ? o1 : o2);
-  if (!o) return;
-  float s = 0.f;
-  for (int q = 0; q < Q; ++q) s += in[(size_t)q * C + idx];
-  if (accumulate) s += bf2f(o[c]);
-  o[c] = f2bf(s);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    int p = w;
+    for (; p + 56 < P; p += 64) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += in[(size_t)(p + 8 * j) * C + c];
+    }
+    for (; p < P; p += 8) a[0] += in[(size_t)p * C + c];
+  }
+  part[w][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (w == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += part[k][lane];
+    const int k = c / cols, cc = c % cols;
+    uint16_t* o = k == 0 ? o0 : (k == 1 ? o1 : o2);
+    if (o) {
+      if (accumulate) t += bf2f(o[cc]);
+      o[cc] = f2bf(t);
+    }
+  }
 }
 
 // Column sum of a bf16 matrix [rows, cols] -> fp32 partials [rows/64][cols]
@@ -379,17 +383,10 @@ MX_EXPORT int64_t mx_colreduce_scratch(int P, int C) { return (int64_t)((P + 63)
 MX_EXPORT int mx_colsum_finalize(const float* partial, int nparts, int cols, int nvec,
                                  void* o0, void* o1, void* o2, int accumulate, float* scratch,
                                  hipStream_t s) {
+  (void)scratch;  // single-level reduction: no scratch needed (kept for ABI stability)
   const int C = nvec * cols;
-  const float* src = partial;
-  int Q = nparts;
-  if (nparts > 64) {
-    dim3 g1((C + 255) / 256, (nparts + 63) / 64);
-    hipLaunchKernelGGL(colreduce_l1_kernel, g1, dim3(256), 0, s, partial, nparts, C, scratch);
-    src = scratch;
-    Q = g1.y;
-  }
-  hipLaunchKernelGGL(colreduce_l2_kernel, dim3((C + 255) / 256), dim3(256), 0, s, src, Q, cols,
-                     nvec, (uint16_t*)o0, (uint16_t*)o1, (uint16_t*)o2, accumulate);
+  hipLaunchKernelGGL(colreduce_kernel, dim3((C + 63) / 64), dim3(512), 0, s, partial, nparts, cols, nvec,
+                     (uint16_t*)o0, (uint16_t*)o1, (uint16_t*)o2, accumulate);
   return hipGetLastError();
 }
 

@@ -62,7 +62,20 @@ __global__ void sum_partials_kernel(const float* __restrict__ partial, int n,
   }
 }
 
-// 4 elements per thread-iteration; wd_flags has one byte per 64-element chunk.
+// 8 elements per thread-iteration (two float4 of each fp32 state, one 16-B bf16 grad
+// load, one 16-B bf16 param store), every load of the iteration issued before any math,
+// non-temporal access (the 28 B/element stream is touched exactly once per step and
+// must not evict anything useful from L2).  wd_flags has one byte per 64-element chunk.
+typedef float nf4 __attribute__((ext_vector_type(4)));
+typedef unsigned int nu4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldnt4(const float* p) {   // one global_load_dwordx4 ... nt
+  const nf4 v = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void stnt4(float* p, float4 v) {
+  __builtin_nontemporal_store((nf4){v.x, v.y, v.z, v.w}, reinterpret_cast<nf4*>(p));
+}
+
 __global__ __launch_bounds__(256) void adamw_kernel(
     float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
     const uint16_t* __restrict__ grad, uint16_t* __restrict__ param_out,
@@ -81,32 +94,37 @@ __global__ __launch_bounds__(256) void adamw_kernel(
   }
   const float step_size = lr / bc1;
   const float inv_sqrt_bc2 = rsqrtf(bc2);
-  const int64_t nvec = n / 4;
+  const int64_t nvec = n / 8;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
-    float4 p = reinterpret_cast<float4*>(master)[i];
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
-    uint2 graw = reinterpret_cast<const uint2*>(grad)[i];
-    const float decay = (wd_flags == nullptr || wd_flags[(i * 4) >> 6]) ? wd : 0.f;
-    float g[4] = {lo_bf(graw.x) * gs, hi_bf(graw.x) * gs, lo_bf(graw.y) * gs,
-                  hi_bf(graw.y) * gs};
-    float* pp = &p.x;
-    float* pm = &mm.x;
-    float* pv = &vv.x;
+    const int64_t e = i * 8;
+    const float4 p0 = ldnt4(master + e), p1 = ldnt4(master + e + 4);
+    const float4 m0 = ldnt4(m + e), m1 = ldnt4(m + e + 4);
+    const float4 v0 = ldnt4(v + e), v1 = ldnt4(v + e + 4);
+    const nu4 gr = __builtin_nontemporal_load(reinterpret_cast<const nu4*>(grad) + i);
+    const uint4 graw = make_uint4(gr.x, gr.y, gr.z, gr.w);
+    const float decay = (wd_flags == nullptr || wd_flags[e >> 6]) ? wd : 0.f;
+    float g[8];
+    unpack8(graw, g);
+    float pp[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+    float pm[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+    float pv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    const float keep = 1.f - lr * decay;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      pm[j] = b1 * pm[j] + (1.f - b1) * g[j];
-      pv[j] = b2 * pv[j] + (1.f - b2) * g[j] * g[j];
+    for (int j = 0; j < 8; ++j) {
+      const float gj = g[j] * gs;
+      pm[j] = b1 * pm[j] + (1.f - b1) * gj;
+      pv[j] = b2 * pv[j] + (1.f - b2) * gj * gj;
       const float denom = sqrtf(pv[j]) * inv_sqrt_bc2 + eps;
-      pp[j] = pp[j] * (1.f - lr * decay) - step_size * pm[j] / denom;
+      pp[j] = pp[j] * keep - step_size * pm[j] / denom;
     }
-    reinterpret_cast<float4*>(master)[i] = p;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
-    uint2 out;
-    out.x = pack2(p.x, p.y);
-    out.y = pack2(p.z, p.w);
-    reinterpret_cast<uint2*>(param_out)[i] = out;
+    stnt4(master + e, make_float4(pp[0], pp[1], pp[2], pp[3]));
+    stnt4(master + e + 4, make_float4(pp[4], pp[5], pp[6], pp[7]));
+    stnt4(m + e, make_float4(pm[0], pm[1], pm[2], pm[3]));
+    stnt4(m + e + 4, make_float4(pm[4], pm[5], pm[6], pm[7]));
+    stnt4(v + e, make_float4(pv[0], pv[1], pv[2], pv[3]));
+    stnt4(v + e + 4, make_float4(pv[4], pv[5], pv[6], pv[7]));
+    const uint4 po = pack8(pp);
+    __builtin_nontemporal_store((nu4){po.x, po.y, po.z, po.w}, reinterpret_cast<nu4*>(param_out) + i);
   }
 }
 
@@ -131,8 +149,9 @@ MX_EXPORT int mx_sumsq_bf16(const void* g, int64_t n, float scale, const uint8_t
 MX_EXPORT int mx_adamw_step(float* master, float* m, float* v, const void* grad,
                             void* param_out, const uint8_t* wd_flags, int64_t n,
                             const float* hyper, const float* normsq, hipStream_t s) {
-  int64_t blocks = (n / 4 + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
+  if (n % 8) return hipErrorInvalidValue;  // flat shards are 64-element aligned
+  int64_t blocks = (n / 8 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, s, master, m, v,
                      (const uint16_t*)grad, (uint16_t*)param_out, wd_flags, n, hyper, normsq);

@@ -249,6 +249,9 @@ class Supervisor:
         self._stopping = True
 
     def run(self, timeout: Optional[float] = None) -> int:
+        import threading
+        if threading.current_thread() is not threading.main_thread():
+            return self._run(timeout)   # e.g. parallel HPO trials: signals stay with the main thread
         prev = (signal.signal(signal.SIGTERM, self._on_signal), signal.signal(signal.SIGINT, self._on_signal))
         try:
             return self._run(timeout)

@@ -226,3 +226,23 @@ def test_gpu_ledger_disjoint(tmp_path):
         b.allocate(1)
     a.release(ga)
     assert len(b.allocate(4)) == 4
+
+
+def test_hpo_random_and_grid_search(home, tmp_path):
+    """Katib-style experiment over the data-process chart: the trial prints a loss that
+    is minimal at x=3; grid search must find it, StdOut collector parses it."""
+    from mxtrain.hpo import run_experiment
+    exp = {"name": "quad", "objective": {"type": "minimize", "objectiveMetricName": "loss"},
+           "algorithm": {"algorithmName": "grid"}, "parallelTrialCount": 2, "maxTrialCount": 5,
+           "parameters": [{"name": "x", "parameterType": "int", "feasibleSpace": {"min": "1", "max": "5"}}],
+           "trialTemplate": {"chart": os.path.join(CHARTS, "data-prep", "data-process"),
+                             "set": ["process.command[0]=python3", "process.args[0]=-c",
+                                     "process.args[1]=\"print('step 10 loss: %f' % ((${trialParameters.x}-3)**2+0.5))\""]}}
+    res = run_experiment(exp, log=lambda *a: None)
+    assert res["condition"] == "Succeeded" and len(res["trials"]) == 5
+    assert res["best"]["parameters"]["x"] == "3" and res["best"]["metrics"]["loss"] == pytest.approx(0.5)
+    exp["algorithm"] = {"algorithmName": "random", "seed": 1}
+    exp["name"] = "quad-r"
+    exp["earlyStopping"] = {"algorithmName": "medianstop", "minTrialsRequired": 2}
+    res = run_experiment(exp, log=lambda *a: None)
+    assert {t["status"] for t in res["trials"]} <= {"Succeeded", "EarlyStopped"}
