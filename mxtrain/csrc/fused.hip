@@ -57,6 +57,80 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
   for (int j = 0; j < 8; ++j) p[j] = acc[j];
 }
 
+// ---------------------------------------------------------------- bias + SwiGLU
+// pre = [a | b] (each `f` columns, Megatron --swiglu layout); y = silu(a + ba) * (b + bb)
+__device__ __forceinline__ float silu_f(float x) {
+  return x * __builtin_amdgcn_rcpf(1.f + __expf(-x));
+}
+__global__ __launch_bounds__(256) void bias_swiglu_fwd_kernel(
+    const uint16_t* __restrict__ pre, const uint16_t* __restrict__ bias,
+    uint16_t* __restrict__ y, int rows, int f) {
+  const int nv = f / 8;
+  const int64_t total = (int64_t)rows * nv;
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < total;
+       w += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(w / nv);
+    const int c = (int)(w % nv) * 8;
+    const uint16_t* row = pre + (size_t)r * 2 * f;
+    float a[8], b[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(row + c), a);
+    unpack8(*reinterpret_cast<const uint4*>(row + f + c), b);
+    if (bias) {
+      float ba[8], bb[8];
+      unpack8(*reinterpret_cast<const uint4*>(bias + c), ba);
+      unpack8(*reinterpret_cast<const uint4*>(bias + f + c), bb);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a[j] += ba[j]; b[j] += bb[j]; }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = silu_f(a[j]) * b[j];
+    *reinterpret_cast<uint4*>(y + (size_t)r * f + c) = pack8(o);
+  }
+}
+
+// da = dy * b * silu'(a), db = dy * silu(a); partial[blockIdx.y][0..2f) = row-block sums
+__global__ __launch_bounds__(256) void bias_swiglu_bwd_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ pre,
+    const uint16_t* __restrict__ bias, uint16_t* __restrict__ dpre, int rows, int f,
+    int rows_per_block, float* __restrict__ partial) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= f) return;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  float ba[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (bias) {
+    unpack8(*reinterpret_cast<const uint4*>(bias + c), ba);
+    unpack8(*reinterpret_cast<const uint4*>(bias + f + c), bb);
+  }
+  float acca[8] = {0, 0, 0, 0, 0, 0, 0, 0}, accb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = r0; r < r1; ++r) {
+    const uint16_t* row = pre + (size_t)r * 2 * f;
+    float g[8], a[8], b[8], da[8], db[8];
+    unpack8(*reinterpret_cast<const uint4*>(dy + (size_t)r * f + c), g);
+    unpack8(*reinterpret_cast<const uint4*>(row + c), a);
+    unpack8(*reinterpret_cast<const uint4*>(row + f + c), b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = a[j] + ba[j], v = b[j] + bb[j];
+      const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-x));
+      const float sl = x * sg;
+      da[j] = g[j] * v * (sg + sl * (1.f - sg));
+      db[j] = g[j] * sl;
+    }
+    uint4 pa = pack8(da), pb = pack8(db);
+    uint16_t* drow = dpre + (size_t)r * 2 * f;
+    *reinterpret_cast<uint4*>(drow + c) = pa;
+    *reinterpret_cast<uint4*>(drow + f + c) = pb;
+    unpack8(pa, da);
+    unpack8(pb, db);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { acca[j] += da[j]; accb[j] += db[j]; }
+  }
+  float* p = partial + (size_t)blockIdx.y * 2 * f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { p[c + j] = acca[j]; p[f + c + j] = accb[j]; }
+}
+
 // ---------------------------------------------------------------- embedding
 // out[t] = wte[ids[t] - vocab_start] (+ wpe[t % seq]); rows outside the local vocab
 // shard are zero (vocab-parallel embedding; the TP all-reduce sums the shards).
@@ -253,6 +327,32 @@ MX_EXPORT int mx_bias_gelu_bwd(const void* dy, const void* x, const void* bias, 
   if (dbias)
     return mx_colsum_finalize(partial, (int)grid.y, cols, 1, dbias, nullptr, nullptr,
                               accumulate, partial + (size_t)grid.y * cols, s);
+  return hipGetLastError();
+}
+
+MX_EXPORT int mx_bias_swiglu_fwd(const void* pre, const void* bias, void* y, int rows, int f,
+                                 hipStream_t s) {
+  if (f % 8) return hipErrorInvalidValue;
+  int64_t blocks = ((int64_t)rows * (f / 8) + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(bias_swiglu_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                     (const uint16_t*)pre, (const uint16_t*)bias, (uint16_t*)y, rows, f);
+  return hipGetLastError();
+}
+
+// partial: ceil(rows/16)*2f floats + mx_colreduce_scratch(ceil(rows/16), 2f) behind it
+MX_EXPORT int mx_bias_swiglu_bwd(const void* dy, const void* pre, const void* bias, void* dpre,
+                                 void* dbias, int accumulate, float* partial, int rows, int f,
+                                 hipStream_t s) {
+  if (f % 8) return hipErrorInvalidValue;
+  const int rpb = 16;
+  dim3 grid((f / 8 + 255) / 256, (rows + rpb - 1) / rpb);
+  hipLaunchKernelGGL(bias_swiglu_bwd_kernel, grid, dim3(256), 0, s, (const uint16_t*)dy,
+                     (const uint16_t*)pre, (const uint16_t*)bias, (uint16_t*)dpre, rows, f, rpb,
+                     partial);
+  if (dbias)
+    return mx_colsum_finalize(partial, (int)grid.y, 2 * f, 1, dbias, nullptr, nullptr,
+                              accumulate, partial + (size_t)grid.y * 2 * f, s);
   return hipGetLastError();
 }
 

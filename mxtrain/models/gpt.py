@@ -33,8 +33,9 @@ import torch
 from .. import ops
 from ..ops import attention as attn_ops
 from ..ops.norm import bda_norm_fwd, colsum, layernorm_fwd, norm_bwd
-from ..ops.fused import (bias_gelu_bwd, bias_gelu_fwd, cross_entropy_fwd_bwd, embed_bwd,
-                         embed_fwd, pos_embed_bwd)
+from ..ops.rope import apply_rope_
+from ..ops.fused import (bias_gelu_bwd, bias_gelu_fwd, bias_swiglu_bwd, bias_swiglu_fwd,
+                         cross_entropy_fwd_bwd, embed_bwd, embed_fwd, pos_embed_bwd)
 from ..parallel import collectives as C
 from ..parallel.buffers import ParamSpec
 
@@ -56,6 +57,9 @@ class GPTConfig:
     init_method_std: float = 0.02
     normalization: str = "layernorm"       # layernorm | rmsnorm
     position_embedding: str = "learned"    # learned | rope
+    rotary_percent: float = 1.0
+    swiglu: bool = False                   # fc1 -> [a | b], silu(a) * b (Megatron --swiglu)
+    rotary_base: float = 10000.0
     tie_embeddings: bool = True
 
     def __post_init__(self):
@@ -76,8 +80,9 @@ class GPTConfig:
         h, f, L = self.hidden_size, self.ffn_hidden_size, self.num_layers
         V = self.padded_vocab(tp)
         kvh = self.num_kv_heads * self.head_dim
+        f1 = 2 * f if self.swiglu else f
         per_layer = (2 * h + (h * (h + 2 * kvh) + h + 2 * kvh) + (h * h + h) + 2 * h
-                     + (h * f + f) + (f * h + h))
+                     + (h * f1 + f1) + (f * h + h))
         if self.normalization == "rmsnorm":
             per_layer -= 2 * h
         n = V * h + L * per_layer + 2 * h
@@ -123,6 +128,7 @@ def gpt_param_specs(cfg: GPTConfig, tp: int = 1, pp: int = 1, pp_rank: int = 0,
     hl = cfg.num_attention_heads // tp
     kvl = cfg.num_kv_heads // tp
     fl = cfg.ffn_hidden_size // tp
+    f1l = 2 * fl if cfg.swiglu else fl
     V = cfg.padded_vocab(tp) // tp
     std = cfg.init_method_std
     rms = cfg.normalization == "rmsnorm"
@@ -162,8 +168,8 @@ def gpt_param_specs(cfg: GPTConfig, tp: int = 1, pp: int = 1, pp_rank: int = 0,
         ]
         norm(p + "ln2", u)
         specs += [
-            ParamSpec(p + "fc1_w", (fl, h), std=std, unit=u, tp_duplicated=nd),
-            ParamSpec(p + "fc1_b", (fl,), "zeros", weight_decay=False, unit=u, tp_duplicated=nd),
+            ParamSpec(p + "fc1_w", (f1l, h), std=std, unit=u, tp_duplicated=nd),
+            ParamSpec(p + "fc1_b", (f1l,), "zeros", weight_decay=False, unit=u, tp_duplicated=nd),
             ParamSpec(p + "fc2_w", (h, fl), "scaled_normal", std=std, unit=u, tp_duplicated=nd),
             ParamSpec(p + "fc2_b", (h,), "zeros", weight_decay=False, unit=u, sp_reduce=sp),
         ]
@@ -206,6 +212,11 @@ def shard_gpt_state(global_sd: Dict[str, torch.Tensor], cfg: GPTConfig, tp: int 
             v = t[(H + KV) * D:]
             t = torch.cat([q[r * hl * D:(r + 1) * hl * D], k[r * kvl * D:(r + 1) * kvl * D],
                            v[r * kvl * D:(r + 1) * kvl * D]], 0)
+        elif base in ("fc1_w", "fc1_b") and cfg.swiglu:
+            # column-parallel [a | b]: every rank keeps matching slices of both halves
+            fh = t.shape[0] // 2
+            n = fh // tp
+            t = torch.cat([t[r * n:(r + 1) * n], t[fh + r * n:fh + (r + 1) * n]], 0)
         elif base in ("fc1_w", "fc1_b"):
             n = t.shape[0] // tp
             t = t[r * n:(r + 1) * n]
@@ -244,6 +255,17 @@ class StepRuntime:
     @property
     def rms(self):
         return self.cfg.normalization == "rmsnorm"
+
+    def rope_(self, x, hl, kvl, inverse=False):
+        """RoPE (K5) in place on the Q and K blocks of a packed [T, (hl+2kvl)*D] buffer."""
+        cfg = self.cfg
+        if cfg.position_embedding != "rope":
+            return
+        D = cfg.head_dim
+        rd = int(D * cfg.rotary_percent) // 8 * 8
+        for col0, nh in ((0, hl), (hl * D, kvl)):
+            apply_rope_(x, col0, nh, D, self.S, rd, cfg.rotary_base,
+                        max_pos=cfg.max_position_embeddings, inverse=inverse)
 
     def norm_params(self, prefix):
         w = self.params[prefix + "_w"]
@@ -359,6 +381,7 @@ class GPTLayerFn(torch.autograd.Function):
         eps = cfg.layernorm_epsilon
         a_full = _gather(a, rt)
         qkv = torch.addmm(P[p + "qkv_b"], a_full, P[p + "qkv_w"].t())
+        rt.rope_(qkv, hl, kvl)
         q = qkv[:, : hl * D]
         k = qkv[:, hl * D:(hl + kvl) * D]
         v = qkv[:, (hl + kvl) * D:]
@@ -369,7 +392,10 @@ class GPTLayerFn(torch.autograd.Function):
                                            rt.salt(1000 + 2 * i), rt.rms)
         m_full = _gather(m, rt)
         pre = torch.mm(m_full, P[p + "fc1_w"].t())
-        f = bias_gelu_fwd(pre, P[p + "fc1_b"])
+        if cfg.swiglu:
+            f = bias_swiglu_fwd(pre, P[p + "fc1_b"])
+        else:
+            f = bias_gelu_fwd(pre, P[p + "fc1_b"])
         g = _reduce(torch.mm(f, P[p + "fc2_w"].t()), rt)
         if next_norm is not None:
             wn, bn = rt.norm_params(next_norm)
@@ -413,8 +439,11 @@ class GPTLayerFn(torch.autograd.Function):
         dg_full = _gather(dg, rt)
         _wgrad(G[p + "fc2_w"], dg_full, f)
         df = torch.mm(dg_full, P[p + "fc2_w"])
-        dpre = bias_gelu_bwd(df, pre, P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True,
-                             inplace=True)
+        if cfg.swiglu:
+            dpre = bias_swiglu_bwd(df, pre, P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True)
+        else:
+            dpre = bias_gelu_bwd(df, pre, P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True,
+                                 inplace=True)
         _wgrad(G[p + "fc1_w"], dpre, m_full)
         dm = _reduce(torch.mm(dpre, P[p + "fc1_w"]), rt)
         # ---- BDA-LN2 backward
@@ -434,6 +463,7 @@ class GPTLayerFn(torch.autograd.Function):
         attn_ops.attn_bwd(dctx, q, k, v, ctx_, lse, rt.B, rt.S, hl, kvl, D, causal=True,
                           dq=dqkv[:, : hl * D], dk=dqkv[:, hl * D:(hl + kvl) * D],
                           dv=dqkv[:, (hl + kvl) * D:])
+        rt.rope_(dqkv, hl, kvl, inverse=True)
         colsum(dqkv, G[p + "qkv_b"], accumulate=True)
         _wgrad(G[p + "qkv_w"], dqkv, a_full)
         da = _reduce(torch.mm(dqkv, P[p + "qkv_w"]), rt)

@@ -10,6 +10,7 @@ from .fused import (bias_gelu, bias_gelu_bwd, bias_gelu_fwd, ce_stats,  # noqa: 
 from .norm import (bda_norm_fwd, colsum, layer_norm, layernorm_fwd, norm_bwd,  # noqa: F401
                    rms_norm)
 from .optim import adamw_step, sumsq_bf16  # noqa: F401
+from .rope import apply_rope_, rope  # noqa: F401
 
 
 def library_loaded() -> bool:

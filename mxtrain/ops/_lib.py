@@ -40,6 +40,8 @@ SIGNATURES = {
     "mx_bias_gelu_fwd": [P, P, P, I, I, P],
     "mx_bias_gelu_bwd_rows_per_block": [],
     "mx_bias_gelu_bwd": [P, P, P, P, P, I, P, I, I, P],
+    "mx_bias_swiglu_fwd": [P, P, P, I, I, P],
+    "mx_bias_swiglu_bwd": [P, P, P, P, P, I, P, I, I, P],
     "mx_embed_fwd": [P, P, P, P, I, I, I, I64, I64, I, P],
     "mx_embed_bwd": [P, P, P, P, I, I, I64, I64, P],
     "mx_pos_embed_bwd": [P, P, I, I, I, P],
@@ -54,6 +56,8 @@ SIGNATURES = {
     "mx_attn_fwd": [P, P, P, I, I, I, P, I, P, I, I, I, I, I, I, P, F, P],
     "mx_attn_bwd": [P, P, P, I, I, I, P, I, P, I, P, P, P, P, I, P, P, I, I, I, I, I, I, I,
                     I, P, F, P],
+    # rope.hip
+    "mx_rope": [P, I64, I, I, I, I, I, I, I, P, P, P, I, P],
     # vision.hip
     "mx_roi_align_fwd": [P, P, P, P, I, I, F, I, P, I, I, I, I, I, I, P, P],
     "mx_roi_align_bwd": [P, P, P, P, I, I, F, I, P, I, I, I, I, I, I, P, P],

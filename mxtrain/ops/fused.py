@@ -75,6 +75,48 @@ def bias_gelu(x, bias):
     return BiasGeluFn.apply(x, bias)
 
 
+# ------------------------------------------------------------------ bias + SwiGLU
+def _silu(x):
+    return x * torch.sigmoid(x)
+
+
+def bias_swiglu_fwd(pre, bias=None):
+    """pre [rows, 2f] = [a | b] -> silu(a + ba) * (b + bb) [rows, f] (Megatron --swiglu)."""
+    rows, f2 = pre.shape
+    f = f2 // 2
+    if not _lib.use_hip(pre):
+        x = pre.float() + (bias.float() if bias is not None else 0.0)
+        return (_silu(x[:, :f]) * x[:, f:]).to(pre.dtype)
+    y = torch.empty(rows, f, dtype=pre.dtype, device=pre.device)
+    _lib.call("mx_bias_swiglu_fwd", _lib.ptr(pre), _lib.ptr(bias), _lib.ptr(y), rows, f,
+              _lib.stream())
+    return y
+
+
+def bias_swiglu_bwd(dy, pre, bias=None, dbias=None, accumulate=False):
+    """dpre [rows, 2f] from dy [rows, f]; dbias (+)= dpre.sum(0)."""
+    rows, f = dy.shape
+    if not _lib.use_hip(dy):
+        x = pre.float() + (bias.float() if bias is not None else 0.0)
+        a, b = x[:, :f], x[:, f:]
+        sg = torch.sigmoid(a)
+        g = dy.float()
+        dpre = torch.cat([g * b * (sg + a * sg * (1 - sg)), g * a * sg], 1).to(dy.dtype)
+        if dbias is not None:
+            v = dpre.float().sum(0)
+            if accumulate:
+                v = v + dbias.float()
+            dbias.copy_(v.to(dbias.dtype))
+        return dpre
+    dpre = torch.empty_like(pre)
+    nparts = (rows + 15) // 16
+    scratch_n = _lib.query64("mx_colreduce_scratch", nparts, 2 * f)
+    partial = torch.empty(nparts * 2 * f + scratch_n, dtype=torch.float32, device=dy.device)
+    _lib.call("mx_bias_swiglu_bwd", _lib.ptr(dy), _lib.ptr(pre), _lib.ptr(bias), _lib.ptr(dpre),
+              _lib.ptr(dbias), int(accumulate), _lib.ptr(partial), rows, f, _lib.stream())
+    return dpre
+
+
 # ------------------------------------------------------------------ embedding
 def embed_fwd(ids, wte, wpe=None, seq=None, vocab_start=0, pos_offset=0):
     """ids [ntok] int64 -> wte[ids - vocab_start] (+ wpe[t % seq + pos_offset]).

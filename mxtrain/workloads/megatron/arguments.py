@@ -50,6 +50,8 @@ def build_parser() -> argparse.ArgumentParser:
     a("--normalization", default="LayerNorm", choices=["LayerNorm", "RMSNorm", "layernorm", "rmsnorm"])
     a("--position-embedding-type", default="learned_absolute", choices=["learned_absolute", "rope"])
     a("--use-rotary-position-embeddings", action="store_true")
+    a("--rotary-percent", type=float, default=1.0)
+    a("--rotary-base", "--rope-theta", dest="rotary_base", type=float, default=10000.0)
     a("--untie-embeddings-and-output-weights", action="store_true")
     a("--swiglu", action="store_true")
     # training
@@ -145,6 +147,9 @@ def parse_args(argv: Optional[List[str]] = None):
         args.position_embedding_type = "rope"
     if args.max_position_embeddings is None:
         args.max_position_embeddings = args.seq_length
+    if args.swiglu and args.ffn_hidden_size is None:
+        # Megatron-DeepSpeed: 2/3 of 4h (keeps the MLP FLOPs of the GeLU variant), 64-aligned
+        args.ffn_hidden_size = int((4 * args.hidden_size * 2 / 3) / 64) * 64
     ds = load_ds_config(args.deepspeed_config) if args.deepspeed else {}
     args.ds_config = ds
     # DeepSpeed JSON subset: batch geometry, ZeRO stage, precision, clipping, optimizer

@@ -74,6 +74,8 @@ def main(argv=None):
                     attention_dropout=0.0, layernorm_epsilon=args.layernorm_epsilon,
                     init_method_std=args.init_method_std, normalization=args.normalization,
                     position_embedding="rope" if args.position_embedding_type == "rope" else "learned",
+                    rotary_percent=args.rotary_percent, rotary_base=args.rotary_base,
+                    swiglu=args.swiglu,
                     tie_embeddings=not args.untie_embeddings_and_output_weights)
     tcfg = TrainConfig(micro_batch_size=args.micro_batch_size, global_batch_size=args.global_batch_size,
                        lr=args.lr, min_lr=args.min_lr, lr_warmup_iters=args.lr_warmup_iters,

@@ -10,6 +10,17 @@ def gelu_tanh(x):
     return 0.5 * x * (1.0 + torch.tanh(0.7978845608028654 * (x + 0.044715 * x ** 3)))
 
 
+def rope_complex(x, rd, base):
+    """Independent RoPE oracle: rotate-half as a complex multiply on (x[i], x[i+rd/2])."""
+    B_, H_, S_, D_ = x.shape
+    half = rd // 2
+    inv = 1.0 / (base ** (torch.arange(0, rd, 2, dtype=torch.float64) / rd))
+    ang = torch.arange(S_, dtype=torch.float64)[:, None] * inv[None, :]
+    rot = torch.polar(torch.ones_like(ang), ang).to(torch.complex64)
+    z = torch.complex(x[..., :half], x[..., half:rd]) * rot
+    return torch.cat([z.real, z.imag, x[..., rd:]], -1)
+
+
 def ref_loss(P, ids, labels, cfg, B, S, head="wte"):
     h = cfg.hidden_size
     nh = cfg.num_attention_heads
@@ -28,16 +39,29 @@ def ref_loss(P, ids, labels, cfg, B, S, head="wte"):
         p = f"layers.{i}."
         a = ln(x, p + "ln1")
         qkv = a @ P[p + "qkv_w"].t() + P[p + "qkv_b"]
-        q, k, v = qkv.split(h, dim=-1)
+        kvh = cfg.num_kv_heads
+        q, k, v = qkv.split([h, kvh * D, kvh * D], dim=-1)
         q = q.view(B, S, nh, D).transpose(1, 2)
-        k = k.view(B, S, nh, D).transpose(1, 2)
-        v = v.view(B, S, nh, D).transpose(1, 2)
+        k = k.view(B, S, kvh, D).transpose(1, 2)
+        v = v.view(B, S, kvh, D).transpose(1, 2)
+        if cfg.position_embedding == "rope":
+            rd = int(D * cfg.rotary_percent) // 8 * 8
+            q = rope_complex(q, rd, cfg.rotary_base)
+            k = rope_complex(k, rd, cfg.rotary_base)
+        if kvh != nh:
+            k = k.repeat_interleave(nh // kvh, 1)
+            v = v.repeat_interleave(nh // kvh, 1)
         s = (q @ k.transpose(-1, -2)) / math.sqrt(D)
         s = s.masked_fill(torch.ones(S, S, dtype=torch.bool).triu(1), float("-inf"))
         ctx = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * S, h)
         x = x + ctx @ P[p + "proj_w"].t() + P[p + "proj_b"]
         m = ln(x, p + "ln2")
-        f = gelu_tanh(m @ P[p + "fc1_w"].t() + P[p + "fc1_b"])
+        pre = m @ P[p + "fc1_w"].t() + P[p + "fc1_b"]
+        if getattr(cfg, "swiglu", False):
+            a_, b_ = pre.chunk(2, dim=-1)
+            f = F.silu(a_) * b_
+        else:
+            f = gelu_tanh(pre)
         x = x + f @ P[p + "fc2_w"].t() + P[p + "fc2_b"]
     xf = ln(x, "final_ln")
     logits = xf @ P[head].t()

@@ -17,6 +17,15 @@ CFG = dict(num_layers=2, hidden_size=64, num_attention_heads=4, seq_length=16,
            max_position_embeddings=16, vocab_size=256, hidden_dropout=0.0)
 
 
+# LLaMA-style variant: RoPE + GQA + RMSNorm + SwiGLU (column-parallel [a|b] fc1 split)
+CFG_LLAMA = dict(CFG, num_kv_heads=2, normalization="rmsnorm", position_embedding="rope",
+                 swiglu=True, ffn_hidden_size=96)
+
+
+def _cfg(mode):
+    return CFG_LLAMA if mode.endswith(":llama") else CFG
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -48,6 +57,8 @@ def _worker(rank, world, port, mode, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     torch.manual_seed(0)
+    ccfg = _cfg(mode)
+    mode = mode.split(":")[0]
     from mxtrain.models.gpt import GPTConfig, shard_gpt_state
     from mxtrain.parallel import state as pstate
     from mxtrain.training import GPTTrainer, TrainConfig
@@ -55,9 +66,9 @@ def _worker(rank, world, port, mode, q):
     pp = 2 if mode in ("pp", "3d", "3dsp") else 1
     ps = pstate.initialize_model_parallel(tp=tp, pp=pp, sequence_parallel=mode in ("sp", "3dsp"),
                                           backend="gloo", device_type="cpu")
-    cfg = GPTConfig(**CFG)
+    cfg = GPTConfig(**ccfg)
     # reference init (identical on every rank), then take this rank's shard
-    _, _, init_sd = _ref_init()
+    _, _, init_sd = _ref_init(ccfg)
     tcfg = TrainConfig(micro_batch_size=2, global_batch_size=4, lr=1e-3, overlap_grad_reduce=False)
     tr = GPTTrainer(cfg, tcfg, ps, dtype=torch.float32)
     if ps.dp > 1:
@@ -81,16 +92,17 @@ def _worker(rank, world, port, mode, q):
 _REF = {}
 
 
-def _ref_init():
-    if "init" not in _REF:
+def _ref_init(ccfg=CFG):
+    key = "init" if ccfg is CFG else "init_llama"
+    if key not in _REF:
         from mxtrain.models.gpt import GPTConfig
         from mxtrain.parallel.state import ParallelState
         from mxtrain.training import GPTTrainer, TrainConfig
-        cfg = GPTConfig(**CFG)
+        cfg = GPTConfig(**ccfg)
         tr = GPTTrainer(cfg, TrainConfig(micro_batch_size=2, global_batch_size=4),
                         ParallelState(), dtype=torch.float32)
-        _REF["init"] = (None, None, tr.flat.state_dict())
-    return _REF["init"]
+        _REF[key] = (None, None, tr.flat.state_dict())
+    return _REF[key]
 
 
 def _run(mode, world=2):
@@ -108,14 +120,13 @@ def _run(mode, world=2):
     return sorted(res, key=lambda t: t[0])
 
 
-@pytest.fixture(scope="module")
-def reference():
+def _make_reference(ccfg):
     # the reference trainer must start from the same init the workers shard
     from mxtrain.models.gpt import GPTConfig
     from mxtrain.parallel.state import ParallelState
     from mxtrain.training import GPTTrainer, TrainConfig
-    cfg = GPTConfig(**CFG)
-    _, _, init_sd = _ref_init()
+    cfg = GPTConfig(**ccfg)
+    _, _, init_sd = _ref_init(ccfg)
     tr = GPTTrainer(cfg, TrainConfig(micro_batch_size=2, global_batch_size=4, lr=1e-3,
                                      overlap_grad_reduce=False), ParallelState(),
                     dtype=torch.float32)
@@ -126,6 +137,11 @@ def reference():
     return cfg, losses, tr.flat.state_dict()
 
 
+@pytest.fixture(scope="module")
+def reference():
+    return _make_reference(CFG)
+
+
 def _check(mode, reference, loss_ranks):
     from mxtrain.models.gpt import shard_gpt_state
     cfg, ref_losses, ref_sd = reference
@@ -134,8 +150,9 @@ def _check(mode, reference, loss_ranks):
         if rank in loss_ranks:
             for a, b in zip(losses, ref_losses):
                 assert abs(a - b) < 2e-5 * max(1.0, abs(b)), (mode, rank, losses, ref_losses)
-        exp = shard_gpt_state(ref_sd, cfg, 2 if mode in ("tp", "sp") else 1, tpr,
-                              2 if mode == "pp" else 1, ppr)
+        m = mode.split(":")[0]
+        exp = shard_gpt_state(ref_sd, cfg, 2 if m in ("tp", "sp") else 1, tpr,
+                              2 if m == "pp" else 1, ppr)
         for n, t in exp.items():
             assert torch.allclose(params[n], t, atol=3e-5, rtol=1e-4), (mode, rank, n,
                                                                         (params[n] - t).abs().max())
@@ -159,6 +176,11 @@ def test_tp2_matches_single(reference):
 
 def test_tp2_sequence_parallel_matches_single(reference):
     _check("sp", reference, loss_ranks=(0, 1))
+
+
+def test_tp2_sp_llama_style_matches_single():
+    """RoPE + GQA + RMSNorm + SwiGLU under TP2 + sequence parallel."""
+    _check("sp:llama", _make_reference(CFG_LLAMA), loss_ranks=(0, 1))
 
 
 def test_pp2_1f1b_matches_single(reference):

@@ -58,6 +58,47 @@ def test_gpt_rmsnorm_variant():
         assert torch.allclose(flat.grads[n], p.grad, atol=2e-5, rtol=1e-4), n
 
 
+def test_gpt_rope_gqa_variant():
+    """RoPE (K5, partial rotary) + GQA + RMSNorm + SwiGLU (LLaMA-style)."""
+    cfg = GPTConfig(num_layers=2, hidden_size=64, num_attention_heads=4, num_kv_heads=2,
+                    seq_length=8, max_position_embeddings=8, vocab_size=50, hidden_dropout=0.0,
+                    normalization="rmsnorm", position_embedding="rope", rotary_percent=0.5,
+                    swiglu=True, ffn_hidden_size=96)
+    B, S = 2, 8
+    flat, ids, labels = _setup(cfg, B, S, seed=5)
+    assert "wpe" not in flat.params
+    stage = GPTStage(cfg, flat.params, flat.grads)
+    stage.rt.grad_scale = 1.0 / (B * S)
+    loss = stage.forward(ids=ids, labels=labels, B=B, S=S)
+    loss.backward()
+    P = {n: p.detach().clone().requires_grad_(True) for n, p in flat.params.items()}
+    ref = ref_loss(P, ids, labels, cfg, B, S)
+    ref.backward()
+    assert torch.allclose(loss, ref, atol=1e-5), (float(loss), float(ref))
+    for n, p in P.items():
+        assert torch.allclose(flat.grads[n], p.grad, atol=2e-5, rtol=1e-4), n
+
+
+def test_rope_op_inverse_and_grad():
+    from mxtrain.ops.rope import apply_rope_, rope
+    T, H, D = 12, 3, 16
+    x = torch.randn(T, H * D)
+    y = x.clone()
+    apply_rope_(y, 0, H, D, seq=6, rotary_dim=8)
+    assert not torch.allclose(y, x)
+    assert torch.allclose(y[:, 8:16], x[:, 8:16])     # un-rotated tail of head 0
+    apply_rope_(y, 0, H, D, seq=6, rotary_dim=8, inverse=True)
+    assert torch.allclose(y, x, atol=1e-6)
+    xr = x.clone().requires_grad_(True)
+    g = torch.randn(T, H * D)
+    rope(xr, H, D, 6, 8).backward(g)
+    xa = x.clone().requires_grad_(True)
+    from gpt_reference import rope_complex
+    ya = rope_complex(xa.view(2, 6, H, D).transpose(1, 2), 8, 10000.0).transpose(1, 2).reshape(T, H * D)
+    ya.backward(g)
+    assert torch.allclose(xr.grad, xa.grad, atol=1e-5)
+
+
 def test_dropout_mask_reproducible():
     from mxtrain.ops.rng import keep_mask
     m1 = keep_mask(10000, 123, 0.1)

@@ -228,3 +228,75 @@ def test_gpt_layer_gpu_matches_cpu_reference():
         a, b = fg.grads[n].float().cpu(), fc.grads[n]
         rel = (a - b).norm() / (b.norm() + 1e-6)
         assert rel < 5e-2, (n, float(rel))
+
+
+@pytest.mark.parametrize("H,KV,D,rd", [(16, 16, 64, 64), (8, 2, 128, 64), (4, 4, 128, 128)])
+def test_rope_fwd_bwd(H, KV, D, rd):
+    from mxtrain.ops.rope import apply_rope_
+    B, S = 2, 256
+    ld = (H + 2 * KV) * D
+    x = _bf(torch.randn(B * S, ld))
+    xd = x.to(DEV)
+    for col0, nh in ((0, H), (H * D, KV)):
+        apply_rope_(xd, col0, nh, D, S, rd, max_pos=S)
+        apply_rope_(x, col0, nh, D, S, rd, max_pos=S)
+    _close(xd, x, 2e-2, 1e-2, "rope fwd")
+    y = xd.clone()
+    for col0, nh in ((0, H), (H * D, KV)):
+        apply_rope_(y, col0, nh, D, S, rd, max_pos=S, inverse=True)
+        apply_rope_(x, col0, nh, D, S, rd, max_pos=S, inverse=True)
+    _close(y, x, 2e-2, 1e-2, "rope inverse")
+    # position ids override (e.g. packed / context-parallel shards)
+    pid = torch.randint(0, 4096, (B * S,))
+    z = _bf(torch.randn(B * S, H * D))
+    zd = z.to(DEV)
+    apply_rope_(zd, 0, H, D, S, rd, pos_ids=pid.to(DEV), max_pos=4096)
+    apply_rope_(z, 0, H, D, S, rd, pos_ids=pid, max_pos=4096)
+    _close(zd, z, 2e-2, 1e-2, "rope pos_ids")
+
+
+def test_gpt_llama_style_layer_gpu_matches_cpu_reference():
+    """RoPE + GQA + RMSNorm stage on the GPU (HIP kernels) vs the fp32 CPU path."""
+    from mxtrain.models.gpt import GPTConfig, GPTStage, gpt_param_specs
+    from mxtrain.parallel.buffers import FlatParams
+    cfg = GPTConfig(num_layers=2, hidden_size=512, num_attention_heads=4, num_kv_heads=2,
+                    seq_length=128, max_position_embeddings=128, vocab_size=512,
+                    hidden_dropout=0.0, normalization="rmsnorm", position_embedding="rope",
+                    swiglu=True, ffn_hidden_size=1024)
+    B, S = 2, 128
+    specs = gpt_param_specs(cfg)
+    fc = FlatParams(specs, "cpu", torch.float32)
+    fc.initialize(torch.Generator().manual_seed(0), cfg.num_layers)
+    fc.data.copy_(fc.data.to(torch.bfloat16).float())
+    fg = FlatParams(specs, DEV, torch.bfloat16)
+    fg.data.copy_(fc.data.to(torch.bfloat16))
+    ids = torch.randint(0, cfg.vocab_size, (B * S,))
+    labels = torch.randint(0, cfg.vocab_size, (B * S,))
+    sc = GPTStage(cfg, fc.params, fc.grads)
+    sg = GPTStage(cfg, fg.params, fg.grads)
+    for st in (sc, sg):
+        st.rt.grad_scale = 1.0 / (B * S)
+    lc = sc.forward(ids=ids, labels=labels, B=B, S=S)
+    lc.backward()
+    lg = sg.forward(ids=ids.to(DEV), labels=labels.to(DEV), B=B, S=S)
+    lg.backward()
+    assert abs(float(lg.detach()) - float(lc.detach())) < 2e-2
+    for n in fc.grads:
+        a, b = fg.grads[n].float().cpu(), fc.grads[n]
+        rel = (a - b).norm() / (b.norm() + 1e-6)
+        assert rel < 5e-2, (n, float(rel))
+
+
+@pytest.mark.parametrize("rows,f", [(512, 1024), (300, 2752)])
+def test_bias_swiglu_fwd_bwd(rows, f):
+    pre = _bf(torch.randn(rows, 2 * f))
+    b = _bf(0.1 * torch.randn(2 * f))
+    dy = _bf(torch.randn(rows, f))
+    y = Fu.bias_swiglu_fwd(pre.to(DEV), b.to(DEV))
+    _close(y, Fu.bias_swiglu_fwd(pre, b), 2e-2, 2e-2, "swiglu y")
+    db = torch.zeros(2 * f, dtype=torch.bfloat16, device=DEV)
+    dbr = torch.zeros(2 * f, dtype=torch.bfloat16)
+    dp = Fu.bias_swiglu_bwd(dy.to(DEV), pre.to(DEV), b.to(DEV), dbias=db)
+    dpr = Fu.bias_swiglu_bwd(dy, pre, b, dbias=dbr)
+    _close(dp, dpr, 3e-2, 2e-2, "swiglu dpre")
+    _close(db, dbr, 0.25, 2e-2, "swiglu dbias")
