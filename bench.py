@@ -22,6 +22,22 @@ import sys
 import time
 
 
+def _coll_summary(tr):
+    comms = getattr(tr, "xgmi_comms", {}) or {}
+    if not comms:
+        return "rccl"
+    out = {}
+    for name, c in comms.items():
+        if c is None:
+            out[name] = "rccl (xgmi setup failed)"
+        elif c.prefer is None:
+            out[name] = "xgmi"
+        else:
+            out[name] = {op: [[nb, "xgmi" if win else "rccl"] for nb, win in v] for op, v in c.prefer.items()} \
+                or "rccl (xgmi check failed)"
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -40,7 +56,19 @@ def main():
                     help="capture the step in a hipGraph also when N > 1 (default: single GPU only; "
                          "eager and graph steps measure the same on MI355X, the step is GPU-bound)")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--no-tuned-gemm", action="store_true",
+                    help="do not load the checked-in TunableOp GEMM solution tables")
+    ap.add_argument("--tune-gemm", action="store_true",
+                    help="TunableOp: benchmark every GEMM solution during warmup and write the table "
+                         "to $PYTORCH_TUNABLEOP_FILENAME (see scripts/tune_gemms.sh)")
+    ap.add_argument("--wgrad-stream", action="store_true",
+                    help="run weight-gradient GEMMs on a concurrent side stream")
+    ap.add_argument("--xgmi", choices=["0", "1", "auto"], default="auto",
+                    help="direct xGMI peer-to-peer collectives (csrc/comm/xgmi.hip) for the DP "
+                         "reduce-scatter / all-gather and TP all-reduce: 0 = RCCL only, 1 = always, "
+                         "auto = verify against RCCL and keep the faster per message size (N > 1)")
     args = ap.parse_args()
+    os.environ.setdefault("MXTRAIN_XGMI", args.xgmi)
 
     import torch
     import torch.distributed as dist
@@ -59,9 +87,13 @@ def main():
         torch.backends.cuda.preferred_blas_library("hipblaslt")
     except Exception:
         pass
+    from mxtrain.runtime.gemm_tuning import use_tuned_gemms
+    n_tables = 0 if args.no_tuned_gemm else use_tuned_gemms(tune=args.tune_gemm,
+                                                               tables=[] if args.tune_gemm else None)
     cfg = GPTConfig(**GPT_CONFIGS[args.model])
     tcfg = TrainConfig(micro_batch_size=args.micro_batch_size, global_batch_size=args.global_batch_size,
-                       overlap_grad_reduce=not args.no_overlap, lr_warmup_iters=0)
+                       overlap_grad_reduce=not args.no_overlap, lr_warmup_iters=0,
+                       wgrad_stream=args.wgrad_stream)
     tr = GPTTrainer(cfg, tcfg, ps)
     gen = torch.Generator().manual_seed(1 + ps.dp_rank)
     tokens, labels = synthetic_batch(cfg, tr.num_micro, args.micro_batch_size, ps.device, gen)
@@ -138,6 +170,9 @@ def main():
                 "hidden_dropout": cfg.hidden_dropout,
                 "attention_dropout": cfg.attention_dropout,
                 "hipgraph": use_graph,
+                "wgrad_stream": args.wgrad_stream,
+                "tuned_gemm_tables": n_tables,
+                "collectives": _coll_summary(tr),
             },
             "tflops_per_gpu": round(flops / world / 1e12, 1),
             "mfu_bf16_dense_2.5pf": round(flops / world / 2.5e15, 4),

@@ -1,0 +1,256 @@
+// Direct peer-to-peer collectives over xGMI for one MI355X node.
+//
+// RCCL's ring moves every byte over ONE outbound xGMI link per GPU (~153 GB/s), so a
+// ring all-reduce is per-link bound.  Here every rank maps every peer's registered
+// buffer (hipIpcGetMemHandle / hipIpcOpenMemHandle, handles exchanged through the c10d
+// store) and a kernel reads all 7 peers at once, so all 7 links carry traffic:
+//
+//   one-shot all-reduce (small messages):  copy-in -> barrier -> every rank reads the
+//       whole message from every peer and reduces it locally -> barrier
+//   two-shot all-reduce (large):  copy-in -> barrier -> rank r reduces shard r from all
+//       peers into its own buffer -> barrier -> every rank gathers all shards -> barrier
+//   reduce-scatter (ZeRO-1 gradient shard) and all-gather (parameter shard): halves
+//       of the two-shot algorithm
+//
+// Synchronisation is per workgroup, never grid-wide: workgroup b of every rank
+// copies exactly the pieces that workgroup b of the other ranks read next (the
+// piece partition is the same on every rank), so a barrier between the b-th
+// workgroups of all ranks is enough.  Barrier = release fence (system scope; writes
+// the L2 back so peers reading over xGMI see the data) -> one lane per peer stores
+// the epoch into that peer's flag slot [b][my rank] (uncached memory) -> one lane per
+// peer polls our own slot [b][peer] -> acquire fence.  Epochs are per-workgroup
+// counters kept in device memory and advanced by the kernel itself, so the same
+// launch can be replayed from a hipGraph.  Every poll is bounded (s_memrealtime,
+// 100 MHz): on timeout the kernel records an error word and exits, so a rank that
+// never arrives cannot hang the GPU; the host checks the word (mx_xgmi_error).
+#include <cstring>
+
+#include "../common.h"
+
+using namespace mx;
+
+namespace {
+
+constexpr int kMaxRanks = 8;
+constexpr int kMaxBlocks = 128;
+constexpr int kThreads = 512;
+
+struct Flags {                                  // one per rank, uncached device memory
+  uint32_t slot[3][kMaxBlocks][kMaxRanks];      // [phase][workgroup][source rank]
+  uint32_t counter[kMaxBlocks];                 // last completed epoch per workgroup
+  uint32_t error;                               // nonzero after a barrier timeout
+};
+
+struct Peers {
+  char* data[kMaxRanks];
+  Flags* flags[kMaxRanks];
+};
+
+__device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+
+// cross-rank barrier between the b-th workgroups; false on timeout
+__device__ bool xbarrier(const Peers& pp, int phase, int rank, int world, uint32_t epoch,
+                         uint64_t timeout_ticks) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: drain + L2 write-back
+  __syncthreads();
+  const int b = blockIdx.x, t = threadIdx.x;
+  __shared__ int ok_s;
+  if (t == 0) ok_s = 1;
+  __syncthreads();
+  if (t < world) {
+    __hip_atomic_store(&pp.flags[t]->slot[phase][b][rank], epoch, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* mine = &pp.flags[rank]->slot[phase][b][t];
+    const uint64_t t0 = now_ticks();
+    while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+      if (now_ticks() - t0 > timeout_ticks) {
+        __hip_atomic_store(&pp.flags[rank]->error, 1u + (uint32_t)phase, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        ok_s = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // drop stale lines before peer reads
+  return ok_s != 0;
+}
+
+// 16-byte vector accumulate helpers (bf16 x 8 or fp32 x 4)
+template <bool kBF16>
+struct Vec;
+template <>
+struct Vec<true> {
+  float f[8];
+  __device__ void zero() {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = 0.f;
+  }
+  __device__ void add(const uint4& v) {
+    float g[8];
+    unpack8(v, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] += g[j];
+  }
+  __device__ uint4 pack() const { return pack8(f); }
+};
+template <>
+struct Vec<false> {
+  float f[4];
+  __device__ void zero() { f[0] = f[1] = f[2] = f[3] = 0.f; }
+  __device__ void add(const uint4& v) {
+    f[0] += __uint_as_float(v.x); f[1] += __uint_as_float(v.y);
+    f[2] += __uint_as_float(v.z); f[3] += __uint_as_float(v.w);
+  }
+  __device__ uint4 pack() const {
+    return make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]),
+                      __float_as_uint(f[3]));
+  }
+};
+
+template <bool kBF16>
+__device__ __forceinline__ uint4 reduce_at(const Peers& pp, int64_t v, int rank, int world) {
+  Vec<kBF16> acc;
+  acc.zero();
+  uint4 x[kMaxRanks];
+#pragma unroll
+  for (int i = 0; i < kMaxRanks; ++i)   // issue all peer loads before using any (7 links)
+    if (i < world) x[i] = reinterpret_cast<const uint4*>(pp.data[(rank + i) % world])[v];
+#pragma unroll
+  for (int i = 0; i < kMaxRanks; ++i)
+    if (i < world) acc.add(x[i]);
+  return acc.pack();
+}
+
+// piece partition of [lo, hi): workgroup b, thread t take lo + b*T + t, stride G*T
+#define FOR_PIECE(v, lo, hi) \
+  for (int64_t v = (lo) + (int64_t)blockIdx.x * kThreads + threadIdx.x; v < (hi); \
+       v += (int64_t)gridDim.x * kThreads)
+
+enum Op { kAllReduce1 = 0, kAllReduce2 = 1, kReduceScatter = 2, kAllGather = 3 };
+
+// nvec = 16-B vectors of the FULL message (all-gather: of the gathered output);
+// shard = ceil(nvec / world) vectors (shards 0..world-2 full, last may be short)
+template <bool kBF16>
+__global__ __launch_bounds__(kThreads) void xgmi_kernel(Peers pp, const uint4* in,
+                                                         uint4* out, int64_t nvec,
+                                                         int rank, int world, int op,
+                                                         uint64_t timeout_ticks) {
+  Flags* self = pp.flags[rank];
+  const int b = blockIdx.x;
+  const uint32_t epoch = self->counter[b] + 1;
+  uint4* mine = reinterpret_cast<uint4*>(pp.data[rank]);
+  const int64_t shard = (nvec + world - 1) / world;
+  auto lo = [&](int q) { return min((int64_t)q * shard, nvec); };
+  auto hi = [&](int q) { return min((int64_t)(q + 1) * shard, nvec); };
+  bool ok = true;
+
+  if (op == kAllReduce1) {
+    FOR_PIECE(v, 0, nvec) mine[v] = in[v];
+    ok = xbarrier(pp, 0, rank, world, epoch, timeout_ticks);
+    if (ok) FOR_PIECE(v, 0, nvec) out[v] = reduce_at<kBF16>(pp, v, rank, world);
+  } else if (op == kAllGather) {
+    // in = my shard (hi(rank) - lo(rank) vectors); out = full [nvec]
+    FOR_PIECE(v, lo(rank), hi(rank)) mine[v] = in[v - lo(rank)];
+    ok = xbarrier(pp, 0, rank, world, epoch, timeout_ticks);
+    if (ok)
+      for (int i = 0; i < world; ++i) {
+        const int q = (rank + i) % world;
+        const uint4* src = reinterpret_cast<const uint4*>(pp.data[q]);
+        FOR_PIECE(v, lo(q), hi(q)) out[v] = src[v];
+      }
+  } else {
+    // reduce-scatter / two-shot: copy pieces of every shard, reduce my shard
+    for (int q = 0; q < world; ++q) FOR_PIECE(v, lo(q), hi(q)) mine[v] = in[v];
+    ok = xbarrier(pp, 0, rank, world, epoch, timeout_ticks);
+    if (ok) {
+      if (op == kReduceScatter) {
+        FOR_PIECE(v, lo(rank), hi(rank)) out[v - lo(rank)] = reduce_at<kBF16>(pp, v, rank, world);
+      } else {
+        FOR_PIECE(v, lo(rank), hi(rank)) mine[v] = reduce_at<kBF16>(pp, v, rank, world);
+        ok = xbarrier(pp, 1, rank, world, epoch, timeout_ticks);
+        if (ok)
+          for (int i = 0; i < world; ++i) {
+            const int q = (rank + i) % world;
+            const uint4* src = reinterpret_cast<const uint4*>(pp.data[q]);
+            FOR_PIECE(v, lo(q), hi(q)) out[v] = src[v];
+          }
+      }
+    }
+  }
+  // nobody may overwrite its buffer (next call) while a peer still reads it
+  if (ok) ok = xbarrier(pp, 2, rank, world, epoch, timeout_ticks);
+  if (threadIdx.x == 0) self->counter[b] = epoch;
+}
+
+}  // namespace
+
+MX_EXPORT int mx_xgmi_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+MX_EXPORT int mx_xgmi_flags_bytes() { return (int)((sizeof(Flags) + 255) / 256 * 256); }
+MX_EXPORT int mx_xgmi_max_ranks() { return kMaxRanks; }
+
+// data: plain device memory (cached in the owner's L2; the barrier writes it back);
+// flags: uncached device memory (polled across GPUs).  Both zeroed.
+MX_EXPORT int mx_xgmi_alloc(int64_t data_bytes, void** data, void** flags) {
+  hipError_t e = hipMalloc(data, (size_t)data_bytes);
+  if (e != hipSuccess) return e;
+  e = hipExtMallocWithFlags(flags, (size_t)mx_xgmi_flags_bytes(), hipDeviceMallocUncached);
+  if (e != hipSuccess) return e;
+  e = hipMemset(*flags, 0, (size_t)mx_xgmi_flags_bytes());
+  if (e != hipSuccess) return e;
+  e = hipMemset(*data, 0, (size_t)data_bytes);
+  if (e != hipSuccess) return e;
+  return hipDeviceSynchronize();
+}
+
+MX_EXPORT int mx_xgmi_free(void* data, void* flags) {
+  hipError_t e = hipFree(data);
+  hipError_t f = hipFree(flags);
+  return e != hipSuccess ? e : f;
+}
+
+MX_EXPORT int mx_xgmi_get_handle(void* ptr, void* out) {
+  return hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(out), ptr);
+}
+
+MX_EXPORT int mx_xgmi_open_handle(const void* handle, void** ptr) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  return hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+MX_EXPORT int mx_xgmi_close_handle(void* ptr) { return hipIpcCloseMemHandle(ptr); }
+
+// error word of this rank's flags (synchronous read; 0 = healthy)
+MX_EXPORT int mx_xgmi_error(void* flags, uint32_t* out) {
+  return hipMemcpy(out, &reinterpret_cast<Flags*>(flags)->error, 4, hipMemcpyDeviceToHost);
+}
+
+// datas / flagss: world device pointers (this rank's own + mapped peers), in rank order.
+// nbytes: bytes of the full message (% 16 == 0).  bf16: reduce in bf16 (else fp32).
+MX_EXPORT int mx_xgmi_collective(void* const* datas, void* const* flagss, int world, int rank,
+                                 const void* in, void* out, int64_t nbytes, int bf16, int op,
+                                 int blocks, double timeout_s, hipStream_t stream) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || nbytes % 16)
+    return hipErrorInvalidValue;
+  Peers pp = {};
+  for (int i = 0; i < world; ++i) {
+    pp.data[i] = reinterpret_cast<char*>(datas[i]);
+    pp.flags[i] = reinterpret_cast<Flags*>(flagss[i]);
+  }
+  const int64_t nvec = nbytes / 16;
+  if (blocks <= 0) {
+    const int64_t want = (nvec + kThreads - 1) / kThreads;
+    blocks = (int)(want < 64 ? (want < 1 ? 1 : want) : 64);
+  }
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  const uint64_t ticks = (uint64_t)(timeout_s * 1e8);   // s_memrealtime: 100 MHz
+  if (bf16)
+    hipLaunchKernelGGL(xgmi_kernel<true>, dim3(blocks), dim3(kThreads), 0, stream, pp,
+                       (const uint4*)in, (uint4*)out, nvec, rank, world, op, ticks);
+  else
+    hipLaunchKernelGGL(xgmi_kernel<false>, dim3(blocks), dim3(kThreads), 0, stream, pp,
+                       (const uint4*)in, (uint4*)out, nvec, rank, world, op, ticks);
+  return hipGetLastError();
+}

@@ -247,6 +247,10 @@ class StepRuntime:
     unit_done: Optional[Callable[[int], None]] = None
     before_unit: Optional[Callable[[int], None]] = None   # wait for the unit's params (AG overlap)
     grad_scale: float = 1.0       # loss gradient scale (1 / tokens / microbatches)
+    # weight-gradient GEMMs run on this side stream, concurrently with the dgrad GEMM and
+    # the memory-bound backward kernels of the main stream (None: inline)
+    wgrad_stream: Optional[object] = None
+    _wgrad_live: bool = False
 
     @property
     def p_drop(self):
@@ -275,7 +279,29 @@ class StepRuntime:
     def norm_grads(self, prefix):
         return self.grads[prefix + "_w"], self.grads.get(prefix + "_b")
 
+    def wgrad(self, gbuf, dy, x):
+        """gbuf += dy^T x.  On the side stream when enabled: it forks from the main
+        stream here and is joined in done() (before the unit's gradient bucket can be
+        reduced); every operand stays referenced by the caller's frame until then, so the
+        caching allocator cannot hand its memory to main-stream work that is unordered
+        with the side-stream GEMM."""
+        ws = self.wgrad_stream
+        if ws is None:
+            _wgrad(gbuf, dy, x)
+            return
+        main = torch.cuda.current_stream(gbuf.device)
+        ws.wait_stream(main)
+        with torch.cuda.stream(ws):
+            _wgrad(gbuf, dy, x)
+        self._wgrad_live = True
+
+    def join_wgrad(self):
+        if self._wgrad_live:
+            torch.cuda.current_stream().wait_stream(self.wgrad_stream)
+            self._wgrad_live = False
+
     def done(self, unit):
+        self.join_wgrad()
         if self.unit_done is not None:
             self.unit_done(unit)
 
@@ -437,14 +463,14 @@ class GPTLayerFn(torch.autograd.Function):
                                dbias=G[p + "fc2_b"], accumulate=True)
         # ---- MLP backward
         dg_full = _gather(dg, rt)
-        _wgrad(G[p + "fc2_w"], dg_full, f)
+        rt.wgrad(G[p + "fc2_w"], dg_full, f)
         df = torch.mm(dg_full, P[p + "fc2_w"])
         if cfg.swiglu:
             dpre = bias_swiglu_bwd(df, pre, P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True)
         else:
             dpre = bias_gelu_bwd(df, pre, P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True,
                                  inplace=True)
-        _wgrad(G[p + "fc1_w"], dpre, m_full)
+        rt.wgrad(G[p + "fc1_w"], dpre, m_full)
         dm = _reduce(torch.mm(dpre, P[p + "fc1_w"]), rt)
         # ---- BDA-LN2 backward
         w2, _ = rt.norm_params(p + "ln2")
@@ -454,7 +480,7 @@ class GPTLayerFn(torch.autograd.Function):
                            dbeta=gb2, dbias=G[p + "proj_b"], accumulate=True)
         # ---- attention backward
         do_full = _gather(do_, rt)
-        _wgrad(G[p + "proj_w"], do_full, ctx_)
+        rt.wgrad(G[p + "proj_w"], do_full, ctx_)
         dctx = torch.mm(do_full, P[p + "proj_w"])
         dqkv = torch.empty_like(qkv)
         q = qkv[:, : hl * D]
@@ -465,7 +491,7 @@ class GPTLayerFn(torch.autograd.Function):
                           dv=dqkv[:, (hl + kvl) * D:])
         rt.rope_(dqkv, hl, kvl, inverse=True)
         colsum(dqkv, G[p + "qkv_b"], accumulate=True)
-        _wgrad(G[p + "qkv_w"], dqkv, a_full)
+        rt.wgrad(G[p + "qkv_w"], dqkv, a_full)
         da = _reduce(torch.mm(dqkv, P[p + "qkv_w"]), rt)
         rt.done(i + 1)
         return dh, da, None, None, None

@@ -9,6 +9,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from . import xgmi as _xgmi
+
 
 def world(group) -> int:
     return dist.get_world_size(group) if group is not None else 1
@@ -17,6 +19,10 @@ def world(group) -> int:
 def all_reduce_(t: torch.Tensor, group, op=None):
     if group is None or world(group) == 1:
         return t
+    if (op is None or op == dist.ReduceOp.SUM) and t.is_contiguous():
+        c = _xgmi.route(group, t, "all_reduce", t.numel() * t.element_size())
+        if c is not None:
+            return c.all_reduce_(t)
     dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=group)
     return t
 
@@ -26,6 +32,9 @@ def all_gather_dim0(t: torch.Tensor, group) -> torch.Tensor:
     if n == 1:
         return t
     out = torch.empty((t.shape[0] * n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    c = _xgmi.route(group, t, "all_gather", out.numel() * out.element_size())
+    if c is not None:
+        return c.all_gather(out, t.contiguous())
     dist.all_gather_into_tensor(out, t.contiguous(), group=group)
     return out
 
@@ -36,6 +45,9 @@ def reduce_scatter_dim0(t: torch.Tensor, group) -> torch.Tensor:
         return t
     assert t.shape[0] % n == 0
     out = torch.empty((t.shape[0] // n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    c = _xgmi.route(group, t, "reduce_scatter", t.numel() * t.element_size())
+    if c is not None:
+        return c.reduce_scatter(out, t.contiguous())
     dist.reduce_scatter_tensor(out, t.contiguous(), group=group)
     return out
 

@@ -1,0 +1,346 @@
+"""Direct xGMI peer-to-peer collectives (``csrc/comm/xgmi.hip``).
+
+Every rank of a single-node group allocates one registered buffer (+ an uncached flag
+block), exports IPC handles, and maps every peer's buffer; the handles travel through
+``dist.all_gather_object`` on the group (the c10d store / gloo also work).  A collective
+is then ONE kernel that reads from all peers at once -- all 7 xGMI links of an MI355X
+carry traffic, where RCCL's ring uses one outbound link per GPU.
+
+    comm = XGMICommunicator(group, device, max_bytes=256 << 20)
+    comm.all_reduce_(t)                  # one-shot below ``oneshot_max``, else two-shot
+    comm.reduce_scatter(out, inp)        # ZeRO-1 gradient shard
+    comm.all_gather(out, inp)            # ZeRO-1 parameter shard
+
+Selection vs RCCL is explicit: ``MXTRAIN_XGMI=1`` (or ``enable_xgmi()``) routes the
+DP reduce-scatter / all-gather and the TP all-reduce through it; ``autotune()`` times
+both on the live group and keeps the faster per message-size class.  Barrier waits in
+the kernel are bounded; ``check()`` raises if any timed out (a peer never arrived).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _lib
+
+OP_ALLREDUCE_1SHOT, OP_ALLREDUCE_2SHOT, OP_REDUCE_SCATTER, OP_ALL_GATHER = 0, 1, 2, 3
+
+_SIGS = {
+    "mx_xgmi_handle_size": [],
+    "mx_xgmi_flags_bytes": [],
+    "mx_xgmi_max_ranks": [],
+    "mx_xgmi_alloc": [ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p)],
+    "mx_xgmi_free": [ctypes.c_void_p, ctypes.c_void_p],
+    "mx_xgmi_get_handle": [ctypes.c_void_p, ctypes.c_void_p],
+    "mx_xgmi_open_handle": [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)],
+    "mx_xgmi_close_handle": [ctypes.c_void_p],
+    "mx_xgmi_error": [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)],
+    "mx_xgmi_collective": [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                           ctypes.c_double, ctypes.c_void_p],
+}
+
+
+def _fn(name):
+    lib = _lib.lib()
+    f = getattr(lib, name)
+    f.argtypes = _SIGS[name]
+    f.restype = ctypes.c_int
+    return f
+
+
+def _check(err, what):
+    if err != 0:
+        raise RuntimeError(f"{what} failed with hipError {err}")
+
+
+class XGMIUnavailable(RuntimeError):
+    """Raised on EVERY rank of the group when any rank could not set the communicator up."""
+
+
+class XGMICommunicator:
+    def __init__(self, group, device, max_bytes: int = 256 << 20, oneshot_max: int = 512 << 10,
+                 timeout_s: float = 30.0, blocks: int = 0):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = torch.device(device)
+        assert self.world <= _fn("mx_xgmi_max_ranks")(), "xGMI collectives are single-node (<= 8 ranks)"
+        self.max_bytes = (max_bytes + 15) // 16 * 16
+        self.oneshot_max = oneshot_max
+        self.timeout_s = timeout_s
+        self.blocks = blocks
+        self._data = ctypes.c_void_p()
+        self._flags = ctypes.c_void_p()
+        self._opened: List[ctypes.c_void_p] = []
+        err = None
+        mine = None
+        with torch.cuda.device(self.device):
+            try:
+                _check(_fn("mx_xgmi_alloc")(self.max_bytes, ctypes.byref(self._data),
+                                            ctypes.byref(self._flags)), "mx_xgmi_alloc")
+                hs = _fn("mx_xgmi_handle_size")()
+                hd, hf = ctypes.create_string_buffer(hs), ctypes.create_string_buffer(hs)
+                _check(_fn("mx_xgmi_get_handle")(self._data, hd), "hipIpcGetMemHandle(data)")
+                _check(_fn("mx_xgmi_get_handle")(self._flags, hf), "hipIpcGetMemHandle(flags)")
+                mine = (bytes(hd.raw), bytes(hf.raw))
+            except Exception as e:  # keep going: every rank must reach the collectives below
+                err = repr(e)
+            allh: List = [None] * self.world
+            dist.all_gather_object(allh, mine, group=group)
+            datas, flags = [], []
+            if err is None and all(h is not None for h in allh):
+                try:
+                    for r, (d, f) in enumerate(allh):
+                        if r == self.rank:
+                            datas.append(self._data.value)
+                            flags.append(self._flags.value)
+                            continue
+                        pd, pf = ctypes.c_void_p(), ctypes.c_void_p()
+                        _check(_fn("mx_xgmi_open_handle")(d, ctypes.byref(pd)),
+                               f"hipIpcOpenMemHandle(rank {r})")
+                        self._opened.append(pd)
+                        _check(_fn("mx_xgmi_open_handle")(f, ctypes.byref(pf)),
+                               f"hipIpcOpenMemHandle(rank {r} flags)")
+                        self._opened.append(pf)
+                        datas.append(pd.value)
+                        flags.append(pf.value)
+                except Exception as e:
+                    err = repr(e)
+            elif err is None:
+                err = "a peer failed to allocate / export its buffer"
+        # every rank learns whether every rank mapped every peer before any kernel runs
+        errs: List = [None] * self.world
+        dist.all_gather_object(errs, err, group=group)
+        bad = [(r, e) for r, e in enumerate(errs) if e is not None]
+        if bad:
+            self.close()
+            raise XGMIUnavailable(f"xGMI communicator setup failed: {bad}")
+        self._datas = (ctypes.c_void_p * self.world)(*datas)
+        self._flagss = (ctypes.c_void_p * self.world)(*flags)
+
+    # ------------------------------------------------------------------ core
+    def _launch(self, inp: torch.Tensor, out: torch.Tensor, nbytes: int, op: int):
+        assert inp.is_contiguous() and out.is_contiguous()
+        assert inp.dtype in (torch.bfloat16, torch.float32) and out.dtype == inp.dtype
+        if nbytes > self.max_bytes or nbytes % 16:
+            raise ValueError(f"xGMI message of {nbytes} B (max {self.max_bytes}, multiple of 16)")
+        _check(_fn("mx_xgmi_collective")(self._datas, self._flagss, self.world, self.rank,
+                                         inp.data_ptr(), out.data_ptr(), nbytes,
+                                         int(inp.dtype == torch.bfloat16), op, self.blocks,
+                                         self.timeout_s, _lib.stream()), "mx_xgmi_collective")
+
+    def supports(self, t: torch.Tensor, shard_multiple: bool = False) -> bool:
+        nb = t.numel() * t.element_size()
+        ok = t.is_cuda and t.dtype in (torch.bfloat16, torch.float32) and nb % 16 == 0
+        ok = ok and nb <= self.max_bytes
+        if shard_multiple:
+            ok = ok and nb % (16 * self.world) == 0
+        return ok
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        nb = t.numel() * t.element_size()
+        op = OP_ALLREDUCE_1SHOT if nb <= self.oneshot_max else OP_ALLREDUCE_2SHOT
+        self._launch(t, t, nb, op)
+        return t
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """out [n / world] = (sum over ranks of inp [n]) shard ``rank``."""
+        nb = inp.numel() * inp.element_size()
+        assert out.numel() * self.world == inp.numel() and nb % (16 * self.world) == 0
+        self._launch(inp, out, nb, OP_REDUCE_SCATTER)
+        return out
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """out [n * world] = concat over ranks of inp [n]."""
+        nb = out.numel() * out.element_size()
+        assert inp.numel() * self.world == out.numel() and nb % (16 * self.world) == 0
+        self._launch(inp, out, nb, OP_ALL_GATHER)
+        return out
+
+    def check(self):
+        """Raise if a barrier in any earlier collective timed out (synchronises)."""
+        v = ctypes.c_uint32(0)
+        torch.cuda.synchronize(self.device)
+        _check(_fn("mx_xgmi_error")(self._flags, ctypes.byref(v)), "mx_xgmi_error")
+        if v.value:
+            raise RuntimeError(f"xGMI collective barrier timed out on rank {self.rank} "
+                               f"(phase {v.value - 1}); a peer never arrived")
+
+    def close(self):
+        torch.cuda.synchronize(self.device)
+        for p in getattr(self, "_opened", []):
+            if p.value:
+                _fn("mx_xgmi_close_handle")(p)
+        self._opened = []
+        if getattr(self, "_data", None) is not None and (self._data.value or self._flags.value):
+            _fn("mx_xgmi_free")(self._data, self._flags)
+        self._data = ctypes.c_void_p()
+        self._flags = ctypes.c_void_p()
+
+    # ------------------------------------------------------------------ selection
+    # prefer[op] = [(message bytes, xgmi faster?)] measured by autotune(); None = always use
+    prefer: Optional[Dict[str, List]] = None
+    autotune_ok: Optional[bool] = None
+
+    def use_for(self, op: str, nbytes: int) -> bool:
+        if nbytes > self.max_bytes or nbytes % (16 * self.world):
+            return False
+        if self.prefer is None:
+            return True
+        table = self.prefer.get(op) or []
+        if not table:
+            return False
+        # nearest measured size class (log scale)
+        best = min(table, key=lambda e: abs(math.log2(e[0]) - math.log2(max(nbytes, 16))))
+        return bool(best[1])
+
+    def _rccl(self, op, out, inp):
+        if op == "all_reduce":
+            dist.all_reduce(out, group=self.group)
+        elif op == "reduce_scatter":
+            dist.reduce_scatter_tensor(out, inp, group=self.group)
+        else:
+            dist.all_gather_into_tensor(out, inp, group=self.group)
+
+    def _mine(self, op, out, inp):
+        if op == "all_reduce":
+            self.all_reduce_(out)
+        elif op == "reduce_scatter":
+            self.reduce_scatter(out, inp)
+        else:
+            self.all_gather(out, inp)
+
+    def autotune(self, sizes=(1 << 16, 1 << 20, 8 << 20, 64 << 20), iters: int = 8) -> Dict:
+        """Check this kernel against RCCL on the live group (integer-valued fp32 data, so
+        both must agree exactly) and time both per op and message size.  Timings are
+        max-reduced over the ranks so every rank takes the same decision; a mismatch or a
+        timed-out barrier on any rank disables the kernel (prefer = {} -> RCCL)."""
+        res = {}
+        w = self.world
+        ok = True
+        try:
+            for op in ("all_reduce", "reduce_scatter", "all_gather"):
+                for nb in sizes:
+                    if nb > self.max_bytes or nb % (16 * w):
+                        continue
+                    n = nb // 4
+                    big = torch.arange(n, device=self.device, dtype=torch.float32).remainder(13)
+                    big.add_(self.rank)
+                    small = big[: n // w].clone()
+                    inp = big if op == "reduce_scatter" else (small if op == "all_gather" else None)
+
+                    def fresh():
+                        if op == "all_reduce":
+                            return big.clone()
+                        return torch.empty(n // w if op == "reduce_scatter" else n, device=self.device)
+
+                    a, b = fresh(), fresh()
+                    self._mine(op, a, inp)
+                    self._rccl(op, b, inp)
+                    torch.cuda.synchronize(self.device)
+                    ok = ok and torch.equal(a, b)
+                    times = []
+                    for fn in (self._mine, self._rccl):
+                        o = fresh()
+                        for _ in range(2):
+                            fn(op, o, inp)
+                        torch.cuda.synchronize(self.device)
+                        e0 = torch.cuda.Event(enable_timing=True)
+                        e1 = torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        for _ in range(iters):
+                            fn(op, o, inp)
+                        e1.record()
+                        torch.cuda.synchronize(self.device)
+                        times.append(e0.elapsed_time(e1) / iters)
+                    res[(op, nb)] = times
+            self.check()
+        except Exception:
+            ok = False
+        flag = torch.tensor([0.0 if ok else 1.0], device=self.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        keys = sorted(res)
+        tt = torch.tensor([res[k] for k in keys] or [[0.0, 0.0]], device=self.device,
+                          dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=self.group)
+        prefer: Dict[str, List] = {"all_reduce": [], "reduce_scatter": [], "all_gather": []}
+        self.autotune_ok = float(flag.item()) == 0.0
+        if self.autotune_ok:
+            for k, (tx, tr) in zip(keys, tt.tolist()):
+                prefer[k[0]].append((k[1], tx < tr))
+                res[k] = (tx, tr)
+        else:
+            prefer = {}
+        self.prefer = prefer
+        return res
+
+
+_COMMS: Dict[int, Optional[XGMICommunicator]] = {}
+
+
+def mode() -> str:
+    """MXTRAIN_XGMI: 0 = RCCL only (default), 1 = xGMI kernels for every supported
+    message, auto = check + time both on the live group and keep the faster per size."""
+    return os.environ.get("MXTRAIN_XGMI", "0")
+
+
+def enabled() -> bool:
+    return mode() in ("1", "auto")
+
+
+def enable_xgmi(on="1"):
+    os.environ["MXTRAIN_XGMI"] = {True: "1", False: "0"}.get(on, on)
+
+
+def get_comm(group, device) -> Optional[XGMICommunicator]:
+    """The group's communicator when xGMI collectives are enabled and usable (GPU, one
+    node, <= 8 ranks), else None (callers use RCCL)."""
+    if not enabled() or group is None or not torch.cuda.is_available():
+        return None
+    if dist.get_world_size(group) == 1:
+        return None
+    key = id(group)
+    if key in _COMMS:
+        return _COMMS[key]
+    max_mb = int(os.environ.get("MXTRAIN_XGMI_MAX_MB", "256"))
+    try:
+        c = XGMICommunicator(group, device, max_bytes=max_mb << 20,
+                             timeout_s=float(os.environ.get("MXTRAIN_XGMI_TIMEOUT_S", "30")))
+    except XGMIUnavailable as e:   # agreed on every rank -> RCCL everywhere
+        if dist.get_rank(group) == 0:
+            print(f"[mxtrain] {e}; using RCCL", flush=True)
+        c = None
+    if c is not None and mode() == "auto":
+        c.autotune()
+        if dist.get_rank(group) == 0:
+            print(f"[mxtrain] xGMI autotune (world {c.world}): ok={c.autotune_ok} prefer={c.prefer}",
+                  flush=True)
+    _COMMS[key] = c
+    return c
+
+
+def route(group, t: torch.Tensor, op: str, nbytes: int) -> Optional[XGMICommunicator]:
+    """Communicator to use for this call, or None for RCCL.  Never builds a communicator
+    while a hipGraph is being captured (allocation + handle exchange are not capturable)."""
+    if not enabled() or group is None or not t.is_cuda:
+        return None
+    if id(group) not in _COMMS and torch.cuda.is_current_stream_capturing():
+        return None   # (build it eagerly first: e.g. warmup steps before the graph capture)
+    c = get_comm(group, t.device)
+    if c is None or not c.use_for(op, nbytes):
+        return None
+    return c
+
+
+def destroy_all():
+    for c in _COMMS.values():
+        if c is not None:
+            c.close()
+    _COMMS.clear()

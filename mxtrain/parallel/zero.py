@@ -22,6 +22,8 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
+from . import xgmi as _xgmi
+
 from ..ops import optim as optim_ops
 from .buffers import ALIGN, FlatParams
 
@@ -143,6 +145,23 @@ class DistributedOptimizer:
         self.units_left = {b: len(u) for b, u in self._bucket_units.items()}
         self.started = set()
 
+    # ------------------------------------------------------------------ DP collectives
+    def _rs(self, out, inp):
+        """Bucket gradient reduce-scatter: direct xGMI kernel when selected, else RCCL."""
+        c = _xgmi.route(self.dp_group, inp, "reduce_scatter", inp.numel() * inp.element_size())
+        if c is not None:
+            c.reduce_scatter(out, inp)
+        else:
+            dist.reduce_scatter_tensor(out, inp, group=self.dp_group)
+
+    def _ag(self, out, inp):
+        """Parameter-shard all-gather: direct xGMI kernel when selected, else RCCL."""
+        c = _xgmi.route(self.dp_group, inp, "all_gather", out.numel() * out.element_size())
+        if c is not None:
+            c.all_gather(out, inp)
+        else:
+            dist.all_gather_into_tensor(out, inp, group=self.dp_group)
+
     # ------------------------------------------------------------------ grad sync
     def _sp_allreduce(self, bucket):
         if self.sp_group is None:
@@ -165,12 +184,10 @@ class DistributedOptimizer:
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
                 self._sp_allreduce(b)
-                dist.reduce_scatter_tensor(self.grad_shard[so:so + n],
-                                           self.flat.grad[b.start:b.end], group=self.dp_group)
+                self._rs(self.grad_shard[so:so + n], self.flat.grad[b.start:b.end])
         else:
             self._sp_allreduce(b)
-            dist.reduce_scatter_tensor(self.grad_shard[so:so + n], self.flat.grad[b.start:b.end],
-                                       group=self.dp_group)
+            self._rs(self.grad_shard[so:so + n], self.flat.grad[b.start:b.end])
 
     def unit_done(self, unit: int):
         bi = self.flat.unit_to_bucket.get(unit)
@@ -242,8 +259,7 @@ class DistributedOptimizer:
             self.gather_pending = True
             return
         for (b, fs, so, n) in self.slices:
-            dist.all_gather_into_tensor(self.flat.data[b.start:b.end], self.param_shard[so:so + n],
-                                        group=self.dp_group)
+            self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n])
 
     def begin_param_gather(self):
         if not self.gather_pending:
@@ -257,12 +273,10 @@ class DistributedOptimizer:
             if cur is not None:
                 with torch.cuda.stream(self.comm_stream):
                     self.comm_stream.wait_event(ev0)
-                    dist.all_gather_into_tensor(self.flat.data[b.start:b.end], self.param_shard[so:so + n],
-                                                group=self.dp_group)
+                    self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n])
                     self._gather_events[bi] = self.comm_stream.record_event()
             else:
-                dist.all_gather_into_tensor(self.flat.data[b.start:b.end], self.param_shard[so:so + n],
-                                            group=self.dp_group)
+                self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n])
 
     def wait_unit(self, unit: int):
         bi = self.flat.unit_to_bucket.get(unit)
@@ -292,5 +306,4 @@ class DistributedOptimizer:
             self.param_shard[so:so + n].copy_(self.master[so:so + n].to(self.flat.dtype))
         if self.world > 1:
             for (b, fs, so, n) in self.slices:
-                dist.all_gather_into_tensor(self.flat.data[b.start:b.end],
-                                            self.param_shard[so:so + n], group=self.dp_group)
+                self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n])

@@ -42,6 +42,9 @@ class TrainConfig:
     overlap_grad_reduce: bool = True
     bucket_numel: int = 40_000_000
     capture_graph: bool = False
+    # weight-gradient GEMMs on a side HIP stream (GPU only).  Off by default: measured no
+    # gain at GPT-2 345M (19.97 vs 19.81 ms/step) -- hipBLASLt tiles already occupy every CU
+    wgrad_stream: bool = False
 
 
 class GPTTrainer:
@@ -65,6 +68,8 @@ class GPTTrainer:
         self.stage = GPTStage(cfg, self.flat.params, self.flat.grads, tp=ps.tp, tp_rank=ps.tp_rank,
                               tp_group=ps.tp_group, pp=ps.pp, pp_rank=ps.pp_rank,
                               sequence_parallel=ps.sequence_parallel, seed_t=self.seed.t)
+        if tcfg.wgrad_stream and self.device.type == "cuda":
+            self.stage.rt.wgrad_stream = torch.cuda.Stream(device=self.device)
         sched = LRSchedule(tcfg.lr, tcfg.min_lr, tcfg.lr_warmup_iters, tcfg.lr_decay_iters,
                            tcfg.lr_decay_style)
         self.opt = DistributedOptimizer(
@@ -76,6 +81,7 @@ class GPTTrainer:
             mp_group=ps.mp_group if ps.tp * ps.pp > 1 else None,
             embed_group=ps.embed_group if ps.pp > 1 and cfg.tie_embeddings else None,
             pp_rank=ps.pp_rank, schedule=sched)
+        self._setup_xgmi()
         self.pipeline = None
         if ps.pp > 1:
             from .parallel.pipeline import PipelineSchedule
@@ -85,6 +91,18 @@ class GPTTrainer:
         self._static = None
 
     # ------------------------------------------------------------------ init
+    def _setup_xgmi(self):
+        """Build the direct-xGMI communicators (MXTRAIN_XGMI=1|auto) eagerly, in the same
+        group order on every rank, so no handle exchange / autotune happens mid-step."""
+        from .parallel import xgmi
+        ps = self.ps
+        self.xgmi_comms = {}
+        if not xgmi.enabled() or self.device.type != "cuda":
+            return
+        for name, g, n in (("dp", ps.dp_group, ps.dp), ("tp", ps.tp_group, ps.tp)):
+            if g is not None and n > 1:
+                self.xgmi_comms[name] = xgmi.get_comm(g, self.device)
+
     def _sync_initial_params(self):
         ps = self.ps
         # DP replicas start identical (same generator seed per (pp, tp) already); tied

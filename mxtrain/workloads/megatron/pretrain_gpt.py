@@ -48,6 +48,8 @@ def main(argv=None):
     backend = "nccl" if (use_cuda and args.distributed_backend in ("nccl", "rccl")) else "gloo"
     if use_cuda and hasattr(torch.backends.cuda, "preferred_blas_library"):
         torch.backends.cuda.preferred_blas_library("hipblaslt")
+        from mxtrain.runtime.gemm_tuning import use_tuned_gemms
+        use_tuned_gemms()
     ps = pstate.initialize_model_parallel(args.tensor_model_parallel_size, args.pipeline_model_parallel_size,
                                           args.sequence_parallel, backend=backend,
                                           device_type="cuda" if use_cuda else "cpu")
