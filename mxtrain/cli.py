@@ -10,6 +10,8 @@
     python -m mxtrain pipeline run <pipeline.yaml>                        (KFP chart pipeline)
     python -m mxtrain node [--check]                                      (topology / GPU ledger / acceptance)
     python -m mxtrain hpo run <experiment.yaml>                           (Katib-style search)
+    python -m mxtrain dashboard [--port 8080]                             (central dashboard)
+    python -m mxtrain profile create|list|delete|poddefault <ns> ...      (Profiles / PodDefaults)
 """
 from __future__ import annotations
 
@@ -146,6 +148,41 @@ def cmd_node(a):
     return 0
 
 
+def cmd_dashboard(a):
+    from .mlplatform.dashboard import main as dash
+    argv = ["--host", a.host, "--port", str(a.port)]
+    for k in ("certfile", "keyfile", "htpasswd"):
+        if getattr(a, k):
+            argv += [f"--{k}", getattr(a, k)]
+    return dash(argv)
+
+
+def cmd_profile(a):
+    from .mlplatform import profiles as pr
+    if a.action == "create":
+        prof = pr.create(a.name, owner=a.owner, gpu_quota=a.gpu_quota, contributors=a.contributor)
+        print(json.dumps(prof, indent=1))
+    elif a.action == "delete":
+        pr.delete(a.name)
+        print(f'profile "{a.name}" deleted')
+    elif a.action == "poddefault":
+        import yaml
+        with open(a.file) as f:
+            pd = yaml.safe_load(f)
+        if pd.get("kind") == "PodDefault":    # accept the Kubernetes object form too
+            spec = pd.get("spec") or {}
+            pd = dict(spec, name=pd["metadata"]["name"])
+        pr.set_pod_default(a.name, pd)
+        print(f'poddefault "{pd.get("name")}" applied to {a.name}')
+    else:
+        for p in pr.list_profiles():
+            spec = p.get("spec") or {}
+            print(f"{p['metadata']['name']:32s} owner={(spec.get('owner') or {}).get('name')} "
+                  f"quota={((spec.get('resourceQuotaSpec') or {}).get('hard') or {})} "
+                  f"poddefaults={[d.get('name') for d in p.get('podDefaults') or []]}")
+    return 0
+
+
 def build_parser():
     p = argparse.ArgumentParser(prog="mxtrain")
     sp = p.add_subparsers(dest="cmd", required=True)
@@ -193,6 +230,21 @@ def build_parser():
     q.add_argument("--check", action="store_true", help="run the node acceptance checks (GPUs, HBM, RCCL, PV)")
     q.add_argument("--gpus", type=int, default=None)
     q.set_defaults(fn=cmd_node)
+    q = sp.add_parser("dashboard", help="central dashboard (jobs, volumes, tensorboards, HPO, pipelines)")
+    q.add_argument("--host", default="127.0.0.1")
+    q.add_argument("--port", type=int, default=8080)
+    q.add_argument("--certfile")
+    q.add_argument("--keyfile")
+    q.add_argument("--htpasswd")
+    q.set_defaults(fn=cmd_dashboard)
+    q = sp.add_parser("profile", help="namespaces (Kubeflow Profiles): quotas, owners, PodDefaults")
+    q.add_argument("action", choices=["create", "list", "delete", "poddefault"])
+    q.add_argument("name", nargs="?", default=rel.DEFAULT_NS)
+    q.add_argument("--owner", default="user@example.com")
+    q.add_argument("--gpu-quota", type=int, default=None)
+    q.add_argument("--contributor", action="append", default=[])
+    q.add_argument("-f", "--file", help="PodDefault YAML (poddefault action)")
+    q.set_defaults(fn=cmd_profile)
     q = sp.add_parser("hpo")
     q.add_argument("action", choices=["run"])
     q.add_argument("file")

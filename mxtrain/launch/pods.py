@@ -173,9 +173,15 @@ def build_pod(name: str, pod_template: dict, reldir: str, cm_dirs: Dict[str, str
               container_index: int = 0, command_override: Optional[List[str]] = None,
               role: str = "", index: int = 0):
     """Return (PodSpec, MountPlan) for one replica of a pod template."""
+    import copy
+    pod_template = copy.deepcopy(pod_template)
     spec = pod_template.get("spec", pod_template)
     containers = spec.get("containers") or [{}]
     c = containers[container_index]
+    # PodDefaults of the release's namespace (admission-webhook semantics, C50)
+    from ..mlplatform.profiles import apply_pod_defaults
+    ns = os.path.basename(os.path.dirname(os.path.abspath(reldir)))
+    applied = apply_pod_defaults(ns, pod_template if "spec" in pod_template else {"spec": spec}, c)
     plan = plan_mounts(c.get("volumeMounts") or [], spec.get("volumes") or [],
                        extra=_configmap_mounts(spec, cm_dirs, c))
     env = base_env()
@@ -186,6 +192,8 @@ def build_pod(name: str, pod_template: dict, reldir: str, cm_dirs: Dict[str, str
     env["HOSTNAME"] = name
     env["MXTRAIN_POD_NAME"] = name
     env["MXTRAIN_MOUNTS"] = json.dumps(plan.mounts)
+    if applied:
+        env["MXTRAIN_POD_DEFAULTS"] = ",".join(applied)
     if gpus:
         env["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in gpus)
     elif "HIP_VISIBLE_DEVICES" not in os.environ:

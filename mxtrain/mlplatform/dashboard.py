@@ -1,0 +1,327 @@
+"""Central dashboard for one MI355X node: the Kubeflow UI services of the reference
+(``charts/ml-platform/*``) as one small HTTP server.
+
+    python -m mxtrain dashboard [--port 8080] [--host 127.0.0.1]
+        [--certfile c.crt --keyfile c.key] [--htpasswd f]
+
+Replaces, per reference component:
+
+* C49 central dashboard menu (``kubeflow-central-dashboard/templates/config_map.yaml:11-97``)
+  -> ``GET /`` (HTML index, links below) and ``GET /api``;
+* C20/C21/C21b job views (``kubectl get pytorchjobs/mpijobs/rayjobs``) ->
+  ``GET /api/jobs[?namespace=]``, ``GET /api/jobs/<ns>/<name>`` (status + resources),
+  ``GET /api/jobs/<ns>/<name>/logs[?pod=]``;
+* C47 volumes web app -> ``GET /api/volumes`` (claims under the PV root, size, files),
+  ``GET /api/volumes/<claim>?path=<rel>`` (directory listing, read-only);
+* C44 Tensorboards (``Tensorboard.spec.logspath``) -> ``GET /api/tensorboards?logdir=<dir>``
+  (every scalar series of the tfevents files under a log dir, see obs/tensorboard.py)
+  and ``GET /tensorboard?logdir=<dir>`` (inline SVG charts);
+* C45 Katib UI -> ``GET /api/experiments`` (HPO experiments, trials, best);
+* C46 KFP UI -> ``GET /api/pipelines`` (recorded pipeline runs);
+* C48 profiles / KFAM -> ``GET /api/profiles``;
+* C22-C26 node view (Karpenter / device plugins) -> ``GET /api/node`` (GPUs, ledger,
+  node profile, sysfs power/clock samples);
+* C39/C40 Istio ingress + Dex/oauth2-proxy -> optional TLS and HTTP basic auth in front of
+  every route (same htpasswd format as the testing charts' nginx).
+
+Read-only by design: jobs are created with ``mxtrain install`` / the pipeline runner.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import html
+import json
+import os
+import ssl
+import urllib.parse
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Dict, List, Optional
+
+from ..runtime.storage import mxtrain_home, pv_root
+
+MENU = [
+    ("Jobs", "/api/jobs"), ("Volumes", "/api/volumes"), ("Tensorboards", "/tensorboard"),
+    ("Experiments (AutoML)", "/api/experiments"), ("Pipelines", "/api/pipelines"),
+    ("Profiles", "/api/profiles"), ("Node", "/api/node"),
+]
+
+
+# ----------------------------------------------------------------------------- data views
+def jobs(namespace: Optional[str] = None) -> List[dict]:
+    from ..launch import release as rel
+    out = []
+    for st in rel.list_releases(namespace):
+        out.append({"name": st.get("name"), "namespace": st.get("namespace"), "chart": st.get("chart"),
+                    "phase": st.get("phase"), "installed": st.get("installed"),
+                    "kinds": sorted({r.get("kind") for r in (st.get("resources") or {}).values()
+                                     if r.get("kind")})})
+    return out
+
+
+def job(namespace: str, name: str) -> dict:
+    from ..launch import release as rel
+    return rel.read_status(name, namespace)
+
+
+def job_logs(namespace: str, name: str, pod: Optional[str] = None) -> str:
+    from ..launch import release as rel
+    return rel.logs(name, namespace, pod)
+
+
+def _du(path: str, limit: int = 200000) -> Dict:
+    size = files = 0
+    for root, _, fs in os.walk(path):
+        for f in fs:
+            try:
+                size += os.path.getsize(os.path.join(root, f))
+            except OSError:
+                pass
+            files += 1
+            if files >= limit:
+                return {"bytes": size, "files": files, "truncated": True}
+    return {"bytes": size, "files": files}
+
+
+def volumes() -> List[dict]:
+    root = pv_root()
+    if not os.path.isdir(root):
+        return []
+    out = []
+    for claim in sorted(os.listdir(root)):
+        d = os.path.join(root, claim)
+        if os.path.isdir(d):
+            out.append(dict(name=claim, path=d, reclaimPolicy="Retain", accessModes=["ReadWriteMany"],
+                            **_du(d)))
+    return out
+
+
+def volume_browse(claim: str, rel_path: str = "") -> dict:
+    root = os.path.realpath(os.path.join(pv_root(), claim))
+    target = os.path.realpath(os.path.join(root, rel_path.lstrip("/")))
+    if not (target == root or target.startswith(root + os.sep)):
+        raise PermissionError("path escapes the volume")
+    if os.path.isfile(target):
+        return {"claim": claim, "path": rel_path, "file": True, "bytes": os.path.getsize(target)}
+    ents = []
+    for e in sorted(os.listdir(target))[:1000]:
+        p = os.path.join(target, e)
+        ents.append({"name": e, "dir": os.path.isdir(p),
+                     "bytes": os.path.getsize(p) if os.path.isfile(p) else None})
+    return {"claim": claim, "path": rel_path, "entries": ents}
+
+
+def tensorboard(logdir: str) -> dict:
+    from ..obs.tensorboard import read_scalars
+    if not os.path.isdir(logdir):
+        raise FileNotFoundError(logdir)
+    return {k: [{"step": s, "wall_time": w, "value": v} for s, w, v in series]
+            for k, series in read_scalars(logdir).items()}
+
+
+def experiments() -> List[dict]:
+    out = []
+    for p in sorted(glob.glob(os.path.join(mxtrain_home(), "hpo", "*", "experiment.json"))):
+        with open(p) as f:
+            e = json.load(f)
+        out.append({"name": e.get("name"), "condition": e.get("condition"), "objective": e.get("objective"),
+                    "trials": len(e.get("trials") or []), "best": e.get("best")})
+    return out
+
+
+def pipelines() -> List[dict]:
+    from ..pipeline import runs_dir
+    out = []
+    for p in sorted(glob.glob(os.path.join(runs_dir(), "*.json"))):
+        with open(p) as f:
+            out.append(json.load(f))
+    return out
+
+
+def profiles() -> List[dict]:
+    from .profiles import list_profiles
+    return list_profiles()
+
+
+def node() -> dict:
+    from ..runtime.topology import NODE_PROFILES, num_gpus
+    led_p = os.path.join(mxtrain_home(), "gpu-ledger.json")
+    led = {}
+    if os.path.exists(led_p):
+        try:
+            with open(led_p) as f:
+                led = json.load(f)
+        except ValueError:
+            led = {}
+    n = num_gpus()
+    try:
+        from ..obs.metrics import gpu_sample
+        sample = gpu_sample()
+    except Exception:
+        sample = {}
+    return {"gpus": n, "profile": f"mi355x.{n}x", "allocated": led, "free": n - len(led),
+            "pv_root": pv_root(), "sysfs": sample, "known_instance_types": NODE_PROFILES}
+
+
+# ----------------------------------------------------------------------------- HTML
+def _svg_series(points: List[dict], w: int = 480, h: int = 160) -> str:
+    if not points:
+        return ""
+    xs = [p["step"] for p in points]
+    ys = [p["value"] for p in points]
+    x0, x1 = min(xs), max(xs) or 1
+    y0, y1 = min(ys), max(ys)
+    if y1 == y0:
+        y1 = y0 + 1
+    sx = lambda x: 40 + (w - 50) * ((x - x0) / ((x1 - x0) or 1))  # noqa: E731
+    sy = lambda y: h - 20 - (h - 30) * ((y - y0) / (y1 - y0))  # noqa: E731
+    path = " ".join(f"{'M' if i == 0 else 'L'}{sx(x):.1f},{sy(y):.1f}" for i, (x, y) in enumerate(zip(xs, ys)))
+    return (f'<svg width="{w}" height="{h}" style="border:1px solid #ccc">'
+            f'<path d="{path}" fill="none" stroke="#1f77b4" stroke-width="1.5"/>'
+            f'<text x="2" y="12" font-size="10">{y1:.4g}</text><text x="2" y="{h - 22}" font-size="10">{y0:.4g}</text>'
+            f'<text x="40" y="{h - 4}" font-size="10">{x0}</text><text x="{w - 40}" y="{h - 4}" font-size="10">{x1}</text>'
+            "</svg>")
+
+
+def _index_html() -> str:
+    rows = "".join(f'<li><a href="{u}">{html.escape(n)}</a></li>' for n, u in MENU)
+    js = "".join(f"<tr><td>{html.escape(str(j['namespace']))}</td><td>"
+                 f"<a href=\"/api/jobs/{j['namespace']}/{j['name']}\">{html.escape(str(j['name']))}</a></td>"
+                 f"<td>{html.escape(str(j['chart']))}</td><td>{html.escape(str(j['phase']))}</td></tr>"
+                 for j in jobs())
+    return (f"<html><head><title>mxtrain dashboard</title></head><body><h2>mxtrain (MI355X node)</h2>"
+            f"<ul>{rows}</ul><h3>Jobs</h3><table border=1 cellpadding=3><tr><th>namespace</th><th>name</th>"
+            f"<th>chart</th><th>phase</th></tr>{js}</table></body></html>")
+
+
+def _tensorboard_html(logdir: Optional[str]) -> str:
+    if not logdir:
+        return ("<html><body><form action='/tensorboard'>log dir: <input name='logdir' size=60>"
+                "<input type=submit value='open'></form></body></html>")
+    data = tensorboard(logdir)
+    parts = [f"<h3>{html.escape(k)}</h3>{_svg_series(v)}" for k, v in sorted(data.items())]
+    return f"<html><body><h2>{html.escape(logdir)}</h2>{''.join(parts) or 'no scalars'}</body></html>"
+
+
+# ----------------------------------------------------------------------------- server
+class Auth:
+    def __init__(self, htpasswd: Optional[str]):
+        self.users: Dict[str, str] = {}
+        if htpasswd and os.path.exists(htpasswd):
+            with open(htpasswd) as f:
+                for line in f:
+                    line = line.strip()
+                    if ":" in line:
+                        u, h = line.split(":", 1)
+                        self.users[u] = h
+
+    def ok(self, header: Optional[str]) -> bool:
+        if not self.users:
+            return True
+        import base64
+        import hashlib
+        if not header or not header.startswith("Basic "):
+            return False
+        try:
+            u, p = base64.b64decode(header[6:]).decode().split(":", 1)
+        except Exception:  # noqa: BLE001
+            return False
+        h = self.users.get(u)
+        if h is None:
+            return False
+        if h.startswith("{SHA}"):
+            return h[5:] == base64.b64encode(hashlib.sha1(p.encode()).digest()).decode()
+        return h == p
+
+
+def route(path: str, q: Dict[str, str]):
+    """(status, content-type, body) for a GET; shared by the server and the tests."""
+    parts = [urllib.parse.unquote(x) for x in path.strip("/").split("/") if x]
+    js = "application/json"
+    try:
+        if not parts:
+            return 200, "text/html; charset=utf-8", _index_html()
+        if parts == ["tensorboard"]:
+            return 200, "text/html; charset=utf-8", _tensorboard_html(q.get("logdir"))
+        if parts[0] != "api":
+            return 404, js, json.dumps({"error": "not found"})
+        rest = parts[1:]
+        if not rest:
+            return 200, js, json.dumps({"menu": [{"name": n, "href": u} for n, u in MENU]})
+        k = rest[0]
+        if k == "jobs" and len(rest) == 1:
+            return 200, js, json.dumps(jobs(q.get("namespace")))
+        if k == "jobs" and len(rest) == 3:
+            return 200, js, json.dumps(job(rest[1], rest[2]), default=str)
+        if k == "jobs" and len(rest) == 4 and rest[3] == "logs":
+            return 200, "text/plain; charset=utf-8", job_logs(rest[1], rest[2], q.get("pod"))
+        if k == "volumes" and len(rest) == 1:
+            return 200, js, json.dumps(volumes())
+        if k == "volumes" and len(rest) == 2:
+            return 200, js, json.dumps(volume_browse(rest[1], q.get("path", "")))
+        if k == "tensorboards":
+            return 200, js, json.dumps(tensorboard(q["logdir"]))
+        if k == "experiments":
+            return 200, js, json.dumps(experiments(), default=str)
+        if k == "pipelines":
+            return 200, js, json.dumps(pipelines(), default=str)
+        if k == "profiles":
+            return 200, js, json.dumps(profiles(), default=str)
+        if k == "node":
+            return 200, js, json.dumps(node(), default=str)
+        return 404, js, json.dumps({"error": "not found"})
+    except (FileNotFoundError, KeyError) as e:
+        return 404, js, json.dumps({"error": repr(e)})
+    except PermissionError as e:
+        return 403, js, json.dumps({"error": repr(e)})
+
+
+def make_server(host: str, port: int, auth: Auth, certfile=None, keyfile=None) -> ThreadingHTTPServer:
+    class H(BaseHTTPRequestHandler):
+        def log_message(self, fmt, *a):
+            pass
+
+        def do_GET(self):  # noqa: N802
+            if not auth.ok(self.headers.get("Authorization")):
+                self.send_response(401)
+                self.send_header("WWW-Authenticate", 'Basic realm="mxtrain"')
+                self.end_headers()
+                return
+            u = urllib.parse.urlparse(self.path)
+            q = {k: v[0] for k, v in urllib.parse.parse_qs(u.query).items()}
+            code, ctype, body = route(u.path, q)
+            b = body.encode() if isinstance(body, str) else body
+            self.send_response(code)
+            self.send_header("Content-Type", ctype)
+            self.send_header("Content-Length", str(len(b)))
+            self.end_headers()
+            self.wfile.write(b)
+
+    srv = ThreadingHTTPServer((host, port), H)
+    if certfile and keyfile:
+        ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+        ctx.load_cert_chain(certfile, keyfile)
+        srv.socket = ctx.wrap_socket(srv.socket, server_side=True)
+    return srv
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="mxtrain dashboard")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=8080)
+    ap.add_argument("--certfile")
+    ap.add_argument("--keyfile")
+    ap.add_argument("--htpasswd")
+    a = ap.parse_args(argv)
+    srv = make_server(a.host, a.port, Auth(a.htpasswd), a.certfile, a.keyfile)
+    print(f"mxtrain dashboard on {'https' if a.certfile else 'http'}://{a.host}:{srv.server_address[1]}/",
+          flush=True)
+    try:
+        srv.serve_forever()
+    except KeyboardInterrupt:
+        pass
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -20,12 +20,13 @@ Differences from the reference, deliberately:
 """
 from __future__ import annotations
 
+import json
 import os
 import signal
 import sys
 import tempfile
 import time
-from typing import Dict, List
+from typing import Dict, List, Optional
 
 import yaml
 
@@ -139,11 +140,38 @@ class ChartHandler:
             return 1
 
 
-def run_pipeline(chart_configs: List[Dict], log=print) -> str:
+def runs_dir() -> str:
+    from .runtime.storage import mxtrain_home
+    return os.path.join(mxtrain_home(), "pipelines", "runs")
+
+
+def run_pipeline(chart_configs: List[Dict], log=print, run_name: Optional[str] = None) -> str:
+    """Sequential install -> wait -> uninstall of every chart config; "Failure" at the first
+    failing step.  The run (steps, timings, result) is recorded under
+    ``$MXTRAIN_HOME/pipelines/runs/`` (KFP run history, C46; shown by the dashboard)."""
+    run_name = run_name or time.strftime("run-%Y%m%d-%H%M%S")
+    rec = {"name": run_name, "started": time.time(), "steps": [], "result": None}
+
+    def _save():
+        os.makedirs(runs_dir(), exist_ok=True)
+        with open(os.path.join(runs_dir(), run_name + ".json"), "w") as f:
+            json.dump(rec, f, indent=1, default=str)
+
+    result = "Success"
     for cfg in chart_configs:
-        if ChartHandler(cfg, log)() > 0:
-            return "Failure"
-    return "Success"
+        t0 = time.time()
+        rc = ChartHandler(cfg, log)()
+        rec["steps"].append({"release": cfg.get("release_name"), "namespace": cfg.get("namespace"),
+                             "chart": cfg.get("chart") or cfg.get("path"), "exit_code": rc,
+                             "seconds": round(time.time() - t0, 2)})
+        _save()
+        if rc > 0:
+            result = "Failure"
+            break
+    rec["result"] = result
+    rec["finished"] = time.time()
+    _save()
+    return result
 
 
 def load_pipeline(path: str) -> List[Dict]:

@@ -132,6 +132,17 @@ class NodeLedger(GPUAllocator):
 
     def allocate(self, n: int) -> List[int]:
         def take(led):
+            ns = self.owner.split("/", 1)[0]
+            try:
+                from ..mlplatform.profiles import gpu_quota
+                quota = gpu_quota(ns)
+            except Exception:
+                quota = None
+            if quota is not None:
+                used = sum(1 for o in led.values() if str(o.get("owner", "")).split("/", 1)[0] == ns)
+                if used + n > quota:
+                    raise RuntimeError(f"exceeded quota: namespace {ns} requested {n} GPUs with "
+                                       f"{used} in use, limit amd.com/gpu={quota}")
             free = [g for g in self._free if str(g) not in led]
             if n > len(free):
                 busy = sorted({o["owner"] for o in led.values()})

@@ -242,6 +242,7 @@ def main(argv=None):
         return 0
 
     # ---------------------------------------------------------------- training
+    tbw = None
     train_sets = [COCODetection(cfg.DATA.BASEDIR, n, training=True) for n in cfg.DATA.TRAIN]
     ds = DetectionDataset(train_sets[0], short, max_size, training=True, with_masks=bool(cfg.MODE_MASK), seed=rank)
     bs = int(cfg.TRAIN.BATCH_SIZE_PER_GPU)
@@ -311,6 +312,13 @@ def main(argv=None):
                 lv = {kk: round(float(v.detach()), 4) for kk, v in losses.items()}
                 ips = (timed_imgs / (time.time() - t_timed)) if t_timed and timed_imgs else 0.0
                 log(f"step {step} lr {lr:.5f} {lv} images/s {ips:.2f}")
+                if rank == 0:   # tensorpack writes its monitors as TensorBoard events in logdir
+                    if tbw is None:
+                        from mxtrain.obs.tensorboard import SummaryWriter
+                        tbw = SummaryWriter(args.logdir)
+                    tbw.add_scalars_flat(dict(lv, learning_rate=lr, **({"throughput": ips} if ips else {})),
+                                         step)
+                    tbw.flush()
             if max_steps and step >= max_steps:
                 done = True
                 break

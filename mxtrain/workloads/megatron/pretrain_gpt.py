@@ -125,6 +125,10 @@ def main(argv=None):
     # ---------------------------------------------------------------- observability
     logs_dir = args.mx_metrics_dir or os.environ.get("LOGS_DIR") or os.path.join(os.environ.get("HOME", "."), "logs")
     metrics = MetricsWriter(logs_dir, ps.rank)
+    tb = None
+    if args.tensorboard_dir and ps.is_last_stage and ps.tp_rank == 0 and ps.dp_rank == 0:
+        from mxtrain.obs.tensorboard import SummaryWriter
+        tb = SummaryWriter(args.tensorboard_dir)
     fault = FaultInjector(ps.rank)
     watchdog = Watchdog(os.path.join(logs_dir, "heartbeat"), ps.rank, args.mx_watchdog)
     profiler = None
@@ -179,6 +183,11 @@ def main(argv=None):
                 metrics.write(step=it, loss=lv, lr=lr, grad_norm=gn, ms_per_step=dt * 1000, tokens_per_s=toks,
                               samples_per_s=gb / dt, tflops_per_gpu=tflops, consumed_samples=loader.consumed,
                               **hbm_stats(ps.device))
+            if tb is not None:   # Megatron's tensorboard tags
+                tb.add_scalars_flat({"lm loss": lv, "learning-rate": lr, "grad-norm": gn,
+                                     "iteration-time": dt, "tokens-per-sec": toks,
+                                     "lm loss vs samples": lv}, it)
+                tb.flush()
             loss_acc.zero_()
             t_log, it_log = time.time(), it
         if valid_loader is not None and args.eval_interval and it % args.eval_interval == 0 and args.eval_iters:

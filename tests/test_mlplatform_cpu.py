@@ -1,0 +1,134 @@
+"""ML-platform layer on CPU: TensorBoard event files (native CRC-32C), Profiles with GPU
+quotas, PodDefault injection into launched replicas, the central dashboard API
+(§5.5)."""
+import base64
+import json
+import os
+import threading
+import urllib.request
+
+import pytest
+import yaml
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHARTS = os.path.join(REPO, "charts", "machine-learning")
+
+
+@pytest.fixture()
+def home(tmp_path, monkeypatch):
+    monkeypatch.setenv("MXTRAIN_HOME", str(tmp_path / "home"))
+    monkeypatch.setenv("MXTRAIN_NUM_GPUS", "0")
+    monkeypatch.setenv("MXTRAIN_PV_LINK", "0")
+    return tmp_path
+
+
+def test_tfevents_roundtrip_and_crc(tmp_path):
+    from mxtrain.obs import tensorboard as tb
+    assert tb._py_crc32c(b"123456789") == 0xE3069283           # CRC-32C check value
+    data = os.urandom(3000)
+    assert tb.masked_crc32c(data) == ((((tb._py_crc32c(data) >> 15) | (tb._py_crc32c(data) << 17))
+                                       + 0xA282EAD8) & 0xFFFFFFFF)
+    with tb.SummaryWriter(str(tmp_path / "run1")) as w:
+        for s in range(5):
+            w.add_scalars_flat({"lm loss": 10.0 - s, "lr": 1e-4 * s}, s)
+    with tb.SummaryWriter(str(tmp_path / "run2")) as w:
+        w.add_scalar("lm loss", 3.5, 7)
+    sc = tb.read_scalars(str(tmp_path))
+    assert [v for _, _, v in sc["run1/lm loss"]] == [10.0, 9.0, 8.0, 7.0, 6.0]
+    assert sc["run2/lm loss"][0][0] == 7 and sc["run2/lm loss"][0][2] == 3.5
+    # first record is the file_version event
+    p = tb.event_files(str(tmp_path / "run2"))[0]
+    first = next(tb.read_records(p))
+    assert tb.decode_event(first)["file_version"] == "brain.Event:2"
+    # corruption is detected
+    raw = bytearray(open(p, "rb").read())
+    raw[-6] ^= 0xFF
+    open(p, "wb").write(bytes(raw))
+    with pytest.raises(ValueError):
+        list(tb.read_records(p))
+
+
+def test_profile_quota_blocks_gpu_allocation(home):
+    from mxtrain.mlplatform import profiles as pr
+    from mxtrain.runtime.topology import NodeLedger
+    pr.create("team-a", owner="a@x", gpu_quota=2, contributors=["b@x"])
+    assert pr.gpu_quota("team-a") == 2
+    assert pr.can("a@x", "delete", "team-a") and pr.can("b@x", "create", "team-a")
+    assert not pr.can("c@x", "get", "team-a") and not pr.can("b@x", "admin", "team-a")
+    led_path = str(home / "home" / "gpu-ledger.json")
+    l1 = NodeLedger(led_path, "team-a/job1", total=8)
+    assert len(l1.allocate(2)) == 2
+    l2 = NodeLedger(led_path, "team-a/job2", total=8)
+    with pytest.raises(RuntimeError, match="exceeded quota"):
+        l2.allocate(1)
+    l3 = NodeLedger(led_path, "team-b/job", total=8)     # no profile -> no quota
+    assert len(l3.allocate(4)) == 4
+
+
+def test_pod_default_injected_into_replicas(home):
+    from mxtrain.launch import release as rel
+    from mxtrain.mlplatform import profiles as pr
+    ns = "kubeflow-user-example-com"
+    pr.load(ns)   # default profile with access-ml-pipeline
+    pr.set_pod_default(ns, {"name": "hf-offline",
+                            "selector": {"matchExpressions": [
+                                {"key": "app.kubernetes.io/managed-by", "operator": "Exists"}]},
+                            "env": [{"name": "HF_HUB_OFFLINE", "value": "1"},
+                                    {"name": "HOME", "value": "/should/not/override"}]})
+    v = home / "v.yaml"
+    v.write_text(yaml.safe_dump({"train": {"env": [{"name": "HOME", "value": str(home / "h")}],
+                                           "command": ["python3", "-c"],
+                                           "args": ["\"import os; print('PD', os.environ.get('HF_HUB_OFFLINE'), "
+                                                    "os.environ['HOME'], os.environ.get('MXTRAIN_POD_DEFAULTS'))\""]},
+                                 "resources": {"nnodes": 1, "nproc_per_node": 1}}))
+    st = rel.install(os.path.join(CHARTS, "training/pytorchjob-distributed"), "pdtest", value_files=[str(v)],
+                     wait=True, timeout=120)
+    assert st["phase"] == "Succeeded", st
+    log = rel.logs("pdtest", ns, None)
+    assert f"PD 1 {home / 'h'} hf-offline" in log, log
+
+
+def test_dashboard_routes_and_auth(home, tmp_path):
+    from mxtrain.launch import release as rel
+    from mxtrain.mlplatform import dashboard as db
+    from mxtrain.obs.tensorboard import SummaryWriter
+    v = home / "v.yaml"
+    v.write_text(yaml.safe_dump({"pvc": [{"name": "pv-fsx", "mount_path": "/fsx"}],
+                                 "pre_script": ["mkdir -p /fsx/data", "echo hi > /fsx/data/a.txt"],
+                                 "process": {"command": ["true"]}}))
+    st = rel.install(os.path.join(CHARTS, "data-prep/data-process"), "dash", value_files=[str(v)],
+                     wait=True, timeout=120)
+    assert st["phase"] == "Succeeded"
+    with SummaryWriter(str(tmp_path / "tb")) as w:
+        w.add_scalar("loss", 2.0, 1)
+    code, _, body = db.route("/api/jobs", {})
+    assert code == 200 and any(j["name"] == "dash" and j["phase"] == "Succeeded" for j in json.loads(body))
+    code, _, body = db.route("/api/jobs/kubeflow-user-example-com/dash/logs", {})
+    assert code == 200 and "Processing script done" in body
+    code, _, body = db.route("/api/volumes", {})
+    vols = {x["name"]: x for x in json.loads(body)}
+    assert vols["pv-fsx"]["files"] >= 1
+    code, _, body = db.route("/api/volumes/pv-fsx", {"path": "data"})
+    assert [e["name"] for e in json.loads(body)["entries"]] == ["a.txt"]
+    assert db.route("/api/volumes/pv-fsx", {"path": "../../.."})[0] == 403
+    code, _, body = db.route("/api/tensorboards", {"logdir": str(tmp_path / "tb")})
+    assert json.loads(body)["loss"][0]["value"] == 2.0
+    assert db.route("/tensorboard", {"logdir": str(tmp_path / "tb")})[2].count("<svg") == 1
+    assert db.route("/api/nope", {})[0] == 404
+    for p in ("/", "/api", "/api/node", "/api/profiles", "/api/experiments", "/api/pipelines"):
+        assert db.route(p, {})[0] == 200, p
+    # live server with basic auth
+    ht = tmp_path / "htpasswd"
+    ht.write_text("admin:{SHA}" + base64.b64encode(__import__("hashlib").sha1(b"pw").digest()).decode() + "\n")
+    srv = db.make_server("127.0.0.1", 0, db.Auth(str(ht)))
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    try:
+        url = f"http://127.0.0.1:{srv.server_address[1]}/api/jobs"
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(url, timeout=10)
+        assert e.value.code == 401
+        req = urllib.request.Request(url, headers={"Authorization": "Basic " + base64.b64encode(b"admin:pw").decode()})
+        assert json.loads(urllib.request.urlopen(req, timeout=10).read())
+    finally:
+        srv.shutdown()
