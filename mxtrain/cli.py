@@ -9,6 +9,7 @@
     python -m mxtrain lint <chart> [-f ...]
     python -m mxtrain pipeline run <pipeline.yaml>                        (KFP chart pipeline)
     python -m mxtrain node [--check]                                      (topology / GPU ledger / acceptance)
+    python -m mxtrain node init -f infra/node.yaml | stage-data <src> <claim>:<path> | export <claim> | attach-pvc
     python -m mxtrain hpo run <experiment.yaml>                           (Katib-style search)
     python -m mxtrain dashboard [--port 8080]                             (central dashboard)
     python -m mxtrain profile create|list|delete|poddefault <ns> ...      (Profiles / PodDefaults)
@@ -136,6 +137,19 @@ def cmd_hpo(a):
 
 
 def cmd_node(a):
+    from .tools import node_init as ni
+    if a.action == "init":
+        print(json.dumps(ni.init_node(ni.load_config(a.file)), indent=1))
+        return 0
+    if a.action == "stage-data":
+        print(json.dumps(ni.stage_data(a.args[0], a.args[1])))
+        return 0
+    if a.action == "export":
+        print(json.dumps(ni.export_volume(a.args[0])))
+        return 0
+    if a.action == "attach-pvc":
+        print(json.dumps(ni.attach_info(), indent=1))
+        return 0
     if a.check:
         from .runtime.nodecheck import main as nodecheck
         return nodecheck([] if a.gpus is None else ["--gpus", str(a.gpus)])
@@ -227,6 +241,10 @@ def build_parser():
     q.add_argument("file")
     q.set_defaults(fn=cmd_pipeline)
     q = sp.add_parser("node")
+    q.add_argument("action", nargs="?", default="info",
+                   choices=["info", "init", "stage-data", "export", "attach-pvc"])
+    q.add_argument("args", nargs="*")
+    q.add_argument("-f", "--file", default=None, help="node config (infra/node.yaml) for init")
     q.add_argument("--check", action="store_true", help="run the node acceptance checks (GPUs, HBM, RCCL, PV)")
     q.add_argument("--gpus", type=int, default=None)
     q.set_defaults(fn=cmd_node)

@@ -73,8 +73,10 @@ print(json.dumps({"name": torch.cuda.get_device_name(0), "hbm_copy_tb_s": round(
 _COLL_PROBE = r"""
 import json, os, time, torch, torch.distributed as dist
 r, w = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-torch.cuda.set_device(0)
-dev = torch.device("cuda", 0)
+# one GPU per process: spawned with HIP_VISIBLE_DEVICES=<rank> (local) or under torchrun
+lr = int(os.environ.get("LOCAL_RANK", "0")) if torch.cuda.device_count() > 1 else 0
+torch.cuda.set_device(lr)
+dev = torch.device("cuda", lr)
 dist.init_process_group("nccl", rank=r, world_size=w, device_id=dev)
 out = {}
 for mb in (16, 256):
@@ -92,6 +94,18 @@ for mb in (16, 256):
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / 10
         out[f"{name}_{mb}MB_busbw_gb_s"] = round(n * 2 * factor / dt / 1e9, 1)
+if os.environ.get("MXTRAIN_XGMI", "0") in ("1", "auto") and w <= 8:
+    # the direct peer-to-peer kernels, checked against RCCL and timed per size
+    from mxtrain.parallel.xgmi import XGMICommunicator, XGMIUnavailable
+    try:
+        c = XGMICommunicator(dist.group.WORLD, dev, max_bytes=256 << 20)
+        res = c.autotune(sizes=(1 << 20, 16 << 20, 64 << 20))
+        out["xgmi_ok"] = c.autotune_ok
+        out["xgmi_vs_rccl_ms"] = {f"{op}_{nb >> 20}MB": [round(a, 4), round(b, 4)] for (op, nb), (a, b) in res.items()}
+        c.close()
+    except XGMIUnavailable as e:
+        out["xgmi_ok"] = False
+        out["xgmi_error"] = str(e)[:300]
 if r == 0:
     print(json.dumps(out))
 dist.destroy_process_group()
@@ -149,7 +163,13 @@ def main(argv=None):
     ap.add_argument("--json", default=None)
     ap.add_argument("--skip-collectives", action="store_true")
     ap.add_argument("--skip-devices", action="store_true")
+    ap.add_argument("--collectives-only", action="store_true",
+                    help="this process is one rank of an external launch (torchrun / mpirun): run "
+                         "only the collective probe in-process")
     a = ap.parse_args(argv)
+    if a.collectives_only:
+        exec(compile(_COLL_PROBE, "nodecheck-collectives", "exec"), {"__name__": "__nodecheck__"})
+        return 0
     inv = kfd_inventory()
     n = a.gpus if a.gpus is not None else len(inv)
     rep = {"time": time.strftime("%Y-%m-%dT%H:%M:%S"), "gpus_found": len(inv), "inventory": inv,

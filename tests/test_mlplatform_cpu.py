@@ -132,3 +132,43 @@ def test_dashboard_routes_and_auth(home, tmp_path):
         assert json.loads(urllib.request.urlopen(req, timeout=10).read())
     finally:
         srv.shutdown()
+
+
+def test_node_init_stage_export_and_images(home, tmp_path, monkeypatch):
+    import subprocess
+    import sys
+    repo_dir = tmp_path / "datarepo"
+    (repo_dir / "coco").mkdir(parents=True)
+    (repo_dir / "coco" / "a.json").write_text("{}")
+    cfg = tmp_path / "node.yaml"
+    base = yaml.safe_load(open(os.path.join(REPO, "infra", "node.yaml")))
+    base["volumes"][1]["data_repository"] = {"import_path": str(repo_dir)}
+    base["profiles"][0]["gpu_quota"] = 4
+    cfg.write_text(yaml.safe_dump(base))
+    env = dict(os.environ, PYTHONPATH=REPO)
+    r = subprocess.run([sys.executable, "-m", "mxtrain", "node", "init", "-f", str(cfg)], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    rep = json.loads(r.stdout)
+    pv = home / "home" / "pv"
+    assert rep["volumes"]["pv-fsx"]["import"]["copied"] == 1
+    assert (pv / "pv-fsx" / "coco" / "a.json").exists() and (pv / "pv-efs" / "home").is_dir()
+    from mxtrain.mlplatform import profiles as pr
+    assert pr.gpu_quota("kubeflow-user-example-com") == 4
+    src = tmp_path / "stage"
+    src.mkdir()
+    (src / "x.bin").write_bytes(b"1234")
+    from mxtrain.tools import node_init as ni
+    assert ni.stage_data(str(src), "pv-fsx:data/coco2017") == {"copied": 1, "skipped": 0}
+    assert ni.stage_data(str(src), "pv-fsx:data/coco2017") == {"copied": 0, "skipped": 1}
+    (pv / "pv-fsx" / "new.txt").write_text("n")
+    assert ni.export_volume("pv-fsx")["copied"] >= 1 and (repo_dir / "new.txt").exists()
+    assert {x["claim"] for x in ni.attach_info()} == {"pv-efs", "pv-fsx"}
+    # image-reference rewriting of values files (build_and_push.sh)
+    from mxtrain.tools import images
+    vf = tmp_path / "vals" / "v.yaml"
+    vf.parent.mkdir()
+    vf.write_text("image: 'old/megatron:1'  # pinned\nx:\n  - image: other/img\n  image: \"{{ .Values.x }}\"\n")
+    assert images.set_image("reg/mxtrain:rocm", [str(vf.parent)], match="megatron") == [str(vf)]
+    txt = vf.read_text()
+    assert "image: 'reg/mxtrain:rocm'  # pinned" in txt and "- image: other/img" in txt and "{{ .Values.x }}" in txt
