@@ -165,3 +165,19 @@ def test_legacy_maskrcnn_chart_renders_inline_mpirun(home):
     r2 = render_chart(load_chart(os.path.join(CHARTS, "training", "maskrcnn-optimized")), "mr")
     a2 = r2.by_kind("MPIJob")[0]["spec"]["mpiReplicaSpecs"]["Launcher"]["template"]["spec"]["containers"][0]["args"]
     assert "--images_per_epoch" in a2 and "TRAIN.BATCH_SIZE_PER_GPU=4" in a2 and "PREPROC.PREDEFINED_PADDING=True" in a2
+
+
+def test_redpajama_data_chart_offline(home):
+    """redpajama-data chart: idempotent download step writes DATA_DIR/data.jsonl (synthetic
+    RedPajama-style documents on the offline node) on the claim."""
+    import json as _j
+    from mxtrain.launch import release as rel
+    st = rel.install(os.path.join(CHARTS, "data-prep", "redpajama-data"), "rp", sets=["synthetic.num_docs=50"],
+                     wait=True, timeout=300)
+    assert st["phase"] == "Succeeded", rel.logs("rp")
+    f = home / "home" / "pv" / "pv-fsx" / "data" / "redpajama" / "data.jsonl"
+    lines = f.read_text().splitlines()
+    assert len(lines) == 50 and "text" in _j.loads(lines[0])
+    st = rel.install(os.path.join(CHARTS, "data-prep", "redpajama-data"), "rp2", sets=["synthetic.num_docs=50"],
+                     wait=True, timeout=300)
+    assert "already exists" in rel.logs("rp2")
