@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--sequence-parallel", action="store_true")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--pp", type=int, default=1)
+    ap.add_argument("--cp", type=int, default=1, help="Ulysses context-parallel size (sequence split)")
+    ap.add_argument("--seq-length", type=int, default=None, help="override the model's sequence length")
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph step capture")
     ap.add_argument("--graph", action="store_true",
                     help="capture the step in a hipGraph also when N > 1 (default: single GPU only; "
@@ -78,7 +80,8 @@ def main():
     from mxtrain.parallel import state as pstate
     from mxtrain.training import GPTTrainer, TrainConfig, synthetic_batch
 
-    ps = pstate.initialize_model_parallel(tp=args.tp, pp=args.pp, sequence_parallel=args.sequence_parallel)
+    ps = pstate.initialize_model_parallel(tp=args.tp, pp=args.pp, sequence_parallel=args.sequence_parallel,
+                                          cp=args.cp)
     world = ps.world_size
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
@@ -90,7 +93,11 @@ def main():
     from mxtrain.runtime.gemm_tuning import use_tuned_gemms
     n_tables = 0 if args.no_tuned_gemm else use_tuned_gemms(tune=args.tune_gemm,
                                                                tables=[] if args.tune_gemm else None)
-    cfg = GPTConfig(**GPT_CONFIGS[args.model])
+    mcfg = dict(GPT_CONFIGS[args.model])
+    if args.seq_length:
+        mcfg.update(seq_length=args.seq_length,
+                    max_position_embeddings=max(args.seq_length, mcfg.get("max_position_embeddings", 0)))
+    cfg = GPTConfig(**mcfg)
     tcfg = TrainConfig(micro_batch_size=args.micro_batch_size, global_batch_size=args.global_batch_size,
                        overlap_grad_reduce=not args.no_overlap, lr_warmup_iters=0,
                        wgrad_stream=args.wgrad_stream)
@@ -166,7 +173,8 @@ def main():
                 "seq_len": cfg.seq_length,
                 "parallelism": f"dp{ps.dp}" + (f"_tp{args.tp}" if args.tp > 1 else "")
                                + (f"_pp{args.pp}" if args.pp > 1 else "")
-                               + ("_sp" if ps.sequence_parallel else "") + "_zero1",
+                               + ("_sp" if ps.sequence_parallel else "") + (f"_cp{ps.cp}" if ps.cp > 1 else "")
+                               + "_zero1",
                 "hidden_dropout": cfg.hidden_dropout,
                 "attention_dropout": cfg.attention_dropout,
                 "hipgraph": use_graph,

@@ -324,7 +324,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 template <int D>
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(
     const uint16_t* __restrict__ o, int ldo, const uint16_t* __restrict__ dout, int lddo,
-    float* __restrict__ delta, int B, int S, int Hq) {
+    float* __restrict__ delta, int B, int S, int Hq, float* __restrict__ dq_zero) {
   constexpr int LPR = D / 8;  // lanes per (token, head) row
   const int gid = (blockIdx.x * 256 + threadIdx.x);
   const int row = gid / LPR, sub = gid % LPR;  // row = (b*S + s)*Hq + h
@@ -337,6 +337,11 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(
     unpack8(*reinterpret_cast<const uint4*>(dout + (size_t)tok * lddo + h * D + sub * 8), bb);
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc += a[j] * bb[j];
+    if (dq_zero) {  // the dQ atomics accumulator starts at zero (saves a separate fill)
+      float4* z = reinterpret_cast<float4*>(dq_zero + (size_t)tok * Hq * D + h * D + sub * 8);
+      z[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+      z[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   }
 #pragma unroll
   for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
@@ -722,11 +727,11 @@ MX_EXPORT int mx_attn_bwd(const void* q, const void* k, const void* v, int ldq, 
     if (D == 64)
       hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, dim3((unsigned)((threads + 255) / 256)),
                          dim3(256), 0, s, (const uint16_t*)o, ldo, (const uint16_t*)dout, lddo,
-                         delta, B, S, Hq);
+                         delta, B, S, Hq, dq_acc);
     else if (D == 128)
       hipLaunchKernelGGL(attn_bwd_pre_kernel<128>, dim3((unsigned)((threads + 255) / 256)),
                          dim3(256), 0, s, (const uint16_t*)o, ldo, (const uint16_t*)dout, lddo,
-                         delta, B, S, Hq);
+                         delta, B, S, Hq, dq_acc);
     else
       return hipErrorInvalidValue;
   }

@@ -76,6 +76,7 @@ __device__ __forceinline__ void stnt4(float* p, float4 v) {
   __builtin_nontemporal_store((nf4){v.x, v.y, v.z, v.w}, reinterpret_cast<nf4*>(p));
 }
 
+template <int U>
 __global__ __launch_bounds__(256) void adamw_kernel(
     float* __restrict__ master, float* __restrict__ m, float* __restrict__ v,
     const uint16_t* __restrict__ grad, uint16_t* __restrict__ param_out,
@@ -95,42 +96,69 @@ __global__ __launch_bounds__(256) void adamw_kernel(
   const float step_size = lr / bc1;
   const float inv_sqrt_bc2 = rsqrtf(bc2);
   const int64_t nvec = n / 8;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
-    const int64_t e = i * 8;
-    const float4 p0 = ldnt4(master + e), p1 = ldnt4(master + e + 4);
-    const float4 m0 = ldnt4(m + e), m1 = ldnt4(m + e + 4);
-    const float4 v0 = ldnt4(v + e), v1 = ldnt4(v + e + 4);
-    const nu4 gr = __builtin_nontemporal_load(reinterpret_cast<const nu4*>(grad) + i);
-    const uint4 graw = make_uint4(gr.x, gr.y, gr.z, gr.w);
-    const float decay = (wd_flags == nullptr || wd_flags[e >> 6]) ? wd : 0.f;
-    float g[8];
-    unpack8(graw, g);
-    float pp[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-    float pm[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
-    float pv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    const float keep = 1.f - lr * decay;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  // U independent 8-element vectors per thread-iteration: all 7*U loads are issued
+  // before any math, so more bytes are in flight per wave (HBM3E needs ~MBs in flight)
+  for (int64_t i0 = blockIdx.x * 256ll + threadIdx.x; i0 < nvec; i0 += stride * U) {
+    float4 p0[U], p1[U], m0[U], m1[U], v0[U], v1[U];
+    nu4 gr[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float gj = g[j] * gs;
-      pm[j] = b1 * pm[j] + (1.f - b1) * gj;
-      pv[j] = b2 * pv[j] + (1.f - b2) * gj * gj;
-      const float denom = sqrtf(pv[j]) * inv_sqrt_bc2 + eps;
-      pp[j] = pp[j] * keep - step_size * pm[j] / denom;
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i < nvec) {
+        const int64_t e = i * 8;
+        p0[u] = ldnt4(master + e); p1[u] = ldnt4(master + e + 4);
+        m0[u] = ldnt4(m + e); m1[u] = ldnt4(m + e + 4);
+        v0[u] = ldnt4(v + e); v1[u] = ldnt4(v + e + 4);
+        gr[u] = __builtin_nontemporal_load(reinterpret_cast<const nu4*>(grad) + i);
+      }
     }
-    stnt4(master + e, make_float4(pp[0], pp[1], pp[2], pp[3]));
-    stnt4(master + e + 4, make_float4(pp[4], pp[5], pp[6], pp[7]));
-    stnt4(m + e, make_float4(pm[0], pm[1], pm[2], pm[3]));
-    stnt4(m + e + 4, make_float4(pm[4], pm[5], pm[6], pm[7]));
-    stnt4(v + e, make_float4(pv[0], pv[1], pv[2], pv[3]));
-    stnt4(v + e + 4, make_float4(pv[4], pv[5], pv[6], pv[7]));
-    const uint4 po = pack8(pp);
-    __builtin_nontemporal_store((nu4){po.x, po.y, po.z, po.w}, reinterpret_cast<nu4*>(param_out) + i);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= nvec) break;
+      const int64_t e = i * 8;
+      const float decay = (wd_flags == nullptr || wd_flags[e >> 6]) ? wd : 0.f;
+      float g[8];
+      unpack8(make_uint4(gr[u].x, gr[u].y, gr[u].z, gr[u].w), g);
+      float pp[8] = {p0[u].x, p0[u].y, p0[u].z, p0[u].w, p1[u].x, p1[u].y, p1[u].z, p1[u].w};
+      float pm[8] = {m0[u].x, m0[u].y, m0[u].z, m0[u].w, m1[u].x, m1[u].y, m1[u].z, m1[u].w};
+      float pv[8] = {v0[u].x, v0[u].y, v0[u].z, v0[u].w, v1[u].x, v1[u].y, v1[u].z, v1[u].w};
+      const float keep = 1.f - lr * decay;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gj = g[j] * gs;
+        pm[j] = b1 * pm[j] + (1.f - b1) * gj;
+        pv[j] = b2 * pv[j] + (1.f - b2) * gj * gj;
+        const float denom = sqrtf(pv[j]) * inv_sqrt_bc2 + eps;
+        pp[j] = pp[j] * keep - step_size * pm[j] / denom;
+      }
+      stnt4(master + e, make_float4(pp[0], pp[1], pp[2], pp[3]));
+      stnt4(master + e + 4, make_float4(pp[4], pp[5], pp[6], pp[7]));
+      stnt4(m + e, make_float4(pm[0], pm[1], pm[2], pm[3]));
+      stnt4(m + e + 4, make_float4(pm[4], pm[5], pm[6], pm[7]));
+      stnt4(v + e, make_float4(pv[0], pv[1], pv[2], pv[3]));
+      stnt4(v + e + 4, make_float4(pv[4], pv[5], pv[6], pv[7]));
+      const uint4 po = pack8(pp);
+      __builtin_nontemporal_store((nu4){po.x, po.y, po.z, po.w}, reinterpret_cast<nu4*>(param_out) + i);
+    }
   }
 }
+
+int g_adam_unroll = 1;
+int g_adam_blocks = 4096;
 
 }  // namespace
 
 MX_EXPORT int mx_sumsq_nparts() { return 1024; }
+
+// launch shape of mx_adamw_step (unroll 1|2 vectors per thread-iteration, max blocks)
+MX_EXPORT int mx_adamw_config(int unroll, int blocks) {
+  if (unroll != 1 && unroll != 2) return hipErrorInvalidValue;
+  g_adam_unroll = unroll;
+  if (blocks > 0) g_adam_blocks = blocks;
+  return hipSuccess;
+}
 
 // normsq_out[0] (+)= sum((g*scale)^2); partial must hold mx_sumsq_nparts() floats
 MX_EXPORT int mx_sumsq_bf16(const void* g, int64_t n, float scale, const uint8_t* flags,
@@ -151,9 +179,13 @@ MX_EXPORT int mx_adamw_step(float* master, float* m, float* v, const void* grad,
                             const float* hyper, const float* normsq, hipStream_t s) {
   if (n % 8) return hipErrorInvalidValue;  // flat shards are 64-element aligned
   int64_t blocks = (n / 8 + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
+  if (blocks > g_adam_blocks) blocks = g_adam_blocks;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, s, master, m, v,
-                     (const uint16_t*)grad, (uint16_t*)param_out, wd_flags, n, hyper, normsq);
+  if (g_adam_unroll == 2)
+    hipLaunchKernelGGL(adamw_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, master, m, v,
+                       (const uint16_t*)grad, (uint16_t*)param_out, wd_flags, n, hyper, normsq);
+  else
+    hipLaunchKernelGGL(adamw_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, master, m, v,
+                       (const uint16_t*)grad, (uint16_t*)param_out, wd_flags, n, hyper, normsq);
   return hipGetLastError();
 }

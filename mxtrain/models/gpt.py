@@ -38,6 +38,7 @@ from ..ops.fused import (bias_gelu_bwd, bias_gelu_fwd, bias_swiglu_bwd, bias_swi
                          cross_entropy_fwd_bwd, embed_bwd, embed_fwd, pos_embed_bwd)
 from ..parallel import collectives as C
 from ..parallel.buffers import ParamSpec
+from ..parallel.ulysses import head_to_seq, seq_to_head
 
 
 @dataclass
@@ -241,6 +242,9 @@ class StepRuntime:
     tp: int = 1
     tp_rank: int = 0
     sp: bool = False
+    cp: int = 1                   # Ulysses context parallel: tokens here are S/cp of each sequence
+    cp_rank: int = 0
+    cp_group: Optional[object] = None
     seed_t: Optional[torch.Tensor] = None
     training: bool = True
     vocab_start: int = 0
@@ -261,14 +265,15 @@ class StepRuntime:
         return self.cfg.normalization == "rmsnorm"
 
     def rope_(self, x, hl, kvl, inverse=False):
-        """RoPE (K5) in place on the Q and K blocks of a packed [T, (hl+2kvl)*D] buffer."""
+        """RoPE (K5) in place on the Q and K blocks of a packed [T, (hl+2kvl)*D] buffer
+        holding whole sequences (under context parallelism: after the Ulysses exchange)."""
         cfg = self.cfg
         if cfg.position_embedding != "rope":
             return
         D = cfg.head_dim
         rd = int(D * cfg.rotary_percent) // 8 * 8
         for col0, nh in ((0, hl), (hl * D, kvl)):
-            apply_rope_(x, col0, nh, D, self.S, rd, cfg.rotary_base,
+            apply_rope_(x, col0, nh, D, self.S * self.cp, rd, cfg.rotary_base,
                         max_pos=cfg.max_position_embeddings, inverse=inverse)
 
     def norm_params(self, prefix):
@@ -339,7 +344,8 @@ class EmbedFn(torch.autograd.Function):
         # vocab-parallel: every TP rank gathers its vocab shard and the shards are summed
         # by the all-reduce, so the (replicated) position table is added by rank 0 only
         wpe = P.get("wpe") if rt.tp_rank == 0 else None
-        e = embed_fwd(ids, P["wte"], wpe, seq=rt.S, vocab_start=rt.vocab_start)
+        e = embed_fwd(ids, P["wte"], wpe, seq=rt.S, vocab_start=rt.vocab_start,
+                      pos_offset=rt.cp_rank * rt.S)
         if rt.tp > 1:
             C.all_reduce_(e, rt.tp_group)
             if rt.sp:
@@ -365,7 +371,8 @@ class EmbedFn(torch.autograd.Function):
             de = C.all_gather_dim0(de, rt.tp_group)
         embed_bwd(ids, de, rt.grads["wte"], rt.vocab_start)
         if "wpe" in rt.grads:
-            pos_embed_bwd(de, rt.grads["wpe"], rt.B, rt.S)
+            off = rt.cp_rank * rt.S
+            pos_embed_bwd(de, rt.grads["wpe"][off:off + rt.S], rt.B, rt.S)
         rt.done(0)
         ctx.saved = None
         return None, None, None, None
@@ -407,11 +414,17 @@ class GPTLayerFn(torch.autograd.Function):
         eps = cfg.layernorm_epsilon
         a_full = _gather(a, rt)
         qkv = torch.addmm(P[p + "qkv_b"], a_full, P[p + "qkv_w"].t())
-        rt.rope_(qkv, hl, kvl)
-        q = qkv[:, : hl * D]
-        k = qkv[:, hl * D:(hl + kvl) * D]
-        v = qkv[:, (hl + kvl) * D:]
-        ctx_, lse = attn_ops.attn_fwd(q, k, v, rt.B, rt.S, hl, kvl, D, causal=True)
+        if rt.cp > 1:   # Ulysses: whole sequences, 1/cp of the heads
+            qkv_a = seq_to_head(qkv, (hl * D, kvl * D, kvl * D), rt.B, rt.S, rt.cp_group)
+            ha, kva = hl // rt.cp, kvl // rt.cp
+        else:
+            qkv_a, ha, kva = qkv, hl, kvl
+        rt.rope_(qkv_a, ha, kva)
+        q = qkv_a[:, : ha * D]
+        k = qkv_a[:, ha * D:(ha + kva) * D]
+        v = qkv_a[:, (ha + kva) * D:]
+        ctx_a, lse = attn_ops.attn_fwd(q, k, v, rt.B, rt.S * rt.cp, ha, kva, D, causal=True)
+        ctx_ = head_to_seq(ctx_a, (hl * D,), rt.B, rt.S, rt.cp_group) if rt.cp > 1 else ctx_a
         o = _reduce(torch.mm(ctx_, P[p + "proj_w"].t()), rt)
         w2, b2 = rt.norm_params(p + "ln2")
         h1, m, mean2, rstd2 = bda_norm_fwd(o, P[p + "proj_b"], h, w2, b2, eps, rt.p_drop, rt.seed_t,
@@ -429,7 +442,7 @@ class GPTLayerFn(torch.autograd.Function):
             wn, bn = P[p + "ln2_w"], P.get(p + "ln2_b")
         h2, a2, mean_n, rstd_n = bda_norm_fwd(g, P[p + "fc2_b"], h1, wn, bn, eps, rt.p_drop,
                                               rt.seed_t, rt.salt(1001 + 2 * i), rt.rms)
-        ctx.saved = (a_full, qkv, ctx_, lse, h1, mean2, rstd2, m_full, pre, f, h2, mean_n, rstd_n)
+        ctx.saved = (a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2, m_full, pre, f, h2, mean_n, rstd_n)
         ctx.rt, ctx.i, ctx.next_norm = rt, i, next_norm
         if next_norm is None:
             return h2, torch.empty(0, device=h2.device, dtype=h2.dtype)
@@ -444,7 +457,7 @@ class GPTLayerFn(torch.autograd.Function):
         D = cfg.head_dim
         hl = cfg.num_attention_heads // rt.tp
         kvl = cfg.num_kv_heads // rt.tp
-        (a_full, qkv, ctx_, lse, h1, mean2, rstd2, m_full, pre, f, h2, mean_n, rstd_n) = ctx.saved
+        (a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2, m_full, pre, f, h2, mean_n, rstd_n) = ctx.saved
         ctx.saved = None
         dh2 = dh2.contiguous()
         # ---- BDA-LN(next) backward
@@ -482,14 +495,21 @@ class GPTLayerFn(torch.autograd.Function):
         do_full = _gather(do_, rt)
         rt.wgrad(G[p + "proj_w"], do_full, ctx_)
         dctx = torch.mm(do_full, P[p + "proj_w"])
-        dqkv = torch.empty_like(qkv)
-        q = qkv[:, : hl * D]
-        k = qkv[:, hl * D:(hl + kvl) * D]
-        v = qkv[:, (hl + kvl) * D:]
-        attn_ops.attn_bwd(dctx, q, k, v, ctx_, lse, rt.B, rt.S, hl, kvl, D, causal=True,
-                          dq=dqkv[:, : hl * D], dk=dqkv[:, hl * D:(hl + kvl) * D],
-                          dv=dqkv[:, (hl + kvl) * D:])
-        rt.rope_(dqkv, hl, kvl, inverse=True)
+        if rt.cp > 1:
+            dctx = seq_to_head(dctx, (hl * D,), rt.B, rt.S, rt.cp_group)
+            ha, kva = hl // rt.cp, kvl // rt.cp
+        else:
+            ha, kva = hl, kvl
+        dqkv = torch.empty_like(qkv_a)
+        q = qkv_a[:, : ha * D]
+        k = qkv_a[:, ha * D:(ha + kva) * D]
+        v = qkv_a[:, (ha + kva) * D:]
+        attn_ops.attn_bwd(dctx, q, k, v, ctx_a, lse, rt.B, rt.S * rt.cp, ha, kva, D, causal=True,
+                          dq=dqkv[:, : ha * D], dk=dqkv[:, ha * D:(ha + kva) * D],
+                          dv=dqkv[:, (ha + kva) * D:])
+        rt.rope_(dqkv, ha, kva, inverse=True)
+        if rt.cp > 1:
+            dqkv = head_to_seq(dqkv, (hl * D, kvl * D, kvl * D), rt.B, rt.S, rt.cp_group)
         colsum(dqkv, G[p + "qkv_b"], accumulate=True)
         rt.wgrad(G[p + "qkv_w"], dqkv, a_full)
         da = _reduce(torch.mm(dqkv, P[p + "qkv_w"]), rt)
@@ -531,14 +551,17 @@ class GPTStage:
     """The layers of one pipeline stage (all layers when pp == 1)."""
 
     def __init__(self, cfg: GPTConfig, params, grads, tp=1, tp_rank=0, tp_group=None, pp=1,
-                 pp_rank=0, sequence_parallel=False, seed_t=None):
+                 pp_rank=0, sequence_parallel=False, seed_t=None, cp=1, cp_rank=0, cp_group=None):
         self.cfg = cfg
         self.l0, self.l1 = stage_layer_range(cfg, pp, pp_rank)
         self.first, self.last = pp_rank == 0, pp_rank == pp - 1
         V = cfg.padded_vocab(tp) // tp
         self.rt = StepRuntime(cfg=cfg, params=params, grads=grads, tp_group=tp_group, tp=tp,
                               tp_rank=tp_rank, sp=sequence_parallel and tp > 1, seed_t=seed_t,
-                              vocab_start=tp_rank * V)
+                              vocab_start=tp_rank * V, cp=cp, cp_rank=cp_rank, cp_group=cp_group)
+        if cp > 1:
+            assert (cfg.num_attention_heads // tp) % cp == 0 and (cfg.num_kv_heads // tp) % cp == 0, \
+                "Ulysses needs the (per-TP-rank) query and KV head counts divisible by the cp size"
         self.anchor = torch.zeros(1, requires_grad=True)
         if self.last:
             if cfg.tie_embeddings:

@@ -51,6 +51,7 @@ SIGNATURES = {
     # optim.hip
     "mx_sumsq_nparts": [],
     "mx_sumsq_bf16": [P, I64, F, P, P, P, I, P],
+    "mx_adamw_config": [I, I],
     "mx_adamw_step": [P, P, P, P, P, P, I64, P, P, P],
     # attention.hip
     "mx_attn_fwd": [P, P, P, I, I, I, P, I, P, I, I, I, I, I, I, P, F, P],

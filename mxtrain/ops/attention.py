@@ -79,7 +79,8 @@ def attn_bwd(dout, q, k, v, o, lse, B, S, Hq, Hkv, D, causal=True, klen=None, sc
     if dv is None:
         dv = torch.empty(B * S, Hkv * D, dtype=q.dtype, device=q.device)
     delta = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
-    dq_acc = torch.zeros(B * S, Hq * D, dtype=torch.float32, device=q.device)
+    # zeroed by the delta pre-pass inside mx_attn_bwd
+    dq_acc = torch.empty(B * S, Hq * D, dtype=torch.float32, device=q.device)
     kl = klen.to(torch.int32).contiguous() if klen is not None else None
     _lib.call("mx_attn_bwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), q.stride(0), k.stride(0),
               v.stride(0), _lib.ptr(o), o.stride(0), _lib.ptr(dout), dout.stride(0), _lib.ptr(lse),

@@ -27,10 +27,14 @@ class ParallelState:
     tp: int = 1
     pp: int = 1
     dp: int = 1
+    cp: int = 1                              # Ulysses context parallel (sequence split)
     tp_rank: int = 0
     pp_rank: int = 0
     dp_rank: int = 0
+    cp_rank: int = 0
     sequence_parallel: bool = False
+    cp_group: Optional[object] = None
+    grad_group: Optional[object] = None      # dp x cp: replicas that reduce gradients
     tp_group: Optional[object] = None
     pp_group: Optional[object] = None
     dp_group: Optional[object] = None
@@ -38,6 +42,10 @@ class ParallelState:
     embed_group: Optional[object] = None     # first + last pipeline stage (tied embedding)
     pp_ranks: List[int] = field(default_factory=list)
     device: torch.device = torch.device("cpu")
+
+    @property
+    def grad_world(self):
+        return self.dp * self.cp
 
     @property
     def is_first_stage(self):
@@ -98,51 +106,76 @@ def init_distributed(backend: Optional[str] = None, device_type: Optional[str] =
 
 
 def initialize_model_parallel(tp: int = 1, pp: int = 1, sequence_parallel: bool = False,
-                              backend: Optional[str] = None, device_type: Optional[str] = None
-                              ) -> ParallelState:
+                              backend: Optional[str] = None, device_type: Optional[str] = None,
+                              cp: int = 1) -> ParallelState:
+    """Rank order (Megatron): tensor fastest, then context (Ulysses), then data, then
+    pipeline: rank = ((p * dp + d) * cp + c) * tp + t.  The gradient-reduction group of
+    a rank is its dp x cp replicas (context-parallel ranks hold the same weights and see
+    different tokens of the same sequences)."""
     global _STATE
     world, rank, local_rank, device = init_distributed(backend, device_type)
-    assert world % (tp * pp) == 0, f"world {world} not divisible by tp*pp={tp * pp}"
-    dp = world // (tp * pp)
-    st = ParallelState(world_size=world, rank=rank, local_rank=local_rank, tp=tp, pp=pp, dp=dp,
+    assert world % (tp * pp * cp) == 0, f"world {world} not divisible by tp*pp*cp={tp * pp * cp}"
+    dp = world // (tp * pp * cp)
+    st = ParallelState(world_size=world, rank=rank, local_rank=local_rank, tp=tp, pp=pp, dp=dp, cp=cp,
                        sequence_parallel=sequence_parallel and tp > 1, device=device)
 
-    def rank_of(p, d, t):
-        return p * dp * tp + d * tp + t
+    def rank_of(p, d, t, c=0):
+        return ((p * dp + d) * cp + c) * tp + t
 
-    st.pp_rank = rank // (dp * tp)
-    st.dp_rank = (rank // tp) % dp
     st.tp_rank = rank % tp
-    st.pp_ranks = [rank_of(p, st.dp_rank, st.tp_rank) for p in range(pp)]
+    st.cp_rank = (rank // tp) % cp
+    st.dp_rank = (rank // (tp * cp)) % dp
+    st.pp_rank = rank // (dp * cp * tp)
+    st.pp_ranks = [rank_of(p, st.dp_rank, st.tp_rank, st.cp_rank) for p in range(pp)]
     if world > 1:
         # every rank must call new_group for every group, in the same order
         for p in range(pp):
             for d in range(dp):
-                ranks = [rank_of(p, d, t) for t in range(tp)]
-                g = dist.new_group(ranks)
-                if rank in ranks:
-                    st.tp_group = g
+                for c in range(cp):
+                    ranks = [rank_of(p, d, t, c) for t in range(tp)]
+                    g = dist.new_group(ranks)
+                    if rank in ranks:
+                        st.tp_group = g
         for p in range(pp):
             for t in range(tp):
-                ranks = [rank_of(p, d, t) for d in range(dp)]
+                for c in range(cp):
+                    ranks = [rank_of(p, d, t, c) for d in range(dp)]
+                    g = dist.new_group(ranks)
+                    if rank in ranks:
+                        st.dp_group = g
+        if cp > 1:
+            for p in range(pp):
+                for d in range(dp):
+                    for t in range(tp):
+                        ranks = [rank_of(p, d, t, c) for c in range(cp)]
+                        g = dist.new_group(ranks)
+                        if rank in ranks:
+                            st.cp_group = g
+            for p in range(pp):
+                for t in range(tp):
+                    ranks = [rank_of(p, d, t, c) for d in range(dp) for c in range(cp)]
+                    g = dist.new_group(ranks)
+                    if rank in ranks:
+                        st.grad_group = g
+        for d in range(dp):
+            for c in range(cp):
+                for t in range(tp):
+                    ranks = [rank_of(p, d, t, c) for p in range(pp)]
+                    g = dist.new_group(ranks)
+                    if rank in ranks:
+                        st.pp_group = g
+                    eranks = sorted({ranks[0], ranks[-1]})
+                    eg = dist.new_group(eranks)
+                    if rank in eranks:
+                        st.embed_group = eg
+        for d in range(dp):
+            for c in range(cp):
+                ranks = [rank_of(p, d, t, c) for p in range(pp) for t in range(tp)]
                 g = dist.new_group(ranks)
                 if rank in ranks:
-                    st.dp_group = g
-        for d in range(dp):
-            for t in range(tp):
-                ranks = [rank_of(p, d, t) for p in range(pp)]
-                g = dist.new_group(ranks)
-                if rank in ranks:
-                    st.pp_group = g
-                eranks = sorted({ranks[0], ranks[-1]})
-                eg = dist.new_group(eranks)
-                if rank in eranks:
-                    st.embed_group = eg
-        for d in range(dp):
-            ranks = [rank_of(p, d, t) for p in range(pp) for t in range(tp)]
-            g = dist.new_group(ranks)
-            if rank in ranks:
-                st.mp_group = g
+                    st.mp_group = g
+    if cp == 1:
+        st.grad_group = st.dp_group
     _STATE = st
     return st
 

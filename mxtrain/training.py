@@ -54,26 +54,28 @@ class GPTTrainer:
         self.ps = ps = ps or pstate.get()
         self.device = ps.device
         self.dtype = dtype
+        # (context-parallel ranks share sequences: the batch is split over dp only)
         gb = tcfg.global_batch_size or tcfg.micro_batch_size * ps.dp
         assert gb % (tcfg.micro_batch_size * ps.dp) == 0, "global batch must divide mbs*dp"
         self.num_micro = gb // (tcfg.micro_batch_size * ps.dp)
         self.global_batch = gb
         specs = gpt_param_specs(cfg, ps.tp, ps.pp, ps.pp_rank, ps.sequence_parallel)
-        self.flat = FlatParams(specs, self.device, dtype, dp_world=ps.dp,
+        self.flat = FlatParams(specs, self.device, dtype, dp_world=ps.grad_world,
                                bucket_numel=tcfg.bucket_numel)
         gen = torch.Generator().manual_seed(tcfg.seed + 1000 * ps.pp_rank + 100 * ps.tp_rank)
         self.flat.initialize(gen, cfg.num_layers)
         self._sync_initial_params()
-        self.seed = DropoutSeed(self.device, tcfg.seed + 7 * ps.dp_rank)
+        self.seed = DropoutSeed(self.device, tcfg.seed + 7 * (ps.dp_rank * ps.cp + ps.cp_rank))
         self.stage = GPTStage(cfg, self.flat.params, self.flat.grads, tp=ps.tp, tp_rank=ps.tp_rank,
                               tp_group=ps.tp_group, pp=ps.pp, pp_rank=ps.pp_rank,
-                              sequence_parallel=ps.sequence_parallel, seed_t=self.seed.t)
+                              sequence_parallel=ps.sequence_parallel, seed_t=self.seed.t,
+                              cp=ps.cp, cp_rank=ps.cp_rank, cp_group=ps.cp_group)
         if tcfg.wgrad_stream and self.device.type == "cuda":
             self.stage.rt.wgrad_stream = torch.cuda.Stream(device=self.device)
         sched = LRSchedule(tcfg.lr, tcfg.min_lr, tcfg.lr_warmup_iters, tcfg.lr_decay_iters,
                            tcfg.lr_decay_style)
         self.opt = DistributedOptimizer(
-            self.flat, dp_group=ps.dp_group if ps.dp > 1 else None, lr=tcfg.lr,
+            self.flat, dp_group=ps.grad_group if ps.grad_world > 1 else None, lr=tcfg.lr,
             betas=(tcfg.adam_beta1, tcfg.adam_beta2), eps=tcfg.adam_eps,
             weight_decay=tcfg.weight_decay, clip_grad=tcfg.clip_grad,
             overlap=tcfg.overlap_grad_reduce, tp_rank=ps.tp_rank, tp_group=ps.tp_group,
@@ -99,7 +101,7 @@ class GPTTrainer:
         self.xgmi_comms = {}
         if not xgmi.enabled() or self.device.type != "cuda":
             return
-        for name, g, n in (("dp", ps.dp_group, ps.dp), ("tp", ps.tp_group, ps.tp)):
+        for name, g, n in (("dp", ps.grad_group, ps.grad_world), ("tp", ps.tp_group, ps.tp)):
             if g is not None and n > 1:
                 self.xgmi_comms[name] = xgmi.get_comm(g, self.device)
 
@@ -121,9 +123,24 @@ class GPTTrainer:
         loss.backward()
         return loss.detach()
 
+    def _local(self, t: torch.Tensor) -> torch.Tensor:
+        """Whole sequences in, this context-parallel rank's S/cp slice out."""
+        if self.ps.cp == 1:
+            return t
+        from .parallel.ulysses import local_chunk
+        return local_chunk(t, self.ps.cp, self.ps.cp_rank)
+
+    def _cp_mean(self, loss: torch.Tensor) -> torch.Tensor:
+        if self.ps.cp > 1:
+            dist.all_reduce(loss, group=self.ps.cp_group)
+            loss = loss / self.ps.cp
+        return loss
+
     def train_step(self, tokens: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-        """tokens/labels: [num_micro, micro_batch, seq] int64 on device.  Returns the
-        mean loss over the step as a device scalar (last stage; 0 elsewhere)."""
+        """tokens/labels: [num_micro, micro_batch, seq] int64 on device (whole sequences,
+        also under context parallelism).  Returns the mean loss over the step as a device
+        scalar (last stage; 0 elsewhere)."""
+        tokens, labels = self._local(tokens), self._local(labels)
         if self._graph is not None:
             self._static[0].copy_(tokens)
             self._static[1].copy_(labels)
@@ -153,7 +170,7 @@ class GPTTrainer:
                                                            m == nm - 1)
         self.opt.step()
         self.iteration += 1
-        return loss
+        return self._cp_mean(loss)
 
     def capture(self, tokens, labels, warmup: int = 2):
         """Capture one whole training step (fwd, bwd, grad reduce, optimizer) into a
@@ -161,6 +178,7 @@ class GPTTrainer:
         side-stream steps are real training steps on (tokens, labels); the loss of the
         last one is returned so callers can account for it."""
         assert self.device.type == "cuda"
+        tokens, labels = self._local(tokens), self._local(labels)
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         last = None
@@ -209,7 +227,7 @@ class GPTTrainer:
         o.gather_pending = False   # (overlap mode) the next replay's body gathers
         o._gather_events.clear()
         o.reset_pending()
-        return loss
+        return self._cp_mean(loss)
 
     def _begin_step(self):
         self.opt.begin_param_gather()
@@ -224,6 +242,7 @@ class GPTTrainer:
     def eval_step(self, tokens: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         """Forward-only loss (dropout off, no gradients, optimizer untouched); mean over
         the step's tokens on the last stage."""
+        tokens, labels = self._local(tokens), self._local(labels)
         nm, B, S = tokens.shape
         self.sync_params()
         rt = self.stage.rt
@@ -232,12 +251,12 @@ class GPTTrainer:
         rt.grad_scale = 1.0 / (nm * B * S)
         try:
             if self.pipeline is not None:
-                return self.pipeline.run_forward_only(tokens, labels)
+                return self._cp_mean(self.pipeline.run_forward_only(tokens, labels))
             loss = torch.zeros((), dtype=torch.float32, device=self.device)
             for m in range(nm):
                 loss = loss + self.stage.forward(ids=tokens[m].reshape(-1), labels=labels[m].reshape(-1),
                                                  B=B, S=S).detach()
-            return loss
+            return self._cp_mean(loss)
         finally:
             rt.training = True
 

@@ -90,7 +90,10 @@ def build_parser() -> argparse.ArgumentParser:
     a("--distributed-backend", default="nccl", choices=["nccl", "gloo", "rccl"])
     a("--local_rank", "--local-rank", dest="local_rank", type=int, default=None)
     a("--DDP-impl", default="local")
-    a("--ds-sequence-parallel-size", type=int, default=1)
+    # Ulysses context parallelism (DeepSpeed --ds-sequence-parallel-size; Megatron-core
+    # spelling --context-parallel-size is accepted too)
+    a("--ds-sequence-parallel-size", "--context-parallel-size", dest="ds_sequence_parallel_size",
+      type=int, default=1)
     # data
     a("--data-path", nargs="*", default=None)
     a("--data-cache-path", default=None)
@@ -175,9 +178,9 @@ def parse_args(argv: Optional[List[str]] = None):
     args.ds_train_batch_size = ds.get("train_batch_size")
     args.world_size = int(os.environ.get("WORLD_SIZE", "1"))
     args.rank = int(os.environ.get("RANK", "0"))
-    mp = args.tensor_model_parallel_size * args.pipeline_model_parallel_size
+    mp = args.tensor_model_parallel_size * args.pipeline_model_parallel_size * args.ds_sequence_parallel_size
     if args.world_size % mp:
-        raise SystemExit(f"world size {args.world_size} not divisible by TP*PP={mp}")
+        raise SystemExit(f"world size {args.world_size} not divisible by TP*PP*CP={mp}")
     args.data_parallel_size = args.world_size // mp
     if args.global_batch_size is None:
         args.global_batch_size = (args.ds_train_batch_size or

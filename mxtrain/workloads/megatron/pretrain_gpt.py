@@ -52,8 +52,9 @@ def main(argv=None):
         use_tuned_gemms()
     ps = pstate.initialize_model_parallel(args.tensor_model_parallel_size, args.pipeline_model_parallel_size,
                                           args.sequence_parallel, backend=backend,
-                                          device_type="cuda" if use_cuda else "cpu")
-    print_rank_0(f"> initialized mxtrain: world {ps.world_size} = TP {ps.tp} x PP {ps.pp} x DP {ps.dp}, "
+                                          device_type="cuda" if use_cuda else "cpu",
+                                          cp=args.ds_sequence_parallel_size)
+    print_rank_0(f"> initialized mxtrain: world {ps.world_size} = TP {ps.tp} x PP {ps.pp} x CP {ps.cp} x DP {ps.dp}, "
                  f"backend {backend}{' (RCCL)' if backend == 'nccl' else ''}, device {ps.device}")
 
     # ---------------------------------------------------------------- tokenizer / vocab

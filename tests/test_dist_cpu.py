@@ -62,10 +62,11 @@ def _worker(rank, world, port, mode, q):
     from mxtrain.models.gpt import GPTConfig, shard_gpt_state
     from mxtrain.parallel import state as pstate
     from mxtrain.training import GPTTrainer, TrainConfig
-    tp = 2 if mode in ("tp", "sp", "3d", "3dsp") else 1
+    tp = 2 if mode in ("tp", "sp", "3d", "3dsp", "tpcp") else 1
     pp = 2 if mode in ("pp", "3d", "3dsp") else 1
+    cp = 2 if mode in ("cp", "tpcp") else 1
     ps = pstate.initialize_model_parallel(tp=tp, pp=pp, sequence_parallel=mode in ("sp", "3dsp"),
-                                          backend="gloo", device_type="cpu")
+                                          backend="gloo", device_type="cpu", cp=cp)
     cfg = GPTConfig(**ccfg)
     # reference init (identical on every rank), then take this rank's shard
     _, _, init_sd = _ref_init(ccfg)
@@ -151,7 +152,7 @@ def _check(mode, reference, loss_ranks):
             for a, b in zip(losses, ref_losses):
                 assert abs(a - b) < 2e-5 * max(1.0, abs(b)), (mode, rank, losses, ref_losses)
         m = mode.split(":")[0]
-        exp = shard_gpt_state(ref_sd, cfg, 2 if m in ("tp", "sp") else 1, tpr,
+        exp = shard_gpt_state(ref_sd, cfg, 2 if m in ("tp", "sp", "tpcp") else 1, tpr,
                               2 if m == "pp" else 1, ppr)
         for n, t in exp.items():
             assert torch.allclose(params[n], t, atol=3e-5, rtol=1e-4), (mode, rank, n,
@@ -181,6 +182,29 @@ def test_tp2_sequence_parallel_matches_single(reference):
 def test_tp2_sp_llama_style_matches_single():
     """RoPE + GQA + RMSNorm + SwiGLU under TP2 + sequence parallel."""
     _check("sp:llama", _make_reference(CFG_LLAMA), loss_ranks=(0, 1))
+
+
+def test_ulysses_cp2_matches_single(reference):
+    """Ulysses context parallelism (P8): each rank holds half of every sequence; the
+    attention runs on half the heads over whole sequences after an all-to-all."""
+    _check("cp", reference, loss_ranks=(0, 1))
+
+
+def test_ulysses_cp2_rope_gqa_matches_single():
+    _check("cp:llama", _make_reference(CFG_LLAMA), loss_ranks=(0, 1))
+
+
+def test_tp2_x_ulysses_cp2_matches_single(reference):
+    """4 ranks: TP2 (heads split) x CP2 (sequence split, head groups within each TP shard)."""
+    cfg, ref_losses, ref_sd = reference
+    from mxtrain.models.gpt import shard_gpt_state
+    res = _run("tpcp", world=4)
+    for rank, _, losses, params, (tpr, ppr, dpr) in res:
+        for a, b in zip(losses, ref_losses):
+            assert abs(a - b) < 2e-5 * max(1.0, abs(b)), (rank, losses, ref_losses)
+        exp = shard_gpt_state(ref_sd, cfg, 2, tpr, 1, 0)
+        for n, t in exp.items():
+            assert torch.allclose(params[n], t, atol=3e-5, rtol=1e-4), (rank, n, (params[n] - t).abs().max())
 
 
 def test_pp2_1f1b_matches_single(reference):
