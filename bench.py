@@ -53,6 +53,9 @@ def main():
     ap.add_argument("--pp", type=int, default=1)
     ap.add_argument("--cp", type=int, default=1, help="Ulysses context-parallel size (sequence split)")
     ap.add_argument("--seq-length", type=int, default=None, help="override the model's sequence length")
+    ap.add_argument("--num-experts", type=int, default=0, help="MoE: experts per MoE layer (every 2nd layer)")
+    ap.add_argument("--ep", type=int, default=1, help="MoE expert-parallel size")
+    ap.add_argument("--topk", type=int, default=1)
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph step capture")
     ap.add_argument("--graph", action="store_true",
                     help="capture the step in a hipGraph also when N > 1 (default: single GPU only; "
@@ -97,10 +100,12 @@ def main():
     if args.seq_length:
         mcfg.update(seq_length=args.seq_length,
                     max_position_embeddings=max(args.seq_length, mcfg.get("max_position_embeddings", 0)))
+    if args.num_experts > 1:
+        mcfg.update(num_experts=args.num_experts, moe_topk=args.topk)
     cfg = GPTConfig(**mcfg)
     tcfg = TrainConfig(micro_batch_size=args.micro_batch_size, global_batch_size=args.global_batch_size,
                        overlap_grad_reduce=not args.no_overlap, lr_warmup_iters=0,
-                       wgrad_stream=args.wgrad_stream)
+                       wgrad_stream=args.wgrad_stream, moe_expert_parallel_size=args.ep)
     tr = GPTTrainer(cfg, tcfg, ps)
     gen = torch.Generator().manual_seed(1 + ps.dp_rank)
     tokens, labels = synthetic_batch(cfg, tr.num_micro, args.micro_batch_size, ps.device, gen)
@@ -174,6 +179,7 @@ def main():
                 "parallelism": f"dp{ps.dp}" + (f"_tp{args.tp}" if args.tp > 1 else "")
                                + (f"_pp{args.pp}" if args.pp > 1 else "")
                                + ("_sp" if ps.sequence_parallel else "") + (f"_cp{ps.cp}" if ps.cp > 1 else "")
+                               + (f"_moe{args.num_experts}x_ep{args.ep}_top{args.topk}" if args.num_experts > 1 else "")
                                + "_zero1",
                 "hidden_dropout": cfg.hidden_dropout,
                 "attention_dropout": cfg.attention_dropout,

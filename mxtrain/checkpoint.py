@@ -41,7 +41,12 @@ _LAYER_MAP = {
     "ln2_w": "post_attention_layernorm.weight", "ln2_b": "post_attention_layernorm.bias",
     "fc1_w": "mlp.dense_h_to_4h.weight", "fc1_b": "mlp.dense_h_to_4h.bias",
     "fc2_w": "mlp.dense_4h_to_h.weight", "fc2_b": "mlp.dense_4h_to_h.bias",
+    "router_w": "mlp.deepspeed_moe.gate.wg.weight",
 }
+# expert tensors, one file per (layer, global expert id) as DeepSpeed MoE writes them:
+# layer_<L>_expert_<E>_mp_rank_<MM>_model_states.pt
+_EXPERT_MAP = {"fc1_w": "dense_h_to_4h.weight", "fc1_b": "dense_h_to_4h.bias",
+               "fc2_w": "dense_4h_to_h.weight", "fc2_b": "dense_4h_to_h.bias"}
 _LAYER_RMAP = {v: k for k, v in _LAYER_MAP.items()}
 
 
@@ -125,6 +130,47 @@ def _mp_rank(ps) -> int:
     return ps.pp_rank * ps.tp + ps.tp_rank
 
 
+def _grad_rank(ps) -> int:
+    """Index of this rank's ZeRO-1 shard in its gradient (dp x cp) group."""
+    return ps.dp_rank * ps.cp + ps.cp_rank
+
+
+def _optim_state(opt, sched, partitions):
+    return {
+        "zero_stage": 1, "loss_scaler": None, "dynamic_loss_scale": False, "overflow": False,
+        "clip_grad": opt.clip, "partition_count": [partitions],
+        "base_optimizer_state": {
+            "state": {0: {"step": opt.step_count, "exp_avg": opt.exp_avg.detach().cpu(),
+                          "exp_avg_sq": opt.exp_avg_sq.detach().cpu()}},
+            "param_groups": [{"lr": sched(opt.step_count), "betas": list(opt.betas), "eps": opt.eps,
+                              "weight_decay": opt.wd, "params": [0]}]},
+        "single_partition_of_fp32_groups": [opt.master.detach().cpu()],
+        "mx_shard_layout": [[int(b.start), int(b.end), int(so), int(n)] for (b, fs, so, n) in opt.slices],
+    }
+
+
+def _load_optim(opt, path):
+    o = torch.load(path, map_location="cpu", weights_only=True)["optimizer_state_dict"]
+    base = o["base_optimizer_state"]["state"][0]
+    opt.load_shard_state({"master": o["single_partition_of_fp32_groups"][0],
+                          "exp_avg": base["exp_avg"], "exp_avg_sq": base["exp_avg_sq"],
+                          "step": base["step"]})
+
+
+def _expert_files(trainer, d, mp):
+    """[(path, {our name: tensor view})] for this EP rank's experts."""
+    out = []
+    El = trainer.cfg.num_experts // trainer.tcfg.moe_expert_parallel_size
+    for name, t in trainer.eflat.params.items():
+        _, i, _, leaf = name.split(".", 3)
+        for j in range(El):
+            e = trainer.ep_rank * El + j
+            out.append((os.path.join(d, f"layer_{int(i)}_expert_{e}_mp_rank_{mp:02d}_model_states.pt"),
+                        f"language_model.encoder.layers.{int(i)}.mlp.deepspeed_moe.experts."
+                        f"deepspeed_experts.{e}.{_EXPERT_MAP[leaf]}", name, j))
+    return out
+
+
 def _atomic_save(obj, path):
     tmp = path + f".tmp{os.getpid()}"
     torch.save(obj, tmp)
@@ -145,7 +191,7 @@ def save_checkpoint(save_dir: str, trainer, iteration: int, consumed_samples: in
     sched = opt.schedule
     lr_state = {"max_lr": sched.lr, "min_lr": sched.min_lr, "warmup_steps": sched.warmup,
                 "num_steps": opt.step_count, "decay_steps": sched.decay, "decay_style": sched.style}
-    if ps.dp_rank == 0:
+    if ps.dp_rank == 0 and ps.cp_rank == 0:
         module = to_megatron_state(trainer.flat.params, trainer.cfg, ps.tp, ps.pp, ps.pp_rank)
         state = {
             "module": module, "buffer_names": [], "optimizer": None, "lr_scheduler": lr_state,
@@ -158,21 +204,21 @@ def save_checkpoint(save_dir: str, trainer, iteration: int, consumed_samples: in
             "mx_config": trainer.cfg.__dict__.copy(),
         }
         _atomic_save(state, os.path.join(d, f"mp_rank_{mp:02d}_model_states.pt"))
-    optim = {
-        "optimizer_state_dict": {
-            "zero_stage": 1, "loss_scaler": None, "dynamic_loss_scale": False, "overflow": False,
-            "clip_grad": opt.clip, "partition_count": [ps.dp],
-            "base_optimizer_state": {
-                "state": {0: {"step": opt.step_count, "exp_avg": opt.exp_avg.detach().cpu(),
-                              "exp_avg_sq": opt.exp_avg_sq.detach().cpu()}},
-                "param_groups": [{"lr": sched(opt.step_count), "betas": list(opt.betas), "eps": opt.eps,
-                                  "weight_decay": opt.wd, "params": [0]}]},
-            "single_partition_of_fp32_groups": [opt.master.detach().cpu()],
-            "mx_shard_layout": [[int(b.start), int(b.end), int(so), int(n)] for (b, fs, so, n) in opt.slices],
-        },
-        "ds_config": ds_config or {}, "ds_version": DS_VERSION,
-    }
-    _atomic_save(optim, os.path.join(d, f"zero_pp_rank_{ps.dp_rank}_mp_rank_{mp:02d}_optim_states.pt"))
+    optim = {"optimizer_state_dict": _optim_state(opt, sched, ps.grad_world),
+             "ds_config": ds_config or {}, "ds_version": DS_VERSION}
+    _atomic_save(optim, os.path.join(d, f"zero_pp_rank_{_grad_rank(ps)}_mp_rank_{mp:02d}_optim_states.pt"))
+    if trainer.eflat is not None:
+        eo = trainer.eopt
+        edp_rank = _grad_rank(ps) // trainer.tcfg.moe_expert_parallel_size
+        if edp_rank == 0:   # one replica of each expert set writes the expert files
+            files: Dict[str, Dict[str, torch.Tensor]] = {}
+            for path, key, name, j in _expert_files(trainer, d, mp):
+                files.setdefault(path, {})[key] = trainer.eflat.params[name][j].detach().cpu().clone()
+            for path, sd_e in files.items():
+                _atomic_save(sd_e, path)
+        _atomic_save({"optimizer_state_dict": _optim_state(eo, sched, eo.world), "ds_version": DS_VERSION},
+                     os.path.join(d, f"expp_rank_{trainer.ep_rank}_zero_pp_rank_{edp_rank}"
+                                     f"_mp_rank_{mp:02d}_optim_states.pt"))
     if dist.is_initialized():
         dist.barrier()
     if local_leader is None:
@@ -206,7 +252,7 @@ def load_checkpoint(load_dir: str, trainer, load_optim: bool = True) -> Optional
     ps = trainer.ps
     d = os.path.join(load_dir, f"global_step{it}")
     mp = _mp_rank(ps)
-    opt_path = os.path.join(d, f"zero_pp_rank_{ps.dp_rank}_mp_rank_{mp:02d}_optim_states.pt")
+    opt_path = os.path.join(d, f"zero_pp_rank_{_grad_rank(ps)}_mp_rank_{mp:02d}_optim_states.pt")
     model_path = os.path.join(d, f"mp_rank_{mp:02d}_model_states.pt")
     info = {"iteration": it, "consumed_samples": 0}
     if os.path.exists(model_path):
@@ -215,17 +261,27 @@ def load_checkpoint(load_dir: str, trainer, load_optim: bool = True) -> Optional
         trainer.flat.load_state_dict(sd)
         info["consumed_samples"] = int(st.get("global_samples", 0))
         trainer.opt._refresh_master()
+    if trainer.eflat is not None:
+        cache: Dict[str, Dict[str, torch.Tensor]] = {}
+        for path, key, name, j in _expert_files(trainer, d, mp):
+            if os.path.exists(path):
+                if path not in cache:
+                    cache[path] = torch.load(path, map_location="cpu", weights_only=True)
+                trainer.eflat.params[name][j].copy_(cache[path][key].to(trainer.eflat.dtype))
+        if cache:
+            trainer.eopt._refresh_master()
+        edp_rank = _grad_rank(ps) // trainer.tcfg.moe_expert_parallel_size
+        ep_path = os.path.join(d, f"expp_rank_{trainer.ep_rank}_zero_pp_rank_{edp_rank}"
+                                  f"_mp_rank_{mp:02d}_optim_states.pt")
+        if load_optim and os.path.exists(ep_path):
+            _load_optim(trainer.eopt, ep_path)
     if load_optim and os.path.exists(opt_path):
-        o = torch.load(opt_path, map_location="cpu", weights_only=True)["optimizer_state_dict"]
-        base = o["base_optimizer_state"]["state"][0]
-        trainer.opt.load_shard_state({"master": o["single_partition_of_fp32_groups"][0],
-                                      "exp_avg": base["exp_avg"], "exp_avg_sq": base["exp_avg_sq"],
-                                      "step": base["step"]})
+        _load_optim(trainer.opt, opt_path)
     elif not os.path.exists(model_path):
         raise FileNotFoundError(f"no model or optimizer state for mp_rank {mp} / dp_rank {ps.dp_rank} in {d}")
     if "consumed_samples" not in info or info["consumed_samples"] == 0:
         info["consumed_samples"] = it * trainer.global_batch
     trainer.iteration = it
     # dropout stream continues where it stopped (one advance per optimizer step)
-    trainer.seed.set_step(trainer.tcfg.seed + 7 * ps.dp_rank, trainer.opt.step_count)
+    trainer.seed.set_step(trainer.tcfg.seed + 7 * (ps.dp_rank * ps.cp + ps.cp_rank), trainer.opt.step_count)
     return info

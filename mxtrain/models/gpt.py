@@ -39,6 +39,7 @@ from ..ops.fused import (bias_gelu_bwd, bias_gelu_fwd, bias_swiglu_bwd, bias_swi
 from ..parallel import collectives as C
 from ..parallel.buffers import ParamSpec
 from ..parallel.ulysses import head_to_seq, seq_to_head
+from .moe import is_moe_layer, moe_mlp
 
 
 @dataclass
@@ -60,6 +61,14 @@ class GPTConfig:
     position_embedding: str = "learned"    # learned | rope
     rotary_percent: float = 1.0
     swiglu: bool = False                   # fc1 -> [a | b], silu(a) * b (Megatron --swiglu)
+    # Mixture of Experts (Megatron-DeepSpeed MoE flags; models/moe.py)
+    num_experts: int = 0                   # <= 1: dense MLP everywhere
+    expert_interval: int = 2               # MoE MLP in every expert_interval-th layer
+    moe_topk: int = 1
+    moe_train_capacity_factor: float = 1.0
+    moe_eval_capacity_factor: float = 1.0
+    moe_min_capacity: int = 4
+    moe_loss_coeff: float = 0.01
     rotary_base: float = 10000.0
     tie_embeddings: bool = True
 
@@ -168,12 +177,15 @@ def gpt_param_specs(cfg: GPTConfig, tp: int = 1, pp: int = 1, pp_rank: int = 0,
             ParamSpec(p + "proj_b", (h,), "zeros", weight_decay=False, unit=u, sp_reduce=sp),
         ]
         norm(p + "ln2", u)
-        specs += [
-            ParamSpec(p + "fc1_w", (f1l, h), std=std, unit=u, tp_duplicated=nd),
-            ParamSpec(p + "fc1_b", (f1l,), "zeros", weight_decay=False, unit=u, tp_duplicated=nd),
-            ParamSpec(p + "fc2_w", (h, fl), "scaled_normal", std=std, unit=u, tp_duplicated=nd),
-            ParamSpec(p + "fc2_b", (h,), "zeros", weight_decay=False, unit=u, sp_reduce=sp),
-        ]
+        if is_moe_layer(cfg, i):
+            specs.append(ParamSpec(p + "router_w", (cfg.num_experts, h), std=std, unit=u))
+        else:
+            specs += [
+                ParamSpec(p + "fc1_w", (f1l, h), std=std, unit=u, tp_duplicated=nd),
+                ParamSpec(p + "fc1_b", (f1l,), "zeros", weight_decay=False, unit=u, tp_duplicated=nd),
+                ParamSpec(p + "fc2_w", (h, fl), "scaled_normal", std=std, unit=u, tp_duplicated=nd),
+                ParamSpec(p + "fc2_b", (h,), "zeros", weight_decay=False, unit=u, sp_reduce=sp),
+            ]
         if i + 1 < l1:
             norm(f"layers.{i + 1}.ln1", u)
         elif last:
@@ -255,6 +267,12 @@ class StepRuntime:
     # the memory-bound backward kernels of the main stream (None: inline)
     wgrad_stream: Optional[object] = None
     _wgrad_live: bool = False
+    # MoE: this rank's experts (separate flat buffer), the EP group, aux-loss gradient
+    eparams: Optional[Dict[str, torch.Tensor]] = None
+    egrads: Optional[Dict[str, torch.Tensor]] = None
+    ep_group: Optional[object] = None
+    aux_scale: float = 0.0        # d(total loss)/d(l_aux of one layer) = coeff / micro-batches
+    aux_log: Optional[List] = None
 
     @property
     def p_drop(self):
@@ -430,20 +448,38 @@ class GPTLayerFn(torch.autograd.Function):
         h1, m, mean2, rstd2 = bda_norm_fwd(o, P[p + "proj_b"], h, w2, b2, eps, rt.p_drop, rt.seed_t,
                                            rt.salt(1000 + 2 * i), rt.rms)
         m_full = _gather(m, rt)
-        pre = torch.mm(m_full, P[p + "fc1_w"].t())
-        if cfg.swiglu:
-            f = bias_swiglu_fwd(pre, P[p + "fc1_b"])
+        moe = None
+        if is_moe_layer(cfg, i):
+            # MoE MLP under autograd: the inner graph is kept for backward (models/moe.py)
+            e = p + "experts."
+            leaves = [P[p + "router_w"]] + [rt.eparams[e + n] for n in ("fc1_w", "fc1_b", "fc2_w", "fc2_b")]
+            leaves = [t.detach().requires_grad_(True) for t in leaves]
+            m_leaf = m_full.detach().requires_grad_(True)
+            with torch.enable_grad():
+                g_moe, l_aux, _ = moe_mlp(m_leaf, *leaves, cfg, rt.ep_group, training=rt.training)
+            if rt.aux_log is not None:
+                rt.aux_log.append(l_aux.detach())
+            moe = (m_leaf, leaves, g_moe, l_aux)
+            g = g_moe.detach()
+            pre = f = None
+            b_fc2 = None
         else:
-            f = bias_gelu_fwd(pre, P[p + "fc1_b"])
-        g = _reduce(torch.mm(f, P[p + "fc2_w"].t()), rt)
+            pre = torch.mm(m_full, P[p + "fc1_w"].t())
+            if cfg.swiglu:
+                f = bias_swiglu_fwd(pre, P[p + "fc1_b"])
+            else:
+                f = bias_gelu_fwd(pre, P[p + "fc1_b"])
+            g = _reduce(torch.mm(f, P[p + "fc2_w"].t()), rt)
+            b_fc2 = P[p + "fc2_b"]
         if next_norm is not None:
             wn, bn = rt.norm_params(next_norm)
         else:  # stage boundary: plain bias-dropout-add; normalise into a throwaway
             wn, bn = P[p + "ln2_w"], P.get(p + "ln2_b")
-        h2, a2, mean_n, rstd_n = bda_norm_fwd(g, P[p + "fc2_b"], h1, wn, bn, eps, rt.p_drop,
+        h2, a2, mean_n, rstd_n = bda_norm_fwd(g, b_fc2, h1, wn, bn, eps, rt.p_drop,
                                               rt.seed_t, rt.salt(1001 + 2 * i), rt.rms)
         ctx.saved = (a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2, m_full, pre, f, h2, mean_n, rstd_n)
         ctx.rt, ctx.i, ctx.next_norm = rt, i, next_norm
+        ctx.moe = moe
         if next_norm is None:
             return h2, torch.empty(0, device=h2.device, dtype=h2.dtype)
         return h2, a2
@@ -466,15 +502,29 @@ class GPTLayerFn(torch.autograd.Function):
             gwn, gbn = rt.norm_grads(ctx.next_norm)
             dh1, dg = norm_bwd(da2.contiguous(), dh2, h2, mean_n, rstd_n, wn, want_dx=True,
                                p=rt.p_drop, seed_t=rt.seed_t, salt=rt.salt(1001 + 2 * i),
-                               rms=rt.rms, dgamma=gwn, dbeta=gbn, dbias=G[p + "fc2_b"],
+                               rms=rt.rms, dgamma=gwn, dbeta=gbn, dbias=G.get(p + "fc2_b"),
                                accumulate=True)
         else:
             wn = P[p + "ln2_w"]
             zero = torch.zeros_like(dh2)
             dh1, dg = norm_bwd(zero, dh2, h2, mean_n, rstd_n, wn, want_dx=True, p=rt.p_drop,
                                seed_t=rt.seed_t, salt=rt.salt(1001 + 2 * i), rms=rt.rms,
-                               dbias=G[p + "fc2_b"], accumulate=True)
+                               dbias=G.get(p + "fc2_b"), accumulate=True)
         # ---- MLP backward
+        if ctx.moe is not None:
+            m_leaf, leaves, g_moe, l_aux = ctx.moe
+            ctx.moe = None
+            outs, gos = [g_moe], [dg]
+            if rt.aux_scale:
+                outs.append(l_aux)
+                gos.append(torch.full_like(l_aux, rt.aux_scale))
+            grads = torch.autograd.grad(outs, [m_leaf] + leaves, gos)
+            e = p + "experts."
+            for gbuf, gr in zip([G[p + "router_w"]] + [rt.egrads[e + n] for n in ("fc1_w", "fc1_b", "fc2_w", "fc2_b")],
+                                grads[1:]):
+                gbuf.add_(gr.to(gbuf.dtype))
+            dm = grads[0].to(dg.dtype)
+            return GPTLayerFn._attn_backward(ctx, dm, dh1, a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2)
         dg_full = _gather(dg, rt)
         rt.wgrad(G[p + "fc2_w"], dg_full, f)
         df = torch.mm(dg_full, P[p + "fc2_w"])
@@ -485,6 +535,17 @@ class GPTLayerFn(torch.autograd.Function):
                                  inplace=True)
         rt.wgrad(G[p + "fc1_w"], dpre, m_full)
         dm = _reduce(torch.mm(dpre, P[p + "fc1_w"]), rt)
+        return GPTLayerFn._attn_backward(ctx, dm, dh1, a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2)
+
+    @staticmethod
+    def _attn_backward(ctx, dm, dh1, a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2):
+        rt, i = ctx.rt, ctx.i
+        cfg = rt.cfg
+        P, G = rt.params, rt.grads
+        p = f"layers.{i}."
+        D = cfg.head_dim
+        hl = cfg.num_attention_heads // rt.tp
+        kvl = cfg.num_kv_heads // rt.tp
         # ---- BDA-LN2 backward
         w2, _ = rt.norm_params(p + "ln2")
         gw2, gb2 = rt.norm_grads(p + "ln2")
@@ -551,14 +612,18 @@ class GPTStage:
     """The layers of one pipeline stage (all layers when pp == 1)."""
 
     def __init__(self, cfg: GPTConfig, params, grads, tp=1, tp_rank=0, tp_group=None, pp=1,
-                 pp_rank=0, sequence_parallel=False, seed_t=None, cp=1, cp_rank=0, cp_group=None):
+                 pp_rank=0, sequence_parallel=False, seed_t=None, cp=1, cp_rank=0, cp_group=None,
+                 eparams=None, egrads=None, ep_group=None):
         self.cfg = cfg
         self.l0, self.l1 = stage_layer_range(cfg, pp, pp_rank)
         self.first, self.last = pp_rank == 0, pp_rank == pp - 1
         V = cfg.padded_vocab(tp) // tp
         self.rt = StepRuntime(cfg=cfg, params=params, grads=grads, tp_group=tp_group, tp=tp,
                               tp_rank=tp_rank, sp=sequence_parallel and tp > 1, seed_t=seed_t,
-                              vocab_start=tp_rank * V, cp=cp, cp_rank=cp_rank, cp_group=cp_group)
+                              vocab_start=tp_rank * V, cp=cp, cp_rank=cp_rank, cp_group=cp_group,
+                              eparams=eparams, egrads=egrads, ep_group=ep_group)
+        if cfg.num_experts > 1:
+            assert tp == 1, "MoE layers run with tensor-parallel size 1 (expert parallelism instead)"
         if cp > 1:
             assert (cfg.num_attention_heads // tp) % cp == 0 and (cfg.num_kv_heads // tp) % cp == 0, \
                 "Ulysses needs the (per-TP-rank) query and KV head counts divisible by the cp size"

@@ -180,6 +180,41 @@ def initialize_model_parallel(tp: int = 1, pp: int = 1, sequence_parallel: bool 
     return st
 
 
+def make_expert_groups(st: ParallelState, ep: int):
+    """Expert parallelism over the gradient (dp x cp) group: consecutive blocks of ``ep``
+    replicas form an EP group (experts split E/ep per rank, tokens exchanged all-to-all);
+    replicas holding the same experts form the expert-data-parallel group.  Every rank
+    calls new_group for every group in the same order.  Returns (ep_group, edp_group,
+    ep_rank); groups are None when their size is 1."""
+    W = st.dp * st.cp
+    assert W % ep == 0, f"expert-parallel size {ep} must divide dp*cp = {W}"
+    tp, pp, dp, cp = st.tp, st.pp, st.dp, st.cp
+
+    def rank_of(p, d, t, c):
+        return ((p * dp + d) * cp + c) * tp + t
+
+    ep_group = edp_group = None
+    my_idx = None
+    for p in range(pp):
+        for t in range(tp):
+            members = [rank_of(p, d, t, c) for d in range(dp) for c in range(cp)]
+            if st.rank in members:
+                my_idx = members.index(st.rank)
+            if ep > 1:
+                for b in range(W // ep):
+                    ranks = members[b * ep:(b + 1) * ep]
+                    g = dist.new_group(ranks)
+                    if st.rank in ranks:
+                        ep_group = g
+            if W // ep > 1:
+                for j in range(ep):
+                    ranks = members[j::ep]
+                    g = dist.new_group(ranks)
+                    if st.rank in ranks:
+                        edp_group = g
+    return ep_group, edp_group, (my_idx or 0) % ep
+
+
 def destroy():
     global _STATE
     if dist.is_initialized():

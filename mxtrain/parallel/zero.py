@@ -58,12 +58,17 @@ class DistributedOptimizer:
                  weight_decay=0.01, clip_grad=1.0, overlap: bool = True, tp_rank: int = 0,
                  tp_group=None, sp_group=None, mp_group=None, embed_group=None,
                  pp_rank: int = 0, schedule: Optional[LRSchedule] = None,
-                 overlap_param_gather: Optional[bool] = None):
+                 overlap_param_gather: Optional[bool] = None,
+                 grad_scale_world: Optional[int] = None, norm_groups=()):
         self.flat = flat
         self.dp_group = dp_group
         self.world = dist.get_world_size(dp_group) if dp_group is not None else 1
         self.rank = dist.get_rank(dp_group) if dp_group is not None else 0
         self.betas, self.eps, self.wd, self.clip = betas, eps, weight_decay, clip_grad
+        # gradients are sum-reduced over dp_group and divided by gs_world (= the number of
+        # replicas whose losses are averaged; larger than dp_group for expert parameters)
+        self.gs_world = grad_scale_world or self.world
+        self.norm_groups = [g for g in norm_groups if g is not None]
         self.schedule = schedule or LRSchedule(lr)
         self.tp_group, self.sp_group, self.mp_group, self.embed_group = (
             tp_group, sp_group, mp_group, embed_group)
@@ -223,19 +228,22 @@ class DistributedOptimizer:
         h[optim_ops.H_WD] = self.wd
         h[optim_ops.H_BC1] = 1.0 - b1 ** t
         h[optim_ops.H_BC2] = 1.0 - b2 ** t
-        h[optim_ops.H_GS] = 1.0 / self.world
+        h[optim_ops.H_GS] = 1.0 / self.gs_world
         h[optim_ops.H_CLIP] = self.clip if self.clip else 0.0
         self.hyper.copy_(h, non_blocking=True)
         if self.device.type == "cuda" and not torch.cuda.is_current_stream_capturing():
             self._hyper_events[i] = torch.cuda.current_stream(self.device).record_event()
 
     def grad_norm_sq(self) -> torch.Tensor:
-        optim_ops.sumsq_bf16(self.grad_shard, 1.0 / self.world, out=self.normsq,
+        optim_ops.sumsq_bf16(self.grad_shard, 1.0 / self.gs_world, out=self.normsq,
                              flags=self.norm_flags)
         if self.world > 1:
             dist.all_reduce(self.normsq, group=self.dp_group)
         if self.mp_group is not None and dist.get_world_size(self.mp_group) > 1:
             dist.all_reduce(self.normsq, group=self.mp_group)
+        for g in self.norm_groups:
+            if dist.get_world_size(g) > 1:
+                dist.all_reduce(self.normsq, group=g)
         return self.normsq
 
     def step(self, lr: Optional[float] = None):
@@ -307,3 +315,31 @@ class DistributedOptimizer:
         if self.world > 1:
             for (b, fs, so, n) in self.slices:
                 self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n])
+
+
+def joint_update(opts: List["DistributedOptimizer"]) -> torch.Tensor:
+    """Optimizer body over several flat buffers (dense + MoE experts) that share ONE
+    gradient-clipping norm: finish every reduction, sum the squared norms, one fused
+    AdamW per buffer, then the parameter all-gathers.  Hyper-parameters must already be
+    set (set_hyper); no host synchronisation (capturable)."""
+    for o in opts:
+        o.finish_grads()
+    total = opts[0].grad_norm_sq()
+    for o in opts[1:]:
+        total.add_(o.grad_norm_sq())
+    for o in opts:
+        optim_ops.adamw_step(o.master, o.exp_avg, o.exp_avg_sq, o.grad_shard, o.param_shard,
+                             o.hyper, normsq=total, wd_flags=o.wd_flags)
+    for o in opts:
+        o.gather_params()
+    return total
+
+
+def joint_step(opts: List["DistributedOptimizer"], lr: Optional[float] = None) -> torch.Tensor:
+    for o in opts:
+        o.step_count += 1
+        o.set_hyper(lr if lr is not None else o.schedule(o.step_count))
+    total = joint_update(opts)
+    for o in opts:
+        o.reset_pending()
+    return total

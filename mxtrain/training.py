@@ -45,6 +45,7 @@ class TrainConfig:
     # weight-gradient GEMMs on a side HIP stream (GPU only).  Off by default: measured no
     # gain at GPT-2 345M (19.97 vs 19.81 ms/step) -- hipBLASLt tiles already occupy every CU
     wgrad_stream: bool = False
+    moe_expert_parallel_size: int = 1   # --moe-expert-parallel-size
 
 
 class GPTTrainer:
@@ -74,6 +75,9 @@ class GPTTrainer:
             self.stage.rt.wgrad_stream = torch.cuda.Stream(device=self.device)
         sched = LRSchedule(tcfg.lr, tcfg.min_lr, tcfg.lr_warmup_iters, tcfg.lr_decay_iters,
                            tcfg.lr_decay_style)
+        self.eflat = self.eopt = None
+        if cfg.num_experts > 1:
+            self._setup_moe(cfg, tcfg, ps, dtype, sched)
         self.opt = DistributedOptimizer(
             self.flat, dp_group=ps.grad_group if ps.grad_world > 1 else None, lr=tcfg.lr,
             betas=(tcfg.adam_beta1, tcfg.adam_beta2), eps=tcfg.adam_eps,
@@ -93,6 +97,32 @@ class GPTTrainer:
         self._static = None
 
     # ------------------------------------------------------------------ init
+    def _setup_moe(self, cfg, tcfg, ps, dtype, sched):
+        """Expert parameters: E/ep experts per rank in a second flat buffer with its own
+        ZeRO-1 optimizer over the expert-data-parallel group (models/moe.py)."""
+        from .models.gpt import stage_layer_range
+        from .models.moe import moe_param_specs
+        ep = tcfg.moe_expert_parallel_size
+        assert cfg.num_experts % ep == 0, "num_experts must be divisible by the EP size"
+        assert ps.pp == 1, "MoE runs with pipeline-parallel size 1 (use expert parallelism)"
+        self.ep_group, self.edp_group, self.ep_rank = pstate.make_expert_groups(ps, ep) \
+            if ps.world_size > 1 else (None, None, 0)
+        edp = ps.grad_world // ep
+        l0, l1 = stage_layer_range(cfg, ps.pp, ps.pp_rank)
+        especs = moe_param_specs(cfg, l0, l1, ep)
+        self.eflat = FlatParams(especs, self.device, dtype, dp_world=edp, bucket_numel=tcfg.bucket_numel)
+        # every EP rank initialises different experts; replicas of the same experts agree
+        gen = torch.Generator().manual_seed(tcfg.seed + 7777 + 31 * self.ep_rank + 1000 * ps.pp_rank)
+        self.eflat.initialize(gen, cfg.num_layers)
+        self.eopt = DistributedOptimizer(
+            self.eflat, dp_group=self.edp_group, lr=tcfg.lr, betas=(tcfg.adam_beta1, tcfg.adam_beta2),
+            eps=tcfg.adam_eps, weight_decay=tcfg.weight_decay, clip_grad=tcfg.clip_grad,
+            overlap=tcfg.overlap_grad_reduce, schedule=sched, grad_scale_world=ps.grad_world,
+            mp_group=ps.mp_group if ps.tp * ps.pp > 1 else None, norm_groups=(self.ep_group,))
+        rt = self.stage.rt
+        rt.eparams, rt.egrads, rt.ep_group = self.eflat.params, self.eflat.grads, self.ep_group
+        rt.aux_log = []
+
     def _setup_xgmi(self):
         """Build the direct-xGMI communicators (MXTRAIN_XGMI=1|auto) eagerly, in the same
         group order on every rank, so no handle exchange / autotune happens mid-step."""
@@ -116,9 +146,16 @@ class GPTTrainer:
                 dist.broadcast(self.flat.params[name], src=src, group=ps.embed_group)
 
     # ------------------------------------------------------------------ step
+    def _unit_done(self, unit):
+        self.opt.unit_done(unit)
+        self.eopt.unit_done(unit)
+
     def _micro_forward_backward(self, ids, labels, B, S, last_micro):
         rt = self.stage.rt
-        rt.unit_done = self.opt.unit_done if last_micro else None
+        if self.eopt is not None:
+            rt.unit_done = self._unit_done if last_micro else None
+        else:
+            rt.unit_done = self.opt.unit_done if last_micro else None
         loss = self.stage.forward(ids=ids, labels=labels, B=B, S=S)
         loss.backward()
         return loss.detach()
@@ -144,22 +181,35 @@ class GPTTrainer:
         if self._graph is not None:
             self._static[0].copy_(tokens)
             self._static[1].copy_(labels)
-            self.opt.step_count += 1   # bias corrections use the new step, as in eager step()
-            self.opt.set_hyper(self.opt.schedule(self.opt.step_count))
+            for o in self._opts:
+                o.step_count += 1   # bias corrections use the new step, as in eager step()
+                o.set_hyper(o.schedule(o.step_count))
             self._graph.replay()
             # the replay left this step's update un-gathered (the next replay's body, or a
             # sync_params(), gathers it; re-gathering an unchanged shard is idempotent)
-            self.opt.gather_pending = self.opt.overlap_param_gather
+            for o in self._opts:
+                o.gather_pending = o.overlap_param_gather
             self.iteration += 1
             return self._static_loss
         return self._train_step_eager(tokens, labels)
 
-    def _train_step_eager(self, tokens, labels):
-        nm, B, S = tokens.shape
+    @property
+    def _opts(self):
+        return [self.opt] + ([self.eopt] if self.eopt is not None else [])
+
+    def _prepare_step(self, nm, B, S):
         self._begin_step()
         self.flat.zero_grad()
+        if self.eflat is not None:
+            self.eflat.zero_grad()
+            self.stage.rt.aux_scale = self.cfg.moe_loss_coeff / nm
+            self.stage.rt.aux_log.clear()
         self.seed.advance()
         self.stage.rt.grad_scale = 1.0 / (nm * B * S)
+
+    def _train_step_eager(self, tokens, labels):
+        nm, B, S = tokens.shape
+        self._prepare_step(nm, B, S)
         if self.pipeline is not None:
             loss = self.pipeline.run(tokens, labels)
         else:
@@ -168,7 +218,11 @@ class GPTTrainer:
                 loss = loss + self._micro_forward_backward(tokens[m].reshape(-1),
                                                            labels[m].reshape(-1), B, S,
                                                            m == nm - 1)
-        self.opt.step()
+        if self.eopt is not None:
+            from .parallel.zero import joint_step
+            joint_step(self._opts)
+        else:
+            self.opt.step()
         self.iteration += 1
         return self._cp_mean(loss)
 
@@ -191,10 +245,11 @@ class GPTTrainer:
         g = torch.cuda.CUDAGraph()
         # the optimizer step counter / hyper-parameters are host-driven: set_hyper copies
         # from a pinned buffer that the captured memcpy re-reads on every replay
-        step0 = self.opt.step_count
+        step0 = [o.step_count for o in self._opts]
         with torch.cuda.graph(g, stream=s):
             loss = self._graph_body()
-        self.opt.step_count = step0
+        for o, c in zip(self._opts, step0):
+            o.step_count = c
         self._graph = g
         self._static_loss = loss
         return last
@@ -203,11 +258,9 @@ class GPTTrainer:
         tokens, labels = self._static
         nm, B, S = tokens.shape
         # the captured step starts by gathering the shards the previous replay updated
-        self.opt.gather_pending = self.opt.overlap_param_gather
-        self._begin_step()
-        self.flat.zero_grad()
-        self.seed.advance()
-        self.stage.rt.grad_scale = 1.0 / (nm * B * S)
+        for o in self._opts:
+            o.gather_pending = o.overlap_param_gather
+        self._prepare_step(nm, B, S)
         if self.pipeline is not None:
             loss = self.pipeline.run(tokens, labels)
         else:
@@ -217,25 +270,30 @@ class GPTTrainer:
                                                            labels[m].reshape(-1), B, S,
                                                            m == nm - 1)
         # optimizer body without host-side hyper update (done before each replay)
-        o = self.opt
-        o.finish_grads()
-        normsq = o.grad_norm_sq()
-        from .ops import optim as optim_ops
-        optim_ops.adamw_step(o.master, o.exp_avg, o.exp_avg_sq, o.grad_shard, o.param_shard,
-                             o.hyper, normsq=normsq, wd_flags=o.wd_flags)
-        o.gather_params()
-        o.gather_pending = False   # (overlap mode) the next replay's body gathers
-        o._gather_events.clear()
-        o.reset_pending()
+        from .parallel.zero import joint_update
+        joint_update(self._opts)
+        for o in self._opts:
+            o.gather_pending = False   # (overlap mode) the next replay's body gathers
+            o._gather_events.clear()
+            o.reset_pending()
         return self._cp_mean(loss)
 
+    def _wait_unit_all(self, unit):
+        for o in self._opts:
+            o.wait_unit(unit)
+
     def _begin_step(self):
-        self.opt.begin_param_gather()
-        self.stage.rt.before_unit = self.opt.wait_unit if self.opt.overlap_param_gather else None
+        for o in self._opts:
+            o.begin_param_gather()
+        if any(o.overlap_param_gather for o in self._opts):
+            self.stage.rt.before_unit = self._wait_unit_all if self.eopt is not None else self.opt.wait_unit
+        else:
+            self.stage.rt.before_unit = None
 
     def sync_params(self):
         """Complete a deferred parameter all-gather (call before reading parameters)."""
-        self.opt.finish_param_gather()
+        for o in self._opts:
+            o.finish_param_gather()
         self.stage.rt.before_unit = None
 
     @torch.no_grad()

@@ -54,6 +54,15 @@ def build_parser() -> argparse.ArgumentParser:
     a("--rotary-base", "--rope-theta", dest="rotary_base", type=float, default=10000.0)
     a("--untie-embeddings-and-output-weights", action="store_true")
     a("--swiglu", action="store_true")
+    # Megatron-DeepSpeed MoE
+    a("--num-experts", type=int, nargs="+", default=[1])
+    a("--expert-interval", type=int, default=2)
+    a("--topk", type=int, default=1)
+    a("--moe-expert-parallel-size", "--ep-world-size", dest="moe_expert_parallel_size", type=int, default=1)
+    a("--moe-train-capacity-factor", type=float, default=1.0)
+    a("--moe-eval-capacity-factor", type=float, default=1.0)
+    a("--moe-min-capacity", type=int, default=4)
+    a("--moe-loss-coeff", type=float, default=0.1)
     # training
     a("--micro-batch-size", type=int, default=4)
     a("--global-batch-size", type=int, default=None)

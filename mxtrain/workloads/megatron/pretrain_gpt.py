@@ -79,12 +79,17 @@ def main(argv=None):
                     position_embedding="rope" if args.position_embedding_type == "rope" else "learned",
                     rotary_percent=args.rotary_percent, rotary_base=args.rotary_base,
                     swiglu=args.swiglu,
+                    num_experts=max(args.num_experts), expert_interval=args.expert_interval,
+                    moe_topk=args.topk, moe_train_capacity_factor=args.moe_train_capacity_factor,
+                    moe_eval_capacity_factor=args.moe_eval_capacity_factor,
+                    moe_min_capacity=args.moe_min_capacity, moe_loss_coeff=args.moe_loss_coeff,
                     tie_embeddings=not args.untie_embeddings_and_output_weights)
     tcfg = TrainConfig(micro_batch_size=args.micro_batch_size, global_batch_size=args.global_batch_size,
                        lr=args.lr, min_lr=args.min_lr, lr_warmup_iters=args.lr_warmup_iters,
                        lr_decay_iters=args.lr_decay_iters, lr_decay_style=args.lr_decay_style,
                        weight_decay=args.weight_decay, adam_beta1=args.adam_beta1, adam_beta2=args.adam_beta2,
-                       adam_eps=args.adam_eps, clip_grad=args.clip_grad, seed=args.seed)
+                       adam_eps=args.adam_eps, clip_grad=args.clip_grad, seed=args.seed,
+                       moe_expert_parallel_size=args.moe_expert_parallel_size)
     t0 = time.time()
     trainer = GPTTrainer(cfg, tcfg, ps)
     print_rank_0(f"> GPT: {cfg.num_layers} layers, hidden {cfg.hidden_size}, heads {cfg.num_attention_heads}, "

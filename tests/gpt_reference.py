@@ -21,7 +21,7 @@ def rope_complex(x, rd, base):
     return torch.cat([z.real, z.imag, x[..., rd:]], -1)
 
 
-def ref_loss(P, ids, labels, cfg, B, S, head="wte"):
+def ref_loss(P, ids, labels, cfg, B, S, head="wte", mlp_hook=None):
     h = cfg.hidden_size
     nh = cfg.num_attention_heads
     D = h // nh
@@ -56,6 +56,9 @@ def ref_loss(P, ids, labels, cfg, B, S, head="wte"):
         ctx = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * S, h)
         x = x + ctx @ P[p + "proj_w"].t() + P[p + "proj_b"]
         m = ln(x, p + "ln2")
+        if mlp_hook is not None and (p + "router_w") in P:
+            x = x + mlp_hook(m, i)
+            continue
         pre = m @ P[p + "fc1_w"].t() + P[p + "fc1_b"]
         if getattr(cfg, "swiglu", False):
             a_, b_ = pre.chunk(2, dim=-1)
