@@ -360,7 +360,12 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(
 //            16 d-columns) -> fp32 LDS image                                   | barrier
 //   phase C  row-contiguous fp32 atomics of the dQ image (one 256-B wave-instruction
 //            per row, the full-rate atomic shape) + staging of the next Q/dO tile | barrier
-template <int D, bool CAUSAL>
+// DP (D-pass): 0 = whole head dim in one pass (D = 64).  D = 128 keeps dK^T/dV^T for all
+// 128 columns + K/V rows + Q/dO fragments = ~370 live VGPRs at 2 waves/SIMD (256 max:
+// ~100 spilled to scratch, 7.5x the forward time), so it runs as two passes that each
+// accumulate half of the dK/dV columns: DP = 1 (columns 0-63, plus dQ), DP = 2 (columns
+// 64-127, S and dP recomputed, no dQ).  1.4x the MFMA work, no scratch traffic.
+template <int D, bool CAUSAL, int DP = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, int ldq, int ldk, int ldv,
@@ -369,6 +374,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, int lddk, int lddv, int S, int Hq,
     int Hkv, const int* __restrict__ klen, float c, float scale) {
   constexpr int KB = 128, KW = 256, QT = 32, NKK = D / 16, NDT = D / 32;
+  constexpr int NDL = DP == 0 ? NDT : NDT / 2;      // dK/dV column tiles of this pass
+  constexpr int DT0 = DP == 2 ? NDT / 2 : 0;        // first column tile of this pass
+  constexpr bool DO_DQ = DP != 2;
   constexpr int KTILE = KW * D * 2;  // bytes
   constexpr int QTILE = QT * D * 2;
   constexpr int CPR = D / 8;
@@ -407,14 +415,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int key = kw0 + r;                 // this lane's key (column of S / dP)
   const bool key_ok = half_on && key < kl;
 
-  bf16x8 kf[NKK], vf[NKK];
+  // D = 128: the lane's K row is NOT kept in registers (it is read back from the K tile
+  // in LDS per use) and Q/dO rows are read per MFMA step -- keeping all of them resident
+  // (kf + vf + qr + orr = 128 VGPRs next to 128 accumulator VGPRs) spilled ~170 VGPRs.
+  constexpr bool KREG = D <= 64;
+  bf16x8 kf[KREG ? NKK : 1], vf[NKK];
   {
     const bool in = half_on && key < S;
     const uint16_t* kp = k + (size_t)(b * S + key) * ldk + hk * D + 8 * hh;
     const uint16_t* vp = v + (size_t)(b * S + key) * ldv + hk * D + 8 * hh;
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
-      kf[kk] = in ? ld8(kp + 16 * kk) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if constexpr (KREG) kf[kk] = in ? ld8(kp + 16 * kk) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       vf[kk] = in ? ld8(vp + 16 * kk) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   }
@@ -431,9 +443,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     *reinterpret_cast<uint4*>(smem + OFF_K + toff_k<D>(row, ch)) = val;
   }
 
-  f32x16 dvacc[NDT], dkacc[NDT];
+  f32x16 dvacc[NDL], dkacc[NDL];
 #pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) { dvacc[dt] = f32x16{}; dkacc[dt] = f32x16{}; }
+  for (int dt = 0; dt < NDL; ++dt) { dvacc[dt] = f32x16{}; dkacc[dt] = f32x16{}; }
 
   const int nqt = (S + QT - 1) / QT;
   const int first_kb = CAUSAL ? pair : 2 * pair;
@@ -509,16 +521,32 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         sacc[e] = Ls[ql];
         dpacc[e] = DLs[ql];
       }
-      bf16x8 qr[NKK], orr[NKK];  // batch the row reads ahead of the MFMAs
+      if constexpr (KREG) {
+        bf16x8 qr[NKK], orr[NKK];  // batch the row reads ahead of the MFMAs
 #pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        qr[kk] = lds8(Qt, toff<D>(r, 2 * kk + hh));
-        orr[kk] = lds8(Ot, toff<D>(r, 2 * kk + hh));
-      }
+        for (int kk = 0; kk < NKK; ++kk) {
+          qr[kk] = lds8(Qt, toff<D>(r, 2 * kk + hh));
+          orr[kk] = lds8(Ot, toff<D>(r, 2 * kk + hh));
+        }
 #pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        sacc = mfma32(qr[kk], kf[kk], sacc);
-        dpacc = mfma32(orr[kk], vf[kk], dpacc);
+        for (int kk = 0; kk < NKK; ++kk) {
+          sacc = mfma32(qr[kk], kf[kk], sacc);
+          dpacc = mfma32(orr[kk], vf[kk], dpacc);
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < NKK; kk += 2) {   // two steps of row reads in flight
+          const bf16x8 q0 = lds8(Qt, toff<D>(r, 2 * kk + hh));
+          const bf16x8 o0 = lds8(Ot, toff<D>(r, 2 * kk + hh));
+          const bf16x8 k0 = lds8(smem + OFF_K, toff_k<D>(krow, 2 * kk + hh));
+          const bf16x8 q1 = lds8(Qt, toff<D>(r, 2 * kk + 2 + hh));
+          const bf16x8 o1 = lds8(Ot, toff<D>(r, 2 * kk + 2 + hh));
+          const bf16x8 k1 = lds8(smem + OFF_K, toff_k<D>(krow, 2 * kk + 2 + hh));
+          sacc = mfma32(q0, k0, sacc);
+          dpacc = mfma32(o0, vf[kk], dpacc);
+          sacc = mfma32(q1, k1, sacc);
+          dpacc = mfma32(o1, vf[kk + 1], dpacc);
+        }
       }
 #pragma unroll
       for (int e = 0; e < 16; ++e) sacc[e] = __builtin_amdgcn_exp2f(c * sacc[e]);
@@ -536,14 +564,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const float p = sacc[e];
         dpacc[e] = p * dpacc[e];
       }
-#pragma unroll
+      constexpr int SUNROLL = D <= 64 ? 2 : 1;   // D=128: don't hoist both halves' reads
+#pragma unroll SUNROLL
       for (int s = 0; s < 2; ++s) {
         const bf16x8 pb = pack_acc8(sacc, 8 * s);
         const bf16x8 db = pack_acc8(dpacc, 8 * s);
         const int row0 = 16 * s + 4 * hh + (gi >> 2);
 #pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-          const int col = 32 * dt + 16 * (g & 1) + 4 * (gi & 3);
+        for (int dt = 0; dt < NDL; ++dt) {
+          const int col = 32 * (dt + DT0) + 16 * (g & 1) + 4 * (gi & 3);
           const int within = (col & 7) * 2;
           const bf16x8 dot = cat(tr_read(Ot, toff<D>(row0, col >> 3) + within),
                                  tr_read(Ot, toff<D>(row0 + 8, col >> 3) + within));
@@ -554,14 +583,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
       }
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
+      for (int g4 = 0; g4 < (DO_DQ ? 4 : 0); ++g4) {
         const int ql = 8 * g4 + 4 * hh;
         uint2 u;
         u.x = pack2(dpacc[4 * g4 + 0], dpacc[4 * g4 + 1]);
         u.y = pack2(dpacc[4 * g4 + 2], dpacc[4 * g4 + 3]);
         *reinterpret_cast<uint2*>(dsimg + ds_off(krow, ql * 2)) = u;
       }
-    } else {
+    } else if (DO_DQ) {
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int ql = 8 * g4 + 4 * hh;
@@ -570,7 +599,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     __syncthreads();
     // ---------------- phase B: dQ[q][d] = sum over 256 keys dS[q][key] K[key][d]
-    {
+    if constexpr (DO_DQ) {
       const int qtile = w & 1;
       f32x4 dq[DQT];
 #pragma unroll
@@ -603,7 +632,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // ---------------- phase C: next-tile staging FIRST (its vmcnt wait must not cover the
     // atomics), then row-contiguous fp32 atomics that stay in flight across the barrier
     if (it + 1 < total) swrite((it + 1) & 1);
-    {
+    if constexpr (DO_DQ) {
       constexpr int RPW = QT / 8;       // rows per wave
       constexpr int IPR = D / 64;       // 64-lane instructions per row
       float vals[RPW][IPR];
@@ -629,10 +658,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     uint16_t* dkp = dk + (size_t)(b * S + key) * lddk + hk * D;
     uint16_t* dvp = dv + (size_t)(b * S + key) * lddv + hk * D;
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
+    for (int dt = 0; dt < NDL; ++dt)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = 32 * dt + 8 * g4 + 4 * hh;
+        const int d = 32 * (dt + DT0) + 8 * g4 + 4 * hh;
         uint2 u;
         u.x = pack2(dkacc[dt][4 * g4 + 0] * scale, dkacc[dt][4 * g4 + 1] * scale);
         u.y = pack2(dkacc[dt][4 * g4 + 2] * scale, dkacc[dt][4 * g4 + 3] * scale);
@@ -680,14 +709,18 @@ hipError_t bwd_dispatch(bool causal, dim3 grid, hipStream_t s, const uint16_t* q
                         const uint16_t* dout, int lddo, const float* lse, const float* delta,
                         float* dq_acc, int lddq, uint16_t* dk, uint16_t* dv, int lddk, int lddv,
                         int S, int Hq, int Hkv, const int* klen, float c, float scale) {
-  if (causal)
-    hipLaunchKernelGGL((attn_bwd_kernel<D, true>), grid, dim3(512), 0, s, q, k, v, ldq, ldk,
-                       ldv, dout, lddo, lse, delta, dq_acc, lddq, dk, dv, lddk, lddv, S, Hq, Hkv,
-                       klen, c, scale);
-  else
-    hipLaunchKernelGGL((attn_bwd_kernel<D, false>), grid, dim3(512), 0, s, q, k, v, ldq, ldk,
-                       ldv, dout, lddo, lse, delta, dq_acc, lddq, dk, dv, lddk, lddv, S, Hq, Hkv,
-                       klen, c, scale);
+#define MX_ATTN_BWD(C, P)                                                                  \
+  hipLaunchKernelGGL((attn_bwd_kernel<D, C, P>), grid, dim3(512), 0, s, q, k, v, ldq, ldk, ldv, \
+                     dout, lddo, lse, delta, dq_acc, lddq, dk, dv, lddk, lddv, S, Hq, Hkv, klen, \
+                     c, scale)
+  if constexpr (D <= 64) {
+    if (causal) MX_ATTN_BWD(true, 0);
+    else MX_ATTN_BWD(false, 0);
+  } else {
+    if (causal) { MX_ATTN_BWD(true, 1); MX_ATTN_BWD(true, 2); }
+    else { MX_ATTN_BWD(false, 1); MX_ATTN_BWD(false, 2); }
+  }
+#undef MX_ATTN_BWD
   return hipGetLastError();
 }
 

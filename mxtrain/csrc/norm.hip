@@ -120,7 +120,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
 // REG (cols <= 2048): each lane keeps its columns' running sums in registers across all
 // rows it handles; the 4 waves fold them into the block's LDS slab once at the end
 // (4-way LDS atomics, once per column).  Wider rows use per-row LDS atomics.
-template <int NV, bool RMS, bool REG>
+// COLS=false: row-wise part only (dh, dx); the column sums of wide rows come from
+// ln_bwd_cols_kernel instead (per-element LDS atomics made cols >= 2560 ~10x slower).
+template <int NV, bool RMS, bool REG, bool COLS = true>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dres,
     const uint16_t* __restrict__ h, const float* __restrict__ mean_in,
@@ -129,7 +131,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     float* __restrict__ partial, int rows, int cols, uint32_t thresh, float keep_scale,
     const uint32_t* __restrict__ seed_ptr, uint32_t salt) {
   extern __shared__ __attribute__((aligned(16))) float slab[];  // [3][cols]
-  if constexpr (!REG) {  // REG: [4 waves][3][cols] slabs, fully overwritten -> no zeroing
+  if constexpr (!REG && COLS) {  // REG: [4 waves][3][cols] slabs, fully overwritten -> no zeroing
     for (int i = threadIdx.x; i < 3 * cols; i += blockDim.x) slab[i] = 0.f;
     __syncthreads();
   }
@@ -174,7 +176,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
           if constexpr (REG) {
             ag[i][j] += dv[j] * xh[i][j];
             ab[i][j] += dv[j];
-          } else {
+          } else if constexpr (COLS) {
             atomicAdd(&slab[c + j], dv[j] * xh[i][j]);
             atomicAdd(&slab[cols + c + j], dv[j]);
           }
@@ -209,17 +211,20 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
           }
           uint4 pk = pack8(dx);
           *reinterpret_cast<uint4*>(dx_drop + base + c) = pk;
-          float dxr[8];
-          unpack8(pk, dxr);
+          if constexpr (COLS) {
+            float dxr[8];
+            unpack8(pk, dxr);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            if constexpr (REG) ax[i][j] += dxr[j];
-            else atomicAdd(&slab[2 * cols + c + j], dxr[j]);
+            for (int j = 0; j < 8; ++j) {
+              if constexpr (REG) ax[i][j] += dxr[j];
+              else atomicAdd(&slab[2 * cols + c + j], dxr[j]);
+            }
           }
         }
       }
     }
   }
+  if constexpr (!COLS) return;
   float* out = partial + (size_t)blockIdx.x * 3 * cols;
   if constexpr (REG) {
     // every wave stores its register partials into its OWN slab with plain 16-B LDS
@@ -338,6 +343,52 @@ hipError_t launch_fwd(const void* x, const void* bias, const void* residual,
   return hipGetLastError();
 }
 
+// Column sums of the LN backward for wide rows: partial[blk.y][0|1|2][c] over the
+// block's row stripe of  dy * xhat,  dy,  dx  (xhat recomputed from h, mean, rstd; dx
+// re-read in bf16, exactly the values written).  Lane = 8 consecutive columns, 16-B loads.
+template <bool RMS>
+__global__ __launch_bounds__(256) void ln_bwd_cols_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ h,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const uint16_t* __restrict__ dx, float* __restrict__ partial, int rows, int cols,
+    int rows_per_block) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= cols) return;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  float ag[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ab[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float ax[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = r0; r < r1; ++r) {
+    const size_t off = (size_t)r * cols + c;
+    const float mean = RMS ? 0.f : mean_in[r];
+    const float rstd = rstd_in[r];
+    float hv[8], dv[8];
+    unpack8(*reinterpret_cast<const uint4*>(h + off), hv);
+    unpack8(*reinterpret_cast<const uint4*>(dy + off), dv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ag[j] += dv[j] * ((hv[j] - mean) * rstd);
+      ab[j] += dv[j];
+    }
+    if (dx) {
+      float xv[8];
+      unpack8(*reinterpret_cast<const uint4*>(dx + off), xv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ax[j] += xv[j];
+    }
+  }
+  float* out = partial + (size_t)blockIdx.y * 3 * cols;
+#pragma unroll
+  for (int j = 0; j < 8; j += 4) {
+    *reinterpret_cast<float4*>(out + c + j) = make_float4(ag[j], ag[j + 1], ag[j + 2], ag[j + 3]);
+    *reinterpret_cast<float4*>(out + cols + c + j) = make_float4(ab[j], ab[j + 1], ab[j + 2], ab[j + 3]);
+    *reinterpret_cast<float4*>(out + 2 * cols + c + j) = make_float4(ax[j], ax[j + 1], ax[j + 2], ax[j + 3]);
+  }
+}
+
+constexpr int kSplitCols = 2048;   // wider rows: row kernel without column sums + column kernel
+constexpr int kColsRowsPerBlock = 32;
+
 int bwd_grid(int rows) {
   int g = (rows + 7) / 8;  // 2 rows per wave
   if (g > 512) g = 512;
@@ -354,6 +405,30 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
   const uint32_t thresh = p > 0.f ? (uint32_t)((double)p * 4294967296.0) : 0u;
   const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
   dim3 grid(bwd_grid(rows)), block(256);
+  if (cols > kSplitCols) {
+    // row-wise pass (no LDS), then the column sums in a column-parallel pass
+#define MX_LNB_SPLIT(N)                                                                \
+  case N:                                                                              \
+    hipLaunchKernelGGL((ln_bwd_kernel<N, RMS, false, false>), grid, block, 0, s,       \
+                       (const uint16_t*)dy, (const uint16_t*)dres, (const uint16_t*)h, \
+                       mean, rstd, (const uint16_t*)gamma, (uint16_t*)dh_out,          \
+                       (uint16_t*)dx_drop, partial, rows, cols, thresh, ks, seed,      \
+                       salt);                                                          \
+    break;
+    switch (nv) {
+      MX_LNB_SPLIT(5) MX_LNB_SPLIT(6) MX_LNB_SPLIT(8) MX_LNB_SPLIT(10) MX_LNB_SPLIT(12)
+      MX_LNB_SPLIT(16)
+      default: return hipErrorInvalidValue;
+    }
+#undef MX_LNB_SPLIT
+    if (partial) {
+      dim3 cg((cols / 8 + 255) / 256, (rows + kColsRowsPerBlock - 1) / kColsRowsPerBlock);
+      hipLaunchKernelGGL(ln_bwd_cols_kernel<RMS>, cg, dim3(256), 0, s, (const uint16_t*)dy,
+                         (const uint16_t*)h, mean, rstd, (const uint16_t*)dx_drop, partial, rows,
+                         cols, kColsRowsPerBlock);
+    }
+    return hipGetLastError();
+  }
   const size_t lds = (size_t)(nv <= 4 ? 12 : 3) * cols * sizeof(float);
 #define MX_LNB_CASE(N)                                                                 \
   case N:                                                                              \
@@ -376,6 +451,9 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
 
 // number of partial slabs the norm backward writes (caller sizes `partial`)
 MX_EXPORT int mx_norm_bwd_nparts(int rows) { return bwd_grid(rows); }
+MX_EXPORT int mx_norm_bwd_nparts2(int rows, int cols) {
+  return cols > kSplitCols ? (rows + kColsRowsPerBlock - 1) / kColsRowsPerBlock : bwd_grid(rows);
+}
 // floats of level-1 scratch needed to finalize P partial rows of C columns
 MX_EXPORT int64_t mx_colreduce_scratch(int P, int C) { return (int64_t)((P + 63) / 64) * C; }
 

@@ -119,7 +119,7 @@ def norm_bwd(dy, dres, h, mean, rstd, gamma, want_dx=False, p=0.0, seed_t=None, 
                 else:
                     buf.copy_(val.to(buf.dtype))
         return dh, dx
-    nparts = _lib.query("mx_norm_bwd_nparts", rows)
+    nparts = _lib.query("mx_norm_bwd_nparts2", rows, cols)
     scratch_n = _lib.query64("mx_colreduce_scratch", nparts, 3 * cols)
     partial = torch.empty(nparts * 3 * cols + scratch_n, dtype=torch.float32, device=dy.device)
     dh = torch.empty_like(dy)

@@ -71,6 +71,30 @@ def main():
                                                          dq=dqkv[:, :h], dk=dqkv[:, h:2 * h],
                                                          dv=dqkv[:, 2 * h:])), flops=2.5 * fl)
         rec("attn_fwd full", timeit(lambda: A.attn_fwd(q, k, v, B, S, H, H, D, False)), flops=2 * fl)
+    if want("attn128"):   # GPT-3 6.7B shapes: B=2, S=2048, H=32, D=128
+        B2, S2, H2, D2 = 2, 2048, 32, 128
+        T2, h2 = B2 * S2, H2 * D2
+        qkv = torch.randn(T2, 3 * h2, device=dev).to(bf)
+        q, k, v = qkv[:, :h2], qkv[:, h2:2 * h2], qkv[:, 2 * h2:]
+        fl = 4 * B2 * H2 * S2 * S2 * D2 / 2
+        o, lse = A.attn_fwd(q, k, v, B2, S2, H2, H2, D2, True)
+        rec("attn128_fwd causal", timeit(lambda: A.attn_fwd(q, k, v, B2, S2, H2, H2, D2, True)), flops=fl)
+        do = torch.randn(T2, h2, device=dev).to(bf)
+        dqkv = torch.empty_like(qkv)
+        rec("attn128_bwd causal", timeit(lambda: A.attn_bwd(do, q, k, v, o, lse, B2, S2, H2, H2, D2, True,
+                                                            dq=dqkv[:, :h2], dk=dqkv[:, h2:2 * h2],
+                                                            dv=dqkv[:, 2 * h2:])), flops=2.5 * fl)
+    if want("norm4096"):
+        rows, cols = 4096, 4096
+        x = torch.randn(rows, cols, device=dev).to(bf)
+        g = torch.ones(cols, device=dev, dtype=bf)
+        bb = torch.zeros(cols, device=dev, dtype=bf)
+        seed = torch.tensor([1], dtype=torch.int32, device=dev)
+        hh_, y_, mean_, rstd_ = N.bda_norm_fwd(x, bb, x, g, bb, p=0.1, seed_t=seed)
+        dg, db, dbi = (torch.zeros(cols, device=dev, dtype=bf) for _ in range(3))
+        rec("ln_bwd 4096x4096 (bda)", timeit(lambda: N.norm_bwd(x, x, hh_, mean_, rstd_, g, want_dx=True, p=0.1,
+                                                                 seed_t=seed, dgamma=dg, dbeta=db, dbias=dbi,
+                                                                 accumulate=True)), rows * cols * 2 * 5)
     if want("norm"):
         x = torch.randn(T, h, device=dev).to(bf)
         r_ = torch.randn(T, h, device=dev).to(bf)

@@ -38,7 +38,7 @@ def _seed():
     assert torch.cuda.is_available()
 
 
-@pytest.mark.parametrize("cols", [768, 1024, 4096])
+@pytest.mark.parametrize("cols", [768, 1024, 4096, 8192])
 def test_layernorm_fwd_bwd(cols):
     rows = 512
     x = _bf(torch.randn(rows, cols))
@@ -60,9 +60,9 @@ def test_layernorm_fwd_bwd(cols):
     _close(db, dbr, 0.5, 2e-2, "dbeta")
 
 
-@pytest.mark.parametrize("rms", [False, True])
-def test_bda_norm_with_dropout(rms):
-    rows, cols = 256, 1024
+@pytest.mark.parametrize("rms,cols", [(False, 1024), (True, 1024), (False, 4096), (True, 5120)])
+def test_bda_norm_with_dropout(rms, cols):
+    rows = 256
     x = _bf(torch.randn(rows, cols))
     bias = _bf(0.1 * torch.randn(cols))
     res = _bf(torch.randn(rows, cols))
