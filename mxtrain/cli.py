@@ -33,8 +33,14 @@ def _add_values(p):
 
 
 def cmd_install(a):
+    from .obs.profile import debug_env, profile_env
+    launch_env = {}
+    if a.profile:
+        launch_env.update(profile_env("torch", a.profile_steps))
+    if a.debug_mode:
+        launch_env.update(debug_env())
     st = rel.install(a.chart, a.release, a.namespace, a.values, a.set, a.set_string, wait=a.wait,
-                     timeout=a.timeout)
+                     timeout=a.timeout, launch_env=launch_env or None)
     if a.debug:
         print(open(os.path.join(rel.release_dir(a.release, a.namespace), "manifest.yaml")).read())
     print(f"NAME: {a.release}\nNAMESPACE: {a.namespace}\nSTATUS: {st.get('phase')}")
@@ -206,7 +212,14 @@ def build_parser():
     _add_values(q)
     q.add_argument("--wait", action="store_true", help="run in the foreground until the jobs finish")
     q.add_argument("--timeout", type=float, default=None)
-    q.add_argument("--debug", action="store_true")
+    q.add_argument("--debug", action="store_true", help="print the rendered manifest (helm --debug)")
+    q.add_argument("--profile", action="store_true",
+                   help="torch.profiler (ROCm) trace + kernel table of a step window per rank into "
+                        "$HOME/logs/<pod>/profile")
+    q.add_argument("--profile-steps", default="5:8")
+    q.add_argument("--debug-mode", action="store_true",
+                   help="serialised kernels, synchronous HIP errors, TORCH_DISTRIBUTED_DEBUG=DETAIL, "
+                        "NCCL_DEBUG=INFO, per-step inf/nan checks")
     q.set_defaults(fn=cmd_install)
     q = sp.add_parser("uninstall")
     q.add_argument("release")

@@ -386,7 +386,7 @@ __global__ __launch_bounds__(256) void ln_bwd_cols_kernel(
   }
 }
 
-constexpr int kSplitCols = 2048;   // wider rows: row kernel without column sums + column kernel
+int kSplitCols = 2048;   // wider rows: row kernel without column sums + column kernel
 constexpr int kColsRowsPerBlock = 32;
 
 int bwd_grid(int rows) {
@@ -416,6 +416,7 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
                        salt);                                                          \
     break;
     switch (nv) {
+      MX_LNB_SPLIT(1) MX_LNB_SPLIT(2) MX_LNB_SPLIT(3) MX_LNB_SPLIT(4)
       MX_LNB_SPLIT(5) MX_LNB_SPLIT(6) MX_LNB_SPLIT(8) MX_LNB_SPLIT(10) MX_LNB_SPLIT(12)
       MX_LNB_SPLIT(16)
       default: return hipErrorInvalidValue;
@@ -451,6 +452,12 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
 
 // number of partial slabs the norm backward writes (caller sizes `partial`)
 MX_EXPORT int mx_norm_bwd_nparts(int rows) { return bwd_grid(rows); }
+// rows wider than this use the split (row + column) backward; returns the old value
+MX_EXPORT int mx_norm_split_cols(int c) {
+  const int old = kSplitCols;
+  if (c > 0) kSplitCols = c;
+  return old;
+}
 MX_EXPORT int mx_norm_bwd_nparts2(int rows, int cols) {
   return cols > kSplitCols ? (rows + kColsRowsPerBlock - 1) / kColsRowsPerBlock : bwd_grid(rows);
 }

@@ -188,6 +188,11 @@ def build_pod(name: str, pod_template: dict, reldir: str, cm_dirs: Dict[str, str
     for k, v in container_env(c).items():
         # env values may reference earlier variables with $(VAR), as in a pod spec
         env[k] = plan.rewrite(expand_k8s_vars(v, env))
+    # release-wide launch options (mxtrain install --profile / --debug-mode)
+    le = os.path.join(reldir, "launch_env.json")
+    if os.path.exists(le):
+        with open(le) as f:
+            env.update({k: str(v) for k, v in json.load(f).items()})
     env.update(extra_env)
     env["HOSTNAME"] = name
     env["MXTRAIN_POD_NAME"] = name

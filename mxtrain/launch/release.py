@@ -23,7 +23,7 @@ import signal
 import subprocess
 import sys
 import time
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 import yaml
 
@@ -77,7 +77,9 @@ def list_releases(namespace: Optional[str] = None) -> List[dict]:
 # ---------------------------------------------------------------------------- install
 def install(chart_path: str, name: str, namespace: str = DEFAULT_NS, value_files: List[str] = (),
             sets: List[str] = (), set_strings: List[str] = (), wait: bool = False,
-            timeout: Optional[float] = None) -> dict:
+            timeout: Optional[float] = None, launch_env: Optional[Dict[str, str]] = None) -> dict:
+    """Render the chart and start (or, with ``wait``, run) the release.  ``launch_env`` is
+    added to every replica's environment (profiling / debug modes, see obs/profile.py)."""
     reldir = release_dir(name, namespace)
     if os.path.exists(os.path.join(reldir, "status.json")):
         st = read_status(name, namespace)
@@ -91,6 +93,8 @@ def install(chart_path: str, name: str, namespace: str = DEFAULT_NS, value_files
         f.write(rendered.text)
     with open(os.path.join(reldir, "values.yaml"), "w") as f:
         yaml.safe_dump(rendered.values, f, sort_keys=False)
+    if launch_env:
+        _write_json(os.path.join(reldir, "launch_env.json"), dict(launch_env))
     _write_json(os.path.join(reldir, "chart.json"),
                 {"chart": os.path.abspath(chart_path), "chart_name": chart.name,
                  "version": chart.meta.get("version"), "values": [os.path.abspath(v) for v in value_files],

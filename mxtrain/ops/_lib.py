@@ -30,6 +30,7 @@ SIGNATURES = {
     # norm.hip
     "mx_norm_bwd_nparts": [I],
     "mx_norm_bwd_nparts2": [I, I],
+    "mx_norm_split_cols": [I],
     "mx_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],
     "mx_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
     "mx_bda_norm_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, F, P, U32, I, P],

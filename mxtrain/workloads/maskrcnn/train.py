@@ -243,6 +243,9 @@ def main(argv=None):
 
     # ---------------------------------------------------------------- training
     tbw = None
+    from mxtrain.obs.profile import StepProfiler, check_finite, check_finite_enabled
+    prof = StepProfiler(rank, out_dir=os.path.join(args.logdir, "profile") if os.environ.get("MXTRAIN_PROFILE") else None)
+    debug_finite = check_finite_enabled()
     train_sets = [COCODetection(cfg.DATA.BASEDIR, n, training=True) for n in cfg.DATA.TRAIN]
     ds = DetectionDataset(train_sets[0], short, max_size, training=True, with_masks=bool(cfg.MODE_MASK), seed=rank)
     bs = int(cfg.TRAIN.BATCH_SIZE_PER_GPU)
@@ -302,6 +305,9 @@ def main(argv=None):
                 torch.nn.utils.clip_grad_norm_(params, clip)
             opt.step()
             step += 1
+            prof.step(step)
+            if debug_finite:
+                check_finite(step, total_loss=losses["total_loss"])
             if step == args.mx_warmup_steps:
                 if device.type == "cuda":
                     torch.cuda.synchronize()

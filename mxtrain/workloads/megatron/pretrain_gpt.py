@@ -137,7 +137,10 @@ def main(argv=None):
         tb = SummaryWriter(args.tensorboard_dir)
     fault = FaultInjector(ps.rank)
     watchdog = Watchdog(os.path.join(logs_dir, "heartbeat"), ps.rank, args.mx_watchdog)
-    profiler = None
+    from mxtrain.obs.profile import StepProfiler, check_finite, check_finite_enabled
+    profiler = StepProfiler(ps.rank, out_dir=os.path.join(logs_dir, "profile") if args.mx_profile else None,
+                            mode="torch" if args.mx_profile else None)
+    debug_finite = check_finite_enabled()
 
     # ---------------------------------------------------------------- train loop
     it = trainer.iteration
@@ -158,18 +161,11 @@ def main(argv=None):
             graph_ready = True
         else:
             loss = None
-        if args.mx_profile and it == 5 and profiler is None:
-            profiler = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
-                                                          torch.profiler.ProfilerActivity.CUDA])
-            profiler.__enter__()
         if loss is None:
             loss = trainer.train_step(tokens, labels)
-        if profiler is not None and it == 7:
-            profiler.__exit__(None, None, None)
-            pdir = os.path.join(logs_dir, "profile")
-            os.makedirs(pdir, exist_ok=True)
-            profiler.export_chrome_trace(os.path.join(pdir, f"trace-rank{ps.rank}.json"))
-            profiler = None
+        profiler.step(it + 1)
+        if debug_finite:
+            check_finite(it + 1, loss=loss, grad_norm_sq=trainer.opt.normsq)
         it += 1
         loss_acc += loss
         watchdog.beat(it)

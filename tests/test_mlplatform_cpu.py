@@ -172,3 +172,35 @@ def test_node_init_stage_export_and_images(home, tmp_path, monkeypatch):
     assert images.set_image("reg/mxtrain:rocm", [str(vf.parent)], match="megatron") == [str(vf)]
     txt = vf.read_text()
     assert "image: 'reg/mxtrain:rocm'  # pinned" in txt and "- image: other/img" in txt and "{{ .Values.x }}" in txt
+
+
+def test_profile_and_debug_modes_reach_replicas(home, tmp_path):
+    """mxtrain install --profile / --debug-mode: launch env in every replica, and the
+    step profiler writes a trace + kernel table for its window."""
+    import subprocess
+    import sys
+    v = home / "v.yaml"
+    v.write_text(yaml.safe_dump({"train": {"env": [{"name": "HOME", "value": str(home / "h")}],
+                                           "command": ["python3", "-c"],
+                                           "args": ["\"import os; print('ENV', os.environ.get('MXTRAIN_PROFILE'), "
+                                                    "os.environ.get('AMD_SERIALIZE_KERNEL'), "
+                                                    "os.environ.get('MXTRAIN_CHECK_FINITE'))\""]},
+                                 "resources": {"nnodes": 1, "nproc_per_node": 1}}))
+    env = dict(os.environ, PYTHONPATH=REPO)
+    r = subprocess.run([sys.executable, "-m", "mxtrain", "install", "pm", os.path.join(CHARTS, "training",
+                        "pytorchjob-distributed"), "-f", str(v), "--wait", "--profile", "--debug-mode"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    from mxtrain.launch import release as rel
+    assert "ENV torch 3 1" in rel.logs("pm")
+    from mxtrain.obs.profile import StepProfiler, check_finite
+    import torch
+    prof = StepProfiler(0, out_dir=str(tmp_path / "prof"), mode="torch", steps="1:3")
+    x = torch.randn(64, 64)
+    for it in range(1, 5):
+        (x @ x).sum()
+        prof.step(it)
+    assert (tmp_path / "prof" / "trace-rank0.json").exists()
+    assert "Self CPU" in (tmp_path / "prof" / "kernels-rank0.txt").read_text()
+    with pytest.raises(FloatingPointError):
+        check_finite(3, loss=torch.tensor(float("nan")))
