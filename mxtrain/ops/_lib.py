@@ -97,6 +97,14 @@ def lib():
     return _load()
 
 
+# per-call host cost matters: an eager GPT-2 345M step issues ~1000 launches and its
+# Python side was within 20% of the GPU time, so the helpers below avoid torch's
+# device/stream bookkeeping and ctypes object churn (raw ints for pointers, cached
+# function objects, environment read once)
+_FN = {}
+_FALLBACK = None
+
+
 def available() -> bool:
     try:
         _load()
@@ -106,7 +114,10 @@ def available() -> bool:
 
 
 def fallback_allowed() -> bool:
-    return os.environ.get("MXTRAIN_ALLOW_TORCH_FALLBACK", "0") == "1"
+    global _FALLBACK
+    if _FALLBACK is None:
+        _FALLBACK = os.environ.get("MXTRAIN_ALLOW_TORCH_FALLBACK", "0") == "1"
+    return _FALLBACK
 
 
 def use_hip(t: torch.Tensor) -> bool:
@@ -119,28 +130,47 @@ def use_hip(t: torch.Tensor) -> bool:
 
 
 def stream():
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    """The current HIP stream of the current device, as a raw handle (int)."""
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
 
 
 def ptr(t):
     if t is None:
         return None
-    return ctypes.c_void_p(t.data_ptr())
+    return t.data_ptr()
+
+
+def _fn(name):
+    f = _FN.get(name)
+    if f is None:
+        f = _FN[name] = getattr(_load(), name)
+    return f
 
 
 def call(name, *args):
-    fn = getattr(_load(), name)
-    err = fn(*args)
+    err = _fn(name)(*args)
     if err != 0:
         raise RuntimeError(f"{name} failed with hipError {err}")
     return err
 
 
+_QCACHE = {}
+
+
 def query(name, *args) -> int:
-    return getattr(_load(), name)(*args)
+    """Pure size/shape queries of the library (partial counts, scratch sizes): memoised."""
+    key = (name,) + args
+    v = _QCACHE.get(key)
+    if v is None:
+        v = _QCACHE[key] = _fn(name)(*args)
+    return v
 
 
 def query64(name, *args) -> int:
-    fn = getattr(_load(), name)
-    fn.restype = ctypes.c_int64
-    return fn(*args)
+    key = (name,) + args
+    v = _QCACHE.get(key)
+    if v is None:
+        fn = _fn(name)
+        fn.restype = ctypes.c_int64
+        v = _QCACHE[key] = fn(*args)
+    return v

@@ -107,9 +107,11 @@ def main():
         fn = lambda: N.norm_bwd(x, x, hh_, mean_, rstd_, g, want_dx=True, p=0.1, seed_t=seed,  # noqa: E731
                                 dgamma=dg, dbeta=db, dbias=dbi, accumulate=True)
         for thr in (2048, 512):
-            old = _lib.query("mx_norm_split_cols", thr)
+            old = _lib._fn("mx_norm_split_cols")(thr)   # a setter: never through the memoised query
+            _lib._QCACHE.clear()
             rec(f"ln_bwd 4096x1024 split>{thr}", timeit(fn), rows * cols * 2 * 5)
-            _lib.query("mx_norm_split_cols", old)
+            _lib._fn("mx_norm_split_cols")(old)
+            _lib._QCACHE.clear()
         rec("bda_ln_fwd 4096x1024", timeit(lambda: N.bda_norm_fwd(x, bb, x, g, bb, p=0.1, seed_t=seed)),
             rows * cols * 2 * 4)
     if want("norm"):
