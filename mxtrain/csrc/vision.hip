@@ -335,6 +335,40 @@ __global__ __launch_bounds__(256) void crop_resize_masks_kernel(const uint8_t* _
   out[i] = v;
 }
 
+// Same targets from packed per-instance crops (data/coco.py mask_crop): table[g] =
+// (offset, x0, y0, w, h) of instance g's crop inside `flat`; a mask is zero outside its
+// crop, so a bilinear tap outside the crop reads 0 -- identical to the full-image path.
+// H, W are the (padded) image dims the full masks would have had (border clamping).
+__global__ __launch_bounds__(256) void crop_resize_mask_crops_kernel(const uint8_t* __restrict__ flat,
+                                                                     const int* __restrict__ table, int H, int W,
+                                                                     const float4* __restrict__ boxes,
+                                                                     const int* __restrict__ gidx, int R, int M,
+                                                                     float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * M * M) return;
+  const int r = i / (M * M), py = (i / M) % M, px = i % M;
+  const float4 b = boxes[r];
+  const int* t = table + 5 * gidx[r];
+  const int off = t[0], cx0 = t[1], cy0 = t[2], cw = t[3], ch = t[4];
+  const float y = b.y + (py + 0.5f) * (b.w - b.y) / M - 0.5f;
+  const float x = b.x + (px + 0.5f) * (b.z - b.x) / M - 0.5f;
+  float v = 0.f;
+  if (cw > 0 && !(y < -1.f || y > (float)H || x < -1.f || x > (float)W)) {
+    const float yc = fmaxf(y, 0.f), xc = fmaxf(x, 0.f);
+    int yl = (int)yc, xl = (int)xc, yh, xh;
+    float yy = yc, xx = xc;
+    if (yl >= H - 1) { yh = yl = H - 1; yy = (float)yl; } else { yh = yl + 1; }
+    if (xl >= W - 1) { xh = xl = W - 1; xx = (float)xl; } else { xh = xl + 1; }
+    const float ly = yy - yl, lx = xx - xl;
+    auto at = [&](int yi, int xi) -> float {
+      const int u = yi - cy0, w = xi - cx0;
+      return (u >= 0 && u < ch && w >= 0 && w < cw) ? (float)flat[(size_t)off + u * cw + w] : 0.f;
+    };
+    v = (1.f - ly) * ((1.f - lx) * at(yl, xl) + lx * at(yl, xh)) + ly * ((1.f - lx) * at(yh, xl) + lx * at(yh, xh));
+  }
+  out[i] = v;
+}
+
 Levels make_levels(const void* const* feats, float* const* grads, const int* H, const int* W, const float* scales,
                    int n, int lvl_min, float canon, int canon_lvl) {
   Levels L;
@@ -425,5 +459,15 @@ MX_EXPORT int mx_crop_resize_masks(const void* masks, int H, int W, const float*
   const int total = R * M * M;
   hipLaunchKernelGGL(crop_resize_masks_kernel, dim3((total + 255) / 256), dim3(256), 0, s, (const uint8_t*)masks, H, W,
                      (const float4*)boxes, gidx, R, M, out);
+  return hipGetLastError();
+}
+
+// flat uint8 crops, table int32 [G_total, 5], boxes fp32 [R, 4], gidx int32 [R] -> out fp32 [R, M, M]
+MX_EXPORT int mx_crop_resize_mask_crops(const void* flat, const int* table, int H, int W, const float* boxes,
+                                        const int* gidx, int R, int M, float* out, hipStream_t s) {
+  if (R == 0) return hipSuccess;
+  const int total = R * M * M;
+  hipLaunchKernelGGL(crop_resize_mask_crops_kernel, dim3((total + 255) / 256), dim3(256), 0, s,
+                     (const uint8_t*)flat, table, H, W, (const float4*)boxes, gidx, R, M, out);
   return hipGetLastError();
 }

@@ -275,7 +275,10 @@ class MaskRCNN(nn.Module):
         L = len(boxes_all)
         boxes = torch.stack(boxes_all, 1).reshape(B * L, pre, 4)               # problem = (image, level)
         scores = torch.stack(scores_all, 1).reshape(B * L, pre)
-        cnt = torch.tensor(counts, dtype=torch.int32, device=boxes.device).repeat(B)
+        ck = ("nms_counts", tuple(counts), B, str(boxes.device))
+        if ck not in self._anchor_cache:   # (no host->device copy inside a captured step)
+            self._anchor_cache[ck] = torch.tensor(counts, dtype=torch.int32, device=boxes.device).repeat(B)
+        cnt = self._anchor_cache[ck]
         keep, nk = V.batched_nms_sorted(boxes, cnt, cfg.rpn_nms_thresh, pre)
         valid = keep >= 0
         ki = keep.clamp(min=0)
@@ -323,9 +326,11 @@ class MaskRCNN(nn.Module):
         return torch.cat([bi, boxes.float()], -1).reshape(-1, 5)
 
     # ------------------------------------------------------------------ forward
-    def forward(self, images, img_hw, gt_boxes=None, gt_labels=None, gt_count=None, gt_masks=None):
+    def forward(self, images, img_hw, gt_boxes=None, gt_labels=None, gt_count=None, gt_masks=None,
+                gt_mask_table=None):
         """Training: returns dict of losses.  images [B,3,H,W] (padded), img_hw [B,2] real
-        sizes, gt_* padded to G per image, gt_masks uint8 [B, G, H, W]."""
+        sizes, gt_* padded to G per image; gt_masks uint8 [B, G, H, W], or (with
+        gt_mask_table int32 [B, G, 5]) the flat uint8 buffer of packed instance crops."""
         cfg = self.cfg
         P = self.features(images)
         lv = [self.rpn(p) for p in P]
@@ -361,10 +366,14 @@ class MaskRCNN(nn.Module):
             ml = self.mask_head(mf)                                               # [R, 80, 28, 28]
             ml = torch.gather(ml, 1, (fg_lab - 1).clamp(min=0)[:, None, None, None].expand(-1, 1, *ml.shape[2:]))
             ml = ml.squeeze(1).float()
-            G = gt_masks.shape[1]
+            G = (gt_mask_table if gt_mask_table is not None else gt_masks).shape[1]
             flat_gid = (torch.arange(B, device=images.device)[:, None] * G + gidx[:, :nfg]).reshape(-1)
-            tgt_m = V.crop_resize_masks(gt_masks.reshape(-1, *gt_masks.shape[2:]), fg_rois.reshape(-1, 4), flat_gid,
-                                        cfg.mask_size)
+            if gt_mask_table is not None:
+                tgt_m = V.crop_resize_mask_crops(gt_masks, gt_mask_table.reshape(-1, 5), images.shape[2],
+                                                 images.shape[3], fg_rois.reshape(-1, 4), flat_gid, cfg.mask_size)
+            else:
+                tgt_m = V.crop_resize_masks(gt_masks.reshape(-1, *gt_masks.shape[2:]), fg_rois.reshape(-1, 4),
+                                            flat_gid, cfg.mask_size)
             tgt_m = (tgt_m >= 0.5).float()
             bce = F.binary_cross_entropy_with_logits(ml, tgt_m, reduction="none").mean(dim=(1, 2))
             out["maskrcnn_loss"] = (bce * fg_valid).sum() / fg_valid.sum().clamp(min=1)

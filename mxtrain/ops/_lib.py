@@ -69,6 +69,7 @@ SIGNATURES = {
     "mx_match": [P, I, I, P, P, I, I, P, P, P, P, P],
     "mx_decode_clip": [P, P, I, I, F, F, F, F, F, P, I, P, P],
     "mx_crop_resize_masks": [P, I, I, P, P, I, I, P, P],
+    "mx_crop_resize_mask_crops": [P, P, I, I, P, P, I, I, P, P],
 }
 
 

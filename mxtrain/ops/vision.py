@@ -332,3 +332,22 @@ def crop_resize_masks(masks: torch.Tensor, boxes: torch.Tensor, gidx: torch.Tens
     v = ((1 - ly) * ((1 - lx) * m[gi, yl, xl] + lx * m[gi, yl, xh]) +
          ly * ((1 - lx) * m[gi, yh, xl] + lx * m[gi, yh, xh]))
     return v * valid
+
+
+def crop_resize_mask_crops(flat: torch.Tensor, table: torch.Tensor, H: int, W: int, boxes: torch.Tensor,
+                           gidx: torch.Tensor, M: int = 28) -> torch.Tensor:
+    """``crop_resize_masks`` over packed per-instance crops (data/coco.py ``mask_crop``):
+    flat uint8 crops, table int32 [G, 5] = (offset, x0, y0, w, h), H x W the padded
+    image the full masks would cover.  Same result as unpacking to full masks."""
+    R = boxes.shape[0]
+    if _lib.use_hip(boxes):
+        out = torch.empty(R, M, M, dtype=torch.float32, device=boxes.device)
+        if flat.numel() == 0:
+            flat = torch.zeros(1, dtype=torch.uint8, device=boxes.device)
+        _lib.call("mx_crop_resize_mask_crops", _lib.ptr(flat), _lib.ptr(table.to(torch.int32).contiguous()), H, W,
+                  _lib.ptr(boxes.float().contiguous()), _lib.ptr(gidx.to(torch.int32).contiguous()), R, M,
+                  _lib.ptr(out), _lib.stream())
+        return out
+    from ..data.coco import unpack_mask_crops
+    full = unpack_mask_crops(flat, table.reshape(1, -1, 5), H, W)[0].to(boxes.device)
+    return crop_resize_masks(full, boxes, gidx, M)

@@ -1,0 +1,144 @@
+"""Whole-step hipGraph replay for Mask R-CNN training (forward, backward, gradient clip,
+SGD-momentum update in ONE graph launch per step).
+
+Why: the eager step issues ~2100 kernels per iteration; at batch 4 the host needs
+~37 ms to enqueue them while the GPU needs less, so the GPU idles on Python (measured:
+host enqueue 37.2 ms + loader wait 9.2 ms per 48 ms step).  The model is written with
+static per-step shapes (models/maskrcnn.py: fixed-size proposals, fixed 512 RoIs/image,
+rank-based sampling, no nonzero()/host sync), so once the inputs have static shapes the
+whole step is capturable:
+
+* images: one padded canvas per orientation (data/coco.py ``collate``);
+* ground truth: ``fixed_gt`` pads boxes/labels to ``max_gt`` slots;
+* masks: packed per-instance crops of variable total size are copied into the prefix
+  of a fixed-capacity device buffer the graph reads through the crop table.
+
+So there is one graph per (batch, canvas) shape -- two for COCO -- captured lazily the
+first time a shape is seen (that step runs eagerly: it also warms MIOpen/BLAS, the
+anchor caches and the momentum buffers, none of which may be created during capture).
+Graphs share one memory pool (they never run concurrently and keep no state between
+replays except the parameters and optimizer buffers, which live outside the pool).
+The learning rate is a device scalar filled before each replay.
+
+The reference trains this model eagerly under TensorFlow/Horovod
+(examples/maskrcnn/train-maskrcnn-tensorpack.yaml); this replaces its per-op runtime
+dispatch, not its math: ``sgd_momentum_`` is torch.optim.SGD's update (dampening 0,
+no Nesterov), so eager and graph steps are interchangeable and checkpoints are the same.
+"""
+from __future__ import annotations
+
+import os
+import sys
+from typing import Dict, List, Optional
+
+import torch
+
+LOSS_NAMES = ("rpn_cls_loss", "rpn_box_loss", "fastrcnn_cls_loss", "fastrcnn_box_loss", "maskrcnn_loss",
+              "total_loss")
+INPUT_KEYS = ("images", "hw", "gt_boxes", "gt_labels", "gt_count", "gt_mask_table")
+
+
+@torch.no_grad()
+def sgd_momentum_(opt: torch.optim.SGD, lr) -> None:
+    """torch.optim.SGD's step with a tensor (device) learning rate: d = g + wd p,
+    buf = m buf + d (buf starts at 0, so the first step gives buf = d), p -= lr buf."""
+    for g in opt.param_groups:
+        ps = [p for p in g["params"] if p.grad is not None]
+        if not ps:
+            continue
+        grads = [p.grad for p in ps]
+        if g["weight_decay"]:
+            torch._foreach_add_(grads, ps, alpha=g["weight_decay"])
+        bufs = []
+        for p in ps:
+            st = opt.state[p]
+            if st.get("momentum_buffer") is None:
+                assert not (p.is_cuda and torch.cuda.is_current_stream_capturing()), \
+                    "momentum buffers must exist before capture"
+                st["momentum_buffer"] = torch.zeros_like(p)
+            bufs.append(st["momentum_buffer"])
+        if g["momentum"]:
+            torch._foreach_mul_(bufs, g["momentum"])
+            torch._foreach_add_(bufs, grads)
+            upd = bufs
+        else:
+            upd = grads
+        if torch.is_tensor(lr):
+            torch._foreach_add_(ps, torch._foreach_mul(upd, -lr))
+        else:
+            torch._foreach_add_(ps, upd, alpha=-lr)
+
+
+class GraphedTrainStep:
+    def __init__(self, model, opt: torch.optim.SGD, params: List[torch.Tensor], clip: float, device,
+                 flat_capacity: int = 16 << 20):
+        self.model, self.opt, self.params, self.clip, self.device = model, opt, params, clip, device
+        self.graphs: Dict[tuple, tuple] = {}
+        self.lr = torch.zeros((), dtype=torch.float32, device=device)
+        self.pool = torch.cuda.graph_pool_handle()
+        self.stream = torch.cuda.Stream(device)
+        self.flat = torch.zeros(flat_capacity, dtype=torch.uint8, device=device)
+        self.captures = 0
+        self.replays = 0
+        # MXTRAIN_GRAPH_DEBUG=1: synchronise after every step and log capture/replay events
+        self.debug = os.environ.get("MXTRAIN_GRAPH_DEBUG", "0") == "1"
+
+    def _dbg(self, what: str, key) -> None:
+        if self.debug:
+            torch.cuda.synchronize(self.device)
+            print(f"[graphed] {what} key={key} captures={self.captures} replays={self.replays} "
+                  f"graphs={len(self.graphs)}", file=sys.stderr, flush=True)
+
+    def _body(self, st: Dict[str, torch.Tensor]) -> torch.Tensor:
+        losses = self.model(st["images"], st["hw"], st["gt_boxes"], st["gt_labels"], st["gt_count"], self.flat,
+                            st["gt_mask_table"])
+        losses["total_loss"].backward()
+        if self.clip > 0:
+            torch.nn.utils.clip_grad_norm_(self.params, self.clip, foreach=True)
+        sgd_momentum_(self.opt, self.lr)
+        return torch.stack([losses[k].detach().float() for k in LOSS_NAMES])
+
+    def _ensure_capacity(self, n: int) -> None:
+        if n <= self.flat.numel():
+            return
+        cap = self.flat.numel()
+        while cap < n:
+            cap *= 2
+        # the graphs read the old buffer's address: drop them (recaptured on next use)
+        self.graphs.clear()
+        self.flat = torch.zeros(cap, dtype=torch.uint8, device=self.device)
+
+    def __call__(self, batch: Dict[str, torch.Tensor], lr: float) -> Dict[str, torch.Tensor]:
+        flat = batch["gt_mask_flat"]
+        self._ensure_capacity(flat.numel())
+        key = tuple(tuple(batch[k].shape) for k in INPUT_KEYS)
+        cur = torch.cuda.current_stream(self.device)
+        self.lr.fill_(lr)
+        entry = self.graphs.get(key)
+        if entry is None:
+            st = {k: batch[k].to(self.device, non_blocking=True) for k in INPUT_KEYS}
+            self.flat[:flat.numel()].copy_(flat, non_blocking=True)
+            self.stream.wait_stream(cur)
+            with torch.cuda.stream(self.stream):
+                # eager step with this batch (a real update): warms every lazy cache
+                self.opt.zero_grad(set_to_none=True)
+                out = self._body(st)
+                # capture: grads are allocated inside the graph's pool, never zeroed
+                self.opt.zero_grad(set_to_none=True)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self.pool, stream=self.stream):
+                    sout = self._body(st)
+            cur.wait_stream(self.stream)
+            self.graphs[key] = (g, st, sout)
+            self.captures += 1
+            self._dbg("captured", key)
+            return dict(zip(LOSS_NAMES, out.unbind(0)))
+        g, st, sout = entry
+        for k in INPUT_KEYS:
+            st[k].copy_(batch[k], non_blocking=True)
+        self.flat[:flat.numel()].copy_(flat, non_blocking=True)
+        g.replay()
+        self.replays += 1
+        self._dbg("replayed", key)
+        # the pool is shared: copy the losses out before another graph can reuse it
+        return dict(zip(LOSS_NAMES, sout.clone().unbind(0)))

@@ -175,6 +175,8 @@ def get_args(argv=None):
                    help="stop after N steps (bounded runs / benchmarks)")
     p.add_argument("--mx-warmup-steps", type=int, default=5, help="steps excluded from the images/s figure")
     p.add_argument("--mx-bench-json", default=None, help="append a JSON images/s record to this file")
+    p.add_argument("--mx-graph", choices=("auto", "0", "1"), default=os.environ.get("MXTRAIN_GRAPH", "0"),
+                   help="replay the whole training step as a hipGraph (auto: on for 1 GPU, off in debug mode)")
     return p.parse_args(argv)
 
 
@@ -247,11 +249,15 @@ def main(argv=None):
     prof = StepProfiler(rank, out_dir=os.path.join(args.logdir, "profile") if os.environ.get("MXTRAIN_PROFILE") else None)
     debug_finite = check_finite_enabled()
     train_sets = [COCODetection(cfg.DATA.BASEDIR, n, training=True) for n in cfg.DATA.TRAIN]
-    ds = DetectionDataset(train_sets[0], short, max_size, training=True, with_masks=bool(cfg.MODE_MASK), seed=rank)
+    use_graph = (args.mx_graph == "1" or (args.mx_graph == "auto" and world == 1 and not debug_finite)) \
+        and device.type == "cuda" and world == 1 and bool(cfg.MODE_MASK)
+    ds = DetectionDataset(train_sets[0], short, max_size, training=True, with_masks=bool(cfg.MODE_MASK), seed=rank,
+                          mask_format="crops")
+    train_coll = functools.partial(collate, short=short, max_size=max_size, fixed_gt=use_graph)
     bs = int(cfg.TRAIN.BATCH_SIZE_PER_GPU)
     sampler = AspectGroupedSampler(ds, bs, rank, world, seed=42)
     nw = int(cfg.DATA.NUM_WORKERS)
-    loader = torch.utils.data.DataLoader(ds, batch_sampler=sampler, num_workers=nw, collate_fn=coll,
+    loader = torch.utils.data.DataLoader(ds, batch_sampler=sampler, num_workers=nw, collate_fn=train_coll,
                                          pin_memory=device.type == "cuda", persistent_workers=nw > 0,
                                          prefetch_factor=4 if nw > 0 else None)
     decay, no_decay = [], []
@@ -279,8 +285,14 @@ def main(argv=None):
     dmodel = hvd.DistributedDataParallel(model)
     params = decay + no_decay
     clip = float(cfg.TRAIN.GRADIENT_CLIP or 0.0)
+    gstep = None
+    if use_graph:
+        from mxtrain.workloads.maskrcnn.graphed import GraphedTrainStep
+        gstep = GraphedTrainStep(model, opt, params, clip, device)
+        log("Training step runs as a hipGraph (one graph per input shape)")
     max_steps = args.mx_max_steps
     timed_imgs, t_timed = 0, None
+    t_wait = t_enq = 0.0
     done = False
     for epoch in range(start_epoch, int(cfg.TRAIN.MAX_EPOCH) + 1):
         sampler.set_epoch(epoch)
@@ -288,22 +300,32 @@ def main(argv=None):
         t_ep = time.time()
         it = iter(loader)
         for k in range(int(cfg.TRAIN.STEPS_PER_EPOCH)):
+            t_a = time.time()
             try:
                 batch = next(it)
             except StopIteration:
                 sampler.set_epoch(epoch * 1000 + k)
                 it = iter(loader)
                 batch = next(it)
+            t_b = time.time()
             lr = C.lr_at(cfg, step)
             for g in opt.param_groups:
                 g["lr"] = lr
-            d = {kk: v.to(device, non_blocking=True) for kk, v in batch.items() if torch.is_tensor(v)}
-            losses = dmodel(d["images"], d["hw"], d["gt_boxes"], d["gt_labels"], d["gt_count"], d.get("gt_masks"))
-            opt.zero_grad(set_to_none=True)
-            losses["total_loss"].backward()
-            if clip > 0:
-                torch.nn.utils.clip_grad_norm_(params, clip)
-            opt.step()
+            if gstep is not None:
+                losses = gstep(batch, lr)
+            else:
+                d = {kk: v.to(device, non_blocking=True) for kk, v in batch.items() if torch.is_tensor(v)}
+                losses = dmodel(d["images"], d["hw"], d["gt_boxes"], d["gt_labels"], d["gt_count"],
+                                d.get("gt_mask_flat", d.get("gt_masks")), d.get("gt_mask_table"))
+                opt.zero_grad(set_to_none=True)
+                losses["total_loss"].backward()
+                if clip > 0:
+                    torch.nn.utils.clip_grad_norm_(params, clip)
+                opt.step()
+            t_c = time.time()
+            if t_timed is not None:   # host-side accounting: loader wait vs enqueue time
+                t_wait += t_b - t_a
+                t_enq += t_c - t_b
             step += 1
             prof.step(step)
             if debug_finite:
@@ -317,7 +339,9 @@ def main(argv=None):
             if args.verbose or step % args.throughput_log_freq == 0:
                 lv = {kk: round(float(v.detach()), 4) for kk, v in losses.items()}
                 ips = (timed_imgs / (time.time() - t_timed)) if t_timed and timed_imgs else 0.0
-                log(f"step {step} lr {lr:.5f} {lv} images/s {ips:.2f}")
+                nst = max(1, step - args.mx_warmup_steps)
+                log(f"step {step} lr {lr:.5f} {lv} images/s {ips:.2f} "
+                    f"(per step: loader wait {1e3 * t_wait / nst:.1f} ms, host enqueue {1e3 * t_enq / nst:.1f} ms)")
                 if rank == 0:   # tensorpack writes its monitors as TensorBoard events in logdir
                     if tbw is None:
                         from mxtrain.obs.tensorboard import SummaryWriter

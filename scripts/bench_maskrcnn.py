@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--data", default="/tmp/mx_coco_bench")
     ap.add_argument("--workers", type=int, default=6)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--graph", choices=("auto", "0", "1"), default="0",
+                    help="whole-step hipGraph replay (train.py --mx-graph)")
     ap.add_argument("extra", nargs="*")
     a = ap.parse_args()
     rank = int(os.environ.get("RANK", os.environ.get("OMPI_COMM_WORLD_RANK", "0")))
@@ -39,7 +41,7 @@ def main():
     out = a.out or os.path.join(REPO, "gpurun_out", "maskrcnn_bench.jsonl")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     args = ["--logdir", "/tmp/mx_mrcnn_log", "--mx-max-steps", str(a.steps), "--mx-warmup-steps", str(a.warmup),
-            "--throughput_log_freq", "10", "--mx-bench-json", out, "--config", "MODE_MASK=True", "MODE_FPN=True",
+            "--throughput_log_freq", "10", "--mx-bench-json", out, "--mx-graph", a.graph, "--config", "MODE_MASK=True", "MODE_FPN=True",
             f"DATA.BASEDIR={a.data}", "TRAINER=horovod", f"TRAIN.BATCH_SIZE_PER_GPU={a.batch}",
             f"TRAIN.STEPS_PER_EPOCH={a.steps}", "TRAIN.EVAL_PERIOD=1000", "TRAIN.CHECKPOINT_PERIOD=1000",
             f"DATA.NUM_WORKERS={a.workers}", "DATA.VAL=()"] + a.extra

@@ -151,3 +151,83 @@ def test_jupyter_chart_viewer_serves_predictions(coco_dir, tmp_path, monkeypatch
         assert rec["output"].endswith(".png") and isinstance(rec["boxes"], list)
     finally:
         rel.uninstall("viewer")
+
+
+def _small_model_cfg():
+    from mxtrain.models.maskrcnn import MaskRCNNConfig
+    return MaskRCNNConfig(train_per_level_topk=300, train_post_nms_topk=300, frcnn_batch_per_im=64,
+                          fc_dim=256, mask_head_dim=64)
+
+
+def test_mask_crops_equal_full_masks(coco_dir):
+    """Packed per-instance crops carry the full-image masks (up to PIL tie rounding at
+    single pixels), and the crop-table target op equals the full-mask op on them."""
+    from mxtrain.data.coco import COCODetection, DetectionDataset, collate, unpack_mask_crops
+    from mxtrain.ops import vision as V
+    coco = COCODetection(coco_dir, "coco_train2017")
+    full = DetectionDataset(coco, 320, 512)
+    crop = DetectionDataset(coco, 320, 512, mask_format="crops")
+    idx = [0, 1]
+    bf = collate([full[i] for i in idx], 320, 512)
+    bc = collate([crop[i] for i in idx], 320, 512, fixed_gt=True, max_gt=16)
+    assert bc["gt_boxes"].shape[1] == 16 and bc["gt_mask_table"].shape == (2, 16, 5)
+    B, G = bf["gt_boxes"].shape[:2]
+    H, W = bf["images"].shape[2:]
+    un = unpack_mask_crops(bc["gt_mask_flat"], bc["gt_mask_table"], H, W)
+    ref = bf["gt_masks"][:, :G]
+    mism = (un[:, :G] != ref).sum().item()
+    assert mism <= max(2, ref.numel() // 100000), mism
+    assert un[:, G:].sum() == 0 and bc["gt_mask_flat"].numel() < ref.numel() // 2
+    g = torch.Generator().manual_seed(0)
+    R = 40
+    gid = torch.randint(0, G, (R,), generator=g)
+    bi = torch.randint(0, B, (R,), generator=g)
+    boxes = torch.gather(bf["gt_boxes"][bi], 1, gid[:, None, None].expand(-1, 1, 4))[:, 0]
+    boxes = boxes + torch.randn(R, 4, generator=g) * 4
+    a = V.crop_resize_mask_crops(bc["gt_mask_flat"], bc["gt_mask_table"].reshape(-1, 5), H, W, boxes,
+                                 bi * 16 + gid)
+    b = V.crop_resize_masks(un.reshape(-1, H, W), boxes, bi * 16 + gid)
+    torch.testing.assert_close(a, b)
+
+
+def test_sgd_momentum_matches_torch_sgd():
+    from mxtrain.workloads.maskrcnn.graphed import sgd_momentum_
+    torch.manual_seed(0)
+    ps = [torch.randn(5, 3), torch.randn(7)]
+    qs = [p.clone() for p in ps]
+    o1 = torch.optim.SGD([{"params": [ps[0]], "weight_decay": 1e-4}, {"params": [ps[1]], "weight_decay": 0.0}],
+                         lr=0.1, momentum=0.9)
+    o2 = torch.optim.SGD([{"params": [qs[0]], "weight_decay": 1e-4}, {"params": [qs[1]], "weight_decay": 0.0}],
+                         lr=0.1, momentum=0.9)
+    for it in range(4):
+        gs = [torch.randn_like(p) for p in ps]
+        lr = 0.1 * (it + 1)
+        for p, q, gg in zip(ps, qs, gs):
+            p.grad, q.grad = gg.clone(), gg.clone()
+        for grp in o1.param_groups:
+            grp["lr"] = lr
+        o1.step()
+        sgd_momentum_(o2, torch.tensor(lr) if it % 2 else lr)
+        for p, q in zip(ps, qs):
+            torch.testing.assert_close(p, q, rtol=1e-6, atol=1e-6)
+    # the state dict stays torch.optim.SGD's (checkpoints interchange)
+    assert set(o2.state[qs[0]]) == {"momentum_buffer"}
+
+
+def test_model_losses_crops_equal_full(coco_dir):
+    """Training losses from packed crops == from the same masks unpacked to full images."""
+    from mxtrain.data.coco import COCODetection, DetectionDataset, collate, unpack_mask_crops
+    from mxtrain.models.maskrcnn import MaskRCNN
+    crop = DetectionDataset(COCODetection(coco_dir, "coco_train2017"), 256, 384, mask_format="crops")
+    b = collate([crop[0], crop[1]], 256, 384, fixed_gt=True, max_gt=12)
+    H, W = b["images"].shape[2:]
+    full = unpack_mask_crops(b["gt_mask_flat"], b["gt_mask_table"], H, W)
+    torch.manual_seed(0)
+    m = MaskRCNN(_small_model_cfg()).train()
+    out = []
+    for masks, table in ((b["gt_mask_flat"], b["gt_mask_table"]), (full, None)):
+        torch.manual_seed(5)
+        with torch.no_grad():
+            out.append(m(b["images"], b["hw"], b["gt_boxes"], b["gt_labels"], b["gt_count"], masks, table))
+    for k in out[0]:
+        torch.testing.assert_close(out[0][k], out[1][k], rtol=1e-5, atol=1e-6)

@@ -142,3 +142,30 @@ def test_nms_match_decode_gpu():
     hw = torch.tensor([[800.0, 1344.0]])
     torch.testing.assert_close(V.decode_boxes(anchors.cuda(), d.cuda(), (10, 10, 5, 5), hw.cuda()).cpu(),
                                V.decode_boxes(anchors, d, (10, 10, 5, 5), hw), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.gpu
+def test_crop_resize_mask_crops_gpu():
+    """Packed-crop mask targets (HIP) == full-mask fp32 reference on the unpacked masks."""
+    from mxtrain.data.coco import unpack_mask_crops
+    g = torch.Generator().manual_seed(5)
+    B, G, H, W = 2, 6, 320, 512
+    table = torch.zeros(B, G, 5, dtype=torch.int32)
+    parts, off = [], 0
+    for b in range(B):
+        for k in range(G - 1):                      # last slot is padding (w = h = 0)
+            x0, y0 = int(torch.randint(0, W - 40, (1,), generator=g)), int(torch.randint(0, H - 40, (1,), generator=g))
+            cw, ch = int(torch.randint(1, W - x0, (1,), generator=g)), int(torch.randint(1, H - y0, (1,), generator=g))
+            c = (torch.rand(ch, cw, generator=g) > 0.4).to(torch.uint8)
+            table[b, k] = torch.tensor([off, x0, y0, cw, ch])
+            parts.append(c.reshape(-1))
+            off += ch * cw
+    flat = torch.cat(parts)
+    full = unpack_mask_crops(flat, table, H, W).reshape(-1, H, W)
+    R = 500
+    gid = torch.randint(0, B * G, (R,), generator=g)
+    xy = torch.rand(R, 2, generator=g) * torch.tensor([W, H]) - 20
+    boxes = torch.cat([xy, xy + torch.rand(R, 2, generator=g) * 200 + 1], 1)
+    ref = V.crop_resize_masks(full, boxes, gid)
+    out = V.crop_resize_mask_crops(flat.cuda(), table.reshape(-1, 5).cuda(), H, W, boxes.cuda(), gid.cuda())
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-4, atol=1e-4)   # fma vs separate mul-add
