@@ -81,14 +81,21 @@ def level_anchors(stride: int, size: int, ratios, H: int, W: int, device) -> tor
     return (ctr + base[None]).reshape(-1, 4)
 
 
-def _rank_select(key: torch.Tensor, want: torch.Tensor, eligible: torch.Tensor) -> torch.Tensor:
-    """Per row: choose up to want[row] random eligible entries (key = random uniform).
-    Vectorised: rank of every entry among the eligible ones of its row, no host sync."""
+def _rank_select(key: torch.Tensor, want: torch.Tensor, eligible: torch.Tensor, max_want: int) -> torch.Tensor:
+    """Per row: choose up to want[row] (<= max_want) random eligible entries (key = random
+    uniform in [0, 1)); no host sync.
+
+    The max_want smallest keys of a row (ineligible entries keyed 2.0) come from a bounded
+    top-k (radix select + in-place sort of max_want values): unlike a full argsort of a
+    ~270k-anchor row, which goes to a segmented device radix sort, it is safe inside a
+    captured hipGraph step (workloads/maskrcnn/graphed.py)."""
     k = torch.where(eligible, key, torch.full_like(key, 2.0))
-    order = k.argsort(dim=-1)
-    rank = torch.empty_like(order)
-    rank.scatter_(-1, order, torch.arange(order.shape[-1], device=key.device).expand_as(order))
-    return eligible & (rank < want[:, None])
+    m = min(max_want, k.shape[-1])
+    kv, idx = k.topk(m, dim=-1, largest=False)                     # ascending: position = rank
+    take = (kv < 2.0) & (torch.arange(m, device=key.device)[None] < want[:, None])
+    out = torch.zeros_like(eligible)
+    out.scatter_(-1, idx, take)
+    return out
 
 
 def huber(x: torch.Tensor, delta: float) -> torch.Tensor:
@@ -232,9 +239,9 @@ class MaskRCNN(nn.Module):
         neg = (mi < cfg.rpn_bg_thresh) & ~pos & inside
         g = torch.rand(mi.shape, device=mi.device)
         nfg_max = int(cfg.rpn_batch_per_im * cfg.rpn_fg_ratio)
-        sel_pos = _rank_select(g, torch.full((B,), nfg_max, device=mi.device), pos)
+        sel_pos = _rank_select(g, torch.full((B,), nfg_max, device=mi.device), pos, nfg_max)
         npos = sel_pos.sum(1)
-        sel_neg = _rank_select(g, cfg.rpn_batch_per_im - npos, neg)
+        sel_neg = _rank_select(g, cfg.rpn_batch_per_im - npos, neg, cfg.rpn_batch_per_im)
         matched = torch.where(lq >= 0, lq, am).clamp(min=0)
         tgt_boxes = torch.gather(gt_boxes, 1, matched[..., None].expand(-1, -1, 4))
         return sel_pos, sel_neg, tgt_boxes
@@ -308,7 +315,7 @@ class MaskRCNN(nn.Module):
         N = cfg.frcnn_batch_per_im
         nfg = int(N * cfg.frcnn_fg_ratio)
         r = torch.rand(mi.shape, device=mi.device)
-        sel_fg = _rank_select(r, torch.full((B,), nfg, device=mi.device), fg)
+        sel_fg = _rank_select(r, torch.full((B,), nfg, device=mi.device), fg, nfg)
         key = torch.where(sel_fg, 2.0 + r, torch.where(bg, 1.0 + r, torch.zeros_like(r)))
         _, idx = key.topk(N, dim=1)                                                        # fg first, then bg
         rois = torch.gather(cand, 1, idx[..., None].expand(-1, -1, 4))

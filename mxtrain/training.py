@@ -42,6 +42,11 @@ class TrainConfig:
     overlap_grad_reduce: bool = True
     bucket_numel: int = 40_000_000
     capture_graph: bool = False
+    # AdamW of step N runs at the start of step N+1, per bucket on a side stream,
+    # overlapped with the forward (DistributedOptimizer overlap_update; GPU, pp = 1, dense,
+    # not combined with wgrad_stream).  Off by default: at GPT-2 345M on one MI355X the
+    # memory-bound update slows the concurrent forward GEMMs by more than it hides
+    overlap_optimizer: bool = False
     # weight-gradient GEMMs on a side HIP stream (GPU only).  Off by default: measured no
     # gain at GPT-2 345M (19.97 vs 19.81 ms/step) -- hipBLASLt tiles already occupy every CU
     wgrad_stream: bool = False
@@ -86,7 +91,9 @@ class GPTTrainer:
             sp_group=ps.tp_group if ps.sequence_parallel else None,
             mp_group=ps.mp_group if ps.tp * ps.pp > 1 else None,
             embed_group=ps.embed_group if ps.pp > 1 and cfg.tie_embeddings else None,
-            pp_rank=ps.pp_rank, schedule=sched)
+            pp_rank=ps.pp_rank, schedule=sched,
+            overlap_update=(tcfg.overlap_optimizer and self.device.type == "cuda" and ps.pp == 1
+                            and self.eopt is None and not tcfg.wgrad_stream))
         self._setup_xgmi()
         self.pipeline = None
         if ps.pp > 1:
@@ -157,6 +164,8 @@ class GPTTrainer:
         else:
             rt.unit_done = self.opt.unit_done if last_micro else None
         loss = self.stage.forward(ids=ids, labels=labels, B=B, S=S)
+        if self.opt.overlap_update and self.device.type == "cuda":
+            self.opt.wait_all()   # deferred AdamW read/zeroed the grads the backward writes
         loss.backward()
         return loss.detach()
 
@@ -178,7 +187,9 @@ class GPTTrainer:
         also under context parallelism).  Returns the mean loss over the step as a device
         scalar (last stage; 0 elsewhere)."""
         tokens, labels = self._local(tokens), self._local(labels)
-        if self._graph is not None:
+        # the captured body starts with the previous step's deferred update: replay only
+        # when one is pending (after a sync_params() flush, one eager step re-arms it)
+        if self._graph is not None and all(o.update_pending or not o.overlap_update for o in self._opts):
             self._static[0].copy_(tokens)
             self._static[1].copy_(labels)
             for o in self._opts:
@@ -189,6 +200,7 @@ class GPTTrainer:
             # sync_params(), gathers it; re-gathering an unchanged shard is idempotent)
             for o in self._opts:
                 o.gather_pending = o.overlap_param_gather
+                o.update_pending = o.overlap_update
             self.iteration += 1
             return self._static_loss
         return self._train_step_eager(tokens, labels)
@@ -198,8 +210,10 @@ class GPTTrainer:
         return [self.opt] + ([self.eopt] if self.eopt is not None else [])
 
     def _prepare_step(self, nm, B, S):
+        zeroed = self.opt.zeroes_grads   # (a deferred update zeroes each bucket after reading it)
         self._begin_step()
-        self.flat.zero_grad()
+        if not zeroed:
+            self.flat.zero_grad()
         if self.eflat is not None:
             self.eflat.zero_grad()
             self.stage.rt.aux_scale = self.cfg.moe_loss_coeff / nm
@@ -260,6 +274,7 @@ class GPTTrainer:
         # the captured step starts by gathering the shards the previous replay updated
         for o in self._opts:
             o.gather_pending = o.overlap_param_gather
+            o.update_pending = o.overlap_update
         self._prepare_step(nm, B, S)
         if self.pipeline is not None:
             loss = self.pipeline.run(tokens, labels)
@@ -270,11 +285,18 @@ class GPTTrainer:
                                                            labels[m].reshape(-1), B, S,
                                                            m == nm - 1)
         # optimizer body without host-side hyper update (done before each replay)
-        from .parallel.zero import joint_update
-        joint_update(self._opts)
+        if self.opt.overlap_update:
+            # (dense only) grad norm now, AdamW deferred into the next replay's body
+            self.opt.finish_grads()
+            self.opt.grad_norm_sq()
+            self.opt.defer_update()
+        else:
+            from .parallel.zero import joint_update
+            joint_update(self._opts)
         for o in self._opts:
             o.gather_pending = False   # (overlap mode) the next replay's body gathers
             o._gather_events.clear()
+            o._last_event = None
             o.reset_pending()
         return self._cp_mean(loss)
 
@@ -285,7 +307,7 @@ class GPTTrainer:
     def _begin_step(self):
         for o in self._opts:
             o.begin_param_gather()
-        if any(o.overlap_param_gather for o in self._opts):
+        if any(o.overlap_param_gather or o.overlap_update for o in self._opts):
             self.stage.rt.before_unit = self._wait_unit_all if self.eopt is not None else self.opt.wait_unit
         else:
             self.stage.rt.before_unit = None

@@ -327,6 +327,36 @@ def test_wgrad_side_stream_matches_inline(graph):
     assert torch.equal(runs[0][1], runs[1][1])
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_deferred_optimizer_matches_inline(graph):
+    """AdamW deferred into the next step's forward (per bucket, side stream; eager and
+    hipGraph-replayed, with a sync_params() flush mid-run) gives the inline optimizer's
+    losses and parameters bit for bit."""
+    from mxtrain.models.gpt import GPTConfig
+    from mxtrain.parallel import state as pstate
+    from mxtrain.training import GPTTrainer, TrainConfig, synthetic_batch
+    ps = pstate.initialize_model_parallel()
+    cfg = GPTConfig(num_layers=3, hidden_size=256, num_attention_heads=4, seq_length=256,
+                    max_position_embeddings=256, vocab_size=1024)
+    runs = []
+    for ov in (False, True):
+        tr = GPTTrainer(cfg, TrainConfig(micro_batch_size=2, overlap_optimizer=ov, bucket_numel=400_000), ps)
+        assert tr.opt.overlap_update == ov and len(tr.flat.buckets) > 2
+        tok, lab = synthetic_batch(cfg, 1, 2, ps.device, torch.Generator().manual_seed(3))
+        losses = [float(tr.train_step(tok, lab))]
+        if graph:
+            tr.capture(tok, lab, warmup=1)
+        losses += [float(tr.train_step(tok, lab)) for _ in range(2)]
+        tr.sync_params()                       # flush mid-run (eval / checkpoint)
+        losses += [float(tr.train_step(tok, lab)) for _ in range(3)]
+        torch.cuda.synchronize()
+        tr.sync_params()
+        runs.append((losses, tr.flat.data.clone(), tr.opt.exp_avg.clone()))
+    assert runs[0][0] == runs[1][0], (runs[0][0], runs[1][0])
+    assert torch.equal(runs[0][1], runs[1][1])
+    assert torch.equal(runs[0][2], runs[1][2])
+
+
 def test_moe_gpt_gpu_matches_cpu_and_captures():
     """MoE GPT (top-2, capacity routing, 4 experts) on the GPU vs the fp32 CPU path, then
     the same trainer captured in a hipGraph (static shapes end to end) and replayed."""
