@@ -64,6 +64,25 @@ __device__ __forceinline__ Bilinear bilinear(float y, float x, int H, int W) {
   return b;
 }
 
+// one axis of bilinear(): the same validity, clamping and lo/hi weights
+struct Axis {
+  int lo, hi;
+  float wlo, whi;
+  bool valid;
+};
+
+__device__ __forceinline__ Axis axis_weights(float y, int H) {
+  Axis a;
+  a.valid = !(y < -1.f || y > (float)H);
+  y = fmaxf(y, 0.f);
+  int l = (int)y;
+  if (l >= H - 1) { a.lo = a.hi = H - 1; y = (float)a.lo; } else { a.lo = l; a.hi = l + 1; }
+  const float f = y - a.lo;
+  a.wlo = 1.f - f;
+  a.whi = f;
+  return a;
+}
+
 // one thread = (roi, bin, 8-channel chunk)
 __global__ __launch_bounds__(256) void roi_align_fwd_kernel(Levels L, const float* __restrict__ rois, int R,
                                                             int C, int PH, int PW, int sr, int aligned,
@@ -139,6 +158,53 @@ __global__ __launch_bounds__(256) void roi_align_bwd_kernel(Levels L, const floa
 #pragma unroll
   for (int g = 0; g < 8; ++g) go[g] = g < ng ? bf2f(d[g * 64]) : 0.f;
   const float inv = 1.f / (float)(sr * sr);
+  if (sr <= 2) {
+    // The bilinear weights are separable: a sample at (y, x) puts wy(row) * wx(col) on
+    // its 4 corners, and validity is valid(y) && valid(x), so the bin's total weight on
+    // pixel (row, col) is Wy[row] * Wx[col] with Wy / Wx summed over the sr samples of
+    // each axis.  Rows (columns) shared by the two samples merge into one entry: a bin
+    // of ~1-2 feature pixels touches 2-3 rows x 2-3 columns, 4-9 atomics per channel
+    // instead of 16.  Entries: (lo, hi) of sample 0, then of sample 1, per axis; weight
+    // 0 = unused; every index is a compile-time constant after unrolling (no scratch).
+    int ry[4], rx[4];
+    float wy[4], wx[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool use = i < sr;
+      const Axis a = axis_weights(y0 + ph * bh + (i + 0.5f) * bh / sr, H);
+      const Axis c = axis_weights(x0 + pw * bw + (i + 0.5f) * bw / sr, W);
+      ry[2 * i] = a.lo; ry[2 * i + 1] = a.hi;
+      wy[2 * i] = use && a.valid ? a.wlo : 0.f; wy[2 * i + 1] = use && a.valid ? a.whi : 0.f;
+      rx[2 * i] = c.lo; rx[2 * i + 1] = c.hi;
+      wx[2 * i] = use && c.valid ? c.wlo : 0.f; wx[2 * i + 1] = use && c.valid ? c.whi : 0.f;
+    }
+    // fold duplicate rows / columns into their first occurrence
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      bool fy = false, fx = false;
+#pragma unroll
+      for (int i = 0; i < j; ++i) {
+        if (!fy && ry[i] == ry[j]) { wy[i] += wy[j]; fy = true; }
+        if (!fx && rx[i] == rx[j]) { wx[i] += wx[j]; fx = true; }
+      }
+      if (fy) wy[j] = 0.f;
+      if (fx) wx[j] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (wy[i] == 0.f) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float wk = wy[i] * wx[j] * inv;
+        if (wk == 0.f) continue;
+        float* gp = gbase + (size_t)(ry[i] * W + rx[j]) * C;
+#pragma unroll
+        for (int g = 0; g < 8; ++g)
+          if (g < ng) unsafeAtomicAdd(gp + g * 64, wk * go[g]);
+      }
+    }
+    return;
+  }
   for (int iy = 0; iy < sr; ++iy) {
     const float y = y0 + ph * bh + (iy + 0.5f) * bh / sr;
     for (int ix = 0; ix < sr; ++ix) {
@@ -200,8 +266,12 @@ __global__ __launch_bounds__(64) void nms_keep_kernel(const unsigned long long* 
   const int p = blockIdx.x;
   const int lane = threadIdx.x;
   const int n = counts ? counts[p] : N;
-  // the 64 mask rows of the current chunk are staged in LDS with one coalesced batch of
-  // loads, so the serial pass waits on LDS (~100 cycles) instead of HBM per box
+  // The 64 mask rows of the current chunk are staged in LDS with one coalesced batch of
+  // loads.  The serial keep/suppress decision inside a chunk only needs each row's word
+  // for the chunk itself: lane ii holds row ii's word, and the scan reads it with a
+  // scalar readlane, so the dependent chain is a few SALU ops per box (no LDS round trip).
+  // The kept rows' suppression of later chunks is then OR-ed in parallel (lane w owns
+  // word w of the distributed removed-mask), off the serial path.
   __shared__ unsigned long long rows[64 * 64];
   unsigned long long removed = 0ull;
   int out = 0;
@@ -210,16 +280,29 @@ __global__ __launch_bounds__(64) void nms_keep_kernel(const unsigned long long* 
     const int cn = min(64, n - c0);
     for (int k = lane; k < cn * NB; k += 64) rows[k] = m[(size_t)c0 * NB + k];
     __syncthreads();
-    const unsigned long long word0 = __shfl(removed, c0 >> 6);
-    unsigned long long word = word0;
-    for (int ii = 0; ii < cn && out < max_out; ++ii) {
+    const int cw = c0 >> 6;
+    const unsigned long long intra = lane < cn ? rows[lane * NB + cw] : 0ull;
+    const unsigned lo = (unsigned)intra, hi = (unsigned)(intra >> 32);
+    unsigned long long word = __shfl(removed, cw);
+    unsigned long long kept = 0ull;
+    int room = max_out - out;
+    for (int ii = 0; ii < cn && room > 0; ++ii) {
       if ((word >> ii) & 1ull) continue;
-      if (lane == 0) keep[(size_t)p * max_out + out] = c0 + ii;
-      ++out;
-      const unsigned long long rw = lane < NB ? rows[ii * NB + lane] : 0ull;
-      removed |= rw;
-      // suppression of later boxes in this chunk comes from word (c0 >> 6) of the row
-      word |= rows[ii * NB + (c0 >> 6)];
+      kept |= 1ull << ii;
+      --room;
+      word |= ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)hi, ii) << 32) |
+              (unsigned)__builtin_amdgcn_readlane((int)lo, ii);
+    }
+    if ((kept >> lane) & 1ull)
+      keep[(size_t)p * max_out + out + __popcll(kept & ((1ull << lane) - 1ull))] = c0 + lane;
+    out += __popcll(kept);
+    if (lane < NB) {
+      unsigned long long k = kept;
+      while (k) {
+        const int ii = __ffsll((long long)k) - 1;
+        k &= k - 1ull;
+        removed |= rows[ii * NB + lane];
+      }
     }
     __syncthreads();
   }

@@ -44,6 +44,7 @@ class ConvNorm(nn.Module):
         self.norm_kind = norm
         self.norm = FrozenBN(cout) if norm == "frozen" else nn.BatchNorm2d(cout)
         self.relu = relu
+        self._fold = None   # (key, per-channel scale, folded weight or None, bias) -- see _folded()
 
     calibrating = False
 
@@ -60,12 +61,33 @@ class ConvNorm(nn.Module):
                 self.norm.weight.fill_(1.0)
                 self.norm.bias.zero_()
         if self.norm_kind == "frozen":
-            s, b = self.norm.scale_shift()
-            y = F.conv2d(x, (w * s[:, None, None, None]).to(dt), b.to(dt), self.conv.stride, self.conv.padding,
-                         self.conv.dilation)
+            wf, bf = self._folded(w, dt)
+            y = F.conv2d(x, wf, bf, self.conv.stride, self.conv.padding, self.conv.dilation)
         else:
             y = self.norm(F.conv2d(x, w.to(dt), None, self.conv.stride, self.conv.padding, self.conv.dilation))
         return F.relu(y, inplace=True) if self.relu else y
+
+    def _folded(self, w: torch.Tensor, dt: torch.dtype):
+        """FrozenBN folded into the conv: weight * s (per output channel) and bias
+        b - mean * s.  The frozen statistics change only through in-place writes
+        (calibration, checkpoint load), which bump the tensors' version counters, so the
+        per-channel affine -- and, for a conv whose weight is frozen too (stem and res2,
+        FREEZE_AT=2), the folded bf16 weight -- is cached against those versions instead
+        of being recomputed with ~8 small kernels per conv on every step."""
+        n = self.norm
+        frozen_w = not w.requires_grad
+        key = (n.weight._version, n.bias._version, n.running_mean._version, n.running_var._version,
+               w._version if frozen_w else -1, w.data_ptr() if frozen_w else 0, dt, w.device)
+        c = self._fold
+        if c is None or c[0] != key:
+            with torch.no_grad():
+                s, b = n.scale_shift()
+                s4 = s[:, None, None, None].contiguous()
+                c = self._fold = (key, s4, (w * s4).to(dt) if frozen_w else None, b.to(dt))
+        _, s4, wf, bf = c
+        if wf is None:
+            wf = (w * s4).to(dt)
+        return wf, bf
 
 
 class Bottleneck(nn.Module):

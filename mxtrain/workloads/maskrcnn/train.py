@@ -198,6 +198,9 @@ def main(argv=None):
     # MIOpen exhaustive find costs minutes on a fresh node (it times naive kernels too);
     # opt in with MXTRAIN_CONV_BENCHMARK=1 when the find-db is warm
     torch.backends.cudnn.benchmark = os.environ.get("MXTRAIN_CONV_BENCHMARK", "0") == "1"
+    # MXTRAIN_MIOPEN=0: convolutions through torch's native GEMM path instead of MIOpen
+    if os.environ.get("MXTRAIN_MIOPEN", "1") == "0":
+        torch.backends.cudnn.enabled = False
     os.makedirs(args.logdir, exist_ok=True)
     log(f"Config: world {world} x {cfg.TRAIN.BATCH_SIZE_PER_GPU} img/GPU, device {device}, "
         f"lr {cfg.TRAIN.LR:.5f}, steps/epoch {cfg.TRAIN.STEPS_PER_EPOCH}, epochs {cfg.TRAIN.MAX_EPOCH}")
@@ -354,7 +357,8 @@ def main(argv=None):
                 break
         if device.type == "cuda":
             torch.cuda.synchronize()
-        log(f"Epoch {epoch} (global_step {step}) finished, time:{time.time() - t_ep:.2f} sec.")
+        t_end = time.time()   # throughput excludes the checkpoint save / eval below
+        log(f"Epoch {epoch} (global_step {step}) finished, time:{t_end - t_ep:.2f} sec.")
         last = done or epoch == int(cfg.TRAIN.MAX_EPOCH)
         if rank == 0 and (epoch % int(cfg.TRAIN.CHECKPOINT_PERIOD) == 0 or last):
             save_ckpt(model, opt, args.logdir, step, epoch)
@@ -364,9 +368,7 @@ def main(argv=None):
         if done:
             break
     if t_timed is not None and timed_imgs:
-        if device.type == "cuda":
-            torch.cuda.synchronize()
-        ips = timed_imgs / (time.time() - t_timed)
+        ips = timed_imgs / (t_end - t_timed)
         log(f"Throughput: {ips:.2f} images/s over {timed_imgs} images ({world} ranks)")
         if args.mx_bench_json and rank == 0:
             with open(args.mx_bench_json, "a") as f:
