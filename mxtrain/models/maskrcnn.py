@@ -30,7 +30,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import vision as V
-from .resnet import resnet50
+from .compute_weights import ComputeWeights, cw
+from .resnet import ConvNorm, resnet50
 
 
 @dataclass
@@ -115,10 +116,10 @@ class FPN(nn.Module):
 
     def forward(self, feats: List[torch.Tensor]) -> List[torch.Tensor]:
         dt = feats[0].dtype
-        lat = [F.conv2d(f, m.weight.to(dt), m.bias.to(dt)) for f, m in zip(feats, self.lateral)]
+        lat = [F.conv2d(f, cw(m.weight, dt), cw(m.bias, dt)) for f, m in zip(feats, self.lateral)]
         for i in range(len(lat) - 2, -1, -1):
             lat[i] = lat[i] + F.interpolate(lat[i + 1], scale_factor=2, mode="nearest")
-        outs = [F.conv2d(x, m.weight.to(dt), m.bias.to(dt), padding=1) for x, m in zip(lat, self.output)]
+        outs = [F.conv2d(x, cw(m.weight, dt), cw(m.bias, dt), padding=1) for x, m in zip(lat, self.output)]
         outs.append(F.max_pool2d(outs[-1], 1, 2))   # P6
         return outs
 
@@ -135,9 +136,9 @@ class RPNHead(nn.Module):
 
     def forward(self, x):
         dt = x.dtype
-        t = F.relu(F.conv2d(x, self.conv.weight.to(dt), self.conv.bias.to(dt), padding=1), inplace=True)
-        lg = F.conv2d(t, self.cls.weight.to(dt), self.cls.bias.to(dt))
-        bx = F.conv2d(t, self.box.weight.to(dt), self.box.bias.to(dt))
+        t = F.relu(F.conv2d(x, cw(self.conv.weight, dt), cw(self.conv.bias, dt), padding=1), inplace=True)
+        lg = F.conv2d(t, cw(self.cls.weight, dt), cw(self.cls.bias, dt))
+        bx = F.conv2d(t, cw(self.box.weight, dt), cw(self.box.bias, dt))
         B = x.shape[0]
         # NHWC flatten -> [B, H*W*A] / [B, H*W*A, 4] (cell-major, anchor-minor)
         return lg.permute(0, 2, 3, 1).reshape(B, -1), bx.permute(0, 2, 3, 1).reshape(B, -1, 4)
@@ -164,8 +165,8 @@ class BoxHead(nn.Module):
         x = x.reshape(x.shape[0], -1)
         x = F.relu(F.linear(x, self.fc1.weight.to(dt), self.fc1.bias.to(dt)), inplace=True)
         x = F.relu(F.linear(x, self.fc2.weight.to(dt), self.fc2.bias.to(dt)), inplace=True)
-        return (F.linear(x, self.cls.weight.to(dt), self.cls.bias.to(dt)).float(),
-                F.linear(x, self.box.weight.to(dt), self.box.bias.to(dt)).float().view(x.shape[0], -1, 4))
+        return (F.linear(x, cw(self.cls.weight, dt), cw(self.cls.bias, dt)).float(),
+                F.linear(x, cw(self.box.weight, dt), cw(self.box.bias, dt)).float().view(x.shape[0], -1, 4))
 
 
 class MaskHead(nn.Module):
@@ -184,9 +185,9 @@ class MaskHead(nn.Module):
         dt = x.dtype
         x = x.permute(0, 3, 1, 2)    # NCHW view of NHWC memory (channels_last)
         for m in self.convs:
-            x = F.relu(F.conv2d(x, m.weight.to(dt), m.bias.to(dt), padding=1), inplace=True)
-        x = F.relu(F.conv_transpose2d(x, self.deconv.weight.to(dt), self.deconv.bias.to(dt), stride=2), inplace=True)
-        return F.conv2d(x, self.pred.weight.to(dt), self.pred.bias.to(dt))
+            x = F.relu(F.conv2d(x, cw(m.weight, dt), cw(m.bias, dt), padding=1), inplace=True)
+        x = F.relu(F.conv_transpose2d(x, cw(self.deconv.weight, dt), cw(self.deconv.bias, dt), stride=2), inplace=True)
+        return F.conv2d(x, cw(self.pred.weight, dt), cw(self.pred.bias, dt))
 
 
 # ---------------------------------------------------------------------------- model
@@ -333,8 +334,31 @@ class MaskRCNN(nn.Module):
         return torch.cat([bi, boxes.float()], -1).reshape(-1, 5)
 
     # ------------------------------------------------------------------ forward
+    def compute_weight_specs(self):
+        """[(trainable parameter, fold scale or None)] for the batched bf16 compute
+        copies (models/compute_weights.py): folded frozen-BN convs carry their scale."""
+        specs = []
+        folded = set()
+        for m in self.modules():
+            if isinstance(m, ConvNorm):
+                sf = m.fold_scale_full()
+                if sf is not None:
+                    specs.append((m.conv.weight, sf))
+                    folded.add(id(m.conv.weight))
+        for p in self.parameters():
+            if p.requires_grad and id(p) not in folded:
+                specs.append((p, None))
+        return specs
+
     def forward(self, images, img_hw, gt_boxes=None, gt_labels=None, gt_count=None, gt_masks=None,
                 gt_mask_table=None):
+        if images.device.type != "cuda" or not torch.is_grad_enabled():
+            return self._forward(images, img_hw, gt_boxes, gt_labels, gt_count, gt_masks, gt_mask_table)
+        with ComputeWeights(self.compute_weight_specs(), self.compute_dtype(images.device)):
+            return self._forward(images, img_hw, gt_boxes, gt_labels, gt_count, gt_masks, gt_mask_table)
+
+    def _forward(self, images, img_hw, gt_boxes=None, gt_labels=None, gt_count=None, gt_masks=None,
+                 gt_mask_table=None):
         """Training: returns dict of losses.  images [B,3,H,W] (padded), img_hw [B,2] real
         sizes, gt_* padded to G per image; gt_masks uint8 [B, G, H, W], or (with
         gt_mask_table int32 [B, G, 5]) the flat uint8 buffer of packed instance crops."""

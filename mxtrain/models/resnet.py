@@ -18,6 +18,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import compute_weights as _cw
+
 
 class FrozenBN(nn.Module):
     def __init__(self, c: int, eps: float = 1e-5):
@@ -86,8 +88,24 @@ class ConvNorm(nn.Module):
                 c = self._fold = (key, s4, (w * s4).to(dt) if frozen_w else None, b.to(dt))
         _, s4, wf, bf = c
         if wf is None:
-            wf = (w * s4).to(dt)
+            wf = _cw.cw(w, dt) if _cw.has(w) else (w * s4).to(dt)
         return wf, bf
+
+    def fold_scale_full(self) -> Optional[torch.Tensor]:
+        """The FrozenBN scale broadcast to the conv weight's shape (cached against the
+        statistics' versions), for the batched compute-weight fold
+        (models/compute_weights.py); None unless this is a trainable frozen-BN conv."""
+        w = self.conv.weight
+        if self.norm_kind != "frozen" or not w.requires_grad:
+            return None
+        n = self.norm
+        key = (n.weight._version, n.bias._version, n.running_mean._version, n.running_var._version, w.device)
+        c = getattr(self, "_sfull", None)
+        if c is None or c[0] != key:
+            with torch.no_grad():
+                s, _ = n.scale_shift()
+                c = self._sfull = (key, s[:, None, None, None].expand_as(w).contiguous())
+        return c[1]
 
 
 class Bottleneck(nn.Module):

@@ -231,3 +231,36 @@ def test_model_losses_crops_equal_full(coco_dir):
             out.append(m(b["images"], b["hw"], b["gt_boxes"], b["gt_labels"], b["gt_count"], masks, table))
     for k in out[0]:
         torch.testing.assert_close(out[0][k], out[1][k], rtol=1e-5, atol=1e-6)
+
+
+def test_compute_weights_batched_cast_matches_per_tensor_casts():
+    """models/compute_weights.py: one autograd node producing every bf16 compute copy
+    (with a folded per-channel scale) gives the same outputs and fp32 gradients as the
+    per-module casts it replaces."""
+    import torch.nn.functional as F
+    from mxtrain.models.compute_weights import ComputeWeights, cw
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(8, 4)
+    conv = torch.nn.Conv2d(3, 5, 3)
+    s = (torch.rand(5, 1, 1, 1) + 0.5).expand_as(conv.weight).contiguous()
+    x = torch.randn(2, 8).bfloat16()
+    xi = torch.randn(2, 3, 6, 6).bfloat16()
+    bf = torch.bfloat16
+
+    def step(batched):
+        for p in (lin.weight, lin.bias, conv.weight):
+            p.grad = None
+        specs = [(conv.weight, s), (lin.weight, None), (lin.bias, None)]
+        with ComputeWeights(specs if batched else [], bf):
+            wc = cw(conv.weight, bf) if batched else (conv.weight * s).to(bf)
+            y = F.conv2d(xi, wc).float().square().sum() + F.linear(x, cw(lin.weight, bf), cw(lin.bias, bf)).float().square().sum()
+        y.backward()
+        return float(y), [p.grad.clone() for p in (lin.weight, lin.bias, conv.weight)]
+
+    ya, ga = step(False)
+    yb, gb = step(True)
+    # (the batched conv copy is channels_last, so the bf16 conv may sum in another order)
+    assert abs(ya - yb) <= 1e-5 * abs(ya)
+    for a, b in zip(ga[:2], gb[:2]):
+        assert a.dtype == torch.float32 and torch.equal(a, b)
+    assert gb[2].dtype == torch.float32 and torch.allclose(ga[2], gb[2], rtol=2e-2, atol=1e-2)
