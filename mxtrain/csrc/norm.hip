@@ -160,6 +160,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const float rstd = rstd_in[row];
     float xh[NV][8], gy[NV][8];
     float s1 = 0.f, s2 = 0.f;
+    // the residual gradient is loaded with h and dy, before the row reductions, so its
+    // HBM latency overlaps theirs instead of following the two wave_sum()s
+    uint4 rraw[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (lane + 64 * i) * 8;
+      rraw[i] = (dres && c < cols) ? *reinterpret_cast<const uint4*>(dres + base + c) : make_uint4(0, 0, 0, 0);
+    }
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (lane + 64 * i) * 8;
@@ -193,11 +201,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       const int c = (lane + 64 * i) * 8;
       if (c < cols) {
         float r[8], o[8];
-        if (dres) unpack8(*reinterpret_cast<const uint4*>(dres + base + c), r);
-        else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) r[j] = 0.f;
-        }
+        unpack8(rraw[i], r);   // zeros when there is no residual gradient
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = r[j] + rstd * (gy[i][j] - m1 - xh[i][j] * m2);
         *reinterpret_cast<uint4*>(dh_out + base + c) = pack8(o);

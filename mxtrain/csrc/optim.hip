@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(
 }
 
 int g_adam_unroll = 1;
-int g_adam_blocks = 4096;
+int g_adam_blocks = 16384;   // kbench: 2056 us vs 2122 us at 4096 blocks (355M elements)
 
 }  // namespace
 
