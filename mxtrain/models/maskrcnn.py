@@ -163,8 +163,8 @@ class BoxHead(nn.Module):
     def forward(self, x):
         dt = x.dtype
         x = x.reshape(x.shape[0], -1)
-        x = F.relu(F.linear(x, self.fc1.weight.to(dt), self.fc1.bias.to(dt)), inplace=True)
-        x = F.relu(F.linear(x, self.fc2.weight.to(dt), self.fc2.bias.to(dt)), inplace=True)
+        x = F.relu(F.linear(x, cw(self.fc1.weight, dt), cw(self.fc1.bias, dt)), inplace=True)
+        x = F.relu(F.linear(x, cw(self.fc2.weight, dt), cw(self.fc2.bias, dt)), inplace=True)
         return (F.linear(x, cw(self.cls.weight, dt), cw(self.cls.bias, dt)).float(),
                 F.linear(x, cw(self.box.weight, dt), cw(self.box.bias, dt)).float().view(x.shape[0], -1, 4))
 
@@ -337,17 +337,29 @@ class MaskRCNN(nn.Module):
     def compute_weight_specs(self):
         """[(trainable parameter, fold scale or None)] for the batched bf16 compute
         copies (models/compute_weights.py): folded frozen-BN convs carry their scale."""
+        cache = self.__dict__.get("_cw_cache")
+        if cache is None:
+            convs = [m for m in self.modules() if isinstance(m, ConvNorm)]
+            cache = self.__dict__["_cw_cache"] = [convs, list(self.parameters()), None, None]
+        convs, params, key, specs = cache
+        # the list only changes when frozen statistics are rewritten (calibration,
+        # checkpoint load: version bumps) or parameters are (un)frozen
+        nkey = (tuple(m.norm.running_var._version + m.norm.running_mean._version + m.norm.weight._version
+                      + m.norm.bias._version for m in convs if m.norm_kind == "frozen"),
+                tuple(p.requires_grad for p in params))
+        if nkey == key:
+            return specs
         specs = []
         folded = set()
-        for m in self.modules():
-            if isinstance(m, ConvNorm):
-                sf = m.fold_scale_full()
-                if sf is not None:
-                    specs.append((m.conv.weight, sf))
-                    folded.add(id(m.conv.weight))
-        for p in self.parameters():
+        for m in convs:
+            sf = m.fold_scale_full()
+            if sf is not None:
+                specs.append((m.conv.weight, sf))
+                folded.add(id(m.conv.weight))
+        for p in params:
             if p.requires_grad and id(p) not in folded:
                 specs.append((p, None))
+        cache[2], cache[3] = nkey, specs
         return specs
 
     def forward(self, images, img_hw, gt_boxes=None, gt_labels=None, gt_count=None, gt_masks=None,
