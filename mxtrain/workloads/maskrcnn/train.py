@@ -195,9 +195,18 @@ def main(argv=None):
     C.finalize(cfg, world, args.images_per_epoch)
     if device.type == "cuda" and hasattr(torch.backends.cuda, "preferred_blas_library"):
         torch.backends.cuda.preferred_blas_library("hipblaslt")
-    # MIOpen exhaustive find costs minutes on a fresh node (it times naive kernels too);
-    # opt in with MXTRAIN_CONV_BENCHMARK=1 when the find-db is warm
-    torch.backends.cudnn.benchmark = os.environ.get("MXTRAIN_CONV_BENCHMARK", "0") == "1"
+    # Convolution algorithm search: torch's benchmark mode runs MIOpen find once per conv
+    # shape and caches the choice, so a steady-state conv call skips the per-call solution
+    # query of immediate mode (~30 us host per call, ~240 calls per step) and gets the
+    # found solver.  MIOPEN_FIND_MODE=FAST keeps the search to the fast candidates.
+    # Measured on one MI355X: 1 img/GPU 51 -> 66 img/s, 4 img/GPU 108 -> 129 img/s; the
+    # one-time search costs ~4 minutes on a fresh node (MIOpen's user find-db keeps it for
+    # later runs).  MXTRAIN_CONV_BENCHMARK=0 returns to immediate mode.
+    torch.backends.cudnn.benchmark = os.environ.get("MXTRAIN_CONV_BENCHMARK", "1") == "1"
+    if torch.backends.cudnn.benchmark:
+        os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+        log("Convolution algorithm search on (MIOpen find, FAST mode): the first steps of each "
+            "input shape take minutes on a node without a MIOpen find-db")
     # MXTRAIN_MIOPEN=0: convolutions through torch's native GEMM path instead of MIOpen
     if os.environ.get("MXTRAIN_MIOPEN", "1") == "0":
         torch.backends.cudnn.enabled = False
