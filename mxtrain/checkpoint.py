@@ -283,5 +283,6 @@ def load_checkpoint(load_dir: str, trainer, load_optim: bool = True) -> Optional
         info["consumed_samples"] = it * trainer.global_batch
     trainer.iteration = it
     # dropout stream continues where it stopped (one advance per optimizer step)
-    trainer.seed.set_step(trainer.tcfg.seed + 7 * (ps.dp_rank * ps.cp + ps.cp_rank), trainer.opt.step_count)
+    hid_seed, attn_seed = trainer.seed_bases(trainer.tcfg, ps)
+    trainer.seed.set_step(hid_seed, trainer.opt.step_count, attn_seed=attn_seed)
     return info

@@ -29,6 +29,18 @@
 // global atomics (one 256-B wave-instruction per row: the full-rate shape of
 // MI355X_MICROARCH.md "Global float atomics"), converted to bf16 once.
 //
+// Attention dropout (Megatron --attention-dropout, HF attention_probs_dropout_prob): the
+// keep-mask M[b,h,q,k] is a pure function of (seed, global row, key) --
+//   keep <=> ((hash32(row * 0x85EBCA6B + (k >> 1), seed) >> 16 * (k & 1)) & 0xFFFF) >= thr16,
+//   row = (b * Hg + h_global) * S + q
+// (16-bit threshold: p is exact to 2^-16).  attn_dropmask_kernel evaluates it once per
+// forward into two lane-bit images, one per MFMA accumulator layout: the forward's
+// query-on-lane image (one 8-B word per lane per 128-key tile) and the backward's
+// key-on-lane image (one 2-B word per lane per 32x32 block).  The main loops then pay two
+// VALU ops per element (v_bfe_i32 + v_and on P); dS = P (Z dP~ - delta) with Z = M/(1-p)
+// is formed with one v_bfi per element from a -delta(1-p) accumulator preload, and the
+// 1/(1-p) factors are folded into the O / dK / dV / dQ epilogue scales.
+//
 // Every LDS tile uses a 16-B chunk XOR swizzle chosen so that both the row reads
 // (ds_read_b128 of 32 different rows) and the transposed reads (4 consecutive rows x
 // 32 columns per half-wave) are bank-conflict free (derivation in Swz below).
@@ -103,19 +115,74 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// ============================================================================ dropout mask
+// One wave per 32x32 (query block, key block).  Lane (r, hh) owns query 32qb + r and, in
+// the forward image, keys crow(e, hh) = (e&3) + 8(e>>2) + 4hh of the block (e = 0..15, the
+// 32x32 accumulator rows of a lane); its 16 keep bits are 8 hashes.  The backward image
+// (lane = key, e -> query crow(e, hh)) is the transpose, formed through LDS.
+__device__ __forceinline__ int crow(int e, int hh) { return (e & 3) + 8 * (e >> 2) + 4 * hh; }
+
+__global__ __launch_bounds__(64) void attn_dropmask_kernel(
+    const uint32_t* __restrict__ seed_ptr, uint32_t salt, uint32_t thr16, int S, int Hq,
+    int h_off, int Hg, int NB, int NKT, int causal, uint16_t* __restrict__ fwd_bits,
+    uint16_t* __restrict__ bwd_bits) {
+  const int qb = blockIdx.x, kb = blockIdx.y, bh = blockIdx.z;
+  if (causal && kb > qb) return;  // never read (whole block above the diagonal)
+  const int b = bh / Hq, h = bh - b * Hq;
+  const uint32_t seed = *seed_ptr + salt;
+  const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
+  const uint32_t row = (uint32_t)(((long long)b * Hg + h_off + h) * S + qb * 32 + r);
+  const uint32_t rbase = row * 0x85EBCA6Bu;
+  uint32_t fbits = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const uint32_t kp = (uint32_t)(kb * 16 + 4 * j + 2 * hh + half);
+      const uint32_t hv = hash32(rbase + kp, seed);
+      const int e = 4 * j + 2 * half;
+      fbits |= (uint32_t)((hv & 0xFFFFu) >= thr16) << e;
+      fbits |= (uint32_t)((hv >> 16) >= thr16) << (e + 1);
+    }
+  // forward image: [bh][qb][kt = kb/4][lane] u64, 16 bits per key block (kb % 4)
+  fwd_bits[((((size_t)bh * NB + qb) * NKT + (kb >> 2)) * 64 + lane) * 4 + (kb & 3)] = (uint16_t)fbits;
+  __shared__ uint16_t fw[64];
+  fw[lane] = (uint16_t)fbits;
+  __syncthreads();
+  // backward image: lane = key kl; element e = query crow(e, hh) -> forward lane
+  // crow(e, hh) + 32 * ((kl >> 2) & 1), forward bit (kl & 3) + 4 (kl >> 3)
+  const int kl = r;
+  const int fbit = (kl & 3) + 4 * (kl >> 3), fhi = 32 * ((kl >> 2) & 1);
+  uint32_t bbits = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) bbits |= (((uint32_t)fw[crow(e, hh) + fhi] >> fbit) & 1u) << e;
+  bwd_bits[(((size_t)bh * NB + kb) * NB + qb) * 64 + lane] = (uint16_t)bbits;
+}
+
+// p if element bit `bit` of `m` is set, else +0 (v_bfe_i32 + v_and)
+__device__ __forceinline__ float keep_or_zero(float p, uint32_t m, int bit) {
+  return __uint_as_float(__float_as_uint(p) & (uint32_t)__builtin_amdgcn_sbfe((int)m, (uint32_t)bit, 1u));
+}
+// x if the bit is set else y (v_bfe_i32 + v_bfi_b32)
+__device__ __forceinline__ float keep_sel(float x, float y, uint32_t m, int bit) {
+  const uint32_t mk = (uint32_t)__builtin_amdgcn_sbfe((int)m, (uint32_t)bit, 1u);
+  return __uint_as_float((__float_as_uint(x) & mk) | (__float_as_uint(y) & ~mk));
+}
+
 // ============================================================================ forward
 // Workgroup = 8 waves = two 128-row query blocks.  Causal: the pair (i, nqb-1-i), so every
 // workgroup does the same number of K/V tiles (light block + its mirrored heavy block)
 // and the grid is exactly one workgroup per CU with no tail; the two halves share every
 // K/V tile staged in LDS.  Non-causal: blocks (2i, 2i+1).
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool DROP>
 // waves_per_eu(2,2): one 8-wave workgroup per CU is the design point, so let the
 // scheduler spend the full 256-VGPR budget on read batching instead of occupancy.
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, int ldq, int ldk, int ldv, uint16_t* __restrict__ o,
     int ldo, float* __restrict__ lse, int S, int Hq, int Hkv, const int* __restrict__ klen,
-    float c /* scale*log2(e) */) {
+    float c /* scale*log2(e) */, const uint64_t* __restrict__ dbits, int NB, int NKT,
+    float oscale /* 1/(1-p) */) {
   // 128-key K/V tiles: one tile of compute per wave must cover the HBM latency of the
   // next tile's register-staged prefetch (64-key tiles left the loop latency-bound)
   constexpr int BQ = 128, BK = 128, NSUB = BK / 32, NKK = D / 16, NDT = D / 32;
@@ -197,6 +264,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) oacc[dt] = f32x16{};
 
+  // dropout bits of this lane's query row: one 8-B word per 128-key tile (4 x 16 bits)
+  const uint64_t* dmrow = DROP ? dbits + ((size_t)(b * Hq + hq) * NB + (qw >> 5)) * NKT * 64 + lane : nullptr;
+  uint64_t dm_cur = 0, dm_next = 0;
+  if constexpr (DROP) {
+    if (nt > 0 && half_on && qw < S) dm_cur = dmrow[0];
+  }
   if (nt > 0) {
     FWD_GLOAD(0);
     FWD_SWRITE(0);
@@ -227,7 +300,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     // T14: the next tile's global loads are issued only after QK^T, so their latency
     // hides under softmax + PV and no wait lands in front of the first MFMA
-    if (j + 1 < nt) { FWD_GLOAD(j + 1); }
+    if (j + 1 < nt) {
+      FWD_GLOAD(j + 1);
+      if constexpr (DROP) {
+        if (half_on && qw < S && (!CAUSAL || qw + 31 >= (j + 1) * BK)) dm_next = dmrow[(size_t)(j + 1) * 64];
+      }
+    }
     if (active) {
       const bool need_mask = (CAUSAL && kv0 + 32 * nsub - 1 > qw) || (kv0 + BK > kl);
       if (need_mask) {
@@ -271,8 +349,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const float p = __builtin_amdgcn_exp2f(sacc[t][e] * c - mc);
-            sacc[t][e] = p;
-            rs += p;
+            rs += p;  // the normaliser sums the undropped probabilities
+            sacc[t][e] = DROP ? keep_or_zero(p, (uint32_t)(dm_cur >> (16 * t)), e) : p;
           }
         }
       l_i += rs;
@@ -297,11 +375,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
     }
     if (j + 1 < nt) { FWD_SWRITE((j + 1) & 1); }
+    if constexpr (DROP) dm_cur = dm_next;
     __syncthreads();
   }
 
   const float lt = xhalf_sum(l_i);
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  const float inv = lt > 0.f ? oscale / lt : 0.f;
   if (half_on && qrow < S) {
     uint16_t* op = o + (size_t)(b * S + qrow) * ldo + hq * D;
 #pragma unroll
@@ -365,14 +444,15 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(
 // ~100 spilled to scratch, 7.5x the forward time), so it runs as two passes that each
 // accumulate half of the dK/dV columns: DP = 1 (columns 0-63, plus dQ), DP = 2 (columns
 // 64-127, S and dP recomputed, no dQ).  1.4x the MFMA work, no scratch traffic.
-template <int D, bool CAUSAL, int DP = 0>
+template <int D, bool CAUSAL, int DP, bool DROP>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, int ldq, int ldk, int ldv,
     const uint16_t* __restrict__ dout, int lddo, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dq_acc, int lddq,
     uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, int lddk, int lddv, int S, int Hq,
-    int Hkv, const int* __restrict__ klen, float c, float scale) {
+    int Hkv, const int* __restrict__ klen, float c, float dkscale, float dvscale,
+    const uint16_t* __restrict__ dbitsT, int NB, float dkeep /* 1-p */) {
   constexpr int KB = 128, KW = 256, QT = 32, NKK = D / 16, NDT = D / 32;
   constexpr int NDL = DP == 0 ? NDT : NDT / 2;      // dK/dV column tiles of this pass
   constexpr int DT0 = DP == 2 ? NDT / 2 : 0;        // first column tile of this pass
@@ -456,9 +536,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   uint4 qreg[QCH], dreg[QCH];
   float lreg = 0.f, dlreg = 0.f;
   int lq = 0;
+  uint32_t dm_next = 0;
   auto gload = [&](int it) {
     const int hq = hk * grp + it / per_head;
     const int qs = (qt0 + it % per_head) * QT;
+    if constexpr (DROP) {  // key-on-lane dropout bits of this wave's 32x32 block
+      if (half_on && kw0 < S && (!CAUSAL || qs + QT - 1 >= kw0))
+        dm_next = dbitsT[(((size_t)(b * Hq + hq) * NB + (kw0 >> 5)) * NB + (qs >> 5)) * 64 + lane];
+    }
     // rows past S are clamped (finite duplicates; their P is forced to 0 via lse=-inf)
 #pragma unroll
     for (int i = 0; i < QCH; ++i) {
@@ -490,7 +575,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     if (tid < QT) {
       reinterpret_cast<float*>(smem + OFF_L)[buf * QT + tid] = lq < S ? -lreg / c : -INFINITY;
-      reinterpret_cast<float*>(smem + OFF_DL)[buf * QT + tid] = lq < S ? -dlreg : 0.f;
+      reinterpret_cast<float*>(smem + OFF_DL)[buf * QT + tid] = lq < S ? -dlreg * dkeep : 0.f;
     }
   };
 
@@ -502,9 +587,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   char* dsimg = smem + OFF_DS;
   float* dqimg = reinterpret_cast<float*>(smem + OFF_DQ);
   const int krow = KB * half + 32 * wl + r;  // this lane's row in the dS^T image / K tile
+  uint32_t dm = 0;
   for (int it = 0; it < total; ++it) {
     const int hq = hk * grp + it / per_head;
     const int qs = (qt0 + it % per_head) * QT;
+    if constexpr (DROP) dm = dm_next;
     if (it + 1 < total) gload(it + 1);
     const int buf = it & 1;
     const char* Qt = smem + OFF_Q + buf * QTILE;
@@ -559,10 +646,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           sacc[e] = dead ? 0.f : sacc[e];
         }
       }
+      if constexpr (DROP) {
+        // dpacc = dP~ - delta(1-p): kept -> P * dpacc, dropped -> P * (-delta(1-p)) (the
+        // common 1/(1-p) is in dkscale / the dQ scale); dV^T takes the dropped P
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const float p = sacc[e];
-        dpacc[e] = p * dpacc[e];
+        for (int e = 0; e < 16; ++e) {
+          const float p = sacc[e];
+          const int ql = (e & 3) + 8 * (e >> 2) + 4 * hh;
+          dpacc[e] = p * keep_sel(dpacc[e], DLs[ql], dm, e);
+          sacc[e] = keep_or_zero(p, dm, e);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float p = sacc[e];
+          dpacc[e] = p * dpacc[e];
+        }
       }
       constexpr int SUNROLL = D <= 64 ? 2 : 1;   // D=128: don't hoist both halves' reads
 #pragma unroll SUNROLL
@@ -663,11 +762,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int g4 = 0; g4 < 4; ++g4) {
         const int d = 32 * (dt + DT0) + 8 * g4 + 4 * hh;
         uint2 u;
-        u.x = pack2(dkacc[dt][4 * g4 + 0] * scale, dkacc[dt][4 * g4 + 1] * scale);
-        u.y = pack2(dkacc[dt][4 * g4 + 2] * scale, dkacc[dt][4 * g4 + 3] * scale);
+        u.x = pack2(dkacc[dt][4 * g4 + 0] * dkscale, dkacc[dt][4 * g4 + 1] * dkscale);
+        u.y = pack2(dkacc[dt][4 * g4 + 2] * dkscale, dkacc[dt][4 * g4 + 3] * dkscale);
         *reinterpret_cast<uint2*>(dkp + d) = u;
-        u.x = pack2(dvacc[dt][4 * g4 + 0], dvacc[dt][4 * g4 + 1]);
-        u.y = pack2(dvacc[dt][4 * g4 + 2], dvacc[dt][4 * g4 + 3]);
+        u.x = pack2(dvacc[dt][4 * g4 + 0] * dvscale, dvacc[dt][4 * g4 + 1] * dvscale);
+        u.y = pack2(dvacc[dt][4 * g4 + 2] * dvscale, dvacc[dt][4 * g4 + 3] * dvscale);
         *reinterpret_cast<uint2*>(dvp + d) = u;
       }
   }
@@ -690,69 +789,97 @@ __global__ __launch_bounds__(256) void dq_convert_kernel(const float* __restrict
 }
 
 template <int D>
-hipError_t fwd_dispatch(bool causal, dim3 grid, hipStream_t s, const uint16_t* q,
+hipError_t fwd_dispatch(bool causal, bool drop, dim3 grid, hipStream_t s, const uint16_t* q,
                         const uint16_t* k, const uint16_t* v, int ldq, int ldk, int ldv,
                         uint16_t* o, int ldo, float* lse, int S, int Hq, int Hkv,
-                        const int* klen, float c) {
-  if (causal)
-    hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(512), 0, s, q, k, v, ldq, ldk,
-                       ldv, o, ldo, lse, S, Hq, Hkv, klen, c);
-  else
-    hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(512), 0, s, q, k, v, ldq, ldk,
-                       ldv, o, ldo, lse, S, Hq, Hkv, klen, c);
+                        const int* klen, float c, const uint64_t* dbits, int NB, int NKT,
+                        float oscale) {
+#define MX_ATTN_FWD(C, DR)                                                                  \
+  hipLaunchKernelGGL((attn_fwd_kernel<D, C, DR>), grid, dim3(512), 0, s, q, k, v, ldq, ldk, ldv, o, \
+                     ldo, lse, S, Hq, Hkv, klen, c, dbits, NB, NKT, oscale)
+  if (causal) {
+    if (drop) MX_ATTN_FWD(true, true); else MX_ATTN_FWD(true, false);
+  } else {
+    if (drop) MX_ATTN_FWD(false, true); else MX_ATTN_FWD(false, false);
+  }
+#undef MX_ATTN_FWD
   return hipGetLastError();
 }
 
 template <int D>
-hipError_t bwd_dispatch(bool causal, dim3 grid, hipStream_t s, const uint16_t* q,
+hipError_t bwd_dispatch(bool causal, bool drop, dim3 grid, hipStream_t s, const uint16_t* q,
                         const uint16_t* k, const uint16_t* v, int ldq, int ldk, int ldv,
                         const uint16_t* dout, int lddo, const float* lse, const float* delta,
                         float* dq_acc, int lddq, uint16_t* dk, uint16_t* dv, int lddk, int lddv,
-                        int S, int Hq, int Hkv, const int* klen, float c, float scale) {
-#define MX_ATTN_BWD(C, P)                                                                  \
-  hipLaunchKernelGGL((attn_bwd_kernel<D, C, P>), grid, dim3(512), 0, s, q, k, v, ldq, ldk, ldv, \
-                     dout, lddo, lse, delta, dq_acc, lddq, dk, dv, lddk, lddv, S, Hq, Hkv, klen, \
-                     c, scale)
+                        int S, int Hq, int Hkv, const int* klen, float c, float dkscale,
+                        float dvscale, const uint16_t* dbitsT, int NB, float dkeep) {
+#define MX_ATTN_BWD(C, P, DR)                                                              \
+  hipLaunchKernelGGL((attn_bwd_kernel<D, C, P, DR>), grid, dim3(512), 0, s, q, k, v, ldq, ldk,  \
+                     ldv, dout, lddo, lse, delta, dq_acc, lddq, dk, dv, lddk, lddv, S, Hq, Hkv,   \
+                     klen, c, dkscale, dvscale, dbitsT, NB, dkeep)
+#define MX_ATTN_BWD_P(C, P) \
+  { if (drop) MX_ATTN_BWD(C, P, true); else MX_ATTN_BWD(C, P, false); }
   if constexpr (D <= 64) {
-    if (causal) MX_ATTN_BWD(true, 0);
-    else MX_ATTN_BWD(false, 0);
+    if (causal) MX_ATTN_BWD_P(true, 0)
+    else MX_ATTN_BWD_P(false, 0)
   } else {
-    if (causal) { MX_ATTN_BWD(true, 1); MX_ATTN_BWD(true, 2); }
-    else { MX_ATTN_BWD(false, 1); MX_ATTN_BWD(false, 2); }
+    if (causal) { MX_ATTN_BWD_P(true, 1) MX_ATTN_BWD_P(true, 2) }
+    else { MX_ATTN_BWD_P(false, 1) MX_ATTN_BWD_P(false, 2) }
   }
+#undef MX_ATTN_BWD_P
 #undef MX_ATTN_BWD
   return hipGetLastError();
 }
 
 }  // namespace
 
+// Dropout keep-mask images for one attention call (see the header comment).
+// fwd_bits: u16 [B*Hq][NB][NKT*4][64] (NB = ceil(S/32), NKT = ceil(NB/4));
+// bwd_bits: u16 [B*Hq][NB][NB][64].  h_off / Hg: this rank's first global head / the
+// model's head count (so tensor/context-parallel shards draw the single-GPU mask).
+MX_EXPORT int mx_attn_dropmask(const uint32_t* seed, uint32_t salt, float p, int B, int S, int Hq,
+                               int h_off, int Hg, int causal, void* fwd_bits, void* bwd_bits,
+                               hipStream_t s) {
+  const int NB = (S + 31) / 32, NKT = (NB + 3) / 4;
+  const uint32_t thr16 = (uint32_t)(p * 65536.0f + 0.5f);
+  hipLaunchKernelGGL(attn_dropmask_kernel, dim3(NB, NB, B * Hq), dim3(64), 0, s, seed, salt, thr16,
+                     S, Hq, h_off, Hg, NB, NKT, causal, (uint16_t*)fwd_bits, (uint16_t*)bwd_bits);
+  return hipGetLastError();
+}
+
 // Q/K/V/O are bf16 with token strides ld*; head h lives at column h*D.
 // lse: fp32 [B, Hq, S] (base 2).  klen: int32 [B] valid key count or null.
+// fwd_bits: dropout image from mx_attn_dropmask or null (no dropout); keep_scale = 1/(1-p).
 MX_EXPORT int mx_attn_fwd(const void* q, const void* k, const void* v, int ldq, int ldk,
                           int ldv, void* o, int ldo, float* lse, int B, int S, int Hq, int Hkv,
-                          int D, int causal, const int* klen, float scale, hipStream_t s) {
+                          int D, int causal, const int* klen, float scale, const void* fwd_bits,
+                          float keep_scale, hipStream_t s) {
   if (Hq % Hkv) return hipErrorInvalidValue;
   const float c = scale * 1.4426950408889634f;
   const int nqb = (S + 127) / 128;
+  const int NB = (S + 31) / 32, NKT = (NB + 3) / 4;
   dim3 grid((nqb + 1) / 2, Hq, B);
+  const bool drop = fwd_bits != nullptr;
+  const float osc = drop ? keep_scale : 1.f;
   if (D == 64)
-    return fwd_dispatch<64>(causal, grid, s, (const uint16_t*)q, (const uint16_t*)k,
+    return fwd_dispatch<64>(causal, drop, grid, s, (const uint16_t*)q, (const uint16_t*)k,
                             (const uint16_t*)v, ldq, ldk, ldv, (uint16_t*)o, ldo, lse, S, Hq,
-                            Hkv, klen, c);
+                            Hkv, klen, c, (const uint64_t*)fwd_bits, NB, NKT, osc);
   if (D == 128)
-    return fwd_dispatch<128>(causal, grid, s, (const uint16_t*)q, (const uint16_t*)k,
+    return fwd_dispatch<128>(causal, drop, grid, s, (const uint16_t*)q, (const uint16_t*)k,
                              (const uint16_t*)v, ldq, ldk, ldv, (uint16_t*)o, ldo, lse, S, Hq,
-                             Hkv, klen, c);
+                             Hkv, klen, c, (const uint64_t*)fwd_bits, NB, NKT, osc);
   return hipErrorInvalidValue;
 }
 
-// dq_acc: fp32 [B*S, Hq*D] zero-initialised workspace; delta: fp32 [B, Hq, S] workspace.
+// dq_acc: fp32 [B*S, Hq*D] workspace (zeroed here); delta: fp32 [B, Hq, S] workspace.
+// bwd_bits: the dropout image of the forward (or null); keep_scale = 1/(1-p).
 MX_EXPORT int mx_attn_bwd(const void* q, const void* k, const void* v, int ldq, int ldk,
                           int ldv, const void* o, int ldo, const void* dout, int lddo,
                           const float* lse, float* delta, float* dq_acc, void* dq, int lddq,
                           void* dk, void* dv, int lddk, int lddv, int B, int S, int Hq,
                           int Hkv, int D, int causal, const int* klen, float scale,
-                          hipStream_t s) {
+                          const void* bwd_bits, float keep_scale, hipStream_t s) {
   if (Hq % Hkv) return hipErrorInvalidValue;
   const float c = scale * 1.4426950408889634f;
   {
@@ -769,22 +896,26 @@ MX_EXPORT int mx_attn_bwd(const void* q, const void* k, const void* v, int ldq, 
       return hipErrorInvalidValue;
   }
   const int nkb = (S + 127) / 128;
+  const int NB = (S + 31) / 32;
   dim3 grid((nkb + 1) / 2, Hkv, B);
   const int lddq_acc = Hq * D;
+  const bool drop = bwd_bits != nullptr;
+  const float ks = drop ? keep_scale : 1.f;
+  const float dkeep = drop ? 1.f / keep_scale : 1.f;
   hipError_t e;
   if (D == 64)
-    e = bwd_dispatch<64>(causal, grid, s, (const uint16_t*)q, (const uint16_t*)k,
+    e = bwd_dispatch<64>(causal, drop, grid, s, (const uint16_t*)q, (const uint16_t*)k,
                          (const uint16_t*)v, ldq, ldk, ldv, (const uint16_t*)dout, lddo, lse,
                          delta, dq_acc, lddq_acc, (uint16_t*)dk, (uint16_t*)dv, lddk, lddv, S,
-                         Hq, Hkv, klen, c, scale);
+                         Hq, Hkv, klen, c, scale * ks, ks, (const uint16_t*)bwd_bits, NB, dkeep);
   else
-    e = bwd_dispatch<128>(causal, grid, s, (const uint16_t*)q, (const uint16_t*)k,
+    e = bwd_dispatch<128>(causal, drop, grid, s, (const uint16_t*)q, (const uint16_t*)k,
                           (const uint16_t*)v, ldq, ldk, ldv, (const uint16_t*)dout, lddo, lse,
                           delta, dq_acc, lddq_acc, (uint16_t*)dk, (uint16_t*)dv, lddk, lddv, S,
-                          Hq, Hkv, klen, c, scale);
+                          Hq, Hkv, klen, c, scale * ks, ks, (const uint16_t*)bwd_bits, NB, dkeep);
   if (e != hipSuccess) return e;
   const int64_t nv = (int64_t)B * S * Hq * D / 8;
   hipLaunchKernelGGL(dq_convert_kernel, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s,
-                     dq_acc, lddq_acc, (uint16_t*)dq, lddq, B * S, Hq * D, scale);
+                     dq_acc, lddq_acc, (uint16_t*)dq, lddq, B * S, Hq * D, scale * ks);
   return hipGetLastError();
 }

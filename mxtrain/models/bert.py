@@ -45,7 +45,7 @@ class BertConfig:
     max_position_embeddings: int = 512
     type_vocab_size: int = 2
     hidden_dropout_prob: float = 0.1
-    attention_probs_dropout_prob: float = 0.1   # not applied inside the flash kernel
+    attention_probs_dropout_prob: float = 0.1   # applied to P inside the flash kernels
     layer_norm_eps: float = 1e-12
     initializer_range: float = 0.02
     num_labels: int = 2
@@ -88,13 +88,14 @@ class BertLayer(nn.Module):
         self.ln2_weight = nn.Parameter(torch.ones(h))
         self.ln2_bias = nn.Parameter(torch.zeros(h))
 
-    def forward(self, x, B, S, klen, p, seed_t, dt):
+    def forward(self, x, B, S, klen, p, seed_t, dt, pa=0.0):
         cfg = self.cfg
         H, D = cfg.num_attention_heads, cfg.head_dim
         h = cfg.hidden_size
         qkv = F.linear(x, _c(self.qkv_weight, dt), _c(self.qkv_bias, dt))
         q, k, v = qkv[:, :h], qkv[:, h:2 * h], qkv[:, 2 * h:]
-        ctx = flash_attention(q, k, v, B, S, H, H, D, causal=False, klen=klen, scale=1.0 / math.sqrt(D))
+        ctx = flash_attention(q, k, v, B, S, H, H, D, causal=False, klen=klen, scale=1.0 / math.sqrt(D),
+                              dropout_p=pa, seed_t=seed_t, salt=30011 + self.index)
         a = F.linear(ctx, _c(self.attn_out_weight, dt))
         salt = 101 + 2 * self.index
         x1 = bda_norm(a, _c(self.attn_out_bias, dt), x, _c(self.ln1_weight, dt), _c(self.ln1_bias, dt),
@@ -169,8 +170,9 @@ class BertForSequenceClassification(nn.Module):
         seed = self._seed(dev)
         if self.training:
             seed.advance()
+        pa = cfg.attention_probs_dropout_prob if self.training else 0.0
         for layer in self.layers:
-            x = layer(x, B, S, klen, p, seed.t, dt)
+            x = layer(x, B, S, klen, p, seed.t, dt, pa)
         cls = x.view(B, S, -1)[:, 0]
         pooled = torch.tanh(F.linear(cls, _c(self.pooler_weight, dt), _c(self.pooler_bias, dt)))
         if p > 0:

@@ -54,7 +54,7 @@ class GPTConfig:
     seq_length: int = 1024
     max_position_embeddings: int = 1024
     hidden_dropout: float = 0.1
-    attention_dropout: float = 0.0
+    attention_dropout: float = 0.1         # Megatron default (--attention-dropout 0.1)
     layernorm_epsilon: float = 1e-5
     init_method_std: float = 0.02
     normalization: str = "layernorm"       # layernorm | rmsnorm
@@ -71,6 +71,9 @@ class GPTConfig:
     moe_loss_coeff: float = 0.01
     rotary_base: float = 10000.0
     tie_embeddings: bool = True
+    # Megatron --recompute-activations / --checkpoint-activations (granularity "full"): each
+    # layer keeps only its inputs and re-runs its forward inside its backward
+    recompute: bool = False
 
     def __post_init__(self):
         if self.ffn_hidden_size is None:
@@ -117,6 +120,7 @@ GPT_CONFIGS = {
 }
 
 SALT_EMB = 7
+SALT_ATTN = 50000   # + layer index; the attention mask is keyed on GLOBAL heads, so no TP term
 _NORM_PARAMS = ("ln1_w", "ln1_b")
 
 
@@ -258,6 +262,7 @@ class StepRuntime:
     cp_rank: int = 0
     cp_group: Optional[object] = None
     seed_t: Optional[torch.Tensor] = None
+    attn_seed_t: Optional[torch.Tensor] = None   # attention-dropout seed (shared across CP ranks)
     training: bool = True
     vocab_start: int = 0
     unit_done: Optional[Callable[[int], None]] = None
@@ -277,6 +282,10 @@ class StepRuntime:
     @property
     def p_drop(self):
         return self.cfg.hidden_dropout if self.training else 0.0
+
+    @property
+    def p_attn(self):
+        return self.cfg.attention_dropout if self.training else 0.0
 
     @property
     def rms(self):
@@ -423,6 +432,22 @@ class NormFn(torch.autograd.Function):
 class GPTLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, a, rt: StepRuntime, i: int, next_norm: Optional[str]):
+        h2, a2, saved, dmask, moe = GPTLayerFn._forward_body(rt, i, next_norm, h, a)
+        ctx.rt, ctx.i, ctx.next_norm = rt, i, next_norm
+        if rt.cfg.recompute and rt.training:
+            # activation recompute: keep the layer inputs only (the dropout masks are pure
+            # functions of the step's seed, so the re-run forward is bit-identical)
+            ctx.saved, ctx.dmask, ctx.moe = None, None, None
+            ctx.inputs = (h.detach(), a.detach())
+        else:
+            ctx.saved, ctx.dmask, ctx.moe = saved, dmask, moe
+            ctx.inputs = None
+        if next_norm is None:
+            return h2, torch.empty(0, device=h2.device, dtype=h2.dtype)
+        return h2, a2
+
+    @staticmethod
+    def _forward_body(rt: StepRuntime, i: int, next_norm: Optional[str], h, a, recomputing=False):
         cfg = rt.cfg
         P = rt.params
         p = f"layers.{i}."
@@ -441,7 +466,11 @@ class GPTLayerFn(torch.autograd.Function):
         q = qkv_a[:, : ha * D]
         k = qkv_a[:, ha * D:(ha + kva) * D]
         v = qkv_a[:, (ha + kva) * D:]
-        ctx_a, lse = attn_ops.attn_fwd(q, k, v, rt.B, rt.S * rt.cp, ha, kva, D, causal=True)
+        ctx_a, lse, dmask = attn_ops.attn_fwd(
+            q, k, v, rt.B, rt.S * rt.cp, ha, kva, D, causal=True, dropout_p=rt.p_attn,
+            seed_t=rt.attn_seed_t if rt.attn_seed_t is not None else rt.seed_t,
+            salt=SALT_ATTN + i, head_offset=rt.tp_rank * hl + rt.cp_rank * ha,
+            total_heads=cfg.num_attention_heads)
         ctx_ = head_to_seq(ctx_a, (hl * D,), rt.B, rt.S, rt.cp_group) if rt.cp > 1 else ctx_a
         o = _reduce(torch.mm(ctx_, P[p + "proj_w"].t()), rt)
         w2, b2 = rt.norm_params(p + "ln2")
@@ -457,7 +486,7 @@ class GPTLayerFn(torch.autograd.Function):
             m_leaf = m_full.detach().requires_grad_(True)
             with torch.enable_grad():
                 g_moe, l_aux, _ = moe_mlp(m_leaf, *leaves, cfg, rt.ep_group, training=rt.training)
-            if rt.aux_log is not None:
+            if rt.aux_log is not None and not recomputing:
                 rt.aux_log.append(l_aux.detach())
             moe = (m_leaf, leaves, g_moe, l_aux)
             g = g_moe.detach()
@@ -477,12 +506,8 @@ class GPTLayerFn(torch.autograd.Function):
             wn, bn = P[p + "ln2_w"], P.get(p + "ln2_b")
         h2, a2, mean_n, rstd_n = bda_norm_fwd(g, b_fc2, h1, wn, bn, eps, rt.p_drop,
                                               rt.seed_t, rt.salt(1001 + 2 * i), rt.rms)
-        ctx.saved = (a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2, m_full, pre, f, h2, mean_n, rstd_n)
-        ctx.rt, ctx.i, ctx.next_norm = rt, i, next_norm
-        ctx.moe = moe
-        if next_norm is None:
-            return h2, torch.empty(0, device=h2.device, dtype=h2.dtype)
-        return h2, a2
+        saved = (a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2, m_full, pre, f, h2, mean_n, rstd_n)
+        return h2, a2, saved, dmask, moe
 
     @staticmethod
     def backward(ctx, dh2, da2):
@@ -493,6 +518,12 @@ class GPTLayerFn(torch.autograd.Function):
         D = cfg.head_dim
         hl = cfg.num_attention_heads // rt.tp
         kvl = cfg.num_kv_heads // rt.tp
+        if ctx.inputs is not None:   # activation recompute
+            h_in, a_in = ctx.inputs
+            ctx.inputs = None
+            with torch.no_grad():
+                _, _, ctx.saved, ctx.dmask, ctx.moe = GPTLayerFn._forward_body(rt, i, ctx.next_norm, h_in, a_in,
+                                                                              recomputing=True)
         (a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2, m_full, pre, f, h2, mean_n, rstd_n) = ctx.saved
         ctx.saved = None
         dh2 = dh2.contiguous()
@@ -567,7 +598,8 @@ class GPTLayerFn(torch.autograd.Function):
         v = qkv_a[:, (ha + kva) * D:]
         attn_ops.attn_bwd(dctx, q, k, v, ctx_a, lse, rt.B, rt.S * rt.cp, ha, kva, D, causal=True,
                           dq=dqkv[:, : ha * D], dk=dqkv[:, ha * D:(ha + kva) * D],
-                          dv=dqkv[:, (ha + kva) * D:])
+                          dv=dqkv[:, (ha + kva) * D:], dmask=ctx.dmask, dropout_p=rt.p_attn)
+        ctx.dmask = None
         rt.rope_(dqkv, ha, kva, inverse=True)
         if rt.cp > 1:
             dqkv = head_to_seq(dqkv, (hl * D, kvl * D, kvl * D), rt.B, rt.S, rt.cp_group)
@@ -613,7 +645,7 @@ class GPTStage:
 
     def __init__(self, cfg: GPTConfig, params, grads, tp=1, tp_rank=0, tp_group=None, pp=1,
                  pp_rank=0, sequence_parallel=False, seed_t=None, cp=1, cp_rank=0, cp_group=None,
-                 eparams=None, egrads=None, ep_group=None):
+                 eparams=None, egrads=None, ep_group=None, attn_seed_t=None):
         self.cfg = cfg
         self.l0, self.l1 = stage_layer_range(cfg, pp, pp_rank)
         self.first, self.last = pp_rank == 0, pp_rank == pp - 1
@@ -621,7 +653,8 @@ class GPTStage:
         self.rt = StepRuntime(cfg=cfg, params=params, grads=grads, tp_group=tp_group, tp=tp,
                               tp_rank=tp_rank, sp=sequence_parallel and tp > 1, seed_t=seed_t,
                               vocab_start=tp_rank * V, cp=cp, cp_rank=cp_rank, cp_group=cp_group,
-                              eparams=eparams, egrads=egrads, ep_group=ep_group)
+                              eparams=eparams, egrads=egrads, ep_group=ep_group,
+                              attn_seed_t=attn_seed_t)
         if cfg.num_experts > 1:
             assert tp == 1, "MoE layers run with tensor-parallel size 1 (expert parallelism instead)"
         if cp > 1:

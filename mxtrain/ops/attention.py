@@ -3,6 +3,14 @@
 Tensors are token-major: ``q``, ``k``, ``v`` are 2-D views [B*S, H*D] with an arbitrary
 row stride (so the packed QKV projection output is consumed in place); the output is
 [B*S, Hq*D].  ``lse`` is the base-2 log-sum-exp [B, Hq, S] the backward needs.
+
+Attention dropout (Megatron ``--attention-dropout``, default 0.1 in the reference's GPT
+configs: examples/megatron-deepspeed/gpt2_345m/pretrain-ddp-zero1.yaml:39-53 sets no
+override; HF BERT ``attention_probs_dropout_prob`` 0.1) is applied to the softmax
+probabilities inside the kernels.  The keep-mask is a pure function of (seed, salt, batch,
+GLOBAL head, query, key) -- :func:`dropout_keep_mask` is the definition, bit-identical to
+``attn_dropmask_kernel`` -- so tensor- and context-parallel shards (``head_offset``) draw
+exactly the single-GPU mask, and backward reuses the forward's key-on-lane image.
 """
 from __future__ import annotations
 
@@ -11,11 +19,40 @@ import math
 import torch
 
 from . import _lib
+from .rng import M32, hash32
 
 LOG2E = 1.4426950408889634
 
 
-def _ref_fwd(q, k, v, B, S, Hq, Hkv, D, causal, klen, scale):
+def dropout_threshold(p: float) -> int:
+    """16-bit keep threshold (an element is kept when its 16-bit hash >= thr)."""
+    return int(p * 65536.0 + 0.5)
+
+
+def effective_keep_scale(p: float) -> float:
+    """1 / (1 - p_eff), p_eff = thr/65536 (the probability the kernels actually drop)."""
+    thr = dropout_threshold(p)
+    return 65536.0 / (65536.0 - thr)
+
+
+def dropout_keep_mask(B, S, Hq, seed: int, salt: int, p: float, head_offset: int = 0,
+                      total_heads=None, device="cpu") -> torch.Tensor:
+    """Dense boolean keep-mask [B, Hq, S(q), S(k)]: keep <=> ((hash32(row*0x85EBCA6B +
+    (k >> 1), seed + salt) >> 16 (k & 1)) & 0xFFFF) >= thr, row = (b*Hg + h_global)*S + q."""
+    Hg = total_heads or Hq
+    seed = (int(seed) + int(salt)) & M32
+    b = torch.arange(B, dtype=torch.int64, device=device).view(B, 1, 1, 1)
+    h = torch.arange(Hq, dtype=torch.int64, device=device).view(1, Hq, 1, 1) + head_offset
+    q = torch.arange(S, dtype=torch.int64, device=device).view(1, 1, S, 1)
+    k = torch.arange(S, dtype=torch.int64, device=device).view(1, 1, 1, S)
+    row = ((b * Hg + h) * S + q) & M32
+    x = (row * 0x85EBCA6B + (k >> 1)) & M32
+    hv = hash32(x, seed)
+    h16 = (hv >> (16 * (k & 1))) & 0xFFFF
+    return h16 >= dropout_threshold(p)
+
+
+def _ref_fwd(q, k, v, B, S, Hq, Hkv, D, causal, klen, scale, keep=None, keep_scale=1.0):
     qf = q.float().reshape(B, S, Hq, D).transpose(1, 2)
     kf = k.float().reshape(B, S, Hkv, D).transpose(1, 2)
     vf = v.float().reshape(B, S, Hkv, D).transpose(1, 2)
@@ -32,37 +69,60 @@ def _ref_fwd(q, k, v, B, S, Hq, Hkv, D, causal, klen, scale):
     s = s.masked_fill(mask, float("-inf"))
     lse = torch.logsumexp(s, -1)  # natural
     p = torch.exp(s - lse[..., None])
+    if keep is not None:
+        p = p * keep.to(p.device, p.dtype) * keep_scale
     o = torch.matmul(p, vf).transpose(1, 2).reshape(B * S, Hq * D)
     return o, lse * LOG2E
 
 
-def attn_fwd(q, k, v, B, S, Hq, Hkv, D, causal=True, klen=None, scale=None):
+def attn_fwd(q, k, v, B, S, Hq, Hkv, D, causal=True, klen=None, scale=None, dropout_p=0.0,
+             seed_t=None, salt=0, head_offset=0, total_heads=None):
+    """Returns (o, lse, dmask): dmask is the dropout state backward needs (the kernel's
+    key-on-lane bit image on the GPU, the dense keep-mask on the CPU path) or None."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    drop = dropout_p > 0.0
+    if drop:
+        assert seed_t is not None, "attention dropout needs the device seed tensor"
     if not _lib.use_hip(q):
-        o, lse = _ref_fwd(q, k, v, B, S, Hq, Hkv, D, causal, klen, scale)
-        return o.to(q.dtype), lse
+        keep = (dropout_keep_mask(B, S, Hq, int(seed_t.reshape(-1)[0]), salt, dropout_p, head_offset,
+                                  total_heads, q.device) if drop else None)
+        o, lse = _ref_fwd(q, k, v, B, S, Hq, Hkv, D, causal, klen, scale, keep,
+                          effective_keep_scale(dropout_p) if drop else 1.0)
+        return o.to(q.dtype), lse, keep
     assert q.dtype == torch.bfloat16 and D in (64, 128)
     assert q.stride(1) == 1 and k.stride(1) == 1 and v.stride(1) == 1
     o = torch.empty(B * S, Hq * D, dtype=q.dtype, device=q.device)
     lse = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
     kl = klen.to(torch.int32).contiguous() if klen is not None else None
+    fbits = bbits = None
+    if drop:
+        NB = (S + 31) // 32
+        NKT = (NB + 3) // 4
+        fbits = torch.empty(B * Hq * NB * NKT * 64 * 4, dtype=torch.int16, device=q.device)
+        bbits = torch.empty(B * Hq * NB * NB * 64, dtype=torch.int16, device=q.device)
+        _lib.call("mx_attn_dropmask", _lib.ptr(seed_t), int(salt) & M32, float(dropout_p), B, S, Hq,
+                  int(head_offset), int(total_heads or Hq), int(causal), _lib.ptr(fbits),
+                  _lib.ptr(bbits), _lib.stream())
+    ks = effective_keep_scale(dropout_p) if drop else 1.0
     _lib.call("mx_attn_fwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), q.stride(0), k.stride(0),
               v.stride(0), _lib.ptr(o), o.stride(0), _lib.ptr(lse), B, S, Hq, Hkv, D, int(causal),
-              _lib.ptr(kl), float(scale), _lib.stream())
-    return o, lse
+              _lib.ptr(kl), float(scale), _lib.ptr(fbits), float(ks), _lib.stream())
+    return o, lse, ((bbits, float(dropout_p)) if drop else None)
 
 
 def attn_bwd(dout, q, k, v, o, lse, B, S, Hq, Hkv, D, causal=True, klen=None, scale=None,
-             dq=None, dk=None, dv=None):
+             dq=None, dk=None, dv=None, dmask=None, dropout_p=0.0):
     """Returns (dq, dk, dv); if views dq/dk/dv (e.g. slices of a packed dqkv) are given
-    they are written in place."""
+    they are written in place.  ``dmask`` is the third output of :func:`attn_fwd`."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if not _lib.use_hip(q):
+        keep = dmask
         with torch.enable_grad():
             qq = q.detach().float().requires_grad_(True)
             kk = k.detach().float().requires_grad_(True)
             vv = v.detach().float().requires_grad_(True)
-            oo, _ = _ref_fwd(qq, kk, vv, B, S, Hq, Hkv, D, causal, klen, scale)
+            oo, _ = _ref_fwd(qq, kk, vv, B, S, Hq, Hkv, D, causal, klen, scale, keep,
+                             effective_keep_scale(dropout_p) if keep is not None else 1.0)
             gq, gk, gv = torch.autograd.grad(oo, (qq, kk, vv), dout.float())
         outs = []
         for g, buf in ((gq, dq), (gk, dk), (gv, dv)):
@@ -82,11 +142,15 @@ def attn_bwd(dout, q, k, v, o, lse, B, S, Hq, Hkv, D, causal=True, klen=None, sc
     # zeroed by the delta pre-pass inside mx_attn_bwd
     dq_acc = torch.empty(B * S, Hq * D, dtype=torch.float32, device=q.device)
     kl = klen.to(torch.int32).contiguous() if klen is not None else None
+    bbits, ks = None, 1.0
+    if dmask is not None:
+        bbits, p = dmask
+        ks = effective_keep_scale(p)
     _lib.call("mx_attn_bwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), q.stride(0), k.stride(0),
               v.stride(0), _lib.ptr(o), o.stride(0), _lib.ptr(dout), dout.stride(0), _lib.ptr(lse),
               _lib.ptr(delta), _lib.ptr(dq_acc), _lib.ptr(dq), dq.stride(0), _lib.ptr(dk),
               _lib.ptr(dv), dk.stride(0), dv.stride(0), B, S, Hq, Hkv, D, int(causal), _lib.ptr(kl),
-              float(scale), _lib.stream())
+              float(scale), _lib.ptr(bbits), float(ks), _lib.stream())
     return dq, dk, dv
 
 
@@ -94,20 +158,23 @@ class FlashAttnFn(torch.autograd.Function):
     """Autograd wrapper over [B, S, H, D]-style inputs flattened to [B*S, H*D]."""
 
     @staticmethod
-    def forward(ctx, q, k, v, B, S, Hq, Hkv, D, causal, klen, scale):
-        o, lse = attn_fwd(q, k, v, B, S, Hq, Hkv, D, causal, klen, scale)
+    def forward(ctx, q, k, v, B, S, Hq, Hkv, D, causal, klen, scale, dropout_p, seed_t, salt):
+        o, lse, dmask = attn_fwd(q, k, v, B, S, Hq, Hkv, D, causal, klen, scale, dropout_p, seed_t, salt)
         ctx.save_for_backward(q, k, v, o, lse, klen if klen is not None else torch.empty(0))
-        ctx.meta = (B, S, Hq, Hkv, D, causal, scale, klen is not None)
+        ctx.dmask = dmask
+        ctx.meta = (B, S, Hq, Hkv, D, causal, scale, klen is not None, dropout_p)
         return o
 
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse, kl = ctx.saved_tensors
-        B, S, Hq, Hkv, D, causal, scale, has_kl = ctx.meta
+        B, S, Hq, Hkv, D, causal, scale, has_kl, p = ctx.meta
         dq, dk, dv = attn_bwd(do.contiguous(), q, k, v, o, lse, B, S, Hq, Hkv, D, causal,
-                              kl if has_kl else None, scale)
-        return dq, dk, dv, None, None, None, None, None, None, None, None
+                              kl if has_kl else None, scale, dmask=ctx.dmask, dropout_p=p)
+        ctx.dmask = None
+        return dq, dk, dv, None, None, None, None, None, None, None, None, None, None, None
 
 
-def flash_attention(q, k, v, B, S, Hq, Hkv, D, causal=True, klen=None, scale=None):
-    return FlashAttnFn.apply(q, k, v, B, S, Hq, Hkv, D, causal, klen, scale)
+def flash_attention(q, k, v, B, S, Hq, Hkv, D, causal=True, klen=None, scale=None, dropout_p=0.0,
+                    seed_t=None, salt=0):
+    return FlashAttnFn.apply(q, k, v, B, S, Hq, Hkv, D, causal, klen, scale, dropout_p, seed_t, salt)

@@ -40,13 +40,20 @@ def keep_mask(numel: int, seed: int, p: float, device="cpu", base: int = 0) -> t
 
 
 class DropoutSeed:
-    """Device-resident dropout seed, advanced once per training step."""
+    """Device-resident dropout seeds, advanced once per training step.
 
-    def __init__(self, device, seed: int = 1234):
-        self.t = torch.tensor([seed & 0x7FFFFFFF], dtype=torch.int32, device=device)
+    Element 0 seeds the token-local dropouts (hidden / residual; it differs across data-
+    and context-parallel ranks, which hold different tokens); element 1 (``attn_t``, when
+    ``attn_seed`` is given) seeds attention dropout, whose mask is keyed on the global
+    (batch, head, query, key) and so must be the SAME on every context-parallel rank."""
+
+    def __init__(self, device, seed: int = 1234, attn_seed=None):
+        vals = [seed & 0x7FFFFFFF] + ([attn_seed & 0x7FFFFFFF] if attn_seed is not None else [])
+        self.t = torch.tensor(vals, dtype=torch.int32, device=device)
+        self.attn_t = self.t[1:2] if attn_seed is not None else self.t[0:1]
 
     def value(self) -> int:
-        return int(self.t.item())
+        return int(self.t[0].item())
 
     INC = 0x61C88647 & 0x7FFFFFFF
 
@@ -55,6 +62,8 @@ class DropoutSeed:
         self.t.add_(self.INC)
         self.t.bitwise_and_(0x7FFFFFFF)
 
-    def set_step(self, seed: int, steps: int):
+    def set_step(self, seed: int, steps: int, attn_seed=None):
         """State after `steps` advances from `seed` (checkpoint resume)."""
-        self.t.fill_(((seed & 0x7FFFFFFF) + steps * self.INC) % (1 << 31))
+        self.t[0] = ((seed & 0x7FFFFFFF) + steps * self.INC) % (1 << 31)
+        if attn_seed is not None and self.t.numel() > 1:
+            self.t[1] = ((attn_seed & 0x7FFFFFFF) + steps * self.INC) % (1 << 31)

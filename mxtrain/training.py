@@ -71,11 +71,12 @@ class GPTTrainer:
         gen = torch.Generator().manual_seed(tcfg.seed + 1000 * ps.pp_rank + 100 * ps.tp_rank)
         self.flat.initialize(gen, cfg.num_layers)
         self._sync_initial_params()
-        self.seed = DropoutSeed(self.device, tcfg.seed + 7 * (ps.dp_rank * ps.cp + ps.cp_rank))
+        self.seed = DropoutSeed(self.device, *self.seed_bases(tcfg, ps))
         self.stage = GPTStage(cfg, self.flat.params, self.flat.grads, tp=ps.tp, tp_rank=ps.tp_rank,
                               tp_group=ps.tp_group, pp=ps.pp, pp_rank=ps.pp_rank,
                               sequence_parallel=ps.sequence_parallel, seed_t=self.seed.t,
-                              cp=ps.cp, cp_rank=ps.cp_rank, cp_group=ps.cp_group)
+                              cp=ps.cp, cp_rank=ps.cp_rank, cp_group=ps.cp_group,
+                              attn_seed_t=self.seed.attn_t)
         if tcfg.wgrad_stream and self.device.type == "cuda":
             self.stage.rt.wgrad_stream = torch.cuda.Stream(device=self.device)
         sched = LRSchedule(tcfg.lr, tcfg.min_lr, tcfg.lr_warmup_iters, tcfg.lr_decay_iters,
@@ -104,6 +105,14 @@ class GPTTrainer:
         self._static = None
 
     # ------------------------------------------------------------------ init
+    @staticmethod
+    def seed_bases(tcfg, ps):
+        """(hidden-dropout seed, attention-dropout seed) of this rank before any step:
+        hidden dropout differs per data/context-parallel rank (different tokens); the
+        attention mask is keyed on global heads/positions, so it is shared by CP ranks."""
+        return (tcfg.seed + 7 * (ps.dp_rank * ps.cp + ps.cp_rank),
+                tcfg.seed + 7 * ps.dp_rank * ps.cp + 3)
+
     def _setup_moe(self, cfg, tcfg, ps, dtype, sched):
         """Expert parameters: E/ep experts per rank in a second flat buffer with its own
         ZeRO-1 optimizer over the expert-data-parallel group (models/moe.py)."""

@@ -8,6 +8,12 @@ on MI355X the fused HIP kernels are always used.
 
 Precision: ``--fp16`` (the reference's setting) runs the MI355X-native bf16 path --
 same 16-bit storage/throughput class, no loss scaling needed; ``--bf16`` is explicit.
+
+Nothing is rewritten silently: every place where the effective run differs from what the
+flags ask for (``--fp16`` -> bf16 and its loss-scaler settings, ZeRO stage > 1 -> 1,
+ignored implementation-selection flags) is collected in ``args.mx_deviations``, printed
+once at start-up and recorded in the checkpoint ``args`` and the metrics JSONL
+(``args.mx_effective`` holds the effective precision / dropout / recompute settings).
 """
 from __future__ import annotations
 
@@ -16,14 +22,16 @@ import json
 import os
 from typing import List, Optional
 
+# flags that only pick a CUDA implementation (or a Megatron code path with no numerical
+# effect here); they are accepted, listed in args.mx_deviations when given, and ignored
 IGNORED_FLAGS = [
     "--no-masked-softmax-fusion", "--no-bias-gelu-fusion", "--no-bias-dropout-fusion",
     "--no-gradient-accumulation-fusion", "--use-flash-attn", "--use-flash-attn-v2",
-    "--no-async-tensor-model-parallel-allreduce", "--checkpoint-activations", "--no-pipeline-parallel",
+    "--no-async-tensor-model-parallel-allreduce", "--no-pipeline-parallel",
     "--use-cpu-initialization", "--log-timers-to-tensorboard", "--log-batch-size-to-tensorboard",
     "--log-validation-ppl-to-tensorboard", "--log-memory-to-tensorboard", "--log-num-zeros-in-grad",
     "--log-params-norm", "--use-distributed-optimizer", "--overlap-grad-reduce", "--overlap-param-gather",
-    "--deepspeed-activation-checkpointing", "--no-query-key-layer-scaling", "--apply-query-key-layer-scaling",
+    "--no-query-key-layer-scaling", "--apply-query-key-layer-scaling",
     "--attention-softmax-in-fp32", "--accumulate-allreduce-grads-in-fp32", "--no-load-rng",
     "--use-contiguous-buffers-in-local-ddp", "--sync-tp-duplicated-parameters", "--empty-unused-memory-level",
 ]
@@ -90,8 +98,12 @@ def build_parser() -> argparse.ArgumentParser:
     a("--seed", type=int, default=1234)
     a("--exit-interval", type=int, default=None)
     a("--exit-duration-in-mins", type=float, default=None)
+    # activation recompute (Megatron / DeepSpeed spellings): "full" re-runs each
+    # transformer layer's forward inside its backward instead of keeping its activations
     a("--recompute-activations", action="store_true")
-    a("--recompute-granularity", default=None)
+    a("--checkpoint-activations", action="store_true")
+    a("--deepspeed-activation-checkpointing", action="store_true")
+    a("--recompute-granularity", default=None, choices=[None, "full", "selective"])
     # parallelism
     a("--tensor-model-parallel-size", type=int, default=1)
     a("--pipeline-model-parallel-size", type=int, default=1)
@@ -204,7 +216,38 @@ def parse_args(argv: Optional[List[str]] = None):
         args.lr_warmup_iters = int(args.lr_warmup_fraction * args.lr_decay_iters)
     elif args.lr_warmup_samples:
         args.lr_warmup_iters = args.lr_warmup_samples // args.global_batch_size
-    if args.zero_stage > 1:
-        print(f"[mxtrain] ZeRO stage {args.zero_stage} requested: running stage-1 sharding "
-              "(optimizer state sharded; 288 GB HBM holds full bf16 grads)", flush=True)
+    _effective(args, argv)
     return args
+
+
+def _effective(args, argv):
+    """Fill args.mx_effective / args.mx_deviations and print every deviation once."""
+    dev = []
+    if args.fp16:
+        msg = "--fp16 -> bf16 compute (fp32 master weights); no dynamic loss scaler is needed or used"
+        if args.loss_scale or args.initial_loss_scale:
+            msg += f" (loss_scale={args.loss_scale}, initial_loss_scale={args.initial_loss_scale} ignored)"
+        dev.append(msg)
+    if args.zero_stage > 1:
+        dev.append(f"ZeRO stage {args.zero_stage} -> stage 1 (optimizer state sharded; "
+                   "288 GB HBM holds the full bf16 gradients)")
+    if args.recompute_granularity == "selective":
+        dev.append("--recompute-granularity selective -> full layer recompute")
+    given = set(a.split("=")[0] for a in (argv if argv is not None else __import__("sys").argv[1:]))
+    ign = [f for f in IGNORED_FLAGS if f in given]
+    if ign:
+        dev.append("accepted without effect (implementation selection only): " + " ".join(ign))
+    recompute = bool(args.recompute_activations or args.checkpoint_activations
+                     or args.deepspeed_activation_checkpointing or args.recompute_granularity)
+    args.mx_recompute = recompute
+    args.mx_effective = {
+        "compute_dtype": "bf16", "master_dtype": "fp32", "loss_scaling": False,
+        "requested_precision": "fp16" if args.fp16 else ("bf16" if args.bf16 else "fp32-flag (bf16 kernels)"),
+        "hidden_dropout": args.hidden_dropout, "attention_dropout": args.attention_dropout,
+        "activation_recompute": "full" if recompute else None,
+        "zero_stage": 1,
+    }
+    args.mx_deviations = dev
+    if int(os.environ.get("RANK", "0")) == 0:
+        for d in dev:
+            print(f"[mxtrain] WARNING: {d}", flush=True)

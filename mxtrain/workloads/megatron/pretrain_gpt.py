@@ -65,16 +65,13 @@ def main(argv=None):
         tokenizer = build_tokenizer(args.tokenizer_type, args.vocab_file, args.merge_file, args.vocab_size)
         vocab_size = tokenizer.vocab_size
     vocab_size = vocab_size or 50257
-    if args.attention_dropout > 0:
-        print_rank_0(f"[mxtrain] note: --attention-dropout {args.attention_dropout} -> 0.0 "
-                     "(flash attention kernel runs without attention dropout)")
     cfg = GPTConfig(num_layers=args.num_layers, hidden_size=args.hidden_size,
                     num_attention_heads=args.num_attention_heads,
                     num_kv_heads=args.num_key_value_heads if args.group_query_attention or args.num_key_value_heads else None,
                     ffn_hidden_size=args.ffn_hidden_size, vocab_size=vocab_size,
                     make_vocab_size_divisible_by=args.make_vocab_size_divisible_by, seq_length=args.seq_length,
                     max_position_embeddings=args.max_position_embeddings, hidden_dropout=args.hidden_dropout,
-                    attention_dropout=0.0, layernorm_epsilon=args.layernorm_epsilon,
+                    attention_dropout=args.attention_dropout, layernorm_epsilon=args.layernorm_epsilon,
                     init_method_std=args.init_method_std, normalization=args.normalization,
                     position_embedding="rope" if args.position_embedding_type == "rope" else "learned",
                     rotary_percent=args.rotary_percent, rotary_base=args.rotary_base,
@@ -83,7 +80,8 @@ def main(argv=None):
                     moe_topk=args.topk, moe_train_capacity_factor=args.moe_train_capacity_factor,
                     moe_eval_capacity_factor=args.moe_eval_capacity_factor,
                     moe_min_capacity=args.moe_min_capacity, moe_loss_coeff=args.moe_loss_coeff,
-                    tie_embeddings=not args.untie_embeddings_and_output_weights)
+                    tie_embeddings=not args.untie_embeddings_and_output_weights,
+                    recompute=args.mx_recompute)
     tcfg = TrainConfig(micro_batch_size=args.micro_batch_size, global_batch_size=args.global_batch_size,
                        lr=args.lr, min_lr=args.min_lr, lr_warmup_iters=args.lr_warmup_iters,
                        lr_decay_iters=args.lr_decay_iters, lr_decay_style=args.lr_decay_style,
@@ -131,6 +129,9 @@ def main(argv=None):
     # ---------------------------------------------------------------- observability
     logs_dir = args.mx_metrics_dir or os.environ.get("LOGS_DIR") or os.path.join(os.environ.get("HOME", "."), "logs")
     metrics = MetricsWriter(logs_dir, ps.rank)
+    # effective settings + every deviation from the requested flags, once, in the JSONL
+    metrics.write(step=trainer.iteration, event="config", effective=args.mx_effective,
+                  deviations=args.mx_deviations)
     tb = None
     if args.tensorboard_dir and ps.is_last_stage and ps.tp_rank == 0 and ps.dp_rank == 0:
         from mxtrain.obs.tensorboard import SummaryWriter
@@ -242,6 +243,8 @@ def _plain(d):
             out[k] = v
         elif isinstance(v, (list, tuple)) and all(isinstance(x, (int, float, str, bool)) for x in v):
             out[k] = list(v)
+        elif isinstance(v, dict) and k == "mx_effective":   # effective settings (deviations recorded)
+            out[k] = {kk: vv for kk, vv in v.items() if isinstance(vv, (int, float, str, bool)) or vv is None}
     return out
 
 

@@ -63,7 +63,7 @@ def main():
         qkv = torch.randn(T, 3 * h, device=dev).to(bf)
         q, k, v = qkv[:, :h], qkv[:, h:2 * h], qkv[:, 2 * h:]
         fl = 4 * B * H * S * S * D / 2
-        o, lse = A.attn_fwd(q, k, v, B, S, H, H, D, True)
+        o, lse, _ = A.attn_fwd(q, k, v, B, S, H, H, D, True)
         rec("attn_fwd causal", timeit(lambda: A.attn_fwd(q, k, v, B, S, H, H, D, True)), flops=fl)
         do = torch.randn(T, h, device=dev).to(bf)
         dqkv = torch.empty_like(qkv)
@@ -71,13 +71,21 @@ def main():
                                                          dq=dqkv[:, :h], dk=dqkv[:, h:2 * h],
                                                          dv=dqkv[:, 2 * h:])), flops=2.5 * fl)
         rec("attn_fwd full", timeit(lambda: A.attn_fwd(q, k, v, B, S, H, H, D, False)), flops=2 * fl)
+        sd = torch.tensor([7], dtype=torch.int32, device=dev)
+        o, lse, dm = A.attn_fwd(q, k, v, B, S, H, H, D, True, dropout_p=0.1, seed_t=sd)
+        rec("attn_fwd causal drop0.1", timeit(lambda: A.attn_fwd(q, k, v, B, S, H, H, D, True, dropout_p=0.1,
+                                                                 seed_t=sd)), flops=fl)
+        rec("attn_bwd causal drop0.1", timeit(lambda: A.attn_bwd(do, q, k, v, o, lse, B, S, H, H, D, True,
+                                                                 dq=dqkv[:, :h], dk=dqkv[:, h:2 * h],
+                                                                 dv=dqkv[:, 2 * h:], dmask=dm, dropout_p=0.1)),
+            flops=2.5 * fl)
     if want("attn128"):   # GPT-3 6.7B shapes: B=2, S=2048, H=32, D=128
         B2, S2, H2, D2 = 2, 2048, 32, 128
         T2, h2 = B2 * S2, H2 * D2
         qkv = torch.randn(T2, 3 * h2, device=dev).to(bf)
         q, k, v = qkv[:, :h2], qkv[:, h2:2 * h2], qkv[:, 2 * h2:]
         fl = 4 * B2 * H2 * S2 * S2 * D2 / 2
-        o, lse = A.attn_fwd(q, k, v, B2, S2, H2, H2, D2, True)
+        o, lse, _ = A.attn_fwd(q, k, v, B2, S2, H2, H2, D2, True)
         rec("attn128_fwd causal", timeit(lambda: A.attn_fwd(q, k, v, B2, S2, H2, H2, D2, True)), flops=fl)
         do = torch.randn(T2, h2, device=dev).to(bf)
         dqkv = torch.empty_like(qkv)

@@ -21,7 +21,8 @@ def rope_complex(x, rd, base):
     return torch.cat([z.real, z.imag, x[..., rd:]], -1)
 
 
-def ref_loss(P, ids, labels, cfg, B, S, head="wte", mlp_hook=None):
+def ref_loss(P, ids, labels, cfg, B, S, head="wte", mlp_hook=None, attn_keep=None):
+    """attn_keep(i) -> (keep [B, H, S, S] bool, scale): attention-dropout mask of layer i."""
     h = cfg.hidden_size
     nh = cfg.num_attention_heads
     D = h // nh
@@ -53,7 +54,11 @@ def ref_loss(P, ids, labels, cfg, B, S, head="wte", mlp_hook=None):
             v = v.repeat_interleave(nh // kvh, 1)
         s = (q @ k.transpose(-1, -2)) / math.sqrt(D)
         s = s.masked_fill(torch.ones(S, S, dtype=torch.bool).triu(1), float("-inf"))
-        ctx = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * S, h)
+        prob = torch.softmax(s, -1)
+        if attn_keep is not None:
+            keep, ks = attn_keep(i)
+            prob = prob * keep.float() * ks
+        ctx = (prob @ v).transpose(1, 2).reshape(B * S, h)
         x = x + ctx @ P[p + "proj_w"].t() + P[p + "proj_b"]
         m = ln(x, p + "ln2")
         if mlp_hook is not None and (p + "router_w") in P:

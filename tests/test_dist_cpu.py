@@ -14,7 +14,7 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.dist
 
 CFG = dict(num_layers=2, hidden_size=64, num_attention_heads=4, seq_length=16,
-           max_position_embeddings=16, vocab_size=256, hidden_dropout=0.0)
+           max_position_embeddings=16, vocab_size=256, hidden_dropout=0.0, attention_dropout=0.0)
 
 
 # LLaMA-style variant: RoPE + GQA + RMSNorm + SwiGLU (column-parallel [a|b] fc1 split)
@@ -22,8 +22,17 @@ CFG_LLAMA = dict(CFG, num_kv_heads=2, normalization="rmsnorm", position_embeddin
                  swiglu=True, ffn_hidden_size=96)
 
 
+# attention dropout on: the keep-mask is keyed on the GLOBAL head index, so TP / CP head
+# shards must still reproduce the single-process run exactly
+CFG_ADROP = dict(CFG, attention_dropout=0.1)
+
+
 def _cfg(mode):
-    return CFG_LLAMA if mode.endswith(":llama") else CFG
+    if mode.endswith(":llama"):
+        return CFG_LLAMA
+    if mode.endswith(":adrop"):
+        return CFG_ADROP
+    return CFG
 
 
 def _free_port():
@@ -124,7 +133,7 @@ def test_deferred_update_matches_eager_single():
 
 
 def _ref_init(ccfg=CFG):
-    key = "init" if ccfg is CFG else "init_llama"
+    key = "init_llama" if ccfg is CFG_LLAMA else "init"
     if key not in _REF:
         from mxtrain.models.gpt import GPTConfig
         from mxtrain.parallel.state import ParallelState
@@ -235,6 +244,13 @@ def test_tp2_x_ulysses_cp2_matches_single(reference):
         exp = shard_gpt_state(ref_sd, cfg, 2, tpr, 1, 0)
         for n, t in exp.items():
             assert torch.allclose(params[n], t, atol=3e-5, rtol=1e-4), (rank, n, (params[n] - t).abs().max())
+
+
+@pytest.mark.parametrize("mode", ["tp:adrop", "cp:adrop"])
+def test_attention_dropout_sharded_matches_single(mode):
+    """Attention dropout 0.1 under TP2 (heads split) and Ulysses CP2 (head groups after the
+    all-to-all): the shards draw the single-process keep-mask, so losses and updates match."""
+    _check(mode, _make_reference(CFG_ADROP), loss_ranks=(0, 1))
 
 
 def test_pp2_1f1b_matches_single(reference):

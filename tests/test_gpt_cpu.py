@@ -23,7 +23,7 @@ def _setup(cfg, B, S, seed=0):
 
 def test_gpt_loss_and_grads_match_autograd():
     cfg = GPTConfig(num_layers=2, hidden_size=64, num_attention_heads=4, seq_length=16,
-                    max_position_embeddings=16, vocab_size=100, hidden_dropout=0.0)
+                    max_position_embeddings=16, vocab_size=100, hidden_dropout=0.0, attention_dropout=0.0)
     B, S = 2, 16
     flat, ids, labels = _setup(cfg, B, S)
     stage = GPTStage(cfg, flat.params, flat.grads)
@@ -40,9 +40,33 @@ def test_gpt_loss_and_grads_match_autograd():
         assert torch.allclose(g, p.grad, atol=2e-5, rtol=1e-4), (n, (g - p.grad).abs().max())
 
 
+def test_gpt_attention_dropout_matches_autograd():
+    """Attention dropout 0.1 (Megatron default) through the CPU path of the flash op: the
+    hand-written backward equals autograd of a plain softmax * keep / (1-p) attention."""
+    from mxtrain.models.gpt import SALT_ATTN
+    from mxtrain.ops.attention import dropout_keep_mask, effective_keep_scale
+    cfg = GPTConfig(num_layers=2, hidden_size=64, num_attention_heads=4, seq_length=16,
+                    max_position_embeddings=16, vocab_size=100, hidden_dropout=0.0, attention_dropout=0.1)
+    B, S = 2, 16
+    flat, ids, labels = _setup(cfg, B, S, seed=5)
+    seed = torch.tensor([987], dtype=torch.int32)
+    stage = GPTStage(cfg, flat.params, flat.grads, seed_t=seed, attn_seed_t=seed)
+    stage.rt.grad_scale = 1.0 / (B * S)
+    loss = stage.forward(ids=ids, labels=labels, B=B, S=S)
+    loss.backward()
+    P = {n: p.detach().clone().requires_grad_(True) for n, p in flat.params.items()}
+    keep = lambda i: (dropout_keep_mask(B, S, 4, 987, SALT_ATTN + i, 0.1), effective_keep_scale(0.1))
+    assert 0.05 < 1 - keep(0)[0].float().mean() < 0.15
+    ref = ref_loss(P, ids, labels, cfg, B, S, attn_keep=keep)
+    ref.backward()
+    assert torch.allclose(loss, ref, atol=1e-5), (float(loss), float(ref))
+    for n, p in P.items():
+        assert torch.allclose(flat.grads[n], p.grad, atol=2e-5, rtol=1e-4), (n, (flat.grads[n] - p.grad).abs().max())
+
+
 def test_gpt_rmsnorm_variant():
     cfg = GPTConfig(num_layers=2, hidden_size=64, num_attention_heads=4, seq_length=8,
-                    max_position_embeddings=8, vocab_size=50, hidden_dropout=0.0,
+                    max_position_embeddings=8, vocab_size=50, hidden_dropout=0.0, attention_dropout=0.0,
                     normalization="rmsnorm")
     B, S = 2, 8
     flat, ids, labels = _setup(cfg, B, S, seed=3)
@@ -61,7 +85,7 @@ def test_gpt_rmsnorm_variant():
 def test_gpt_rope_gqa_variant():
     """RoPE (K5, partial rotary) + GQA + RMSNorm + SwiGLU (LLaMA-style)."""
     cfg = GPTConfig(num_layers=2, hidden_size=64, num_attention_heads=4, num_kv_heads=2,
-                    seq_length=8, max_position_embeddings=8, vocab_size=50, hidden_dropout=0.0,
+                    seq_length=8, max_position_embeddings=8, vocab_size=50, hidden_dropout=0.0, attention_dropout=0.0,
                     normalization="rmsnorm", position_embedding="rope", rotary_percent=0.5,
                     swiglu=True, ffn_hidden_size=96)
     B, S = 2, 8
@@ -106,3 +130,24 @@ def test_dropout_mask_reproducible():
     assert torch.equal(m1, m2)
     frac = 1 - m1.float().mean().item()
     assert 0.08 < frac < 0.12
+
+
+def test_activation_recompute_is_bit_identical():
+    """--checkpoint-activations / --recompute-activations: each layer keeps only its inputs and
+    re-runs its forward in backward; with dropout on, losses and gradients are unchanged."""
+    B, S = 2, 16
+    out = []
+    for rc in (False, True):
+        cfg = GPTConfig(num_layers=2, hidden_size=64, num_attention_heads=4, seq_length=16,
+                        max_position_embeddings=16, vocab_size=100, hidden_dropout=0.1,
+                        attention_dropout=0.1, recompute=rc)
+        flat, ids, labels = _setup(cfg, B, S, seed=9)
+        seed = torch.tensor([31], dtype=torch.int32)
+        stage = GPTStage(cfg, flat.params, flat.grads, seed_t=seed, attn_seed_t=seed)
+        stage.rt.grad_scale = 1.0 / (B * S)
+        loss = stage.forward(ids=ids, labels=labels, B=B, S=S)
+        loss.backward()
+        out.append((float(loss), flat.grads))
+    assert out[0][0] == out[1][0]
+    for n in out[0][1]:
+        assert torch.equal(out[0][1][n], out[1][1][n]), n

@@ -167,37 +167,105 @@ def test_adamw_and_norm():
 
 
 ATTN_CASES = [
-    # B, S, H, D, causal, padded
-    (2, 256, 4, 64, True, False),
-    (1, 1024, 2, 64, True, False),
-    (2, 128, 4, 64, False, True),
-    (2, 200, 2, 64, True, False),
-    (1, 256, 2, 128, True, False),
-    (2, 128, 2, 128, False, True),
+    # B, S, Hq, Hkv, D, causal, padded, dropout
+    (2, 256, 4, 4, 64, True, False, 0.0),
+    (1, 1024, 2, 2, 64, True, False, 0.0),
+    (2, 128, 4, 4, 64, False, True, 0.0),
+    (2, 200, 2, 2, 64, True, False, 0.0),
+    (1, 256, 2, 2, 128, True, False, 0.0),
+    (2, 128, 2, 2, 128, False, True, 0.0),
+    # production GPT-3 6.7B head shape (S 2048, D 128, causal; two-pass backward)
+    (1, 2048, 2, 2, 128, True, False, 0.0),
+    # grouped-query attention (Hq != Hkv)
+    (2, 512, 8, 2, 64, True, False, 0.0),
+    (1, 512, 8, 2, 128, True, False, 0.0),
+    # attention dropout (Megatron default 0.1): identical keep-mask in the reference
+    (2, 256, 4, 4, 64, True, False, 0.1),
+    (1, 1024, 2, 2, 64, True, False, 0.1),
+    (2, 200, 2, 2, 64, True, False, 0.1),
+    (2, 128, 4, 4, 64, False, True, 0.1),
+    (1, 512, 4, 2, 128, True, False, 0.1),
+    (2, 128, 2, 2, 128, False, True, 0.3),
 ]
 
 
-@pytest.mark.parametrize("B,S,H,D,causal,padded", ATTN_CASES)
-def test_flash_attention_fwd_bwd(B, S, H, D, causal, padded):
-    qkv = _bf(torch.randn(B * S, 3 * H * D))
-    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+@pytest.mark.parametrize("B,S,Hq,Hkv,D,causal,padded,pdrop", ATTN_CASES)
+def test_flash_attention_fwd_bwd(B, S, Hq, Hkv, D, causal, padded, pdrop):
+    W = (Hq + 2 * Hkv) * D
+    qkv = _bf(torch.randn(B * S, W))
+    sl = (slice(0, Hq * D), slice(Hq * D, (Hq + Hkv) * D), slice((Hq + Hkv) * D, W))
+    q, k, v = (qkv[:, c] for c in sl)
     klen = torch.tensor([S, S * 3 // 4][:B], dtype=torch.int32) if padded else None
     qkvd = qkv.to(DEV)
-    qd, kd, vd = qkvd[:, :H * D], qkvd[:, H * D:2 * H * D], qkvd[:, 2 * H * D:]
-    o, lse = A.attn_fwd(qd, kd, vd, B, S, H, H, D, causal, klen.to(DEV) if padded else None)
-    orf, lser = A.attn_fwd(q, k, v, B, S, H, H, D, causal, klen)
+    qd, kd, vd = (qkvd[:, c] for c in sl)
+    seed = torch.tensor([12345], dtype=torch.int32)
+    kw = dict(dropout_p=pdrop, salt=77, head_offset=0, total_heads=Hq) if pdrop else {}
+    o, lse, dm = A.attn_fwd(qd, kd, vd, B, S, Hq, Hkv, D, causal, klen.to(DEV) if padded else None,
+                            seed_t=seed.to(DEV), **kw)
+    orf, lser, dmr = A.attn_fwd(q, k, v, B, S, Hq, Hkv, D, causal, klen, seed_t=seed, **kw)
     _close(o, orf, 2e-2, 2e-2, "attn o")
     _close(lse, lser, 2e-3, 1e-3, "attn lse")
-    do = _bf(torch.randn(B * S, H * D))
+    do = _bf(torch.randn(B * S, Hq * D))
     dqkv = torch.empty_like(qkvd)
-    A.attn_bwd(do.to(DEV), qd, kd, vd, o, lse, B, S, H, H, D, causal,
-               klen.to(DEV) if padded else None, dq=dqkv[:, :H * D], dk=dqkv[:, H * D:2 * H * D],
-               dv=dqkv[:, 2 * H * D:])
-    dq, dk, dv = A.attn_bwd(do, q, k, v, orf, lser, B, S, H, H, D, causal, klen)
+    A.attn_bwd(do.to(DEV), qd, kd, vd, o, lse, B, S, Hq, Hkv, D, causal,
+               klen.to(DEV) if padded else None, dq=dqkv[:, sl[0]], dk=dqkv[:, sl[1]],
+               dv=dqkv[:, sl[2]], dmask=dm, dropout_p=pdrop)
+    dq, dk, dv = A.attn_bwd(do, q, k, v, orf, lser, B, S, Hq, Hkv, D, causal, klen, dmask=dmr,
+                            dropout_p=pdrop)
     scale = max(dq.abs().max().item(), 1.0)
-    _close(dqkv[:, :H * D], dq, 3e-2 * scale, 3e-2, "dq")
-    _close(dqkv[:, H * D:2 * H * D], dk, 3e-2 * scale, 3e-2, "dk")
-    _close(dqkv[:, 2 * H * D:], dv, 3e-2 * scale, 3e-2, "dv")
+    _close(dqkv[:, sl[0]], dq, 3e-2 * scale, 3e-2, "dq")
+    _close(dqkv[:, sl[1]], dk, 3e-2 * scale, 3e-2, "dk")
+    _close(dqkv[:, sl[2]], dv, 3e-2 * scale, 3e-2, "dv")
+
+
+def _crow(e, hh):
+    return (e & 3) + 8 * (e >> 2) + 4 * hh
+
+
+@pytest.mark.parametrize("S,causal", [(256, True), (200, False), (96, True)])
+def test_attention_dropout_mask_images(S, causal):
+    """attn_dropmask_kernel's forward (query-on-lane) and backward (key-on-lane) bit images
+    both decode to the reference keep-mask (dropout_keep_mask), and the drop rate is p."""
+    from mxtrain.ops import _lib
+    B, Hq, p, salt = 2, 3, 0.1, 5
+    NB = (S + 31) // 32
+    NKT = (NB + 3) // 4
+    seed = torch.tensor([424242], dtype=torch.int32, device=DEV)
+    fb = torch.zeros(B * Hq * NB * NKT * 64 * 4, dtype=torch.int16, device=DEV)
+    bb = torch.zeros(B * Hq * NB * NB * 64, dtype=torch.int16, device=DEV)
+    _lib.call("mx_attn_dropmask", _lib.ptr(seed), salt, p, B, S, Hq, 1, Hq + 2, int(causal),
+              _lib.ptr(fb), _lib.ptr(bb), _lib.stream())
+    torch.cuda.synchronize()
+    ref = A.dropout_keep_mask(B, S, Hq, 424242, salt, p, head_offset=1, total_heads=Hq + 2)
+    P = NB * 32
+    keepf = torch.zeros(B * Hq, P, P, dtype=torch.bool)
+    keepb = torch.zeros(B * Hq, P, P, dtype=torch.bool)
+    fbits = fb.cpu().view(B * Hq, NB, NKT, 64, 4).to(torch.int64) & 0xFFFF
+    bbits = bb.cpu().view(B * Hq, NB, NB, 64).to(torch.int64) & 0xFFFF
+    lane = torch.arange(64)
+    for qb in range(NB):
+        for kb in range(NB):
+            if causal and kb > qb:
+                continue
+            wf = fbits[:, qb, kb // 4, :, kb % 4]      # [BH, 64]
+            wb = bbits[:, kb, qb, :]
+            for e in range(16):
+                bit_f = ((wf >> e) & 1).bool()
+                bit_b = ((wb >> e) & 1).bool()
+                qf = 32 * qb + (lane & 31)
+                kf = 32 * kb + _crow(e, lane >> 5)
+                keepf[:, qf, kf] = bit_f
+                kbk = 32 * kb + (lane & 31)
+                qbk = 32 * qb + _crow(e, lane >> 5)
+                keepb[:, qbk, kbk] = bit_b
+    refp = ref.reshape(B * Hq, S, S)
+    valid = torch.ones(S, S, dtype=torch.bool)
+    if causal:
+        valid = torch.ones(S, S, dtype=torch.bool).tril()
+    for got in (keepf[:, :S, :S], keepb[:, :S, :S]):
+        assert torch.equal(got[:, valid], refp[:, valid])
+    rate = 1.0 - refp[:, valid].float().mean().item()
+    assert abs(rate - p) < 0.02, rate
 
 
 def test_gpt_layer_gpu_matches_cpu_reference():
@@ -205,7 +273,7 @@ def test_gpt_layer_gpu_matches_cpu_reference():
     from mxtrain.models.gpt import GPTConfig, GPTStage, gpt_param_specs
     from mxtrain.parallel.buffers import FlatParams
     cfg = GPTConfig(num_layers=2, hidden_size=256, num_attention_heads=4, seq_length=128,
-                    max_position_embeddings=128, vocab_size=512, hidden_dropout=0.0)
+                    max_position_embeddings=128, vocab_size=512, hidden_dropout=0.0, attention_dropout=0.0)
     B, S = 2, 128
     specs = gpt_param_specs(cfg)
     fc = FlatParams(specs, "cpu", torch.float32)
@@ -261,7 +329,7 @@ def test_gpt_llama_style_layer_gpu_matches_cpu_reference():
     from mxtrain.parallel.buffers import FlatParams
     cfg = GPTConfig(num_layers=2, hidden_size=512, num_attention_heads=4, num_kv_heads=2,
                     seq_length=128, max_position_embeddings=128, vocab_size=512,
-                    hidden_dropout=0.0, normalization="rmsnorm", position_embedding="rope",
+                    hidden_dropout=0.0, attention_dropout=0.0, normalization="rmsnorm", position_embedding="rope",
                     swiglu=True, ffn_hidden_size=1024)
     B, S = 2, 128
     specs = gpt_param_specs(cfg)
@@ -366,7 +434,7 @@ def test_moe_gpt_gpu_matches_cpu_and_captures():
     from mxtrain.parallel.buffers import FlatParams
     from mxtrain.training import GPTTrainer, TrainConfig, synthetic_batch
     cfg = GPTConfig(num_layers=2, hidden_size=256, num_attention_heads=4, seq_length=128,
-                    max_position_embeddings=128, vocab_size=512, hidden_dropout=0.0, num_experts=4,
+                    max_position_embeddings=128, vocab_size=512, hidden_dropout=0.0, attention_dropout=0.0, num_experts=4,
                     expert_interval=1, moe_topk=2, moe_train_capacity_factor=2.0)
     B, S = 2, 128
     gen = torch.Generator().manual_seed(0)

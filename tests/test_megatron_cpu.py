@@ -149,6 +149,12 @@ def test_pretrain_resume_is_exact(tmp_path, monkeypatch):
     assert oa["zero_stage"] == 1 and oa["base_optimizer_state"]["state"][0]["step"] == 8
     lines = [json.loads(x) for x in open(tmp_path / "logs" / "metrics-rank0.jsonl")]
     assert [r["step"] for r in lines if "loss" in r][:4] == [2, 4, 6, 8]
+    # the --fp16 -> bf16 rewrite and the effective dropout settings are recorded, not silent
+    cfg_ev = [r for r in lines if r.get("event") == "config"]
+    assert cfg_ev and cfg_ev[0]["effective"]["attention_dropout"] == 0.1
+    assert any("--fp16 -> bf16" in d for d in cfg_ev[0]["deviations"])
+    assert a["args"]["mx_effective"]["compute_dtype"] == "bf16"
+    assert any("--fp16 -> bf16" in d for d in a["args"]["mx_deviations"])
 
 
 def test_qkv_megatron_interleave_roundtrip():
@@ -175,3 +181,8 @@ def test_ds_config_and_megatron_flags(tmp_path):
                     "--tensor-model-parallel-size", "1"])
     assert a.micro_batch_size == 8 and a.zero_stage == 1 and a.fp16
     assert a.lr_warmup_iters == 3200 and a.global_batch_size == 8
+    assert any("--no-masked-softmax-fusion" in d for d in a.mx_deviations)
+    assert a.mx_effective["attention_dropout"] == 0.1 and not a.mx_recompute
+    b = parse_args(["--checkpoint-activations", "--zero-stage", "2"])
+    assert b.mx_recompute and b.mx_effective["activation_recompute"] == "full"
+    assert any("ZeRO stage 2 -> stage 1" in d for d in b.mx_deviations)

@@ -17,7 +17,7 @@ from mxtrain.parallel.buffers import FlatParams
 from gpt_reference import gelu_tanh, ref_loss
 
 MOE = dict(num_layers=2, hidden_size=32, num_attention_heads=2, seq_length=8,
-           max_position_embeddings=8, vocab_size=64, hidden_dropout=0.0, num_experts=4,
+           max_position_embeddings=8, vocab_size=64, hidden_dropout=0.0, attention_dropout=0.0, num_experts=4,
            expert_interval=1, moe_topk=2, moe_train_capacity_factor=1.0, moe_min_capacity=2,
            moe_loss_coeff=0.05)
 
