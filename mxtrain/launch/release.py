@@ -39,8 +39,24 @@ def releases_root() -> str:
     return os.path.join(mxtrain_home(), "releases")
 
 
+_NAME_RE = None
+
+
+def check_name(value: str, what: str = "name") -> str:
+    """Release / namespace / claim names are single path components (Kubernetes object
+    names): no separators, no '..', no leading dot.  Everything that turns an API path
+    segment into a file path goes through here."""
+    global _NAME_RE
+    if _NAME_RE is None:
+        import re
+        _NAME_RE = re.compile(r"^[A-Za-z0-9_][A-Za-z0-9_.\-]{0,252}$")
+    if not isinstance(value, str) or not _NAME_RE.match(value) or ".." in value:
+        raise PermissionError(f"invalid {what}: {value!r}")
+    return value
+
+
 def release_dir(name: str, namespace: str = DEFAULT_NS) -> str:
-    return os.path.join(releases_root(), namespace, name)
+    return os.path.join(releases_root(), check_name(namespace, "namespace"), check_name(name, "release name"))
 
 
 def _write_json(path: str, obj):

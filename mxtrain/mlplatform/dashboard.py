@@ -66,6 +66,8 @@ def job(namespace: str, name: str) -> dict:
 
 def job_logs(namespace: str, name: str, pod: Optional[str] = None) -> str:
     from ..launch import release as rel
+    if pod is not None:
+        rel.check_name(pod, "pod")
     return rel.logs(name, namespace, pod)
 
 
@@ -97,7 +99,14 @@ def volumes() -> List[dict]:
 
 
 def volume_browse(claim: str, rel_path: str = "") -> dict:
-    root = os.path.realpath(os.path.join(pv_root(), claim))
+    from ..launch.release import check_name
+    base = os.path.realpath(pv_root())
+    check_name(claim, "claim")
+    if claim not in os.listdir(base):
+        raise FileNotFoundError(f"no volume {claim!r}")
+    root = os.path.realpath(os.path.join(base, claim))
+    if os.path.commonpath([base, root]) != base:
+        raise PermissionError("volume escapes the PV root")
     target = os.path.realpath(os.path.join(root, rel_path.lstrip("/")))
     if not (target == root or target.startswith(root + os.sep)):
         raise PermissionError("path escapes the volume")

@@ -14,7 +14,11 @@ fp32 gradients the same way; the modules look their copy up with ``cw(param, dty
         losses = model(...)            # modules call cw(p, dt) / folded convs call cw(w)
 
 Gradients reach the fp32 parameters through the Function, so optimizers, clipping and
-gradient hooks are unchanged.  Frozen parameters (requires_grad False) are not
+gradient hooks are unchanged.  Under data parallelism the specs are cut into ``groups``
+contiguous node groups (model order): a group's fp32 gradients -- and so its DDP / Horovod
+bucket hooks -- become ready as soon as backward has passed the first module that uses
+it, instead of all at the very end of backward, so the gradient all-reduce overlaps the
+rest of backward again.  Frozen parameters (requires_grad False) are not
 included: their modules keep caching their own copies (resnet.ConvNorm._folded).
 """
 from __future__ import annotations
@@ -83,18 +87,38 @@ class ComputeWeights:
     """Context manager: builds the compute copies of ``specs`` = [(param, fold_scale or
     None)] once on entry (one autograd node) and makes them visible to cw()."""
 
-    def __init__(self, specs: Sequence[Tuple[torch.Tensor, Optional[torch.Tensor]]], dt: torch.dtype):
+    def __init__(self, specs: Sequence[Tuple[torch.Tensor, Optional[torch.Tensor]]], dt: torch.dtype,
+                 groups: int = 1):
         self.specs = [(p, s) for p, s in specs if p.requires_grad]
         self.dt = dt
+        self.groups = max(1, int(groups))
+
+    @staticmethod
+    def split(specs, groups: int):
+        """Contiguous chunks of ~equal parameter count (model order kept)."""
+        if groups <= 1 or len(specs) <= 1:
+            return [list(specs)]
+        total = sum(p.numel() for p, _ in specs)
+        out, cur, acc = [], [], 0
+        for p, s in specs:
+            cur.append((p, s))
+            acc += p.numel()
+            if acc >= total * (len(out) + 1) / groups and len(out) < groups - 1:
+                out.append(cur)
+                cur = []
+        if cur:
+            out.append(cur)
+        return out
 
     def __enter__(self):
         if self.specs and torch.is_grad_enabled():
-            params = [p for p, _ in self.specs]
-            scales = [s for _, s in self.specs]
-            scaled = [i for i, s in enumerate(scales) if s is not None]
-            outs = _CastAll.apply(self.dt, scales, scaled, *params)
-            for p, o in zip(params, outs):
-                _ACTIVE[id(p)] = o
+            for chunk in self.split(self.specs, self.groups):
+                params = [p for p, _ in chunk]
+                scales = [s for _, s in chunk]
+                scaled = [i for i, s in enumerate(scales) if s is not None]
+                outs = _CastAll.apply(self.dt, scales, scaled, *params)
+                for p, o in zip(params, outs):
+                    _ACTIVE[id(p)] = o
         return self
 
     def __exit__(self, *exc):

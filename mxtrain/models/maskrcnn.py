@@ -344,9 +344,14 @@ class MaskRCNN(nn.Module):
         convs, params, key, specs = cache
         # the list only changes when frozen statistics are rewritten (calibration,
         # checkpoint load: version bumps) or parameters are (un)frozen
-        nkey = (tuple(m.norm.running_var._version + m.norm.running_mean._version + m.norm.weight._version
-                      + m.norm.bias._version for m in convs if m.norm_kind == "frozen"),
-                tuple(p.requires_grad for p in params))
+        # (device and storage identity too: .to(device) / load_state_dict(assign=True)
+        # replace the buffers with fresh version-0 tensors)
+        nkey = (tuple((m.norm.running_var._version + m.norm.running_mean._version + m.norm.weight._version
+                       + m.norm.bias._version, m.norm.running_var.data_ptr(), m.norm.running_mean.data_ptr(),
+                       m.norm.weight.data_ptr(), m.norm.bias.data_ptr())
+                      for m in convs if m.norm_kind == "frozen"),
+                tuple((p.requires_grad, p.data_ptr()) for p in params),
+                str(params[0].device) if params else "")
         if nkey == key:
             return specs
         specs = []
@@ -366,7 +371,11 @@ class MaskRCNN(nn.Module):
                 gt_mask_table=None):
         if images.device.type != "cuda" or not torch.is_grad_enabled():
             return self._forward(images, img_hw, gt_boxes, gt_labels, gt_count, gt_masks, gt_mask_table)
-        with ComputeWeights(self.compute_weight_specs(), self.compute_dtype(images.device)):
+        # under data parallelism several cast nodes, so gradient buckets become ready in
+        # backward order (all-reduce overlapped with backward); one node on a single GPU
+        groups = 8 if (torch.distributed.is_available() and torch.distributed.is_initialized()
+                       and torch.distributed.get_world_size() > 1) else 1
+        with ComputeWeights(self.compute_weight_specs(), self.compute_dtype(images.device), groups=groups):
             return self._forward(images, img_hw, gt_boxes, gt_labels, gt_count, gt_masks, gt_mask_table)
 
     def _forward(self, images, img_hw, gt_boxes=None, gt_labels=None, gt_count=None, gt_masks=None,

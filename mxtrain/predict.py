@@ -58,7 +58,7 @@ def predict_images(model, paths, device, out_dir, short=800, max_size=1333, scor
             m28 = res["masks"][0].cpu()[valid].numpy()
             canvas = np.asarray(overlay).copy()
             for k in range(len(scores)):
-                full = paste_mask(m28[k], boxes[k], h0, w0)
+                full = paste_mask(m28[k], boxes[k], h0, w0, mask_thresh)
                 mask_px.append(int(full.sum()))
                 col = np.array([(37 * int(labels[k])) % 255, (91 * int(labels[k])) % 255, 160])
                 canvas[full] = (0.5 * canvas[full] + 0.5 * col).astype(np.uint8)

@@ -12,8 +12,12 @@ mode predict (the notebook):   GET /             newest checkpoint, links
 mode metrics (TensorBoard):    GET /             stats.json (COCO mAP per epoch) + training
                                                  metrics JSONL as tables
                                GET /stats.json   raw
-Both modes: optional TLS (--certfile/--keyfile) and HTTP basic auth (--htpasswd with
-`user:{SHA}base64` or `user:plaintext` lines, like the nginx front-end).
+Both modes: TLS (--certfile/--keyfile) and HTTP basic auth (--htpasswd with
+`user:{SHA}base64` or `user:plaintext` lines, like the nginx front-end).  Fail-closed: a
+--certfile / --keyfile / --htpasswd that is given but missing (or an htpasswd with no
+users) stops the server instead of silently serving plain HTTP or no auth (``--tls off``
+and ``--insecure-no-auth`` are the explicit opt-outs; the latter is refused on a
+non-loopback bind address), and ``?image=`` only opens files under --data-dir.
 """
 from __future__ import annotations
 
@@ -33,6 +37,32 @@ import urllib.parse
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
 
+class ConfigError(SystemExit):
+    pass
+
+
+def load_users(path):
+    users = {}
+    for line in open(path):
+        line = line.strip()
+        if ":" in line:
+            u, h = line.split(":", 1)
+            if u and h:
+                users[u] = h
+    return users
+
+
+def safe_image_path(data_dir: str, img: str) -> str:
+    """realpath of a requested image, which must lie under realpath(data_dir)."""
+    root = os.path.realpath(data_dir)
+    cand = os.path.realpath(img if os.path.isabs(img) else os.path.join(root, img))
+    if os.path.commonpath([root, cand]) != root:
+        raise PermissionError(f"image outside the data directory: {img}")
+    if not os.path.isfile(cand):
+        raise FileNotFoundError(img)
+    return cand
+
+
 class State:
     def __init__(self, args):
         self.args = args
@@ -40,12 +70,16 @@ class State:
         self.ckpt = None
         self.lock = threading.Lock()
         self.users = {}
-        if args.htpasswd and os.path.exists(args.htpasswd):
-            for line in open(args.htpasswd):
-                line = line.strip()
-                if ":" in line:
-                    u, h = line.split(":", 1)
-                    self.users[u] = h
+        if args.htpasswd:
+            if not os.path.isfile(args.htpasswd):
+                raise ConfigError(f"--htpasswd {args.htpasswd} does not exist (refusing to serve without auth)")
+            self.users = load_users(args.htpasswd)
+            if not self.users:
+                raise ConfigError(f"--htpasswd {args.htpasswd} holds no user:hash line")
+        elif not getattr(args, "insecure_no_auth", False):
+            raise ConfigError("no --htpasswd given: pass one, or --insecure-no-auth for a loopback-only viewer")
+        elif args.host not in ("127.0.0.1", "localhost", "::1"):
+            raise ConfigError(f"--insecure-no-auth is only allowed on a loopback address, not {args.host}")
 
     def check_auth(self, header) -> bool:
         if not self.users:
@@ -110,6 +144,8 @@ def make_handler(st: State):
                 if st.args.mode == "metrics":
                     return self.metrics(u.path)
                 return self.predict(u.path, q)
+            except PermissionError as e:
+                return self._send(403, html.escape(str(e)).encode())
             except FileNotFoundError as e:
                 return self._send(404, html.escape(str(e)).encode())
             except Exception as e:  # noqa: BLE001
@@ -144,7 +180,9 @@ def make_handler(st: State):
                 import tempfile
                 from ..predict import predict_images
                 img = (q.get("image") or [None])[0]
-                if not img:
+                if img:
+                    img = safe_image_path(st.args.data_dir, img)
+                else:
                     c = sorted(glob.glob(os.path.join(st.args.data_dir, "test2017", "*.jpg")))
                     if not c:
                         raise FileNotFoundError(f"no test2017 images under {st.args.data_dir}")
@@ -153,7 +191,8 @@ def make_handler(st: State):
                     m = st.load_model()
                     out = tempfile.mkdtemp(prefix="viewer-")
                     rec = predict_images(m, [img], st.dev, out, st.cfg.PREPROC.TRAIN_SHORT,
-                                         int(st.cfg.PREPROC.MAX_SIZE), st.args.score_thresh)[0]
+                                         int(st.cfg.PREPROC.MAX_SIZE), st.args.score_thresh,
+                                         st.args.mask_thresh)[0]
                 if path == "/predict.json":
                     return self._send(200, json.dumps(rec).encode(), "application/json")
                 return self._send(200, open(rec["output"], "rb").read(), "image/png")
@@ -169,20 +208,35 @@ def main(argv=None):
     ap.add_argument("--mode", default="predict", choices=["predict", "metrics"])
     ap.add_argument("--data-dir", default="/fsx/data/coco2017")
     ap.add_argument("--score-thresh", type=float, default=0.7)
+    ap.add_argument("--mask-thresh", type=float, default=0.5)
     ap.add_argument("--certfile", default=None)
     ap.add_argument("--keyfile", default=None)
+    ap.add_argument("--tls", default="auto", choices=["auto", "off"],
+                    help="auto: TLS when --certfile/--keyfile are given (they must exist); off: plain HTTP")
     ap.add_argument("--htpasswd", default=None)
+    ap.add_argument("--insecure-no-auth", action="store_true",
+                    help="serve without basic auth (loopback bind addresses only)")
     ap.add_argument("--config", nargs="*", default=[])
     a = ap.parse_args(argv)
-    st = State(a)
+    try:
+        st = State(a)
+        ctx = None
+        if a.tls != "off" and (a.certfile or a.keyfile):
+            for f in (a.certfile, a.keyfile):
+                if not f or not os.path.isfile(f):
+                    raise ConfigError(f"TLS certificate/key {f!r} missing (use --tls off to serve plain HTTP)")
+            ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+            ctx.load_cert_chain(a.certfile, a.keyfile)
+    except ConfigError as e:
+        print(f"[viewer] refusing to start: {e}", file=sys.stderr, flush=True)
+        return 2
     srv = ThreadingHTTPServer((a.host, a.port), make_handler(st))
-    if a.certfile and a.keyfile and os.path.exists(a.certfile) and os.path.exists(a.keyfile):
-        ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
-        ctx.load_cert_chain(a.certfile, a.keyfile)
+    if ctx is not None:
         srv.socket = ctx.wrap_socket(srv.socket, server_side=True)
-    print(f"[viewer] serving {a.mode} for {a.logdir} on {a.host}:{a.port}", flush=True)
+    print(f"[viewer] serving {a.mode} for {a.logdir} on {a.host}:{a.port} "
+          f"({'https' if ctx else 'http'}, basic auth {'on' if st.users else 'OFF (loopback)'})", flush=True)
     srv.serve_forever()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

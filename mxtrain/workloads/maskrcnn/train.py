@@ -106,7 +106,7 @@ def run_inference(model, loader, device, with_masks=True):
     return out
 
 
-def paste_mask(m28, box, H, W):
+def paste_mask(m28, box, H, W, thresh=0.5):
     import numpy as np
     import torch.nn.functional as F
     x0, y0, x1, y1 = [float(v) for v in box]
@@ -117,7 +117,7 @@ def paste_mask(m28, box, H, W):
     xs, ys = max(xa, 0), max(ya, 0)
     xe, ye = min(xa + w, W), min(ya + h, H)
     if xe > xs and ye > ys:
-        full[ys:ye, xs:xe] = (m[ys - ya:ye - ya, xs - xa:xe - xa] >= 0.5).numpy()
+        full[ys:ye, xs:xe] = (m[ys - ya:ye - ya, xs - xa:xe - xa] >= thresh).numpy()
     return full
 
 
@@ -195,18 +195,6 @@ def main(argv=None):
     C.finalize(cfg, world, args.images_per_epoch)
     if device.type == "cuda" and hasattr(torch.backends.cuda, "preferred_blas_library"):
         torch.backends.cuda.preferred_blas_library("hipblaslt")
-    # Convolution algorithm search: torch's benchmark mode runs MIOpen find once per conv
-    # shape and caches the choice, so a steady-state conv call skips the per-call solution
-    # query of immediate mode (~30 us host per call, ~240 calls per step) and gets the
-    # found solver.  MIOPEN_FIND_MODE=FAST keeps the search to the fast candidates.
-    # Measured on one MI355X: 1 img/GPU 51 -> 66 img/s, 4 img/GPU 108 -> 129 img/s; the
-    # one-time search costs ~4 minutes on a fresh node (MIOpen's user find-db keeps it for
-    # later runs).  MXTRAIN_CONV_BENCHMARK=0 returns to immediate mode.
-    torch.backends.cudnn.benchmark = os.environ.get("MXTRAIN_CONV_BENCHMARK", "1") == "1"
-    if torch.backends.cudnn.benchmark:
-        os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
-        log("Convolution algorithm search on (MIOpen find, FAST mode): the first steps of each "
-            "input shape take minutes on a node without a MIOpen find-db")
     # MXTRAIN_MIOPEN=0: convolutions through torch's native GEMM path instead of MIOpen
     if os.environ.get("MXTRAIN_MIOPEN", "1") == "0":
         torch.backends.cudnn.enabled = False
@@ -256,6 +244,20 @@ def main(argv=None):
         return 0
 
     # ---------------------------------------------------------------- training
+    # Convolution algorithm search: torch's benchmark mode runs MIOpen find once per conv
+    # shape and caches the choice, so a steady-state conv call skips the per-call solution
+    # query of immediate mode (~30 us host per call, ~240 calls per step) and gets the
+    # found solver.  MIOPEN_FIND_MODE=FAST keeps the search to the fast candidates.
+    # Measured on one MI355X: 1 img/GPU 51 -> 66 img/s, 4 img/GPU 108 -> 129 img/s; the
+    # one-time search costs ~4 minutes on a fresh node (MIOpen's user find-db keeps it for
+    # later runs).  MXTRAIN_CONV_BENCHMARK=0 returns to immediate mode.
+    # Training only: the fixed training canvases make the search a one-time cost; predict /
+    # evaluate see arbitrary image sizes and stay in immediate mode (evaluate_epoch too).
+    torch.backends.cudnn.benchmark = os.environ.get("MXTRAIN_CONV_BENCHMARK", "1") == "1"
+    if torch.backends.cudnn.benchmark:
+        os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+        log("Convolution algorithm search on (MIOpen find, FAST mode): the first steps of each "
+            "input shape take minutes on a node without a MIOpen find-db")
     tbw = None
     from mxtrain.obs.profile import StepProfiler, check_finite, check_finite_enabled
     prof = StepProfiler(rank, out_dir=os.path.join(args.logdir, "profile") if os.environ.get("MXTRAIN_PROFILE") else None)
@@ -388,6 +390,15 @@ def main(argv=None):
 
 
 def evaluate_epoch(model, cfg, coll, device, rank, world, logdir, epoch, step):
+    bench = torch.backends.cudnn.benchmark
+    torch.backends.cudnn.benchmark = False   # arbitrary validation image sizes: no per-shape find
+    try:
+        _evaluate_epoch(model, cfg, coll, device, rank, world, logdir, epoch, step)
+    finally:
+        torch.backends.cudnn.benchmark = bench
+
+
+def _evaluate_epoch(model, cfg, coll, device, rank, world, logdir, epoch, step):
     from mxtrain.data.coco import COCODetection, DetectionDataset
     try:
         val = COCODetection(cfg.DATA.BASEDIR, cfg.DATA.VAL[0], training=False)

@@ -128,7 +128,8 @@ def test_jupyter_chart_viewer_serves_predictions(coco_dir, tmp_path, monkeypatch
     p1, p2 = _free_port(), _free_port()
     pw_hash = "{SHA}" + base64.b64encode(hashlib.sha1(b"secret").digest()).decode()
     rel.install(os.path.join(REPO, "charts", "machine-learning", "testing", "maskrcnn-jupyter"), "viewer",
-                sets=["global.log_dir=logs/run1", f"jupyter.target_port={p1}", f"tensorboard.target_port={p2}"],
+                sets=["global.log_dir=logs/run1", f"jupyter.target_port={p1}", f"tensorboard.target_port={p2}",
+                      "global.source_cidr=127.0.0.1/32", "nginx.tls=off"],
                 set_strings=[f"nginx.htpasswd={pw_hash}"])
     try:
         auth = {"Authorization": "Basic " + base64.b64encode(b"tensorboard:secret").decode()}
@@ -149,8 +150,81 @@ def test_jupyter_chart_viewer_serves_predictions(coco_dir, tmp_path, monkeypatch
         rec = json.loads(urllib.request.urlopen(urllib.request.Request(
             f"http://127.0.0.1:{p1}/predict.json", headers=auth), timeout=120).read())
         assert rec["output"].endswith(".png") and isinstance(rec["boxes"], list)
+        # ?image= is confined to --data-dir
+        with pytest.raises(urllib.error.HTTPError) as ei:
+            urllib.request.urlopen(urllib.request.Request(
+                f"http://127.0.0.1:{p1}/predict.json?image=/etc/passwd", headers=auth), timeout=30)
+        assert ei.value.code == 403
     finally:
         rel.uninstall("viewer")
+
+
+def test_jupyter_chart_requires_auth_and_cidr():
+    """the internet-facing testing charts must not render without an htpasswd
+    and a source CIDR (the reference marks both `required`)."""
+    from mxtrain.chart.render import load_chart, render_chart
+    from mxtrain.chart.template import TemplateError
+    for chart in ("maskrcnn-jupyter", "maskrcnn-optimized-jupyter"):
+        c = load_chart(os.path.join(REPO, "charts", "machine-learning", "testing", chart))
+        with pytest.raises(TemplateError, match="source_cidr"):
+            render_chart(c, "v", set_strings=["nginx.htpasswd=x"])
+        with pytest.raises(TemplateError, match="htpasswd"):
+            render_chart(c, "v", sets=["global.source_cidr=10.0.0.0/8"])
+        r = render_chart(c, "v", sets=["global.source_cidr=10.0.0.0/8"], set_strings=["nginx.htpasswd=x"])
+        dep = [m for m in r.manifests if m["kind"] == "Deployment"][0]
+        for ctr in dep["spec"]["template"]["spec"]["containers"]:
+            assert "--htpasswd=/etc/nginx/.htpasswd" in ctr["args"] and "--tls=auto" in ctr["args"]
+
+
+def test_viewer_fails_closed(tmp_path):
+    from mxtrain.serve import viewer
+    logdir = str(tmp_path)
+    # no auth configured on a public bind address, a missing htpasswd, an empty one, a
+    # missing certificate: the server refuses to start (exit 2) instead of degrading
+    assert viewer.main(["--logdir", logdir]) == 2
+    assert viewer.main(["--logdir", logdir, "--insecure-no-auth"]) == 2          # 0.0.0.0
+    assert viewer.main(["--logdir", logdir, "--htpasswd", str(tmp_path / "none")]) == 2
+    (tmp_path / "empty").write_text("\n")
+    assert viewer.main(["--logdir", logdir, "--htpasswd", str(tmp_path / "empty")]) == 2
+    (tmp_path / "pw").write_text("u:{SHA}abc\n")
+    assert viewer.main(["--logdir", logdir, "--htpasswd", str(tmp_path / "pw"),
+                        "--certfile", str(tmp_path / "c.crt"), "--keyfile", str(tmp_path / "c.key")]) == 2
+    data = tmp_path / "data"
+    (data / "test2017").mkdir(parents=True)
+    (data / "test2017" / "a.jpg").write_bytes(b"x")
+    assert viewer.safe_image_path(str(data), "test2017/a.jpg").endswith("a.jpg")
+    for bad in ("/etc/passwd", "../pw", "test2017/../../pw"):
+        with pytest.raises(PermissionError):
+            viewer.safe_image_path(str(data), bad)
+
+
+def test_prediction_flow_thresholds(tmp_path):
+    """The notebooks' visualisation flow (mask-rcnn-tensorflow-viz.ipynb show_detection_results,
+    get_mask; mask-rcnn-tensorpack-viz.ipynb newest model-*.index): newest checkpoint, boxes
+    with score >= 0.7 only, mask pixels where the pasted mask >= 0.5."""
+    import numpy as np
+    from PIL import Image
+    from mxtrain.predict import predict_images
+    from mxtrain.workloads.maskrcnn.train import latest_ckpt
+    for step in (5, 120, 40):
+        (tmp_path / f"model-{step}.index").write_text("")
+    assert latest_ckpt(str(tmp_path)).endswith("model-120")
+    Image.fromarray(np.zeros((64, 96, 3), dtype=np.uint8)).save(tmp_path / "img.jpg")
+    m = torch.zeros(3, 28, 28)
+    m[0, :14] = 0.9      # top half above the mask threshold
+    m[1] = 0.49          # everywhere just below it
+    m[2] = 1.0
+
+    class Fake(torch.nn.Module):
+        def forward(self, images, sizes):
+            return {"boxes": torch.tensor([[[0., 0., 40., 40.], [10., 10., 30., 30.], [5., 5., 9., 9.]]]),
+                    "scores": torch.tensor([[0.95, 0.70, 0.69]]),
+                    "labels": torch.tensor([[1, 2, 3]]), "masks": m[None]}
+    rec = predict_images(Fake(), [str(tmp_path / "img.jpg")], "cpu", str(tmp_path / "out"), short=64, max_size=96)[0]
+    assert rec["scores"] == pytest.approx([0.95, 0.7])   # 0.69 < 0.7 dropped
+    assert rec["mask_pixels"][1] == 0                    # 0.49 < 0.5 everywhere
+    assert 0 < rec["mask_pixels"][0] < 40 * 40
+    assert os.path.exists(rec["output"])
 
 
 def _small_model_cfg():

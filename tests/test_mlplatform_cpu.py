@@ -111,6 +111,13 @@ def test_dashboard_routes_and_auth(home, tmp_path):
     code, _, body = db.route("/api/volumes/pv-fsx", {"path": "data"})
     assert [e["name"] for e in json.loads(body)["entries"]] == ["a.txt"]
     assert db.route("/api/volumes/pv-fsx", {"path": "../../.."})[0] == 403
+    # encoded separators in the claim / namespace / name segments cannot escape
+    assert db.route("/api/volumes/..%2F..%2F..", {"path": "etc"})[0] == 403
+    assert db.route("/api/volumes/no-such-claim", {})[0] == 404
+    assert db.route("/api/jobs/..%2F..%2F../dash/logs", {})[0] == 403
+    assert db.route("/api/jobs/kubeflow-user-example-com/..%2Fx/logs", {})[0] == 403
+    assert db.route("/api/jobs/kubeflow-user-example-com/..", {})[0] == 403
+    assert db.route("/api/jobs/kubeflow-user-example-com/dash/logs", {"pod": "../x"})[0] == 403
     code, _, body = db.route("/api/tensorboards", {"logdir": str(tmp_path / "tb")})
     assert json.loads(body)["loss"][0]["value"] == 2.0
     assert db.route("/tensorboard", {"logdir": str(tmp_path / "tb")})[2].count("<svg") == 1
