@@ -1,0 +1,1082 @@
+// Flash attention v3 for gfx950 (CDNA4): forward, atomics-free backward, attention dropout.
+//
+// Replaces the Megatron fused `scaled_upper_triang_masked_softmax` + two batched GEMMs +
+// attention dropout (GPT, causal) and the HF BERT padded-softmax attention + dropout the
+// reference runs upstream (containers/megatron-deepspeed/Dockerfile:13, examples/
+// megatron-deepspeed/gpt2_345m/pretrain-ddp-zero1.yaml:39-53 -- Megatron's default
+// --attention-dropout 0.1 --; examples/accelerate/bert-glue-mrpc/pretrain.yaml:45;
+// SURVEY §2.8 K1/K2).  No S x S matrix is materialised.
+//
+// Layout: Q/K/V are read in place from the packed QKV projection output ([tokens, heads, D]
+// with a token stride), O / dQ / dK / dV are written token-major, so the model needs no
+// transposes.  lse is base-2: lse2 = max*c + log2(sum), c = scale*log2(e).
+//
+// Three kernels, 4-wave workgroups (two per CU = 2 waves per SIMD), one barrier per tile.
+// One 128-row block per workgroup: every wave is busy on every tile it waits for (a
+// mirrored causal pair in one workgroup left half of the waves idle for most tiles), the two
+// workgroups of a CU hide each other's barriers, and under a causal mask the heaviest blocks
+// are dispatched first so the hardware dispatcher balances the tail; the blocks of one head
+// are dealt to one XCD, so its K/V (or Q/dO) stream is shared in that XCD's L2.
+//   qmajor<FWD>  each wave owns 32 query rows (query on the MFMA lane: S^T = K Q^T,
+//                O^T = V^T P^T, the row statistics are lane-local plus one permlane32 swap).  K/V tiles of 128 keys arrive by LDS-DMA
+//                (global_load_lds_dwordx4: no staging registers, no ds_write) into a two-slot
+//                ring; the swizzle is applied on the SOURCE addresses so the 1-KiB DMA pieces
+//                land in the conflict-free image the row reads (ds_read_b128) and transposed
+//                reads (ds_read_b64_tr_b16) both use.
+//   qmajor<DQ>   same skeleton for dQ: recomputes S^T and dP^T = V dO^T per 32-key subtile,
+//                dS^T = P^T (dP^T - delta) -> dQ^T += K^T dS^T (K^T by transposed LDS reads).
+//                delta = rowsum(dO O) is computed in the prologue (no pre-pass kernel) and
+//                published for kmajor; dQ is written once in bf16 (no fp32 accumulator, no
+//                atomics, no convert kernel).
+//   kmajor       each wave keeps dK^T / dV^T of its 32 keys in accumulators (key on the lane: P and dS are
+//                ready-made B operands) while Q / dO / lse / delta tiles of 64 rows stream
+//                through an LDS-DMA ring (32 rows for D = 128).  D = 128 keeps K in LDS and
+//                splits the dK/dV columns into two passes (register budget at 2 waves/SIMD).
+// The 5-GEMM single backward would need dQ summed across key blocks: with fp32 atomics that
+// is bounded by the ~1.3 TB/s chip atomic rate (MI355X_MICROARCH.md "Global float atomics"),
+// 33 MB / 26 us per GPT-2 layer; the recompute costs 1.4x the MFMA work but no atomics.
+//
+// Attention dropout: keep-mask M[b,h,q,k] is a pure function of (seed, global row, key):
+// per (row, 32-key block, lane half) one hash32 seeds an xorshift32 stream whose 16-bit
+// halves are the draws (drop_stream_bits; keep <=> draw >= thr16), row = (b * Hg + h_global)
+// * S + q (16-bit threshold: p exact to 2^-16; ops/attention.py::dropout_keep_mask is the
+// reference).
+// flash_dropmask_kernel evaluates it once per forward (on a side stream, concurrent with the
+// QKV GEMM) into two lane-bit images laid out so that each packed bf16 pair is masked with
+// three VALU ops (shift, v_pk_ashrrev_i16, and): 16 bits per lane per 32x32 block, element
+// 2j at bit sh+j and 2j+1 at bit sh+16+j of a 32-bit word holding two blocks (sh = 0 / 8).
+#include "common.h"
+
+using namespace mx;
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef short short2_t __attribute__((ext_vector_type(2)));
+
+// ------------------------------------------------------------------------------ helpers
+// Chunk swizzle for a [rows][D] bf16 tile (D*2-byte rows, 16-B chunks).
+//  D=64 (128-B rows, two rows per 256-B bank row): f = x ^ ((x&1)<<2), x = (row>>1)&7
+//  D=128 (256-B rows): f = ((row&3)<<2) | ((row>>2)&3)
+// Both keep the row reads (ds_read_b128, 32 rows) and the transposed reads (4 consecutive
+// rows x 32 columns per half-wave) conflict-free; f depends on row bits 0-3 only, so a
+// 32-row step is an immediate offset.
+template <int D>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (D == 64) {
+    int x = (row >> 1) & 7;
+    return x ^ ((x & 1) << 2);
+  } else {
+    return ((row & 3) << 2) | ((row >> 2) & 3);
+  }
+}
+template <int D>
+__device__ __forceinline__ int toff(int row, int chunk) {
+  return row * (D * 2) + ((chunk ^ swz<D>(row)) << 4);
+}
+__device__ __forceinline__ bf16x4 tr_read(const char* lds, int byte_off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(lds + byte_off));
+}
+__device__ __forceinline__ bf16x8 cat(bf16x4 a, bf16x4 b) {
+  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+__device__ __forceinline__ bf16x8 ld8(const uint16_t* p) {
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p));
+}
+__device__ __forceinline__ bf16x8 lds8(const char* base, int off) {
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + off));
+}
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int crow(int e, int hh) { return (e & 3) + 8 * (e >> 2) + 4 * hh; }
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// one 1-KiB LDS-DMA piece: lane i's 16 B from `g` land at lds_base + 16 i
+__device__ __forceinline__ void dma16(const void* g, char* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void_t*)lds_base, 16, 0, 0);
+}
+__device__ __forceinline__ void dma4(const void* g, char* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void_t*)lds_base, 4, 0, 0);
+}
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// dropout: all-ones halves for the kept elements of packed pair j (elements 2j, 2j+1)
+__device__ __forceinline__ uint32_t pair_keep(uint32_t w, int sh, int j) {
+  short2_t v = __builtin_bit_cast(short2_t, w << (15 - sh - j));
+  v = v >> (short2_t){15, 15};
+  return __builtin_bit_cast(uint32_t, v);
+}
+// all-ones if element e is kept
+__device__ __forceinline__ uint32_t elem_keep(uint32_t w, int sh, int e) {
+  return (uint32_t)__builtin_amdgcn_sbfe((int)w, (uint32_t)(sh + 16 * (e & 1) + (e >> 1)), 1u);
+}
+__device__ __forceinline__ bf16x8 pack8(const f32x16& acc, int base) {
+  uint4 u;
+  u.x = pack2(acc[base + 0], acc[base + 1]);
+  u.y = pack2(acc[base + 2], acc[base + 3]);
+  u.z = pack2(acc[base + 4], acc[base + 5]);
+  u.w = pack2(acc[base + 6], acc[base + 7]);
+  return __builtin_bit_cast(bf16x8, u);
+}
+__device__ __forceinline__ bf16x8 pack8_keep(const f32x16& acc, int base, uint32_t w, int sh) {
+  const int j0 = base >> 1;
+  uint4 u;
+  u.x = pack2(acc[base + 0], acc[base + 1]) & pair_keep(w, sh, j0 + 0);
+  u.y = pack2(acc[base + 2], acc[base + 3]) & pair_keep(w, sh, j0 + 1);
+  u.z = pack2(acc[base + 4], acc[base + 5]) & pair_keep(w, sh, j0 + 2);
+  u.w = pack2(acc[base + 6], acc[base + 7]) & pair_keep(w, sh, j0 + 3);
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+// workgroup id -> (block rank, head): block ranks in dispatch order (rank 0 first, so the
+// caller maps rank 0 to the heaviest causal block), and, when the head count is a multiple
+// of 8, every block of a head on one XCD (workgroups are dealt round-robin over the 8 XCDs,
+// id % 8): its K/V (Q/dO) stream is then read once into that XCD's L2.
+__device__ __forceinline__ void block_map(int nheads, int& rank, int& head) {
+  const int L = blockIdx.x;
+  if ((nheads & 7) == 0) {
+    const int x = L & 7, idx = L >> 3, nh8 = nheads >> 3;
+    rank = idx / nh8;
+    head = (idx - rank * nh8) * 8 + x;
+  } else {
+    rank = L / nheads;
+    head = L - rank * nheads;
+  }
+}
+
+// ============================================================================ dropout mask
+// The random bits of one (query row, 32-key block, lane half hh) -- the 16 keys
+// crow(e, hh) of a lane -- come from ONE hash and an xorshift32 stream: x0 = hash32(row *
+// 0x85EBCA6B + 2 kb + hh, seed) (| 1: never the all-zero fixed point), x_{j+1} = xorshift(x_j);
+// x_j holds the 16-bit draws of the lane's pair j (elements 2j, 2j+1 = keys crow(2j, hh) and
+// +1) in its low / high half.  Returns the lane's 16 keep bits in pair layout: element 2j at
+// bit j, 2j+1 at bit 8 + j -- so a 32-bit word of two blocks holds (sh = 0 / 8) element 2j
+// at sh + j and 2j+1 at sh + 16 + j after the second block is shifted in by 8.
+__device__ __forceinline__ uint32_t drop_stream_bits(uint32_t rbase, uint32_t kb, int hh,
+                                                     uint32_t seed, uint32_t thr16) {
+  uint32_t x = hash32(rbase + 2u * kb + (uint32_t)hh, seed) | 1u;
+  // both 16-bit draws of x at once: sat(x - (thr-1)) is non-zero iff draw >= thr, min(., 1)
+  // leaves the keep bit at bit 0 / 16 (v_pk_sub_u16 clamp + v_pk_min_u16), then shift-or
+  // (thr16 == 0: thr2 = 0xFFFF'FFFF subtracts to 0 only for 0xFFFF draws -- p = 0 never
+  // reaches here, the host only generates masks for p > 0)
+  const uint32_t thr2 = ((thr16 - 1) & 0xFFFFu) * 0x00010001u;
+  const uint32_t one2 = 0x00010001u;
+  uint32_t bits = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (j) { x ^= x << 13; x ^= x >> 17; x ^= x << 5; }
+    uint32_t t;
+    asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(t) : "v"(x), "v"(thr2));
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(t) : "v"(t), "v"(one2));
+    bits |= t << j;
+  }
+  return bits;
+}
+
+// One wave per 64x64 group (query blocks 2qb2, 2qb2+1 x key blocks 2kb2, 2kb2+1).
+// fwd image (query on lane): u64 [B*Hq][NB][NKT][64 lanes], 16 bits per 32-key subtile,
+//   subtile t of a 128-key tile in word t>>1 at sh = 8 (t & 1).
+// bwd image (key on lane):   u32 [B*Hq][NB][NQT][64 lanes], 16 bits per 32-query half of a
+//   64-query tile at sh = 8 u.
+__global__ __launch_bounds__(256) void flash_dropmask_kernel(
+    const uint32_t* __restrict__ seed_ptr, uint32_t salt, uint32_t thr16, int S, int Hq,
+    int h_off, int Hg, int NB, int NKT, int NQT, int causal, uint32_t* __restrict__ fwd_bits,
+    uint32_t* __restrict__ bwd_bits) {
+  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
+  const int qb2 = blockIdx.x, kb2 = blockIdx.y * 4 + w, bh = blockIdx.z;
+  const int NB2 = (NB + 1) >> 1;
+  __shared__ uint32_t fw[4][2][64];
+  const bool live = kb2 < NB2 && !(causal && kb2 > qb2);
+  const int b = bh / Hq, h = bh - b * Hq;
+  const int r = lane & 31, hh = lane >> 5;
+  if (live) {
+    const uint32_t seed = *seed_ptr + salt;
+    uint32_t fb[2][2];
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      const uint32_t row = (uint32_t)(((long long)b * Hg + h_off + h) * S + (2 * qb2 + qq) * 32 + r);
+      const uint32_t rbase = row * 0x85EBCA6Bu;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        fb[qq][kk] = drop_stream_bits(rbase, (uint32_t)(2 * kb2 + kk), hh, seed, thr16);
+      // forward word of query block 2 qb2 + qq: key blocks 2 kb2 (sh 0) and 2 kb2 + 1 (sh 8)
+      const int qb = 2 * qb2 + qq;
+      if (qb < NB)
+        fwd_bits[(((size_t)bh * NB + qb) * NKT + (kb2 >> 1)) * 128 + lane * 2 + (kb2 & 1)] =
+            fb[qq][0] | (fb[qq][1] << 8);
+      fw[w][qq][lane] = fb[qq][0] | (fb[qq][1] << 8);
+    }
+  }
+  __syncthreads();
+  if (!live) return;
+  // backward image: lane = key kl of key block 2 kb2 + kk; element e -> query crow(e, hh) of
+  // query block 2 qb2 + u, read from forward lane crow(e, hh) + 32 ((kl >> 2) & 1), whose
+  // element ef = (kl & 3) + 4 (kl >> 3) sits at bit 8 kk + 16 (ef & 1) + (ef >> 1)
+  const int kl = r;
+  const int ef = (kl & 3) + 4 * (kl >> 3), fhi = 32 * ((kl >> 2) & 1);
+  const int fpos = 16 * (ef & 1) + (ef >> 1);
+  uint32_t wb[2] = {0u, 0u};
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t src = fw[w][u][crow(e, hh) + fhi];
+      const int pos = 8 * u + 16 * (e & 1) + (e >> 1);
+      wb[0] |= __builtin_amdgcn_ubfe(src, (uint32_t)fpos, 1u) << pos;
+      wb[1] |= __builtin_amdgcn_ubfe(src, (uint32_t)(8 + fpos), 1u) << pos;
+    }
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int kb = 2 * kb2 + kk;
+    if (kb < NB) bwd_bits[(((size_t)bh * NB + kb) * NQT + qb2) * 64 + lane] = wb[kk];
+  }
+}
+
+// ============================================================================ query-major
+// DQ false: forward (o, lse out).  DQ true: dQ (o, dout, lse in; delta, dq out).
+//
+// PAIR (D = 64): one 8-wave workgroup = two 4-wave teams with a K/V ring each.  Causal: the
+// mirrored block pair (L = i, H = n-1-i) holds n+1 key tiles of work; team 0 takes H's first
+// T = ceil(total/2) tiles, team 1 takes all of L and H's remaining tiles, so both teams run
+// T steps (one shared barrier per step) and every workgroup does the same work.  Team 1
+// hands its partial (m, l, O^T) -- or dQ^T -- of H to team 0 through LDS at the end (same
+// lane <-> (row, column) mapping in both teams: an element-wise merge).  Non-causal: team
+// t takes block 2i+t whole.  The critical path is ~half the heaviest block's tiles.
+// !PAIR (D = 128): one 4-wave workgroup per block (two per CU), heaviest block first.
+template <int D, bool PAIR>
+struct QCfg {
+  static constexpr int BK = 64;
+  static constexpr int NT = PAIR ? 512 : 256;
+  static constexpr int WPE = 2;
+};
+
+template <int D, bool CAUSAL, bool DROP, bool DQ, bool PAIR>
+__global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_eu(2, 2))) void flash_qmajor_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, int ldq, int ldk, int ldv,
+    const uint16_t* __restrict__ dout, int lddo, uint16_t* __restrict__ o, int ldo,
+    float* __restrict__ lse, float* __restrict__ delta, uint16_t* __restrict__ dq, int lddq,
+    int S, int Hq, int Hkv, const int* __restrict__ klen, float c,
+    float oscale /* FWD 1/(1-p); DQ scale/(1-p) */, float dkeep /* 1-p */,
+    const uint64_t* __restrict__ dbits, int NB, int NKT) {
+  constexpr int BQ = 128, BK = QCfg<D, PAIR>::BK, NSUB = BK / 32, NKK = D / 16, NDT = D / 32;
+  constexpr int RB = D * 2, CPR = D / 8, RPP = 64 / CPR;
+  constexpr int TILE = BK * RB, PIECES = TILE / 1024, PPW = PIECES / 4;
+  constexpr int T2 = PAIR ? TILE : 16;
+  constexpr int NREG = NDT * 16 + 2;                       // merged registers per lane
+  constexpr int MRG = PAIR ? 4 * NREG * 64 : 4;
+  __shared__ __attribute__((aligned(16))) char k0[TILE];
+  __shared__ __attribute__((aligned(16))) char k1[TILE];
+  __shared__ __attribute__((aligned(16))) char v0[TILE];
+  __shared__ __attribute__((aligned(16))) char v1[TILE];
+  __shared__ __attribute__((aligned(16))) char k2[T2];
+  __shared__ __attribute__((aligned(16))) char k3[T2];
+  __shared__ __attribute__((aligned(16))) char v2[T2];
+  __shared__ __attribute__((aligned(16))) char v3[T2];
+  __shared__ __attribute__((aligned(16))) float mrg[MRG];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = uni(tid >> 6);
+  const int team = PAIR ? (w >> 2) : 0, wl = w & 3;
+  const int r = lane & 31, hh = lane >> 5, g = lane >> 4, gi = lane & 15;
+  const int nqb = (S + BQ - 1) / BQ;
+  const int nunits = PAIR ? (nqb + 1) / 2 : nqb;
+  int rank, head;
+  block_map((int)gridDim.x / nunits, rank, head);   // grid = nunits x (B * Hq)
+  const int hq = head % Hq, b = head / Hq;
+  const int hk = hq / (Hq / Hkv);
+  const int kl = klen ? klen[b] : S;
+  auto ntiles = [&](int qb_) __attribute__((always_inline)) {
+    const int lim = CAUSAL ? min(kl, min(S, (qb_ + 1) * BQ)) : kl;
+    return (lim + BK - 1) / BK;
+  };
+  // ---- schedule: this team's items (block, key tile) for steps 0..T-1
+  int blk0, cnt, sw = 1 << 30, blk1 = -1, t1 = 0, T;
+  bool merge = false;
+  if (!PAIR) {
+    blk0 = CAUSAL ? nqb - 1 - rank : rank;          // causal: heaviest block first
+    cnt = T = ntiles(blk0);
+  } else if (CAUSAL) {
+    const int H = nqb - 1 - rank, L = rank;
+    const int tH = ntiles(H), tL = L != H ? ntiles(L) : 0;
+    const int tot = tH + tL;
+    T = (tot + 1) / 2;
+    merge = tot - T > tL;                            // team 1 computed part of H
+    if (team == 0) { blk0 = H; cnt = T; }
+    else { blk0 = tL > 0 ? L : H; cnt = tot - T; sw = tL > 0 ? tL : (1 << 30); blk1 = H; t1 = T; }
+    if (team == 1 && tL == 0) t1 = T;                // middle block: H tiles from T on
+  } else {
+    blk0 = 2 * rank + team;
+    T = ntiles(2 * rank);
+    cnt = blk0 < nqb ? ntiles(blk0) : 0;
+  }
+  T = uni(T); cnt = uni(cnt);
+  // key tile of step t
+  auto tile_of = [&](int t) __attribute__((always_inline)) -> int {
+    if (!PAIR || !CAUSAL || team == 0) return t;
+    if (t < sw) return blk0 == blk1 ? t1 + t : t;    // (middle block: starts at T)
+    return t1 + (t - sw);
+  };
+
+  // ---- per-wave row state
+  int qb, qw, qrow;
+  bool row_ok;
+  bf16x8 qf[NKK];
+  bf16x8 dof[DQ ? NKK : 1];
+  float lse2 = 0.f, dl = 0.f;
+  const uint64_t* dmrow = dbits;
+  auto load_rows = [&](int qb_) __attribute__((always_inline)) {
+    qb = qb_;
+    qw = qb * BQ + 32 * wl;
+    qrow = qw + r;
+    row_ok = qw < S;
+    const int qrow_c = min(qrow, S - 1);
+    const uint16_t* qp = q + (size_t)(b * S + qrow_c) * ldq + hq * D + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) qf[kk] = ld8(qp + 16 * kk);
+    if constexpr (DQ) {
+      const uint16_t* dp = dout + (size_t)(b * S + qrow_c) * lddo + hq * D + 8 * hh;
+      const uint16_t* op = o + (size_t)(b * S + qrow_c) * ldo + hq * D + 8 * hh;
+      float a = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        dof[kk] = ld8(dp + 16 * kk);
+        const uint4 ov = *reinterpret_cast<const uint4*>(op + 16 * kk);
+        const uint4 dv = __builtin_bit_cast(uint4, dof[kk]);
+        a += lo_bf(ov.x) * lo_bf(dv.x) + hi_bf(ov.x) * hi_bf(dv.x);
+        a += lo_bf(ov.y) * lo_bf(dv.y) + hi_bf(ov.y) * hi_bf(dv.y);
+        a += lo_bf(ov.z) * lo_bf(dv.z) + hi_bf(ov.z) * hi_bf(dv.z);
+        a += lo_bf(ov.w) * lo_bf(dv.w) + hi_bf(ov.w) * hi_bf(dv.w);
+      }
+      const float dsum = xhalf_sum(a);     // delta = rowsum(dO * O)
+      const size_t li = ((size_t)b * Hq + hq) * S + qrow_c;
+      lse2 = lse[li];
+      dl = dsum * dkeep;                   // delta (1 - p): the dropped branch of dS
+      // published for kmajor (both teams of a split block write the same value)
+      if (row_ok && hh == 0 && qrow < S) delta[li] = dl;
+    }
+    dmrow = dbits + ((size_t)(b * Hq + hq) * NB + (min(qw, S - 1) >> 5)) * NKT * 64 + lane;
+  };
+  float m_i = -INFINITY, l_i = 0.f;
+  f32x16 acc[NDT];   // FWD: O^T, DQ: dQ^T
+  auto reset = [&]() __attribute__((always_inline)) {
+    m_i = -INFINITY;
+    l_i = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) acc[dt] = f32x16{};
+  };
+  auto finalize = [&]() __attribute__((always_inline)) {
+    if (!(row_ok && qrow < S)) return;
+    float sc = oscale;
+    if constexpr (!DQ) {
+      const float lt = xhalf_sum(l_i);
+      sc = lt > 0.f ? oscale / lt : 0.f;
+      if (hh == 0) lse[((size_t)b * Hq + hq) * S + qrow] = lt > 0.f ? m_i * c + __log2f(lt) : INFINITY;
+    }
+    uint16_t* op = DQ ? dq + (size_t)(b * S + qrow) * lddq + hq * D : o + (size_t)(b * S + qrow) * ldo + hq * D;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * dt + 8 * g4 + 4 * hh;
+        uint2 u;
+        u.x = pack2(acc[dt][4 * g4 + 0] * sc, acc[dt][4 * g4 + 1] * sc);
+        u.y = pack2(acc[dt][4 * g4 + 2] * sc, acc[dt][4 * g4 + 3] * sc);
+        *reinterpret_cast<uint2*>(op + d) = u;
+      }
+  };
+  reset();
+  load_rows(blk0);
+
+  // lane-constant LDS offsets (the 32-row subtile steps are immediates)
+  int offK[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) offK[kk] = toff<D>(r, 2 * kk + hh);
+  int offT[NDT][2];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    const int col = 32 * dt + 16 * (g & 1) + 4 * (gi & 3);
+    const int row0 = 4 * hh + (gi >> 2);
+    offT[dt][0] = toff<D>(row0, col >> 3) + (col & 7) * 2;
+    offT[dt][1] = toff<D>(row0 + 8, col >> 3) + (col & 7) * 2;
+  }
+  // causal diagonal: element e of a lane is dead when crow(e, 0) > r - 4 hh
+  const int rr = r - 4 * hh;
+
+  const uint16_t* kbase = k + (size_t)b * S * ldk + hk * D;
+  const uint16_t* vbase = v + (size_t)b * S * ldv + hk * D;
+  const int prow = lane / CPR, slot = lane % CPR;
+  auto issue = [&](char* kd, char* vd, int j) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int p = wl + 4 * i;
+      const int R = p * RPP + prow;
+      const int key = min(j * BK + R, S - 1);  // tail rows: finite duplicates, masked later
+      const int ch = slot ^ swz<D>(R);
+      dma16(kbase + (size_t)key * ldk + ch * 8, kd + p * 1024);
+      dma16(vbase + (size_t)key * ldv + ch * 8, vd + p * 1024);
+    }
+  };
+  uint64_t dm_cur = 0, dm_next = 0;
+  // dropout words of step t (the rows of the block that step belongs to)
+  auto dmload = [&](int t) __attribute__((always_inline)) -> uint64_t {
+    if (!DROP) return 0;
+    const int qb_ = (PAIR && CAUSAL && team == 1 && t >= sw) ? blk1 : blk0;
+    const int qw_ = qb_ * BQ + 32 * wl;
+    if (qw_ >= S) return 0;
+    const uint64_t* row = dbits + ((size_t)(b * Hq + hq) * NB + (qw_ >> 5)) * NKT * 64 + lane;
+    return row[(size_t)((tile_of(t) * BK) >> 7) * 64];
+  };
+
+  auto compute = [&](const char* Kt, const char* Vt, int j) __attribute__((always_inline)) {
+    const int kv0 = j * BK;
+    int nsub = NSUB;
+    // (qw, kv0 are 32-aligned: subtiles up to and including the diagonal one)
+    if (CAUSAL) nsub = qw >= kv0 ? min(NSUB, (qw - kv0) / 32 + 1) : 0;
+    nsub = uni(row_ok ? nsub : 0);
+    if (nsub == 0) return;
+    // the subtile on the causal diagonal (qw is 32-aligned) and the padded-key tail
+    const int tdiag = CAUSAL ? uni((qw - kv0) >> 5) : -1;
+    const bool tail = uni(kv0 + BK > kl ? 1 : 0);
+    if constexpr (!DQ) {
+      f32x16 sacc[NSUB];
+#pragma unroll
+      for (int t = 0; t < NSUB; ++t) {
+        if (t < nsub) {
+          bf16x8 kr[NKK];
+#pragma unroll
+          for (int kk = 0; kk < NKK; ++kk) kr[kk] = lds8(Kt + 32 * t * RB, offK[kk]);
+          sacc[t] = f32x16{};
+#pragma unroll
+          for (int kk = 0; kk < NKK; ++kk) sacc[t] = mfma32(kr[kk], qf[kk], sacc[t]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NSUB; ++t) {
+        if (CAUSAL && t == tdiag) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) sacc[t][e] = crow(e, 0) > rr ? -INFINITY : sacc[t][e];
+        }
+        if (!CAUSAL && tail && t < nsub) {
+          const int lim = kl - kv0 - 32 * t - 4 * hh;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) sacc[t][e] = crow(e, 0) >= lim ? -INFINITY : sacc[t][e];
+        }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < NSUB; ++t)
+        if (t < nsub) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sacc[t][e]);
+        }
+      mx = xhalf_max(mx);
+      // exact deferred rescale (T13, threshold 0): skipped when no row raised its max
+      if (!__all(mx <= m_i)) {
+        const float m_new = fmaxf(m_i, mx);
+        const float alpha = m_new == -INFINITY ? 1.f : __builtin_amdgcn_exp2f((m_i - m_new) * c);
+        l_i *= alpha;
+        m_i = m_new;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[dt][e] *= alpha;
+      }
+      const float mc = m_i == -INFINITY ? 0.f : m_i * c;
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < NSUB; ++t)
+        if (t < nsub) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[t][e], c, -mc));
+            sacc[t][e] = p;
+            rs += p;
+          }
+        }
+      l_i += rs;
+#pragma unroll
+      for (int t = 0; t < NSUB; ++t)
+        if (t < nsub) {
+          const uint32_t wd = (uint32_t)(dm_cur >> (32 * ((((kv0 >> 5) + t) >> 1) & 1)));
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            bf16x8 vr[NDT];
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt)
+              vr[dt] = cat(tr_read(Vt + (32 * t + 16 * s) * RB, offT[dt][0]),
+                           tr_read(Vt + (32 * t + 16 * s) * RB, offT[dt][1]));
+            const bf16x8 pb = DROP ? pack8_keep(sacc[t], 8 * s, wd, 8 * (t & 1)) : pack8(sacc[t], 8 * s);
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) acc[dt] = mfma32(vr[dt], pb, acc[dt]);
+          }
+        }
+    } else {
+#pragma unroll
+      for (int t = 0; t < NSUB; ++t) {
+        if (t < nsub) {
+          bf16x8 kr[NKK], vr[NKK];
+#pragma unroll
+          for (int kk = 0; kk < NKK; ++kk) {
+            kr[kk] = lds8(Kt + 32 * t * RB, offK[kk]);
+            vr[kk] = lds8(Vt + 32 * t * RB, offK[kk]);
+          }
+          f32x16 s_ = f32x16{}, dp = f32x16{};
+#pragma unroll
+          for (int kk = 0; kk < NKK; ++kk) {
+            s_ = mfma32(kr[kk], qf[kk], s_);
+            dp = mfma32(vr[kk], dof[kk], dp);
+          }
+          const uint32_t wd = (uint32_t)(dm_cur >> (32 * ((((kv0 >> 5) + t) >> 1) & 1)));
+          const int lim = kl - kv0 - 32 * t - 4 * hh;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s_[e], c, -lse2));
+            if (CAUSAL && t == tdiag) p = crow(e, 0) > rr ? 0.f : p;
+            if (!CAUSAL && tail) p = crow(e, 0) >= lim ? 0.f : p;
+            float x = dp[e] - dl;
+            if (DROP) {
+              const uint32_t mk = elem_keep(wd, 8 * (t & 1), e);
+              x = __uint_as_float((__float_as_uint(x) & mk) | (__float_as_uint(-dl) & ~mk));
+            }
+            s_[e] = p * x;   // dS^T (the common 1/(1-p) is in oscale)
+          }
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const bf16x8 db = pack8(s_, 8 * s);
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+              const bf16x8 ktr = cat(tr_read(Kt + (32 * t + 16 * s) * RB, offT[dt][0]),
+                                     tr_read(Kt + (32 * t + 16 * s) * RB, offT[dt][1]));
+              acc[dt] = mfma32(ktr, db, acc[dt]);
+            }
+          }
+        }
+      }
+    }
+  };
+
+  // one step: wait for this step's tile, hand the other slot to the next step's DMA, compute
+  auto step = [&](char* Kc, char* Vc, char* Kn, char* Vn, int t) __attribute__((always_inline)) {
+    vm_drain();
+    __syncthreads();
+    if (t + 1 < cnt) {
+      issue(Kn, Vn, tile_of(t + 1));
+      dm_next = dmload(t + 1);
+    }
+    if (t < cnt) {
+      if (PAIR && CAUSAL && team == 1 && t == sw) {   // team 1: L done, continue with H
+        finalize();
+        reset();
+        load_rows(blk1);
+      }
+      compute(Kc, Vc, tile_of(t));
+    }
+    dm_cur = dm_next;
+  };
+  auto run = [&](char* ka, char* kb_, char* va, char* vb) __attribute__((always_inline)) {
+    if (cnt > 0) {
+      issue(ka, va, tile_of(0));
+      dm_cur = dmload(0);
+    }
+    for (int t = 0; t < T; t += 2) {
+      step(ka, va, kb_, vb, t);
+      if (t + 1 < T) step(kb_, vb, ka, va, t + 1);
+    }
+  };
+  if (!PAIR || team == 0) run(k0, k1, v0, v1);
+  else run(k2, k3, v2, v3);
+
+  if constexpr (PAIR) {
+    if (CAUSAL && merge) {
+      // team 1's partial of block H -> team 0 (identical lane mapping: element-wise)
+      float* mw = mrg + wl * NREG * 64 + lane;
+      if (team == 1) {
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) mw[(dt * 16 + e) * 64] = acc[dt][e];
+        mw[(NDT * 16) * 64] = m_i;
+        mw[(NDT * 16 + 1) * 64] = l_i;
+      }
+      __syncthreads();
+      if (team == 0) {
+        if constexpr (DQ) {
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[dt][e] += mw[(dt * 16 + e) * 64];
+        } else {
+          const float mB = mw[(NDT * 16) * 64], lB = mw[(NDT * 16 + 1) * 64];
+          const float m = fmaxf(m_i, mB);
+          const float aA = m_i == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m_i - m) * c);
+          const float aB = mB == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((mB - m) * c);
+          l_i = l_i * aA + lB * aB;
+          m_i = m;
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[dt][e] = acc[dt][e] * aA + mw[(dt * 16 + e) * 64] * aB;
+        }
+      }
+      if (team == 0) finalize();
+      return;
+    }
+    if (cnt > 0 || team == 0) finalize();
+    return;
+  }
+  finalize();
+}
+
+// ============================================================================ key-major
+// dK, dV.  DP: 0 = every dK/dV column in one pass (D = 64, K and V rows in registers);
+// 1 / 2 = columns [0, D/2) / [D/2, D) (D = 128: K rows read from LDS, S and dP recomputed
+// by the second pass -- the accumulators of all 128 columns plus the operands exceed the
+// 256-register budget of two waves per SIMD).
+// PAIR (D = 64): two 4-wave teams as in qmajor; the heavy key block (most query rows, the
+// smallest index under a causal mask) is split between the teams and team 1's partial
+// dK^T / dV^T are summed into team 0's through LDS.
+template <int D, bool CAUSAL, bool DROP, int DP, bool PAIR>
+__global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_eu(2, 2))) void flash_kmajor_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, int ldq, int ldk, int ldv,
+    const uint16_t* __restrict__ dout, int lddo, const float* __restrict__ lse,
+    const float* __restrict__ delta, uint16_t* __restrict__ dk, uint16_t* __restrict__ dv,
+    int lddk, int lddv, int S, int Hq, int Hkv, const int* __restrict__ klen, float c,
+    float dkscale, float dvscale, const uint32_t* __restrict__ dbits, int NB, int NQT) {
+  // 64-row Q/dO tiles (32 for D = 128: K image + ring = 65 KB, two workgroups per CU)
+  constexpr int KB = 128, KW = 128, QT = D == 64 ? 64 : 32, NQS = QT / 32, NKK = D / 16, NDT = D / 32;
+  constexpr int NDL = DP == 0 ? NDT : NDT / 2;
+  constexpr int DT0 = DP == 2 ? NDT / 2 : 0;
+  constexpr int RB = D * 2, CPR = D / 8, RPP = 64 / CPR;
+  constexpr int QTILE = QT * RB, PIECES = QTILE / 1024, PPW = (2 * PIECES) / 4;
+  constexpr bool KREG = D <= 64;
+  static_assert(KREG || !PAIR, "PAIR needs K rows in registers");
+  constexpr int KT_BYTES = KREG ? 16 : KW * RB;
+  constexpr int Q2 = PAIR ? QTILE : 16, L2 = PAIR ? 64 : 4;
+  constexpr int NREG = 2 * NDL * 16;
+  constexpr int MRG = PAIR ? 4 * NREG * 64 : 4;
+  __shared__ __attribute__((aligned(16))) char q0[QTILE];
+  __shared__ __attribute__((aligned(16))) char q1[QTILE];
+  __shared__ __attribute__((aligned(16))) char o0[QTILE];
+  __shared__ __attribute__((aligned(16))) char o1[QTILE];
+  __shared__ __attribute__((aligned(16))) float l0[64];   // one dword-DMA wave instruction
+  __shared__ __attribute__((aligned(16))) float l1[64];
+  __shared__ __attribute__((aligned(16))) float d0[64];
+  __shared__ __attribute__((aligned(16))) float d1[64];
+  __shared__ __attribute__((aligned(16))) char q2[Q2];
+  __shared__ __attribute__((aligned(16))) char q3[Q2];
+  __shared__ __attribute__((aligned(16))) char o2[Q2];
+  __shared__ __attribute__((aligned(16))) char o3[Q2];
+  __shared__ __attribute__((aligned(16))) float l2[L2];
+  __shared__ __attribute__((aligned(16))) float l3[L2];
+  __shared__ __attribute__((aligned(16))) float d2[L2];
+  __shared__ __attribute__((aligned(16))) float d3[L2];
+  __shared__ __attribute__((aligned(16))) char kt_lds[KT_BYTES];
+  __shared__ __attribute__((aligned(16))) float mrg[MRG];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = uni(tid >> 6);
+  const int team = PAIR ? (w >> 2) : 0, wl = w & 3;
+  const int r = lane & 31, hh = lane >> 5, g = lane >> 4, gi = lane & 15;
+  const int nkb = (S + KB - 1) / KB;
+  const int nunits = PAIR ? (nkb + 1) / 2 : nkb;
+  int rank, head;
+  block_map((int)gridDim.x / nunits, rank, head);   // grid = nunits x (B * Hkv)
+  const int hk = head % Hkv, b = head / Hkv;
+  const int grp = Hq / Hkv;
+  const int kl = klen ? klen[b] : S;
+  const int nqt = (S + QT - 1) / QT;
+  auto qt0_of = [&](int kb_) __attribute__((always_inline)) { return CAUSAL ? kb_ * KB / QT : 0; };
+  auto items_of = [&](int kb_) __attribute__((always_inline)) { return (nqt - qt0_of(kb_)) * grp; };
+  // ---- schedule (items = (query head, query tile) of a key block)
+  int blk0, cnt, sw = 1 << 30, blk1 = -1, t1 = 0, T;
+  bool merge = false;
+  if (!PAIR) {
+    blk0 = rank;                                     // causal: block 0 (most rows) first
+    cnt = T = items_of(blk0);
+  } else if (CAUSAL) {
+    const int Hb = rank, Lb = nkb - 1 - rank;        // heavy = small index
+    const int tH = items_of(Hb), tL = Lb != Hb ? items_of(Lb) : 0;
+    const int tot = tH + tL;
+    T = (tot + 1) / 2;
+    merge = tot - T > tL;
+    if (team == 0) { blk0 = Hb; cnt = T; }
+    else { blk0 = tL > 0 ? Lb : Hb; cnt = tot - T; sw = tL > 0 ? tL : (1 << 30); blk1 = Hb; t1 = T; }
+  } else {
+    blk0 = 2 * rank + team;
+    T = items_of(2 * rank);
+    cnt = blk0 < nkb ? items_of(blk0) : 0;
+  }
+  T = uni(T); cnt = uni(cnt);
+  auto item_of = [&](int t) __attribute__((always_inline)) -> int {               // item index within the block of step t
+    if (!PAIR || !CAUSAL || team == 0) return t;
+    if (t < sw) return blk0 == blk1 ? t1 + t : t;
+    return t1 + (t - sw);
+  };
+  auto blk_of = [&](int t) __attribute__((always_inline)) -> int {
+    return (PAIR && CAUSAL && team == 1 && t >= sw) ? blk1 : blk0;
+  };
+
+  // ---- per-wave key state
+  int kb, kw0, key;
+  bool key_ok, wave_on;
+  bf16x8 kf[KREG ? NKK : 1], vf[NKK];
+  f32x16 dvacc[NDL], dkacc[NDL];
+  auto load_keys = [&](int kb_) __attribute__((always_inline)) {
+    kb = kb_;
+    kw0 = kb * KB + 32 * wl;
+    key = kw0 + r;
+    key_ok = key < kl;
+    wave_on = kw0 < S;
+    const int key_c = min(key, S - 1);
+    const uint16_t* kp = k + (size_t)(b * S + key_c) * ldk + hk * D + 8 * hh;
+    const uint16_t* vp = v + (size_t)(b * S + key_c) * ldv + hk * D + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      if constexpr (KREG) kf[kk] = ld8(kp + 16 * kk);
+      vf[kk] = ld8(vp + 16 * kk);
+    }
+#pragma unroll
+    for (int dt = 0; dt < NDL; ++dt) { dvacc[dt] = f32x16{}; dkacc[dt] = f32x16{}; }
+  };
+  auto finalize = [&]() __attribute__((always_inline)) {
+    if (!(key < S)) return;
+    uint16_t* dkp = dk + (size_t)(b * S + key) * lddk + hk * D;
+    uint16_t* dvp = dv + (size_t)(b * S + key) * lddv + hk * D;
+#pragma unroll
+    for (int dt = 0; dt < NDL; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * (dt + DT0) + 8 * g4 + 4 * hh;
+        uint2 u;
+        u.x = pack2(dkacc[dt][4 * g4 + 0] * dkscale, dkacc[dt][4 * g4 + 1] * dkscale);
+        u.y = pack2(dkacc[dt][4 * g4 + 2] * dkscale, dkacc[dt][4 * g4 + 3] * dkscale);
+        *reinterpret_cast<uint2*>(dkp + d) = u;
+        u.x = pack2(dvacc[dt][4 * g4 + 0] * dvscale, dvacc[dt][4 * g4 + 1] * dvscale);
+        u.y = pack2(dvacc[dt][4 * g4 + 2] * dvscale, dvacc[dt][4 * g4 + 3] * dvscale);
+        *reinterpret_cast<uint2*>(dvp + d) = u;
+      }
+  };
+  load_keys(blk0);
+  const int krow = 32 * wl + r;   // this lane's row of the K image (D = 128)
+  if constexpr (!KREG) {
+    constexpr int KCH = KW * CPR / 256;
+#pragma unroll
+    for (int i = 0; i < KCH; ++i) {
+      const int ci = tid + 256 * i, row = ci / CPR, ch = ci % CPR;
+      const int kk_ = min(kb * KB + row, S - 1);
+      *reinterpret_cast<uint4*>(kt_lds + toff<D>(row, ch)) =
+          *reinterpret_cast<const uint4*>(k + (size_t)(b * S + kk_) * ldk + hk * D + ch * 8);
+    }
+  }
+
+  int offQ[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) offQ[kk] = toff<D>(r, 2 * kk + hh);
+  int offKl[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) offKl[kk] = KREG ? 0 : toff<D>(krow, 2 * kk + hh);
+  int offT[NDL][2];
+#pragma unroll
+  for (int dt = 0; dt < NDL; ++dt) {
+    const int col = 32 * (dt + DT0) + 16 * (g & 1) + 4 * (gi & 3);
+    const int row0 = 4 * hh + (gi >> 2);
+    offT[dt][0] = toff<D>(row0, col >> 3) + (col & 7) * 2;
+    offT[dt][1] = toff<D>(row0 + 8, col >> 3) + (col & 7) * 2;
+  }
+  const int rr = r - 4 * hh;   // diagonal: element e dead when r - 4hh > crow(e, 0)
+
+  const int prow = lane / CPR, slot = lane % CPR;
+  auto decode = [&](int t, int& hq, int& qs) __attribute__((always_inline)) {
+    const int kb_ = blk_of(t), it = item_of(t);
+    const int ph = nqt - qt0_of(kb_);
+    hq = hk * grp + it / ph;
+    qs = (qt0_of(kb_) + it % ph) * QT;
+  };
+  auto issue = [&](char* qd, char* od, float* ld, float* dd, int t) __attribute__((always_inline)) {
+    int hq, qs;
+    decode(t, hq, qs);
+    const uint16_t* qb_ = q + (size_t)b * S * ldq + hq * D;
+    const uint16_t* ob_ = dout + (size_t)b * S * lddo + hq * D;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int p = wl + 4 * i;                // 0 .. 2*PIECES-1: Q pieces then dO pieces
+      const bool isq = p < PIECES;
+      const int pp = isq ? p : p - PIECES;
+      const int R = pp * RPP + prow;
+      const int row = min(qs + R, S - 1);
+      const int ch = slot ^ swz<D>(R);
+      if (isq) dma16(qb_ + (size_t)row * ldq + ch * 8, qd + pp * 1024);
+      else dma16(ob_ + (size_t)row * lddo + ch * 8, od + pp * 1024);
+    }
+    if (wl < 2) {
+      const size_t li = ((size_t)b * Hq + hq) * S + min(qs + lane, S - 1);
+      if (wl == 0) dma4(lse + li, (char*)ld);
+      else dma4(delta + li, (char*)dd);
+    }
+  };
+  auto dmload = [&](int t) __attribute__((always_inline)) -> uint32_t {
+    if (!DROP) return 0u;
+    int hq, qs;
+    decode(t, hq, qs);
+    const int kw = blk_of(t) * KB + 32 * wl;
+    if (kw >= S) return 0u;
+    return dbits[(((size_t)(b * Hq + hq) * NB + (kw >> 5)) * NQT + (qs >> 6)) * 64 + lane];
+  };
+  uint32_t dm_cur = 0, dm_next = 0;
+
+  auto compute = [&](const char* Qt, const char* Ot, const float* Lt, const float* Dt, int t) __attribute__((always_inline)) {
+    int hq, qs;
+    decode(t, hq, qs);
+    (void)hq;
+#pragma unroll
+    for (int u = 0; u < NQS; ++u) {
+      const int qsu = qs + 32 * u;
+      const bool act = uni(wave_on && qsu < S && (!CAUSAL || qsu + 31 >= kw0) ? 1 : 0);
+      if (!act) continue;
+      f32x16 sacc = f32x16{}, dpacc = f32x16{};
+      const char* Qu = Qt + 32 * u * RB;
+      const char* Ou = Ot + 32 * u * RB;
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        const bf16x8 qa = lds8(Qu, offQ[kk]);
+        const bf16x8 oa = lds8(Ou, offQ[kk]);
+        const bf16x8 kb_ = KREG ? kf[kk] : lds8(kt_lds, offKl[kk]);
+        sacc = mfma32(qa, kb_, sacc);
+        dpacc = mfma32(oa, vf[kk], dpacc);
+      }
+      const bool diag = CAUSAL && qsu == kw0;
+      const bool qtail = qsu + 32 > S;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        // row constants of the lane's query rows, 4 consecutive per e >> 2 (one ds_read_b128)
+        float4 lsq, dlq;
+        if ((e & 3) == 0) {
+          lsq = *reinterpret_cast<const float4*>(Lt + 32 * u + 8 * (e >> 2) + 4 * hh);
+          dlq = *reinterpret_cast<const float4*>(Dt + 32 * u + 8 * (e >> 2) + 4 * hh);
+        }
+        const float lse_e = (e & 3) == 0 ? lsq.x : (e & 3) == 1 ? lsq.y : (e & 3) == 2 ? lsq.z : lsq.w;
+        const float dl_e = (e & 3) == 0 ? dlq.x : (e & 3) == 1 ? dlq.y : (e & 3) == 2 ? dlq.z : dlq.w;
+        float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[e], c, -lse_e));
+        if (diag) p = rr > crow(e, 0) ? 0.f : p;
+        if (qtail) p = qsu + crow(e, hh) >= S ? 0.f : p;
+        p = key_ok ? p : 0.f;
+        float x = dpacc[e] - dl_e;
+        if (DROP) {
+          const uint32_t mk = elem_keep(dm_cur, 8 * ((qsu >> 5) & 1), e);
+          x = __uint_as_float((__float_as_uint(x) & mk) | (__float_as_uint(-dl_e) & ~mk));
+        }
+        sacc[e] = p;
+        dpacc[e] = p * x;   // dS (1/(1-p) in dkscale)
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pb = DROP ? pack8_keep(sacc, 8 * s, dm_cur, 8 * ((qsu >> 5) & 1)) : pack8(sacc, 8 * s);
+        const bf16x8 db = pack8(dpacc, 8 * s);
+        const int rofs = (32 * u + 16 * s) * RB;
+#pragma unroll
+        for (int dt = 0; dt < NDL; ++dt) {
+          const bf16x8 dot = cat(tr_read(Ot + rofs, offT[dt][0]), tr_read(Ot + rofs, offT[dt][1]));
+          dvacc[dt] = mfma32(dot, pb, dvacc[dt]);
+          const bf16x8 qtr = cat(tr_read(Qt + rofs, offT[dt][0]), tr_read(Qt + rofs, offT[dt][1]));
+          dkacc[dt] = mfma32(qtr, db, dkacc[dt]);
+        }
+      }
+    }
+  };
+
+  auto step = [&](char* Qc, char* Oc, float* Lc, float* Dc, char* Qn, char* On, float* Ln, float* Dn,
+                  int t) __attribute__((always_inline)) {
+    vm_drain();
+    __syncthreads();
+    if (t + 1 < cnt) {
+      issue(Qn, On, Ln, Dn, t + 1);
+      dm_next = dmload(t + 1);
+    }
+    if (t < cnt) {
+      if (PAIR && CAUSAL && team == 1 && t == sw) {   // team 1: light block done, on to the heavy one
+        finalize();
+        load_keys(blk1);
+      }
+      compute(Qc, Oc, Lc, Dc, t);
+    }
+    dm_cur = dm_next;
+  };
+  auto run = [&](char* qa, char* qb_, char* oa, char* ob, float* la, float* lb, float* da, float* db) __attribute__((always_inline)) {
+    if (cnt > 0) {
+      issue(qa, oa, la, da, 0);
+      dm_cur = dmload(0);
+    }
+    for (int t = 0; t < T; t += 2) {
+      step(qa, oa, la, da, qb_, ob, lb, db, t);
+      if (t + 1 < T) step(qb_, ob, lb, db, qa, oa, la, da, t + 1);
+    }
+  };
+  if (!PAIR || team == 0) run(q0, q1, o0, o1, l0, l1, d0, d1);
+  else run(q2, q3, o2, o3, l2, l3, d2, d3);
+
+  if constexpr (PAIR) {
+    if (CAUSAL && merge) {
+      float* mw = mrg + wl * NREG * 64 + lane;
+      if (team == 1) {
+#pragma unroll
+        for (int dt = 0; dt < NDL; ++dt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            mw[(dt * 16 + e) * 64] = dkacc[dt][e];
+            mw[((NDL + dt) * 16 + e) * 64] = dvacc[dt][e];
+          }
+      }
+      __syncthreads();
+      if (team == 0) {
+#pragma unroll
+        for (int dt = 0; dt < NDL; ++dt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            dkacc[dt][e] += mw[(dt * 16 + e) * 64];
+            dvacc[dt][e] += mw[((NDL + dt) * 16 + e) * 64];
+          }
+        finalize();
+      }
+      return;
+    }
+    if (cnt > 0 || team == 0) finalize();
+    return;
+  }
+  finalize();
+}
+
+// ------------------------------------------------------------------------------ launch
+template <int D, bool DQ>
+hipError_t launch_qmajor(bool causal, bool drop, int S, int B, hipStream_t s,
+                         const uint16_t* q, const uint16_t* k, const uint16_t* v, int ldq, int ldk,
+                         int ldv, const uint16_t* dout, int lddo, uint16_t* o, int ldo, float* lse,
+                         float* delta, uint16_t* dq, int lddq, int Hq, int Hkv,
+                         const int* klen, float c, float oscale, float dkeep,
+                         const uint64_t* dbits, int NB, int NKT) {
+  constexpr bool PAIR = D == 64;
+  const int nqb = (S + 127) / 128;
+  const dim3 grid((PAIR ? (nqb + 1) / 2 : nqb) * Hq * B);
+#define MX_QM(C, DR)                                                                              \
+  hipLaunchKernelGGL((flash_qmajor_kernel<D, C, DR, DQ, PAIR>), grid, dim3(PAIR ? 512 : 256), 0, s, \
+                     q, k, v, ldq, ldk, ldv, dout, lddo, o, ldo, lse, delta, dq, lddq, S, Hq, Hkv,  \
+                     klen, c, oscale, dkeep, dbits, NB, NKT)
+  if (causal) { if (drop) MX_QM(true, true); else MX_QM(true, false); }
+  else { if (drop) MX_QM(false, true); else MX_QM(false, false); }
+#undef MX_QM
+  return hipGetLastError();
+}
+
+template <int D>
+hipError_t launch_kmajor(bool causal, bool drop, int S, int B, hipStream_t s,
+                         const uint16_t* q, const uint16_t* k, const uint16_t* v, int ldq, int ldk,
+                         int ldv, const uint16_t* dout, int lddo, const float* lse,
+                         const float* delta, uint16_t* dk, uint16_t* dv, int lddk, int lddv,
+                         int Hq, int Hkv, const int* klen, float c, float dkscale, float dvscale,
+                         const uint32_t* dbits, int NB, int NQT) {
+  constexpr bool PAIR = D == 64;
+  const int nkb = (S + 127) / 128;
+  const dim3 grid((PAIR ? (nkb + 1) / 2 : nkb) * Hkv * B);
+#define MX_KM(C, DR, P)                                                                          \
+  hipLaunchKernelGGL((flash_kmajor_kernel<D, C, DR, P, PAIR>), grid, dim3(PAIR ? 512 : 256), 0, s, \
+                     q, k, v, ldq, ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq, Hkv, \
+                     klen, c, dkscale, dvscale, dbits, NB, NQT)
+#define MX_KM_P(P)                                                                   \
+  {                                                                                  \
+    if (causal) { if (drop) MX_KM(true, true, P); else MX_KM(true, false, P); }      \
+    else { if (drop) MX_KM(false, true, P); else MX_KM(false, false, P); }           \
+  }
+  if constexpr (D <= 64) {
+    MX_KM_P(0)
+  } else {
+    MX_KM_P(1)
+    MX_KM_P(2)
+  }
+#undef MX_KM_P
+#undef MX_KM
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// Dropout keep-mask images for one attention call (layouts in flash_dropmask_kernel).
+// fwd_bits: u64 [B*Hq][NB][NKT][64]; bwd_bits: u32 [B*Hq][NB][NQT][64], NB = ceil(S/32),
+// NKT = ceil(S/128), NQT = ceil(S/64).  h_off / Hg: this rank's first global head / the
+// model's head count (tensor/context-parallel shards draw the single-GPU mask).
+MX_EXPORT int mx_flash_dropmask(const uint32_t* seed, uint32_t salt, float p, int B, int S,
+                                int Hq, int h_off, int Hg, int causal, void* fwd_bits,
+                                void* bwd_bits, hipStream_t s) {
+  const int NB = (S + 31) / 32, NKT = (S + 127) / 128, NQT = (S + 63) / 64;
+  const int NB2 = (NB + 1) / 2;
+  const uint32_t thr16 = (uint32_t)(p * 65536.0f + 0.5f);
+  hipLaunchKernelGGL(flash_dropmask_kernel, dim3(NB2, (NB2 + 3) / 4, B * Hq), dim3(256), 0, s, seed,
+                     salt, thr16, S, Hq, h_off, Hg, NB, NKT, NQT, causal, (uint32_t*)fwd_bits,
+                     (uint32_t*)bwd_bits);
+  return hipGetLastError();
+}
+
+// Q/K/V/O bf16 with token strides ld*; head h at column h*D.  lse: fp32 [B, Hq, S] (base 2).
+// klen: int32 [B] valid key count or null.  fwd_bits: dropout image or null; keep_scale =
+// 1/(1-p).
+MX_EXPORT int mx_flash_fwd(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv,
+                           void* o, int ldo, float* lse, int B, int S, int Hq, int Hkv, int D,
+                           int causal, const int* klen, float scale, const void* fwd_bits,
+                           float keep_scale, hipStream_t s) {
+  if (Hq % Hkv || S <= 0) return hipErrorInvalidValue;
+  const float c = scale * 1.4426950408889634f;
+  const int NB = (S + 31) / 32, NKT = (S + 127) / 128;
+  const bool drop = fwd_bits != nullptr;
+  const float osc = drop ? keep_scale : 1.f;
+  if (D == 64)
+    return launch_qmajor<64, false>(causal, drop, S, B, s, (const uint16_t*)q, (const uint16_t*)k,
+                                    (const uint16_t*)v, ldq, ldk, ldv, nullptr, 0, (uint16_t*)o, ldo,
+                                    lse, nullptr, nullptr, 0, Hq, Hkv, klen, c, osc, 1.f,
+                                    (const uint64_t*)fwd_bits, NB, NKT);
+  if (D == 128)
+    return launch_qmajor<128, false>(causal, drop, S, B, s, (const uint16_t*)q, (const uint16_t*)k,
+                                     (const uint16_t*)v, ldq, ldk, ldv, nullptr, 0, (uint16_t*)o, ldo,
+                                     lse, nullptr, nullptr, 0, Hq, Hkv, klen, c, osc, 1.f,
+                                     (const uint64_t*)fwd_bits, NB, NKT);
+  return hipErrorInvalidValue;
+}
+
+// delta: fp32 [B, Hq, S] workspace (written by the dQ kernel, read by the dK/dV kernel).
+// fwd_bits / bwd_bits: the forward's dropout images (both null without dropout).
+MX_EXPORT int mx_flash_bwd(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv,
+                           const void* o, int ldo, const void* dout, int lddo, const float* lse,
+                           float* delta, void* dq, int lddq, void* dk, void* dv, int lddk,
+                           int lddv, int B, int S, int Hq, int Hkv, int D, int causal,
+                           const int* klen, float scale, const void* fwd_bits,
+                           const void* bwd_bits, float keep_scale, hipStream_t s) {
+  if (Hq % Hkv || S <= 0 || (D != 64 && D != 128)) return hipErrorInvalidValue;
+  if ((fwd_bits == nullptr) != (bwd_bits == nullptr)) return hipErrorInvalidValue;
+  const float c = scale * 1.4426950408889634f;
+  const bool drop = fwd_bits != nullptr;
+  const float ks = drop ? keep_scale : 1.f;
+  const float dkeep = drop ? 1.f / keep_scale : 1.f;
+  const int NB = (S + 31) / 32, NKT = (S + 127) / 128, NQT = (S + 63) / 64;
+  hipError_t e;
+  if (D == 64)
+    e = launch_qmajor<64, true>(causal, drop, S, B, s, (const uint16_t*)q, (const uint16_t*)k,
+                                (const uint16_t*)v, ldq, ldk, ldv, (const uint16_t*)dout, lddo,
+                                (uint16_t*)o, ldo, (float*)lse, delta, (uint16_t*)dq, lddq, Hq, Hkv,
+                                klen, c, scale * ks, dkeep, (const uint64_t*)fwd_bits, NB, NKT);
+  else
+    e = launch_qmajor<128, true>(causal, drop, S, B, s, (const uint16_t*)q, (const uint16_t*)k,
+                                 (const uint16_t*)v, ldq, ldk, ldv, (const uint16_t*)dout, lddo,
+                                 (uint16_t*)o, ldo, (float*)lse, delta, (uint16_t*)dq, lddq, Hq, Hkv,
+                                 klen, c, scale * ks, dkeep, (const uint64_t*)fwd_bits, NB, NKT);
+  if (e != hipSuccess) return e;
+  if (D == 64)
+    e = launch_kmajor<64>(causal, drop, S, B, s, (const uint16_t*)q, (const uint16_t*)k,
+                          (const uint16_t*)v, ldq, ldk, ldv, (const uint16_t*)dout, lddo, lse, delta,
+                          (uint16_t*)dk, (uint16_t*)dv, lddk, lddv, Hq, Hkv, klen, c, scale * ks, ks,
+                          (const uint32_t*)bwd_bits, NB, NQT);
+  else
+    e = launch_kmajor<128>(causal, drop, S, B, s, (const uint16_t*)q, (const uint16_t*)k,
+                           (const uint16_t*)v, ldq, ldk, ldv, (const uint16_t*)dout, lddo, lse, delta,
+                           (uint16_t*)dk, (uint16_t*)dv, lddk, lddv, Hq, Hkv, klen, c, scale * ks, ks,
+                           (const uint32_t*)bwd_bits, NB, NQT);
+  return e;
+}

@@ -25,6 +25,7 @@ token shards with all-gather / reduce-scatter instead of all-reduce) are built i
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
 
@@ -272,6 +273,10 @@ class StepRuntime:
     # the memory-bound backward kernels of the main stream (None: inline)
     wgrad_stream: Optional[object] = None
     _wgrad_live: bool = False
+    # optional side stream for work that depends only on the step seed (attention-dropout
+    # mask generation) to overlap the layer's QKV GEMM; off by default (MXTRAIN_AUX_STREAM=1):
+    # measured on one MI355X the concurrent generator slowed the GEMM by more than it hid
+    aux_stream: Optional[object] = None
     # MoE: this rank's experts (separate flat buffer), the EP group, aux-loss gradient
     eparams: Optional[Dict[str, torch.Tensor]] = None
     egrads: Optional[Dict[str, torch.Tensor]] = None
@@ -456,6 +461,16 @@ class GPTLayerFn(torch.autograd.Function):
         kvl = cfg.num_kv_heads // rt.tp
         eps = cfg.layernorm_epsilon
         a_full = _gather(a, rt)
+        dmask = None
+        if rt.p_attn > 0:
+            # the keep-mask depends only on the seed: generated on the side stream while the
+            # QKV GEMM runs (the GEMM's grid leaves CUs free)
+            ha_ = hl // rt.cp
+            dmask = attn_ops.dropmask(rt.B, rt.S * rt.cp, ha_, rt.p_attn,
+                                      rt.attn_seed_t if rt.attn_seed_t is not None else rt.seed_t,
+                                      salt=SALT_ATTN + i, head_offset=rt.tp_rank * hl + rt.cp_rank * ha_,
+                                      total_heads=cfg.num_attention_heads, causal=True, device=a.device,
+                                      stream=rt.aux_stream)
         qkv = torch.addmm(P[p + "qkv_b"], a_full, P[p + "qkv_w"].t())
         if rt.cp > 1:   # Ulysses: whole sequences, 1/cp of the heads
             qkv_a = seq_to_head(qkv, (hl * D, kvl * D, kvl * D), rt.B, rt.S, rt.cp_group)
@@ -466,11 +481,8 @@ class GPTLayerFn(torch.autograd.Function):
         q = qkv_a[:, : ha * D]
         k = qkv_a[:, ha * D:(ha + kva) * D]
         v = qkv_a[:, (ha + kva) * D:]
-        ctx_a, lse, dmask = attn_ops.attn_fwd(
-            q, k, v, rt.B, rt.S * rt.cp, ha, kva, D, causal=True, dropout_p=rt.p_attn,
-            seed_t=rt.attn_seed_t if rt.attn_seed_t is not None else rt.seed_t,
-            salt=SALT_ATTN + i, head_offset=rt.tp_rank * hl + rt.cp_rank * ha,
-            total_heads=cfg.num_attention_heads)
+        ctx_a, lse, dmask = attn_ops.attn_fwd(q, k, v, rt.B, rt.S * rt.cp, ha, kva, D, causal=True,
+                                              dmask=dmask)
         ctx_ = head_to_seq(ctx_a, (hl * D,), rt.B, rt.S, rt.cp_group) if rt.cp > 1 else ctx_a
         o = _reduce(torch.mm(ctx_, P[p + "proj_w"].t()), rt)
         w2, b2 = rt.norm_params(p + "ln2")
@@ -598,7 +610,7 @@ class GPTLayerFn(torch.autograd.Function):
         v = qkv_a[:, (ha + kva) * D:]
         attn_ops.attn_bwd(dctx, q, k, v, ctx_a, lse, rt.B, rt.S * rt.cp, ha, kva, D, causal=True,
                           dq=dqkv[:, : ha * D], dk=dqkv[:, ha * D:(ha + kva) * D],
-                          dv=dqkv[:, (ha + kva) * D:], dmask=ctx.dmask, dropout_p=rt.p_attn)
+                          dv=dqkv[:, (ha + kva) * D:], dmask=ctx.dmask)
         ctx.dmask = None
         rt.rope_(dqkv, ha, kva, inverse=True)
         if rt.cp > 1:
@@ -655,6 +667,9 @@ class GPTStage:
                               vocab_start=tp_rank * V, cp=cp, cp_rank=cp_rank, cp_group=cp_group,
                               eparams=eparams, egrads=egrads, ep_group=ep_group,
                               attn_seed_t=attn_seed_t)
+        dev = next(iter(params.values())).device if params else None
+        if dev is not None and dev.type == "cuda" and os.environ.get("MXTRAIN_AUX_STREAM", "0") == "1":
+            self.rt.aux_stream = torch.cuda.Stream(device=dev)
         if cfg.num_experts > 1:
             assert tp == 1, "MoE layers run with tensor-parallel size 1 (expert parallelism instead)"
         if cp > 1:

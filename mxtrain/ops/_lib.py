@@ -55,11 +55,11 @@ SIGNATURES = {
     "mx_sumsq_bf16": [P, I64, F, P, P, P, I, P],
     "mx_adamw_config": [I, I],
     "mx_adamw_step": [P, P, P, P, P, P, I64, P, P, P],
-    # attention.hip
-    "mx_attn_dropmask": [P, U32, F, I, I, I, I, I, I, P, P, P],
-    "mx_attn_fwd": [P, P, P, I, I, I, P, I, P, I, I, I, I, I, I, P, F, P, F, P],
-    "mx_attn_bwd": [P, P, P, I, I, I, P, I, P, I, P, P, P, P, I, P, P, I, I, I, I, I, I, I,
-                    I, P, F, P, F, P],
+    # flash.hip
+    "mx_flash_dropmask": [P, U32, F, I, I, I, I, I, I, P, P, P],
+    "mx_flash_fwd": [P, P, P, I, I, I, P, I, P, I, I, I, I, I, I, P, F, P, F, P],
+    "mx_flash_bwd": [P, P, P, I, I, I, P, I, P, I, P, P, P, I, P, P, I, I, I, I, I, I, I, I,
+                     P, F, P, P, F, P],
     # rope.hip
     "mx_rope": [P, I64, I, I, I, I, I, I, I, P, P, P, I, P],
     # vision.hip

@@ -37,19 +37,36 @@ def effective_keep_scale(p: float) -> float:
 
 def dropout_keep_mask(B, S, Hq, seed: int, salt: int, p: float, head_offset: int = 0,
                       total_heads=None, device="cpu") -> torch.Tensor:
-    """Dense boolean keep-mask [B, Hq, S(q), S(k)]: keep <=> ((hash32(row*0x85EBCA6B +
-    (k >> 1), seed + salt) >> 16 (k & 1)) & 0xFFFF) >= thr, row = (b*Hg + h_global)*S + q."""
+    """Dense boolean keep-mask [B, Hq, S(q), S(k)] -- the definition the kernels implement
+    (flash.hip drop_stream_bits).  For query row q of head h (row = (b*Hg + h_global)*S + q)
+    and key k = 32 kb + kk: the lane half hh = (kk >> 2) & 1 and pair j = ((kk & 3) + 4 (kk >> 3))
+    >> 1 select the j-th output of an xorshift32 stream seeded by hash32(row*0x85EBCA6B +
+    2 kb + hh, seed + salt) | 1; its low (k even) or high (k odd) 16 bits are the draw, and the
+    element is kept when draw >= round(p * 65536)."""
     Hg = total_heads or Hq
     seed = (int(seed) + int(salt)) & M32
-    b = torch.arange(B, dtype=torch.int64, device=device).view(B, 1, 1, 1)
-    h = torch.arange(Hq, dtype=torch.int64, device=device).view(1, Hq, 1, 1) + head_offset
-    q = torch.arange(S, dtype=torch.int64, device=device).view(1, 1, S, 1)
-    k = torch.arange(S, dtype=torch.int64, device=device).view(1, 1, 1, S)
+    NB = (S + 31) // 32
+    b = torch.arange(B, dtype=torch.int64, device=device).view(B, 1, 1, 1, 1)
+    h = torch.arange(Hq, dtype=torch.int64, device=device).view(1, Hq, 1, 1, 1) + head_offset
+    q = torch.arange(S, dtype=torch.int64, device=device).view(1, 1, S, 1, 1)
+    kb = torch.arange(NB, dtype=torch.int64, device=device).view(1, 1, 1, NB, 1)
+    hh = torch.arange(2, dtype=torch.int64, device=device).view(1, 1, 1, 1, 2)
     row = ((b * Hg + h) * S + q) & M32
-    x = (row * 0x85EBCA6B + (k >> 1)) & M32
-    hv = hash32(x, seed)
-    h16 = (hv >> (16 * (k & 1))) & 0xFFFF
-    return h16 >= dropout_threshold(p)
+    x = hash32((row * 0x85EBCA6B + 2 * kb + hh) & M32, seed) | 1
+    xs = [x]
+    for _ in range(7):
+        x = x ^ ((x << 13) & M32)
+        x = x ^ (x >> 17)
+        x = x ^ ((x << 5) & M32)
+        xs.append(x)
+    X = torch.stack(xs, -1)                                   # [B, Hq, S, NB, 2, 8]
+    k = torch.arange(S, dtype=torch.int64, device=device)
+    kk = k % 32
+    sel_kb, sel_hh = k // 32, (kk >> 2) & 1
+    sel_j = ((kk & 3) + 4 * (kk >> 3)) >> 1
+    draws = X[:, :, :, sel_kb, sel_hh, sel_j]                 # [B, Hq, S, S]
+    draws = (draws >> (16 * (kk & 1))) & 0xFFFF
+    return draws >= dropout_threshold(p)
 
 
 def _ref_fwd(q, k, v, B, S, Hq, Hkv, D, causal, klen, scale, keep=None, keep_scale=1.0):
@@ -75,39 +92,77 @@ def _ref_fwd(q, k, v, B, S, Hq, Hkv, D, causal, klen, scale, keep=None, keep_sca
     return o, lse * LOG2E
 
 
+class DropMask:
+    """Attention-dropout state of one forward, kept for its backward: the kernels' two bit
+    images (query-on-lane for the forward / dQ kernels, key-on-lane for dK/dV) on the GPU,
+    the dense keep-mask on the CPU path; ``event`` marks the side-stream generation."""
+
+    __slots__ = ("fbits", "bbits", "keep", "p", "event")
+
+    def __init__(self, p, fbits=None, bbits=None, keep=None, event=None):
+        self.p, self.fbits, self.bbits, self.keep, self.event = p, fbits, bbits, keep, event
+
+    @property
+    def keep_scale(self):
+        return effective_keep_scale(self.p)
+
+    def ready(self):
+        if self.event is not None:
+            torch.cuda.current_stream().wait_event(self.event)
+            self.event = None
+
+
+def dropmask(B, S, Hq, p, seed_t, salt=0, head_offset=0, total_heads=None, causal=True,
+             device=None, stream=None) -> DropMask:
+    """Generate the keep-mask images.  With ``stream`` the generator runs there (it depends
+    only on the seed, so it overlaps the QKV projection GEMM, which leaves CUs idle); the
+    consumer joins through the returned event (DropMask.ready)."""
+    device = device if device is not None else seed_t.device
+    if device.type != "cuda" or not _lib.use_hip(seed_t):
+        keep = dropout_keep_mask(B, S, Hq, int(seed_t.reshape(-1)[0]), salt, p, head_offset, total_heads, device)
+        return DropMask(p, keep=keep)
+    NB, NKT, NQT = (S + 31) // 32, (S + 127) // 128, (S + 63) // 64
+    fbits = torch.empty(B * Hq * NB * NKT * 64, dtype=torch.int64, device=device)
+    bbits = torch.empty(B * Hq * NB * NQT * 64, dtype=torch.int32, device=device)
+    args = (_lib.ptr(seed_t), int(salt) & M32, float(p), B, S, Hq, int(head_offset),
+            int(total_heads or Hq), int(causal), _lib.ptr(fbits), _lib.ptr(bbits))
+    if stream is None:
+        _lib.call("mx_flash_dropmask", *args, _lib.stream())
+        return DropMask(p, fbits, bbits)
+    main = torch.cuda.current_stream(device)
+    stream.wait_stream(main)            # the seed is advanced on the main stream
+    with torch.cuda.stream(stream):
+        _lib.call("mx_flash_dropmask", *args, _lib.stream())
+        ev = torch.cuda.Event()
+        ev.record(stream)
+    return DropMask(p, fbits, bbits, event=ev)
+
+
 def attn_fwd(q, k, v, B, S, Hq, Hkv, D, causal=True, klen=None, scale=None, dropout_p=0.0,
-             seed_t=None, salt=0, head_offset=0, total_heads=None):
-    """Returns (o, lse, dmask): dmask is the dropout state backward needs (the kernel's
-    key-on-lane bit image on the GPU, the dense keep-mask on the CPU path) or None."""
+             seed_t=None, salt=0, head_offset=0, total_heads=None, dmask=None):
+    """Returns (o, lse, dmask): dmask is the DropMask backward needs (None without dropout).
+    A pre-generated ``dmask`` (see dropmask(stream=...)) is used as is."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    drop = dropout_p > 0.0
-    if drop:
+    drop = dropout_p > 0.0 or dmask is not None
+    if drop and dmask is None:
         assert seed_t is not None, "attention dropout needs the device seed tensor"
+        dmask = dropmask(B, S, Hq, dropout_p, seed_t, salt, head_offset, total_heads, causal, device=q.device)
     if not _lib.use_hip(q):
-        keep = (dropout_keep_mask(B, S, Hq, int(seed_t.reshape(-1)[0]), salt, dropout_p, head_offset,
-                                  total_heads, q.device) if drop else None)
-        o, lse = _ref_fwd(q, k, v, B, S, Hq, Hkv, D, causal, klen, scale, keep,
-                          effective_keep_scale(dropout_p) if drop else 1.0)
-        return o.to(q.dtype), lse, keep
+        o, lse = _ref_fwd(q, k, v, B, S, Hq, Hkv, D, causal, klen, scale,
+                          dmask.keep if drop else None, dmask.keep_scale if drop else 1.0)
+        return o.to(q.dtype), lse, dmask
     assert q.dtype == torch.bfloat16 and D in (64, 128)
     assert q.stride(1) == 1 and k.stride(1) == 1 and v.stride(1) == 1
     o = torch.empty(B * S, Hq * D, dtype=q.dtype, device=q.device)
     lse = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
     kl = klen.to(torch.int32).contiguous() if klen is not None else None
-    fbits = bbits = None
     if drop:
-        NB = (S + 31) // 32
-        NKT = (NB + 3) // 4
-        fbits = torch.empty(B * Hq * NB * NKT * 64 * 4, dtype=torch.int16, device=q.device)
-        bbits = torch.empty(B * Hq * NB * NB * 64, dtype=torch.int16, device=q.device)
-        _lib.call("mx_attn_dropmask", _lib.ptr(seed_t), int(salt) & M32, float(dropout_p), B, S, Hq,
-                  int(head_offset), int(total_heads or Hq), int(causal), _lib.ptr(fbits),
-                  _lib.ptr(bbits), _lib.stream())
-    ks = effective_keep_scale(dropout_p) if drop else 1.0
-    _lib.call("mx_attn_fwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), q.stride(0), k.stride(0),
+        dmask.ready()
+    _lib.call("mx_flash_fwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), q.stride(0), k.stride(0),
               v.stride(0), _lib.ptr(o), o.stride(0), _lib.ptr(lse), B, S, Hq, Hkv, D, int(causal),
-              _lib.ptr(kl), float(scale), _lib.ptr(fbits), float(ks), _lib.stream())
-    return o, lse, ((bbits, float(dropout_p)) if drop else None)
+              _lib.ptr(kl), float(scale), _lib.ptr(dmask.fbits) if drop else None,
+              float(dmask.keep_scale) if drop else 1.0, _lib.stream())
+    return o, lse, dmask
 
 
 def attn_bwd(dout, q, k, v, o, lse, B, S, Hq, Hkv, D, causal=True, klen=None, scale=None,
@@ -116,13 +171,13 @@ def attn_bwd(dout, q, k, v, o, lse, B, S, Hq, Hkv, D, causal=True, klen=None, sc
     they are written in place.  ``dmask`` is the third output of :func:`attn_fwd`."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if not _lib.use_hip(q):
-        keep = dmask
+        keep = dmask.keep if dmask is not None else None
         with torch.enable_grad():
             qq = q.detach().float().requires_grad_(True)
             kk = k.detach().float().requires_grad_(True)
             vv = v.detach().float().requires_grad_(True)
             oo, _ = _ref_fwd(qq, kk, vv, B, S, Hq, Hkv, D, causal, klen, scale, keep,
-                             effective_keep_scale(dropout_p) if keep is not None else 1.0)
+                             dmask.keep_scale if keep is not None else 1.0)
             gq, gk, gv = torch.autograd.grad(oo, (qq, kk, vv), dout.float())
         outs = []
         for g, buf in ((gq, dq), (gk, dk), (gv, dv)):
@@ -139,18 +194,14 @@ def attn_bwd(dout, q, k, v, o, lse, B, S, Hq, Hkv, D, causal=True, klen=None, sc
     if dv is None:
         dv = torch.empty(B * S, Hkv * D, dtype=q.dtype, device=q.device)
     delta = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
-    # zeroed by the delta pre-pass inside mx_attn_bwd
-    dq_acc = torch.empty(B * S, Hq * D, dtype=torch.float32, device=q.device)
     kl = klen.to(torch.int32).contiguous() if klen is not None else None
-    bbits, ks = None, 1.0
-    if dmask is not None:
-        bbits, p = dmask
-        ks = effective_keep_scale(p)
-    _lib.call("mx_attn_bwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), q.stride(0), k.stride(0),
+    _lib.call("mx_flash_bwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), q.stride(0), k.stride(0),
               v.stride(0), _lib.ptr(o), o.stride(0), _lib.ptr(dout), dout.stride(0), _lib.ptr(lse),
-              _lib.ptr(delta), _lib.ptr(dq_acc), _lib.ptr(dq), dq.stride(0), _lib.ptr(dk),
-              _lib.ptr(dv), dk.stride(0), dv.stride(0), B, S, Hq, Hkv, D, int(causal), _lib.ptr(kl),
-              float(scale), _lib.ptr(bbits), float(ks), _lib.stream())
+              _lib.ptr(delta), _lib.ptr(dq), dq.stride(0), _lib.ptr(dk), _lib.ptr(dv), dk.stride(0),
+              dv.stride(0), B, S, Hq, Hkv, D, int(causal), _lib.ptr(kl), float(scale),
+              _lib.ptr(dmask.fbits) if dmask is not None else None,
+              _lib.ptr(dmask.bbits) if dmask is not None else None,
+              float(dmask.keep_scale) if dmask is not None else 1.0, _lib.stream())
     return dq, dk, dv
 
 

@@ -222,46 +222,38 @@ def _crow(e, hh):
     return (e & 3) + 8 * (e >> 2) + 4 * hh
 
 
-@pytest.mark.parametrize("S,causal", [(256, True), (200, False), (96, True)])
+@pytest.mark.parametrize("S,causal", [(256, True), (200, False), (96, True), (320, False)])
 def test_attention_dropout_mask_images(S, causal):
-    """attn_dropmask_kernel's forward (query-on-lane) and backward (key-on-lane) bit images
+    """flash_dropmask_kernel's forward (query-on-lane) and backward (key-on-lane) bit images
     both decode to the reference keep-mask (dropout_keep_mask), and the drop rate is p."""
-    from mxtrain.ops import _lib
     B, Hq, p, salt = 2, 3, 0.1, 5
     NB = (S + 31) // 32
-    NKT = (NB + 3) // 4
     seed = torch.tensor([424242], dtype=torch.int32, device=DEV)
-    fb = torch.zeros(B * Hq * NB * NKT * 64 * 4, dtype=torch.int16, device=DEV)
-    bb = torch.zeros(B * Hq * NB * NB * 64, dtype=torch.int16, device=DEV)
-    _lib.call("mx_attn_dropmask", _lib.ptr(seed), salt, p, B, S, Hq, 1, Hq + 2, int(causal),
-              _lib.ptr(fb), _lib.ptr(bb), _lib.stream())
+    dm = A.dropmask(B, S, Hq, p, seed, salt, head_offset=1, total_heads=Hq + 2, causal=causal)
     torch.cuda.synchronize()
     ref = A.dropout_keep_mask(B, S, Hq, 424242, salt, p, head_offset=1, total_heads=Hq + 2)
+    NKT, NQT = (S + 127) // 128, (S + 63) // 64
+    fw = dm.fbits.cpu().view(B * Hq, NB, NKT, 64)
+    bw = dm.bbits.cpu().view(B * Hq, NB, NQT, 64).to(torch.int64) & 0xFFFFFFFF
     P = NB * 32
     keepf = torch.zeros(B * Hq, P, P, dtype=torch.bool)
     keepb = torch.zeros(B * Hq, P, P, dtype=torch.bool)
-    fbits = fb.cpu().view(B * Hq, NB, NKT, 64, 4).to(torch.int64) & 0xFFFF
-    bbits = bb.cpu().view(B * Hq, NB, NB, 64).to(torch.int64) & 0xFFFF
     lane = torch.arange(64)
     for qb in range(NB):
         for kb in range(NB):
             if causal and kb > qb:
                 continue
-            wf = fbits[:, qb, kb // 4, :, kb % 4]      # [BH, 64]
-            wb = bbits[:, kb, qb, :]
+            wf = (fw[:, qb, kb // 4, :] >> (32 * ((kb & 3) >> 1))) & 0xFFFFFFFF     # [BH, 64]
+            wb = bw[:, kb, qb // 2, :]
             for e in range(16):
-                bit_f = ((wf >> e) & 1).bool()
-                bit_b = ((wb >> e) & 1).bool()
-                qf = 32 * qb + (lane & 31)
-                kf = 32 * kb + _crow(e, lane >> 5)
-                keepf[:, qf, kf] = bit_f
-                kbk = 32 * kb + (lane & 31)
-                qbk = 32 * qb + _crow(e, lane >> 5)
-                keepb[:, qbk, kbk] = bit_b
+                pf = 8 * (kb & 1) + 16 * (e & 1) + (e >> 1)
+                pb = 8 * (qb & 1) + 16 * (e & 1) + (e >> 1)
+                keepf[:, 32 * qb + (lane & 31), 32 * kb + _crow(e, lane >> 5)] = ((wf >> pf) & 1).bool()
+                keepb[:, 32 * qb + _crow(e, lane >> 5), 32 * kb + (lane & 31)] = ((wb >> pb) & 1).bool()
     refp = ref.reshape(B * Hq, S, S)
     valid = torch.ones(S, S, dtype=torch.bool)
     if causal:
-        valid = torch.ones(S, S, dtype=torch.bool).tril()
+        valid = valid.tril()
     for got in (keepf[:, :S, :S], keepb[:, :S, :S]):
         assert torch.equal(got[:, valid], refp[:, valid])
     rate = 1.0 - refp[:, valid].float().mean().item()
