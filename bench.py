@@ -12,6 +12,14 @@ weights (no dataset / checkpoint on the box).
         bench.py --gpus 8 --steps 20 --warmup 5
 
 Rank 0 prints exactly one JSON line (value = whole-job tokens/s, max step time over ranks).
+
+On one GPU the line also carries the second half of BASELINE.json's metric, Mask R-CNN
+R50-FPN training images/s at the reference's two configs (tensorpack: 1 img/GPU,
+examples/maskrcnn/train-maskrcnn-tensorpack.yaml:16-35; aws-samples: 4 img/GPU,
+examples/maskrcnn/train-maskrcnn-aws.yaml:29), measured after the GPT window by
+scripts/bench_maskrcnn.py in a child process (synthetic COCO-shaped 800 x <=1333 images,
+random-init weights, full training step incl. SGD; the in-repo MIOpen find-db skips the
+conv search).  --no-maskrcnn skips it.
 """
 from __future__ import annotations
 
@@ -36,6 +44,28 @@ def _coll_summary(tr):
             out[name] = {op: [[nb, "xgmi" if win else "rccl"] for nb, win in v] for op, v in c.prefer.items()} \
                 or "rccl (xgmi check failed)"
     return out
+
+
+def run_maskrcnn(batch: int, steps: int, warmup: int, timeout: float = 420.0) -> dict:
+    """One Mask R-CNN training throughput run (child process) -> {"img_s": .., ...}."""
+    import subprocess
+    import tempfile
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = tempfile.mktemp(prefix="mx_mrcnn_", suffix=".jsonl")
+    cmd = [sys.executable, os.path.join(here, "scripts", "bench_maskrcnn.py"), "--batch", str(batch),
+           "--steps", str(steps), "--warmup", str(warmup), "--out", out]
+    t0 = time.time()
+    try:
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout)
+        rec = json.loads(open(out).read().splitlines()[-1]) if r.returncode == 0 and os.path.exists(out) else None
+        if rec is None:
+            return {"error": f"rc={r.returncode}: " + r.stdout[-300:]}
+        return {"img_s": rec["value"], "steps": steps, "warmup": warmup, "wall_s": round(time.time() - t0, 1)}
+    except Exception as e:  # noqa: BLE001 -- the GPT number must still be reported
+        return {"error": repr(e)[:300]}
+    finally:
+        if os.path.exists(out):
+            os.remove(out)
 
 
 def main():
@@ -71,6 +101,8 @@ def main():
                          "to $PYTORCH_TUNABLEOP_FILENAME (see scripts/tune_gemms.sh)")
     ap.add_argument("--wgrad-stream", action="store_true",
                     help="run weight-gradient GEMMs on a concurrent side stream")
+    ap.add_argument("--no-maskrcnn", action="store_true",
+                    help="skip the Mask R-CNN images/s measurements (run on one GPU only)")
     ap.add_argument("--xgmi", choices=["0", "1", "auto"], default="auto",
                     help="direct xGMI peer-to-peer collectives (csrc/comm/xgmi.hip) for the DP "
                          "reduce-scatter / all-gather and TP all-reduce: 0 = RCCL only, 1 = always, "
@@ -202,6 +234,20 @@ def main():
         }
         if graph_err:
             out["graph_error"] = graph_err
+        if world == 1 and not args.no_maskrcnn:
+            # BASELINE.json metric, part 2: Mask R-CNN images/s (outside the GPT timed window)
+            del tr
+            torch.cuda.empty_cache()
+            m1 = run_maskrcnn(1, 60, 15)
+            m4 = run_maskrcnn(4, 40, 10)
+            out["maskrcnn_img_s_1img"] = m1.get("img_s")
+            out["maskrcnn_img_s_4img"] = m4.get("img_s")
+            out["maskrcnn_config"] = {
+                "model": "Mask R-CNN R50-FPN (tensorpack layout)", "n_gpus": 1, "dtype": "bf16",
+                "data": "synthetic COCO-shaped 800x<=1333, random-init weights",
+                "1img": {k: v for k, v in m1.items() if k != "img_s"},
+                "4img": {k: v for k, v in m4.items() if k != "img_s"},
+                "unit": "images/s", "conv_search": "MIOpen find (in-repo find-db)"}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -82,6 +82,7 @@ class GraphedTrainStep:
         self.replays = 0
         # MXTRAIN_GRAPH_DEBUG=1: synchronise after every step and log capture/replay events
         self.debug = os.environ.get("MXTRAIN_GRAPH_DEBUG", "0") == "1"
+        self.marker = None   # diagnostics hook: called around the capture window
 
     def _dbg(self, what: str, key) -> None:
         if self.debug:
@@ -126,8 +127,13 @@ class GraphedTrainStep:
                 # capture: grads are allocated inside the graph's pool, never zeroed
                 self.opt.zero_grad(set_to_none=True)
                 g = torch.cuda.CUDAGraph()
+                if self.marker is not None:
+                    torch.cuda.synchronize(self.device)
+                    self.marker("capture-begin")
                 with torch.cuda.graph(g, pool=self.pool, stream=self.stream):
                     sout = self._body(st)
+                if self.marker is not None:
+                    self.marker("capture-end")
             cur.wait_stream(self.stream)
             self.graphs[key] = (g, st, sout)
             self.captures += 1

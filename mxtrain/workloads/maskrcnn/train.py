@@ -160,6 +160,30 @@ def coco_evaluate(dets, coco, with_masks=True):
 
 
 # ------------------------------------------------------------------------------ main
+def use_shipped_find_db():
+    """Point MIOpen's user find/perf db at a writable copy of the in-repo one
+    (mxtrain/tuning/miopen: the conv solutions found for the training shapes of this model on
+    gfx950 with this image's MIOpen), so a fresh node skips the ~4-minute search.  An
+    explicitly set MIOPEN_USER_DB_PATH wins.  Returns the directory or None."""
+    if os.environ.get("MIOPEN_USER_DB_PATH"):
+        return os.environ["MIOPEN_USER_DB_PATH"]
+    src = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                       "tuning", "miopen")
+    files = glob.glob(os.path.join(src, "*.txt"))
+    if not files:
+        return None
+    import shutil
+    import tempfile
+    dst = os.path.join(tempfile.gettempdir(), f"mxtrain-miopen-{os.getuid()}")
+    os.makedirs(dst, exist_ok=True)
+    for f in files:
+        t = os.path.join(dst, os.path.basename(f))
+        if not os.path.exists(t) or os.path.getsize(t) < os.path.getsize(f):
+            shutil.copyfile(f, t)
+    os.environ["MIOPEN_USER_DB_PATH"] = dst
+    return dst
+
+
 def get_args(argv=None):
     p = argparse.ArgumentParser(allow_abbrev=False)
     p.add_argument("--logdir", default="train_log/maskrcnn")
@@ -256,8 +280,10 @@ def main(argv=None):
     torch.backends.cudnn.benchmark = os.environ.get("MXTRAIN_CONV_BENCHMARK", "1") == "1"
     if torch.backends.cudnn.benchmark:
         os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
-        log("Convolution algorithm search on (MIOpen find, FAST mode): the first steps of each "
-            "input shape take minutes on a node without a MIOpen find-db")
+        db = use_shipped_find_db()
+        log("Convolution algorithm search on (MIOpen find, FAST mode)" +
+            (f"; find-db {db}" if db else ": the first steps of each input shape take minutes on a node "
+             "without a MIOpen find-db"))
     tbw = None
     from mxtrain.obs.profile import StepProfiler, check_finite, check_finite_enabled
     prof = StepProfiler(rank, out_dir=os.path.join(args.logdir, "profile") if os.environ.get("MXTRAIN_PROFILE") else None)
