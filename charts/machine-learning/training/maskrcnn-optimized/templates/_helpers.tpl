@@ -29,8 +29,9 @@ app.kubernetes.io/managed-by: {{ .Release.Service }}
 {{- end }}
 
 {{- define "mr.mpiargs" -}}
+{{- /* MI355X: each rank pinned to disjoint cores of its GPU's NUMA node (reference: none) */}}
 - -bind-to
-- none
+- core
 - -map-by
 - slot
 - -mca

@@ -21,8 +21,9 @@ import json
 import os
 import socket
 import time
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
+from ..runtime import affinity
 from ..runtime.topology import GPUAllocator, gpus_requested
 from .pods import Pod, build_pod, materialize_configmaps, python_exe
 
@@ -85,9 +86,34 @@ class JobController:
         return pod.spec.restart_policy in ("OnFailure", "Always")
 
     def status(self) -> dict:
-        return {"kind": self.kind, "name": self.name, "phase": self.phase, "restarts": self.restarts,
-                "message": self.message, "gpus": self.gpus, "mounts": self.mounts,
-                "pods": {p.spec.name: p.to_status() for p in self.pods}}
+        st = {"kind": self.kind, "name": self.name, "phase": self.phase, "restarts": self.restarts,
+              "message": self.message, "gpus": self.gpus, "mounts": self.mounts,
+              "pods": {p.spec.name: p.to_status() for p in self.pods}}
+        pl = self.placement()
+        if pl:
+            st["placement"] = pl
+        return st
+
+    def placement(self) -> Optional[dict]:
+        """Per-rank CPU/NUMA placement (rank -> gpu, numa node, cpuset)."""
+        return getattr(self, "_placement", None)
+
+    def place(self, gpu_sets: List[List[int]]) -> List[Tuple[List[int], Dict[str, str]]]:
+        """NUMA-local cpusets for replicas that drive ``gpu_sets`` (one rank per GPU):
+        returns per replica (cpuset of the replica = union of its ranks', env carrying the
+        per-LOCAL_RANK sets).  Policy: MXTRAIN_CPU_BIND (core|numa|none)."""
+        pol = affinity.default_bind()
+        flat = [g for s in gpu_sets for g in s]
+        if pol == "none" or not flat:
+            return [([], {}) for _ in gpu_sets]
+        pls = affinity.plan(flat, pol)
+        self._placement = {"bind_to": pol, "ranks": [p.to_json() for p in pls]}
+        out, i = [], 0
+        for s in gpu_sets:
+            mine = pls[i:i + len(s)]
+            i += len(s)
+            out.append((sorted({c for p in mine for c in p.cpus}), affinity.rank_env(mine) if mine else {}))
+        return out
 
     def _emit(self):
         if self.status_cb:
@@ -175,12 +201,20 @@ class PyTorchJobController(JobController):
         self.master_port = free_port()
         pods = []
         node_rank = 0
+        sets = []
+        for role, n, rs in reps:
+            nproc = self._nproc(rs.get("template") or {})
+            for i in range(n):
+                gpus = self.alloc.allocate(nproc) if self.alloc.total > 0 else []
+                self.gpus += gpus
+                sets.append(gpus)
+        placed = self.place(sets)
         for role, n, rs in reps:
             tmpl = rs.get("template") or {}
             nproc = self._nproc(tmpl)
             for i in range(n):
-                gpus = self.alloc.allocate(nproc) if self.alloc.total > 0 else []
-                self.gpus += gpus
+                gpus = sets[node_rank]
+                cpus, penv = placed[node_rank]
                 env = {"PET_NPROC_PER_NODE": str(nproc), "PET_NODE_RANK": str(node_rank),
                        "PET_MASTER_ADDR": "127.0.0.1", "PET_MASTER_PORT": str(self.master_port),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(self.master_port),
@@ -196,8 +230,10 @@ class PyTorchJobController(JobController):
                                 "PET_RDZV_ID": str(elastic.get("rdzvId", self.release)),
                                 "PET_MAX_RESTARTS": str(elastic.get("maxRestarts", 3))})
                 name = f"{self.name}-{role.lower()}-{i}"
+                env.update(penv)
                 spec, plan = build_pod(name, tmpl, self.reldir, self.cm_dirs, env, gpus,
                                        rs.get("restartPolicy", "Never"), role=role, index=i)
+                spec.cpus = cpus
                 self.mounts.update(plan.mounts)
                 pods.append(Pod(spec))
                 node_rank += 1
@@ -250,7 +286,9 @@ class MPIJobController(JobController):
         cmd = list(lc.get("command") or []) + list(lc.get("args") or [])
         if cmd and os.path.basename(cmd[0]) == "mpirun":
             cmd = [python_exe(), "-m", "mxtrain.launch.mpirun"] + cmd[1:]
-        env = {"MXTRAIN_MPI_WORKERS": wfile, "MXTRAIN_MPI_SLOTS": str(slots)}
+        self.placement_file = os.path.join(self.reldir, "mpi-placement.json")
+        env = {"MXTRAIN_MPI_WORKERS": wfile, "MXTRAIN_MPI_SLOTS": str(slots),
+               "MXTRAIN_MPI_PLACEMENT": self.placement_file}
         # the launcher has no PVCs in the reference; resolve paths with the workers' plan
         lspec, _ = build_pod(f"{self.name}-launcher", lt, self.reldir, self.cm_dirs, env, [],
                              (lt.get("spec") or {}).get("restartPolicy", "OnFailure"),
@@ -265,6 +303,13 @@ class MPIJobController(JobController):
         if p.phase == "Succeeded":
             return "Succeeded"
         return None
+
+    def placement(self):
+        try:
+            with open(self.placement_file) as f:
+                return json.load(f)
+        except (AttributeError, OSError, ValueError):
+            return None
 
 
 # ============================================================================ RayJob
@@ -299,8 +344,11 @@ class RayJobController(JobController):
                 env["MXTRAIN_RAY_PIP_IGNORED"] = json.dumps(renv.get("pip"))
         entry = spec.get("entrypoint") or ""
         cmd = ["bash", "-c", entry] if entry else []
+        (cpus, penv), = self.place([gpus])
+        env.update(penv)
         pspec, plan = build_pod(f"rayjob-{self.release}-submitter", head, self.reldir, self.cm_dirs,
                                 env, gpus, "Never", command_override=cmd, role="Submitter")
+        pspec.cpus = cpus
         # the entrypoint is a shell line; rewrite mount prefixes inside it as well
         pspec.command = [plan.rewrite(x) for x in pspec.command]
         self.mounts.update(plan.mounts)
@@ -320,8 +368,10 @@ class PodController(JobController):
         n = gpus_requested(c.get("resources"))
         gpus = self.alloc.allocate(n) if (n and self.alloc.total) else []
         self.gpus = gpus
-        pspec, plan = build_pod(self.name, {"spec": spec}, self.reldir, self.cm_dirs, {}, gpus,
+        (cpus, penv), = self.place([gpus])
+        pspec, plan = build_pod(self.name, {"spec": spec}, self.reldir, self.cm_dirs, penv, gpus,
                                 spec.get("restartPolicy", "Always"))
+        pspec.cpus = cpus
         self.mounts.update(plan.mounts)
         return [Pod(pspec)]
 

@@ -11,13 +11,21 @@ workload initialises RCCL directly (mxtrain.dist.hvd).
 
 Supported options (the subset the reference's mpirun.args use, values.yaml:60-122):
   -np/-n/-c N, -x VAR[=VAL], --output-filename DIR, --tag-output, --timestamp-output,
-  --display-map, -bind-to/--bind-to X, -map-by/--map-by X (slot|node|ppr:N:node),
+  --display-map, --report-bindings, -bind-to/--bind-to X (none|core|hwthread|numa|socket),
+  -map-by/--map-by X (slot|node|ppr:N:node),
   -H/--host, --hostfile, -mca/--mca K V (ignored, echoed with -v), --allow-run-as-root,
   --oversubscribe, -wdir/--wdir DIR.
 Ranks are mapped onto the worker replicas of the MPIJob (MXTRAIN_MPI_WORKERS json written
 by the controller): map-by slot fills worker 0's slots first, map-by node round-robins.
 If any rank fails the others are terminated (OpenMPI's default abort semantics) and the
 failing rank's exit code is returned.
+
+Binding: every rank is pinned (sched_setaffinity before exec) to a cpuset on the NUMA node
+of the GPU it drives (runtime.affinity): ``core`` = disjoint equal slices of that node,
+``numa``/``socket`` = the whole node, ``none`` = unpinned.  Without ``-bind-to`` the policy
+is ``MXTRAIN_CPU_BIND`` (default ``core``).  The placement is printed by --display-map /
+--report-bindings and written to ``MXTRAIN_MPI_PLACEMENT`` (the controller puts it in the
+job status).
 """
 from __future__ import annotations
 
@@ -31,6 +39,8 @@ import threading
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
+
+from ..runtime import affinity
 
 FLAGS_WITH_ARG = {"-np", "-n", "-c", "--np", "-x", "--output-filename", "-output-filename",
                   "-bind-to", "--bind-to", "-map-by", "--map-by", "-H", "--host", "-host",
@@ -48,7 +58,8 @@ class MpirunArgs:
     timestamp_output: bool = False
     display_map: bool = False
     map_by: str = "slot"
-    bind_to: str = "none"
+    bind_to: Optional[str] = None
+    report_bindings: bool = False
     mca: Dict[str, str] = field(default_factory=dict)
     wdir: Optional[str] = None
     verbose: bool = False
@@ -94,9 +105,11 @@ def parse_args(argv: List[str]) -> MpirunArgs:
             a.timestamp_output = True
         elif t in ("--display-map", "-display-map"):
             a.display_map = True
+        elif t in ("--report-bindings", "-report-bindings"):
+            a.report_bindings = True
         elif t in ("-v", "--verbose"):
             a.verbose = True
-        # --allow-run-as-root, --oversubscribe, --report-bindings, -q ... are no-ops here
+        # --allow-run-as-root, --oversubscribe, -q ... are no-ops here
         i += 1
     if not a.program:
         raise SystemExit("mpirun: no executable specified")
@@ -124,6 +137,31 @@ def rank_map(np_: int, nworkers: int, slots: int, map_by: str) -> List[int]:
         return [r % nworkers for r in range(np_)]
     # slot (default): fill each worker's slots, wrap (oversubscribe) if np > total
     return [(r // slots) % nworkers for r in range(np_)]
+
+
+def bind_policy(args: MpirunArgs) -> str:
+    return (args.bind_to or affinity.default_bind()).lower()
+
+
+def rank_placements(args: MpirunArgs, workers: List[dict], wmap: List[int]) -> List[Optional["affinity.Placement"]]:
+    """rank -> Placement (None when unbound).  A rank drives GPU ``gpus[local_rank]`` of
+    its worker (HIP_VISIBLE_DEVICES holds the worker's set, the rank picks by LOCAL_RANK)."""
+    pol = bind_policy(args)
+    if pol == "none":
+        return [None] * len(wmap)
+    gpus, counters = [], {}
+    for w in wmap:
+        lr = counters.get(w, 0)
+        counters[w] = lr + 1
+        g = workers[w].get("gpus") or []
+        gpus.append(g[lr % len(g)] if g else None)
+    return affinity.plan(gpus, pol)
+
+
+def _bound(p) -> str:
+    if p is None:
+        return "N/A"
+    return f"numa {p.numa}[cpus {affinity.format_cpulist(p.cpus)}]" + (f" gpu {p.gpu}" if p.gpu is not None else "")
 
 
 def _free_port() -> int:
@@ -202,14 +240,23 @@ def run(argv: List[str]) -> int:
     wmap = rank_map(np_, len(workers), slots, args.map_by)
     local_sizes = {w: wmap.count(w) for w in set(wmap)}
     port = _free_port()
+    placements = rank_placements(args, workers, wmap)
+    ppath = os.environ.get("MXTRAIN_MPI_PLACEMENT")
+    if ppath:
+        with open(ppath, "w") as f:
+            json.dump({"bind_to": bind_policy(args), "map_by": args.map_by,
+                       "ranks": [p.to_json() if p else None for p in placements]}, f, indent=1)
     if args.display_map:
         print(" ========================   JOB MAP   ========================")
         for wi, w in enumerate(workers):
             ranks = [r for r in range(np_) if wmap[r] == wi]
             print(f"\n Data for node: {w.get('name')}\tNum slots: {slots}\tNum procs: {len(ranks)}")
             for r in ranks:
-                print(f" \tProcess OMPI jobid: [1,0] App: 0 Process rank: {r} Bound: N/A")
+                print(f" \tProcess OMPI jobid: [1,0] App: 0 Process rank: {r} Bound: {_bound(placements[r])}")
         print("\n =============================================================", flush=True)
+    if args.report_bindings:
+        for r, p in enumerate(placements):
+            sys.stderr.write(f"[mxtrain-mpirun] MCW rank {r} bound to {_bound(p)}\n")
     base = dict(os.environ)
     procs: List[subprocess.Popen] = []
     pumps: List[_Pump] = []
@@ -226,8 +273,9 @@ def run(argv: List[str]) -> int:
         cwd = args.wdir or spec.get("workdir") or os.getcwd()
         if not os.path.isdir(cwd):
             cwd = os.getcwd()
+        pl = placements[r]
         p = subprocess.Popen(prog, env=env, cwd=cwd, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                             start_new_session=True)
+                             start_new_session=True, preexec_fn=affinity.preexec(pl.cpus) if pl else None)
         procs.append(p)
         for stream, kind in ((p.stdout, "stdout"), (p.stderr, "stderr")):
             t = _Pump(stream, r, kind, args, lock)

@@ -35,6 +35,7 @@ class PodSpec:
     restart_policy: str = "Never"
     role: str = ""
     index: int = 0
+    cpus: List[int] = field(default_factory=list)   # NUMA-local cpuset (empty = unpinned)
 
 
 class Pod:
@@ -61,8 +62,10 @@ class Pod:
         log.write(f"==== {time.strftime('%Y-%m-%dT%H:%M:%S')} start {self.spec.name} "
                   f"(restart {self.restarts}) gpus={self.spec.gpus}\n".encode())
         env = dict(self.spec.env)
+        from ..runtime.affinity import preexec
         self.proc = subprocess.Popen(self.spec.command, cwd=self.spec.workdir, env=env, stdout=log,
-                                     stderr=subprocess.STDOUT, start_new_session=True)
+                                     stderr=subprocess.STDOUT, start_new_session=True,
+                                     preexec_fn=preexec(self.spec.cpus) if self.spec.cpus else None)
         log.close()
         self.returncode = None
         self.started_at = time.time()
@@ -97,7 +100,13 @@ class Pod:
 
     def to_status(self) -> dict:
         return {"phase": self.phase, "restarts": self.restarts, "exit_code": self.returncode,
-                "gpus": self.spec.gpus, "log": self.spec.log_path, "pid": self.proc.pid if self.proc else None}
+                "gpus": self.spec.gpus, "log": self.spec.log_path, "pid": self.proc.pid if self.proc else None,
+                "cpus": _fmt(self.spec.cpus)}
+
+
+def _fmt(cpus):
+    from ..runtime.affinity import format_cpulist
+    return format_cpulist(cpus) if cpus else None
 
 
 # --------------------------------------------------------------------------- spec building

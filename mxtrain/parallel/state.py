@@ -86,6 +86,11 @@ def init_distributed(backend: Optional[str] = None, device_type: Optional[str] =
     world = _env_int("WORLD_SIZE", 1)
     rank = _env_int("RANK", 0)
     local_rank = _env_int("LOCAL_RANK", 0)
+    # NUMA-local cpuset chosen by the job controller (runtime.affinity)
+    from ..runtime.affinity import pin_self_from_env
+    cpus = pin_self_from_env(local_rank)
+    if cpus and "OMP_NUM_THREADS" not in os.environ:
+        torch.set_num_threads(max(1, len(cpus)))
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if device_type == "cuda":

@@ -246,3 +246,145 @@ def test_hpo_random_and_grid_search(home, tmp_path):
     exp["earlyStopping"] = {"algorithmName": "medianstop", "minTrialsRequired": 2}
     res = run_experiment(exp, log=lambda *a: None)
     assert {t["status"] for t in res["trials"]} <= {"Succeeded", "EarlyStopped"}
+
+
+# --------------------------------------------------------------------------- CPU / NUMA placement
+def fake_topology(root, sockets=2, cores=32, smt=2, gpus_per_socket=4, io_link_only=()):
+    """Fake sysfs: `sockets` NUMA nodes of `cores` SMT-`smt` cores (CPU numbering as on
+    Linux: all first threads, then the siblings), KFD CPU nodes first, then the GPUs
+    with PCI locations whose numa_node says their socket (GPUs in `io_link_only` carry
+    only a KFD io_link to their CPU node)."""
+    ncpu = sockets * cores
+    for s in range(sockets):
+        first = list(range(s * cores, (s + 1) * cores))
+        cpus = first + [c + ncpu * t for t in range(1, smt) for c in first]
+        d = root / f"sys/devices/system/node/node{s}"
+        d.mkdir(parents=True)
+        from mxtrain.runtime.affinity import format_cpulist
+        (d / "cpulist").write_text(format_cpulist(cpus) + "\n")
+        for c in first:
+            sib = [c + ncpu * t for t in range(smt)]
+            for x in sib:
+                t = root / f"sys/devices/system/cpu/cpu{x}/topology"
+                t.mkdir(parents=True, exist_ok=True)
+                (t / "thread_siblings_list").write_text(",".join(map(str, sib)) + "\n")
+    kfd = root / "sys/class/kfd/kfd/topology/nodes"
+    for s in range(sockets):
+        n = kfd / str(s)
+        n.mkdir(parents=True)
+        (n / "properties").write_text(f"cpu_cores_count {cores * smt}\nsimd_count 0\ngfx_target_version 0\n")
+    for g in range(sockets * gpus_per_socket):
+        s = g // gpus_per_socket
+        n = kfd / str(sockets + g)
+        (n / "io_links/0").mkdir(parents=True)
+        (n / "io_links/0/properties").write_text(f"type 11\nnode_from {sockets + g}\nnode_to {s}\n")
+        bus = 0x10 + 0x10 * g
+        if g in io_link_only:
+            (n / "properties").write_text("cpu_cores_count 0\nsimd_count 1024\ngfx_target_version 90500\n")
+            continue
+        (n / "properties").write_text(f"cpu_cores_count 0\nsimd_count 1024\ngfx_target_version 90500\n"
+                                      f"location_id {bus << 8}\ndomain 0\n")
+        p = root / f"sys/bus/pci/devices/0000:{bus:02x}:00.0"
+        p.mkdir(parents=True)
+        (p / "numa_node").write_text(f"{s}\n")
+    return root
+
+
+def test_numa_plan_disjoint_local_8_ranks(tmp_path):
+    from mxtrain.runtime import affinity as af
+    root = str(fake_topology(tmp_path, io_link_only=(5,)))
+    assert af.gpu_numa_nodes(root) == [0, 0, 0, 0, 1, 1, 1, 1]
+    nodes = af.numa_cpus(root)
+    allowed = range(128)
+    pl = af.plan(list(range(8)), "core", root=root, allowed=allowed)
+    seen = set()
+    for p in pl:
+        assert p.numa == p.gpu // 4
+        assert set(p.cpus) <= set(nodes[p.numa])                  # NUMA-local
+        assert not (set(p.cpus) & seen)                           # disjoint
+        assert len(p.cpus) == 16                                  # 8 cores x 2 threads
+        assert all((c + 64) in p.cpus for c in p.cpus if c < 64)  # SMT siblings kept together
+        seen |= set(p.cpus)
+    assert len(seen) == 128
+    # a GPU subset + rank order from a launcher (HIP ids 6,1 -> numa 1, 0)
+    pl = af.plan([6, 1], "core", root=root, allowed=allowed)
+    assert [p.numa for p in pl] == [1, 0] and len(pl[0].cpus) == 64
+    # numa/socket: whole local node; hwthread: a single CPU; bad mode raises
+    assert af.plan([0, 7], "numa", root=root, allowed=allowed)[1].cpus == nodes[1]
+    assert len(af.plan([0], "hwthread", root=root, allowed=allowed)[0].cpus) == 1
+    with pytest.raises(ValueError):
+        af.plan([0], "bogus", root=root)
+    # cpuset restricted by the launcher's own affinity
+    pl = af.plan([0, 1], "core", root=root, allowed=[0, 1, 2, 3, 64, 65, 66, 67])
+    assert pl[0].cpus == [0, 1, 64, 65] and pl[1].cpus == [2, 3, 66, 67]
+    # env round trip for torchrun-started local ranks
+    env = af.rank_env(pl)
+    assert af.parse_cpulist(json.loads(env["MXTRAIN_RANK_CPUSETS"])[1]) == [2, 3, 66, 67]
+
+
+def _small_topology(tmp_path):
+    # the test host may have only a few CPUs: 2 sockets x 2 cores x SMT2 over cpus 0-7
+    n = min(8, len(os.sched_getaffinity(0)))
+    assert n >= 8 or pytest.skip("needs 8 CPUs")
+    return fake_topology(tmp_path / "sysfs", sockets=2, cores=2, smt=2, gpus_per_socket=2)
+
+
+def test_mpirun_binds_ranks_numa_local(tmp_path):
+    root = _small_topology(tmp_path)
+    wf = tmp_path / "workers.json"
+    wf.write_text(json.dumps({"workers": [{"name": "w0", "gpus": [0, 2]}, {"name": "w1", "gpus": [1, 3]}],
+                              "slots": 2}))
+    probe = ("import os, json; print('AFF', os.environ['OMPI_COMM_WORLD_RANK'], "
+             "json.dumps(sorted(os.sched_getaffinity(0)), separators=(',', ':')))")
+    env = dict(os.environ, PYTHONPATH=REPO, MXTRAIN_SYSFS_ROOT=str(root), MXTRAIN_MPI_WORKERS=str(wf),
+               MXTRAIN_MPI_PLACEMENT=str(tmp_path / "pl.json"))
+    r = subprocess.run([sys.executable, "-m", "mxtrain.launch.mpirun", "-np", "4", "-bind-to", "core",
+                        "--report-bindings", "--tag-output", sys.executable, "-c", probe],
+                       env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    aff = {}
+    for line in r.stdout.splitlines():
+        if "AFF " in line:
+            rank, lst = line.split("AFF ", 1)[1].split()
+            aff[int(rank)] = json.loads(lst)
+    # map-by slot: ranks 0,1 on w0 (GPUs 0,2 -> numa 0,1), ranks 2,3 on w1 (GPUs 1,3 -> numa 0,1)
+    node0, node1 = {0, 1, 4, 5}, {2, 3, 6, 7}
+    assert set(aff[0]) <= node0 and set(aff[2]) <= node0
+    assert set(aff[1]) <= node1 and set(aff[3]) <= node1
+    assert not set(aff[0]) & set(aff[2]) and not set(aff[1]) & set(aff[3])
+    assert "MCW rank 3 bound to numa 1" in r.stderr
+    pl = json.loads((tmp_path / "pl.json").read_text())
+    assert pl["bind_to"] == "core" and [x["gpu"] for x in pl["ranks"]] == [0, 2, 1, 3]
+    # -bind-to none (the reference's setting) leaves ranks unpinned
+    r = subprocess.run([sys.executable, "-m", "mxtrain.launch.mpirun", "-np", "2", "-bind-to", "none",
+                        sys.executable, "-c", probe], env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    full = sorted(os.sched_getaffinity(0))
+    rows = [line.split()[2] for line in r.stdout.splitlines() if line.startswith("AFF")]
+    assert len(rows) == 2 and all(json.loads(x) == full for x in rows)
+
+
+def test_pytorchjob_records_and_applies_placement(home, monkeypatch):
+    root = _small_topology(home)
+    monkeypatch.setenv("MXTRAIN_SYSFS_ROOT", str(root))
+    monkeypatch.setenv("MXTRAIN_NUM_GPUS", "4")
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    probe = ("import os, json; print('AFF', os.environ['HOSTNAME'], os.environ['MXTRAIN_RANK_CPUSETS'].replace(' ', ''), "
+             "json.dumps(sorted(os.sched_getaffinity(0)), separators=(',', ':')))")
+    v = _values(home, {"resources": {"nnodes": 2, "nproc_per_node": 2},
+                       "train": {"command": ["python3"], "args": ["-c", f'"{probe}"']}})
+    st = _install("training/pytorchjob-distributed", "numa", [v])
+    assert st["phase"] == "Succeeded", st
+    job = st["resources"]["PyTorchJob/pytorchjob-numa"]
+    ranks = job["placement"]["ranks"]
+    from mxtrain.runtime.affinity import parse_cpulist
+    assert [r["gpu"] for r in ranks] == [0, 1, 2, 3] and [r["numa"] for r in ranks] == [0, 0, 1, 1]
+    sets = [set(parse_cpulist(r["cpus"])) for r in ranks]
+    assert all(not (sets[i] & sets[j]) for i in range(4) for j in range(i))
+    for pod in ("pytorchjob-numa-master-0", "pytorchjob-numa-worker-0"):
+        line = [x for x in _log("numa", pod).splitlines() if x.startswith("AFF")][0]
+        _, host, per_rank, aff = line.split()
+        i = 0 if "master" in pod else 2
+        assert set(json.loads(aff)) == sets[i] | sets[i + 1]          # replica = its ranks' union
+        assert [set(parse_cpulist(x)) for x in json.loads(per_rank)] == sets[i:i + 2]
+        assert job["pods"][pod]["cpus"]
