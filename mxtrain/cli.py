@@ -63,6 +63,14 @@ def cmd_uninstall(a):
     return 0
 
 
+def cmd_scale(a):
+    """Elastic PyTorchJob membership (kubectl scale analogue): the controller clamps to
+    [minReplicas, maxReplicas]; new replicas join at the next rendezvous round."""
+    rel.scale(a.release, a.replicas, a.namespace)
+    print(f'release "{a.release}" scaled to {a.replicas} replica(s)')
+    return 0
+
+
 def cmd_status(a):
     st = rel.read_status(a.release, a.namespace)
     if a.output == "json":
@@ -225,6 +233,11 @@ def build_parser():
     q.add_argument("release")
     q.add_argument("-n", "--namespace", default=rel.DEFAULT_NS)
     q.set_defaults(fn=cmd_uninstall)
+    q = sp.add_parser("scale", help="change the replica count of an elastic PyTorchJob")
+    q.add_argument("release")
+    q.add_argument("--replicas", type=int, required=True)
+    q.add_argument("-n", "--namespace", default=rel.DEFAULT_NS)
+    q.set_defaults(fn=cmd_scale)
     q = sp.add_parser("status")
     q.add_argument("release")
     q.add_argument("-n", "--namespace", default=rel.DEFAULT_NS)

@@ -9,6 +9,8 @@ Single-node replacements of the Kubeflow training-operator, mpi-operator and kub
   `pytorchjob-<rel>-master-0` / `-worker-<i>`, and a disjoint MI355X set (nproc_per_node
   GPUs) through HIP_VISIBLE_DEVICES.  restartPolicy OnFailure + runPolicy.backoffLimit are
   honoured as gang restarts; cleanPodPolicy Running stops the survivors when the job ends.
+  With elasticPolicy the job is elastic instead (ElasticPyTorchJobController): hosted
+  c10d rendezvous, per-replica restarts, min/max membership, scaling.
 * MPIJob -- the launcher's `mpirun ... /etc/config/train-script.sh` runs through
   mxtrain.launch.mpirun (no ssh, no OpenMPI): np ranks on the worker replicas' slots.
 * RayJob -- head group + worker group are realised as a GPU pool; the entrypoint runs as
@@ -196,7 +198,6 @@ class PyTorchJobController(JobController):
 
     def create_pods(self):
         reps = self._replicas()
-        elastic = (self.m.get("spec") or {}).get("elasticPolicy")
         nnodes = sum(n for _, n, _ in reps)
         self.master_port = free_port()
         pods = []
@@ -219,16 +220,6 @@ class PyTorchJobController(JobController):
                        "PET_MASTER_ADDR": "127.0.0.1", "PET_MASTER_PORT": str(self.master_port),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(self.master_port),
                        "WORLD_SIZE": str(nnodes), "RANK": str(node_rank), "PET_NNODES": str(nnodes)}
-                if elastic:
-                    port = free_port(elastic.get("rdzvPort")) if node_rank == 0 else self.rdzv_port
-                    self.rdzv_port = port
-                    mn = elastic.get("minReplicas", nnodes)
-                    mx = elastic.get("maxReplicas", nnodes)
-                    env.update({"PET_NNODES": f"{mn}:{mx}" if mn != mx else str(mn),
-                                "PET_RDZV_BACKEND": str(elastic.get("rdzvBackend", "c10d")),
-                                "PET_RDZV_ENDPOINT": f"127.0.0.1:{port}",
-                                "PET_RDZV_ID": str(elastic.get("rdzvId", self.release)),
-                                "PET_MAX_RESTARTS": str(elastic.get("maxRestarts", 3))})
                 name = f"{self.name}-{role.lower()}-{i}"
                 env.update(penv)
                 spec, plan = build_pod(name, tmpl, self.reldir, self.cm_dirs, env, gpus,
@@ -247,6 +238,192 @@ class PyTorchJobController(JobController):
         elif self.pods and all(p.phase == "Succeeded" for p in self.pods):
             return "Succeeded"
         return None
+
+
+# ============================================================================ elastic PyTorchJob
+class ElasticPyTorchJobController(PyTorchJobController):
+    """PyTorchJob with ``elasticPolicy`` (reference: charts/machine-learning/training/
+    pytorchjob-elastic/templates/train.yaml:59-64; training-operator CRD
+    crds/pytorchjobs.yaml:40-60).  Semantics, split as in Kubernetes between the
+    operator and the torchrun elastic agent inside every replica:
+
+    * the controller hosts the c10d rendezvous store (a TCPStore on ``rdzvPort``, so the
+      rendezvous survives any replica) and hands every replica ``PET_NNODES=min:max``,
+      ``PET_RDZV_*``, ``PET_MAX_RESTARTS=maxRestarts`` and ``PET_RDZV_CONF`` (+is_host=false);
+    * a failing *worker process* is the agent's business: torchrun restarts its worker
+      group (up to maxRestarts) and every agent re-rendezvouses, so the job re-forms
+      without the operator touching the other replicas;
+    * a failing *replica* (the agent itself exits non-zero) is restarted alone while the
+      job's restart count is under ``runPolicy.backoffLimit`` -- no gang restart; once the
+      budget is spent the replica stays down and the job continues while at least
+      ``minReplicas`` replicas are alive;
+    * membership changes between min and max with ``mxtrain scale <release> --replicas N``
+      (``<reldir>/scale.json``): new replicas join at the next rendezvous round, removed
+      ones leave and the survivors re-form;
+    * the job succeeds when its replicas have exited and at least one succeeded (torchrun
+      agents finish together); it fails when fewer than minReplicas remain.
+    """
+
+    def _policy(self):
+        ep = (self.m.get("spec") or {}).get("elasticPolicy") or {}
+        role, n, rs = [r for r in self._replicas() if r[0] == "Worker"][0]
+        self.rs = rs
+        self.min = int(ep.get("minReplicas") or n or 1)
+        self.max = max(int(ep.get("maxReplicas") or max(n, self.min)), self.min)
+        self.want = min(max(n, self.min), self.max)
+        self.ep = ep
+
+    def _host_store(self):
+        from datetime import timedelta
+        from torch.distributed import TCPStore
+        last = None
+        for port in (self.ep.get("rdzvPort"), 0):
+            try:
+                self.store = TCPStore("127.0.0.1", int(port or 0), is_master=True, multi_tenant=True,
+                                      wait_for_workers=False, timeout=timedelta(seconds=600))
+                self.rdzv_port = self.store.port
+                return
+            except (RuntimeError, ValueError) as e:   # preferred port busy -> any port
+                last = e
+        raise RuntimeError(f"cannot host the rendezvous store: {last}")
+
+    def _rdzv_conf(self) -> str:
+        kv = {}
+        for item in self.ep.get("rdzvConf") or []:
+            if isinstance(item, dict) and "key" in item:
+                kv[str(item["key"])] = str(item.get("value", ""))
+        kv["is_host"] = "false"
+        return ",".join(f"{k}={v}" for k, v in kv.items())
+
+    def _worker(self, index: int) -> Pod:
+        tmpl = self.rs.get("template") or {}
+        nproc = self._nproc(tmpl)
+        gpus = self.alloc.allocate(nproc) if self.alloc.total > 0 else []
+        self.gpus += gpus
+        (cpus, penv), = self.place([gpus])
+        nn = f"{self.min}:{self.max}" if self.min != self.max else str(self.min)
+        env = {"PET_NNODES": nn, "PET_NPROC_PER_NODE": str(nproc), "PET_NODE_RANK": str(index),
+               "PET_RDZV_BACKEND": str(self.ep.get("rdzvBackend", "c10d")),
+               "PET_RDZV_ENDPOINT": f"127.0.0.1:{self.rdzv_port}",
+               "PET_RDZV_ID": str(self.ep.get("rdzvId", self.release)),
+               "PET_RDZV_CONF": self._rdzv_conf(), "PET_LOCAL_ADDR": "127.0.0.1",
+               "PET_MAX_RESTARTS": str(self.ep.get("maxRestarts", 3)),
+               "MASTER_ADDR": "127.0.0.1",
+               # the agents' shared bootstrap store is built once per agent, in its first
+               # round: a replica joining a later round then waits forever for a
+               # MASTER_ADDR the round's rank 0 never republishes -> publish every round
+               "TORCH_DISABLE_SHARE_RDZV_TCP_STORE": "1"}
+        env.update(penv)
+        spec, plan = build_pod(f"{self.name}-worker-{index}", tmpl, self.reldir, self.cm_dirs, env, gpus,
+                               self.rs.get("restartPolicy", "Never"), role="Worker", index=index)
+        spec.cpus = cpus
+        self.mounts.update(plan.mounts)
+        return Pod(spec)
+
+    def create_pods(self):
+        self._policy()
+        self._host_store()
+        self.down: List[str] = []        # replicas out of the job (budget spent / scaled down)
+        self.next_index = self.want
+        self._scale_mtime = None
+        return [self._worker(i) for i in range(self.want)]
+
+    def status(self):
+        st = super().status()
+        if not hasattr(self, "down"):
+            return st
+        st["elastic"] = {"minReplicas": self.min, "maxReplicas": self.max, "replicas": len(self._live()),
+                         "rdzvEndpoint": f"127.0.0.1:{getattr(self, 'rdzv_port', None)}", "removed": self.down}
+        return st
+
+    def _live(self) -> List[Pod]:
+        return [p for p in self.pods if p.spec.name not in self.down]
+
+    def _drop(self, pod: Pod, why: str):
+        pod.kill()
+        self.down.append(pod.spec.name)
+        if pod.spec.gpus:
+            self.alloc.release(pod.spec.gpus)
+            self.gpus = [g for g in self.gpus if g not in pod.spec.gpus]
+        self.message = why
+
+    def _rescale(self):
+        path = os.path.join(self.reldir, "scale.json")
+        try:
+            mt = os.path.getmtime(path)
+        except OSError:
+            return
+        if mt == self._scale_mtime:
+            return
+        self._scale_mtime = mt
+        try:
+            with open(path) as f:
+                n = int(json.load(f)["replicas"])
+        except (OSError, ValueError, KeyError, TypeError):
+            return
+        n = min(max(n, self.min), self.max)
+        live = [p for p in self._live() if p.phase in ("Running", "Pending")]
+        while len(live) < n:
+            try:
+                p = self._worker(self.next_index)
+            except RuntimeError as e:    # no GPU free -> stay at the current size
+                self.message = f"scale to {n}: {e}"
+                break
+            self.next_index += 1
+            p.start()
+            self.pods.append(p)
+            live.append(p)
+            self.message = f"scaled up: {p.spec.name} joins at the next rendezvous"
+        for p in sorted(live, key=lambda q: -q.spec.index)[:max(0, len(live) - n)]:
+            self._drop(p, f"scaled down: {p.spec.name} removed, survivors re-form")
+
+    def step(self) -> bool:
+        for p in self.pods:
+            p.poll()
+        self._rescale()
+        for p in self._live():
+            if p.phase != "Failed":
+                continue
+            if self.restartable(p) and self.restarts < self.backoff_limit():
+                self.restarts += 1
+                p.restarts += 1
+                self.message = (f"replica {p.spec.name} failed (rc={p.returncode}); restarting it alone "
+                                f"({self.restarts}/{self.backoff_limit()}), it rejoins the rendezvous")
+                p.start()
+            else:
+                self._drop(p, f"replica {p.spec.name} failed (rc={p.returncode}); restart budget spent")
+        live = self._live()
+        verdict = None
+        if len(live) < self.min and not any(p.phase == "Succeeded" for p in live):
+            verdict = "Failed"
+            self.message = (f"{len(live)} replica(s) alive < minReplicas={self.min}" +
+                            (f"; {self.message}" if self.message else ""))
+        elif live and all(p.phase in ("Succeeded", "Failed") for p in live) and \
+                any(p.phase == "Succeeded" for p in live):
+            verdict = "Succeeded"
+        if verdict is not None:
+            self.phase = verdict
+            for p in self.pods:
+                p.kill()
+            self.release_gpus()
+            self._stop_store()
+            self._emit()
+            return False
+        self._emit()
+        return True
+
+    def stop(self):
+        super().stop()
+        self._stop_store()
+
+    def _stop_store(self):
+        self.store = None
+
+
+def _pytorchjob(manifest, *a, **kw):
+    if (manifest.get("spec") or {}).get("elasticPolicy"):
+        return ElasticPyTorchJobController(manifest, *a, **kw)
+    return PyTorchJobController(manifest, *a, **kw)
 
 
 # ============================================================================ MPIJob
@@ -406,7 +583,7 @@ class DeploymentController(JobController):
         return None  # runs until uninstalled
 
 
-CONTROLLERS = {"PyTorchJob": PyTorchJobController, "MPIJob": MPIJobController,
+CONTROLLERS = {"PyTorchJob": _pytorchjob, "MPIJob": MPIJobController,
                "RayJob": RayJobController, "Pod": PodController, "Deployment": DeploymentController}
 PASSIVE_KINDS = {"ConfigMap", "Secret", "Service", "PersistentVolumeClaim", "PersistentVolume",
                  "StorageClass", "ServiceAccount"}

@@ -213,6 +213,16 @@ def uninstall(name: str, namespace: str = DEFAULT_NS, keep_history: bool = False
         shutil.rmtree(reldir, ignore_errors=True)
 
 
+def scale(name: str, replicas: int, namespace: str = DEFAULT_NS) -> None:
+    """Ask the release's elastic PyTorchJob controller for ``replicas`` workers."""
+    d = release_dir(name, namespace)
+    if not os.path.isdir(d):
+        raise FileNotFoundError(f"release {namespace}/{name} not found")
+    if replicas < 1:
+        raise ValueError("replicas must be >= 1")
+    _write_json(os.path.join(d, "scale.json"), {"replicas": int(replicas), "requested": time.time()})
+
+
 def logs(name: str, namespace: str = DEFAULT_NS, pod: Optional[str] = None) -> str:
     d = os.path.join(release_dir(name, namespace), "logs")
     if not os.path.isdir(d):
