@@ -47,6 +47,8 @@
 // 2j at bit sh+j and 2j+1 at bit sh+16+j of a 32-bit word holding two blocks (sh = 0 / 8).
 #include "common.h"
 
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is clobbered on purpose (dma16 / dma4)
+
 using namespace mx;
 
 namespace {
@@ -93,12 +95,23 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
 __device__ __forceinline__ int crow(int e, int hh) { return (e & 3) + 8 * (e >> 2) + 4 * hh; }
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// one 1-KiB LDS-DMA piece: lane i's 16 B from `g` land at lds_base + 16 i
+// one 1-KiB LDS-DMA piece: lane i's 16 B from `g` land at lds_base + 16 i.  Issued from
+// inline asm: for the builtin, the compiler cannot prove that a later ds_read of another
+// ring slot does not alias the in-flight DMA (no alias-scope info on either access) and
+// waits vmcnt(0) before the first LDS read after every issue -- the next tile's DMA was
+// drained before the current tile's first MFMA, serialising load and compute.  The kernels
+// order DMA and reads themselves (vm_drain + barrier at the top of every tile).  M0 = LDS
+// base (wave-uniform); one wait state between the M0 write and the DMA.
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const lds_void_t*)p);
+}
 __device__ __forceinline__ void dma16(const void* g, char* lds_base) {
-  __builtin_amdgcn_global_load_lds(g, (lds_void_t*)lds_base, 16, 0, 0);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :: "v"(g), "s"(lds_u32(lds_base)) : "memory", "m0");
 }
 __device__ __forceinline__ void dma4(const void* g, char* lds_base) {
-  __builtin_amdgcn_global_load_lds(g, (lds_void_t*)lds_base, 4, 0, 0);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
+               :: "v"(g), "s"(lds_u32(lds_base)) : "memory", "m0");
 }
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 

@@ -34,6 +34,7 @@ import torch
 from .. import ops
 from ..ops import attention as attn_ops
 from ..ops.norm import bda_norm_fwd, colsum, layernorm_fwd, norm_bwd
+from ..ops.gemm import wgrad_group
 from ..ops.rope import apply_rope_
 from ..ops.fused import (bias_gelu_bwd, bias_gelu_fwd, bias_swiglu_bwd, bias_swiglu_fwd,
                          cross_entropy_fwd_bwd, embed_bwd, embed_fwd, pos_embed_bwd)
@@ -273,6 +274,10 @@ class StepRuntime:
     # the memory-bound backward kernels of the main stream (None: inline)
     wgrad_stream: Optional[object] = None
     _wgrad_live: bool = False
+    # the first micro-batch of a step WRITES the weight gradients (GEMM beta = 0) instead of
+    # accumulating into a zero-filled buffer (set by the trainer, which then zeroes only the
+    # other gradients)
+    wgrad_overwrite: bool = False
     # optional side stream for work that depends only on the step seed (attention-dropout
     # mask generation) to overlap the layer's QKV GEMM; off by default (MXTRAIN_AUX_STREAM=1):
     # measured on one MI355X the concurrent generator slowed the GEMM by more than it hid
@@ -316,20 +321,23 @@ class StepRuntime:
     def norm_grads(self, prefix):
         return self.grads[prefix + "_w"], self.grads.get(prefix + "_b")
 
-    def wgrad(self, gbuf, dy, x):
-        """gbuf += dy^T x.  On the side stream when enabled: it forks from the main
-        stream here and is joined in done() (before the unit's gradient bucket can be
-        reduced); every operand stays referenced by the caller's frame until then, so the
-        caching allocator cannot hand its memory to main-stream work that is unordered
-        with the side-stream GEMM."""
+    def wgrad(self, *items):
+        """gbuf (+)= dy^T x for every (gbuf, dy, x) -- one grouped MFMA launch
+        (ops/gemm.py: the layer's weight gradients that become ready together).  Written
+        (beta = 0) on the first micro-batch when ``wgrad_overwrite``.  On the side stream
+        when enabled: it forks from the main stream here and is joined in done() (before
+        the unit's gradient bucket can be reduced); every operand stays referenced by the
+        caller's frame until then, so the caching allocator cannot hand its memory to
+        main-stream work that is unordered with the side-stream GEMM."""
+        acc = not self.wgrad_overwrite
         ws = self.wgrad_stream
         if ws is None:
-            _wgrad(gbuf, dy, x)
+            wgrad_group(items, accumulate=acc)
             return
-        main = torch.cuda.current_stream(gbuf.device)
+        main = torch.cuda.current_stream(items[0][0].device)
         ws.wait_stream(main)
         with torch.cuda.stream(ws):
-            _wgrad(gbuf, dy, x)
+            wgrad_group(items, accumulate=acc)
         self._wgrad_live = True
 
     def join_wgrad(self):
@@ -365,7 +373,7 @@ def _reduce(x, rt):
 
 def _wgrad(gbuf, dy, x):
     """gbuf += dy^T x (beta=1 GEMM straight into the flat gradient buffer)."""
-    gbuf.addmm_(dy.t(), x)
+    wgrad_group([(gbuf, dy, x)], accumulate=True)
 
 
 # ============================================================================== Functions
@@ -569,14 +577,14 @@ class GPTLayerFn(torch.autograd.Function):
             dm = grads[0].to(dg.dtype)
             return GPTLayerFn._attn_backward(ctx, dm, dh1, a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2)
         dg_full = _gather(dg, rt)
-        rt.wgrad(G[p + "fc2_w"], dg_full, f)
         df = torch.mm(dg_full, P[p + "fc2_w"])
         if cfg.swiglu:
             dpre = bias_swiglu_bwd(df, pre, P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True)
         else:
             dpre = bias_gelu_bwd(df, pre, P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True,
                                  inplace=True)
-        rt.wgrad(G[p + "fc1_w"], dpre, m_full)
+        # fc2 and fc1 weight gradients in one grouped launch (both operands read in place)
+        rt.wgrad((G[p + "fc2_w"], dg_full, f), (G[p + "fc1_w"], dpre, m_full))
         dm = _reduce(torch.mm(dpre, P[p + "fc1_w"]), rt)
         return GPTLayerFn._attn_backward(ctx, dm, dh1, a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2)
 
@@ -597,7 +605,6 @@ class GPTLayerFn(torch.autograd.Function):
                            dbeta=gb2, dbias=G[p + "proj_b"], accumulate=True)
         # ---- attention backward
         do_full = _gather(do_, rt)
-        rt.wgrad(G[p + "proj_w"], do_full, ctx_)
         dctx = torch.mm(do_full, P[p + "proj_w"])
         if rt.cp > 1:
             dctx = seq_to_head(dctx, (hl * D,), rt.B, rt.S, rt.cp_group)
@@ -616,7 +623,7 @@ class GPTLayerFn(torch.autograd.Function):
         if rt.cp > 1:
             dqkv = head_to_seq(dqkv, (hl * D, kvl * D, kvl * D), rt.B, rt.S, rt.cp_group)
         colsum(dqkv, G[p + "qkv_b"], accumulate=True)
-        rt.wgrad(G[p + "qkv_w"], dqkv, a_full)
+        rt.wgrad((G[p + "proj_w"], do_full, ctx_), (G[p + "qkv_w"], dqkv, a_full))
         da = _reduce(torch.mm(dqkv, P[p + "qkv_w"]), rt)
         rt.done(i + 1)
         return dh, da, None, None, None
@@ -645,7 +652,7 @@ class LMHeadLossFn(torch.autograd.Function):
         ctx.saved = None
         W = rt.params[ctx.wname]
         gv = g.reshape(1).to(x_full.dtype)
-        _wgrad(rt.grads[ctx.wname], dlogits, x_full * gv)
+        wgrad_group([(rt.grads[ctx.wname], dlogits, x_full * gv)], accumulate=not rt.wgrad_overwrite)
         dx = torch.mm(dlogits, W) * gv
         dx = _reduce(dx, rt)
         return dx, None, None, None
@@ -682,6 +689,22 @@ class GPTStage:
             else:
                 self.head_name = "lm_head"
 
+
+    def gemm_grad_names(self) -> List[str]:
+        """Gradients written whole by the backward's weight-gradient GEMMs (GPTLayerFn /
+        LMHeadLossFn): with ``rt.wgrad_overwrite`` the first micro-batch writes them with
+        beta = 0, so the trainer's per-step zero-fill can skip them."""
+        cfg = self.cfg
+        names = []
+        for i in range(self.l0, self.l1):
+            if is_moe_layer(cfg, i):
+                names.append(f"layers.{i}.proj_w")
+                names.append(f"layers.{i}.qkv_w")
+                continue
+            names += [f"layers.{i}.{n}" for n in ("qkv_w", "proj_w", "fc1_w", "fc2_w")]
+        if self.last:
+            names.append(self.head_name)
+        return names
     def forward(self, ids=None, hidden=None, labels=None, B=1, S=None):
         """First stage takes token ids [B*S]; later stages take the hidden state
         [tokens, h] (requires_grad).  Last stage returns the scalar loss, other stages

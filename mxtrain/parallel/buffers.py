@@ -132,8 +132,41 @@ class FlatParams:
                 t.normal_(0.0, std, generator=generator)
                 p.copy_(t.to(self.dtype))
 
+    def set_overwritten(self, names) -> None:
+        """Gradients in ``names`` are written whole (beta = 0 GEMMs) by the first
+        micro-batch of every step: zero_grad() / zero_grad_range() then clear only the other
+        elements (norm / bias / embedding gradients, ~1 % of the buffer) with one
+        index_fill instead of a fill of the whole flat buffer."""
+        keep = torch.ones(self.numel, dtype=torch.bool)
+        for n in names:
+            o = self.offsets[n]
+            keep[o:o + self.spec_by_name[n].numel] = False
+        idx = keep.nonzero().flatten()
+        self._zero_idx = idx.to(self.device)
+        self._zero_idx_cpu = idx
+
     def zero_grad(self):
-        self.grad.zero_()
+        idx = getattr(self, "_zero_idx", None)
+        if idx is None:
+            self.grad.zero_()
+        else:
+            self.grad.index_fill_(0, idx, 0)
+
+    def zero_grad_range(self, start: int, end: int):
+        """zero_grad() restricted to grad[start:end] (one bucket)."""
+        idx = getattr(self, "_zero_idx", None)
+        if idx is None:
+            self.grad[start:end].zero_()
+            return
+        cache = self.__dict__.setdefault("_zero_idx_ranges", {})
+        sub = cache.get((start, end))
+        if sub is None:
+            cpu = self._zero_idx_cpu
+            lo = int(torch.searchsorted(cpu, start))
+            hi = int(torch.searchsorted(cpu, end))
+            sub = cache[(start, end)] = idx[lo:hi]
+        if sub.numel():
+            self.grad.index_fill_(0, sub, 0)
 
     def state_dict(self):
         return {n: p.detach().clone().cpu() for n, p in self.params.items()}

@@ -294,7 +294,7 @@ class DistributedOptimizer:
                              self.grad_shard[so:so + n], self.param_shard[so:so + n], self.hyper_pending,
                              normsq=self.normsq, wd_flags=self.wd_flags[c0:c1])
         if self.world == 1:
-            self.flat.grad[b.start:b.end].zero_()
+            self.flat.zero_grad_range(b.start, b.end)
 
     # ------------------------------------------------------------------ param all-gather
     def gather_params(self):

@@ -50,6 +50,9 @@ class TrainConfig:
     # weight-gradient GEMMs on a side HIP stream (GPU only).  Off by default: measured no
     # gain at GPT-2 345M (19.97 vs 19.81 ms/step) -- hipBLASLt tiles already occupy every CU
     wgrad_stream: bool = False
+    # the first micro-batch's weight-gradient GEMMs write their gradients (beta = 0), so the
+    # per-step zero-fill covers only the other ~1 % of the flat gradient buffer (pp = 1)
+    overwrite_wgrads: bool = True
     moe_expert_parallel_size: int = 1   # --moe-expert-parallel-size
 
 
@@ -79,6 +82,9 @@ class GPTTrainer:
                               attn_seed_t=self.seed.attn_t)
         if tcfg.wgrad_stream and self.device.type == "cuda":
             self.stage.rt.wgrad_stream = torch.cuda.Stream(device=self.device)
+        self._overwrite = bool(tcfg.overwrite_wgrads and ps.pp == 1)
+        if self._overwrite:
+            self.flat.set_overwritten(self.stage.gemm_grad_names())
         sched = LRSchedule(tcfg.lr, tcfg.min_lr, tcfg.lr_warmup_iters, tcfg.lr_decay_iters,
                            tcfg.lr_decay_style)
         self.eflat = self.eopt = None
@@ -166,8 +172,9 @@ class GPTTrainer:
         self.opt.unit_done(unit)
         self.eopt.unit_done(unit)
 
-    def _micro_forward_backward(self, ids, labels, B, S, last_micro):
+    def _micro_forward_backward(self, ids, labels, B, S, last_micro, first_micro=False):
         rt = self.stage.rt
+        rt.wgrad_overwrite = self._overwrite and first_micro
         if self.eopt is not None:
             rt.unit_done = self._unit_done if last_micro else None
         else:
@@ -240,7 +247,7 @@ class GPTTrainer:
             for m in range(nm):
                 loss = loss + self._micro_forward_backward(tokens[m].reshape(-1),
                                                            labels[m].reshape(-1), B, S,
-                                                           m == nm - 1)
+                                                           m == nm - 1, m == 0)
         if self.eopt is not None:
             from .parallel.zero import joint_step
             joint_step(self._opts)
@@ -292,7 +299,7 @@ class GPTTrainer:
             for m in range(nm):
                 loss = loss + self._micro_forward_backward(tokens[m].reshape(-1),
                                                            labels[m].reshape(-1), B, S,
-                                                           m == nm - 1)
+                                                           m == nm - 1, m == 0)
         # optimizer body without host-side hyper update (done before each replay)
         if self.opt.overlap_update:
             # (dense only) grad norm now, AdamW deferred into the next replay's body

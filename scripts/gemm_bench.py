@@ -1,61 +1,80 @@
-"""Time every GEMM of one GPT-2 345M training step (mbs 4, seq 1024) in the exact call
-form the model uses (hipBLASLt through torch), report TFLOP/s per shape and the step total.
-
-    python scripts/gemm_bench.py [--iters 50]
-"""
-import argparse
-import json
+#!/usr/bin/env python3
+"""Weight-gradient GEMMs of GPT-2 345M (T = 4096 tokens): hipBLASLt (torch.addmm, with the
+checked-in TunableOp table) vs csrc/gemm.hip grouped launches.  Interleaved rounds in one
+process; prints per-group median microseconds and PF/s."""
+import os
+import statistics
+import sys
 
 import torch
 
-
-def bench(fn, iters):
-    for _ in range(5):
-        fn()
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mxtrain.ops.gemm import wgrad_group  # noqa: E402
+from mxtrain.runtime.gemm_tuning import use_tuned_gemms  # noqa: E402
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--tokens", type=int, default=4096)
-    a = ap.parse_args()
-    torch.backends.cuda.preferred_blas_library("hipblaslt")
-    T, h, f, V, L = a.tokens, 1024, 4096, 50304, 24
+    use_tuned_gemms()
+    T, h = 4096, 1024
     dev = "cuda"
-    bf = torch.bfloat16
-    rows = []
-    total = 0.0
-    for name, n_out, k_in, per_step in (("qkv", 3 * h, h, L), ("proj", h, h, L), ("fc1", f, h, L), ("fc2", h, f, L),
-                                         ("head", V, h, 1)):
-        W = torch.randn(n_out, k_in, device=dev, dtype=bf) * 0.02
-        b = torch.zeros(n_out, device=dev, dtype=bf)
-        x = torch.randn(T, k_in, device=dev, dtype=bf)
-        dy = torch.randn(T, n_out, device=dev, dtype=bf)
-        g = torch.zeros(n_out, k_in, device=dev, dtype=bf)
-        fl = 2.0 * T * n_out * k_in
-        for kind, fn in (("fwd", lambda: torch.addmm(b, x, W.t())),
-                         ("dgrad", lambda: torch.mm(dy, W)),
-                         ("wgrad", lambda: g.addmm_(dy.t(), x))):
-            if name == "head" and kind == "fwd":
-                fn = lambda: torch.mm(x, W.t())  # noqa: E731
-            ms = bench(fn, a.iters)
-            tf = fl / ms / 1e9
-            rows.append({"gemm": name, "kind": kind, "M": T if kind != "wgrad" else n_out,
-                         "N": n_out if kind == "fwd" else (k_in if kind == "dgrad" else k_in),
-                         "K": k_in if kind == "fwd" else (n_out if kind == "dgrad" else T),
-                         "ms": round(ms, 4), "tflops": round(tf, 1), "ms_per_step": round(ms * per_step, 3)})
-            total += ms * per_step
-    for r in rows:
-        print(json.dumps(r))
-    print(json.dumps({"gemm_ms_per_step": round(total, 3)}))
+    groups = {"fc2+fc1": [(h, 4 * h), (4 * h, h)], "proj+qkv": [(h, h), (3 * h, h)],
+              "proj": [(h, h)], "qkv": [(3 * h, h)], "fc1": [(4 * h, h)], "fc2": [(h, 4 * h)]}
+    data = {}
+    for name, shapes in groups.items():
+        items = []
+        for M, N in shapes:
+            dy = torch.randn(T, M, device=dev).to(torch.bfloat16)
+            x = torch.randn(T, N, device=dev).to(torch.bfloat16)
+            gb = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
+            items.append((gb, dy, x))
+        data[name] = items
+    # numerics
+    for name, items in data.items():
+        wgrad_group(items, accumulate=False)
+        for gb, dy, x in items:
+            ref = dy.float().t() @ x.float()
+            err = ((gb.float() - ref).abs().max() / ref.abs().max()).item()
+            print(f"check {name} {tuple(gb.shape)} rel-max-err {err:.2e}")
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+
+    def t_once(fn, reps=20):
+        ev[0].record()
+        for _ in range(reps):
+            fn()
+        ev[1].record()
+        torch.cuda.synchronize()
+        return ev[0].elapsed_time(ev[1]) * 1000 / reps
+
+    from mxtrain.ops.gemm import plan
+    cfgs = {}
+    for name, items in data.items():
+        cfgs[name] = [("auto", -1, 0)]
+        for v, bm, bn in ((0, 128, 128), (3, 128, 128), (5, 128, 128), (6, 128, 128)):
+            if any(dy.shape[1] % bm or x.shape[1] % bn for _, dy, x in items):
+                continue
+            for sp in (1, 2) if v in (0, 5) else (1,):
+                cfgs[name].append((f"v{v}s{sp}", v, sp))
+        print(name, "auto plan:", plan(items, T))
+    for name, items in data.items():
+        for label, v, sp in cfgs[name]:
+            wgrad_group(items, accumulate=False, variant=v, splits=sp)
+            for gb, dy, x in items:
+                ref = dy.float().t() @ x.float()
+                err = ((gb.float() - ref).abs().max() / ref.abs().max()).item()
+                assert err < 1e-2, (name, label, err)
+    res = {n: {"torch": [], **{c[0]: [] for c in cfgs[n]}} for n in groups}
+    for _ in range(7):
+        for name, items in data.items():
+            res[name]["torch"].append(t_once(lambda: [gb.addmm_(dy.t(), x) for gb, dy, x in items]))
+            for label, v, sp in cfgs[name]:
+                res[name][label].append(t_once(lambda: wgrad_group(items, accumulate=True, variant=v, splits=sp)))
+    for name, items in data.items():
+        fl = sum(2 * T * gb.shape[0] * gb.shape[1] for gb, _, _ in items)
+        print(f"== {name} ({fl / 1e9:.1f} GFLOP)")
+        for k, vals in res[name].items():
+            if vals:
+                tm = statistics.median(vals)
+                print(f"   {k:8s} {tm:7.1f} us {fl / tm / 1e9:5.3f} PF/s")
 
 
 if __name__ == "__main__":

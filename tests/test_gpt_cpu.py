@@ -151,3 +151,36 @@ def test_activation_recompute_is_bit_identical():
     assert out[0][0] == out[1][0]
     for n in out[0][1]:
         assert torch.equal(out[0][1][n], out[1][1][n]), n
+
+
+def test_first_micro_batch_overwrites_gemm_grads():
+    """overwrite_wgrads: the first micro-batch's weight-gradient GEMMs write (beta = 0) and
+    the per-step zero-fill clears only the other gradients -- same gradients and updates as
+    zero-fill + accumulate, over two steps of two micro-batches with garbage left in the
+    GEMM-written gradient ranges between steps."""
+    from mxtrain.parallel import state as pstate
+    from mxtrain.training import GPTTrainer, TrainConfig
+    cfg = GPTConfig(num_layers=2, hidden_size=64, num_attention_heads=4, seq_length=16,
+                    max_position_embeddings=16, vocab_size=128, hidden_dropout=0.0, attention_dropout=0.0)
+    ps = pstate.initialize_model_parallel(device_type="cpu")
+    g = torch.Generator().manual_seed(3)
+    tokens = torch.randint(0, 128, (2, 2, 16), generator=g)
+    labels = torch.randint(0, 128, (2, 2, 16), generator=g)
+    runs = {}
+    for ow in (False, True):
+        tc = TrainConfig(micro_batch_size=2, global_batch_size=4, lr=1e-3, overwrite_wgrads=ow,
+                         overlap_grad_reduce=False)
+        tr = GPTTrainer(cfg, tc, ps, dtype=torch.float32)
+        assert tr._overwrite == ow
+        losses = []
+        for _ in range(2):
+            if ow:   # the overwritten ranges may hold anything before the step
+                for n in tr.stage.gemm_grad_names():
+                    tr.flat.grads[n].fill_(1e3)
+            losses.append(float(tr.train_step(tokens, labels)))
+        runs[ow] = (losses, {n: p.clone() for n, p in tr.flat.params.items()},
+                    {n: p.clone() for n, p in tr.flat.grads.items()})
+    assert runs[True][0] == runs[False][0]
+    for n in runs[False][1]:
+        assert torch.equal(runs[True][1][n], runs[False][1][n]), n
+        assert torch.equal(runs[True][2][n], runs[False][2][n]), n

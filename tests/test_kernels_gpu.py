@@ -464,3 +464,39 @@ def test_moe_gpt_gpu_matches_cpu_and_captures():
     ls = [float(tr.train_step(tok, lab)) for _ in range(4)]
     torch.cuda.synchronize()
     assert all(x == x for x in ls) and ls[-1] < l0, (l0, ls)
+
+
+@pytest.mark.parametrize("T,shapes,accumulate,strided,variant,splits", [
+    (256, [(128, 128)], False, False, 0, 1),
+    (1024, [(1024, 1024), (1024, 3072)], True, True, 6, 1),
+    (512, [(1024, 1024), (3072, 1024)], False, True, -1, 0),
+    (512, [(4096, 1024), (1024, 4096)], True, False, -1, 0),
+    (4096, [(1024, 1024), (3072, 1024), (384, 256), (256, 640)], True, True, 0, 1),
+    (4096, [(1024, 1024), (3072, 1024)], True, True, 2, 4),
+    (2048, [(4096, 1024), (1024, 4096)], False, False, 2, 2),
+    (1024, [(512, 256), (256, 512)], True, True, 1, 2),
+])
+def test_gemm_wgrad_group(T, shapes, accumulate, strided, variant, splits):
+    """csrc/gemm.hip grouped dW = dY^T X against an fp32 reference (asymmetric data, strided
+    dY/X rows, beta 0 and 1); an untileable problem in the group goes through torch."""
+    from mxtrain.ops.gemm import wgrad_group
+    g = torch.Generator(device="cuda").manual_seed(0)
+    items, refs = [], []
+    for (M, N) in shapes + [(200, 128)]:
+        pad = 64 if strided else 0
+        dy = torch.randn(T, M + pad, device="cuda", generator=g).to(torch.bfloat16)[:, :M]
+        x = (torch.randn(T, N + pad, device="cuda", generator=g) + 0.25).to(torch.bfloat16)[:, pad:]
+        gb = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
+        ref = dy.float().t() @ x.float() + (gb.float() if accumulate else 0)
+        items.append((gb, dy, x))
+        refs.append(ref)
+    if variant >= 0:   # forced tiles: the untileable extra problem goes through torch
+        pass
+    wgrad_group(items, accumulate=accumulate, variant=variant, splits=splits)
+    wgrad_group(items[:-1], accumulate=True, variant=variant, splits=splits)   # second launch: tickets reset
+    torch.cuda.synchronize()
+    for (gb, dy, x), ref in zip(items[:-1], refs[:-1]):
+        ref += dy.float().t() @ x.float()
+    for (gb, _, _), ref in zip(items, refs):
+        err = (gb.float() - ref).abs().max().item()
+        assert err <= 0.01 * ref.abs().max().item() + 0.05, (gb.shape, err)
