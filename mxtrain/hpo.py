@@ -1,13 +1,17 @@
-"""Hyper-parameter search over chart releases -- the single-node stand-in for Katib
-(random / grid search, StdOut metrics collector, median early stopping,
-trial templates that launch a PyTorchJob).
+"""Hyper-parameter and architecture search over chart releases -- the single-node
+stand-in for Katib.  Suggestion algorithms: random, grid, sobol, tpe,
+multivariate-tpe, bayesianoptimization, cmaes, hyperband, pbt, enas, darts
+(mxtrain/katib/suggest.py; reference charts/ml-platform/kubeflow-katib/templates/
+config_maps.yaml:26-64).  Metrics collectors: StdOut, File (TEXT/JSON), TensorFlowEvent
+(mxtrain/katib/collectors.py; config_maps.yaml:9-25).  Early stopping: medianstop.
 
 An experiment file (YAML) mirrors Katib's Experiment spec::
 
     name: gpt-lr
     objective: {type: minimize, objectiveMetricName: lm_loss, goal: 5.0,
-                additionalMetricNames: [grad_norm]}
-    algorithm: {algorithmName: random, seed: 0}            # random | grid
+                additionalMetricNames: [grad_norm],
+                metricStrategies: [{name: lm_loss, value: latest}]}   # default: min/max
+    algorithm: {algorithmName: tpe, algorithmSettings: [{name: random_state, value: "1"}]}
     parallelTrialCount: 1
     maxTrialCount: 6
     maxFailedTrialCount: 2
@@ -19,102 +23,63 @@ An experiment file (YAML) mirrors Katib's Experiment spec::
       chart: charts/machine-learning/training/pytorchjob-distributed
       values: [examples/.../pretrain.yaml]                   # -f files
       set: ["train.env[0].value=${trialParameters.lr}"]      # --set with substitution
-      metricsCollector: {kind: StdOut, format: "(?P<name>[\\w\\s]+?):\\s*(?P<value>[-+0-9.eE]+)"}
+    metricsCollectorSpec:                                    # default StdOut
+      collector: {kind: File}
+      source: {fileSystemPath: {path: /efs/hpo/${trialName}/metrics.jsonl, format: JSON}}
 
-Trials are installed as releases ``<experiment>-<n>`` and run to completion (the GPU
-ledger serialises trials that would not fit); the metric is the last value the collector
-finds in the trial's logs (Katib's default "latest" strategy).  Results go to
-``$MXTRAIN_HOME/hpo/<name>/experiment.json`` and the best trial is printed.
+``${trialParameters.<name>}`` and ``${trialName}`` are substituted into the template's
+``set`` values and the collector path.  Trials are installed as releases ``<name>-<n>``
+and run to completion (the GPU ledger serialises trials that would not fit).  Adaptive
+algorithms see every finished trial before their next suggestion; rung/generation based
+ones (hyperband, cmaes, pbt) wait for the running trials when they need their results.
+Results go to ``$MXTRAIN_HOME/hpo/<name>/experiment.json``.
 """
 from __future__ import annotations
 
 import concurrent.futures as cf
-import itertools
 import json
-import math
 import os
-import random
 import re
 import statistics
 from typing import Dict, List, Optional
 
 import yaml
 
+from .katib import collectors as kc
+from .katib.suggest import WAIT, make_suggester
 from .launch import release as rel
 from .runtime.storage import mxtrain_home
 
-DEFAULT_FORMAT = r"(?P<name>[A-Za-z_][\w \-/()]*?)\s*[:=]\s*(?P<value>[-+]?\d+\.?\d*(?:[eE][-+]?\d+)?)"
-
-
-def _sample(p: dict, r: random.Random):
-    fs = p.get("feasibleSpace", {})
-    t = p.get("parameterType", "double")
-    if t == "categorical":
-        return r.choice(list(fs["list"]))
-    lo, hi = float(fs["min"]), float(fs["max"])
-    if p.get("scale") == "log":
-        v = math.exp(r.uniform(math.log(lo), math.log(hi)))
-    else:
-        v = r.uniform(lo, hi)
-    if t == "int":
-        return str(int(round(v)))
-    return f"{v:.6g}"
-
-
-def _grid(p: dict) -> List[str]:
-    fs = p.get("feasibleSpace", {})
-    t = p.get("parameterType", "double")
-    if t == "categorical":
-        return [str(x) for x in fs["list"]]
-    lo, hi = float(fs["min"]), float(fs["max"])
-    if t == "int":
-        step = int(fs.get("step", 1))
-        return [str(v) for v in range(int(lo), int(hi) + 1, step)]
-    step = float(fs.get("step", (hi - lo) / 4 if hi > lo else 1.0))
-    out, v = [], lo
-    while v <= hi + 1e-12:
-        out.append(f"{v:.6g}")
-        v += step
-    return out
+DEFAULT_FORMAT = kc.DEFAULT_FORMAT
 
 
 def suggestions(exp: dict):
-    alg = (exp.get("algorithm") or {}).get("algorithmName", "random")
-    params = exp["parameters"]
-    n = int(exp.get("maxTrialCount", 10))
-    if alg == "grid":
-        combos = itertools.product(*[_grid(p) for p in params])
-        for k, c in enumerate(combos):
-            if k >= n:
-                break
-            yield {p["name"]: v for p, v in zip(params, c)}
-    elif alg == "random":
-        r = random.Random(int((exp.get("algorithm") or {}).get("seed", 0)))
-        for _ in range(n):
-            yield {p["name"]: _sample(p, r) for p in params}
-    else:
-        raise ValueError(f"algorithm {alg} not supported (random, grid)")
+    """All suggestions of a non-adaptive algorithm (random / grid / sobol)."""
+    s = make_suggester(exp)
+    while True:
+        p = s.ask([])
+        if p is None or p is WAIT:
+            return
+        yield p
 
 
-def _subst(s: str, params: Dict[str, str]) -> str:
-    return re.sub(r"\$\{trialParameters\.([A-Za-z0-9_]+)\}", lambda m: params[m.group(1)], s)
+def _subst(s: str, params: Dict[str, str], trial: str = "") -> str:
+    s = re.sub(r"\$\{trialParameters\.([A-Za-z0-9_\-]+)\}", lambda m: str(params[m.group(1)]), s)
+    return s.replace("${trialName}", trial).replace("${trialSpec.Name}", trial)
 
 
 def collect(text: str, names: List[str], fmt: Optional[str] = None) -> Dict[str, float]:
-    rx = re.compile(fmt or DEFAULT_FORMAT)
-    want = {n.lower().replace(" ", "_"): n for n in names}
-    out: Dict[str, float] = {}
-    for line in text.splitlines():
-        for m in rx.finditer(line):
-            key = m.group("name").strip().lower().replace(" ", "_")
-            # "step 10 loss: 4.5" reports metric "loss"; "lm loss: ..." reports "lm_loss"
-            hit = key if key in want else next((w for w in want if key.endswith("_" + w)), None)
-            if hit is not None:
-                try:
-                    out[want[hit]] = float(m.group("value"))
-                except ValueError:
-                    pass
-    return out
+    """StdOut collector with the ``latest`` strategy (kept for callers of the old API)."""
+    return {k: v[-1] for k, v in kc.parse_text(text, names, fmt).items()}
+
+
+def _collector_spec(exp: dict) -> dict:
+    mc = exp.get("metricsCollectorSpec")
+    if mc:
+        return mc
+    old = (exp.get("trialTemplate") or {}).get("metricsCollector") or {}
+    return {"collector": {"kind": old.get("kind", "StdOut")}, "format": old.get("format"),
+            "source": old.get("source")}
 
 
 def run_experiment(exp: dict, namespace: str = rel.DEFAULT_NS, log=print) -> dict:
@@ -122,36 +87,49 @@ def run_experiment(exp: dict, namespace: str = rel.DEFAULT_NS, log=print) -> dic
     obj = exp["objective"]
     metric = obj["objectiveMetricName"]
     names = [metric] + list(obj.get("additionalMetricNames") or [])
+    strat = kc.strategies(obj)
     minimize = obj.get("type", "minimize") == "minimize"
     goal = obj.get("goal")
     tmpl = exp["trialTemplate"]
-    fmt = (tmpl.get("metricsCollector") or {}).get("format")
+    mc = _collector_spec(exp)
     es = exp.get("earlyStopping") or {}
     out_dir = os.path.join(mxtrain_home(), "hpo", name)
     os.makedirs(out_dir, exist_ok=True)
+    sug = make_suggester(exp, root=out_dir)
     trials: List[dict] = []
+    history: List[dict] = []
     failed = 0
+    max_failed = int(exp.get("maxFailedTrialCount", 10 ** 9))
 
     def one(k: int, params: Dict[str, str]) -> dict:
         rname = f"{name}-{k}"
-        sets = [_subst(s, params) for s in tmpl.get("set", [])]
+        sets = [_subst(s, params, rname) for s in tmpl.get("set", [])]
         st = rel.install(tmpl["chart"], rname, namespace, list(tmpl.get("values", [])), sets, wait=True,
                          timeout=tmpl.get("timeout"))
         text = rel.logs(rname, namespace)
-        m = collect(text, names, fmt)
-        rec = {"trial": rname, "parameters": params, "phase": st["phase"], "metrics": m}
+        obs = kc.collect(mc, names, text, lambda s: _subst(s, params, rname))
+        rec = {"trial": rname, "parameters": params, "phase": st["phase"], "metrics": kc.reduce(obs, strat),
+               "observations": {k2: len(v) for k2, v in obs.items()}}
         rel.uninstall(rname, namespace, keep_history=True)
         return rec
 
     par = max(1, int(exp.get("parallelTrialCount", 1)))
-    sug = list(suggestions(exp))
+    stop = False
+    k = 0
     with cf.ThreadPoolExecutor(max_workers=par) as ex:
         futs = {}
-        k = 0
-        while k < len(sug) or futs:
-            while k < len(sug) and len(futs) < par:
-                futs[ex.submit(one, k, sug[k])] = k
+        while True:
+            while not stop and len(futs) < par:
+                p = sug.ask(history)
+                if p is None:
+                    stop = True
+                    break
+                if p is WAIT:
+                    break
+                futs[ex.submit(one, k, p)] = k
                 k += 1
+            if not futs:
+                break
             done, _ = cf.wait(list(futs), return_when=cf.FIRST_COMPLETED)
             for f in done:
                 futs.pop(f)
@@ -170,15 +148,17 @@ def run_experiment(exp: dict, namespace: str = rel.DEFAULT_NS, log=print) -> dic
                         if (v > med) if minimize else (v < med):
                             rec["status"] = "EarlyStopped"
                 trials.append(rec)
+                history.append({"name": rec["trial"], "parameters": rec["parameters"], "value": v,
+                                "status": rec["status"]})
                 log(f"[hpo] {rec['trial']} {rec['parameters']} -> {rec['status']} {rec['metrics']}")
-                if failed > int(exp.get("maxFailedTrialCount", len(sug))):
-                    k = len(sug)
+                if failed > max_failed:
+                    stop = True
                 if goal is not None and v is not None and ((v <= goal) if minimize else (v >= goal)):
-                    k = len(sug)     # goal reached: stop scheduling new trials
+                    stop = True      # goal reached: stop scheduling new trials
     good = [t for t in trials if t.get("status") == "Succeeded"]
     best = (min if minimize else max)(good, key=lambda t: t["metrics"][metric]) if good else None
-    res = {"name": name, "objective": obj, "trials": trials, "best": best,
-           "condition": "Succeeded" if best else "Failed"}
+    res = {"name": name, "objective": obj, "algorithm": (exp.get("algorithm") or {}).get("algorithmName", "random"),
+           "trials": trials, "best": best, "condition": "Succeeded" if best else "Failed"}
     with open(os.path.join(out_dir, "experiment.json"), "w") as f:
         json.dump(res, f, indent=1)
     return res

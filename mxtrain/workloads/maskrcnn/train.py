@@ -124,7 +124,7 @@ def paste_mask(m28, box, H, W, thresh=0.5):
 def coco_evaluate(dets, coco, with_masks=True):
     import numpy as np
     from PIL import Image, ImageDraw
-    from mxtrain.workloads.maskrcnn.coco_eval import evaluate
+    from mxtrain.workloads.maskrcnn.coco_eval import evaluate, tensorpack_stats
     from mxtrain.data.coco import CAT_TO_CONTIG
     gts_b, gts_m, d_b, d_m = [], [], [], []
     ids = {d["image_id"] for d in dets}
@@ -133,13 +133,13 @@ def coco_evaluate(dets, coco, with_masks=True):
         for a in coco.anns.get(iid, []):
             x, y, w, h = a["bbox"]
             gts_b.append({"image_id": iid, "category": CAT_TO_CONTIG[a["category_id"]],
-                          "box": np.array([x, y, x + w, y + h])})
+                          "box": np.array([x, y, x + w, y + h]), "area": a.get("area")})
             if with_masks:
                 mk = Image.new("L", (im["width"], im["height"]), 0)
                 for poly in a.get("segmentation") or []:
                     ImageDraw.Draw(mk).polygon([tuple(p) for p in np.asarray(poly).reshape(-1, 2).tolist()], fill=1)
                 gts_m.append({"image_id": iid, "category": CAT_TO_CONTIG[a["category_id"]],
-                              "mask": np.asarray(mk, dtype=bool)})
+                              "mask": np.asarray(mk, dtype=bool), "area": a.get("area")})
     for d in dets:
         im = coco.images[d["image_id"]]
         for k in range(len(d["scores"])):
@@ -149,13 +149,9 @@ def coco_evaluate(dets, coco, with_masks=True):
                 d_m.append({"image_id": d["image_id"], "category": int(d["labels"][k]),
                             "score": float(d["scores"][k]),
                             "mask": paste_mask(d["mask28"][k], d["boxes"][k], im["height"], im["width"])})
-    stats = {}
-    r = evaluate(d_b, gts_b, "bbox")
-    stats.update({"mAP(bbox)/IoU=0.5:0.95": r["AP"], "mAP(bbox)/IoU=0.5": r["AP50"], "mAP(bbox)/IoU=0.75": r["AP75"]})
+    stats = tensorpack_stats(evaluate(d_b, gts_b, "bbox"), "bbox")
     if with_masks and d_m:
-        r = evaluate(d_m, gts_m, "segm")
-        stats.update({"mAP(segm)/IoU=0.5:0.95": r["AP"], "mAP(segm)/IoU=0.5": r["AP50"],
-                      "mAP(segm)/IoU=0.75": r["AP75"]})
+        stats.update(tensorpack_stats(evaluate(d_m, gts_m, "segm"), "segm"))
     return stats
 
 

@@ -39,6 +39,30 @@ def test_coco_eval_perfect_and_empty():
     assert evaluate(shifted, gts)["AP"] == pytest.approx(0.0)
 
 
+def test_coco_eval_area_ranges_and_recall():
+    """COCOeval's area-range ignore rules and maxDets recall, hand-checked:
+    one small and one large GT; the large one is found (0.9), a small FP fires (0.8)."""
+    from mxtrain.workloads.maskrcnn.coco_eval import evaluate, tensorpack_stats
+    gts = [{"image_id": 1, "category": 1, "box": np.array([0, 0, 10, 10.])},
+           {"image_id": 1, "category": 1, "box": np.array([0, 0, 200, 200.])}]
+    dets = [{"image_id": 1, "category": 1, "score": 0.9, "box": np.array([0, 0, 200, 200.])},
+            {"image_id": 1, "category": 1, "score": 0.8, "box": np.array([500, 500, 505, 505.])}]
+    r = evaluate(dets, gts)
+    assert r["AP"] == pytest.approx(51 / 101)      # recall 0.5 at precision 1: 51 of 101 points
+    assert r["APl"] == pytest.approx(1.0)          # the small FP is outside the range -> ignored
+    assert r["APs"] == pytest.approx(0.0)          # large det matched an ignored GT; small FP counts
+    assert r["APm"] == -1.0                        # no medium GT: missing, as COCOeval prints
+    assert r["AR1"] == pytest.approx(0.5) and r["AR100"] == pytest.approx(0.5)
+    assert r["ARl"] == pytest.approx(1.0) and r["ARs"] == pytest.approx(0.0)
+    st = tensorpack_stats(r, "bbox")
+    assert set(st) == {"mAP(bbox)/IoU=0.5:0.95", "mAP(bbox)/IoU=0.5", "mAP(bbox)/IoU=0.75", "mAP(bbox)/small",
+                       "mAP(bbox)/medium", "mAP(bbox)/large"}
+    # an explicit annotation area (COCO segment area) decides the range, not the box
+    gts2 = [dict(gts[1], area=500.0)]
+    r2 = evaluate(dets[:1], gts2)
+    assert r2["APs"] == pytest.approx(1.0) and r2["APl"] == -1.0
+
+
 @pytest.fixture(scope="module")
 def coco_dir(tmp_path_factory):
     d = tmp_path_factory.mktemp("coco")
