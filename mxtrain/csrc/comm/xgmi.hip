@@ -11,6 +11,10 @@
 //       peers into its own buffer -> barrier -> every rank gathers all shards -> barrier
 //   reduce-scatter (ZeRO-1 gradient shard) and all-gather (parameter shard): halves
 //       of the two-shot algorithm
+//   direct reduce-scatter / all-gather on REGISTERED buffers (the flat gradient buffer,
+//       the ZeRO-1 parameter shard): every peer's buffer is IPC-mapped once, so the
+//       kernel reads the peers' bucket in place -- no copy-in through a staging buffer
+//       (one HBM read + write less per byte), barrier -> read -> barrier
 //
 // Synchronisation is per workgroup, never grid-wide: workgroup b of every rank
 // copies exactly the pieces that workgroup b of the other ranks read next (the
@@ -38,8 +42,13 @@ constexpr int kThreads = 512;
 struct Flags {                                  // one per rank, uncached device memory
   uint32_t slot[3][kMaxBlocks][kMaxRanks];      // [phase][workgroup][source rank]
   uint32_t counter[kMaxBlocks];                 // last completed epoch per workgroup
-  uint32_t error;                               // nonzero after a barrier timeout
+  uint32_t error;                               // nonzero after a barrier timeout / mismatch
+  uint32_t sig[4];                              // validation: op, bytes lo/hi, host sequence no.
 };
+
+// error word: 1 + phase for a barrier timeout; kErrSig + peer for a call-signature
+// mismatch (validation mode: ranks are not in the same collective call)
+constexpr uint32_t kErrSig = 0x100;
 
 struct Peers {
   char* data[kMaxRanks];
@@ -128,15 +137,45 @@ __device__ __forceinline__ uint4 reduce_at(const Peers& pp, int64_t v, int rank,
   for (int64_t v = (lo) + (int64_t)blockIdx.x * kThreads + threadIdx.x; v < (hi); \
        v += (int64_t)gridDim.x * kThreads)
 
-enum Op { kAllReduce1 = 0, kAllReduce2 = 1, kReduceScatter = 2, kAllGather = 3 };
+enum Op {
+  kAllReduce1 = 0, kAllReduce2 = 1, kReduceScatter = 2, kAllGather = 3,
+  kReduceScatterDirect = 4,   // pp.data[i] = peer i's registered input (the full message)
+  kAllGatherDirect = 5        // pp.data[i] = peer i's registered shard (hi(i) - lo(i) vectors)
+};
+
+// validation mode: workgroup 0 publishes this call's signature before the first barrier
+// and compares every peer's after it (peers cannot start their next call before the last
+// barrier of this one, so the slot is stable while it is read)
+__device__ __forceinline__ void publish_sig(Flags* self, const uint32_t* sig) {
+  if (blockIdx.x == 0 && threadIdx.x < 4)
+    __hip_atomic_store(&self->sig[threadIdx.x], sig[threadIdx.x], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void check_sig(const Peers& pp, int rank, int world, const uint32_t* sig) {
+  if (blockIdx.x != 0 || threadIdx.x >= world) return;
+  const int peer = threadIdx.x;
+  bool same = true;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    same &= __hip_atomic_load(&pp.flags[peer]->sig[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == sig[j];
+  if (!same)
+    __hip_atomic_store(&pp.flags[rank]->error, kErrSig + (uint32_t)peer, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // nvec = 16-B vectors of the FULL message (all-gather: of the gathered output);
 // shard = ceil(nvec / world) vectors (shards 0..world-2 full, last may be short)
+struct Sig {
+  uint32_t v[4];
+};
+
 template <bool kBF16>
 __global__ __launch_bounds__(kThreads) void xgmi_kernel(Peers pp, const uint4* in,
                                                          uint4* out, int64_t nvec,
                                                          int rank, int world, int op,
-                                                         uint64_t timeout_ticks) {
+                                                         uint64_t timeout_ticks, Sig sig,
+                                                         int validate) {
   Flags* self = pp.flags[rank];
   const int b = blockIdx.x;
   const uint32_t epoch = self->counter[b] + 1;
@@ -145,15 +184,31 @@ __global__ __launch_bounds__(kThreads) void xgmi_kernel(Peers pp, const uint4* i
   auto lo = [&](int q) { return min((int64_t)q * shard, nvec); };
   auto hi = [&](int q) { return min((int64_t)(q + 1) * shard, nvec); };
   bool ok = true;
+  if (validate) publish_sig(self, sig.v);
 
-  if (op == kAllReduce1) {
+  if (op == kReduceScatterDirect) {
+    ok = xbarrier(pp, 0, rank, world, epoch, timeout_ticks);
+    if (validate) check_sig(pp, rank, world, sig.v);
+    if (ok) FOR_PIECE(v, lo(rank), hi(rank)) out[v - lo(rank)] = reduce_at<kBF16>(pp, v, rank, world);
+  } else if (op == kAllGatherDirect) {
+    ok = xbarrier(pp, 0, rank, world, epoch, timeout_ticks);
+    if (validate) check_sig(pp, rank, world, sig.v);
+    if (ok)
+      for (int i = 0; i < world; ++i) {
+        const int q = (rank + i) % world;
+        const uint4* src = reinterpret_cast<const uint4*>(pp.data[q]);
+        FOR_PIECE(v, lo(q), hi(q)) out[v] = src[v - lo(q)];
+      }
+  } else if (op == kAllReduce1) {
     FOR_PIECE(v, 0, nvec) mine[v] = in[v];
     ok = xbarrier(pp, 0, rank, world, epoch, timeout_ticks);
+    if (validate) check_sig(pp, rank, world, sig.v);
     if (ok) FOR_PIECE(v, 0, nvec) out[v] = reduce_at<kBF16>(pp, v, rank, world);
   } else if (op == kAllGather) {
     // in = my shard (hi(rank) - lo(rank) vectors); out = full [nvec]
     FOR_PIECE(v, lo(rank), hi(rank)) mine[v] = in[v - lo(rank)];
     ok = xbarrier(pp, 0, rank, world, epoch, timeout_ticks);
+    if (validate) check_sig(pp, rank, world, sig.v);
     if (ok)
       for (int i = 0; i < world; ++i) {
         const int q = (rank + i) % world;
@@ -164,6 +219,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_kernel(Peers pp, const uint4* i
     // reduce-scatter / two-shot: copy pieces of every shard, reduce my shard
     for (int q = 0; q < world; ++q) FOR_PIECE(v, lo(q), hi(q)) mine[v] = in[v];
     ok = xbarrier(pp, 0, rank, world, epoch, timeout_ticks);
+    if (validate) check_sig(pp, rank, world, sig.v);
     if (ok) {
       if (op == kReduceScatter) {
         FOR_PIECE(v, lo(rank), hi(rank)) out[v - lo(rank)] = reduce_at<kBF16>(pp, v, rank, world);
@@ -222,6 +278,19 @@ MX_EXPORT int mx_xgmi_open_handle(const void* handle, void** ptr) {
 
 MX_EXPORT int mx_xgmi_close_handle(void* ptr) { return hipIpcCloseMemHandle(ptr); }
 
+// Registration of an existing device allocation (e.g. a torch tensor from the caching
+// allocator): the IPC handle names the whole underlying allocation, so the byte offset of
+// ``ptr`` inside it travels with the handle and the peer adds it to its mapping.
+MX_EXPORT int mx_xgmi_register(void* ptr, void* handle_out, int64_t* offset_out, int64_t* alloc_bytes) {
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  hipError_t e = hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(ptr));
+  if (e != hipSuccess) return e;
+  *offset_out = reinterpret_cast<char*>(ptr) - reinterpret_cast<char*>(base);
+  *alloc_bytes = (int64_t)size;
+  return hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle_out), reinterpret_cast<void*>(base));
+}
+
 // error word of this rank's flags (synchronous read; 0 = healthy)
 MX_EXPORT int mx_xgmi_error(void* flags, uint32_t* out) {
   return hipMemcpy(out, &reinterpret_cast<Flags*>(flags)->error, 4, hipMemcpyDeviceToHost);
@@ -229,11 +298,16 @@ MX_EXPORT int mx_xgmi_error(void* flags, uint32_t* out) {
 
 // datas / flagss: world device pointers (this rank's own + mapped peers), in rank order.
 // nbytes: bytes of the full message (% 16 == 0).  bf16: reduce in bf16 (else fp32).
+// Direct ops (4, 5): datas are the registered regions of this call (offset-adjusted by the
+// caller); ``in`` is unused.  seq / validate: the call signature check (validation mode).
 MX_EXPORT int mx_xgmi_collective(void* const* datas, void* const* flagss, int world, int rank,
                                  const void* in, void* out, int64_t nbytes, int bf16, int op,
-                                 int blocks, double timeout_s, hipStream_t stream) {
-  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || nbytes % 16)
+                                 int blocks, double timeout_s, uint32_t seq, int validate,
+                                 hipStream_t stream) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || nbytes % 16 || op < 0 ||
+      op > kAllGatherDirect)
     return hipErrorInvalidValue;
+  Sig sig = {{(uint32_t)op, (uint32_t)(nbytes & 0xffffffffu), (uint32_t)(nbytes >> 32), seq}};
   Peers pp = {};
   for (int i = 0; i < world; ++i) {
     pp.data[i] = reinterpret_cast<char*>(datas[i]);
@@ -248,9 +322,9 @@ MX_EXPORT int mx_xgmi_collective(void* const* datas, void* const* flagss, int wo
   const uint64_t ticks = (uint64_t)(timeout_s * 1e8);   // s_memrealtime: 100 MHz
   if (bf16)
     hipLaunchKernelGGL(xgmi_kernel<true>, dim3(blocks), dim3(kThreads), 0, stream, pp,
-                       (const uint4*)in, (uint4*)out, nvec, rank, world, op, ticks);
+                       (const uint4*)in, (uint4*)out, nvec, rank, world, op, ticks, sig, validate);
   else
     hipLaunchKernelGGL(xgmi_kernel<false>, dim3(blocks), dim3(kThreads), 0, stream, pp,
-                       (const uint4*)in, (uint4*)out, nvec, rank, world, op, ticks);
+                       (const uint4*)in, (uint4*)out, nvec, rank, world, op, ticks, sig, validate);
   return hipGetLastError();
 }

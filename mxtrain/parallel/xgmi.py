@@ -10,6 +10,17 @@ carry traffic, where RCCL's ring uses one outbound link per GPU.
     comm.all_reduce_(t)                  # one-shot below ``oneshot_max``, else two-shot
     comm.reduce_scatter(out, inp)        # ZeRO-1 gradient shard
     comm.all_gather(out, inp)            # ZeRO-1 parameter shard
+    comm.register("grad", flat_grad)     # collective: map every peer's buffer once
+    comm.reduce_scatter_direct(out, "grad", byte_off, nbytes)   # reads peers in place
+    comm.all_gather_direct(out, "pshard", byte_off)             # ditto, no copy-in
+
+Validation mode (``MXTRAIN_XGMI_VALIDATE=1``, SURVEY §5.2 race detection): every call
+carries a sequence number + signature (op, bytes) that the kernel compares across ranks
+after its first barrier (ranks in different collectives -> error word), and the host
+checks the result after each call: all-reduce / all-gather outputs must be bit-identical
+on every rank (64-bit position-weighted hash, all-gathered), and sum(outputs) must match
+sum(inputs) over the group for reductions (fp64, relative 1e-3).  Debug only: it
+synchronises after every call.
 
 Selection vs RCCL is explicit: ``MXTRAIN_XGMI=1`` (or ``enable_xgmi()``) routes the
 DP reduce-scatter / all-gather and the TP all-reduce through it; ``autotune()`` times
@@ -40,11 +51,23 @@ _SIGS = {
     "mx_xgmi_open_handle": [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)],
     "mx_xgmi_close_handle": [ctypes.c_void_p],
     "mx_xgmi_error": [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)],
+    "mx_xgmi_register": [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
+                         ctypes.POINTER(ctypes.c_int64)],
     "mx_xgmi_collective": [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                            ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                           ctypes.c_double, ctypes.c_void_p],
+                           ctypes.c_double, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p],
 }
+OP_RS_DIRECT, OP_AG_DIRECT = 4, 5
+ERR_SIG = 0x100
+
+
+def _hash64(t: torch.Tensor) -> int:
+    """Position-weighted 64-bit hash of a tensor's bits (validation mode)."""
+    w = t.contiguous().view(-1)
+    bits = w.view(torch.int16 if w.element_size() == 2 else torch.int32).to(torch.int64)
+    pos = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64).remainder(1 << 20).add(1)
+    return int((bits * pos).sum().item())
 
 
 def _fn(name):
@@ -124,17 +147,150 @@ class XGMICommunicator:
             raise XGMIUnavailable(f"xGMI communicator setup failed: {bad}")
         self._datas = (ctypes.c_void_p * self.world)(*datas)
         self._flagss = (ctypes.c_void_p * self.world)(*flags)
+        self.seq = 0
+        self.validate = os.environ.get("MXTRAIN_XGMI_VALIDATE", "0") == "1"
+        self.regions: Dict[str, tuple] = {}     # name -> (local ptr, nbytes, [ptr per rank])
+        self._mapped: Dict[tuple, int] = {}     # (rank, handle bytes) -> mapped base
+        self._region_tensor: Dict[str, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ core
-    def _launch(self, inp: torch.Tensor, out: torch.Tensor, nbytes: int, op: int):
-        assert inp.is_contiguous() and out.is_contiguous()
-        assert inp.dtype in (torch.bfloat16, torch.float32) and out.dtype == inp.dtype
-        if nbytes > self.max_bytes or nbytes % 16:
-            raise ValueError(f"xGMI message of {nbytes} B (max {self.max_bytes}, multiple of 16)")
-        _check(_fn("mx_xgmi_collective")(self._datas, self._flagss, self.world, self.rank,
-                                         inp.data_ptr(), out.data_ptr(), nbytes,
-                                         int(inp.dtype == torch.bfloat16), op, self.blocks,
-                                         self.timeout_s, _lib.stream()), "mx_xgmi_collective")
+    def _launch(self, inp: torch.Tensor, out: torch.Tensor, nbytes: int, op: int, datas=None):
+        assert out.is_contiguous() and out.dtype in (torch.bfloat16, torch.float32)
+        if inp is not None:
+            assert inp.is_contiguous() and out.dtype == inp.dtype
+        if op not in (OP_RS_DIRECT, OP_AG_DIRECT) and nbytes > self.max_bytes:
+            raise ValueError(f"xGMI message of {nbytes} B (max {self.max_bytes})")
+        if nbytes % 16:
+            raise ValueError(f"xGMI message of {nbytes} B (must be a multiple of 16)")
+        self.seq = (self.seq + 1) & 0xFFFFFFFF
+        _check(_fn("mx_xgmi_collective")(datas if datas is not None else self._datas, self._flagss,
+                                         self.world, self.rank,
+                                         inp.data_ptr() if inp is not None else None, out.data_ptr(), nbytes,
+                                         int(out.dtype == torch.bfloat16), op, self.blocks,
+                                         self.timeout_s, self.seq, int(self.validate), _lib.stream()),
+               "mx_xgmi_collective")
+
+    # ------------------------------------------------------------------ registered buffers
+    def register(self, name: str, t: torch.Tensor) -> None:
+        """Collective over the group: map every rank's ``t`` (same shape on every rank, e.g.
+        the flat gradient buffer) into this process, so direct ops read peers in place.
+        ``t`` must stay alive (and not be reallocated) while registered."""
+        assert t.is_cuda and t.is_contiguous()
+        err, mine = None, None
+        try:
+            hs = _fn("mx_xgmi_handle_size")()
+            h = ctypes.create_string_buffer(hs)
+            off, size = ctypes.c_int64(), ctypes.c_int64()
+            _check(_fn("mx_xgmi_register")(t.data_ptr(), h, ctypes.byref(off), ctypes.byref(size)),
+                   "mx_xgmi_register")
+            mine = (bytes(h.raw), off.value, t.numel() * t.element_size())
+        except Exception as e:   # every rank must still reach the exchange
+            err = repr(e)
+        allh: List = [None] * self.world
+        dist.all_gather_object(allh, mine, group=self.group)
+        ptrs = []
+        if err is None:
+            try:
+                for r, entry in enumerate(allh):
+                    if entry is None:
+                        raise RuntimeError(f"rank {r} could not export {name}")
+                    hb, off, nb = entry
+                    if nb != mine[2]:
+                        raise RuntimeError(f"{name}: rank {r} registers {nb} B, this rank {mine[2]} B")
+                    if r == self.rank:
+                        ptrs.append(t.data_ptr())
+                        continue
+                    key = (r, hb)
+                    if key not in self._mapped:
+                        pd = ctypes.c_void_p()
+                        _check(_fn("mx_xgmi_open_handle")(hb, ctypes.byref(pd)),
+                               f"hipIpcOpenMemHandle(rank {r}, {name})")
+                        self._opened.append(pd)
+                        self._mapped[key] = pd.value
+                    ptrs.append(self._mapped[key] + off)
+            except Exception as e:
+                err = repr(e)
+        errs: List = [None] * self.world
+        dist.all_gather_object(errs, err, group=self.group)
+        bad = [(r, e) for r, e in enumerate(errs) if e is not None]
+        if bad:
+            raise XGMIUnavailable(f"xGMI register({name}) failed: {bad}")
+        self.regions[name] = (t.data_ptr(), t.numel() * t.element_size(), ptrs)
+        self._region_tensor[name] = t
+
+    def has_region(self, name: str, t: Optional[torch.Tensor] = None) -> bool:
+        r = self.regions.get(name)
+        return r is not None and (t is None or r[0] == t.data_ptr())
+
+    def _region_ptrs(self, name: str, byte_off: int, nbytes: int):
+        base, total, ptrs = self.regions[name]
+        assert 0 <= byte_off and byte_off + nbytes <= total and byte_off % 16 == 0, (name, byte_off, nbytes)
+        return (ctypes.c_void_p * self.world)(*[p + byte_off for p in ptrs])
+
+    def reduce_scatter_direct(self, out: torch.Tensor, name: str, byte_off: int, nbytes: int) -> torch.Tensor:
+        """out = shard ``rank`` of the sum over ranks of region[name][byte_off : +nbytes]
+        (read in place from every peer's registered buffer)."""
+        assert out.numel() * out.element_size() * self.world == nbytes and nbytes % (16 * self.world) == 0
+        ptrs = self._region_ptrs(name, byte_off, nbytes)
+        if self.validate:
+            self._validated("reduce_scatter", out, self._view(name, byte_off, nbytes),
+                            lambda: self._launch(None, out, nbytes, OP_RS_DIRECT, ptrs))
+            return out
+        self._launch(None, out, nbytes, OP_RS_DIRECT, ptrs)
+        return out
+
+    def all_gather_direct(self, out: torch.Tensor, name: str, byte_off: int) -> torch.Tensor:
+        """out [n * world] = concat over ranks of region[name][byte_off : +n] (every rank's
+        shard read in place from its registered buffer)."""
+        nb = out.numel() * out.element_size()
+        assert nb % (16 * self.world) == 0
+        shard_nb = nb // self.world
+        ptrs = self._region_ptrs(name, byte_off, shard_nb)
+        if self.validate:
+            self._validated("all_gather", out, self._view(name, byte_off, shard_nb),
+                            lambda: self._launch(None, out, nb, OP_AG_DIRECT, ptrs))
+            return out
+        self._launch(None, out, nb, OP_AG_DIRECT, ptrs)
+        return out
+
+    def _view(self, name, byte_off, nbytes):
+        """The local registered bytes [byte_off, +nbytes) as a tensor (validation only)."""
+        t = self._region_tensor[name]
+        es = t.element_size()
+        return t.view(-1)[byte_off // es:(byte_off + nbytes) // es]
+
+    # ------------------------------------------------------------------ validation mode
+    def _validated(self, op: str, out: torch.Tensor, inp: torch.Tensor, launch) -> None:
+        """Run ``launch`` and check its result across the group (synchronising)."""
+        in_sum = float(inp.double().sum()) if op != "all_gather" else 0.0
+        seq = self.seq + 1
+        launch()
+        torch.cuda.synchronize(self.device)
+        v = ctypes.c_uint32(0)
+        _check(_fn("mx_xgmi_error")(self._flags, ctypes.byref(v)), "mx_xgmi_error")
+        errs = []
+        if v.value >= ERR_SIG:
+            errs.append(f"call signature mismatch with rank {v.value - ERR_SIG} (ranks in different collectives)")
+        elif v.value:
+            errs.append(f"barrier timeout in phase {v.value - 1}")
+        stats = torch.tensor([in_sum, float(out.double().sum())], dtype=torch.float64)
+        allstats: List = [None] * self.world
+        h = _hash64(out) if op in ("all_reduce", "all_gather") else 0
+        dist.all_gather_object(allstats, (stats.tolist(), h, errs), group=self.group)
+        if op in ("all_reduce", "all_gather") and len({x[1] for x in allstats}) != 1:
+            errs.append("outputs differ across ranks: " + str([x[1] for x in allstats]))
+        if op == "all_gather":
+            mine = out.view(-1)[self.rank * inp.numel():(self.rank + 1) * inp.numel()]
+            if not torch.equal(mine, inp.view(-1)):
+                errs.append("own shard not reproduced in the gathered output")
+        else:
+            tot_in = sum(x[0][0] for x in allstats)
+            tot_out = sum(x[0][1] for x in allstats) if op == "reduce_scatter" else allstats[self.rank][0][1]
+            if abs(tot_out - tot_in) > 1e-3 * max(1.0, abs(tot_in)) + 1e-2:
+                errs.append(f"sum(out)={tot_out:.6g} != sum(in)={tot_in:.6g}")
+        others = [(r, x[2]) for r, x in enumerate(allstats) if x[2] and r != self.rank]
+        if errs or others:
+            raise RuntimeError(f"xGMI validation failed: {op} seq={seq} rank={self.rank}: {errs} peers={others}")
 
     def supports(self, t: torch.Tensor, shard_multiple: bool = False) -> bool:
         nb = t.numel() * t.element_size()
@@ -147,6 +303,9 @@ class XGMICommunicator:
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         nb = t.numel() * t.element_size()
         op = OP_ALLREDUCE_1SHOT if nb <= self.oneshot_max else OP_ALLREDUCE_2SHOT
+        if self.validate:
+            self._validated("all_reduce", t, t.clone(), lambda: self._launch(t, t, nb, op))
+            return t
         self._launch(t, t, nb, op)
         return t
 
@@ -154,6 +313,9 @@ class XGMICommunicator:
         """out [n / world] = (sum over ranks of inp [n]) shard ``rank``."""
         nb = inp.numel() * inp.element_size()
         assert out.numel() * self.world == inp.numel() and nb % (16 * self.world) == 0
+        if self.validate:
+            self._validated("reduce_scatter", out, inp, lambda: self._launch(inp, out, nb, OP_REDUCE_SCATTER))
+            return out
         self._launch(inp, out, nb, OP_REDUCE_SCATTER)
         return out
 
@@ -161,6 +323,9 @@ class XGMICommunicator:
         """out [n * world] = concat over ranks of inp [n]."""
         nb = out.numel() * out.element_size()
         assert inp.numel() * self.world == out.numel() and nb % (16 * self.world) == 0
+        if self.validate:
+            self._validated("all_gather", out, inp, lambda: self._launch(inp, out, nb, OP_ALL_GATHER))
+            return out
         self._launch(inp, out, nb, OP_ALL_GATHER)
         return out
 
@@ -179,6 +344,7 @@ class XGMICommunicator:
             if p.value:
                 _fn("mx_xgmi_close_handle")(p)
         self._opened = []
+        self.regions, self._mapped, self._region_tensor = {}, {}, {}
         if getattr(self, "_data", None) is not None and (self._data.value or self._flags.value):
             _fn("mx_xgmi_free")(self._data, self._flags)
         self._data = ctypes.c_void_p()
@@ -293,6 +459,11 @@ def mode() -> str:
 
 def enabled() -> bool:
     return mode() in ("1", "auto")
+
+
+def direct_enabled() -> bool:
+    """MXTRAIN_XGMI_DIRECT (default 1): ZeRO-1 buckets use the registered-buffer kernels."""
+    return os.environ.get("MXTRAIN_XGMI_DIRECT", "1") == "1"
 
 
 def enable_xgmi(on="1"):

@@ -127,6 +127,9 @@ class DistributedOptimizer:
         self._sp_names = [s.name for s in flat.specs if s.sp_reduce]
         self.started = set()
         self.reset_pending()
+        # xGMI registered-buffer mode (see _direct); names are local keys only
+        self._direct_state: Optional[bool] = None
+        self._rg_grad, self._rg_pshard = f"zero{id(self)}.grad", f"zero{id(self)}.pshard"
         # ZeRO-1 parameter all-gather deferred to the start of the next step and overlapped
         # with its forward (bucket by bucket, in forward order); the layers wait on their
         # bucket's event (StepRuntime.before_unit -> wait_unit)
@@ -165,19 +168,47 @@ class DistributedOptimizer:
         self.started = set()
 
     # ------------------------------------------------------------------ DP collectives
-    def _rs(self, out, inp):
-        """Bucket gradient reduce-scatter: direct xGMI kernel when selected, else RCCL."""
-        c = _xgmi.route(self.dp_group, inp, "reduce_scatter", inp.numel() * inp.element_size())
+    def _direct(self, c) -> bool:
+        """Register the flat gradient buffer and the parameter shard with the xGMI
+        communicator (once, collectively) so bucket reduce-scatters / all-gathers read the
+        peers' buffers in place instead of staging each bucket through a copy-in buffer.
+        Never during a hipGraph capture; any failure -> the staged kernels."""
+        if self._direct_state is not None:
+            return self._direct_state
+        if torch.cuda.is_current_stream_capturing() or not _xgmi.direct_enabled():
+            return False
+        try:
+            c.register(self._rg_grad, self.flat.grad)
+            c.register(self._rg_pshard, self.param_shard)
+            self._direct_state = True
+        except _xgmi.XGMIUnavailable as e:
+            if self.rank == 0:
+                print(f"[mxtrain] {e}; xGMI collectives keep the staged path", flush=True)
+            self._direct_state = False
+        return self._direct_state
+
+    def _rs(self, out, inp, bstart: Optional[int] = None):
+        """Bucket gradient reduce-scatter: direct xGMI kernel when selected (reading the
+        peers' registered gradient buckets in place), else RCCL."""
+        nb = inp.numel() * inp.element_size()
+        c = _xgmi.route(self.dp_group, inp, "reduce_scatter", nb)
         if c is not None:
-            c.reduce_scatter(out, inp)
+            if bstart is not None and self._direct(c):
+                c.reduce_scatter_direct(out, self._rg_grad, bstart * inp.element_size(), nb)
+            else:
+                c.reduce_scatter(out, inp)
         else:
             dist.reduce_scatter_tensor(out, inp, group=self.dp_group)
 
-    def _ag(self, out, inp):
-        """Parameter-shard all-gather: direct xGMI kernel when selected, else RCCL."""
+    def _ag(self, out, inp, shard_off: Optional[int] = None):
+        """Parameter-shard all-gather: direct xGMI kernel when selected (every rank's new
+        shard read in place from its registered param_shard), else RCCL."""
         c = _xgmi.route(self.dp_group, inp, "all_gather", out.numel() * out.element_size())
         if c is not None:
-            c.all_gather(out, inp)
+            if shard_off is not None and self._direct(c):
+                c.all_gather_direct(out, self._rg_pshard, shard_off * inp.element_size())
+            else:
+                c.all_gather(out, inp)
         else:
             dist.all_gather_into_tensor(out, inp, group=self.dp_group)
 
@@ -203,10 +234,10 @@ class DistributedOptimizer:
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
                 self._sp_allreduce(b)
-                self._rs(self.grad_shard[so:so + n], self.flat.grad[b.start:b.end])
+                self._rs(self.grad_shard[so:so + n], self.flat.grad[b.start:b.end], b.start)
         else:
             self._sp_allreduce(b)
-            self._rs(self.grad_shard[so:so + n], self.flat.grad[b.start:b.end])
+            self._rs(self.grad_shard[so:so + n], self.flat.grad[b.start:b.end], b.start)
 
     def unit_done(self, unit: int):
         bi = self.flat.unit_to_bucket.get(unit)
@@ -306,7 +337,7 @@ class DistributedOptimizer:
             self.gather_pending = True
             return
         for (b, fs, so, n) in self.slices:
-            self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n])
+            self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n], so)
 
     def begin_param_gather(self):
         """Start the work deferred from the previous step, per bucket in forward order:
@@ -330,13 +361,13 @@ class DistributedOptimizer:
                     if upd:
                         self._update_slice(bi)
                     if gat:
-                        self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n])
+                        self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n], so)
                     self._gather_events[bi] = self._last_event = side.record_event()
             else:
                 if upd:
                     self._update_slice(bi)
                 if gat:
-                    self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n])
+                    self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n], so)
 
     def wait_unit(self, unit: int):
         bi = self.flat.unit_to_bucket.get(unit)

@@ -202,6 +202,14 @@ def get_args(argv=None):
 
 def main(argv=None):
     args = get_args(argv)
+    if args.mx_graph != "0":
+        # Whole-step hipGraph replay faults under the HIP runtime's graph packet-capture
+        # mode (kernel dispatch packets pre-built at instantiation) with MIOpen's assembly
+        # convolution kernels, and replays cleanly with it off (scripts/graph_diag.py, one
+        # MI355X, same inputs).  It is read when the HIP runtime initialises, so it is set
+        # before the first GPU call; the graph's kernels are then dispatched one by one by
+        # the runtime -- still no Python / ATen dispatch per op.
+        os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
     from mxtrain.data.coco import AspectGroupedSampler, COCODetection, DetectionDataset, collate
     from mxtrain.models.maskrcnn import MaskRCNN
     from mxtrain.parallel import hvd

@@ -99,6 +99,44 @@ def _worker(rank, world, port, q):
         out["autotune_ok"] = 0.0 if comm.autotune_ok else 1.0
         out["autotune_ops"] = 0.0 if set(comm.prefer) == {"all_reduce", "reduce_scatter", "all_gather"} \
             and all(len(v) == 2 for v in comm.prefer.values()) else 1.0
+
+        # registered buffers: the kernels read the peers' tensors in place (ZeRO-1 flat
+        # gradient buffer / parameter shard), at a byte offset inside the registration
+        n = 8 * 1024 * world
+        big = torch.zeros(3 * n, device=dev, dtype=torch.float32)   # a caching-allocator tensor
+        grad = big[n:]                                                # registered at an offset
+        grad.copy_(torch.arange(2 * n, device=dev, dtype=torch.float32).remainder(5).add(rank))
+        comm.register("grad", grad)
+        rs = torch.empty(n // world, device=dev, dtype=torch.float32)
+        comm.reduce_scatter_direct(rs, "grad", n * 4, n * 4)        # second half of grad
+        full = torch.arange(2 * n, device=dev, dtype=torch.float32).remainder(5)[n:] * world \
+            + world * (world - 1) / 2
+        out["rs_direct"] = float((rs - full[rank * (n // world):(rank + 1) * (n // world)]).abs().max())
+        m = 4096
+        pshard = torch.arange(3 * m, device=dev, dtype=torch.float32).add(1000 * rank).to(torch.bfloat16)
+        comm.register("pshard", pshard)
+        ag = torch.empty(m * world, device=dev, dtype=torch.bfloat16)
+        comm.all_gather_direct(ag, "pshard", m * 2)                 # every rank's [m, 2m)
+        exp = torch.cat([torch.arange(m, 2 * m, device=dev, dtype=torch.float32).add(1000 * r) for r in range(world)])
+        out["ag_direct"] = float((ag.float() - exp.to(torch.bfloat16).float()).abs().max())
+
+        # validation mode (§5.2): clean calls pass the cross-rank checks ...
+        comm.validate = True
+        t = torch.arange(4096, device=dev, dtype=torch.float32).remainder(3).add(rank)
+        comm.all_reduce_(t)
+        comm.reduce_scatter_direct(rs, "grad", 0, n * 4)
+        comm.all_gather_direct(ag, "pshard", 0)
+        out["validate_clean"] = 0.0
+        # ... and ranks in different collectives (same size, different op) are caught
+        x = torch.ones(4096, device=dev, dtype=torch.float32)
+        try:
+            if rank == 0:
+                comm.all_reduce_(x)
+            else:
+                comm.all_gather(x, x[: 4096 // world].clone())
+            out["validate_mismatch"] = 1.0
+        except RuntimeError as e:
+            out["validate_mismatch"] = 0.0 if "validation failed" in str(e) else 1.0
         comm.close()
         dist.barrier()
         dist.destroy_process_group()
@@ -121,5 +159,5 @@ def test_xgmi_collectives_multi_process(world):
     for rank, out, err in res:
         assert err is None, (rank, err)
         for k, v in out.items():
-            tol = 0.0 if "float32" in k or k == "graph" else 1.0  # bf16 keeps 8 bits
+            tol = 1.0 if "bfloat16" in k else 0.0  # bf16 sums keep 8 bits
             assert v <= tol, (rank, k, v)
