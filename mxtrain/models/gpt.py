@@ -288,6 +288,12 @@ class StepRuntime:
     ep_group: Optional[object] = None
     aux_scale: float = 0.0        # d(total loss)/d(l_aux of one layer) = coeff / micro-batches
     aux_log: Optional[List] = None
+    # TP communication overlap (MXTRAIN_TP_OVERLAP, default on): the row-parallel dgrad's
+    # all-reduce / reduce-scatter runs asynchronously while the layer's weight-gradient
+    # GEMMs run; under SP the all-gather feeding a column-parallel GEMM overlaps the GEMM
+    # of this rank's own token chunk (the other chunks' GEMMs follow the gather)
+    tp_overlap: bool = True
+    sp_gemm_overlap: bool = True
 
     @property
     def p_drop(self):
@@ -369,6 +375,50 @@ def _reduce(x, rt):
     if rt.sp:
         return C.reduce_scatter_dim0(x, rt.tp_group)
     return C.all_reduce_(x, rt.tp_group)
+
+
+def _reduce_start(x, rt):
+    """Start the row-parallel combine of ``x`` (a dgrad partial sum); ``.wait()`` gives the
+    result.  Synchronous (done on return) unless ``rt.tp_overlap``."""
+    if rt.tp == 1:
+        return C.Pending(x)
+    if not rt.tp_overlap:
+        return C.Pending(_reduce(x, rt))
+    if rt.sp:
+        return C.reduce_scatter_dim0_async(x, rt.tp_group)
+    return C.all_reduce_async(x, rt.tp_group)
+
+
+def _mm_into(out, a, w, trans, bias=None):
+    b = w.t() if trans else w
+    if bias is None:
+        torch.mm(a, b, out=out)
+    else:
+        torch.addmm(bias, a, b, out=out)
+
+
+def _gather_mm(x, w, rt, trans=True, bias=None):
+    """(x_full, x_full @ W^T [+ bias]) (``trans=False``: @ W) for a column-parallel GEMM
+    whose input is sequence-parallel: with ``rt.sp_gemm_overlap`` the token-chunk GEMM of
+    this rank runs while the all-gather brings the other chunks, then the rest."""
+    if not rt.sp:
+        y = torch.addmm(bias, x, w.t() if trans else w) if bias is not None else torch.mm(x, w.t() if trans else w)
+        return x, y
+    if not rt.sp_gemm_overlap:
+        x_full = _gather(x, rt)
+        y = torch.addmm(bias, x_full, w.t() if trans else w) if bias is not None \
+            else torch.mm(x_full, w.t() if trans else w)
+        return x_full, y
+    pend = C.all_gather_dim0_async(x, rt.tp_group)
+    c, r, n = x.shape[0], rt.tp_rank, rt.tp
+    y = torch.empty((c * n, w.shape[0] if trans else w.shape[1]), dtype=x.dtype, device=x.device)
+    _mm_into(y[r * c:(r + 1) * c], x, w, trans, bias)
+    x_full = pend.wait()
+    if r > 0:
+        _mm_into(y[:r * c], x_full[:r * c], w, trans, bias)
+    if r < n - 1:
+        _mm_into(y[(r + 1) * c:], x_full[(r + 1) * c:], w, trans, bias)
+    return x_full, y
 
 
 def _wgrad(gbuf, dy, x):
@@ -468,7 +518,6 @@ class GPTLayerFn(torch.autograd.Function):
         hl = cfg.num_attention_heads // rt.tp
         kvl = cfg.num_kv_heads // rt.tp
         eps = cfg.layernorm_epsilon
-        a_full = _gather(a, rt)
         dmask = None
         if rt.p_attn > 0:
             # the keep-mask depends only on the seed: generated on the side stream while the
@@ -479,7 +528,7 @@ class GPTLayerFn(torch.autograd.Function):
                                       salt=SALT_ATTN + i, head_offset=rt.tp_rank * hl + rt.cp_rank * ha_,
                                       total_heads=cfg.num_attention_heads, causal=True, device=a.device,
                                       stream=rt.aux_stream)
-        qkv = torch.addmm(P[p + "qkv_b"], a_full, P[p + "qkv_w"].t())
+        a_full, qkv = _gather_mm(a, P[p + "qkv_w"], rt, bias=P[p + "qkv_b"])
         if rt.cp > 1:   # Ulysses: whole sequences, 1/cp of the heads
             qkv_a = seq_to_head(qkv, (hl * D, kvl * D, kvl * D), rt.B, rt.S, rt.cp_group)
             ha, kva = hl // rt.cp, kvl // rt.cp
@@ -496,9 +545,9 @@ class GPTLayerFn(torch.autograd.Function):
         w2, b2 = rt.norm_params(p + "ln2")
         h1, m, mean2, rstd2 = bda_norm_fwd(o, P[p + "proj_b"], h, w2, b2, eps, rt.p_drop, rt.seed_t,
                                            rt.salt(1000 + 2 * i), rt.rms)
-        m_full = _gather(m, rt)
         moe = None
         if is_moe_layer(cfg, i):
+            m_full = _gather(m, rt)
             # MoE MLP under autograd: the inner graph is kept for backward (models/moe.py)
             e = p + "experts."
             leaves = [P[p + "router_w"]] + [rt.eparams[e + n] for n in ("fc1_w", "fc1_b", "fc2_w", "fc2_b")]
@@ -513,7 +562,7 @@ class GPTLayerFn(torch.autograd.Function):
             pre = f = None
             b_fc2 = None
         else:
-            pre = torch.mm(m_full, P[p + "fc1_w"].t())
+            m_full, pre = _gather_mm(m, P[p + "fc1_w"], rt)
             if cfg.swiglu:
                 f = bias_swiglu_fwd(pre, P[p + "fc1_b"])
             else:
@@ -576,16 +625,17 @@ class GPTLayerFn(torch.autograd.Function):
                 gbuf.add_(gr.to(gbuf.dtype))
             dm = grads[0].to(dg.dtype)
             return GPTLayerFn._attn_backward(ctx, dm, dh1, a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2)
-        dg_full = _gather(dg, rt)
-        df = torch.mm(dg_full, P[p + "fc2_w"])
+        dg_full, df = _gather_mm(dg, P[p + "fc2_w"], rt, trans=False)
         if cfg.swiglu:
             dpre = bias_swiglu_bwd(df, pre, P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True)
         else:
             dpre = bias_gelu_bwd(df, pre, P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True,
                                  inplace=True)
-        # fc2 and fc1 weight gradients in one grouped launch (both operands read in place)
+        # dgrad first: its TP combine overlaps the fc2 + fc1 weight-gradient GEMMs (one
+        # grouped launch, both operands read in place)
+        pend = _reduce_start(torch.mm(dpre, P[p + "fc1_w"]), rt)
         rt.wgrad((G[p + "fc2_w"], dg_full, f), (G[p + "fc1_w"], dpre, m_full))
-        dm = _reduce(torch.mm(dpre, P[p + "fc1_w"]), rt)
+        dm = pend.wait()
         return GPTLayerFn._attn_backward(ctx, dm, dh1, a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2)
 
     @staticmethod
@@ -604,8 +654,7 @@ class GPTLayerFn(torch.autograd.Function):
                            seed_t=rt.seed_t, salt=rt.salt(1000 + 2 * i), rms=rt.rms, dgamma=gw2,
                            dbeta=gb2, dbias=G[p + "proj_b"], accumulate=True)
         # ---- attention backward
-        do_full = _gather(do_, rt)
-        dctx = torch.mm(do_full, P[p + "proj_w"])
+        do_full, dctx = _gather_mm(do_, P[p + "proj_w"], rt, trans=False)
         if rt.cp > 1:
             dctx = seq_to_head(dctx, (hl * D,), rt.B, rt.S, rt.cp_group)
             ha, kva = hl // rt.cp, kvl // rt.cp
@@ -622,9 +671,10 @@ class GPTLayerFn(torch.autograd.Function):
         rt.rope_(dqkv, ha, kva, inverse=True)
         if rt.cp > 1:
             dqkv = head_to_seq(dqkv, (hl * D, kvl * D, kvl * D), rt.B, rt.S, rt.cp_group)
+        pend = _reduce_start(torch.mm(dqkv, P[p + "qkv_w"]), rt)
         colsum(dqkv, G[p + "qkv_b"], accumulate=True)
         rt.wgrad((G[p + "proj_w"], do_full, ctx_), (G[p + "qkv_w"], dqkv, a_full))
-        da = _reduce(torch.mm(dqkv, P[p + "qkv_w"]), rt)
+        da = pend.wait()
         rt.done(i + 1)
         return dh, da, None, None, None
 
@@ -636,8 +686,7 @@ class LMHeadLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, labels, rt: StepRuntime, wname: str):
         W = rt.params[wname]
-        x_full = _gather(x, rt)
-        logits = torch.mm(x_full, W.t())
+        x_full, logits = _gather_mm(x, W, rt)
         losses = cross_entropy_fwd_bwd(logits, labels, rt.grad_scale,
                                        tp_group=rt.tp_group if rt.tp > 1 else None,
                                        vocab_start=rt.vocab_start)
@@ -652,9 +701,9 @@ class LMHeadLossFn(torch.autograd.Function):
         ctx.saved = None
         W = rt.params[ctx.wname]
         gv = g.reshape(1).to(x_full.dtype)
+        pend = _reduce_start(torch.mm(dlogits, W) * gv, rt)
         wgrad_group([(rt.grads[ctx.wname], dlogits, x_full * gv)], accumulate=not rt.wgrad_overwrite)
-        dx = torch.mm(dlogits, W) * gv
-        dx = _reduce(dx, rt)
+        dx = pend.wait()
         return dx, None, None, None
 
 
@@ -674,6 +723,8 @@ class GPTStage:
                               vocab_start=tp_rank * V, cp=cp, cp_rank=cp_rank, cp_group=cp_group,
                               eparams=eparams, egrads=egrads, ep_group=ep_group,
                               attn_seed_t=attn_seed_t)
+        ov = os.environ.get("MXTRAIN_TP_OVERLAP", "1") == "1"
+        self.rt.tp_overlap = self.rt.sp_gemm_overlap = ov
         dev = next(iter(params.values())).device if params else None
         if dev is not None and dev.type == "cuda" and os.environ.get("MXTRAIN_AUX_STREAM", "0") == "1":
             self.rt.aux_stream = torch.cuda.Stream(device=dev)

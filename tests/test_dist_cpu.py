@@ -67,6 +67,8 @@ def _worker(rank, world, port, mode, q):
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     torch.manual_seed(0)
     ccfg = _cfg(mode)
+    if mode.endswith(":sync"):
+        os.environ["MXTRAIN_TP_OVERLAP"] = "0"   # collectives complete before the next GEMM
     mode = mode.split(":")[0]
     from mxtrain.models.gpt import GPTConfig, shard_gpt_state
     from mxtrain.parallel import state as pstate
@@ -251,6 +253,18 @@ def test_attention_dropout_sharded_matches_single(mode):
     """Attention dropout 0.1 under TP2 (heads split) and Ulysses CP2 (head groups after the
     all-to-all): the shards draw the single-process keep-mask, so losses and updates match."""
     _check(mode, _make_reference(CFG_ADROP), loss_ranks=(0, 1))
+
+
+@pytest.mark.parametrize("mode", ["tp", "sp"])
+def test_tp_comm_overlap_bit_identical(mode):
+    """TP communication overlap (async dgrad all-reduce / reduce-scatter across the
+    weight-gradient GEMMs; under SP the all-gather overlapping the own-chunk GEMM) gives
+    bit-identical losses and parameters to the synchronous path."""
+    a, b = _run(mode), _run(mode + ":sync")
+    for (ra, _, la, pa, _), (rb, _, lb, pb, _) in zip(a, b):
+        assert ra == rb and la == lb, (mode, la, lb)
+        for n in pa:
+            assert torch.equal(pa[n], pb[n]), (mode, ra, n, (pa[n] - pb[n]).abs().max())
 
 
 def test_pp2_1f1b_matches_single(reference):
