@@ -21,6 +21,21 @@ if TYPE_CHECKING:  # pragma: no cover
     from ..training import GPTTrainer
 
 
+class _P2P:
+    """Posted batch of p2p ops: ``wait()`` completes them and returns the received
+    tensor (None for send-only batches); the send tensor is kept alive until then."""
+    __slots__ = ("reqs", "rbuf", "keep")
+
+    def __init__(self, reqs, rbuf, keep):
+        self.reqs, self.rbuf, self.keep = reqs, rbuf, keep
+
+    def wait(self):
+        for r in self.reqs:
+            r.wait()
+        self.reqs, self.keep = [], None
+        return self.rbuf
+
+
 class PipelineSchedule:
     def __init__(self, trainer: "GPTTrainer"):
         self.tr = trainer
@@ -34,23 +49,32 @@ class PipelineSchedule:
         return (tokens, self.tr.cfg.hidden_size)
 
     # ---------------------------------------------------------------- p2p primitives
-    # Opposite-direction transfers between a pair of stages are always posted together in
-    # one batch_isend_irecv, so blocking p2p can never deadlock in the steady state.
+    # Every transfer is posted without waiting; the consumer waits right before it uses
+    # the tensor (a stream dependency under RCCL, not a host block), and sends are only
+    # waited for at the end of the schedule (their tensors stay referenced until then).
+    # Receives are posted as early as the schedule allows -- the next forward's input
+    # before this step's backward, the next backward's gradient before this backward --
+    # so the transfer runs under compute.  Opposite-direction transfers that are needed
+    # together (send activation / receive its gradient) are posted in one
+    # batch_isend_irecv so the pair can never deadlock.
     def _buf(self, shape):
         return torch.empty(shape, dtype=self.tr.dtype, device=self.tr.device)
 
-    def _exchange(self, send_t=None, send_to=None, recv_shape=None, recv_from=None):
+    def _post(self, send_t=None, send_to=None, recv_shape=None, recv_from=None):
         ops = []
         rbuf = None
         if send_t is not None:
-            ops.append(dist.P2POp(dist.isend, send_t.contiguous(), send_to))
+            send_t = send_t.contiguous()
+            ops.append(dist.P2POp(dist.isend, send_t, send_to))
         if recv_shape is not None:
             rbuf = self._buf(recv_shape)
             ops.append(dist.P2POp(dist.irecv, rbuf, recv_from))
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
-        return rbuf
+        reqs = dist.batch_isend_irecv(ops) if ops else []
+        return _P2P(reqs, rbuf, send_t)
+
+    def _exchange(self, send_t=None, send_to=None, recv_shape=None, recv_from=None):
+        """Blocking form (evaluation path): post and wait."""
+        return self._post(send_t, send_to, recv_shape, recv_from).wait()
 
     def run(self, tokens: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         tr, ps = self.tr, self.ps
@@ -64,6 +88,7 @@ class PipelineSchedule:
         remaining = nm - warm
         loss_total = torch.zeros((), dtype=torch.float32, device=tr.device)
         inflight = deque()
+        sends = []          # posted sends, waited for at the end
         fwd_i = 0
         bwd_i = 0
 
@@ -91,40 +116,47 @@ class PipelineSchedule:
                 torch.autograd.backward(out, grad_tensors=out_grad)
             return None if first else inp.grad
 
-        def recv_forward():
-            if first:
-                return None
-            return self._exchange(recv_shape=shape, recv_from=prev).requires_grad_(True)
+        def post_recv_fwd():
+            return None if first else self._post(recv_shape=shape, recv_from=prev)
 
-        # warm-up forwards
-        for _ in range(warm):
-            out = fwd(recv_forward())
+        def take(pend, grad=False):
+            if pend is None:
+                return None
+            t = pend.wait()
+            return t.requires_grad_(True) if grad else t
+
+        # warm-up forwards (the next input is prefetched while this forward runs)
+        nin = post_recv_fwd() if (warm > 0 or remaining > 0) else None
+        for k in range(warm):
+            inp = take(nin, grad=True)
+            nin = post_recv_fwd() if (k + 1 < warm or remaining > 0) else None
+            out = fwd(inp)
             if not last:
-                self._exchange(send_t=out.detach(), send_to=nxt)
+                sends.append(self._post(send_t=out.detach(), send_to=nxt))
         # steady state: 1F1B
-        inp = recv_forward() if remaining > 0 else None
+        inp = take(nin, grad=True) if remaining > 0 else None
+        nin = None
         for i in range(remaining):
             out = fwd(inp)
             out_grad = None
             if not last:
-                out_grad = self._exchange(send_t=out.detach(), send_to=nxt, recv_shape=shape,
-                                          recv_from=nxt)
-            in_grad = bwd(out_grad)
-            if i == remaining - 1:
-                if not first:
-                    self._exchange(send_t=in_grad, send_to=prev)
-            else:
-                if first:
-                    inp = None
-                else:
-                    inp = self._exchange(send_t=in_grad, send_to=prev, recv_shape=shape,
-                                         recv_from=prev).requires_grad_(True)
-        # cool-down backwards
-        for _ in range(warm):
-            out_grad = None if last else self._exchange(recv_shape=shape, recv_from=nxt)
+                out_grad = self._post(send_t=out.detach(), send_to=nxt, recv_shape=shape, recv_from=nxt).wait()
+            # prefetch the next forward's input before running this backward
+            nin = post_recv_fwd() if i < remaining - 1 else None
             in_grad = bwd(out_grad)
             if not first:
-                self._exchange(send_t=in_grad, send_to=prev)
+                sends.append(self._post(send_t=in_grad, send_to=prev))
+            inp = take(nin, grad=True) if i < remaining - 1 else None
+        # cool-down backwards (the next gradient is prefetched while this backward runs)
+        ng = None if (last or warm == 0) else self._post(recv_shape=shape, recv_from=nxt)
+        for k in range(warm):
+            out_grad = take(ng)
+            ng = None if (last or k + 1 >= warm) else self._post(recv_shape=shape, recv_from=nxt)
+            in_grad = bwd(out_grad)
+            if not first:
+                sends.append(self._post(send_t=in_grad, send_to=prev))
+        for sd in sends:
+            sd.wait()
         return loss_total
 
     @torch.no_grad()

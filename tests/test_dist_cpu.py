@@ -67,6 +67,7 @@ def _worker(rank, world, port, mode, q):
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     torch.manual_seed(0)
     ccfg = _cfg(mode)
+    full_mode = mode
     if mode.endswith(":sync"):
         os.environ["MXTRAIN_TP_OVERLAP"] = "0"   # collectives complete before the next GEMM
     mode = mode.split(":")[0]
@@ -81,7 +82,8 @@ def _worker(rank, world, port, mode, q):
     cfg = GPTConfig(**ccfg)
     # reference init (identical on every rank), then take this rank's shard
     _, _, init_sd = _ref_init(ccfg)
-    tcfg = TrainConfig(micro_batch_size=2, global_batch_size=4, lr=1e-3, overlap_grad_reduce=False)
+    mb1 = ":mb1" in full_mode   # 4 micro-batches of 1 sequence: deeper 1F1B steady state
+    tcfg = TrainConfig(micro_batch_size=1 if mb1 else 2, global_batch_size=4, lr=1e-3, overlap_grad_reduce=False)
     tr = GPTTrainer(cfg, tcfg, ps, dtype=torch.float32)
     if ps.dp > 1:
         # exercise the deferred (next-step, per-bucket) ZeRO-1 parameter all-gather path
@@ -95,6 +97,8 @@ def _worker(rank, world, port, mode, q):
     tok, lab = _data()
     if ps.dp > 1:
         tok, lab = tok[ps.dp_rank:ps.dp_rank + 1], lab[ps.dp_rank:ps.dp_rank + 1]
+    if mb1:
+        tok, lab = tok.reshape(-1, 1, tok.shape[-1]), lab.reshape(-1, 1, lab.shape[-1])
     losses = [float(tr.train_step(tok, lab)) for _ in range(2)]
     tr.sync_params()
     # numpy copies: tensors sent through a spawn queue are fd-shared and vanish with the
@@ -269,6 +273,11 @@ def test_tp_comm_overlap_bit_identical(mode):
 
 def test_pp2_1f1b_matches_single(reference):
     _check("pp", reference, loss_ranks=(1,))
+
+
+def test_pp2_1f1b_four_microbatches_matches_single(reference):
+    """Non-blocking p2p with prefetched receives over a longer 1F1B steady state."""
+    _check("pp:mb1", reference, loss_ranks=(1,))
 
 
 @pytest.mark.parametrize("mode", ["3d", "3dsp"])
