@@ -247,7 +247,8 @@ def main():
                 "data": "synthetic COCO-shaped 800x<=1333, random-init weights",
                 "1img": {k: v for k, v in m1.items() if k != "img_s"},
                 "4img": {k: v for k, v in m4.items() if k != "img_s"},
-                "unit": "images/s", "conv_search": "MIOpen find (in-repo find-db)"}
+                "unit": "images/s", "conv_search": "MIOpen find (in-repo find-db)",
+                "step": "whole-step hipGraph replay (1 GPU)"}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

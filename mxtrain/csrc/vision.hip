@@ -224,6 +224,210 @@ __global__ __launch_bounds__(256) void roi_align_bwd_kernel(Levels L, const floa
   }
 }
 
+// ------------------------------------------------------------ RoIAlign backward, tiled
+// Atomics-free (for the gradient values) RoIAlign backward, SURVEY K13.  The gradient of
+// every level is cut into 8 x 8-pixel tiles; each (roi, bin) "item" touches a few tiles
+// (its sr x sr samples' bilinear corners, <= 4 rows x 4 columns of pixels).  A counting
+// sort buckets the items per tile (integer atomics on the bucket counters only), then ONE
+// workgroup per tile accumulates its items into an fp32 LDS tile [64 px][C] -- wave w
+// owns channels [64w, 64w + 64), lane = channel, so every LDS update is a plain
+// read-modify-write by the owning lane, no LDS or global float atomics -- in ascending
+// item order (bitonic-sorted in LDS), which makes the result deterministic, and writes
+// the tile straight to the bf16 NHWC gradient.  Every pixel of every level is written
+// exactly once (empty tiles write zeros): no fp32 gradient buffer, no zero-fill, no cast.
+constexpr int kTile = 8;
+constexpr int kSortCap = 2048;
+constexpr int kMaxTileC = 256;   // 64 px x 256 ch fp32 = 64 KB + 8 KB keys of the 160 KB LDS
+
+struct GOut {
+  uint16_t* p[4];   // bf16 NHWC gradient per level
+};
+
+struct TileGeo {
+  int base[5];   // first tile id of each level (base[n] = total tiles)
+  int th[4];     // tiles per column / row of a level image
+  int tw[4];
+  int B;
+};
+
+struct Foot {
+  int ry[4], rx[4];
+  float wy[4], wx[4];   // per-axis weights, 0 = unused; duplicate rows/columns merged
+  int lv, b;
+};
+
+// the sr <= 2 separable footprint of item (roi, bin) (same arithmetic as roi_align_bwd_kernel)
+__device__ __forceinline__ Foot footprint(const Levels& L, const float* __restrict__ rois, int item, int PH,
+                                          int PW, int sr, int aligned) {
+  Foot f;
+  const int bin = item % (PH * PW);
+  const int r = item / (PH * PW);
+  const float* rr = rois + (size_t)r * 5;
+  f.b = (int)rr[0];
+  f.lv = roi_level(L, rr[1], rr[2], rr[3], rr[4]);
+  const float s = L.scale[f.lv];
+  const float off = aligned ? 0.5f : 0.f;
+  const float x0 = rr[1] * s - off, y0 = rr[2] * s - off;
+  float rw = rr[3] * s - off - x0, rh = rr[4] * s - off - y0;
+  if (!aligned) { rw = fmaxf(rw, 1.f); rh = fmaxf(rh, 1.f); }
+  const float bw = rw / PW, bh = rh / PH;
+  const int ph = bin / PW, pw = bin % PW;
+  const int H = L.H[f.lv], W = L.W[f.lv];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const bool use = i < sr;
+    const Axis a = axis_weights(y0 + ph * bh + (i + 0.5f) * bh / sr, H);
+    const Axis c = axis_weights(x0 + pw * bw + (i + 0.5f) * bw / sr, W);
+    f.ry[2 * i] = a.lo; f.ry[2 * i + 1] = a.hi;
+    f.wy[2 * i] = use && a.valid ? a.wlo : 0.f; f.wy[2 * i + 1] = use && a.valid ? a.whi : 0.f;
+    f.rx[2 * i] = c.lo; f.rx[2 * i + 1] = c.hi;
+    f.wx[2 * i] = use && c.valid ? c.wlo : 0.f; f.wx[2 * i + 1] = use && c.valid ? c.whi : 0.f;
+  }
+#pragma unroll
+  for (int j = 1; j < 4; ++j) {
+    bool fy = false, fx = false;
+#pragma unroll
+    for (int i = 0; i < j; ++i) {
+      if (!fy && f.ry[i] == f.ry[j]) { f.wy[i] += f.wy[j]; fy = true; }
+      if (!fx && f.rx[i] == f.rx[j]) { f.wx[i] += f.wx[j]; fx = true; }
+    }
+    if (fy) f.wy[j] = 0.f;
+    if (fx) f.wx[j] = 0.f;
+  }
+  return f;
+}
+
+// distinct tile coordinates of the used rows (or columns); returns how many
+__device__ __forceinline__ int distinct_tiles(const int* idx, const float* w, int* out) {
+  int n = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (w[i] == 0.f) continue;
+    const int t = idx[i] / kTile;
+    bool seen = false;
+    for (int k = 0; k < n; ++k) seen |= out[k] == t;
+    if (!seen) out[n++] = t;
+  }
+  return n;
+}
+
+// kCount: counts[tile]++ per touched tile; else entries[cursor[tile]++] = item
+template <bool kCount>
+__global__ __launch_bounds__(256) void roi_tiles_kernel(Levels L, TileGeo G, const float* __restrict__ rois,
+                                                        int items, int PH, int PW, int sr, int aligned,
+                                                        int* __restrict__ counter, int* __restrict__ entries) {
+  const int item = blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= items) return;
+  const Foot f = footprint(L, rois, item, PH, PW, sr, aligned);
+  if (f.b < 0 || f.b >= G.B) return;   // malformed batch index: never index outside the tiles
+  int ty[4], tx[4];
+  const int ny = distinct_tiles(f.ry, f.wy, ty), nx = distinct_tiles(f.rx, f.wx, tx);
+  for (int i = 0; i < ny; ++i)
+    for (int j = 0; j < nx; ++j) {
+      const int t = G.base[f.lv] + (f.b * G.th[f.lv] + ty[i]) * G.tw[f.lv] + tx[j];
+      if (kCount) {
+        atomicAdd(counter + t, 1);
+      } else {
+        entries[atomicAdd(counter + t, 1)] = item;
+      }
+    }
+}
+
+// exclusive scan of counts[T] -> offsets[T + 1] and cursor[T] (one workgroup)
+__global__ __launch_bounds__(1024) void tile_scan_kernel(const int* __restrict__ counts, int T,
+                                                         int* __restrict__ offsets, int* __restrict__ cursor) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int per = (T + 1023) / 1024;
+  const int lo = min(t * per, T), hi = min(lo + per, T);
+  int sum = 0;
+  for (int i = lo; i < hi; ++i) sum += counts[i];
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {   // Hillis-Steele inclusive scan of the partials
+    const int v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - sum;
+  for (int i = lo; i < hi; ++i) {
+    offsets[i] = run;
+    cursor[i] = run;
+    run += counts[i];
+  }
+  if (t == 1023) offsets[T] = part[1023];
+}
+
+// one workgroup (C threads = C / 64 waves) per tile
+__global__ __launch_bounds__(256) void roi_align_bwd_tile_kernel(Levels L, TileGeo G, const float* __restrict__ rois,
+                                                                 int C, int PH, int PW, int sr, int aligned,
+                                                                 const uint16_t* __restrict__ dout,
+                                                                 const int* __restrict__ offsets,
+                                                                 const int* __restrict__ entries, GOut gout) {
+  __shared__ __attribute__((aligned(16))) float acc[kTile * kTile * kMaxTileC];   // [64 px][C]
+  __shared__ int keys[kSortCap];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int tile = blockIdx.x;
+  int lv = 0;
+  while (lv + 1 < L.n && tile >= G.base[lv + 1]) ++lv;
+  const int local = tile - G.base[lv];
+  const int tx = local % G.tw[lv], ty = (local / G.tw[lv]) % G.th[lv], b = local / (G.tw[lv] * G.th[lv]);
+  const int H = L.H[lv], W = L.W[lv];
+  const int y0 = ty * kTile, x0 = tx * kTile;
+  for (int i = tid * 4; i < kTile * kTile * C; i += nt * 4)
+    *reinterpret_cast<float4*>(acc + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int beg = offsets[tile], n = offsets[tile + 1] - beg;
+  const bool sorted = n > 1 && n <= kSortCap;
+  if (sorted) {   // bitonic sort of the item ids (padded to a power of two)
+    int np = 1;
+    while (np < n) np <<= 1;
+    for (int i = tid; i < np; i += nt) keys[i] = i < n ? entries[beg + i] : 0x7fffffff;
+    __syncthreads();
+    for (int k = 2; k <= np; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < np; i += nt) {
+          const int p = i ^ j;
+          if (p > i) {
+            const int a = keys[i], c = keys[p];
+            if ((a > c) == ((i & k) == 0)) { keys[i] = c; keys[p] = a; }
+          }
+        }
+        __syncthreads();
+      }
+  }
+  __syncthreads();
+  const int c = tid;   // this thread's channel (blockDim == C)
+  const float inv = 1.f / (float)(sr * sr);
+  for (int e = 0; e < n; ++e) {
+    const int item = sorted ? keys[e] : entries[beg + e];
+    const Foot f = footprint(L, rois, item, PH, PW, sr, aligned);
+    const float go = bf2f(dout[(size_t)item * C + c]) * inv;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int yy = f.ry[i] - y0;
+      if (f.wy[i] == 0.f || yy < 0 || yy >= kTile) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int xx = f.rx[j] - x0;
+        if (f.wx[j] == 0.f || xx < 0 || xx >= kTile) continue;
+        float* a = acc + (yy * kTile + xx) * C + c;
+        *a += f.wy[i] * f.wx[j] * go;
+      }
+    }
+  }
+  __syncthreads();
+  uint16_t* g = gout.p[lv];
+  const int c8 = C / 8;
+  for (int q = tid; q < kTile * kTile * c8; q += nt) {
+    const int p = q / c8, ch = (q % c8) * 8;
+    const int y = y0 + p / kTile, x = x0 + p % kTile;
+    if (y >= H || x >= W) continue;
+    const float* a = acc + p * C + ch;
+    *reinterpret_cast<uint4*>(g + (((size_t)b * H + y) * W + x) * C + ch) = pack8(a);
+  }
+}
+
 // ------------------------------------------------------------------------------ NMS
 __device__ __forceinline__ float iou4(const float4 a, const float4 b) {
   const float iw = fminf(a.z, b.z) - fmaxf(a.x, b.x);
@@ -494,6 +698,55 @@ MX_EXPORT int mx_roi_align_bwd(float* const* grads, const int* H, const int* W, 
   const long waves = (long)R * PH * PW;
   hipLaunchKernelGGL(roi_align_bwd_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, L, rois, R, C, PH,
                      PW, sampling, aligned, (const uint16_t*)dout);
+  return hipGetLastError();
+}
+
+// Tiled, float-atomics-free backward (sr <= 2, C % 64 == 0, C <= 256) writing bf16 NHWC
+// gradients directly.  ws: int32 workspace of 3 T + 1 + R * PH * PW * 16 entries (T = tiles
+// of all levels: sum over levels of B * ceil(H / 8) * ceil(W / 8)).
+static TileGeo tile_geo(const int* H, const int* W, int n, int B) {
+  TileGeo G = {};
+  G.B = B;
+  int base = 0;
+  for (int i = 0; i < n; ++i) {
+    G.base[i] = base;
+    G.th[i] = (H[i] + kTile - 1) / kTile;
+    G.tw[i] = (W[i] + kTile - 1) / kTile;
+    base += B * G.th[i] * G.tw[i];
+  }
+  for (int i = n; i < 5; ++i) G.base[i] = base;
+  return G;
+}
+
+MX_EXPORT int mx_roi_align_bwd_tiled(void* const* grads, const int* H, const int* W, const float* scales, int n,
+                                     int lvl_min, float canon, int canon_lvl, int B, const float* rois, int R, int C,
+                                     int PH, int PW, int sampling, int aligned, const void* dout, int* ws,
+                                     hipStream_t s) {
+  if (n < 1 || n > 4 || (C & 63) || C > kMaxTileC || sampling < 1 || sampling > 2 || B < 1)
+    return hipErrorInvalidValue;
+  Levels L = make_levels(nullptr, nullptr, H, W, scales, n, lvl_min, canon, canon_lvl);
+  const TileGeo G = tile_geo(H, W, n, B);
+  const int T = G.base[n];
+  const int items = R * PH * PW;
+  int* counts = ws;
+  int* offsets = ws + T;
+  int* cursor = offsets + T + 1;
+  int* entries = cursor + T;
+  hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * (size_t)T, s);
+  if (e != hipSuccess) return e;
+  if (items > 0) {
+    hipLaunchKernelGGL(roi_tiles_kernel<true>, dim3((items + 255) / 256), dim3(256), 0, s, L, G, rois, items, PH, PW,
+                       sampling, aligned, counts, (int*)nullptr);
+  }
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, counts, T, offsets, cursor);
+  if (items > 0) {
+    hipLaunchKernelGGL(roi_tiles_kernel<false>, dim3((items + 255) / 256), dim3(256), 0, s, L, G, rois, items, PH, PW,
+                       sampling, aligned, cursor, entries);
+  }
+  GOut go = {};
+  for (int i = 0; i < n; ++i) go.p[i] = (uint16_t*)grads[i];
+  hipLaunchKernelGGL(roi_align_bwd_tile_kernel, dim3(T), dim3(C), 0, s, L, G, rois, C, PH, PW, sampling, aligned,
+                     (const uint16_t*)dout, offsets, entries, go);
   return hipGetLastError();
 }
 

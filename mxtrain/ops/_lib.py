@@ -68,6 +68,7 @@ SIGNATURES = {
     # vision.hip
     "mx_roi_align_fwd": [P, P, P, P, I, I, F, I, P, I, I, I, I, I, I, P, P],
     "mx_roi_align_bwd": [P, P, P, P, I, I, F, I, P, I, I, I, I, I, I, P, P],
+    "mx_roi_align_bwd_tiled": [P, P, P, P, I, I, F, I, I, P, I, I, I, I, I, I, P, P, P],
     "mx_nms_workspace_words": [I],
     "mx_nms": [P, P, I, I, F, I, P, P, P, P],
     "mx_match": [P, I, I, P, P, I, I, P, P, P, P, P],

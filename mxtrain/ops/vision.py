@@ -7,6 +7,7 @@ Conventions: boxes are fp32 ``[x1, y1, x2, y2]`` in input-image pixels; RoIs are
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from typing import List, Optional, Sequence, Tuple
 
@@ -94,6 +95,11 @@ def _ptr_array(ts, ctype=ctypes.c_void_p):
     return arr
 
 
+# MXTRAIN_ROIALIGN_TILED=0: the fp32-atomic backward (roi_align_bwd_kernel) instead of the
+# tiled one (roi_align_bwd_tile_kernel)
+_TILED = os.environ.get("MXTRAIN_ROIALIGN_TILED", "1") == "1"
+
+
 class RoIAlignFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, rois, PH, PW, sr, aligned, lvl_min, canon, canon_lvl, scales, *feats):
@@ -117,12 +123,26 @@ class RoIAlignFn(torch.autograd.Function):
     def backward(ctx, dout):
         (rois,) = ctx.saved_tensors
         PH, PW, sr, aligned, lvl_min, canon, canon_lvl, scales = ctx.meta
-        grads = [torch.zeros(s, dtype=torch.float32, device=rois.device) for s in ctx.shapes]
         d = dout.contiguous().to(torch.bfloat16)
-        n = len(grads)
+        n = len(ctx.shapes)
+        C = ctx.shapes[0][-1]
         H = (ctypes.c_int * 4)(*[s[1] for s in ctx.shapes] + [0] * (4 - n))
         W = (ctypes.c_int * 4)(*[s[2] for s in ctx.shapes] + [0] * (4 - n))
         S = (ctypes.c_float * 4)(*list(scales) + [0.0] * (4 - n))
+        R = rois.shape[0]
+        if _TILED and sr <= 2 and C % 64 == 0 and C <= 256:
+            # tiled, deterministic, float-atomics-free kernel straight into bf16 gradients
+            B = ctx.shapes[0][0]
+            grads = [torch.empty(s, dtype=torch.bfloat16, device=rois.device) for s in ctx.shapes]
+            # workspace: tile counts, offsets (+1), cursors, and <= 16 tile entries per item
+            T = sum(B * (-(-s[1] // 8)) * (-(-s[2] // 8)) for s in ctx.shapes)
+            ws = torch.empty(3 * T + 1 + R * PH * PW * 16, dtype=torch.int32, device=rois.device)
+            _lib.call("mx_roi_align_bwd_tiled", ctypes.cast(_ptr_array(grads), ctypes.c_void_p),
+                      ctypes.cast(H, ctypes.c_void_p), ctypes.cast(W, ctypes.c_void_p),
+                      ctypes.cast(S, ctypes.c_void_p), n, lvl_min, float(canon), canon_lvl, B, _lib.ptr(rois), R, C,
+                      PH, PW, sr, int(aligned), _lib.ptr(d), _lib.ptr(ws), _lib.stream())
+            return (None,) * 9 + tuple(g if dt == torch.bfloat16 else g.to(dt) for g, dt in zip(grads, ctx.dtypes))
+        grads = [torch.zeros(s, dtype=torch.float32, device=rois.device) for s in ctx.shapes]
         _lib.call("mx_roi_align_bwd", ctypes.cast(_ptr_array(grads), ctypes.c_void_p),
                   ctypes.cast(H, ctypes.c_void_p), ctypes.cast(W, ctypes.c_void_p), ctypes.cast(S, ctypes.c_void_p),
                   n, lvl_min, float(canon), canon_lvl, _lib.ptr(rois), rois.shape[0], ctx.shapes[0][-1], PH, PW, sr,

@@ -195,7 +195,7 @@ def get_args(argv=None):
                    help="stop after N steps (bounded runs / benchmarks)")
     p.add_argument("--mx-warmup-steps", type=int, default=5, help="steps excluded from the images/s figure")
     p.add_argument("--mx-bench-json", default=None, help="append a JSON images/s record to this file")
-    p.add_argument("--mx-graph", choices=("auto", "0", "1"), default=os.environ.get("MXTRAIN_GRAPH", "0"),
+    p.add_argument("--mx-graph", choices=("auto", "0", "1"), default=os.environ.get("MXTRAIN_GRAPH", "auto"),
                    help="replay the whole training step as a hipGraph (auto: on for 1 GPU, off in debug mode)")
     return p.parse_args(argv)
 
@@ -203,12 +203,14 @@ def get_args(argv=None):
 def main(argv=None):
     args = get_args(argv)
     if args.mx_graph != "0":
-        # Whole-step hipGraph replay faults under the HIP runtime's graph packet-capture
-        # mode (kernel dispatch packets pre-built at instantiation) with MIOpen's assembly
-        # convolution kernels, and replays cleanly with it off (scripts/graph_diag.py, one
-        # MI355X, same inputs).  It is read when the HIP runtime initialises, so it is set
-        # before the first GPU call; the graph's kernels are then dispatched one by one by
-        # the runtime -- still no Python / ATen dispatch per op.
+        # Whole-step hipGraph replay with the convolution solvers MIOpen's find picks
+        # (the in-repo find-db) takes an illegal-address fault under the HIP runtime's graph
+        # packet-capture mode (dispatch packets pre-built at instantiation) and replays
+        # cleanly with it off; immediate-mode solvers replay cleanly either way (one
+        # MI355X, scripts/bench_maskrcnn.py --graph 1 and scripts/graph_diag.py, same
+        # inputs).  The flag is read when the HIP runtime initialises, so it is set before
+        # the first GPU call; the graph's kernels are then dispatched one by one by the
+        # runtime -- still no Python / ATen dispatch per op.
         os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
     from mxtrain.data.coco import AspectGroupedSampler, COCODetection, DetectionDataset, collate
     from mxtrain.models.maskrcnn import MaskRCNN

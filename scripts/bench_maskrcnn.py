@@ -23,8 +23,8 @@ def main():
     ap.add_argument("--data", default="/tmp/mx_coco_bench")
     ap.add_argument("--workers", type=int, default=6)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--graph", choices=("auto", "0", "1"), default="0",
-                    help="whole-step hipGraph replay (train.py --mx-graph)")
+    ap.add_argument("--graph", choices=("auto", "0", "1"), default="auto",
+                    help="whole-step hipGraph replay (train.py --mx-graph; auto = on for 1 GPU)")
     ap.add_argument("extra", nargs="*")
     a = ap.parse_args()
     rank = int(os.environ.get("RANK", os.environ.get("OMPI_COMM_WORLD_RANK", "0")))

@@ -1,5 +1,8 @@
-mkdir -p gpurun_out/c6
-DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 timeout -k 10 300 python -u scripts/bench_maskrcnn.py --batch 1 --graph 1 --out gpurun_out/c6/b1_graph_pc.jsonl > gpurun_out/c6/b1_graph_pc.log 2>&1 && \
-DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 timeout -k 10 300 python -u scripts/bench_maskrcnn.py --batch 4 --graph 1 --out gpurun_out/c6/b4_graph_pc.jsonl > gpurun_out/c6/b4_graph_pc.log 2>&1
-echo "rc=$?"
-cat gpurun_out/c6/*.jsonl
+mkdir -p gpurun_out/c8
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+for t in 1 0; do
+MXTRAIN_ROIALIGN_TILED=$t timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_t$t -o run -- python -u scripts/bench_maskrcnn.py --batch 4 --graph 0 --steps 20 --warmup 10 --out gpurun_out/c8/b4_t$t.jsonl > gpurun_out/c8/b4_t$t.log 2>&1 || exit 1
+db=$(find /tmp/prof_t$t -name "*.db" | head -1)
+python3 scripts/rocpd_stats.py "$db" --csv gpurun_out/c8/kstats_t$t.csv --top 50 > gpurun_out/c8/kstats_t$t.txt
+done
+cat gpurun_out/c8/*.jsonl

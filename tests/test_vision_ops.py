@@ -98,7 +98,12 @@ def test_decode_inverts_encode():
 
 
 @pytest.mark.gpu
-def test_roi_align_gpu_fwd_bwd():
+@pytest.mark.parametrize("tiled", [True, False])
+@pytest.mark.parametrize("out_hw", [7, 14])
+def test_roi_align_gpu_fwd_bwd(tiled, out_hw, monkeypatch):
+    """Forward and both backward kernels (tiled / fp32 atomics) vs the fp32 torch
+    reference; the tiled backward is also bitwise deterministic across runs."""
+    monkeypatch.setattr(V, "_TILED", tiled)
     g = torch.Generator().manual_seed(3)
     B, C = 2, 256
     shapes = [(200, 336), (100, 168), (50, 84), (25, 42)]
@@ -106,9 +111,9 @@ def test_roi_align_gpu_fwd_bwd():
     feats = [torch.randn(B, h, w, C, generator=g).bfloat16() for h, w in shapes]
     rois = _rand_rois(300, B, 800, 1344, g)
     ref_in = [f.float().requires_grad_(True) for f in feats]
-    ref = V._ref_roi_align(ref_in, scales, rois, 7, 7, 2, True, 2, 224.0, 4)
+    ref = V._ref_roi_align(ref_in, scales, rois, out_hw, out_hw, 2, True, 2, 224.0, 4)
     fg = [f.cuda().requires_grad_(True) for f in feats]
-    out = V.roi_align(fg, rois.cuda(), (7, 7), scales)
+    out = V.roi_align(fg, rois.cuda(), (out_hw, out_hw), scales)
     torch.testing.assert_close(out.float().cpu(), ref, rtol=2e-2, atol=2e-2)
     dout = torch.randn(ref.shape, generator=g)
     (ref * dout).sum().backward()
@@ -116,6 +121,13 @@ def test_roi_align_gpu_fwd_bwd():
     for a, b in zip(fg, ref_in):
         err = (a.grad.float().cpu() - b.grad).norm() / (b.grad.norm() + 1e-6)
         assert err < 2e-2, float(err)
+    if tiled:
+        first = [f.grad.clone() for f in fg]
+        for f in fg:
+            f.grad = None
+        out = V.roi_align(fg, rois.cuda(), (out_hw, out_hw), scales)
+        (out.float() * dout.cuda()).sum().backward()
+        assert all(torch.equal(a, f.grad) for a, f in zip(first, fg))
 
 
 @pytest.mark.gpu
