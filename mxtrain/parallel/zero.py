@@ -17,6 +17,7 @@ With dp == 1 the shard IS the flat buffer (no copies, no collectives).
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -129,6 +130,8 @@ class DistributedOptimizer:
         self.reset_pending()
         # xGMI registered-buffer mode (see _direct); names are local keys only
         self._direct_state: Optional[bool] = None
+        self.comm_timing = os.environ.get("MXTRAIN_COMM_TIMING", "0") == "1"
+        self._comm_events: List = []
         self._rg_grad, self._rg_pshard = f"zero{id(self)}.grad", f"zero{id(self)}.pshard"
         # ZeRO-1 parameter all-gather deferred to the start of the next step and overlapped
         # with its forward (bucket by bucket, in forward order); the layers wait on their
@@ -167,6 +170,29 @@ class DistributedOptimizer:
         self.units_left = {b: len(u) for b, u in self._bucket_units.items()}
         self.started = set()
 
+    # ------------------------------------------------------------------ comm timing
+    def _timed(self, fn):
+        """Run one DP collective; with comm timing on (MXTRAIN_COMM_TIMING=1 or
+        ``comm_timing = True``) bracket it with timing events on the stream it runs on.
+        Never inside a hipGraph capture (timing events are not capturable)."""
+        if not self.comm_timing or self.device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+            return fn()
+        s = torch.cuda.current_stream(self.device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        out = fn()
+        e1.record(s)
+        self._comm_events.append((e0, e1))
+        return out
+
+    def take_comm_ms(self) -> Optional[float]:
+        """Total GPU time of the DP collectives issued since the last call (ms; their
+        events must have completed -- call after a synchronize), or None when off."""
+        if not self.comm_timing:
+            return None
+        ev, self._comm_events = self._comm_events, []
+        return sum(a.elapsed_time(b) for a, b in ev)
+
     # ------------------------------------------------------------------ DP collectives
     def _direct(self, c) -> bool:
         """Register the flat gradient buffer and the parameter shard with the xGMI
@@ -188,6 +214,12 @@ class DistributedOptimizer:
         return self._direct_state
 
     def _rs(self, out, inp, bstart: Optional[int] = None):
+        return self._timed(lambda: self._rs_body(out, inp, bstart))
+
+    def _ag(self, out, inp, shard_off: Optional[int] = None):
+        return self._timed(lambda: self._ag_body(out, inp, shard_off))
+
+    def _rs_body(self, out, inp, bstart: Optional[int] = None):
         """Bucket gradient reduce-scatter: direct xGMI kernel when selected (reading the
         peers' registered gradient buckets in place), else RCCL."""
         nb = inp.numel() * inp.element_size()
@@ -200,7 +232,7 @@ class DistributedOptimizer:
         else:
             dist.reduce_scatter_tensor(out, inp, group=self.dp_group)
 
-    def _ag(self, out, inp, shard_off: Optional[int] = None):
+    def _ag_body(self, out, inp, shard_off: Optional[int] = None):
         """Parameter-shard all-gather: direct xGMI kernel when selected (every rank's new
         shard read in place from its registered param_shard), else RCCL."""
         c = _xgmi.route(self.dp_group, inp, "all_gather", out.numel() * out.element_size())

@@ -40,7 +40,7 @@ def main(argv=None):
     from mxtrain.data.gpt_dataset import DistributedSampleLoader, build_train_valid_test
     from mxtrain.models.gpt import GPTConfig
     from mxtrain.obs.fault import FaultInjector, Watchdog
-    from mxtrain.obs.metrics import MetricsWriter, hbm_stats, megatron_line
+    from mxtrain.obs.metrics import GPUSampler, MetricsWriter, drm_card_for_device, hbm_stats, megatron_line
     from mxtrain.parallel import state as pstate
     from mxtrain.training import GPTTrainer, TrainConfig
 
@@ -129,6 +129,10 @@ def main(argv=None):
     # ---------------------------------------------------------------- observability
     logs_dir = args.mx_metrics_dir or os.environ.get("LOGS_DIR") or os.path.join(os.environ.get("HOME", "."), "logs")
     metrics = MetricsWriter(logs_dir, ps.rank)
+    # power / clocks of this rank's GPU (sysfs, background thread) and the DP collectives'
+    # GPU time per step, reported per logging interval
+    sampler = GPUSampler(drm_card_for_device(ps.device) if use_cuda else None)
+    trainer.opt.comm_timing = trainer.opt.comm_timing or (use_cuda and ps.dp > 1 and not args.mx_graph)
     # effective settings + every deviation from the requested flags, once, in the JSONL
     metrics.write(step=trainer.iteration, event="config", effective=args.mx_effective,
                   deviations=args.mx_deviations)
@@ -182,10 +186,14 @@ def main(argv=None):
             tflops = toks * flops_tok / ps.world_size / 1e12
             print_rank_last(ps, megatron_line(it, args.train_iters, loader.consumed, dt * 1000, lr, gb, lv, gn,
                                               samples_per_sec=gb / dt, tflops=tflops, tokens_per_sec=toks))
+            comm_ms = trainer.opt.take_comm_ms()
+            extra = dict(hbm_stats(ps.device), **sampler.take())
+            if comm_ms is not None:
+                extra["dp_comm_ms_per_step"] = comm_ms / n
             if ps.is_last_stage and ps.tp_rank == 0:
                 metrics.write(step=it, loss=lv, lr=lr, grad_norm=gn, ms_per_step=dt * 1000, tokens_per_s=toks,
                               samples_per_s=gb / dt, tflops_per_gpu=tflops, consumed_samples=loader.consumed,
-                              **hbm_stats(ps.device))
+                              **extra)
             if tb is not None:   # Megatron's tensorboard tags
                 tb.add_scalars_flat({"lm loss": lv, "learning-rate": lr, "grad-norm": gn,
                                      "iteration-time": dt, "tokens-per-sec": toks,
@@ -215,6 +223,7 @@ def main(argv=None):
         dist.barrier()
     print_rank_0(f"> training finished after {it} iterations ({time.time() - start_wall:.1f}s)")
     pstate.destroy()
+    sampler.close()
     return 0
 
 

@@ -186,3 +186,25 @@ def test_ds_config_and_megatron_flags(tmp_path):
     b = parse_args(["--checkpoint-activations", "--zero-stage", "2"])
     assert b.mx_recompute and b.mx_effective["activation_recompute"] == "full"
     assert any("ZeRO stage 2 -> stage 1" in d for d in b.mx_deviations)
+
+
+def test_gpu_sampler_fake_sysfs(tmp_path):
+    """§5.5: power / clock / temperature sampling from the amdgpu hwmon nodes."""
+    import time
+    from mxtrain.obs.metrics import GPUSampler, gpu_sample
+    hw = tmp_path / "class/drm/card3/device/hwmon/hwmon0"
+    hw.mkdir(parents=True)
+    (hw / "power1_average").write_text("750000000\n")      # uW
+    (hw / "freq1_input").write_text("2400000000\n")        # Hz
+    (hw / "temp2_input").write_text("65000\n")             # mC
+    s = gpu_sample(3, str(tmp_path))
+    assert s == {"power_w": 750.0, "sclk_mhz": 2400.0, "temp_junction_c": 65.0}
+    smp = GPUSampler(3, interval_s=0.02, root=str(tmp_path))
+    time.sleep(0.2)
+    (hw / "power1_average").write_text("950000000\n")
+    time.sleep(0.2)
+    out = smp.take()
+    smp.close()
+    assert out["gpu_samples"] >= 3 and out["gpu_power_w_max"] == 950.0
+    assert 750.0 <= out["gpu_power_w_mean"] <= 950.0 and out["gpu_sclk_mhz_mean"] == 2400.0
+    assert GPUSampler(None).take() == {}
