@@ -225,19 +225,31 @@ __global__ __launch_bounds__(256) void roi_align_bwd_kernel(Levels L, const floa
 }
 
 // ------------------------------------------------------------ RoIAlign backward, tiled
-// Atomics-free (for the gradient values) RoIAlign backward, SURVEY K13.  The gradient of
-// every level is cut into 8 x 8-pixel tiles; each (roi, bin) "item" touches a few tiles
-// (its sr x sr samples' bilinear corners, <= 4 rows x 4 columns of pixels).  A counting
-// sort buckets the items per tile (integer atomics on the bucket counters only), then ONE
-// workgroup per tile accumulates its items into an fp32 LDS tile [64 px][C] -- wave w
-// owns channels [64w, 64w + 64), lane = channel, so every LDS update is a plain
-// read-modify-write by the owning lane, no LDS or global float atomics -- in ascending
-// item order (bitonic-sorted in LDS), which makes the result deterministic, and writes
-// the tile straight to the bf16 NHWC gradient.  Every pixel of every level is written
-// exactly once (empty tiles write zeros): no fp32 gradient buffer, no zero-fill, no cast.
+// Float-atomics-free RoIAlign backward.  The gradient of every level is cut
+// into 8 x 8-pixel tiles; each (roi, bin) "item" touches at most 2 x 2 tiles (its sr x sr
+// samples' bilinear corners span <= bin + 2 pixels per axis and a bin is <= 6 feature
+// pixels at every FPN level for <= 1344-pixel images).  Pipeline:
+//   1. items: the item's separable footprint (<= 4 rows x 4 columns, weights with
+//      1/sr^2 folded in) is computed ONCE and stored packed (48 B); tile counters ++
+//      (integer atomics: bucket sizes only);
+//   2. one-workgroup scan: entry offsets, cursors, and work chunks of <= kChunk entries
+//      per tile (a heavy tile on a coarse level is split so no workgroup runs a long
+//      serial chain), plus partial-slot offsets for split tiles;
+//   3. scatter item ids into their tiles' lists;
+//   4. one workgroup per chunk: its entry ids are bitonic-sorted in LDS (deterministic
+//      order), their footprints staged in LDS, and wave w / lane l accumulate channel
+//      64 w + l of the tile's 64 pixels in an fp32 LDS tile -- each LDS word has exactly
+//      one writer, so no atomics; the gradient rows are prefetched a batch ahead;
+//      single-chunk tiles (all but the heaviest) write bf16 NHWC directly, split tiles
+//      write an fp32 partial;
+//   5. split tiles: partials summed in chunk order -> bf16.
+// Every pixel of every level is written exactly once (empty tiles write zeros): no fp32
+// gradient buffer, zero-fill or cast.  Deterministic (entry lists sorted by item id) for
+// tiles of <= kSortBig entries.
 constexpr int kTile = 8;
-constexpr int kSortCap = 2048;
-constexpr int kMaxTileC = 256;   // 64 px x 256 ch fp32 = 64 KB + 8 KB keys of the 160 KB LDS
+constexpr int kChunk = 256;       // entries per work chunk (and sort capacity)
+constexpr int kMaxTileC = 256;    // 64 px x 256 ch fp32 = 64 KB (+ 13 KB) of the 160 KB LDS
+constexpr int kBatch = 16;        // gradient rows in flight per lane
 
 struct GOut {
   uint16_t* p[4];   // bf16 NHWC gradient per level
@@ -254,6 +266,11 @@ struct Foot {
   int ry[4], rx[4];
   float wy[4], wx[4];   // per-axis weights, 0 = unused; duplicate rows/columns merged
   int lv, b;
+};
+
+struct __attribute__((aligned(16))) FootP {   // packed footprint (48 B)
+  int16_t ry[4], rx[4];
+  float wy[4], wx[4];   // wy carries 1 / sr^2
 };
 
 // the sr <= 2 separable footprint of item (roi, bin) (same arithmetic as roi_align_bwd_kernel)
@@ -311,15 +328,26 @@ __device__ __forceinline__ int distinct_tiles(const int* idx, const float* w, in
   return n;
 }
 
-// kCount: counts[tile]++ per touched tile; else entries[cursor[tile]++] = item
+// kCount: footprint -> fp[item], counts[tile]++; else entries[cursor[tile]++] = item
 template <bool kCount>
 __global__ __launch_bounds__(256) void roi_tiles_kernel(Levels L, TileGeo G, const float* __restrict__ rois,
                                                         int items, int PH, int PW, int sr, int aligned,
-                                                        int* __restrict__ counter, int* __restrict__ entries) {
+                                                        FootP* __restrict__ fp, int* __restrict__ counter,
+                                                        int* __restrict__ entries) {
   const int item = blockIdx.x * blockDim.x + threadIdx.x;
   if (item >= items) return;
   const Foot f = footprint(L, rois, item, PH, PW, sr, aligned);
   if (f.b < 0 || f.b >= G.B) return;   // malformed batch index: never index outside the tiles
+  if (kCount) {
+    FootP q;
+    const float inv = 1.f / (float)(sr * sr);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      q.ry[i] = (int16_t)f.ry[i]; q.rx[i] = (int16_t)f.rx[i];
+      q.wy[i] = f.wy[i] * inv; q.wx[i] = f.wx[i];
+    }
+    fp[item] = q;
+  }
   int ty[4], tx[4];
   const int ny = distinct_tiles(f.ry, f.wy, ty), nx = distinct_tiles(f.rx, f.wx, tx);
   for (int i = 0; i < ny; ++i)
@@ -333,98 +361,272 @@ __global__ __launch_bounds__(256) void roi_tiles_kernel(Levels L, TileGeo G, con
     }
 }
 
-// exclusive scan of counts[T] -> offsets[T + 1] and cursor[T] (one workgroup)
+// one-workgroup exclusive scans over the T tiles:
+//   offsets[t] = sum counts[< t] (+ offsets[T]), cursor = offsets,
+//   coff[t] = sum of chunks(< t), chunks(t) = max(1, ceil(counts / kChunk)) (+ coff[T]),
+//   poff[t] = sum of chunks(< t) over split tiles (chunks > 1)
+__device__ void block_scan(int* part, int t, int v, int& excl, int& total) {
+  part[t] = v;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {   // Hillis-Steele inclusive scan
+    const int x = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  excl = part[t] - v;
+  total = part[1023];
+  __syncthreads();
+}
+
+__device__ __forceinline__ int chunks_of(int n) { return n <= kChunk ? 1 : (n + kChunk - 1) / kChunk; }
+
 __global__ __launch_bounds__(1024) void tile_scan_kernel(const int* __restrict__ counts, int T,
-                                                         int* __restrict__ offsets, int* __restrict__ cursor) {
+                                                         int* __restrict__ offsets, int* __restrict__ cursor,
+                                                         int* __restrict__ coff, int* __restrict__ poff,
+                                                         int* __restrict__ ctile, int grid,
+                                                         int* __restrict__ overflow) {
   __shared__ int part[1024];
   const int t = threadIdx.x;
   const int per = (T + 1023) / 1024;
   const int lo = min(t * per, T), hi = min(lo + per, T);
-  int sum = 0;
-  for (int i = lo; i < hi; ++i) sum += counts[i];
-  part[t] = sum;
-  __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {   // Hillis-Steele inclusive scan of the partials
-    const int v = t >= d ? part[t - d] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  int run = part[t] - sum;
+  int se = 0, sc = 0, sp = 0;
   for (int i = lo; i < hi; ++i) {
-    offsets[i] = run;
-    cursor[i] = run;
-    run += counts[i];
+    const int n = counts[i], c = chunks_of(n);
+    se += n;
+    sc += c;
+    sp += c > 1 ? c : 0;
   }
-  if (t == 1023) offsets[T] = part[1023];
+  int e0, c0, p0, et, ct, pt;
+  block_scan(part, t, se, e0, et);
+  block_scan(part, t, sc, c0, ct);
+  block_scan(part, t, sp, p0, pt);
+  for (int i = lo; i < hi; ++i) {
+    const int n = counts[i], c = chunks_of(n);
+    offsets[i] = e0; cursor[i] = e0; coff[i] = c0; poff[i] = p0;
+    for (int q = 0; q < c; ++q)          // chunk -> tile map (one load per workgroup later)
+      if (c0 + q < grid) ctile[c0 + q] = i;
+    e0 += n; c0 += c; p0 += c > 1 ? c : 0;
+  }
+  if (t == 1023) {
+    offsets[T] = et; coff[T] = ct; poff[T] = pt;
+    if (ct > grid) *overflow = 1;   // more chunks than launched workgroups
+  }
 }
 
-// one workgroup (C threads = C / 64 waves) per tile
-__global__ __launch_bounds__(256) void roi_align_bwd_tile_kernel(Levels L, TileGeo G, const float* __restrict__ rois,
-                                                                 int C, int PH, int PW, int sr, int aligned,
-                                                                 const uint16_t* __restrict__ dout,
-                                                                 const int* __restrict__ offsets,
-                                                                 const int* __restrict__ entries, GOut gout) {
-  __shared__ __attribute__((aligned(16))) float acc[kTile * kTile * kMaxTileC];   // [64 px][C]
-  __shared__ int keys[kSortCap];
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const int tile = blockIdx.x;
-  int lv = 0;
+__device__ __forceinline__ void decode_tile(const Levels& L, const TileGeo& G, int tile, int& lv, int& b, int& ty,
+                                            int& tx) {
+  lv = 0;
   while (lv + 1 < L.n && tile >= G.base[lv + 1]) ++lv;
   const int local = tile - G.base[lv];
-  const int tx = local % G.tw[lv], ty = (local / G.tw[lv]) % G.th[lv], b = local / (G.tw[lv] * G.th[lv]);
-  const int H = L.H[lv], W = L.W[lv];
-  const int y0 = ty * kTile, x0 = tx * kTile;
-  for (int i = tid * 4; i < kTile * kTile * C; i += nt * 4)
-    *reinterpret_cast<float4*>(acc + i) = make_float4(0.f, 0.f, 0.f, 0.f);
-  const int beg = offsets[tile], n = offsets[tile + 1] - beg;
-  const bool sorted = n > 1 && n <= kSortCap;
-  if (sorted) {   // bitonic sort of the item ids (padded to a power of two)
-    int np = 1;
-    while (np < n) np <<= 1;
-    for (int i = tid; i < np; i += nt) keys[i] = i < n ? entries[beg + i] : 0x7fffffff;
-    __syncthreads();
-    for (int k = 2; k <= np; k <<= 1)
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = tid; i < np; i += nt) {
-          const int p = i ^ j;
-          if (p > i) {
-            const int a = keys[i], c = keys[p];
-            if ((a > c) == ((i & k) == 0)) { keys[i] = c; keys[p] = a; }
-          }
-        }
-        __syncthreads();
-      }
-  }
-  __syncthreads();
-  const int c = tid;   // this thread's channel (blockDim == C)
-  const float inv = 1.f / (float)(sr * sr);
-  for (int e = 0; e < n; ++e) {
-    const int item = sorted ? keys[e] : entries[beg + e];
-    const Foot f = footprint(L, rois, item, PH, PW, sr, aligned);
-    const float go = bf2f(dout[(size_t)item * C + c]) * inv;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int yy = f.ry[i] - y0;
-      if (f.wy[i] == 0.f || yy < 0 || yy >= kTile) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int xx = f.rx[j] - x0;
-        if (f.wx[j] == 0.f || xx < 0 || xx >= kTile) continue;
-        float* a = acc + (yy * kTile + xx) * C + c;
-        *a += f.wy[i] * f.wx[j] * go;
-      }
-    }
-  }
-  __syncthreads();
-  uint16_t* g = gout.p[lv];
+  tx = local % G.tw[lv];
+  ty = (local / G.tw[lv]) % G.th[lv];
+  b = local / (G.tw[lv] * G.th[lv]);
+}
+
+__device__ __forceinline__ void write_tile_bf16(const float* acc, uint16_t* g, int C, int H, int W, int b, int y0,
+                                                int x0, int tid, int nt) {
   const int c8 = C / 8;
   for (int q = tid; q < kTile * kTile * c8; q += nt) {
     const int p = q / c8, ch = (q % c8) * 8;
     const int y = y0 + p / kTile, x = x0 + p % kTile;
     if (y >= H || x >= W) continue;
-    const float* a = acc + p * C + ch;
-    *reinterpret_cast<uint4*>(g + (((size_t)b * H + y) * W + x) * C + ch) = pack8(a);
+    *reinterpret_cast<uint4*>(g + (((size_t)b * H + y) * W + x) * C + ch) = pack8(acc + p * C + ch);
+  }
+}
+
+// split tiles (kChunk < n <= kSortBig): sort the whole entry list once, so the chunks'
+// membership and order -- and so the result -- are deterministic
+constexpr int kSortBig = 4096;
+__global__ __launch_bounds__(1024) void tile_sort_kernel(const int* __restrict__ offsets, int T,
+                                                         int* __restrict__ entries) {
+  __shared__ int keys[kSortBig];
+  const int tile = blockIdx.x;
+  const int beg = offsets[tile], n = offsets[tile + 1] - beg;
+  if (n <= kChunk || n > kSortBig) return;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  int np = 1;
+  while (np < n) np <<= 1;
+  for (int i = tid; i < np; i += nt) keys[i] = i < n ? entries[beg + i] : 0x7fffffff;
+  __syncthreads();
+  for (int kk = 2; kk <= np; kk <<= 1)
+    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+      for (int i = tid; i < np; i += nt) {
+        const int p = i ^ jj;
+        if (p > i) {
+          const int a = keys[i], c = keys[p];
+          if ((a > c) == ((i & kk) == 0)) { keys[i] = c; keys[p] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = tid; i < n; i += nt) entries[beg + i] = keys[i];
+}
+
+// one workgroup (C threads = C / 64 waves) per work chunk
+__global__ __launch_bounds__(256) void roi_align_bwd_tile_kernel(Levels L, TileGeo G, int T, int C,
+                                                                 const uint16_t* __restrict__ dout,
+                                                                 const FootP* __restrict__ fp,
+                                                                 const int* __restrict__ offsets,
+                                                                 const int* __restrict__ coff,
+                                                                 const int* __restrict__ poff,
+                                                                 const int* __restrict__ ctile,
+                                                                 const int* __restrict__ entries, GOut gout,
+                                                                 float* __restrict__ partial, int pslots,
+                                                                 int* __restrict__ overflow,
+                                                                 long long* __restrict__ dbg, int dmode) {
+  const long long t_start = dbg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
+  __shared__ __attribute__((aligned(16))) float acc[(kTile * kTile + 1) * kMaxTileC];   // [64 px + trash][C]
+  __shared__ int keys[kChunk];
+  __shared__ FootP fs[kChunk];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int k = blockIdx.x;
+  if (k >= coff[T]) return;                      // grid is an upper bound on the chunks
+  const int tile = ctile[k];
+  const int j = k - coff[tile], nch = coff[tile + 1] - coff[tile];
+  int lv, b, ty, tx;
+  decode_tile(L, G, tile, lv, b, ty, tx);
+  const int H = L.H[lv], W = L.W[lv];
+  const int y0 = ty * kTile, x0 = tx * kTile;
+  const int ebeg = offsets[tile] + j * kChunk;
+  const int n = min(kChunk, offsets[tile + 1] - ebeg);
+  if (n == 0) {   // empty tile (most of the fine levels): zeros straight to global
+    uint16_t* g = gout.p[lv];
+    const int c8 = C / 8;
+    for (int q = tid; q < kTile * kTile * c8; q += nt) {
+      const int p = q / c8, ch = (q % c8) * 8;
+      const int y = y0 + p / kTile, x = x0 + p % kTile;
+      if (y < H && x < W) *reinterpret_cast<uint4*>(g + (((size_t)b * H + y) * W + x) * C + ch) = make_uint4(0, 0, 0, 0);
+    }
+    return;
+  }
+  for (int i = tid * 4; i < kTile * kTile * C; i += nt * 4)
+    *reinterpret_cast<float4*>(acc + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+  int np = 1;
+  while (np < n) np <<= 1;
+  for (int i = tid; i < np; i += nt) keys[i] = i < n ? entries[ebeg + i] : 0x7fffffff;
+  __syncthreads();
+  if (nch == 1)   // (split tiles were sorted whole by tile_sort_kernel)
+  for (int kk = 2; kk <= np; kk <<= 1)           // bitonic sort: deterministic order
+    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+      for (int i = tid; i < np; i += nt) {
+        const int p = i ^ jj;
+        if (p > i) {
+          const int a = keys[i], c = keys[p];
+          if ((a > c) == ((i & kk) == 0)) { keys[i] = c; keys[p] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = tid; i < n; i += nt) fs[i] = fp[keys[i]];
+  __syncthreads();
+  const int c = tid;   // this thread's channel (blockDim == C)
+  // One entry, branch-free: its footprint is read as 3 x 16 B, and its 4 x 4 (row, column)
+  // slots map to distinct tile pixels -- or, when the slot is unused (zero weight: merged
+  // duplicate row / column) or outside this tile, to a scratch row past the tile -- so all
+  // 16 LDS reads are issued back to back before the 16 writes: two LDS round trips per
+  // entry instead of a wait per pixel (and no exec-mask branching).
+  // (the entry index is made opaque to the uniformity analysis -- mbcnt of an empty mask is
+  // 0 -- so the footprint stays in VGPRs and the 16 slot addresses are v_cndmask selects:
+  // scalarised, the same code became ~30 uniform branches per entry)
+  const int lane0 = (int)__builtin_amdgcn_mbcnt_lo(0u, 0u);
+  auto apply = [&](int e, float go) {
+    const uint4* fv = reinterpret_cast<const uint4*>(fs + e + lane0);
+    const uint4 a0 = fv[0], a1 = fv[1], a2 = fv[2];
+    const int ry[4] = {(int)(int16_t)(a0.x & 0xffffu), (int)(int16_t)(a0.x >> 16), (int)(int16_t)(a0.y & 0xffffu),
+                       (int)(int16_t)(a0.y >> 16)};
+    const int rx[4] = {(int)(int16_t)(a0.z & 0xffffu), (int)(int16_t)(a0.z >> 16), (int)(int16_t)(a0.w & 0xffffu),
+                       (int)(int16_t)(a0.w >> 16)};
+    const float wy[4] = {__uint_as_float(a1.x), __uint_as_float(a1.y), __uint_as_float(a1.z), __uint_as_float(a1.w)};
+    const float wx[4] = {__uint_as_float(a2.x), __uint_as_float(a2.y), __uint_as_float(a2.z), __uint_as_float(a2.w)};
+    float* ad[16];
+    float wv[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jx = 0; jx < 4; ++jx) {
+        const int yy = ry[i] - y0, xx = rx[jx] - x0;
+        // bitwise, not short-circuit: one v_cndmask per slot, no control flow
+        const int in = (int)(wy[i] != 0.f) & (int)(wx[jx] != 0.f) & (int)((unsigned)yy < (unsigned)kTile) &
+                       (int)((unsigned)xx < (unsigned)kTile);
+        const int off = in ? (yy * kTile + xx) * C : kTile * kTile * C;
+        ad[i * 4 + jx] = acc + off + c;
+        wv[i * 4 + jx] = wy[i] * wx[jx] * go;
+      }
+    if (dmode & 2) return;   // (debug: no LDS accumulation)
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = *ad[q];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) *ad[q] = v[q] + wv[q];
+  };
+  auto load = [&](int ee) {
+    if (dmode & 1) return 1.f;   // (debug: no gradient loads)
+    return ee < n ? bf2f(dout[(size_t)keys[ee] * C + c]) : 0.f;
+  };
+  // gradient rows double-buffered a batch ahead: batch A's loads are in flight while
+  // batch B is applied and vice versa (no register copy between them, so no wait)
+  float ga[kBatch], gb[kBatch];
+#pragma unroll
+  for (int q = 0; q < kBatch; ++q) ga[q] = load(q);
+  for (int e = 0; e < n; e += 2 * kBatch) {
+#pragma unroll
+    for (int q = 0; q < kBatch; ++q) gb[q] = load(e + kBatch + q);
+#pragma unroll
+    for (int q = 0; q < kBatch; ++q)
+      if (e + q < n) apply(e + q, ga[q]);
+    if (e + kBatch >= n) break;
+#pragma unroll
+    for (int q = 0; q < kBatch; ++q) ga[q] = load(e + 2 * kBatch + q);
+#pragma unroll
+    for (int q = 0; q < kBatch; ++q)
+      if (e + kBatch + q < n) apply(e + kBatch + q, gb[q]);
+  }
+  __syncthreads();
+  if (dbg && tid == 0) {   // per-workgroup timing probe (100 MHz ticks): chunk, tile, entries, time
+    dbg[4 * k] = k; dbg[4 * k + 1] = tile; dbg[4 * k + 2] = n;
+    dbg[4 * k + 3] = (long long)__builtin_amdgcn_s_memrealtime() - t_start;
+  }
+  if (nch == 1) {
+    write_tile_bf16(acc, gout.p[lv], C, H, W, b, y0, x0, tid, nt);
+    return;
+  }
+  const int slot = poff[tile] + j;
+  if (slot >= pslots) {   // beyond the geometric bound the host sized for: flag it
+    if (tid == 0) atomicAdd(overflow, 1);
+    return;
+  }
+  float* dst = partial + (size_t)slot * kTile * kTile * C;
+  for (int i = tid * 4; i < kTile * kTile * C; i += nt * 4)
+    *reinterpret_cast<float4*>(dst + i) = *reinterpret_cast<const float4*>(acc + i);
+}
+
+// split tiles: sum the chunk partials in chunk order -> bf16
+__global__ __launch_bounds__(256) void roi_align_bwd_combine_kernel(Levels L, TileGeo G, int C,
+                                                                    const int* __restrict__ coff,
+                                                                    const int* __restrict__ poff,
+                                                                    const float* __restrict__ partial, int pslots,
+                                                                    GOut gout) {
+  const int tile = blockIdx.x;
+  const int nch = coff[tile + 1] - coff[tile];
+  if (nch <= 1 || poff[tile] + nch > pslots) return;
+  int lv, b, ty, tx;
+  decode_tile(L, G, tile, lv, b, ty, tx);
+  const int H = L.H[lv], W = L.W[lv];
+  const int y0 = ty * kTile, x0 = tx * kTile;
+  const float* src = partial + (size_t)poff[tile] * kTile * kTile * C;
+  const int c8 = C / 8;
+  for (int q = threadIdx.x; q < kTile * kTile * c8; q += blockDim.x) {
+    const int p = q / c8, ch = (q % c8) * 8;
+    const int y = y0 + p / kTile, x = x0 + p % kTile;
+    if (y >= H || x >= W) continue;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int jj = 0; jj < nch; ++jj) {
+      const float* a = src + (size_t)jj * kTile * kTile * C + p * C + ch;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += a[e];
+    }
+    *reinterpret_cast<uint4*>(gout.p[lv] + (((size_t)b * H + y) * W + x) * C + ch) = pack8(s);
   }
 }
 
@@ -702,8 +904,12 @@ MX_EXPORT int mx_roi_align_bwd(float* const* grads, const int* H, const int* W, 
 }
 
 // Tiled, float-atomics-free backward (sr <= 2, C % 64 == 0, C <= 256) writing bf16 NHWC
-// gradients directly.  ws: int32 workspace of 3 T + 1 + R * PH * PW * 16 entries (T = tiles
-// of all levels: sum over levels of B * ceil(H / 8) * ceil(W / 8)).
+// gradients directly.  Workspaces (sizes from mx_roi_align_bwd_tiled_ws):
+//   ws  int32: FootP items * 12 | counts T | offsets T+1 | cursor T | coff T+1 | poff T+1 |
+//              overflow 1 | chunk->tile map (grid) | entries 16 * items  (ny, nx <= 4 distinct tiles per axis: never
+//              overflows; the 2 x 2 geometric bound only sizes the launch and partials,
+//              and exceeding it sets the overflow word instead of touching memory)
+//   partial fp32: pslots * 64 * C   (pslots = ceil(8 * items / kChunk) + 1)
 static TileGeo tile_geo(const int* H, const int* W, int n, int B) {
   TileGeo G = {};
   G.B = B;
@@ -718,35 +924,67 @@ static TileGeo tile_geo(const int* H, const int* W, int n, int B) {
   return G;
 }
 
+MX_EXPORT int64_t mx_roi_align_bwd_tiled_ws(const int* H, const int* W, int n, int B, int items, int C,
+                                            int64_t* partial_floats) {
+  const TileGeo G = tile_geo(H, W, n, B);
+  const int64_t T = G.base[n];
+  const int64_t pslots = (8 * (int64_t)items + kChunk - 1) / kChunk + 1;
+  if (partial_floats) *partial_floats = pslots * kTile * kTile * C;
+  const int64_t grid = 2 * T + (4 * (int64_t)items + kChunk - 1) / kChunk;
+  return 5 * T + 4 + grid + 16 * (int64_t)items + (int64_t)items * (sizeof(FootP) / 4);
+}
+
+static long long* g_tile_dbg = nullptr;
+static int g_tile_dmode = 0;
+// debugging: per-workgroup timing records of the next tiled backward (4 x int64 per chunk);
+// mode bit 0 = skip the gradient loads, bit 1 = skip the LDS accumulation
+MX_EXPORT void mx_roi_align_bwd_tiled_debug(long long* buf, int mode) {
+  g_tile_dbg = buf;
+  g_tile_dmode = mode;
+}
+
 MX_EXPORT int mx_roi_align_bwd_tiled(void* const* grads, const int* H, const int* W, const float* scales, int n,
                                      int lvl_min, float canon, int canon_lvl, int B, const float* rois, int R, int C,
                                      int PH, int PW, int sampling, int aligned, const void* dout, int* ws,
-                                     hipStream_t s) {
+                                     float* partial, hipStream_t s) {
   if (n < 1 || n > 4 || (C & 63) || C > kMaxTileC || sampling < 1 || sampling > 2 || B < 1)
     return hipErrorInvalidValue;
   Levels L = make_levels(nullptr, nullptr, H, W, scales, n, lvl_min, canon, canon_lvl);
   const TileGeo G = tile_geo(H, W, n, B);
   const int T = G.base[n];
   const int items = R * PH * PW;
-  int* counts = ws;
-  int* offsets = ws + T;
+  const int pslots = (int)((8 * (int64_t)items + kChunk - 1) / kChunk + 1);
+  FootP* fp = reinterpret_cast<FootP*>(ws);                 // 16-B aligned (caller's buffer)
+  int* counts = ws + (size_t)items * (sizeof(FootP) / 4);
+  int* offsets = counts + T;
   int* cursor = offsets + T + 1;
-  int* entries = cursor + T;
+  int* coff = cursor + T;
+  int* poff = coff + T + 1;
+  int* overflow = poff + T + 1;
+  // chunks <= T + entries / kChunk + T (rounding) with entries <= 4 items (2 x 2 tiles)
+  const int grid = 2 * T + (4 * items + kChunk - 1) / kChunk;
+  int* ctile = overflow + 1;
+  int* entries = ctile + grid;
+  // counts + the overflow word are not contiguous: clear both
   hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * (size_t)T, s);
   if (e != hipSuccess) return e;
-  if (items > 0) {
+  e = hipMemsetAsync(overflow, 0, sizeof(int), s);
+  if (e != hipSuccess) return e;
+  if (items > 0)
     hipLaunchKernelGGL(roi_tiles_kernel<true>, dim3((items + 255) / 256), dim3(256), 0, s, L, G, rois, items, PH, PW,
-                       sampling, aligned, counts, (int*)nullptr);
-  }
-  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, counts, T, offsets, cursor);
-  if (items > 0) {
+                       sampling, aligned, fp, counts, (int*)nullptr);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, counts, T, offsets, cursor, coff, poff, ctile,
+                     grid, overflow);
+  if (items > 0)
     hipLaunchKernelGGL(roi_tiles_kernel<false>, dim3((items + 255) / 256), dim3(256), 0, s, L, G, rois, items, PH, PW,
-                       sampling, aligned, cursor, entries);
-  }
+                       sampling, aligned, fp, cursor, entries);
+  hipLaunchKernelGGL(tile_sort_kernel, dim3(T), dim3(1024), 0, s, offsets, T, entries);
   GOut go = {};
   for (int i = 0; i < n; ++i) go.p[i] = (uint16_t*)grads[i];
-  hipLaunchKernelGGL(roi_align_bwd_tile_kernel, dim3(T), dim3(C), 0, s, L, G, rois, C, PH, PW, sampling, aligned,
-                     (const uint16_t*)dout, offsets, entries, go);
+  hipLaunchKernelGGL(roi_align_bwd_tile_kernel, dim3(grid), dim3(C), 0, s, L, G, T, C, (const uint16_t*)dout, fp,
+                     offsets, coff, poff, ctile, entries, go, partial, pslots, overflow, g_tile_dbg,
+                     g_tile_dmode);
+  hipLaunchKernelGGL(roi_align_bwd_combine_kernel, dim3(T), dim3(256), 0, s, L, G, C, coff, poff, partial, pslots, go);
   return hipGetLastError();
 }
 

@@ -100,6 +100,37 @@ def _ptr_array(ts, ctype=ctypes.c_void_p):
 _TILED = os.environ.get("MXTRAIN_ROIALIGN_TILED", "1") == "1"
 
 
+_WS_CACHE = {}
+_LAST_WS = None   # the last tiled-backward workspace (tests read its overflow word)
+
+
+def _tiled_ws(shapes, B, items, C):
+    """(int32 workspace entries, fp32 partial entries) of mx_roi_align_bwd_tiled."""
+    key = (tuple(tuple(s) for s in shapes), B, items, C)
+    v = _WS_CACHE.get(key)
+    if v is None:
+        n = len(shapes)
+        H = (ctypes.c_int * 4)(*[s[1] for s in shapes] + [0] * (4 - n))
+        W = (ctypes.c_int * 4)(*[s[2] for s in shapes] + [0] * (4 - n))
+        fn = _lib.lib().mx_roi_align_bwd_tiled_ws
+        fn.restype = ctypes.c_int64
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                       ctypes.POINTER(ctypes.c_int64)]
+        part = ctypes.c_int64(0)
+        nws = fn(ctypes.cast(H, ctypes.c_void_p), ctypes.cast(W, ctypes.c_void_p), n, B, items, C, ctypes.byref(part))
+        v = _WS_CACHE[key] = (int(nws), int(part.value))
+    return v
+
+
+def tiled_overflow() -> int:
+    """Overflow word of the last tiled RoIAlign backward (0 = every chunk was processed
+    within the geometric bounds the workspace was sized for); synchronises."""
+    if _LAST_WS is None:
+        return 0
+    ws, idx = _LAST_WS
+    return int(ws[idx].item())
+
+
 class RoIAlignFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, rois, PH, PW, sr, aligned, lvl_min, canon, canon_lvl, scales, *feats):
@@ -134,13 +165,16 @@ class RoIAlignFn(torch.autograd.Function):
             # tiled, deterministic, float-atomics-free kernel straight into bf16 gradients
             B = ctx.shapes[0][0]
             grads = [torch.empty(s, dtype=torch.bfloat16, device=rois.device) for s in ctx.shapes]
-            # workspace: tile counts, offsets (+1), cursors, and <= 16 tile entries per item
-            T = sum(B * (-(-s[1] // 8)) * (-(-s[2] // 8)) for s in ctx.shapes)
-            ws = torch.empty(3 * T + 1 + R * PH * PW * 16, dtype=torch.int32, device=rois.device)
+            nws, npart = _tiled_ws(tuple(ctx.shapes), B, R * PH * PW, C)
+            ws = torch.empty(nws, dtype=torch.int32, device=rois.device)
+            part = torch.empty(npart, dtype=torch.float32, device=rois.device)
             _lib.call("mx_roi_align_bwd_tiled", ctypes.cast(_ptr_array(grads), ctypes.c_void_p),
                       ctypes.cast(H, ctypes.c_void_p), ctypes.cast(W, ctypes.c_void_p),
                       ctypes.cast(S, ctypes.c_void_p), n, lvl_min, float(canon), canon_lvl, B, _lib.ptr(rois), R, C,
-                      PH, PW, sr, int(aligned), _lib.ptr(d), _lib.ptr(ws), _lib.stream())
+                      PH, PW, sr, int(aligned), _lib.ptr(d), _lib.ptr(ws), _lib.ptr(part), _lib.stream())
+            global _LAST_WS
+            T = sum(B * (-(-s[1] // 8)) * (-(-s[2] // 8)) for s in ctx.shapes)
+            _LAST_WS = (ws, R * PH * PW * 12 + 5 * T + 3)   # footprints, 5 tile arrays, overflow
             return (None,) * 9 + tuple(g if dt == torch.bfloat16 else g.to(dt) for g, dt in zip(grads, ctx.dtypes))
         grads = [torch.zeros(s, dtype=torch.float32, device=rois.device) for s in ctx.shapes]
         _lib.call("mx_roi_align_bwd", ctypes.cast(_ptr_array(grads), ctypes.c_void_p),

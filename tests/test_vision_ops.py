@@ -122,6 +122,7 @@ def test_roi_align_gpu_fwd_bwd(tiled, out_hw, monkeypatch):
         err = (a.grad.float().cpu() - b.grad).norm() / (b.grad.norm() + 1e-6)
         assert err < 2e-2, float(err)
     if tiled:
+        assert V.tiled_overflow() == 0
         first = [f.grad.clone() for f in fg]
         for f in fg:
             f.grad = None
