@@ -218,6 +218,47 @@ class XGMICommunicator:
         self.regions[name] = (t.data_ptr(), t.numel() * t.element_size(), ptrs)
         self._region_tensor[name] = t
 
+    def selftest_direct(self) -> bool:
+        """Collective: check the registered-buffer path on this group before real buffers
+        use it -- a scratch tensor from the caching allocator (registered at an offset, as
+        the flat buffers are) with small-integer data, direct reduce-scatter / all-gather
+        vs the staged kernels (exact in bf16), agreed over all ranks."""
+        ok = True
+        before = set(self._mapped)
+        try:
+            n = 64 * 1024 * self.world
+            big = torch.zeros(n + 4096, dtype=torch.bfloat16, device=self.device)
+            buf = big[4096:]
+            buf.copy_(torch.arange(n, device=self.device).remainder(7).add(self.rank).to(torch.bfloat16))
+            self.register("_selftest", buf)
+            a = torch.empty(n // self.world, dtype=torch.bfloat16, device=self.device)
+            b = torch.empty_like(a)
+            self.reduce_scatter_direct(a, "_selftest", 0, n * 2)
+            self.reduce_scatter(b, buf)
+            ok = torch.equal(a, b)
+            g1 = torch.empty(n, dtype=torch.bfloat16, device=self.device)
+            g2 = torch.empty_like(g1)
+            self.all_gather_direct(g1, "_selftest", 0)
+            self.all_gather(g2, buf[: n // self.world].contiguous())
+            ok = ok and torch.equal(g1, g2)
+            self.check()
+        except Exception:   # noqa: BLE001 -- any failure means: do not use the direct path
+            ok = False
+        flag = torch.tensor([0.0 if ok else 1.0], device=self.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        self.regions.pop("_selftest", None)
+        self._region_tensor.pop("_selftest", None)
+        # unmap the scratch segment's peer mappings: its memory returns to the allocator
+        torch.cuda.synchronize(self.device)
+        for key in set(self._mapped) - before:
+            ptr = self._mapped.pop(key)
+            for p in self._opened:
+                if p.value == ptr:
+                    _fn("mx_xgmi_close_handle")(p)
+                    p.value = None
+        self._opened = [p for p in self._opened if p.value]
+        return float(flag.item()) == 0.0
+
     def has_region(self, name: str, t: Optional[torch.Tensor] = None) -> bool:
         r = self.regions.get(name)
         return r is not None and (t is None or r[0] == t.data_ptr())

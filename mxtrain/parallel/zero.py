@@ -204,6 +204,8 @@ class DistributedOptimizer:
         if torch.cuda.is_current_stream_capturing() or not _xgmi.direct_enabled():
             return False
         try:
+            if not c.selftest_direct():
+                raise _xgmi.XGMIUnavailable("registered-buffer self-test failed")
             c.register(self._rg_grad, self.flat.grad)
             c.register(self._rg_pshard, self.param_shard)
             self._direct_state = True

@@ -120,6 +120,8 @@ def _worker(rank, world, port, q):
         exp = torch.cat([torch.arange(m, 2 * m, device=dev, dtype=torch.float32).add(1000 * r) for r in range(world)])
         out["ag_direct"] = float((ag.float() - exp.to(torch.bfloat16).float()).abs().max())
 
+        out["selftest_direct"] = 0.0 if comm.selftest_direct() else 1.0
+
         # validation mode (§5.2): clean calls pass the cross-rank checks ...
         comm.validate = True
         t = torch.arange(4096, device=dev, dtype=torch.float32).remainder(3).add(rank)
