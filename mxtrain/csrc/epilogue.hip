@@ -1,0 +1,147 @@
+// Convolution epilogues for the NHWC (channels_last) bf16 CNN workloads (Mask R-CNN
+// backbone / FPN / RPN / mask head): MIOpen runs the convolution WITHOUT its
+// bias, and one pass applies bias (+ residual) (+ ReLU) in place.  PyTorch's own path for
+// a channels_last conv with bias is conv -> broadcast add (a non-vectorised elementwise
+// kernel) -> clamp (ReLU) [-> add residual -> clamp]: 2-4 extra passes over the
+// activation and as many launches.  The backward pass fuses the ReLU mask with the bias
+// gradient's column partial sums (one read of the incoming gradient), folded by the
+// deterministic colreduce_kernel (norm.hip).
+//
+// Layout: [M, C] with M = N*H*W rows (NHWC memory), C % 8 == 0; 16-byte vectors (8 bf16),
+// lane-contiguous, so every load/store is a full 16 B per lane.
+#include "common.h"
+
+using namespace mx;
+
+namespace {
+
+// y = act(y + b (+ res)) in place; one thread per 8-channel vector
+template <bool kRes, bool kRelu>
+__global__ __launch_bounds__(256) void bias_act_fwd_kernel(uint16_t* __restrict__ y, const uint16_t* __restrict__ b,
+                                                           const uint16_t* __restrict__ res, int64_t nvec, int c8) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    float x[8], bb[8];
+    unpack8(reinterpret_cast<const uint4*>(y)[v], x);
+    if (b) {
+      unpack8(reinterpret_cast<const uint4*>(b)[v % c8], bb);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] += bb[j];
+    }
+    if (kRes) {
+      float r[8];
+      unpack8(reinterpret_cast<const uint4*>(res)[v], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] += r[j];
+    }
+    if (kRelu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = fmaxf(x[j], 0.f);
+    }
+    reinterpret_cast<uint4*>(y)[v] = pack8(x);
+  }
+}
+
+// dy = relu ? g * (out > 0) : g, and (kDb) partial[blockIdx.y][C] = column sums of dy over
+// the block's row stripe.  Block: 256 threads = (256 / c8) rows x c8 vectors of a row.
+template <bool kRelu, bool kDb>
+__global__ __launch_bounds__(256) void bias_act_bwd_kernel(const uint16_t* __restrict__ g,
+                                                           const uint16_t* __restrict__ out,
+                                                           uint16_t* __restrict__ dy, float* __restrict__ partial,
+                                                           int M, int C, int rows_per_block) {
+  const int c8 = C / 8;
+  const int rpi = blockDim.x / c8;               // rows per iteration
+  const int tr = threadIdx.x / c8, tv = threadIdx.x % c8;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (tr < rpi) {
+    for (int r = r0 + tr; r < r1; r += rpi) {
+      const int64_t v = (int64_t)r * c8 + tv;
+      float x[8];
+      unpack8(reinterpret_cast<const uint4*>(g)[v], x);
+      if (kRelu) {
+        const uint4 o = reinterpret_cast<const uint4*>(out)[v];
+        const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {   // bf16 > 0 <=> sign bit clear and nonzero
+          const uint32_t lo = w[j] & 0xffffu, hi = w[j] >> 16;
+          if (!(lo != 0u && !(lo & 0x8000u))) x[2 * j] = 0.f;
+          if (!(hi != 0u && !(hi & 0x8000u))) x[2 * j + 1] = 0.f;
+        }
+        reinterpret_cast<uint4*>(dy)[v] = pack8(x);
+      }
+      if (kDb) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += x[j];
+      }
+    }
+  }
+  if (!kDb) return;
+  // fold the rpi row-groups of the block in LDS (fixed order -> deterministic)
+  __shared__ float red[256][9];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = acc[j];
+  __syncthreads();
+  if (tr == 0) {
+    for (int k = 1; k < rpi; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += red[k * c8 + tv][j];
+    float* p = partial + (size_t)blockIdx.x * C + tv * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = acc[j];
+  }
+}
+
+}  // namespace
+
+// colreduce (norm.hip): fold fp32 partials [P][C] into a bf16 vector
+extern "C" int mx_colsum_finalize(const float* partial, int nparts, int cols, int nvec, void* o0, void* o1,
+                                  void* o2, int accumulate, float* scratch, hipStream_t s);
+
+// y [M, C] bf16 in place: y = act(y + b (+ res)); b may be null (no bias)
+MX_EXPORT int mx_bias_act_fwd(void* y, const void* b, const void* res, int64_t M, int C, int relu, hipStream_t s) {
+  if (C % 8 || C > 2048) return hipErrorInvalidValue;
+  const int64_t nvec = M * (C / 8);
+  if (nvec == 0) return hipSuccess;
+  const int64_t want = (nvec + 255) / 256;
+  const unsigned grid = (unsigned)(want < 8192 ? want : 8192);
+#define MX_BA(R, A)                                                                                        \
+  hipLaunchKernelGGL((bias_act_fwd_kernel<R, A>), dim3(grid), dim3(256), 0, s, (uint16_t*)y, (const uint16_t*)b, \
+                     (const uint16_t*)res, nvec, C / 8)
+  if (res) {
+    if (relu) MX_BA(true, true); else MX_BA(true, false);
+  } else {
+    if (relu) MX_BA(false, true); else MX_BA(false, false);
+  }
+#undef MX_BA
+  return hipGetLastError();
+}
+
+// rows of the bias-gradient partial stripes (one per workgroup)
+MX_EXPORT int mx_bias_act_bwd_parts(int64_t M, int C) {
+  (void)C;
+  const int rpb = 128;
+  return (int)((M + rpb - 1) / rpb);
+}
+
+// dy = relu ? g * (out > 0) : g (dy may alias g); db (bf16 [C], optional) (+)= column sums
+// of dy; partial: mx_bias_act_bwd_parts(M, C) * C floats.  C <= 2048, C % 8 == 0.
+MX_EXPORT int mx_bias_act_bwd(const void* g, const void* out, void* dy, void* db, float* partial, int64_t M, int C,
+                              int relu, int accumulate, hipStream_t s) {
+  if (C % 8 || C > 2048 || (!relu && !db)) return hipErrorInvalidValue;
+  if (M == 0) return hipSuccess;
+  const int rpb = 128;
+  const int nparts = mx_bias_act_bwd_parts(M, C);
+#define MX_BB(R, D)                                                                                       \
+  hipLaunchKernelGGL((bias_act_bwd_kernel<R, D>), dim3(nparts), dim3(256), 0, s, (const uint16_t*)g,            \
+                     (const uint16_t*)out, (uint16_t*)dy, partial, (int)M, C, rpb)
+  if (relu) {
+    if (db) MX_BB(true, true); else MX_BB(true, false);
+  } else {
+    MX_BB(false, true);
+  }
+#undef MX_BB
+  if (db) return mx_colsum_finalize(partial, nparts, C, 1, db, nullptr, nullptr, accumulate, nullptr, s);
+  return hipGetLastError();
+}

@@ -29,6 +29,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.epilogue import conv_bias_act, conv_transpose_bias_act
 from ..ops import vision as V
 from .compute_weights import ComputeWeights, cw
 from .resnet import ConvNorm, resnet50
@@ -116,10 +117,10 @@ class FPN(nn.Module):
 
     def forward(self, feats: List[torch.Tensor]) -> List[torch.Tensor]:
         dt = feats[0].dtype
-        lat = [F.conv2d(f, cw(m.weight, dt), cw(m.bias, dt)) for f, m in zip(feats, self.lateral)]
+        lat = [conv_bias_act(f, cw(m.weight, dt), cw(m.bias, dt)) for f, m in zip(feats, self.lateral)]
         for i in range(len(lat) - 2, -1, -1):
             lat[i] = lat[i] + F.interpolate(lat[i + 1], scale_factor=2, mode="nearest")
-        outs = [F.conv2d(x, cw(m.weight, dt), cw(m.bias, dt), padding=1) for x, m in zip(lat, self.output)]
+        outs = [conv_bias_act(x, cw(m.weight, dt), cw(m.bias, dt), padding=1) for x, m in zip(lat, self.output)]
         outs.append(F.max_pool2d(outs[-1], 1, 2))   # P6
         return outs
 
@@ -136,9 +137,9 @@ class RPNHead(nn.Module):
 
     def forward(self, x):
         dt = x.dtype
-        t = F.relu(F.conv2d(x, cw(self.conv.weight, dt), cw(self.conv.bias, dt), padding=1), inplace=True)
-        lg = F.conv2d(t, cw(self.cls.weight, dt), cw(self.cls.bias, dt))
-        bx = F.conv2d(t, cw(self.box.weight, dt), cw(self.box.bias, dt))
+        t = conv_bias_act(x, cw(self.conv.weight, dt), cw(self.conv.bias, dt), padding=1, relu=True)
+        lg = conv_bias_act(t, cw(self.cls.weight, dt), cw(self.cls.bias, dt))
+        bx = conv_bias_act(t, cw(self.box.weight, dt), cw(self.box.bias, dt))
         B = x.shape[0]
         # NHWC flatten -> [B, H*W*A] / [B, H*W*A, 4] (cell-major, anchor-minor)
         return lg.permute(0, 2, 3, 1).reshape(B, -1), bx.permute(0, 2, 3, 1).reshape(B, -1, 4)
@@ -185,9 +186,9 @@ class MaskHead(nn.Module):
         dt = x.dtype
         x = x.permute(0, 3, 1, 2)    # NCHW view of NHWC memory (channels_last)
         for m in self.convs:
-            x = F.relu(F.conv2d(x, cw(m.weight, dt), cw(m.bias, dt), padding=1), inplace=True)
-        x = F.relu(F.conv_transpose2d(x, cw(self.deconv.weight, dt), cw(self.deconv.bias, dt), stride=2), inplace=True)
-        return F.conv2d(x, cw(self.pred.weight, dt), cw(self.pred.bias, dt))
+            x = conv_bias_act(x, cw(m.weight, dt), cw(m.bias, dt), padding=1, relu=True)
+        x = conv_transpose_bias_act(x, cw(self.deconv.weight, dt), cw(self.deconv.bias, dt), stride=2, relu=True)
+        return conv_bias_act(x, cw(self.pred.weight, dt), cw(self.pred.bias, dt))
 
 
 # ---------------------------------------------------------------------------- model

@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import compute_weights as _cw
+from ..ops.epilogue import conv_bias_act
 
 
 class FrozenBN(nn.Module):
@@ -50,7 +51,10 @@ class ConvNorm(nn.Module):
 
     calibrating = False
 
-    def forward(self, x):
+    def forward(self, x, residual=None, relu=None):
+        """act(conv(x) [+ folded FrozenBN] (+ residual)); ``relu`` overrides the module's
+        activation (the bottleneck applies its ReLU after the residual add)."""
+        relu = self.relu if relu is None else relu
         dt = x.dtype
         w = self.conv.weight
         if self.norm_kind == "frozen" and ConvNorm.calibrating:
@@ -64,10 +68,13 @@ class ConvNorm(nn.Module):
                 self.norm.bias.zero_()
         if self.norm_kind == "frozen":
             wf, bf = self._folded(w, dt)
-            y = F.conv2d(x, wf, bf, self.conv.stride, self.conv.padding, self.conv.dilation)
-        else:
-            y = self.norm(F.conv2d(x, w.to(dt), None, self.conv.stride, self.conv.padding, self.conv.dilation))
-        return F.relu(y, inplace=True) if self.relu else y
+            # one MIOpen conv + one fused bias (+ residual) (+ ReLU) pass (ops/epilogue.py)
+            return conv_bias_act(x, wf, bf, self.conv.stride, self.conv.padding, self.conv.dilation, relu=relu,
+                                 residual=residual)
+        y = self.norm(F.conv2d(x, w.to(dt), None, self.conv.stride, self.conv.padding, self.conv.dilation))
+        if residual is not None:
+            y = y + residual
+        return F.relu(y, inplace=True) if relu else y
 
     def _folded(self, w: torch.Tensor, dt: torch.dtype):
         """FrozenBN folded into the conv: weight * s (per output channel) and bias
@@ -124,7 +131,7 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         idt = self.shortcut(x) if self.shortcut is not None else x
-        return F.relu(self.conv3(self.conv2(self.conv1(x))) + idt, inplace=True)
+        return self.conv3(self.conv2(self.conv1(x)), residual=idt, relu=True)
 
 
 class ResNet(nn.Module):

@@ -38,6 +38,10 @@ SIGNATURES = {
     "mx_colsum_finalize": [P, I, I, I, P, P, P, I, P, P],
     "mx_colreduce_scratch": [I, I],
     "mx_colsum_bf16": [P, I, I, P, P, I, P],
+    # epilogue.hip
+    "mx_bias_act_fwd": [P, P, P, I64, I, I, P],
+    "mx_bias_act_bwd_parts": [I64, I],
+    "mx_bias_act_bwd": [P, P, P, P, P, I64, I, I, I, P],
     # fused.hip
     "mx_bias_gelu_fwd": [P, P, P, I, I, P],
     "mx_bias_gelu_bwd_rows_per_block": [],
@@ -68,7 +72,7 @@ SIGNATURES = {
     # vision.hip
     "mx_roi_align_fwd": [P, P, P, P, I, I, F, I, P, I, I, I, I, I, I, P, P],
     "mx_roi_align_bwd": [P, P, P, P, I, I, F, I, P, I, I, I, I, I, I, P, P],
-    "mx_roi_align_bwd_tiled": [P, P, P, P, I, I, F, I, I, P, I, I, I, I, I, I, P, P, P],
+    "mx_roi_align_bwd_tiled": [P, P, P, P, I, I, F, I, I, P, I, I, I, I, I, I, P, P, P, P],
     "mx_nms_workspace_words": [I],
     "mx_nms": [P, P, I, I, F, I, P, P, P, P],
     "mx_match": [P, I, I, P, P, I, I, P, P, P, P, P],

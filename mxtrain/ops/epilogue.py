@@ -1,0 +1,103 @@
+"""Fused convolution epilogues for NHWC bf16 CNNs (csrc/epilogue.hip).
+
+``conv_bias_act(x, w, b, ..., relu, residual)`` = act(conv(x, w) + b (+ residual)): MIOpen
+runs the convolution without its bias and one HIP pass applies bias, residual and ReLU in
+place; the backward fuses the ReLU mask with the bias gradient's column sums.  Replaces
+PyTorch's channels_last path (conv, broadcast bias add, clamp, residual add, clamp) --
+2-4 extra passes over every activation and as many launches per conv.
+
+CPU / non-channels_last tensors take the plain PyTorch ops (same math).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+_ENABLED = os.environ.get("MXTRAIN_CONV_EPILOGUE", "1") == "1"
+
+
+def _rows_cols(y: torch.Tensor):
+    return y.numel() // y.shape[1], y.shape[1]
+
+
+def _nhwc(t: Optional[torch.Tensor]) -> bool:
+    return t is None or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
+
+
+class BiasActFn(torch.autograd.Function):
+    """y <- act(y + b (+ res)) in place on the conv output y (channels_last bf16)."""
+
+    @staticmethod
+    def forward(ctx, y, b, res, relu: bool):
+        M, C = _rows_cols(y)
+        _lib.call("mx_bias_act_fwd", _lib.ptr(y), _lib.ptr(b), _lib.ptr(res), M, C, int(relu), _lib.stream())
+        ctx.mark_dirty(y)
+        ctx.relu, ctx.has_res, ctx.want_db = relu, res is not None, b is not None and b.requires_grad
+        ctx.bdtype = b.dtype if b is not None else None
+        if relu:
+            ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        relu, want_db = ctx.relu, ctx.want_db and ctx.needs_input_grad[1]
+        if not relu and not want_db:
+            return g, None, (g if ctx.has_res else None), None
+        if not _nhwc(g):
+            g = g.contiguous(memory_format=torch.channels_last)
+        M, C = _rows_cols(g)
+        dy = torch.empty_like(g) if relu else g
+        db = torch.empty(C, dtype=torch.bfloat16, device=g.device) if want_db else None
+        nparts = _lib.query("mx_bias_act_bwd_parts", M, C)
+        partial = torch.empty(nparts * C, dtype=torch.float32, device=g.device) if want_db else None
+        out = ctx.saved_tensors[0] if relu else None
+        _lib.call("mx_bias_act_bwd", _lib.ptr(g), _lib.ptr(out), _lib.ptr(dy), _lib.ptr(db), _lib.ptr(partial),
+                  M, C, int(relu), 0, _lib.stream())
+        if db is not None and db.dtype != ctx.bdtype:
+            db = db.to(ctx.bdtype)
+        return dy, db, (dy if ctx.has_res else None), None
+
+
+def _fused_ok(y, b, residual) -> bool:
+    return (_ENABLED and y.is_cuda and y.dtype == torch.bfloat16 and _nhwc(y) and _nhwc(residual)
+            and y.shape[1] % 8 == 0 and y.shape[1] <= 2048
+            and (b is None or (b.dtype == torch.bfloat16 and b.is_contiguous()))
+            and (residual is None or (residual.dtype == torch.bfloat16 and residual.shape == y.shape)))
+
+
+def bias_act(y: torch.Tensor, b: Optional[torch.Tensor], residual: Optional[torch.Tensor] = None,
+             relu: bool = False) -> torch.Tensor:
+    """act(y + b (+ residual)); in place on ``y`` when the fused kernel runs."""
+    if _fused_ok(y, b, residual):
+        if b is None and residual is None and not relu:
+            return y
+        return BiasActFn.apply(y, b, residual, relu)
+    if b is not None:
+        y = y + b.view(1, -1, 1, 1)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+def conv_bias_act(x, w, b=None, stride=1, padding=0, dilation=1, relu: bool = False,
+                  residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """act(conv2d(x, w) + b (+ residual)) -- one MIOpen conv + one fused epilogue pass."""
+    if _fused_ok(x, b, residual) and x.shape[1] == w.shape[1]:
+        return bias_act(F.conv2d(x, w, None, stride, padding, dilation), b, residual, relu)
+    y = F.conv2d(x, w, b, stride, padding, dilation)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y, inplace=True) if relu else y
+
+
+def conv_transpose_bias_act(x, w, b=None, stride=1, relu: bool = False) -> torch.Tensor:
+    if _fused_ok(x, b, None):
+        return bias_act(F.conv_transpose2d(x, w, None, stride=stride), b, None, relu)
+    y = F.conv_transpose2d(x, w, b, stride=stride)
+    return F.relu(y, inplace=True) if relu else y

@@ -1,8 +1,7 @@
-mkdir -p gpurun_out/c8
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-for t in 1 0; do
-MXTRAIN_ROIALIGN_TILED=$t timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_t$t -o run -- python -u scripts/bench_maskrcnn.py --batch 4 --graph 0 --steps 20 --warmup 10 --out gpurun_out/c8/b4_t$t.jsonl > gpurun_out/c8/b4_t$t.log 2>&1 || exit 1
-db=$(find /tmp/prof_t$t -name "*.db" | head -1)
-python3 scripts/rocpd_stats.py "$db" --csv gpurun_out/c8/kstats_t$t.csv --top 50 > gpurun_out/c8/kstats_t$t.txt
+mkdir -p gpurun_out/c21
+timeout -k 10 200 python -u -m pytest tests/test_vision_ops.py tests/test_maskrcnn_gpu.py -x -q --timeout 120 --timeout-method thread -m gpu > gpurun_out/c21/tests.log 2>&1 || { tail -30 gpurun_out/c21/tests.log; exit 1; }
+tail -2 gpurun_out/c21/tests.log
+for b in 1 4; do
+timeout -k 10 300 python -u scripts/bench_maskrcnn.py --batch $b --out gpurun_out/c21/b$b.jsonl > gpurun_out/c21/b$b.log 2>&1 || { tail -5 gpurun_out/c21/b$b.log; exit 1; }
 done
-cat gpurun_out/c8/*.jsonl
+cat gpurun_out/c21/*.jsonl

@@ -182,3 +182,42 @@ def test_crop_resize_mask_crops_gpu():
     ref = V.crop_resize_masks(full, boxes, gid)
     out = V.crop_resize_mask_crops(flat.cuda(), table.reshape(-1, 5).cuda(), H, W, boxes.cuda(), gid.cuda())
     torch.testing.assert_close(out.cpu(), ref, rtol=1e-4, atol=1e-4)   # fma vs separate mul-add
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("relu,res,bias_grad", [(True, False, False), (False, False, True), (True, True, False),
+                                                (True, False, True)])
+def test_conv_bias_act_gpu(relu, res, bias_grad):
+    """Fused conv epilogue (csrc/epilogue.hip) vs the fp32 torch reference: forward and
+    the gradients of input, weight, bias and residual."""
+    from mxtrain.ops import epilogue as E
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 64, 20, 24, generator=g)
+    w = torch.randn(128, 64, 3, 3, generator=g) * 0.05
+    b = torch.randn(128, generator=g)
+    r = torch.randn(2, 128, 20, 24, generator=g)
+    dout = torch.randn(2, 128, 20, 24, generator=g)
+
+    def run(dev, dt, fused):
+        xx = x.to(dev, dt).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        ww = w.to(dev, dt).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        bb = b.detach().clone().to(dev, dt).requires_grad_(bias_grad)
+        rr = r.to(dev, dt).contiguous(memory_format=torch.channels_last).requires_grad_(True) if res else None
+        if fused:
+            y = E.conv_bias_act(xx, ww, bb, padding=1, relu=relu, residual=rr)
+        else:
+            y = torch.nn.functional.conv2d(xx, ww, bb, padding=1)
+            y = y + rr if res else y
+            y = torch.relu(y) if relu else y
+        (y.float() * dout.to(dev)).sum().backward()
+        grads = [xx.grad, ww.grad] + ([bb.grad] if bias_grad else []) + ([rr.grad] if res else [])
+        return y.detach().float().cpu(), [t.float().cpu() for t in grads]
+
+    y_ref, g_ref = run("cpu", torch.float32, False)
+    y_t, g_t = run("cuda", torch.bfloat16, False)     # PyTorch's own bf16 path on the GPU
+    y, gs = run("cuda", torch.bfloat16, True)
+    assert (y - y_ref).abs().max() / y_ref.abs().max() < 2e-2
+    errs = [(float((a - r).norm() / (r.norm() + 1e-6)), float((t - r).norm() / (r.norm() + 1e-6)))
+            for a, t, r in zip(gs, g_t, g_ref)]
+    for fused_err, torch_err in errs:   # as close to fp32 as the unfused bf16 ops are
+        assert fused_err < max(2e-2, 1.5 * torch_err), errs
