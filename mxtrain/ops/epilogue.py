@@ -85,10 +85,32 @@ def bias_act(y: torch.Tensor, b: Optional[torch.Tensor], residual: Optional[torc
     return F.relu(y) if relu else y
 
 
+_GEMM_1X1 = os.environ.get("MXTRAIN_CONV1X1_GEMM", "1") == "1"
+
+
+def _as_int(v):
+    return v if isinstance(v, int) else (v[0] if all(e == v[0] for e in v) else None)
+
+
+def conv1x1_gemm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """A stride-1 1x1 convolution of an NHWC tensor IS a GEMM over the N*H*W rows:
+    y[M, Cout] = x[M, Cin] @ w[Cout, Cin]^T, with autograd's mm backward giving the data
+    gradient (dy @ w) and the weight gradient (dy^T @ x) -- three hipBLASLt GEMMs, no
+    MIOpen solver, workspace zero-fill, cast or layout-transpose helper kernels."""
+    N, C, H, W = x.shape
+    x2 = x.permute(0, 2, 3, 1).reshape(N * H * W, C)
+    y2 = torch.mm(x2, w.reshape(w.shape[0], C).t())
+    return y2.view(N, H, W, w.shape[0]).permute(0, 3, 1, 2)
+
+
 def conv_bias_act(x, w, b=None, stride=1, padding=0, dilation=1, relu: bool = False,
                   residual: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """act(conv2d(x, w) + b (+ residual)) -- one MIOpen conv + one fused epilogue pass."""
+    """act(conv2d(x, w) + b (+ residual)) -- one conv (hipBLASLt GEMM for 1x1 stride-1,
+    MIOpen otherwise) + one fused epilogue pass."""
     if _fused_ok(x, b, residual) and x.shape[1] == w.shape[1]:
+        if (_GEMM_1X1 and w.shape[2] == 1 and w.shape[3] == 1 and _as_int(stride) == 1 and _as_int(padding) == 0
+                and w.dtype == x.dtype):
+            return bias_act(conv1x1_gemm(x, w), b, residual, relu)
         return bias_act(F.conv2d(x, w, None, stride, padding, dilation), b, residual, relu)
     y = F.conv2d(x, w, b, stride, padding, dilation)
     if residual is not None:

@@ -185,15 +185,16 @@ def test_crop_resize_mask_crops_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("relu,res,bias_grad", [(True, False, False), (False, False, True), (True, True, False),
-                                                (True, False, True)])
-def test_conv_bias_act_gpu(relu, res, bias_grad):
+@pytest.mark.parametrize("relu,res,bias_grad,k", [(True, False, False, 3), (False, False, True, 3),
+                                                  (True, True, False, 3), (True, False, True, 3),
+                                                  (True, True, True, 1), (False, False, True, 1)])
+def test_conv_bias_act_gpu(relu, res, bias_grad, k):
     """Fused conv epilogue (csrc/epilogue.hip) vs the fp32 torch reference: forward and
     the gradients of input, weight, bias and residual."""
     from mxtrain.ops import epilogue as E
     g = torch.Generator().manual_seed(11)
     x = torch.randn(2, 64, 20, 24, generator=g)
-    w = torch.randn(128, 64, 3, 3, generator=g) * 0.05
+    w = torch.randn(128, 64, k, k, generator=g) * 0.05
     b = torch.randn(128, generator=g)
     r = torch.randn(2, 128, 20, 24, generator=g)
     dout = torch.randn(2, 128, 20, 24, generator=g)
@@ -204,9 +205,9 @@ def test_conv_bias_act_gpu(relu, res, bias_grad):
         bb = b.detach().clone().to(dev, dt).requires_grad_(bias_grad)
         rr = r.to(dev, dt).contiguous(memory_format=torch.channels_last).requires_grad_(True) if res else None
         if fused:
-            y = E.conv_bias_act(xx, ww, bb, padding=1, relu=relu, residual=rr)
+            y = E.conv_bias_act(xx, ww, bb, padding=k // 2, relu=relu, residual=rr)
         else:
-            y = torch.nn.functional.conv2d(xx, ww, bb, padding=1)
+            y = torch.nn.functional.conv2d(xx, ww, bb, padding=k // 2)
             y = y + rr if res else y
             y = torch.relu(y) if relu else y
         (y.float() * dout.to(dev)).sum().backward()
