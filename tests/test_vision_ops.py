@@ -200,10 +200,11 @@ def test_conv_bias_act_gpu(relu, res, bias_grad, k):
     dout = torch.randn(2, 128, 20, 24, generator=g)
 
     def run(dev, dt, fused):
-        xx = x.to(dev, dt).contiguous(memory_format=torch.channels_last).requires_grad_(True)
-        ww = w.to(dev, dt).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        xx = x.detach().clone().to(dev, dt).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        ww = w.detach().clone().to(dev, dt).contiguous(memory_format=torch.channels_last).requires_grad_(True)
         bb = b.detach().clone().to(dev, dt).requires_grad_(bias_grad)
-        rr = r.to(dev, dt).contiguous(memory_format=torch.channels_last).requires_grad_(True) if res else None
+        rr = (r.detach().clone().to(dev, dt).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+              if res else None)
         if fused:
             y = E.conv_bias_act(xx, ww, bb, padding=k // 2, relu=relu, residual=rr)
         else:
