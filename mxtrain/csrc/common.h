@@ -105,23 +105,23 @@ __device__ __forceinline__ bool dropout_keep(uint64_t idx, uint32_t seed, uint32
   return h >= thresh;  // thresh = p * 2^32
 }
 
-// tanh via one v_exp + one v_rcp (libm tanhf is ~40 VALU ops and made the GeLU
-// kernels VALU-bound); saturates correctly for |u| -> inf.
-__device__ __forceinline__ float fast_tanh(float u) {
-  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * u));
+// tanh-approximation GeLU (Megatron bias_gelu / HF "gelu_new") in its sigmoid form:
+//   0.5 x (1 + tanh(u)) = x s,  s = sigmoid(2u) = 1 / (1 + 2^(x (A + B x^2))),
+//   u = k0 x (1 + k1 x^2),  A = -2 k0 log2(e),  B = A k1
+// (one v_exp + one v_rcp and 5 VALU ops per element: the tanh form took ~12 and made the
+// GeLU kernels VALU-bound).  Saturates: x -> -inf gives -0, x -> +inf gives x.
+constexpr float kGeluA = -2.f * 0.7978845608028654f * 1.4426950408889634f;
+constexpr float kGeluB = kGeluA * 0.044715f;
+__device__ __forceinline__ float gelu_sig(float x, float x2) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * __builtin_fmaf(kGeluB, x2, kGeluA)));
 }
-// tanh-approximation GeLU (Megatron bias_gelu / HF "gelu_new")
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * x * (1.f + k1 * x * x);
-  return 0.5f * x * (1.f + fast_tanh(u));
-}
+__device__ __forceinline__ float gelu_tanh(float x) { return x * gelu_sig(x, x * x); }
+// d/dx = s + x s (1 - s) 2 k0 (1 + 3 k1 x^2) = s (1 + x (1 - s) (C1 + C2 x^2))
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float x2 = x * x;
-  float u = k0 * x * (1.f + k1 * x2);
-  float t = fast_tanh(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+  constexpr float C1 = 2.f * 0.7978845608028654f, C2 = 3.f * 0.044715f * C1;
+  const float x2 = x * x;
+  const float s = gelu_sig(x, x2);
+  return s * __builtin_fmaf(x * (1.f - s), __builtin_fmaf(C2, x2, C1), 1.f);
 }
 
 // bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5 "XCD swizzle

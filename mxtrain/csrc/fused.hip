@@ -12,23 +12,39 @@ using namespace mx;
 namespace {
 
 // ---------------------------------------------------------------- bias + GeLU
+// Each thread handles FV 16-B vectors 256 apart (coalesced), all loads issued before the
+// math: with one load in flight per thread the kernel could not cover HBM latency.
+constexpr int kGeluFV = 2;
 __global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ bias,
     uint16_t* __restrict__ y, int64_t n, int cols) {
   const int64_t nvec = n / 8;
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nvec;
-       v += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)((v * 8) % cols);
-    float a[8], b[8], o[8];
-    unpack8(*reinterpret_cast<const uint4*>(x + v * 8), a);
-    unpack8(*reinterpret_cast<const uint4*>(bias + c), b);
+  const int64_t v0 = (int64_t)blockIdx.x * (256 * kGeluFV) + threadIdx.x;
+  uint4 raw[kGeluFV], braw[kGeluFV];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = gelu_tanh(a[j] + b[j]);
-    *reinterpret_cast<uint4*>(y + v * 8) = pack8(o);
+  for (int u = 0; u < kGeluFV; ++u) {
+    const int64_t v = v0 + 256 * u;
+    if (v < nvec) {
+      raw[u] = *reinterpret_cast<const uint4*>(x + v * 8);
+      braw[u] = *reinterpret_cast<const uint4*>(bias + (int)((v * 8) % cols));
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kGeluFV; ++u) {
+    const int64_t v = v0 + 256 * u;
+    if (v < nvec) {
+      float a[8], b[8], o[8];
+      unpack8(raw[u], a);
+      unpack8(braw[u], b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = gelu_tanh(a[j] + b[j]);
+      *reinterpret_cast<uint4*>(y + v * 8) = pack8(o);
+    }
   }
 }
 
-// dx = dy * gelu'(x + b); partial[blockIdx.y][c] = sum over the block's rows of dx
+// dx = dy * gelu'(x + b); partial[blockIdx.y][c] = sum over the block's rows of dx.
+// Rows in groups of 4 with the group's 8 loads issued first (memory-level parallelism).
 __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
     const uint16_t* __restrict__ bias, uint16_t* __restrict__ dx, int rows, int cols,
@@ -39,18 +55,33 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
   const int r1 = min(rows, r0 + rows_per_block);
   float b[8], acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unpack8(*reinterpret_cast<const uint4*>(bias + c), b);
-  for (int r = r0; r < r1; ++r) {
-    const size_t off = (size_t)r * cols + c;
-    float g[8], a[8], o[8];
-    unpack8(*reinterpret_cast<const uint4*>(dy + off), g);
-    unpack8(*reinterpret_cast<const uint4*>(x + off), a);
+  constexpr int G = 4;
+  for (int r = r0; r < r1; r += G) {
+    uint4 gr[G], ar[G];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = g[j] * gelu_tanh_grad(a[j] + b[j]);
-    uint4 pk = pack8(o);
-    *reinterpret_cast<uint4*>(dx + off) = pk;
-    unpack8(pk, o);
+    for (int u = 0; u < G; ++u) {
+      if (r + u < r1) {
+        const size_t off = (size_t)(r + u) * cols + c;
+        gr[u] = *reinterpret_cast<const uint4*>(dy + off);
+        ar[u] = *reinterpret_cast<const uint4*>(x + off);
+      }
+    }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += o[j];
+    for (int u = 0; u < G; ++u) {
+      if (r + u < r1) {
+        const size_t off = (size_t)(r + u) * cols + c;
+        float g[8], a[8], o[8];
+        unpack8(gr[u], g);
+        unpack8(ar[u], a);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = g[j] * gelu_tanh_grad(a[j] + b[j]);
+        uint4 pk = pack8(o);
+        *reinterpret_cast<uint4*>(dx + off) = pk;
+        unpack8(pk, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += o[j];
+      }
+    }
   }
   float* p = partial + (size_t)blockIdx.y * cols + c;
 #pragma unroll
@@ -301,8 +332,8 @@ __global__ void ce_lse_kernel(const float* __restrict__ m, const float* __restri
 MX_EXPORT int mx_bias_gelu_fwd(const void* x, const void* bias, void* y, int rows, int cols,
                                hipStream_t s) {
   const int64_t n = (int64_t)rows * cols;
-  int64_t blocks = (n / 8 + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
+  if (n % 8) return hipErrorInvalidValue;
+  const int64_t blocks = (n / 8 + 256 * kGeluFV - 1) / (256 * kGeluFV);
   hipLaunchKernelGGL(bias_gelu_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
                      (const uint16_t*)x, (const uint16_t*)bias, (uint16_t*)y, n, cols);
   return hipGetLastError();

@@ -154,27 +154,46 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   for (int i = 0; i < NR; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) { ag[i][j] = 0.f; ab[i][j] = 0.f; ax[i][j] = 0.f; }
-  for (int row = wid; row < rows; row += nw) {
-    const size_t base = (size_t)row * cols;
-    const float mean = RMS ? 0.f : mean_in[row];
-    const float rstd = rstd_in[row];
-    float xh[NV][8], gy[NV][8];
-    float s1 = 0.f, s2 = 0.f;
-    // the residual gradient is loaded with h and dy, before the row reductions, so its
-    // HBM latency overlaps theirs instead of following the two wave_sum()s
-    uint4 rraw[NV];
+  // Software pipeline: the next row's h / dy / dres (and statistics) are loaded before the
+  // current row's math, so every wave keeps two rows of loads in flight (the grid has only
+  // a few waves per SIMD: each wave handles several rows to amortise its column partials).
+  uint4 hraw[NV], draw[NV], rraw[NV];
+  float mean_c = 0.f, rstd_c = 0.f;
+  auto load_row = [&](int row_, uint4 (&hr)[NV], uint4 (&dr)[NV], uint4 (&rr)[NV], float& mn, float& rs)
+      __attribute__((always_inline)) {
+    const size_t b_ = (size_t)row_ * cols;
+    mn = RMS ? 0.f : mean_in[row_];
+    rs = rstd_in[row_];
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (lane + 64 * i) * 8;
-      rraw[i] = (dres && c < cols) ? *reinterpret_cast<const uint4*>(dres + base + c) : make_uint4(0, 0, 0, 0);
+      const bool ok = c < cols;
+      hr[i] = ok ? *reinterpret_cast<const uint4*>(h + b_ + c) : make_uint4(0, 0, 0, 0);
+      dr[i] = ok ? *reinterpret_cast<const uint4*>(dy + b_ + c) : make_uint4(0, 0, 0, 0);
+      rr[i] = (dres && ok) ? *reinterpret_cast<const uint4*>(dres + b_ + c) : make_uint4(0, 0, 0, 0);
     }
+  };
+  if (wid < rows) load_row(wid, hraw, draw, rraw, mean_c, rstd_c);
+  for (int row = wid; row < rows; row += nw) {
+    const size_t base = (size_t)row * cols;
+    const float mean = mean_c;
+    const float rstd = rstd_c;
+    uint4 hcur[NV], dcur[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) { hcur[i] = hraw[i]; dcur[i] = draw[i]; }
+    uint4 rcur[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) rcur[i] = rraw[i];
+    if (row + nw < rows) load_row(row + nw, hraw, draw, rraw, mean_c, rstd_c);
+    float xh[NV][8], gy[NV][8];
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (lane + 64 * i) * 8;
       if (c < cols) {
         float hv[8], dv[8];
-        unpack8(*reinterpret_cast<const uint4*>(h + base + c), hv);
-        unpack8(*reinterpret_cast<const uint4*>(dy + base + c), dv);
+        unpack8(hcur[i], hv);
+        unpack8(dcur[i], dv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[i][j] = (hv[j] - mean) * rstd;
@@ -201,7 +220,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       const int c = (lane + 64 * i) * 8;
       if (c < cols) {
         float r[8], o[8];
-        unpack8(rraw[i], r);   // zeros when there is no residual gradient
+        unpack8(rcur[i], r);   // zeros when there is no residual gradient
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = r[j] + rstd * (gy[i][j] - m1 - xh[i][j] * m2);
         *reinterpret_cast<uint4*>(dh_out + base + c) = pack8(o);
@@ -266,32 +285,34 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 //            [nvec][cols] layout goes to output k = c / cols.
 namespace {
 // One-launch deterministic column reduction of fp32 partial rows [P][nvec*cols] into up to
-// three bf16 vectors.  Block = 8 waves over 64 columns (lane = column, 256-B coalesced
-// row reads); wave w sums rows w, w+8, ... with 8 loads in flight, then the 8 wave sums
-// are folded in LDS in a fixed order.  (The previous two-level l1/l2 pair cost two
-// latency-bound launches per norm backward.)
-__global__ __launch_bounds__(512) void colreduce_kernel(const float* __restrict__ in, int P, int cols, int nvec,
+// three bf16 vectors.  Block = 4 waves over 16 columns: thread t sums column t & 15 over the
+// rows of phase t >> 4 (rows ph, ph + 16, ...; 8 loads in flight, 64-B row segments), then
+// the 16 phase sums are folded in LDS in a fixed order.  16 columns per block give
+// C / 16 workgroups (192 for a 3 x 1024 LN backward): 64 columns per block left all but
+// 48 CUs idle on these ~3-6 MB reductions.
+__global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict__ in, int P, int cols, int nvec,
                                                         uint16_t* __restrict__ o0, uint16_t* __restrict__ o1,
                                                         uint16_t* __restrict__ o2, int accumulate) {
-  __shared__ float part[8][64];
+  __shared__ float part[16][17];
   const int C = nvec * cols;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int cl = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < C) {
-    int p = w;
-    for (; p + 56 < P; p += 64) {
+    int p = ph;
+    for (; p + 112 < P; p += 128) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] += in[(size_t)(p + 8 * j) * C + c];
+      for (int j = 0; j < 8; ++j) a[j] += in[(size_t)(p + 16 * j) * C + c];
     }
-    for (; p < P; p += 8) a[0] += in[(size_t)p * C + c];
+    for (; p < P; p += 16) a[0] += in[(size_t)p * C + c];
   }
-  part[w][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  part[ph][cl] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   __syncthreads();
-  if (w == 0 && c < C) {
+  if (ph == 0 && c < C) {
+    const int lane = cl;
     float t = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) t += part[k][lane];
+    for (int k = 0; k < 16; ++k) t += part[k][lane];
     const int k = c / cols, cc = c % cols;
     uint16_t* o = k == 0 ? o0 : (k == 1 ? o1 : o2);
     if (o) {
@@ -310,11 +331,19 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(
   if (c >= cols) return;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int r1 = min(rows, r0 + rows_per_block);
-  for (int r = r0; r < r1; ++r) {
-    float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(x + (size_t)r * cols + c), v);
+  constexpr int G = 4;   // rows per group, loads issued together (memory-level parallelism)
+  for (int r = r0; r < r1; r += G) {
+    uint4 raw[G];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    for (int u = 0; u < G; ++u)
+      raw[u] = r + u < r1 ? *reinterpret_cast<const uint4*>(x + (size_t)(r + u) * cols + c) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      float v[8];
+      unpack8(raw[u], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
   }
   float* o = partial + (size_t)blockIdx.y * cols + c;
 #pragma unroll
@@ -393,8 +422,11 @@ __global__ __launch_bounds__(256) void ln_bwd_cols_kernel(
 int kSplitCols = 2048;   // wider rows: row kernel without column sums + column kernel
 constexpr int kColsRowsPerBlock = 32;
 
+int kBwdRowsPerWave = 4;   // (2 before the row pipeline: 512 blocks' column partials cost
+                           //  as much as the rows at 4096 x 1024)
 int bwd_grid(int rows) {
-  int g = (rows + 7) / 8;  // 2 rows per wave
+  const int rpb = 4 * kBwdRowsPerWave;
+  int g = (rows + rpb - 1) / rpb;
   if (g > 512) g = 512;
   if (g < 1) g = 1;
   return g;
@@ -456,6 +488,12 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
 
 // number of partial slabs the norm backward writes (caller sizes `partial`)
 MX_EXPORT int mx_norm_bwd_nparts(int rows) { return bwd_grid(rows); }
+// rows per wave of the fused (register-partial) backward; returns the old value
+MX_EXPORT int mx_norm_bwd_rows_per_wave(int r) {
+  const int old = kBwdRowsPerWave;
+  if (r > 0) kBwdRowsPerWave = r;
+  return old;
+}
 // rows wider than this use the split (row + column) backward; returns the old value
 MX_EXPORT int mx_norm_split_cols(int c) {
   const int old = kSplitCols;
@@ -474,7 +512,7 @@ MX_EXPORT int mx_colsum_finalize(const float* partial, int nparts, int cols, int
                                  hipStream_t s) {
   (void)scratch;  // single-level reduction: no scratch needed (kept for ABI stability)
   const int C = nvec * cols;
-  hipLaunchKernelGGL(colreduce_kernel, dim3((C + 63) / 64), dim3(512), 0, s, partial, nparts, cols, nvec,
+  hipLaunchKernelGGL(colreduce_kernel, dim3((C + 15) / 16), dim3(256), 0, s, partial, nparts, cols, nvec,
                      (uint16_t*)o0, (uint16_t*)o1, (uint16_t*)o2, accumulate);
   return hipGetLastError();
 }

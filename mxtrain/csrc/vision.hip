@@ -664,7 +664,18 @@ __global__ __launch_bounds__(64) void nms_mask_kernel(const float4* __restrict__
   mask[((size_t)p * N + i) * NB + cb] = bits;
 }
 
-// one wave per problem; lane w owns removed-word w (NB <= 64 -> N <= 4096)
+// one wave per problem; lane w owns removed-word w (NB <= NBM <= 64 -> N <= 64 NBM)
+//
+// Chunks of 64 boxes.  The chunk's 64 mask rows (only their words cw .. NB-1 matter: the
+// mask is upper-triangular) are loaded into registers one chunk AHEAD -- issued before the
+// current chunk's serial scan, so their L2 latency hides behind it -- and staged in LDS.
+// (Loading each chunk's rows with a load -> ds_write loop after the previous chunk had
+// finished serialised ~NB dependent L2 round trips per chunk: ~0.5 ms for the 5 x 2000-box
+// RPN problems of a training step.)  The serial keep/suppress decision reads each row's
+// word of the chunk itself with a scalar readlane (SALU chain, surviving candidates only);
+// the kept rows' suppression of later
+// chunks is OR-ed in parallel (lane w owns word w) with a fully unrolled, branch-free pass.
+template <int NBM>
 __global__ __launch_bounds__(64) void nms_keep_kernel(const unsigned long long* __restrict__ mask,
                                                       const int* __restrict__ counts, int N, int NB,
                                                       int max_out, int* __restrict__ keep,
@@ -672,43 +683,63 @@ __global__ __launch_bounds__(64) void nms_keep_kernel(const unsigned long long* 
   const int p = blockIdx.x;
   const int lane = threadIdx.x;
   const int n = counts ? counts[p] : N;
-  // The 64 mask rows of the current chunk are staged in LDS with one coalesced batch of
-  // loads.  The serial keep/suppress decision inside a chunk only needs each row's word
-  // for the chunk itself: lane ii holds row ii's word, and the scan reads it with a
-  // scalar readlane, so the dependent chain is a few SALU ops per box (no LDS round trip).
-  // The kept rows' suppression of later chunks is then OR-ed in parallel (lane w owns
-  // word w of the distributed removed-mask), off the serial path.
-  __shared__ unsigned long long rows[64 * 64];
+  __shared__ unsigned long long rows[64 * NBM];
   unsigned long long removed = 0ull;
   int out = 0;
   const unsigned long long* m = mask + (size_t)p * N * NB;
+  // lane's share of a chunk: flat indices k = lane + 64 q of [cn rows][NB words]
+  unsigned long long pre[NBM];
+  auto fetch = [&](int c0) __attribute__((always_inline)) {
+    const int cn = min(64, n - c0), cw = c0 >> 6;
+#pragma unroll
+    for (int q = 0; q < NBM; ++q) {
+      const int k = lane + 64 * q;
+      const int r = k / NB, w = k - (k / NB) * NB;
+      pre[q] = (q < NB && r < cn && w >= cw) ? m[(size_t)c0 * NB + k] : 0ull;
+    }
+  };
+  if (n > 0) fetch(0);
   for (int c0 = 0; c0 < n && out < max_out; c0 += 64) {
     const int cn = min(64, n - c0);
-    for (int k = lane; k < cn * NB; k += 64) rows[k] = m[(size_t)c0 * NB + k];
+#pragma unroll
+    for (int q = 0; q < NBM; ++q)
+      if (q < NB) rows[lane + 64 * q] = pre[q];
     __syncthreads();
+    if (c0 + 64 < n) fetch(c0 + 64);      // next chunk in flight during this one's scan
     const int cw = c0 >> 6;
     const unsigned long long intra = lane < cn ? rows[lane * NB + cw] : 0ull;
     const unsigned lo = (unsigned)intra, hi = (unsigned)(intra >> 32);
-    unsigned long long word = __shfl(removed, cw);
+    // the scan runs on SCALAR registers: the removed word is made wave-uniform with
+    // readfirstlane (a __shfl result is a VGPR to the divergence analysis, which had turned
+    // the whole chain into exec-masked vector code at ~350 cycles per box); it visits only
+    // the surviving candidates (lowest first): kept |= ii, candidates &= ~row(ii)
+    const unsigned long long word = __shfl(removed, cw);
+    unsigned long long avail =
+        ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(word >> 32)) << 32) |
+        (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)word);
+    avail = ~avail & (cn == 64 ? ~0ull : ((1ull << cn) - 1ull));
     unsigned long long kept = 0ull;
-    int room = max_out - out;
-    for (int ii = 0; ii < cn && room > 0; ++ii) {
-      if ((word >> ii) & 1ull) continue;
+    int room = __builtin_amdgcn_readfirstlane(max_out - out);
+    while (avail && room > 0) {
+      const int ii = __builtin_ctzll(avail);
       kept |= 1ull << ii;
       --room;
-      word |= ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)hi, ii) << 32) |
-              (unsigned)__builtin_amdgcn_readlane((int)lo, ii);
+      avail &= avail - 1ull;
+      const unsigned long long row = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)hi, ii) << 32) |
+                                     (unsigned)__builtin_amdgcn_readlane((int)lo, ii);
+      avail &= ~row;
     }
     if ((kept >> lane) & 1ull)
       keep[(size_t)p * max_out + out + __popcll(kept & ((1ull << lane) - 1ull))] = c0 + lane;
     out += __popcll(kept);
-    if (lane < NB) {
-      unsigned long long k = kept;
-      while (k) {
-        const int ii = __ffsll((long long)k) - 1;
-        k &= k - 1ull;
-        removed |= rows[ii * NB + lane];
+    if (lane < NB && lane > cw) {
+      unsigned long long acc = removed;
+#pragma unroll
+      for (int ii = 0; ii < 64; ++ii) {
+        const unsigned long long sel = 0ull - ((kept >> ii) & 1ull);   // all-ones if row ii kept
+        if (ii < cn) acc |= rows[ii * NB + lane] & sel;
       }
+      removed = acc;
     }
     __syncthreads();
   }
@@ -998,8 +1029,15 @@ MX_EXPORT int mx_nms(const float* boxes, const int* counts, int P, int N, float 
   if (P == 0 || N == 0) return hipSuccess;
   hipLaunchKernelGGL(nms_mask_kernel, dim3(NB, NB, P), dim3(64), 0, s, (const float4*)boxes, counts, N, NB, thr,
                      (unsigned long long*)mask_ws);
-  hipLaunchKernelGGL(nms_keep_kernel, dim3(P), dim3(64), 0, s, (const unsigned long long*)mask_ws, counts, N, NB,
-                     max_out, keep, nkeep);
+  if (NB <= 16)
+    hipLaunchKernelGGL(nms_keep_kernel<16>, dim3(P), dim3(64), 0, s, (const unsigned long long*)mask_ws, counts, N,
+                       NB, max_out, keep, nkeep);
+  else if (NB <= 32)
+    hipLaunchKernelGGL(nms_keep_kernel<32>, dim3(P), dim3(64), 0, s, (const unsigned long long*)mask_ws, counts, N,
+                       NB, max_out, keep, nkeep);
+  else
+    hipLaunchKernelGGL(nms_keep_kernel<64>, dim3(P), dim3(64), 0, s, (const unsigned long long*)mask_ws, counts, N,
+                       NB, max_out, keep, nkeep);
   return hipGetLastError();
 }
 

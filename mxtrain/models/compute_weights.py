@@ -23,6 +23,7 @@ included: their modules keep caching their own copies (resnet.ConvNorm._folded).
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -125,3 +126,273 @@ class ComputeWeights:
         for p, _ in self.specs:
             _ACTIVE.pop(id(p), None)
         return False
+
+
+# ------------------------------------------------------------------------- flat master
+def _align8(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+class _FlatCast(torch.autograd.Function):
+    """Forward: the FlatMaster's persistent compute copies (refreshed by the optimizer
+    pass, re-cast only when stale); backward: every gradient into the flat fp32 buffer in
+    one launch (returned as views of it)."""
+
+    @staticmethod
+    def forward(ctx, fm, *params):
+        ctx.fm = fm
+        fm.ensure_fresh()
+        return tuple(fm.compute_views())
+
+    @staticmethod
+    def backward(ctx, *grads):
+        return (None, *ctx.fm.grads_in(grads))
+
+
+class FlatMaster:
+    """Flat fp32 master weights, gradients and SGD momentum for a single-process training
+    loop, plus persistent bf16 compute copies (folded FrozenBN scale applied, conv weights
+    channels_last) written by the optimizer pass itself (csrc/multitensor.hip):
+
+        forward   no cast kernels (the copies are current)
+        backward  1 launch: bf16 grads -> flat fp32 grads (x fold scale) + sum-of-squares
+                  partials, 1 launch: ||g||^2
+        optimizer 1 launch: clip + SGD momentum + compute-copy refresh
+
+    torch.optim.SGD semantics (dampening 0, no Nesterov, per-group weight decay) and
+    torch.nn.utils.clip_grad_norm_'s coefficient; the SGD instance keeps its param groups
+    and its momentum buffers (views of the flat buffer), so state_dict() and checkpoints
+    are unchanged (call ``rebind_state()`` after ``opt.load_state_dict``).  Parameters
+    become views of the flat buffer (``p.data``), so in-place writes (checkpoint load)
+    land in it and bump the versions that mark the copies stale.
+    """
+
+    def __init__(self, model, opt: torch.optim.SGD, clip: float, dt: torch.dtype = torch.bfloat16):
+        from ..ops import _lib
+        self.model, self.opt, self.dt = model, opt, dt
+        mom = {g["momentum"] for g in opt.param_groups}
+        wds = {float(g["weight_decay"]) for g in opt.param_groups} - {0.0}
+        assert len(mom) == 1 and len(wds) <= 1, "one momentum and one non-zero weight decay"
+        assert all(not g.get("nesterov") and not g.get("dampening") for g in opt.param_groups)
+        self.params, wdf = [], []
+        for g in opt.param_groups:
+            for p in g["params"]:
+                if p.requires_grad:
+                    self.params.append(p)
+                    wdf.append(1 if g["weight_decay"] else 0)
+        dev = self.params[0].device
+        self.device = dev
+        self.cuda = dev.type == "cuda"
+        self.chunk = _lib.query("mx_mt_chunk") if self.cuda else 2048
+        self.sizes = [p.numel() for p in self.params]
+        self.offs, off = [], 0
+        for n in self.sizes:
+            self.offs.append(off)
+            off += _align8(n)
+        total = max(off, 8)
+        self.P = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.G = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.M = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.W = torch.zeros(total, dtype=dt, device=dev)
+        with torch.no_grad():
+            for p, o, n in zip(self.params, self.offs, self.sizes):
+                self.P[o:o + n].copy_(p.detach().reshape(-1))
+                p.data = self.P[o:o + n].view(p.shape)
+        self.rebind_state()
+        # layout: fp32 [d0, d1, inner]; bf16 copy channels_last for 4-D weights
+        self.geo = []
+        for p in self.params:
+            s = p.shape
+            d0 = s[0] if p.dim() >= 1 else 1
+            d1 = s[1] if p.dim() >= 2 else 1
+            inner = int(torch.Size(s[2:]).numel()) if p.dim() >= 3 else 1
+            self.geo.append((d0, d1, inner, 1 if p.dim() == 4 else 0))
+        nb = [(n + self.chunk - 1) // self.chunk for n in self.sizes]
+        self.bstart_host = [0]
+        for k in nb:
+            self.bstart_host.append(self.bstart_host[-1] + k)
+        self.nblocks = self.bstart_host[-1]
+        bmap = [t for t, k in enumerate(nb) for _ in range(k)]
+        self.bmap = torch.tensor(bmap or [0], dtype=torch.int32, device=dev)
+        self.bstart = torch.tensor(self.bstart_host, dtype=torch.int32, device=dev)
+        self._bstart_arr = ctypes_int_array(self.bstart_host)   # kept alive: its address is passed
+        self.bstart_c = ctypes.addressof(self._bstart_arr)
+        self.wdf = wdf
+        self.scales: List[Optional[torch.Tensor]] = [None] * len(self.params)
+        self._scale_key = None
+        self.tab = torch.zeros(len(self.params), 8, dtype=torch.int64, device=dev)
+        self.hyper = torch.zeros(4, dtype=torch.float32, device=dev)
+        self.hyper[1] = float(mom.pop())
+        self.hyper[2] = float(wds.pop()) if wds else 0.0
+        self.hyper[3] = float(clip or 0.0)
+        self.lr = self.hyper[0:1].view(())   # device scalar: fill_ before a (graph) step
+        self.normsq = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.partial = torch.zeros(max(self.nblocks, 1), dtype=torch.float32, device=dev)
+        self.zero_bf16 = torch.zeros(_align8(max(self.sizes)), dtype=dt, device=dev)
+        self._wkey = None
+        self._cw_specs = None
+
+    # -------------------------------------------------------------- optimizer state
+    def rebind_state(self) -> None:
+        """Momentum buffers as views of the flat buffer (after construction or after
+        ``opt.load_state_dict``, which installs fresh tensors)."""
+        with torch.no_grad():
+            for p, o, n in zip(self.params, self.offs, self.sizes):
+                st = self.opt.state[p]
+                buf = st.get("momentum_buffer")
+                view = self.M[o:o + n].view(p.shape)
+                if buf is not None and buf.data_ptr() != view.data_ptr():
+                    view.copy_(buf)
+                st["momentum_buffer"] = view
+
+    # -------------------------------------------------------------- fold scales
+    def refresh_scales(self) -> None:
+        specs = self.model.compute_weight_specs()
+        if specs is self._cw_specs:
+            return
+        self._cw_specs = specs
+        full = {id(p): s for p, s in specs}
+        scales = []
+        for p, (d0, _, _, _) in zip(self.params, self.geo):
+            s = full.get(id(p))
+            scales.append(None if s is None else s.reshape(d0, -1)[:, 0].float().contiguous())
+        self.scales = scales
+        rows = []
+        for t, (p, o, n) in enumerate(zip(self.params, self.offs, self.sizes)):
+            d0, d1, inner, cl = self.geo[t]
+            sp = scales[t].data_ptr() if (scales[t] is not None and self.cuda) else 0
+            rows.append([o, n, d0, d1, inner, cl, sp, self.wdf[t]])
+        self.tab.copy_(torch.tensor(rows, dtype=torch.int64))
+        self._scale_key = object()   # new identity: the copies must be re-cast
+
+    def _key(self):
+        return (tuple(p._version for p in self.params), self._scale_key)
+
+    # -------------------------------------------------------------- compute copies
+    def compute_views(self) -> List[torch.Tensor]:
+        outs = []
+        for p, o, n, (d0, d1, inner, cl) in zip(self.params, self.offs, self.sizes, self.geo):
+            v = self.W[o:o + n]
+            if cl:
+                kh, kw = p.shape[2], p.shape[3]
+                outs.append(v.view(d0, kh, kw, d1).permute(0, 3, 1, 2))
+            else:
+                outs.append(v.view(p.shape))
+        return outs
+
+    def ensure_fresh(self) -> None:
+        self.refresh_scales()
+        key = self._key()
+        if key == self._wkey:
+            return
+        if self.cuda:
+            from ..ops import _lib
+            _lib.call("mx_mt_cast", self.tab.data_ptr(), self.bmap.data_ptr(), self.bstart.data_ptr(),
+                      self.nblocks, self.P.data_ptr(), self.W.data_ptr(), _lib.stream())
+        else:
+            with torch.no_grad():
+                for p, v, s in zip(self.params, self.compute_views(), self.scales):
+                    w = p.detach() if s is None else p.detach() * s.view(-1, *([1] * (p.dim() - 1)))
+                    v.copy_(w)
+        self._wkey = key
+
+    def compute_weights(self):
+        """Context manager registering the compute copies for ``cw()`` (one autograd
+        node; under no_grad the copies are plain views)."""
+        fm = self
+
+        class _Ctx:
+            def __enter__(self_):
+                if torch.is_grad_enabled():
+                    outs = _FlatCast.apply(fm, *fm.params)
+                else:
+                    fm.ensure_fresh()
+                    outs = fm.compute_views()
+                for p, o in zip(fm.params, outs):
+                    _ACTIVE[id(p)] = o
+                return self_
+
+            def __exit__(self_, *exc):
+                for p in fm.params:
+                    _ACTIVE.pop(id(p), None)
+                return False
+        return _Ctx()
+
+    # -------------------------------------------------------------- backward / step
+    def grads_in(self, grads) -> List[torch.Tensor]:
+        srcs = []
+        keep = []
+        for t, (g, p) in enumerate(zip(grads, self.params)):
+            d0, d1, inner, cl = self.geo[t]
+            if g is None:
+                srcs.append(None)
+                continue
+            if cl and inner > 1:
+                if not g.is_contiguous(memory_format=torch.channels_last):
+                    g = g.contiguous(memory_format=torch.channels_last)
+            elif not g.is_contiguous() and not (cl and g.is_contiguous(memory_format=torch.channels_last)):
+                g = g.contiguous()
+            if g.dtype != self.dt:
+                g = g.to(self.dt)
+            if self.cuda and g.data_ptr() % 16:
+                g = g.clone(memory_format=torch.channels_last if (cl and inner > 1) else torch.contiguous_format)
+            keep.append(g)
+            srcs.append(g)
+        if self.cuda:
+            from ..ops import _lib
+            ptrs = [(s.data_ptr() if s is not None else self.zero_bf16.data_ptr()) for s in srcs]
+            arr = ctypes_int64_array(ptrs)
+            _lib.call("mx_mt_grad_in", self.tab.data_ptr(), self.bmap.data_ptr(), self.bstart.data_ptr(),
+                      self.bstart_c, len(ptrs), ctypes.addressof(arr), self.G.data_ptr(), self.partial.data_ptr(),
+                      _lib.stream())
+            _lib.call("mx_mt_sumsq_fin", self.partial.data_ptr(), self.nblocks, self.normsq.data_ptr(),
+                      _lib.stream())
+        else:
+            with torch.no_grad():
+                acc = torch.zeros((), dtype=torch.float32)
+                for t, (s, p) in enumerate(zip(srcs, self.params)):
+                    o, n = self.offs[t], self.sizes[t]
+                    gv = torch.zeros(p.shape) if s is None else s.float()
+                    if self.scales[t] is not None:
+                        gv = gv * self.scales[t].view(-1, *([1] * (p.dim() - 1)))
+                    self.G[o:o + n].copy_(gv.reshape(-1) if gv.is_contiguous() else gv.contiguous().reshape(-1))
+                    acc = acc + gv.pow(2).sum()
+                self.normsq.fill_(float(acc))
+        return [self.G[o:o + n].view(p.shape) for p, o, n in zip(self.params, self.offs, self.sizes)]
+
+    def step(self, lr=None) -> None:
+        """clip + SGD momentum + compute-copy refresh (lr: float, or None when the
+        device scalar ``self.lr`` was filled already -- graph replay)."""
+        if lr is not None:
+            self.lr.fill_(float(lr))
+        if self.cuda:
+            from ..ops import _lib
+            _lib.call("mx_mt_sgd", self.tab.data_ptr(), self.bmap.data_ptr(), self.bstart.data_ptr(), self.nblocks,
+                      self.P.data_ptr(), self.G.data_ptr(), self.M.data_ptr(), self.W.data_ptr(),
+                      self.hyper.data_ptr(), self.normsq.data_ptr(), _lib.stream())
+        else:
+            with torch.no_grad():
+                lr_, mom, wd, clip = (float(x) for x in self.hyper.tolist())
+                cc = 1.0
+                if clip > 0:
+                    cc = min(1.0, clip / (float(self.normsq[0]) ** 0.5 + 1e-6))
+                n_all = self.P.numel()
+                wdv = torch.zeros(n_all)
+                for t, (o, n) in enumerate(zip(self.offs, self.sizes)):
+                    if self.wdf[t]:
+                        wdv[o:o + n] = wd
+                d = self.G * cc + wdv * self.P
+                self.M.mul_(mom).add_(d)
+                self.P.sub_(lr_ * self.M)
+                for p, v, s in zip(self.params, self.compute_views(), self.scales):
+                    w = p.detach() if s is None else p.detach() * s.view(-1, *([1] * (p.dim() - 1)))
+                    v.copy_(w)
+        self._wkey = self._key()
+
+
+def ctypes_int64_array(vals):
+    return (ctypes.c_int64 * len(vals))(*vals)
+
+
+def ctypes_int_array(vals):
+    return (ctypes.c_int * len(vals))(*vals)

@@ -372,6 +372,10 @@ class MaskRCNN(nn.Module):
                 gt_mask_table=None):
         if images.device.type != "cuda" or not torch.is_grad_enabled():
             return self._forward(images, img_hw, gt_boxes, gt_labels, gt_count, gt_masks, gt_mask_table)
+        fm = self.__dict__.get("_flat_master")
+        if fm is not None:   # persistent compute copies kept current by the fused optimizer
+            with fm.compute_weights():
+                return self._forward(images, img_hw, gt_boxes, gt_labels, gt_count, gt_masks, gt_mask_table)
         # under data parallelism several cast nodes, so gradient buckets become ready in
         # backward order (all-reduce overlapped with backward); one node on a single GPU
         groups = 8 if (torch.distributed.is_available() and torch.distributed.is_initialized()

@@ -31,6 +31,7 @@ SIGNATURES = {
     "mx_norm_bwd_nparts": [I],
     "mx_norm_bwd_nparts2": [I, I],
     "mx_norm_split_cols": [I],
+    "mx_norm_bwd_rows_per_wave": [I],
     "mx_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],
     "mx_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
     "mx_bda_norm_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, F, P, U32, I, P],
@@ -54,6 +55,13 @@ SIGNATURES = {
     "mx_ce_stats": [P, P, I, I, I64, P, P, P, P],
     "mx_ce_lse": [P, P, P, I, P],
     "mx_ce_grad": [P, P, I, I, I64, P, P, P, P, F, I, P],
+    # multitensor.hip
+    "mx_mt_chunk": [],
+    "mx_mt_max_tensors": [],
+    "mx_mt_grad_in": [P, P, P, P, I, P, P, P, P],
+    "mx_mt_sumsq_fin": [P, I, P, P],
+    "mx_mt_sgd": [P, P, P, I, P, P, P, P, P, P, P],
+    "mx_mt_cast": [P, P, P, I, P, P, P],
     # optim.hip
     "mx_sumsq_nparts": [],
     "mx_sumsq_bf16": [P, I64, F, P, P, P, I, P],

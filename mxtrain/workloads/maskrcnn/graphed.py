@@ -71,10 +71,13 @@ def sgd_momentum_(opt: torch.optim.SGD, lr) -> None:
 
 class GraphedTrainStep:
     def __init__(self, model, opt: torch.optim.SGD, params: List[torch.Tensor], clip: float, device,
-                 flat_capacity: int = 16 << 20):
+                 flat_capacity: int = 16 << 20, flat_master=None):
         self.model, self.opt, self.params, self.clip, self.device = model, opt, params, clip, device
         self.graphs: Dict[tuple, tuple] = {}
-        self.lr = torch.zeros((), dtype=torch.float32, device=device)
+        # with a FlatMaster (models/compute_weights.py) the update is its fused clip + SGD
+        # launch and the learning rate its device scalar
+        self.fm = flat_master
+        self.lr = flat_master.lr if flat_master is not None else torch.zeros((), dtype=torch.float32, device=device)
         self.pool = torch.cuda.graph_pool_handle()
         self.stream = torch.cuda.Stream(device)
         self.flat = torch.zeros(flat_capacity, dtype=torch.uint8, device=device)
@@ -94,9 +97,12 @@ class GraphedTrainStep:
         losses = self.model(st["images"], st["hw"], st["gt_boxes"], st["gt_labels"], st["gt_count"], self.flat,
                             st["gt_mask_table"])
         losses["total_loss"].backward()
-        if self.clip > 0:
-            torch.nn.utils.clip_grad_norm_(self.params, self.clip, foreach=True)
-        sgd_momentum_(self.opt, self.lr)
+        if self.fm is not None:
+            self.fm.step()
+        else:
+            if self.clip > 0:
+                torch.nn.utils.clip_grad_norm_(self.params, self.clip, foreach=True)
+            sgd_momentum_(self.opt, self.lr)
         return torch.stack([losses[k].detach().float() for k in LOSS_NAMES])
 
     def _ensure_capacity(self, n: int) -> None:

@@ -332,9 +332,17 @@ def main(argv=None):
     params = decay + no_decay
     clip = float(cfg.TRAIN.GRADIENT_CLIP or 0.0)
     gstep = None
+    fm = None
+    if world == 1 and device.type == "cuda" and os.environ.get("MXTRAIN_FLAT_SGD", "1") != "0":
+        # flat fp32 master / grads / momentum + persistent bf16 compute copies: one launch
+        # each for the gradient cast, its norm and the clip + SGD + copy refresh
+        from mxtrain.models.compute_weights import FlatMaster
+        fm = FlatMaster(model, opt, clip)
+        model.__dict__["_flat_master"] = fm
+        log("Optimizer: fused flat SGD-momentum (+ clip, + bf16 compute copies)")
     if use_graph:
         from mxtrain.workloads.maskrcnn.graphed import GraphedTrainStep
-        gstep = GraphedTrainStep(model, opt, params, clip, device)
+        gstep = GraphedTrainStep(model, opt, params, clip, device, flat_master=fm)
         log("Training step runs as a hipGraph (one graph per input shape)")
     max_steps = args.mx_max_steps
     timed_imgs, t_timed = 0, None
@@ -365,9 +373,12 @@ def main(argv=None):
                                 d.get("gt_mask_flat", d.get("gt_masks")), d.get("gt_mask_table"))
                 opt.zero_grad(set_to_none=True)
                 losses["total_loss"].backward()
-                if clip > 0:
-                    torch.nn.utils.clip_grad_norm_(params, clip)
-                opt.step()
+                if fm is not None:
+                    fm.step(lr)
+                else:
+                    if clip > 0:
+                        torch.nn.utils.clip_grad_norm_(params, clip)
+                    opt.step()
             t_c = time.time()
             if t_timed is not None:   # host-side accounting: loader wait vs enqueue time
                 t_wait += t_b - t_a

@@ -122,6 +122,12 @@ def main():
             _lib._QCACHE.clear()
         rec("bda_ln_fwd 4096x1024", timeit(lambda: N.bda_norm_fwd(x, bb, x, g, bb, p=0.1, seed_t=seed)),
             rows * cols * 2 * 4)
+        for rpw in (2, 4, 8):   # rows per wave of the fused backward (row pipeline + partials)
+            old = _lib._fn("mx_norm_bwd_rows_per_wave")(rpw)
+            _lib._QCACHE.clear()
+            rec(f"ln_bwd 4096x1024 rpw{rpw}", timeit(fn), rows * cols * 2 * 5)
+            _lib._fn("mx_norm_bwd_rows_per_wave")(old)
+            _lib._QCACHE.clear()
     if want("norm"):
         x = torch.randn(T, h, device=dev).to(bf)
         r_ = torch.randn(T, h, device=dev).to(bf)

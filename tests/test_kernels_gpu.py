@@ -38,9 +38,8 @@ def _seed():
     assert torch.cuda.is_available()
 
 
-@pytest.mark.parametrize("cols", [768, 1024, 4096, 8192])
-def test_layernorm_fwd_bwd(cols):
-    rows = 512
+@pytest.mark.parametrize("rows,cols", [(512, 768), (512, 1024), (4100, 1024), (512, 4096), (512, 8192)])
+def test_layernorm_fwd_bwd(rows, cols):
     x = _bf(torch.randn(rows, cols))
     g = _bf(1 + 0.1 * torch.randn(cols))
     b = _bf(0.1 * torch.randn(cols))
@@ -90,8 +89,8 @@ def test_bda_norm_with_dropout(rms, cols):
     _close(outs[2], outr[2], 1.0, 3e-2, "dbias")
 
 
-def test_bias_gelu():
-    rows, cols = 512, 4096
+@pytest.mark.parametrize("rows,cols", [(512, 4096), (300, 1000)])
+def test_bias_gelu(rows, cols):
     x = _bf(torch.randn(rows, cols))
     b = _bf(0.1 * torch.randn(cols))
     y = Fu.bias_gelu_fwd(x.to(DEV), b.to(DEV))

@@ -66,3 +66,39 @@ def test_graphed_step_matches_eager(tmp_path):
             assert abs(float(x[k]) - float(y[k])) <= tol * abs(float(x[k])) + 1e-3, \
                 (s, k, float(x[k]), float(y[k]), num / den)
     assert num / den < 1e-3, num / den
+
+
+@pytest.mark.gpu
+def test_flat_master_gpu_matches_cpu():
+    """csrc/multitensor.hip (gradient cast + fold scale + sumsq, clip + SGD + compute-copy
+    refresh) against the FlatMaster's torch path on identical gradients: fp32 master and
+    momentum to fp32 rounding, bf16 copies (channels_last for the convs) to one bf16 ulp."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_flat_master_cpu import Tiny, _opt
+    from mxtrain.models.compute_weights import FlatMaster
+    torch.manual_seed(3)
+    cpu = Tiny()
+    gpu = copy.deepcopy(cpu).cuda()
+    fc = FlatMaster(cpu, _opt(cpu), 0.05, dt=torch.bfloat16)
+    fg = FlatMaster(gpu, _opt(gpu), 0.05, dt=torch.bfloat16)
+    fc.ensure_fresh()
+    fg.ensure_fresh()
+    for step in range(3):
+        views = fc.compute_views()
+        grads = [torch.randn(v.shape).to(torch.bfloat16) for v in views]
+        # the GPU copies' grads in their layout (channels_last conv weights)
+        ggrads = [g.cuda().contiguous(memory_format=torch.channels_last) if g.dim() == 4 else g.cuda()
+                  for g in grads]
+        fc.grads_in(grads)
+        fg.grads_in(ggrads)
+        torch.testing.assert_close(fg.normsq.cpu(), fc.normsq, rtol=1e-5, atol=0)
+        fc.step(0.1 * (step + 1))
+        fg.step(0.1 * (step + 1))
+        torch.cuda.synchronize()
+        torch.testing.assert_close(fg.P.cpu(), fc.P, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(fg.M.cpu(), fc.M, rtol=1e-6, atol=1e-6)
+        for a, b in zip(fg.compute_views(), fc.compute_views()):
+            assert a.shape == b.shape
+            torch.testing.assert_close(a.float().cpu(), b.float(), rtol=8e-3, atol=1e-6)

@@ -132,14 +132,15 @@ def test_roi_align_gpu_fwd_bwd(tiled, out_hw, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_nms_match_decode_gpu():
+@pytest.mark.parametrize("N,max_out", [(2000, 1000), (700, 700), (3000, 3000)])
+def test_nms_match_decode_gpu(N, max_out):
     g = torch.Generator().manual_seed(4)
-    P, N = 5, 2000
+    P = 5
     xy = torch.rand(P, N, 2, generator=g) * 700
     boxes = torch.cat([xy, xy + torch.rand(P, N, 2, generator=g) * 120 + 4], 2)
-    counts = torch.tensor([2000, 1500, 64, 1, 0])
-    kg, ng = V.batched_nms_sorted(boxes.cuda(), counts.cuda(), 0.7, 1000)
-    kc, nc = V.batched_nms_sorted(boxes, counts, 0.7, 1000)
+    counts = torch.tensor([N, min(N, 1500), 64, 1, 0])
+    kg, ng = V.batched_nms_sorted(boxes.cuda(), counts.cuda(), 0.7, max_out)
+    kc, nc = V.batched_nms_sorted(boxes, counts, 0.7, max_out)
     assert ng.cpu().tolist() == nc.tolist()
     assert torch.equal(kg.cpu(), kc)
     anchors = boxes[0]
