@@ -30,6 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.epilogue import conv_bias_act, conv_transpose_bias_act
+from ..ops import detloss as D
 from ..ops import vision as V
 from .compute_weights import ComputeWeights, cw
 from .resnet import ConvNorm, resnet50
@@ -166,8 +167,9 @@ class BoxHead(nn.Module):
         x = x.reshape(x.shape[0], -1)
         x = F.relu(F.linear(x, cw(self.fc1.weight, dt), cw(self.fc1.bias, dt)), inplace=True)
         x = F.relu(F.linear(x, cw(self.fc2.weight, dt), cw(self.fc2.bias, dt)), inplace=True)
-        return (F.linear(x, cw(self.cls.weight, dt), cw(self.cls.bias, dt)).float(),
-                F.linear(x, cw(self.box.weight, dt), cw(self.box.bias, dt)).float().view(x.shape[0], -1, 4))
+        # compute-dtype logits [R, C] and deltas [R, C * 4] (the fused losses read bf16)
+        return (F.linear(x, cw(self.cls.weight, dt), cw(self.cls.bias, dt)),
+                F.linear(x, cw(self.box.weight, dt), cw(self.box.bias, dt)))
 
 
 class MaskHead(nn.Module):
@@ -251,15 +253,10 @@ class MaskRCNN(nn.Module):
     def rpn_losses(self, logits, deltas, anchors, gt_boxes, gt_count, img_hw):
         cfg = self.cfg
         sel_pos, sel_neg, tgt = self.rpn_targets(anchors, gt_boxes, gt_count, img_hw)
-        sel = sel_pos | sel_neg
-        lab = sel_pos.float()
-        nsel = sel.sum().clamp(min=1).float()
-        cls_loss = (F.binary_cross_entropy_with_logits(logits.float(), lab, reduction="none") * sel).sum() / nsel
         B = logits.shape[0]
         enc = V.encode_boxes(anchors[None].expand(B, -1, -1).reshape(-1, 4), tgt.reshape(-1, 4)).view(B, -1, 4)
-        box = huber(deltas.float() - enc, 1.0 / 9).sum(-1)
-        box_loss = (box * sel_pos).sum() / (B * cfg.rpn_batch_per_im)
-        return cls_loss, box_loss
+        # BCE over the sampled anchors / #sampled, huber(1/9) over the positives / (B * 256)
+        return D.rpn_loss(logits, deltas, enc, sel_pos, sel_neg, B * cfg.rpn_batch_per_im)
 
     @torch.no_grad()
     def proposals(self, logits_lv, deltas_lv, anchors_lv, img_hw, training: bool):
@@ -268,22 +265,11 @@ class MaskRCNN(nn.Module):
         B = logits_lv[0].shape[0]
         pre = cfg.train_per_level_topk if training else cfg.test_per_level_topk
         post = cfg.train_post_nms_topk if training else cfg.test_post_nms_topk
-        boxes_all, scores_all, counts = [], [], []
-        for lg, dl, an in zip(logits_lv, deltas_lv, anchors_lv):
-            k = min(pre, lg.shape[1])
-            sc, idx = lg.float().topk(k, dim=1)                                # sorted desc
-            d = torch.gather(dl.float(), 1, idx[..., None].expand(-1, -1, 4))
-            ref = an[idx.reshape(-1)]
-            bx = V.decode_boxes(ref, d.reshape(-1, 4), (1.0, 1.0, 1.0, 1.0), img_hw, rows_per_img=k).view(B, k, 4)
-            if k < pre:
-                bx = F.pad(bx, (0, 0, 0, pre - k))
-                sc = F.pad(sc, (0, pre - k), value=-float("inf"))
-            boxes_all.append(bx)
-            scores_all.append(sc)
-            counts.append(k)
-        L = len(boxes_all)
-        boxes = torch.stack(boxes_all, 1).reshape(B * L, pre, 4)               # problem = (image, level)
-        scores = torch.stack(scores_all, 1).reshape(B * L, pre)
+        # per (image, level): top-k logits (sorted) + decoded, clipped boxes, -inf padded
+        bxs, scs, counts = V.level_topk_decode(logits_lv, deltas_lv, anchors_lv, img_hw, pre)
+        L = len(counts)
+        boxes = bxs.reshape(B * L, pre, 4)                                       # problem = (image, level)
+        scores = scs.reshape(B * L, pre)
         ck = ("nms_counts", tuple(counts), B, str(boxes.device))
         if ck not in self._anchor_cache:   # (no host->device copy inside a captured step)
             self._anchor_cache[ck] = torch.tensor(counts, dtype=torch.int32, device=boxes.device).repeat(B)
@@ -408,10 +394,8 @@ class MaskRCNN(nn.Module):
         roi_feat = V.roi_align(feats, self._with_batch(rois), (7, 7), scales)
         cls_logits, box_deltas = self.box_head(roi_feat)
         lab = labels.reshape(-1)
-        cls_loss = F.cross_entropy(cls_logits, lab)
-        fgm = is_fg.reshape(-1)
-        pick = torch.gather(box_deltas, 1, lab[:, None, None].expand(-1, 1, 4)).squeeze(1)
-        box_loss = (huber(pick - tgt.reshape(-1, 4), 1.0).sum(-1) * fgm).sum() / (B * N)
+        # softmax CE (mean) + huber(1) of the labelled class's deltas over the fg RoIs / (B * N)
+        cls_loss, box_loss = D.frcnn_loss(cls_logits, box_deltas, lab, tgt.reshape(-1, 4), is_fg.reshape(-1), B * N)
         out = {"rpn_cls_loss": rpn_cls, "rpn_box_loss": rpn_box, "fastrcnn_cls_loss": cls_loss,
                "fastrcnn_box_loss": box_loss}
         if self.mask_head is not None:
@@ -421,8 +405,6 @@ class MaskRCNN(nn.Module):
             fg_lab = labels[:, :nfg].reshape(-1)
             mf = V.roi_align(feats, self._with_batch(fg_rois), (14, 14), scales)
             ml = self.mask_head(mf)                                               # [R, 80, 28, 28]
-            ml = torch.gather(ml, 1, (fg_lab - 1).clamp(min=0)[:, None, None, None].expand(-1, 1, *ml.shape[2:]))
-            ml = ml.squeeze(1).float()
             G = (gt_mask_table if gt_mask_table is not None else gt_masks).shape[1]
             flat_gid = (torch.arange(B, device=images.device)[:, None] * G + gidx[:, :nfg]).reshape(-1)
             if gt_mask_table is not None:
@@ -431,9 +413,8 @@ class MaskRCNN(nn.Module):
             else:
                 tgt_m = V.crop_resize_masks(gt_masks.reshape(-1, *gt_masks.shape[2:]), fg_rois.reshape(-1, 4),
                                             flat_gid, cfg.mask_size)
-            tgt_m = (tgt_m >= 0.5).float()
-            bce = F.binary_cross_entropy_with_logits(ml, tgt_m, reduction="none").mean(dim=(1, 2))
-            out["maskrcnn_loss"] = (bce * fg_valid).sum() / fg_valid.sum().clamp(min=1)
+            # per-RoI mean BCE of the labelled class's mask vs (target >= 0.5), over valid fg RoIs
+            out["maskrcnn_loss"] = D.mask_loss(ml, fg_lab, tgt_m, fg_valid)
         out["total_loss"] = sum(out.values())
         return out
 
@@ -446,6 +427,8 @@ class MaskRCNN(nn.Module):
         scales = [1.0 / s for s in cfg.anchor_strides[:4]]
         roi_feat = V.roi_align(feats, self._with_batch(props), (7, 7), scales)
         cls_logits, box_deltas = self.box_head(roi_feat)
+        cls_logits = cls_logits.float()
+        box_deltas = box_deltas.float().view(cls_logits.shape[0], -1, 4)
         prob = cls_logits.softmax(-1).view(B, K, -1)[..., 1:]                    # [B, K, C]
         C = prob.shape[-1]
         ref = props.reshape(-1, 1, 4).expand(-1, C, 4).reshape(-1, 4)

@@ -55,6 +55,14 @@ SIGNATURES = {
     "mx_ce_stats": [P, P, I, I, I64, P, P, P, P],
     "mx_ce_lse": [P, P, P, I, P],
     "mx_ce_grad": [P, P, I, I, I64, P, P, P, P, F, I, P],
+    # detloss.hip
+    "mx_detloss_max_blocks": [],
+    "mx_rpn_loss_fwd": [P, P, P, P, P, I, F, P, P, P],
+    "mx_rpn_loss_bwd": [P, P, P, P, P, I, P, P, P, P, P, P],
+    "mx_frcnn_loss_fwd": [P, P, P, P, P, I, I, F, P, P, P],
+    "mx_frcnn_loss_bwd": [P, P, P, P, P, I, I, P, P, P, P, P, P],
+    "mx_mask_loss_fwd": [P, P, P, P, I, I, I, P, P, P],
+    "mx_mask_loss_bwd": [P, P, P, P, I, I, I, P, P, P, P],
     # multitensor.hip
     "mx_mt_chunk": [],
     "mx_mt_max_tensors": [],
@@ -82,6 +90,9 @@ SIGNATURES = {
     "mx_roi_align_bwd": [P, P, P, P, I, I, F, I, P, I, I, I, I, I, I, P, P],
     "mx_roi_align_bwd_tiled": [P, P, P, P, I, I, F, I, I, P, I, I, I, I, I, I, P, P, P, P],
     "mx_nms_workspace_words": [I],
+    "mx_topk_chunk": [],
+    "mx_topk_max_rows": [],
+    "mx_level_topk_decode": [P, I, I, P, F, P, P, P, P, I, P, P, P, P],
     "mx_nms": [P, P, I, I, F, I, P, P, P, P],
     "mx_match": [P, I, I, P, P, I, I, P, P, P, P, P],
     "mx_decode_clip": [P, P, I, I, F, F, F, F, F, P, I, P, P],

@@ -405,3 +405,70 @@ def crop_resize_mask_crops(flat: torch.Tensor, table: torch.Tensor, H: int, W: i
     from ..data.coco import unpack_mask_crops
     full = unpack_mask_crops(flat, table.reshape(1, -1, 5), H, W)[0].to(boxes.device)
     return crop_resize_masks(full, boxes, gidx, M)
+
+
+# ------------------------------------------------------------------ RPN level top-k + decode
+_TK_CACHE = {}
+
+
+def _level_topk_decode_ref(logits_lv, deltas_lv, anchors_lv, img_hw, k):
+    B = logits_lv[0].shape[0]
+    boxes, scores, counts = [], [], []
+    for lg, dl, an in zip(logits_lv, deltas_lv, anchors_lv):
+        kk = min(k, lg.shape[1])
+        sc, idx = lg.float().topk(kk, dim=1)                                 # sorted desc
+        d = torch.gather(dl.float(), 1, idx[..., None].expand(-1, -1, 4))
+        ref = an[idx.reshape(-1)]
+        bx = decode_boxes(ref, d.reshape(-1, 4), (1.0, 1.0, 1.0, 1.0), img_hw, rows_per_img=kk).view(B, kk, 4)
+        if kk < k:
+            bx = torch.nn.functional.pad(bx, (0, 0, 0, k - kk))
+            sc = torch.nn.functional.pad(sc, (0, k - kk), value=-float("inf"))
+        boxes.append(bx)
+        scores.append(sc)
+        counts.append(kk)
+    return torch.stack(boxes, 1), torch.stack(scores, 1), counts
+
+
+def level_topk_decode(logits_lv: Sequence[torch.Tensor], deltas_lv: Sequence[torch.Tensor],
+                      anchors_lv: Sequence[torch.Tensor], img_hw: torch.Tensor, k: int):
+    """Per (image, level): the k highest objectness logits (sorted; ties -> lower anchor
+    index), their anchors decoded with the level's deltas (weights 1, clamp, clipped to the
+    image).  logits [B, n_l], deltas [B, n_l, 4], anchors [n_l, 4]; returns boxes
+    [B, L, k, 4], scores [B, L, k] (-inf padded past n_l) and counts [min(k, n_l)].
+    On the GPU: 6 launches for every row of the step (csrc/vision.hip tk_*)."""
+    L = len(logits_lv)
+    B = logits_lv[0].shape[0]
+    lg0 = logits_lv[0]
+    ok = (_lib.use_hip(lg0) and k <= 2048 and B * L <= _lib.query("mx_topk_max_rows")
+          and all(t.dtype == torch.bfloat16 and t.is_contiguous() for t in logits_lv)
+          and all(t.dtype == torch.bfloat16 and t.is_contiguous() for t in deltas_lv)
+          and all(t.dtype == torch.float32 and t.is_contiguous() for t in anchors_lv))
+    if not ok:
+        return _level_topk_decode_ref(logits_lv, deltas_lv, anchors_lv, img_hw, k)
+    dev = lg0.device
+    R = B * L
+    rows = []
+    for b in range(B):
+        for lg, dl, an in zip(logits_lv, deltas_lv, anchors_lv):
+            n = lg.shape[1]
+            rows += [lg.data_ptr() + 2 * b * n, dl.data_ptr() + 2 * 4 * b * n, an.data_ptr(), n, b, 0]
+    chunk = _lib.query("mx_topk_chunk")
+    nchunks = sum((lg.shape[1] + chunk - 1) // chunk for lg in logits_lv) * B
+    key = (str(dev), R)
+    bufs = _TK_CACHE.get(key)
+    if bufs is None or bufs[2].numel() < 2 * nchunks:
+        maxr = _lib.query("mx_topk_max_rows")
+        tables = torch.empty(maxr * 6 * 8 + (maxr + 1) * 4, dtype=torch.uint8, device=dev)
+        hist = torch.zeros(2, R, 256, dtype=torch.int32, device=dev)      # zero between calls
+        bcnt = torch.empty(2 * max(nchunks, 1), dtype=torch.int32, device=dev)
+        cand = torch.empty(R * 2048 * 2, dtype=torch.int32, device=dev)
+        bufs = _TK_CACHE[key] = (tables, hist, bcnt, cand)
+    tables, hist, bcnt, cand = bufs
+    boxes = torch.empty(B, L, k, 4, dtype=torch.float32, device=dev)
+    scores = torch.empty(B, L, k, dtype=torch.float32, device=dev)
+    hw = img_hw.float().contiguous()
+    arr = (ctypes.c_int64 * len(rows))(*rows)
+    _lib.call("mx_level_topk_decode", ctypes.addressof(arr), R, k, _lib.ptr(hw), float(BBOX_CLAMP),
+              _lib.ptr(tables), _lib.ptr(hist[0]), _lib.ptr(hist[1]), _lib.ptr(bcnt), bcnt.numel() // 2,
+              _lib.ptr(cand), _lib.ptr(boxes), _lib.ptr(scores), _lib.stream())
+    return boxes, scores, [min(k, lg.shape[1]) for lg in logits_lv]
