@@ -689,20 +689,24 @@ __global__ __launch_bounds__(64) void nms_keep_kernel(const unsigned long long* 
   const unsigned long long* m = mask + (size_t)p * N * NB;
   // lane's share of a chunk: flat indices k = lane + 64 q of [cn rows][NB words]
   unsigned long long pre[NBM];
-  // (row, word) of the lane's flat indices, packed r * 64 + w: chunk-invariant, computed
-  // once (a runtime-divisor division per index per chunk cost more than the scan itself)
-  int rw[NBM];
-#pragma unroll
-  for (int q = 0; q < NBM; ++q) {
-    const int k = lane + 64 * q, r = k / NB;
-    rw[q] = r * 64 + (k - r * NB);
-  }
+  // (row, word) of flat index k: r = k / NB by a float reciprocal (exact for k < 4096),
+  // not an integer division by a runtime divisor (~40 VALU ops each)
+  const float inv_nb = 1.f / (float)NB;
+  // The loads are unconditional (out-of-range entries read word 0 of the problem) and the
+  // validity mask is applied when the chunk is staged: a `cond ? load : 0` select made the
+  // compiler wait for every load right after issuing it (33 vmcnt(0) waits per chunk
+  // -> ~8 us per chunk, the whole prefetch serialised).
+  unsigned long long valid = 0ull;   // bit q: entry q of the lane's share is in range
   auto fetch = [&](int c0) __attribute__((always_inline)) {
     const int cn = min(64, n - c0), cw = c0 >> 6;
+    valid = 0ull;
 #pragma unroll
     for (int q = 0; q < NBM; ++q) {
       const int k = lane + 64 * q;
-      pre[q] = (q < NB && (rw[q] >> 6) < cn && (rw[q] & 63) >= cw) ? m[(size_t)c0 * NB + k] : 0ull;
+      const int r = (int)(((float)k + 0.5f) * inv_nb), w = k - r * NB;
+      const bool ok = q < NB && r < cn && w >= cw;
+      valid |= (ok ? 1ull : 0ull) << q;
+      pre[q] = m[ok ? (size_t)c0 * NB + k : 0];
     }
   };
   if (n > 0) fetch(0);
@@ -710,7 +714,7 @@ __global__ __launch_bounds__(64) void nms_keep_kernel(const unsigned long long* 
     const int cn = min(64, n - c0);
 #pragma unroll
     for (int q = 0; q < NBM; ++q)
-      if (q < NB) rows[lane + 64 * q] = pre[q];
+      if (q < NB) rows[lane + 64 * q] = ((valid >> q) & 1ull) ? pre[q] : 0ull;
     __syncthreads();
     if (c0 + 64 < n) fetch(c0 + 64);      // next chunk in flight during this one's scan
     const int cw = c0 >> 6;
@@ -741,10 +745,16 @@ __global__ __launch_bounds__(64) void nms_keep_kernel(const unsigned long long* 
     out += __popcll(kept);
     if (lane < NB && lane > cw) {
       unsigned long long acc = removed;
+      // batches of 8 independent LDS reads, then the masked OR (kept bit ii: all-ones select;
+      // never set for ii >= cn, whose LDS rows are stale); a guarded read per row had the
+      // compiler wait for each one
 #pragma unroll
-      for (int ii = 0; ii < 64; ++ii) {
-        const unsigned long long sel = 0ull - ((kept >> ii) & 1ull);   // all-ones if row ii kept
-        if (ii < cn) acc |= rows[ii * NB + lane] & sel;
+      for (int i0 = 0; i0 < 64; i0 += 8) {
+        unsigned long long v8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v8[j] = rows[(i0 + j) * NB + lane];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc |= v8[j] & (0ull - ((kept >> (i0 + j)) & 1ull));
       }
       removed = acc;
     }

@@ -17,7 +17,9 @@ Replaces, per reference component:
   (every scalar series of the tfevents files under a log dir, see obs/tensorboard.py)
   and ``GET /tensorboard?logdir=<dir>`` (inline SVG charts);
 * C45 Katib UI -> ``GET /api/experiments`` (HPO experiments, trials, best);
-* C46 KFP UI -> ``GET /api/pipelines`` (recorded pipeline runs);
+* C46 KFP UI + API server -> ``GET /api/pipelines`` (recorded pipeline runs),
+  ``GET|POST /api/pipelines/defs`` (stored pipelines), ``GET|POST /api/runs``,
+  ``GET /api/runs/<run>``, ``POST /api/runs/<run>/terminate`` (asynchronous runs);
 * C48 profiles / KFAM -> ``GET /api/profiles``;
 * C22-C26 node view (Karpenter / device plugins) -> ``GET /api/node`` (GPUs, ledger,
   node profile, sysfs power/clock samples);
@@ -243,11 +245,52 @@ class Auth:
         return h == p
 
 
-def route(path: str, q: Dict[str, str]):
-    """(status, content-type, body) for a GET; shared by the server and the tests."""
+def _body_doc(body: bytes):
+    """JSON or YAML request body -> object (safe loader only)."""
+    import yaml
+    if not body:
+        return {}
+    txt = body.decode("utf-8")
+    try:
+        return json.loads(txt)
+    except ValueError:
+        return yaml.safe_load(txt)
+
+
+def route_post(parts: List[str], q: Dict[str, str], body: bytes):
+    """Pipelines API writes (KFP backend, C46):
+      POST /api/pipelines/defs            {name, chart_configs, description?}  -> 201
+      POST /api/runs                      {pipeline | chart_configs, name?}    -> 201 {run}
+      POST /api/runs/<name>/terminate                                          -> 200"""
+    from .. import pipeline as pl
+    js = "application/json"
+    rest = parts[1:]
+    doc = _body_doc(body)
+    if rest == ["pipelines", "defs"]:
+        if not isinstance(doc, dict):
+            raise ValueError("body must be a mapping")
+        out = pl.save_pipeline(str(doc.get("name", "")), doc.get("chart_configs"), str(doc.get("description", "")))
+        return 201, js, json.dumps(out)
+    if rest == ["runs"]:
+        if not isinstance(doc, dict):
+            raise ValueError("body must be a mapping")
+        run = pl.submit_run(chart_configs=doc.get("chart_configs"), pipeline=doc.get("pipeline"),
+                            run_name=doc.get("name"))
+        return 201, js, json.dumps({"run": run})
+    if len(rest) == 3 and rest[0] == "runs" and rest[2] == "terminate":
+        return 200, js, json.dumps({"run": rest[1], "terminating": pl.terminate_run(rest[1])})
+    return 404, js, json.dumps({"error": "not found"})
+
+
+def route(path: str, q: Dict[str, str], method: str = "GET", body: bytes = b""):
+    """(status, content-type, body) for a request; shared by the server and the tests."""
     parts = [urllib.parse.unquote(x) for x in path.strip("/").split("/") if x]
     js = "application/json"
     try:
+        if method == "POST":
+            if not parts or parts[0] != "api":
+                return 404, js, json.dumps({"error": "not found"})
+            return route_post(parts, q, body)
         if not parts:
             return 200, "text/html; charset=utf-8", _index_html()
         if parts == ["tensorboard"]:
@@ -272,8 +315,19 @@ def route(path: str, q: Dict[str, str]):
             return 200, js, json.dumps(tensorboard(q["logdir"]))
         if k == "experiments":
             return 200, js, json.dumps(experiments(), default=str)
-        if k == "pipelines":
+        if k == "pipelines" and len(rest) == 1:
             return 200, js, json.dumps(pipelines(), default=str)
+        if k == "pipelines" and rest[1:] == ["defs"]:
+            from ..pipeline import list_pipeline_defs
+            return 200, js, json.dumps(list_pipeline_defs(), default=str)
+        if k == "pipelines" and len(rest) == 3 and rest[1] == "defs":
+            from ..pipeline import get_pipeline
+            return 200, js, json.dumps(get_pipeline(rest[2]), default=str)
+        if k == "runs" and len(rest) == 1:
+            return 200, js, json.dumps(pipelines(), default=str)
+        if k == "runs" and len(rest) == 2:
+            from ..pipeline import get_run
+            return 200, js, json.dumps(get_run(rest[1]), default=str)
         if k == "profiles":
             return 200, js, json.dumps(profiles(), default=str)
         if k == "node":
@@ -283,9 +337,13 @@ def route(path: str, q: Dict[str, str]):
         return 404, js, json.dumps({"error": repr(e)})
     except PermissionError as e:
         return 403, js, json.dumps({"error": repr(e)})
+    except ValueError as e:
+        return 400, js, json.dumps({"error": repr(e)})
 
 
 def make_server(host: str, port: int, auth: Auth, certfile=None, keyfile=None) -> ThreadingHTTPServer:
+    loopback = host in ("127.0.0.1", "localhost", "::1")
+
     class H(BaseHTTPRequestHandler):
         def log_message(self, fmt, *a):
             pass
@@ -299,12 +357,35 @@ def make_server(host: str, port: int, auth: Auth, certfile=None, keyfile=None) -
             u = urllib.parse.urlparse(self.path)
             q = {k: v[0] for k, v in urllib.parse.parse_qs(u.query).items()}
             code, ctype, body = route(u.path, q)
+            self._send(code, ctype, body)
+
+        def _send(self, code, ctype, body):
             b = body.encode() if isinstance(body, str) else body
             self.send_response(code)
             self.send_header("Content-Type", ctype)
             self.send_header("Content-Length", str(len(b)))
             self.end_headers()
             self.wfile.write(b)
+
+        def do_POST(self):  # noqa: N802
+            if not auth.ok(self.headers.get("Authorization")):
+                self.send_response(401)
+                self.send_header("WWW-Authenticate", 'Basic realm="mxtrain"')
+                self.end_headers()
+                return
+            # writes (starting jobs) need authenticated users, except on a loopback bind
+            if not auth.users and not loopback:
+                self._send(403, "application/json", json.dumps({"error": "writes need --htpasswd"}))
+                return
+            n = int(self.headers.get("Content-Length") or 0)
+            if n > (1 << 20):
+                self._send(413, "application/json", json.dumps({"error": "body too large"}))
+                return
+            data = self.rfile.read(n) if n else b""
+            u = urllib.parse.urlparse(self.path)
+            q = {k: v[0] for k, v in urllib.parse.parse_qs(u.query).items()}
+            code, ctype, body = route(u.path, q, "POST", data)
+            self._send(code, ctype, body)
 
     srv = ThreadingHTTPServer((host, port), H)
     if certfile and keyfile:

@@ -25,6 +25,7 @@ import os
 import signal
 import sys
 import tempfile
+import threading
 import time
 from typing import Dict, List, Optional
 
@@ -55,15 +56,18 @@ def resolve_chart(cfg: Dict) -> str:
 
 
 class ChartHandler:
-    def __init__(self, cfg: Dict, log=print):
+    def __init__(self, cfg: Dict, log=print, cancel: Optional[threading.Event] = None):
         self.cfg = cfg
         self.log = log
         self.name = cfg["release_name"]
         self.ns = cfg.get("namespace", "default")
         self._installed = False
+        self.cancel = cancel
 
     def __call__(self) -> int:
-        prev = {s: signal.signal(s, self._on_signal) for s in (signal.SIGINT, signal.SIGTERM)}
+        # signal handlers only from the main thread (API-server runs execute in threads)
+        main = threading.current_thread() is threading.main_thread()
+        prev = {s: signal.signal(s, self._on_signal) for s in (signal.SIGINT, signal.SIGTERM)} if main else {}
         exit_code = 1
         try:
             exit_code = self.install()
@@ -110,6 +114,9 @@ class ChartHandler:
         check = min(float(self.cfg.get("pod_check_secs", 300)), 1.0)
         t0 = time.time()
         while True:
+            if self.cancel is not None and self.cancel.is_set():
+                self.log(f"release {self.name}: run terminated")
+                return 1
             try:
                 st = rel.read_status(self.name, self.ns)
             except FileNotFoundError:
@@ -145,22 +152,32 @@ def runs_dir() -> str:
     return os.path.join(mxtrain_home(), "pipelines", "runs")
 
 
-def run_pipeline(chart_configs: List[Dict], log=print, run_name: Optional[str] = None) -> str:
+def run_pipeline(chart_configs: List[Dict], log=print, run_name: Optional[str] = None,
+                 cancel: Optional[threading.Event] = None, pipeline: Optional[str] = None) -> str:
     """Sequential install -> wait -> uninstall of every chart config; "Failure" at the first
-    failing step.  The run (steps, timings, result) is recorded under
-    ``$MXTRAIN_HOME/pipelines/runs/`` (KFP run history, C46; shown by the dashboard)."""
-    run_name = run_name or time.strftime("run-%Y%m%d-%H%M%S")
-    rec = {"name": run_name, "started": time.time(), "steps": [], "result": None}
+    failing step.  The run (steps, timings, result, KFP-style status Running / Succeeded /
+    Failed / Terminated) is recorded under ``$MXTRAIN_HOME/pipelines/runs/`` (KFP run
+    history, C46; shown and driven by the dashboard's pipelines API)."""
+    from .launch.release import check_name
+    run_name = check_name(run_name or time.strftime("run-%Y%m%d-%H%M%S"), "run name")
+    rec = {"name": run_name, "pipeline": pipeline, "started": time.time(), "steps": [], "result": None,
+           "status": "Running"}
 
     def _save():
         os.makedirs(runs_dir(), exist_ok=True)
-        with open(os.path.join(runs_dir(), run_name + ".json"), "w") as f:
+        tmp = os.path.join(runs_dir(), f".{run_name}.json.tmp")
+        with open(tmp, "w") as f:
             json.dump(rec, f, indent=1, default=str)
+        os.replace(tmp, os.path.join(runs_dir(), run_name + ".json"))
 
+    _save()
     result = "Success"
     for cfg in chart_configs:
+        if cancel is not None and cancel.is_set():
+            result = "Failure"
+            break
         t0 = time.time()
-        rc = ChartHandler(cfg, log)()
+        rc = ChartHandler(cfg, log, cancel)()
         rec["steps"].append({"release": cfg.get("release_name"), "namespace": cfg.get("namespace"),
                              "chart": cfg.get("chart") or cfg.get("path"), "exit_code": rc,
                              "seconds": round(time.time() - t0, 2)})
@@ -169,9 +186,117 @@ def run_pipeline(chart_configs: List[Dict], log=print, run_name: Optional[str] =
             result = "Failure"
             break
     rec["result"] = result
+    rec["status"] = ("Terminated" if cancel is not None and cancel.is_set()
+                     else "Succeeded" if result == "Success" else "Failed")
     rec["finished"] = time.time()
     _save()
     return result
+
+
+# ------------------------------------------------------------ pipelines API (KFP backend)
+# Stored pipeline definitions (``pipelines/defs/<name>.yaml``: {chart_configs: [...]}) and
+# asynchronous runs in server threads, with terminate -- the KFP API server's pipeline /
+# run / terminate surface (reference: charts/ml-platform/kubeflow-pipelines, used by
+# kfp/pipelines/helm_charts_pipeline.py) over this node's chart runner.
+_RUNS: Dict[str, Dict] = {}
+_RUNS_LOCK = threading.Lock()
+
+
+def defs_dir() -> str:
+    from .runtime.storage import mxtrain_home
+    return os.path.join(mxtrain_home(), "pipelines", "defs")
+
+
+def save_pipeline(name: str, chart_configs: List[Dict], description: str = "") -> Dict:
+    from .launch.release import check_name
+    check_name(name, "pipeline name")
+    if not isinstance(chart_configs, list) or not all(isinstance(c, dict) and c.get("release_name")
+                                                       for c in chart_configs):
+        raise ValueError("chart_configs must be a list of chart configs with release_name")
+    for c in chart_configs:
+        check_name(str(c["release_name"]), "release name")
+        check_name(str(c.get("namespace", "default")), "namespace")
+    os.makedirs(defs_dir(), exist_ok=True)
+    doc = {"name": name, "description": description, "created": time.time(), "chart_configs": chart_configs}
+    with open(os.path.join(defs_dir(), name + ".yaml"), "w") as f:
+        yaml.safe_dump(doc, f, default_flow_style=False)
+    return {"name": name, "steps": len(chart_configs)}
+
+
+def get_pipeline(name: str) -> Dict:
+    from .launch.release import check_name
+    with open(os.path.join(defs_dir(), check_name(name, "pipeline name") + ".yaml")) as f:
+        return yaml.safe_load(f)
+
+
+def list_pipeline_defs() -> List[Dict]:
+    import glob
+    out = []
+    for p in sorted(glob.glob(os.path.join(defs_dir(), "*.yaml"))):
+        with open(p) as f:
+            d = yaml.safe_load(f) or {}
+        out.append({"name": d.get("name"), "description": d.get("description", ""),
+                    "steps": len(d.get("chart_configs") or [])})
+    return out
+
+
+def submit_run(chart_configs: Optional[List[Dict]] = None, pipeline: Optional[str] = None,
+               run_name: Optional[str] = None, log=None) -> str:
+    """Start a run (a stored pipeline or inline chart configs) in a background thread;
+    returns the run name.  Status: ``get_run``; stop: ``terminate_run``."""
+    from .launch.release import check_name
+    if chart_configs is None:
+        if not pipeline:
+            raise ValueError("need a pipeline name or chart_configs")
+        chart_configs = list(get_pipeline(pipeline).get("chart_configs") or [])
+    run_name = check_name(run_name or f"run-{time.strftime('%Y%m%d-%H%M%S')}-{os.getpid()}-{len(_RUNS)}",
+                          "run name")
+    cancel = threading.Event()
+    logs: List[str] = []
+
+    def body():
+        run_pipeline(chart_configs, log=(log or logs.append), run_name=run_name, cancel=cancel, pipeline=pipeline)
+
+    t = threading.Thread(target=body, name=f"pipeline-{run_name}", daemon=True)
+    with _RUNS_LOCK:
+        if run_name in _RUNS:
+            raise ValueError(f"run {run_name} exists")
+        _RUNS[run_name] = {"thread": t, "cancel": cancel, "logs": logs}
+    t.start()
+    return run_name
+
+
+def get_run(name: str) -> Dict:
+    from .launch.release import check_name
+    p = os.path.join(runs_dir(), check_name(name, "run name") + ".json")
+    with _RUNS_LOCK:
+        live = _RUNS.get(name)
+    if not os.path.exists(p):
+        if live is not None:
+            return {"name": name, "status": "Pending", "steps": []}
+        raise FileNotFoundError(name)
+    with open(p) as f:
+        rec = json.load(f)
+    if live is not None:
+        rec["log"] = list(live["logs"])[-50:]
+    return rec
+
+
+def terminate_run(name: str) -> bool:
+    with _RUNS_LOCK:
+        live = _RUNS.get(name)
+    if live is None:
+        return False
+    live["cancel"].set()
+    return True
+
+
+def wait_run(name: str, timeout: Optional[float] = None) -> Dict:
+    with _RUNS_LOCK:
+        live = _RUNS.get(name)
+    if live is not None:
+        live["thread"].join(timeout)
+    return get_run(name)
 
 
 def load_pipeline(path: str) -> List[Dict]:

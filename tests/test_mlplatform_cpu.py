@@ -211,3 +211,52 @@ def test_profile_and_debug_modes_reach_replicas(home, tmp_path):
     assert "Self CPU" in (tmp_path / "prof" / "kernels-rank0.txt").read_text()
     with pytest.raises(FloatingPointError):
         check_finite(3, loss=torch.tensor(float("nan")))
+
+
+def test_pipelines_api_defs_runs_terminate(home):
+    """KFP backend (C46): stored pipeline definitions, asynchronous runs over the HTTP API,
+    run status, terminate of a running step (its release is uninstalled)."""
+    import time
+    from mxtrain import pipeline as pl
+    from mxtrain.launch import release as rel
+    from mxtrain.mlplatform import dashboard as db
+    dp = "charts/machine-learning/data-prep/data-process"
+    ok = {"release_name": "api-a", "namespace": "default", "path": dp, "values": {"process": {"command": ["true"]}}}
+    ok2 = dict(ok, release_name="api-b")
+    code, _, body = db.route("/api/pipelines/defs", {}, "POST",
+                             json.dumps({"name": "two-steps", "chart_configs": [ok, ok2]}).encode())
+    assert code == 201 and json.loads(body)["steps"] == 2
+    assert [d["name"] for d in json.loads(db.route("/api/pipelines/defs", {})[2])] == ["two-steps"]
+    assert db.route("/api/pipelines/defs", {}, "POST", b"{\"name\": \"../x\", \"chart_configs\": []}")[0] == 403
+    srv = db.make_server("127.0.0.1", 0, db.Auth(None))
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    try:
+        url = f"http://127.0.0.1:{srv.server_address[1]}"
+        req = urllib.request.Request(url + "/api/runs", data=json.dumps({"pipeline": "two-steps", "name": "r1"}).encode(),
+                                     method="POST")
+        with urllib.request.urlopen(req, timeout=30) as r:
+            assert r.status == 201 and json.loads(r.read())["run"] == "r1"
+        rec = pl.wait_run("r1", timeout=120)
+        assert rec["status"] == "Succeeded" and rec["result"] == "Success" and len(rec["steps"]) == 2
+        with urllib.request.urlopen(url + "/api/runs/r1", timeout=30) as r:
+            assert json.loads(r.read())["pipeline"] == "two-steps"
+    finally:
+        srv.shutdown()
+    slow = dict(ok, release_name="api-slow", values={"process": {"command": ["sleep"], "args": ["60"]}})
+    code, _, body = db.route("/api/runs", {}, "POST", json.dumps({"chart_configs": [slow, ok], "name": "r2"}).encode())
+    assert code == 201
+    t0 = time.time()
+    while time.time() - t0 < 60:
+        try:
+            if rel.read_status("api-slow", "default")["phase"] == "Running":
+                break
+        except FileNotFoundError:
+            pass
+        time.sleep(0.2)
+    code, _, body = db.route("/api/runs/r2/terminate", {}, "POST")
+    assert code == 200 and json.loads(body)["terminating"]
+    rec = pl.wait_run("r2", timeout=60)
+    assert rec["status"] == "Terminated" and rec["result"] == "Failure" and len(rec["steps"]) == 1
+    assert rel.read_status("api-slow", "default")["phase"] == "Uninstalled"
+    assert time.time() - t0 < 45
