@@ -13,7 +13,9 @@ Replaces, per reference component:
   ``GET /api/jobs/<ns>/<name>/logs[?pod=]``;
 * C47 volumes web app -> ``GET /api/volumes`` (claims under the PV root, size, files),
   ``GET /api/volumes/<claim>?path=<rel>`` (directory listing, read-only);
-* C44 Tensorboards (``Tensorboard.spec.logspath``) -> ``GET /api/tensorboards?logdir=<dir>``
+* C44 Tensorboards (``Tensorboard.spec.logspath``, pvc://claim/path) -> ``POST|GET /api/tensorboards``
+  (resources), ``GET /tensorboard/<name>`` (per-tag run overlays, debiased EMA smoothing,
+  tag regex), ``GET /api/tensorboards?logdir=<dir>[&view=tags]``
   (every scalar series of the tfevents files under a log dir, see obs/tensorboard.py)
   and ``GET /tensorboard?logdir=<dir>`` (inline SVG charts);
 * C45 Katib UI -> ``GET /api/experiments`` (HPO experiments, trials, best);
@@ -205,13 +207,113 @@ def _index_html() -> str:
             f"<th>chart</th><th>phase</th></tr>{js}</table></body></html>")
 
 
-def _tensorboard_html(logdir: Optional[str]) -> str:
+_COLORS = ("#1f77b4", "#ff7f0e", "#2ca02c", "#d62728", "#9467bd", "#8c564b", "#e377c2", "#7f7f7f")
+
+
+def smooth_ema(values: List[float], weight: float) -> List[float]:
+    """TensorBoard's scalar smoothing: debiased exponential moving average."""
+    out, last, n = [], 0.0, 0
+    for v in values:
+        last = last * weight + (1 - weight) * v
+        n += 1
+        out.append(last / (1 - weight ** n) if weight > 0 else v)
+    return out
+
+
+def _svg_multi(series: Dict[str, List[dict]], smoothing: float, w: int = 560, h: int = 200) -> str:
+    """One tag, one line per run (raw faint, smoothed solid), shared axes, legend."""
+    pts = [p for v in series.values() for p in v]
+    if not pts:
+        return ""
+    x0, x1 = min(p["step"] for p in pts), max(p["step"] for p in pts)
+    y0, y1 = min(p["value"] for p in pts), max(p["value"] for p in pts)
+    if y1 == y0:
+        y1 = y0 + 1
+    sx = lambda x: 50 + (w - 60) * ((x - x0) / ((x1 - x0) or 1))  # noqa: E731
+    sy = lambda y: h - 20 - (h - 30) * ((y - y0) / (y1 - y0))  # noqa: E731
+    lines, legend = [], []
+    for i, (run, v) in enumerate(sorted(series.items())):
+        c = _COLORS[i % len(_COLORS)]
+        xs = [p["step"] for p in v]
+        raw = [p["value"] for p in v]
+        for ys, op in ((raw, "0.25"), (smooth_ema(raw, smoothing), "1")):
+            d = " ".join(f"{'M' if j == 0 else 'L'}{sx(x):.1f},{sy(y):.1f}" for j, (x, y) in enumerate(zip(xs, ys)))
+            lines.append(f'<path d="{d}" fill="none" stroke="{c}" stroke-opacity="{op}" stroke-width="1.5"/>')
+        legend.append(f'<text x="{w - 150}" y="{14 + 12 * i}" font-size="10" fill="{c}">{html.escape(run)}</text>')
+    return (f'<svg width="{w}" height="{h}" style="border:1px solid #ccc">{"".join(lines)}{"".join(legend)}'
+            f'<text x="2" y="12" font-size="10">{y1:.4g}</text><text x="2" y="{h - 22}" font-size="10">{y0:.4g}</text>'
+            f'<text x="50" y="{h - 4}" font-size="10">{x0}</text><text x="{w - 60}" y="{h - 4}" font-size="10">{x1}</text>'
+            "</svg>")
+
+
+def tensorboard_view(logdir: str, tag_re: Optional[str] = None) -> Dict[str, Dict[str, List[dict]]]:
+    """{tag: {run: points}} -- runs are the event files' directories under logdir."""
+    import re
+    rx = re.compile(tag_re) if tag_re else None
+    out: Dict[str, Dict[str, List[dict]]] = {}
+    from ..obs.tensorboard import event_files, read_scalars
+    runs = sorted({os.path.relpath(os.path.dirname(p), logdir) for p in event_files(logdir)}, key=len, reverse=True)
+    for key, pts in tensorboard(logdir).items():
+        run = next((r for r in runs if r != "." and key.startswith(r + "/")), ".")
+        tag = key[len(run) + 1:] if run != "." else key
+        if rx and not rx.search(tag):
+            continue
+        out.setdefault(tag, {})[run] = pts
+    return out
+
+
+# Tensorboard resources (Kubeflow ``Tensorboard`` CR: metadata.name + spec.logspath, with
+# pvc://<claim>/<path> resolved under the PV root) -> the viewer page /tensorboard/<name>
+def tensorboards_dir() -> str:
+    return os.path.join(mxtrain_home(), "tensorboards")
+
+
+def resolve_logspath(logspath: str) -> str:
+    if logspath.startswith("pvc://"):
+        claim, _, rel = logspath[len("pvc://"):].partition("/")
+        from ..launch.release import check_name
+        root = os.path.realpath(os.path.join(pv_root(), check_name(claim, "claim")))
+        target = os.path.realpath(os.path.join(root, rel))
+        if not (target == root or target.startswith(root + os.sep)):
+            raise PermissionError(logspath)
+        return target
+    return logspath
+
+
+def create_tensorboard(name: str, logspath: str) -> dict:
+    from ..launch.release import check_name
+    check_name(name, "tensorboard name")
+    resolve_logspath(logspath)
+    os.makedirs(tensorboards_dir(), exist_ok=True)
+    rec = {"name": name, "logspath": logspath, "url": f"/tensorboard/{name}"}
+    with open(os.path.join(tensorboards_dir(), name + ".json"), "w") as f:
+        json.dump(rec, f)
+    return rec
+
+
+def list_tensorboards() -> List[dict]:
+    out = []
+    for p in sorted(glob.glob(os.path.join(tensorboards_dir(), "*.json"))):
+        with open(p) as f:
+            out.append(json.load(f))
+    return out
+
+
+def _tensorboard_html(logdir: Optional[str], q: Optional[Dict[str, str]] = None) -> str:
+    q = q or {}
     if not logdir:
-        return ("<html><body><form action='/tensorboard'>log dir: <input name='logdir' size=60>"
+        items = "".join(f'<li><a href="{html.escape(t["url"])}">{html.escape(t["name"])}</a> '
+                        f'({html.escape(t["logspath"])})</li>' for t in list_tensorboards())
+        return ("<html><body><h2>Tensorboards</h2><ul>" + items + "</ul>"
+                "<form action='/tensorboard'>log dir: <input name='logdir' size=60>"
                 "<input type=submit value='open'></form></body></html>")
-    data = tensorboard(logdir)
-    parts = [f"<h3>{html.escape(k)}</h3>{_svg_series(v)}" for k, v in sorted(data.items())]
-    return f"<html><body><h2>{html.escape(logdir)}</h2>{''.join(parts) or 'no scalars'}</body></html>"
+    smoothing = min(max(float(q.get("smoothing", "0.6")), 0.0), 0.999)
+    view = tensorboard_view(logdir, q.get("tag"))
+    parts = [f"<h3>{html.escape(tag)}</h3>{_svg_multi(runs, smoothing)}" for tag, runs in sorted(view.items())]
+    form = (f"<form>smoothing <input name='smoothing' value='{smoothing}' size=5> tag regex "
+            f"<input name='tag' value='{html.escape(q.get('tag', ''))}'>"
+            f"<input type=hidden name='logdir' value='{html.escape(logdir)}'><input type=submit value='apply'></form>")
+    return f"<html><body><h2>{html.escape(logdir)}</h2>{form}{''.join(parts) or 'no scalars'}</body></html>"
 
 
 # ----------------------------------------------------------------------------- server
@@ -271,6 +373,10 @@ def route_post(parts: List[str], q: Dict[str, str], body: bytes):
             raise ValueError("body must be a mapping")
         out = pl.save_pipeline(str(doc.get("name", "")), doc.get("chart_configs"), str(doc.get("description", "")))
         return 201, js, json.dumps(out)
+    if rest == ["tensorboards"]:
+        if not isinstance(doc, dict):
+            raise ValueError("body must be a mapping")
+        return 201, js, json.dumps(create_tensorboard(str(doc.get("name", "")), str(doc.get("logspath", ""))))
     if rest == ["runs"]:
         if not isinstance(doc, dict):
             raise ValueError("body must be a mapping")
@@ -294,7 +400,12 @@ def route(path: str, q: Dict[str, str], method: str = "GET", body: bytes = b""):
         if not parts:
             return 200, "text/html; charset=utf-8", _index_html()
         if parts == ["tensorboard"]:
-            return 200, "text/html; charset=utf-8", _tensorboard_html(q.get("logdir"))
+            return 200, "text/html; charset=utf-8", _tensorboard_html(q.get("logdir"), q)
+        if len(parts) == 2 and parts[0] == "tensorboard":
+            from ..launch.release import check_name
+            with open(os.path.join(tensorboards_dir(), check_name(parts[1], "tensorboard name") + ".json")) as f:
+                rec = json.load(f)
+            return 200, "text/html; charset=utf-8", _tensorboard_html(resolve_logspath(rec["logspath"]), q)
         if parts[0] != "api":
             return 404, js, json.dumps({"error": "not found"})
         rest = parts[1:]
@@ -311,8 +422,12 @@ def route(path: str, q: Dict[str, str], method: str = "GET", body: bytes = b""):
             return 200, js, json.dumps(volumes())
         if k == "volumes" and len(rest) == 2:
             return 200, js, json.dumps(volume_browse(rest[1], q.get("path", "")))
-        if k == "tensorboards":
+        if k == "tensorboards" and "logdir" in q:
+            if q.get("view") == "tags":
+                return 200, js, json.dumps(tensorboard_view(q["logdir"], q.get("tag")))
             return 200, js, json.dumps(tensorboard(q["logdir"]))
+        if k == "tensorboards":
+            return 200, js, json.dumps(list_tensorboards())
         if k == "experiments":
             return 200, js, json.dumps(experiments(), default=str)
         if k == "pipelines" and len(rest) == 1:

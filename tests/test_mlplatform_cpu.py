@@ -260,3 +260,30 @@ def test_pipelines_api_defs_runs_terminate(home):
     assert rec["status"] == "Terminated" and rec["result"] == "Failure" and len(rec["steps"]) == 1
     assert rel.read_status("api-slow", "default")["phase"] == "Uninstalled"
     assert time.time() - t0 < 45
+
+
+def test_tensorboard_resources_runs_and_smoothing(home, tmp_path):
+    """Tensorboards (C44): Tensorboard resources with pvc:// logspaths, one chart per tag
+    with the runs overlaid, TensorBoard's debiased EMA smoothing, tag filter."""
+    from mxtrain.mlplatform import dashboard as db
+    from mxtrain.obs.tensorboard import SummaryWriter
+    from mxtrain.runtime.storage import pv_root
+    logs = os.path.join(pv_root(), "pv-fsx", "exp1")
+    for run, scale in (("run-a", 1.0), ("run-b", 2.0)):
+        with SummaryWriter(os.path.join(logs, run)) as w:
+            for s in range(5):
+                w.add_scalar("loss", scale / (s + 1), s)
+                w.add_scalar("lr", 0.1, s)
+    code, _, body = db.route("/api/tensorboards", {}, "POST",
+                             json.dumps({"name": "tb1", "logspath": "pvc://pv-fsx/exp1"}).encode())
+    assert code == 201 and json.loads(body)["url"] == "/tensorboard/tb1"
+    assert db.route("/api/tensorboards", {}, "POST",
+                    json.dumps({"name": "tb2", "logspath": "pvc://pv-fsx/../../etc"}).encode())[0] == 403
+    assert [t["name"] for t in json.loads(db.route("/api/tensorboards", {})[2])] == ["tb1"]
+    view = json.loads(db.route("/api/tensorboards", {"logdir": logs, "view": "tags"})[2])
+    assert set(view) == {"loss", "lr"} and set(view["loss"]) == {"run-a", "run-b"}
+    assert [p["value"] for p in view["loss"]["run-b"]][:2] == [2.0, 1.0]
+    code, ctype, page = db.route("/tensorboard/tb1", {"tag": "^loss$", "smoothing": "0.5"})
+    assert code == 200 and "run-a" in page and "run-b" in page and "<h3>loss</h3>" in page and "<h3>lr</h3>" not in page
+    sm = db.smooth_ema([1.0, 0.0, 0.0], 0.5)
+    assert sm[0] == 1.0 and abs(sm[1] - (0.5 * 0.5) / (1 - 0.25)) < 1e-12
