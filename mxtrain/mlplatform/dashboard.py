@@ -318,8 +318,12 @@ def _tensorboard_html(logdir: Optional[str], q: Optional[Dict[str, str]] = None)
 
 # ----------------------------------------------------------------------------- server
 class Auth:
-    def __init__(self, htpasswd: Optional[str]):
+    """Basic auth (htpasswd) and, with ``oidc``, bearer / session-cookie JWTs from the
+    node's identity provider (mlplatform/identity.py: the Dex + oauth2-proxy roles)."""
+
+    def __init__(self, htpasswd: Optional[str], oidc: bool = False):
         self.users: Dict[str, str] = {}
+        self.oidc = oidc
         if htpasswd and os.path.exists(htpasswd):
             with open(htpasswd) as f:
                 for line in f:
@@ -328,9 +332,37 @@ class Auth:
                         u, h = line.split(":", 1)
                         self.users[u] = h
 
-    def ok(self, header: Optional[str]) -> bool:
-        if not self.users:
+    @property
+    def enabled(self) -> bool:
+        return bool(self.users) or self.oidc
+
+    def token_user(self, header: Optional[str], cookie: Optional[str]) -> Optional[str]:
+        """Email of a valid bearer token / session cookie, else None."""
+        if not self.oidc:
+            return None
+        from .identity import verify_token
+        tok = None
+        if header and header.startswith("Bearer "):
+            tok = header[7:].strip()
+        elif cookie:
+            for part in cookie.split(";"):
+                k, _, v = part.strip().partition("=")
+                if k == "mxtrain_session":
+                    tok = v
+        if not tok:
+            return None
+        try:
+            return verify_token(tok).get("email")
+        except PermissionError:
+            return None
+
+    def ok(self, header: Optional[str], cookie: Optional[str] = None) -> bool:
+        if not self.enabled:
             return True
+        if self.token_user(header, cookie):
+            return True
+        if not self.users:
+            return False
         import base64
         import hashlib
         if not header or not header.startswith("Basic "):
@@ -463,8 +495,52 @@ def make_server(host: str, port: int, auth: Auth, certfile=None, keyfile=None) -
         def log_message(self, fmt, *a):
             pass
 
+        def _public(self, method: str, u, data: bytes = b"") -> bool:
+            """OIDC endpoints served without a session (token issuance, discovery)."""
+            if not auth.oidc:
+                return False
+            from . import identity as idp
+            if method == "GET" and u.path == "/.well-known/openid-configuration":
+                scheme = "https" if certfile else "http"
+                base = f"{scheme}://{self.headers.get('Host', host)}"
+                self._send(200, "application/json", json.dumps(idp.discovery(base)))
+                return True
+            if method == "POST" and u.path == "/auth/token":
+                ct = self.headers.get("Content-Type", "")
+                if ct.startswith("application/x-www-form-urlencoded"):
+                    f = {k: v[0] for k, v in urllib.parse.parse_qs(data.decode()).items()}
+                else:
+                    f = _body_doc(data) or {}
+                try:
+                    tok = idp.password_grant(str(f.get("username", "")), str(f.get("password", "")))
+                except PermissionError:
+                    self._send(401, "application/json", json.dumps({"error": "invalid_grant"}))
+                    return True
+                b = json.dumps(tok).encode()
+                self.send_response(200)
+                self.send_header("Content-Type", "application/json")
+                self.send_header("Set-Cookie", f"mxtrain_session={tok['access_token']}; HttpOnly; SameSite=Strict"
+                                 + ("; Secure" if certfile else ""))
+                self.send_header("Content-Length", str(len(b)))
+                self.end_headers()
+                self.wfile.write(b)
+                return True
+            if method == "GET" and u.path == "/auth/userinfo":
+                user = auth.token_user(self.headers.get("Authorization"), self.headers.get("Cookie"))
+                if not user:
+                    self._send(401, "application/json", json.dumps({"error": "invalid_token"}))
+                else:
+                    from .identity import load_users
+                    info = load_users().get(user, {})
+                    self._send(200, "application/json", json.dumps({"sub": user, "email": user,
+                                                                    "groups": info.get("groups", [])}))
+                return True
+            return False
+
         def do_GET(self):  # noqa: N802
-            if not auth.ok(self.headers.get("Authorization")):
+            if self._public("GET", urllib.parse.urlparse(self.path)):
+                return
+            if not auth.ok(self.headers.get("Authorization"), self.headers.get("Cookie")):
                 self.send_response(401)
                 self.send_header("WWW-Authenticate", 'Basic realm="mxtrain"')
                 self.end_headers()
@@ -483,21 +559,23 @@ def make_server(host: str, port: int, auth: Auth, certfile=None, keyfile=None) -
             self.wfile.write(b)
 
         def do_POST(self):  # noqa: N802
-            if not auth.ok(self.headers.get("Authorization")):
-                self.send_response(401)
-                self.send_header("WWW-Authenticate", 'Basic realm="mxtrain"')
-                self.end_headers()
-                return
-            # writes (starting jobs) need authenticated users, except on a loopback bind
-            if not auth.users and not loopback:
-                self._send(403, "application/json", json.dumps({"error": "writes need --htpasswd"}))
-                return
             n = int(self.headers.get("Content-Length") or 0)
             if n > (1 << 20):
                 self._send(413, "application/json", json.dumps({"error": "body too large"}))
                 return
             data = self.rfile.read(n) if n else b""
             u = urllib.parse.urlparse(self.path)
+            if self._public("POST", u, data):
+                return
+            if not auth.ok(self.headers.get("Authorization"), self.headers.get("Cookie")):
+                self.send_response(401)
+                self.send_header("WWW-Authenticate", 'Basic realm="mxtrain"')
+                self.end_headers()
+                return
+            # writes (starting jobs) need authenticated users, except on a loopback bind
+            if not auth.enabled and not loopback:
+                self._send(403, "application/json", json.dumps({"error": "writes need --htpasswd or --oidc"}))
+                return
             q = {k: v[0] for k, v in urllib.parse.parse_qs(u.query).items()}
             code, ctype, body = route(u.path, q, "POST", data)
             self._send(code, ctype, body)
@@ -517,8 +595,17 @@ def main(argv=None):
     ap.add_argument("--certfile")
     ap.add_argument("--keyfile")
     ap.add_argument("--htpasswd")
+    ap.add_argument("--oidc", action="store_true",
+                    help="accept bearer / session JWTs of the node identity provider (POST /auth/token)")
+    ap.add_argument("--tls-auto", action="store_true",
+                    help="serve HTTPS with a certificate issued (and renewed) by the node CA")
     a = ap.parse_args(argv)
-    srv = make_server(a.host, a.port, Auth(a.htpasswd), a.certfile, a.keyfile)
+    if a.tls_auto and not a.certfile:
+        from .identity import issue_cert
+        c = issue_cert("dashboard", ["localhost", a.host] if a.host not in ("127.0.0.1", "0.0.0.0") else ["localhost"],
+                       ips=["127.0.0.1"])
+        a.certfile, a.keyfile = c["cert"], c["key"]
+    srv = make_server(a.host, a.port, Auth(a.htpasswd, oidc=a.oidc), a.certfile, a.keyfile)
     print(f"mxtrain dashboard on {'https' if a.certfile else 'http'}://{a.host}:{srv.server_address[1]}/",
           flush=True)
     try:

@@ -287,3 +287,61 @@ def test_tensorboard_resources_runs_and_smoothing(home, tmp_path):
     assert code == 200 and "run-a" in page and "run-b" in page and "<h3>loss</h3>" in page and "<h3>lr</h3>" not in page
     sm = db.smooth_ema([1.0, 0.0, 0.0], 0.5)
     assert sm[0] == 1.0 and abs(sm[1] - (0.5 * 0.5) / (1 - 0.25)) < 1e-12
+
+
+def test_identity_tokens_and_node_certificates(home, tmp_path):
+    """Dex + oauth2-proxy + cert-manager roles (C38-C40): password-grant JWTs accepted as
+    bearer / session cookie, tampered / expired tokens refused, discovery + userinfo; node
+    CA issuing a server certificate with SANs (renewal only near expiry) served over TLS."""
+    import ssl
+    import subprocess
+    import urllib.error
+    from mxtrain.mlplatform import dashboard as db
+    from mxtrain.mlplatform import identity as idp
+    idp.add_user("alice@example.com", "s3cret", ["ml"])
+    assert idp.password_grant("alice@example.com", "s3cret")["token_type"] == "Bearer"
+    with pytest.raises(PermissionError):
+        idp.password_grant("alice@example.com", "wrong")
+    tok = idp.issue_token("alice@example.com", 60)
+    assert idp.verify_token(tok)["email"] == "alice@example.com"
+    h, b, s = tok.split(".")
+    with pytest.raises(PermissionError):
+        idp.verify_token(f"{h}.{b}.{s[:-2]}AA")
+    with pytest.raises(PermissionError):
+        idp.verify_token(idp.issue_token("alice@example.com", -5))
+    c = idp.issue_cert("dash", ["localhost"], ["127.0.0.1"])
+    assert c["renewed"] == "yes" and idp.issue_cert("dash", ["localhost"], ["127.0.0.1"])["renewed"] == "no"
+    r = subprocess.run(["openssl", "verify", "-CAfile", c["ca"], c["cert"]], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    txt = subprocess.run(["openssl", "x509", "-in", c["cert"], "-noout", "-text"], capture_output=True, text=True).stdout
+    assert "DNS:localhost" in txt and "IP Address:127.0.0.1" in txt
+    srv = db.make_server("127.0.0.1", 0, db.Auth(None, oidc=True), c["cert"], c["key"])
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    ctx = ssl.create_default_context(cafile=c["ca"])
+    url = f"https://localhost:{srv.server_address[1]}"
+    try:
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(url + "/api", context=ctx, timeout=30)
+        assert e.value.code == 401
+        with urllib.request.urlopen(url + "/.well-known/openid-configuration", context=ctx, timeout=30) as r:
+            assert json.loads(r.read())["token_endpoint"].endswith("/auth/token")
+        req = urllib.request.Request(url + "/auth/token", data=b"username=alice%40example.com&password=s3cret",
+                                     headers={"Content-Type": "application/x-www-form-urlencoded"}, method="POST")
+        with urllib.request.urlopen(req, context=ctx, timeout=30) as r:
+            cookie = r.headers["Set-Cookie"].split(";")[0]
+            access = json.loads(r.read())["access_token"]
+        for hdr in ({"Authorization": f"Bearer {access}"}, {"Cookie": cookie}):
+            with urllib.request.urlopen(urllib.request.Request(url + "/api", headers=hdr), context=ctx, timeout=30) as r:
+                assert r.status == 200
+        with urllib.request.urlopen(urllib.request.Request(url + "/auth/userinfo",
+                                                           headers={"Authorization": f"Bearer {access}"}),
+                                    context=ctx, timeout=30) as r:
+            assert json.loads(r.read()) == {"sub": "alice@example.com", "email": "alice@example.com", "groups": ["ml"]}
+        bad = urllib.request.Request(url + "/auth/token", data=b"username=alice%40example.com&password=x",
+                                     headers={"Content-Type": "application/x-www-form-urlencoded"}, method="POST")
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(bad, context=ctx, timeout=30)
+        assert e.value.code == 401
+    finally:
+        srv.shutdown()
