@@ -401,6 +401,12 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
   };
   reset();
   load_rows(blk0);
+  // The row operands (Q, dO, O, lse) are complete before the tile loop.  This must be the
+  // compiler-visible builtin, not asm: the waitcnt pass does not see the LDS-DMA issued
+  // from inline asm, so without it the pass keeps these pre-loop loads "in flight" and
+  // puts vmcnt(3..0) waits in front of the loop's MFMAs -- which the hardware counter
+  // resolves by waiting for the NEXT tile's DMA too (load latency exposed every tile).
+  __builtin_amdgcn_s_waitcnt(0);
 
   // lane-constant LDS offsets (the 32-row subtile steps are immediates)
   int offK[NKK];
@@ -583,6 +589,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
         finalize();
         reset();
         load_rows(blk1);
+        __builtin_amdgcn_s_waitcnt(0);   // (see after the first load_rows)
       }
       compute(Kc, Vc, tile_of(t));
     }
@@ -772,6 +779,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
       }
   };
   load_keys(blk0);
+  __builtin_amdgcn_s_waitcnt(0);  // K / V rows complete before the loop (see qmajor)
   const int krow = 32 * wl + r;   // this lane's row of the K image (D = 128)
   if constexpr (!KREG) {
     constexpr int KCH = KW * CPR / 256;
@@ -911,6 +919,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
       if (PAIR && CAUSAL && team == 1 && t == sw) {   // team 1: light block done, on to the heavy one
         finalize();
         load_keys(blk1);
+        __builtin_amdgcn_s_waitcnt(0);   // (see qmajor)
       }
       compute(Qc, Oc, Lc, Dc, t);
     }
