@@ -113,7 +113,11 @@ __device__ __forceinline__ void dma4(const void* g, char* lds_base) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
                :: "v"(g), "s"(lds_u32(lds_base)) : "memory", "m0");
 }
-__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// vmcnt(0) through the builtin (expcnt / lgkmcnt fields at their "no wait" maxima), not asm:
+// the waitcnt pass then knows every compiler-visible load (e.g. the dropout words of the
+// previous step) is complete, instead of re-waiting for them mid-tile with a vmcnt(N) that
+// the hardware also applies to the asm-issued DMA of the next tile.
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 // dropout: all-ones halves for the kept elements of packed pair j (elements 2j, 2j+1)
 __device__ __forceinline__ uint32_t pair_keep(uint32_t w, int sh, int j) {
