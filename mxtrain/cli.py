@@ -182,7 +182,46 @@ def cmd_dashboard(a):
     for k in ("certfile", "keyfile", "htpasswd"):
         if getattr(a, k):
             argv += [f"--{k}", getattr(a, k)]
+    for k in ("oidc", "tls_auto"):
+        if getattr(a, k, False):
+            argv.append("--" + k.replace("_", "-"))
     return dash(argv)
+
+
+def cmd_identity(a):
+    from .mlplatform.identity import main as idm
+    return idm(a.args)
+
+
+def cmd_platform(a):
+    """The Kubeflow module of the reference (terraform kubeflow/): bring up the node's
+    platform services in one step -- the user's profile (namespace, owner, GPU quota), the
+    identity-provider user, the dashboard's certificate from the node CA, then the central
+    dashboard behind TLS + OIDC sessions (jobs, volumes, tensorboards, HPO, pipelines API)."""
+    from .mlplatform import identity as idp
+    from .mlplatform import profiles as pr
+    ns = a.namespace
+    plan = {"profile": ns, "owner": a.user}
+    if not any((p.get("metadata") or {}).get("name") == ns for p in pr.list_profiles()):
+        pr.create(ns, owner=a.user, gpu_quota=a.gpu_quota)
+        plan["profile_created"] = True
+    if a.user not in idp.load_users():
+        pw = os.environ.get("MXTRAIN_PLATFORM_PASSWORD") or sys.stdin.readline().rstrip("\n")
+        if not pw:
+            print("platform up: the first run needs the user's password on stdin "
+                  "(or MXTRAIN_PLATFORM_PASSWORD)", file=sys.stderr)
+            return 2
+        idp.add_user(a.user, pw)
+        plan["user_created"] = True
+    dns = ["localhost"] + ([a.host] if a.host not in ("127.0.0.1", "0.0.0.0", "localhost") else [])
+    cert = idp.issue_cert("dashboard", dns, ips=["127.0.0.1"])
+    plan.update({"cert": cert["cert"], "ca": cert["ca"], "url": f"https://{dns[-1]}:{a.port}/"})
+    print(json.dumps(plan, indent=1), flush=True)
+    if a.dry_run:
+        return 0
+    from .mlplatform.dashboard import main as dash
+    return dash(["--host", a.host, "--port", str(a.port), "--certfile", cert["cert"], "--keyfile", cert["key"],
+                 "--oidc"])
 
 
 def cmd_profile(a):
@@ -280,7 +319,21 @@ def build_parser():
     q.add_argument("--certfile")
     q.add_argument("--keyfile")
     q.add_argument("--htpasswd")
+    q.add_argument("--oidc", action="store_true", help="bearer / session JWTs of the node identity provider")
+    q.add_argument("--tls-auto", action="store_true", help="HTTPS with a certificate from the node CA")
     q.set_defaults(fn=cmd_dashboard)
+    q = sp.add_parser("identity", help="identity provider users / node certificates (Dex, cert-manager roles)")
+    q.add_argument("args", nargs=argparse.REMAINDER)
+    q.set_defaults(fn=cmd_identity)
+    q = sp.add_parser("platform", help="bring up the platform services (profile, user, certificate, dashboard)")
+    q.add_argument("action", choices=["up"])
+    q.add_argument("--user", default="user@example.com")
+    q.add_argument("--namespace", default=rel.DEFAULT_NS)
+    q.add_argument("--gpu-quota", type=int, default=None)
+    q.add_argument("--host", default="127.0.0.1")
+    q.add_argument("--port", type=int, default=8443)
+    q.add_argument("--dry-run", action="store_true", help="set up, print the plan, do not serve")
+    q.set_defaults(fn=cmd_platform)
     q = sp.add_parser("profile", help="namespaces (Kubeflow Profiles): quotas, owners, PodDefaults")
     q.add_argument("action", choices=["create", "list", "delete", "poddefault"])
     q.add_argument("name", nargs="?", default=rel.DEFAULT_NS)

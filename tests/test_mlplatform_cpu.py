@@ -345,3 +345,26 @@ def test_identity_tokens_and_node_certificates(home, tmp_path):
         assert e.value.code == 401
     finally:
         srv.shutdown()
+
+
+def test_platform_up_dry_run(home):
+    """`mxtrain platform up` (the reference's Kubeflow module): profile + identity user +
+    dashboard certificate in one step; idempotent on a second run."""
+    import subprocess
+    import sys
+    env = dict(os.environ, PYTHONPATH=REPO, MXTRAIN_PLATFORM_PASSWORD="pw1")
+    cmd = [sys.executable, "-m", "mxtrain", "platform", "up", "--user", "bob@example.com", "--namespace", "team-a",
+           "--gpu-quota", "4", "--dry-run"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    plan = json.loads(r.stdout)
+    assert plan["profile_created"] and plan["user_created"] and plan["url"].startswith("https://")
+    from mxtrain.mlplatform import identity as idp
+    from mxtrain.mlplatform import profiles as pr
+    assert idp.password_grant("bob@example.com", "pw1")["token_type"] == "Bearer"
+    assert pr.gpu_quota("team-a") == 4 and pr.can("bob@example.com", "create", "team-a")
+    r = subprocess.run(cmd, env=dict(env, MXTRAIN_PLATFORM_PASSWORD=""), capture_output=True, text=True, timeout=120,
+                       stdin=subprocess.DEVNULL)
+    assert r.returncode == 0, r.stderr
+    plan = json.loads(r.stdout)
+    assert "profile_created" not in plan and "user_created" not in plan
