@@ -103,10 +103,12 @@ def main():
                     help="run weight-gradient GEMMs on a concurrent side stream")
     ap.add_argument("--no-maskrcnn", action="store_true",
                     help="skip the Mask R-CNN images/s measurements (run on one GPU only)")
-    ap.add_argument("--xgmi", choices=["0", "1", "auto"], default="auto",
+    ap.add_argument("--xgmi", choices=["0", "1", "auto"], default="0",
                     help="direct xGMI peer-to-peer collectives (csrc/comm/xgmi.hip) for the DP "
-                         "reduce-scatter / all-gather and TP all-reduce: 0 = RCCL only, 1 = always, "
-                         "auto = verify against RCCL and keep the faster per message size (N > 1)")
+                         "reduce-scatter / all-gather and TP all-reduce: 0 = RCCL only (default: the "
+                         "xGMI kernels have only been exercised by processes sharing one GPU, so the "
+                         "scaling runs use RCCL over xGMI), 1 = always, auto = verify against RCCL and "
+                         "keep the faster per message size (N > 1)")
     args = ap.parse_args()
     os.environ.setdefault("MXTRAIN_XGMI", args.xgmi)
 
