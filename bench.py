@@ -115,6 +115,10 @@ def main():
     import torch
     import torch.distributed as dist
 
+    def _sync():
+        if torch.cuda.is_available():   # (CPU / gloo rehearsal runs: tests/test_bench_cpu.py)
+            torch.cuda.synchronize()
+
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from mxtrain.models.gpt import GPT_CONFIGS, GPTConfig
     from mxtrain.parallel import state as pstate
@@ -175,9 +179,9 @@ def main():
                 graph_err = graph_err or "capture failed on another rank"
     for _ in range(2 if use_graph else 0):
         tr.train_step(tokens, labels)
-    torch.cuda.synchronize()
+    _sync()
     barrier()
-    torch.cuda.synchronize()
+    _sync()
     t0 = time.perf_counter()
     loss = None
     for _ in range(args.steps):
@@ -185,9 +189,9 @@ def main():
     # a deferred AdamW (overlap_optimizer) of the last step is applied inside the timed
     # window too: K + 1 optimizer updates are timed for K steps
     tr.sync_params()
-    torch.cuda.synchronize()
+    _sync()
     barrier()
-    torch.cuda.synchronize()
+    _sync()
     t1 = time.perf_counter()
     ms = (t1 - t0) * 1000.0 / args.steps
     if world > 1:
@@ -239,7 +243,8 @@ def main():
         if world == 1 and not args.no_maskrcnn:
             # BASELINE.json metric, part 2: Mask R-CNN images/s (outside the GPT timed window)
             del tr
-            torch.cuda.empty_cache()
+            if torch.cuda.is_available():
+                torch.cuda.empty_cache()
             m1 = run_maskrcnn(1, 60, 15)
             m4 = run_maskrcnn(4, 40, 10)
             out["maskrcnn_img_s_1img"] = m1.get("img_s")

@@ -1,0 +1,30 @@
+"""bench.py contract rehearsed on the CPU: two gloo ranks through torch.distributed.run
+(127.0.0.1 rendezvous), a tiny GPT, one JSON line from rank 0 with the driver's fields --
+the N > 1 path (MAX over ranks, whole-job tokens/s) the scaling runs take on MI355X."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_two_ranks_gloo_json_line():
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--model", "gpt-tiny", "--no-maskrcnn",
+           "--no-tuned-gemm"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
+    assert d["config"]["parallelism"].startswith("dp2") and d["value"] > 0
+    # whole-job tokens/s: global batch x seq / step time
+    tok = d["config"]["global_batch"] * d["config"]["seq_len"]
+    assert abs(d["value"] - tok / (d["ms_per_step"] / 1000.0)) / d["value"] < 0.01
