@@ -197,12 +197,19 @@ __device__ __forceinline__ uint32_t drop_stream_bits(uint32_t rbase, uint32_t kb
 //   subtile t of a 128-key tile in word t>>1 at sh = 8 (t & 1).
 // bwd image (key on lane):   u32 [B*Hq][NB][NQT][64 lanes], 16 bits per 32-query half of a
 //   64-query tile at sh = 8 u.
+// blockIdx.z = layer * BH + bh: the images of several layers (salt + layer, images at
+// layer * stride) in one launch -- every layer's masks of a step depend only on the seed, so
+// the model generates them all up front (one launch instead of one per layer).
 __global__ __launch_bounds__(256) void flash_dropmask_kernel(
     const uint32_t* __restrict__ seed_ptr, uint32_t salt, uint32_t thr16, int S, int Hq,
     int h_off, int Hg, int NB, int NKT, int NQT, int causal, uint32_t* __restrict__ fwd_bits,
-    uint32_t* __restrict__ bwd_bits) {
+    uint32_t* __restrict__ bwd_bits, int BH, long long fwd_stride, long long bwd_stride) {
   const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
-  const int qb2 = blockIdx.x, kb2 = blockIdx.y * 4 + w, bh = blockIdx.z;
+  const int layer = blockIdx.z / BH;
+  const int qb2 = blockIdx.x, kb2 = blockIdx.y * 4 + w, bh = blockIdx.z - layer * BH;
+  salt += (uint32_t)layer;
+  fwd_bits += (size_t)layer * fwd_stride;
+  bwd_bits += (size_t)layer * bwd_stride;
   const int NB2 = (NB + 1) >> 1;
   __shared__ uint32_t fw[4][2][64];
   const bool live = kb2 < NB2 && !(causal && kb2 > qb2);
@@ -1038,7 +1045,22 @@ MX_EXPORT int mx_flash_dropmask(const uint32_t* seed, uint32_t salt, float p, in
   const uint32_t thr16 = (uint32_t)(p * 65536.0f + 0.5f);
   hipLaunchKernelGGL(flash_dropmask_kernel, dim3(NB2, (NB2 + 3) / 4, B * Hq), dim3(256), 0, s, seed,
                      salt, thr16, S, Hq, h_off, Hg, NB, NKT, NQT, causal, (uint32_t*)fwd_bits,
-                     (uint32_t*)bwd_bits);
+                     (uint32_t*)bwd_bits, B * Hq, 0ll, 0ll);
+  return hipGetLastError();
+}
+
+// the images of L layers (salts salt, salt + 1, ...) in one launch; layer l's images start
+// at fwd_bits + l * fwd_words (uint32 words) and bwd_bits + l * bwd_words
+MX_EXPORT int mx_flash_dropmask_layers(const uint32_t* seed, uint32_t salt, float p, int B, int S, int Hq,
+                                       int h_off, int Hg, int causal, int L, void* fwd_bits, void* bwd_bits,
+                                       long long fwd_words, long long bwd_words, hipStream_t s) {
+  if (L < 1 || (long long)B * Hq * L > 65535) return hipErrorInvalidValue;
+  const int NB = (S + 31) / 32, NKT = (S + 127) / 128, NQT = (S + 63) / 64;
+  const int NB2 = (NB + 1) / 2;
+  const uint32_t thr16 = (uint32_t)(p * 65536.0f + 0.5f);
+  hipLaunchKernelGGL(flash_dropmask_kernel, dim3(NB2, (NB2 + 3) / 4, B * Hq * L), dim3(256), 0, s, seed,
+                     salt, thr16, S, Hq, h_off, Hg, NB, NKT, NQT, causal, (uint32_t*)fwd_bits,
+                     (uint32_t*)bwd_bits, B * Hq, fwd_words, bwd_words);
   return hipGetLastError();
 }
 

@@ -294,6 +294,16 @@ class StepRuntime:
     # of this rank's own token chunk (the other chunks' GEMMs follow the gather)
     tp_overlap: bool = True
     sp_gemm_overlap: bool = True
+    # deferred column reductions (ops/norm.py ColReduceQueue: LN / bias gradients folded in one
+    # launch at the end of backward); set by the trainer when no per-bucket gradient
+    # reduction runs during backward (one DP rank, no TP / PP)
+    colq: Optional[object] = None
+    # attention-dropout masks of every layer of the stage for the current step (generated in
+    # one launch before the first layer; reset by the trainer at each step start)
+    dmasks: Optional[List] = None
+    dmask_l0: int = 0
+    dmask_key: Optional[tuple] = None
+    batch_dmasks: bool = False    # GPTTrainer turns it on (it resets dmasks when the seed advances)
 
     @property
     def p_drop(self):
@@ -456,7 +466,7 @@ class EmbedFn(torch.autograd.Function):
         gw, gb = rt.norm_grads(f"layers.{ctx.first_layer}.ln1")
         _, de = norm_bwd(da.contiguous(), dh.contiguous(), h, mean, rstd, w, want_dx=True,
                          p=rt.p_drop, seed_t=rt.seed_t, salt=rt.salt(SALT_EMB), rms=rt.rms,
-                         dgamma=gw, dbeta=gb, accumulate=True)
+                         dgamma=gw, dbeta=gb, accumulate=True, defer=rt.colq)
         if rt.sp:
             de = C.all_gather_dim0(de, rt.tp_group)
         embed_bwd(ids, de, rt.grads["wte"], rt.vocab_start)
@@ -485,7 +495,7 @@ class NormFn(torch.autograd.Function):
         h, mean, rstd = ctx.saved
         w, _ = rt.norm_params(ctx.prefix)
         gw, gb = rt.norm_grads(ctx.prefix)
-        dh, _ = norm_bwd(da.contiguous(), None, h, mean, rstd, w, rms=rt.rms, dgamma=gw,
+        dh, _ = norm_bwd(da.contiguous(), None, h, mean, rstd, w, rms=rt.rms, defer=rt.colq, dgamma=gw,
                          dbeta=gb, accumulate=True)
         ctx.saved = None
         rt.done(ctx.unit)
@@ -519,7 +529,9 @@ class GPTLayerFn(torch.autograd.Function):
         kvl = cfg.num_kv_heads // rt.tp
         eps = cfg.layernorm_epsilon
         dmask = None
-        if rt.p_attn > 0:
+        if rt.p_attn > 0 and rt.dmasks is not None:   # this step's masks, all layers at once
+            dmask = rt.dmasks[i - rt.dmask_l0]
+        elif rt.p_attn > 0:
             # the keep-mask depends only on the seed: generated on the side stream while the
             # QKV GEMM runs (the GEMM's grid leaves CUs free)
             ha_ = hl // rt.cp
@@ -603,13 +615,13 @@ class GPTLayerFn(torch.autograd.Function):
             dh1, dg = norm_bwd(da2.contiguous(), dh2, h2, mean_n, rstd_n, wn, want_dx=True,
                                p=rt.p_drop, seed_t=rt.seed_t, salt=rt.salt(1001 + 2 * i),
                                rms=rt.rms, dgamma=gwn, dbeta=gbn, dbias=G.get(p + "fc2_b"),
-                               accumulate=True)
+                               accumulate=True, defer=rt.colq)
         else:
             wn = P[p + "ln2_w"]
             zero = torch.zeros_like(dh2)
             dh1, dg = norm_bwd(zero, dh2, h2, mean_n, rstd_n, wn, want_dx=True, p=rt.p_drop,
                                seed_t=rt.seed_t, salt=rt.salt(1001 + 2 * i), rms=rt.rms,
-                               dbias=G.get(p + "fc2_b"), accumulate=True)
+                               dbias=G.get(p + "fc2_b"), accumulate=True, defer=rt.colq)
         # ---- MLP backward
         if ctx.moe is not None:
             m_leaf, leaves, g_moe, l_aux = ctx.moe
@@ -630,7 +642,7 @@ class GPTLayerFn(torch.autograd.Function):
             dpre = bias_swiglu_bwd(df, pre, P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True)
         else:
             dpre = bias_gelu_bwd(df, pre, P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True,
-                                 inplace=True)
+                                 inplace=True, defer=rt.colq)
         # dgrad first: its TP combine overlaps the fc2 + fc1 weight-gradient GEMMs (one
         # grouped launch, both operands read in place)
         pend = _reduce_start(torch.mm(dpre, P[p + "fc1_w"]), rt)
@@ -652,7 +664,7 @@ class GPTLayerFn(torch.autograd.Function):
         gw2, gb2 = rt.norm_grads(p + "ln2")
         dh, do_ = norm_bwd(dm, dh1, h1, mean2, rstd2, w2, want_dx=True, p=rt.p_drop,
                            seed_t=rt.seed_t, salt=rt.salt(1000 + 2 * i), rms=rt.rms, dgamma=gw2,
-                           dbeta=gb2, dbias=G[p + "proj_b"], accumulate=True)
+                           dbeta=gb2, dbias=G[p + "proj_b"], accumulate=True, defer=rt.colq)
         # ---- attention backward
         do_full, dctx = _gather_mm(do_, P[p + "proj_w"], rt, trans=False)
         if rt.cp > 1:
@@ -672,7 +684,7 @@ class GPTLayerFn(torch.autograd.Function):
         if rt.cp > 1:
             dqkv = head_to_seq(dqkv, (hl * D, kvl * D, kvl * D), rt.B, rt.S, rt.cp_group)
         pend = _reduce_start(torch.mm(dqkv, P[p + "qkv_w"]), rt)
-        colsum(dqkv, G[p + "qkv_b"], accumulate=True)
+        colsum(dqkv, G[p + "qkv_b"], accumulate=True, defer=rt.colq)
         rt.wgrad((G[p + "proj_w"], do_full, ctx_), (G[p + "qkv_w"], dqkv, a_full))
         da = pend.wait()
         rt.done(i + 1)
@@ -769,6 +781,20 @@ class GPTStage:
             h = hidden
             rt.need(self.l0)
             a = NormFn.apply(h, rt, f"layers.{self.l0}.ln1", self.l0)
+        if rt.dmasks is not None and rt.dmask_key != (rt.B, rt.S):
+            rt.dmasks = None
+        if (rt.p_attn > 0 and rt.batch_dmasks and rt.dmasks is None and self.l1 > self.l0
+                and rt.seed_t is not None and rt.seed_t.is_cuda):
+            rt.dmask_key = (rt.B, rt.S)
+            cfg = self.cfg
+            hl = cfg.num_attention_heads // rt.tp
+            ha_ = hl // rt.cp
+            rt.dmask_l0 = self.l0
+            rt.dmasks = attn_ops.dropmask_layers(rt.B, rt.S * rt.cp, ha_, rt.p_attn,
+                                                 rt.attn_seed_t if rt.attn_seed_t is not None else rt.seed_t,
+                                                 SALT_ATTN + self.l0, self.l1 - self.l0,
+                                                 head_offset=rt.tp_rank * hl + rt.cp_rank * ha_,
+                                                 total_heads=cfg.num_attention_heads, causal=True)
         for i in range(self.l0, self.l1):
             if i + 1 < self.l1:
                 nxt = f"layers.{i + 1}.ln1"

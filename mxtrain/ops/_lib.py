@@ -39,6 +39,8 @@ SIGNATURES = {
     "mx_colsum_finalize": [P, I, I, I, P, P, P, I, P, P],
     "mx_colreduce_scratch": [I, I],
     "mx_colsum_bf16": [P, I, I, P, P, I, P],
+    "mx_colreduce_batched": [P, I, I, P],
+    "mx_colsum_partial_bf16": [P, I, I, P, P],
     # epilogue.hip
     "mx_bias_act_fwd": [P, P, P, I64, I, I, P],
     "mx_bias_act_bwd_parts": [I64, I],
@@ -77,6 +79,7 @@ SIGNATURES = {
     "mx_adamw_step": [P, P, P, P, P, P, I64, P, P, P],
     # flash.hip
     "mx_flash_dropmask": [P, U32, F, I, I, I, I, I, I, P, P, P],
+    "mx_flash_dropmask_layers": [P, U32, F, I, I, I, I, I, I, I, P, P, I64, I64, P],
     "mx_flash_fwd": [P, P, P, I, I, I, P, I, P, I, I, I, I, I, I, P, F, P, F, P],
     "mx_flash_bwd": [P, P, P, I, I, I, P, I, P, I, P, P, P, I, P, P, I, I, I, I, I, I, I, I,
                      P, F, P, P, F, P],

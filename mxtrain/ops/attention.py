@@ -138,6 +138,24 @@ def dropmask(B, S, Hq, p, seed_t, salt=0, head_offset=0, total_heads=None, causa
     return DropMask(p, fbits, bbits, event=ev)
 
 
+def dropmask_layers(B, S, Hq, p, seed_t, salt, L, head_offset=0, total_heads=None, causal=True,
+                    device=None):
+    """The keep-mask images of L consecutive layers (salts salt .. salt + L - 1) in ONE
+    launch -- identical to L dropmask() calls; a step's masks depend only on its seed, so
+    the model generates them all before the first layer (one launch instead of one per
+    layer, and the single large grid keeps the chip full).  Returns [DropMask] * L."""
+    device = device if device is not None else seed_t.device
+    if device.type != "cuda" or not _lib.use_hip(seed_t):
+        return [dropmask(B, S, Hq, p, seed_t, salt + l, head_offset, total_heads, causal, device) for l in range(L)]
+    NB, NKT, NQT = (S + 31) // 32, (S + 127) // 128, (S + 63) // 64
+    nf, nb = B * Hq * NB * NKT * 64, B * Hq * NB * NQT * 64
+    fbits = torch.empty(L, nf, dtype=torch.int64, device=device)
+    bbits = torch.empty(L, nb, dtype=torch.int32, device=device)
+    _lib.call("mx_flash_dropmask_layers", _lib.ptr(seed_t), int(salt) & M32, float(p), B, S, Hq, int(head_offset),
+              int(total_heads or Hq), int(causal), L, _lib.ptr(fbits), _lib.ptr(bbits), 2 * nf, nb, _lib.stream())
+    return [DropMask(p, fbits[l], bbits[l]) for l in range(L)]
+
+
 def attn_fwd(q, k, v, B, S, Hq, Hkv, D, causal=True, klen=None, scale=None, dropout_p=0.0,
              seed_t=None, salt=0, head_offset=0, total_heads=None, dmask=None):
     """Returns (o, lse, dmask): dmask is the DropMask backward needs (None without dropout).

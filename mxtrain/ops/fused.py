@@ -30,7 +30,7 @@ def bias_gelu_fwd(x, bias):
     return y
 
 
-def bias_gelu_bwd(dy, x, bias, dbias=None, accumulate=False, inplace=False):
+def bias_gelu_bwd(dy, x, bias, dbias=None, accumulate=False, inplace=False, defer=None):
     """dx = dy * gelu'(x + b); dbias (+)= dx.sum(0).  ``inplace`` writes dx over dy."""
     rows, cols = dy.shape
     if not _lib.use_hip(dy):
@@ -47,6 +47,13 @@ def bias_gelu_bwd(dy, x, bias, dbias=None, accumulate=False, inplace=False):
     dx = dy if inplace else torch.empty_like(dy)
     rpb = _lib.query("mx_bias_gelu_bwd_rows_per_block")
     nparts = (rows + rpb - 1) // rpb
+    partial = None
+    if defer is not None and dbias is not None:
+        partial = defer.partial((dbias.data_ptr(),), (dbias, None, None), nparts, cols, 1, cols, accumulate)
+    if partial is not None:   # partials now, the dbias reduction in the step's batched flush
+        _lib.call("mx_bias_gelu_bwd", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(bias), _lib.ptr(dx),
+                  None, int(accumulate), _lib.ptr(partial), rows, cols, _lib.stream())
+        return dx
     scratch_n = _lib.query64("mx_colreduce_scratch", nparts, cols)
     partial = torch.empty(nparts * cols + scratch_n, dtype=torch.float32, device=dy.device)
     _lib.call("mx_bias_gelu_bwd", _lib.ptr(dy), _lib.ptr(x), _lib.ptr(bias), _lib.ptr(dx),

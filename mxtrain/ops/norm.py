@@ -85,7 +85,7 @@ def bda_norm_fwd(x, bias, residual, gamma, beta, eps=1e-5, p=0.0, seed_t=None, s
 
 # ------------------------------------------------------------------ backward
 def norm_bwd(dy, dres, h, mean, rstd, gamma, want_dx=False, p=0.0, seed_t=None, salt=0,
-             rms=False, dgamma=None, dbeta=None, dbias=None, accumulate=False):
+             rms=False, dgamma=None, dbeta=None, dbias=None, accumulate=False, defer=None):
     """Backward of (bda_)norm.
 
     dh = dres + dnorm/dh;  dx = dh * dropout-mask * 1/(1-p) (if want_dx).
@@ -120,14 +120,22 @@ def norm_bwd(dy, dres, h, mean, rstd, gamma, want_dx=False, p=0.0, seed_t=None, 
                     buf.copy_(val.to(buf.dtype))
         return dh, dx
     nparts = _lib.query("mx_norm_bwd_nparts2", rows, cols)
-    scratch_n = _lib.query64("mx_colreduce_scratch", nparts, 3 * cols)
-    partial = torch.empty(nparts * 3 * cols + scratch_n, dtype=torch.float32, device=dy.device)
+    outs = (dgamma, dbeta, dbias if want_dx else None)
+    want = any(t is not None for t in outs)
+    partial = None
+    if defer is not None and want:
+        partial = defer.partial(tuple(t.data_ptr() if t is not None else 0 for t in outs), outs, nparts,
+                                3 * cols, 3, cols, accumulate)
+    deferred = partial is not None
+    if partial is None:
+        scratch_n = _lib.query64("mx_colreduce_scratch", nparts, 3 * cols)
+        partial = torch.empty(nparts * 3 * cols + scratch_n, dtype=torch.float32, device=dy.device)
     dh = torch.empty_like(dy)
     dx = torch.empty_like(dy) if want_dx else None
     _lib.call("mx_norm_bwd", _lib.ptr(dy), _lib.ptr(dres), _lib.ptr(h), _lib.ptr(mean),
               _lib.ptr(rstd), _lib.ptr(gamma), _lib.ptr(dh), _lib.ptr(dx), _lib.ptr(partial),
               rows, cols, float(p), _lib.ptr(seed_t), salt, int(rms), _lib.stream())
-    if dgamma is not None or dbeta is not None or dbias is not None:
+    if want and not deferred:
         scratch = partial[nparts * 3 * cols:]
         _lib.call("mx_colsum_finalize", _lib.ptr(partial), nparts, cols, 3, _lib.ptr(dgamma),
                   _lib.ptr(dbeta), _lib.ptr(dbias if want_dx else None), int(accumulate),
@@ -135,8 +143,9 @@ def norm_bwd(dy, dres, h, mean, rstd, gamma, want_dx=False, p=0.0, seed_t=None, 
     return dh, dx
 
 
-def colsum(x, out, accumulate=False):
-    """out (bf16 [cols]) (+)= x.sum(0) for x [rows, cols] bf16."""
+def colsum(x, out, accumulate=False, defer=None):
+    """out (bf16 [cols]) (+)= x.sum(0) for x [rows, cols] bf16 (``defer``: partials now,
+    reduction in the step's batched flush)."""
     rows, cols = x.shape
     if not _lib.use_hip(x):
         v = x.float().sum(0)
@@ -145,11 +154,101 @@ def colsum(x, out, accumulate=False):
         out.copy_(v.to(out.dtype))
         return out
     nparts = (rows + 15) // 16
+    if defer is not None:
+        part = defer.partial((out.data_ptr(),), (out, None, None), nparts, cols, 1, cols, accumulate)
+        if part is not None:
+            _lib.call("mx_colsum_partial_bf16", _lib.ptr(x), rows, cols, _lib.ptr(part), _lib.stream())
+            return out
     scratch_n = _lib.query64("mx_colreduce_scratch", nparts, cols)
     partial = torch.empty(nparts * cols + scratch_n, dtype=torch.float32, device=x.device)
     _lib.call("mx_colsum_bf16", _lib.ptr(x), rows, cols, _lib.ptr(partial), _lib.ptr(out),
               int(accumulate), _lib.stream())
     return out
+
+
+# ------------------------------------------------------------------ deferred column sums
+class ColReduceQueue:
+    """Column reductions of a training step deferred to ONE batched launch
+    (``mx_colreduce_batched``) at the end of backward, instead of one colreduce launch per
+    norm / bias-GeLU / bias producer (~100 per GPT-2 345M step).
+
+    Every distinct output (LN dgamma/dbeta/dbias triple, bias gradient) owns a fixed region
+    of a persistent fp32 arena holding the partials of all its producer calls of the step
+    (micro-batches stacked), so the flush is one job per output -- a single accumulate
+    into the bf16 gradient, no two jobs writing the same output.  The layout is recorded
+    on the first step (which reduces immediately), then reused; a step whose producer
+    sequence differs from the recorded one is an error (the step structure is static for a
+    fixed model / batch configuration).  Only used when nothing consumes these gradients
+    before the optimizer (one data-parallel rank, no TP / PP: no per-bucket reductions
+    during backward)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.layout = None      # [(key, nparts, C, nvec, cols, accumulate)] in call order
+        self.rec = []
+        self.arena = None
+        self.table = None
+        self.regions = {}       # key -> (offset, rows_total, C, nvec, cols, outs, acc)
+        self.i = 0
+        self.active = False
+
+    def begin(self):
+        self.i = 0
+        self.rec = []
+        self.fill = {}
+        self.active = self.layout is not None
+
+    def partial(self, key, outs, nparts: int, C: int, nvec: int, cols: int, accumulate: bool):
+        """fp32 [nparts * C] view for this producer's partials when deferred, else None
+        (caller finalizes immediately; the call is recorded for the layout)."""
+        spec = (key, nparts, C, nvec, cols, bool(accumulate))
+        if not self.active:
+            self.rec.append((spec, outs))
+            return None
+        if self.i >= len(self.layout) or self.layout[self.i] != spec:
+            raise RuntimeError("deferred column reductions: the step's producer sequence changed "
+                               f"at call {self.i} ({spec[1:]})")
+        self.i += 1
+        off, rows, *_ = self.regions[key]
+        k = self.fill.get(key, 0)
+        self.fill[key] = k + nparts
+        return self.arena[off + k * C: off + (k + nparts) * C]
+
+    def flush(self):
+        """End of backward: reduce every deferred job (one launch); on the recording step
+        build the layout for the next ones."""
+        if self.active:
+            if self.i != len(self.layout):
+                raise RuntimeError("deferred column reductions: step ended after "
+                                   f"{self.i} of {len(self.layout)} producers")
+            _lib.call("mx_colreduce_batched", _lib.ptr(self.table), self.njobs, self.nblocks, _lib.stream())
+            return
+        if not self.rec or torch.cuda.is_current_stream_capturing():
+            return
+        regions, order, off = {}, [], 0
+        for (key, nparts, C, nvec, cols, acc), outs in self.rec:
+            if key not in regions:
+                regions[key] = [off, 0, C, nvec, cols, outs, acc]
+                order.append(key)
+            r = regions[key]
+            if (r[2], r[3], r[4], r[6]) != (C, nvec, cols, acc):
+                return    # the same output reduced with different shapes: keep immediate mode
+            r[1] += nparts
+        for key in order:           # regions laid out in first-use order
+            r = regions[key]
+            r[0] = off
+            off += r[1] * r[2]
+        self.arena = torch.empty(max(off, 1), dtype=torch.float32, device=self.device)
+        rows, blk = [], 0
+        for key in order:
+            o, nrows, C, nvec, cols, outs, acc = regions[key]
+            rows.append([self.arena.data_ptr() + 4 * o, nrows, C, cols] +
+                        [(t.data_ptr() if t is not None else 0) for t in outs] + [int(acc), blk])
+            blk += (C + 15) // 16
+        self.table = torch.tensor(rows, dtype=torch.int64).to(self.device)
+        self.njobs, self.nblocks = len(rows), blk
+        self.regions = {k: tuple(v) for k, v in regions.items()}
+        self.layout = [spec for spec, _ in self.rec]
 
 
 # ------------------------------------------------------------------ autograd wrappers

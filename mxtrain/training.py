@@ -10,6 +10,7 @@ step (`capture_graph=True`).
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass
 from typing import Optional
@@ -80,6 +81,7 @@ class GPTTrainer:
                               sequence_parallel=ps.sequence_parallel, seed_t=self.seed.t,
                               cp=ps.cp, cp_rank=ps.cp_rank, cp_group=ps.cp_group,
                               attn_seed_t=self.seed.attn_t)
+        self.stage.rt.batch_dmasks = os.environ.get("MXTRAIN_BATCH_DMASKS", "1") != "0"
         if tcfg.wgrad_stream and self.device.type == "cuda":
             self.stage.rt.wgrad_stream = torch.cuda.Stream(device=self.device)
         self._overwrite = bool(tcfg.overwrite_wgrads and ps.pp == 1)
@@ -102,6 +104,13 @@ class GPTTrainer:
             overlap_update=(tcfg.overlap_optimizer and self.device.type == "cuda" and ps.pp == 1
                             and self.eopt is None and not tcfg.wgrad_stream))
         self._setup_xgmi()
+        # LN / bias gradient column reductions folded into one launch at the end of backward
+        # when nothing reads those gradients before the optimizer (no DP / TP / PP reduction
+        # during backward): ~100 colreduce launches of a GPT-2 step become one
+        if (self.device.type == "cuda" and ps.grad_world == 1 and ps.tp == 1 and ps.pp == 1 and self.eopt is None
+                and not self.opt.overlap_update and os.environ.get("MXTRAIN_DEFER_COLREDUCE", "1") != "0"):
+            from .ops.norm import ColReduceQueue
+            self.stage.rt.colq = ColReduceQueue(self.device)
         self.pipeline = None
         if ps.pp > 1:
             from .parallel.pipeline import PipelineSchedule
@@ -236,6 +245,9 @@ class GPTTrainer:
             self.stage.rt.aux_log.clear()
         self.seed.advance()
         self.stage.rt.grad_scale = 1.0 / (nm * B * S)
+        if self.stage.rt.colq is not None:
+            self.stage.rt.colq.begin()
+        self.stage.rt.dmasks = None   # regenerated (all layers, one launch) by the first forward
 
     def _train_step_eager(self, tokens, labels):
         nm, B, S = tokens.shape
@@ -248,6 +260,8 @@ class GPTTrainer:
                 loss = loss + self._micro_forward_backward(tokens[m].reshape(-1),
                                                            labels[m].reshape(-1), B, S,
                                                            m == nm - 1, m == 0)
+        if self.stage.rt.colq is not None:
+            self.stage.rt.colq.flush()
         if self.eopt is not None:
             from .parallel.zero import joint_step
             joint_step(self._opts)
@@ -300,6 +314,8 @@ class GPTTrainer:
                 loss = loss + self._micro_forward_backward(tokens[m].reshape(-1),
                                                            labels[m].reshape(-1), B, S,
                                                            m == nm - 1, m == 0)
+        if self.stage.rt.colq is not None:
+            self.stage.rt.colq.flush()
         # optimizer body without host-side hyper update (done before each replay)
         if self.opt.overlap_update:
             # (dense only) grad norm now, AdamW deferred into the next replay's body

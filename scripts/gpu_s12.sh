@@ -1,0 +1,6 @@
+set -o pipefail
+cd /root/repo && export TMPDIR=/tmp
+timeout -k 10 500 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t12.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --no-maskrcnn > gpurun_out/bench12.log 2>&1 || exit 1
+timeout -k 10 300 env MXTRAIN_DEFER_COLREDUCE=0 python bench.py --no-maskrcnn > gpurun_out/bench12_nodefer.log 2>&1 || exit 1
+bash scripts/gpu_prof_gpt.sh

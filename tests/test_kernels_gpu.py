@@ -499,3 +499,61 @@ def test_gemm_wgrad_group(T, shapes, accumulate, strided, variant, splits):
     for (gb, _, _), ref in zip(items, refs):
         err = (gb.float() - ref).abs().max().item()
         assert err <= 0.01 * ref.abs().max().item() + 0.05, (gb.shape, err)
+
+
+@pytest.mark.parametrize("graph,nm", [(False, 1), (True, 1), (False, 2)])
+def test_deferred_colreduce_matches_immediate(graph, nm, monkeypatch):
+    """LN / bias column reductions deferred to one batched launch at the end of backward
+    (ops/norm.py ColReduceQueue) give the immediate path's trajectory: bit for bit with one
+    micro-batch (same partials, same fixed-order sums), to bf16 rounding with two (one
+    accumulate instead of one per micro-batch)."""
+    from mxtrain.models.gpt import GPTConfig
+    from mxtrain.parallel import state as pstate
+    from mxtrain.training import GPTTrainer, TrainConfig, synthetic_batch
+    ps = pstate.initialize_model_parallel()
+    cfg = GPTConfig(num_layers=3, hidden_size=256, num_attention_heads=4, seq_length=256,
+                    max_position_embeddings=256, vocab_size=1024)
+    runs = []
+    for defer in ("0", "1"):
+        monkeypatch.setenv("MXTRAIN_DEFER_COLREDUCE", defer)
+        tr = GPTTrainer(cfg, TrainConfig(micro_batch_size=2, global_batch_size=2 * nm), ps)
+        assert (tr.stage.rt.colq is not None) == (defer == "1")
+        tok, lab = synthetic_batch(cfg, nm, 2, ps.device, torch.Generator().manual_seed(3))
+        losses = [float(tr.train_step(tok, lab)) for _ in range(2)]
+        if graph:
+            tr.capture(tok, lab, warmup=1)
+        losses += [float(tr.train_step(tok, lab)) for _ in range(3)]
+        torch.cuda.synchronize()
+        tr.sync_params()
+        if defer == "1":
+            assert tr.stage.rt.colq.layout is not None and tr.stage.rt.colq.njobs > 0
+        runs.append((losses, tr.flat.data.clone().float()))
+    if nm == 1:
+        assert runs[0][0] == runs[1][0], (runs[0][0], runs[1][0])
+        assert torch.equal(runs[0][1], runs[1][1])
+    else:
+        for a, b in zip(runs[0][0], runs[1][0]):
+            assert abs(a - b) < 2e-3 * max(1.0, abs(a)), (runs[0][0], runs[1][0])
+        torch.testing.assert_close(runs[1][1], runs[0][1], rtol=2e-2, atol=2e-3)
+
+
+def test_dropmask_layers_match_per_layer_calls(monkeypatch):
+    """All layers' attention-dropout images from one launch equal the per-layer ones (salt +
+    layer), and a GPT training trajectory is unchanged bit for bit."""
+    # (the images' dead causal blocks are never written, so the comparison is the training
+    # trajectory, which reads every live word of every layer's images in fwd, dQ and dK/dV)
+    from mxtrain.models.gpt import GPTConfig
+    from mxtrain.parallel import state as pstate
+    from mxtrain.training import GPTTrainer, TrainConfig, synthetic_batch
+    ps = pstate.initialize_model_parallel()
+    cfg = GPTConfig(num_layers=3, hidden_size=256, num_attention_heads=4, seq_length=256,
+                    max_position_embeddings=256, vocab_size=1024, attention_dropout=0.1)
+    runs = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("MXTRAIN_BATCH_DMASKS", on)
+        tr = GPTTrainer(cfg, TrainConfig(micro_batch_size=2), ps)
+        tok, lab = synthetic_batch(cfg, 1, 2, ps.device, torch.Generator().manual_seed(5))
+        losses = [float(tr.train_step(tok, lab)) for _ in range(3)]
+        torch.cuda.synchronize()
+        runs.append((losses, tr.flat.data.clone()))
+    assert runs[0][0] == runs[1][0] and torch.equal(runs[0][1], runs[1][1])
