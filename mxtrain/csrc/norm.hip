@@ -159,10 +159,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   // a few waves per SIMD: each wave handles several rows to amortise its column partials).
   uint4 hraw[NV], draw[NV], rraw[NV];
   float mean_c = 0.f, rstd_c = 0.f;
-  // (unconditional loads from clamped addresses; the column / dres guards apply where the
-  // values are used: a `cond ? load : 0` select makes the compiler wait for the load right
-  // away, which turned the prefetch back into a serial load -> compute chain)
-  const uint16_t* rsrc = dres ? dres : h;
   auto load_row = [&](int row_, uint4 (&hr)[NV], uint4 (&dr)[NV], uint4 (&rr)[NV], float& mn, float& rs)
       __attribute__((always_inline)) {
     const size_t b_ = (size_t)row_ * cols;
@@ -170,19 +166,25 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     rs = rstd_in[row_];
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      const int c = min((lane + 64 * i) * 8, cols - 8);
-      hr[i] = *reinterpret_cast<const uint4*>(h + b_ + c);
-      dr[i] = *reinterpret_cast<const uint4*>(dy + b_ + c);
-      rr[i] = *reinterpret_cast<const uint4*>(rsrc + b_ + c);
+      const int c = (lane + 64 * i) * 8;
+      const bool ok = c < cols;
+      hr[i] = ok ? *reinterpret_cast<const uint4*>(h + b_ + c) : make_uint4(0, 0, 0, 0);
+      dr[i] = ok ? *reinterpret_cast<const uint4*>(dy + b_ + c) : make_uint4(0, 0, 0, 0);
+      rr[i] = (dres && ok) ? *reinterpret_cast<const uint4*>(dres + b_ + c) : make_uint4(0, 0, 0, 0);
     }
   };
-  // ping-pong register sets A / B (no copy between them: a register copy of an in-flight
-  // load would wait for it right there)
-  uint4 hB[NV], dB[NV], rB[NV];
-  float mean_b = 0.f, rstd_b = 0.f;
-  auto process = [&](int row, const uint4 (&hcur)[NV], const uint4 (&dcur)[NV], const uint4 (&rcur)[NV],
-                     float mean, float rstd) __attribute__((always_inline)) {
+  if (wid < rows) load_row(wid, hraw, draw, rraw, mean_c, rstd_c);
+  for (int row = wid; row < rows; row += nw) {
     const size_t base = (size_t)row * cols;
+    const float mean = mean_c;
+    const float rstd = rstd_c;
+    uint4 hcur[NV], dcur[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) { hcur[i] = hraw[i]; dcur[i] = draw[i]; }
+    uint4 rcur[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) rcur[i] = rraw[i];
+    if (row + nw < rows) load_row(row + nw, hraw, draw, rraw, mean_c, rstd_c);
     float xh[NV][8], gy[NV][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -218,7 +220,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       const int c = (lane + 64 * i) * 8;
       if (c < cols) {
         float r[8], o[8];
-        unpack8(dres ? rcur[i] : make_uint4(0, 0, 0, 0), r);   // zeros without a residual gradient
+        unpack8(rcur[i], r);   // zeros when there is no residual gradient
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = r[j] + rstd * (gy[i][j] - m1 - xh[i][j] * m2);
         *reinterpret_cast<uint4*>(dh_out + base + c) = pack8(o);
@@ -244,14 +246,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         }
       }
     }
-  };
-  if (wid < rows) load_row(wid, hraw, draw, rraw, mean_c, rstd_c);
-  for (int row = wid; row < rows; row += 2 * nw) {
-    if (row + nw < rows) load_row(row + nw, hB, dB, rB, mean_b, rstd_b);
-    process(row, hraw, draw, rraw, mean_c, rstd_c);
-    if (row + nw >= rows) break;
-    if (row + 2 * nw < rows) load_row(row + 2 * nw, hraw, draw, rraw, mean_c, rstd_c);
-    process(row + nw, hB, dB, rB, mean_b, rstd_b);
   }
   if constexpr (!COLS) return;
   float* out = partial + (size_t)blockIdx.x * 3 * cols;
@@ -335,7 +329,9 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict_
 // first block}; block b serves 16 columns of the job whose block range holds b (same
 // fixed-order summation as colreduce_kernel).
 __global__ __launch_bounds__(256) void colreduce_batched_kernel(const int64_t* __restrict__ tab, int njobs) {
-  __shared__ float part[16][17];
+  // block = 64 columns: thread t reads float4 (columns 4 (t & 15) ..) of rows t >> 4, + 16, ...
+  // (16-B loads: these ~330 MB of partials per GPT-2 step stream from HBM)
+  __shared__ float4 part[16][17];
   const int b = blockIdx.x;
   int lo = 0, hi = njobs - 1;
   while (lo < hi) {   // last job whose first block <= b
@@ -346,28 +342,48 @@ __global__ __launch_bounds__(256) void colreduce_batched_kernel(const int64_t* _
   const int64_t* J = tab + 9 * lo;
   const float* in = reinterpret_cast<const float*>(J[0]);
   const int P = (int)J[1], C = (int)J[2], cols = (int)J[3];
-  const int cl = threadIdx.x & 15, ph = threadIdx.x >> 4;
-  const int c = (b - (int)J[8]) * 16 + cl;
-  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (c < C) {
+  const int q = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int c0 = (b - (int)J[8]) * 64 + 4 * q;     // C % 4 == 0 (host-checked)
+  float4 a[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c0 < C) {
     int p = ph;
     for (; p + 112 < P; p += 128) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] += in[(size_t)(p + 16 * j) * C + c];
+      for (int j = 0; j < 8; ++j) {
+        const float4 v = *reinterpret_cast<const float4*>(in + (size_t)(p + 16 * j) * C + c0);
+        a[j].x += v.x; a[j].y += v.y; a[j].z += v.z; a[j].w += v.w;
+      }
     }
-    for (; p < P; p += 16) a[0] += in[(size_t)p * C + c];
+    for (; p < P; p += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(in + (size_t)p * C + c0);
+      a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
+    }
   }
-  part[ph][cl] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  float4 t4;
+  t4.x = ((a[0].x + a[1].x) + (a[2].x + a[3].x)) + ((a[4].x + a[5].x) + (a[6].x + a[7].x));
+  t4.y = ((a[0].y + a[1].y) + (a[2].y + a[3].y)) + ((a[4].y + a[5].y) + (a[6].y + a[7].y));
+  t4.z = ((a[0].z + a[1].z) + (a[2].z + a[3].z)) + ((a[4].z + a[5].z) + (a[6].z + a[7].z));
+  t4.w = ((a[0].w + a[1].w) + (a[2].w + a[3].w)) + ((a[4].w + a[5].w) + (a[6].w + a[7].w));
+  part[ph][q] = t4;
   __syncthreads();
-  if (ph == 0 && c < C) {
-    float t = 0.f;
+  // 64 columns: thread t < 64 folds column t (16 phases in fixed order)
+  if (threadIdx.x < 64) {
+    const int cl = threadIdx.x, c = (b - (int)J[8]) * 64 + cl;
+    if (c < C) {
+      float t = 0.f;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) t += part[k][cl];
-    const int k = c / cols, cc = c - k * cols;
-    uint16_t* o = reinterpret_cast<uint16_t*>(k == 0 ? J[4] : (k == 1 ? J[5] : J[6]));
-    if (o) {
-      if (J[7]) t += bf2f(o[cc]);
-      o[cc] = f2bf(t);
+      for (int k = 0; k < 16; ++k) {
+        const float4 v = part[k][cl >> 2];
+        t += (cl & 3) == 0 ? v.x : (cl & 3) == 1 ? v.y : (cl & 3) == 2 ? v.z : v.w;
+      }
+      const int k = c / cols, cc = c - k * cols;
+      uint16_t* o = reinterpret_cast<uint16_t*>(k == 0 ? J[4] : (k == 1 ? J[5] : J[6]));
+      if (o) {
+        if (J[7]) t += bf2f(o[cc]);
+        o[cc] = f2bf(t);
+      }
     }
   }
 }
@@ -617,7 +633,7 @@ MX_EXPORT int mx_colsum_bf16(const void* x, int rows, int cols, float* partial, 
                             partial + (size_t)nparts * cols, s);
 }
 
-// deferred-reduction table (see colreduce_batched_kernel); total_blocks = sum ceil(C / 16)
+// deferred-reduction table (see colreduce_batched_kernel); total_blocks = sum ceil(C / 64)
 MX_EXPORT int mx_colreduce_batched(const int64_t* table, int njobs, int total_blocks, hipStream_t s) {
   if (njobs <= 0 || total_blocks <= 0) return hipSuccess;
   hipLaunchKernelGGL(colreduce_batched_kernel, dim3(total_blocks), dim3(256), 0, s, table, njobs);

@@ -231,8 +231,8 @@ class ColReduceQueue:
                 regions[key] = [off, 0, C, nvec, cols, outs, acc]
                 order.append(key)
             r = regions[key]
-            if (r[2], r[3], r[4], r[6]) != (C, nvec, cols, acc):
-                return    # the same output reduced with different shapes: keep immediate mode
+            if (r[2], r[3], r[4], r[6]) != (C, nvec, cols, acc) or C % 4:
+                return    # (same output with different shapes / unaligned rows: keep immediate mode)
             r[1] += nparts
         for key in order:           # regions laid out in first-use order
             r = regions[key]
@@ -244,7 +244,7 @@ class ColReduceQueue:
             o, nrows, C, nvec, cols, outs, acc = regions[key]
             rows.append([self.arena.data_ptr() + 4 * o, nrows, C, cols] +
                         [(t.data_ptr() if t is not None else 0) for t in outs] + [int(acc), blk])
-            blk += (C + 15) // 16
+            blk += (C + 63) // 64
         self.table = torch.tensor(rows, dtype=torch.int64).to(self.device)
         self.njobs, self.nblocks = len(rows), blk
         self.regions = {k: tuple(v) for k, v in regions.items()}
