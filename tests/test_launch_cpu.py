@@ -382,7 +382,10 @@ def test_pytorchjob_records_and_applies_placement(home, monkeypatch):
     sets = [set(parse_cpulist(r["cpus"])) for r in ranks]
     assert all(not (sets[i] & sets[j]) for i in range(4) for j in range(i))
     for pod in ("pytorchjob-numa-master-0", "pytorchjob-numa-worker-0"):
-        line = [x for x in _log("numa", pod).splitlines() if x.startswith("AFF")][0]
+        log = _log("numa", pod)
+        lines = [x for x in log.splitlines() if x.startswith("AFF")]
+        assert lines, f"{pod}: no AFF line in its log:\n{log[-2000:]}"
+        line = lines[0]
         _, host, per_rank, aff = line.split()
         i = 0 if "master" in pod else 2
         assert set(json.loads(aff)) == sets[i] | sets[i + 1]          # replica = its ranks' union
