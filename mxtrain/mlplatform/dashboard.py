@@ -356,6 +356,20 @@ class Auth:
         except PermissionError:
             return None
 
+    def user(self, header: Optional[str], cookie: Optional[str] = None) -> Optional[str]:
+        """The authenticated identity (token email or basic-auth user name), None when the
+        server runs without auth."""
+        u = self.token_user(header, cookie)
+        if u:
+            return u
+        if self.users and header and header.startswith("Basic "):
+            import base64
+            try:
+                return base64.b64decode(header[6:]).decode().split(":", 1)[0]
+            except Exception:  # noqa: BLE001
+                return None
+        return None
+
     def ok(self, header: Optional[str], cookie: Optional[str] = None) -> bool:
         if not self.enabled:
             return True
@@ -391,7 +405,19 @@ def _body_doc(body: bytes):
         return yaml.safe_load(txt)
 
 
-def route_post(parts: List[str], q: Dict[str, str], body: bytes):
+def _authorize_configs(user: Optional[str], chart_configs) -> None:
+    """KFAM: an authenticated user may only start releases in namespaces whose profile
+    makes them owner / contributor (mlplatform/profiles.py ``can``)."""
+    if user is None:
+        return
+    from .profiles import can
+    for c in chart_configs or []:
+        ns = str((c or {}).get("namespace", "default"))
+        if not can(user, "create", ns):
+            raise PermissionError(f"{user} may not create jobs in namespace {ns}")
+
+
+def route_post(parts: List[str], q: Dict[str, str], body: bytes, user: Optional[str] = None):
     """Pipelines API writes (KFP backend, C46):
       POST /api/pipelines/defs            {name, chart_configs, description?}  -> 201
       POST /api/runs                      {pipeline | chart_configs, name?}    -> 201 {run}
@@ -403,6 +429,7 @@ def route_post(parts: List[str], q: Dict[str, str], body: bytes):
     if rest == ["pipelines", "defs"]:
         if not isinstance(doc, dict):
             raise ValueError("body must be a mapping")
+        _authorize_configs(user, doc.get("chart_configs"))
         out = pl.save_pipeline(str(doc.get("name", "")), doc.get("chart_configs"), str(doc.get("description", "")))
         return 201, js, json.dumps(out)
     if rest == ["tensorboards"]:
@@ -412,6 +439,10 @@ def route_post(parts: List[str], q: Dict[str, str], body: bytes):
     if rest == ["runs"]:
         if not isinstance(doc, dict):
             raise ValueError("body must be a mapping")
+        cfgs = doc.get("chart_configs")
+        if cfgs is None and doc.get("pipeline"):
+            cfgs = pl.get_pipeline(str(doc["pipeline"])).get("chart_configs")
+        _authorize_configs(user, cfgs)
         run = pl.submit_run(chart_configs=doc.get("chart_configs"), pipeline=doc.get("pipeline"),
                             run_name=doc.get("name"))
         return 201, js, json.dumps({"run": run})
@@ -420,7 +451,7 @@ def route_post(parts: List[str], q: Dict[str, str], body: bytes):
     return 404, js, json.dumps({"error": "not found"})
 
 
-def route(path: str, q: Dict[str, str], method: str = "GET", body: bytes = b""):
+def route(path: str, q: Dict[str, str], method: str = "GET", body: bytes = b"", user: Optional[str] = None):
     """(status, content-type, body) for a request; shared by the server and the tests."""
     parts = [urllib.parse.unquote(x) for x in path.strip("/").split("/") if x]
     js = "application/json"
@@ -428,7 +459,7 @@ def route(path: str, q: Dict[str, str], method: str = "GET", body: bytes = b""):
         if method == "POST":
             if not parts or parts[0] != "api":
                 return 404, js, json.dumps({"error": "not found"})
-            return route_post(parts, q, body)
+            return route_post(parts, q, body, user)
         if not parts:
             return 200, "text/html; charset=utf-8", _index_html()
         if parts == ["tensorboard"]:
@@ -577,7 +608,8 @@ def make_server(host: str, port: int, auth: Auth, certfile=None, keyfile=None) -
                 self._send(403, "application/json", json.dumps({"error": "writes need --htpasswd or --oidc"}))
                 return
             q = {k: v[0] for k, v in urllib.parse.parse_qs(u.query).items()}
-            code, ctype, body = route(u.path, q, "POST", data)
+            code, ctype, body = route(u.path, q, "POST", data,
+                                      auth.user(self.headers.get("Authorization"), self.headers.get("Cookie")))
             self._send(code, ctype, body)
 
     srv = ThreadingHTTPServer((host, port), H)

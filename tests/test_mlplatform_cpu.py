@@ -368,3 +368,18 @@ def test_platform_up_dry_run(home):
     assert r.returncode == 0, r.stderr
     plan = json.loads(r.stdout)
     assert "profile_created" not in plan and "user_created" not in plan
+
+
+def test_pipelines_api_enforces_profile_roles(home):
+    """An authenticated user may start pipeline runs only in namespaces whose profile lists
+    them (owner / contributor); unauthenticated loopback use is unchanged."""
+    from mxtrain.mlplatform import dashboard as db
+    from mxtrain.mlplatform import profiles as pr
+    pr.create("team-b", owner="carol@example.com")
+    cfg = {"release_name": "rb", "namespace": "team-b", "path": "charts/machine-learning/data-prep/data-process",
+           "values": {"process": {"command": ["true"]}}}
+    body = json.dumps({"name": "p-b", "chart_configs": [cfg]}).encode()
+    assert db.route("/api/pipelines/defs", {}, "POST", body, user="mallory@example.com")[0] == 403
+    assert db.route("/api/pipelines/defs", {}, "POST", body, user="carol@example.com")[0] == 201
+    run = json.dumps({"pipeline": "p-b", "name": "rb1"}).encode()
+    assert db.route("/api/runs", {}, "POST", run, user="mallory@example.com")[0] == 403
