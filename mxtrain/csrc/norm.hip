@@ -31,47 +31,64 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     int rows, int cols, float eps, uint32_t thresh, float keep_scale,
     const uint32_t* __restrict__ seed_ptr, uint32_t salt) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (row >= rows) return;
   const uint32_t seed = HAS_BDA && seed_ptr ? (*seed_ptr + salt) : 0u;
   const size_t base = (size_t)row * cols;
+  // Every load of the row (x, bias, residual, gamma, beta) is issued before any math:
+  // one memory round trip per row instead of one per 512-column vector plus one for the
+  // affine parameters.  Columns are clamped into the row and the loads unconditional;
+  // lanes past the row end are masked at use and only the stores are predicated.  The
+  // optional operands are zeroed through masks the optimiser cannot see through (a
+  // `bias ? load : 0` select became a branch around a load issued last).
+  constexpr bool EARLY = NV <= 4;  // wider rows load the affine parameters at use
+  uint4 xr[NV], br[NV], rr[NV], gr[NV], er[NV];
+  const uint16_t* bsrc = bias ? bias : gamma;
+  const uint16_t* rsrc = residual ? residual : x;
+  const uint16_t* esrc = beta ? beta : gamma;
+  uint32_t bm = bias ? ~0u : 0u, rmk = residual ? ~0u : 0u, em = beta ? ~0u : 0u;
+  asm volatile("" : "+v"(bm), "+v"(rmk), "+v"(em));
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = min((lane + 64 * i) * 8, cols - 8);
+    xr[i] = *reinterpret_cast<const uint4*>(x + base + c);
+    if constexpr (HAS_BDA) {
+      br[i] = *reinterpret_cast<const uint4*>(bsrc + c);
+      rr[i] = *reinterpret_cast<const uint4*>(rsrc + base + c);
+    }
+    if constexpr (EARLY) {
+      gr[i] = *reinterpret_cast<const uint4*>(gamma + c);
+      if constexpr (!RMS) er[i] = *reinterpret_cast<const uint4*>(esrc + c);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  auto and4 = [](uint4 a, uint32_t m) __attribute__((always_inline)) {
+    return make_uint4(a.x & m, a.y & m, a.z & m, a.w & m);
+  };
   float v[NV][8];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (lane + 64 * i) * 8;
-    if (c < cols) {
-      uint4 raw = *reinterpret_cast<const uint4*>(x + base + c);
-      unpack8(raw, v[i]);
-      if constexpr (HAS_BDA) {
-        float b[8], r[8];
-        if (bias) {
-          unpack8(*reinterpret_cast<const uint4*>(bias + c), b);
-        } else {
+    const bool ok = c < cols;
+    unpack8(xr[i], v[i]);
+    if constexpr (HAS_BDA) {
+      float b[8], r[8];
+      unpack8(and4(br[i], bm), b);
+      unpack8(and4(rr[i], rmk), r);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) b[j] = 0.f;
-        }
-        if (residual) {
-          unpack8(*reinterpret_cast<const uint4*>(residual + base + c), r);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) r[j] = 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float t = v[i][j] + b[j];
-          if (thresh) t = dropout_keep(base + c + j, seed, thresh) ? t * keep_scale : 0.f;
-          v[i][j] = r[j] + t;
-        }
-        // the residual stream is stored in bf16; normalise the rounded value so that
-        // backward (which re-reads h_out) sees exactly the forward's input
-        uint4 packed = pack8(v[i]);
-        *reinterpret_cast<uint4*>(h_out + base + c) = packed;
-        unpack8(packed, v[i]);
+      for (int j = 0; j < 8; ++j) {
+        float t = v[i][j] + b[j];
+        if (thresh) t = dropout_keep(base + c + j, seed, thresh) ? t * keep_scale : 0.f;
+        v[i][j] = r[j] + t;
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+      // the residual stream is stored in bf16; normalise the rounded value so that
+      // backward (which re-reads h_out) sees exactly the forward's input
+      uint4 packed = pack8(v[i]);
+      if (ok) *reinterpret_cast<uint4*>(h_out + base + c) = packed;
+      unpack8(packed, v[i]);
     }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[i][j] = ok ? v[i][j] : 0.f;
   }
   float mean = 0.f;
   if constexpr (!RMS) {
@@ -85,11 +102,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int c = (lane + 64 * i) * 8;
-    if (c < cols) {
+    const bool ok = (lane + 64 * i) * 8 < cols;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { float d = v[i][j] - mean; ss += d * d; }
-    }
+    for (int j = 0; j < 8; ++j) { float d = v[i][j] - mean; ss += ok ? d * d : 0.f; }
   }
   const float rstd = rsqrtf(wave_sum(ss) / (float)cols + eps);
   if (lane == 0) {
@@ -99,19 +114,18 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (lane + 64 * i) * 8;
-    if (c < cols) {
-      float g[8], bt[8], o[8];
-      unpack8(*reinterpret_cast<const uint4*>(gamma + c), g);
-      if (!RMS && beta) {
-        unpack8(*reinterpret_cast<const uint4*>(beta + c), bt);
-      } else {
+    if (!EARLY && c >= cols) continue;
+    const int cc = min(c, cols - 8);
+    float g[8], bt[8], o[8];
+    unpack8(EARLY ? gr[i] : *reinterpret_cast<const uint4*>(gamma + cc), g);
+    if constexpr (!RMS) unpack8(and4(EARLY ? er[i] : *reinterpret_cast<const uint4*>(esrc + cc), em), bt);
+    else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) bt[j] = 0.f;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + bt[j];
-      *reinterpret_cast<uint4*>(y + base + c) = pack8(o);
+      for (int j = 0; j < 8; ++j) bt[j] = 0.f;
     }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + bt[j];
+    if (c < cols) *reinterpret_cast<uint4*>(y + base + c) = pack8(o);
   }
 }
 
@@ -137,7 +151,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
   const uint32_t seed = seed_ptr ? (*seed_ptr + salt) : 0u;
   const int lane = threadIdx.x & 63;
-  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // wave-uniform row index (scalar statistics loads and row addressing)
+  const int wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int nw = gridDim.x * 4;
   constexpr int NR = REG ? NV : 1;
   float g[NV][8], ag[NR][8], ab[NR][8], ax[NR][8];
@@ -154,48 +169,65 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   for (int i = 0; i < NR; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) { ag[i][j] = 0.f; ab[i][j] = 0.f; ax[i][j] = 0.f; }
-  // Software pipeline: the next row's h / dy / dres (and statistics) are loaded before the
-  // current row's math, so every wave keeps two rows of loads in flight (the grid has only
-  // a few waves per SIMD: each wave handles several rows to amortise its column partials).
-  uint4 hraw[NV], draw[NV], rraw[NV];
-  float mean_c = 0.f, rstd_c = 0.f;
-  auto load_row = [&](int row_, uint4 (&hr)[NV], uint4 (&dr)[NV], uint4 (&rr)[NV], float& mn, float& rs)
-      __attribute__((always_inline)) {
-    const size_t b_ = (size_t)row_ * cols;
-    mn = RMS ? 0.f : mean_in[row_];
-    rs = rstd_in[row_];
+  // Load groups: a wave issues the h / dy / dres loads (and statistics) of its next G rows
+  // before any of their math, so G rows of loads are in flight per wave (the grid has one
+  // wave per SIMD: each wave handles several rows to amortise its column partials, and a
+  // one-row-ahead prefetch left only one row in flight at every wait).  Addresses are
+  // clamped into the tensor and the loads unconditional: a `cond ? load : 0` select makes
+  // the compiler wait for the load right where it is issued.
+  constexpr int G = NV <= 2 ? 4 : (NV <= 4 ? 2 : 1);
+  const uint16_t* rsrc = dres ? dres : h;
+  // residual-gradient mask, opaque to the optimiser: `dres ? load : 0` was turned into a
+  // branch around the load, issued last and waited for with vmcnt(0) before row 0's math
+  uint32_t rm = dres ? ~0u : 0u;
+  asm volatile("" : "+v"(rm));
+  for (int row0 = wid; row0 < rows; row0 += G * nw) {
+    uint4 hb[G][NV], db[G][NV], rb[G][NV];
+    float mb[G], sb[G];
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = (lane + 64 * i) * 8;
-      const bool ok = c < cols;
-      hr[i] = ok ? *reinterpret_cast<const uint4*>(h + b_ + c) : make_uint4(0, 0, 0, 0);
-      dr[i] = ok ? *reinterpret_cast<const uint4*>(dy + b_ + c) : make_uint4(0, 0, 0, 0);
-      rr[i] = (dres && ok) ? *reinterpret_cast<const uint4*>(dres + b_ + c) : make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < G; ++k) {
+      const int rl = min(row0 + k * nw, rows - 1);
+      const size_t b_ = (size_t)rl * cols;
+      mb[k] = RMS ? 0.f : mean_in[rl];
+      sb[k] = rstd_in[rl];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = min((lane + 64 * i) * 8, cols - 8);
+        hb[k][i] = *reinterpret_cast<const uint4*>(h + b_ + c);
+        db[k][i] = *reinterpret_cast<const uint4*>(dy + b_ + c);
+        rb[k][i] = *reinterpret_cast<const uint4*>(rsrc + b_ + c);
+      }
     }
-  };
-  if (wid < rows) load_row(wid, hraw, draw, rraw, mean_c, rstd_c);
-  for (int row = wid; row < rows; row += nw) {
-    const size_t base = (size_t)row * cols;
-    const float mean = mean_c;
-    const float rstd = rstd_c;
-    uint4 hcur[NV], dcur[NV];
+    __builtin_amdgcn_sched_barrier(0);  // keep the whole group's loads ahead of its math
 #pragma unroll
-    for (int i = 0; i < NV; ++i) { hcur[i] = hraw[i]; dcur[i] = draw[i]; }
+  for (int k = 0; k < G; ++k) {
+    const int row = row0 + k * nw;
+    if (row >= rows) break;
+    const size_t base = (size_t)row * cols;
+    const float mean = mb[k];
+    const float rstd = sb[k];
+    const uint4 (&hcur)[NV] = hb[k];
+    const uint4 (&dcur)[NV] = db[k];
     uint4 rcur[NV];
 #pragma unroll
-    for (int i = 0; i < NV; ++i) rcur[i] = rraw[i];
-    if (row + nw < rows) load_row(row + nw, hraw, draw, rraw, mean_c, rstd_c);
+    for (int i = 0; i < NV; ++i)
+      rcur[i] = make_uint4(rb[k][i].x & rm, rb[k][i].y & rm, rb[k][i].z & rm, rb[k][i].w & rm);
     float xh[NV][8], gy[NV][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (lane + 64 * i) * 8;
-      if (c < cols) {
+      const bool ok = c < cols;
+      // REG: branch-free (lanes past the row end read clamped data and contribute zeros);
+      // execution-mask branches around the math made the compiler drain every load in
+      // flight (vmcnt(0)) before the first store of the group
+      if (REG || ok) {
         float hv[8], dv[8];
         unpack8(hcur[i], hv);
         unpack8(dcur[i], dv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
+          if constexpr (REG) dv[j] = ok ? dv[j] : 0.f;
           xh[i][j] = (hv[j] - mean) * rstd;
           gy[i][j] = dv[j] * g[i][j];
           s1 += gy[i][j];
@@ -218,12 +250,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (lane + 64 * i) * 8;
-      if (c < cols) {
+      const bool ok = c < cols;
+      if (REG || ok) {
         float r[8], o[8];
         unpack8(rcur[i], r);   // zeros when there is no residual gradient
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = r[j] + rstd * (gy[i][j] - m1 - xh[i][j] * m2);
-        *reinterpret_cast<uint4*>(dh_out + base + c) = pack8(o);
+        const uint4 po = pack8(o);
+        if (ok) *reinterpret_cast<uint4*>(dh_out + base + c) = po;
         if (dx_drop) {
           float dx[8];
 #pragma unroll
@@ -233,19 +267,20 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
             dx[j] = t;
           }
           uint4 pk = pack8(dx);
-          *reinterpret_cast<uint4*>(dx_drop + base + c) = pk;
+          if (ok) *reinterpret_cast<uint4*>(dx_drop + base + c) = pk;
           if constexpr (COLS) {
             float dxr[8];
             unpack8(pk, dxr);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-              if constexpr (REG) ax[i][j] += dxr[j];
+              if constexpr (REG) ax[i][j] += ok ? dxr[j] : 0.f;
               else atomicAdd(&slab[2 * cols + c + j], dxr[j]);
             }
           }
         }
       }
     }
+  }
   }
   if constexpr (!COLS) return;
   float* out = partial + (size_t)blockIdx.x * 3 * cols;
@@ -421,6 +456,7 @@ hipError_t launch_fwd(const void* x, const void* bias, const void* residual,
                       const void* gamma, const void* beta, void* h_out, void* y,
                       float* mean, float* rstd, int rows, int cols, float eps,
                       float p, const uint32_t* seed, uint32_t salt, hipStream_t s) {
+  if (cols < 8 || cols % 8 || rows <= 0) return hipErrorInvalidValue;  // 16-B row vectors
   const int nv = (cols + 511) / 512;
   const uint32_t thresh = p > 0.f ? (uint32_t)((double)p * 4294967296.0) : 0u;
   const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
@@ -503,6 +539,7 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
                       const float* rstd, const void* gamma, void* dh_out, void* dx_drop,
                       float* partial, int rows, int cols, float p, const uint32_t* seed,
                       uint32_t salt, hipStream_t s) {
+  if (cols < 8 || cols % 8 || rows <= 0) return hipErrorInvalidValue;  // 16-B row vectors
   const int nv = (cols + 511) / 512;
   const uint32_t thresh = p > 0.f ? (uint32_t)((double)p * 4294967296.0) : 0u;
   const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
