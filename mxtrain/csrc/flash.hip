@@ -269,14 +269,8 @@ __global__ __launch_bounds__(256) void flash_dropmask_kernel(
 // lane <-> (row, column) mapping in both teams: an element-wise merge).  Non-causal: team
 // t takes block 2i+t whole.  The critical path is ~half the heaviest block's tiles.
 // !PAIR (D = 128): one 4-wave workgroup per block (two per CU), heaviest block first.
-template <int D, bool PAIR>
-struct QCfg {
-  static constexpr int BK = 64;
-  static constexpr int NT = PAIR ? 512 : 256;
-  static constexpr int WPE = 2;
-};
 
-template <int D, bool CAUSAL, bool DROP, bool DQ, bool PAIR>
+template <int D, bool CAUSAL, bool DROP, bool DQ, bool PAIR, int BKT = 64>
 __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_eu(2, 2))) void flash_qmajor_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, int ldq, int ldk, int ldv,
@@ -285,7 +279,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
     int S, int Hq, int Hkv, const int* __restrict__ klen, float c,
     float oscale /* FWD 1/(1-p); DQ scale/(1-p) */, float dkeep /* 1-p */,
     const uint64_t* __restrict__ dbits, int NB, int NKT) {
-  constexpr int BQ = 128, BK = QCfg<D, PAIR>::BK, NSUB = BK / 32, NKK = D / 16, NDT = D / 32;
+  constexpr int BQ = 128, BK = BKT, NSUB = BK / 32, NKK = D / 16, NDT = D / 32;
   constexpr int RB = D * 2, CPR = D / 8, RPP = 64 / CPR;
   constexpr int TILE = BK * RB, PIECES = TILE / 1024, PPW = PIECES / 4;
   constexpr int T2 = PAIR ? TILE : 16;
@@ -295,11 +289,16 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
   __shared__ __attribute__((aligned(16))) char k1[TILE];
   __shared__ __attribute__((aligned(16))) char v0[TILE];
   __shared__ __attribute__((aligned(16))) char v1[TILE];
-  __shared__ __attribute__((aligned(16))) char k2[T2];
-  __shared__ __attribute__((aligned(16))) char k3[T2];
-  __shared__ __attribute__((aligned(16))) char v2[T2];
-  __shared__ __attribute__((aligned(16))) char v3[T2];
-  __shared__ __attribute__((aligned(16))) float mrg[MRG];
+  // team 1's tiles; the end-of-loop merge area aliases them (written after a barrier that
+  // team 1 reaches only once its last tile is consumed): 4 x 16 KB tiles at BK 128 + the
+  // 34 KB merge area would not fit next to team 0's 64 KB otherwise
+  constexpr int T1B = 4 * T2 > MRG * 4 ? 4 * T2 : MRG * 4;
+  __shared__ __attribute__((aligned(16))) char t1buf[T1B];
+  char* const k2 = t1buf;
+  char* const k3 = t1buf + T2;
+  char* const v2 = t1buf + 2 * T2;
+  char* const v3 = t1buf + 3 * T2;
+  float* const mrg = reinterpret_cast<float*>(t1buf);
 
   const int tid = threadIdx.x, lane = tid & 63, w = uni(tid >> 6);
   const int team = PAIR ? (w >> 2) : 0, wl = w & 3;
@@ -623,6 +622,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
     if (CAUSAL && merge) {
       // team 1's partial of block H -> team 0 (identical lane mapping: element-wise)
       float* mw = mrg + wl * NREG * 64 + lane;
+      __syncthreads();   // the merge area aliases team 1's tiles
       if (team == 1) {
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
@@ -952,6 +952,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
   if constexpr (PAIR) {
     if (CAUSAL && merge) {
       float* mw = mrg + wl * NREG * 64 + lane;
+      __syncthreads();   // the merge area aliases team 1's tiles
       if (team == 1) {
 #pragma unroll
         for (int dt = 0; dt < NDL; ++dt)
@@ -981,6 +982,8 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
 }
 
 // ------------------------------------------------------------------------------ launch
+int g_qbk_fwd = 128, g_qbk_dq = 128;   // key-tile rows of the D 64 query-major kernels
+
 template <int D, bool DQ>
 hipError_t launch_qmajor(bool causal, bool drop, int S, int B, hipStream_t s,
                          const uint16_t* q, const uint16_t* k, const uint16_t* v, int ldq, int ldk,
@@ -991,12 +994,25 @@ hipError_t launch_qmajor(bool causal, bool drop, int S, int B, hipStream_t s,
   constexpr bool PAIR = D == 64;
   const int nqb = (S + 127) / 128;
   const dim3 grid((PAIR ? (nqb + 1) / 2 : nqb) * Hq * B);
-#define MX_QM(C, DR)                                                                              \
-  hipLaunchKernelGGL((flash_qmajor_kernel<D, C, DR, DQ, PAIR>), grid, dim3(PAIR ? 512 : 256), 0, s, \
-                     q, k, v, ldq, ldk, ldv, dout, lddo, o, ldo, lse, delta, dq, lddq, S, Hq, Hkv,  \
+#define MX_QM(C, DR, BKT)                                                                              \
+  hipLaunchKernelGGL((flash_qmajor_kernel<D, C, DR, DQ, PAIR, BKT>), grid, dim3(PAIR ? 512 : 256), 0, s, \
+                     q, k, v, ldq, ldk, ldv, dout, lddo, o, ldo, lse, delta, dq, lddq, S, Hq, Hkv,       \
                      klen, c, oscale, dkeep, dbits, NB, NKT)
-  if (causal) { if (drop) MX_QM(true, true); else MX_QM(true, false); }
-  else { if (drop) MX_QM(false, true); else MX_QM(false, false); }
+#define MX_QM_B(BKT)                                                          \
+  {                                                                           \
+    if (causal) { if (drop) MX_QM(true, true, BKT); else MX_QM(true, false, BKT); } \
+    else { if (drop) MX_QM(false, true, BKT); else MX_QM(false, false, BKT); }    \
+  }
+  // D 64: 128-key tiles (half the steps, each with twice the compute under the next
+  // tile's DMA; the GPT-2 shapes run only ~9 dependent steps per team and were latency-
+  // bound at 64).  D 128 keeps 64 (two waves per SIMD need the registers).
+  if constexpr (PAIR) {
+    if ((DQ ? g_qbk_dq : g_qbk_fwd) == 128) MX_QM_B(128)
+    else MX_QM_B(64)
+  } else {
+    MX_QM_B(64)
+  }
+#undef MX_QM_B
 #undef MX_QM
   return hipGetLastError();
 }
@@ -1032,6 +1048,15 @@ hipError_t launch_kmajor(bool causal, bool drop, int S, int B, hipStream_t s,
 }
 
 }  // namespace
+
+// key-tile rows (64 or 128) of the D 64 forward / dQ kernels; returns the old values
+// (fwd * 1000 + dq).  A value of 0 keeps the current setting.
+MX_EXPORT int mx_flash_qmajor_bk(int fwd, int dq) {
+  const int old = g_qbk_fwd * 1000 + g_qbk_dq;
+  if (fwd == 64 || fwd == 128) g_qbk_fwd = fwd;
+  if (dq == 64 || dq == 128) g_qbk_dq = dq;
+  return old;
+}
 
 // Dropout keep-mask images for one attention call (layouts in flash_dropmask_kernel).
 // fwd_bits: u64 [B*Hq][NB][NKT][64]; bwd_bits: u32 [B*Hq][NB][NQT][64], NB = ceil(S/32),
