@@ -104,6 +104,14 @@ __device__ __forceinline__ bool dropout_keep(uint64_t idx, uint32_t seed, uint32
   uint32_t h = hash32((uint32_t)idx ^ (uint32_t)(idx >> 32) * 0x85ebca6bu, seed);
   return h >= thresh;  // thresh = p * 2^32
 }
+// keep flags of the 8 elements idx0 .. idx0 + 7, idx0 % 8 == 0: bit-identical to
+// dropout_keep, with the high word's multiply done once (the 8 indices share it)
+__device__ __forceinline__ void dropout_keep8(uint64_t idx0, uint32_t seed, uint32_t thresh, bool (&k)[8]) {
+  const uint32_t hi = (uint32_t)(idx0 >> 32) * 0x85ebca6bu;
+  const uint32_t lo = (uint32_t)idx0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) k[j] = hash32((lo + j) ^ hi, seed) >= thresh;
+}
 
 // tanh-approximation GeLU (Megatron bias_gelu / HF "gelu_new") in its sigmoid form:
 //   0.5 x (1 + tanh(u)) = x s,  s = sigmoid(2u) = 1 / (1 + 2^(x (A + B x^2))),

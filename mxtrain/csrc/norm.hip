@@ -75,10 +75,12 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
       float b[8], r[8];
       unpack8(and4(br[i], bm), b);
       unpack8(and4(rr[i], rmk), r);
+      bool km[8];
+      if (thresh) dropout_keep8(base + c, seed, thresh, km);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float t = v[i][j] + b[j];
-        if (thresh) t = dropout_keep(base + c + j, seed, thresh) ? t * keep_scale : 0.f;
+        if (thresh) t = km[j] ? t * keep_scale : 0.f;
         v[i][j] = r[j] + t;
       }
       // the residual stream is stored in bf16; normalise the rounded value so that
@@ -260,10 +262,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         if (ok) *reinterpret_cast<uint4*>(dh_out + base + c) = po;
         if (dx_drop) {
           float dx[8];
+          bool km[8];
+          if (thresh) dropout_keep8(base + c, seed, thresh, km);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             float t = o[j];
-            if (thresh) t = dropout_keep(base + c + j, seed, thresh) ? t * keep_scale : 0.f;
+            if (thresh) t = km[j] ? t * keep_scale : 0.f;
             dx[j] = t;
           }
           uint4 pk = pack8(dx);
@@ -524,8 +528,10 @@ __global__ __launch_bounds__(256) void ln_bwd_cols_kernel(
 int kSplitCols = 2048;   // wider rows: row kernel without column sums + column kernel
 constexpr int kColsRowsPerBlock = 32;
 
-int kBwdRowsPerWave = 4;   // (2 before the row pipeline: 512 blocks' column partials cost
-                           //  as much as the rows at 4096 x 1024)
+// rows per wave of the fused backward: 2 (BDA-LN at 4096 x 1024 with its column reduction,
+// scripts/ln_ab.py: 16.0 us at 2, 17.2 at 4, 16.2 at 1 -- with load groups, two waves per
+// SIMD hide each other's dropout-hash VALU better than the halved partials save)
+int kBwdRowsPerWave = 2;
 int bwd_grid(int rows) {
   const int rpb = 4 * kBwdRowsPerWave;
   int g = (rows + rpb - 1) / rpb;
