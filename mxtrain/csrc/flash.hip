@@ -982,7 +982,10 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
 }
 
 // ------------------------------------------------------------------------------ launch
-int g_qbk_fwd = 128, g_qbk_dq = 128;   // key-tile rows of the D 64 query-major kernels
+// key-tile rows of the D 64 query-major kernels (rocprofv3, GPT-2 shapes, dropout 0.1, one
+// box: forward 25.8 us at 64 / 24.4 at 128; dQ 32.5 at 64 / 34.0 at 128 -- the dQ step
+// holds S, dP and dQ^T, and its longer per-tile chain already covers the next tile's DMA)
+int g_qbk_fwd = 128, g_qbk_dq = 64;
 
 template <int D, bool DQ>
 hipError_t launch_qmajor(bool causal, bool drop, int S, int B, hipStream_t s,
@@ -1003,9 +1006,9 @@ hipError_t launch_qmajor(bool causal, bool drop, int S, int B, hipStream_t s,
     if (causal) { if (drop) MX_QM(true, true, BKT); else MX_QM(true, false, BKT); } \
     else { if (drop) MX_QM(false, true, BKT); else MX_QM(false, false, BKT); }    \
   }
-  // D 64: 128-key tiles (half the steps, each with twice the compute under the next
-  // tile's DMA; the GPT-2 shapes run only ~9 dependent steps per team and were latency-
-  // bound at 64).  D 128 keeps 64 (two waves per SIMD need the registers).
+  // D 64 forward: 128-key tiles (half the steps, each with twice the compute under the
+  // next tile's DMA; the GPT-2 shapes run only ~9 dependent steps per team).  D 128 keeps
+  // 64 (two waves per SIMD need the registers).
   if constexpr (PAIR) {
     if ((DQ ? g_qbk_dq : g_qbk_fwd) == 128) MX_QM_B(128)
     else MX_QM_B(64)

@@ -18,7 +18,12 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--dropout", type=float, default=0.0)
     ap.add_argument("--fwd-only", action="store_true")
+    ap.add_argument("--qbk", default="", help="key-tile rows of the D 64 forward / dQ kernels, e.g. 64,128")
     a = ap.parse_args()
+    if a.qbk:
+        from mxtrain.ops import _lib
+        f, q = (int(x) for x in a.qbk.split(","))
+        _lib._fn("mx_flash_qmajor_bk")(f, q)
     B, S, H, D = (4, 1024, 16, 64) if a.shape == "gpt2" else (2, 2048, 32, 128)
     dev = "cuda"
     torch.manual_seed(0)
