@@ -10,6 +10,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 import pytest
 import yaml
@@ -382,8 +383,15 @@ def test_pytorchjob_records_and_applies_placement(home, monkeypatch):
     sets = [set(parse_cpulist(r["cpus"])) for r in ranks]
     assert all(not (sets[i] & sets[j]) for i in range(4) for j in range(i))
     for pod in ("pytorchjob-numa-master-0", "pytorchjob-numa-worker-0"):
-        log = _log("numa", pod)
-        lines = [x for x in log.splitlines() if x.startswith("AFF")]
+        # the job succeeds with its master (training-operator semantics): a worker can
+        # still be starting its interpreter on a loaded host, so give its log time
+        deadline = time.time() + 60
+        while True:
+            log = _log("numa", pod)
+            lines = [x for x in log.splitlines() if x.startswith("AFF")]
+            if lines or time.time() > deadline:
+                break
+            time.sleep(0.5)
         assert lines, f"{pod}: no AFF line in its log:\n{log[-2000:]}"
         line = lines[0]
         _, host, per_rank, aff = line.split()
