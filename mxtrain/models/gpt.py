@@ -304,6 +304,7 @@ class StepRuntime:
     dmask_l0: int = 0
     dmask_key: Optional[tuple] = None
     batch_dmasks: bool = False    # GPTTrainer turns it on (it resets dmasks when the seed advances)
+    side_dmasks: bool = False     # layers 1.. of the batched masks on aux_stream (MXTRAIN_SIDE_DMASKS)
 
     @property
     def p_drop(self):
@@ -794,7 +795,8 @@ class GPTStage:
                                                  rt.attn_seed_t if rt.attn_seed_t is not None else rt.seed_t,
                                                  SALT_ATTN + self.l0, self.l1 - self.l0,
                                                  head_offset=rt.tp_rank * hl + rt.cp_rank * ha_,
-                                                 total_heads=cfg.num_attention_heads, causal=True)
+                                                 total_heads=cfg.num_attention_heads, causal=True,
+                                                 stream=rt.aux_stream if rt.side_dmasks else None)
         for i in range(self.l0, self.l1):
             if i + 1 < self.l1:
                 nxt = f"layers.{i + 1}.ln1"

@@ -139,11 +139,14 @@ def dropmask(B, S, Hq, p, seed_t, salt=0, head_offset=0, total_heads=None, causa
 
 
 def dropmask_layers(B, S, Hq, p, seed_t, salt, L, head_offset=0, total_heads=None, causal=True,
-                    device=None):
+                    device=None, stream=None):
     """The keep-mask images of L consecutive layers (salts salt .. salt + L - 1) in ONE
     launch -- identical to L dropmask() calls; a step's masks depend only on its seed, so
     the model generates them all before the first layer (one launch instead of one per
-    layer, and the single large grid keeps the chip full).  Returns [DropMask] * L."""
+    layer, and the single large grid keeps the chip full).  With ``stream``: the first
+    layer's images on the current stream, the other L - 1 layers' in one launch on
+    ``stream`` (VALU-bound hashing beside the first layers' MFMA-bound GEMMs), joined
+    through a shared event at each later layer's first use.  Returns [DropMask] * L."""
     device = device if device is not None else seed_t.device
     if device.type != "cuda" or not _lib.use_hip(seed_t):
         return [dropmask(B, S, Hq, p, seed_t, salt + l, head_offset, total_heads, causal, device) for l in range(L)]
@@ -151,9 +154,23 @@ def dropmask_layers(B, S, Hq, p, seed_t, salt, L, head_offset=0, total_heads=Non
     nf, nb = B * Hq * NB * NKT * 64, B * Hq * NB * NQT * 64
     fbits = torch.empty(L, nf, dtype=torch.int64, device=device)
     bbits = torch.empty(L, nb, dtype=torch.int32, device=device)
-    _lib.call("mx_flash_dropmask_layers", _lib.ptr(seed_t), int(salt) & M32, float(p), B, S, Hq, int(head_offset),
-              int(total_heads or Hq), int(causal), L, _lib.ptr(fbits), _lib.ptr(bbits), 2 * nf, nb, _lib.stream())
-    return [DropMask(p, fbits[l], bbits[l]) for l in range(L)]
+
+    def launch(l0, n):
+        _lib.call("mx_flash_dropmask_layers", _lib.ptr(seed_t), (int(salt) + l0) & M32, float(p), B, S, Hq,
+                  int(head_offset), int(total_heads or Hq), int(causal), n, _lib.ptr(fbits[l0]), _lib.ptr(bbits[l0]),
+                  2 * nf, nb, _lib.stream())
+
+    if stream is None or L < 2:
+        launch(0, L)
+        return [DropMask(p, fbits[l], bbits[l]) for l in range(L)]
+    launch(0, 1)
+    main = torch.cuda.current_stream(device)
+    stream.wait_stream(main)            # the seed is advanced on the main stream
+    with torch.cuda.stream(stream):
+        launch(1, L - 1)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+    return [DropMask(p, fbits[0], bbits[0])] + [DropMask(p, fbits[l], bbits[l], event=ev) for l in range(1, L)]
 
 
 def attn_fwd(q, k, v, B, S, Hq, Hkv, D, causal=True, klen=None, scale=None, dropout_p=0.0,

@@ -82,6 +82,7 @@ class GPTTrainer:
                               cp=ps.cp, cp_rank=ps.cp_rank, cp_group=ps.cp_group,
                               attn_seed_t=self.seed.attn_t)
         self.stage.rt.batch_dmasks = os.environ.get("MXTRAIN_BATCH_DMASKS", "1") != "0"
+        self.stage.rt.side_dmasks = os.environ.get("MXTRAIN_SIDE_DMASKS", "0") == "1"
         if tcfg.wgrad_stream and self.device.type == "cuda":
             self.stage.rt.wgrad_stream = torch.cuda.Stream(device=self.device)
         self._overwrite = bool(tcfg.overwrite_wgrads and ps.pp == 1)
