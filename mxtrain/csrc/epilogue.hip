@@ -18,13 +18,16 @@ namespace {
 // y = act(y + b (+ res)) in place; one thread per 8-channel vector
 template <bool kRes, bool kRelu>
 __global__ __launch_bounds__(256) void bias_act_fwd_kernel(uint16_t* __restrict__ y, const uint16_t* __restrict__ b,
-                                                           const uint16_t* __restrict__ res, int64_t nvec, int c8) {
+                                                           const uint16_t* __restrict__ res, int64_t nvec, int c8,
+                                                           int c8m) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
     float x[8], bb[8];
     unpack8(reinterpret_cast<const uint4*>(y)[v], x);
     if (b) {
-      unpack8(reinterpret_cast<const uint4*>(b)[v % c8], bb);
+      // bias vector: a mask for power-of-two channel counts (64..2048 here), else the
+      // 64-bit modulo (a software division)
+      unpack8(reinterpret_cast<const uint4*>(b)[c8m >= 0 ? (int)(v & c8m) : (int)(v % c8)], bb);
 #pragma unroll
       for (int j = 0; j < 8; ++j) x[j] += bb[j];
     }
@@ -108,7 +111,7 @@ MX_EXPORT int mx_bias_act_fwd(void* y, const void* b, const void* res, int64_t M
   const unsigned grid = (unsigned)(want < 8192 ? want : 8192);
 #define MX_BA(R, A)                                                                                        \
   hipLaunchKernelGGL((bias_act_fwd_kernel<R, A>), dim3(grid), dim3(256), 0, s, (uint16_t*)y, (const uint16_t*)b, \
-                     (const uint16_t*)res, nvec, C / 8)
+                     (const uint16_t*)res, nvec, C / 8, ((C / 8) & (C / 8 - 1)) == 0 ? C / 8 - 1 : -1)
   if (res) {
     if (relu) MX_BA(true, true); else MX_BA(true, false);
   } else {

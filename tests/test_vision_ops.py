@@ -186,19 +186,20 @@ def test_crop_resize_mask_crops_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("relu,res,bias_grad,k", [(True, False, False, 3), (False, False, True, 3),
-                                                  (True, True, False, 3), (True, False, True, 3),
-                                                  (True, True, True, 1), (False, False, True, 1)])
-def test_conv_bias_act_gpu(relu, res, bias_grad, k):
+@pytest.mark.parametrize("relu,res,bias_grad,k,cout", [(True, False, False, 3, 128), (False, False, True, 3, 128),
+                                                       (True, True, False, 3, 128), (True, False, True, 3, 128),
+                                                       (True, True, True, 1, 128), (False, False, True, 1, 128),
+                                                       (True, True, True, 3, 120)])   # 120: non-power-of-two bias index
+def test_conv_bias_act_gpu(relu, res, bias_grad, k, cout):
     """Fused conv epilogue (csrc/epilogue.hip) vs the fp32 torch reference: forward and
     the gradients of input, weight, bias and residual."""
     from mxtrain.ops import epilogue as E
     g = torch.Generator().manual_seed(11)
     x = torch.randn(2, 64, 20, 24, generator=g)
-    w = torch.randn(128, 64, k, k, generator=g) * 0.05
-    b = torch.randn(128, generator=g)
-    r = torch.randn(2, 128, 20, 24, generator=g)
-    dout = torch.randn(2, 128, 20, 24, generator=g)
+    w = torch.randn(cout, 64, k, k, generator=g) * 0.05
+    b = torch.randn(cout, generator=g)
+    r = torch.randn(2, cout, 20, 24, generator=g)
+    dout = torch.randn(2, cout, 20, 24, generator=g)
 
     def run(dev, dt, fused):
         xx = x.detach().clone().to(dev, dt).contiguous(memory_format=torch.channels_last).requires_grad_(True)
