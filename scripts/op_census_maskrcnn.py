@@ -73,6 +73,21 @@ def main():
     print(f"kernels attributed to aten ops: {tot}")
     for (name, where), n in agg.most_common(150):
         print(f"{n:5d}  {name:40s} {where}")
+    # which ops launch the kernels matching CENSUS_KERNELS (regex)
+    import re
+    pat = re.compile(os.environ.get("CENSUS_KERNELS", "rocprim|fillBuffer|SubTensorOp|CUDAFunctor_add"))
+    sel = collections.Counter()
+    for e in evs:
+        if e.device_type.name != "CPU" or not e.name.startswith("aten::"):
+            continue
+        frames = [f for f in (e.stack or []) if "mxtrain" in f]
+        where = frames[0].split("mxtrain/")[-1] if frames else "?"
+        for k in getattr(e, "kernels", []) or []:
+            if pat.search(k.name):
+                sel[(k.name[:60], e.name, where)] += 1
+    print("\nselected kernels by launching op:")
+    for (kn, name, where), n in sel.most_common(80):
+        print(f"{n:5d}  {kn:60s} {name:32s} {where}")
 
 
 if __name__ == "__main__":
