@@ -101,6 +101,9 @@ def main():
                          "to $PYTORCH_TUNABLEOP_FILENAME (see scripts/tune_gemms.sh)")
     ap.add_argument("--wgrad-stream", action="store_true",
                     help="run weight-gradient GEMMs on a concurrent side stream")
+    ap.add_argument("--no-fused-linear", action="store_true",
+                    help="hipBLASLt for the Linear forward / dgrad GEMMs + separate bias-GeLU kernels "
+                         "(default: csrc/gemm_nt.hip with fused epilogues)")
     ap.add_argument("--no-maskrcnn", action="store_true",
                     help="skip the Mask R-CNN images/s measurements (run on one GPU only)")
     ap.add_argument("--xgmi", choices=["0", "1", "auto"], default="0",
@@ -147,7 +150,7 @@ def main():
     tcfg = TrainConfig(micro_batch_size=args.micro_batch_size, global_batch_size=args.global_batch_size,
                        overlap_grad_reduce=not args.no_overlap, lr_warmup_iters=0,
                        wgrad_stream=args.wgrad_stream, moe_expert_parallel_size=args.ep,
-                       overlap_optimizer=args.overlap_optimizer)
+                       overlap_optimizer=args.overlap_optimizer, fused_linear=not args.no_fused_linear)
     tr = GPTTrainer(cfg, tcfg, ps)
     gen = torch.Generator().manual_seed(1 + ps.dp_rank)
     tokens, labels = synthetic_batch(cfg, tr.num_micro, args.micro_batch_size, ps.device, gen)
@@ -233,6 +236,7 @@ def main():
                 "optimizer": "adamw_deferred_overlapped" if tr.opt.overlap_update else "adamw",
                 "tuned_gemm_tables": n_tables,
                 "collectives": _coll_summary(tr),
+                "fused_linear": not args.no_fused_linear,
             },
             "tflops_per_gpu": round(flops / world / 1e12, 1),
             "mfu_bf16_dense_2.5pf": round(flops / world / 2.5e15, 4),

@@ -1,0 +1,367 @@
+// Forward and data-gradient GEMMs of the transformer Linear layers, with the elementwise
+// work that follows them fused into the epilogue (gfx950, bf16 in, fp32 accumulate):
+//
+//   forward  C[M][N] = A[M][K] . W[N][K]^T   (W read in place, K contiguous: "B_KC")
+//   dgrad    C[M][N] = A[M][K] . W[K][N]     (the same weight, now K-major)
+//
+// with A the activations / output gradients ([tokens, features], K contiguous) and the
+// epilogue EPI one of
+//   0  C = acc
+//   1  C = acc + bias[n]                                   (QKV projection)
+//   2  H = acc + bias[n] -> aux (bf16), C = gelu(H)        (fc1: Megatron bias_gelu fused)
+//   3  D = acc * gelu'(aux[m][n]) -> C, plus fp32 column partial sums of D (the fc1 bias
+//      gradient) per 16*FM-row wave block                 (fc2 dgrad: bias_gelu backward)
+// Reference: Megatron-DeepSpeed's ColumnParallelLinear / RowParallelLinear GEMMs and its
+// fused `bias_gelu_impl` (pinned by /root/reference/containers/megatron-deepspeed/
+// Dockerfile:13, configured by examples/megatron-deepspeed/gpt2_345m/pretrain-ddp-zero1.yaml:
+// 39-53); SURVEY §2.8 K6/K12.
+//
+// Why hand-written: hipBLASLt on gfx950 has no bf16 AUX/DGELU epilogue (it returns no
+// algorithm), so bias-GeLU cost two extra memory passes per layer, and its picks for the
+// hidden = 1024 shapes ran at ~0.76 PF/s (profiles/r2_gpt_s3/SPEED_OF_LIGHT.md).
+//
+// Design (cdna_hip_programming.md §5):
+//  * one output tile per workgroup, tiles sized so one launch has ~256 of them (BM x BN in
+//    {256x256, 256x192, 256x128, 128x256, 128x128}); waves own 16*FM x 16*FN sub-blocks;
+//  * operands staged by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction, no
+//    staging registers) into an NSLOT ring, one raw barrier per 64-deep K-step, counted
+//    vmcnt waits so the next steps' DMA stays in flight across the barrier;
+//  * K-contiguous images are [row][64 k] with 128-B rows whose 16-B chunks are XOR-swizzled
+//    by (row & 7) on the DMA SOURCE address (the LDS write stays lane-linear); MFMA
+//    fragments are plain ds_read_b128 (conflict-free over every 16-lane read group);
+//    the K-major weight image of dgrad uses gemm.hip's transposed-read scheme;
+//  * the weight fragment is the MFMA's A operand, so a lane ends with 4 CONSECUTIVE output
+//    columns of one row: 8-B stores, 4 bias values per 8-B load, 4 aux values per 8-B load;
+//  * XCD-aware grouped tile order: the tiles one XCD runs are a compact (gm x n) block.
+#include "gemm_common.h"
+
+using namespace mx;
+using namespace mx::gemm;
+
+namespace {
+
+struct Args {
+  const uint16_t* a;     // [M][lda], K contiguous
+  const uint16_t* b;     // B_KC: [N][ldb] K contiguous; else [K][ldb]
+  uint16_t* c;           // [M][ldc]
+  uint16_t* aux;         // EPI 2: pre-activation out; EPI 3: pre-activation in ([M][ldx])
+  const uint16_t* bias;  // EPI 1, 2: [N]
+  float* part;           // EPI 3: [M / (16 FM)][N] fp32 column partials
+  int lda, ldb, ldc, ldx;
+  int K, N;
+  int tiles_n, gm;
+};
+
+__device__ __forceinline__ float dpp_rowsum16(float v) {
+  v += MX_DPP(v, 0xB1);   // quad_perm [1,0,3,2]
+  v += MX_DPP(v, 0x4E);   // quad_perm [2,3,0,1]
+  v += MX_DPP(v, 0x124);  // row_ror:4
+  v += MX_DPP(v, 0x128);  // row_ror:8  -> every lane of a 16-lane row holds the row sum
+  return v;
+}
+
+template <bool BKC, int WM, int WN, int FM, int FN, int NSLOT>
+struct Geo {
+  static constexpr int BKT = 64;
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
+  static constexpr int RA = BKT * 2;                   // [m][k] image row bytes
+  static constexpr int IA = BM * RA;
+  static constexpr int RB = BKC ? BKT * 2 : BN * 2;    // [n][k] or [k][n] image row bytes
+  static constexpr int IB = BKC ? BN * RB : BKT * RB;
+  static constexpr int PA = IA / 1024 / NW, PB = IB / 1024 / NW;
+  static constexpr int SLOT = IA + IB, LDS = NSLOT * SLOT;
+  static_assert(PA * NW * 1024 == IA && PB * NW * 1024 == IB, "DMA pieces per wave");
+  static_assert(BKC || (RB >= 256 && (BN & (BN - 1)) == 0), "K-major weight image needs BN = 2^k >= 128");
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+template <bool BKC, int WM, int WN, int FM, int FN, int NSLOT, int MINB, int EPI>
+__global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_nt_kernel(const Args g) {
+  using Gm = Geo<BKC, WM, WN, FM, FN, NSLOT>;
+  constexpr int BKT = Gm::BKT, BM = Gm::BM, BN = Gm::BN, RA = Gm::RA, RB = Gm::RB, IA = Gm::IA;
+  constexpr int PA = Gm::PA, PB = Gm::PB, SLOT = Gm::SLOT;
+  constexpr int PER = PA + PB;   // DMA instructions per wave per K-step
+  __shared__ __attribute__((aligned(1024))) char smem[Gm::LDS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // grouped, XCD-contiguous tile order: consecutive logical ids walk gm row-tiles first
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = g.gm * g.tiles_n;
+  const int grp = wg / per_group, rem = wg - grp * per_group;
+  const int tm = grp * g.gm + rem % g.gm, tn = rem / g.gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = g.K / BKT;
+
+  // ---- LDS-DMA sources.  K-contiguous image: a 1-KiB piece = 8 rows x 128 B; lane l fills
+  // row l/8, physical chunk l%8, i.e. logical chunk (l%8) ^ (row & 7)
+  const uint16_t* srcA[PA];
+  const uint16_t* srcB[PB];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    const int row = (PA * wave + j) * 8 + (lane >> 3);
+    srcA[j] = g.a + (size_t)(m0 + row) * g.lda + 8 * ((lane & 7) ^ (row & 7));
+  }
+  if constexpr (BKC) {
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int row = (PB * wave + j) * 8 + (lane >> 3);
+      srcB[j] = g.b + (size_t)(n0 + row) * g.ldb + 8 * ((lane & 7) ^ (row & 7));
+    }
+  } else {
+    constexpr int CB = RB / 16;   // chunks per k-row
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int k = (PB * wave + j) * (1024 / RB) + lane / CB;
+      srcB[j] = g.b + (size_t)k * g.ldb + n0 + 8 * pchunk(k, lane % CB);
+    }
+  }
+  const size_t stepB = BKC ? (size_t)BKT : (size_t)BKT * g.ldb;
+
+  // ---- fragment offsets: lane (G, i) reads row i of a 16-row subtile, k 8G .. 8G + 7 (+32 kk)
+  const int G = lane >> 4, i = lane & 15;
+  const int wm = wave / WN, wn = wave % WN;
+  int offA[FM], offB[FN];
+#pragma unroll
+  for (int s = 0; s < FM; ++s) offA[s] = (16 * (FM * wm + s) + i) * RA;
+  int cA[BKT / 32];
+#pragma unroll
+  for (int kk = 0; kk < BKT / 32; ++kk) cA[kk] = 16 * ((4 * kk + G) ^ (i & 7));
+  if constexpr (BKC) {
+#pragma unroll
+    for (int u = 0; u < FN; ++u) offB[u] = (16 * (FN * wn + u) + i) * RB;
+  } else {
+    const int krow = 8 * G + (i >> 2);
+    const int gg = gsw(krow);
+#pragma unroll
+    for (int u = 0; u < FN; ++u)
+      offB[u] = krow * RB + ((((FN * wn + u) ^ gg) << 1) | ((i & 3) >> 1)) * 16 + (i & 1) * 8;
+  }
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int s = 0; s < FM; ++s)
+#pragma unroll
+    for (int u = 0; u < FN; ++u) acc[s][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const uint32_t lds0 = lds_addr(smem);
+  // one DMA piece j of K-step `it` into ring slot `slot` (pieces 0 .. PA-1: A, then B)
+  auto piece = [&](int slot, int it, int j) __attribute__((always_inline)) {
+    if (j < PA) {
+      const uint32_t b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + (PA * wave + j) * 1024);
+      dma16(srcA[j] + (size_t)it * BKT, b0);
+    } else {
+      const uint32_t b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + (PB * wave + j - PA) * 1024);
+      dma16(srcB[j - PA] + it * stepB, b1);
+    }
+  };
+
+#pragma unroll
+  for (int q = 0; q < NSLOT - 1; ++q)
+    if (q < nk) {
+#pragma unroll
+      for (int j = 0; j < PER; ++j) piece(q, q, j);
+    }
+  // the next step's pieces are spread over the first half of this step's MFMA sequence
+  // (one or two per fragment row) instead of being issued back to back after the barrier:
+  // an LDS-DMA issue costs ~60-185 cycles of the wave's issue slot, so a burst of PER of
+  // them left the matrix pipe idle at the top of every K-step
+  constexpr int NS = (BKT / 32) * FM;            // fragment-row steps per K-step
+  constexpr int SPREAD = NS / 2 >= PER ? NS / 2 : NS;
+  int slot = 0;
+  for (int it = 0; it < nk; ++it) {
+    // retire step it's pieces (later steps stay in flight), then one barrier: every wave's
+    // pieces of step it have landed and every wave is done reading step it - 1's slot
+    const int later = nk - 1 - it;
+    if (NSLOT >= 4 && later >= 2) vm_wait<(NSLOT >= 4 ? 2 : 0) * PER>();
+    else if (NSLOT >= 3 && later >= 1) vm_wait<(NSLOT >= 3 ? 1 : 0) * PER>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    const bool fetch = it + NSLOT - 1 < nk;
+    int ns = slot + NSLOT - 1;
+    if (ns >= NSLOT) ns -= NSLOT;
+    const char* As = smem + slot * SLOT;
+    const char* Bs = As + IA;
+#pragma unroll
+    for (int kk = 0; kk < BKT / 32; ++kk) {
+      bf16x8 w[FN];
+#pragma unroll
+      for (int u = 0; u < FN; ++u) {
+        if constexpr (BKC) w[u] = lds_read8(Bs, offB[u] + cA[kk]);
+        else w[u] = cat(tr_read(Bs, offB[u] + 32 * RB * kk), tr_read(Bs, offB[u] + 32 * RB * kk + 4 * RB));
+      }
+#pragma unroll
+      for (int s = 0; s < FM; ++s) {
+        const bf16x8 x = lds_read8(As, offA[s] + cA[kk]);
+        const int q = kk * FM + s;
+#pragma unroll
+        for (int j = 0; j < PER; ++j)
+          if (q < SPREAD && j * SPREAD / PER == q && fetch) piece(ns, it + NSLOT - 1, j);
+#pragma unroll
+        for (int u = 0; u < FN; ++u) acc[s][u] = mfma16(w[u], x, acc[s][u]);
+      }
+    }
+    if (++slot == NSLOT) slot = 0;
+  }
+
+  // ---- epilogue: lane holds C[m0 + 16 (FM wm + s) + i][n0 + 16 (FN wn + u) + 4 G + e]
+  const int row0 = m0 + 16 * FM * wm + i;
+  const int col0 = n0 + 16 * FN * wn + 4 * G;
+  float bias[FN][4];
+  if constexpr (EPI == 1 || EPI == 2) {
+#pragma unroll
+    for (int u = 0; u < FN; ++u) {
+      const uint2 bv = *reinterpret_cast<const uint2*>(g.bias + col0 + 16 * u);
+      bias[u][0] = lo_bf(bv.x); bias[u][1] = hi_bf(bv.x);
+      bias[u][2] = lo_bf(bv.y); bias[u][3] = hi_bf(bv.y);
+    }
+  }
+  float csum[FN][4];
+  if constexpr (EPI == 3) {
+#pragma unroll
+    for (int u = 0; u < FN; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) csum[u][e] = 0.f;
+  }
+#pragma unroll
+  for (int s = 0; s < FM; ++s) {
+    const size_t r = (size_t)(row0 + 16 * s);
+    uint16_t* crow = g.c + r * g.ldc + col0;
+#pragma unroll
+    for (int u = 0; u < FN; ++u) {
+      float v[4] = {acc[s][u][0], acc[s][u][1], acc[s][u][2], acc[s][u][3]};
+      if constexpr (EPI == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += bias[u][e];
+      } else if constexpr (EPI == 2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += bias[u][e];
+        *reinterpret_cast<uint2*>(g.aux + r * g.ldx + col0 + 16 * u) =
+            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
+      } else if constexpr (EPI == 3) {
+        const uint2 hv = *reinterpret_cast<const uint2*>(g.aux + r * g.ldx + col0 + 16 * u);
+        const float h[4] = {lo_bf(hv.x), hi_bf(hv.x), lo_bf(hv.y), hi_bf(hv.y)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] *= gelu_tanh_grad(h[e]);
+          csum[u][e] += v[e];
+        }
+      }
+      *reinterpret_cast<uint2*>(crow + 16 * u) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    }
+  }
+  if constexpr (EPI == 3) {
+    // column sums of this wave's 16 FM rows: over the 16 lanes of a row (i), lane i == 0
+    // of each G writes 4 consecutive columns
+    float* prow = g.part + (size_t)(tm * WM + wm) * g.N + col0;
+#pragma unroll
+    for (int u = 0; u < FN; ++u) {
+      float t[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[e] = dpp_rowsum16(csum[u][e]);
+      if (i == 0) *reinterpret_cast<float4*>(prow + 16 * u) = make_float4(t[0], t[1], t[2], t[3]);
+    }
+  }
+}
+
+template <bool BKC, int WM, int WN, int FM, int FN, int NSLOT, int MINB, int EPI>
+int launch(Args a, int M, hipStream_t stream) {
+  using Gm = Geo<BKC, WM, WN, FM, FN, NSLOT>;
+  if (M % Gm::BM || a.N % Gm::BN || a.K % Gm::BKT || a.K <= 0) return (int)hipErrorInvalidValue;
+  const int tiles_m = M / Gm::BM;
+  a.tiles_n = a.N / Gm::BN;
+  int gm = 8;
+  while (gm > 1 && tiles_m % gm) gm >>= 1;
+  a.gm = gm;
+  hipLaunchKernelGGL((gemm_nt_kernel<BKC, WM, WN, FM, FN, NSLOT, MINB, EPI>), dim3(tiles_m * a.tiles_n),
+                     dim3(Gm::NT), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+// variant -> {BM, BN, rows per column-partial block (16 FM), B may be K-major}
+struct Variant {
+  int bm, bn, part_rows, kmajor_ok;
+};
+constexpr Variant kVariants[] = {
+    {256, 256, 128, 1},   // 0: 8 waves 2 x 4 of 128 x 64, 2-slot ring (128 KiB)
+    {256, 192, 64, 0},    // 1: 8 waves 4 x 2 of 64 x 96, 2-slot ring (112 KiB); forward only
+    {128, 128, 64, 1},    // 2: 4 waves 2 x 2 of 64 x 64, 2-slot ring, two workgroups per CU
+    {128, 128, 64, 1},    // 3: 8 waves 2 x 4 of 64 x 32, 4-slot ring
+    {256, 128, 64, 1},    // 4: 8 waves 4 x 2 of 64 x 64, 2-slot ring (96 KiB)
+    {128, 256, 64, 1},    // 5: 8 waves 2 x 4 of 64 x 64, 2-slot ring (96 KiB)
+    {128, 128, 64, 1},    // 6: 4 waves 2 x 2 of 64 x 64, 3-slot ring, one workgroup per CU
+};
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+template <bool BKC, int EPI>
+int dispatch(int variant, const Args& a, int M, hipStream_t st) {
+  switch (variant) {
+    case 0: return launch<BKC, 2, 4, 8, 4, 2, 1, EPI>(a, M, st);
+    case 1:
+      if constexpr (BKC) return launch<BKC, 4, 2, 4, 6, 2, 1, EPI>(a, M, st);
+      else return (int)hipErrorInvalidValue;
+    case 2: return launch<BKC, 2, 2, 4, 4, 2, 2, EPI>(a, M, st);
+    case 3: return launch<BKC, 2, 4, 4, 2, 4, 1, EPI>(a, M, st);
+    case 4: return launch<BKC, 4, 2, 4, 4, 2, 1, EPI>(a, M, st);
+    case 5: return launch<BKC, 2, 4, 4, 4, 2, 1, EPI>(a, M, st);
+    case 6: return launch<BKC, 2, 2, 4, 4, 3, 1, EPI>(a, M, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+// Tile geometry of a variant: what = 0 -> BM, 1 -> BN, 2 -> rows per column-partial block,
+// 3 -> 1 when the weight may be K-major (dgrad).  -1 for an unknown variant.
+MX_EXPORT int mx_gemm_nt_tile(int variant, int what) {
+  if (variant < 0 || variant >= kNumVariants) return -1;
+  const Variant& v = kVariants[variant];
+  return what == 0 ? v.bm : what == 1 ? v.bn : what == 2 ? v.part_rows : v.kmajor_ok;
+}
+
+// C[M][N] = A[M][K] . op(B) with the epilogue `epi` (see the file comment).
+//   b_kmajor = 0: B is [N][ldb] (forward, C = A B^T);  1: B is [K][ldb] (dgrad, C = A B).
+//   aux [M][ldx]: EPI 2 output / EPI 3 input; bias [N] (EPI 1, 2); part (EPI 3): fp32
+//   [M / part_rows][N] column partial sums.
+// Contract (checked): M, N multiples of the variant's tile, K a multiple of 64, every
+// pointer 16-B aligned and every leading dimension a multiple of 8 elements.
+MX_EXPORT int mx_gemm_nt(const void* a, const void* b, void* c, void* aux, const void* bias, void* part,
+                         int lda, int ldb, int ldc, int ldx, int M, int N, int K, int b_kmajor, int epi,
+                         int variant, void* stream) {
+  if (variant < 0 || variant >= kNumVariants || M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  if ((((uintptr_t)a) | ((uintptr_t)b) | ((uintptr_t)c)) & 15) return (int)hipErrorInvalidValue;
+  if ((lda & 7) || (ldb & 7) || (ldc & 7) || lda < K || ldc < N) return (int)hipErrorInvalidValue;
+  if (b_kmajor ? ldb < N : ldb < K) return (int)hipErrorInvalidValue;
+  if ((epi == 1 || epi == 2) && (bias == nullptr || ((uintptr_t)bias & 7))) return (int)hipErrorInvalidValue;
+  if ((epi == 2 || epi == 3) && (aux == nullptr || ((uintptr_t)aux & 7) || (ldx & 3) || ldx < N))
+    return (int)hipErrorInvalidValue;
+  if (epi == 3 && (part == nullptr || ((uintptr_t)part & 15))) return (int)hipErrorInvalidValue;
+  Args g{};
+  g.a = (const uint16_t*)a;
+  g.b = (const uint16_t*)b;
+  g.c = (uint16_t*)c;
+  g.aux = (uint16_t*)aux;
+  g.bias = (const uint16_t*)bias;
+  g.part = (float*)part;
+  g.lda = lda;
+  g.ldb = ldb;
+  g.ldc = ldc;
+  g.ldx = ldx;
+  g.K = K;
+  g.N = N;
+  hipStream_t st = (hipStream_t)stream;
+  if (!b_kmajor) {
+    switch (epi) {
+      case 0: return dispatch<true, 0>(variant, g, M, st);
+      case 1: return dispatch<true, 1>(variant, g, M, st);
+      case 2: return dispatch<true, 2>(variant, g, M, st);
+      default: return (int)hipErrorInvalidValue;
+    }
+  }
+  switch (epi) {
+    case 0: return dispatch<false, 0>(variant, g, M, st);
+    case 3: return dispatch<false, 3>(variant, g, M, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}

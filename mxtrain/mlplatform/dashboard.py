@@ -280,12 +280,28 @@ def resolve_logspath(logspath: str) -> str:
     return logspath
 
 
-def create_tensorboard(name: str, logspath: str) -> dict:
+def safe_logdir(logdir: str) -> str:
+    """A log directory the viewer may read: pvc://claim/path, or a path that resolves inside
+    the PV root or the mxtrain home (job logs) -- never an arbitrary server directory."""
+    if logdir.startswith("pvc://"):
+        return resolve_logspath(logdir)
+    target = os.path.realpath(logdir)
+    for root in (pv_root(), mxtrain_home()):
+        r = os.path.realpath(root)
+        if target == r or target.startswith(r + os.sep):
+            return target
+    raise PermissionError(f"log dir outside the PV root: {logdir}")
+
+
+def create_tensorboard(name: str, logspath: str, namespace: str = "kubeflow-user-example-com") -> dict:
     from ..launch.release import check_name
     check_name(name, "tensorboard name")
+    check_name(namespace, "namespace")
+    if not logspath.startswith("pvc://"):
+        raise PermissionError("Tensorboard logspath must be pvc://<claim>/<path>")
     resolve_logspath(logspath)
     os.makedirs(tensorboards_dir(), exist_ok=True)
-    rec = {"name": name, "logspath": logspath, "url": f"/tensorboard/{name}"}
+    rec = {"name": name, "logspath": logspath, "namespace": namespace, "url": f"/tensorboard/{name}"}
     with open(os.path.join(tensorboards_dir(), name + ".json"), "w") as f:
         json.dump(rec, f)
     return rec
@@ -308,7 +324,7 @@ def _tensorboard_html(logdir: Optional[str], q: Optional[Dict[str, str]] = None)
                 "<form action='/tensorboard'>log dir: <input name='logdir' size=60>"
                 "<input type=submit value='open'></form></body></html>")
     smoothing = min(max(float(q.get("smoothing", "0.6")), 0.0), 0.999)
-    view = tensorboard_view(logdir, q.get("tag"))
+    view = tensorboard_view(safe_logdir(logdir), q.get("tag"))
     parts = [f"<h3>{html.escape(tag)}</h3>{_svg_multi(runs, smoothing)}" for tag, runs in sorted(view.items())]
     form = (f"<form>smoothing <input name='smoothing' value='{smoothing}' size=5> tag regex "
             f"<input name='tag' value='{html.escape(q.get('tag', ''))}'>"
@@ -393,6 +409,9 @@ class Auth:
         return h == p
 
 
+_API_CTYPES = ("application/json", "application/yaml", "application/x-yaml", "text/yaml")
+
+
 def _body_doc(body: bytes):
     """JSON or YAML request body -> object (safe loader only)."""
     import yaml
@@ -435,7 +454,12 @@ def route_post(parts: List[str], q: Dict[str, str], body: bytes, user: Optional[
     if rest == ["tensorboards"]:
         if not isinstance(doc, dict):
             raise ValueError("body must be a mapping")
-        return 201, js, json.dumps(create_tensorboard(str(doc.get("name", "")), str(doc.get("logspath", ""))))
+        ns = str(doc.get("namespace", "kubeflow-user-example-com"))
+        if user is not None:
+            from .profiles import can
+            if not can(user, "create", ns):
+                raise PermissionError(f"{user} may not create Tensorboards in namespace {ns}")
+        return 201, js, json.dumps(create_tensorboard(str(doc.get("name", "")), str(doc.get("logspath", "")), ns))
     if rest == ["runs"]:
         if not isinstance(doc, dict):
             raise ValueError("body must be a mapping")
@@ -447,6 +471,11 @@ def route_post(parts: List[str], q: Dict[str, str], body: bytes, user: Optional[
                             run_name=doc.get("name"))
         return 201, js, json.dumps({"run": run})
     if len(rest) == 3 and rest[0] == "runs" and rest[2] == "terminate":
+        if user is not None:   # KFAM: only an owner / contributor of every namespace the run touches
+            from .profiles import can
+            for ns in pl.run_namespaces(rest[1]):
+                if not can(user, "delete", ns):
+                    raise PermissionError(f"{user} may not terminate runs in namespace {ns}")
         return 200, js, json.dumps({"run": rest[1], "terminating": pl.terminate_run(rest[1])})
     return 404, js, json.dumps({"error": "not found"})
 
@@ -486,9 +515,10 @@ def route(path: str, q: Dict[str, str], method: str = "GET", body: bytes = b"", 
         if k == "volumes" and len(rest) == 2:
             return 200, js, json.dumps(volume_browse(rest[1], q.get("path", "")))
         if k == "tensorboards" and "logdir" in q:
+            logdir = safe_logdir(q["logdir"])
             if q.get("view") == "tags":
-                return 200, js, json.dumps(tensorboard_view(q["logdir"], q.get("tag")))
-            return 200, js, json.dumps(tensorboard(q["logdir"]))
+                return 200, js, json.dumps(tensorboard_view(logdir, q.get("tag")))
+            return 200, js, json.dumps(tensorboard(logdir))
         if k == "tensorboards":
             return 200, js, json.dumps(list_tensorboards())
         if k == "experiments":
@@ -606,6 +636,13 @@ def make_server(host: str, port: int, auth: Auth, certfile=None, keyfile=None) -
             # writes (starting jobs) need authenticated users, except on a loopback bind
             if not auth.enabled and not loopback:
                 self._send(403, "application/json", json.dumps({"error": "writes need --htpasswd or --oidc"}))
+                return
+            # CSRF: a browser holding cached credentials can be made to send a cross-site
+            # text/plain or form POST, but not an application/json one without a preflight
+            ctype = self.headers.get("Content-Type", "").split(";")[0].strip().lower()
+            if ctype not in _API_CTYPES:
+                self._send(415, "application/json",
+                           json.dumps({"error": "Content-Type must be application/json or YAML"}))
                 return
             q = {k: v[0] for k, v in urllib.parse.parse_qs(u.query).items()}
             code, ctype, body = route(u.path, q, "POST", data,

@@ -34,7 +34,7 @@ import torch
 from .. import ops
 from ..ops import attention as attn_ops
 from ..ops.norm import bda_norm_fwd, colsum, layernorm_fwd, norm_bwd
-from ..ops.gemm import wgrad_group
+from ..ops.gemm import linear_dgrad, linear_fwd, wgrad_group
 from ..ops.rope import apply_rope_
 from ..ops.fused import (bias_gelu_bwd, bias_gelu_fwd, bias_swiglu_bwd, bias_swiglu_fwd,
                          cross_entropy_fwd_bwd, embed_bwd, embed_fwd, pos_embed_bwd)
@@ -123,6 +123,10 @@ GPT_CONFIGS = {
 
 SALT_EMB = 7
 SALT_ATTN = 50000   # + layer index; the attention mask is keyed on GLOBAL heads, so no TP term
+# + micro-batch index x MICRO_SALT: every micro-batch of a step draws fresh dropout masks
+# (Megatron draws a new mask on every call); micro-batch 0 keeps the plain salts
+MICRO_SALT = 0x2545F491
+M32 = 0xFFFFFFFF
 _NORM_PARAMS = ("ln1_w", "ln1_b")
 
 
@@ -304,6 +308,11 @@ class StepRuntime:
     dmask_l0: int = 0
     dmask_key: Optional[tuple] = None
     batch_dmasks: bool = False    # GPTTrainer turns it on (it resets dmasks when the seed advances)
+    micro: int = 0                # micro-batch index within the step (dropout-mask key)
+    # forward / dgrad GEMMs of the layer through csrc/gemm_nt.hip with the bias, bias-GeLU
+    # and GeLU' + bias-gradient epilogues fused (ops/gemm.py linear_fwd / linear_dgrad);
+    # False: hipBLASLt + the separate bias-GeLU kernels (the LM head always uses hipBLASLt)
+    fused_linear: bool = True
     side_dmasks: bool = False     # layers 1.. of the batched masks on aux_stream (MXTRAIN_SIDE_DMASKS)
 
     @property
@@ -371,8 +380,13 @@ class StepRuntime:
         if self.before_unit is not None:
             self.before_unit(unit)
 
-    def salt(self, base):
-        return base + (7919 * self.tp_rank if self.sp else 0)
+    def salt(self, base, micro=None):
+        m = self.micro if micro is None else micro
+        return (base + (7919 * self.tp_rank if self.sp else 0) + MICRO_SALT * m) & M32
+
+    def attn_salt(self, layer, micro=None):
+        m = self.micro if micro is None else micro
+        return (SALT_ATTN + layer + MICRO_SALT * m) & M32
 
 
 def _gather(x, rt):
@@ -400,35 +414,45 @@ def _reduce_start(x, rt):
     return C.all_reduce_async(x, rt.tp_group)
 
 
-def _mm_into(out, a, w, trans, bias=None):
+def _mm(a, w, trans=True, bias=None, out=None, fused=False):
+    """a @ W^T (+ bias) (``trans=False``: a @ W, the dgrad of a Linear): through the
+    hand-written MFMA GEMM with the bias in its epilogue when ``fused``, else hipBLASLt."""
+    if fused:
+        if trans:
+            return linear_fwd(a, w, bias, out=out)
+        assert bias is None
+        return linear_dgrad(a, w, out=out)
     b = w.t() if trans else w
+    if out is None:
+        return torch.addmm(bias, a, b) if bias is not None else torch.mm(a, b)
     if bias is None:
-        torch.mm(a, b, out=out)
-    else:
-        torch.addmm(bias, a, b, out=out)
+        return torch.mm(a, b, out=out)
+    return torch.addmm(bias, a, b, out=out)
 
 
-def _gather_mm(x, w, rt, trans=True, bias=None):
+def _mm_into(out, a, w, trans, bias=None, fused=False):
+    _mm(a, w, trans, bias, out=out, fused=fused)
+
+
+def _gather_mm(x, w, rt, trans=True, bias=None, fused=None):
     """(x_full, x_full @ W^T [+ bias]) (``trans=False``: @ W) for a column-parallel GEMM
     whose input is sequence-parallel: with ``rt.sp_gemm_overlap`` the token-chunk GEMM of
     this rank runs while the all-gather brings the other chunks, then the rest."""
+    fused = rt.fused_linear if fused is None else fused
     if not rt.sp:
-        y = torch.addmm(bias, x, w.t() if trans else w) if bias is not None else torch.mm(x, w.t() if trans else w)
-        return x, y
+        return x, _mm(x, w, trans, bias, fused=fused)
     if not rt.sp_gemm_overlap:
         x_full = _gather(x, rt)
-        y = torch.addmm(bias, x_full, w.t() if trans else w) if bias is not None \
-            else torch.mm(x_full, w.t() if trans else w)
-        return x_full, y
+        return x_full, _mm(x_full, w, trans, bias, fused=fused)
     pend = C.all_gather_dim0_async(x, rt.tp_group)
     c, r, n = x.shape[0], rt.tp_rank, rt.tp
     y = torch.empty((c * n, w.shape[0] if trans else w.shape[1]), dtype=x.dtype, device=x.device)
-    _mm_into(y[r * c:(r + 1) * c], x, w, trans, bias)
+    _mm_into(y[r * c:(r + 1) * c], x, w, trans, bias, fused)
     x_full = pend.wait()
     if r > 0:
-        _mm_into(y[:r * c], x_full[:r * c], w, trans, bias)
+        _mm_into(y[:r * c], x_full[:r * c], w, trans, bias, fused)
     if r < n - 1:
-        _mm_into(y[(r + 1) * c:], x_full[(r + 1) * c:], w, trans, bias)
+        _mm_into(y[(r + 1) * c:], x_full[(r + 1) * c:], w, trans, bias, fused)
     return x_full, y
 
 
@@ -456,6 +480,7 @@ class EmbedFn(torch.autograd.Function):
                                         rt.seed_t, rt.salt(SALT_EMB), rt.rms)
         ctx.saved = (ids, h, mean, rstd)
         ctx.rt = rt
+        ctx.micro = rt.micro
         ctx.first_layer = first_layer
         return h, a
 
@@ -466,7 +491,7 @@ class EmbedFn(torch.autograd.Function):
         w, _ = rt.norm_params(f"layers.{ctx.first_layer}.ln1")
         gw, gb = rt.norm_grads(f"layers.{ctx.first_layer}.ln1")
         _, de = norm_bwd(da.contiguous(), dh.contiguous(), h, mean, rstd, w, want_dx=True,
-                         p=rt.p_drop, seed_t=rt.seed_t, salt=rt.salt(SALT_EMB), rms=rt.rms,
+                         p=rt.p_drop, seed_t=rt.seed_t, salt=rt.salt(SALT_EMB, ctx.micro), rms=rt.rms,
                          dgamma=gw, dbeta=gb, accumulate=True, defer=rt.colq)
         if rt.sp:
             de = C.all_gather_dim0(de, rt.tp_group)
@@ -506,8 +531,8 @@ class NormFn(torch.autograd.Function):
 class GPTLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, a, rt: StepRuntime, i: int, next_norm: Optional[str]):
-        h2, a2, saved, dmask, moe = GPTLayerFn._forward_body(rt, i, next_norm, h, a)
-        ctx.rt, ctx.i, ctx.next_norm = rt, i, next_norm
+        h2, a2, saved, dmask, moe = GPTLayerFn._forward_body(rt, i, next_norm, h, a, micro=rt.micro)
+        ctx.rt, ctx.i, ctx.next_norm, ctx.micro = rt, i, next_norm, rt.micro
         if rt.cfg.recompute and rt.training:
             # activation recompute: keep the layer inputs only (the dropout masks are pure
             # functions of the step's seed, so the re-run forward is bit-identical)
@@ -521,7 +546,7 @@ class GPTLayerFn(torch.autograd.Function):
         return h2, a2
 
     @staticmethod
-    def _forward_body(rt: StepRuntime, i: int, next_norm: Optional[str], h, a, recomputing=False):
+    def _forward_body(rt: StepRuntime, i: int, next_norm: Optional[str], h, a, recomputing=False, micro=0):
         cfg = rt.cfg
         P = rt.params
         p = f"layers.{i}."
@@ -530,7 +555,8 @@ class GPTLayerFn(torch.autograd.Function):
         kvl = cfg.num_kv_heads // rt.tp
         eps = cfg.layernorm_epsilon
         dmask = None
-        if rt.p_attn > 0 and rt.dmasks is not None:   # this step's masks, all layers at once
+        if rt.p_attn > 0 and rt.dmasks is not None and rt.dmask_key == (rt.B, rt.S, micro):
+            # this micro-batch's masks, all layers at once
             dmask = rt.dmasks[i - rt.dmask_l0]
         elif rt.p_attn > 0:
             # the keep-mask depends only on the seed: generated on the side stream while the
@@ -538,7 +564,7 @@ class GPTLayerFn(torch.autograd.Function):
             ha_ = hl // rt.cp
             dmask = attn_ops.dropmask(rt.B, rt.S * rt.cp, ha_, rt.p_attn,
                                       rt.attn_seed_t if rt.attn_seed_t is not None else rt.seed_t,
-                                      salt=SALT_ATTN + i, head_offset=rt.tp_rank * hl + rt.cp_rank * ha_,
+                                      salt=rt.attn_salt(i, micro), head_offset=rt.tp_rank * hl + rt.cp_rank * ha_,
                                       total_heads=cfg.num_attention_heads, causal=True, device=a.device,
                                       stream=rt.aux_stream)
         a_full, qkv = _gather_mm(a, P[p + "qkv_w"], rt, bias=P[p + "qkv_b"])
@@ -554,10 +580,10 @@ class GPTLayerFn(torch.autograd.Function):
         ctx_a, lse, dmask = attn_ops.attn_fwd(q, k, v, rt.B, rt.S * rt.cp, ha, kva, D, causal=True,
                                               dmask=dmask)
         ctx_ = head_to_seq(ctx_a, (hl * D,), rt.B, rt.S, rt.cp_group) if rt.cp > 1 else ctx_a
-        o = _reduce(torch.mm(ctx_, P[p + "proj_w"].t()), rt)
+        o = _reduce(_mm(ctx_, P[p + "proj_w"], fused=rt.fused_linear), rt)
         w2, b2 = rt.norm_params(p + "ln2")
         h1, m, mean2, rstd2 = bda_norm_fwd(o, P[p + "proj_b"], h, w2, b2, eps, rt.p_drop, rt.seed_t,
-                                           rt.salt(1000 + 2 * i), rt.rms)
+                                           rt.salt(1000 + 2 * i, micro), rt.rms)
         moe = None
         if is_moe_layer(cfg, i):
             m_full = _gather(m, rt)
@@ -575,19 +601,25 @@ class GPTLayerFn(torch.autograd.Function):
             pre = f = None
             b_fc2 = None
         else:
-            m_full, pre = _gather_mm(m, P[p + "fc1_w"], rt)
-            if cfg.swiglu:
-                f = bias_swiglu_fwd(pre, P[p + "fc1_b"])
+            if rt.fused_linear and not rt.sp and not cfg.swiglu:
+                # fc1 GEMM + bias + GeLU in one kernel; pre = the biased pre-activation
+                m_full = m
+                f, pre = linear_fwd(m, P[p + "fc1_w"], P[p + "fc1_b"], gelu=True)
             else:
-                f = bias_gelu_fwd(pre, P[p + "fc1_b"])
-            g = _reduce(torch.mm(f, P[p + "fc2_w"].t()), rt)
+                m_full, pre = _gather_mm(m, P[p + "fc1_w"], rt)
+                if cfg.swiglu:
+                    f = bias_swiglu_fwd(pre, P[p + "fc1_b"])
+                else:
+                    f = bias_gelu_fwd(pre, P[p + "fc1_b"])
+                    pre = (pre,)   # (un-biased pre-activation: backward adds the bias)
+            g = _reduce(_mm(f, P[p + "fc2_w"], fused=rt.fused_linear), rt)
             b_fc2 = P[p + "fc2_b"]
         if next_norm is not None:
             wn, bn = rt.norm_params(next_norm)
         else:  # stage boundary: plain bias-dropout-add; normalise into a throwaway
             wn, bn = P[p + "ln2_w"], P.get(p + "ln2_b")
         h2, a2, mean_n, rstd_n = bda_norm_fwd(g, b_fc2, h1, wn, bn, eps, rt.p_drop,
-                                              rt.seed_t, rt.salt(1001 + 2 * i), rt.rms)
+                                              rt.seed_t, rt.salt(1001 + 2 * i, micro), rt.rms)
         saved = (a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2, m_full, pre, f, h2, mean_n, rstd_n)
         return h2, a2, saved, dmask, moe
 
@@ -605,7 +637,7 @@ class GPTLayerFn(torch.autograd.Function):
             ctx.inputs = None
             with torch.no_grad():
                 _, _, ctx.saved, ctx.dmask, ctx.moe = GPTLayerFn._forward_body(rt, i, ctx.next_norm, h_in, a_in,
-                                                                              recomputing=True)
+                                                                              recomputing=True, micro=ctx.micro)
         (a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2, m_full, pre, f, h2, mean_n, rstd_n) = ctx.saved
         ctx.saved = None
         dh2 = dh2.contiguous()
@@ -614,14 +646,14 @@ class GPTLayerFn(torch.autograd.Function):
             wn, _ = rt.norm_params(ctx.next_norm)
             gwn, gbn = rt.norm_grads(ctx.next_norm)
             dh1, dg = norm_bwd(da2.contiguous(), dh2, h2, mean_n, rstd_n, wn, want_dx=True,
-                               p=rt.p_drop, seed_t=rt.seed_t, salt=rt.salt(1001 + 2 * i),
+                               p=rt.p_drop, seed_t=rt.seed_t, salt=rt.salt(1001 + 2 * i, ctx.micro),
                                rms=rt.rms, dgamma=gwn, dbeta=gbn, dbias=G.get(p + "fc2_b"),
                                accumulate=True, defer=rt.colq)
         else:
             wn = P[p + "ln2_w"]
             zero = torch.zeros_like(dh2)
             dh1, dg = norm_bwd(zero, dh2, h2, mean_n, rstd_n, wn, want_dx=True, p=rt.p_drop,
-                               seed_t=rt.seed_t, salt=rt.salt(1001 + 2 * i), rms=rt.rms,
+                               seed_t=rt.seed_t, salt=rt.salt(1001 + 2 * i, ctx.micro), rms=rt.rms,
                                dbias=G.get(p + "fc2_b"), accumulate=True, defer=rt.colq)
         # ---- MLP backward
         if ctx.moe is not None:
@@ -638,15 +670,21 @@ class GPTLayerFn(torch.autograd.Function):
                 gbuf.add_(gr.to(gbuf.dtype))
             dm = grads[0].to(dg.dtype)
             return GPTLayerFn._attn_backward(ctx, dm, dh1, a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2)
-        dg_full, df = _gather_mm(dg, P[p + "fc2_w"], rt, trans=False)
         if cfg.swiglu:
+            dg_full, df = _gather_mm(dg, P[p + "fc2_w"], rt, trans=False)
             dpre = bias_swiglu_bwd(df, pre, P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True)
-        else:
-            dpre = bias_gelu_bwd(df, pre, P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True,
+        elif isinstance(pre, tuple):
+            dg_full, df = _gather_mm(dg, P[p + "fc2_w"], rt, trans=False)
+            dpre = bias_gelu_bwd(df, pre[0], P[p + "fc1_b"], dbias=G[p + "fc1_b"], accumulate=True,
                                  inplace=True, defer=rt.colq)
+        else:
+            # fc2 dgrad GEMM x GeLU'(pre) with the fc1 bias-gradient column sums in its epilogue
+            dg_full = dg
+            dpre = linear_dgrad(dg, P[p + "fc2_w"], gelu_aux=pre, dbias=G[p + "fc1_b"], accumulate=True,
+                                defer=rt.colq)
         # dgrad first: its TP combine overlaps the fc2 + fc1 weight-gradient GEMMs (one
         # grouped launch, both operands read in place)
-        pend = _reduce_start(torch.mm(dpre, P[p + "fc1_w"]), rt)
+        pend = _reduce_start(_mm(dpre, P[p + "fc1_w"], trans=False, fused=rt.fused_linear), rt)
         rt.wgrad((G[p + "fc2_w"], dg_full, f), (G[p + "fc1_w"], dpre, m_full))
         dm = pend.wait()
         return GPTLayerFn._attn_backward(ctx, dm, dh1, a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2)
@@ -664,7 +702,7 @@ class GPTLayerFn(torch.autograd.Function):
         w2, _ = rt.norm_params(p + "ln2")
         gw2, gb2 = rt.norm_grads(p + "ln2")
         dh, do_ = norm_bwd(dm, dh1, h1, mean2, rstd2, w2, want_dx=True, p=rt.p_drop,
-                           seed_t=rt.seed_t, salt=rt.salt(1000 + 2 * i), rms=rt.rms, dgamma=gw2,
+                           seed_t=rt.seed_t, salt=rt.salt(1000 + 2 * i, ctx.micro), rms=rt.rms, dgamma=gw2,
                            dbeta=gb2, dbias=G[p + "proj_b"], accumulate=True, defer=rt.colq)
         # ---- attention backward
         do_full, dctx = _gather_mm(do_, P[p + "proj_w"], rt, trans=False)
@@ -684,7 +722,7 @@ class GPTLayerFn(torch.autograd.Function):
         rt.rope_(dqkv, ha, kva, inverse=True)
         if rt.cp > 1:
             dqkv = head_to_seq(dqkv, (hl * D, kvl * D, kvl * D), rt.B, rt.S, rt.cp_group)
-        pend = _reduce_start(torch.mm(dqkv, P[p + "qkv_w"]), rt)
+        pend = _reduce_start(_mm(dqkv, P[p + "qkv_w"], trans=False, fused=rt.fused_linear), rt)
         colsum(dqkv, G[p + "qkv_b"], accumulate=True, defer=rt.colq)
         rt.wgrad((G[p + "proj_w"], do_full, ctx_), (G[p + "qkv_w"], dqkv, a_full))
         da = pend.wait()
@@ -699,7 +737,7 @@ class LMHeadLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, labels, rt: StepRuntime, wname: str):
         W = rt.params[wname]
-        x_full, logits = _gather_mm(x, W, rt)
+        x_full, logits = _gather_mm(x, W, rt, fused=False)   # (hipBLASLt: 256-wide tiles win at V = 50k)
         losses = cross_entropy_fwd_bwd(logits, labels, rt.grad_scale,
                                        tp_group=rt.tp_group if rt.tp > 1 else None,
                                        vocab_start=rt.vocab_start)
@@ -769,12 +807,13 @@ class GPTStage:
         if self.last:
             names.append(self.head_name)
         return names
-    def forward(self, ids=None, hidden=None, labels=None, B=1, S=None):
+    def forward(self, ids=None, hidden=None, labels=None, B=1, S=None, micro: int = 0):
         """First stage takes token ids [B*S]; later stages take the hidden state
         [tokens, h] (requires_grad).  Last stage returns the scalar loss, other stages
         the hidden state to send downstream."""
         rt = self.rt
         rt.B, rt.S = B, S or self.cfg.seq_length
+        rt.micro = micro
         if self.first:
             rt.need(0)
             h, a = EmbedFn.apply(self.anchor, ids, rt, self.l0)
@@ -782,18 +821,18 @@ class GPTStage:
             h = hidden
             rt.need(self.l0)
             a = NormFn.apply(h, rt, f"layers.{self.l0}.ln1", self.l0)
-        if rt.dmasks is not None and rt.dmask_key != (rt.B, rt.S):
+        if rt.dmasks is not None and rt.dmask_key != (rt.B, rt.S, micro):
             rt.dmasks = None
         if (rt.p_attn > 0 and rt.batch_dmasks and rt.dmasks is None and self.l1 > self.l0
                 and rt.seed_t is not None and rt.seed_t.is_cuda):
-            rt.dmask_key = (rt.B, rt.S)
+            rt.dmask_key = (rt.B, rt.S, micro)
             cfg = self.cfg
             hl = cfg.num_attention_heads // rt.tp
             ha_ = hl // rt.cp
             rt.dmask_l0 = self.l0
             rt.dmasks = attn_ops.dropmask_layers(rt.B, rt.S * rt.cp, ha_, rt.p_attn,
                                                  rt.attn_seed_t if rt.attn_seed_t is not None else rt.seed_t,
-                                                 SALT_ATTN + self.l0, self.l1 - self.l0,
+                                                 rt.attn_salt(self.l0, micro), self.l1 - self.l0,
                                                  head_offset=rt.tp_rank * hl + rt.cp_rank * ha_,
                                                  total_heads=cfg.num_attention_heads, causal=True,
                                                  stream=rt.aux_stream if rt.side_dmasks else None)

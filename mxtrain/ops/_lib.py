@@ -87,6 +87,9 @@ SIGNATURES = {
     # gemm.hip
     "mx_gemm_kk_tile": [I, I],
     "mx_gemm_kk": [I, P, I, F, I, I, P, P, P],
+    # gemm_nt.hip
+    "mx_gemm_nt_tile": [I, I],
+    "mx_gemm_nt": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
     # rope.hip
     "mx_rope": [P, I64, I, I, I, I, I, I, I, P, P, P, I, P],
     # vision.hip

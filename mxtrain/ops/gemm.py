@@ -136,3 +136,152 @@ def _torch_wgrad(gbuf, dy, x, accumulate):
 
 def wgrad(gbuf, dy, x, accumulate: bool = True):
     wgrad_group([(gbuf, dy, x)], accumulate)
+
+
+# ============================================================================== forward / dgrad
+# csrc/gemm_nt.hip: C = A W^T (forward) or C = A W (dgrad) with the Linear layer's
+# elementwise tail fused into the epilogue (bias; bias + GeLU saving the pre-activation;
+# GeLU' + bias-gradient column partials).  Shapes the kernel does not tile go through
+# torch (part of the contract, like wgrad above); CPU tensors always do.
+_NT_TILE = {}
+_NT_FORCE = os.environ.get("MXTRAIN_GEMM_NT_VARIANT")
+# preference order: big tiles first (less L2 traffic per FLOP), as long as one launch still
+# has >= ~one tile per CU
+_NT_ORDER = (0, 1, 4, 5, 3, 2)
+
+
+def _nt_tile(variant):
+    t = _NT_TILE.get(variant)
+    if t is None:
+        t = _NT_TILE[variant] = tuple(_lib.query("mx_gemm_nt_tile", variant, w) for w in range(4))
+    return t
+
+
+def nt_plan(M: int, N: int, K: int, kmajor: bool) -> int:
+    """Variant of csrc/gemm_nt.hip for an [M, K] x [K, N] problem, or -1 (not tileable)."""
+    if K % 64:
+        return -1
+    if _NT_FORCE:
+        v = int(_NT_FORCE)
+        bm, bn, _, kok = _nt_tile(v)
+        return v if (M % bm == 0 and N % bn == 0 and (kok or not kmajor)) else -1
+    fallback = -1
+    for v in _NT_ORDER:
+        bm, bn, _, kok = _nt_tile(v)
+        if M % bm or N % bn or (kmajor and not kok):
+            continue
+        if (M // bm) * (N // bn) >= 224:
+            return v
+        if fallback < 0 or (M // bm) * (N // bn) > (M // _nt_tile(fallback)[0]) * (N // _nt_tile(fallback)[1]):
+            fallback = v
+    return fallback
+
+
+def _nt_ok(t: torch.Tensor) -> bool:
+    return (t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0
+            and t.data_ptr() % 16 == 0)
+
+
+def _gelu_ref(h):
+    return 0.5 * h * (1.0 + torch.tanh(0.7978845608028654 * (h + 0.044715 * h * h * h)))
+
+
+def _gelu_grad_ref(h):
+    t = torch.tanh(0.7978845608028654 * (h + 0.044715 * h * h * h))
+    return 0.5 * (1.0 + t) + 0.5 * h * (1.0 - t * t) * 0.7978845608028654 * (1.0 + 3 * 0.044715 * h * h)
+
+
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias=None, gelu: bool = False, out=None, variant: int = -1):
+    """y = x @ w^T (+ bias), x [M, K], w [N, K].  With ``gelu``: returns (gelu(h), h) where
+    h = x w^T + bias is the bf16 pre-activation kept for backward (Megatron bias_gelu)."""
+    M, K = x.shape
+    N = w.shape[0]
+    assert w.shape[1] == K, (x.shape, w.shape)
+    assert bias is not None or not gelu
+    v = variant
+    hip = _lib.use_hip(x)
+    if hip and v < 0 and _nt_ok(x) and _nt_ok(w) and (bias is None or bias.is_contiguous()) \
+            and (out is None or _nt_ok(out)):
+        v = nt_plan(M, N, K, False)
+    if not hip or v < 0:
+        if gelu:
+            h = torch.addmm(bias, x, w.t()) if hip else (x.float() @ w.float().t() + bias.float())
+            y = _gelu_ref(h.float()).to(x.dtype)
+            h = h.to(x.dtype)
+            if out is not None:
+                out.copy_(y)
+                y = out
+            return y, h
+        if hip:
+            y = torch.addmm(bias, x, w.t()) if bias is not None else torch.mm(x, w.t())
+        else:
+            y32 = x.float() @ w.float().t()
+            if bias is not None:
+                y32 = y32 + bias.float()
+            y = y32.to(x.dtype)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    y = out if out is not None else torch.empty((M, N), dtype=x.dtype, device=x.device)
+    h = torch.empty((M, N), dtype=x.dtype, device=x.device) if gelu else None
+    epi = 2 if gelu else (1 if bias is not None else 0)
+    _lib.call("mx_gemm_nt", x.data_ptr(), w.data_ptr(), y.data_ptr(), _lib.ptr(h), _lib.ptr(bias), None,
+              x.stride(0), w.stride(0), y.stride(0), N, M, N, K, 0, epi, v, _lib.stream())
+    return (y, h) if gelu else y
+
+
+def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, gelu_aux=None, dbias=None, accumulate: bool = True,
+                 defer=None, variant: int = -1, out=None):
+    """dx = dy @ w, dy [M, N_out], w [N_out, K_in] -> dx [M, K_in].  With ``gelu_aux`` (the
+    pre-activation h of the layer that produced dy's input... i.e. the fc1 output): returns
+    dx * gelu'(h), and ``dbias`` (bf16 [K_in]) (+)= its column sums -- the fc1 bias gradient
+    (``defer``: ops/norm.py ColReduceQueue, reduced in the step's batched flush)."""
+    M, Kd = dy.shape
+    N = w.shape[1]
+    assert w.shape[0] == Kd, (dy.shape, w.shape)
+    hip = _lib.use_hip(dy)
+    v = variant
+    if hip and v < 0 and _nt_ok(dy) and _nt_ok(w) and (gelu_aux is None or _nt_ok(gelu_aux)) \
+            and (out is None or _nt_ok(out)):
+        v = nt_plan(M, N, Kd, True)
+    if not hip or v < 0:
+        if hip and gelu_aux is None:
+            return torch.mm(dy, w, out=out) if out is not None else torch.mm(dy, w)
+        d32 = torch.mm(dy, w).float() if hip else dy.float() @ w.float()
+        if gelu_aux is None:
+            if out is not None:
+                out.copy_(d32)
+                return out
+            return d32.to(dy.dtype)
+        d32 = d32 * _gelu_grad_ref(gelu_aux.float())
+        if dbias is not None:
+            s = d32.sum(0)
+            if accumulate:
+                s = s + dbias.float()
+            dbias.copy_(s.to(dbias.dtype))
+        if out is not None:
+            out.copy_(d32)
+            return out
+        return d32.to(dy.dtype)
+    dx = out if out is not None else torch.empty((M, N), dtype=dy.dtype, device=dy.device)
+    if gelu_aux is None:
+        _lib.call("mx_gemm_nt", dy.data_ptr(), w.data_ptr(), dx.data_ptr(), None, None, None,
+                  dy.stride(0), w.stride(0), dx.stride(0), 0, M, N, Kd, 1, 0, v, _lib.stream())
+        return dx
+    prow = _nt_tile(v)[2]
+    nparts = M // prow
+    part = None
+    if defer is not None and dbias is not None:
+        part = defer.partial((dbias.data_ptr(),), (dbias, None, None), nparts, N, 1, N, accumulate)
+    deferred = part is not None
+    if part is None:
+        scratch_n = _lib.query64("mx_colreduce_scratch", nparts, N)
+        part = torch.empty(nparts * N + scratch_n, dtype=torch.float32, device=dy.device)
+    _lib.call("mx_gemm_nt", dy.data_ptr(), w.data_ptr(), dx.data_ptr(), gelu_aux.data_ptr(), None,
+              part.data_ptr(), dy.stride(0), w.stride(0), dx.stride(0), gelu_aux.stride(0), M, N, Kd, 1, 3, v,
+              _lib.stream())
+    if dbias is not None and not deferred:
+        _lib.call("mx_colsum_finalize", part.data_ptr(), nparts, N, 1, dbias.data_ptr(), None, None,
+                  int(accumulate), part[nparts * N:].data_ptr(), _lib.stream())
+    return dx

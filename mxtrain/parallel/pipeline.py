@@ -97,9 +97,9 @@ class PipelineSchedule:
             m = fwd_i
             fwd_i += 1
             if first:
-                out = stage.forward(ids=tokens[m].reshape(-1), labels=labels[m].reshape(-1), B=B, S=S)
+                out = stage.forward(ids=tokens[m].reshape(-1), labels=labels[m].reshape(-1), B=B, S=S, micro=m)
             else:
-                out = stage.forward(hidden=inp, labels=labels[m].reshape(-1), B=B, S=S)
+                out = stage.forward(hidden=inp, labels=labels[m].reshape(-1), B=B, S=S, micro=m)
             if last:
                 loss_total = loss_total + out.detach()
             inflight.append((inp, out))
@@ -172,10 +172,10 @@ class PipelineSchedule:
         loss_total = torch.zeros((), dtype=torch.float32, device=tr.device)
         for m in range(nm):
             if first:
-                out = stage.forward(ids=tokens[m].reshape(-1), labels=labels[m].reshape(-1), B=B, S=S)
+                out = stage.forward(ids=tokens[m].reshape(-1), labels=labels[m].reshape(-1), B=B, S=S, micro=m)
             else:
                 inp = self._exchange(recv_shape=shape, recv_from=prev)
-                out = stage.forward(hidden=inp, labels=labels[m].reshape(-1), B=B, S=S)
+                out = stage.forward(hidden=inp, labels=labels[m].reshape(-1), B=B, S=S, micro=m)
             if last:
                 loss_total = loss_total + out.detach()
             else:

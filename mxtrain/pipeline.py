@@ -261,7 +261,8 @@ def submit_run(chart_configs: Optional[List[Dict]] = None, pipeline: Optional[st
     with _RUNS_LOCK:
         if run_name in _RUNS:
             raise ValueError(f"run {run_name} exists")
-        _RUNS[run_name] = {"thread": t, "cancel": cancel, "logs": logs}
+        _RUNS[run_name] = {"thread": t, "cancel": cancel, "logs": logs,
+                           "namespaces": sorted({str((c or {}).get("namespace", "default")) for c in chart_configs})}
     t.start()
     return run_name
 
@@ -280,6 +281,18 @@ def get_run(name: str) -> Dict:
     if live is not None:
         rec["log"] = list(live["logs"])[-50:]
     return rec
+
+
+def run_namespaces(name: str) -> List[str]:
+    """Namespaces a run installs releases into (the KFAM check of terminate)."""
+    with _RUNS_LOCK:
+        live = _RUNS.get(name)
+    if live is not None:
+        return list(live["namespaces"])
+    try:
+        return sorted({str(s.get("namespace") or "default") for s in get_run(name).get("steps", [])})
+    except FileNotFoundError:
+        return []
 
 
 def terminate_run(name: str) -> bool:

@@ -55,6 +55,9 @@ class TrainConfig:
     # per-step zero-fill covers only the other ~1 % of the flat gradient buffer (pp = 1)
     overwrite_wgrads: bool = True
     moe_expert_parallel_size: int = 1   # --moe-expert-parallel-size
+    # Linear forward / dgrad GEMMs with fused bias / bias-GeLU / GeLU' epilogues
+    # (csrc/gemm_nt.hip); False = hipBLASLt + separate bias-GeLU kernels
+    fused_linear: bool = True
 
 
 class GPTTrainer:
@@ -83,6 +86,7 @@ class GPTTrainer:
                               attn_seed_t=self.seed.attn_t)
         self.stage.rt.batch_dmasks = os.environ.get("MXTRAIN_BATCH_DMASKS", "1") != "0"
         self.stage.rt.side_dmasks = os.environ.get("MXTRAIN_SIDE_DMASKS", "0") == "1"
+        self.stage.rt.fused_linear = tcfg.fused_linear
         if tcfg.wgrad_stream and self.device.type == "cuda":
             self.stage.rt.wgrad_stream = torch.cuda.Stream(device=self.device)
         self._overwrite = bool(tcfg.overwrite_wgrads and ps.pp == 1)
@@ -182,14 +186,14 @@ class GPTTrainer:
         self.opt.unit_done(unit)
         self.eopt.unit_done(unit)
 
-    def _micro_forward_backward(self, ids, labels, B, S, last_micro, first_micro=False):
+    def _micro_forward_backward(self, ids, labels, B, S, last_micro, first_micro=False, micro=0):
         rt = self.stage.rt
         rt.wgrad_overwrite = self._overwrite and first_micro
         if self.eopt is not None:
             rt.unit_done = self._unit_done if last_micro else None
         else:
             rt.unit_done = self.opt.unit_done if last_micro else None
-        loss = self.stage.forward(ids=ids, labels=labels, B=B, S=S)
+        loss = self.stage.forward(ids=ids, labels=labels, B=B, S=S, micro=micro)
         if self.opt.overlap_update and self.device.type == "cuda":
             self.opt.wait_all()   # deferred AdamW read/zeroed the grads the backward writes
         loss.backward()
@@ -260,7 +264,7 @@ class GPTTrainer:
             for m in range(nm):
                 loss = loss + self._micro_forward_backward(tokens[m].reshape(-1),
                                                            labels[m].reshape(-1), B, S,
-                                                           m == nm - 1, m == 0)
+                                                           m == nm - 1, m == 0, micro=m)
         if self.stage.rt.colq is not None:
             self.stage.rt.colq.flush()
         if self.eopt is not None:
@@ -314,7 +318,7 @@ class GPTTrainer:
             for m in range(nm):
                 loss = loss + self._micro_forward_backward(tokens[m].reshape(-1),
                                                            labels[m].reshape(-1), B, S,
-                                                           m == nm - 1, m == 0)
+                                                           m == nm - 1, m == 0, micro=m)
         if self.stage.rt.colq is not None:
             self.stage.rt.colq.flush()
         # optimizer body without host-side hyper update (done before each replay)
@@ -368,7 +372,7 @@ class GPTTrainer:
             loss = torch.zeros((), dtype=torch.float32, device=self.device)
             for m in range(nm):
                 loss = loss + self.stage.forward(ids=tokens[m].reshape(-1), labels=labels[m].reshape(-1),
-                                                 B=B, S=S).detach()
+                                                 B=B, S=S, micro=m).detach()
             return self._cp_mean(loss)
         finally:
             rt.training = True

@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 3: new forward/dgrad GEMM numerics + microbench
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "gemm_nt" > gpurun_out/r3a_tests.log 2>&1 || { tail -30 gpurun_out/r3a_tests.log; exit 1; }
+tail -3 gpurun_out/r3a_tests.log
+timeout -k 10 300 python -u scripts/gemm_nt_bench.py > gpurun_out/r3a_bench.log 2>&1 || { tail -30 gpurun_out/r3a_bench.log; exit 1; }
+grep -v "^check" gpurun_out/r3a_bench.log

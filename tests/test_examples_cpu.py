@@ -152,7 +152,9 @@ def test_coco_data_then_mpijob_maskrcnn_cpu(home, monkeypatch):
     assert "Loaded 265 backbone tensors" in log
     logs = home / "home" / "pv" / "pv-efs" / "home" / "maskrcnn-tensorpack" / "logs"
     run = [d for d in os.listdir(logs) if d.startswith("maskrcnn-tensorpack-")]
-    assert run and any(f.endswith(".index") for f in os.listdir(logs / run[0]))
+    # every rank runs the script's `DATE=$(date ...)` (as in the reference), so ranks that start
+    # on either side of a second boundary log to two directories; rank 0's holds the checkpoint
+    assert run and any(f.endswith(".index") for r in run for f in os.listdir(logs / r))
 
 
 def test_legacy_maskrcnn_chart_renders_inline_mpirun(home):

@@ -184,3 +184,31 @@ def test_first_micro_batch_overwrites_gemm_grads():
     for n in runs[False][1]:
         assert torch.equal(runs[True][1][n], runs[False][1][n]), n
         assert torch.equal(runs[True][2][n], runs[False][2][n]), n
+
+
+def test_each_micro_batch_draws_fresh_dropout_masks():
+    """Gradient accumulation: micro-batches 0 and 1 of one step must not reuse the same
+    hidden / attention dropout masks (Megatron draws a fresh mask on every call).  The same
+    tokens fed as micro-batch 0 and micro-batch 1 give different losses; micro-batch 0 is
+    unchanged against the un-indexed call (the bench's single micro-batch keeps its masks),
+    and re-running micro-batch 1 (recompute / pipeline backward) reproduces it exactly."""
+    from mxtrain.models.gpt import MICRO_SALT, SALT_ATTN
+    from mxtrain.ops.attention import dropout_keep_mask
+    cfg = GPTConfig(num_layers=2, hidden_size=64, num_attention_heads=4, seq_length=16,
+                    max_position_embeddings=16, vocab_size=100, hidden_dropout=0.1, attention_dropout=0.1)
+    B, S = 2, 16
+    flat, ids, labels = _setup(cfg, B, S, seed=4)
+    seed = torch.tensor([77], dtype=torch.int32)
+    stage = GPTStage(cfg, flat.params, flat.grads, seed_t=seed, attn_seed_t=seed)
+    stage.rt.grad_scale = 1.0 / (B * S)
+    with torch.no_grad():
+        l_plain = float(stage.forward(ids=ids, labels=labels, B=B, S=S))
+        l0 = float(stage.forward(ids=ids, labels=labels, B=B, S=S, micro=0))
+        l1 = float(stage.forward(ids=ids, labels=labels, B=B, S=S, micro=1))
+        l1b = float(stage.forward(ids=ids, labels=labels, B=B, S=S, micro=1))
+    assert l_plain == l0 and l1 == l1b and l0 != l1, (l_plain, l0, l1, l1b)
+    rt = stage.rt
+    assert rt.salt(1000, 0) != rt.salt(1000, 1) and rt.attn_salt(3, 0) == SALT_ATTN + 3
+    m0 = dropout_keep_mask(B, S, 4, 77, rt.attn_salt(0, 0), 0.1)
+    m1 = dropout_keep_mask(B, S, 4, 77, rt.attn_salt(0, 1), 0.1)
+    assert not torch.equal(m0, m1) and rt.attn_salt(0, 1) == (SALT_ATTN + MICRO_SALT) & 0xFFFFFFFF

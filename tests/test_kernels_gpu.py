@@ -557,3 +557,63 @@ def test_dropmask_layers_match_per_layer_calls(monkeypatch):
         torch.cuda.synchronize()
         runs.append((losses, tr.flat.data.clone()))
     assert runs[0][0] == runs[1][0] and torch.equal(runs[0][1], runs[1][1])
+
+
+# ------------------------------------------------------------------ forward / dgrad GEMMs
+NT_VARIANTS = [0, 1, 2, 3, 4, 5, 6]
+
+
+@pytest.mark.parametrize("variant", NT_VARIANTS)
+@pytest.mark.parametrize("epi", ["none", "bias", "gelu"])
+def test_gemm_nt_forward_epilogues(variant, epi):
+    """csrc/gemm_nt.hip forward (y = x w^T [+ b] [gelu]) against the fp32 reference, for
+    every tile variant (one tile multiple in M, two in N, K = 3 K-steps ... )."""
+    from mxtrain.ops import gemm as Gm
+    bm, bn, _, _ = Gm._nt_tile(variant)
+    M, N, K = 2 * bm, 3 * bn, 192
+    x = _bf(torch.randn(M, K))
+    w = _bf(torch.randn(N, K) * 0.1)
+    b = _bf(torch.randn(N)) if epi != "none" else None
+    out = Gm.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV) if b is not None else None, gelu=epi == "gelu",
+                        variant=variant)
+    ref = Gm.linear_fwd(x, w, b, gelu=epi == "gelu")
+    if epi == "gelu":
+        _close(out[1], ref[1], 2e-2, 1e-2, "pre-activation")
+        _close(out[0], ref[0], 2e-2, 1e-2, "gelu")
+    else:
+        _close(out, ref, 2e-2, 1e-2, "y")
+
+
+@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("gelu", [False, True])
+def test_gemm_nt_dgrad_epilogues(variant, gelu):
+    """dgrad dx = dy w (w K-major) and the fused GeLU' + bias-gradient epilogue."""
+    from mxtrain.ops import gemm as Gm
+    bm, bn, _, _ = Gm._nt_tile(variant)
+    M, N, K = 2 * bm, 2 * bn, 320
+    dy = _bf(torch.randn(M, K))
+    w = _bf(torch.randn(K, N) * 0.1)
+    h = _bf(torch.randn(M, N) * 2) if gelu else None
+    db = _bf(torch.randn(N)) if gelu else None
+    dbg = db.to(DEV) if gelu else None
+    out = Gm.linear_dgrad(dy.to(DEV), w.to(DEV), gelu_aux=h.to(DEV) if gelu else None, dbias=dbg,
+                          accumulate=True, variant=variant)
+    ref = Gm.linear_dgrad(dy, w, gelu_aux=h, dbias=db, accumulate=True)
+    _close(out, ref, 2e-2, 1e-2, "dx")
+    if gelu:
+        _close(dbg, db, 0.25, 2e-2, "dbias")
+
+
+def test_gemm_nt_strided_inputs_and_plan():
+    """Row-strided operands (views into a packed buffer, as the QKV / attention code passes
+    them) and the automatic variant plan at the GPT-2 345M shapes."""
+    from mxtrain.ops import gemm as Gm
+    big = _bf(torch.randn(512, 3 * 1024)).to(DEV)
+    x = big[:, 1024:2048]
+    w = _bf(torch.randn(1024, 1024) * 0.05).to(DEV)
+    y = Gm.linear_fwd(x, w)
+    ref = (x.float() @ w.float().t())
+    _close(y, ref, 3e-2, 1e-2, "strided")
+    for (M, N, K, km) in [(4096, 3072, 1024, False), (4096, 4096, 1024, False), (4096, 1024, 4096, False),
+                          (4096, 1024, 1024, False), (4096, 1024, 3072, True), (4096, 4096, 1024, True)]:
+        assert Gm.nt_plan(M, N, K, km) >= 0, (M, N, K, km)

@@ -99,7 +99,11 @@ def test_dashboard_routes_and_auth(home, tmp_path):
     st = rel.install(os.path.join(CHARTS, "data-prep/data-process"), "dash", value_files=[str(v)],
                      wait=True, timeout=120)
     assert st["phase"] == "Succeeded"
-    with SummaryWriter(str(tmp_path / "tb")) as w:
+    from mxtrain.runtime.storage import pv_root
+    tbdir = os.path.join(pv_root(), "pv-fsx", "tb")
+    with SummaryWriter(tbdir) as w:
+        w.add_scalar("loss", 2.0, 1)
+    with SummaryWriter(str(tmp_path / "outside")) as w:
         w.add_scalar("loss", 2.0, 1)
     code, _, body = db.route("/api/jobs", {})
     assert code == 200 and any(j["name"] == "dash" and j["phase"] == "Succeeded" for j in json.loads(body))
@@ -118,9 +122,13 @@ def test_dashboard_routes_and_auth(home, tmp_path):
     assert db.route("/api/jobs/kubeflow-user-example-com/..%2Fx/logs", {})[0] == 403
     assert db.route("/api/jobs/kubeflow-user-example-com/..", {})[0] == 403
     assert db.route("/api/jobs/kubeflow-user-example-com/dash/logs", {"pod": "../x"})[0] == 403
-    code, _, body = db.route("/api/tensorboards", {"logdir": str(tmp_path / "tb")})
+    code, _, body = db.route("/api/tensorboards", {"logdir": tbdir})
     assert json.loads(body)["loss"][0]["value"] == 2.0
-    assert db.route("/tensorboard", {"logdir": str(tmp_path / "tb")})[2].count("<svg") == 1
+    assert db.route("/tensorboard", {"logdir": tbdir})[2].count("<svg") == 1
+    assert db.route("/api/tensorboards", {"logdir": "pvc://pv-fsx/tb"})[0] == 200
+    # the viewer reads only under the PV root / mxtrain home
+    assert db.route("/api/tensorboards", {"logdir": str(tmp_path / "outside")})[0] == 403
+    assert db.route("/tensorboard", {"logdir": "/etc"})[0] == 403
     assert db.route("/api/nope", {})[0] == 404
     for p in ("/", "/api", "/api/node", "/api/profiles", "/api/experiments", "/api/pipelines"):
         assert db.route(p, {})[0] == 200, p
@@ -233,8 +241,14 @@ def test_pipelines_api_defs_runs_terminate(home):
     th.start()
     try:
         url = f"http://127.0.0.1:{srv.server_address[1]}"
+        # a text/plain or form POST is refused before it reaches the API
+        req = urllib.request.Request(url + "/api/runs", data=json.dumps({"pipeline": "two-steps", "name": "rx"}).encode(),
+                                     method="POST", headers={"Content-Type": "text/plain"})
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(req, timeout=30)
+        assert e.value.code == 415
         req = urllib.request.Request(url + "/api/runs", data=json.dumps({"pipeline": "two-steps", "name": "r1"}).encode(),
-                                     method="POST")
+                                     method="POST", headers={"Content-Type": "application/json"})
         with urllib.request.urlopen(req, timeout=30) as r:
             assert r.status == 201 and json.loads(r.read())["run"] == "r1"
         rec = pl.wait_run("r1", timeout=120)
@@ -254,6 +268,8 @@ def test_pipelines_api_defs_runs_terminate(home):
         except FileNotFoundError:
             pass
         time.sleep(0.2)
+    # a user without a role in the run's namespace cannot terminate it
+    assert db.route("/api/runs/r2/terminate", {}, "POST", user="mallory@example.com")[0] == 403
     code, _, body = db.route("/api/runs/r2/terminate", {}, "POST")
     assert code == 200 and json.loads(body)["terminating"]
     rec = pl.wait_run("r2", timeout=60)
@@ -279,6 +295,11 @@ def test_tensorboard_resources_runs_and_smoothing(home, tmp_path):
     assert code == 201 and json.loads(body)["url"] == "/tensorboard/tb1"
     assert db.route("/api/tensorboards", {}, "POST",
                     json.dumps({"name": "tb2", "logspath": "pvc://pv-fsx/../../etc"}).encode())[0] == 403
+    # only pvc:// logspaths, and only in a namespace the user may write to
+    assert db.route("/api/tensorboards", {}, "POST",
+                    json.dumps({"name": "tb3", "logspath": "/etc"}).encode())[0] == 403
+    assert db.route("/api/tensorboards", {}, "POST", json.dumps({"name": "tb4", "logspath": "pvc://pv-fsx/exp1"}).encode(),
+                    user="mallory@example.com")[0] == 403
     assert [t["name"] for t in json.loads(db.route("/api/tensorboards", {})[2])] == ["tb1"]
     view = json.loads(db.route("/api/tensorboards", {"logdir": logs, "view": "tags"})[2])
     assert set(view) == {"loss", "lr"} and set(view["loss"]) == {"run-a", "run-b"}
