@@ -9,8 +9,6 @@
 //
 // Layout: [M, C] with M = N*H*W rows (NHWC memory), C % 8 == 0; 16-byte vectors (8 bf16),
 // lane-contiguous, so every load/store is a full 16 B per lane.
-#include <cstdlib>
-
 #include "common.h"
 
 using namespace mx;
@@ -20,16 +18,15 @@ namespace {
 // y = act(y + b (+ res)) in place; one thread per 8-channel vector
 template <bool kRes, bool kRelu>
 __global__ __launch_bounds__(256) void bias_act_fwd_kernel(uint16_t* __restrict__ y, const uint16_t* __restrict__ b,
-                                                           const uint16_t* __restrict__ res, int64_t nvec, int c8,
-                                                           int c8m) {
+                                                           const uint16_t* __restrict__ res, int64_t nvec, int c8) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
     float x[8], bb[8];
     unpack8(reinterpret_cast<const uint4*>(y)[v], x);
     if (b) {
-      // bias vector: a mask for power-of-two channel counts (64..2048 here), else the
-      // 64-bit modulo (a software division)
-      unpack8(reinterpret_cast<const uint4*>(b)[c8m >= 0 ? (int)(v & c8m) : (int)(v % c8)], bb);
+      // bias vector of this 8-channel slot (a mask index for power-of-two channel counts was
+      // A/B'd on Mask R-CNN in round 2 and measured no faster, so it was removed)
+      unpack8(reinterpret_cast<const uint4*>(b)[(int)(v % c8)], bb);
 #pragma unroll
       for (int j = 0; j < 8; ++j) x[j] += bb[j];
     }
@@ -111,18 +108,9 @@ MX_EXPORT int mx_bias_act_fwd(void* y, const void* b, const void* res, int64_t M
   if (nvec == 0) return hipSuccess;
   const int64_t want = (nvec + 255) / 256;
   const unsigned grid = (unsigned)(want < 8192 ? want : 8192);
-  // MXTRAIN_EPI_MASK=1: bias index by mask for power-of-two channel counts.  Off by
-  // default until a same-box A/B: the Mask R-CNN runs after the change read 82.8-83.3 /
-  // 161.9 img/s against 83.3-83.5 / 166.7-169.5 before (within the box-to-box spread,
-  // but all on the low side)
-  static const bool use_mask = [] {
-    const char* e = getenv("MXTRAIN_EPI_MASK");
-    return e && e[0] == '1';
-  }();
-  const int c8m = use_mask && ((C / 8) & (C / 8 - 1)) == 0 ? C / 8 - 1 : -1;
 #define MX_BA(R, A)                                                                                        \
   hipLaunchKernelGGL((bias_act_fwd_kernel<R, A>), dim3(grid), dim3(256), 0, s, (uint16_t*)y, (const uint16_t*)b, \
-                     (const uint16_t*)res, nvec, C / 8, c8m)
+                     (const uint16_t*)res, nvec, C / 8)
   if (res) {
     if (relu) MX_BA(true, true); else MX_BA(true, false);
   } else {

@@ -560,7 +560,7 @@ def test_dropmask_layers_match_per_layer_calls(monkeypatch):
 
 
 # ------------------------------------------------------------------ forward / dgrad GEMMs
-NT_VARIANTS = [0, 1, 2, 3, 4, 5, 6]
+NT_VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8]
 
 
 @pytest.mark.parametrize("variant", NT_VARIANTS)
@@ -584,7 +584,7 @@ def test_gemm_nt_forward_epilogues(variant, epi):
         _close(out, ref, 2e-2, 1e-2, "y")
 
 
-@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("gelu", [False, True])
 def test_gemm_nt_dgrad_epilogues(variant, gelu):
     """dgrad dx = dy w (w K-major) and the fused GeLU' + bias-gradient epilogue."""
