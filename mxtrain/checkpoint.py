@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import json
 import os
+import threading
 import time
 from typing import Dict, Optional
 
@@ -71,12 +72,12 @@ def qkv_from_megatron(t: torch.Tensor, hl: int, kvl: int, D: int) -> torch.Tenso
 
 # ---------------------------------------------------------------------- name mapping
 def to_megatron_state(params: Dict[str, torch.Tensor], cfg: GPTConfig, tp: int, pp: int,
-                      pp_rank: int) -> Dict[str, torch.Tensor]:
+                      pp_rank: int, host: bool = True) -> Dict[str, torch.Tensor]:
     l0, _ = stage_layer_range(cfg, pp, pp_rank)
     hl, kvl, D = cfg.num_attention_heads // tp, cfg.num_kv_heads // tp, cfg.head_dim
     out = {}
     for name, t in params.items():
-        t = t.detach().cpu().clone()
+        t = t.detach().cpu().clone() if host else t.detach()
         if name == "wte":
             out["language_model.embedding.word_embeddings.weight"] = t
         elif name == "wpe":
@@ -140,11 +141,11 @@ def _optim_state(opt, sched, partitions):
         "zero_stage": 1, "loss_scaler": None, "dynamic_loss_scale": False, "overflow": False,
         "clip_grad": opt.clip, "partition_count": [partitions],
         "base_optimizer_state": {
-            "state": {0: {"step": opt.step_count, "exp_avg": opt.exp_avg.detach().cpu(),
-                          "exp_avg_sq": opt.exp_avg_sq.detach().cpu()}},
+            "state": {0: {"step": opt.step_count, "exp_avg": opt.exp_avg.detach(),
+                          "exp_avg_sq": opt.exp_avg_sq.detach()}},
             "param_groups": [{"lr": sched(opt.step_count), "betas": list(opt.betas), "eps": opt.eps,
                               "weight_decay": opt.wd, "params": [0]}]},
-        "single_partition_of_fp32_groups": [opt.master.detach().cpu()],
+        "single_partition_of_fp32_groups": [opt.master.detach()],
         "mx_shard_layout": [[int(b.start), int(b.end), int(so), int(n)] for (b, fs, so, n) in opt.slices],
     }
 
@@ -177,22 +178,31 @@ def _atomic_save(obj, path):
     os.replace(tmp, path)
 
 
-def save_checkpoint(save_dir: str, trainer, iteration: int, consumed_samples: int = 0,
-                    args: Optional[dict] = None, ds_config: Optional[dict] = None,
-                    local_leader: Optional[bool] = None) -> str:
-    """Every rank calls this (collective barrier at the end)."""
+def _map_tensors(obj, fn):
+    """obj with every tensor t replaced by fn(t) (dicts / lists / tuples walked)."""
+    if isinstance(obj, torch.Tensor):
+        return fn(obj)
+    if isinstance(obj, dict):
+        return {k: _map_tensors(v, fn) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_map_tensors(v, fn) for v in obj)
+    return obj
+
+
+def _collect(save_dir: str, trainer, iteration: int, consumed_samples: int, args, ds_config):
+    """[(path, state)] of this rank's files for global_step<iteration>; tensors are still the
+    live (device) tensors or fresh device temporaries -- the caller copies them to host."""
     ps = trainer.ps
     trainer.sync_params()
-    tag = f"global_step{iteration}"
-    d = os.path.join(save_dir, tag)
-    os.makedirs(d, exist_ok=True)
+    d = os.path.join(save_dir, f"global_step{iteration}")
     mp = _mp_rank(ps)
     opt = trainer.opt
     sched = opt.schedule
     lr_state = {"max_lr": sched.lr, "min_lr": sched.min_lr, "warmup_steps": sched.warmup,
                 "num_steps": opt.step_count, "decay_steps": sched.decay, "decay_style": sched.style}
+    files = []
     if ps.dp_rank == 0 and ps.cp_rank == 0:
-        module = to_megatron_state(trainer.flat.params, trainer.cfg, ps.tp, ps.pp, ps.pp_rank)
+        module = to_megatron_state(trainer.flat.params, trainer.cfg, ps.tp, ps.pp, ps.pp_rank, host=False)
         state = {
             "module": module, "buffer_names": [], "optimizer": None, "lr_scheduler": lr_state,
             "sparse_tensor_module_names": [], "skipped_steps": 0, "global_steps": iteration,
@@ -200,37 +210,162 @@ def save_checkpoint(save_dir: str, trainer, iteration: int, consumed_samples: in
             "ds_config": ds_config or {}, "ds_version": DS_VERSION, "args": args or {},
             "iteration": iteration, "checkpoint_version": 3.0,
             "rng_state": [{"torch_rng_state": torch.get_rng_state(),
-                           "mx_dropout_seed": trainer.seed.t.detach().cpu().clone()}],
+                           "mx_dropout_seed": trainer.seed.t.detach()}],
             "mx_config": trainer.cfg.__dict__.copy(),
         }
-        _atomic_save(state, os.path.join(d, f"mp_rank_{mp:02d}_model_states.pt"))
+        files.append((os.path.join(d, f"mp_rank_{mp:02d}_model_states.pt"), state))
     optim = {"optimizer_state_dict": _optim_state(opt, sched, ps.grad_world),
              "ds_config": ds_config or {}, "ds_version": DS_VERSION}
-    _atomic_save(optim, os.path.join(d, f"zero_pp_rank_{_grad_rank(ps)}_mp_rank_{mp:02d}_optim_states.pt"))
+    files.append((os.path.join(d, f"zero_pp_rank_{_grad_rank(ps)}_mp_rank_{mp:02d}_optim_states.pt"), optim))
     if trainer.eflat is not None:
         eo = trainer.eopt
         edp_rank = _grad_rank(ps) // trainer.tcfg.moe_expert_parallel_size
         if edp_rank == 0:   # one replica of each expert set writes the expert files
-            files: Dict[str, Dict[str, torch.Tensor]] = {}
+            ef: Dict[str, Dict[str, torch.Tensor]] = {}
             for path, key, name, j in _expert_files(trainer, d, mp):
-                files.setdefault(path, {})[key] = trainer.eflat.params[name][j].detach().cpu().clone()
-            for path, sd_e in files.items():
-                _atomic_save(sd_e, path)
-        _atomic_save({"optimizer_state_dict": _optim_state(eo, sched, eo.world), "ds_version": DS_VERSION},
-                     os.path.join(d, f"expp_rank_{trainer.ep_rank}_zero_pp_rank_{edp_rank}"
-                                     f"_mp_rank_{mp:02d}_optim_states.pt"))
+                ef.setdefault(path, {})[key] = trainer.eflat.params[name][j].detach()
+            files.extend(ef.items())
+        files.append((os.path.join(d, f"expp_rank_{trainer.ep_rank}_zero_pp_rank_{edp_rank}"
+                                      f"_mp_rank_{mp:02d}_optim_states.pt"),
+                      {"optimizer_state_dict": _optim_state(eo, sched, eo.world), "ds_version": DS_VERSION}))
+    return d, files
+
+
+def _commit(save_dir: str, iteration: int, local_leader: Optional[bool]):
+    """Point `latest` at global_step<iteration> once EVERY rank's files are on disk
+    (collective: a barrier before the leader writes, one after)."""
     if dist.is_initialized():
         dist.barrier()
     if local_leader is None:
         local_leader = int(os.environ.get("LOCAL_RANK", "0")) == 0
     if local_leader:
-        with open(os.path.join(save_dir, "latest"), "w") as f:
-            f.write(tag)
-        with open(os.path.join(save_dir, "latest_checkpointed_iteration.txt"), "w") as f:
-            f.write(str(iteration))
+        for name, text in (("latest", f"global_step{iteration}"), ("latest_checkpointed_iteration.txt", str(iteration))):
+            tmp = os.path.join(save_dir, f".{name}.tmp{os.getpid()}")
+            with open(tmp, "w") as f:
+                f.write(text)
+            os.replace(tmp, os.path.join(save_dir, name))
     if dist.is_initialized():
         dist.barrier()
+
+
+def save_checkpoint(save_dir: str, trainer, iteration: int, consumed_samples: int = 0,
+                    args: Optional[dict] = None, ds_config: Optional[dict] = None,
+                    local_leader: Optional[bool] = None) -> str:
+    """Synchronous save.  Every rank calls this (collective barrier at the end)."""
+    d, files = _collect(save_dir, trainer, iteration, consumed_samples, args, ds_config)
+    os.makedirs(d, exist_ok=True)
+    for path, state in files:
+        _atomic_save(_map_tensors(state, lambda t: t.detach().cpu().clone()), path)
+    _commit(save_dir, iteration, local_leader)
     return d
+
+
+class AsyncCheckpointer:
+    """Checkpoint writes that overlap training (the reference's Megatron-
+    DeepSpeed image pulls DeepSpeed async-IO for this, containers/megatron-deepspeed/
+    Dockerfile:12,16, and saves every --save-interval, examples/megatron-deepspeed/
+    gpt2_345m/pretrain-ddp-zero1.yaml:55,83).
+
+    ``save()`` snapshots this rank's model / ZeRO-shard tensors into pinned host buffers
+    with device-to-host copies on a side HIP stream (the copy engines, no CU time), then a
+    background thread serialises them in the unchanged DeepSpeed layout.  The host returns
+    immediately; the GPU only waits for the snapshot copies before the next optimizer
+    update touches the parameters / fp32 master / moments (``fence()``, called by the
+    trainer).  ``latest`` is advanced by ``wait()`` -- at the next save or at the end of
+    training -- after a barrier, so it never names a checkpoint some rank has not
+    finished.  Pinned buffers are allocated on the first save and reused (the ZeRO shard of
+    GPT-3 6.7B at DP 8 is ~13 GB; re-pinning per save would cost more than the copy)."""
+
+    def __init__(self, trainer):
+        self.trainer = trainer
+        self.device = trainer.device
+        self._cuda = self.device.type == "cuda"
+        self._stream = torch.cuda.Stream(device=self.device) if self._cuda else None
+        self._host: Dict[int, torch.Tensor] = {}
+        self._thread: Optional[threading.Thread] = None
+        self._err: Optional[BaseException] = None
+        self._commit_args = None
+        self._event = None
+        self.last_snapshot_s = 0.0
+        self.last_write_s = 0.0
+
+    # ---------------------------------------------------------------- snapshot
+    def _host_copy(self, slot: int, t: torch.Tensor) -> torch.Tensor:
+        t = t.detach()
+        if not t.is_cuda:
+            return t.clone()
+        h = self._host.get(slot)
+        if h is None or h.shape != t.shape or h.dtype != t.dtype:
+            h = self._host[slot] = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        src = t if t.is_contiguous() else t.contiguous()
+        src.record_stream(self._stream)
+        h.copy_(src, non_blocking=True)
+        return h
+
+    def save(self, save_dir: str, iteration: int, consumed_samples: int = 0, args: Optional[dict] = None,
+             ds_config: Optional[dict] = None, local_leader: Optional[bool] = None) -> str:
+        self.wait()
+        t0 = time.time()
+        d, files = _collect(save_dir, self.trainer, iteration, consumed_samples, args, ds_config)
+        os.makedirs(d, exist_ok=True)
+        counter = [0]
+
+        def copy(t):
+            counter[0] += 1
+            return self._host_copy(counter[0], t)
+
+        if self._cuda:
+            main = torch.cuda.current_stream(self.device)
+            self._stream.wait_stream(main)
+            with torch.cuda.stream(self._stream):
+                host_files = [(p, _map_tensors(s, copy)) for p, s in files]
+                self._event = torch.cuda.Event()
+                self._event.record(self._stream)
+        else:
+            host_files = [(p, _map_tensors(s, copy)) for p, s in files]
+            self._event = None
+        self.last_snapshot_s = time.time() - t0
+        self._commit_args = (save_dir, iteration, local_leader)
+        self._err = None
+        self._thread = threading.Thread(target=self._write, args=(host_files, self._event), daemon=True,
+                                        name=f"mx-ckpt-{iteration}")
+        self._thread.start()
+        return d
+
+    def _write(self, host_files, event):
+        t0 = time.time()
+        try:
+            if event is not None:
+                event.synchronize()
+            for path, state in host_files:
+                _atomic_save(state, path)
+        except BaseException as e:  # surfaced by wait() on the training thread
+            self._err = e
+        self.last_write_s = time.time() - t0
+
+    def fence(self):
+        """Make the current stream wait for the snapshot copies (before anything writes the
+        parameters or optimizer state again).  Host never blocks; no-op without a save."""
+        if self._event is not None and self._cuda:
+            torch.cuda.current_stream(self.device).wait_event(self._event)
+            self._event = None
+
+    @property
+    def pending(self) -> bool:
+        return self._thread is not None
+
+    def wait(self):
+        """Finish the in-flight write (if any) and advance `latest` to it (collective)."""
+        if self._thread is None:
+            return
+        self._thread.join()
+        self._thread = None
+        if self._err is not None:
+            err, self._err = self._err, None
+            raise RuntimeError(f"async checkpoint write failed: {err!r}") from err
+        save_dir, iteration, leader = self._commit_args
+        self._commit_args = None
+        _commit(save_dir, iteration, leader)
 
 
 def latest_iteration(load_dir: str) -> Optional[int]:

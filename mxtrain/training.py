@@ -123,6 +123,9 @@ class GPTTrainer:
         self.iteration = 0
         self._graph = None
         self._static = None
+        # checkpoint.AsyncCheckpointer.fence: makes the stream wait for an in-flight
+        # checkpoint snapshot before the optimizer rewrites what it is copying
+        self.ckpt_fence = None
 
     # ------------------------------------------------------------------ init
     @staticmethod
@@ -225,6 +228,8 @@ class GPTTrainer:
             for o in self._opts:
                 o.step_count += 1   # bias corrections use the new step, as in eager step()
                 o.set_hyper(o.schedule(o.step_count))
+            if self.ckpt_fence is not None:
+                self.ckpt_fence()
             self._graph.replay()
             # the replay left this step's update un-gathered (the next replay's body, or a
             # sync_params(), gathers it; re-gathering an unchanged shard is idempotent)
@@ -256,6 +261,8 @@ class GPTTrainer:
 
     def _train_step_eager(self, tokens, labels):
         nm, B, S = tokens.shape
+        if self.ckpt_fence is not None and any(o.overlap_update or o.overlap_param_gather for o in self._opts):
+            self.ckpt_fence()   # the deferred update / parameter gather runs at the step's start
         self._prepare_step(nm, B, S)
         if self.pipeline is not None:
             loss = self.pipeline.run(tokens, labels)
@@ -267,6 +274,8 @@ class GPTTrainer:
                                                            m == nm - 1, m == 0, micro=m)
         if self.stage.rt.colq is not None:
             self.stage.rt.colq.flush()
+        if self.ckpt_fence is not None:
+            self.ckpt_fence()
         if self.eopt is not None:
             from .parallel.zero import joint_step
             joint_step(self._opts)

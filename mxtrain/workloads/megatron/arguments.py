@@ -147,6 +147,8 @@ def build_parser() -> argparse.ArgumentParser:
     a("--mx-metrics-dir", default=None, help="per-rank JSONL metrics (default $LOGS_DIR or $HOME/logs)")
     a("--mx-watchdog", type=float, default=0.0, help="abort a rank after N s without progress")
     a("--mx-auto-resume", action="store_true", help="--load from --save if a checkpoint exists")
+    a("--async-save", "--mx-async-save", dest="async_save", action="store_true",
+      help="checkpoint writes overlap training (pinned snapshot + writer thread; checkpoint.AsyncCheckpointer)")
     a("--mx-profile", action="store_true", help="torch.profiler trace of steps 5-7 into <metrics>/profile")
     for f in IGNORED_FLAGS:
         p.add_argument(f, action="store_true", help=argparse.SUPPRESS)

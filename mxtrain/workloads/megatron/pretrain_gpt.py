@@ -36,7 +36,7 @@ def print_rank_0(*a):
 
 def main(argv=None):
     args = parse_args(argv)
-    from mxtrain.checkpoint import latest_iteration, load_checkpoint, save_checkpoint
+    from mxtrain.checkpoint import AsyncCheckpointer, latest_iteration, load_checkpoint, save_checkpoint
     from mxtrain.data.gpt_dataset import DistributedSampleLoader, build_train_valid_test
     from mxtrain.models.gpt import GPTConfig
     from mxtrain.obs.fault import FaultInjector, Watchdog
@@ -147,6 +147,21 @@ def main(argv=None):
                             mode="torch" if args.mx_profile else None)
     debug_finite = check_finite_enabled()
 
+    # ---------------------------------------------------------------- checkpoint writer
+    ackpt = None
+    if args.save and args.async_save:
+        ackpt = AsyncCheckpointer(trainer)
+        trainer.ckpt_fence = ackpt.fence
+
+    def save(it):
+        if ackpt is not None:
+            ackpt.save(args.save, it, loader.consumed, args=_plain(vars(args)), ds_config=args.ds_config)
+            print_rank_0(f"  checkpoint at iteration {it:7d} snapshotted in {ackpt.last_snapshot_s:.2f}s, "
+                         f"writing to {args.save} in the background")
+        else:
+            save_checkpoint(args.save, trainer, it, loader.consumed, args=_plain(vars(args)), ds_config=args.ds_config)
+            print_rank_0(f"  successfully saved checkpoint at iteration {it:7d} to {args.save}")
+
     # ---------------------------------------------------------------- train loop
     it = trainer.iteration
     flops_tok = cfg.flops_per_token()
@@ -205,16 +220,18 @@ def main(argv=None):
             evaluate(trainer, valid_loader, args.eval_iters, to_device, ps, it, metrics, "validation")
             t_log = time.time()
         if args.save and args.save_interval and it % args.save_interval == 0:
-            save_checkpoint(args.save, trainer, it, loader.consumed, args=_plain(vars(args)), ds_config=args.ds_config)
-            print_rank_0(f"  successfully saved checkpoint at iteration {it:7d} to {args.save}")
+            save(it)
             t_log = time.time()
         if args.exit_interval and it % args.exit_interval == 0:
             break
         if args.exit_duration_in_mins and (time.time() - start_wall) / 60 > args.exit_duration_in_mins:
             break
     if args.save and (not args.save_interval or it % args.save_interval != 0):
-        save_checkpoint(args.save, trainer, it, loader.consumed, args=_plain(vars(args)), ds_config=args.ds_config)
-        print_rank_0(f"  successfully saved checkpoint at iteration {it:7d} to {args.save}")
+        save(it)
+    if ackpt is not None:
+        ackpt.wait()
+        print_rank_0(f"  successfully saved checkpoint at iteration {it:7d} to {args.save} "
+                     f"(last background write {ackpt.last_write_s:.2f}s)")
     if test_ds is not None and args.eval_iters:
         test_loader = DistributedSampleLoader(test_ds, args.micro_batch_size, gb, ps.dp_rank, ps.dp)
         evaluate(trainer, test_loader, args.eval_iters, to_device, ps, it, metrics, "test")

@@ -157,6 +157,73 @@ def test_pretrain_resume_is_exact(tmp_path, monkeypatch):
     assert any("--fp16 -> bf16" in d for d in a["args"]["mx_deviations"])
 
 
+def test_async_save_resume_is_exact(tmp_path, monkeypatch):
+    """--async-save: snapshots + background writes every --save-interval; `latest` only
+    ever names a finished checkpoint; resuming from the async checkpoint reproduces the
+    synchronous run bit for bit."""
+    monkeypatch.setenv("MXTRAIN_CPU_ONLY", "1")
+    ds = tmp_path / "ds.json"
+    ds.write_text(json.dumps({"zero_optimization": {"stage": 1}, "train_micro_batch_size_per_gpu": 2,
+                              "gradient_accumulation_steps": 2}))
+    base = TINY + ["--deepspeed", "--deepspeed_config", str(ds), "--lr-decay-iters", "8",
+                   "--mx-metrics-dir", str(tmp_path / "logs")]
+    assert _run_pretrain(base + ["--train-iters", "8", "--save", str(tmp_path / "s")]) == 0
+    assert _run_pretrain(base + ["--train-iters", "4", "--save-interval", "2", "--async-save",
+                                 "--save", str(tmp_path / "a")]) == 0
+    assert open(tmp_path / "a" / "latest").read() == "global_step4"
+    assert sorted(os.listdir(tmp_path / "a" / "global_step2")) == sorted(os.listdir(tmp_path / "a" / "global_step4"))
+    assert not [f for f in os.listdir(tmp_path / "a" / "global_step4") if ".tmp" in f]
+    assert _run_pretrain(base + ["--train-iters", "8", "--async-save", "--save", str(tmp_path / "a"),
+                                 "--load", str(tmp_path / "a")]) == 0
+    assert open(tmp_path / "a" / "latest_checkpointed_iteration.txt").read() == "8"
+    for name in ("mp_rank_00_model_states.pt", "zero_pp_rank_0_mp_rank_00_optim_states.pt"):
+        s = torch.load(tmp_path / "s" / "global_step8" / name, weights_only=True)
+        a = torch.load(tmp_path / "a" / "global_step8" / name, weights_only=True)
+        if "module" in s:
+            for k in s["module"]:
+                torch.testing.assert_close(s["module"][k], a["module"][k], rtol=0, atol=0, msg=k)
+        else:
+            so, ao = s["optimizer_state_dict"], a["optimizer_state_dict"]
+            torch.testing.assert_close(so["single_partition_of_fp32_groups"][0],
+                                       ao["single_partition_of_fp32_groups"][0], rtol=0, atol=0)
+            torch.testing.assert_close(so["base_optimizer_state"]["state"][0]["exp_avg_sq"],
+                                       ao["base_optimizer_state"]["state"][0]["exp_avg_sq"], rtol=0, atol=0)
+
+
+def test_async_checkpointer_snapshot_is_isolated(tmp_path):
+    """The snapshot holds the values at save() time even when training mutates the
+    parameters before the background write runs; a write error surfaces in wait()."""
+    from mxtrain.checkpoint import AsyncCheckpointer
+    from mxtrain.models.gpt import GPTConfig
+    from mxtrain.parallel.state import ParallelState
+    from mxtrain.training import GPTTrainer, TrainConfig, synthetic_batch
+    cfg = GPTConfig(num_layers=2, hidden_size=32, num_attention_heads=4, seq_length=16,
+                    max_position_embeddings=16, vocab_size=64)
+    tr = GPTTrainer(cfg, TrainConfig(micro_batch_size=2), ParallelState())
+    tok, lab = synthetic_batch(cfg, 1, 2, "cpu", torch.Generator().manual_seed(0))
+    tr.train_step(tok, lab)
+    ck = AsyncCheckpointer(tr)
+    tr.ckpt_fence = ck.fence
+    before = {k: v.clone() for k, v in tr.flat.params.items()}
+    master = tr.opt.master.clone()
+    ck.save(str(tmp_path), 1)
+    tr.train_step(tok, lab)   # mutates params / master while the writer may still be running
+    ck.wait()
+    assert open(tmp_path / "latest").read() == "global_step1"
+    m = torch.load(tmp_path / "global_step1" / "mp_rank_00_model_states.pt", weights_only=True)["module"]
+    torch.testing.assert_close(m["language_model.embedding.word_embeddings.weight"], before["wte"], rtol=0, atol=0)
+    o = torch.load(tmp_path / "global_step1" / "zero_pp_rank_0_mp_rank_00_optim_states.pt", weights_only=True)
+    torch.testing.assert_close(o["optimizer_state_dict"]["single_partition_of_fp32_groups"][0], master,
+                               rtol=0, atol=0)
+    assert not torch.equal(tr.flat.params["wte"], before["wte"])
+    # a failing write (target is a file, not a directory) is raised on the training thread
+    bad = tmp_path / "notadir"
+    bad.write_text("x")
+    with pytest.raises(Exception):
+        ck.save(str(bad), 2)
+        ck.wait()
+
+
 def test_qkv_megatron_interleave_roundtrip():
     from mxtrain.checkpoint import qkv_from_megatron, qkv_to_megatron
     for hl, kvl in ((4, 4), (4, 2), (8, 1)):
