@@ -99,18 +99,22 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x, uint32_t seed) {
   x ^= x >> 16;
   return x;
 }
-// keep-probability test: returns true when the element is kept
-__device__ __forceinline__ bool dropout_keep(uint64_t idx, uint32_t seed, uint32_t thresh) {
-  uint32_t h = hash32((uint32_t)idx ^ (uint32_t)(idx >> 32) * 0x85ebca6bu, seed);
-  return h >= thresh;  // thresh = p * 2^32
-}
-// keep flags of the 8 elements idx0 .. idx0 + 7, idx0 % 8 == 0: bit-identical to
-// dropout_keep, with the high word's multiply done once (the 8 indices share it)
+// Keep flags of the 8 elements idx0 .. idx0 + 7 (idx0 % 8 == 0), thresh = p * 2^32 (> 0).
+// ONE hash per 8-element group seeds an xorshift32 stream: x0 = hash32(group ^ hi, seed) | 1
+// (never the all-zero fixed point), x_{j+1} = xorshift(x_j); x_j's low / high 16 bits are the
+// draws of elements 2j / 2j + 1, kept when >= round(p * 2^16).  (8 full hashes per group --
+// 16 quarter-rate multiplies -- made the LN backward VALU-bound; ops/rng.py keep_mask is the
+// bit-identical reference.)
 __device__ __forceinline__ void dropout_keep8(uint64_t idx0, uint32_t seed, uint32_t thresh, bool (&k)[8]) {
-  const uint32_t hi = (uint32_t)(idx0 >> 32) * 0x85ebca6bu;
-  const uint32_t lo = (uint32_t)idx0;
+  const uint32_t g = (uint32_t)(idx0 >> 3) ^ (uint32_t)(idx0 >> 35) * 0x85ebca6bu;
+  const uint32_t thr = (uint32_t)(((uint64_t)thresh + 0x8000u) >> 16);
+  uint32_t x = hash32(g, seed) | 1u;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) k[j] = hash32((lo + j) ^ hi, seed) >= thresh;
+  for (int j = 0; j < 4; ++j) {
+    if (j) { x ^= x << 13; x ^= x >> 17; x ^= x << 5; }
+    k[2 * j] = (x & 0xFFFFu) >= thr;
+    k[2 * j + 1] = (x >> 16) >= thr;
+  }
 }
 
 // tanh-approximation GeLU (Megatron bias_gelu / HF "gelu_new") in its sigmoid form:

@@ -93,6 +93,28 @@ __global__ __launch_bounds__(256) void grad_in_kernel(const int64_t* __restrict_
   if (threadIdx.x == 0) partial[b] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// data-parallel: G (all-reduced sum over ranks) *= scale (1 / world), partial[b] = sum g^2 of
+// the block's CH elements (n a multiple of 8, G 32-B aligned)
+__global__ __launch_bounds__(256) void scale_sumsq_kernel(float* __restrict__ G, int64_t n, float scale,
+                                                          float* __restrict__ partial) {
+  __shared__ float red[4];
+  const int64_t e0 = (int64_t)blockIdx.x * CH + threadIdx.x * 8;
+  float acc = 0.f;
+  if (e0 < n) {
+    float4* g = reinterpret_cast<float4*>(G + e0);
+    float4 a = g[0], b = g[1];
+    a.x *= scale; a.y *= scale; a.z *= scale; a.w *= scale;
+    b.x *= scale; b.y *= scale; b.z *= scale; b.w *= scale;
+    g[0] = a;
+    g[1] = b;
+    acc = (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w) + (b.x * b.x + b.y * b.y) + (b.z * b.z + b.w * b.w);
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 __global__ __launch_bounds__(256) void sumsq_fin_kernel(const float* __restrict__ partial, int n,
                                                         float* __restrict__ out) {
   __shared__ float red[4];
@@ -182,18 +204,35 @@ __global__ __launch_bounds__(256) void update_kernel(const int64_t* __restrict__
 MX_EXPORT int mx_mt_chunk() { return CH; }
 MX_EXPORT int mx_mt_max_tensors() { return MAXT; }
 
-// src: host array of T bf16 gradient pointers (tensor order of the table); nblocks = total
-// blocks (bstart[T]); partial: nblocks floats.
-MX_EXPORT int mx_mt_grad_in(const int64_t* tab, const int* bmap, const int* bstart, const int* bstart_host, int T,
-                            const int64_t* src, float* G, float* partial, hipStream_t s) {
-  for (int t0 = 0; t0 < T; t0 += MAXT) {
-    const int t1 = min(T, t0 + MAXT);
+// Tensors [tb, te) of the table (a data-parallel bucket, or all of them): src = host array of
+// their te - tb bf16 gradient pointers; partial: the blocks' sum-of-squares slots
+// (partial[bstart[t] ..] for tensor t).
+MX_EXPORT int mx_mt_grad_in_range(const int64_t* tab, const int* bmap, const int* bstart, const int* bstart_host,
+                                  int tb, int te, const int64_t* src, float* G, float* partial, hipStream_t s) {
+  for (int t0 = tb; t0 < te; t0 += MAXT) {
+    const int t1 = min(te, t0 + MAXT);
     Ptrs ptrs{};
-    for (int t = t0; t < t1; ++t) ptrs.p[t - t0] = reinterpret_cast<const void*>(src[t]);
+    for (int t = t0; t < t1; ++t) ptrs.p[t - t0] = reinterpret_cast<const void*>(src[t - tb]);
     const int b0 = bstart_host[t0], nb = bstart_host[t1] - b0;
     if (nb > 0)
       hipLaunchKernelGGL(grad_in_kernel, dim3(nb), dim3(256), 0, s, tab, bmap, bstart, t0, b0, ptrs, G, partial);
   }
+  return hipGetLastError();
+}
+
+// src: host array of T bf16 gradient pointers (tensor order of the table); nblocks = total
+// blocks (bstart[T]); partial: nblocks floats.
+MX_EXPORT int mx_mt_grad_in(const int64_t* tab, const int* bmap, const int* bstart, const int* bstart_host, int T,
+                            const int64_t* src, float* G, float* partial, hipStream_t s) {
+  return mx_mt_grad_in_range(tab, bmap, bstart, bstart_host, 0, T, src, G, partial, s);
+}
+
+// G[0, n) *= scale with per-2048-element sum-of-squares partials (ceil(n / 2048) of them);
+// n a multiple of 8, G 32-B aligned
+MX_EXPORT int mx_mt_scale_sumsq(float* G, int64_t n, float scale, float* partial, hipStream_t s) {
+  if (n <= 0 || (n & 7) || ((uintptr_t)G & 31)) return (int)hipErrorInvalidValue;
+  const int64_t nb = (n + CH - 1) / CH;
+  hipLaunchKernelGGL(scale_sumsq_kernel, dim3((unsigned)nb), dim3(256), 0, s, G, n, scale, partial);
   return hipGetLastError();
 }
 

@@ -133,20 +133,26 @@ def _align8(n: int) -> int:
     return (n + 7) // 8 * 8
 
 
+def _align(n: int, a: int) -> int:
+    return (n + a - 1) // a * a
+
+
 class _FlatCast(torch.autograd.Function):
-    """Forward: the FlatMaster's persistent compute copies (refreshed by the optimizer
-    pass, re-cast only when stale); backward: every gradient into the flat fp32 buffer in
-    one launch (returned as views of it)."""
+    """Forward: the FlatMaster's persistent compute copies of one bucket (refreshed by the
+    optimizer pass, re-cast only when stale); backward: the bucket's gradients into the flat
+    fp32 buffer in one launch (returned as views of it) -- and, data-parallel, that slice's
+    all-reduce is started right away, while backward continues with earlier layers."""
 
     @staticmethod
-    def forward(ctx, fm, *params):
-        ctx.fm = fm
+    def forward(ctx, fm, k, *params):
+        ctx.fm, ctx.k = fm, k
         fm.ensure_fresh()
-        return tuple(fm.compute_views())
+        tb, te = fm.buckets[k][:2]
+        return tuple(fm.compute_views()[tb:te])
 
     @staticmethod
     def backward(ctx, *grads):
-        return (None, *ctx.fm.grads_in(grads))
+        return (None, None, *ctx.fm.grads_in(grads, ctx.k))
 
 
 class FlatMaster:
@@ -165,30 +171,62 @@ class FlatMaster:
     are unchanged (call ``rebind_state()`` after ``opt.load_state_dict``).  Parameters
     become views of the flat buffer (``p.data``), so in-place writes (checkpoint load)
     land in it and bump the versions that mark the copies stale.
+
+    Data parallel (``group`` with world > 1; the reference's Horovod Mask R-CNN runs,
+    examples/maskrcnn/train-maskrcnn-tensorpack.yaml:34, mpijob-horovod values.yaml:64-66):
+    parameters are laid out in model order and cut into ~``bucket_bytes`` buckets, one
+    autograd node each.  When backward has produced a bucket's gradients (the heads first,
+    the backbone stem last) its flat fp32 slice is all-reduced at once -- RCCL
+    asynchronously, or the direct xGMI kernel (parallel/xgmi.py, MXTRAIN_XGMI) on a side
+    stream -- in a fixed bucket order on every rank.  ``step()`` joins them, averages and
+    takes ||g||^2 of the averaged gradient in one pass (clip as Horovod + clip_grad_norm_),
+    then runs the same fused clip + SGD launch.  Every piece is capturable, so the whole
+    data-parallel step can be one hipGraph.
     """
 
-    def __init__(self, model, opt: torch.optim.SGD, clip: float, dt: torch.dtype = torch.bfloat16):
+    def __init__(self, model, opt: torch.optim.SGD, clip: float, dt: torch.dtype = torch.bfloat16,
+                 group=None, bucket_bytes: int = 32 << 20):
         from ..ops import _lib
         self.model, self.opt, self.dt = model, opt, dt
         mom = {g["momentum"] for g in opt.param_groups}
         wds = {float(g["weight_decay"]) for g in opt.param_groups} - {0.0}
         assert len(mom) == 1 and len(wds) <= 1, "one momentum and one non-zero weight decay"
         assert all(not g.get("nesterov") and not g.get("dampening") for g in opt.param_groups)
+        import torch.distributed as dist
+        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.group = group
         self.params, wdf = [], []
         for g in opt.param_groups:
             for p in g["params"]:
                 if p.requires_grad:
                     self.params.append(p)
                     wdf.append(1 if g["weight_decay"] else 0)
+        if self.world > 1:
+            # model order: backward finishes the last modules' gradients first
+            order = {id(p): i for i, p in enumerate(model.parameters())}
+            pairs = sorted(zip(self.params, wdf), key=lambda pw: order.get(id(pw[0]), len(order)))
+            self.params, wdf = [p for p, _ in pairs], [w for _, w in pairs]
         dev = self.params[0].device
         self.device = dev
         self.cuda = dev.type == "cuda"
         self.chunk = _lib.query("mx_mt_chunk") if self.cuda else 2048
         self.sizes = [p.numel() for p in self.params]
+        # buckets (tensor range, flat element range); bucket slices start 64-element
+        # (256-B) aligned so every all-reduce message divides over 8 ranks in 16-B units
         self.offs, off = [], 0
-        for n in self.sizes:
+        self.buckets: List[Tuple[int, int, int, int]] = []
+        cap = max(1, bucket_bytes // 4) if self.world > 1 else None
+        tb, e0 = 0, 0
+        for t, n in enumerate(self.sizes):
             self.offs.append(off)
             off += _align8(n)
+            if cap is not None and off - e0 >= cap and t + 1 < len(self.sizes):
+                off = _align(off, 64)
+                self.buckets.append((tb, t + 1, e0, off))
+                tb, e0 = t + 1, off
+        if cap is not None:
+            off = _align(max(off, 8), 64)
+        self.buckets.append((tb, len(self.sizes), e0, max(off, 8)))
         total = max(off, 8)
         self.P = torch.zeros(total, dtype=torch.float32, device=dev)
         self.G = torch.zeros(total, dtype=torch.float32, device=dev)
@@ -227,10 +265,15 @@ class FlatMaster:
         self.hyper[3] = float(clip or 0.0)
         self.lr = self.hyper[0:1].view(())   # device scalar: fill_ before a (graph) step
         self.normsq = torch.zeros(1, dtype=torch.float32, device=dev)
-        self.partial = torch.zeros(max(self.nblocks, 1), dtype=torch.float32, device=dev)
+        self.partial = torch.zeros(max(self.nblocks, (total + self.chunk - 1) // self.chunk, 1), dtype=torch.float32,
+                                   device=dev)
         self.zero_bf16 = torch.zeros(_align8(max(self.sizes)), dtype=dt, device=dev)
         self._wkey = None
         self._cw_specs = None
+        self._dp_stream = torch.cuda.Stream(device=dev) if (self.cuda and self.world > 1) else None
+        self.dp_route = None     # route of the last bucket reduced: "xgmi" / "rccl" / "gloo"
+        self.dp_routes = set()   # every route used so far
+        self._dp_reset()
 
     # -------------------------------------------------------------- optimizer state
     def rebind_state(self) -> None:
@@ -304,7 +347,10 @@ class FlatMaster:
         class _Ctx:
             def __enter__(self_):
                 if torch.is_grad_enabled():
-                    outs = _FlatCast.apply(fm, *fm.params)
+                    fm._dp_reset()
+                    outs = []
+                    for k, (tb, te, _, _) in enumerate(fm.buckets):
+                        outs.extend(_FlatCast.apply(fm, k, *fm.params[tb:te]))
                 else:
                     fm.ensure_fresh()
                     outs = fm.compute_views()
@@ -319,10 +365,13 @@ class FlatMaster:
         return _Ctx()
 
     # -------------------------------------------------------------- backward / step
-    def grads_in(self, grads) -> List[torch.Tensor]:
+    def grads_in(self, grads, k: int = 0) -> List[torch.Tensor]:
+        """Gradients of bucket k's compute copies (bf16, copy layout; None = no gradient)
+        -> its slice of the flat fp32 buffer (x fold scale), with sum-of-squares partials."""
+        tb, te, _, _ = self.buckets[k]
         srcs = []
         keep = []
-        for t, (g, p) in enumerate(zip(grads, self.params)):
+        for t, g in zip(range(tb, te), grads):
             d0, d1, inner, cl = self.geo[t]
             if g is None:
                 srcs.append(None)
@@ -342,29 +391,96 @@ class FlatMaster:
             from ..ops import _lib
             ptrs = [(s.data_ptr() if s is not None else self.zero_bf16.data_ptr()) for s in srcs]
             arr = ctypes_int64_array(ptrs)
-            _lib.call("mx_mt_grad_in", self.tab.data_ptr(), self.bmap.data_ptr(), self.bstart.data_ptr(),
-                      self.bstart_c, len(ptrs), ctypes.addressof(arr), self.G.data_ptr(), self.partial.data_ptr(),
+            _lib.call("mx_mt_grad_in_range", self.tab.data_ptr(), self.bmap.data_ptr(), self.bstart.data_ptr(),
+                      self.bstart_c, tb, te, ctypes.addressof(arr), self.G.data_ptr(), self.partial.data_ptr(),
                       _lib.stream())
-            _lib.call("mx_mt_sumsq_fin", self.partial.data_ptr(), self.nblocks, self.normsq.data_ptr(),
-                      _lib.stream())
+            if self.world == 1:
+                _lib.call("mx_mt_sumsq_fin", self.partial.data_ptr(), self.nblocks, self.normsq.data_ptr(),
+                          _lib.stream())
         else:
             with torch.no_grad():
                 acc = torch.zeros((), dtype=torch.float32)
-                for t, (s, p) in enumerate(zip(srcs, self.params)):
+                for t, s in zip(range(tb, te), srcs):
+                    p = self.params[t]
                     o, n = self.offs[t], self.sizes[t]
                     gv = torch.zeros(p.shape) if s is None else s.float()
                     if self.scales[t] is not None:
                         gv = gv * self.scales[t].view(-1, *([1] * (p.dim() - 1)))
                     self.G[o:o + n].copy_(gv.reshape(-1) if gv.is_contiguous() else gv.contiguous().reshape(-1))
                     acc = acc + gv.pow(2).sum()
-                self.normsq.fill_(float(acc))
-        return [self.G[o:o + n].view(p.shape) for p, o, n in zip(self.params, self.offs, self.sizes)]
+                if self.world == 1:
+                    self.normsq.fill_(float(acc))
+        if self.world > 1:
+            self._dp_ready(k)
+        return [self.G[self.offs[t]:self.offs[t] + self.sizes[t]].view(self.params[t].shape) for t in range(tb, te)]
+
+    # -------------------------------------------------------------- data parallel
+    def _dp_reset(self) -> None:
+        self._ready = set()
+        self._next = len(self.buckets) - 1   # buckets are reduced last-to-first on every rank
+        self._works = []
+        self._side_used = False
+
+    def _dp_ready(self, k: int) -> None:
+        self._ready.add(k)
+        while self._next >= 0 and self._next in self._ready:
+            self._reduce_bucket(self._next)
+            self._next -= 1
+
+    def _reduce_bucket(self, k: int) -> None:
+        import torch.distributed as dist
+        _, _, e0, e1 = self.buckets[k]
+        seg = self.G[e0:e1]
+        if self.cuda:
+            from ..parallel import xgmi
+            comm = xgmi.route(self.group, seg, "all_reduce", seg.numel() * 4)
+            if comm is not None:
+                cur = torch.cuda.current_stream(self.device)
+                self._dp_stream.wait_stream(cur)
+                with torch.cuda.stream(self._dp_stream):
+                    comm.all_reduce_(seg)
+                self._side_used = True
+                self.dp_route = "xgmi"
+                self.dp_routes.add("xgmi")
+                return
+        self._works.append(dist.all_reduce(seg, group=self.group, async_op=True))
+        self.dp_route = "rccl" if self.cuda else "gloo"
+        self.dp_routes.add(self.dp_route)
+
+    def finish_grads(self) -> None:
+        """Data parallel: make sure every bucket was reduced (a bucket whose parameters
+        got no gradient at all still contributes zeros), join the reductions, average and
+        take ||g||^2 of the averaged gradient."""
+        if self.world == 1:
+            return
+        for k in range(self._next, -1, -1):
+            if k not in self._ready:
+                tb, te, _, _ = self.buckets[k]
+                self.grads_in([None] * (te - tb), k)
+        for w in self._works:
+            w.wait()
+        if self._side_used:
+            torch.cuda.current_stream(self.device).wait_stream(self._dp_stream)
+        if self.cuda:
+            from ..ops import _lib
+            n = self.buckets[-1][3]
+            nparts = (n + self.chunk - 1) // self.chunk
+            assert nparts <= self.partial.numel()
+            _lib.call("mx_mt_scale_sumsq", self.G.data_ptr(), n, 1.0 / self.world, self.partial.data_ptr(),
+                      _lib.stream())
+            _lib.call("mx_mt_sumsq_fin", self.partial.data_ptr(), nparts, self.normsq.data_ptr(), _lib.stream())
+        else:
+            with torch.no_grad():
+                self.G.mul_(1.0 / self.world)
+                self.normsq.fill_(float(self.G.double().pow(2).sum()))
+        self._dp_reset()
 
     def step(self, lr=None) -> None:
         """clip + SGD momentum + compute-copy refresh (lr: float, or None when the
         device scalar ``self.lr`` was filled already -- graph replay)."""
         if lr is not None:
             self.lr.fill_(float(lr))
+        self.finish_grads()
         if self.cuda:
             from ..ops import _lib
             _lib.call("mx_mt_sgd", self.tab.data_ptr(), self.bmap.data_ptr(), self.bstart.data_ptr(), self.nblocks,

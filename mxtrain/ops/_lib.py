@@ -70,6 +70,8 @@ SIGNATURES = {
     "mx_mt_chunk": [],
     "mx_mt_max_tensors": [],
     "mx_mt_grad_in": [P, P, P, P, I, P, P, P, P],
+    "mx_mt_grad_in_range": [P, P, P, P, I, I, P, P, P, P],
+    "mx_mt_scale_sumsq": [P, I64, F, P, P],
     "mx_mt_sumsq_fin": [P, I, P, P],
     "mx_mt_sgd": [P, P, P, I, P, P, P, P, P, P, P],
     "mx_mt_cast": [P, P, P, I, P, P, P],

@@ -1,8 +1,10 @@
 """Counter-based dropout RNG shared by the HIP kernels and the CPU reference.
 
-``keep(idx)`` = hash32(lo(idx) ^ hi(idx)*0x85ebca6b, seed) >= p*2^32, bit-identical to
-``mx::dropout_keep`` in ``csrc/common.h``.  Masks are never stored: backward
-regenerates them from the same (seed, element index).
+Elements come in aligned groups of 8: group g = idx >> 3 seeds an xorshift32 stream with
+``x0 = hash32(lo(g) ^ hi(g)*0x85ebca6b, seed) | 1``; word j of the stream holds the 16-bit
+draws of elements 8g + 2j (low half) and 8g + 2j + 1 (high half), kept when
+>= round(p * 2^16).  Bit-identical to ``mx::dropout_keep8`` in ``csrc/common.h``.  Masks are
+never stored: backward regenerates them from the same (seed, element index).
 
 The seed lives in a 1-element int32 device tensor so a hipGraph-captured step sees a
 fresh value on every replay (``DropoutSeed.advance`` is itself captured).
@@ -28,15 +30,35 @@ def hash32(x: torch.Tensor, seed: int) -> torch.Tensor:
     return x
 
 
+def _xorshift(x: torch.Tensor) -> torch.Tensor:
+    x = x ^ _u32(x << 13)
+    x = x ^ (x >> 17)
+    return x ^ _u32(x << 5)
+
+
+def keep_threshold16(p: float) -> int:
+    """16-bit keep threshold from p, exactly as the kernels derive it from p * 2^32."""
+    t32 = int(p * 4294967296.0) if p > 0 else 0
+    return (t32 + 0x8000) >> 16
+
+
 def keep_mask(numel: int, seed: int, p: float, device="cpu", base: int = 0) -> torch.Tensor:
     """Boolean keep-mask for flat element indices base..base+numel-1."""
-    idx = torch.arange(base, base + numel, dtype=torch.int64, device=device)
-    lo = idx & M32
-    hi = (idx >> 32) & M32
-    x = lo ^ _u32(hi * 0x85EBCA6B)
-    h = hash32(x, seed)
-    thresh = int(p * 4294967296.0) if p > 0 else 0
-    return h >= thresh
+    if p <= 0:
+        return torch.ones(numel, dtype=torch.bool, device=device)
+    g0, g1 = base >> 3, (base + numel + 7) >> 3
+    g = torch.arange(g0, g1, dtype=torch.int64, device=device)
+    x = (g & M32) ^ _u32(((g >> 32) & M32) * 0x85EBCA6B)
+    x = hash32(x, seed) | 1
+    words = [x]
+    for _ in range(3):
+        x = _xorshift(x)
+        words.append(x)
+    w = torch.stack(words, 1)                                   # [G, 4]
+    draws = torch.stack([w & 0xFFFF, w >> 16], 2).reshape(-1)   # element order 2j, 2j + 1
+    keep = draws >= keep_threshold16(p)
+    off = base - 8 * g0
+    return keep[off:off + numel]
 
 
 class DropoutSeed:

@@ -71,7 +71,7 @@ def sgd_momentum_(opt: torch.optim.SGD, lr) -> None:
 
 class GraphedTrainStep:
     def __init__(self, model, opt: torch.optim.SGD, params: List[torch.Tensor], clip: float, device,
-                 flat_capacity: int = 16 << 20, flat_master=None):
+                 flat_capacity: int = 16 << 20, flat_master=None, allow_rccl_capture: bool = False):
         self.model, self.opt, self.params, self.clip, self.device = model, opt, params, clip, device
         self.graphs: Dict[tuple, tuple] = {}
         # with a FlatMaster (models/compute_weights.py) the update is its fused clip + SGD
@@ -83,6 +83,12 @@ class GraphedTrainStep:
         self.flat = torch.zeros(flat_capacity, dtype=torch.uint8, device=device)
         self.captures = 0
         self.replays = 0
+        self.eager_steps = 0
+        # data parallel (FlatMaster world > 1): the gradient all-reduces are captured with the
+        # step when they run on the xGMI kernel (device-side barrier epochs: replay-safe);
+        # RCCL inside a capture only when forced (--mx-graph 1)
+        self.allow_rccl_capture = allow_rccl_capture
+        self.capturable = True
         # MXTRAIN_GRAPH_DEBUG=1: synchronise after every step and log capture/replay events
         self.debug = os.environ.get("MXTRAIN_GRAPH_DEBUG", "0") == "1"
         self.marker = None   # diagnostics hook: called around the capture window
@@ -105,6 +111,22 @@ class GraphedTrainStep:
             sgd_momentum_(self.opt, self.lr)
         return torch.stack([losses[k].detach().float() for k in LOSS_NAMES])
 
+    def _route_capturable(self) -> bool:
+        fm = self.fm
+        if fm is None or fm.world == 1 or self.allow_rccl_capture:
+            return True
+        return fm.dp_routes == {"xgmi"}
+
+    def _eager(self, batch) -> Dict[str, torch.Tensor]:
+        """The same step without a graph (data-parallel over RCCL, not forced into capture)."""
+        flat = batch["gt_mask_flat"]
+        st = {k: batch[k].to(self.device, non_blocking=True) for k in INPUT_KEYS}
+        self.flat[:flat.numel()].copy_(flat, non_blocking=True)
+        self.opt.zero_grad(set_to_none=True)
+        out = self._body(st)
+        self.eager_steps += 1
+        return dict(zip(LOSS_NAMES, out.unbind(0)))
+
     def _ensure_capacity(self, n: int) -> None:
         if n <= self.flat.numel():
             return
@@ -122,6 +144,8 @@ class GraphedTrainStep:
         cur = torch.cuda.current_stream(self.device)
         self.lr.fill_(lr)
         entry = self.graphs.get(key)
+        if entry is None and not self.capturable:
+            return self._eager(batch)
         if entry is None:
             st = {k: batch[k].to(self.device, non_blocking=True) for k in INPUT_KEYS}
             self.flat[:flat.numel()].copy_(flat, non_blocking=True)
@@ -130,6 +154,11 @@ class GraphedTrainStep:
                 # eager step with this batch (a real update): warms every lazy cache
                 self.opt.zero_grad(set_to_none=True)
                 out = self._body(st)
+                if not self._route_capturable():
+                    cur.wait_stream(self.stream)
+                    self.capturable = False
+                    self.eager_steps += 1
+                    return dict(zip(LOSS_NAMES, out.unbind(0)))
                 # capture: grads are allocated inside the graph's pool, never zeroed
                 self.opt.zero_grad(set_to_none=True)
                 g = torch.cuda.CUDAGraph()

@@ -295,8 +295,16 @@ def main(argv=None):
     prof = StepProfiler(rank, out_dir=os.path.join(args.logdir, "profile") if os.environ.get("MXTRAIN_PROFILE") else None)
     debug_finite = check_finite_enabled()
     train_sets = [COCODetection(cfg.DATA.BASEDIR, n, training=True) for n in cfg.DATA.TRAIN]
-    use_graph = (args.mx_graph == "1" or (args.mx_graph == "auto" and world == 1 and not debug_finite)) \
-        and device.type == "cuda" and world == 1 and bool(cfg.MODE_MASK)
+    flat_sgd = device.type == "cuda" and os.environ.get("MXTRAIN_FLAT_SGD", "1") != "0"
+    if world > 1 and flat_sgd:
+        # data-parallel gradient all-reduce inside the fused step: the direct xGMI kernel
+        # (checked against RCCL and timed on the live group; RCCL where it loses) -- it is
+        # graph-capturable, so the whole step stays one hipGraph at world > 1
+        os.environ.setdefault("MXTRAIN_XGMI", "auto")
+    # whole-step hipGraph: 1 GPU, or world > 1 with the fused flat SGD (the replay checks the
+    # gradient reduction route after its eager warm-up step: xGMI, or RCCL when forced)
+    use_graph = (args.mx_graph == "1" or (args.mx_graph == "auto" and not debug_finite)) \
+        and device.type == "cuda" and bool(cfg.MODE_MASK) and (world == 1 or flat_sgd)
     ds = DetectionDataset(train_sets[0], short, max_size, training=True, with_masks=bool(cfg.MODE_MASK), seed=rank,
                           mask_format="crops")
     train_coll = functools.partial(collate, short=short, max_size=max_size, fixed_gt=use_graph)
@@ -328,21 +336,26 @@ def main(argv=None):
         calibrate_frozen_bn(model.backbone, x)
         log("Calibrated FrozenBN statistics of the random-init backbone")
     hvd.broadcast_parameters(model.state_dict().values())
-    dmodel = hvd.DistributedDataParallel(model)
     params = decay + no_decay
     clip = float(cfg.TRAIN.GRADIENT_CLIP or 0.0)
     gstep = None
     fm = None
-    if world == 1 and device.type == "cuda" and os.environ.get("MXTRAIN_FLAT_SGD", "1") != "0":
+    if flat_sgd:
         # flat fp32 master / grads / momentum + persistent bf16 compute copies: one launch
-        # each for the gradient cast, its norm and the clip + SGD + copy refresh
+        # each for the gradient cast, its norm and the clip + SGD + copy refresh; at world > 1
+        # the flat gradient is all-reduced bucket by bucket as backward produces it
         from mxtrain.models.compute_weights import FlatMaster
         fm = FlatMaster(model, opt, clip)
         model.__dict__["_flat_master"] = fm
-        log("Optimizer: fused flat SGD-momentum (+ clip, + bf16 compute copies)")
+        log("Optimizer: fused flat SGD-momentum (+ clip, + bf16 compute copies)" +
+            (f"; data-parallel: {len(fm.buckets)} gradient buckets all-reduced during backward" if world > 1 else ""))
+        dmodel = model
+    else:
+        dmodel = hvd.DistributedDataParallel(model)
     if use_graph:
         from mxtrain.workloads.maskrcnn.graphed import GraphedTrainStep
-        gstep = GraphedTrainStep(model, opt, params, clip, device, flat_master=fm)
+        gstep = GraphedTrainStep(model, opt, params, clip, device, flat_master=fm,
+                                 allow_rccl_capture=args.mx_graph == "1")
         log("Training step runs as a hipGraph (one graph per input shape)")
     max_steps = args.mx_max_steps
     timed_imgs, t_timed = 0, None
@@ -424,10 +437,19 @@ def main(argv=None):
     if t_timed is not None and timed_imgs:
         ips = timed_imgs / (t_end - t_timed)
         log(f"Throughput: {ips:.2f} images/s over {timed_imgs} images ({world} ranks)")
+        if gstep is not None:
+            log(f"Step path: hipGraph captures {gstep.captures}, replays {gstep.replays}, eager {gstep.eager_steps}"
+                + (f"; fused flat SGD, gradient all-reduce via {sorted(fm.dp_routes)}" if fm is not None and world > 1
+                   else "; fused flat SGD" if fm is not None else ""))
         if args.mx_bench_json and rank == 0:
             with open(args.mx_bench_json, "a") as f:
                 f.write(json.dumps({"metric": "Mask R-CNN R50-FPN train images/sec", "value": round(ips, 2),
-                                    "n_gpus": world, "batch_per_gpu": bs}) + "\n")
+                                    "n_gpus": world, "batch_per_gpu": bs,
+                                    "graph": None if gstep is None else
+                                    {"captures": gstep.captures, "replays": gstep.replays,
+                                     "eager": gstep.eager_steps},
+                                    "flat_sgd": fm is not None,
+                                    "dp_routes": sorted(fm.dp_routes) if fm is not None else None}) + "\n")
     hvd.shutdown()
     return 0
 

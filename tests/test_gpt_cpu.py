@@ -132,6 +132,27 @@ def test_dropout_mask_reproducible():
     assert 0.08 < frac < 0.12
 
 
+def test_dropout_mask_stream_properties():
+    """One hash per 8-element group + xorshift16 draws: drop rate within 0.5 % (relative)
+    of p over 4M draws, any sub-range equals the slice of the full mask (the kernels index by
+    absolute element), and neighbouring seeds / groups are uncorrelated."""
+    from mxtrain.ops.rng import keep_mask, keep_threshold16
+    n = 1 << 22
+    for p in (0.1, 0.5):
+        m = keep_mask(n, 99, p)
+        rate = 1 - m.float().mean().item()
+        assert abs(rate - p) < 0.005 * p, (p, rate)
+        assert abs(keep_threshold16(p) / 65536 - p) < 2 ** -16
+    full = keep_mask(1000, 7, 0.1)
+    for base, cnt in ((3, 100), (8, 64), (517, 300)):
+        assert torch.equal(keep_mask(cnt, 7, 0.1, base=base), full[base:base + cnt])
+    a, b = keep_mask(n, 1, 0.5).float(), keep_mask(n, 2, 0.5).float()
+    assert abs(((a - 0.5) * (b - 0.5)).mean().item()) < 2e-3
+    # lag-1 and lag-8 autocorrelation within one stream
+    for lag in (1, 2, 8):
+        assert abs(((a[lag:] - 0.5) * (a[:-lag] - 0.5)).mean().item()) < 2e-3, lag
+
+
 def test_activation_recompute_is_bit_identical():
     """--checkpoint-activations / --recompute-activations: each layer keeps only its inputs and
     re-runs its forward in backward; with dropout on, losses and gradients are unchanged."""
