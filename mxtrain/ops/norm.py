@@ -178,12 +178,21 @@ class ColReduceQueue:
     into the bf16 gradient, no two jobs writing the same output.  The layout is recorded
     on the first step (which reduces immediately), then reused; a step whose producer
     sequence differs from the recorded one is an error (the step structure is static for a
-    fixed model / batch configuration).  Only used when nothing consumes these gradients
-    before the optimizer (one data-parallel rank, no TP / PP: no per-bucket reductions
-    during backward)."""
+    fixed model / batch configuration).
 
-    def __init__(self, device):
+    Data parallel (``group_of``: output pointer -> gradient bucket): the jobs are split into
+    one table per bucket and ``flush_group(b)`` reduces bucket b's outputs right before that
+    bucket's reduce-scatter is issued (parallel/zero.py ``pre_reduce``) -- ~one launch per
+    bucket instead of one per producer, and the gradients are final when they are
+    communicated.  Outputs of one region must fall in one bucket, and no output may appear
+    in two regions (two jobs would read-modify-write the same bf16 gradient); otherwise the
+    queue stays in immediate mode."""
+
+    def __init__(self, device, group_of=None):
         self.device = device
+        self.group_of = group_of
+        self.tables = {}        # group -> (table, njobs, nblocks)
+        self.flushed = set()
         self.layout = None      # [(key, nparts, C, nvec, cols, accumulate)] in call order
         self.rec = []
         self.arena = None
@@ -196,6 +205,7 @@ class ColReduceQueue:
         self.i = 0
         self.rec = []
         self.fill = {}
+        self.flushed = set()
         self.active = self.layout is not None
 
     def partial(self, key, outs, nparts: int, C: int, nvec: int, cols: int, accumulate: bool):
@@ -214,14 +224,24 @@ class ColReduceQueue:
         self.fill[key] = k + nparts
         return self.arena[off + k * C: off + (k + nparts) * C]
 
+    def flush_group(self, g):
+        """Reduce the deferred jobs of gradient bucket ``g`` now (its producers are done)."""
+        if not self.active or g in self.flushed:
+            return
+        self.flushed.add(g)
+        t = self.tables.get(g)
+        if t is not None:
+            _lib.call("mx_colreduce_batched", _lib.ptr(t[0]), t[1], t[2], _lib.stream())
+
     def flush(self):
-        """End of backward: reduce every deferred job (one launch); on the recording step
-        build the layout for the next ones."""
+        """End of backward: reduce every deferred job not reduced yet (one launch per
+        group); on the recording step build the layout for the next ones."""
         if self.active:
             if self.i != len(self.layout):
                 raise RuntimeError("deferred column reductions: step ended after "
                                    f"{self.i} of {len(self.layout)} producers")
-            _lib.call("mx_colreduce_batched", _lib.ptr(self.table), self.njobs, self.nblocks, _lib.stream())
+            for g in self.tables:
+                self.flush_group(g)
             return
         if not self.rec or torch.cuda.is_current_stream_capturing():
             return
@@ -234,19 +254,36 @@ class ColReduceQueue:
             if (r[2], r[3], r[4], r[6]) != (C, nvec, cols, acc) or C % 4:
                 return    # (same output with different shapes / unaligned rows: keep immediate mode)
             r[1] += nparts
+        # every output pointer belongs to exactly one region, each region to one group
+        seen, groups = set(), {}
+        for key in order:
+            ptrs = [t.data_ptr() for t in regions[key][5] if t is not None]
+            if seen.intersection(ptrs) or len(set(ptrs)) != len(ptrs):
+                return    # (an output shared by two jobs: a read-modify-write race -> immediate mode)
+            seen.update(ptrs)
+            gs = {self.group_of(p) for p in ptrs} if self.group_of is not None else {None}
+            if len(gs) != 1:
+                return    # (one job's outputs in two buckets: cannot be reduced per bucket)
+            groups[key] = gs.pop()
         for key in order:           # regions laid out in first-use order
             r = regions[key]
             r[0] = off
             off += r[1] * r[2]
         self.arena = torch.empty(max(off, 1), dtype=torch.float32, device=self.device)
-        rows, blk = [], 0
+        by_group = {}
         for key in order:
-            o, nrows, C, nvec, cols, outs, acc = regions[key]
-            rows.append([self.arena.data_ptr() + 4 * o, nrows, C, cols] +
-                        [(t.data_ptr() if t is not None else 0) for t in outs] + [int(acc), blk])
-            blk += (C + 63) // 64
-        self.table = torch.tensor(rows, dtype=torch.int64).to(self.device)
-        self.njobs, self.nblocks = len(rows), blk
+            by_group.setdefault(groups[key], []).append(key)
+        self.tables = {}
+        for g, keys in by_group.items():
+            rows, blk = [], 0
+            for key in keys:
+                o, nrows, C, nvec, cols, outs, acc = regions[key]
+                rows.append([self.arena.data_ptr() + 4 * o, nrows, C, cols] +
+                            [(t.data_ptr() if t is not None else 0) for t in outs] + [int(acc), blk])
+                blk += (C + 63) // 64
+            self.tables[g] = (torch.tensor(rows, dtype=torch.int64).to(self.device), len(rows), blk)
+        self.njobs = sum(t[1] for t in self.tables.values())
+        self.nblocks = sum(t[2] for t in self.tables.values())
         self.regions = {k: tuple(v) for k, v in regions.items()}
         self.layout = [spec for spec, _ in self.rec]
 

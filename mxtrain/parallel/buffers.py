@@ -116,6 +116,18 @@ class FlatParams:
                 flags[o:o + _round_up(s.numel, ALIGN) // ALIGN] = 1
         self.wd_flags = flags.to(self.device)
 
+    def bucket_of_grad_ptr(self, ptr: int) -> Optional[int]:
+        """Index of the bucket whose slice of the flat gradient buffer holds address
+        ``ptr`` (None: not in the buffer)."""
+        base = self.grad.data_ptr()
+        e = (ptr - base) // self.grad.element_size()
+        if e < 0 or e >= self.numel:
+            return None
+        for b in self.buckets:
+            if b.start <= e < b.end:
+                return b.index
+        return None
+
     # ----------------------------------------------------------------- init
     def initialize(self, generator: Optional[torch.Generator] = None, num_layers: int = 1):
         for s in self.specs:

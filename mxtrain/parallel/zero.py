@@ -128,6 +128,10 @@ class DistributedOptimizer:
         self._sp_names = [s.name for s in flat.specs if s.sp_reduce]
         self.started = set()
         self.reset_pending()
+        # called with a bucket index right before that bucket's gradients are communicated
+        # (the trainer's deferred LN / bias column reductions of that bucket: ops/norm.py
+        # ColReduceQueue.flush_group)
+        self.pre_reduce = None
         # xGMI registered-buffer mode (see _direct); names are local keys only
         self._direct_state: Optional[bool] = None
         self.comm_timing = os.environ.get("MXTRAIN_COMM_TIMING", "0") == "1"
@@ -259,6 +263,8 @@ class DistributedOptimizer:
             return
         self.started.add(bi)
         b = self.flat.buckets[bi]
+        if self.pre_reduce is not None:
+            self.pre_reduce(bi)
         if self.world == 1:
             self._sp_allreduce(b)
             return

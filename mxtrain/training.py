@@ -109,13 +109,18 @@ class GPTTrainer:
             overlap_update=(tcfg.overlap_optimizer and self.device.type == "cuda" and ps.pp == 1
                             and self.eopt is None and not tcfg.wgrad_stream))
         self._setup_xgmi()
-        # LN / bias gradient column reductions folded into one launch at the end of backward
-        # when nothing reads those gradients before the optimizer (no DP / TP / PP reduction
-        # during backward): ~100 colreduce launches of a GPT-2 step become one
-        if (self.device.type == "cuda" and ps.grad_world == 1 and ps.tp == 1 and ps.pp == 1 and self.eopt is None
+        # LN / bias gradient column reductions deferred and batched: ~100 colreduce launches
+        # of a GPT-2 step become one at the end of backward (one rank), or one per gradient
+        # bucket right before its reduce-scatter is issued (data parallel)
+        if (self.device.type == "cuda" and ps.tp == 1 and ps.pp == 1 and self.eopt is None
                 and not self.opt.overlap_update and os.environ.get("MXTRAIN_DEFER_COLREDUCE", "1") != "0"):
             from .ops.norm import ColReduceQueue
-            self.stage.rt.colq = ColReduceQueue(self.device)
+            group_of = None
+            if ps.grad_world > 1:
+                group_of = self.flat.bucket_of_grad_ptr
+            self.stage.rt.colq = ColReduceQueue(self.device, group_of=group_of)
+            if group_of is not None:
+                self.opt.pre_reduce = self.stage.rt.colq.flush_group
         self.pipeline = None
         if ps.pp > 1:
             from .parallel.pipeline import PipelineSchedule

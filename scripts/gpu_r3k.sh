@@ -6,7 +6,9 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 timeout -k 10 330 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_maskrcnn_dp_gpu.py > gpurun_out/r3k_dp.log 2>&1 || { tail -60 gpurun_out/r3k_dp.log; exit 1; }
 tail -3 gpurun_out/r3k_dp.log
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/r3k_tests.log 2>&1 || { tail -40 gpurun_out/r3k_tests.log; exit 1; }
+timeout -k 10 620 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_tp_gpu.py > gpurun_out/r3k_tp.log 2>&1 || { tail -60 gpurun_out/r3k_tp.log; exit 1; }
+tail -5 gpurun_out/r3k_tp.log
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu --deselect tests/test_tp_gpu.py --deselect tests/test_maskrcnn_dp_gpu.py > gpurun_out/r3k_tests.log 2>&1 || { tail -40 gpurun_out/r3k_tests.log; exit 1; }
 tail -2 gpurun_out/r3k_tests.log
 timeout -k 10 300 python -u scripts/gemm_nt_bench.py > gpurun_out/r3k_gemm.log 2>&1 || { tail -30 gpurun_out/r3k_gemm.log; exit 1; }
 grep -v "^check" gpurun_out/r3k_gemm.log | tail -50

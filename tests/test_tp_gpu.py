@@ -1,0 +1,167 @@
+"""Tensor / sequence / data parallelism on real HIP streams (the side-stream code that
+the gloo CPU tests only exercise synchronously): 2 ranks as 2 processes on the test box's
+one MI355X, the direct xGMI kernels (parallel/xgmi.py) as the TP / DP transport, gloo as
+the control plane (RCCL cannot put two ranks on one GPU).
+
+* TP2 and TP2 + SP with ``tp_overlap`` / ``sp_gemm_overlap`` on (async dgrad all-reduce /
+  reduce-scatter across the wgrad GEMMs on a side stream; the SP all-gather overlapping the
+  own-chunk GEMM) must be BIT-identical to the same run with the overlap off, and track the
+  single-rank GPU trajectory to bf16 tolerance;
+* DP2 with the deferred, per-bucket LN / bias column reductions (ops/norm.py
+  ColReduceQueue.flush_group before each bucket's reduce-scatter) must be bit-identical to
+  immediate reductions.
+Reference: examples/megatron-deepspeed/gpt2_345m/pretrain-ddp-tp-pp-zero1.yaml:39-40."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+CFG = dict(num_layers=2, hidden_size=256, num_attention_heads=4, seq_length=256, max_position_embeddings=256,
+           vocab_size=1024, hidden_dropout=0.0, attention_dropout=0.0)
+STEPS = 3
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data():
+    g = torch.Generator().manual_seed(11)
+    x = torch.randint(0, CFG["vocab_size"], (1, 4, CFG["seq_length"] + 1), generator=g)
+    return x[..., :-1].contiguous(), x[..., 1:].contiguous()
+
+
+def _run_trainer(ps, init_sd, tok, lab, env):
+    from mxtrain.models.gpt import GPTConfig, shard_gpt_state
+    from mxtrain.training import GPTTrainer, TrainConfig
+    os.environ.update(env)
+    cfg = GPTConfig(**CFG)
+    tr = GPTTrainer(cfg, TrainConfig(micro_batch_size=tok.shape[1], lr=1e-3), ps)
+    tr.flat.load_state_dict(shard_gpt_state(init_sd, cfg, ps.tp, ps.tp_rank, 1, 0))
+    tr.opt._refresh_master()
+    dev = ps.device
+    losses = [float(tr.train_step(tok.to(dev), lab.to(dev))) for _ in range(STEPS)]
+    tr.sync_params()
+    torch.cuda.synchronize()
+    return losses, {n: p.detach().float().cpu().numpy() for n, p in tr.flat.params.items()}, tr
+
+
+def _worker(rank, world, port, mode, init_path, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK="0", MXTRAIN_XGMI="1", MXTRAIN_XGMI_TIMEOUT_S="20", MXTRAIN_XGMI_MAX_MB="32")
+        from mxtrain.parallel import state as pstate
+        from mxtrain.parallel import xgmi
+        tp = 2 if mode in ("tp", "sp") else 1
+        ps = pstate.initialize_model_parallel(tp=tp, sequence_parallel=mode == "sp", backend="gloo",
+                                              device_type="cuda")
+        init_sd = torch.load(init_path, weights_only=True)
+        tok, lab = _data()
+        if mode == "dp":
+            tok, lab = tok[:, 2 * rank:2 * rank + 2], lab[:, 2 * rank:2 * rank + 2]
+            a = _run_trainer(ps, init_sd, tok, lab, {"MXTRAIN_DEFER_COLREDUCE": "1"})
+            assert a[2].stage.rt.colq is not None and a[2].opt.pre_reduce is not None
+            deferred = a[2].stage.rt.colq.layout is not None and len(a[2].stage.rt.colq.tables) >= 1
+            b = _run_trainer(ps, init_sd, tok, lab, {"MXTRAIN_DEFER_COLREDUCE": "0"})
+            extra = {"deferred": deferred, "groups": len(a[2].stage.rt.colq.tables)}
+        else:
+            a = _run_trainer(ps, init_sd, tok, lab, {"MXTRAIN_TP_OVERLAP": "1"})
+            assert a[2].stage.rt.tp_overlap
+            b = _run_trainer(ps, init_sd, tok, lab, {"MXTRAIN_TP_OVERLAP": "0"})
+            extra = {}
+        for c in xgmi._COMMS.values():
+            if c is not None:
+                c.check()
+        q.put((rank, a[0], a[1], b[0], b[1], (ps.tp_rank, ps.dp_rank), extra))
+        import torch.distributed as dist
+        dist.barrier()
+        xgmi.destroy_all()
+        pstate.destroy()
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()[-3000:], None, None, None, None))
+        raise
+
+
+def _reference(tmp_path):
+    """Single-rank GPU run from the same init (the init is also what the workers shard)."""
+    from mxtrain.models.gpt import GPTConfig
+    from mxtrain.parallel.state import ParallelState
+    from mxtrain.training import GPTTrainer, TrainConfig
+    cfg = GPTConfig(**CFG)
+    ps = ParallelState(device=torch.device("cuda"))
+    tr = GPTTrainer(cfg, TrainConfig(micro_batch_size=4, lr=1e-3), ps)
+    init = {k: v.detach().cpu().clone() for k, v in tr.flat.state_dict().items()}
+    path = tmp_path / "init.pt"
+    torch.save(init, path)
+    tok, lab = _data()
+    losses = [float(tr.train_step(tok.cuda(), lab.cuda())) for _ in range(STEPS)]
+    final = {k: v.detach().float().cpu() for k, v in tr.flat.state_dict().items()}
+    return cfg, str(path), init, losses, final
+
+
+def _spawn(mode, init_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, init_path, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted([q.get(timeout=200) for _ in procs], key=lambda t: t[0])
+        for p in procs:
+            p.join(timeout=30)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    for r in res:
+        assert r[1] != "error", r[2]
+    return res
+
+
+@pytest.mark.timeout(280)
+@pytest.mark.parametrize("mode", ["tp", "sp"])
+def test_tp2_side_streams_on_gpu(tmp_path, mode):
+    import numpy as np
+    from mxtrain.models.gpt import shard_gpt_state
+    cfg, init_path, init, ref_losses, ref_final = _reference(tmp_path)
+    res = _spawn(mode, init_path)
+    for rank, la, pa, lb, pb, (tpr, _), _ in res:
+        # overlap on == overlap off, bit for bit
+        assert la == lb, (mode, rank, la, lb)
+        for n in pa:
+            assert np.array_equal(pa[n], pb[n]), (mode, rank, n)
+        # and the single-rank trajectory to bf16 tolerance
+        for x, y in zip(la, ref_losses):
+            assert abs(x - y) <= 2e-2 * abs(y), (mode, rank, la, ref_losses)
+        exp = shard_gpt_state(ref_final, cfg, 2, tpr, 1, 0)
+        ini = shard_gpt_state(init, cfg, 2, tpr, 1, 0)
+        num = sum(float(((torch.from_numpy(pa[n]) - t) ** 2).sum()) for n, t in exp.items()) ** 0.5
+        den = sum(float(((t - ini[n].float()) ** 2).sum()) for n, t in exp.items()) ** 0.5
+        # (Adam's first steps move every weight by ~lr whatever the gradient's size, so
+        # bf16 rounding differences in near-zero gradients show up as sign flips)
+        assert num < 0.35 * den, (mode, rank, num / den)
+
+
+@pytest.mark.timeout(280)
+def test_dp2_deferred_colreduce_bit_identical_on_gpu(tmp_path):
+    import numpy as np
+    cfg, init_path, init, ref_losses, ref_final = _reference(tmp_path)
+    res = _spawn("dp", init_path)
+    for rank, la, pa, lb, pb, _, extra in res:
+        assert extra["deferred"] and extra["groups"] >= 1, extra
+        assert la == lb, (rank, la, lb)
+        for n in pa:
+            assert np.array_equal(pa[n], pb[n]), (rank, n)
+    # both DP ranks hold the same parameters
+    for n in res[0][2]:
+        assert np.array_equal(res[0][2][n], res[1][2][n]), n
