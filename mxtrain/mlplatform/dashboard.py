@@ -21,7 +21,10 @@ Replaces, per reference component:
 * C45 Katib UI -> ``GET /api/experiments`` (HPO experiments, trials, best);
 * C46 KFP UI + API server -> ``GET /api/pipelines`` (recorded pipeline runs),
   ``GET|POST /api/pipelines/defs`` (stored pipelines), ``GET|POST /api/runs``,
-  ``GET /api/runs/<run>``, ``POST /api/runs/<run>/terminate`` (asynchronous runs);
+  ``GET /api/runs/<run>``, ``POST /api/runs/<run>/terminate`` (asynchronous runs; with
+  ``cache: true`` steps whose inputs succeeded before are served from the step cache),
+  ``GET|POST /api/recurringruns``, ``POST /api/recurringruns/<name>/enable|disable``
+  (cron / interval schedules fired by the scheduler thread);
 * C48 profiles / KFAM -> ``GET /api/profiles``;
 * C22-C26 node view (Karpenter / device plugins) -> ``GET /api/node`` (GPUs, ledger,
   node profile, sysfs power/clock samples);
@@ -468,8 +471,26 @@ def route_post(parts: List[str], q: Dict[str, str], body: bytes, user: Optional[
             cfgs = pl.get_pipeline(str(doc["pipeline"])).get("chart_configs")
         _authorize_configs(user, cfgs)
         run = pl.submit_run(chart_configs=doc.get("chart_configs"), pipeline=doc.get("pipeline"),
-                            run_name=doc.get("name"))
+                            run_name=doc.get("name"), cache=bool(doc.get("cache", False)))
         return 201, js, json.dumps({"run": run})
+    if rest == ["recurringruns"]:
+        if not isinstance(doc, dict):
+            raise ValueError("body must be a mapping")
+        cfgs = pl.get_pipeline(str(doc.get("pipeline", ""))).get("chart_configs")
+        _authorize_configs(user, cfgs)
+        out = pl.save_recurring_run(str(doc.get("name", "")), str(doc.get("pipeline", "")), cron=doc.get("cron"),
+                                    interval=doc.get("interval"), max_concurrency=int(doc.get("max_concurrency", 1)),
+                                    enabled=bool(doc.get("enabled", True)), cache=bool(doc.get("cache", False)),
+                                    start_time=doc.get("start_time"), end_time=doc.get("end_time"),
+                                    namespaces=sorted({str((c or {}).get("namespace", "default")) for c in cfgs or []}))
+        return 201, js, json.dumps(out, default=str)
+    if len(rest) == 3 and rest[0] == "recurringruns" and rest[2] in ("enable", "disable"):
+        if user is not None:
+            from .profiles import can
+            for ns in pl.get_recurring_run(rest[1]).get("namespaces") or ["default"]:
+                if not can(user, "create", ns):
+                    raise PermissionError(f"{user} may not change recurring runs in namespace {ns}")
+        return 200, js, json.dumps(pl.set_recurring_enabled(rest[1], rest[2] == "enable"), default=str)
     if len(rest) == 3 and rest[0] == "runs" and rest[2] == "terminate":
         if user is not None:   # KFAM: only an owner / contributor of every namespace the run touches
             from .profiles import can
@@ -533,6 +554,14 @@ def route(path: str, q: Dict[str, str], method: str = "GET", body: bytes = b"", 
             return 200, js, json.dumps(get_pipeline(rest[2]), default=str)
         if k == "runs" and len(rest) == 1:
             return 200, js, json.dumps(pipelines(), default=str)
+        if k == "recurringruns" and len(rest) == 1:
+            from ..pipeline import list_recurring_runs
+            return 200, js, json.dumps(list_recurring_runs(), default=str)
+        if k == "recurringruns" and len(rest) == 2:
+            from ..pipeline import get_recurring_run, next_fire
+            d = get_recurring_run(rest[1])
+            d["next_fire"] = next_fire(d)
+            return 200, js, json.dumps(d, default=str)
         if k == "runs" and len(rest) == 2:
             from ..pipeline import get_run
             return 200, js, json.dumps(get_run(rest[1]), default=str)
@@ -668,7 +697,11 @@ def main(argv=None):
                     help="accept bearer / session JWTs of the node identity provider (POST /auth/token)")
     ap.add_argument("--tls-auto", action="store_true",
                     help="serve HTTPS with a certificate issued (and renewed) by the node CA")
+    ap.add_argument("--no-scheduler", action="store_true", help="do not fire recurring runs from this server")
     a = ap.parse_args(argv)
+    if not a.no_scheduler:
+        from ..pipeline import Scheduler
+        Scheduler().start()
     if a.tls_auto and not a.certfile:
         from .identity import issue_cert
         c = issue_cert("dashboard", ["localhost", a.host] if a.host not in ("127.0.0.1", "0.0.0.0") else ["localhost"],

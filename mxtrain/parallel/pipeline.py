@@ -37,6 +37,8 @@ class _P2P:
 
 
 class PipelineSchedule:
+    SEND_WINDOW = 2   # outstanding posted sends before the oldest is waited for
+
     def __init__(self, trainer: "GPTTrainer"):
         self.tr = trainer
         self.ps = trainer.ps
@@ -50,8 +52,8 @@ class PipelineSchedule:
 
     # ---------------------------------------------------------------- p2p primitives
     # Every transfer is posted without waiting; the consumer waits right before it uses
-    # the tensor (a stream dependency under RCCL, not a host block), and sends are only
-    # waited for at the end of the schedule (their tensors stay referenced until then).
+    # the tensor (a stream dependency under RCCL, not a host block); at most SEND_WINDOW
+    # sends stay outstanding (their tensors referenced) before the oldest is waited for.
     # Receives are posted as early as the schedule allows -- the next forward's input
     # before this step's backward, the next backward's gradient before this backward --
     # so the transfer runs under compute.  Opposite-direction transfers that are needed
@@ -88,7 +90,14 @@ class PipelineSchedule:
         remaining = nm - warm
         loss_total = torch.zeros((), dtype=torch.float32, device=tr.device)
         inflight = deque()
-        sends = []          # posted sends, waited for at the end
+        # posted sends: a bounded window (each keeps its activation / gradient tensor alive
+        # until waited), so memory does not grow with the number of micro-batches
+        sends = deque()
+
+        def push_send(sd):
+            sends.append(sd)
+            while len(sends) > self.SEND_WINDOW:
+                sends.popleft().wait()
         fwd_i = 0
         bwd_i = 0
 
@@ -132,7 +141,7 @@ class PipelineSchedule:
             nin = post_recv_fwd() if (k + 1 < warm or remaining > 0) else None
             out = fwd(inp)
             if not last:
-                sends.append(self._post(send_t=out.detach(), send_to=nxt))
+                push_send(self._post(send_t=out.detach(), send_to=nxt))
         # steady state: 1F1B
         inp = take(nin, grad=True) if remaining > 0 else None
         nin = None
@@ -145,7 +154,7 @@ class PipelineSchedule:
             nin = post_recv_fwd() if i < remaining - 1 else None
             in_grad = bwd(out_grad)
             if not first:
-                sends.append(self._post(send_t=in_grad, send_to=prev))
+                push_send(self._post(send_t=in_grad, send_to=prev))
             inp = take(nin, grad=True) if i < remaining - 1 else None
         # cool-down backwards (the next gradient is prefetched while this backward runs)
         ng = None if (last or warm == 0) else self._post(recv_shape=shape, recv_from=nxt)
@@ -154,7 +163,7 @@ class PipelineSchedule:
             ng = None if (last or k + 1 >= warm) else self._post(recv_shape=shape, recv_from=nxt)
             in_grad = bwd(out_grad)
             if not first:
-                sends.append(self._post(send_t=in_grad, send_to=prev))
+                push_send(self._post(send_t=in_grad, send_to=prev))
         for sd in sends:
             sd.wait()
         return loss_total

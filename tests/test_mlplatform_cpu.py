@@ -404,3 +404,120 @@ def test_pipelines_api_enforces_profile_roles(home):
     assert db.route("/api/pipelines/defs", {}, "POST", body, user="carol@example.com")[0] == 201
     run = json.dumps({"pipeline": "p-b", "name": "rb1"}).encode()
     assert db.route("/api/runs", {}, "POST", run, user="mallory@example.com")[0] == 403
+
+
+def test_pipeline_step_cache(home):
+    """KFP cache server (C46): with caching on, a step whose chart files + values already
+    succeeded is served from the cache (recorded with the execution it reused); a changed
+    value, a failed step or a stale entry runs again."""
+    from mxtrain import pipeline as pl
+    from mxtrain.mlplatform import dashboard as db
+    dp = "charts/machine-learning/data-prep/data-process"
+    marker = home / "ran.txt"
+    step = {"release_name": "c-a", "namespace": "default", "path": dp,
+            "values": {"process": {"command": ["echo"], "args": ["x", ">>", str(marker)]}}}
+    assert pl.run_pipeline([step], run_name="c1", cache=True) == "Success"
+    assert pl.run_pipeline([step], run_name="c2", cache=True) == "Success"
+    assert marker.read_text().count("x") == 1                      # second run: cached
+    r2 = pl.get_run("c2")
+    assert r2["steps"][0]["cached"] and r2["steps"][0]["cached_from"] == "c1"
+    assert r2["steps"][0]["cache_key"] == pl.get_run("c1")["steps"][0]["cache_key"]
+    # cache off (the default): runs again
+    assert pl.run_pipeline([step], run_name="c3") == "Success"
+    assert marker.read_text().count("x") == 2
+    # a different value is a different key
+    step2 = dict(step, values={"process": {"command": ["echo"], "args": ["y", ">>", str(marker)]}})
+    assert pl.run_pipeline([step2], run_name="c4", cache=True) == "Success"
+    assert "y" in marker.read_text() and not pl.get_run("c4")["steps"][0]["cached"]
+    # staleness bound: an entry older than max_cache_staleness is not reused
+    assert pl.run_pipeline([dict(step, max_cache_staleness=0)], run_name="c5", cache=True) == "Success"
+    assert marker.read_text().count("x") == 3
+    # failures are never cached
+    bad = dict(step, release_name="c-bad", values={"process": {"command": ["false"]}})
+    assert pl.run_pipeline([bad], run_name="c6", cache=True) == "Failure"
+    assert pl.run_pipeline([bad], run_name="c7", cache=True) == "Failure"
+    assert not pl.get_run("c7")["steps"][0]["cached"]
+    # over the API: POST /api/runs {cache: true}
+    code, _, body = db.route("/api/runs", {}, "POST", json.dumps({"chart_configs": [step], "name": "c8",
+                                                                   "cache": True}).encode())
+    assert code == 201
+    rec = pl.wait_run("c8", timeout=60)
+    assert rec["cache"] and rec["steps"][0]["cached"]
+
+
+def test_cron_expressions():
+    import datetime as dt
+    from mxtrain.pipeline import Cron
+    t0 = dt.datetime(2026, 10, 17, 10, 7, 30).timestamp()           # a Saturday
+    nxt = lambda e, t=t0: dt.datetime.fromtimestamp(Cron(e).next_after(t))  # noqa: E731
+    assert nxt("*/15 * * * *") == dt.datetime(2026, 10, 17, 10, 15)
+    assert nxt("0 2 * * 1-5") == dt.datetime(2026, 10, 19, 2, 0)         # next weekday
+    assert nxt("0 0 1 * *") == dt.datetime(2026, 11, 1)
+    assert nxt("30 0 9 * * 0") == dt.datetime(2026, 10, 18, 9, 0, 30)     # 6 fields (KFP): Sunday
+    assert nxt("0 9 * * 7") == dt.datetime(2026, 10, 18, 9, 0)            # 7 = Sunday too
+    assert nxt("0 12 29 2 *") == dt.datetime(2028, 2, 29, 12, 0)          # leap day
+    for bad in ("* * *", "61 * * * *", "*/0 * * * *"):
+        with pytest.raises(ValueError):
+            Cron(bad)
+
+
+def test_recurring_runs_schedule_concurrency_and_api(home):
+    """ScheduledWorkflow (C46): interval / cron recurring runs of a stored pipeline, fired by
+    Scheduler.tick, at most max_concurrency at once, no catch-up, enable / disable and
+    end time; exposed under /api/recurringruns with KFAM checks."""
+    import time
+    from mxtrain import pipeline as pl
+    from mxtrain.mlplatform import dashboard as db
+    from mxtrain.mlplatform import profiles as pr
+    dp = "charts/machine-learning/data-prep/data-process"
+    ok = {"release_name": "rr-a", "namespace": "default", "path": dp, "values": {"process": {"command": ["true"]}}}
+    pl.save_pipeline("nightly", [ok])
+    submitted = []
+    sch = pl.Scheduler(submit=lambda **kw: submitted.append(kw))
+    code, _, body = db.route("/api/recurringruns", {}, "POST", json.dumps(
+        {"name": "every-min", "pipeline": "nightly", "interval": 60, "cache": True}).encode())
+    assert code == 201, body
+    d = pl.get_recurring_run("every-min")
+    t = d["created"]
+    assert sch.tick(t + 30) == []                          # not due yet
+    fired = sch.tick(t + 61)
+    assert len(fired) == 1 and submitted[-1]["pipeline"] == "nightly" and submitted[-1]["cache"]
+    assert submitted[-1]["recurring"] == "every-min"
+    assert sch.tick(t + 62) == []                          # next period counts from the fire
+    # no catch-up: a long gap fires once, not once per missed period
+    assert len(sch.tick(t + 1000)) == 1 and sch.tick(t + 1001) == []
+    # concurrency: a still-active run blocks the next period
+    pl.save_pipeline("slow", [dict(ok, release_name="rr-slow", values={"process": {"command": ["sleep"],
+                                                                                   "args": ["30"]}})])
+    pl.save_recurring_run("slow-rr", "slow", interval=1, max_concurrency=1)
+    real = pl.Scheduler()
+    t1 = time.time() + 2
+    assert len(real.tick(t1)) == 1
+    assert real.tick(t1 + 5) == []                         # first run still active
+    run = pl.get_recurring_run("slow-rr")["runs"][0]
+    pl.terminate_run(run)
+    pl.wait_run(run, timeout=60)
+    assert pl.get_run(run)["recurring_run"] == "slow-rr"
+    assert len(real.tick(t1 + 10)) == 1                    # free again
+    for r in pl.get_recurring_run("slow-rr")["runs"]:
+        pl.terminate_run(r)
+        pl.wait_run(r, timeout=60)
+    # disable / enable over the API; a user without a role in the namespace is refused
+    pr.create("default", owner="owner@x")
+    assert db.route("/api/recurringruns/every-min/disable", {}, "POST", user="mallory@x")[0] == 403
+    assert db.route("/api/recurringruns/every-min/disable", {}, "POST", user="owner@x")[0] == 200
+    assert sch.tick(time.time() + 10 ** 6) == [] or all("every-min" not in f for f in sch.tick(time.time() + 10 ** 6))
+    assert json.loads(db.route("/api/recurringruns/every-min", {})[2])["next_fire"] is None
+    assert db.route("/api/recurringruns/every-min/enable", {}, "POST")[0] == 200
+    lst = json.loads(db.route("/api/recurringruns", {})[2])
+    assert {x["name"] for x in lst} == {"every-min", "slow-rr"}
+    # end time: nothing fires after it
+    pl.save_recurring_run("ended", "nightly", cron="* * * * *", end_time=time.time() - 1)
+    assert pl.next_fire(pl.get_recurring_run("ended")) is None
+    # validation
+    assert db.route("/api/recurringruns", {}, "POST", json.dumps(
+        {"name": "bad", "pipeline": "nightly", "cron": "* * *"}).encode())[0] == 400
+    assert db.route("/api/recurringruns", {}, "POST", json.dumps(
+        {"name": "bad", "pipeline": "nightly"}).encode())[0] == 400
+    assert db.route("/api/recurringruns", {}, "POST", json.dumps(
+        {"name": "bad", "pipeline": "missing", "interval": 5}).encode())[0] == 404
