@@ -1016,6 +1016,132 @@ __global__ __launch_bounds__(1024) void tk_sort_decode_kernel(const int64_t* __r
   }
 }
 
+// ------------------------------------------------------------------ generic row top-k
+// The k largest (or smallest) fp32 values of each row, sorted, ties by lower index, with
+// their indices -- the large-k selections of the Mask R-CNN step (post-NMS top 2000 of
+// ~10000 proposals, RoI sampling's 512 of ~2000 candidates, the rank-based fg/bg picks),
+// which torch's topk serves with a rocprim segmented merge sort (~40 launches and ~0.3 ms
+// per step, profiles/r2_maskrcnn_s4/README.md).  One 1024-thread workgroup per row, ONE
+// launch per call:
+//   1. radix select on the order-preserving u32 key, 4 passes of 8 bits (LDS histogram of
+//      the keys that match the prefix so far; wave 0 finds the bin holding the k-th key)
+//      -> threshold T and the number of == T keys still needed;
+//   2. keys > T land in a candidate list in any order; keys == T in index order (ballot
+//      prefix sums) until the need is met;
+//   3. bitonic sort of the <= 2048 (key, ~index) pairs in LDS, values re-read from the row.
+constexpr int kTkrMaxK = 2048;
+
+__device__ __forceinline__ uint32_t tkr_key(float f, bool largest) {
+  const uint32_t u = __float_as_uint(f);
+  const uint32_t k = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return largest ? k : ~k;
+}
+
+__global__ __launch_bounds__(1024) void topk_rows_kernel(const float* __restrict__ x, int n, int ld, int k, int largest,
+                                                         float* __restrict__ ov, int64_t* __restrict__ oi) {
+  __shared__ int hist[256];
+  __shared__ int sel[2];
+  __shared__ int wc[16];
+  __shared__ int ngt;
+  __shared__ unsigned long long cand[kTkrMaxK];
+  const int r = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const float* row = x + (size_t)r * ld;
+  const bool lg = largest != 0;
+  uint32_t prefix = 0u, pmask = 0u;
+  int rem = k;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    if (t < 256) hist[t] = 0;
+    __syncthreads();
+    for (int e = t; e < n; e += 1024) {
+      const uint32_t key = tkr_key(row[e], lg);
+      if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1);
+    }
+    __syncthreads();
+    if (w == 0) {
+      // lane l owns bins 255 - 4l .. 252 - 4l (top first); inclusive prefix over lanes
+      int c[4], sum = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c[j] = hist[255 - 4 * lane - j];
+        sum += c[j];
+      }
+      int incl = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+      }
+      const int excl = incl - sum;
+      if (excl < rem && incl >= rem) {
+        int acc = excl, j = 0;
+        for (; j < 3; ++j) {
+          if (acc + c[j] >= rem) break;
+          acc += c[j];
+        }
+        sel[0] = 255 - 4 * lane - j;
+        sel[1] = rem - acc;
+      }
+    }
+    __syncthreads();
+    prefix |= (uint32_t)sel[0] << shift;
+    pmask |= 255u << shift;
+    rem = sel[1];
+    __syncthreads();
+  }
+  const uint32_t T = prefix;
+  const int need_eq = rem, n_gt = k - need_eq;
+  if (t == 0) ngt = 0;
+  __syncthreads();
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int eq_base = 0;
+  for (int e0 = 0; e0 < n; e0 += 1024) {
+    const int e = e0 + t;
+    const uint32_t key = e < n ? tkr_key(row[e], lg) : 0u;
+    const bool gt = e < n && key > T, eq = e < n && key == T;
+    if (gt) {
+      const int pos = atomicAdd(&ngt, 1);
+      cand[pos] = ((unsigned long long)key << 32) | (uint32_t)(~(uint32_t)e);
+    }
+    const unsigned long long bq = __ballot(eq);
+    if (lane == 0) wc[w] = __popcll(bq);
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int x2 = 0; x2 < 16; ++x2) {
+      off += x2 < w ? wc[x2] : 0;
+      tot += wc[x2];
+    }
+    if (eq) {
+      const int re = eq_base + off + __popcll(bq & below);
+      if (re < need_eq) cand[n_gt + re] = ((unsigned long long)key << 32) | (uint32_t)(~(uint32_t)e);
+    }
+    eq_base += tot;
+    __syncthreads();
+    if (eq_base >= need_eq && ngt >= n_gt) break;   // (uniform: shared values after the barrier)
+  }
+  int P = 1;
+  while (P < k) P <<= 1;
+  for (int i = k + t; i < P; i += 1024) cand[i] = 0ull;   // pads sort last (descending)
+  __syncthreads();
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = t; i < P / 2; i += 1024) {
+        const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const unsigned long long a = cand[lo], b = cand[hi];
+        if ((a < b) == desc) { cand[lo] = b; cand[hi] = a; }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = t; i < k; i += 1024) {
+    const int idx = (int)(~(uint32_t)cand[i]);
+    ov[(size_t)r * k + i] = row[idx];
+    oi[(size_t)r * k + i] = idx;
+  }
+}
+
 // ------------------------------------------------------------------------------ matching
 // per (image, anchor): max IoU over that image's gt boxes and its argmax; per gt: the
 // best IoU over anchors (atomicMax on the float bits -- IoU >= 0).
@@ -1358,6 +1484,16 @@ MX_EXPORT int mx_crop_resize_mask_crops(const void* flat, const int* table, int 
 // before the first call (the last kernel re-zeroes them); bcnt: nchunks int2; cand: R x
 // 2048 uint2; outputs boxes [R][K] float4, scores [R][K].
 MX_EXPORT int mx_topk_chunk() { return kTkChunk; }
+
+// x [R][ld] fp32 (n valid columns) -> the k largest (largest = 1) or smallest values per
+// row, sorted, ties by lower index: ov [R][k] fp32, oi [R][k] int64.  1 <= k <= min(n, 2048).
+MX_EXPORT int mx_topk_rows(const float* x, int R, int n, int ld, int k, int largest, float* ov, int64_t* oi,
+                           hipStream_t s) {
+  if (R <= 0 || k <= 0 || k > n || k > kTkrMaxK || ld < n || n >= (1 << 30)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(topk_rows_kernel, dim3(R), dim3(1024), 0, s, x, n, ld, k, largest, ov, oi);
+  return hipGetLastError();
+}
+MX_EXPORT int mx_topk_rows_max_k() { return kTkrMaxK; }
 // host_rows: R x 6 int64 {logits, deltas, anchors, n, image, 0}; tables: device scratch of
 // kTkMaxRows * 6 int64 followed by kTkMaxRows + 1 int32
 MX_EXPORT int mx_topk_max_rows() { return kTkMaxRows; }

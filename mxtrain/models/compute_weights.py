@@ -193,8 +193,10 @@ class FlatMaster:
         assert len(mom) == 1 and len(wds) <= 1, "one momentum and one non-zero weight decay"
         assert all(not g.get("nesterov") and not g.get("dampening") for g in opt.param_groups)
         import torch.distributed as dist
-        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
-        self.group = group
+        dist_on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if dist_on else 1
+        # an explicit group object: the xGMI communicator registry is keyed on it
+        self.group = group if (group is not None or not dist_on) else dist.group.WORLD
         self.params, wdf = [], []
         for g in opt.param_groups:
             for p in g["params"]:

@@ -94,7 +94,7 @@ def _rank_select(key: torch.Tensor, want: torch.Tensor, eligible: torch.Tensor, 
     captured hipGraph step (workloads/maskrcnn/graphed.py)."""
     k = torch.where(eligible, key, torch.full_like(key, 2.0))
     m = min(max_want, k.shape[-1])
-    kv, idx = k.topk(m, dim=-1, largest=False)                     # ascending: position = rank
+    kv, idx = V.topk_rows(k, m, largest=False)                     # ascending: position = rank
     take = (kv < 2.0) & (torch.arange(m, device=key.device)[None] < want[:, None])
     out = torch.zeros_like(eligible)
     out.scatter_(-1, idx, take)
@@ -282,7 +282,7 @@ class MaskRCNN(nn.Module):
         kb = kb.view(B, L * pre, 4)
         ks = ks.view(B, L * pre)
         top = min(post, ks.shape[1])
-        s, i = ks.topk(top, dim=1)
+        s, i = V.topk_rows(ks, top)
         b = torch.gather(kb, 1, i[..., None].expand(-1, -1, 4))
         return b.detach(), s.detach()
 
@@ -305,7 +305,7 @@ class MaskRCNN(nn.Module):
         r = torch.rand(mi.shape, device=mi.device)
         sel_fg = _rank_select(r, torch.full((B,), nfg, device=mi.device), fg, nfg)
         key = torch.where(sel_fg, 2.0 + r, torch.where(bg, 1.0 + r, torch.zeros_like(r)))
-        _, idx = key.topk(N, dim=1)                                                        # fg first, then bg
+        _, idx = V.topk_rows(key, N)                                                       # fg first, then bg
         rois = torch.gather(cand, 1, idx[..., None].expand(-1, -1, 4))
         is_fg = torch.gather(sel_fg, 1, idx)
         g = torch.gather(am.clamp(min=0), 1, idx)

@@ -101,6 +101,8 @@ SIGNATURES = {
     "mx_roi_align_bwd_tiled": [P, P, P, P, I, I, F, I, I, P, I, I, I, I, I, I, P, P, P, P],
     "mx_nms_workspace_words": [I],
     "mx_topk_chunk": [],
+    "mx_topk_rows": [P, I, I, I, I, I, P, P, P],
+    "mx_topk_rows_max_k": [],
     "mx_topk_max_rows": [],
     "mx_level_topk_decode": [P, I, I, P, F, P, P, P, P, I, P, P, P, P],
     "mx_nms": [P, P, I, I, F, I, P, P, P, P],

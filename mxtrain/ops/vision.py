@@ -411,6 +411,23 @@ def crop_resize_mask_crops(flat: torch.Tensor, table: torch.Tensor, H: int, W: i
 _TK_CACHE = {}
 
 
+def topk_rows(x: torch.Tensor, k: int, largest: bool = True):
+    """(values, int64 indices) of the k largest / smallest entries of each row of a 2-D
+    fp32 tensor, sorted, ties by lower index -- torch.topk(x, k, dim=1, largest) semantics
+    in ONE launch (csrc/vision.hip topk_rows_kernel; capture-safe).  One workgroup per row
+    suits rows up to ~32k entries (the proposal / RoI selections); longer rows (the ~270k
+    RPN anchors), k > 2048, other dtypes / dims and CPU tensors go through torch.topk."""
+    if (not _lib.use_hip(x) or x.dim() != 2 or x.dtype != torch.float32 or x.stride(1) != 1
+            or k < 1 or k > x.shape[1] or k > 2048 or x.shape[0] == 0 or x.shape[1] > 32768):
+        return x.topk(k, dim=1, largest=largest)
+    R, n = x.shape
+    ov = torch.empty((R, k), dtype=torch.float32, device=x.device)
+    oi = torch.empty((R, k), dtype=torch.int64, device=x.device)
+    _lib.call("mx_topk_rows", x.data_ptr(), R, n, x.stride(0), k, int(largest), ov.data_ptr(), oi.data_ptr(),
+              _lib.stream())
+    return ov, oi
+
+
 def _level_topk_decode_ref(logits_lv, deltas_lv, anchors_lv, img_hw, k):
     B = logits_lv[0].shape[0]
     boxes, scores, counts = [], [], []

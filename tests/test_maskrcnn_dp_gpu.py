@@ -70,7 +70,7 @@ def _worker(rank, world, port, data_dir, q):
                         d["gt_mask_table"])
             losses["total_loss"].backward()
             fa.step(lr)
-            la.append(float(losses["total_loss"]))
+            la.append(float(losses["total_loss"].detach()))
         torch.cuda.manual_seed(7)
         lb = [float(gs(b, lr)["total_loss"]) for b, lr in plan]
         torch.cuda.synchronize()

@@ -308,3 +308,27 @@ def test_fused_detection_losses_match_torch():
     tm = torch.rand(R, 28, 28, generator=g).to(dev)
     valid = (torch.rand(R, generator=g) < 0.7).float().to(dev)
     run(D.mask_loss, D.mask_loss_ref, [ml, ml_lab, tm, valid], (0,))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,n,k,largest", [(2, 10000, 2000, True), (4, 2100, 512, True), (2, 2100, 128, False),
+                                           (1, 300, 300, True), (3, 32768, 2048, False), (8, 64, 1, True)])
+def test_topk_rows_matches_torch(R, n, k, largest):
+    """csrc/vision.hip topk_rows_kernel vs torch.topk: identical values; indices point at
+    those values, are distinct, and order equal values by lower index (ties forced by
+    -inf padding / repeated keys)."""
+    from mxtrain.ops.vision import topk_rows
+    g = torch.Generator(device="cuda").manual_seed(n + k)
+    x = torch.rand(R, n, device="cuda", generator=g)
+    x[:, ::7] = -float("inf") if largest else float("inf")     # many exact ties
+    x[:, 1::5] = 0.5                                            # ties inside the selection
+    v, i = topk_rows(x, k, largest=largest)
+    rv, _ = x.topk(k, dim=1, largest=largest)
+    torch.cuda.synchronize()
+    assert torch.equal(v, rv)
+    assert torch.equal(torch.gather(x, 1, i), v)
+    for r in range(R):
+        assert i[r].unique().numel() == k
+        # equal values: lower index first
+        same = v[r, 1:] == v[r, :-1]
+        assert bool((i[r, 1:][same] > i[r, :-1][same]).all())
