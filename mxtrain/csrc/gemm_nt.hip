@@ -133,6 +133,97 @@ __device__ __forceinline__ void dma16s(const void* sbase, uint32_t voff, uint32_
                :: "v"(voff), "s"(sbase), "s"(lds_base) : "memory", "m0");
 }
 
+// ---- epilogue: lane holds C[m0 + 16 (FM wm + s) + i][n0 + 16 (FN wn + u) + 4 G + e].
+// Elementwise math runs in that layout; each pair of 16-column subtiles (u0, u1) is then
+// re-dealt with one permlane32 + one permlane16 swap per dword so lane G holds 8
+// consecutive columns 32 up + 8 G .. +7 of its row: 16-B stores, one wave instruction =
+// 16 rows x 64 B (the 8-B / 32-B-segment stores made the epilogue a quarter of the tile
+// time -- in-kernel stamps, scripts/gemm_stamps.py)
+template <int WM, int WN, int FM, int FN, int EPI>
+__device__ __forceinline__ void epilogue(const Args& g, f32x4 (&acc)[FM][FN], int tm, int m0, int n0, int wave,
+                                         int lane) {
+  const int G = lane >> 4, i = lane & 15;
+  const int wm = wave / WN, wn = wave % WN;
+  const int row0 = m0 + 16 * FM * wm + i;
+  const int colw = n0 + 16 * FN * wn;            // the wave's first column
+  const int col0 = colw + 4 * G;                 // this lane's first column, MFMA layout
+  float bias[FN][4];
+  if constexpr (EPI == 1 || EPI == 2) {
+#pragma unroll
+    for (int u = 0; u < FN; ++u) {
+      const uint2 bv = *reinterpret_cast<const uint2*>(g.bias + col0 + 16 * u);
+      bias[u][0] = lo_bf(bv.x); bias[u][1] = hi_bf(bv.x);
+      bias[u][2] = lo_bf(bv.y); bias[u][3] = hi_bf(bv.y);
+    }
+  }
+  float csum[FN][4];
+  if constexpr (EPI == 3) {
+#pragma unroll
+    for (int u = 0; u < FN; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) csum[u][e] = 0.f;
+  }
+  static_assert(FN % 2 == 0, "the 16-B store re-deal pairs subtiles");
+#pragma unroll
+  for (int s = 0; s < FM; ++s) {
+    const size_t r = (size_t)(row0 + 16 * s);
+    uint16_t* crow = g.c + r * g.ldc + colw + 8 * G;
+#pragma unroll
+    for (int up = 0; up < FN / 2; ++up) {
+      uint32_t c[2][2], h[2][2];
+      if constexpr (EPI == 3) {   // aux (pre-activation) read as 16 B, re-dealt to the MFMA layout
+        const uint4 hv = *reinterpret_cast<const uint4*>(g.aux + r * g.ldx + colw + 32 * up + 8 * G);
+        h[0][0] = hv.x; h[0][1] = hv.y; h[1][0] = hv.z; h[1][1] = hv.w;
+        undeal(h[0][0], h[0][1], h[1][0], h[1][1]);
+      }
+#pragma unroll
+      for (int hlf = 0; hlf < 2; ++hlf) {
+        const int u = 2 * up + hlf;
+        float v[4] = {acc[s][u][0], acc[s][u][1], acc[s][u][2], acc[s][u][3]};
+        if constexpr (EPI == 1 || EPI == 2) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += bias[u][e];
+        }
+        if constexpr (EPI == 2) {
+          h[hlf][0] = pack2(v[0], v[1]);
+          h[hlf][1] = pack2(v[2], v[3]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
+        }
+        if constexpr (EPI == 3) {
+          const float hx[4] = {lo_bf(h[hlf][0]), hi_bf(h[hlf][0]), lo_bf(h[hlf][1]), hi_bf(h[hlf][1])};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] *= gelu_tanh_grad(hx[e]);
+            csum[u][e] += v[e];
+          }
+        }
+        c[hlf][0] = pack2(v[0], v[1]);
+        c[hlf][1] = pack2(v[2], v[3]);
+      }
+      if constexpr (EPI == 2) {
+        deal(h[0][0], h[0][1], h[1][0], h[1][1]);
+        *reinterpret_cast<uint4*>(g.aux + r * g.ldx + colw + 32 * up + 8 * G) =
+            make_uint4(h[0][0], h[0][1], h[1][0], h[1][1]);
+      }
+      deal(c[0][0], c[0][1], c[1][0], c[1][1]);
+      *reinterpret_cast<uint4*>(crow + 32 * up) = make_uint4(c[0][0], c[0][1], c[1][0], c[1][1]);
+    }
+  }
+  if constexpr (EPI == 3) {
+    // column sums of this wave's 16 FM rows: over the 16 lanes of a row (i), lane i == 0
+    // of each G writes 4 consecutive columns
+    float* prow = g.part + (size_t)(tm * WM + wm) * g.N + col0;
+#pragma unroll
+    for (int u = 0; u < FN; ++u) {
+      float t[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[e] = dpp_rowsum16(csum[u][e]);
+      if (i == 0) *reinterpret_cast<float4*>(prow + 16 * u) = make_float4(t[0], t[1], t[2], t[3]);
+    }
+  }
+}
+
 // STAMP (diagnostic build, mx_gemm_nt_stamps only): lane 0 of wave 0 records s_memtime /
 // s_memrealtime at tile start, after the first K-step's data landed, after the main loop
 // and after the epilogue into g.part ([tile][8] uint64); no output value depends on them
@@ -314,90 +405,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_nt_kernel(const Args 
   }
 
   stamp(2);
-  // ---- epilogue: lane holds C[m0 + 16 (FM wm + s) + i][n0 + 16 (FN wn + u) + 4 G + e].
-  // Elementwise math runs in that layout; each pair of 16-column subtiles (u0, u1) is then
-  // re-dealt with one permlane32 + one permlane16 swap per dword so lane G holds 8
-  // consecutive columns 32 up + 8 G .. +7 of its row: 16-B stores, one wave instruction =
-  // 16 rows x 64 B (the 8-B / 32-B-segment stores made the epilogue a quarter of the tile
-  // time -- in-kernel stamps, scripts/gemm_stamps.py)
-  const int row0 = m0 + 16 * FM * wm + i;
-  const int colw = n0 + 16 * FN * wn;            // the wave's first column
-  const int col0 = colw + 4 * G;                 // this lane's first column, MFMA layout
-  float bias[FN][4];
-  if constexpr (EPI == 1 || EPI == 2) {
-#pragma unroll
-    for (int u = 0; u < FN; ++u) {
-      const uint2 bv = *reinterpret_cast<const uint2*>(g.bias + col0 + 16 * u);
-      bias[u][0] = lo_bf(bv.x); bias[u][1] = hi_bf(bv.x);
-      bias[u][2] = lo_bf(bv.y); bias[u][3] = hi_bf(bv.y);
-    }
-  }
-  float csum[FN][4];
-  if constexpr (EPI == 3) {
-#pragma unroll
-    for (int u = 0; u < FN; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) csum[u][e] = 0.f;
-  }
-  static_assert(FN % 2 == 0, "the 16-B store re-deal pairs subtiles");
-#pragma unroll
-  for (int s = 0; s < FM; ++s) {
-    const size_t r = (size_t)(row0 + 16 * s);
-    uint16_t* crow = g.c + r * g.ldc + colw + 8 * G;
-#pragma unroll
-    for (int up = 0; up < FN / 2; ++up) {
-      uint32_t c[2][2], h[2][2];
-      if constexpr (EPI == 3) {   // aux (pre-activation) read as 16 B, re-dealt to the MFMA layout
-        const uint4 hv = *reinterpret_cast<const uint4*>(g.aux + r * g.ldx + colw + 32 * up + 8 * G);
-        h[0][0] = hv.x; h[0][1] = hv.y; h[1][0] = hv.z; h[1][1] = hv.w;
-        undeal(h[0][0], h[0][1], h[1][0], h[1][1]);
-      }
-#pragma unroll
-      for (int hlf = 0; hlf < 2; ++hlf) {
-        const int u = 2 * up + hlf;
-        float v[4] = {acc[s][u][0], acc[s][u][1], acc[s][u][2], acc[s][u][3]};
-        if constexpr (EPI == 1 || EPI == 2) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += bias[u][e];
-        }
-        if constexpr (EPI == 2) {
-          h[hlf][0] = pack2(v[0], v[1]);
-          h[hlf][1] = pack2(v[2], v[3]);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
-        }
-        if constexpr (EPI == 3) {
-          const float hx[4] = {lo_bf(h[hlf][0]), hi_bf(h[hlf][0]), lo_bf(h[hlf][1]), hi_bf(h[hlf][1])};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[e] *= gelu_tanh_grad(hx[e]);
-            csum[u][e] += v[e];
-          }
-        }
-        c[hlf][0] = pack2(v[0], v[1]);
-        c[hlf][1] = pack2(v[2], v[3]);
-      }
-      if constexpr (EPI == 2) {
-        deal(h[0][0], h[0][1], h[1][0], h[1][1]);
-        *reinterpret_cast<uint4*>(g.aux + r * g.ldx + colw + 32 * up + 8 * G) =
-            make_uint4(h[0][0], h[0][1], h[1][0], h[1][1]);
-      }
-      deal(c[0][0], c[0][1], c[1][0], c[1][1]);
-      *reinterpret_cast<uint4*>(crow + 32 * up) = make_uint4(c[0][0], c[0][1], c[1][0], c[1][1]);
-    }
-  }
-  if constexpr (EPI == 3 && !STAMP) {
-    // column sums of this wave's 16 FM rows: over the 16 lanes of a row (i), lane i == 0
-    // of each G writes 4 consecutive columns
-    float* prow = g.part + (size_t)(tm * WM + wm) * g.N + col0;
-#pragma unroll
-    for (int u = 0; u < FN; ++u) {
-      float t[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) t[e] = dpp_rowsum16(csum[u][e]);
-      if (i == 0) *reinterpret_cast<float4*>(prow + 16 * u) = make_float4(t[0], t[1], t[2], t[3]);
-    }
-  }
+  epilogue<WM, WN, FM, FN, EPI>(g, acc, tm, m0, n0, wave, lane);
   if constexpr (STAMP) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -419,6 +427,165 @@ int launch(Args a, int M, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+
+// ============================================================================ 8-phase 256 x 256
+// Forward GEMM (B = W [N][K], K contiguous) at 256 x 256 x BK 64 with a phase-split K loop
+// (cdna_hip_programming.md §5 "The 256² 8-phase template": counted vmcnt never 0 in the
+// loop, raw barriers, fragment reads + one half-tile of LDS-DMA + 16 MFMAs per phase,
+// s_setprio around the MFMAs), with this file's own half-tile schedule:
+//   8 waves 2 (M) x 4 (N), each 128 x 64 (FM 8 x FN 4 16x16 subtiles: the epilogue above);
+//   two K-tile buffers of four 16-KiB half-tiles: H0 / H1 = A rows 0-127 / 128-255,
+//   H2 / H3 = B rows (output columns) 0-127 / 128-255; wave (wm, wn) reads A half wm and
+//   B half wn >> 1; every half-tile is 16 1-KiB pieces, 2 per wave.
+// Four phases per K-tile t (buffer t & 1), 16 MFMAs each (64 x 32 quadrant x K 64):
+//   q0  [wait + barrier]  read a = A rows 0-63, b0 = B cols 0-31     issue A(t+1) H0   MFMA a  x b0
+//   q1                    read b1 = B cols 32-63                      issue A(t+1) H1   MFMA a  x b1
+//   q2  [barrier]         read a = A rows 64-127                      issue B(t+2) H2   MFMA a  x b1
+//   q3                    (no reads)                                  issue B(t+2) H3   MFMA a  x b0
+// RAW: at q0 of tile t a wave's outstanding DMAs are, oldest first, ... A(t) H0 H1, then
+// B(t+1) H2 H3 (issued in tile t-1's q2, q3; B(t) two tiles earlier): vmcnt(4) (vmcnt(0)
+// when there is no tile t+1), then the barrier publishes every wave's pieces.
+// WAR: A of a buffer is last read at q2 and restaged at the next tile's q0 / q1 (behind the
+// q0 barrier); B is last read at q1 (b0 stays in registers for q3) and restaged at q2 / q3
+// (behind the q2 barrier).
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_p8_kernel(const Args g) {
+  constexpr int WM = 2, WN = 4, FM = 8, FN = 4, RA = 128;
+  constexpr int HALF = 128 * RA, SLOT = 4 * HALF;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = g.gm * g.tiles_n;
+  const int grp = wg / per_group, rem = wg - grp * per_group;
+  const int tm = grp * g.gm + rem % g.gm, tn = rem / g.gm;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int nk = g.K / 64;
+
+  // LDS-DMA: piece p = 2 wave + j covers half-tile rows 8p .. 8p + 7; lane -> row 8p + lane / 8,
+  // physical chunk lane % 8 <- logical chunk (lane % 8) ^ (row & 7), row & 7 = lane / 8
+  uint32_t voA[2], voB[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * (2 * wave + j) + (lane >> 3);
+    const int ch = (lane & 7) ^ (lane >> 3);
+    voA[j] = (uint32_t)(row * g.lda + 8 * ch) * 2u;
+    voB[j] = (uint32_t)(row * g.ldb + 8 * ch) * 2u;
+  }
+  const char* baseA = reinterpret_cast<const char*>(g.a + (size_t)m0 * g.lda);
+  const char* baseB = reinterpret_cast<const char*>(g.b + (size_t)n0 * g.ldb);
+  const size_t halfA = (size_t)128 * g.lda * 2, halfB = (size_t)128 * g.ldb * 2;
+  const uint32_t lds0 = lds_addr(smem);
+  const uint32_t ldsw = __builtin_amdgcn_readfirstlane(lds0 + 2 * wave * 1024);
+  auto issue = [&](auto hc, int t) __attribute__((always_inline)) {
+    constexpr int H = decltype(hc)::value;
+    if (t >= nk) return;
+    const uint32_t l = ldsw + (t & 1) * SLOT + H * HALF;
+    if constexpr (H < 2) {
+      const char* b = baseA + H * halfA + (size_t)t * 128;
+      dma16s(b, voA[0], l);
+      dma16s(b, voA[1], l + 1024);
+    } else {
+      const char* b = baseB + (H - 2) * halfB + (size_t)t * 128;
+      dma16s(b, voB[0], l);
+      dma16s(b, voB[1], l + 1024);
+    }
+  };
+
+  // fragment reads: lane (G, i) reads row i of a 16-row subtile, k 8G .. 8G + 7 (+ 32 kk)
+  const int G = lane >> 4, i = lane & 15;
+  const int wm = wave / WN, wn = wave % WN;
+  const int cA0 = 16 * ((0 + G) ^ (i & 7)), cA1 = 16 * ((4 + G) ^ (i & 7));
+  const int offA = wm * HALF + i * RA;                       // + (64 ah + 16 s) RA
+  const int offB = 2 * HALF + (wn >> 1) * HALF + ((wn & 1) * 64 + i) * RA;   // + (32 bh + 16 u) RA
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int s = 0; s < FM; ++s)
+#pragma unroll
+    for (int u = 0; u < FN; ++u) acc[s][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(std::integral_constant<int, 2>{}, 0);
+  issue(std::integral_constant<int, 3>{}, 0);
+  issue(std::integral_constant<int, 0>{}, 0);
+  issue(std::integral_constant<int, 1>{}, 0);
+  issue(std::integral_constant<int, 2>{}, 1);
+  issue(std::integral_constant<int, 3>{}, 1);
+
+  bf16x8 xa[4][2], wb0[2][2], wb1[2][2];
+  auto read_a = [&](const char* buf, int ah) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      xa[s][0] = lds_read8(buf, offA + (64 * ah + 16 * s) * RA + cA0);
+      xa[s][1] = lds_read8(buf, offA + (64 * ah + 16 * s) * RA + cA1);
+    }
+  };
+  auto read_b = [&](const char* buf, int bh, bf16x8 (&wb)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      wb[u][0] = lds_read8(buf, offB + (32 * bh + 16 * u) * RA + cA0);
+      wb[u][1] = lds_read8(buf, offB + (32 * bh + 16 * u) * RA + cA1);
+    }
+  };
+  auto quad = [&](int ah, int bh, const bf16x8 (&wb)[2][2]) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          acc[4 * ah + s][2 * bh + u] = mfma16(wb[u][kk], xa[s][kk], acc[4 * ah + s][2 * bh + u]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto barrier = []() __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  for (int t0 = 0; t0 < nk; t0 += 2) {
+    static_for<2>([&](auto bc) __attribute__((always_inline)) {
+      constexpr int b = decltype(bc)::value;
+      const int t = t0 + b;
+      if (t >= nk) return;
+      const char* buf = smem + b * SLOT;
+      // q0
+      if (t + 1 < nk) vm_wait<4>();
+      else vm_wait<0>();
+      barrier();
+      issue(std::integral_constant<int, 0>{}, t + 1);
+      read_a(buf, 0);
+      read_b(buf, 0, wb0);
+      quad(0, 0, wb0);
+      // q1
+      issue(std::integral_constant<int, 1>{}, t + 1);
+      read_b(buf, 1, wb1);
+      quad(0, 1, wb1);
+      // q2
+      barrier();
+      issue(std::integral_constant<int, 2>{}, t + 2);
+      read_a(buf, 1);
+      quad(1, 1, wb1);
+      // q3
+      issue(std::integral_constant<int, 3>{}, t + 2);
+      quad(1, 0, wb0);
+    });
+  }
+  epilogue<WM, WN, FM, FN, EPI>(g, acc, tm, m0, n0, wave, lane);
+}
+
+template <int EPI>
+int launch_p8(Args a, int M, hipStream_t stream) {
+  if (M % 256 || a.N % 256 || a.K % 64 || a.K <= 0) return (int)hipErrorInvalidValue;
+  const int tiles_m = M / 256;
+  a.tiles_n = a.N / 256;
+  int gm = 8;
+  while (gm > 1 && tiles_m % gm) gm >>= 1;
+  a.gm = gm;
+  hipLaunchKernelGGL((gemm_p8_kernel<EPI>), dim3(tiles_m * a.tiles_n), dim3(512), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
 // variant -> {BM, BN, rows per column-partial block (16 FM), B may be K-major}
 struct Variant {
   int bm, bn, part_rows, kmajor_ok;
@@ -433,6 +600,7 @@ constexpr Variant kVariants[] = {
     {256, 256, 128, 1},   // 6: as 0 with BK 64 and a 2-slot ring
     {128, 128, 64, 1},    // 7: 8 waves 2 x 4 of 64 x 32, BK 32, 6-slot ring
     {256, 128, 64, 1},    // 8: 8 waves 4 x 2 of 64 x 64, BK 32, 5-slot ring (120 KiB)
+    {256, 256, 128, 0},   // 9: 8-phase 256 x 256 (gemm_p8_kernel); forward only
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -450,6 +618,9 @@ int dispatch(int variant, const Args& a, int M, hipStream_t st) {
     case 6: return launch<BKC, 2, 4, 8, 4, 64, 2, 1, EPI>(a, M, st);
     case 7: return launch<BKC, 2, 4, 4, 2, 32, 6, 1, EPI>(a, M, st);
     case 8: return launch<BKC, 4, 2, 4, 4, 32, 5, 1, EPI>(a, M, st);
+    case 9:
+      if constexpr (BKC && EPI != 3) return launch_p8<EPI>(a, M, st);
+      else return (int)hipErrorInvalidValue;
     default: return (int)hipErrorInvalidValue;
   }
 }
