@@ -564,12 +564,12 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
             float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s_[e], c, -lse2));
             if (CAUSAL && t == tdiag) p = crow(e, 0) > rr ? 0.f : p;
             if (!CAUSAL && tail) p = crow(e, 0) >= lim ? 0.f : p;
-            float x = dp[e] - dl;
-            if (DROP) {
+            float x = dp[e];
+            if (DROP) {   // (keep ? dP : 0) - delta
               const uint32_t mk = elem_keep(wd, 8 * (t & 1), e);
-              x = __uint_as_float((__float_as_uint(x) & mk) | (__float_as_uint(-dl) & ~mk));
+              x = __uint_as_float(__float_as_uint(x) & mk);
             }
-            s_[e] = p * x;   // dS^T (the common 1/(1-p) is in oscale)
+            s_[e] = p * (x - dl);   // dS^T (the common 1/(1-p) is in oscale)
           }
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
@@ -894,17 +894,21 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
         if (diag) p = rr > crow(e, 0) ? 0.f : p;
         if (qtail) p = qsu + crow(e, hh) >= S ? 0.f : p;
         p = key_ok ? p : 0.f;
-        float x = dpacc[e] - dl_e;
+        // dS = P (keep ? dP - delta : -delta) = P ((keep ? dP : 0) - delta); the dropped P is 0
+        // in dV's operand: one sign-extended bit-field extract serves both
+        float x = dpacc[e];
         if (DROP) {
           const uint32_t mk = elem_keep(dm_cur, 8 * ((qsu >> 5) & 1), e);
-          x = __uint_as_float((__float_as_uint(x) & mk) | (__float_as_uint(-dl_e) & ~mk));
+          x = __uint_as_float(__float_as_uint(x) & mk);
+          sacc[e] = __uint_as_float(__float_as_uint(p) & mk);
+        } else {
+          sacc[e] = p;
         }
-        sacc[e] = p;
-        dpacc[e] = p * x;   // dS (1/(1-p) in dkscale)
+        dpacc[e] = p * (x - dl_e);   // dS (1/(1-p) in dkscale)
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 pb = DROP ? pack8_keep(sacc, 8 * s, dm_cur, 8 * ((qsu >> 5) & 1)) : pack8(sacc, 8 * s);
+        const bf16x8 pb = pack8(sacc, 8 * s);
         const bf16x8 db = pack8(dpacc, 8 * s);
         const int rofs = (32 * u + 16 * s) * RB;
 #pragma unroll
