@@ -448,9 +448,11 @@ int launch(Args a, int M, hipStream_t stream) {
 // WAR: A of a buffer is last read at q2 and restaged at the next tile's q0 / q1 (behind the
 // q0 barrier); B is last read at q1 (b0 stays in registers for q3) and restaged at q2 / q3
 // (behind the q2 barrier).
-template <int EPI>
+template <bool BKC, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(const Args g) {
   constexpr int WM = 2, WN = 4, FM = 8, FN = 4, RA = 128;
+  // dgrad (!BKC): B = W [K][N], N contiguous -> each B half-tile is the [64 k][128 n] image
+  // (256-B k-rows, 16-B chunks XOR-swizzled per k-row by gsw) read with transposed reads
   constexpr int HALF = 128 * RA, SLOT = 4 * HALF;
   __shared__ __attribute__((aligned(1024))) char smem[2 * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -469,11 +471,17 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(const Args g) {
     const int row = 8 * (2 * wave + j) + (lane >> 3);
     const int ch = (lane & 7) ^ (lane >> 3);
     voA[j] = (uint32_t)(row * g.lda + 8 * ch) * 2u;
-    voB[j] = (uint32_t)(row * g.ldb + 8 * ch) * 2u;
+    if constexpr (BKC) {
+      voB[j] = (uint32_t)(row * g.ldb + 8 * ch) * 2u;
+    } else {   // piece p covers k-rows 4p .. 4p + 3: lane -> k-row lane / 16, physical chunk lane % 16
+      const int k = 4 * (2 * wave + j) + (lane >> 4);
+      voB[j] = (uint32_t)(k * g.ldb + 8 * pchunk(k, lane & 15)) * 2u;
+    }
   }
   const char* baseA = reinterpret_cast<const char*>(g.a + (size_t)m0 * g.lda);
-  const char* baseB = reinterpret_cast<const char*>(g.b + (size_t)n0 * g.ldb);
-  const size_t halfA = (size_t)128 * g.lda * 2, halfB = (size_t)128 * g.ldb * 2;
+  const char* baseB = reinterpret_cast<const char*>(BKC ? g.b + (size_t)n0 * g.ldb : g.b + n0);
+  const size_t halfA = (size_t)128 * g.lda * 2, halfB = BKC ? (size_t)128 * g.ldb * 2 : (size_t)128 * 2;
+  const size_t stepB = BKC ? (size_t)128 : (size_t)64 * g.ldb * 2;   // bytes per K-tile
   const uint32_t lds0 = lds_addr(smem);
   const uint32_t ldsw = __builtin_amdgcn_readfirstlane(lds0 + 2 * wave * 1024);
   auto issue = [&](auto hc, int t) __attribute__((always_inline)) {
@@ -485,7 +493,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(const Args g) {
       dma16s(b, voA[0], l);
       dma16s(b, voA[1], l + 1024);
     } else {
-      const char* b = baseB + (H - 2) * halfB + (size_t)t * 128;
+      const char* b = baseB + (H - 2) * halfB + (size_t)t * stepB;
       dma16s(b, voB[0], l);
       dma16s(b, voB[1], l + 1024);
     }
@@ -497,6 +505,12 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(const Args g) {
   const int cA0 = 16 * ((0 + G) ^ (i & 7)), cA1 = 16 * ((4 + G) ^ (i & 7));
   const int offA = wm * HALF + i * RA;                       // + (64 ah + 16 s) RA
   const int offB = 2 * HALF + (wn >> 1) * HALF + ((wn & 1) * 64 + i) * RA;   // + (32 bh + 16 u) RA
+  // K-major image: lane (G, i) reads k-rows 8G + (i >> 2) (+4, +32 kk) of 16-column subtile
+  // uu = 4 (wn & 1) + 2 bh + u (gemm.hip's transposed-read scheme, 256-B rows)
+  const int krow = 8 * G + (i >> 2);
+  auto offBk = [&](int uu) __attribute__((always_inline)) {
+    return 2 * HALF + (wn >> 1) * HALF + krow * 256 + ((((uu) ^ gsw(krow)) << 1) | ((i & 3) >> 1)) * 16 + (i & 1) * 8;
+  };
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -522,8 +536,15 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(const Args g) {
   auto read_b = [&](const char* buf, int bh, bf16x8 (&wb)[2][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      wb[u][0] = lds_read8(buf, offB + (32 * bh + 16 * u) * RA + cA0);
-      wb[u][1] = lds_read8(buf, offB + (32 * bh + 16 * u) * RA + cA1);
+      if constexpr (BKC) {
+        wb[u][0] = lds_read8(buf, offB + (32 * bh + 16 * u) * RA + cA0);
+        wb[u][1] = lds_read8(buf, offB + (32 * bh + 16 * u) * RA + cA1);
+      } else {
+        const int o = offBk(4 * (wn & 1) + 2 * bh + u);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          wb[u][kk] = cat(tr_read(buf, o + 32 * 256 * kk), tr_read(buf, o + 32 * 256 * kk + 4 * 256));
+      }
     }
   };
   auto quad = [&](int ah, int bh, const bf16x8 (&wb)[2][2]) __attribute__((always_inline)) {
@@ -574,7 +595,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(const Args g) {
   epilogue<WM, WN, FM, FN, EPI>(g, acc, tm, m0, n0, wave, lane);
 }
 
-template <int EPI>
+template <bool BKC, int EPI>
 int launch_p8(Args a, int M, hipStream_t stream) {
   if (M % 256 || a.N % 256 || a.K % 64 || a.K <= 0) return (int)hipErrorInvalidValue;
   const int tiles_m = M / 256;
@@ -582,7 +603,7 @@ int launch_p8(Args a, int M, hipStream_t stream) {
   int gm = 8;
   while (gm > 1 && tiles_m % gm) gm >>= 1;
   a.gm = gm;
-  hipLaunchKernelGGL((gemm_p8_kernel<EPI>), dim3(tiles_m * a.tiles_n), dim3(512), 0, stream, a);
+  hipLaunchKernelGGL((gemm_p8_kernel<BKC, EPI>), dim3(tiles_m * a.tiles_n), dim3(512), 0, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -600,7 +621,7 @@ constexpr Variant kVariants[] = {
     {256, 256, 128, 1},   // 6: as 0 with BK 64 and a 2-slot ring
     {128, 128, 64, 1},    // 7: 8 waves 2 x 4 of 64 x 32, BK 32, 6-slot ring
     {256, 128, 64, 1},    // 8: 8 waves 4 x 2 of 64 x 64, BK 32, 5-slot ring (120 KiB)
-    {256, 256, 128, 0},   // 9: 8-phase 256 x 256 (gemm_p8_kernel); forward only
+    {256, 256, 128, 1},   // 9: 8-phase 256 x 256 (gemm_p8_kernel), 2 x 64 KiB
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -618,9 +639,7 @@ int dispatch(int variant, const Args& a, int M, hipStream_t st) {
     case 6: return launch<BKC, 2, 4, 8, 4, 64, 2, 1, EPI>(a, M, st);
     case 7: return launch<BKC, 2, 4, 4, 2, 32, 6, 1, EPI>(a, M, st);
     case 8: return launch<BKC, 4, 2, 4, 4, 32, 5, 1, EPI>(a, M, st);
-    case 9:
-      if constexpr (BKC && EPI != 3) return launch_p8<EPI>(a, M, st);
-      else return (int)hipErrorInvalidValue;
+    case 9: return launch_p8<BKC, EPI>(a, M, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -598,7 +598,7 @@ def test_gemm_p8_k_steps(K):
     _close(out, ref, 2e-2, 1e-2, "y")
 
 
-@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("gelu", [False, True])
 def test_gemm_nt_dgrad_epilogues(variant, gelu):
     """dgrad dx = dy w (w K-major) and the fused GeLU' + bias-gradient epilogue."""
