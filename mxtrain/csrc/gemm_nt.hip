@@ -448,7 +448,7 @@ int launch(Args a, int M, hipStream_t stream) {
 // WAR: A of a buffer is last read at q2 and restaged at the next tile's q0 / q1 (behind the
 // q0 barrier); B is last read at q1 (b0 stays in registers for q3) and restaged at q2 / q3
 // (behind the q2 barrier).
-template <bool BKC, int EPI>
+template <bool BKC, int EPI, int SCHED>
 __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(const Args g) {
   constexpr int WM = 2, WN = 4, FM = 8, FN = 4, RA = 128;
   // dgrad (!BKC): B = W [K][N], N contiguous -> each B half-tile is the [64 k][128 n] image
@@ -518,19 +518,28 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(const Args g) {
 #pragma unroll
     for (int u = 0; u < FN; ++u) acc[s][u] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  issue(std::integral_constant<int, 2>{}, 0);
-  issue(std::integral_constant<int, 3>{}, 0);
-  issue(std::integral_constant<int, 0>{}, 0);
-  issue(std::integral_constant<int, 1>{}, 0);
-  issue(std::integral_constant<int, 2>{}, 1);
-  issue(std::integral_constant<int, 3>{}, 1);
+  if constexpr (SCHED == 0) {
+    issue(std::integral_constant<int, 2>{}, 0);
+    issue(std::integral_constant<int, 3>{}, 0);
+    issue(std::integral_constant<int, 0>{}, 0);
+    issue(std::integral_constant<int, 1>{}, 0);
+    issue(std::integral_constant<int, 2>{}, 1);
+    issue(std::integral_constant<int, 3>{}, 1);
+  } else {   // tiles 0 and 1 whole
+    static_for<2>([&](auto tc) __attribute__((always_inline)) {
+      issue(std::integral_constant<int, 0>{}, decltype(tc)::value);
+      issue(std::integral_constant<int, 1>{}, decltype(tc)::value);
+      issue(std::integral_constant<int, 2>{}, decltype(tc)::value);
+      issue(std::integral_constant<int, 3>{}, decltype(tc)::value);
+    });
+  }
 
-  bf16x8 xa[4][2], wb0[2][2], wb1[2][2];
-  auto read_a = [&](const char* buf, int ah) __attribute__((always_inline)) {
+  bf16x8 xa[4][2], xa1[4][2], wb0[2][2], wb1[2][2];
+  auto read_a = [&](const char* buf, int ah, bf16x8 (&x)[4][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      xa[s][0] = lds_read8(buf, offA + (64 * ah + 16 * s) * RA + cA0);
-      xa[s][1] = lds_read8(buf, offA + (64 * ah + 16 * s) * RA + cA1);
+      x[s][0] = lds_read8(buf, offA + (64 * ah + 16 * s) * RA + cA0);
+      x[s][1] = lds_read8(buf, offA + (64 * ah + 16 * s) * RA + cA1);
     }
   };
   auto read_b = [&](const char* buf, int bh, bf16x8 (&wb)[2][2]) __attribute__((always_inline)) {
@@ -547,7 +556,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(const Args g) {
       }
     }
   };
-  auto quad = [&](int ah, int bh, const bf16x8 (&wb)[2][2]) __attribute__((always_inline)) {
+  auto quad = [&](int ah, int bh, const bf16x8 (&x)[4][2], const bf16x8 (&wb)[2][2]) __attribute__((always_inline)) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -555,7 +564,7 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(const Args g) {
       for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int u = 0; u < 2; ++u)
-          acc[4 * ah + s][2 * bh + u] = mfma16(wb[u][kk], xa[s][kk], acc[4 * ah + s][2 * bh + u]);
+          acc[4 * ah + s][2 * bh + u] = mfma16(wb[u][kk], x[s][kk], acc[4 * ah + s][2 * bh + u]);
     __builtin_amdgcn_s_setprio(0);
   };
   auto barrier = []() __attribute__((always_inline)) {
@@ -570,32 +579,56 @@ __global__ __launch_bounds__(512, 1) void gemm_p8_kernel(const Args g) {
       const int t = t0 + b;
       if (t >= nk) return;
       const char* buf = smem + b * SLOT;
-      // q0
-      if (t + 1 < nk) vm_wait<4>();
-      else vm_wait<0>();
-      barrier();
-      issue(std::integral_constant<int, 0>{}, t + 1);
-      read_a(buf, 0);
-      read_b(buf, 0, wb0);
-      quad(0, 0, wb0);
-      // q1
-      issue(std::integral_constant<int, 1>{}, t + 1);
-      read_b(buf, 1, wb1);
-      quad(0, 1, wb1);
-      // q2
-      barrier();
-      issue(std::integral_constant<int, 2>{}, t + 2);
-      read_a(buf, 1);
-      quad(1, 1, wb1);
-      // q3
-      issue(std::integral_constant<int, 3>{}, t + 2);
-      quad(1, 0, wb0);
+      if constexpr (SCHED == 0) {
+        // q0
+        if (t + 1 < nk) vm_wait<4>();
+        else vm_wait<0>();
+        barrier();
+        issue(std::integral_constant<int, 0>{}, t + 1);
+        read_a(buf, 0, xa);
+        read_b(buf, 0, wb0);
+        quad(0, 0, xa, wb0);
+        // q1
+        issue(std::integral_constant<int, 1>{}, t + 1);
+        read_b(buf, 1, wb1);
+        quad(0, 1, xa, wb1);
+        // q2
+        barrier();
+        issue(std::integral_constant<int, 2>{}, t + 2);
+        read_a(buf, 1, xa);
+        quad(1, 1, xa, wb1);
+        // q3
+        issue(std::integral_constant<int, 3>{}, t + 2);
+        quad(1, 0, xa, wb0);
+      } else {
+        // SCHED 1: every fragment of the tile is read at q0 (the first quadrant's 12 first),
+        // so the buffer is free after q1's barrier and tile t + 2 streams into it during
+        // q1 .. q3: a DMA has a whole K-tile of slack before its q0 (vmcnt(8): tile t + 1's
+        // pieces are all older than tile t + 2's)
+        if (t + 1 < nk) vm_wait<8>();
+        else vm_wait<0>();
+        barrier();
+        read_a(buf, 0, xa);
+        read_b(buf, 0, wb0);
+        read_b(buf, 1, wb1);
+        read_a(buf, 1, xa1);
+        quad(0, 0, xa, wb0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier();   // every wave's reads of this buffer are done
+        issue(std::integral_constant<int, 0>{}, t + 2);
+        issue(std::integral_constant<int, 1>{}, t + 2);
+        quad(0, 1, xa, wb1);
+        issue(std::integral_constant<int, 2>{}, t + 2);
+        quad(1, 1, xa1, wb1);
+        issue(std::integral_constant<int, 3>{}, t + 2);
+        quad(1, 0, xa1, wb0);
+      }
     });
   }
   epilogue<WM, WN, FM, FN, EPI>(g, acc, tm, m0, n0, wave, lane);
 }
 
-template <bool BKC, int EPI>
+template <bool BKC, int EPI, int SCHED>
 int launch_p8(Args a, int M, hipStream_t stream) {
   if (M % 256 || a.N % 256 || a.K % 64 || a.K <= 0) return (int)hipErrorInvalidValue;
   const int tiles_m = M / 256;
@@ -603,7 +636,7 @@ int launch_p8(Args a, int M, hipStream_t stream) {
   int gm = 8;
   while (gm > 1 && tiles_m % gm) gm >>= 1;
   a.gm = gm;
-  hipLaunchKernelGGL((gemm_p8_kernel<BKC, EPI>), dim3(tiles_m * a.tiles_n), dim3(512), 0, stream, a);
+  hipLaunchKernelGGL((gemm_p8_kernel<BKC, EPI, SCHED>), dim3(tiles_m * a.tiles_n), dim3(512), 0, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -622,6 +655,7 @@ constexpr Variant kVariants[] = {
     {128, 128, 64, 1},    // 7: 8 waves 2 x 4 of 64 x 32, BK 32, 6-slot ring
     {256, 128, 64, 1},    // 8: 8 waves 4 x 2 of 64 x 64, BK 32, 5-slot ring (120 KiB)
     {256, 256, 128, 1},   // 9: 8-phase 256 x 256 (gemm_p8_kernel), 2 x 64 KiB
+    {256, 256, 128, 1},   // 10: as 9, every fragment read at q0, next-but-one tile streamed during q1 .. q3
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -639,7 +673,8 @@ int dispatch(int variant, const Args& a, int M, hipStream_t st) {
     case 6: return launch<BKC, 2, 4, 8, 4, 64, 2, 1, EPI>(a, M, st);
     case 7: return launch<BKC, 2, 4, 4, 2, 32, 6, 1, EPI>(a, M, st);
     case 8: return launch<BKC, 4, 2, 4, 4, 32, 5, 1, EPI>(a, M, st);
-    case 9: return launch_p8<BKC, EPI>(a, M, st);
+    case 9: return launch_p8<BKC, EPI, 0>(a, M, st);
+    case 10: return launch_p8<BKC, EPI, 1>(a, M, st);
     default: return (int)hipErrorInvalidValue;
   }
 }
