@@ -428,218 +428,6 @@ int launch(Args a, int M, hipStream_t stream) {
 }
 
 
-// ============================================================================ 8-phase 256 x 256
-// Forward GEMM (B = W [N][K], K contiguous) at 256 x 256 x BK 64 with a phase-split K loop
-// (cdna_hip_programming.md §5 "The 256² 8-phase template": counted vmcnt never 0 in the
-// loop, raw barriers, fragment reads + one half-tile of LDS-DMA + 16 MFMAs per phase,
-// s_setprio around the MFMAs), with this file's own half-tile schedule:
-//   8 waves 2 (M) x 4 (N), each 128 x 64 (FM 8 x FN 4 16x16 subtiles: the epilogue above);
-//   two K-tile buffers of four 16-KiB half-tiles: H0 / H1 = A rows 0-127 / 128-255,
-//   H2 / H3 = B rows (output columns) 0-127 / 128-255; wave (wm, wn) reads A half wm and
-//   B half wn >> 1; every half-tile is 16 1-KiB pieces, 2 per wave.
-// Four phases per K-tile t (buffer t & 1), 16 MFMAs each (64 x 32 quadrant x K 64):
-//   q0  [wait + barrier]  read a = A rows 0-63, b0 = B cols 0-31     issue A(t+1) H0   MFMA a  x b0
-//   q1                    read b1 = B cols 32-63                      issue A(t+1) H1   MFMA a  x b1
-//   q2  [barrier]         read a = A rows 64-127                      issue B(t+2) H2   MFMA a  x b1
-//   q3                    (no reads)                                  issue B(t+2) H3   MFMA a  x b0
-// RAW: at q0 of tile t a wave's outstanding DMAs are, oldest first, ... A(t) H0 H1, then
-// B(t+1) H2 H3 (issued in tile t-1's q2, q3; B(t) two tiles earlier): vmcnt(4) (vmcnt(0)
-// when there is no tile t+1), then the barrier publishes every wave's pieces.
-// WAR: A of a buffer is last read at q2 and restaged at the next tile's q0 / q1 (behind the
-// q0 barrier); B is last read at q1 (b0 stays in registers for q3) and restaged at q2 / q3
-// (behind the q2 barrier).
-template <bool BKC, int EPI, int SCHED>
-__global__ __launch_bounds__(512, 1) void gemm_p8_kernel(const Args g) {
-  constexpr int WM = 2, WN = 4, FM = 8, FN = 4, RA = 128;
-  // dgrad (!BKC): B = W [K][N], N contiguous -> each B half-tile is the [64 k][128 n] image
-  // (256-B k-rows, 16-B chunks XOR-swizzled per k-row by gsw) read with transposed reads
-  constexpr int HALF = 128 * RA, SLOT = 4 * HALF;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * SLOT];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int per_group = g.gm * g.tiles_n;
-  const int grp = wg / per_group, rem = wg - grp * per_group;
-  const int tm = grp * g.gm + rem % g.gm, tn = rem / g.gm;
-  const int m0 = tm * 256, n0 = tn * 256;
-  const int nk = g.K / 64;
-
-  // LDS-DMA: piece p = 2 wave + j covers half-tile rows 8p .. 8p + 7; lane -> row 8p + lane / 8,
-  // physical chunk lane % 8 <- logical chunk (lane % 8) ^ (row & 7), row & 7 = lane / 8
-  uint32_t voA[2], voB[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = 8 * (2 * wave + j) + (lane >> 3);
-    const int ch = (lane & 7) ^ (lane >> 3);
-    voA[j] = (uint32_t)(row * g.lda + 8 * ch) * 2u;
-    if constexpr (BKC) {
-      voB[j] = (uint32_t)(row * g.ldb + 8 * ch) * 2u;
-    } else {   // piece p covers k-rows 4p .. 4p + 3: lane -> k-row lane / 16, physical chunk lane % 16
-      const int k = 4 * (2 * wave + j) + (lane >> 4);
-      voB[j] = (uint32_t)(k * g.ldb + 8 * pchunk(k, lane & 15)) * 2u;
-    }
-  }
-  const char* baseA = reinterpret_cast<const char*>(g.a + (size_t)m0 * g.lda);
-  const char* baseB = reinterpret_cast<const char*>(BKC ? g.b + (size_t)n0 * g.ldb : g.b + n0);
-  const size_t halfA = (size_t)128 * g.lda * 2, halfB = BKC ? (size_t)128 * g.ldb * 2 : (size_t)128 * 2;
-  const size_t stepB = BKC ? (size_t)128 : (size_t)64 * g.ldb * 2;   // bytes per K-tile
-  const uint32_t lds0 = lds_addr(smem);
-  const uint32_t ldsw = __builtin_amdgcn_readfirstlane(lds0 + 2 * wave * 1024);
-  auto issue = [&](auto hc, int t) __attribute__((always_inline)) {
-    constexpr int H = decltype(hc)::value;
-    if (t >= nk) return;
-    const uint32_t l = ldsw + (t & 1) * SLOT + H * HALF;
-    if constexpr (H < 2) {
-      const char* b = baseA + H * halfA + (size_t)t * 128;
-      dma16s(b, voA[0], l);
-      dma16s(b, voA[1], l + 1024);
-    } else {
-      const char* b = baseB + (H - 2) * halfB + (size_t)t * stepB;
-      dma16s(b, voB[0], l);
-      dma16s(b, voB[1], l + 1024);
-    }
-  };
-
-  // fragment reads: lane (G, i) reads row i of a 16-row subtile, k 8G .. 8G + 7 (+ 32 kk)
-  const int G = lane >> 4, i = lane & 15;
-  const int wm = wave / WN, wn = wave % WN;
-  const int cA0 = 16 * ((0 + G) ^ (i & 7)), cA1 = 16 * ((4 + G) ^ (i & 7));
-  const int offA = wm * HALF + i * RA;                       // + (64 ah + 16 s) RA
-  const int offB = 2 * HALF + (wn >> 1) * HALF + ((wn & 1) * 64 + i) * RA;   // + (32 bh + 16 u) RA
-  // K-major image: lane (G, i) reads k-rows 8G + (i >> 2) (+4, +32 kk) of 16-column subtile
-  // uu = 4 (wn & 1) + 2 bh + u (gemm.hip's transposed-read scheme, 256-B rows)
-  const int krow = 8 * G + (i >> 2);
-  auto offBk = [&](int uu) __attribute__((always_inline)) {
-    return 2 * HALF + (wn >> 1) * HALF + krow * 256 + ((((uu) ^ gsw(krow)) << 1) | ((i & 3) >> 1)) * 16 + (i & 1) * 8;
-  };
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int s = 0; s < FM; ++s)
-#pragma unroll
-    for (int u = 0; u < FN; ++u) acc[s][u] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if constexpr (SCHED == 0) {
-    issue(std::integral_constant<int, 2>{}, 0);
-    issue(std::integral_constant<int, 3>{}, 0);
-    issue(std::integral_constant<int, 0>{}, 0);
-    issue(std::integral_constant<int, 1>{}, 0);
-    issue(std::integral_constant<int, 2>{}, 1);
-    issue(std::integral_constant<int, 3>{}, 1);
-  } else {   // tiles 0 and 1 whole
-    static_for<2>([&](auto tc) __attribute__((always_inline)) {
-      issue(std::integral_constant<int, 0>{}, decltype(tc)::value);
-      issue(std::integral_constant<int, 1>{}, decltype(tc)::value);
-      issue(std::integral_constant<int, 2>{}, decltype(tc)::value);
-      issue(std::integral_constant<int, 3>{}, decltype(tc)::value);
-    });
-  }
-
-  bf16x8 xa[4][2], xa1[4][2], wb0[2][2], wb1[2][2];
-  auto read_a = [&](const char* buf, int ah, bf16x8 (&x)[4][2]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      x[s][0] = lds_read8(buf, offA + (64 * ah + 16 * s) * RA + cA0);
-      x[s][1] = lds_read8(buf, offA + (64 * ah + 16 * s) * RA + cA1);
-    }
-  };
-  auto read_b = [&](const char* buf, int bh, bf16x8 (&wb)[2][2]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if constexpr (BKC) {
-        wb[u][0] = lds_read8(buf, offB + (32 * bh + 16 * u) * RA + cA0);
-        wb[u][1] = lds_read8(buf, offB + (32 * bh + 16 * u) * RA + cA1);
-      } else {
-        const int o = offBk(4 * (wn & 1) + 2 * bh + u);
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          wb[u][kk] = cat(tr_read(buf, o + 32 * 256 * kk), tr_read(buf, o + 32 * 256 * kk + 4 * 256));
-      }
-    }
-  };
-  auto quad = [&](int ah, int bh, const bf16x8 (&x)[4][2], const bf16x8 (&wb)[2][2]) __attribute__((always_inline)) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-          acc[4 * ah + s][2 * bh + u] = mfma16(wb[u][kk], x[s][kk], acc[4 * ah + s][2 * bh + u]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto barrier = []() __attribute__((always_inline)) {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  for (int t0 = 0; t0 < nk; t0 += 2) {
-    static_for<2>([&](auto bc) __attribute__((always_inline)) {
-      constexpr int b = decltype(bc)::value;
-      const int t = t0 + b;
-      if (t >= nk) return;
-      const char* buf = smem + b * SLOT;
-      if constexpr (SCHED == 0) {
-        // q0
-        if (t + 1 < nk) vm_wait<4>();
-        else vm_wait<0>();
-        barrier();
-        issue(std::integral_constant<int, 0>{}, t + 1);
-        read_a(buf, 0, xa);
-        read_b(buf, 0, wb0);
-        quad(0, 0, xa, wb0);
-        // q1
-        issue(std::integral_constant<int, 1>{}, t + 1);
-        read_b(buf, 1, wb1);
-        quad(0, 1, xa, wb1);
-        // q2
-        barrier();
-        issue(std::integral_constant<int, 2>{}, t + 2);
-        read_a(buf, 1, xa);
-        quad(1, 1, xa, wb1);
-        // q3
-        issue(std::integral_constant<int, 3>{}, t + 2);
-        quad(1, 0, xa, wb0);
-      } else {
-        // SCHED 1: every fragment of the tile is read at q0 (the first quadrant's 12 first),
-        // so the buffer is free after q1's barrier and tile t + 2 streams into it during
-        // q1 .. q3: a DMA has a whole K-tile of slack before its q0 (vmcnt(8): tile t + 1's
-        // pieces are all older than tile t + 2's)
-        if (t + 1 < nk) vm_wait<8>();
-        else vm_wait<0>();
-        barrier();
-        read_a(buf, 0, xa);
-        read_b(buf, 0, wb0);
-        read_b(buf, 1, wb1);
-        read_a(buf, 1, xa1);
-        quad(0, 0, xa, wb0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        barrier();   // every wave's reads of this buffer are done
-        issue(std::integral_constant<int, 0>{}, t + 2);
-        issue(std::integral_constant<int, 1>{}, t + 2);
-        quad(0, 1, xa, wb1);
-        issue(std::integral_constant<int, 2>{}, t + 2);
-        quad(1, 1, xa1, wb1);
-        issue(std::integral_constant<int, 3>{}, t + 2);
-        quad(1, 0, xa1, wb0);
-      }
-    });
-  }
-  epilogue<WM, WN, FM, FN, EPI>(g, acc, tm, m0, n0, wave, lane);
-}
-
-template <bool BKC, int EPI, int SCHED>
-int launch_p8(Args a, int M, hipStream_t stream) {
-  if (M % 256 || a.N % 256 || a.K % 64 || a.K <= 0) return (int)hipErrorInvalidValue;
-  const int tiles_m = M / 256;
-  a.tiles_n = a.N / 256;
-  int gm = 8;
-  while (gm > 1 && tiles_m % gm) gm >>= 1;
-  a.gm = gm;
-  hipLaunchKernelGGL((gemm_p8_kernel<BKC, EPI, SCHED>), dim3(tiles_m * a.tiles_n), dim3(512), 0, stream, a);
-  return (int)hipGetLastError();
-}
-
 // variant -> {BM, BN, rows per column-partial block (16 FM), B may be K-major}
 struct Variant {
   int bm, bn, part_rows, kmajor_ok;
@@ -654,8 +442,6 @@ constexpr Variant kVariants[] = {
     {256, 256, 128, 1},   // 6: as 0 with BK 64 and a 2-slot ring
     {128, 128, 64, 1},    // 7: 8 waves 2 x 4 of 64 x 32, BK 32, 6-slot ring
     {256, 128, 64, 1},    // 8: 8 waves 4 x 2 of 64 x 64, BK 32, 5-slot ring (120 KiB)
-    {256, 256, 128, 1},   // 9: 8-phase 256 x 256 (gemm_p8_kernel), 2 x 64 KiB
-    {256, 256, 128, 1},   // 10: as 9, every fragment read at q0, next-but-one tile streamed during q1 .. q3
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -673,8 +459,6 @@ int dispatch(int variant, const Args& a, int M, hipStream_t st) {
     case 6: return launch<BKC, 2, 4, 8, 4, 64, 2, 1, EPI>(a, M, st);
     case 7: return launch<BKC, 2, 4, 4, 2, 32, 6, 1, EPI>(a, M, st);
     case 8: return launch<BKC, 4, 2, 4, 4, 32, 5, 1, EPI>(a, M, st);
-    case 9: return launch_p8<BKC, EPI, 0>(a, M, st);
-    case 10: return launch_p8<BKC, EPI, 1>(a, M, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

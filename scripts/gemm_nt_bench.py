@@ -75,7 +75,7 @@ def main():
             if gelu:
                 ref = ref * Gm._gelu_grad_ref(hh.float())
         variants = []
-        for v in range(11):
+        for v in range(9):
             bm, bn, _, kok = Gm._nt_tile(v)
             if M % bm or N % bn or (kind.startswith("dg") and not kok):
                 continue
