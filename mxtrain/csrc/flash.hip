@@ -47,6 +47,8 @@
 // 2j at bit sh+j and 2j+1 at bit sh+16+j of a 32-bit word holding two blocks (sh = 0 / 8).
 #include "common.h"
 
+#include <type_traits>
+
 #pragma clang diagnostic ignored "-Winline-asm"  // m0 is clobbered on purpose (dma16 / dma4)
 
 using namespace mx;
@@ -559,17 +561,25 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
           }
           const uint32_t wd = (uint32_t)(dm_cur >> (32 * ((((kv0 >> 5) + t) >> 1) & 1)));
           const int lim = kl - kv0 - 32 * t - 4 * hh;
+          float pv[16];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) pv[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(s_[e], c, -lse2));
+          // (only the diagonal / padded-tail subtile is masked: a wave-uniform branch)
+          if (uni((CAUSAL && t == tdiag) || (!CAUSAL && tail) ? 1 : 0)) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              if (CAUSAL) pv[e] = crow(e, 0) > rr ? 0.f : pv[e];
+              else pv[e] = crow(e, 0) >= lim ? 0.f : pv[e];
+            }
+          }
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
-            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s_[e], c, -lse2));
-            if (CAUSAL && t == tdiag) p = crow(e, 0) > rr ? 0.f : p;
-            if (!CAUSAL && tail) p = crow(e, 0) >= lim ? 0.f : p;
             float x = dp[e];
             if (DROP) {   // (keep ? dP : 0) - delta
               const uint32_t mk = elem_keep(wd, 8 * (t & 1), e);
               x = __uint_as_float(__float_as_uint(x) & mk);
             }
-            s_[e] = p * (x - dl);   // dS^T (the common 1/(1-p) is in oscale)
+            s_[e] = pv[e] * (x - dl);   // dS^T (the common 1/(1-p) is in oscale)
           }
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
@@ -668,7 +678,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
 // PAIR (D = 64): two 4-wave teams as in qmajor; the heavy key block (most query rows, the
 // smallest index under a causal mask) is split between the teams and team 1's partial
 // dK^T / dV^T are summed into team 0's through LDS.
-template <int D, bool CAUSAL, bool DROP, int DP, bool PAIR>
+template <int D, bool CAUSAL, bool DROP, int DP, bool PAIR, bool RAGGED>
 __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_eu(2, 2))) void flash_kmajor_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, int ldq, int ldk, int ldv,
@@ -880,20 +890,34 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
       }
       const bool diag = CAUSAL && qsu == kw0;
       const bool qtail = qsu + 32 > S;
+      // P of the subtile, unmasked; the causal diagonal subtile (wave-uniform branch) and, in
+      // RAGGED launches only, the query tail / invalid keys are zeroed afterwards
+      float pv[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         // row constants of the lane's query rows, 4 consecutive per e >> 2 (one ds_read_b128)
-        float4 lsq, dlq;
-        if ((e & 3) == 0) {
-          lsq = *reinterpret_cast<const float4*>(Lt + 32 * u + 8 * (e >> 2) + 4 * hh);
-          dlq = *reinterpret_cast<const float4*>(Dt + 32 * u + 8 * (e >> 2) + 4 * hh);
-        }
+        float4 lsq;
+        if ((e & 3) == 0) lsq = *reinterpret_cast<const float4*>(Lt + 32 * u + 8 * (e >> 2) + 4 * hh);
         const float lse_e = (e & 3) == 0 ? lsq.x : (e & 3) == 1 ? lsq.y : (e & 3) == 2 ? lsq.z : lsq.w;
+        pv[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[e], c, -lse_e));
+      }
+      if (uni(diag ? 1 : 0)) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) pv[e] = rr > crow(e, 0) ? 0.f : pv[e];
+      }
+      if constexpr (RAGGED) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          if (qtail) pv[e] = qsu + crow(e, hh) >= S ? 0.f : pv[e];
+          pv[e] = key_ok ? pv[e] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        float4 dlq;
+        if ((e & 3) == 0) dlq = *reinterpret_cast<const float4*>(Dt + 32 * u + 8 * (e >> 2) + 4 * hh);
         const float dl_e = (e & 3) == 0 ? dlq.x : (e & 3) == 1 ? dlq.y : (e & 3) == 2 ? dlq.z : dlq.w;
-        float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[e], c, -lse_e));
-        if (diag) p = rr > crow(e, 0) ? 0.f : p;
-        if (qtail) p = qsu + crow(e, hh) >= S ? 0.f : p;
-        p = key_ok ? p : 0.f;
+        const float p = pv[e];
         // dS = P (keep ? dP - delta : -delta) = P ((keep ? dP : 0) - delta); the dropped P is 0
         // in dV's operand: one sign-extended bit-field extract serves both
         float x = dpacc[e];
@@ -1034,10 +1058,20 @@ hipError_t launch_kmajor(bool causal, bool drop, int S, int B, hipStream_t s,
   constexpr bool PAIR = D == 64;
   const int nkb = (S + 127) / 128;
   const dim3 grid((PAIR ? (nkb + 1) / 2 : nkb) * Hkv * B);
-#define MX_KM(C, DR, P)                                                                          \
-  hipLaunchKernelGGL((flash_kmajor_kernel<D, C, DR, P, PAIR>), grid, dim3(PAIR ? 512 : 256), 0, s, \
-                     q, k, v, ldq, ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq, Hkv, \
-                     klen, c, dkscale, dvscale, dbits, NB, NQT)
+  // RAGGED: padded keys (klen) or a sequence that does not fill the last key block; the
+  // common launch (every key valid, S a multiple of 128) carries no per-element key mask
+  const bool ragged = klen != nullptr || S % 128 != 0;
+#define MX_KM(C, DR, P)                                                                                  \
+  do {                                                                                                   \
+    if (ragged)                                                                                          \
+      hipLaunchKernelGGL((flash_kmajor_kernel<D, C, DR, P, PAIR, true>), grid, dim3(PAIR ? 512 : 256), 0, \
+                         s, q, k, v, ldq, ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq,    \
+                         Hkv, klen, c, dkscale, dvscale, dbits, NB, NQT);                                 \
+    else                                                                                                 \
+      hipLaunchKernelGGL((flash_kmajor_kernel<D, C, DR, P, PAIR, false>), grid, dim3(PAIR ? 512 : 256), 0, \
+                         s, q, k, v, ldq, ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq,    \
+                         Hkv, klen, c, dkscale, dvscale, dbits, NB, NQT);                                 \
+  } while (0)
 #define MX_KM_P(P)                                                                   \
   {                                                                                  \
     if (causal) { if (drop) MX_KM(true, true, P); else MX_KM(true, false, P); }      \

@@ -20,17 +20,26 @@ READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
 
 def blobs(db):
     con = sqlite3.connect(db)
-    cols = [r[1] for r in con.execute("pragma table_info(kern_db)")]
-    for row in con.execute("select * from kern_db"):
-        rec = dict(zip(cols, row))
-        blob = rec.get("kernel_blob")
-        if blob is None:
-            continue
-        try:
-            blob = zlib.decompress(blob)
-        except zlib.error:
-            pass
-        yield rec.get("kernel_name") or rec.get("program_name") or "?", blob
+    tables = [r[0] for r in con.execute("select name from sqlite_master where type='table'")]
+    print(f"{db}: tables {tables}")
+    for tab in tables:
+        cols = [r[1] for r in con.execute(f"pragma table_info({tab})")]
+        n = con.execute(f"select count(*) from {tab}").fetchone()[0]
+        print(f"  {tab}: {n} rows, columns {cols}")
+        for row in con.execute(f"select * from {tab}"):
+            rec = dict(zip(cols, row))
+            for k, v in rec.items():
+                if not isinstance(v, (bytes, bytearray)) or len(v) < 64:
+                    continue
+                blob = bytes(v)
+                for dec in (lambda b: zlib.decompress(b), lambda b: zlib.decompress(b, -15), lambda b: b):
+                    try:
+                        out = dec(blob)
+                    except zlib.error:
+                        continue
+                    if out[:4] == b"\x7fELF":
+                        yield rec.get("kernel_name") or rec.get("program") or rec.get("program_name") or "?", out
+                        break
 
 
 def meta(blob):
