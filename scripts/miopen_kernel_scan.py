@@ -37,9 +37,12 @@ def blobs(db):
                         out = dec(blob)
                     except zlib.error:
                         continue
-                    if out[:4] == b"\x7fELF":
-                        yield rec.get("kernel_name") or rec.get("program") or rec.get("program_name") or "?", out
+                    off = out.find(b"\x7fELF")
+                    if off >= 0:   # a plain code object, or one inside a clang offload bundle
+                        yield rec.get("kernel_name") or rec.get("program") or rec.get("program_name") or "?", out[off:]
                         break
+                    if dec is not None and out is blob:
+                        print(f"    no code object in {rec.get('kernel_name')}: head {blob[:24]!r}")
 
 
 def meta(blob):
