@@ -485,7 +485,9 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
       }
 #pragma unroll
       for (int t = 0; t < NSUB; ++t) {
-        if (CAUSAL && t == tdiag) {
+        // (a wave-uniform branch: only the diagonal subtile pays the per-element select)
+        if (CAUSAL && uni(t == tdiag ? 1 : 0)) {
+          asm volatile("" ::: "memory");   // a real branch, not per-element selects
 #pragma unroll
           for (int e = 0; e < 16; ++e) sacc[t][e] = crow(e, 0) > rr ? -INFINITY : sacc[t][e];
         }
@@ -566,6 +568,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
           for (int e = 0; e < 16; ++e) pv[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(s_[e], c, -lse2));
           // (only the diagonal / padded-tail subtile is masked: a wave-uniform branch)
           if (uni((CAUSAL && t == tdiag) || (!CAUSAL && tail) ? 1 : 0)) {
+            asm volatile("" ::: "memory");   // a real branch, not per-element selects
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
               if (CAUSAL) pv[e] = crow(e, 0) > rr ? 0.f : pv[e];
@@ -902,6 +905,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
         pv[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[e], c, -lse_e));
       }
       if (uni(diag ? 1 : 0)) {
+        asm volatile("" ::: "memory");   // keeps this a real (scalar) branch: not if-converted into selects
 #pragma unroll
         for (int e = 0; e < 16; ++e) pv[e] = rr > crow(e, 0) ? 0.f : pv[e];
       }
