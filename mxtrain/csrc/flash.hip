@@ -1013,11 +1013,257 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
   finalize();
 }
 
+// ====================================================================== key-major, D = 128
+// dK, dV of D = 128 in ONE pass (S and dP computed once per subtile, not once per half of
+// the columns).  One 8-wave workgroup per 128-key block, two waves per SIMD: waves w and
+// w + 4 (same SIMD) own the same 32 keys.  Team 0 (w < 4) holds the keys' K rows and
+// computes S^T -> P; team 1 holds their V rows and computes dP^T -> x = (keep ? dP : 0) -
+// delta.  The two fp32 16-element lane images are swapped through LDS (identical MFMA
+// output layout in both waves: an element-wise exchange, conflict-free 16-B lane slots),
+// then both form dS = P x and the dropped P, and each accumulates its own half of the
+// dK^T / dV^T columns ([0, 64) team 0, [64, 128) team 1).  Per 32 x 32 subtile and key
+// group: 32 MFMAs (8 S + 8 dP + 16 dK/dV) instead of the two-pass 48, and one exp2 per
+// element instead of two.  Q / dO tiles of 32 rows stream through the LDS-DMA ring as in
+// flash_kmajor_kernel; two barriers per tile (ring, exchange), executed by every wave
+// whatever its causal / tail state, so the barrier counts of all waves match.
+template <bool CAUSAL, bool DROP, bool RAGGED>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void flash_kmajor128_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+    const uint16_t* __restrict__ v, int ldq, int ldk, int ldv,
+    const uint16_t* __restrict__ dout, int lddo, const float* __restrict__ lse,
+    const float* __restrict__ delta, uint16_t* __restrict__ dk, uint16_t* __restrict__ dv,
+    int lddk, int lddv, int S, int Hq, int Hkv, const int* __restrict__ klen, float c,
+    float dkscale, float dvscale, const uint32_t* __restrict__ dbits, int NB, int NQT) {
+  constexpr int D = 128, KB = 128, QT = 32, NKK = D / 16, NDL = 2;
+  constexpr int RB = D * 2, CPR = D / 8, RPP = 64 / CPR;
+  constexpr int QTILE = QT * RB, PIECES = QTILE / 1024, PPW = (2 * PIECES) / 8;
+  static_assert(PPW * 8 == 2 * PIECES, "8 waves issue the Q + dO pieces");
+  __shared__ __attribute__((aligned(16))) char q0[QTILE];
+  __shared__ __attribute__((aligned(16))) char q1[QTILE];
+  __shared__ __attribute__((aligned(16))) char o0[QTILE];
+  __shared__ __attribute__((aligned(16))) char o1[QTILE];
+  __shared__ __attribute__((aligned(16))) float l0[64];
+  __shared__ __attribute__((aligned(16))) float l1[64];
+  __shared__ __attribute__((aligned(16))) float d0[64];
+  __shared__ __attribute__((aligned(16))) float d1[64];
+  // [buffer][wave][4 chunks][64 lanes][4 floats]: a wave's 16 elements as four 16-B slots
+  __shared__ __attribute__((aligned(16))) float xch[2 * 8 * 16 * 64];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = uni(tid >> 6);
+  const int team = w >> 2, wl = w & 3;
+  const int r = lane & 31, hh = lane >> 5, g = lane >> 4, gi = lane & 15;
+  const int nkb = (S + KB - 1) / KB;
+  int rank, head;
+  block_map((int)gridDim.x / nkb, rank, head);   // grid = nkb x (B * Hkv)
+  const int hk = head % Hkv, b = head / Hkv;
+  const int grp = Hq / Hkv;
+  const int kl = klen ? klen[b] : S;
+  const int nqt = (S + QT - 1) / QT;
+  const int kb = rank;                            // causal: block 0 (most rows) first
+  const int qt0 = CAUSAL ? kb * KB / QT : 0;
+  const int ph = nqt - qt0;
+  const int cnt = uni(ph * grp);
+
+  const int kw0 = kb * KB + 32 * wl;
+  const int key = kw0 + r;
+  const bool key_ok = key < kl;
+  const bool wave_on = kw0 < S;
+  const int DT0 = 2 * team;
+  // team 0: K rows of the lane's key; team 1: V rows (the B operands of S^T / dP^T)
+  bf16x8 kv[NKK];
+  {
+    const int key_c = min(key, S - 1);
+    const uint16_t* src = team == 0 ? k + (size_t)(b * S + key_c) * ldk : v + (size_t)(b * S + key_c) * ldv;
+    src += hk * D + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) kv[kk] = ld8(src + 16 * kk);
+  }
+  f32x16 dvacc[NDL], dkacc[NDL];
+#pragma unroll
+  for (int dt = 0; dt < NDL; ++dt) { dvacc[dt] = f32x16{}; dkacc[dt] = f32x16{}; }
+  __builtin_amdgcn_s_waitcnt(0);  // K / V rows complete before the loop (see qmajor)
+
+  int offQ[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) offQ[kk] = toff<D>(r, 2 * kk + hh);
+  int offT[NDL][2];
+#pragma unroll
+  for (int dt = 0; dt < NDL; ++dt) {
+    const int col = 32 * (dt + DT0) + 16 * (g & 1) + 4 * (gi & 3);
+    const int row0 = 4 * hh + (gi >> 2);
+    offT[dt][0] = toff<D>(row0, col >> 3) + (col & 7) * 2;
+    offT[dt][1] = toff<D>(row0 + 8, col >> 3) + (col & 7) * 2;
+  }
+  const int rr = r - 4 * hh;   // diagonal: element e dead when r - 4hh > crow(e, 0)
+  float* const xmine = xch + w * 1024 + lane * 4;
+  float* const xother = xch + (w ^ 4) * 1024 + lane * 4;
+
+  const int prow = lane / CPR, slot = lane % CPR;
+  auto decode = [&](int t, int& hq, int& qs) __attribute__((always_inline)) {
+    hq = hk * grp + t / ph;
+    qs = (qt0 + t % ph) * QT;
+  };
+  auto issue = [&](char* qd, char* od, float* ld, float* dd, int t) __attribute__((always_inline)) {
+    int hq, qs;
+    decode(t, hq, qs);
+    const uint16_t* qb_ = q + (size_t)b * S * ldq + hq * D;
+    const uint16_t* ob_ = dout + (size_t)b * S * lddo + hq * D;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int p = w + 8 * i;                 // 0 .. 2*PIECES-1: Q pieces then dO pieces
+      const bool isq = p < PIECES;
+      const int pp = isq ? p : p - PIECES;
+      const int R = pp * RPP + prow;
+      const int row = min(qs + R, S - 1);
+      const int ch = slot ^ swz<D>(R);
+      if (isq) dma16(qb_ + (size_t)row * ldq + ch * 8, qd + pp * 1024);
+      else dma16(ob_ + (size_t)row * lddo + ch * 8, od + pp * 1024);
+    }
+    if (w < 2) {
+      const size_t li = ((size_t)b * Hq + hq) * S + min(qs + lane, S - 1);
+      if (w == 0) dma4(lse + li, (char*)ld);
+      else dma4(delta + li, (char*)dd);
+    }
+  };
+  auto dmload = [&](int t) __attribute__((always_inline)) -> uint32_t {
+    if (!DROP || !wave_on) return 0u;
+    int hq, qs;
+    decode(t, hq, qs);
+    return dbits[(((size_t)(b * Hq + hq) * NB + (kw0 >> 5)) * NQT + (qs >> 6)) * 64 + lane];
+  };
+  uint32_t dm_cur = 0, dm_next = 0;
+
+  auto compute = [&](const char* Qt, const char* Ot, const float* Lt, const float* Dt, int t, float* xm,
+                     const float* xo) __attribute__((always_inline)) {
+    int hq, qs;
+    decode(t, hq, qs);
+    (void)hq;
+    const bool act = uni(wave_on && qs < S && (!CAUSAL || qs + 31 >= kw0) ? 1 : 0);
+    f32x16 acc = f32x16{};
+    if (act) {
+      const char* X = team == 0 ? Qt : Ot;
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) acc = mfma32(lds8(X, offQ[kk]), kv[kk], acc);
+      if (team == 0) {
+        // P of the subtile; the causal diagonal (wave-uniform branch) and, in RAGGED
+        // launches only, the query tail / invalid keys are zeroed afterwards
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          float4 lsq;
+          if ((e & 3) == 0) lsq = *reinterpret_cast<const float4*>(Lt + 8 * (e >> 2) + 4 * hh);
+          const float lse_e = (e & 3) == 0 ? lsq.x : (e & 3) == 1 ? lsq.y : (e & 3) == 2 ? lsq.z : lsq.w;
+          acc[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[e], c, -lse_e));
+        }
+        if (uni(CAUSAL && qs == kw0 ? 1 : 0)) {
+          asm volatile("" ::: "memory");   // a real (scalar) branch, not per-element selects
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[e] = rr > crow(e, 0) ? 0.f : acc[e];
+        }
+        if constexpr (RAGGED) {
+          const bool qtail = qs + 32 > S;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            if (qtail) acc[e] = qs + crow(e, hh) >= S ? 0.f : acc[e];
+            acc[e] = key_ok ? acc[e] : 0.f;
+          }
+        }
+      } else {
+        // x = (keep ? dP : 0) - delta
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          float4 dlq;
+          if ((e & 3) == 0) dlq = *reinterpret_cast<const float4*>(Dt + 8 * (e >> 2) + 4 * hh);
+          const float dl_e = (e & 3) == 0 ? dlq.x : (e & 3) == 1 ? dlq.y : (e & 3) == 2 ? dlq.z : dlq.w;
+          float x = acc[e];
+          if (DROP) x = __uint_as_float(__float_as_uint(x) & elem_keep(dm_cur, 8 * ((qs >> 5) & 1), e));
+          acc[e] = x - dl_e;
+        }
+      }
+#pragma unroll
+      for (int ch = 0; ch < 4; ++ch)
+        *reinterpret_cast<float4*>(xm + ch * 256) =
+            make_float4(acc[4 * ch], acc[4 * ch + 1], acc[4 * ch + 2], acc[4 * ch + 3]);
+    }
+    __syncthreads();   // every wave, active or not: the barrier counts of all waves match
+    if (act) {
+      float o[16];
+#pragma unroll
+      for (int ch = 0; ch < 4; ++ch) {
+        const float4 f = *reinterpret_cast<const float4*>(xo + ch * 256);
+        o[4 * ch] = f.x; o[4 * ch + 1] = f.y; o[4 * ch + 2] = f.z; o[4 * ch + 3] = f.w;
+      }
+      f32x16 pd, ds;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const float p = team == 0 ? acc[e] : o[e];
+        const float x = team == 0 ? o[e] : acc[e];
+        ds[e] = p * x;   // dS (1/(1-p) in dkscale)
+        pd[e] = DROP ? __uint_as_float(__float_as_uint(p) & elem_keep(dm_cur, 8 * ((qs >> 5) & 1), e)) : p;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pb = pack8(pd, 8 * s);
+        const bf16x8 db = pack8(ds, 8 * s);
+        const int rofs = 16 * s * RB;
+#pragma unroll
+        for (int dt = 0; dt < NDL; ++dt) {
+          const bf16x8 dot = cat(tr_read(Ot + rofs, offT[dt][0]), tr_read(Ot + rofs, offT[dt][1]));
+          dvacc[dt] = mfma32(dot, pb, dvacc[dt]);
+          const bf16x8 qtr = cat(tr_read(Qt + rofs, offT[dt][0]), tr_read(Qt + rofs, offT[dt][1]));
+          dkacc[dt] = mfma32(qtr, db, dkacc[dt]);
+        }
+      }
+    }
+  };
+
+  auto step = [&](char* Qc, char* Oc, float* Lc, float* Dc, char* Qn, char* On, float* Ln, float* Dn,
+                  int t, int xb) __attribute__((always_inline)) {
+    vm_drain();
+    __syncthreads();
+    if (t + 1 < cnt) {
+      issue(Qn, On, Ln, Dn, t + 1);
+      dm_next = dmload(t + 1);
+    }
+    compute(Qc, Oc, Lc, Dc, t, xmine + xb * 8 * 1024, xother + xb * 8 * 1024);
+    dm_cur = dm_next;
+  };
+  if (cnt > 0) {
+    issue(q0, o0, l0, d0, 0);
+    dm_cur = dmload(0);
+  }
+  // the exchange buffer alternates per step: a wave's write of step t + 1 cannot reach the
+  // slot its partner is still reading for step t (one barrier lies between them, two before
+  // the same slot is written again)
+  for (int t = 0; t < cnt; t += 2) {
+    step(q0, o0, l0, d0, q1, o1, l1, d1, t, 0);
+    if (t + 1 < cnt) step(q1, o1, l1, d1, q0, o0, l0, d0, t + 1, 1);
+  }
+
+  if (!(key < S)) return;
+  uint16_t* dkp = dk + (size_t)(b * S + key) * lddk + hk * D;
+  uint16_t* dvp = dv + (size_t)(b * S + key) * lddv + hk * D;
+#pragma unroll
+  for (int dt = 0; dt < NDL; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = 32 * (dt + DT0) + 8 * g4 + 4 * hh;
+      uint2 u;
+      u.x = pack2(dkacc[dt][4 * g4 + 0] * dkscale, dkacc[dt][4 * g4 + 1] * dkscale);
+      u.y = pack2(dkacc[dt][4 * g4 + 2] * dkscale, dkacc[dt][4 * g4 + 3] * dkscale);
+      *reinterpret_cast<uint2*>(dkp + d) = u;
+      u.x = pack2(dvacc[dt][4 * g4 + 0] * dvscale, dvacc[dt][4 * g4 + 1] * dvscale);
+      u.y = pack2(dvacc[dt][4 * g4 + 2] * dvscale, dvacc[dt][4 * g4 + 3] * dvscale);
+      *reinterpret_cast<uint2*>(dvp + d) = u;
+    }
+}
+
 // ------------------------------------------------------------------------------ launch
 // key-tile rows of the D 64 query-major kernels (rocprofv3, GPT-2 shapes, dropout 0.1, one
 // box: forward 25.8 us at 64 / 24.4 at 128; dQ 32.5 at 64 / 34.0 at 128 -- the dQ step
 // holds S, dP and dQ^T, and its longer per-tile chain already covers the next tile's DMA)
 int g_qbk_fwd = 128, g_qbk_dq = 64;
+// D 128 dK/dV: single-pass 8-wave kernel (default) or the two column-half passes (A/B only)
+int g_kmajor128_two_pass = 0;
 
 template <int D, bool DQ>
 hipError_t launch_qmajor(bool causal, bool drop, int S, int B, hipStream_t s,
@@ -1083,9 +1329,24 @@ hipError_t launch_kmajor(bool causal, bool drop, int S, int B, hipStream_t s,
   }
   if constexpr (D <= 64) {
     MX_KM_P(0)
-  } else {
+  } else if (g_kmajor128_two_pass) {
     MX_KM_P(1)
     MX_KM_P(2)
+  } else {
+#define MX_K8(C, DR)                                                                                \
+  do {                                                                                              \
+    if (ragged)                                                                                     \
+      hipLaunchKernelGGL((flash_kmajor128_kernel<C, DR, true>), grid, dim3(512), 0, s, q, k, v, ldq, \
+                         ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq, Hkv, klen, c, \
+                         dkscale, dvscale, dbits, NB, NQT);                                         \
+    else                                                                                            \
+      hipLaunchKernelGGL((flash_kmajor128_kernel<C, DR, false>), grid, dim3(512), 0, s, q, k, v,    \
+                         ldq, ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq, Hkv,     \
+                         klen, c, dkscale, dvscale, dbits, NB, NQT);                                \
+  } while (0)
+    if (causal) { if (drop) MX_K8(true, true); else MX_K8(true, false); }
+    else { if (drop) MX_K8(false, true); else MX_K8(false, false); }
+#undef MX_K8
   }
 #undef MX_KM_P
 #undef MX_KM
@@ -1100,6 +1361,14 @@ MX_EXPORT int mx_flash_qmajor_bk(int fwd, int dq) {
   const int old = g_qbk_fwd * 1000 + g_qbk_dq;
   if (fwd == 64 || fwd == 128) g_qbk_fwd = fwd;
   if (dq == 64 || dq == 128) g_qbk_dq = dq;
+  return old;
+}
+
+// D 128 dK/dV kernel choice: 0 = single pass (flash_kmajor128_kernel), 1 = two column-half
+// passes of flash_kmajor_kernel; a negative value keeps the setting.  Returns the old one.
+MX_EXPORT int mx_flash_kmajor128_two_pass(int two_pass) {
+  const int old = g_kmajor128_two_pass;
+  if (two_pass >= 0) g_kmajor128_two_pass = two_pass ? 1 : 0;
   return old;
 }
 

@@ -33,6 +33,7 @@ SIGNATURES = {
     "mx_norm_split_cols": [I],
     "mx_norm_bwd_rows_per_wave": [I],
     "mx_flash_qmajor_bk": [I, I],
+    "mx_flash_kmajor128_two_pass": [I],
     "mx_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],
     "mx_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
     "mx_bda_norm_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, F, P, U32, I, P],

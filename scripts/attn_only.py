@@ -19,7 +19,11 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.0)
     ap.add_argument("--fwd-only", action="store_true")
     ap.add_argument("--qbk", default="", help="key-tile rows of the D 64 forward / dQ kernels, e.g. 64,128")
+    ap.add_argument("--two-pass", action="store_true", help="D 128 dK/dV as the two column-half passes (A/B)")
     a = ap.parse_args()
+    if a.two_pass:
+        from mxtrain.ops import _lib
+        _lib._fn("mx_flash_kmajor128_two_pass")(1)
     if a.qbk:
         from mxtrain.ops import _lib
         f, q = (int(x) for x in a.qbk.split(","))

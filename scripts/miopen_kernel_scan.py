@@ -5,6 +5,7 @@ the dispatch?  Reads the MIOpen user kernel cache the training run just filled
 for every kernel prints its AMDGPU metadata: private (scratch) segment size, dynamic stack,
 kernarg segment size and the hidden arguments it declares -- the dispatch-time properties a
 pre-built (graph packet-capture) AQL packet has to get right.  Read-only; runs no kernel."""
+import bz2
 import glob
 import json
 import os
@@ -32,10 +33,10 @@ def blobs(db):
                 if not isinstance(v, (bytes, bytearray)) or len(v) < 64:
                     continue
                 blob = bytes(v)
-                for dec in (lambda b: zlib.decompress(b), lambda b: zlib.decompress(b, -15), lambda b: b):
+                for dec in (bz2.decompress, lambda b: zlib.decompress(b), lambda b: zlib.decompress(b, -15), lambda b: b):
                     try:
                         out = dec(blob)
-                    except zlib.error:
+                    except (zlib.error, OSError, ValueError):
                         continue
                     off = out.find(b"\x7fELF")
                     if off >= 0:   # a plain code object, or one inside a clang offload bundle
@@ -65,7 +66,7 @@ def meta(blob):
         hidden = sorted(set(re.findall(r"\.value_kind:\s+(hidden_\w+)", blk)))
         ks.append({"name": m.group(1), "scratch": g("private_segment_fixed_size"), "dyn_stack": g("uses_dynamic_stack"),
                    "kernarg": g("kernarg_segment_size"), "group_seg": g("group_segment_fixed_size"),
-                   "hidden": hidden})
+                   "hidden": hidden, "uniform_wg": g("uniform_work_group_size")})
     return ks
 
 

@@ -173,7 +173,7 @@ ATTN_CASES = [
     (2, 200, 2, 2, 64, True, False, 0.0),
     (1, 256, 2, 2, 128, True, False, 0.0),
     (2, 128, 2, 2, 128, False, True, 0.0),
-    # production GPT-3 6.7B head shape (S 2048, D 128, causal; two-pass backward)
+    # production GPT-3 6.7B head shape (S 2048, D 128, causal; single-pass 8-wave dK/dV)
     (1, 2048, 2, 2, 128, True, False, 0.0),
     # grouped-query attention (Hq != Hkv)
     (2, 512, 8, 2, 64, True, False, 0.0),
@@ -185,6 +185,8 @@ ATTN_CASES = [
     (2, 128, 4, 4, 64, False, True, 0.1),
     (1, 512, 4, 2, 128, True, False, 0.1),
     (2, 128, 2, 2, 128, False, True, 0.3),
+    # D 128, causal, S not a multiple of the 128-key block (ragged single-pass dK/dV)
+    (2, 200, 2, 2, 128, True, False, 0.1),
 ]
 
 
@@ -215,6 +217,38 @@ def test_flash_attention_fwd_bwd(B, S, Hq, Hkv, D, causal, padded, pdrop):
     _close(dqkv[:, sl[0]], dq, 3e-2 * scale, 3e-2, "dq")
     _close(dqkv[:, sl[1]], dk, 3e-2 * scale, 3e-2, "dk")
     _close(dqkv[:, sl[2]], dv, 3e-2 * scale, 3e-2, "dv")
+
+
+@pytest.mark.parametrize("S,causal,pdrop,padded", [(1024, True, 0.1, False), (200, True, 0.0, False),
+                                                   (256, False, 0.1, True)])
+def test_flash_d128_single_pass_matches_two_pass(S, causal, pdrop, padded):
+    """The single-pass 8-wave D 128 dK/dV kernel (S and dP once per subtile, exchanged
+    through LDS) does the same fp32 operations in the same MFMA order as the two column-half
+    passes, so dK / dV are bit-identical; dQ comes from the shared query-major kernel."""
+    from mxtrain.ops import _lib
+    B, H, D = 2, 4, 128
+    torch.manual_seed(3)
+    qkv = torch.randn(B * S, 3 * H * D, device=DEV).to(torch.bfloat16)
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    do = torch.randn(B * S, H * D, device=DEV).to(torch.bfloat16)
+    klen = torch.tensor([S, S * 3 // 4], dtype=torch.int32, device=DEV) if padded else None
+    seed = torch.tensor([99], dtype=torch.int32, device=DEV)
+    kw = dict(dropout_p=pdrop, salt=3, head_offset=0, total_heads=H) if pdrop else {}
+    o, lse, dm = A.attn_fwd(q, k, v, B, S, H, H, D, causal, klen, seed_t=seed, **kw)
+    outs = []
+    old = _lib._fn("mx_flash_kmajor128_two_pass")(-1)
+    try:
+        for two in (0, 1):
+            _lib._fn("mx_flash_kmajor128_two_pass")(two)
+            dqkv = torch.zeros_like(qkv)
+            A.attn_bwd(do, q, k, v, o, lse, B, S, H, H, D, causal, klen, dq=dqkv[:, :H * D],
+                       dk=dqkv[:, H * D:2 * H * D], dv=dqkv[:, 2 * H * D:], dmask=dm, dropout_p=pdrop)
+            torch.cuda.synchronize()
+            outs.append(dqkv)
+    finally:
+        _lib._fn("mx_flash_kmajor128_two_pass")(old)
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0], outs[1])
 
 
 def _crow(e, hh):
