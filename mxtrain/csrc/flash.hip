@@ -30,8 +30,12 @@
 //                atomics, no convert kernel).
 //   kmajor       each wave keeps dK^T / dV^T of its 32 keys in accumulators (key on the lane: P and dS are
 //                ready-made B operands) while Q / dO / lse / delta tiles of 64 rows stream
-//                through an LDS-DMA ring (32 rows for D = 128).  D = 128 keeps K in LDS and
-//                splits the dK/dV columns into two passes (register budget at 2 waves/SIMD).
+//                through an LDS-DMA ring (32 rows for D = 128).
+//   kmajor128    D = 128 in one pass: 8 waves, two per 32 keys -- one computes S -> P, its
+//                partner dP -> dP - delta, the halves are swapped through LDS and each wave
+//                accumulates half of the dK/dV columns (the accumulators of all 128 columns
+//                do not fit two waves per SIMD; the earlier two column-half passes recomputed
+//                S and dP twice: 323 -> 275 us at GPT-3 shapes).
 // The 5-GEMM single backward would need dQ summed across key blocks: with fp32 atomics that
 // is bounded by the ~1.3 TB/s chip atomic rate (MI355X_MICROARCH.md "Global float atomics"),
 // 33 MB / 26 us per GPT-2 layer; the recompute costs 1.4x the MFMA work but no atomics.
@@ -1262,8 +1266,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // box: forward 25.8 us at 64 / 24.4 at 128; dQ 32.5 at 64 / 34.0 at 128 -- the dQ step
 // holds S, dP and dQ^T, and its longer per-tile chain already covers the next tile's DMA)
 int g_qbk_fwd = 128, g_qbk_dq = 64;
-// D 128 dK/dV: single-pass 8-wave kernel (default) or the two column-half passes (A/B only)
-int g_kmajor128_two_pass = 0;
+// D 128 dK/dV: 0 = single-pass 8-wave kernel (default), 1 = the two column-half passes
+// (bit-identical; kept for the equality test and A/B runs).  Measured and dropped (GPT-3
+// shapes, dropout 0.1, one MI355X, profiles/r3_s4): static s_setprio 1 for the team-1 half
+// 280.1 vs 280.2 us; a ping-pong schedule (teams offset by one of four barrier-separated
+// segments per tile, 3-slot ring) 452.7 vs 275.3 us -- four barriers per 32-row tile cost
+// more than the matrix / vector pairing recovers, and it spilled at 256 VGPRs.
+int g_kmajor128_variant = 0;
 
 template <int D, bool DQ>
 hipError_t launch_qmajor(bool causal, bool drop, int S, int B, hipStream_t s,
@@ -1329,7 +1338,7 @@ hipError_t launch_kmajor(bool causal, bool drop, int S, int B, hipStream_t s,
   }
   if constexpr (D <= 64) {
     MX_KM_P(0)
-  } else if (g_kmajor128_two_pass) {
+  } else if (g_kmajor128_variant == 1) {
     MX_KM_P(1)
     MX_KM_P(2)
   } else {
@@ -1364,11 +1373,11 @@ MX_EXPORT int mx_flash_qmajor_bk(int fwd, int dq) {
   return old;
 }
 
-// D 128 dK/dV kernel choice: 0 = single pass (flash_kmajor128_kernel), 1 = two column-half
-// passes of flash_kmajor_kernel; a negative value keeps the setting.  Returns the old one.
-MX_EXPORT int mx_flash_kmajor128_two_pass(int two_pass) {
-  const int old = g_kmajor128_two_pass;
-  if (two_pass >= 0) g_kmajor128_two_pass = two_pass ? 1 : 0;
+// D 128 dK/dV kernel choice (g_kmajor128_variant); a negative value keeps the setting.
+// Returns the old one.
+MX_EXPORT int mx_flash_kmajor128_variant(int variant) {
+  const int old = g_kmajor128_variant;
+  if (variant == 0 || variant == 1) g_kmajor128_variant = variant;
   return old;
 }
 

@@ -19,11 +19,12 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.0)
     ap.add_argument("--fwd-only", action="store_true")
     ap.add_argument("--qbk", default="", help="key-tile rows of the D 64 forward / dQ kernels, e.g. 64,128")
-    ap.add_argument("--two-pass", action="store_true", help="D 128 dK/dV as the two column-half passes (A/B)")
+    ap.add_argument("--k128", type=int, default=-1,
+                    help="D 128 dK/dV variant: 0 single pass, 1 two column-half passes")
     a = ap.parse_args()
-    if a.two_pass:
+    if a.k128 >= 0:
         from mxtrain.ops import _lib
-        _lib._fn("mx_flash_kmajor128_two_pass")(1)
+        _lib._fn("mx_flash_kmajor128_variant")(a.k128)
     if a.qbk:
         from mxtrain.ops import _lib
         f, q = (int(x) for x in a.qbk.split(","))

@@ -236,17 +236,17 @@ def test_flash_d128_single_pass_matches_two_pass(S, causal, pdrop, padded):
     kw = dict(dropout_p=pdrop, salt=3, head_offset=0, total_heads=H) if pdrop else {}
     o, lse, dm = A.attn_fwd(q, k, v, B, S, H, H, D, causal, klen, seed_t=seed, **kw)
     outs = []
-    old = _lib._fn("mx_flash_kmajor128_two_pass")(-1)
+    old = _lib._fn("mx_flash_kmajor128_variant")(-1)
     try:
-        for two in (0, 1):
-            _lib._fn("mx_flash_kmajor128_two_pass")(two)
+        for variant in (0, 1):   # single pass, two column-half passes
+            _lib._fn("mx_flash_kmajor128_variant")(variant)
             dqkv = torch.zeros_like(qkv)
             A.attn_bwd(do, q, k, v, o, lse, B, S, H, H, D, causal, klen, dq=dqkv[:, :H * D],
                        dk=dqkv[:, H * D:2 * H * D], dv=dqkv[:, 2 * H * D:], dmask=dm, dropout_p=pdrop)
             torch.cuda.synchronize()
             outs.append(dqkv)
     finally:
-        _lib._fn("mx_flash_kmajor128_two_pass")(old)
+        _lib._fn("mx_flash_kmajor128_variant")(old)
     assert torch.isfinite(outs[0].float()).all()
     assert torch.equal(outs[0], outs[1])
 
