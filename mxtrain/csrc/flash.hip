@@ -1030,7 +1030,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
 // element instead of two.  Q / dO tiles of 32 rows stream through the LDS-DMA ring as in
 // flash_kmajor_kernel; two barriers per tile (ring, exchange), executed by every wave
 // whatever its causal / tail state, so the barrier counts of all waves match.
-template <bool CAUSAL, bool DROP, bool RAGGED>
+template <bool CAUSAL, bool DROP, bool RAGGED, int QT = 32>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void flash_kmajor128_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, int ldq, int ldk, int ldv,
@@ -1038,9 +1038,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const float* __restrict__ delta, uint16_t* __restrict__ dk, uint16_t* __restrict__ dv,
     int lddk, int lddv, int S, int Hq, int Hkv, const int* __restrict__ klen, float c,
     float dkscale, float dvscale, const uint32_t* __restrict__ dbits, int NB, int NQT) {
-  constexpr int D = 128, KB = 128, QT = 32, NKK = D / 16, NDL = 2;
+  // QT query rows per step (32 or 64 = NQS subtiles of 32; one ring barrier and one
+  // exchange barrier per step either way)
+  constexpr int D = 128, KB = 128, NQS = QT / 32, NKK = D / 16, NDL = 2;
   constexpr int RB = D * 2, CPR = D / 8, RPP = 64 / CPR;
   constexpr int QTILE = QT * RB, PIECES = QTILE / 1024, PPW = (2 * PIECES) / 8;
+  static_assert(QT == 32 || QT == 64, "32 or 64 query rows per step");
   static_assert(PPW * 8 == 2 * PIECES, "8 waves issue the Q + dO pieces");
   __shared__ __attribute__((aligned(16))) char q0[QTILE];
   __shared__ __attribute__((aligned(16))) char q1[QTILE];
@@ -1050,8 +1053,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __shared__ __attribute__((aligned(16))) float l1[64];
   __shared__ __attribute__((aligned(16))) float d0[64];
   __shared__ __attribute__((aligned(16))) float d1[64];
-  // [buffer][wave][4 chunks][64 lanes][4 floats]: a wave's 16 elements as four 16-B slots
-  __shared__ __attribute__((aligned(16))) float xch[2 * 8 * 16 * 64];
+  // [wave][subtile][4 chunks][64 lanes][4 floats]: a wave's 16 elements of a subtile as four
+  // 16-B slots.  One buffer: a wave writes it after the ring barrier of step t + 1, and every
+  // partner read of step t precedes that barrier.
+  __shared__ __attribute__((aligned(16))) float xch[8 * NQS * 1024];
 
   const int tid = threadIdx.x, lane = tid & 63, w = uni(tid >> 6);
   const int team = w >> 2, wl = w & 3;
@@ -1099,8 +1104,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     offT[dt][1] = toff<D>(row0 + 8, col >> 3) + (col & 7) * 2;
   }
   const int rr = r - 4 * hh;   // diagonal: element e dead when r - 4hh > crow(e, 0)
-  float* const xmine = xch + w * 1024 + lane * 4;
-  float* const xother = xch + (w ^ 4) * 1024 + lane * 4;
+  float* const xmine = xch + w * NQS * 1024 + lane * 4;
+  const float* const xother = xch + (w ^ 4) * NQS * 1024 + lane * 4;
 
   const int prow = lane / CPR, slot = lane % CPR;
   auto decode = [&](int t, int& hq, int& qs) __attribute__((always_inline)) {
@@ -1137,38 +1142,54 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   };
   uint32_t dm_cur = 0, dm_next = 0;
 
-  auto compute = [&](const char* Qt, const char* Ot, const float* Lt, const float* Dt, int t, float* xm,
-                     const float* xo) __attribute__((always_inline)) {
+  auto compute = [&](const char* Qt, const char* Ot, const float* Lt, const float* Dt, int t)
+      __attribute__((always_inline)) {
     int hq, qs;
     decode(t, hq, qs);
     (void)hq;
-    const bool act = uni(wave_on && qs < S && (!CAUSAL || qs + 31 >= kw0) ? 1 : 0);
-    f32x16 acc = f32x16{};
-    if (act) {
-      const char* X = team == 0 ? Qt : Ot;
+    bool act[NQS];
+    f32x16 acc[NQS];
 #pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) acc = mfma32(lds8(X, offQ[kk]), kv[kk], acc);
+    for (int u = 0; u < NQS; ++u) {
+      const int qsu = qs + 32 * u;
+      act[u] = uni(wave_on && qsu < S && (!CAUSAL || qsu + 31 >= kw0) ? 1 : 0);
+    }
+    // S^T (team 0) / dP^T (team 1) of every subtile first: the MFMAs of subtile u + 1 can
+    // run under the vector work of subtile u
+    const char* X = team == 0 ? Qt : Ot;
+#pragma unroll
+    for (int u = 0; u < NQS; ++u) {
+      acc[u] = f32x16{};
+      if (act[u]) {
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) acc[u] = mfma32(lds8(X + 32 * u * RB, offQ[kk]), kv[kk], acc[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NQS; ++u) {
+      if (!act[u]) continue;
+      const int qsu = qs + 32 * u;
       if (team == 0) {
         // P of the subtile; the causal diagonal (wave-uniform branch) and, in RAGGED
         // launches only, the query tail / invalid keys are zeroed afterwards
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           float4 lsq;
-          if ((e & 3) == 0) lsq = *reinterpret_cast<const float4*>(Lt + 8 * (e >> 2) + 4 * hh);
+          if ((e & 3) == 0) lsq = *reinterpret_cast<const float4*>(Lt + 32 * u + 8 * (e >> 2) + 4 * hh);
           const float lse_e = (e & 3) == 0 ? lsq.x : (e & 3) == 1 ? lsq.y : (e & 3) == 2 ? lsq.z : lsq.w;
-          acc[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[e], c, -lse_e));
+          acc[u][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[u][e], c, -lse_e));
         }
-        if (uni(CAUSAL && qs == kw0 ? 1 : 0)) {
+        if (uni(CAUSAL && qsu == kw0 ? 1 : 0)) {
           asm volatile("" ::: "memory");   // a real (scalar) branch, not per-element selects
 #pragma unroll
-          for (int e = 0; e < 16; ++e) acc[e] = rr > crow(e, 0) ? 0.f : acc[e];
+          for (int e = 0; e < 16; ++e) acc[u][e] = rr > crow(e, 0) ? 0.f : acc[u][e];
         }
         if constexpr (RAGGED) {
-          const bool qtail = qs + 32 > S;
+          const bool qtail = qsu + 32 > S;
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
-            if (qtail) acc[e] = qs + crow(e, hh) >= S ? 0.f : acc[e];
-            acc[e] = key_ok ? acc[e] : 0.f;
+            if (qtail) acc[u][e] = qsu + crow(e, hh) >= S ? 0.f : acc[u][e];
+            acc[u][e] = key_ok ? acc[u][e] : 0.f;
           }
         }
       } else {
@@ -1176,39 +1197,42 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           float4 dlq;
-          if ((e & 3) == 0) dlq = *reinterpret_cast<const float4*>(Dt + 8 * (e >> 2) + 4 * hh);
+          if ((e & 3) == 0) dlq = *reinterpret_cast<const float4*>(Dt + 32 * u + 8 * (e >> 2) + 4 * hh);
           const float dl_e = (e & 3) == 0 ? dlq.x : (e & 3) == 1 ? dlq.y : (e & 3) == 2 ? dlq.z : dlq.w;
-          float x = acc[e];
-          if (DROP) x = __uint_as_float(__float_as_uint(x) & elem_keep(dm_cur, 8 * ((qs >> 5) & 1), e));
-          acc[e] = x - dl_e;
+          float x = acc[u][e];
+          if (DROP) x = __uint_as_float(__float_as_uint(x) & elem_keep(dm_cur, 8 * ((qsu >> 5) & 1), e));
+          acc[u][e] = x - dl_e;
         }
       }
 #pragma unroll
       for (int ch = 0; ch < 4; ++ch)
-        *reinterpret_cast<float4*>(xm + ch * 256) =
-            make_float4(acc[4 * ch], acc[4 * ch + 1], acc[4 * ch + 2], acc[4 * ch + 3]);
+        *reinterpret_cast<float4*>(xmine + u * 1024 + ch * 256) =
+            make_float4(acc[u][4 * ch], acc[u][4 * ch + 1], acc[u][4 * ch + 2], acc[u][4 * ch + 3]);
     }
     __syncthreads();   // every wave, active or not: the barrier counts of all waves match
-    if (act) {
+#pragma unroll
+    for (int u = 0; u < NQS; ++u) {
+      if (!act[u]) continue;
+      const int qsu = qs + 32 * u;
       float o[16];
 #pragma unroll
       for (int ch = 0; ch < 4; ++ch) {
-        const float4 f = *reinterpret_cast<const float4*>(xo + ch * 256);
+        const float4 f = *reinterpret_cast<const float4*>(xother + u * 1024 + ch * 256);
         o[4 * ch] = f.x; o[4 * ch + 1] = f.y; o[4 * ch + 2] = f.z; o[4 * ch + 3] = f.w;
       }
       f32x16 pd, ds;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const float p = team == 0 ? acc[e] : o[e];
-        const float x = team == 0 ? o[e] : acc[e];
+        const float p = team == 0 ? acc[u][e] : o[e];
+        const float x = team == 0 ? o[e] : acc[u][e];
         ds[e] = p * x;   // dS (1/(1-p) in dkscale)
-        pd[e] = DROP ? __uint_as_float(__float_as_uint(p) & elem_keep(dm_cur, 8 * ((qs >> 5) & 1), e)) : p;
+        pd[e] = DROP ? __uint_as_float(__float_as_uint(p) & elem_keep(dm_cur, 8 * ((qsu >> 5) & 1), e)) : p;
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const bf16x8 pb = pack8(pd, 8 * s);
         const bf16x8 db = pack8(ds, 8 * s);
-        const int rofs = 16 * s * RB;
+        const int rofs = (32 * u + 16 * s) * RB;
 #pragma unroll
         for (int dt = 0; dt < NDL; ++dt) {
           const bf16x8 dot = cat(tr_read(Ot + rofs, offT[dt][0]), tr_read(Ot + rofs, offT[dt][1]));
@@ -1221,26 +1245,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   };
 
   auto step = [&](char* Qc, char* Oc, float* Lc, float* Dc, char* Qn, char* On, float* Ln, float* Dn,
-                  int t, int xb) __attribute__((always_inline)) {
+                  int t) __attribute__((always_inline)) {
     vm_drain();
     __syncthreads();
     if (t + 1 < cnt) {
       issue(Qn, On, Ln, Dn, t + 1);
       dm_next = dmload(t + 1);
     }
-    compute(Qc, Oc, Lc, Dc, t, xmine + xb * 8 * 1024, xother + xb * 8 * 1024);
+    compute(Qc, Oc, Lc, Dc, t);
     dm_cur = dm_next;
   };
   if (cnt > 0) {
     issue(q0, o0, l0, d0, 0);
     dm_cur = dmload(0);
   }
-  // the exchange buffer alternates per step: a wave's write of step t + 1 cannot reach the
-  // slot its partner is still reading for step t (one barrier lies between them, two before
-  // the same slot is written again)
   for (int t = 0; t < cnt; t += 2) {
-    step(q0, o0, l0, d0, q1, o1, l1, d1, t, 0);
-    if (t + 1 < cnt) step(q1, o1, l1, d1, q0, o0, l0, d0, t + 1, 1);
+    step(q0, o0, l0, d0, q1, o1, l1, d1, t);
+    if (t + 1 < cnt) step(q1, o1, l1, d1, q0, o0, l0, d0, t + 1);
   }
 
   if (!(key < S)) return;
@@ -1272,6 +1293,7 @@ int g_qbk_fwd = 128, g_qbk_dq = 64;
 // 280.1 vs 280.2 us; a ping-pong schedule (teams offset by one of four barrier-separated
 // segments per tile, 3-slot ring) 452.7 vs 275.3 us -- four barriers per 32-row tile cost
 // more than the matrix / vector pairing recovers, and it spilled at 256 VGPRs.
+// 2 = single pass with 64 query rows per step (two subtiles per ring / exchange barrier).
 int g_kmajor128_variant = 0;
 
 template <int D, bool DQ>
@@ -1348,6 +1370,10 @@ hipError_t launch_kmajor(bool causal, bool drop, int S, int B, hipStream_t s,
       hipLaunchKernelGGL((flash_kmajor128_kernel<C, DR, true>), grid, dim3(512), 0, s, q, k, v, ldq, \
                          ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq, Hkv, klen, c, \
                          dkscale, dvscale, dbits, NB, NQT);                                         \
+    else if (g_kmajor128_variant == 2)                                                              \
+      hipLaunchKernelGGL((flash_kmajor128_kernel<C, DR, false, 64>), grid, dim3(512), 0, s, q, k, v, \
+                         ldq, ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq, Hkv,     \
+                         klen, c, dkscale, dvscale, dbits, NB, NQT);                                \
     else                                                                                            \
       hipLaunchKernelGGL((flash_kmajor128_kernel<C, DR, false>), grid, dim3(512), 0, s, q, k, v,    \
                          ldq, ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq, Hkv,     \
@@ -1377,7 +1403,7 @@ MX_EXPORT int mx_flash_qmajor_bk(int fwd, int dq) {
 // Returns the old one.
 MX_EXPORT int mx_flash_kmajor128_variant(int variant) {
   const int old = g_kmajor128_variant;
-  if (variant == 0 || variant == 1) g_kmajor128_variant = variant;
+  if (variant >= 0 && variant <= 2) g_kmajor128_variant = variant;
   return old;
 }
 

@@ -33,7 +33,12 @@ SIGNATURES = {
     "mx_norm_split_cols": [I],
     "mx_norm_bwd_rows_per_wave": [I],
     "mx_flash_qmajor_bk": [I, I],
-    "mx_flash_kmajor128_two_pass": [I],
+    "mx_flash_kmajor128_variant": [I],
+    # graph.hip (host-side hipGraph post-processing; no stream argument)
+    "mx_graph_census": [P, P, I],
+    "mx_graph_memcpy_nodes": [P, P, I],
+    "mx_graph_snapshot_h2d": [P, P, I],
+    "mx_graph_free": [P, I],
     "mx_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],
     "mx_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
     "mx_bda_norm_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, F, P, U32, I, P],

@@ -33,6 +33,9 @@ def main():
         "proj_dgrad": ("dg0", T, h, h),
         "qkv_dgrad": ("dg0", T, h, 3 * h),
     }
+    if os.environ.get("LMHEAD"):   # tied LM head: logits = X E^T, dX = dlogits E
+        V = int(os.environ.get("V", 50304))
+        probs = {"lm_fwd": ("fwd0", T, V, h), "lm_dgrad": ("dg0", T, h, V)}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 
     def t_once(fn, reps=int(os.environ.get("REPS", 20))):

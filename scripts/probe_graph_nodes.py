@@ -60,6 +60,10 @@ def build_hsaco() -> str:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=300)
+    ap.add_argument("--no-h2d", action="store_true", help="leave the host-to-device copies out of the graph")
+    ap.add_argument("--fix", action="store_true",
+                    help="rewrite the captured host-sourced copies into device snapshots (mxtrain.runtime.graphfix) "
+                         "before instantiation")
     a = ap.parse_args()
     import torch
     hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
@@ -101,7 +105,8 @@ def main() -> int:
                                   ctypes.c_size_t(4 * n), 1, ctypes.c_void_p(stream)) == 0
 
     def body(stream):
-        h2d(stream)
+        if not a.no_h2d:
+            h2d(stream)
         for rd in range(R):
             # memset -> accumulate (x2) -> snapshot: expect 2 everywhere
             assert hip.hipMemsetAsync(ctypes.c_void_p(acc.data_ptr()), 0, ctypes.c_size_t(4 * n), ctypes.c_void_p(stream)) == 0
@@ -122,9 +127,24 @@ def main() -> int:
     torch.cuda.synchronize()
     ref = (out_ms.clone(), out_cp.clone(), out_lds.clone())
     s = torch.cuda.Stream()
-    g = torch.cuda.CUDAGraph()
+    g = torch.cuda.CUDAGraph(keep_graph=True)
     with torch.cuda.graph(g, stream=s):
         body(s.cuda_stream)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from mxtrain.runtime import graphfix
+    print(f"[nodes] census {graphfix.census(g)}", flush=True)
+    try:
+        mc = graphfix.memcpy_nodes(g)
+        kinds = {}
+        for m in mc:
+            kinds[(m["src_mem"], m["dst_mem"])] = kinds.get((m["src_mem"], m["dst_mem"]), 0) + 1
+        print(f"[nodes] memcpy nodes: {len(mc)} by (src, dst) memory {kinds}; first {mc[:2]}", flush=True)
+    except RuntimeError as e:
+        print(f"[nodes] memcpy node params: {e}", flush=True)
+    fix = graphfix.snapshot_host_copies(g) if a.fix else None
+    if fix is not None:
+        print(f"[nodes] rewrote {len(fix)} host-sourced copies into device snapshots", flush=True)
+    g.instantiate()
     for t in (out_ms, out_cp, out_lds, acc, cpy, d_page, d_pin):
         t.fill_(-1)
     for i in range(n):                      # rewrite both host sources after the capture
@@ -149,7 +169,13 @@ def main() -> int:
                                   ("dynamic LDS 48 KiB", out_lds, ref[2], exp_lds)):
         e_ok, r_ok = torch.equal(eager, exp), torch.equal(got, exp)
         bad = int((got != exp).sum().item())
-        print(f"[nodes] {name}: eager_ok={e_ok} replay_ok={r_ok} (wrong {bad}) packet_capture={pc}", flush=True)
+        detail = ""
+        if bad and got.numel() % n == 0:
+            rows = (got != exp).view(-1, n).any(1).nonzero().flatten().tolist()
+            vals = [sorted(set(got.view(-1, n)[r].tolist()))[:4] for r in rows[:4]]
+            detail = f" rounds {rows[:8]} values {vals}"
+        print(f"[nodes] {name}: eager_ok={e_ok} replay_ok={r_ok} (wrong {bad}){detail} packet_capture={pc} "
+              f"fix={a.fix}", flush=True)
         ok &= e_ok and r_ok
     print("[nodes] OK" if ok else "[nodes] MISMATCH", flush=True)
     return 0

@@ -370,8 +370,11 @@ def test_pytorchjob_records_and_applies_placement(home, monkeypatch):
     monkeypatch.setenv("MXTRAIN_SYSFS_ROOT", str(root))
     monkeypatch.setenv("MXTRAIN_NUM_GPUS", "4")
     monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
-    probe = ("import os, json; print('AFF', os.environ['HOSTNAME'], os.environ['MXTRAIN_RANK_CPUSETS'].replace(' ', ''), "
-             "json.dumps(sorted(os.sched_getaffinity(0)), separators=(',', ':')))")
+    # (every replica lingers after printing: the job succeeds with its master and the
+    # controller then stops the workers, so on a loaded host a worker still starting its
+    # interpreter could be stopped before its line)
+    probe = ("import os, json, time; print('AFF', os.environ['HOSTNAME'], os.environ['MXTRAIN_RANK_CPUSETS'].replace(' ', ''), "
+             "json.dumps(sorted(os.sched_getaffinity(0)), separators=(',', ':')), flush=True); time.sleep(8)")
     v = _values(home, {"resources": {"nnodes": 2, "nproc_per_node": 2},
                        "train": {"command": ["python3"], "args": ["-c", f'"{probe}"']}})
     st = _install("training/pytorchjob-distributed", "numa", [v])
