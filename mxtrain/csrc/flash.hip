@@ -1030,7 +1030,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
 // element instead of two.  Q / dO tiles of 32 rows stream through the LDS-DMA ring as in
 // flash_kmajor_kernel; two barriers per tile (ring, exchange), executed by every wave
 // whatever its causal / tail state, so the barrier counts of all waves match.
-template <bool CAUSAL, bool DROP, bool RAGGED, int QT = 32>
+template <bool CAUSAL, bool DROP, bool RAGGED>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void flash_kmajor128_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, int ldq, int ldk, int ldv,
@@ -1038,12 +1038,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const float* __restrict__ delta, uint16_t* __restrict__ dk, uint16_t* __restrict__ dv,
     int lddk, int lddv, int S, int Hq, int Hkv, const int* __restrict__ klen, float c,
     float dkscale, float dvscale, const uint32_t* __restrict__ dbits, int NB, int NQT) {
-  // QT query rows per step (32 or 64 = NQS subtiles of 32; one ring barrier and one
-  // exchange barrier per step either way)
-  constexpr int D = 128, KB = 128, NQS = QT / 32, NKK = D / 16, NDL = 2;
+  // 32 query rows per step (NQS = 1 subtile; 64 rows per step spilled at 256 VGPRs and
+  // measured 349.9 vs 299.7 us).  One exchange buffer: a wave writes it after the ring
+  // barrier of step t + 1, and every partner read of step t precedes that barrier (two
+  // alternating buffers measured the same, 300.2 vs 299.7 us on one box).
+  constexpr int D = 128, KB = 128, QT = 32, NQS = QT / 32, NKK = D / 16, NDL = 2;
   constexpr int RB = D * 2, CPR = D / 8, RPP = 64 / CPR;
   constexpr int QTILE = QT * RB, PIECES = QTILE / 1024, PPW = (2 * PIECES) / 8;
-  static_assert(QT == 32 || QT == 64, "32 or 64 query rows per step");
   static_assert(PPW * 8 == 2 * PIECES, "8 waves issue the Q + dO pieces");
   __shared__ __attribute__((aligned(16))) char q0[QTILE];
   __shared__ __attribute__((aligned(16))) char q1[QTILE];
@@ -1054,8 +1055,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __shared__ __attribute__((aligned(16))) float d0[64];
   __shared__ __attribute__((aligned(16))) float d1[64];
   // [wave][subtile][4 chunks][64 lanes][4 floats]: a wave's 16 elements of a subtile as four
-  // 16-B slots.  One buffer: a wave writes it after the ring barrier of step t + 1, and every
-  // partner read of step t precedes that barrier.
+  // 16-B slots
   __shared__ __attribute__((aligned(16))) float xch[8 * NQS * 1024];
 
   const int tid = threadIdx.x, lane = tid & 63, w = uni(tid >> 6);
@@ -1293,7 +1293,6 @@ int g_qbk_fwd = 128, g_qbk_dq = 64;
 // 280.1 vs 280.2 us; a ping-pong schedule (teams offset by one of four barrier-separated
 // segments per tile, 3-slot ring) 452.7 vs 275.3 us -- four barriers per 32-row tile cost
 // more than the matrix / vector pairing recovers, and it spilled at 256 VGPRs.
-// 2 = single pass with 64 query rows per step (two subtiles per ring / exchange barrier).
 int g_kmajor128_variant = 0;
 
 template <int D, bool DQ>
@@ -1370,10 +1369,6 @@ hipError_t launch_kmajor(bool causal, bool drop, int S, int B, hipStream_t s,
       hipLaunchKernelGGL((flash_kmajor128_kernel<C, DR, true>), grid, dim3(512), 0, s, q, k, v, ldq, \
                          ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq, Hkv, klen, c, \
                          dkscale, dvscale, dbits, NB, NQT);                                         \
-    else if (g_kmajor128_variant == 2)                                                              \
-      hipLaunchKernelGGL((flash_kmajor128_kernel<C, DR, false, 64>), grid, dim3(512), 0, s, q, k, v, \
-                         ldq, ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq, Hkv,     \
-                         klen, c, dkscale, dvscale, dbits, NB, NQT);                                \
     else                                                                                            \
       hipLaunchKernelGGL((flash_kmajor128_kernel<C, DR, false>), grid, dim3(512), 0, s, q, k, v,    \
                          ldq, ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq, Hkv,     \
@@ -1403,7 +1398,7 @@ MX_EXPORT int mx_flash_qmajor_bk(int fwd, int dq) {
 // Returns the old one.
 MX_EXPORT int mx_flash_kmajor128_variant(int variant) {
   const int old = g_kmajor128_variant;
-  if (variant >= 0 && variant <= 2) g_kmajor128_variant = variant;
+  if (variant == 0 || variant == 1) g_kmajor128_variant = variant;
   return old;
 }
 

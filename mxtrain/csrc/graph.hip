@@ -1,24 +1,53 @@
-// hipGraph post-processing between capture and instantiation (host code, HIP runtime API).
+// hipGraph post-processing between capture and instantiation (HIP runtime API + one fill
+// kernel).
 //
 // Why: with the HIP runtime's graph packet capture (dispatch packets pre-built at
-// instantiation, DEBUG_CLR_GRAPH_PACKET_CAPTURE=1, the runtime default), a captured
-// host-to-device memcpy node breaks the ordering of later memset nodes against the kernels
-// around them: scripts/probe_graph_nodes.py, one MI355X, ROCm 7 runtime -- a graph of
-// [H2D copy] then 50 x [memset acc, add_one, add_one, snapshot] replays with one round's
-// snapshot wrong, while the same graph without the H2D node, or with packet capture off,
-// replays exactly.  The whole-step Mask R-CNN graph holds such nodes (library code stages
-// arguments host -> device inside the capture) and its memsets zero buffers that are then
-// accumulated into and used for indexing, hence the illegal-address fault of the replay.
+// instantiation, DEBUG_CLR_GRAPH_PACKET_CAPTURE, the runtime default), MEMSET NODES replay
+// wrong on this runtime (one MI355X, profiles/r3_s4/):
+//   * scripts/probe_graph_memsets.py: [copy, fill, memset, add, checksum] x 40 cases --
+//     the first replay is exact, later replays get 4- and 12-byte memsets wrong;
+//   * tests/test_graph_gpu.py: 64 x [16 KiB memset, add, add, D2D copy, add, snapshot] --
+//     rounds wrong from the first replay;
+//   * scripts/probe_graph_nodes.py: with a host-to-device copy node in front, the first
+//     [memset, add, add, snapshot] round replays with garbage.
+// With packet capture off every case is exact.  The Mask R-CNN whole-step graph holds 124
+// memset nodes (MIOpen zeroes accumulation workspaces and index buffers with
+// hipMemsetAsync), which is what made its replay take an illegal-address fault after a few
+// steps with packet capture on.
 //
-// Fix: after capture, every memcpy node whose source is host memory is rewritten into a
-// device-to-device copy from a device snapshot of the source bytes taken at rewrite time.
-// That is also the only meaning such a node can have in a replayed graph (CUDA refuses a
-// pageable-source copy during capture outright; HIP records it and re-reads the host
-// buffer at every replay -- by then usually freed and reused, see the probe).  The snapshots
-// live as long as the graph (the caller frees them with mx_graph_free).
+// Fix: mx_graph_memsets_to_kernels replaces every memset node by a kernel node of
+// graph_fill_kernel with the same parameters and the same dependency edges, so the graph
+// holds only kernel (and copy) nodes and the packet-capture path builds ordinary dispatch
+// packets for all of it.  mx_graph_census reports node kinds before / after.
 #include "common.h"
 
+#include <algorithm>
 #include <vector>
+
+namespace {
+
+// memset semantics for a [height][width] region of elementSize-byte elements at `pitch`
+// bytes per row: every element = value (1, 2 or 4 bytes).  Rows are filled in 16-byte
+// vectors between an unaligned head and tail (the element pattern repeats every 16 bytes
+// because elementSize divides 16 and dst is elementSize-aligned).
+__global__ __launch_bounds__(256) void graph_fill_kernel(char* __restrict__ dst, size_t pitch, uint32_t value,
+                                                         int esz, size_t width, size_t height) {
+  const uint32_t v = esz == 1 ? (value & 0xFFu) * 0x01010101u : esz == 2 ? (value & 0xFFFFu) * 0x00010001u : value;
+  const uint4 v4 = make_uint4(v, v, v, v);
+  const size_t rowb = width * (size_t)esz;
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+  for (size_t r = 0; r < height; ++r) {
+    char* row = dst + r * pitch;
+    const size_t head = min(rowb, (size_t)((16 - ((uintptr_t)row & 15)) & 15));
+    const size_t nvec = (rowb - head) / 16;
+    const size_t tail0 = head + nvec * 16;
+    for (size_t i = tid; i < nvec; i += nth) *reinterpret_cast<uint4*>(row + head + 16 * i) = v4;
+    for (size_t b = tid; b < head; b += nth) row[b] = (char)(v >> (8 * (((uintptr_t)row + b) & 3)));
+    for (size_t b = tail0 + tid; b < rowb; b += nth) row[b] = (char)(v >> (8 * (((uintptr_t)row + b) & 3)));
+  }
+}
+
+}  // namespace
 
 namespace {
 
@@ -47,104 +76,59 @@ MX_EXPORT int mx_graph_census(void* graph, int* counts, int ncounts) {
   return n;
 }
 
-namespace {
-
-// Parameters of a memcpy node through the driver-style getter (HIP_MEMCPY3D: memory types,
-// host / device pointers, widths), which this runtime fills for the 1-D copies stream
-// capture records; hipGraphMemcpyNodeGetParams leaves its hipMemcpy3DParms unfilled for
-// them (scripts/probe_graph_nodes.py).  Returns false when the node cannot be read or is
-// not a plain 1-D linear copy.
-struct Copy1D {
-  const void* src;
-  void* dst;
-  size_t bytes;
-  bool src_host, dst_host;
-};
-bool read_copy(hipGraphNode_t nd, Copy1D& c) {
-  HIP_MEMCPY3D p{};
-  if (hipDrvGraphMemcpyNodeGetParams(nd, &p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  if (p.srcArray || p.dstArray || p.Height > 1 || p.Depth > 1 || p.srcY || p.srcZ || p.dstY || p.dstZ)
-    return false;
-  c.src_host = p.srcMemoryType == hipMemoryTypeHost || p.srcMemoryType == hipMemoryTypeUnregistered;
-  c.dst_host = p.dstMemoryType == hipMemoryTypeHost || p.dstMemoryType == hipMemoryTypeUnregistered;
-  c.src = c.src_host ? (const char*)p.srcHost + p.srcXInBytes : (const char*)p.srcDevice + p.srcXInBytes;
-  c.dst = c.dst_host ? (char*)p.dstHost + p.dstXInBytes : (char*)p.dstDevice + p.dstXInBytes;
-  c.bytes = p.WidthInBytes;
-  return true;
-}
-
-}  // namespace
-
-// rows of {src, dst, bytes, src_memory_type, dst_memory_type} for every memcpy node (up to
-// max_rows; memory type 1 = host, 2 = device, -1 = unreadable node); returns the number of
-// memcpy nodes or -1 on an API error
-MX_EXPORT int mx_graph_memcpy_nodes(void* graph, int64_t* out, int max_rows) {
+// Replace every memset node of `graph` by a graph_fill_kernel node with the same region and
+// value and the same incoming / outgoing edges (see the top of the file).  Returns the
+// number of replaced nodes, or a negative error: -1 API failure, -2 a memset node whose
+// parameters cannot be read (nothing is changed then), -3 an element size other than
+// 1 / 2 / 4.
+MX_EXPORT int mx_graph_memsets_to_kernels(void* graph) {
+  hipGraph_t g = (hipGraph_t)graph;
   std::vector<hipGraphNode_t> nodes;
-  if (graph_nodes((hipGraph_t)graph, nodes) < 0) return -1;
-  int k = 0;
-  for (auto nd : nodes) {
-    hipGraphNodeType t;
-    if (hipGraphNodeGetType(nd, &t) != hipSuccess) return -1;
-    if (t != hipGraphNodeTypeMemcpy) continue;
-    if (k < max_rows) {
-      int64_t* r = out + 5 * k;
-      Copy1D c{};
-      if (read_copy(nd, c)) {
-        r[0] = (int64_t)(uintptr_t)c.src;
-        r[1] = (int64_t)(uintptr_t)c.dst;
-        r[2] = (int64_t)c.bytes;
-        r[3] = c.src_host ? 1 : 2;
-        r[4] = c.dst_host ? 1 : 2;
-      } else {
-        r[0] = r[1] = r[2] = 0;
-        r[3] = r[4] = -1;
-      }
-    }
-    ++k;
-  }
-  return k;
-}
-
-// Rewrite host-to-device 1-D memcpy nodes into device-to-device copies from device
-// snapshots (see the top of the file).  snaps receives the device buffers (at most
-// max_snaps); returns the number of rewritten nodes, or a negative error without having
-// changed anything (-1 API, -2 a memcpy node is unreadable, -5 too many), or -4 after an
-// allocation failure.
-MX_EXPORT int mx_graph_snapshot_h2d(void* graph, void** snaps, int max_snaps) {
-  std::vector<hipGraphNode_t> nodes;
-  if (graph_nodes((hipGraph_t)graph, nodes) < 0) return -1;
-  std::vector<std::pair<hipGraphNode_t, Copy1D>> todo;
+  if (graph_nodes(g, nodes) < 0) return -1;
+  std::vector<std::pair<hipGraphNode_t, hipMemsetParams>> todo;
   for (auto nd : nodes) {   // read everything first: all-or-nothing
     hipGraphNodeType t;
     if (hipGraphNodeGetType(nd, &t) != hipSuccess) return -1;
-    if (t != hipGraphNodeTypeMemcpy) continue;
-    Copy1D c{};
-    if (!read_copy(nd, c)) return -2;
-    if (c.src_host && !c.dst_host) todo.emplace_back(nd, c);
+    if (t != hipGraphNodeTypeMemset) continue;
+    hipMemsetParams p{};
+    if (hipGraphMemsetNodeGetParams(nd, &p) != hipSuccess) {
+      (void)hipGetLastError();
+      return -2;
+    }
+    if (p.elementSize != 1 && p.elementSize != 2 && p.elementSize != 4) return -3;
+    if (p.height == 0) p.height = 1;
+    if (p.height > 1 && p.pitch < p.width * p.elementSize) return -2;
+    todo.emplace_back(nd, p);
   }
-  if ((int)todo.size() > max_snaps) return -5;
   int k = 0;
-  for (auto& [nd, c] : todo) {
-    void* d = nullptr;
-    if (hipMalloc(&d, c.bytes ? c.bytes : 1) != hipSuccess) return -4;
-    if (c.bytes && hipMemcpy(d, c.src, c.bytes, hipMemcpyHostToDevice) != hipSuccess) {
-      (void)hipFree(d);
-      return -1;
-    }
-    if (hipGraphMemcpyNodeSetParams1D(nd, c.dst, d, c.bytes, hipMemcpyDeviceToDevice) != hipSuccess) {
-      (void)hipFree(d);
-      return -1;
-    }
-    snaps[k++] = d;
+  for (auto& [nd, p] : todo) {
+    size_t nd_in = 0, nd_out = 0;
+    if (hipGraphNodeGetDependencies(nd, nullptr, &nd_in) != hipSuccess) return -1;
+    if (hipGraphNodeGetDependentNodes(nd, nullptr, &nd_out) != hipSuccess) return -1;
+    std::vector<hipGraphNode_t> in(nd_in), out(nd_out);
+    if (nd_in && hipGraphNodeGetDependencies(nd, in.data(), &nd_in) != hipSuccess) return -1;
+    if (nd_out && hipGraphNodeGetDependentNodes(nd, out.data(), &nd_out) != hipSuccess) return -1;
+    char* dst = (char*)p.dst;
+    size_t pitch = p.height > 1 ? p.pitch : 0;
+    uint32_t value = p.value;
+    int esz = (int)p.elementSize;
+    size_t width = p.width, height = p.height;
+    const size_t bytes = width * (size_t)esz;
+    const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>((bytes / 16 + 255) / 256, 1024));
+    void* args[] = {&dst, &pitch, &value, &esz, &width, &height};
+    hipKernelNodeParams kp{};
+    kp.func = (void*)graph_fill_kernel;
+    kp.gridDim = dim3(blocks);
+    kp.blockDim = dim3(256);
+    kp.kernelParams = args;
+    kp.sharedMemBytes = 0;
+    kp.extra = nullptr;
+    hipGraphNode_t kn;
+    if (hipGraphAddKernelNode(&kn, g, in.data(), in.size(), &kp) != hipSuccess) return -1;
+    for (auto d : out)
+      if (hipGraphAddDependencies(g, &kn, &d, 1) != hipSuccess) return -1;
+    if (hipGraphDestroyNode(nd) != hipSuccess) return -1;
+    ++k;
   }
   return k;
-}
-
-MX_EXPORT int mx_graph_free(void** bufs, int n) {
-  for (int i = 0; i < n; ++i)
-    if (bufs[i]) (void)hipFree(bufs[i]);
-  return 0;
 }

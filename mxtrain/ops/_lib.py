@@ -34,11 +34,9 @@ SIGNATURES = {
     "mx_norm_bwd_rows_per_wave": [I],
     "mx_flash_qmajor_bk": [I, I],
     "mx_flash_kmajor128_variant": [I],
-    # graph.hip (host-side hipGraph post-processing; no stream argument)
+    # graph.hip (host-side hipGraph inspection; no stream argument)
     "mx_graph_census": [P, P, I],
-    "mx_graph_memcpy_nodes": [P, P, I],
-    "mx_graph_snapshot_h2d": [P, P, I],
-    "mx_graph_free": [P, I],
+    "mx_graph_memsets_to_kernels": [P],
     "mx_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],
     "mx_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
     "mx_bda_norm_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, F, P, U32, I, P],
@@ -64,6 +62,7 @@ SIGNATURES = {
     "mx_ce_stats": [P, P, I, I, I64, P, P, P, P],
     "mx_ce_lse": [P, P, P, I, P],
     "mx_ce_grad": [P, P, I, I, I64, P, P, P, P, F, I, P],
+    "mx_ce_fused": [P, P, I, I, P, P, F, I, P],
     # detloss.hip
     "mx_detloss_max_blocks": [],
     "mx_rpn_loss_fwd": [P, P, P, P, P, I, F, P, P, P],

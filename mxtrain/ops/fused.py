@@ -235,6 +235,17 @@ def cross_entropy_fwd_bwd(logits, labels, grad_scale, ignore_index=-100, tp_grou
     the row statistics are combined across the tensor-parallel group (vocab-parallel CE,
     three tiny all-reduces: max, rescaled sum, target logit).
     """
+    rows, V = logits.shape
+    if tp_group is None and vocab_start == 0 and _lib.use_hip(logits) and V % 8 == 0 and V <= 64 * 256 * 8:
+        # one pass, the row held in registers (csrc/fused.hip ce_fused_kernel)
+        loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
+        if torch.is_tensor(grad_scale):
+            sp, sv = _lib.ptr(grad_scale), 0.0
+        else:
+            sp, sv = None, float(grad_scale)
+        _lib.call("mx_ce_fused", _lib.ptr(logits), _lib.ptr(labels), rows, V, _lib.ptr(loss), sp, sv,
+                  ignore_index, _lib.stream())
+        return loss
     m, s, tgt = ce_stats(logits, labels, vocab_start)
     if tp_group is not None:
         import torch.distributed as dist

@@ -305,7 +305,7 @@ class GPTTrainer:
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self._static = (tokens.clone(), labels.clone())
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph(keep_graph=True)
         # the optimizer step counter / hyper-parameters are host-driven: set_hyper copies
         # from a pinned buffer that the captured memcpy re-reads on every replay
         step0 = [o.step_count for o in self._opts]
@@ -313,6 +313,12 @@ class GPTTrainer:
             loss = self._graph_body()
         for o, c in zip(self._opts, step0):
             o.step_count = c
+        # memset nodes replay wrong under the runtime's graph packet capture: fill kernels
+        # instead (csrc/graph.hip); the census is kept for diagnostics
+        from mxtrain.runtime import graphfix
+        self.graph_census = graphfix.census(g)
+        self.graph_census["memsets_as_kernels"] = graphfix.memsets_to_kernels(g)
+        g.instantiate()
         self._graph = g
         self._static_loss = loss
         return last

@@ -71,8 +71,7 @@ def sgd_momentum_(opt: torch.optim.SGD, lr) -> None:
 
 class GraphedTrainStep:
     def __init__(self, model, opt: torch.optim.SGD, params: List[torch.Tensor], clip: float, device,
-                 flat_capacity: int = 16 << 20, flat_master=None, allow_rccl_capture: bool = False,
-                 snapshot_host_copies: bool = False):
+                 flat_capacity: int = 16 << 20, flat_master=None, allow_rccl_capture: bool = False):
         self.model, self.opt, self.params, self.clip, self.device = model, opt, params, clip, device
         self.graphs: Dict[tuple, tuple] = {}
         # with a FlatMaster (models/compute_weights.py) the update is its fused clip + SGD
@@ -93,8 +92,7 @@ class GraphedTrainStep:
         # MXTRAIN_GRAPH_DEBUG=1: synchronise after every step and log capture/replay events
         self.debug = os.environ.get("MXTRAIN_GRAPH_DEBUG", "0") == "1"
         self.marker = None   # diagnostics hook: called around the capture window
-        self.graph_info: Dict[tuple, dict] = {}   # per captured shape: node census, rewritten copies
-        self.snapshot_host_copies = snapshot_host_copies
+        self.graph_info: Dict[tuple, dict] = {}   # per captured shape: node census
 
     def _dbg(self, what: str, key) -> None:
         if self.debug:
@@ -141,23 +139,19 @@ class GraphedTrainStep:
         self.flat = torch.zeros(cap, dtype=torch.uint8, device=self.device)
 
     def _drop_graphs(self) -> None:
-        fixes = [e[3] for e in self.graphs.values()]
         self.graphs.clear()
-        torch.cuda.synchronize(self.device)
-        for f in fixes:   # the snapshot buffers outlive every replay of their graph
-            f.release()
 
-    def _finish_capture(self, g, key) -> object:
-        """Between capture and instantiation: host-sourced copy nodes become device-to-device
-        copies from snapshots (csrc/graph.hip: with the runtime's graph packet capture they
-        break the ordering of later memset nodes; CUDA would have refused them outright)."""
+    def _finish_capture(self, g, key) -> None:
+        """Between capture and instantiation: memset nodes (MIOpen zeroes its accumulation
+        workspaces and index buffers with hipMemsetAsync) replay wrong under the runtime's
+        graph packet capture -- the cause of this step's illegal-address fault after a few
+        replays (csrc/graph.hip) -- so they become fill-kernel nodes; the node census before
+        the rewrite is kept for diagnostics."""
         from mxtrain.runtime import graphfix
         info = {"nodes": graphfix.census(g)}
-        fix = graphfix.snapshot_host_copies(g) if self.snapshot_host_copies else graphfix.HostCopySnapshots([])
-        info["host_copies_snapshotted"] = len(fix)
+        info["memsets_as_kernels"] = graphfix.memsets_to_kernels(g)
         self.graph_info[key] = info
         g.instantiate()
-        return fix
 
     def __call__(self, batch: Dict[str, torch.Tensor], lr: float) -> Dict[str, torch.Tensor]:
         flat = batch["gt_mask_flat"]
@@ -191,15 +185,15 @@ class GraphedTrainStep:
                     sout = self._body(st)
                 if self.marker is not None:
                     self.marker("capture-end")
-                fix = self._finish_capture(g, key)
+                self._finish_capture(g, key)
             cur.wait_stream(self.stream)
-            self.graphs[key] = (g, st, sout, fix)
+            self.graphs[key] = (g, st, sout)
             self.captures += 1
             self._dbg("captured", key)
             if self.debug:
                 print(f"[graphed] graph {key}: {self.graph_info[key]}", file=sys.stderr, flush=True)
             return dict(zip(LOSS_NAMES, out.unbind(0)))
-        g, st, sout, _ = entry
+        g, st, sout = entry
         for k in INPUT_KEYS:
             st[k].copy_(batch[k], non_blocking=True)
         self.flat[:flat.numel()].copy_(flat, non_blocking=True)

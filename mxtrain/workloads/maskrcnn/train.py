@@ -447,7 +447,9 @@ def main(argv=None):
                                     "n_gpus": world, "batch_per_gpu": bs,
                                     "graph": None if gstep is None else
                                     {"captures": gstep.captures, "replays": gstep.replays,
-                                     "eager": gstep.eager_steps},
+                                     "eager": gstep.eager_steps,
+                                     "packet_capture": os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "runtime default"),
+                                     "nodes": [v for v in gstep.graph_info.values()]},
                                     "flat_sgd": fm is not None,
                                     "dp_routes": sorted(fm.dp_routes) if fm is not None else None}) + "\n")
     hvd.shutdown()

@@ -12,6 +12,7 @@ def main(path):
     inside = False
     recent = collections.deque(maxlen=3)
     kinds = collections.Counter()
+    msz = collections.Counter()
     shown = 0
     for line in open(path, errors="replace"):
         if "capture-begin" in line:
@@ -30,10 +31,18 @@ def main(path):
             k = re.search(r"(hipMemcpy\w+To\w+|hipMemcpyDefault)", line)
             kind = k.group(1) if k else ("memset" if "Memset" in line else "?")
             kinds[kind] += 1
+            if kind == "memset":
+                m2 = re.search(r"hipMemsetAsync \(\s*(0x[0-9a-f]+),\s*(-?\d+),\s*(\d+)", line)
+                if m2:
+                    ptr, val, size = int(m2.group(1), 16), int(m2.group(2)), int(m2.group(3))
+                    msz[(size, ptr % 16, val)] += 1
             if kind not in ("hipMemcpyDeviceToDevice", "memset") and shown < 40:
                 print(f"{line.strip()[:200]}\n    after: {list(recent)}")
                 shown += 1
     print("inside the capture window:", dict(kinds))
+    print("memsets by (bytes, dst % 16, value):")
+    for (size, al, val), c in sorted(msz.items()):
+        print(f"  {c:4d} x  {size:>12d} B  dst%16={al:2d}  value={val}")
 
 
 if __name__ == "__main__":

@@ -6,10 +6,6 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 200 python -u scripts/probe_graph_nodes.py --rounds 50 --fix > gpurun_out/r3y_nodes_fix.log 2>&1 || { tail -20 gpurun_out/r3y_nodes_fix.log; exit 1; }
-grep nodes gpurun_out/r3y_nodes_fix.log
-timeout -k 10 200 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_graph_gpu.py > gpurun_out/r3y_test_graph.log 2>&1 || { tail -30 gpurun_out/r3y_test_graph.log; exit 1; }
-tail -3 gpurun_out/r3y_test_graph.log
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "d128 or flash_attention" > gpurun_out/r3y_tests.log 2>&1 || { tail -40 gpurun_out/r3y_tests.log; exit 1; }
 tail -2 gpurun_out/r3y_tests.log
 for var in 2 0; do

@@ -61,9 +61,8 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=300)
     ap.add_argument("--no-h2d", action="store_true", help="leave the host-to-device copies out of the graph")
-    ap.add_argument("--fix", action="store_true",
-                    help="rewrite the captured host-sourced copies into device snapshots (mxtrain.runtime.graphfix) "
-                         "before instantiation")
+    ap.add_argument("--memset-kernels", action="store_true",
+                    help="replace the captured memset nodes by fill-kernel nodes (mxtrain.runtime.graphfix)")
     a = ap.parse_args()
     import torch
     hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
@@ -133,17 +132,8 @@ def main() -> int:
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from mxtrain.runtime import graphfix
     print(f"[nodes] census {graphfix.census(g)}", flush=True)
-    try:
-        mc = graphfix.memcpy_nodes(g)
-        kinds = {}
-        for m in mc:
-            kinds[(m["src_mem"], m["dst_mem"])] = kinds.get((m["src_mem"], m["dst_mem"]), 0) + 1
-        print(f"[nodes] memcpy nodes: {len(mc)} by (src, dst) memory {kinds}; first {mc[:2]}", flush=True)
-    except RuntimeError as e:
-        print(f"[nodes] memcpy node params: {e}", flush=True)
-    fix = graphfix.snapshot_host_copies(g) if a.fix else None
-    if fix is not None:
-        print(f"[nodes] rewrote {len(fix)} host-sourced copies into device snapshots", flush=True)
+    if a.memset_kernels:
+        print(f"[nodes] replaced {graphfix.memsets_to_kernels(g)} memset nodes by fill kernels", flush=True)
     g.instantiate()
     for t in (out_ms, out_cp, out_lds, acc, cpy, d_page, d_pin):
         t.fill_(-1)
@@ -175,7 +165,7 @@ def main() -> int:
             vals = [sorted(set(got.view(-1, n)[r].tolist()))[:4] for r in rows[:4]]
             detail = f" rounds {rows[:8]} values {vals}"
         print(f"[nodes] {name}: eager_ok={e_ok} replay_ok={r_ok} (wrong {bad}){detail} packet_capture={pc} "
-              f"fix={a.fix}", flush=True)
+              f"h2d_nodes={not a.no_h2d} memset_kernels={a.memset_kernels}", flush=True)
         ok &= e_ok and r_ok
     print("[nodes] OK" if ok else "[nodes] MISMATCH", flush=True)
     return 0

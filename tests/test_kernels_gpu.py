@@ -238,7 +238,7 @@ def test_flash_d128_single_pass_matches_two_pass(S, causal, pdrop, padded):
     outs = []
     old = _lib._fn("mx_flash_kmajor128_variant")(-1)
     try:
-        for variant in (0, 1, 2):   # single pass, two column-half passes, single pass 64 rows/step
+        for variant in (0, 1):   # single pass, two column-half passes
             _lib._fn("mx_flash_kmajor128_variant")(variant)
             dqkv = torch.zeros_like(qkv)
             A.attn_bwd(do, q, k, v, o, lse, B, S, H, H, D, causal, klen, dq=dqkv[:, :H * D],
@@ -249,7 +249,6 @@ def test_flash_d128_single_pass_matches_two_pass(S, causal, pdrop, padded):
         _lib._fn("mx_flash_kmajor128_variant")(old)
     assert torch.isfinite(outs[0].float()).all()
     assert torch.equal(outs[0], outs[1])
-    assert torch.equal(outs[0], outs[2])
 
 
 def _crow(e, hh):
