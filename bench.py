@@ -244,6 +244,8 @@ def main():
         }
         if graph_err:
             out["graph_error"] = graph_err
+        if use_graph and getattr(tr, "graph_census", None):
+            out["graph_nodes"] = tr.graph_census
         if world == 1 and not args.no_maskrcnn:
             # BASELINE.json metric, part 2: Mask R-CNN images/s (outside the GPT timed window)
             del tr

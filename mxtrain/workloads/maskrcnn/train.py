@@ -202,16 +202,12 @@ def get_args(argv=None):
 
 def main(argv=None):
     args = get_args(argv)
-    if args.mx_graph != "0":
-        # Whole-step hipGraph replay with the convolution solvers MIOpen's find picks
-        # (the in-repo find-db) takes an illegal-address fault under the HIP runtime's graph
-        # packet-capture mode (dispatch packets pre-built at instantiation) and replays
-        # cleanly with it off; immediate-mode solvers replay cleanly either way (one
-        # MI355X, scripts/bench_maskrcnn.py --graph 1 and scripts/graph_diag.py, same
-        # inputs).  The flag is read when the HIP runtime initialises, so it is set before
-        # the first GPU call; the graph's kernels are then dispatched one by one by the
-        # runtime -- still no Python / ATen dispatch per op.
-        os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+    # The whole-step hipGraph replays under the HIP runtime's graph packet capture (its
+    # default: dispatch packets pre-built at instantiation, 0.5 ms of host time per replay
+    # at 1 img/GPU instead of 9.0 ms with node-by-node dispatch).  That needs the graph's
+    # memset nodes rewritten into fill kernels (graphed.py, csrc/graph.hip): MIOpen's
+    # hipMemsetAsync nodes replay wrong in packet-capture mode, which made this step fault
+    # after a few replays until round 3 (profiles/r3_s4/).
     from mxtrain.data.coco import AspectGroupedSampler, COCODetection, DetectionDataset, collate
     from mxtrain.models.maskrcnn import MaskRCNN
     from mxtrain.parallel import hvd
