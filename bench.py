@@ -261,7 +261,7 @@ def main():
                 "1img": {k: v for k, v in m1.items() if k != "img_s"},
                 "4img": {k: v for k, v in m4.items() if k != "img_s"},
                 "unit": "images/s", "conv_search": "MIOpen find (in-repo find-db)",
-                "step": "whole-step hipGraph replay (1 GPU)"}
+                "step": "whole-step hipGraph replay (1 GPU), runtime packet capture on, memset nodes as fill kernels"}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

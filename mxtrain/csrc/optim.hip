@@ -30,23 +30,28 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const uint16_t* __restrict__
   float acc = 0.f;
   const int64_t nvec = n / 8;
   const int64_t stride = (int64_t)gridDim.x * 256;
-  // 4 vectors per thread-iteration, loads issued first: one 16-B load in flight per thread
-  // left this 710 MB (355M-parameter) pass latency-bound at ~3.4 TB/s
-  constexpr int U = 4;
+  // U vectors per thread-iteration, every load issued before any math: addresses are
+  // clamped into the buffer and the loads unconditional (a `ok ? load : 0` select made the
+  // compiler wait for each load where it was issued, and the flag byte gated the data load:
+  // two serial memory latencies per vector); skipped chunks / the overhang are masked after
+  constexpr int U = 8;
   for (int64_t v0 = blockIdx.x * 256ll + threadIdx.x; v0 < nvec; v0 += stride * U) {
     uint4 raw[U];
+    uint8_t fl[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t v = v0 + u * stride;
-      const bool ok = v < nvec && !(flags && !flags[(v * 8) >> 6]);
-      raw[u] = ok ? reinterpret_cast<const uint4*>(g)[v] : make_uint4(0, 0, 0, 0);
+      const int64_t v = min(v0 + u * stride, nvec - 1);
+      fl[u] = flags ? flags[(v * 8) >> 6] : (uint8_t)1;
+      raw[u] = reinterpret_cast<const uint4*>(g)[v];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       float a[8];
       unpack8(raw[u], a);
+      float part = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { float t = a[j] * scale; acc += t * t; }
+      for (int j = 0; j < 8; ++j) { float t = a[j] * scale; part += t * t; }
+      acc += (v0 + u * stride < nvec && fl[u]) ? part : 0.f;
     }
   }
   for (int64_t i = nvec * 8 + blockIdx.x * 256ll + threadIdx.x; i < n;
@@ -163,7 +168,8 @@ int g_adam_blocks = 1 << 20;   // one 8-element vector per thread (no grid-strid
 
 }  // namespace
 
-MX_EXPORT int mx_sumsq_nparts() { return 1024; }
+constexpr int kSumsqParts = 2048;   // blocks of sumsq_kernel = partial slots
+MX_EXPORT int mx_sumsq_nparts() { return kSumsqParts; }
 
 // launch shape of mx_adamw_step (unroll 1|2 vectors per thread-iteration, max blocks)
 MX_EXPORT int mx_adamw_config(int unroll, int blocks) {
@@ -177,7 +183,7 @@ MX_EXPORT int mx_adamw_config(int unroll, int blocks) {
 MX_EXPORT int mx_sumsq_bf16(const void* g, int64_t n, float scale, const uint8_t* flags,
                             float* partial, float* normsq_out, int accumulate, hipStream_t s) {
   int64_t blocks = (n / 8 + 255) / 256;
-  if (blocks > 1024) blocks = 1024;
+  if (blocks > kSumsqParts) blocks = kSumsqParts;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
                      (const uint16_t*)g, n, scale, flags, partial);
