@@ -99,6 +99,38 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ int crow(int e, int hh) { return (e & 3) + 8 * (e >> 2) + 4 * hh; }
+// sum over the 32 lanes of the caller's half-wave (every lane gets it): 16-lane row sum by
+// DPP, then the two rows of the half through v_permlane16_swap
+__device__ __forceinline__ float half_sum(float v) {
+  v += MX_DPP(v, 0xB1);
+  v += MX_DPP(v, 0x4E);
+  v += MX_DPP(v, 0x124);
+  v += MX_DPP(v, 0x128);
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// Bias-gradient column partials of a 32-row MFMA output block (QKV bias = column sums of
+// dQ / dK / dV): acc[dt][e] holds column 32 dt + crow(e, hh) of the lane's row; the 32 rows
+// of a half-wave are summed and lanes 0 / 32 store them (fp32, unrounded) into partial row
+// `prow` at column col0 + d.  The caller guarantees all 32 rows exist (S % 32 == 0).
+template <int N>
+__device__ __forceinline__ void bias_partial_store(const f32x16 (&acc)[N], float sc, float* __restrict__ bp,
+                                                   int ldbp, int prow, int col0, int dt0, int lane) {
+  const int hh = lane >> 5;
+  float* row = bp + (size_t)prow * ldbp + col0;
+#pragma unroll
+  for (int dt = 0; dt < N; ++dt) {
+    float sums[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) sums[e] = half_sum(acc[dt][e] * sc);
+    if ((lane & 31) == 0) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        *reinterpret_cast<float4*>(row + 32 * (dt + dt0) + 8 * g4 + 4 * hh) =
+            make_float4(sums[4 * g4], sums[4 * g4 + 1], sums[4 * g4 + 2], sums[4 * g4 + 3]);
+    }
+  }
+}
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // one 1-KiB LDS-DMA piece: lane i's 16 B from `g` land at lds_base + 16 i.  Issued from
@@ -284,7 +316,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
     float* __restrict__ lse, float* __restrict__ delta, uint16_t* __restrict__ dq, int lddq,
     int S, int Hq, int Hkv, const int* __restrict__ klen, float c,
     float oscale /* FWD 1/(1-p); DQ scale/(1-p) */, float dkeep /* 1-p */,
-    const uint64_t* __restrict__ dbits, int NB, int NKT) {
+    const uint64_t* __restrict__ dbits, int NB, int NKT, float* __restrict__ bpart, int ldbp) {
   constexpr int BQ = 128, BK = BKT, NSUB = BK / 32, NKK = D / 16, NDT = D / 32;
   constexpr int RB = D * 2, CPR = D / 8, RPP = 64 / CPR;
   constexpr int TILE = BK * RB, PIECES = TILE / 1024, PPW = PIECES / 4;
@@ -414,6 +446,8 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
         u.y = pack2(acc[dt][4 * g4 + 2] * sc, acc[dt][4 * g4 + 3] * sc);
         *reinterpret_cast<uint2*>(op + d) = u;
       }
+    // dQ's bias-gradient column partials (S % 32 == 0: every row of the wave is valid)
+    if (DQ && bpart) bias_partial_store<NDT>(acc, sc, bpart, ldbp, (b * S + qw) >> 5, hq * D, 0, lane);
   };
   reset();
   load_rows(blk0);
@@ -692,7 +726,8 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
     const uint16_t* __restrict__ dout, int lddo, const float* __restrict__ lse,
     const float* __restrict__ delta, uint16_t* __restrict__ dk, uint16_t* __restrict__ dv,
     int lddk, int lddv, int S, int Hq, int Hkv, const int* __restrict__ klen, float c,
-    float dkscale, float dvscale, const uint32_t* __restrict__ dbits, int NB, int NQT) {
+    float dkscale, float dvscale, const uint32_t* __restrict__ dbits, int NB, int NQT,
+    float* __restrict__ bpart, int ldbp, int bcol) {
   // 64-row Q/dO tiles (32 for D = 128: K image + ring = 65 KB, two workgroups per CU)
   constexpr int KB = 128, KW = 128, QT = D == 64 ? 64 : 32, NQS = QT / 32, NKK = D / 16, NDT = D / 32;
   constexpr int NDL = DP == 0 ? NDT : NDT / 2;
@@ -805,6 +840,11 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
         u.y = pack2(dvacc[dt][4 * g4 + 2] * dvscale, dvacc[dt][4 * g4 + 3] * dvscale);
         *reinterpret_cast<uint2*>(dvp + d) = u;
       }
+    // dK / dV bias-gradient column partials (S % 32 == 0: every key of the wave is valid)
+    if (bpart) {
+      bias_partial_store<NDL>(dkacc, dkscale, bpart, ldbp, (b * S + kw0) >> 5, bcol + hk * D, DT0, lane);
+      bias_partial_store<NDL>(dvacc, dvscale, bpart, ldbp, (b * S + kw0) >> 5, bcol + (Hkv + hk) * D, DT0, lane);
+    }
   };
   load_keys(blk0);
   __builtin_amdgcn_s_waitcnt(0);  // K / V rows complete before the loop (see qmajor)
@@ -1037,7 +1077,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const uint16_t* __restrict__ dout, int lddo, const float* __restrict__ lse,
     const float* __restrict__ delta, uint16_t* __restrict__ dk, uint16_t* __restrict__ dv,
     int lddk, int lddv, int S, int Hq, int Hkv, const int* __restrict__ klen, float c,
-    float dkscale, float dvscale, const uint32_t* __restrict__ dbits, int NB, int NQT) {
+    float dkscale, float dvscale, const uint32_t* __restrict__ dbits, int NB, int NQT,
+    float* __restrict__ bpart, int ldbp, int bcol) {
   // 32 query rows per step (NQS = 1 subtile; 64 rows per step spilled at 256 VGPRs and
   // measured 349.9 vs 299.7 us).  One exchange buffer: a wave writes it after the ring
   // barrier of step t + 1, and every partner read of step t precedes that barrier (two
@@ -1280,6 +1321,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       u.y = pack2(dvacc[dt][4 * g4 + 2] * dvscale, dvacc[dt][4 * g4 + 3] * dvscale);
       *reinterpret_cast<uint2*>(dvp + d) = u;
     }
+  if (bpart) {   // dK / dV bias-gradient column partials (S % 32 == 0)
+    bias_partial_store<NDL>(dkacc, dkscale, bpart, ldbp, (b * S + kw0) >> 5, bcol + hk * D, DT0, lane);
+    bias_partial_store<NDL>(dvacc, dvscale, bpart, ldbp, (b * S + kw0) >> 5, bcol + (Hkv + hk) * D, DT0, lane);
+  }
 }
 
 // ------------------------------------------------------------------------------ launch
@@ -1301,14 +1346,14 @@ hipError_t launch_qmajor(bool causal, bool drop, int S, int B, hipStream_t s,
                          int ldv, const uint16_t* dout, int lddo, uint16_t* o, int ldo, float* lse,
                          float* delta, uint16_t* dq, int lddq, int Hq, int Hkv,
                          const int* klen, float c, float oscale, float dkeep,
-                         const uint64_t* dbits, int NB, int NKT) {
+                         const uint64_t* dbits, int NB, int NKT, float* bpart = nullptr, int ldbp = 0) {
   constexpr bool PAIR = D == 64;
   const int nqb = (S + 127) / 128;
   const dim3 grid((PAIR ? (nqb + 1) / 2 : nqb) * Hq * B);
 #define MX_QM(C, DR, BKT)                                                                              \
   hipLaunchKernelGGL((flash_qmajor_kernel<D, C, DR, DQ, PAIR, BKT>), grid, dim3(PAIR ? 512 : 256), 0, s, \
                      q, k, v, ldq, ldk, ldv, dout, lddo, o, ldo, lse, delta, dq, lddq, S, Hq, Hkv,       \
-                     klen, c, oscale, dkeep, dbits, NB, NKT)
+                     klen, c, oscale, dkeep, dbits, NB, NKT, bpart, ldbp)
 #define MX_QM_B(BKT)                                                          \
   {                                                                           \
     if (causal) { if (drop) MX_QM(true, true, BKT); else MX_QM(true, false, BKT); } \
@@ -1334,7 +1379,7 @@ hipError_t launch_kmajor(bool causal, bool drop, int S, int B, hipStream_t s,
                          int ldv, const uint16_t* dout, int lddo, const float* lse,
                          const float* delta, uint16_t* dk, uint16_t* dv, int lddk, int lddv,
                          int Hq, int Hkv, const int* klen, float c, float dkscale, float dvscale,
-                         const uint32_t* dbits, int NB, int NQT) {
+                         const uint32_t* dbits, int NB, int NQT, float* bpart, int ldbp, int bcol) {
   constexpr bool PAIR = D == 64;
   const int nkb = (S + 127) / 128;
   const dim3 grid((PAIR ? (nkb + 1) / 2 : nkb) * Hkv * B);
@@ -1346,11 +1391,11 @@ hipError_t launch_kmajor(bool causal, bool drop, int S, int B, hipStream_t s,
     if (ragged)                                                                                          \
       hipLaunchKernelGGL((flash_kmajor_kernel<D, C, DR, P, PAIR, true>), grid, dim3(PAIR ? 512 : 256), 0, \
                          s, q, k, v, ldq, ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq,    \
-                         Hkv, klen, c, dkscale, dvscale, dbits, NB, NQT);                                 \
+                         Hkv, klen, c, dkscale, dvscale, dbits, NB, NQT, bpart, ldbp, bcol);              \
     else                                                                                                 \
       hipLaunchKernelGGL((flash_kmajor_kernel<D, C, DR, P, PAIR, false>), grid, dim3(PAIR ? 512 : 256), 0, \
                          s, q, k, v, ldq, ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq,    \
-                         Hkv, klen, c, dkscale, dvscale, dbits, NB, NQT);                                 \
+                         Hkv, klen, c, dkscale, dvscale, dbits, NB, NQT, bpart, ldbp, bcol);              \
   } while (0)
 #define MX_KM_P(P)                                                                   \
   {                                                                                  \
@@ -1368,11 +1413,11 @@ hipError_t launch_kmajor(bool causal, bool drop, int S, int B, hipStream_t s,
     if (ragged)                                                                                     \
       hipLaunchKernelGGL((flash_kmajor128_kernel<C, DR, true>), grid, dim3(512), 0, s, q, k, v, ldq, \
                          ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq, Hkv, klen, c, \
-                         dkscale, dvscale, dbits, NB, NQT);                                         \
+                         dkscale, dvscale, dbits, NB, NQT, bpart, ldbp, bcol);                      \
     else                                                                                            \
       hipLaunchKernelGGL((flash_kmajor128_kernel<C, DR, false>), grid, dim3(512), 0, s, q, k, v,    \
                          ldq, ldk, ldv, dout, lddo, lse, delta, dk, dv, lddk, lddv, S, Hq, Hkv,     \
-                         klen, c, dkscale, dvscale, dbits, NB, NQT);                                \
+                         klen, c, dkscale, dvscale, dbits, NB, NQT, bpart, ldbp, bcol);             \
   } while (0)
     if (causal) { if (drop) MX_K8(true, true); else MX_K8(true, false); }
     else { if (drop) MX_K8(false, true); else MX_K8(false, false); }
@@ -1465,8 +1510,11 @@ MX_EXPORT int mx_flash_bwd(const void* q, const void* k, const void* v, int ldq,
                            float* delta, void* dq, int lddq, void* dk, void* dv, int lddk,
                            int lddv, int B, int S, int Hq, int Hkv, int D, int causal,
                            const int* klen, float scale, const void* fwd_bits,
-                           const void* bwd_bits, float keep_scale, hipStream_t s) {
+                           const void* bwd_bits, float keep_scale, float* bias_part, int ldbp,
+                           hipStream_t s) {
   if (Hq % Hkv || S <= 0 || (D != 64 && D != 128)) return hipErrorInvalidValue;
+  // bias-gradient partials need whole 32-row groups and room for [dq | dk | dv] columns
+  if (bias_part && (S % 32 || ldbp < (Hq + 2 * Hkv) * D)) return hipErrorInvalidValue;
   if ((fwd_bits == nullptr) != (bwd_bits == nullptr)) return hipErrorInvalidValue;
   const float c = scale * 1.4426950408889634f;
   const bool drop = fwd_bits != nullptr;
@@ -1478,22 +1526,24 @@ MX_EXPORT int mx_flash_bwd(const void* q, const void* k, const void* v, int ldq,
     e = launch_qmajor<64, true>(causal, drop, S, B, s, (const uint16_t*)q, (const uint16_t*)k,
                                 (const uint16_t*)v, ldq, ldk, ldv, (const uint16_t*)dout, lddo,
                                 (uint16_t*)o, ldo, (float*)lse, delta, (uint16_t*)dq, lddq, Hq, Hkv,
-                                klen, c, scale * ks, dkeep, (const uint64_t*)fwd_bits, NB, NKT);
+                                klen, c, scale * ks, dkeep, (const uint64_t*)fwd_bits, NB, NKT, bias_part,
+                                ldbp);
   else
     e = launch_qmajor<128, true>(causal, drop, S, B, s, (const uint16_t*)q, (const uint16_t*)k,
                                  (const uint16_t*)v, ldq, ldk, ldv, (const uint16_t*)dout, lddo,
                                  (uint16_t*)o, ldo, (float*)lse, delta, (uint16_t*)dq, lddq, Hq, Hkv,
-                                 klen, c, scale * ks, dkeep, (const uint64_t*)fwd_bits, NB, NKT);
+                                 klen, c, scale * ks, dkeep, (const uint64_t*)fwd_bits, NB, NKT, bias_part,
+                                 ldbp);
   if (e != hipSuccess) return e;
   if (D == 64)
     e = launch_kmajor<64>(causal, drop, S, B, s, (const uint16_t*)q, (const uint16_t*)k,
                           (const uint16_t*)v, ldq, ldk, ldv, (const uint16_t*)dout, lddo, lse, delta,
                           (uint16_t*)dk, (uint16_t*)dv, lddk, lddv, Hq, Hkv, klen, c, scale * ks, ks,
-                          (const uint32_t*)bwd_bits, NB, NQT);
+                          (const uint32_t*)bwd_bits, NB, NQT, bias_part, ldbp, Hq * D);
   else
     e = launch_kmajor<128>(causal, drop, S, B, s, (const uint16_t*)q, (const uint16_t*)k,
                            (const uint16_t*)v, ldq, ldk, ldv, (const uint16_t*)dout, lddo, lse, delta,
                            (uint16_t*)dk, (uint16_t*)dv, lddk, lddv, Hq, Hkv, klen, c, scale * ks, ks,
-                           (const uint32_t*)bwd_bits, NB, NQT);
+                           (const uint32_t*)bwd_bits, NB, NQT, bias_part, ldbp, Hq * D);
   return e;
 }

@@ -436,18 +436,22 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(
   if (c >= cols) return;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int r1 = min(rows, r0 + rows_per_block);
-  constexpr int G = 4;   // rows per group, loads issued together (memory-level parallelism)
+  // G rows per group, their loads issued together and unconditionally (rows clamped into
+  // the block, the overhang masked after): a `r < r1 ? load : 0` select made the compiler
+  // wait for each load where it was issued
+  constexpr int G = 8;
   for (int r = r0; r < r1; r += G) {
     uint4 raw[G];
 #pragma unroll
     for (int u = 0; u < G; ++u)
-      raw[u] = r + u < r1 ? *reinterpret_cast<const uint4*>(x + (size_t)(r + u) * cols + c) : make_uint4(0, 0, 0, 0);
+      raw[u] = *reinterpret_cast<const uint4*>(x + (size_t)min(r + u, r1 - 1) * cols + c);
 #pragma unroll
     for (int u = 0; u < G; ++u) {
       float v[8];
       unpack8(raw[u], v);
+      const float m = r + u < r1 ? 1.f : 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+      for (int j = 0; j < 8; ++j) acc[j] += v[j] * m;
     }
   }
   float* o = partial + (size_t)blockIdx.y * cols + c;

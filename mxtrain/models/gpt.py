@@ -715,15 +715,31 @@ class GPTLayerFn(torch.autograd.Function):
         q = qkv_a[:, : ha * D]
         k = qkv_a[:, ha * D:(ha + kva) * D]
         v = qkv_a[:, (ha + kva) * D:]
+        # QKV bias gradient: column partials straight from the attention backward kernels
+        # (deferred reduction) when dqkv is final as they write it -- no RoPE / context-
+        # parallel reshuffle afterwards -- instead of a column-sum pass over dqkv
+        bpart, fused_bias = None, False
+        gb = G[p + "qkv_b"]
+        if (rt.colq is not None and cfg.position_embedding != "rope" and rt.cp == 1 and rt.S % 32 == 0
+                and dqkv.is_cuda):
+            ncols = dqkv.shape[1]
+            bpart = rt.colq.partial((gb.data_ptr(),), (gb, None, None), rt.B * rt.S // 32, ncols, 1, ncols,
+                                    True)
+            fused_bias = True
+            if bpart is not None:
+                bpart = bpart.view(rt.B * rt.S // 32, ncols)
         attn_ops.attn_bwd(dctx, q, k, v, ctx_a, lse, rt.B, rt.S * rt.cp, ha, kva, D, causal=True,
                           dq=dqkv[:, : ha * D], dk=dqkv[:, ha * D:(ha + kva) * D],
-                          dv=dqkv[:, (ha + kva) * D:], dmask=ctx.dmask)
+                          dv=dqkv[:, (ha + kva) * D:], dmask=ctx.dmask, bias_partial=bpart)
         ctx.dmask = None
         rt.rope_(dqkv, ha, kva, inverse=True)
         if rt.cp > 1:
             dqkv = head_to_seq(dqkv, (hl * D, kvl * D, kvl * D), rt.B, rt.S, rt.cp_group)
         pend = _reduce_start(_mm(dqkv, P[p + "qkv_w"], trans=False, fused=rt.fused_linear), rt)
-        colsum(dqkv, G[p + "qkv_b"], accumulate=True, defer=rt.colq)
+        if not fused_bias:
+            colsum(dqkv, gb, accumulate=True, defer=rt.colq)
+        elif bpart is None:   # the queue's recording step: reduce now
+            colsum(dqkv, gb, accumulate=True)
         rt.wgrad((G[p + "proj_w"], do_full, ctx_), (G[p + "qkv_w"], dqkv, a_full))
         da = pend.wait()
         rt.done(i + 1)

@@ -90,7 +90,7 @@ SIGNATURES = {
     "mx_flash_dropmask_layers": [P, U32, F, I, I, I, I, I, I, I, P, P, I64, I64, P],
     "mx_flash_fwd": [P, P, P, I, I, I, P, I, P, I, I, I, I, I, I, P, F, P, F, P],
     "mx_flash_bwd": [P, P, P, I, I, I, P, I, P, I, P, P, P, I, P, P, I, I, I, I, I, I, I, I,
-                     P, F, P, P, F, P],
+                     P, F, P, P, F, P, I, P],
     # gemm.hip
     "mx_gemm_kk_tile": [I, I],
     "mx_gemm_kk": [I, P, I, F, I, I, P, P, P],

@@ -201,11 +201,17 @@ def attn_fwd(q, k, v, B, S, Hq, Hkv, D, causal=True, klen=None, scale=None, drop
 
 
 def attn_bwd(dout, q, k, v, o, lse, B, S, Hq, Hkv, D, causal=True, klen=None, scale=None,
-             dq=None, dk=None, dv=None, dmask=None, dropout_p=0.0):
+             dq=None, dk=None, dv=None, dmask=None, dropout_p=0.0, bias_partial=None):
     """Returns (dq, dk, dv); if views dq/dk/dv (e.g. slices of a packed dqkv) are given
-    they are written in place.  ``dmask`` is the third output of :func:`attn_fwd`."""
+    they are written in place.  ``dmask`` is the third output of :func:`attn_fwd`.
+
+    ``bias_partial`` (GPU, S % 32 == 0): fp32 [B*S/32, (Hq + 2 Hkv) * D] that receives the
+    column sums of every 32-row group of [dq | dk | dv] (the QKV bias gradient's partials,
+    reduced later by the deferred column reduction) -- computed from the kernels'
+    accumulators, so dq / dk / dv are not read again."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if not _lib.use_hip(q):
+        assert bias_partial is None, "bias_partial is a GPU-kernel output"
         keep = dmask.keep if dmask is not None else None
         with torch.enable_grad():
             qq = q.detach().float().requires_grad_(True)
@@ -236,7 +242,8 @@ def attn_bwd(dout, q, k, v, o, lse, B, S, Hq, Hkv, D, causal=True, klen=None, sc
               dv.stride(0), B, S, Hq, Hkv, D, int(causal), _lib.ptr(kl), float(scale),
               _lib.ptr(dmask.fbits) if dmask is not None else None,
               _lib.ptr(dmask.bbits) if dmask is not None else None,
-              float(dmask.keep_scale) if dmask is not None else 1.0, _lib.stream())
+              float(dmask.keep_scale) if dmask is not None else 1.0, _lib.ptr(bias_partial),
+              bias_partial.stride(0) if bias_partial is not None else 0, _lib.stream())
     return dq, dk, dv
 
 

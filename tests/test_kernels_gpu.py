@@ -251,6 +251,31 @@ def test_flash_d128_single_pass_matches_two_pass(S, causal, pdrop, padded):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("D,Hq,Hkv,pdrop", [(64, 4, 4, 0.1), (128, 4, 4, 0.1), (64, 8, 2, 0.0), (128, 4, 2, 0.0)])
+def test_flash_bwd_bias_partials_are_column_sums(D, Hq, Hkv, pdrop):
+    """The attention backward's QKV-bias partials (column sums of each 32-row group of
+    [dq | dk | dv], from the kernels' fp32 accumulators) against sums of the bf16 outputs."""
+    B, S = 2, 256
+    torch.manual_seed(5)
+    W = (Hq + 2 * Hkv) * D
+    qkv = torch.randn(B * S, W, device=DEV).to(torch.bfloat16)
+    q, k, v = qkv[:, :Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
+    do = torch.randn(B * S, Hq * D, device=DEV).to(torch.bfloat16)
+    seed = torch.tensor([11], dtype=torch.int32, device=DEV)
+    kw = dict(dropout_p=pdrop, salt=2, head_offset=0, total_heads=Hq) if pdrop else {}
+    o, lse, dm = A.attn_fwd(q, k, v, B, S, Hq, Hkv, D, True, None, seed_t=seed, **kw)
+    dqkv = torch.zeros_like(qkv)
+    part = torch.full((B * S // 32, W), float("nan"), device=DEV)
+    A.attn_bwd(do, q, k, v, o, lse, B, S, Hq, Hkv, D, True, None, dq=dqkv[:, :Hq * D],
+               dk=dqkv[:, Hq * D:(Hq + Hkv) * D], dv=dqkv[:, (Hq + Hkv) * D:], dmask=dm, dropout_p=pdrop,
+               bias_partial=part)
+    torch.cuda.synchronize()
+    assert torch.isfinite(part).all()                       # every row / column written
+    ref = dqkv.float().view(B * S // 32, 32, W).sum(1)
+    scale = ref.abs().max().item()
+    _close(part, ref, 2e-2 * scale + 1e-3, 1e-2, "bias partials")
+
+
 def _crow(e, hh):
     return (e & 3) + 8 * (e >> 2) + 4 * hh
 
