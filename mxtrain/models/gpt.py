@@ -33,7 +33,7 @@ import torch
 
 from .. import ops
 from ..ops import attention as attn_ops
-from ..ops.norm import bda_norm_fwd, colsum, layernorm_fwd, norm_bwd
+from ..ops.norm import bda_norm_fwd, colsum, colsum_finalize, colsum_partials_buffer, layernorm_fwd, norm_bwd
 from ..ops.gemm import linear_dgrad, linear_fwd, wgrad_group
 from ..ops.rope import apply_rope_
 from ..ops.fused import (bias_gelu_bwd, bias_gelu_fwd, bias_swiglu_bwd, bias_swiglu_fwd,
@@ -42,6 +42,11 @@ from ..parallel import collectives as C
 from ..parallel.buffers import ParamSpec
 from ..parallel.ulysses import head_to_seq, seq_to_head
 from .moe import is_moe_layer, moe_mlp
+
+
+# QKV bias gradient from the attention backward kernels' column partials (module switch for
+# A/B runs: scripts/bisect_deferred.py)
+FUSED_QKV_BIAS_GRAD = True
 
 
 @dataclass
@@ -716,21 +721,26 @@ class GPTLayerFn(torch.autograd.Function):
         k = qkv_a[:, ha * D:(ha + kva) * D]
         v = qkv_a[:, (ha + kva) * D:]
         # QKV bias gradient: column partials straight from the attention backward kernels
-        # (deferred reduction) when dqkv is final as they write it -- no RoPE / context-
-        # parallel reshuffle afterwards -- instead of a column-sum pass over dqkv
-        bpart, fused_bias = None, False
+        # when dqkv is final as they write it (no RoPE / context-parallel reshuffle after),
+        # reduced by the deferred batched flush, or right away when there is no queue /
+        # on its recording step -- the same partials and reduction either way
         gb = G[p + "qkv_b"]
-        if (rt.colq is not None and cfg.position_embedding != "rope" and rt.cp == 1 and rt.S % 32 == 0
-                and dqkv.is_cuda):
-            ncols = dqkv.shape[1]
-            bpart = rt.colq.partial((gb.data_ptr(),), (gb, None, None), rt.B * rt.S // 32, ncols, 1, ncols,
-                                    True)
-            fused_bias = True
+        fused_bias = (FUSED_QKV_BIAS_GRAD and cfg.position_embedding != "rope" and rt.cp == 1
+                      and rt.S % 32 == 0 and dqkv.is_cuda)
+        bpart = pbuf = None
+        if fused_bias:
+            nparts, ncols = rt.B * rt.S // 32, dqkv.shape[1]
+            if rt.colq is not None:
+                bpart = rt.colq.partial((gb.data_ptr(),), (gb, None, None), nparts, ncols, 1, ncols, True)
             if bpart is not None:
-                bpart = bpart.view(rt.B * rt.S // 32, ncols)
+                bpart = bpart.view(nparts, ncols)
+            else:
+                bpart, pbuf = colsum_partials_buffer(nparts, ncols, dqkv.device)
         attn_ops.attn_bwd(dctx, q, k, v, ctx_a, lse, rt.B, rt.S * rt.cp, ha, kva, D, causal=True,
                           dq=dqkv[:, : ha * D], dk=dqkv[:, ha * D:(ha + kva) * D],
                           dv=dqkv[:, (ha + kva) * D:], dmask=ctx.dmask, bias_partial=bpart)
+        if pbuf is not None:
+            colsum_finalize(pbuf, nparts, ncols, gb, accumulate=True)
         ctx.dmask = None
         rt.rope_(dqkv, ha, kva, inverse=True)
         if rt.cp > 1:
@@ -738,8 +748,6 @@ class GPTLayerFn(torch.autograd.Function):
         pend = _reduce_start(_mm(dqkv, P[p + "qkv_w"], trans=False, fused=rt.fused_linear), rt)
         if not fused_bias:
             colsum(dqkv, gb, accumulate=True, defer=rt.colq)
-        elif bpart is None:   # the queue's recording step: reduce now
-            colsum(dqkv, gb, accumulate=True)
         rt.wgrad((G[p + "proj_w"], do_full, ctx_), (G[p + "qkv_w"], dqkv, a_full))
         da = pend.wait()
         rt.done(i + 1)

@@ -227,6 +227,10 @@ def lse_from_stats(m, s):
     return lse
 
 
+# one-pass CE kernel when the whole vocabulary is local (module switch for A/B runs)
+SINGLE_PASS_CE = True
+
+
 def cross_entropy_fwd_bwd(logits, labels, grad_scale, ignore_index=-100, tp_group=None,
                           vocab_start=0):
     """Fused CE: returns per-row losses and overwrites ``logits`` with d(loss*grad_scale)/dlogits.
@@ -236,7 +240,8 @@ def cross_entropy_fwd_bwd(logits, labels, grad_scale, ignore_index=-100, tp_grou
     three tiny all-reduces: max, rescaled sum, target logit).
     """
     rows, V = logits.shape
-    if tp_group is None and vocab_start == 0 and _lib.use_hip(logits) and V % 8 == 0 and V <= 64 * 256 * 8:
+    if (SINGLE_PASS_CE and tp_group is None and vocab_start == 0 and _lib.use_hip(logits) and V % 8 == 0
+            and V <= 64 * 256 * 8):
         # one pass, the row held in registers (csrc/fused.hip ce_fused_kernel)
         loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
         if torch.is_tensor(grad_scale):

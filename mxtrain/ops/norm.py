@@ -166,6 +166,23 @@ def colsum(x, out, accumulate=False, defer=None):
     return out
 
 
+def colsum_partials_buffer(nparts: int, cols: int, device):
+    """fp32 buffer for nparts x cols column partials plus the immediate reduction's scratch;
+    returns (partials view [nparts, cols], whole buffer)."""
+    scratch_n = _lib.query64("mx_colreduce_scratch", nparts, cols)
+    buf = torch.empty(nparts * cols + scratch_n, dtype=torch.float32, device=device)
+    return buf[:nparts * cols].view(nparts, cols), buf
+
+
+def colsum_finalize(buf, nparts: int, cols: int, out, accumulate=False):
+    """out (bf16 [cols]) (+)= the column sums of the nparts x cols partials at the start of
+    ``buf`` (from colsum_partials_buffer): the same deterministic reduction the deferred
+    batched flush and colsum() use."""
+    _lib.call("mx_colsum_finalize", _lib.ptr(buf), nparts, cols, 1, _lib.ptr(out), None, None,
+              int(accumulate), _lib.ptr(buf) + 4 * nparts * cols, _lib.stream())
+    return out
+
+
 # ------------------------------------------------------------------ deferred column sums
 class ColReduceQueue:
     """Column reductions of a training step deferred to ONE batched launch
