@@ -56,14 +56,16 @@ def test_graphed_step_matches_eager(tmp_path):
     assert gs.captures == 1 and gs.replays == 3
     num = sum(float((p - q).float().norm() ** 2) for p, q in zip(pa, pb)) ** 0.5
     den = sum(float(p.float().norm() ** 2) for p in pa) ** 0.5
-    # The first steps must agree closely; later ones may drift: GEMM algorithms chosen
-    # under capture can differ from eager ones in rounding, and the discrete proposal /
-    # RoI sampling amplifies the difference, while the parameters stay within 1e-3.
+    # GEMM algorithms chosen under capture can differ from eager ones in rounding, and the
+    # discrete proposal / RoI sampling amplifies the difference, while the parameters stay
+    # within 1e-3.
     rel = [max(abs(float(x[k]) - float(y[k])) / (abs(float(x[k])) + 1e-6) for k in x) for x, y in zip(la, lb)]
     print(f"graphed vs eager, max relative loss difference per step: {[round(r, 4) for r in rel]}; "
           f"params {num / den:.2e}")
+    # (measured with the graph's memset nodes replayed as fill kernels: <= 3.3 % on every
+    # step, profiles/r3_s4/; 15 % was needed on later steps before)
     for s, (x, y) in enumerate(zip(la, lb)):
-        tol = 0.05 if s < 2 else 0.15
+        tol = 0.05
         for k in x:
             assert torch.isfinite(y[k]), (s, k)
             assert abs(float(x[k]) - float(y[k])) <= tol * abs(float(x[k])) + 1e-3, \

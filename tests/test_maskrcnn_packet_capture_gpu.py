@@ -42,5 +42,5 @@ def test_maskrcnn_graph_replays_under_packet_capture_like_eager():
     for s, (a, b) in enumerate(zip(eager, graph)):
         assert b == b and abs(b) < 1e4, (s, b)
         # first steps close; later ones may drift through the discrete proposal / RoI sampling
-        tol = 0.05 if s < 2 else 0.25
+        tol = 0.05 if s < 2 else 0.08   # (measured: <= 4.2 %, profiles/r3_s4/)
         assert abs(a - b) <= tol * abs(a) + 1e-3, (s, a, b, eager, graph)
