@@ -157,9 +157,19 @@ def _nt_tile(variant):
     return t
 
 
+# Above this many multiply-adds hipBLASLt wins even against the fused epilogues: at the
+# GPT-3 6.7B layer shapes (T 4096, hidden 4096: M*N*K 6.9e10 .. 2.7e11) it ran the layer's
+# forward + dgrad GEMMs in 2408 us vs 2771 us for the planned variants (1.3-1.6 vs 1.0-1.3
+# PF/s; profiles/r3_s4/gemm_gpt3_shapes.txt) and the one-GPU GPT-3 bench 22.10k vs 21.06k
+# tokens/s, while at the GPT-2 345M shapes (<= 1.7e10) the hand-written kernels take the
+# layer from 291 to 232 us (profiles/r3_s1/gemm_nt_vs_hipblaslt.txt).
+NT_MAX_MNK = 1 << 35
+
+
 def nt_plan(M: int, N: int, K: int, kmajor: bool) -> int:
-    """Variant of csrc/gemm_nt.hip for an [M, K] x [K, N] problem, or -1 (not tileable)."""
-    if K % 64:
+    """Variant of csrc/gemm_nt.hip for an [M, K] x [K, N] problem, or -1 (not tileable, or
+    large enough that hipBLASLt is faster)."""
+    if K % 64 or M * N * K > NT_MAX_MNK:
         return -1
     if _NT_FORCE:
         v = int(_NT_FORCE)
