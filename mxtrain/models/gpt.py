@@ -34,7 +34,7 @@ import torch
 from .. import ops
 from ..ops import attention as attn_ops
 from ..ops.norm import bda_norm_fwd, colsum, colsum_finalize, colsum_partials_buffer, layernorm_fwd, norm_bwd
-from ..ops.gemm import linear_dgrad, linear_fwd, wgrad_group
+from ..ops.gemm import linear_dgrad, linear_fwd, nt_fits, wgrad_group
 from ..ops.rope import apply_rope_
 from ..ops.fused import (bias_gelu_bwd, bias_gelu_fwd, bias_swiglu_bwd, bias_swiglu_fwd,
                          cross_entropy_fwd_bwd, embed_bwd, embed_fwd, pos_embed_bwd)
@@ -421,7 +421,10 @@ def _reduce_start(x, rt):
 
 def _mm(a, w, trans=True, bias=None, out=None, fused=False):
     """a @ W^T (+ bias) (``trans=False``: a @ W, the dgrad of a Linear): through the
-    hand-written MFMA GEMM with the bias in its epilogue when ``fused``, else hipBLASLt."""
+    hand-written MFMA GEMM with the bias in its epilogue when ``fused`` and the size is one
+    where it wins (ops/gemm.py nt_fits), else hipBLASLt."""
+    if fused and a.is_cuda and not nt_fits(a.shape[0], w.shape[0] if trans else w.shape[1], a.shape[1]):
+        fused = False
     if fused:
         if trans:
             return linear_fwd(a, w, bias, out=out)
@@ -606,7 +609,8 @@ class GPTLayerFn(torch.autograd.Function):
             pre = f = None
             b_fc2 = None
         else:
-            if rt.fused_linear and not rt.sp and not cfg.swiglu:
+            if (rt.fused_linear and not rt.sp and not cfg.swiglu
+                    and (not m.is_cuda or nt_fits(m.shape[0], P[p + "fc1_w"].shape[0], m.shape[1]))):
                 # fc1 GEMM + bias + GeLU in one kernel; pre = the biased pre-activation
                 m_full = m
                 f, pre = linear_fwd(m, P[p + "fc1_w"], P[p + "fc1_b"], gelu=True)

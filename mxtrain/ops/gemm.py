@@ -163,13 +163,19 @@ def _nt_tile(variant):
 # PF/s; profiles/r3_s4/gemm_gpt3_shapes.txt) and the one-GPU GPT-3 bench 22.10k vs 21.06k
 # tokens/s, while at the GPT-2 345M shapes (<= 1.7e10) the hand-written kernels take the
 # layer from 291 to 232 us (profiles/r3_s1/gemm_nt_vs_hipblaslt.txt).
+# The model asks nt_fits() before routing a Linear through these kernels (models/gpt.py);
+# above the limit it takes its hipBLASLt + separate-epilogue path.
 NT_MAX_MNK = 1 << 35
 
 
+def nt_fits(M: int, N: int, K: int) -> bool:
+    """True when the hand-written fused-epilogue GEMM is the faster choice for this size."""
+    return M * N * K <= NT_MAX_MNK
+
+
 def nt_plan(M: int, N: int, K: int, kmajor: bool) -> int:
-    """Variant of csrc/gemm_nt.hip for an [M, K] x [K, N] problem, or -1 (not tileable, or
-    large enough that hipBLASLt is faster)."""
-    if K % 64 or M * N * K > NT_MAX_MNK:
+    """Variant of csrc/gemm_nt.hip for an [M, K] x [K, N] problem, or -1 (not tileable)."""
+    if K % 64:
         return -1
     if _NT_FORCE:
         v = int(_NT_FORCE)
