@@ -1,0 +1,318 @@
+// Convolution weight gradients for NHWC bf16 CNNs on gfx950, as one implicit GEMM per
+// launch: dW[co][r][s][ci] = sum over output pixels p of dY[p][co] * X[pix(p, r, s)][ci],
+// written straight into the channels_last bf16 weight-gradient layout ([Cout][KH][KW][Cin],
+// the layout of the Mask R-CNN compute copies, models/compute_weights.py).
+//
+// Why: in the graphed Mask R-CNN step MIOpen's weight-gradient solvers took ~2.1 ms of the
+// ~12 ms step (CK `batched_gemm_xdlops_bwd_weight` 1.84 ms + `igemm_wrw` 0.27 ms, i.e.
+// ~0.2 PF/s on ~200 G multiply-adds), plus ~0.8 ms of their helper kernels (fp32 workspace
+// zero-fills, SubTensorOp zero / cast passes): profiles/r2_maskrcnn_s3/census_1img_graph_948_kernels.txt,
+// profiles/r2_maskrcnn_s4/README.md.  Reference: the tensorpack / Detectron Mask R-CNN
+// backbone + FPN + heads (examples/maskrcnn/train-maskrcnn-aws.yaml).
+//
+// Design -- the K-major x K-major MFMA GEMM of gemm.hip, with the reduction running over
+// output pixels instead of tokens:
+//  * one tile = (tap, 128-row Cout block, 128-column Cin block); every tap (r, s) of a
+//    KH x KW filter is its own set of tiles in the same launch, so a 3x3 conv is ONE
+//    launch, and no im2col / padded copy of X is ever made: each LDS-DMA lane computes its
+//    input pixel (n, oh*st - pad + r*dil, ow*st - pad + s*dil) from the output-pixel index
+//    and points out-of-image pixels (and rows past the last pixel) at a zero row;
+//  * split-K over the pixels: the output is small (Cout x Cin per tap) and the reduction
+//    long (up to ~270k pixels), so every launch is cut into `splits` pixel ranges, the grid
+//    ordered slice-major (a slice's dY / X panels are shared by all tiles of one XCD in its
+//    L2); fp32 partial tiles go to a slab that a second, chip-wide launch sums in slice
+//    order -- deterministic, no float atomics, no zero-fill.  (A last-arriving-slice
+//    reduction as in gemm.hip serialised up to 7.5 MB of partial reads on one workgroup per
+//    tile: FPN lateral P2 104 us instead of MIOpen's 70 us, profiles/r3_s4/conv_wgrad_*.txt);
+//  * 128 x 128 tiles of 4 waves (64 x 64 each, 16x16x32 bf16 MFMA), BK 64, 2-slot ring,
+//    two workgroups per CU; LDS-DMA (global_load_lds_dwordx4) staging, transposed LDS reads
+//    (ds_read_b64_tr_b16) with the source-side XOR swizzle, as in gemm.hip.
+#include "gemm_common.h"
+
+using namespace mx;
+using namespace mx::gemm;
+
+namespace {
+
+struct ConvWg {
+  const uint16_t* dy;    // [T][ldy]: output pixels (n, oh, ow) row-major, Cout contiguous
+  const uint16_t* x;     // [N * IH * IW][ldx]: input pixels, Cin contiguous
+  const uint16_t* zero;  // >= 256 zero bf16 (16-B aligned)
+  uint16_t* dw;          // [Cout][taps][Cin]
+  float* slab;           // split-K partials [ntiles][splits][NR][NT] float4
+  int ldy, ldx;
+  int T, OH, OW, IH, IW;
+  int KW, taps, stride, pad, dil;
+  int Cin, tiles_n, tiles_tap, ntiles;
+  int splits, nk;        // pixel slices, 64-row K-steps per slice
+  float invOW, invOH, beta;
+};
+
+__device__ __forceinline__ void divmod(int p, int d, float inv, int& q, int& r) {
+  q = (int)((float)p * inv);
+  r = p - q * d;
+  if (r < 0) { --q; r += d; }
+  else if (r >= d) { ++q; r -= d; }
+}
+
+template <int WM, int WN, int FM, int FN, int BKT, int NSLOT, int MINB, bool IDENT>
+__global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const ConvWg cp) {
+  constexpr int NW = WM * WN, NT = 64 * NW;
+  constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
+  constexpr int RA = BM * 2, RB = BN * 2;
+  constexpr int IA = BKT * RA, IB = BKT * RB;
+  constexpr int PA = IA / 1024 / NW, PB = IB / 1024 / NW;
+  constexpr int SLOT = IA + IB;
+  static_assert(PA * NW * 1024 == IA && PB * NW * 1024 == IB, "DMA pieces per wave");
+  __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  // slice-major: consecutive workgroups (one XCD) share a pixel range across tiles
+  const int slice = wg / cp.ntiles, t = wg - slice * cp.ntiles;
+  const int tap = t / cp.tiles_tap, lt = t - tap * cp.tiles_tap;
+  const int m0 = (lt / cp.tiles_n) * BM, n0 = (lt % cp.tiles_n) * BN;
+  const int r = tap / cp.KW, s = tap - r * cp.KW;
+  const int dh = r * cp.dil - cp.pad, dwc = s * cp.dil - cp.pad;
+  const int nk = cp.nk;
+  const int p0 = slice * nk * BKT;
+
+  // ---- per-lane DMA rows: piece j of this wave holds 1024 / R consecutive k-rows
+  constexpr int CA = RA / 16, CB = RB / 16;
+  int kA[PA], cA[PA], kB[PB], cB[PB];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    kA[j] = (PA * wave + j) * (1024 / RA) + lane / CA;
+    cA[j] = m0 + 8 * pchunk(kA[j], lane % CA);
+  }
+#pragma unroll
+  for (int j = 0; j < PB; ++j) {
+    kB[j] = (PB * wave + j) * (1024 / RB) + lane / CB;
+    cB[j] = 8 * pchunk(kB[j], lane % CB);
+  }
+  const int Tm1 = cp.T - 1;
+  auto srcA = [&](int j, int it) __attribute__((always_inline)) {
+    const int p = min(p0 + it * BKT + kA[j], Tm1);   // rows past T: any valid row (B is zero there)
+    return cp.dy + (size_t)p * cp.ldy + cA[j];
+  };
+  auto srcB = [&](int j, int it) __attribute__((always_inline)) {
+    const int p = p0 + it * BKT + kB[j];
+    if (IDENT) {
+      return p < cp.T ? cp.x + (size_t)p * cp.ldx + n0 + cB[j] : cp.zero + cB[j];
+    } else {
+      int q, ow, n, oh;
+      divmod(p, cp.OW, cp.invOW, q, ow);
+      divmod(q, cp.OH, cp.invOH, n, oh);
+      const int ih = oh * cp.stride + dh, iw = ow * cp.stride + dwc;
+      const bool ok = p < cp.T && (unsigned)ih < (unsigned)cp.IH && (unsigned)iw < (unsigned)cp.IW;
+      return ok ? cp.x + ((size_t)(n * cp.IH + ih) * cp.IW + iw) * cp.ldx + n0 + cB[j] : cp.zero + cB[j];
+    }
+  };
+
+  const int G = lane >> 4, i = lane & 15;
+  const int wm = wave / WN, wn = wave % WN;
+  const int krow = 8 * G + (i >> 2);
+  const int g = gsw(krow);
+  int offA[FM], offB[FN];
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+    offA[a] = krow * RA + ((((FM * wm + a) ^ g) << 1) | ((i & 3) >> 1)) * 16 + (i & 1) * 8;
+#pragma unroll
+  for (int u = 0; u < FN; ++u)
+    offB[u] = krow * RB + ((((FN * wn + u) ^ g) << 1) | ((i & 3) >> 1)) * 16 + (i & 1) * 8;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int u = 0; u < FN; ++u) acc[a][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const uint32_t lds0 = lds_addr(smem);
+  auto issue = [&](int slot, int it) __attribute__((always_inline)) {
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
+    const uint32_t b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
+#pragma unroll
+    for (int j = 0; j < PA; ++j) dma16(srcA(j, it), b0 + j * 1024);
+#pragma unroll
+    for (int j = 0; j < PB; ++j) dma16(srcB(j, it), b1 + j * 1024);
+  };
+  constexpr int PER = PA + PB;
+
+#pragma unroll
+  for (int q = 0; q < NSLOT - 1; ++q)
+    if (q < nk) issue(q, q);
+  int slot = 0;
+  for (int it = 0; it < nk; ++it) {
+    const int later = nk - 1 - it;
+    // retire step it's pieces (later steps' stay in flight), then one barrier
+    if (NSLOT >= 4 && later >= 2) vm_wait<(NSLOT >= 4 ? 2 : 0) * PER>();
+    else if (NSLOT >= 3 && later >= 1) vm_wait<(NSLOT >= 3 ? 1 : 0) * PER>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (it + NSLOT - 1 < nk) {
+      int ns = slot + NSLOT - 1;
+      if (ns >= NSLOT) ns -= NSLOT;
+      issue(ns, it + NSLOT - 1);
+    }
+    const char* As = smem + slot * SLOT;
+    const char* Bs = As + IA;
+#pragma unroll
+    for (int kk = 0; kk < BKT / 32; ++kk) {
+      bf16x8 b[FN];
+#pragma unroll
+      for (int u = 0; u < FN; ++u)
+        b[u] = cat(tr_read(Bs, offB[u] + 32 * RB * kk), tr_read(Bs, offB[u] + 32 * RB * kk + 4 * RB));
+#pragma unroll
+      for (int a = 0; a < FM; ++a) {
+        const bf16x8 av = cat(tr_read(As, offA[a] + 32 * RA * kk), tr_read(As, offA[a] + 32 * RA * kk + 4 * RA));
+#pragma unroll
+        for (int u = 0; u < FN; ++u) acc[a][u] = mfma16(av, b[u], acc[a][u]);
+      }
+    }
+    if (++slot == NSLOT) slot = 0;
+  }
+
+  if (cp.splits > 1) {
+    // publish the partial tile; conv_wgrad_reduce sums the slices (spread over the chip)
+    constexpr int NR = FM * FN;
+    float4* mine = reinterpret_cast<float4*>(cp.slab) + ((size_t)(t * cp.splits + slice) * NR) * NT + tid;
+#pragma unroll
+    for (int a = 0; a < FM; ++a)
+#pragma unroll
+      for (int u = 0; u < FN; ++u)
+        mine[(a * FN + u) * NT] = make_float4(acc[a][u][0], acc[a][u][1], acc[a][u][2], acc[a][u][3]);
+    return;
+  }
+
+  // ---- epilogue: lane holds dW[m0 + 16 a + 4 G + e][tap][n0 + 16 u + i] of its wave's block
+  const size_t ldc = (size_t)cp.taps * cp.Cin;
+  uint16_t* C = cp.dw + (size_t)(m0 + 16 * FM * wm + 4 * G) * ldc + (size_t)tap * cp.Cin + n0 + 16 * FN * wn + i;
+  const bool acc_in = cp.beta != 0.f;
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      uint16_t* row = C + (size_t)(16 * a + e) * ldc;
+#pragma unroll
+      for (int u = 0; u < FN; ++u) {
+        float v = acc[a][u][e];
+        if (acc_in) v += cp.beta * bf2f(row[16 * u]);
+        row[16 * u] = f2bf(v);
+      }
+    }
+}
+
+constexpr int kBM = 128, kBN = 128, kBK = 64, kNT = 256;
+
+// Split-K reduction: one thread per (tile, accumulator register group, lane) float4 column,
+// summed over the slices in slice order (deterministic), written to dW with the main
+// kernel's epilogue mapping (4 waves of 64 x 64: WM = WN = 2, FM = FN = 4).
+__global__ __launch_bounds__(64) void conv_wgrad_reduce_kernel(const ConvWg cp) {
+  constexpr int FM = 4, FN = 4, WN = 2, NR = FM * FN, NT = kNT;
+  const int gid = blockIdx.x * 64 + threadIdx.x;           // < ntiles * NR * NT
+  const int tid = gid % NT, rg = (gid / NT) % NR, t = gid / (NT * NR);
+  if (t >= cp.ntiles) return;
+  const float4* src = reinterpret_cast<const float4*>(cp.slab) + ((size_t)t * cp.splits * NR + rg) * NT + tid;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  int q = 0;
+  for (; q + 4 <= cp.splits; q += 4) {
+    const float4 a0 = src[(size_t)(q + 0) * NR * NT], a1 = src[(size_t)(q + 1) * NR * NT];
+    const float4 a2 = src[(size_t)(q + 2) * NR * NT], a3 = src[(size_t)(q + 3) * NR * NT];
+    v.x += a0.x; v.y += a0.y; v.z += a0.z; v.w += a0.w;
+    v.x += a1.x; v.y += a1.y; v.z += a1.z; v.w += a1.w;
+    v.x += a2.x; v.y += a2.y; v.z += a2.z; v.w += a2.w;
+    v.x += a3.x; v.y += a3.y; v.z += a3.z; v.w += a3.w;
+  }
+  for (; q < cp.splits; ++q) {
+    const float4 a0 = src[(size_t)q * NR * NT];
+    v.x += a0.x; v.y += a0.y; v.z += a0.z; v.w += a0.w;
+  }
+  const int tap = t / cp.tiles_tap, lt = t - tap * cp.tiles_tap;
+  const int m0 = (lt / cp.tiles_n) * kBM, n0 = (lt % cp.tiles_n) * kBN;
+  const int lane = tid & 63, wave = tid >> 6, G = lane >> 4, i = lane & 15;
+  const int wm = wave / WN, wn = wave % WN, a = rg / FN, u = rg % FN;
+  const size_t ldc = (size_t)cp.taps * cp.Cin;
+  uint16_t* C = cp.dw + (size_t)(m0 + 16 * FM * wm + 4 * G + 16 * a) * ldc + (size_t)tap * cp.Cin + n0 +
+                16 * FN * wn + 16 * u + i;
+  const float e4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float o = e4[e];
+    if (cp.beta != 0.f) o += cp.beta * bf2f(C[(size_t)e * ldc]);
+    C[(size_t)e * ldc] = f2bf(o);
+  }
+}
+
+}  // namespace
+
+// Tile geometry for the host planner: what = 0 -> BM, 1 -> BN, 2 -> BK (pixel rows per K-step).
+MX_EXPORT int mx_conv_wgrad_tile(int what) { return what == 0 ? kBM : what == 1 ? kBN : kBK; }
+
+// d (int64[20]): {dy, x, zero, dw, slab, 0, ldy, ldx, N, OH, OW, IH, IW, KH, KW, stride,
+// pad, dil, Cout, Cin}.  Cout and Cin multiples of 128; dy / x / zero 16-B aligned with
+// ldy / ldx multiples of 8; dW is written (beta 0) or accumulated (beta 1) in bf16.
+// splits > 1 needs slab (ntiles x splits x 128 x 128 fp32) and adds the reduction launch.
+MX_EXPORT int mx_conv_wgrad(const int64_t* d, float beta, int splits, void* stream) {
+  ConvWg cp{};
+  cp.dy = reinterpret_cast<const uint16_t*>(d[0]);
+  cp.x = reinterpret_cast<const uint16_t*>(d[1]);
+  cp.zero = reinterpret_cast<const uint16_t*>(d[2]);
+  cp.dw = reinterpret_cast<uint16_t*>(d[3]);
+  cp.slab = reinterpret_cast<float*>(d[4]);
+  cp.ldy = (int)d[6];
+  cp.ldx = (int)d[7];
+  const int64_t N = d[8];
+  cp.OH = (int)d[9];
+  cp.OW = (int)d[10];
+  cp.IH = (int)d[11];
+  cp.IW = (int)d[12];
+  const int KH = (int)d[13];
+  cp.KW = (int)d[14];
+  cp.stride = (int)d[15];
+  cp.pad = (int)d[16];
+  cp.dil = (int)d[17];
+  const int Cout = (int)d[18];
+  cp.Cin = (int)d[19];
+  const int64_t T = N * cp.OH * cp.OW;
+  if (N <= 0 || cp.OH <= 0 || cp.OW <= 0 || KH <= 0 || cp.KW <= 0 || cp.stride <= 0 || cp.dil <= 0 ||
+      cp.pad < 0 || T >= (1 << 23) || N * cp.IH * cp.IW >= ((int64_t)1 << 31))
+    return (int)hipErrorInvalidValue;
+  if (Cout % kBM || cp.Cin % kBN || cp.ldy < Cout || cp.ldx < cp.Cin || (cp.ldy & 7) || (cp.ldx & 7))
+    return (int)hipErrorInvalidValue;
+  if ((d[0] | d[1] | d[2]) & 15) return (int)hipErrorInvalidValue;
+  if (splits < 1 || (splits > 1 && cp.slab == nullptr)) return (int)hipErrorInvalidValue;
+  cp.T = (int)T;
+  cp.taps = KH * cp.KW;
+  cp.tiles_n = cp.Cin / kBN;
+  cp.tiles_tap = (Cout / kBM) * cp.tiles_n;
+  cp.ntiles = cp.taps * cp.tiles_tap;
+  const int steps = (int)((T + kBK - 1) / kBK);
+  if (splits > steps) splits = steps;
+  cp.nk = (steps + splits - 1) / splits;
+  splits = (steps + cp.nk - 1) / cp.nk;   // no empty slice
+  cp.splits = splits;
+  cp.invOW = 1.f / (float)cp.OW;
+  cp.invOH = 1.f / (float)cp.OH;
+  cp.beta = beta;
+  const bool ident = cp.taps == 1 && cp.stride == 1 && cp.pad == 0 && cp.OH == cp.IH && cp.OW == cp.IW;
+  const dim3 grid(cp.ntiles * splits);
+  hipStream_t st = (hipStream_t)stream;
+  if (ident)
+    hipLaunchKernelGGL((conv_wgrad_kernel<2, 2, 4, 4, kBK, 2, 2, true>), grid, dim3(kNT), 0, st, cp);
+  else
+    hipLaunchKernelGGL((conv_wgrad_kernel<2, 2, 4, 4, kBK, 2, 2, false>), grid, dim3(kNT), 0, st, cp);
+  if (splits > 1) {
+    const int e = hipGetLastError();
+    if (e) return e;
+    hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(cp.ntiles * 16 * kNT / 64), dim3(64), 0, st, cp);
+  }
+  return (int)hipGetLastError();
+}
+
+// The split count the launch will really use (slices are never empty), for slab sizing.
+MX_EXPORT int mx_conv_wgrad_splits(int64_t T, int splits) {
+  const int steps = (int)((T + kBK - 1) / kBK);
+  if (splits > steps) splits = steps;
+  if (splits < 1) splits = 1;
+  const int nk = (steps + splits - 1) / splits;
+  return (steps + nk - 1) / nk;
+}

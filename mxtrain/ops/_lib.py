@@ -94,6 +94,10 @@ SIGNATURES = {
     # gemm.hip
     "mx_gemm_kk_tile": [I, I],
     "mx_gemm_kk": [I, P, I, F, I, I, P, P, P],
+    # convwg.hip
+    "mx_conv_wgrad_tile": [I],
+    "mx_conv_wgrad": [P, F, I, P],
+    "mx_conv_wgrad_splits": [I64, I],
     # gemm_nt.hip
     "mx_gemm_nt_tile": [I, I],
     "mx_gemm_nt": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],

@@ -1,0 +1,130 @@
+"""Convolution weight gradients as implicit GEMMs (csrc/convwg.hip).
+
+``conv2d_wg(x, w, stride, padding, dilation)`` is ``F.conv2d`` whose backward keeps
+MIOpen for the input gradient and computes the weight gradient with the hand-written
+implicit-GEMM kernel: one launch per conv (every filter tap in it), split over the
+output pixels, written straight into the channels_last bf16 gradient of the compute copy.
+That replaces MIOpen's weight-gradient solvers and their fp32 workspace fill / cast
+helpers, ~2.9 ms of the ~12 ms graphed Mask R-CNN step
+(profiles/r2_maskrcnn_s3/census_1img_graph_948_kernels.txt).
+
+Convs the kernel does not tile (Cout or Cin not a multiple of 128, groups, non-NHWC or
+non-bf16 tensors, CPU) take plain ``F.conv2d`` -- part of the contract, not an error path.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+ENABLED = True          # module switch (A/B runs: scripts/conv_wgrad_bench.py)
+TARGET_WGS = 512        # two 128 x 128 workgroups per CU on 256 CUs
+MIN_STEPS = 8
+_DESC_T = ctypes.c_int64 * 20
+_WS: Dict[torch.device, Tuple[torch.Tensor, torch.Tensor]] = {}
+_RETIRED = []           # outgrown slabs stay alive: a captured hipGraph may still write them
+
+
+def _pair(v) -> Tuple[int, int]:
+    if isinstance(v, int):
+        return v, v
+    v = tuple(v)
+    return (v[0], v[0]) if len(v) == 1 else (v[0], v[1])
+
+
+def _sym(v):
+    a, b = _pair(v)
+    return a if a == b else None
+
+
+def _cl(t: torch.Tensor) -> bool:
+    return t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last)
+
+
+def supported(x: torch.Tensor, w: torch.Tensor, stride=1, padding=0, dilation=1, groups: int = 1) -> bool:
+    return (ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and groups == 1
+            and x.dim() == 4 and w.dim() == 4 and w.requires_grad and w.shape[0] % 128 == 0
+            and w.shape[1] % 128 == 0 and x.shape[1] == w.shape[1] and _cl(x)
+            and None not in (_sym(stride), _sym(padding), _sym(dilation)) and isinstance(padding, (int, tuple, list))
+            and x.data_ptr() % 16 == 0)
+
+
+def plan_splits(T: int, ntiles: int) -> int:
+    """Pixel slices per launch: enough workgroups to fill the chip (TARGET_WGS), each slice
+    at least MIN_STEPS K-steps of 64 pixels (its 64-KiB fp32 partial tile is then small
+    next to its MFMA work)."""
+    bk = 64
+    steps = (T + bk - 1) // bk
+    s = max(1, min(TARGET_WGS // max(ntiles, 1), steps // MIN_STEPS))
+    return int(_lib.query("mx_conv_wgrad_splits", T, max(s, 1)))
+
+
+def _workspace(device, slab_elems: int):
+    """(fp32 split-K slab, 256 zero bf16): grown on demand, so the first (eager) steps size
+    it before a hipGraph capture records its address."""
+    ws = _WS.get(device)
+    if ws is None or ws[0].numel() < slab_elems:
+        if ws is not None:
+            _RETIRED.append(ws)
+        s = max(slab_elems, ws[0].numel() if ws else 0, 1)
+        ws = _WS[device] = (torch.empty(s, device=device, dtype=torch.float32),
+                            torch.zeros(256, device=device, dtype=torch.bfloat16))
+    return ws
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dilation, out=None,
+               beta: float = 0.0, splits: int = 0) -> torch.Tensor:
+    """dW [Cout, Cin, KH, KW] (channels_last bf16) of conv2d(x, w) for the output gradient
+    ``dy`` (NHWC bf16); ``out`` given: written (beta 0) or accumulated (beta 1) in place."""
+    Cout, Cin, KH, KW = w_shape
+    N, _, IH, IW = x.shape
+    _, _, OH, OW = dy.shape
+    if not _cl(dy):
+        dy = dy.contiguous(memory_format=torch.channels_last)
+    if out is None:
+        out = torch.empty((Cout, KH, KW, Cin), dtype=torch.bfloat16, device=x.device).permute(0, 3, 1, 2)
+    assert tuple(out.shape) == (Cout, Cin, KH, KW) and out.stride(1) == 1 and out.stride(0) == KH * KW * Cin
+    T = N * OH * OW
+    ntiles = KH * KW * (Cout // 128) * (Cin // 128)
+    if splits <= 0:
+        splits = plan_splits(T, ntiles)
+    splits = int(_lib.query("mx_conv_wgrad_splits", T, splits))
+    slab, zero = _workspace(x.device, ntiles * splits * 128 * 128 if splits > 1 else 1)
+    d = _DESC_T()
+    d[:] = [dy.data_ptr(), x.data_ptr(), zero.data_ptr(), out.data_ptr(), slab.data_ptr(), 0,
+            Cout, Cin, N, OH, OW, IH, IW, KH, KW, _sym(stride), _sym(padding), _sym(dilation), Cout, Cin]
+    _lib.call("mx_conv_wgrad", d, float(beta), splits, _lib.stream())
+    return out
+
+
+class ConvWgFn(torch.autograd.Function):
+    """conv2d(x, w) with MIOpen forward / input gradient and the implicit-GEMM weight
+    gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, padding, dilation):
+        ctx.conf = (list(_pair(stride)), list(_pair(padding)), list(_pair(dilation)))
+        ctx.save_for_backward(x, w)
+        return F.conv2d(x, w, None, stride, padding, dilation)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        st, pd, dl = ctx.conf
+        if not _cl(g):
+            g = g.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(g, x, w, None, st, pd, dl, False, [0, 0], 1,
+                                                     [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            dw = conv_wgrad(g, x, tuple(w.shape), st, pd, dl)
+        return dx, dw, None, None, None
+
+
+def conv2d_wg(x, w, stride=1, padding=0, dilation=1):
+    return ConvWgFn.apply(x, w, stride, padding, dilation)

@@ -18,6 +18,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
+from . import convwg
 
 _ENABLED = os.environ.get("MXTRAIN_CONV_EPILOGUE", "1") == "1"
 
@@ -140,12 +141,15 @@ def conv1x1_gemm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 def conv_bias_act(x, w, b=None, stride=1, padding=0, dilation=1, relu: bool = False,
                   residual: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """act(conv2d(x, w) + b (+ residual)) -- one conv (hipBLASLt GEMM for 1x1 stride-1,
-    MIOpen otherwise) + one fused epilogue pass."""
+    """act(conv2d(x, w) + b (+ residual)) -- one conv (MIOpen forward and input gradient;
+    the weight gradient from csrc/convwg.hip where it tiles) + one fused epilogue pass."""
     if _fused_ok(x, b, residual) and x.shape[1] == w.shape[1]:
         if (_GEMM_1X1 and w.shape[2] == 1 and w.shape[3] == 1 and _as_int(stride) == 1 and _as_int(padding) == 0
                 and w.dtype == x.dtype):
             return bias_act(conv1x1_gemm(x, w), b, residual, relu)
+        if convwg.supported(x, w, stride, padding, dilation):
+            # MIOpen forward / input gradient, implicit-GEMM weight gradient (ops/convwg.py)
+            return bias_act(convwg.conv2d_wg(x, w, stride, padding, dilation), b, residual, relu)
         return bias_act(F.conv2d(x, w, None, stride, padding, dilation), b, residual, relu)
     y = F.conv2d(x, w, b, stride, padding, dilation)
     if residual is not None:

@@ -1,0 +1,86 @@
+"""Mask R-CNN (1 img, 800 x 1344) convolution weight gradients: MIOpen (torch
+convolution_backward, weight only) vs csrc/convwg.hip, per shape, with TFLOP/s."""
+import sys, os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from mxtrain.ops import convwg
+
+N = int(os.environ.get("IMGS", "1"))
+# name, Cin, Cout, H_in, W_in, k, stride, pad, count per step
+SHAPES = [
+    ("res3.conv1 s2", 256, 128, 200, 336, 1, 2, 0, 1),
+    ("res3.conv2", 128, 128, 100, 168, 3, 1, 1, 4),
+    ("res3.conv3", 128, 512, 100, 168, 1, 1, 0, 4),
+    ("res3.short s2", 256, 512, 200, 336, 1, 2, 0, 1),
+    ("res3.conv1", 512, 128, 100, 168, 1, 1, 0, 3),
+    ("res4.conv1 s2", 512, 256, 100, 168, 1, 2, 0, 1),
+    ("res4.conv2", 256, 256, 50, 84, 3, 1, 1, 6),
+    ("res4.conv3", 256, 1024, 50, 84, 1, 1, 0, 6),
+    ("res4.short s2", 512, 1024, 100, 168, 1, 2, 0, 1),
+    ("res4.conv1", 1024, 256, 50, 84, 1, 1, 0, 5),
+    ("res5.conv1 s2", 1024, 512, 50, 84, 1, 2, 0, 1),
+    ("res5.conv2", 512, 512, 25, 42, 3, 1, 1, 3),
+    ("res5.conv3", 512, 2048, 25, 42, 1, 1, 0, 3),
+    ("res5.short s2", 1024, 2048, 50, 84, 1, 2, 0, 1),
+    ("res5.conv1", 2048, 512, 25, 42, 1, 1, 0, 2),
+    ("fpn.lat2", 256, 256, 200, 336, 1, 1, 0, 1),
+    ("fpn.lat3", 512, 256, 100, 168, 1, 1, 0, 1),
+    ("fpn.lat4", 1024, 256, 50, 84, 1, 1, 0, 1),
+    ("fpn.lat5", 2048, 256, 25, 42, 1, 1, 0, 1),
+    ("fpn.out2 / rpn P2", 256, 256, 200, 336, 3, 1, 1, 2),
+    ("fpn.out3 / rpn P3", 256, 256, 100, 168, 3, 1, 1, 2),
+    ("fpn.out4 / rpn P4", 256, 256, 50, 84, 3, 1, 1, 2),
+    ("fpn.out5 / rpn P5", 256, 256, 25, 42, 3, 1, 1, 2),
+    ("rpn P6", 256, 256, 13, 21, 3, 1, 1, 1),
+    ("mask head (64 rois)", 256, 256, 14, 14, 3, 1, 1, 4),
+]
+
+
+def timeit(fn, it=10, reps=5):
+    """GPU time per call: `it` calls captured in one hipGraph, replayed `reps` times (the
+    eager calls of the small convs are host-bound)."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(it):
+                fn()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        g.replay()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1000 / (it * reps)
+
+
+tot_m = tot_h = 0.0
+cl = torch.channels_last
+print(f"{'conv':22s} {'N':>3s} {'MIOpen us':>10s} {'convwg us':>10s} {'TF/s mi':>8s} {'TF/s wg':>8s}  splits  maxrel")
+for name, Cin, Cout, H, W, k, s, p, cnt in SHAPES:
+    n = 64 * N if name.startswith("mask") else N
+    x = torch.randn(n, Cin, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (torch.randn(Cout, Cin, k, k, device="cuda") * 0.05).to(torch.bfloat16).contiguous(memory_format=cl)
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = torch.randn(n, Cout, OH, OW, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    mi = lambda: torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
+                                                     [False, True, False])
+    wg = lambda: convwg.conv_wgrad(dy, x, (Cout, Cin, k, k), s, p, 1)
+    tm, th = timeit(mi), timeit(wg)
+    ref = mi()[1].float()
+    got = wg().float()
+    rel = ((got - ref).abs().max() / ref.abs().max()).item()
+    fl = 2.0 * n * OH * OW * Cout * Cin * k * k
+    T = n * OH * OW
+    ntiles = k * k * (Cout // 128) * (Cin // 128)
+    print(f"{name:22s} {n:3d} {tm:10.1f} {th:10.1f} {fl / tm / 1e6:8.1f} {fl / th / 1e6:8.1f}  {convwg.plan_splits(T, ntiles):6d}  {rel:.2e}  x{cnt}",
+          flush=True)
+    tot_m += cnt * tm
+    tot_h += cnt * th
+print(f"per step (counts): MIOpen {tot_m:.0f} us, convwg {tot_h:.0f} us")

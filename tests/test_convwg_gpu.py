@@ -1,0 +1,89 @@
+"""Implicit-GEMM convolution weight gradients (csrc/convwg.hip, ops/convwg.py) against the
+plain PyTorch fp32 weight gradient of the same convolution (CPU), for 1x1 / strided 1x1 /
+3x3 / dilated 3x3 filters, pixel counts that are not multiples of 64, several images,
+fixed and planned split counts and accumulation into an existing gradient."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # N, Cin, Cout, H, W, k, stride, pad, dil
+    (1, 128, 256, 17, 23, 1, 1, 0, 1),
+    (2, 256, 128, 16, 17, 1, 2, 0, 1),
+    (1, 128, 128, 25, 42, 3, 1, 1, 1),
+    (3, 256, 256, 14, 14, 3, 1, 1, 1),
+    (1, 128, 128, 19, 21, 3, 1, 2, 2),
+    (2, 128, 256, 9, 11, 3, 2, 1, 1),
+]
+
+
+def _ref(dy, x, w_shape, stride, pad, dil):
+    return torch.ops.aten.convolution_backward(dy.float().cpu(), x.float().cpu(), torch.zeros(w_shape), None,
+                                               [stride] * 2, [pad] * 2, [dil] * 2, False, [0, 0], 1,
+                                               [False, True, False])[1]
+
+
+def _inputs(N, Cin, Cout, H, W, k, stride, pad, dil, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(N, Cin, H, W, generator=g).to(torch.bfloat16)
+    OH = (H + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    OW = (W + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    dy = torch.randn(N, Cout, OH, OW, generator=g).to(torch.bfloat16)
+    cl = torch.channels_last
+    return x.cuda().contiguous(memory_format=cl), dy.cuda().contiguous(memory_format=cl)
+
+
+def _close(out, ref):
+    err = (out.float().cpu() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= 1e-2 * scale + 1e-3, (err, scale)
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("splits", [1, 3, 0])
+def test_conv_wgrad_matches_fp32(case, splits):
+    from mxtrain.ops import convwg
+    N, Cin, Cout, H, W, k, stride, pad, dil = case
+    x, dy = _inputs(*case)
+    out = convwg.conv_wgrad(dy, x, (Cout, Cin, k, k), stride, pad, dil, splits=splits)
+    torch.cuda.synchronize()
+    assert out.is_contiguous(memory_format=torch.channels_last)
+    _close(out, _ref(dy, x, (Cout, Cin, k, k), stride, pad, dil))
+
+
+def test_conv_wgrad_accumulates_and_is_deterministic():
+    from mxtrain.ops import convwg
+    case = (2, 128, 128, 30, 31, 3, 1, 1, 1)
+    N, Cin, Cout, H, W, k, stride, pad, dil = case
+    x, dy = _inputs(*case, seed=3)
+    a = convwg.conv_wgrad(dy, x, (Cout, Cin, k, k), stride, pad, dil, splits=5)
+    b = convwg.conv_wgrad(dy, x, (Cout, Cin, k, k), stride, pad, dil, splits=5)
+    assert torch.equal(a, b)
+    base = torch.randn(Cout, k, k, Cin, device="cuda").to(torch.bfloat16).permute(0, 3, 1, 2)
+    acc = base.clone(memory_format=torch.channels_last)
+    convwg.conv_wgrad(dy, x, (Cout, Cin, k, k), stride, pad, dil, out=acc, beta=1.0, splits=5)
+    torch.cuda.synchronize()
+    _close(acc.float() - base.float(), _ref(dy, x, (Cout, Cin, k, k), stride, pad, dil))
+
+
+def test_conv_wg_autograd_matches_conv2d():
+    """The autograd Function: output and input gradient are MIOpen's (as F.conv2d's, up to
+    the solver MIOpen picks per call), the weight gradient matches the fp32 reference."""
+    from mxtrain.ops import convwg
+    torch.manual_seed(0)
+    cl = torch.channels_last
+    x = torch.randn(2, 128, 20, 24, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (torch.randn(256, 3, 3, 128, device="cuda") * 0.05).to(torch.bfloat16).permute(0, 3, 1, 2)
+    x1, w1 = x.clone().requires_grad_(), w.detach().clone(memory_format=cl).requires_grad_()
+    x2, w2 = x.clone().requires_grad_(), w.detach().clone(memory_format=cl).requires_grad_()
+    assert convwg.supported(x1, w1, 1, 1, 1)
+    y1 = convwg.conv2d_wg(x1, w1, 1, 1, 1)
+    y2 = torch.nn.functional.conv2d(x2, w2, None, 1, 1, 1)
+    _close(y1.detach(), y2.detach().float().cpu())
+    g = torch.randn_like(y1)
+    y1.backward(g)
+    y2.backward(g)
+    _close(x1.grad, x2.grad.float().cpu())
+    ref = _ref(g, x, tuple(w.shape), 1, 1, 1)
+    _close(w1.grad, ref)
