@@ -203,6 +203,157 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
 
 constexpr int kBM = 128, kBN = 128, kBK = 64, kNT = 256;
 
+// ============================================================================ input gradient
+// dX[p][ci] = sum over taps (r, s) and output channels co of dY[q(p, r, s)][co] * W[co][r][s][ci]
+// with q the output pixel whose window puts tap (r, s) on input pixel p (none, i.e. a zero
+// row, when the tap falls outside the output image or between strides).  A GEMM over the
+// input pixels (M) x Cin (N) with the reduction over (tap, co) in 64-deep K-steps: the dY
+// rows are gathered per tap by the LDS-DMA lanes (K-contiguous [m][64 co] image, 128-B rows
+// XOR-swizzled by row & 7, ds_read_b128 fragments), the weight rows [co][Cin] of a tap are
+// a K-major image read with the transposed-read scheme of the weight gradient above.
+// Replaces MIOpen's backward-data solvers (CK grouped bwd-data, igemm_bwd_gtcx35: ~2 ms of
+// the 1-img Mask R-CNN step, profiles/r2_maskrcnn_s3/census_1img_graph_948_kernels.txt).
+struct ConvDg {
+  const uint16_t* dy;    // [N * OH * OW][ldy]
+  const uint16_t* w;     // [Cout][taps][Cin]
+  const uint16_t* zero;  // >= 256 zero bf16
+  uint16_t* dx;          // [N * IH * IW][ldx]
+  int ldy, ldx;
+  int T, OH, OW, IH, IW;
+  int KW, taps, stride, pad, dil;
+  int Cin, tiles_n, nk, cob;
+  float invIW, invIH;
+};
+
+template <int NSLOT>
+__global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
+  constexpr int WN = 2, FM = 4, FN = 4, BKT = 64;
+  constexpr int BM = 128, BN = 128, RA = BKT * 2, RB = BN * 2;
+  constexpr int IA = BM * RA, IB = BKT * RB;
+  constexpr int PA = IA / 1024 / 4, PB = IB / 1024 / 4;
+  constexpr int SLOT = IA + IB, PER = PA + PB;
+  __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  // Cin tiles of one pixel block adjacent (same XCD): they share the gathered dY rows in L2
+  const int tm = wg / cp.tiles_n, tn = wg - tm * cp.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = cp.nk;
+  const size_t ldw = (size_t)cp.taps * cp.Cin;
+
+  // ---- A (gathered dY) rows of this lane: fixed input pixel per DMA piece
+  int an[PA], aih[PA], aiw[PA], ach[PA];
+  bool aok[PA];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    const int row = (PA * wave + j) * (1024 / RA) + lane / (RA / 16);
+    const int p = m0 + row;
+    aok[j] = p < cp.T;
+    int q, iw, n, ih;
+    divmod(aok[j] ? p : 0, cp.IW, cp.invIW, q, iw);
+    divmod(q, cp.IH, cp.invIH, n, ih);
+    an[j] = n; aih[j] = ih; aiw[j] = iw;
+    ach[j] = 8 * ((lane % (RA / 16)) ^ (row & 7));
+  }
+  int kB[PB], cB[PB];
+#pragma unroll
+  for (int j = 0; j < PB; ++j) {
+    kB[j] = (PB * wave + j) * (1024 / RB) + lane / (RB / 16);
+    cB[j] = 8 * pchunk(kB[j], lane % (RB / 16));
+  }
+  auto srcA = [&](int j, int tap, int co0) __attribute__((always_inline)) {
+    const int r = tap / cp.KW, s = tap - r * cp.KW;
+    int oh = aih[j] + cp.pad - r * cp.dil, ow = aiw[j] + cp.pad - s * cp.dil;
+    bool ok = aok[j];
+    if (cp.stride > 1) {
+      ok = ok && (oh % cp.stride) == 0 && (ow % cp.stride) == 0;
+      oh /= cp.stride;
+      ow /= cp.stride;
+    }
+    ok = ok && (unsigned)oh < (unsigned)cp.OH && (unsigned)ow < (unsigned)cp.OW;
+    return ok ? cp.dy + ((size_t)(an[j] * cp.OH + oh) * cp.OW + ow) * cp.ldy + co0 + ach[j] : cp.zero + ach[j];
+  };
+  auto srcB = [&](int j, int tap, int co0) __attribute__((always_inline)) {
+    return cp.w + (size_t)(co0 + kB[j]) * ldw + (size_t)tap * cp.Cin + n0 + cB[j];
+  };
+
+  const int G = lane >> 4, i = lane & 15;
+  const int wm = wave / WN, wn = wave % WN;
+  const int offA = (16 * FM * wm + i) * RA;
+  int cA[BKT / 32];
+#pragma unroll
+  for (int kk = 0; kk < BKT / 32; ++kk) cA[kk] = 16 * ((4 * kk + G) ^ (i & 7));
+  const int krow = 8 * G + (i >> 2);
+  const int gq = gsw(krow);
+  int offB[FN];
+#pragma unroll
+  for (int u = 0; u < FN; ++u)
+    offB[u] = krow * RB + ((((FN * wn + u) ^ gq) << 1) | ((i & 3) >> 1)) * 16 + (i & 1) * 8;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int u = 0; u < FN; ++u) acc[a][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const uint32_t lds0 = lds_addr(smem);
+  auto issue = [&](int slot, int it) __attribute__((always_inline)) {
+    const int tap = it / cp.cob, co0 = (it - tap * cp.cob) * BKT;
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
+    const uint32_t b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
+#pragma unroll
+    for (int j = 0; j < PA; ++j) dma16(srcA(j, tap, co0), b0 + j * 1024);
+#pragma unroll
+    for (int j = 0; j < PB; ++j) dma16(srcB(j, tap, co0), b1 + j * 1024);
+  };
+
+#pragma unroll
+  for (int q = 0; q < NSLOT - 1; ++q)
+    if (q < nk) issue(q, q);
+  int slot = 0;
+  for (int it = 0; it < nk; ++it) {
+    const int later = nk - 1 - it;
+    if (NSLOT >= 4 && later >= 2) vm_wait<(NSLOT >= 4 ? 2 : 0) * PER>();
+    else if (NSLOT >= 3 && later >= 1) vm_wait<(NSLOT >= 3 ? 1 : 0) * PER>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (it + NSLOT - 1 < nk) {
+      int ns = slot + NSLOT - 1;
+      if (ns >= NSLOT) ns -= NSLOT;
+      issue(ns, it + NSLOT - 1);
+    }
+    const char* As = smem + slot * SLOT;
+    const char* Bs = As + IA;
+#pragma unroll
+    for (int kk = 0; kk < BKT / 32; ++kk) {
+      bf16x8 b[FN];
+#pragma unroll
+      for (int u = 0; u < FN; ++u)
+        b[u] = cat(tr_read(Bs, offB[u] + 32 * RB * kk), tr_read(Bs, offB[u] + 32 * RB * kk + 4 * RB));
+#pragma unroll
+      for (int a = 0; a < FM; ++a) {
+        const bf16x8 av = lds_read8(As, offA + 16 * a * RA + cA[kk]);
+#pragma unroll
+        for (int u = 0; u < FN; ++u) acc[a][u] = mfma16(av, b[u], acc[a][u]);
+      }
+    }
+    if (++slot == NSLOT) slot = 0;
+  }
+
+  // ---- epilogue: lane holds dX[m0 + 16 (FM wm + a) + 4 G + e][n0 + 16 (FN wn + u) + i]
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int p = m0 + 16 * (FM * wm + a) + 4 * G + e;
+      if (p < cp.T) {
+        uint16_t* row = cp.dx + (size_t)p * cp.ldx + n0 + 16 * FN * wn + i;
+#pragma unroll
+        for (int u = 0; u < FN; ++u) row[16 * u] = f2bf(acc[a][u][e]);
+      }
+    }
+}
+
 // Split-K reduction: one thread per (tile, accumulator register group, lane) float4 column,
 // summed over the slices in slice order (deterministic), written to dW with the main
 // kernel's epilogue mapping (4 waves of 64 x 64: WM = WN = 2, FM = FN = 4).
@@ -315,4 +466,46 @@ MX_EXPORT int mx_conv_wgrad_splits(int64_t T, int splits) {
   if (splits < 1) splits = 1;
   const int nk = (steps + splits - 1) / splits;
   return (steps + nk - 1) / nk;
+}
+
+// d (int64[20]): {dy, w, zero, dx, 0, 0, ldy, ldx, N, OH, OW, IH, IW, KH, KW, stride, pad,
+// dil, Cout, Cin}: dX of conv2d for the output gradient dY, weight [Cout][KH][KW][Cin]
+// (channels_last).  Cout a multiple of 64, Cin of 128; 16-B aligned operands.
+MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
+  ConvDg cp{};
+  cp.dy = reinterpret_cast<const uint16_t*>(d[0]);
+  cp.w = reinterpret_cast<const uint16_t*>(d[1]);
+  cp.zero = reinterpret_cast<const uint16_t*>(d[2]);
+  cp.dx = reinterpret_cast<uint16_t*>(d[3]);
+  cp.ldy = (int)d[6];
+  cp.ldx = (int)d[7];
+  const int64_t N = d[8];
+  cp.OH = (int)d[9];
+  cp.OW = (int)d[10];
+  cp.IH = (int)d[11];
+  cp.IW = (int)d[12];
+  const int KH = (int)d[13];
+  cp.KW = (int)d[14];
+  cp.stride = (int)d[15];
+  cp.pad = (int)d[16];
+  cp.dil = (int)d[17];
+  const int Cout = (int)d[18];
+  cp.Cin = (int)d[19];
+  const int64_t T = N * cp.IH * cp.IW;
+  if (N <= 0 || cp.IH <= 0 || cp.IW <= 0 || cp.OH <= 0 || cp.OW <= 0 || KH <= 0 || cp.KW <= 0 || cp.stride <= 0 ||
+      cp.dil <= 0 || cp.pad < 0 || T >= (1 << 23) || N * cp.OH * cp.OW >= ((int64_t)1 << 31))
+    return (int)hipErrorInvalidValue;
+  if (Cout % 64 || cp.Cin % 128 || cp.ldy < Cout || cp.ldx < cp.Cin || (cp.ldy & 7) || (cp.ldx & 7))
+    return (int)hipErrorInvalidValue;
+  if ((d[0] | d[1] | d[2] | d[3]) & 15) return (int)hipErrorInvalidValue;
+  cp.T = (int)T;
+  cp.taps = KH * cp.KW;
+  cp.cob = Cout / 64;
+  cp.nk = cp.taps * cp.cob;
+  cp.tiles_n = cp.Cin / 128;
+  cp.invIW = 1.f / (float)cp.IW;
+  cp.invIH = 1.f / (float)cp.IH;
+  const int tiles_m = (int)((T + 127) / 128);
+  hipLaunchKernelGGL(conv_dgrad_kernel<2>, dim3(tiles_m * cp.tiles_n), dim3(256), 0, (hipStream_t)stream, cp);
+  return (int)hipGetLastError();
 }

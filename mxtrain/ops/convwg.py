@@ -1,9 +1,10 @@
 """Convolution weight gradients as implicit GEMMs (csrc/convwg.hip).
 
-``conv2d_wg(x, w, stride, padding, dilation)`` is ``F.conv2d`` whose backward keeps
-MIOpen for the input gradient and computes the weight gradient with the hand-written
-implicit-GEMM kernel: one launch per conv (every filter tap in it), split over the
-output pixels, written straight into the channels_last bf16 gradient of the compute copy.
+``conv2d_wg(x, w, stride, padding, dilation)`` is ``F.conv2d`` (MIOpen forward) whose
+backward computes the weight gradient with the hand-written implicit-GEMM kernel -- one
+launch per conv (every filter tap in it), split over the output pixels, written straight
+into the channels_last bf16 gradient of the compute copy -- and the input gradient with
+its implicit-GEMM counterpart (dY rows gathered per tap).
 That replaces MIOpen's weight-gradient solvers and their fp32 workspace fill / cast
 helpers, ~2.9 ms of the ~12 ms graphed Mask R-CNN step
 (profiles/r2_maskrcnn_s3/census_1img_graph_948_kernels.txt).
@@ -22,6 +23,7 @@ import torch.nn.functional as F
 from . import _lib
 
 ENABLED = True          # module switch (A/B runs: scripts/conv_wgrad_bench.py)
+DGRAD = True            # input gradient from csrc/convwg.hip too (else MIOpen's backward-data)
 TARGET_WGS = 512        # two 128 x 128 workgroups per CU on 256 CUs
 MIN_STEPS = 8
 _DESC_T = ctypes.c_int64 * 20
@@ -101,9 +103,43 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dila
     return out
 
 
+def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride, padding, dilation) -> torch.Tensor:
+    """dX [N, Cin, IH, IW] (channels_last bf16) of conv2d(x, w) for the output gradient
+    ``dy``; ``w`` bf16 [Cout, Cin, KH, KW] (made channels_last if it is not)."""
+    Cout, Cin, KH, KW = w.shape
+    N, _, IH, IW = x_shape
+    _, _, OH, OW = dy.shape
+    if not _cl(dy):
+        dy = dy.contiguous(memory_format=torch.channels_last)
+    if not _cl(w):
+        w = w.contiguous(memory_format=torch.channels_last)
+    dx = torch.empty((N, IH, IW, Cin), dtype=torch.bfloat16, device=dy.device).permute(0, 3, 1, 2)
+    _, zero = _workspace(dy.device, 1)
+    d = _DESC_T()
+    d[:] = [dy.data_ptr(), w.data_ptr(), zero.data_ptr(), dx.data_ptr(), 0, 0,
+            Cout, Cin, N, OH, OW, IH, IW, KH, KW, _sym(stride), _sym(padding), _sym(dilation), Cout, Cin]
+    _lib.call("mx_conv_dgrad", d, _lib.stream())
+    return dx
+
+
+DGRAD_MIN_TILES = 64
+
+
+def dgrad_supported(w: torch.Tensor, x_shape, stride) -> bool:
+    """The implicit-GEMM input gradient where it beat MIOpen's backward-data solvers at the
+    Mask R-CNN shapes (profiles/r3_s4/conv_dgrad_vs_miopen_graphed.txt): at least
+    DGRAD_MIN_TILES 128 x 128 output tiles (fewer: long latency-bound K loops on a mostly
+    idle chip -- res5 3x3 65 vs 40 us), and stride 1 or at most 256 output channels (a
+    strided conv's gathered dY has 3 of 4 rows zero, which costs MFMA time per K-step)."""
+    if not (DGRAD and w.shape[0] % 64 == 0 and w.shape[1] % 128 == 0 and w.data_ptr() % 16 == 0):
+        return False
+    N, Cin, IH, IW = x_shape
+    tiles = (N * IH * IW + 127) // 128 * (Cin // 128)
+    return tiles >= DGRAD_MIN_TILES and (_sym(stride) == 1 or w.shape[0] <= 256)
+
+
 class ConvWgFn(torch.autograd.Function):
-    """conv2d(x, w) with MIOpen forward / input gradient and the implicit-GEMM weight
-    gradient."""
+    """conv2d(x, w): MIOpen forward, implicit-GEMM weight and input gradients."""
 
     @staticmethod
     def forward(ctx, x, w, stride, padding, dilation):
@@ -119,8 +155,11 @@ class ConvWgFn(torch.autograd.Function):
             g = g.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = torch.ops.aten.convolution_backward(g, x, w, None, st, pd, dl, False, [0, 0], 1,
-                                                     [True, False, False])[0]
+            if dgrad_supported(w, tuple(x.shape), st):
+                dx = conv_dgrad(g, w, tuple(x.shape), st, pd, dl)
+            else:
+                dx = torch.ops.aten.convolution_backward(g, x, w, None, st, pd, dl, False, [0, 0], 1,
+                                                         [True, False, False])[0]
         if ctx.needs_input_grad[1]:
             dw = conv_wgrad(g, x, tuple(w.shape), st, pd, dl)
         return dx, dw, None, None, None

@@ -60,9 +60,10 @@ def timeit(fn, it=10, reps=5):
     return a.elapsed_time(b) * 1000 / (it * reps)
 
 
-tot_m = tot_h = 0.0
+tot_m = tot_h = tot_dm = tot_dh = 0.0
 cl = torch.channels_last
-print(f"{'conv':22s} {'N':>3s} {'MIOpen us':>10s} {'convwg us':>10s} {'TF/s mi':>8s} {'TF/s wg':>8s}  splits  maxrel")
+print(f"{'conv':22s} {'N':>3s} {'MIOpen us':>10s} {'convwg us':>10s} {'TF/s mi':>8s} {'TF/s wg':>8s}  splits  maxrel"
+      f"   | dgrad: MIOpen us  convdg us  maxrel")
 for name, Cin, Cout, H, W, k, s, p, cnt in SHAPES:
     n = 64 * N if name.startswith("mask") else N
     x = torch.randn(n, Cin, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
@@ -79,8 +80,18 @@ for name, Cin, Cout, H, W, k, s, p, cnt in SHAPES:
     fl = 2.0 * n * OH * OW * Cout * Cin * k * k
     T = n * OH * OW
     ntiles = k * k * (Cout // 128) * (Cin // 128)
-    print(f"{name:22s} {n:3d} {tm:10.1f} {th:10.1f} {fl / tm / 1e6:8.1f} {fl / th / 1e6:8.1f}  {convwg.plan_splits(T, ntiles):6d}  {rel:.2e}  x{cnt}",
-          flush=True)
+    dmi = lambda: torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
+                                                      [True, False, False])
+    dwg = lambda: convwg.conv_dgrad(dy, w, tuple(x.shape), s, p, 1)
+    dtm, dth = timeit(dmi), timeit(dwg)
+    dref = dmi()[0].float()
+    drel = ((dwg().float() - dref).abs().max() / dref.abs().max()).item()
+    print(f"{name:22s} {n:3d} {tm:10.1f} {th:10.1f} {fl / tm / 1e6:8.1f} {fl / th / 1e6:8.1f}  {convwg.plan_splits(T, ntiles):6d}  {rel:.2e}"
+          f"   | {dtm:8.1f} {dth:9.1f}  {drel:.2e}  x{cnt}", flush=True)
     tot_m += cnt * tm
     tot_h += cnt * th
-print(f"per step (counts): MIOpen {tot_m:.0f} us, convwg {tot_h:.0f} us")
+    if not name.startswith(("res3.conv1 s2", "res3.short", "fpn.lat2")):   # inputs without a gradient
+        tot_dm += cnt * dtm
+        tot_dh += cnt * dth
+print(f"per step (counts): wgrad MIOpen {tot_m:.0f} us, convwg {tot_h:.0f} us; "
+      f"dgrad MIOpen {tot_dm:.0f} us, convdg {tot_dh:.0f} us")

@@ -87,3 +87,22 @@ def test_conv_wg_autograd_matches_conv2d():
     _close(x1.grad, x2.grad.float().cpu())
     ref = _ref(g, x, tuple(w.shape), 1, 1, 1)
     _close(w1.grad, ref)
+
+
+def _ref_dx(dy, w, x_shape, stride, pad, dil):
+    return torch.ops.aten.convolution_backward(dy.float().cpu(), torch.zeros(x_shape), w.float().cpu(), None,
+                                               [stride] * 2, [pad] * 2, [dil] * 2, False, [0, 0], 1,
+                                               [True, False, False])[0]
+
+
+@pytest.mark.parametrize("case", CASES + [(1, 128, 64, 13, 9, 3, 1, 1, 1)])
+def test_conv_dgrad_matches_fp32(case):
+    from mxtrain.ops import convwg
+    N, Cin, Cout, H, W, k, stride, pad, dil = case
+    x, dy = _inputs(*case, seed=7)
+    g = torch.Generator().manual_seed(11)
+    w = (torch.randn(Cout, k, k, Cin, generator=g) * 0.1).to(torch.bfloat16).cuda().permute(0, 3, 1, 2)
+    dx = convwg.conv_dgrad(dy, w, tuple(x.shape), stride, pad, dil)
+    torch.cuda.synchronize()
+    assert dx.is_contiguous(memory_format=torch.channels_last)
+    _close(dx, _ref_dx(dy, w, tuple(x.shape), stride, pad, dil))
