@@ -203,6 +203,141 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
 
 constexpr int kBM = 128, kBN = 128, kBK = 64, kNT = 256;
 
+// ================================================================================= forward
+// y[p][co] = act(sum over taps (r, s) and ci of X[pix(p, r, s)][ci] * W[co][r][s][ci] + b[co]
+// (+ res[p][co])): a GEMM over the output pixels (M) x Cout (N), reduction over (tap, ci)
+// in 64-deep K-steps; the X rows are gathered per tap like the dY rows of the input
+// gradient, the weight rows [co][64 ci] of a tap are a second K-contiguous image, so both
+// MFMA operands are plain ds_read_b128 fragments.  The bias / residual / ReLU epilogue of
+// ops/epilogue.py (the frozen-BN fold, the bottleneck join) is applied before the single
+// store, so the separate in-place bias_act pass disappears too.
+struct ConvFw {
+  const uint16_t* x;     // [N * IH * IW][ldx]
+  const uint16_t* w;     // [Cout][taps][Cin]
+  const uint16_t* zero;
+  uint16_t* y;           // [N * OH * OW][ldy]
+  const uint16_t* bias;  // [Cout] or null
+  const uint16_t* res;   // [N * OH * OW][ldy] or null
+  int ldx, ldy;
+  int T, OH, OW, IH, IW;
+  int KW, taps, stride, pad, dil;
+  int Cin, tiles_n, nk, cib;
+  float invOW, invOH;
+};
+
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
+  constexpr int WN = 2, FM = 4, FN = 4, BKT = 64, NSLOT = 2;
+  constexpr int BM = 128, BN = 128, R = BKT * 2;
+  constexpr int IA = BM * R, IB = BN * R;
+  constexpr int PA = IA / 1024 / 4, PB = IB / 1024 / 4;
+  constexpr int SLOT = IA + IB, PER = PA + PB;
+  __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = wg / cp.tiles_n, tn = wg - tm * cp.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = cp.nk;
+  const size_t ldw = (size_t)cp.taps * cp.Cin;
+
+  int an[PA], aoh[PA], aow[PA], ach[PA];
+  bool aok[PA];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    const int row = (PA * wave + j) * (1024 / R) + lane / (R / 16);
+    const int p = m0 + row;
+    aok[j] = p < cp.T;
+    int q, ow, n, oh;
+    divmod(aok[j] ? p : 0, cp.OW, cp.invOW, q, ow);
+    divmod(q, cp.OH, cp.invOH, n, oh);
+    an[j] = n; aoh[j] = oh * cp.stride - cp.pad; aow[j] = ow * cp.stride - cp.pad;
+    ach[j] = 8 * ((lane % (R / 16)) ^ (row & 7));
+  }
+  int brow[PB];
+#pragma unroll
+  for (int j = 0; j < PB; ++j) brow[j] = n0 + (PB * wave + j) * (1024 / R) + lane / (R / 16);
+  auto srcA = [&](int j, int tap, int ci0) __attribute__((always_inline)) {
+    const int r = tap / cp.KW, s = tap - r * cp.KW;
+    const int ih = aoh[j] + r * cp.dil, iw = aow[j] + s * cp.dil;
+    const bool ok = aok[j] && (unsigned)ih < (unsigned)cp.IH && (unsigned)iw < (unsigned)cp.IW;
+    return ok ? cp.x + ((size_t)(an[j] * cp.IH + ih) * cp.IW + iw) * cp.ldx + ci0 + ach[j] : cp.zero + ach[j];
+  };
+  auto srcB = [&](int j, int tap, int ci0) __attribute__((always_inline)) {
+    return cp.w + (size_t)brow[j] * ldw + (size_t)tap * cp.Cin + ci0 + ach[j];   // same chunk swizzle
+  };
+
+  const int G = lane >> 4, i = lane & 15;
+  const int wm = wave / WN, wn = wave % WN;
+  const int offA = (16 * FM * wm + i) * R, offB = (16 * FN * wn + i) * R;
+  int cK[BKT / 32];
+#pragma unroll
+  for (int kk = 0; kk < BKT / 32; ++kk) cK[kk] = 16 * ((4 * kk + G) ^ (i & 7));
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int u = 0; u < FN; ++u) acc[a][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const uint32_t lds0 = lds_addr(smem);
+  auto issue = [&](int slot, int it) __attribute__((always_inline)) {
+    const int tap = it / cp.cib, ci0 = (it - tap * cp.cib) * BKT;
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
+    const uint32_t b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
+#pragma unroll
+    for (int j = 0; j < PA; ++j) dma16(srcA(j, tap, ci0), b0 + j * 1024);
+#pragma unroll
+    for (int j = 0; j < PB; ++j) dma16(srcB(j, tap, ci0), b1 + j * 1024);
+  };
+
+  if (nk > 0) issue(0, 0);
+  int slot = 0;
+  for (int it = 0; it < nk; ++it) {
+    vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (it + 1 < nk) issue(slot ^ 1, it + 1);
+    const char* As = smem + slot * SLOT;
+    const char* Bs = As + IA;
+#pragma unroll
+    for (int kk = 0; kk < BKT / 32; ++kk) {
+      bf16x8 b[FN];
+#pragma unroll
+      for (int u = 0; u < FN; ++u) b[u] = lds_read8(Bs, offB + 16 * u * R + cK[kk]);
+#pragma unroll
+      for (int a = 0; a < FM; ++a) {
+        const bf16x8 av = lds_read8(As, offA + 16 * a * R + cK[kk]);
+#pragma unroll
+        for (int u = 0; u < FN; ++u) acc[a][u] = mfma16(av, b[u], acc[a][u]);
+      }
+    }
+    slot ^= 1;
+  }
+  (void)PER;
+
+  // ---- epilogue: lane holds y[m0 + 16 (FM wm + a) + 4 G + e][n0 + 16 (FN wn + u) + i]
+  const int col = n0 + 16 * FN * wn + i;
+  float bv[FN];
+#pragma unroll
+  for (int u = 0; u < FN; ++u) bv[u] = cp.bias ? bf2f(cp.bias[col + 16 * u]) : 0.f;
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int p = m0 + 16 * (FM * wm + a) + 4 * G + e;
+      if (p < cp.T) {
+        uint16_t* row = cp.y + (size_t)p * cp.ldy + col;
+        const uint16_t* rr = RES ? cp.res + (size_t)p * cp.ldy + col : nullptr;
+#pragma unroll
+        for (int u = 0; u < FN; ++u) {
+          float v = acc[a][u][e] + bv[u];
+          if (RES) v += bf2f(rr[16 * u]);
+          if (RELU) v = fmaxf(v, 0.f);
+          row[16 * u] = f2bf(v);
+        }
+      }
+    }
+}
+
 // ============================================================================ input gradient
 // dX[p][ci] = sum over taps (r, s) and output channels co of dY[q(p, r, s)][co] * W[co][r][s][ci]
 // with q the output pixel whose window puts tap (r, s) on input pixel p (none, i.e. a zero
@@ -507,5 +642,57 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   cp.invIH = 1.f / (float)cp.IH;
   const int tiles_m = (int)((T + 127) / 128);
   hipLaunchKernelGGL(conv_dgrad_kernel<2>, dim3(tiles_m * cp.tiles_n), dim3(256), 0, (hipStream_t)stream, cp);
+  return (int)hipGetLastError();
+}
+
+// d (int64[24]): {x, w, zero, y, bias, res, ldx, ldy, N, OH, OW, IH, IW, KH, KW, stride, pad,
+// dil, Cout, Cin, relu}: y = act(conv2d(x, w) + bias (+ res)) in NHWC bf16, weight
+// [Cout][KH][KW][Cin] (channels_last).  Cout a multiple of 128, Cin of 64.
+MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
+  ConvFw cp{};
+  cp.x = reinterpret_cast<const uint16_t*>(d[0]);
+  cp.w = reinterpret_cast<const uint16_t*>(d[1]);
+  cp.zero = reinterpret_cast<const uint16_t*>(d[2]);
+  cp.y = reinterpret_cast<uint16_t*>(d[3]);
+  cp.bias = reinterpret_cast<const uint16_t*>(d[4]);
+  cp.res = reinterpret_cast<const uint16_t*>(d[5]);
+  cp.ldx = (int)d[6];
+  cp.ldy = (int)d[7];
+  const int64_t N = d[8];
+  cp.OH = (int)d[9];
+  cp.OW = (int)d[10];
+  cp.IH = (int)d[11];
+  cp.IW = (int)d[12];
+  const int KH = (int)d[13];
+  cp.KW = (int)d[14];
+  cp.stride = (int)d[15];
+  cp.pad = (int)d[16];
+  cp.dil = (int)d[17];
+  const int Cout = (int)d[18];
+  cp.Cin = (int)d[19];
+  const bool relu = d[20] != 0;
+  const int64_t T = N * cp.OH * cp.OW;
+  if (N <= 0 || cp.IH <= 0 || cp.IW <= 0 || cp.OH <= 0 || cp.OW <= 0 || KH <= 0 || cp.KW <= 0 || cp.stride <= 0 ||
+      cp.dil <= 0 || cp.pad < 0 || T >= (1 << 23) || N * cp.IH * cp.IW >= ((int64_t)1 << 31))
+    return (int)hipErrorInvalidValue;
+  if (Cout % 128 || cp.Cin % 64 || cp.ldx < cp.Cin || cp.ldy < Cout || (cp.ldx & 7) || (cp.ldy & 7))
+    return (int)hipErrorInvalidValue;
+  if ((d[0] | d[1] | d[2]) & 15) return (int)hipErrorInvalidValue;
+  cp.T = (int)T;
+  cp.taps = KH * cp.KW;
+  cp.cib = cp.Cin / 64;
+  cp.nk = cp.taps * cp.cib;
+  cp.tiles_n = Cout / 128;
+  cp.invOW = 1.f / (float)cp.OW;
+  cp.invOH = 1.f / (float)cp.OH;
+  const dim3 grid((unsigned)((T + 127) / 128) * cp.tiles_n), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (cp.res) {
+    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<true, true>), grid, block, 0, st, cp);
+    else hipLaunchKernelGGL((conv_fwd_kernel<true, false>), grid, block, 0, st, cp);
+  } else {
+    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<false, true>), grid, block, 0, st, cp);
+    else hipLaunchKernelGGL((conv_fwd_kernel<false, false>), grid, block, 0, st, cp);
+  }
   return (int)hipGetLastError();
 }

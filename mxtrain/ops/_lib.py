@@ -99,6 +99,7 @@ SIGNATURES = {
     "mx_conv_wgrad": [P, F, I, P],
     "mx_conv_wgrad_splits": [I64, I],
     "mx_conv_dgrad": [P, P],
+    "mx_conv_fwd": [P, P],
     # gemm_nt.hip
     "mx_gemm_nt_tile": [I, I],
     "mx_gemm_nt": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],

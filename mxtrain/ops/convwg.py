@@ -24,9 +24,11 @@ from . import _lib
 
 ENABLED = True          # module switch (A/B runs: scripts/conv_wgrad_bench.py)
 DGRAD = True            # input gradient from csrc/convwg.hip too (else MIOpen's backward-data)
+FWD = False             # forward with the fused bias / residual / ReLU epilogue (else MIOpen); off until measured in the step
+FWD_MIN_TILES = 64
 TARGET_WGS = 512        # two 128 x 128 workgroups per CU on 256 CUs
 MIN_STEPS = 8
-_DESC_T = ctypes.c_int64 * 20
+_DESC_T = ctypes.c_int64 * 24
 _WS: Dict[torch.device, Tuple[torch.Tensor, torch.Tensor]] = {}
 _RETIRED = []           # outgrown slabs stay alive: a captured hipGraph may still write them
 
@@ -97,7 +99,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dila
     splits = int(_lib.query("mx_conv_wgrad_splits", T, splits))
     slab, zero = _workspace(x.device, ntiles * splits * 128 * 128 if splits > 1 else 1)
     d = _DESC_T()
-    d[:] = [dy.data_ptr(), x.data_ptr(), zero.data_ptr(), out.data_ptr(), slab.data_ptr(), 0,
+    d[:20] = [dy.data_ptr(), x.data_ptr(), zero.data_ptr(), out.data_ptr(), slab.data_ptr(), 0,
             Cout, Cin, N, OH, OW, IH, IW, KH, KW, _sym(stride), _sym(padding), _sym(dilation), Cout, Cin]
     _lib.call("mx_conv_wgrad", d, float(beta), splits, _lib.stream())
     return out
@@ -116,13 +118,52 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride, padding, dila
     dx = torch.empty((N, IH, IW, Cin), dtype=torch.bfloat16, device=dy.device).permute(0, 3, 1, 2)
     _, zero = _workspace(dy.device, 1)
     d = _DESC_T()
-    d[:] = [dy.data_ptr(), w.data_ptr(), zero.data_ptr(), dx.data_ptr(), 0, 0,
+    d[:20] = [dy.data_ptr(), w.data_ptr(), zero.data_ptr(), dx.data_ptr(), 0, 0,
             Cout, Cin, N, OH, OW, IH, IW, KH, KW, _sym(stride), _sym(padding), _sym(dilation), Cout, Cin]
     _lib.call("mx_conv_dgrad", d, _lib.stream())
     return dx
 
 
 DGRAD_MIN_TILES = 64
+
+
+def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, padding=0, dilation=1) -> bool:
+    """The implicit-GEMM forward: NHWC bf16, Cout a multiple of 128, Cin of 64, and at least
+    FWD_MIN_TILES 128 x 128 output tiles (smaller convs stay on MIOpen)."""
+    if not (FWD and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
+            and w.dim() == 4 and w.shape[0] % 128 == 0 and w.shape[1] % 64 == 0 and x.shape[1] == w.shape[1]
+            and _cl(x) and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+            and None not in (_sym(stride), _sym(padding), _sym(dilation))):
+        return False
+    if b is not None and not (b.dtype == torch.bfloat16 and b.is_contiguous() and b.numel() == w.shape[0]):
+        return False
+    st, pd, dl = _sym(stride), _sym(padding), _sym(dilation)
+    N, _, IH, IW = x.shape
+    OH = (IH + 2 * pd - dl * (w.shape[2] - 1) - 1) // st + 1
+    OW = (IW + 2 * pd - dl * (w.shape[3] - 1) - 1) // st + 1
+    if residual is not None and not (residual.dtype == torch.bfloat16 and _cl(residual)
+                                     and tuple(residual.shape) == (N, w.shape[0], OH, OW)):
+        return False
+    return (N * OH * OW + 127) // 128 * (w.shape[0] // 128) >= FWD_MIN_TILES
+
+
+def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool = False, stride=1, padding=0,
+             dilation=1) -> torch.Tensor:
+    """act(conv2d(x, w) + b (+ residual)), NHWC bf16 in and out, one launch."""
+    Cout, Cin, KH, KW = w.shape
+    N, _, IH, IW = x.shape
+    st, pd, dl = _sym(stride), _sym(padding), _sym(dilation)
+    OH = (IH + 2 * pd - dl * (KH - 1) - 1) // st + 1
+    OW = (IW + 2 * pd - dl * (KW - 1) - 1) // st + 1
+    if not _cl(w):
+        w = w.contiguous(memory_format=torch.channels_last)
+    y = torch.empty((N, OH, OW, Cout), dtype=torch.bfloat16, device=x.device).permute(0, 3, 1, 2)
+    _, zero = _workspace(x.device, 1)
+    d = _DESC_T()
+    d[:21] = [x.data_ptr(), w.data_ptr(), zero.data_ptr(), y.data_ptr(), _lib.ptr(b) or 0,
+              _lib.ptr(residual) or 0, Cin, Cout, N, OH, OW, IH, IW, KH, KW, st, pd, dl, Cout, Cin, int(relu)]
+    _lib.call("mx_conv_fwd", d, _lib.stream())
+    return y
 
 
 def dgrad_supported(w: torch.Tensor, x_shape, stride) -> bool:

@@ -65,6 +65,61 @@ class BiasActFn(torch.autograd.Function):
         return dy, db, (dy if ctx.has_res else None), None
 
 
+def _bias_act_bwd(g, out, relu: bool, want_db: bool):
+    """(dy, db) of y = act(conv + b (+ res)): the ReLU mask and the bias-gradient column sums
+    in one pass (csrc/epilogue.hip)."""
+    if not _nhwc(g):
+        g = g.contiguous(memory_format=torch.channels_last)
+    if not relu and not want_db:
+        return g, None
+    M, C = _rows_cols(g)
+    dy = torch.empty_like(g) if relu else g
+    db = torch.empty(C, dtype=torch.bfloat16, device=g.device) if want_db else None
+    nparts = _lib.query("mx_bias_act_bwd_parts", M, C)
+    partial = torch.empty(nparts * C, dtype=torch.float32, device=g.device) if want_db else None
+    _lib.call("mx_bias_act_bwd", _lib.ptr(g), _lib.ptr(out), _lib.ptr(dy), _lib.ptr(db), _lib.ptr(partial),
+              M, C, int(relu), 0, _lib.stream())
+    return dy, db
+
+
+class ConvBiasActFn(torch.autograd.Function):
+    """act(conv2d(x, w) + b (+ res)) with every direction on csrc/convwg.hip where it tiles:
+    forward = one implicit-GEMM launch with the epilogue fused; backward = the ReLU mask +
+    bias-gradient pass, then the implicit-GEMM input and weight gradients."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, res, relu: bool, stride, padding, dilation):
+        y = convwg.conv_fwd(x, w, b, res, relu, stride, padding, dilation)
+        ctx.conf = (list(convwg._pair(stride)), list(convwg._pair(padding)), list(convwg._pair(dilation)))
+        ctx.relu, ctx.has_res = relu, res is not None
+        ctx.bdtype = b.dtype if b is not None else None
+        ctx.save_for_backward(x, w, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, out = ctx.saved_tensors
+        st, pd, dl = ctx.conf
+        want_db = ctx.needs_input_grad[2]
+        dy, db = _bias_act_bwd(g, out, ctx.relu, want_db)
+        if db is not None and db.dtype != ctx.bdtype:
+            db = db.to(ctx.bdtype)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if convwg.dgrad_supported(w, tuple(x.shape), st):
+                dx = convwg.conv_dgrad(dy, w, tuple(x.shape), st, pd, dl)
+            else:
+                dx = torch.ops.aten.convolution_backward(dy, x, w, None, st, pd, dl, False, [0, 0], 1,
+                                                         [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            if w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0:
+                dw = convwg.conv_wgrad(dy, x, tuple(w.shape), st, pd, dl)
+            else:
+                dw = torch.ops.aten.convolution_backward(dy, x, w, None, st, pd, dl, False, [0, 0], 1,
+                                                         [False, True, False])[1]
+        return dx, dw, db, (dy if ctx.has_res else None), None, None, None, None
+
+
 def _fused_ok(y, b, residual) -> bool:
     return (_ENABLED and y.is_cuda and y.dtype == torch.bfloat16 and _nhwc(y) and _nhwc(residual)
             and y.shape[1] % 8 == 0 and y.shape[1] <= 2048
@@ -147,6 +202,9 @@ def conv_bias_act(x, w, b=None, stride=1, padding=0, dilation=1, relu: bool = Fa
         if (_GEMM_1X1 and w.shape[2] == 1 and w.shape[3] == 1 and _as_int(stride) == 1 and _as_int(padding) == 0
                 and w.dtype == x.dtype):
             return bias_act(conv1x1_gemm(x, w), b, residual, relu)
+        if convwg.fwd_supported(x, w, b, residual, stride, padding, dilation):
+            # forward, input and weight gradients all implicit GEMMs (ops/convwg.py)
+            return ConvBiasActFn.apply(x, w, b, residual, relu, stride, padding, dilation)
         if convwg.supported(x, w, stride, padding, dilation):
             # MIOpen forward / input gradient, implicit-GEMM weight gradient (ops/convwg.py)
             return bias_act(convwg.conv2d_wg(x, w, stride, padding, dilation), b, residual, relu)

@@ -60,10 +60,10 @@ def timeit(fn, it=10, reps=5):
     return a.elapsed_time(b) * 1000 / (it * reps)
 
 
-tot_m = tot_h = tot_dm = tot_dh = 0.0
+tot_m = tot_h = tot_dm = tot_dh = tot_fm = tot_fh = 0.0
 cl = torch.channels_last
 print(f"{'conv':22s} {'N':>3s} {'MIOpen us':>10s} {'convwg us':>10s} {'TF/s mi':>8s} {'TF/s wg':>8s}  splits  maxrel"
-      f"   | dgrad: MIOpen us  convdg us  maxrel")
+      f"   | dgrad: MIOpen us  convdg us  maxrel   | fwd+bias: MIOpen us  convfw us  maxrel")
 for name, Cin, Cout, H, W, k, s, p, cnt in SHAPES:
     n = 64 * N if name.startswith("mask") else N
     x = torch.randn(n, Cin, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
@@ -86,12 +86,21 @@ for name, Cin, Cout, H, W, k, s, p, cnt in SHAPES:
     dtm, dth = timeit(dmi), timeit(dwg)
     dref = dmi()[0].float()
     drel = ((dwg().float() - dref).abs().max() / dref.abs().max()).item()
+    bias = torch.randn(Cout, device="cuda").to(torch.bfloat16)
+    from mxtrain.ops.epilogue import bias_act
+    fmi = lambda: bias_act(torch.nn.functional.conv2d(x, w, None, s, p), bias, None, True)
+    ffw = lambda: convwg.conv_fwd(x, w, bias, None, True, s, p, 1)
+    ftm, fth = timeit(fmi), timeit(ffw)
+    fref = fmi().float()
+    frel = ((ffw().float() - fref).abs().max() / fref.abs().max()).item()
+    tot_fm += cnt * ftm
+    tot_fh += cnt * fth
     print(f"{name:22s} {n:3d} {tm:10.1f} {th:10.1f} {fl / tm / 1e6:8.1f} {fl / th / 1e6:8.1f}  {convwg.plan_splits(T, ntiles):6d}  {rel:.2e}"
-          f"   | {dtm:8.1f} {dth:9.1f}  {drel:.2e}  x{cnt}", flush=True)
+          f"   | {dtm:8.1f} {dth:9.1f}  {drel:.2e}   | {ftm:8.1f} {fth:9.1f}  {frel:.2e}  x{cnt}", flush=True)
     tot_m += cnt * tm
     tot_h += cnt * th
     if not name.startswith(("res3.conv1 s2", "res3.short", "fpn.lat2")):   # inputs without a gradient
         tot_dm += cnt * dtm
         tot_dh += cnt * dth
 print(f"per step (counts): wgrad MIOpen {tot_m:.0f} us, convwg {tot_h:.0f} us; "
-      f"dgrad MIOpen {tot_dm:.0f} us, convdg {tot_dh:.0f} us")
+      f"dgrad MIOpen {tot_dm:.0f} us, convdg {tot_dh:.0f} us; fwd+bias MIOpen {tot_fm:.0f} us, convfw {tot_fh:.0f} us")

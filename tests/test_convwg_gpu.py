@@ -67,17 +67,19 @@ def test_conv_wgrad_accumulates_and_is_deterministic():
     _close(acc.float() - base.float(), _ref(dy, x, (Cout, Cin, k, k), stride, pad, dil))
 
 
-def test_conv_wg_autograd_matches_conv2d():
+@pytest.mark.parametrize("hw", [(20, 24), (64, 64)])   # input gradient: MIOpen / implicit GEMM
+def test_conv_wg_autograd_matches_conv2d(hw):
     """The autograd Function: output and input gradient are MIOpen's (as F.conv2d's, up to
     the solver MIOpen picks per call), the weight gradient matches the fp32 reference."""
     from mxtrain.ops import convwg
     torch.manual_seed(0)
     cl = torch.channels_last
-    x = torch.randn(2, 128, 20, 24, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    x = torch.randn(2, 128, *hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
     w = (torch.randn(256, 3, 3, 128, device="cuda") * 0.05).to(torch.bfloat16).permute(0, 3, 1, 2)
     x1, w1 = x.clone().requires_grad_(), w.detach().clone(memory_format=cl).requires_grad_()
     x2, w2 = x.clone().requires_grad_(), w.detach().clone(memory_format=cl).requires_grad_()
     assert convwg.supported(x1, w1, 1, 1, 1)
+    assert convwg.dgrad_supported(w1, tuple(x.shape), 1) == (hw == (64, 64))
     y1 = convwg.conv2d_wg(x1, w1, 1, 1, 1)
     y2 = torch.nn.functional.conv2d(x2, w2, None, 1, 1, 1)
     _close(y1.detach(), y2.detach().float().cpu())
@@ -106,3 +108,64 @@ def test_conv_dgrad_matches_fp32(case):
     torch.cuda.synchronize()
     assert dx.is_contiguous(memory_format=torch.channels_last)
     _close(dx, _ref_dx(dy, w, tuple(x.shape), stride, pad, dil))
+
+
+@pytest.mark.parametrize("case", [(1, 64, 256, 40, 48, 1, 1, 0, 1), (2, 128, 128, 25, 42, 3, 1, 1, 1),
+                                  (1, 256, 128, 50, 60, 1, 2, 0, 1), (1, 128, 256, 30, 33, 3, 1, 2, 2)])
+@pytest.mark.parametrize("res", [False, True])
+def test_conv_fwd_fused_epilogue_matches_fp32(case, res):
+    from mxtrain.ops import convwg
+    N, Cin, Cout, H, W, k, stride, pad, dil = case
+    x, dy = _inputs(*case, seed=5)
+    g = torch.Generator().manual_seed(13)
+    w = (torch.randn(Cout, k, k, Cin, generator=g) * 0.1).to(torch.bfloat16).cuda().permute(0, 3, 1, 2)
+    b = torch.randn(Cout, generator=g).to(torch.bfloat16).cuda()
+    r = torch.randn(dy.shape, generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=torch.channels_last) \
+        if res else None
+    y = convwg.conv_fwd(x, w, b, r, True, stride, pad, dil)
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.conv2d(x.float().cpu(), w.float().cpu(), b.float().cpu(), stride, pad, dil)
+    if res:
+        ref = ref + r.float().cpu()
+    ref = ref.relu()
+    assert y.is_contiguous(memory_format=torch.channels_last) and y.shape == ref.shape
+    _close(y, ref)
+
+
+def test_conv_bias_act_all_implicit_gemm_matches_fp32():
+    """ops.epilogue.conv_bias_act on the fully implicit-GEMM path (forward with the fused
+    epilogue, ReLU-mask + bias gradient, input and weight gradients) against the same
+    function in fp32 on the CPU."""
+    from mxtrain.ops import convwg
+    from mxtrain.ops.epilogue import conv_bias_act
+    fwd0, convwg.FWD = convwg.FWD, True
+    try:
+        _fused_path_case(convwg, conv_bias_act)
+    finally:
+        convwg.FWD = fwd0
+
+
+def _fused_path_case(convwg, conv_bias_act):
+    torch.manual_seed(1)
+    cl = torch.channels_last
+    x = torch.randn(2, 128, 64, 64).to(torch.bfloat16)
+    w = (torch.randn(256, 128, 3, 3) * 0.05).to(torch.bfloat16)
+    b = (torch.randn(256) * 0.1).to(torch.bfloat16)
+    r = torch.randn(2, 256, 64, 64).to(torch.bfloat16)
+    g = torch.randn(2, 256, 64, 64).to(torch.bfloat16)
+    xg = x.cuda().contiguous(memory_format=cl).requires_grad_()
+    wg = w.cuda().contiguous(memory_format=cl).requires_grad_()
+    bg = b.cuda().requires_grad_()
+    rg = r.cuda().contiguous(memory_format=cl).requires_grad_()
+    assert convwg.fwd_supported(xg, wg, bg, rg, 1, 1, 1) and convwg.dgrad_supported(wg, tuple(xg.shape), 1)
+    y = conv_bias_act(xg, wg, bg, 1, 1, 1, relu=True, residual=rg)
+    y.backward(g.cuda().contiguous(memory_format=cl))
+    yc = torch.relu(torch.nn.functional.conv2d(x.float(), w.float(), b.float(), 1, 1) + r.float())
+    _close(y.detach(), yc)
+    # backward against fp32 with the ReLU mask of the bf16 forward (pre-activations near
+    # zero may take the other side of the mask in fp32)
+    dy = g.float() * (y.detach().float().cpu() > 0)
+    dx, dw, _ = torch.ops.aten.convolution_backward(dy, x.float(), w.float(), None, [1, 1], [1, 1], [1, 1], False,
+                                                    [0, 0], 1, [True, True, False])
+    for got, ref in ((xg.grad, dx), (wg.grad, dw), (bg.grad, dy.sum((0, 2, 3))), (rg.grad, dy)):
+        _close(got, ref)
