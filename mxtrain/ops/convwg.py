@@ -24,7 +24,7 @@ from . import _lib
 
 ENABLED = True          # module switch (A/B runs: scripts/conv_wgrad_bench.py)
 DGRAD = True            # input gradient from csrc/convwg.hip too (else MIOpen's backward-data)
-FWD = False             # forward with the fused bias / residual / ReLU epilogue (else MIOpen); off until measured in the step
+FWD = True              # forward with the fused bias / residual / ReLU epilogue (else MIOpen)
 FWD_MIN_TILES = 64
 TARGET_WGS = 512        # two 128 x 128 workgroups per CU on 256 CUs
 MIN_STEPS = 8
