@@ -210,7 +210,10 @@ def _collect(save_dir: str, trainer, iteration: int, consumed_samples: int, args
             "ds_config": ds_config or {}, "ds_version": DS_VERSION, "args": args or {},
             "iteration": iteration, "checkpoint_version": 3.0,
             "rng_state": [{"torch_rng_state": torch.get_rng_state(),
-                           "mx_dropout_seed": trainer.seed.t.detach()}],
+                           # cloned on the current stream: an async snapshot's side-stream
+                           # copy would otherwise read the live seed after the next step's
+                           # advance (the rest of the state is fenced before the optimizer)
+                           "mx_dropout_seed": trainer.seed.t.detach().clone()}],
             "mx_config": trainer.cfg.__dict__.copy(),
         }
         files.append((os.path.join(d, f"mp_rank_{mp:02d}_model_states.pt"), state))
@@ -360,11 +363,21 @@ class AsyncCheckpointer:
             return
         self._thread.join()
         self._thread = None
-        if self._err is not None:
-            err, self._err = self._err, None
-            raise RuntimeError(f"async checkpoint write failed: {err!r}") from err
+        err, self._err = self._err, None
         save_dir, iteration, leader = self._commit_args
         self._commit_args = None
+        # every rank learns whether ANY rank's write failed before the collective commit:
+        # a rank that raised alone would leave the others blocked in _commit's barrier
+        ok = err is None
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            dev = self.device if dist.get_backend() == "nccl" else torch.device("cpu")
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            ok = bool(int(flag.item()))
+        if err is not None:
+            raise RuntimeError(f"async checkpoint write failed: {err!r}") from err
+        if not ok:
+            raise RuntimeError(f"async checkpoint write of global_step{iteration} failed on another rank")
         _commit(save_dir, iteration, leader)
 
 

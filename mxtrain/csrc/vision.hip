@@ -1112,13 +1112,18 @@ __global__ __launch_bounds__(1024) void topk_rows_kernel(const float* __restrict
       off += x2 < w ? wc[x2] : 0;
       tot += wc[x2];
     }
+    // ngt is read BETWEEN the two barriers: every add of this chunk happened before the
+    // first one, and no wave can add for the next chunk before all have passed the second,
+    // so every wave sees the same count and takes the same exit (a read after the second
+    // barrier could race a fast wave's next-chunk atomicAdd and split the waves' exits)
+    const int ngt_now = ngt;
     if (eq) {
       const int re = eq_base + off + __popcll(bq & below);
       if (re < need_eq) cand[n_gt + re] = ((unsigned long long)key << 32) | (uint32_t)(~(uint32_t)e);
     }
     eq_base += tot;
     __syncthreads();
-    if (eq_base >= need_eq && ngt >= n_gt) break;   // (uniform: shared values after the barrier)
+    if (eq_base >= need_eq && ngt_now >= n_gt) break;   // uniform: wc and ngt_now are per-chunk snapshots
   }
   int P = 1;
   while (P < k) P <<= 1;

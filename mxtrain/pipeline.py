@@ -575,7 +575,13 @@ class Scheduler:
                 continue
             active = [r for r in d.get("runs", []) if run_active(r)]
             if len(active) >= int(d.get("max_concurrency", 1)):
-                continue     # at the concurrency limit: this period is skipped
+                # at the concurrency limit: this period is skipped (not delayed), so the
+                # next fire is a full period from now, as for a fired run
+                d = get_recurring_run(d["name"])
+                d["last_fire"] = now
+                d["skipped"] = int(d.get("skipped", 0)) + 1
+                _write_recurring(d)
+                continue
             run = f"{d['name']}-{time.strftime('%Y%m%d-%H%M%S', time.localtime(now))}-{len(d.get('runs', []))}"
             self.submit(pipeline=d["pipeline"], run_name=run, cache=bool(d.get("cache")), recurring=d["name"])
             d = get_recurring_run(d["name"])

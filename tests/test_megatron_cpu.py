@@ -275,3 +275,56 @@ def test_gpu_sampler_fake_sysfs(tmp_path):
     assert out["gpu_samples"] >= 3 and out["gpu_power_w_max"] == 950.0
     assert 750.0 <= out["gpu_power_w_mean"] <= 950.0 and out["gpu_sclk_mhz_mean"] == 2400.0
     assert GPUSampler(None).take() == {}
+
+
+def _async_fail_worker(rank, world, port, root, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mxtrain.checkpoint import AsyncCheckpointer
+
+        class _T:   # the writer path only needs .device / .trainer
+            device = torch.device("cpu")
+
+        ck = AsyncCheckpointer(_T())
+        good = os.path.join(root, f"r{rank}.pt")
+        bad = os.path.join(root, "notadir", f"r{rank}.pt")   # parent is a file: open() fails
+        path = bad if rank == 1 else good
+        ck._commit_args = (root, 3, rank == 0)
+        ck._err = None
+        import threading
+        ck._thread = threading.Thread(target=ck._write, args=([(path, {"x": torch.ones(2)})], None))
+        ck._thread.start()
+        try:
+            ck.wait()
+            q.put((rank, "no-error"))
+        except RuntimeError as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_async_write_failure_raises_on_every_rank(tmp_path):
+    """one rank's failed background write must fail the save on EVERY rank
+    (an all-reduced error flag before the commit barrier), not leave the others blocked in
+    _commit; `latest` is not advanced."""
+    import socket
+    import torch.multiprocessing as mp
+    (tmp_path / "notadir").write_text("x")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_async_fail_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = dict(q.get(timeout=5) for _ in range(2))
+    assert "failed" in res[0] and "another rank" in res[0]
+    assert "failed" in res[1] and "another rank" not in res[1]
+    assert not (tmp_path / "latest").exists()

@@ -498,6 +498,9 @@ def test_recurring_runs_schedule_concurrency_and_api(home):
     pl.terminate_run(run)
     pl.wait_run(run, timeout=60)
     assert pl.get_run(run)["recurring_run"] == "slow-rr"
+    # the blocked period was SKIPPED, not delayed: the next fire is a period after the skip
+    assert pl.get_recurring_run("slow-rr")["skipped"] == 1
+    assert real.tick(t1 + 5.5) == []
     assert len(real.tick(t1 + 10)) == 1                    # free again
     for r in pl.get_recurring_run("slow-rr")["runs"]:
         pl.terminate_run(r)

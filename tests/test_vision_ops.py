@@ -332,3 +332,30 @@ def test_topk_rows_matches_torch(R, n, k, largest):
         # equal values: lower index first
         same = v[r, 1:] == v[r, :-1]
         assert bool((i[r, 1:][same] > i[r, :-1][same]).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k", [(8192, 100), (16384, 1000), (4100, 64)])
+def test_topk_rows_ties_early_larger_keys_late(n, k):
+    """The exit race of topk_rows_kernel's candidate scan: the threshold ties
+    fill in the FIRST 1024-element chunk while every key above the threshold sits in later
+    chunks, so the scan must keep going after the ties are complete and all waves must
+    leave on the same chunk."""
+    from mxtrain.ops.vision import topk_rows
+    R = 6
+    x = torch.zeros(R, n, device="cuda")
+    x[:, : 2 * k] = 0.5                                # ties: threshold value, chunk 0 only
+    n_gt = k // 2
+    late = torch.linspace(1024, n - 1, n_gt, device="cuda").long()
+    for r in range(R):
+        x[r, late] = 1.0 + torch.arange(n_gt, device="cuda", dtype=torch.float32) / n_gt + r
+    for _ in range(20):                                 # exercise many wave interleavings
+        v, i = topk_rows(x, k, largest=True)
+        rv, ri = x.topk(k, dim=1, largest=True)
+        torch.cuda.synchronize()
+        assert torch.equal(v, rv)
+        assert torch.equal(torch.gather(x, 1, i), v)
+        for r in range(R):
+            assert i[r].unique().numel() == k
+            # the tied part is the lowest indices, in order
+            assert torch.equal(i[r, n_gt:].sort().values, torch.arange(k - n_gt, device="cuda"))
