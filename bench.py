@@ -13,19 +13,25 @@ weights (no dataset / checkpoint on the box).
 
 Rank 0 prints exactly one JSON line (value = whole-job tokens/s, max step time over ranks).
 
-On one GPU the line also carries the second half of BASELINE.json's metric, Mask R-CNN
-R50-FPN training images/s at the reference's two configs (tensorpack: 1 img/GPU,
-examples/maskrcnn/train-maskrcnn-tensorpack.yaml:16-35; aws-samples: 4 img/GPU,
+The line also carries the second half of BASELINE.json's metric, Mask R-CNN R50-FPN
+training images/s (whole job, the same N GPUs) at the reference's two configs (tensorpack:
+1 img/GPU, examples/maskrcnn/train-maskrcnn-tensorpack.yaml:16-35; aws-samples: 4 img/GPU,
 examples/maskrcnn/train-maskrcnn-aws.yaml:29), measured after the GPT window by
-scripts/bench_maskrcnn.py in a child process (synthetic COCO-shaped 800 x <=1333 images,
-random-init weights, full training step incl. SGD; the in-repo MIOpen find-db skips the
-conv search).  --no-maskrcnn skips it.
+scripts/bench_maskrcnn.py: every bench rank starts one child rank, so at N > 1 the children
+are an N-rank data-parallel job (synthetic COCO-shaped 800 x <=1333 images, random-init
+weights, full training step incl. SGD; the in-repo MIOpen find-db skips the conv search).
+--no-maskrcnn skips it.
+
+Both steps are whole-step hipGraph replays at every N: at N > 1 the captured GPT step holds
+its ZeRO-1 reduce-scatter / all-gather, and the Mask R-CNN step its bucketed gradient
+all-reduces (RCCL over xGMI by default; --xgmi selects the direct peer-to-peer kernels).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shlex
 import sys
 import time
 
@@ -46,26 +52,71 @@ def _coll_summary(tr):
     return out
 
 
-def run_maskrcnn(batch: int, steps: int, warmup: int, timeout: float = 420.0) -> dict:
-    """One Mask R-CNN training throughput run (child process) -> {"img_s": .., ...}."""
+def _child_env(world: int, rank: int, port: int) -> dict:
+    """Environment of a Mask R-CNN child rank: the parent's rank / local rank, a NEW
+    rendezvous (own port, own TCPStore hosted by child rank 0).  torchrun's agent-store
+    variables are dropped: with TORCHELASTIC_USE_AGENT_STORE the child would wait for an
+    agent store on the new port that nobody hosts."""
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    for k in ("GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE", "GROUP_WORLD_SIZE", "ROLE_NAME"):
+        env.pop(k, None)
+    if world > 1:
+        env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                   LOCAL_RANK=os.environ.get("LOCAL_RANK", str(rank)),
+                   LOCAL_WORLD_SIZE=os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    else:
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+            env.pop(k, None)
+    return env
+
+
+def run_maskrcnn(batch: int, steps: int, warmup: int, world: int = 1, rank: int = 0, port: int = 0,
+                 extra=(), workers: int = 6, timeout: float = 600.0) -> dict:
+    """One Mask R-CNN training throughput run -> {"img_s": .., ...} (rank 0) / {"rc": 0} (others).
+
+    Every bench rank starts ONE child process (``scripts/bench_maskrcnn.py``) with its own
+    rank, so at N > 1 the children form an N-rank data-parallel job (fresh rendezvous on
+    ``port``) -- the reference's Horovod MPIJob shape, one rank per GPU
+    (examples/maskrcnn/train-maskrcnn-tensorpack.yaml:7,34).  A child, never an exec: this
+    process has initialised the GPU.  The whole-job images/s comes from child rank 0."""
     import subprocess
     import tempfile
     here = os.path.dirname(os.path.abspath(__file__))
-    out = tempfile.mktemp(prefix="mx_mrcnn_", suffix=".jsonl")
+    out = tempfile.mktemp(prefix=f"mx_mrcnn_r{rank}_", suffix=".jsonl")
     cmd = [sys.executable, os.path.join(here, "scripts", "bench_maskrcnn.py"), "--batch", str(batch),
-           "--steps", str(steps), "--warmup", str(warmup), "--out", out]
+           "--steps", str(steps), "--warmup", str(warmup), "--out", out, "--workers", str(workers)] + list(extra)
     t0 = time.time()
     try:
-        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout)
-        rec = json.loads(open(out).read().splitlines()[-1]) if r.returncode == 0 and os.path.exists(out) else None
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout,
+                           env=_child_env(world, rank, port))
+        if r.returncode != 0:
+            return {"error": f"rank {rank} rc={r.returncode}: " + r.stdout[-400:]}
+        if rank != 0:
+            return {"rc": 0}
+        rec = json.loads(open(out).read().splitlines()[-1]) if os.path.exists(out) else None
         if rec is None:
-            return {"error": f"rc={r.returncode}: " + r.stdout[-300:]}
-        return {"img_s": rec["value"], "steps": steps, "warmup": warmup, "wall_s": round(time.time() - t0, 1)}
+            return {"error": "no result record: " + r.stdout[-300:]}
+        res = {"img_s": rec["value"], "n_gpus": rec.get("n_gpus", world), "steps": steps, "warmup": warmup,
+               "wall_s": round(time.time() - t0, 1)}
+        if rec.get("graph"):
+            res["hipgraph"] = {k: rec["graph"][k] for k in ("captures", "replays", "eager")}
+        if rec.get("dp_routes"):
+            res["dp_routes"] = rec["dp_routes"]
+        return res
     except Exception as e:  # noqa: BLE001 -- the GPT number must still be reported
-        return {"error": repr(e)[:300]}
+        return {"error": f"rank {rank}: " + repr(e)[:300]}
     finally:
         if os.path.exists(out):
             os.remove(out)
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
 def main():
@@ -86,26 +137,28 @@ def main():
     ap.add_argument("--num-experts", type=int, default=0, help="MoE: experts per MoE layer (every 2nd layer)")
     ap.add_argument("--ep", type=int, default=1, help="MoE expert-parallel size")
     ap.add_argument("--topk", type=int, default=1)
-    ap.add_argument("--no-graph", action="store_true", help="disable hipGraph step capture")
-    ap.add_argument("--graph", action="store_true",
-                    help="capture the step in a hipGraph also when N > 1 (default: single GPU only; "
-                         "eager and graph steps measure the same on MI355X, the step is GPU-bound)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="disable hipGraph step capture (default: the whole step, its ZeRO-1 "
+                         "reduce-scatter / all-gather included, is one graph at every N)")
     ap.add_argument("--no-overlap", action="store_true")
-    ap.add_argument("--overlap-optimizer", action="store_true",
-                    help="defer each step's AdamW per bucket into the next step's forward on a side "
-                         "stream (default: AdamW at the end of the step)")
     ap.add_argument("--no-tuned-gemm", action="store_true",
                     help="do not load the checked-in TunableOp GEMM solution tables")
     ap.add_argument("--tune-gemm", action="store_true",
                     help="TunableOp: benchmark every GEMM solution during warmup and write the table "
                          "to $PYTORCH_TUNABLEOP_FILENAME (see scripts/tune_gemms.sh)")
-    ap.add_argument("--wgrad-stream", action="store_true",
-                    help="run weight-gradient GEMMs on a concurrent side stream")
     ap.add_argument("--no-fused-linear", action="store_true",
                     help="hipBLASLt for the Linear forward / dgrad GEMMs + separate bias-GeLU kernels "
                          "(default: csrc/gemm_nt.hip with fused epilogues)")
     ap.add_argument("--no-maskrcnn", action="store_true",
-                    help="skip the Mask R-CNN images/s measurements (run on one GPU only)")
+                    help="skip the Mask R-CNN images/s measurements")
+    ap.add_argument("--maskrcnn-batches", default="1,4",
+                    help="images per GPU of the Mask R-CNN runs (tensorpack 1, aws-samples 4)")
+    ap.add_argument("--maskrcnn-steps", default="60:15,40:10",
+                    help="timed:warmup steps per Mask R-CNN run (one pair per batch)")
+    ap.add_argument("--maskrcnn-workers", type=int, default=6)
+    ap.add_argument("--maskrcnn-args", default="",
+                    help="extra arguments for scripts/bench_maskrcnn.py, one shell-quoted string "
+                         "(tests: a small synthetic set and image size on the CPU)")
     ap.add_argument("--xgmi", choices=["0", "1", "auto"], default="0",
                     help="direct xGMI peer-to-peer collectives (csrc/comm/xgmi.hip) for the DP "
                          "reduce-scatter / all-gather and TP all-reduce: 0 = RCCL only (default: the "
@@ -149,8 +202,7 @@ def main():
     cfg = GPTConfig(**mcfg)
     tcfg = TrainConfig(micro_batch_size=args.micro_batch_size, global_batch_size=args.global_batch_size,
                        overlap_grad_reduce=not args.no_overlap, lr_warmup_iters=0,
-                       wgrad_stream=args.wgrad_stream, moe_expert_parallel_size=args.ep,
-                       overlap_optimizer=args.overlap_optimizer, fused_linear=not args.no_fused_linear)
+                       moe_expert_parallel_size=args.ep, fused_linear=not args.no_fused_linear)
     tr = GPTTrainer(cfg, tcfg, ps)
     gen = torch.Generator().manual_seed(1 + ps.dp_rank)
     tokens, labels = synthetic_batch(cfg, tr.num_micro, args.micro_batch_size, ps.device, gen)
@@ -159,7 +211,7 @@ def main():
         if world > 1:
             dist.barrier()
 
-    use_graph = not args.no_graph and (world == 1 or args.graph)
+    use_graph = not args.no_graph and torch.cuda.is_available()
     graph_err = None
     for _ in range(args.warmup):
         tr.train_step(tokens, labels)
@@ -189,8 +241,6 @@ def main():
     loss = None
     for _ in range(args.steps):
         loss = tr.train_step(tokens, labels)
-    # a deferred AdamW (overlap_optimizer) of the last step is applied inside the timed
-    # window too: K + 1 optimizer updates are timed for K steps
     tr.sync_params()
     _sync()
     barrier()
@@ -232,8 +282,7 @@ def main():
                 "hidden_dropout": cfg.hidden_dropout,
                 "attention_dropout": cfg.attention_dropout,
                 "hipgraph": use_graph,
-                "wgrad_stream": args.wgrad_stream,
-                "optimizer": "adamw_deferred_overlapped" if tr.opt.overlap_update else "adamw",
+                "optimizer": "adamw",
                 "tuned_gemm_tables": n_tables,
                 "collectives": _coll_summary(tr),
                 "fused_linear": not args.no_fused_linear,
@@ -246,22 +295,49 @@ def main():
             out["graph_error"] = graph_err
         if use_graph and getattr(tr, "graph_census", None):
             out["graph_nodes"] = tr.graph_census
-        if world == 1 and not args.no_maskrcnn:
-            # BASELINE.json metric, part 2: Mask R-CNN images/s (outside the GPT timed window)
-            del tr
-            if torch.cuda.is_available():
-                torch.cuda.empty_cache()
-            m1 = run_maskrcnn(1, 60, 15)
-            m4 = run_maskrcnn(4, 40, 10)
-            out["maskrcnn_img_s_1img"] = m1.get("img_s")
-            out["maskrcnn_img_s_4img"] = m4.get("img_s")
+    else:
+        out = None
+    if not args.no_maskrcnn:
+        # BASELINE.json metric, part 2: Mask R-CNN images/s with the same N GPUs, outside
+        # the GPT timed window.  The GPT model is freed first; every rank then runs one child.
+        del tr, tokens, labels
+        import gc
+        gc.collect()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        batches = [int(b) for b in args.maskrcnn_batches.split(",") if b]
+        sw = [tuple(int(v) for v in p.split(":")) for p in args.maskrcnn_steps.split(",")]
+        ports = [_free_port() for _ in batches] if ps.rank == 0 else None
+        if world > 1:
+            box = [ports]
+            dist.broadcast_object_list(box, src=0)
+            ports = box[0]
+        res = {}
+        for i, b in enumerate(batches):
+            st, wu = sw[min(i, len(sw) - 1)]
+            res[b] = run_maskrcnn(b, st, wu, world=world, rank=ps.rank, port=ports[i],
+                                  extra=shlex.split(args.maskrcnn_args), workers=args.maskrcnn_workers)
+            if "error" in res[b]:
+                print(f"maskrcnn {b} img/GPU: {res[b]['error']}", file=sys.stderr, flush=True)
+        if world > 1:   # a failed child on any rank is reported by rank 0
+            errs = [None] * world
+            dist.all_gather_object(errs, {b: r.get("error") for b, r in res.items() if r.get("error")})
+            for r_, e in enumerate(errs):
+                for b, msg in (e or {}).items():
+                    if ps.rank == 0 and "error" not in res[b]:
+                        res[b] = {"error": msg}
+        if out is not None:
+            for b in batches:
+                out[f"maskrcnn_img_s_{b}img"] = res[b].get("img_s")
             out["maskrcnn_config"] = {
-                "model": "Mask R-CNN R50-FPN (tensorpack layout)", "n_gpus": 1, "dtype": "bf16",
-                "data": "synthetic COCO-shaped 800x<=1333, random-init weights",
-                "1img": {k: v for k, v in m1.items() if k != "img_s"},
-                "4img": {k: v for k, v in m4.items() if k != "img_s"},
-                "unit": "images/s", "conv_search": "MIOpen find (in-repo find-db)",
-                "step": "whole-step hipGraph replay (1 GPU), runtime packet capture on, memset nodes as fill kernels"}
+                "model": "Mask R-CNN R50-FPN (tensorpack layout)", "n_gpus": world, "dtype": "bf16",
+                "data": "synthetic COCO-shaped 800x<=1333, random-init weights", "unit": "images/s (whole job)",
+                "parallelism": f"dp{world} (one child rank per GPU, bucketed gradient all-reduce)",
+                "conv_search": "MIOpen find (in-repo find-db) + implicit-GEMM HIP convolutions",
+                "step": "whole-step hipGraph replay (gradient all-reduces captured at N > 1)",
+                **{f"{b}img": {k: v for k, v in res[b].items() if k != "img_s"} for b in batches}}
+    if out is not None:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     uint16_t* __restrict__ y,              // [rows, cols]
     float* __restrict__ mean_out, float* __restrict__ rstd_out,
     int rows, int cols, float eps, uint32_t thresh, float keep_scale,
-    const uint32_t* __restrict__ seed_ptr, uint32_t salt) {
+    const uint32_t* __restrict__ seed_ptr, uint32_t salt, uint64_t elem0) {
   const int lane = threadIdx.x & 63;
   const int row = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (row >= rows) return;
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
       unpack8(and4(br[i], bm), b);
       unpack8(and4(rr[i], rmk), r);
       bool km[8];
-      if (thresh) dropout_keep8(base + c, seed, thresh, km);
+      if (thresh) dropout_keep8(elem0 + base + c, seed, thresh, km);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float t = v[i][j] + b[j];
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const float* __restrict__ rstd_in, const uint16_t* __restrict__ gamma,
     uint16_t* __restrict__ dh_out, uint16_t* __restrict__ dx_drop,
     float* __restrict__ partial, int rows, int cols, uint32_t thresh, float keep_scale,
-    const uint32_t* __restrict__ seed_ptr, uint32_t salt) {
+    const uint32_t* __restrict__ seed_ptr, uint32_t salt, uint64_t elem0) {
   extern __shared__ __attribute__((aligned(16))) float slab[];  // [3][cols]
   if constexpr (!REG && COLS) {  // REG: [4 waves][3][cols] slabs, fully overwritten -> no zeroing
     for (int i = threadIdx.x; i < 3 * cols; i += blockDim.x) slab[i] = 0.f;
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         if (dx_drop) {
           float dx[8];
           bool km[8];
-          if (thresh) dropout_keep8(base + c, seed, thresh, km);
+          if (thresh) dropout_keep8(elem0 + base + c, seed, thresh, km);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             float t = o[j];
@@ -463,7 +463,7 @@ template <bool RMS, bool BDA>
 hipError_t launch_fwd(const void* x, const void* bias, const void* residual,
                       const void* gamma, const void* beta, void* h_out, void* y,
                       float* mean, float* rstd, int rows, int cols, float eps,
-                      float p, const uint32_t* seed, uint32_t salt, hipStream_t s) {
+                      float p, const uint32_t* seed, uint32_t salt, uint64_t elem0, hipStream_t s) {
   if (cols < 8 || cols % 8 || rows <= 0) return hipErrorInvalidValue;  // 16-B row vectors
   const int nv = (cols + 511) / 512;
   const uint32_t thresh = p > 0.f ? (uint32_t)((double)p * 4294967296.0) : 0u;
@@ -475,7 +475,7 @@ hipError_t launch_fwd(const void* x, const void* bias, const void* residual,
                        (const uint16_t*)x, (const uint16_t*)bias,                      \
                        (const uint16_t*)residual, (const uint16_t*)gamma,              \
                        (const uint16_t*)beta, (uint16_t*)h_out, (uint16_t*)y, mean,    \
-                       rstd, rows, cols, eps, thresh, ks, seed, salt);                 \
+                       rstd, rows, cols, eps, thresh, ks, seed, salt, elem0);          \
     break;
   switch (nv) {
     MX_LN_CASE(1) MX_LN_CASE(2) MX_LN_CASE(3) MX_LN_CASE(4) MX_LN_CASE(5)
@@ -548,7 +548,7 @@ template <bool RMS>
 hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const float* mean,
                       const float* rstd, const void* gamma, void* dh_out, void* dx_drop,
                       float* partial, int rows, int cols, float p, const uint32_t* seed,
-                      uint32_t salt, hipStream_t s) {
+                      uint32_t salt, uint64_t elem0, hipStream_t s) {
   if (cols < 8 || cols % 8 || rows <= 0) return hipErrorInvalidValue;  // 16-B row vectors
   const int nv = (cols + 511) / 512;
   const uint32_t thresh = p > 0.f ? (uint32_t)((double)p * 4294967296.0) : 0u;
@@ -562,7 +562,7 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
                        (const uint16_t*)dy, (const uint16_t*)dres, (const uint16_t*)h, \
                        mean, rstd, (const uint16_t*)gamma, (uint16_t*)dh_out,          \
                        (uint16_t*)dx_drop, partial, rows, cols, thresh, ks, seed,      \
-                       salt);                                                          \
+                       salt, elem0);                                                   \
     break;
     switch (nv) {
       MX_LNB_SPLIT(1) MX_LNB_SPLIT(2) MX_LNB_SPLIT(3) MX_LNB_SPLIT(4)
@@ -586,7 +586,7 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
                        (const uint16_t*)dy, (const uint16_t*)dres, (const uint16_t*)h, \
                        mean, rstd, (const uint16_t*)gamma, (uint16_t*)dh_out,          \
                        (uint16_t*)dx_drop, partial, rows, cols, thresh, ks, seed,      \
-                       salt);                                                          \
+                       salt, elem0);                                                   \
     break;
   switch (nv) {
     MX_LNB_CASE(1) MX_LNB_CASE(2) MX_LNB_CASE(3) MX_LNB_CASE(4) MX_LNB_CASE(5)
@@ -634,37 +634,40 @@ MX_EXPORT int mx_layernorm_fwd(const void* x, const void* gamma, const void* bet
                                float* mean, float* rstd, int rows, int cols, float eps,
                                hipStream_t s) {
   return launch_fwd<false, false>(x, nullptr, nullptr, gamma, beta, nullptr, y, mean, rstd,
-                                  rows, cols, eps, 0.f, nullptr, 0, s);
+                                  rows, cols, eps, 0.f, nullptr, 0, 0, s);
 }
 
 MX_EXPORT int mx_rmsnorm_fwd(const void* x, const void* gamma, void* y, float* rstd,
                              int rows, int cols, float eps, hipStream_t s) {
   return launch_fwd<true, false>(x, nullptr, nullptr, gamma, nullptr, nullptr, y, nullptr,
-                                 rstd, rows, cols, eps, 0.f, nullptr, 0, s);
+                                 rstd, rows, cols, eps, 0.f, nullptr, 0, 0, s);
 }
 
 // h_out = residual + dropout(x + bias);  y = LayerNorm(h_out)   (RMS: RMSNorm)
+// elem0: flat index of element [0, 0] in the full (unsharded) activation -- the dropout
+// mask is keyed on the GLOBAL element index, so a sequence-parallel shard draws exactly
+// the bits of the same rows of the unsharded tensor
 MX_EXPORT int mx_bda_norm_fwd(const void* x, const void* bias, const void* residual,
                               const void* gamma, const void* beta, void* h_out, void* y,
                               float* mean, float* rstd, int rows, int cols, float eps,
-                              float p, const uint32_t* seed, uint32_t salt, int rms,
+                              float p, const uint32_t* seed, uint32_t salt, int64_t elem0, int rms,
                               hipStream_t s) {
   if (rms)
     return launch_fwd<true, true>(x, bias, residual, gamma, nullptr, h_out, y, nullptr,
-                                  rstd, rows, cols, eps, p, seed, salt, s);
+                                  rstd, rows, cols, eps, p, seed, salt, (uint64_t)elem0, s);
   return launch_fwd<false, true>(x, bias, residual, gamma, beta, h_out, y, mean, rstd, rows,
-                                 cols, eps, p, seed, salt, s);
+                                 cols, eps, p, seed, salt, (uint64_t)elem0, s);
 }
 
 MX_EXPORT int mx_norm_bwd(const void* dy, const void* dres, const void* h, const float* mean,
                           const float* rstd, const void* gamma, void* dh_out, void* dx_drop,
                           float* partial, int rows, int cols, float p, const uint32_t* seed,
-                          uint32_t salt, int rms, hipStream_t s) {
+                          uint32_t salt, int64_t elem0, int rms, hipStream_t s) {
   if (rms)
     return launch_bwd<true>(dy, dres, h, mean, rstd, gamma, dh_out, dx_drop, partial, rows,
-                            cols, p, seed, salt, s);
+                            cols, p, seed, salt, (uint64_t)elem0, s);
   return launch_bwd<false>(dy, dres, h, mean, rstd, gamma, dh_out, dx_drop, partial, rows,
-                           cols, p, seed, salt, s);
+                           cols, p, seed, salt, (uint64_t)elem0, s);
 }
 
 // bf16 column sum: `partial` must hold ceil(rows/16)*cols floats plus

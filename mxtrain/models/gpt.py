@@ -128,8 +128,12 @@ GPT_CONFIGS = {
 
 SALT_EMB = 7
 SALT_ATTN = 50000   # + layer index; the attention mask is keyed on GLOBAL heads, so no TP term
-# + micro-batch index x MICRO_SALT: every micro-batch of a step draws fresh dropout masks
-# (Megatron draws a new mask on every call); micro-batch 0 keeps the plain salts
+# + GLOBAL micro-batch index x MICRO_SALT: every micro-batch of a step draws fresh dropout
+# masks (Megatron draws a new mask on every call).  The index is global over data-parallel
+# ranks (dp_rank x micro-batches per step + m) and hidden-dropout masks are keyed on global
+# element indices (sequence-parallel shards offset by their rows), so the masks -- and the
+# whole training trajectory -- do not depend on the DP / TP / SP / PP layout: a DP2 x TP2 x
+# PP2 run draws the bits of the one-GPU run with the same micro-batches
 MICRO_SALT = 0x2545F491
 M32 = 0xFFFFFFFF
 _NORM_PARAMS = ("ln1_w", "ln1_b")
@@ -314,6 +318,7 @@ class StepRuntime:
     dmask_key: Optional[tuple] = None
     batch_dmasks: bool = False    # GPTTrainer turns it on (it resets dmasks when the seed advances)
     micro: int = 0                # micro-batch index within the step (dropout-mask key)
+    micro_base: int = 0           # global index of this rank's first micro-batch of the step
     # forward / dgrad GEMMs of the layer through csrc/gemm_nt.hip with the bias, bias-GeLU
     # and GeLU' + bias-gradient epilogues fused (ops/gemm.py linear_fwd / linear_dgrad);
     # False: hipBLASLt + the separate bias-GeLU kernels (the LM head always uses hipBLASLt)
@@ -387,11 +392,17 @@ class StepRuntime:
 
     def salt(self, base, micro=None):
         m = self.micro if micro is None else micro
-        return (base + (7919 * self.tp_rank if self.sp else 0) + MICRO_SALT * m) & M32
+        return (base + MICRO_SALT * (self.micro_base + m)) & M32
 
     def attn_salt(self, layer, micro=None):
         m = self.micro if micro is None else micro
-        return (SALT_ATTN + layer + MICRO_SALT * m) & M32
+        return (SALT_ATTN + layer + MICRO_SALT * (self.micro_base + m)) & M32
+
+    def elem0(self, rows: int) -> int:
+        """Global flat index of element [0, 0] of this rank's [rows, hidden] activation
+        shard: under sequence parallelism rank r holds rows r*rows.. of the TP group's
+        tokens, so its hidden-dropout mask is that part of the unsharded mask."""
+        return self.tp_rank * rows * self.cfg.hidden_size if self.sp else 0
 
 
 def _gather(x, rt):
@@ -485,7 +496,7 @@ class EmbedFn(torch.autograd.Function):
                 e = C.split_dim0(e, rt.tp_group)
         w, b = rt.norm_params(f"layers.{first_layer}.ln1")
         h, a, mean, rstd = bda_norm_fwd(e, None, None, w, b, rt.cfg.layernorm_epsilon, rt.p_drop,
-                                        rt.seed_t, rt.salt(SALT_EMB), rt.rms)
+                                        rt.seed_t, rt.salt(SALT_EMB), rt.rms, elem0=rt.elem0(e.shape[0]))
         ctx.saved = (ids, h, mean, rstd)
         ctx.rt = rt
         ctx.micro = rt.micro
@@ -500,7 +511,7 @@ class EmbedFn(torch.autograd.Function):
         gw, gb = rt.norm_grads(f"layers.{ctx.first_layer}.ln1")
         _, de = norm_bwd(da.contiguous(), dh.contiguous(), h, mean, rstd, w, want_dx=True,
                          p=rt.p_drop, seed_t=rt.seed_t, salt=rt.salt(SALT_EMB, ctx.micro), rms=rt.rms,
-                         dgamma=gw, dbeta=gb, accumulate=True, defer=rt.colq)
+                         dgamma=gw, dbeta=gb, accumulate=True, defer=rt.colq, elem0=rt.elem0(da.shape[0]))
         if rt.sp:
             de = C.all_gather_dim0(de, rt.tp_group)
         embed_bwd(ids, de, rt.grads["wte"], rt.vocab_start)
@@ -591,7 +602,7 @@ class GPTLayerFn(torch.autograd.Function):
         o = _reduce(_mm(ctx_, P[p + "proj_w"], fused=rt.fused_linear), rt)
         w2, b2 = rt.norm_params(p + "ln2")
         h1, m, mean2, rstd2 = bda_norm_fwd(o, P[p + "proj_b"], h, w2, b2, eps, rt.p_drop, rt.seed_t,
-                                           rt.salt(1000 + 2 * i, micro), rt.rms)
+                                           rt.salt(1000 + 2 * i, micro), rt.rms, elem0=rt.elem0(o.shape[0]))
         moe = None
         if is_moe_layer(cfg, i):
             m_full = _gather(m, rt)
@@ -628,7 +639,8 @@ class GPTLayerFn(torch.autograd.Function):
         else:  # stage boundary: plain bias-dropout-add; normalise into a throwaway
             wn, bn = P[p + "ln2_w"], P.get(p + "ln2_b")
         h2, a2, mean_n, rstd_n = bda_norm_fwd(g, b_fc2, h1, wn, bn, eps, rt.p_drop,
-                                              rt.seed_t, rt.salt(1001 + 2 * i, micro), rt.rms)
+                                              rt.seed_t, rt.salt(1001 + 2 * i, micro), rt.rms,
+                                              elem0=rt.elem0(g.shape[0]))
         saved = (a_full, qkv_a, ctx_, ctx_a, lse, h1, mean2, rstd2, m_full, pre, f, h2, mean_n, rstd_n)
         return h2, a2, saved, dmask, moe
 
@@ -657,13 +669,14 @@ class GPTLayerFn(torch.autograd.Function):
             dh1, dg = norm_bwd(da2.contiguous(), dh2, h2, mean_n, rstd_n, wn, want_dx=True,
                                p=rt.p_drop, seed_t=rt.seed_t, salt=rt.salt(1001 + 2 * i, ctx.micro),
                                rms=rt.rms, dgamma=gwn, dbeta=gbn, dbias=G.get(p + "fc2_b"),
-                               accumulate=True, defer=rt.colq)
+                               accumulate=True, defer=rt.colq, elem0=rt.elem0(dh2.shape[0]))
         else:
             wn = P[p + "ln2_w"]
             zero = torch.zeros_like(dh2)
             dh1, dg = norm_bwd(zero, dh2, h2, mean_n, rstd_n, wn, want_dx=True, p=rt.p_drop,
                                seed_t=rt.seed_t, salt=rt.salt(1001 + 2 * i, ctx.micro), rms=rt.rms,
-                               dbias=G.get(p + "fc2_b"), accumulate=True, defer=rt.colq)
+                               dbias=G.get(p + "fc2_b"), accumulate=True, defer=rt.colq,
+                               elem0=rt.elem0(dh2.shape[0]))
         # ---- MLP backward
         if ctx.moe is not None:
             m_leaf, leaves, g_moe, l_aux = ctx.moe
@@ -712,7 +725,8 @@ class GPTLayerFn(torch.autograd.Function):
         gw2, gb2 = rt.norm_grads(p + "ln2")
         dh, do_ = norm_bwd(dm, dh1, h1, mean2, rstd2, w2, want_dx=True, p=rt.p_drop,
                            seed_t=rt.seed_t, salt=rt.salt(1000 + 2 * i, ctx.micro), rms=rt.rms, dgamma=gw2,
-                           dbeta=gb2, dbias=G[p + "proj_b"], accumulate=True, defer=rt.colq)
+                           dbeta=gb2, dbias=G[p + "proj_b"], accumulate=True, defer=rt.colq,
+                           elem0=rt.elem0(dm.shape[0]))
         # ---- attention backward
         do_full, dctx = _gather_mm(do_, P[p + "proj_w"], rt, trans=False)
         if rt.cp > 1:

@@ -39,8 +39,8 @@ SIGNATURES = {
     "mx_graph_memsets_to_kernels": [P],
     "mx_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],
     "mx_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
-    "mx_bda_norm_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, F, P, U32, I, P],
-    "mx_norm_bwd": [P, P, P, P, P, P, P, P, P, I, I, F, P, U32, I, P],
+    "mx_bda_norm_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, F, P, U32, I64, I, P],
+    "mx_norm_bwd": [P, P, P, P, P, P, P, P, P, I, I, F, P, U32, I64, I, P],
     "mx_colsum_finalize": [P, I, I, I, P, P, P, I, P, P],
     "mx_colreduce_scratch": [I, I],
     "mx_colsum_bf16": [P, I, I, P, P, I, P],

@@ -33,12 +33,12 @@ def _ref_norm(h32, gamma, beta, eps, rms):
     return y, mean, rstd
 
 
-def _ref_bda(x, bias, residual, p, seed_t, salt):
+def _ref_bda(x, bias, residual, p, seed_t, salt, elem0=0):
     t = x.float()
     if bias is not None:
         t = t + bias.float()
     if p > 0:
-        m = keep_mask(t.numel(), _seed_val(seed_t, salt), p).view_as(t)
+        m = keep_mask(t.numel(), _seed_val(seed_t, salt), p, base=elem0).view_as(t)
         t = torch.where(m, t / (1 - p), torch.zeros_like(t))
     if residual is not None:
         t = t + residual.float()
@@ -65,11 +65,13 @@ def layernorm_fwd(x, gamma, beta, eps=1e-5, rms=False):
 
 
 def bda_norm_fwd(x, bias, residual, gamma, beta, eps=1e-5, p=0.0, seed_t=None, salt=0,
-                 rms=False):
-    """h = residual + dropout(x + bias); y = norm(h).  Returns (h, y, mean, rstd)."""
+                 rms=False, *, elem0: int = 0):
+    """h = residual + dropout(x + bias); y = norm(h).  Returns (h, y, mean, rstd).
+    ``elem0``: flat index of x[0, 0] in the unsharded activation (the dropout mask is keyed
+    on global element indices: a sequence-parallel shard draws the unsharded tensor's bits)."""
     rows, cols = x.shape
     if not _lib.use_hip(x):
-        h32 = _ref_bda(x, bias, residual, p, seed_t, salt)
+        h32 = _ref_bda(x, bias, residual, p, seed_t, salt, elem0)
         h = h32.to(x.dtype)
         y, mean, rstd = _ref_norm(h.float(), gamma, beta, eps, rms)
         return h, y.to(x.dtype), mean, rstd
@@ -79,13 +81,13 @@ def bda_norm_fwd(x, bias, residual, gamma, beta, eps=1e-5, p=0.0, seed_t=None, s
     rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
     _lib.call("mx_bda_norm_fwd", _lib.ptr(x), _lib.ptr(bias), _lib.ptr(residual), _lib.ptr(gamma),
               _lib.ptr(beta), _lib.ptr(h), _lib.ptr(y), _lib.ptr(mean), _lib.ptr(rstd), rows, cols,
-              eps, float(p), _lib.ptr(seed_t), salt, int(rms), _lib.stream())
+              eps, float(p), _lib.ptr(seed_t), salt, int(elem0), int(rms), _lib.stream())
     return h, y, mean, rstd
 
 
 # ------------------------------------------------------------------ backward
 def norm_bwd(dy, dres, h, mean, rstd, gamma, want_dx=False, p=0.0, seed_t=None, salt=0,
-             rms=False, dgamma=None, dbeta=None, dbias=None, accumulate=False, defer=None):
+             rms=False, dgamma=None, dbeta=None, dbias=None, accumulate=False, defer=None, elem0: int = 0):
     """Backward of (bda_)norm.
 
     dh = dres + dnorm/dh;  dx = dh * dropout-mask * 1/(1-p) (if want_dx).
@@ -108,7 +110,7 @@ def norm_bwd(dy, dres, h, mean, rstd, gamma, want_dx=False, p=0.0, seed_t=None, 
         if want_dx:
             t = dh.float()
             if p > 0:
-                m = keep_mask(t.numel(), _seed_val(seed_t, salt), p).view_as(t)
+                m = keep_mask(t.numel(), _seed_val(seed_t, salt), p, base=elem0).view_as(t)
                 t = torch.where(m, t / (1 - p), torch.zeros_like(t))
             dx = t.to(dy.dtype)
         for buf, val in ((dgamma, (d32 * xh).sum(0)), (dbeta, d32.sum(0)),
@@ -134,7 +136,7 @@ def norm_bwd(dy, dres, h, mean, rstd, gamma, want_dx=False, p=0.0, seed_t=None, 
     dx = torch.empty_like(dy) if want_dx else None
     _lib.call("mx_norm_bwd", _lib.ptr(dy), _lib.ptr(dres), _lib.ptr(h), _lib.ptr(mean),
               _lib.ptr(rstd), _lib.ptr(gamma), _lib.ptr(dh), _lib.ptr(dx), _lib.ptr(partial),
-              rows, cols, float(p), _lib.ptr(seed_t), salt, int(rms), _lib.stream())
+              rows, cols, float(p), _lib.ptr(seed_t), salt, int(elem0), int(rms), _lib.stream())
     if want and not deferred:
         scratch = partial[nparts * 3 * cols:]
         _lib.call("mx_colsum_finalize", _lib.ptr(partial), nparts, cols, 3, _lib.ptr(dgamma),

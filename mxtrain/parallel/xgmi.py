@@ -433,7 +433,19 @@ class XGMICommunicator:
         w = self.world
         ok = True
         try:
-            for op in ("all_reduce", "reduce_scatter", "all_gather"):
+            # fail fast: one small all-reduce with a short barrier bound, checked at once --
+            # peers that cannot see each other's flags cost one short timeout, not one 30 s
+            # timeout per timed call below
+            probe = torch.full((64 * w,), float(self.rank + 1), device=self.device)
+            t_keep, self.timeout_s = self.timeout_s, min(self.timeout_s, 5.0)
+            try:
+                self.all_reduce_(probe)
+                self.check()
+            finally:
+                self.timeout_s = t_keep
+            ok = bool((probe == w * (w + 1) / 2).all().item())
+            ops = ("all_reduce", "reduce_scatter", "all_gather") if ok else ()
+            for op in ops:
                 for nb in sizes:
                     if nb > self.max_bytes or nb % (16 * w):
                         continue

@@ -117,7 +117,11 @@ class DistributedOptimizer:
         self._hyper_events = [None] * len(self._hyper_ring)
         self._hyper_i = 0
         self.hyper_host = self._hyper_ring[0]
-        self.normsq = torch.zeros(1, dtype=torch.float32, device=dev)
+        # ||g||^2 is element 0 of a zero-padded 128-byte buffer: the padded size is a
+        # valid xGMI message, so with the direct transport the norm all-reduce runs on the
+        # device like the bucket collectives and the whole step stays graph-capturable
+        self._normsq_buf = torch.zeros(max(32, 4 * self.world), dtype=torch.float32, device=dev)
+        self.normsq = self._normsq_buf[:1]
         self.step_count = 0
         # ---- overlap bookkeeping
         self.overlap = overlap and self.world > 1 and dev.type == "cuda"
@@ -322,13 +326,13 @@ class DistributedOptimizer:
     def grad_norm_sq(self) -> torch.Tensor:
         optim_ops.sumsq_bf16(self.grad_shard, 1.0 / self.gs_world, out=self.normsq,
                              flags=self.norm_flags)
-        if self.world > 1:
-            dist.all_reduce(self.normsq, group=self.dp_group)
-        if self.mp_group is not None and dist.get_world_size(self.mp_group) > 1:
-            dist.all_reduce(self.normsq, group=self.mp_group)
-        for g in self.norm_groups:
-            if dist.get_world_size(g) > 1:
-                dist.all_reduce(self.normsq, group=g)
+        from .collectives import all_reduce_
+        for g in [self.dp_group if self.world > 1 else None, self.mp_group] + self.norm_groups:
+            if g is not None and dist.get_world_size(g) > 1:
+                if self._normsq_buf.numel() * 4 % (16 * dist.get_world_size(g)):
+                    all_reduce_(self.normsq, g)          # (RCCL: no padding needed)
+                else:
+                    all_reduce_(self._normsq_buf, g)     # padding stays 0 on every rank
         return self.normsq
 
     def step(self, lr: Optional[float] = None):

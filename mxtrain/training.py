@@ -84,6 +84,7 @@ class GPTTrainer:
                               sequence_parallel=ps.sequence_parallel, seed_t=self.seed.t,
                               cp=ps.cp, cp_rank=ps.cp_rank, cp_group=ps.cp_group,
                               attn_seed_t=self.seed.attn_t)
+        self.stage.rt.micro_base = ps.dp_rank * self.num_micro   # global micro-batch index base
         self.stage.rt.batch_dmasks = os.environ.get("MXTRAIN_BATCH_DMASKS", "1") != "0"
         self.stage.rt.side_dmasks = os.environ.get("MXTRAIN_SIDE_DMASKS", "0") == "1"
         self.stage.rt.fused_linear = tcfg.fused_linear
@@ -135,11 +136,13 @@ class GPTTrainer:
     # ------------------------------------------------------------------ init
     @staticmethod
     def seed_bases(tcfg, ps):
-        """(hidden-dropout seed, attention-dropout seed) of this rank before any step:
-        hidden dropout differs per data/context-parallel rank (different tokens); the
-        attention mask is keyed on global heads/positions, so it is shared by CP ranks."""
-        return (tcfg.seed + 7 * (ps.dp_rank * ps.cp + ps.cp_rank),
-                tcfg.seed + 7 * ps.dp_rank * ps.cp + 3)
+        """(hidden-dropout seed, attention-dropout seed) of this rank before any step.  The
+        same on every data-parallel rank: the masks are keyed on the GLOBAL micro-batch index
+        (StepRuntime.micro_base) and element / head / position, so DP ranks draw disjoint
+        bits of the one-rank run's masks.  Hidden dropout differs per context-parallel rank
+        (different tokens of each sequence); the attention mask is keyed on global heads /
+        positions, so it is shared by CP ranks."""
+        return (tcfg.seed + 7 * ps.cp_rank, tcfg.seed + 3)
 
     def _setup_moe(self, cfg, tcfg, ps, dtype, sched):
         """Expert parameters: E/ep experts per rank in a second flat buffer with its own

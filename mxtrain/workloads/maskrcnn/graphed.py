@@ -71,7 +71,7 @@ def sgd_momentum_(opt: torch.optim.SGD, lr) -> None:
 
 class GraphedTrainStep:
     def __init__(self, model, opt: torch.optim.SGD, params: List[torch.Tensor], clip: float, device,
-                 flat_capacity: int = 16 << 20, flat_master=None, allow_rccl_capture: bool = False):
+                 flat_capacity: int = 16 << 20, flat_master=None):
         self.model, self.opt, self.params, self.clip, self.device = model, opt, params, clip, device
         self.graphs: Dict[tuple, tuple] = {}
         # with a FlatMaster (models/compute_weights.py) the update is its fused clip + SGD
@@ -84,10 +84,10 @@ class GraphedTrainStep:
         self.captures = 0
         self.replays = 0
         self.eager_steps = 0
-        # data parallel (FlatMaster world > 1): the gradient all-reduces are captured with the
-        # step when they run on the xGMI kernel (device-side barrier epochs: replay-safe);
-        # RCCL inside a capture only when forced (--mx-graph 1)
-        self.allow_rccl_capture = allow_rccl_capture
+        # data parallel (FlatMaster world > 1): the bucketed gradient all-reduces are captured
+        # with the step on either route -- RCCL collectives (its graph-capture support: the
+        # communicator's kernels become graph nodes on its internal stream, joined back by
+        # events) or the xGMI kernel (device-side barrier epochs: replay-safe)
         self.capturable = True
         # MXTRAIN_GRAPH_DEBUG=1: synchronise after every step and log capture/replay events
         self.debug = os.environ.get("MXTRAIN_GRAPH_DEBUG", "0") == "1"
@@ -112,14 +112,8 @@ class GraphedTrainStep:
             sgd_momentum_(self.opt, self.lr)
         return torch.stack([losses[k].detach().float() for k in LOSS_NAMES])
 
-    def _route_capturable(self) -> bool:
-        fm = self.fm
-        if fm is None or fm.world == 1 or self.allow_rccl_capture:
-            return True
-        return fm.dp_routes == {"xgmi"}
-
     def _eager(self, batch) -> Dict[str, torch.Tensor]:
-        """The same step without a graph (data-parallel over RCCL, not forced into capture)."""
+        """The same step without a graph (after a failed capture)."""
         flat = batch["gt_mask_flat"]
         st = {k: batch[k].to(self.device, non_blocking=True) for k in INPUT_KEYS}
         self.flat[:flat.numel()].copy_(flat, non_blocking=True)
@@ -170,23 +164,35 @@ class GraphedTrainStep:
                 # eager step with this batch (a real update): warms every lazy cache
                 self.opt.zero_grad(set_to_none=True)
                 out = self._body(st)
-                if not self._route_capturable():
-                    cur.wait_stream(self.stream)
-                    self.capturable = False
-                    self.eager_steps += 1
-                    return dict(zip(LOSS_NAMES, out.unbind(0)))
                 # capture: grads are allocated inside the graph's pool, never zeroed
                 self.opt.zero_grad(set_to_none=True)
                 g = torch.cuda.CUDAGraph(keep_graph=True)
                 if self.marker is not None:
                     torch.cuda.synchronize(self.device)
                     self.marker("capture-begin")
-                with torch.cuda.graph(g, pool=self.pool, stream=self.stream):
-                    sout = self._body(st)
-                if self.marker is not None:
-                    self.marker("capture-end")
-                self._finish_capture(g, key)
+                err = None
+                try:
+                    with torch.cuda.graph(g, pool=self.pool, stream=self.stream):
+                        sout = self._body(st)
+                    if self.marker is not None:
+                        self.marker("capture-end")
+                    self._finish_capture(g, key)
+                except Exception as e:  # noqa: BLE001 -- fall back to the eager step, loudly
+                    err = repr(e)[:300]
             cur.wait_stream(self.stream)
+            if self.fm is not None and self.fm.world > 1:
+                # every rank takes the same path: a rank whose capture failed runs eager
+                # collectives that the others would otherwise replay from their graphs
+                import torch.distributed as dist
+                ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=self.device)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=self.fm.group)
+                if int(ok.item()) == 0 and err is None:
+                    err = "capture failed on another rank"
+            if err is not None:
+                print(f"[graphed] capture failed, training eagerly: {err}", file=sys.stderr, flush=True)
+                self.capturable = False
+                self.eager_steps += 1
+                return dict(zip(LOSS_NAMES, out.unbind(0)))
             self.graphs[key] = (g, st, sout)
             self.captures += 1
             self._dbg("captured", key)

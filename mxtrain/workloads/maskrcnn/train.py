@@ -175,7 +175,11 @@ def use_shipped_find_db():
     for f in files:
         t = os.path.join(dst, os.path.basename(f))
         if not os.path.exists(t) or os.path.getsize(t) < os.path.getsize(f):
-            shutil.copyfile(f, t)
+            # N ranks of one node copy at once: write a private temporary and rename it
+            # into place, so MIOpen never opens a half-written db
+            tmp = f"{t}.tmp{os.getpid()}"
+            shutil.copyfile(f, tmp)
+            os.replace(tmp, t)
     os.environ["MIOPEN_USER_DB_PATH"] = dst
     return dst
 
@@ -292,13 +296,9 @@ def main(argv=None):
     debug_finite = check_finite_enabled()
     train_sets = [COCODetection(cfg.DATA.BASEDIR, n, training=True) for n in cfg.DATA.TRAIN]
     flat_sgd = device.type == "cuda" and os.environ.get("MXTRAIN_FLAT_SGD", "1") != "0"
-    if world > 1 and flat_sgd:
-        # data-parallel gradient all-reduce inside the fused step: the direct xGMI kernel
-        # (checked against RCCL and timed on the live group; RCCL where it loses) -- it is
-        # graph-capturable, so the whole step stays one hipGraph at world > 1
-        os.environ.setdefault("MXTRAIN_XGMI", "auto")
-    # whole-step hipGraph: 1 GPU, or world > 1 with the fused flat SGD (the replay checks the
-    # gradient reduction route after its eager warm-up step: xGMI, or RCCL when forced)
+    # whole-step hipGraph: 1 GPU, or world > 1 with the fused flat SGD, whose bucketed
+    # gradient all-reduces are captured into the graph -- RCCL by default, or the direct
+    # xGMI kernel with MXTRAIN_XGMI=1/auto (checked against RCCL and timed on the live group)
     use_graph = (args.mx_graph == "1" or (args.mx_graph == "auto" and not debug_finite)) \
         and device.type == "cuda" and bool(cfg.MODE_MASK) and (world == 1 or flat_sgd)
     ds = DetectionDataset(train_sets[0], short, max_size, training=True, with_masks=bool(cfg.MODE_MASK), seed=rank,
@@ -350,8 +350,7 @@ def main(argv=None):
         dmodel = hvd.DistributedDataParallel(model)
     if use_graph:
         from mxtrain.workloads.maskrcnn.graphed import GraphedTrainStep
-        gstep = GraphedTrainStep(model, opt, params, clip, device, flat_master=fm,
-                                 allow_rccl_capture=args.mx_graph == "1")
+        gstep = GraphedTrainStep(model, opt, params, clip, device, flat_master=fm)
         log("Training step runs as a hipGraph (one graph per input shape)")
     max_steps = args.mx_max_steps
     timed_imgs, t_timed = 0, None

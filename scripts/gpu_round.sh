@@ -1,5 +1,9 @@
 #!/bin/bash
-# One gpurun session: kernel numerics tests, smoke, bench, rocprof summary.
+# One gpurun session, parameterised (the one wrapper every GPU call goes through):
+#   STEPS="tests smoke bench"  (also: slice mrcnn mrprof kbench prof pmc)
+#   PYTEST_ARGS / BENCH_ARGS / MRCNN_ARGS / KBENCH_ARGS / PROF_ARGS / SLICE_ARGS
+#   pmc: PMC_CMD (python script + args, run directly after rocprofv3's --), PMC_REGEX
+#        (kernel-name filter), one rocprofv3 pass per counter group (SQ <= 8 per pass)
 # Each GPU step has its own time limit; after a crash/timeout (exit >= 124 or signal)
 # nothing further touches the GPU.
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -11,7 +15,7 @@ STEPS="${STEPS:-tests smoke bench}"
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 ${T_TESTS:-600} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1; rc=$?
+      timeout -k 10 ${T_TESTS:-900} python -u -m pytest tests -m gpu ${PYTEST_X--x} -q --timeout ${T_TEST:-300} --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1; rc=$?
       tail -30 gpurun_out/gpu_tests.log; echo "tests rc=$rc"; ok $rc || exit $rc ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
@@ -36,6 +40,18 @@ for s in $STEPS; do
       cd /tmp && export TMPDIR=/tmp
       timeout -k 10 ${T_PROF:-400} rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --gpus 1 --steps 5 --warmup 3 ${PROF_ARGS:-} > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1; rc=$?
       cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/prof.log; echo "prof rc=$rc"; ok $rc || exit $rc ;;
+    pmc)
+      cd /tmp && export TMPDIR=/tmp
+      G1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES"
+      G2="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM"
+      G3="SQ_ACTIVE_INST_VMEM SQ_INSTS_SMEM SQ_VALU_MFMA_COEXEC_CYCLES SQ_WAVES SQ_INSTS_VALU_TRANS_F32 GRBM_GUI_ACTIVE GRBM_COUNT"
+      i=0
+      for G in "$G1" "$G2" "$G3"; do
+        i=$((i+1))
+        timeout -s KILL ${T_PMC:-120} rocprofv3 --pmc $G --kernel-include-regex "${PMC_REGEX:-.*}" -d "$GRAFT_REPO_ROOT/gpurun_out/pmc$i" -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/$PMC_CMD > "$GRAFT_REPO_ROOT/gpurun_out/pmc$i.log" 2>&1; rc=$?
+        echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || { cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/pmc$i.log; exit $rc; }
+      done
+      cd "$GRAFT_REPO_ROOT" ;;
   esac
 done
 echo ALLDONE

@@ -28,3 +28,27 @@ def test_bench_two_ranks_gloo_json_line():
     # whole-job tokens/s: global batch x seq / step time
     tok = d["config"]["global_batch"] * d["config"]["seq_len"]
     assert abs(d["value"] - tok / (d["ms_per_step"] / 1000.0)) / d["value"] < 0.01
+
+
+def test_bench_two_ranks_gloo_maskrcnn_fields(tmp_path):
+    """N > 1 Mask R-CNN half of the metric: every bench rank starts one child rank after the
+    GPT window, the children rendezvous on a fresh port (torchrun's agent-store variables
+    dropped) and rank 0 reports whole-job images/s for n_gpus = 2."""
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="2")
+    small = ("--images 4 --data {d} PREPROC.TRAIN_SHORT_EDGE_SIZE=[192,192] PREPROC.MAX_SIZE=256 "
+             "RPN.TRAIN_PER_LEVEL_NMS_TOPK=200 RPN.TRAIN_POST_NMS_TOPK=200 FRCNN.BATCH_PER_IM=32").format(
+                 d=tmp_path / "coco")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29537", os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "1", "--model", "gpt-tiny", "--no-tuned-gemm",
+           "--maskrcnn-batches", "1", "--maskrcnn-steps", "2:1", "--maskrcnn-workers", "0",
+           "--maskrcnn-args", small]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2
+    assert d["maskrcnn_img_s_1img"] and d["maskrcnn_img_s_1img"] > 0, d.get("maskrcnn_config")
+    mc = d["maskrcnn_config"]
+    assert mc["n_gpus"] == 2 and mc["1img"]["n_gpus"] == 2 and mc["parallelism"].startswith("dp2")

@@ -27,7 +27,15 @@ CFG_LLAMA = dict(CFG, num_kv_heads=2, normalization="rmsnorm", position_embeddin
 CFG_ADROP = dict(CFG, attention_dropout=0.1)
 
 
+# hidden + attention dropout 0.1 (the reference config's Megatron defaults): the masks are
+# keyed on the global micro-batch index and global element / head indices, so every
+# parallel layout draws the single-process masks
+CFG_DROP = dict(CFG, hidden_dropout=0.1, attention_dropout=0.1)
+
+
 def _cfg(mode):
+    if mode.endswith(":drop"):
+        return CFG_DROP
     if mode.endswith(":llama"):
         return CFG_LLAMA
     if mode.endswith(":adrop"):
@@ -294,5 +302,29 @@ def test_tp2_pp2_dp2_matches_single(reference, mode):
     assert abs(mean_first - ref_losses[0]) < 2e-5 * max(1.0, abs(ref_losses[0]))
     for rank, _, losses, params, (tpr, ppr, dpr) in res:
         exp = shard_gpt_state(ref_sd, cfg, 2, tpr, 2, ppr)
+        for n, t in exp.items():
+            assert torch.allclose(params[n], t, atol=3e-5, rtol=1e-4), (mode, rank, n, (params[n] - t).abs().max())
+
+
+@pytest.mark.parametrize("mode", ["dp:drop", "sp:drop", "3dsp:drop"])
+def test_dropout_masks_layout_invariant(mode):
+    """Hidden and attention dropout 0.1 under DP2 (global micro-batch index), TP2 + SP
+    (sequence shards keyed by global element index) and TP2 x PP2 x DP2 + SP: every rank's
+    parameters after two steps equal the single-process run with the same micro-batches,
+    and the losses match (DP: their mean)."""
+    from mxtrain.models.gpt import shard_gpt_state
+    cfg, ref_losses, ref_sd = _make_reference(CFG_DROP)
+    m = mode.split(":")[0]
+    res = _run(mode, world=8 if m.startswith("3d") else 2)
+    tp = 2 if m in ("sp", "3dsp") else 1
+    pp = 2 if m.startswith("3d") else 1
+    dp = 2 if m in ("dp", "3dsp") else 1
+    last = [r for r in res if r[4][1] == pp - 1 and r[4][0] == 0]
+    assert len(last) == dp
+    for step in range(2):
+        mean = sum(r[2][step] for r in last) / dp
+        assert abs(mean - ref_losses[step]) < 2e-5 * max(1.0, abs(ref_losses[step])), (mode, step, mean, ref_losses)
+    for rank, _, losses, params, (tpr, ppr, dpr) in res:
+        exp = shard_gpt_state(ref_sd, cfg, tp, tpr, pp, ppr)
         for n, t in exp.items():
             assert torch.allclose(params[n], t, atol=3e-5, rtol=1e-4), (mode, rank, n, (params[n] - t).abs().max())

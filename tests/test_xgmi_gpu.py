@@ -147,15 +147,17 @@ def _worker(rank, world, port, q):
         q.put((rank, None, repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_xgmi_collectives_multi_process(world):
+    """world 8 = kMaxRanks (csrc/comm/xgmi.hip): every flag slot and peer pointer of the
+    8-GPU node layout in use, eight processes sharing the box's one GPU."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
     ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = [q.get(timeout=100) for _ in ps]
+    res = [q.get(timeout=100 + 20 * world) for _ in ps]
     for p in ps:
         p.join(timeout=30)
     for rank, out, err in res:
