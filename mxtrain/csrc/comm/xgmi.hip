@@ -240,6 +240,107 @@ __global__ __launch_bounds__(kThreads) void xgmi_kernel(Peers pp, const uint4* i
   if (threadIdx.x == 0) self->counter[b] = epoch;
 }
 
+// ------------------------------------------------------------------ point-to-point
+// Pipeline-parallel 1F1B transfers (one activation / activation gradient per message)
+// between two ranks of one node.  Same memory model as the collectives above: the WRITER
+// of a buffer writes it locally and releases it at system scope (L2 write-back) before it
+// signals; the reader acquires and then reads it over xGMI.  Per directed channel:
+//   * the sender owns a ring of kP2PRing slots (registered, IPC-mapped by the receiver);
+//   * message n goes to slot n % kP2PRing: the sender waits until the receiver has freed
+//     the slot (message n - kP2PRing consumed), copies the payload into it, releases, and
+//     stores n + 1 into the receiver's FULL word of that slot (remote store);
+//   * the receiver polls its own FULL word, acquires, copies the slot into its output
+//     tensor (reads over xGMI), drains its loads, and stores n + 1 into the sender's FREE
+//     word (remote store) -- the sender's next use of the slot waits for it.
+// Every workgroup b handles the same strided share of the message on both sides and has
+// its own FULL / FREE words and its own sequence counter, so no grid-wide sync is needed.
+// The counters live in device memory and are advanced by the kernels (hipGraph replays stay
+// in step); every wait is bounded (error word, as above).
+constexpr int kP2PRing = 4;
+constexpr int kP2PBlocks = 64;
+
+struct P2PCtl {                                 // one per rank per peer, uncached memory
+  uint32_t full[kP2PRing][kP2PBlocks];          // receiver side: message seq + 1 is in slot
+  uint32_t free_[kP2PRing][kP2PBlocks];         // sender side: message seq + 1 was consumed
+  uint32_t send_seq[kP2PBlocks];
+  uint32_t recv_seq[kP2PBlocks];
+  uint32_t error;                               // 1: send wait timed out, 2: recv wait timed out
+};
+
+__device__ __forceinline__ bool p2p_wait(const uint32_t* word, uint32_t target, uint64_t timeout_ticks) {
+  const uint64_t t0 = now_ticks();
+  while ((int32_t)(__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
+    if (now_ticks() - t0 > timeout_ticks) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+// mine: this rank's ctl for the channel; peer: the receiver's ctl (mapped); ring: this
+// rank's own send ring (local); src: the payload (nvec 16-B vectors, nvec <= slot_vec)
+__global__ __launch_bounds__(kThreads) void p2p_send_kernel(P2PCtl* mine, P2PCtl* peer, uint4* ring,
+                                                            int64_t slot_vec, const uint4* src, int64_t nvec,
+                                                            uint64_t timeout_ticks) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  __shared__ int ok_s;
+  const uint32_t n = mine->send_seq[b];
+  const int slot = (int)(n % kP2PRing);
+  if (t == 0) {
+    ok_s = 1;
+    // slot free: message n - kP2PRing consumed (the first kP2PRing messages find it free)
+    if (n >= (uint32_t)kP2PRing && !p2p_wait(&mine->free_[slot][b], n - kP2PRing + 1, timeout_ticks)) {
+      __hip_atomic_store(&mine->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      ok_s = 0;
+    }
+  }
+  __syncthreads();
+  // (the receiver's last reads of this slot completed before it freed it: no acquire needed
+  // before overwriting; a failed wait still writes nothing)
+  if (ok_s) {
+    uint4* dst = ring + (int64_t)slot * slot_vec;
+    for (int64_t v = (int64_t)b * kThreads + t; v < nvec; v += (int64_t)gridDim.x * kThreads) dst[v] = src[v];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: drain + L2 write-back
+  __syncthreads();
+  if (t == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (ok_s) __hip_atomic_store(&peer->full[slot][b], n + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    mine->send_seq[b] = n + 1;
+  }
+}
+
+// mine: this rank's ctl (its FULL words are written by the sender); peer: the sender's ctl
+// (mapped: FREE words); ring: the SENDER's ring (mapped); dst: the output tensor
+__global__ __launch_bounds__(kThreads) void p2p_recv_kernel(P2PCtl* mine, P2PCtl* peer, const uint4* ring,
+                                                            int64_t slot_vec, uint4* dst, int64_t nvec,
+                                                            uint64_t timeout_ticks) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  __shared__ int ok_s;
+  const uint32_t n = mine->recv_seq[b];
+  const int slot = (int)(n % kP2PRing);
+  if (t == 0) {
+    ok_s = 1;
+    if (!p2p_wait(&mine->full[slot][b], n + 1, timeout_ticks)) {
+      __hip_atomic_store(&mine->error, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      ok_s = 0;
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // drop stale lines before the peer reads
+  if (ok_s) {
+    const uint4* src = ring + (int64_t)slot * slot_vec;
+    for (int64_t v = (int64_t)b * kThreads + t; v < nvec; v += (int64_t)gridDim.x * kThreads) dst[v] = src[v];
+  }
+  // every load of the slot has returned (its data is in registers / stored) before the
+  // sender may overwrite the slot
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    if (ok_s) __hip_atomic_store(&peer->free_[slot][b], n + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    mine->recv_seq[b] = n + 1;
+  }
+}
+
 }  // namespace
 
 MX_EXPORT int mx_xgmi_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
@@ -326,5 +427,40 @@ MX_EXPORT int mx_xgmi_collective(void* const* datas, void* const* flagss, int wo
   else
     hipLaunchKernelGGL(xgmi_kernel<false>, dim3(blocks), dim3(kThreads), 0, stream, pp,
                        (const uint4*)in, (uint4*)out, nvec, rank, world, op, ticks, sig, validate);
+  return hipGetLastError();
+}
+
+// ---- point-to-point channel (see p2p_send_kernel): ring of kP2PRing slots of slot_bytes
+MX_EXPORT int mx_xgmi_p2p_ring() { return kP2PRing; }
+MX_EXPORT int mx_xgmi_p2p_ctl_bytes() { return (int)((sizeof(P2PCtl) + 255) / 256 * 256); }
+
+// ring: plain device memory (kP2PRing * slot_bytes); ctl: uncached; both zeroed
+MX_EXPORT int mx_xgmi_p2p_alloc(int64_t slot_bytes, void** ring, void** ctl) {
+  hipError_t e = hipMalloc(ring, (size_t)slot_bytes * kP2PRing);
+  if (e != hipSuccess) return e;
+  e = hipExtMallocWithFlags(ctl, (size_t)mx_xgmi_p2p_ctl_bytes(), hipDeviceMallocUncached);
+  if (e != hipSuccess) return e;
+  e = hipMemset(*ctl, 0, (size_t)mx_xgmi_p2p_ctl_bytes());
+  if (e != hipSuccess) return e;
+  return hipDeviceSynchronize();
+}
+
+MX_EXPORT int mx_xgmi_p2p_error(void* ctl, uint32_t* out) {
+  return hipMemcpy(out, &reinterpret_cast<P2PCtl*>(ctl)->error, 4, hipMemcpyDeviceToHost);
+}
+
+// send: mine = own ctl, peer = receiver's ctl (mapped), ring = own ring
+// recv: mine = own ctl, peer = sender's ctl (mapped), ring = sender's ring (mapped)
+MX_EXPORT int mx_xgmi_p2p(int is_send, void* mine, void* peer, void* ring, int64_t slot_bytes, void* buf,
+                          int64_t nbytes, int blocks, double timeout_s, hipStream_t stream) {
+  if (nbytes % 16 || slot_bytes % 16 || nbytes > slot_bytes || nbytes <= 0) return hipErrorInvalidValue;
+  if (blocks <= 0 || blocks > kP2PBlocks) blocks = kP2PBlocks;
+  const uint64_t ticks = (uint64_t)(timeout_s * 1e8);
+  if (is_send)
+    hipLaunchKernelGGL(p2p_send_kernel, dim3(blocks), dim3(kThreads), 0, stream, (P2PCtl*)mine, (P2PCtl*)peer,
+                       (uint4*)ring, slot_bytes / 16, (const uint4*)buf, nbytes / 16, ticks);
+  else
+    hipLaunchKernelGGL(p2p_recv_kernel, dim3(blocks), dim3(kThreads), 0, stream, (P2PCtl*)mine, (P2PCtl*)peer,
+                       (const uint4*)ring, slot_bytes / 16, (uint4*)buf, nbytes / 16, ticks);
   return hipGetLastError();
 }

@@ -8,6 +8,11 @@ Activations travel as one contiguous [tokens, hidden] bf16 tensor per micro-batc
 (a single xGMI p2p transfer); the activation gradient travels back the same way.
 Each stage reports its gradient units to the DP optimizer only during the LAST
 micro-batch's backward, so bucket reduce-scatters overlap the pipeline drain.
+
+Transport: RCCL ``batch_isend_irecv`` by default; with ``MXTRAIN_XGMI=1`` the direct xGMI
+channels of ``parallel/xgmi.py`` (XGMIP2P: the sender's ring slot read by the receiver over
+xGMI, device-side sequence counters, side streams), which also run between processes
+sharing one GPU -- so the 1F1B schedule executes on real HIP streams in the one-GPU tests.
 """
 from __future__ import annotations
 
@@ -42,6 +47,24 @@ class PipelineSchedule:
     def __init__(self, trainer: "GPTTrainer"):
         self.tr = trainer
         self.ps = trainer.ps
+        self._xp = None          # XGMIP2P channels (MXTRAIN_XGMI), built on first use
+        self._xp_key = None
+
+    def _xgmi(self, shape):
+        """The xGMI p2p channels for activations of ``shape`` (None: RCCL).  Collective over
+        the pipeline group, so every stage calls it at the top of run()."""
+        from . import xgmi
+        ps = self.ps
+        dev = self.tr.device
+        if not xgmi.enabled() or dev.type != "cuda" or ps.pp_group is None:
+            return None
+        nb = shape[0] * shape[1] * torch.empty((), dtype=self.tr.dtype).element_size()
+        if self._xp_key != nb:
+            g = ps.pp_group
+            peers = [dist.get_group_rank(g, r) for r in (ps.prev_rank(), ps.next_rank()) if r is not None]
+            self._xp = xgmi.get_p2p(g, dev, peers, nb)
+            self._xp_key = nb
+        return self._xp
 
     def _act_shape(self, B, S):
         ps = self.ps
@@ -63,6 +86,12 @@ class PipelineSchedule:
         return torch.empty(shape, dtype=self.tr.dtype, device=self.tr.device)
 
     def _post(self, send_t=None, send_to=None, recv_shape=None, recv_from=None):
+        xp = self._xp if self._xp_key is not None else None
+        if xp is not None:
+            g = self.ps.pp_group
+            return xp.post(send_t=send_t, send_to=dist.get_group_rank(g, send_to) if send_t is not None else None,
+                           recv_buf=self._buf(recv_shape) if recv_shape is not None else None,
+                           recv_from=dist.get_group_rank(g, recv_from) if recv_shape is not None else None)
         ops = []
         rbuf = None
         if send_t is not None:
@@ -84,6 +113,7 @@ class PipelineSchedule:
         nm, B, S = tokens.shape
         p, s = ps.pp, ps.pp_rank
         shape = self._act_shape(B, S)
+        self._xgmi(shape)
         first, last = ps.is_first_stage, ps.is_last_stage
         prev, nxt = ps.prev_rank(), ps.next_rank()
         warm = min(p - s - 1, nm)
@@ -176,6 +206,7 @@ class PipelineSchedule:
         stage = tr.stage
         nm, B, S = tokens.shape
         shape = self._act_shape(B, S)
+        self._xgmi(shape)
         first, last = ps.is_first_stage, ps.is_last_stage
         prev, nxt = ps.prev_rank(), ps.next_rank()
         loss_total = torch.zeros((), dtype=torch.float32, device=tr.device)

@@ -57,6 +57,12 @@ _SIGS = {
                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                            ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                            ctypes.c_double, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p],
+    "mx_xgmi_p2p_ring": [],
+    "mx_xgmi_p2p_ctl_bytes": [],
+    "mx_xgmi_p2p_alloc": [ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p)],
+    "mx_xgmi_p2p_error": [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)],
+    "mx_xgmi_p2p": [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                    ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_void_p],
 }
 OP_RS_DIRECT, OP_AG_DIRECT = 4, 5
 ERR_SIG = 0x100
@@ -501,6 +507,161 @@ class XGMICommunicator:
         return res
 
 
+class _P2PHandle:
+    """A posted transfer: ``wait()`` makes the current stream wait for it and returns the
+    received tensor (None for a send); the send tensor is referenced until then."""
+    __slots__ = ("events", "rbuf", "keep")
+
+    def __init__(self, events, rbuf, keep):
+        self.events, self.rbuf, self.keep = events, rbuf, keep
+
+    def wait(self):
+        cur = torch.cuda.current_stream()
+        for e in self.events:
+            cur.wait_event(e)
+        self.events, self.keep = [], None
+        return self.rbuf
+
+
+class XGMIP2P:
+    """Point-to-point channels over xGMI between a rank and its neighbours in ``group``
+    (the pipeline group: previous / next stage), for the 1F1B activation / gradient
+    transfers (csrc/comm/xgmi.hip p2p_send_kernel / p2p_recv_kernel).  Per peer this rank
+    owns a send ring of ``ring`` slots of ``slot_bytes`` and a control block; the peer maps
+    both (IPC handles exchanged over the group, collectively).  Sends and receives run on
+    two side streams, so a receive waiting for its peer never blocks compute; ``post``
+    returns a handle whose ``wait()`` joins the current stream.  Message order per direction
+    is the posting order on both sides (the 1F1B schedule is deterministic); the kernels'
+    sequence counters live on the device, so a captured schedule replays in step."""
+
+    def __init__(self, group, device, peers, slot_bytes: int, timeout_s: float = 30.0, blocks: int = 32):
+        self.group = group
+        self.device = torch.device(device)
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.slot_bytes = (int(slot_bytes) + 15) // 16 * 16
+        self.timeout_s, self.blocks = timeout_s, blocks
+        self.peers = sorted({int(p) for p in peers if p is not None and int(p) != self.rank})
+        self._ring: Dict[int, ctypes.c_void_p] = {}
+        self._ctl: Dict[int, ctypes.c_void_p] = {}
+        self._peer_ring: Dict[int, int] = {}
+        self._peer_ctl: Dict[int, int] = {}
+        self._opened: List[ctypes.c_void_p] = []
+        err, mine = None, {}
+        with torch.cuda.device(self.device):
+            try:
+                hs = _fn("mx_xgmi_handle_size")()
+                for p in self.peers:
+                    r, c = ctypes.c_void_p(), ctypes.c_void_p()
+                    _check(_fn("mx_xgmi_p2p_alloc")(self.slot_bytes, ctypes.byref(r), ctypes.byref(c)),
+                           "mx_xgmi_p2p_alloc")
+                    self._ring[p], self._ctl[p] = r, c
+                    hr, hc = ctypes.create_string_buffer(hs), ctypes.create_string_buffer(hs)
+                    _check(_fn("mx_xgmi_get_handle")(r, hr), "hipIpcGetMemHandle(p2p ring)")
+                    _check(_fn("mx_xgmi_get_handle")(c, hc), "hipIpcGetMemHandle(p2p ctl)")
+                    mine[p] = (bytes(hr.raw), bytes(hc.raw))
+            except Exception as e:  # every rank must still reach the exchange
+                err = repr(e)
+            allh: List = [None] * self.world
+            dist.all_gather_object(allh, (mine, self.peers), group=group)
+            if err is None:
+                try:
+                    for p in self.peers:
+                        theirs, their_peers = allh[p]
+                        if self.rank not in their_peers or self.rank not in theirs:
+                            raise RuntimeError(f"rank {p} has no channel to rank {self.rank}")
+                        hr, hc = theirs[self.rank]
+                        pr, pc = ctypes.c_void_p(), ctypes.c_void_p()
+                        _check(_fn("mx_xgmi_open_handle")(hr, ctypes.byref(pr)), f"hipIpcOpenMemHandle(p2p ring {p})")
+                        self._opened.append(pr)
+                        _check(_fn("mx_xgmi_open_handle")(hc, ctypes.byref(pc)), f"hipIpcOpenMemHandle(p2p ctl {p})")
+                        self._opened.append(pc)
+                        self._peer_ring[p], self._peer_ctl[p] = pr.value, pc.value
+                except Exception as e:
+                    err = repr(e)
+        errs: List = [None] * self.world
+        dist.all_gather_object(errs, err, group=group)
+        bad = [(r, e) for r, e in enumerate(errs) if e is not None]
+        if bad:
+            self.close()
+            raise XGMIUnavailable(f"xGMI p2p setup failed: {bad}")
+        self.s_send = torch.cuda.Stream(device=self.device)
+        self.s_recv = torch.cuda.Stream(device=self.device)
+
+    def _launch(self, is_send: bool, peer: int, t: torch.Tensor):
+        nb = t.numel() * t.element_size()
+        if nb > self.slot_bytes or nb % 16 or not t.is_contiguous():
+            raise ValueError(f"xGMI p2p message of {nb} B (slot {self.slot_bytes} B, contiguous, 16-B multiple)")
+        ring = self._ring[peer].value if is_send else self._peer_ring[peer]
+        _check(_fn("mx_xgmi_p2p")(int(is_send), self._ctl[peer].value, self._peer_ctl[peer], ring,
+                                  self.slot_bytes, t.data_ptr(), nb, self.blocks, self.timeout_s, _lib.stream()),
+               "mx_xgmi_p2p")
+
+    def post(self, send_t=None, send_to=None, recv_buf=None, recv_from=None) -> _P2PHandle:
+        """Post a send of ``send_t`` to group rank ``send_to`` and / or a receive from
+        ``recv_from`` into ``recv_buf`` (both allocated on the current stream)."""
+        cur = torch.cuda.current_stream(self.device)
+        events = []
+        keep = None
+        if send_t is not None:
+            keep = send_t.contiguous()
+            self.s_send.wait_stream(cur)
+            with torch.cuda.stream(self.s_send):
+                self._launch(True, int(send_to), keep)
+            events.append(self.s_send.record_event())
+        if recv_buf is not None:
+            self.s_recv.wait_stream(cur)
+            with torch.cuda.stream(self.s_recv):
+                self._launch(False, int(recv_from), recv_buf)
+            events.append(self.s_recv.record_event())
+        return _P2PHandle(events, recv_buf, keep)
+
+    def check(self):
+        """Raise if a send / receive wait timed out on this rank (synchronises)."""
+        torch.cuda.synchronize(self.device)
+        for p, c in self._ctl.items():
+            v = ctypes.c_uint32(0)
+            _check(_fn("mx_xgmi_p2p_error")(c, ctypes.byref(v)), "mx_xgmi_p2p_error")
+            if v.value:
+                raise RuntimeError(f"xGMI p2p {'send' if v.value == 1 else 'receive'} with rank {p} timed out "
+                                   f"on rank {self.rank}")
+
+    def close(self):
+        if torch.cuda.is_available():
+            torch.cuda.synchronize(self.device)
+        for p in self._opened:
+            if p.value:
+                _fn("mx_xgmi_close_handle")(p)
+        self._opened = []
+        for p in list(self._ring):
+            _fn("mx_xgmi_free")(self._ring[p], self._ctl[p])
+        self._ring, self._ctl = {}, {}
+
+
+_P2PS: Dict[tuple, Optional[XGMIP2P]] = {}
+
+
+def get_p2p(group, device, peers, slot_bytes: int) -> Optional[XGMIP2P]:
+    """The pipeline group's xGMI p2p channels when ``MXTRAIN_XGMI`` is 1 / auto (GPU, one
+    node), else None (RCCL batch_isend_irecv).  Collective over ``group`` on first use."""
+    if not enabled() or group is None or not torch.cuda.is_available():
+        return None
+    key = (id(group), tuple(sorted(p for p in peers if p is not None)), int(slot_bytes))
+    if key in _P2PS:
+        return _P2PS[key]
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    try:
+        c = XGMIP2P(group, device, peers, slot_bytes,
+                    timeout_s=float(os.environ.get("MXTRAIN_XGMI_TIMEOUT_S", "30")))
+    except XGMIUnavailable as e:
+        if dist.get_rank(group) == 0:
+            print(f"[mxtrain] {e}; pipeline p2p uses RCCL", flush=True)
+        c = None
+    _P2PS[key] = c
+    return c
+
+
 _COMMS: Dict[int, Optional[XGMICommunicator]] = {}
 
 
@@ -564,7 +725,8 @@ def route(group, t: torch.Tensor, op: str, nbytes: int) -> Optional[XGMICommunic
 
 
 def destroy_all():
-    for c in _COMMS.values():
+    for c in list(_COMMS.values()) + list(_P2PS.values()):
         if c is not None:
             c.close()
     _COMMS.clear()
+    _P2PS.clear()
