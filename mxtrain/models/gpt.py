@@ -283,18 +283,10 @@ class StepRuntime:
     unit_done: Optional[Callable[[int], None]] = None
     before_unit: Optional[Callable[[int], None]] = None   # wait for the unit's params (AG overlap)
     grad_scale: float = 1.0       # loss gradient scale (1 / tokens / microbatches)
-    # weight-gradient GEMMs run on this side stream, concurrently with the dgrad GEMM and
-    # the memory-bound backward kernels of the main stream (None: inline)
-    wgrad_stream: Optional[object] = None
-    _wgrad_live: bool = False
     # the first micro-batch of a step WRITES the weight gradients (GEMM beta = 0) instead of
     # accumulating into a zero-filled buffer (set by the trainer, which then zeroes only the
     # other gradients)
     wgrad_overwrite: bool = False
-    # optional side stream for work that depends only on the step seed (attention-dropout
-    # mask generation) to overlap the layer's QKV GEMM; off by default (MXTRAIN_AUX_STREAM=1):
-    # measured on one MI355X the concurrent generator slowed the GEMM by more than it hid
-    aux_stream: Optional[object] = None
     # MoE: this rank's experts (separate flat buffer), the EP group, aux-loss gradient
     eparams: Optional[Dict[str, torch.Tensor]] = None
     egrads: Optional[Dict[str, torch.Tensor]] = None
@@ -323,7 +315,6 @@ class StepRuntime:
     # and GeLU' + bias-gradient epilogues fused (ops/gemm.py linear_fwd / linear_dgrad);
     # False: hipBLASLt + the separate bias-GeLU kernels (the LM head always uses hipBLASLt)
     fused_linear: bool = True
-    side_dmasks: bool = False     # layers 1.. of the batched masks on aux_stream (MXTRAIN_SIDE_DMASKS)
 
     @property
     def p_drop(self):
@@ -360,29 +351,10 @@ class StepRuntime:
     def wgrad(self, *items):
         """gbuf (+)= dy^T x for every (gbuf, dy, x) -- one grouped MFMA launch
         (ops/gemm.py: the layer's weight gradients that become ready together).  Written
-        (beta = 0) on the first micro-batch when ``wgrad_overwrite``.  On the side stream
-        when enabled: it forks from the main stream here and is joined in done() (before
-        the unit's gradient bucket can be reduced); every operand stays referenced by the
-        caller's frame until then, so the caching allocator cannot hand its memory to
-        main-stream work that is unordered with the side-stream GEMM."""
-        acc = not self.wgrad_overwrite
-        ws = self.wgrad_stream
-        if ws is None:
-            wgrad_group(items, accumulate=acc)
-            return
-        main = torch.cuda.current_stream(items[0][0].device)
-        ws.wait_stream(main)
-        with torch.cuda.stream(ws):
-            wgrad_group(items, accumulate=acc)
-        self._wgrad_live = True
-
-    def join_wgrad(self):
-        if self._wgrad_live:
-            torch.cuda.current_stream().wait_stream(self.wgrad_stream)
-            self._wgrad_live = False
+        (beta = 0) on the first micro-batch when ``wgrad_overwrite``."""
+        wgrad_group(items, accumulate=not self.wgrad_overwrite)
 
     def done(self, unit):
-        self.join_wgrad()
         if self.unit_done is not None:
             self.unit_done(unit)
 
@@ -578,14 +550,12 @@ class GPTLayerFn(torch.autograd.Function):
             # this micro-batch's masks, all layers at once
             dmask = rt.dmasks[i - rt.dmask_l0]
         elif rt.p_attn > 0:
-            # the keep-mask depends only on the seed: generated on the side stream while the
-            # QKV GEMM runs (the GEMM's grid leaves CUs free)
+            # (unbatched: this layer's keep-mask alone)
             ha_ = hl // rt.cp
             dmask = attn_ops.dropmask(rt.B, rt.S * rt.cp, ha_, rt.p_attn,
                                       rt.attn_seed_t if rt.attn_seed_t is not None else rt.seed_t,
                                       salt=rt.attn_salt(i, micro), head_offset=rt.tp_rank * hl + rt.cp_rank * ha_,
-                                      total_heads=cfg.num_attention_heads, causal=True, device=a.device,
-                                      stream=rt.aux_stream)
+                                      total_heads=cfg.num_attention_heads, causal=True, device=a.device)
         a_full, qkv = _gather_mm(a, P[p + "qkv_w"], rt, bias=P[p + "qkv_b"])
         if rt.cp > 1:   # Ulysses: whole sequences, 1/cp of the heads
             qkv_a = seq_to_head(qkv, (hl * D, kvl * D, kvl * D), rt.B, rt.S, rt.cp_group)
@@ -818,9 +788,6 @@ class GPTStage:
                               attn_seed_t=attn_seed_t)
         ov = os.environ.get("MXTRAIN_TP_OVERLAP", "1") == "1"
         self.rt.tp_overlap = self.rt.sp_gemm_overlap = ov
-        dev = next(iter(params.values())).device if params else None
-        if dev is not None and dev.type == "cuda" and os.environ.get("MXTRAIN_AUX_STREAM", "0") == "1":
-            self.rt.aux_stream = torch.cuda.Stream(device=dev)
         if cfg.num_experts > 1:
             assert tp == 1, "MoE layers run with tensor-parallel size 1 (expert parallelism instead)"
         if cp > 1:
@@ -876,8 +843,7 @@ class GPTStage:
                                                  rt.attn_seed_t if rt.attn_seed_t is not None else rt.seed_t,
                                                  rt.attn_salt(self.l0, micro), self.l1 - self.l0,
                                                  head_offset=rt.tp_rank * hl + rt.cp_rank * ha_,
-                                                 total_heads=cfg.num_attention_heads, causal=True,
-                                                 stream=rt.aux_stream if rt.side_dmasks else None)
+                                                 total_heads=cfg.num_attention_heads, causal=True)
         for i in range(self.l0, self.l1):
             if i + 1 < self.l1:
                 nxt = f"layers.{i + 1}.ln1"

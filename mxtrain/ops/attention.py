@@ -113,10 +113,8 @@ class DropMask:
 
 
 def dropmask(B, S, Hq, p, seed_t, salt=0, head_offset=0, total_heads=None, causal=True,
-             device=None, stream=None) -> DropMask:
-    """Generate the keep-mask images.  With ``stream`` the generator runs there (it depends
-    only on the seed, so it overlaps the QKV projection GEMM, which leaves CUs idle); the
-    consumer joins through the returned event (DropMask.ready)."""
+             device=None) -> DropMask:
+    """Generate the keep-mask images of one attention call."""
     device = device if device is not None else seed_t.device
     if device.type != "cuda" or not _lib.use_hip(seed_t):
         keep = dropout_keep_mask(B, S, Hq, int(seed_t.reshape(-1)[0]), salt, p, head_offset, total_heads, device)
@@ -124,29 +122,17 @@ def dropmask(B, S, Hq, p, seed_t, salt=0, head_offset=0, total_heads=None, causa
     NB, NKT, NQT = (S + 31) // 32, (S + 127) // 128, (S + 63) // 64
     fbits = torch.empty(B * Hq * NB * NKT * 64, dtype=torch.int64, device=device)
     bbits = torch.empty(B * Hq * NB * NQT * 64, dtype=torch.int32, device=device)
-    args = (_lib.ptr(seed_t), int(salt) & M32, float(p), B, S, Hq, int(head_offset),
-            int(total_heads or Hq), int(causal), _lib.ptr(fbits), _lib.ptr(bbits))
-    if stream is None:
-        _lib.call("mx_flash_dropmask", *args, _lib.stream())
-        return DropMask(p, fbits, bbits)
-    main = torch.cuda.current_stream(device)
-    stream.wait_stream(main)            # the seed is advanced on the main stream
-    with torch.cuda.stream(stream):
-        _lib.call("mx_flash_dropmask", *args, _lib.stream())
-        ev = torch.cuda.Event()
-        ev.record(stream)
-    return DropMask(p, fbits, bbits, event=ev)
+    _lib.call("mx_flash_dropmask", _lib.ptr(seed_t), int(salt) & M32, float(p), B, S, Hq, int(head_offset),
+              int(total_heads or Hq), int(causal), _lib.ptr(fbits), _lib.ptr(bbits), _lib.stream())
+    return DropMask(p, fbits, bbits)
 
 
 def dropmask_layers(B, S, Hq, p, seed_t, salt, L, head_offset=0, total_heads=None, causal=True,
-                    device=None, stream=None):
+                    device=None):
     """The keep-mask images of L consecutive layers (salts salt .. salt + L - 1) in ONE
     launch -- identical to L dropmask() calls; a step's masks depend only on its seed, so
     the model generates them all before the first layer (one launch instead of one per
-    layer, and the single large grid keeps the chip full).  With ``stream``: the first
-    layer's images on the current stream, the other L - 1 layers' in one launch on
-    ``stream`` (VALU-bound hashing beside the first layers' MFMA-bound GEMMs), joined
-    through a shared event at each later layer's first use.  Returns [DropMask] * L."""
+    layer, and the single large grid keeps the chip full).  Returns [DropMask] * L."""
     device = device if device is not None else seed_t.device
     if device.type != "cuda" or not _lib.use_hip(seed_t):
         return [dropmask(B, S, Hq, p, seed_t, salt + l, head_offset, total_heads, causal, device) for l in range(L)]
@@ -154,29 +140,16 @@ def dropmask_layers(B, S, Hq, p, seed_t, salt, L, head_offset=0, total_heads=Non
     nf, nb = B * Hq * NB * NKT * 64, B * Hq * NB * NQT * 64
     fbits = torch.empty(L, nf, dtype=torch.int64, device=device)
     bbits = torch.empty(L, nb, dtype=torch.int32, device=device)
-
-    def launch(l0, n):
-        _lib.call("mx_flash_dropmask_layers", _lib.ptr(seed_t), (int(salt) + l0) & M32, float(p), B, S, Hq,
-                  int(head_offset), int(total_heads or Hq), int(causal), n, _lib.ptr(fbits[l0]), _lib.ptr(bbits[l0]),
-                  2 * nf, nb, _lib.stream())
-
-    if stream is None or L < 2:
-        launch(0, L)
-        return [DropMask(p, fbits[l], bbits[l]) for l in range(L)]
-    launch(0, 1)
-    main = torch.cuda.current_stream(device)
-    stream.wait_stream(main)            # the seed is advanced on the main stream
-    with torch.cuda.stream(stream):
-        launch(1, L - 1)
-        ev = torch.cuda.Event()
-        ev.record(stream)
-    return [DropMask(p, fbits[0], bbits[0])] + [DropMask(p, fbits[l], bbits[l], event=ev) for l in range(1, L)]
+    _lib.call("mx_flash_dropmask_layers", _lib.ptr(seed_t), int(salt) & M32, float(p), B, S, Hq,
+              int(head_offset), int(total_heads or Hq), int(causal), L, _lib.ptr(fbits[0]), _lib.ptr(bbits[0]),
+              2 * nf, nb, _lib.stream())
+    return [DropMask(p, fbits[l], bbits[l]) for l in range(L)]
 
 
 def attn_fwd(q, k, v, B, S, Hq, Hkv, D, causal=True, klen=None, scale=None, dropout_p=0.0,
              seed_t=None, salt=0, head_offset=0, total_heads=None, dmask=None):
     """Returns (o, lse, dmask): dmask is the DropMask backward needs (None without dropout).
-    A pre-generated ``dmask`` (see dropmask(stream=...)) is used as is."""
+    A pre-generated ``dmask`` (dropmask / dropmask_layers) is used as is."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     drop = dropout_p > 0.0 or dmask is not None
     if drop and dmask is None:

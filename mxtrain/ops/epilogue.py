@@ -141,67 +141,12 @@ def bias_act(y: torch.Tensor, b: Optional[torch.Tensor], residual: Optional[torc
     return F.relu(y) if relu else y
 
 
-# off by default: measured on one MI355X (Mask R-CNN, 4 img/GPU) 129 img/s with the GEMM path vs
-# 145.6 with MIOpen -- the weight-gradient GEMMs (K = N*H*W, up to 268k) lose to its wrw solvers
-_GEMM_1X1 = os.environ.get("MXTRAIN_CONV1X1_GEMM", "0") == "1"
-
-
-def _as_int(v):
-    return v if isinstance(v, int) else (v[0] if all(e == v[0] for e in v) else None)
-
-
-def _rows(t: torch.Tensor) -> torch.Tensor:
-    """[N, C, H, W] channels_last -> its [N*H*W, C] row-major view."""
-    N, C, H, W = t.shape
-    return t.permute(0, 2, 3, 1).reshape(N * H * W, C)
-
-
-class Conv1x1Fn(torch.autograd.Function):
-    """A stride-1 1x1 convolution of an NHWC tensor IS a GEMM over the N*H*W rows:
-    y[M, Cout] = x[M, Cin] @ w[Cout, Cin]^T; backward dx = dy @ w, dw = dy^T @ x -- three
-    hipBLASLt GEMMs, no MIOpen solver, workspace zero-fill, cast or layout-transpose helper
-    kernels.  The output is a standalone channels_last tensor (the epilogue then works in
-    place on it)."""
-
-    @staticmethod
-    def forward(ctx, x, w):
-        N, C, H, W = x.shape
-        y = torch.empty((N, w.shape[0], H, W), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-        torch.mm(_rows(x), w.reshape(w.shape[0], C).t(), out=_rows(y))
-        ctx.save_for_backward(x, w)
-        return y
-
-    @staticmethod
-    def backward(ctx, g):
-        x, w = ctx.saved_tensors
-        if not _nhwc(g):
-            g = g.contiguous(memory_format=torch.channels_last)
-        g2 = _rows(g)
-        w2 = w.reshape(w.shape[0], x.shape[1])
-        dx = dw = None
-        if ctx.needs_input_grad[0]:
-            dx = torch.empty_like(x, memory_format=torch.channels_last)
-            torch.mm(g2, w2, out=_rows(dx))
-        if ctx.needs_input_grad[1]:
-            dw = torch.mm(g2.t(), _rows(x)).view(w.shape)
-            if dw.stride() != w.stride():
-                dw = dw.contiguous(memory_format=torch.channels_last) if w.is_contiguous(
-                    memory_format=torch.channels_last) else dw.contiguous()
-        return dx, dw
-
-
-def conv1x1_gemm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    return Conv1x1Fn.apply(x, w)
-
 
 def conv_bias_act(x, w, b=None, stride=1, padding=0, dilation=1, relu: bool = False,
                   residual: Optional[torch.Tensor] = None) -> torch.Tensor:
     """act(conv2d(x, w) + b (+ residual)) -- one conv (MIOpen forward and input gradient;
     the weight gradient from csrc/convwg.hip where it tiles) + one fused epilogue pass."""
     if _fused_ok(x, b, residual) and x.shape[1] == w.shape[1]:
-        if (_GEMM_1X1 and w.shape[2] == 1 and w.shape[3] == 1 and _as_int(stride) == 1 and _as_int(padding) == 0
-                and w.dtype == x.dtype):
-            return bias_act(conv1x1_gemm(x, w), b, residual, relu)
         if convwg.fwd_supported(x, w, b, residual, stride, padding, dilation):
             # forward, input and weight gradients all implicit GEMMs (ops/convwg.py)
             return ConvBiasActFn.apply(x, w, b, residual, relu, stride, padding, dilation)

@@ -60,8 +60,7 @@ class DistributedOptimizer:
                  tp_group=None, sp_group=None, mp_group=None, embed_group=None,
                  pp_rank: int = 0, schedule: Optional[LRSchedule] = None,
                  overlap_param_gather: Optional[bool] = None,
-                 grad_scale_world: Optional[int] = None, norm_groups=(),
-                 overlap_update: bool = False):
+                 grad_scale_world: Optional[int] = None, norm_groups=()):
         self.flat = flat
         self.dp_group = dp_group
         self.world = dist.get_world_size(dp_group) if dp_group is not None else 1
@@ -149,18 +148,6 @@ class DistributedOptimizer:
         self.gather_pending = False
         self._gather_events: Dict[int, object] = {}
         self._last_event = None
-        # Deferred AdamW (overlap_update): step() ends after the gradient norm; the update
-        # itself runs at the start of the next step, bucket by bucket in forward order on
-        # a side stream, so each bucket's memory-bound AdamW overlaps the MFMA-bound
-        # forward of the layers before it (the layers wait on their bucket's event, as
-        # for the deferred all-gather).  The step's hyper-parameters and clip norm are
-        # snapshotted on the device, so the result is bit-identical to the eager order.
-        self.overlap_update = bool(overlap_update)
-        self.update_pending = False
-        self.hyper_pending = torch.zeros_like(self.hyper)
-        self.update_stream = None
-        if self.overlap_update and dev.type == "cuda":
-            self.update_stream = self.comm_stream or torch.cuda.Stream(device=dev)
 
     # ------------------------------------------------------------------ helpers
     def _shard_of(self, per_chunk: torch.Tensor) -> torch.Tensor:
@@ -340,36 +327,11 @@ class DistributedOptimizer:
         self.step_count += 1
         self.set_hyper(lr if lr is not None else self.schedule(self.step_count))
         normsq = self.grad_norm_sq()
-        if self.overlap_update:
-            self.defer_update()
-            self.reset_pending()
-            return normsq
         optim_ops.adamw_step(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
                              self.param_shard, self.hyper, normsq=normsq, wd_flags=self.wd_flags)
         self.gather_params()
         self.reset_pending()
         return normsq
-
-    def defer_update(self):
-        """Mark this step's AdamW pending (overlap_update): snapshot its hyper-parameters;
-        the clip norm stays in ``normsq`` until the next step's update has read it."""
-        self.hyper_pending.copy_(self.hyper)
-        self.update_pending = True
-
-    @property
-    def zeroes_grads(self) -> bool:
-        """True when begin_param_gather() will zero the flat gradient buffer itself (a
-        pending single-replica update reads the gradients in place, bucket by bucket)."""
-        return self.update_pending and self.world == 1
-
-    def _update_slice(self, bi: int):
-        b, fs, so, n = self.slices[bi]
-        c0, c1 = so // ALIGN, (so + n) // ALIGN
-        optim_ops.adamw_step(self.master[so:so + n], self.exp_avg[so:so + n], self.exp_avg_sq[so:so + n],
-                             self.grad_shard[so:so + n], self.param_shard[so:so + n], self.hyper_pending,
-                             normsq=self.normsq, wd_flags=self.wd_flags[c0:c1])
-        if self.world == 1:
-            self.flat.zero_grad_range(b.start, b.end)
 
     # ------------------------------------------------------------------ param all-gather
     def gather_params(self):
@@ -384,17 +346,15 @@ class DistributedOptimizer:
             self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n], so)
 
     def begin_param_gather(self):
-        """Start the work deferred from the previous step, per bucket in forward order:
-        the pending AdamW update (overlap_update) and/or the parameter all-gather
-        (overlap_param_gather).  On the GPU it runs on a side stream and records one event
-        per bucket for wait_unit(); on the CPU it runs inline."""
-        upd = self.update_pending
-        gat = (self.gather_pending or upd) and self.world > 1   # new shards must be gathered
-        self.update_pending = self.gather_pending = False
-        if not (upd or gat):
+        """Start the parameter all-gather deferred from the previous step
+        (overlap_param_gather), per bucket in forward order.  On the GPU it runs on the comm
+        stream and records one event per bucket for wait_unit(); on the CPU it runs inline."""
+        gat = self.gather_pending and self.world > 1
+        self.gather_pending = False
+        if not gat:
             return
         cuda = self.device.type == "cuda"
-        side = (self.update_stream if upd else self.comm_stream) if cuda else None
+        side = self.comm_stream if cuda else None
         ev0 = torch.cuda.current_stream(self.device).record_event() if side is not None else None
         # buckets are laid out last-layer-first; the forward needs them in reverse order
         for bi in reversed(range(len(self.slices))):
@@ -402,16 +362,10 @@ class DistributedOptimizer:
             if side is not None:
                 with torch.cuda.stream(side):
                     side.wait_event(ev0)
-                    if upd:
-                        self._update_slice(bi)
-                    if gat:
-                        self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n], so)
+                    self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n], so)
                     self._gather_events[bi] = self._last_event = side.record_event()
             else:
-                if upd:
-                    self._update_slice(bi)
-                if gat:
-                    self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n], so)
+                self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n], so)
 
     def wait_unit(self, unit: int):
         bi = self.flat.unit_to_bucket.get(unit)
@@ -420,9 +374,8 @@ class DistributedOptimizer:
             torch.cuda.current_stream(self.device).wait_event(ev)
 
     def wait_all(self):
-        """Order the current stream after every bucket's deferred work (the side stream
-        is in order, so its last event covers all of them): called before the backward,
-        which rewrites the gradients a pending update reads."""
+        """Order the current stream after every bucket's deferred all-gather (the comm
+        stream is in order, so its last event covers all of them)."""
         self._gather_events.clear()
         if self._last_event is not None:
             torch.cuda.current_stream(self.device).wait_event(self._last_event)
@@ -444,7 +397,6 @@ class DistributedOptimizer:
         self.exp_avg.copy_(sd["exp_avg"])
         self.exp_avg_sq.copy_(sd["exp_avg_sq"])
         self.step_count = int(sd["step"])
-        self.update_pending = False
         # re-materialise bf16 params from the master shard
         for (b, fs, so, n) in self.slices:
             self.param_shard[so:so + n].copy_(self.master[so:so + n].to(self.flat.dtype))

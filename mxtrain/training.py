@@ -43,14 +43,6 @@ class TrainConfig:
     overlap_grad_reduce: bool = True
     bucket_numel: int = 40_000_000
     capture_graph: bool = False
-    # AdamW of step N runs at the start of step N+1, per bucket on a side stream,
-    # overlapped with the forward (DistributedOptimizer overlap_update; GPU, pp = 1, dense,
-    # not combined with wgrad_stream).  Off by default: at GPT-2 345M on one MI355X the
-    # memory-bound update slows the concurrent forward GEMMs by more than it hides
-    overlap_optimizer: bool = False
-    # weight-gradient GEMMs on a side HIP stream (GPU only).  Off by default: measured no
-    # gain at GPT-2 345M (19.97 vs 19.81 ms/step) -- hipBLASLt tiles already occupy every CU
-    wgrad_stream: bool = False
     # the first micro-batch's weight-gradient GEMMs write their gradients (beta = 0), so the
     # per-step zero-fill covers only the other ~1 % of the flat gradient buffer (pp = 1)
     overwrite_wgrads: bool = True
@@ -86,10 +78,7 @@ class GPTTrainer:
                               attn_seed_t=self.seed.attn_t)
         self.stage.rt.micro_base = ps.dp_rank * self.num_micro   # global micro-batch index base
         self.stage.rt.batch_dmasks = os.environ.get("MXTRAIN_BATCH_DMASKS", "1") != "0"
-        self.stage.rt.side_dmasks = os.environ.get("MXTRAIN_SIDE_DMASKS", "0") == "1"
         self.stage.rt.fused_linear = tcfg.fused_linear
-        if tcfg.wgrad_stream and self.device.type == "cuda":
-            self.stage.rt.wgrad_stream = torch.cuda.Stream(device=self.device)
         self._overwrite = bool(tcfg.overwrite_wgrads and ps.pp == 1)
         if self._overwrite:
             self.flat.set_overwritten(self.stage.gemm_grad_names())
@@ -106,15 +95,13 @@ class GPTTrainer:
             sp_group=ps.tp_group if ps.sequence_parallel else None,
             mp_group=ps.mp_group if ps.tp * ps.pp > 1 else None,
             embed_group=ps.embed_group if ps.pp > 1 and cfg.tie_embeddings else None,
-            pp_rank=ps.pp_rank, schedule=sched,
-            overlap_update=(tcfg.overlap_optimizer and self.device.type == "cuda" and ps.pp == 1
-                            and self.eopt is None and not tcfg.wgrad_stream))
+            pp_rank=ps.pp_rank, schedule=sched)
         self._setup_xgmi()
         # LN / bias gradient column reductions deferred and batched: ~100 colreduce launches
         # of a GPT-2 step become one at the end of backward (one rank), or one per gradient
         # bucket right before its reduce-scatter is issued (data parallel)
         if (self.device.type == "cuda" and ps.tp == 1 and ps.pp == 1 and self.eopt is None
-                and not self.opt.overlap_update and os.environ.get("MXTRAIN_DEFER_COLREDUCE", "1") != "0"):
+                and os.environ.get("MXTRAIN_DEFER_COLREDUCE", "1") != "0"):
             from .ops.norm import ColReduceQueue
             group_of = None
             if ps.grad_world > 1:
@@ -205,8 +192,6 @@ class GPTTrainer:
         else:
             rt.unit_done = self.opt.unit_done if last_micro else None
         loss = self.stage.forward(ids=ids, labels=labels, B=B, S=S, micro=micro)
-        if self.opt.overlap_update and self.device.type == "cuda":
-            self.opt.wait_all()   # deferred AdamW read/zeroed the grads the backward writes
         loss.backward()
         return loss.detach()
 
@@ -228,9 +213,7 @@ class GPTTrainer:
         also under context parallelism).  Returns the mean loss over the step as a device
         scalar (last stage; 0 elsewhere)."""
         tokens, labels = self._local(tokens), self._local(labels)
-        # the captured body starts with the previous step's deferred update: replay only
-        # when one is pending (after a sync_params() flush, one eager step re-arms it)
-        if self._graph is not None and all(o.update_pending or not o.overlap_update for o in self._opts):
+        if self._graph is not None:
             self._static[0].copy_(tokens)
             self._static[1].copy_(labels)
             for o in self._opts:
@@ -243,7 +226,6 @@ class GPTTrainer:
             # sync_params(), gathers it; re-gathering an unchanged shard is idempotent)
             for o in self._opts:
                 o.gather_pending = o.overlap_param_gather
-                o.update_pending = o.overlap_update
             self.iteration += 1
             return self._static_loss
         return self._train_step_eager(tokens, labels)
@@ -253,10 +235,8 @@ class GPTTrainer:
         return [self.opt] + ([self.eopt] if self.eopt is not None else [])
 
     def _prepare_step(self, nm, B, S):
-        zeroed = self.opt.zeroes_grads   # (a deferred update zeroes each bucket after reading it)
         self._begin_step()
-        if not zeroed:
-            self.flat.zero_grad()
+        self.flat.zero_grad()
         if self.eflat is not None:
             self.eflat.zero_grad()
             self.stage.rt.aux_scale = self.cfg.moe_loss_coeff / nm
@@ -269,8 +249,8 @@ class GPTTrainer:
 
     def _train_step_eager(self, tokens, labels):
         nm, B, S = tokens.shape
-        if self.ckpt_fence is not None and any(o.overlap_update or o.overlap_param_gather for o in self._opts):
-            self.ckpt_fence()   # the deferred update / parameter gather runs at the step's start
+        if self.ckpt_fence is not None and any(o.overlap_param_gather for o in self._opts):
+            self.ckpt_fence()   # the deferred parameter gather runs at the step's start
         self._prepare_step(nm, B, S)
         if self.pipeline is not None:
             loss = self.pipeline.run(tokens, labels)
@@ -332,7 +312,6 @@ class GPTTrainer:
         # the captured step starts by gathering the shards the previous replay updated
         for o in self._opts:
             o.gather_pending = o.overlap_param_gather
-            o.update_pending = o.overlap_update
         self._prepare_step(nm, B, S)
         if self.pipeline is not None:
             loss = self.pipeline.run(tokens, labels)
@@ -345,14 +324,8 @@ class GPTTrainer:
         if self.stage.rt.colq is not None:
             self.stage.rt.colq.flush()
         # optimizer body without host-side hyper update (done before each replay)
-        if self.opt.overlap_update:
-            # (dense only) grad norm now, AdamW deferred into the next replay's body
-            self.opt.finish_grads()
-            self.opt.grad_norm_sq()
-            self.opt.defer_update()
-        else:
-            from .parallel.zero import joint_update
-            joint_update(self._opts)
+        from .parallel.zero import joint_update
+        joint_update(self._opts)
         for o in self._opts:
             o.gather_pending = False   # (overlap mode) the next replay's body gathers
             o._gather_events.clear()
@@ -367,7 +340,7 @@ class GPTTrainer:
     def _begin_step(self):
         for o in self._opts:
             o.begin_param_gather()
-        if any(o.overlap_param_gather or o.overlap_update for o in self._opts):
+        if any(o.overlap_param_gather for o in self._opts):
             self.stage.rt.before_unit = self._wait_unit_all if self.eopt is not None else self.opt.wait_unit
         else:
             self.stage.rt.before_unit = None

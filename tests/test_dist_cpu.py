@@ -96,9 +96,6 @@ def _worker(rank, world, port, mode, q):
     if ps.dp > 1:
         # exercise the deferred (next-step, per-bucket) ZeRO-1 parameter all-gather path
         tr.opt.overlap_param_gather = True
-    if pp == 1 and mode != "moe":
-        # and the deferred AdamW (next step, per bucket, before each layer's forward)
-        tr.opt.overlap_update = True
     local = shard_gpt_state(init_sd, cfg, ps.tp, ps.tp_rank, ps.pp, ps.pp_rank)
     tr.flat.load_state_dict(local)
     tr.opt._refresh_master()
@@ -117,33 +114,6 @@ def _worker(rank, world, port, mode, q):
 
 
 _REF = {}
-
-
-def test_deferred_update_matches_eager_single():
-    """overlap_update (AdamW of step N applied per bucket at the start of step N+1, then
-    flushed by sync_params) gives exactly the eager optimizer's parameters and state."""
-    from mxtrain.models.gpt import GPTConfig
-    from mxtrain.parallel.state import ParallelState
-    from mxtrain.training import GPTTrainer, TrainConfig
-    cfg = GPTConfig(**CFG)
-    tok, lab = _data()
-    out = []
-    for defer in (False, True):
-        tcfg = TrainConfig(micro_batch_size=2, global_batch_size=4, lr=1e-3, overlap_grad_reduce=False,
-                           bucket_numel=20_000)
-        tr = GPTTrainer(cfg, tcfg, ParallelState(), dtype=torch.float32)
-        assert len(tr.flat.buckets) > 2
-        tr.opt.overlap_update = defer
-        losses = [float(tr.train_step(tok, lab)) for _ in range(3)]
-        if defer:
-            assert tr.opt.update_pending
-        tr.sync_params()
-        assert not tr.opt.update_pending
-        out.append((losses, tr.flat.data.clone(), tr.opt.exp_avg_sq.clone(), tr.opt.step_count))
-    (l0, p0, v0, c0), (l1, p1, v1, c1) = out
-    assert l0 == l1 and c0 == c1 == 3
-    assert torch.equal(p0, p1) and torch.equal(v0, v1)
-    # the flush zeroed the gradients it consumed; a further step still matches
 
 
 def _ref_init(ccfg=CFG):
