@@ -1,0 +1,413 @@
+// Training-mode BatchNorm for NHWC (channels_last) bf16 CNNs, fused with the residual add
+// and the ReLU that follow it in a ResNet bottleneck (BASELINE.json config 5: the Ray Train
+// PyTorch-Lightning ResNet-50, /root/reference/charts/machine-learning/training/raytrain/
+// templates/train.yaml:142-221):
+//
+//   forward   y = act(x * scale[c] + shift[c] (+ res)),  scale = gamma * rstd,
+//             shift = beta - mean * scale,  batch statistics over the N*H*W rows
+//   backward  dz = dy * (y > 0) (ReLU) ;  dres = dz ;  dbeta = sum dz ;  dgamma = sum dz xhat
+//             dx = gamma rstd (dz - dbeta / M - xhat dgamma / M)
+//
+// Layout: [M, C] with M = N*H*W rows (NHWC memory), C % 8 == 0, 16-B vectors (8 bf16) per
+// lane.  Every reduction is two-stage and deterministic: a statistics pass writes per-block
+// partials (fixed row stripes), a per-channel finalize merges them in block order -- no
+// atomics, the same bits on every run.  The forward statistics are merged as (count, mean,
+// M2) with Chan's formula (no E[x^2] - E[x]^2 cancellation over ~10^6 rows); a thread's own
+// rows (<= rows_per_block / rows-per-iteration) use plain sums.
+//
+// Five launches per BN layer (stats, finalize, apply; bwd stats, bwd finalize, bwd apply)
+// where torch's NHWC path takes a statistics kernel, an elementwise kernel and separate
+// add / ReLU passes forward and the same again backward.
+#include "common.h"
+
+using namespace mx;
+
+namespace {
+
+constexpr int kThreads = 256;
+
+struct RowGeo {   // 256 threads = rpi rows x cv 8-channel vectors of a row
+  int c8, cv, rpi, tr, tv;
+  __device__ RowGeo(int C) {
+    c8 = C / 8;
+    cv = c8 < kThreads ? c8 : kThreads;
+    rpi = kThreads / cv;
+    tr = threadIdx.x / cv;
+    tv = threadIdx.x % cv;
+  }
+};
+
+// Chan's parallel merge of (n, mean, M2) into (na, ma, m2a)
+__device__ __forceinline__ void chan_merge(float& na, float& ma, float& m2a, float nb, float mb, float m2b) {
+  const float n = na + nb;
+  if (nb == 0.f) return;
+  const float d = mb - ma;
+  const float f = nb / n;
+  ma += d * f;
+  m2a += m2b + d * d * na * f;
+  na = n;
+}
+
+// pmean / pm2: [nblk][C] per-block statistics; pcount: rows of block b (computed by the
+// finalize).  grid: (ceil(c8 / cv), nblk)
+__global__ __launch_bounds__(kThreads) void bn_stats_kernel(const uint16_t* __restrict__ x, int M, int C,
+                                                            int rows_per_block, float* __restrict__ pmean,
+                                                            float* __restrict__ pm2) {
+  const RowGeo g(C);
+  const int vc = blockIdx.x * g.cv + g.tv;            // this thread's 8-channel vector
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  __shared__ float sm[3][kThreads][8];
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int n = 0;
+  if (vc < g.c8) {
+    for (int r = r0 + g.tr; r < r1; r += g.rpi) {
+      float v[8];
+      unpack8(reinterpret_cast<const uint4*>(x + (size_t)r * C)[vc], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += v[j];
+        q[j] = __builtin_fmaf(v[j], v[j], q[j]);
+      }
+      ++n;
+    }
+  }
+  // per-thread (n, mean, M2), merged over the block's row groups in order by row group 0
+  const float fn = (float)n;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float m = n ? s[j] / fn : 0.f;
+    sm[0][threadIdx.x][j] = fn;
+    sm[1][threadIdx.x][j] = m;
+    sm[2][threadIdx.x][j] = n ? fmaxf(q[j] - s[j] * m, 0.f) : 0.f;
+  }
+  __syncthreads();
+  if (g.tr == 0 && vc < g.c8) {
+    float na[8], ma[8], m2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      na[j] = sm[0][threadIdx.x][j];
+      ma[j] = sm[1][threadIdx.x][j];
+      m2[j] = sm[2][threadIdx.x][j];
+    }
+    for (int k = 1; k < g.rpi; ++k) {
+      const int t = k * g.cv + g.tv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) chan_merge(na[j], ma[j], m2[j], sm[0][t][j], sm[1][t][j], sm[2][t][j]);
+    }
+    float* pmr = pmean + (size_t)blockIdx.y * C + 8 * vc;
+    float* pqr = pm2 + (size_t)blockIdx.y * C + 8 * vc;
+#pragma unroll
+    for (int j = 0; j < 8; j += 4) {
+      *reinterpret_cast<float4*>(pmr + j) = make_float4(ma[j], ma[j + 1], ma[j + 2], ma[j + 3]);
+      *reinterpret_cast<float4*>(pqr + j) = make_float4(m2[j], m2[j + 1], m2[j + 2], m2[j + 3]);
+    }
+  }
+}
+
+// one wave per channel: lane l merges blocks l, l + 64, ... in order, then a fixed
+// butterfly over the lanes (deterministic).  Outputs: mean / rstd (saved for backward),
+// scale / shift (fp32, for the apply pass), running statistics updated in place.
+__global__ __launch_bounds__(kThreads) void bn_finalize_kernel(const float* __restrict__ pmean,
+                                                               const float* __restrict__ pm2, int nblk,
+                                                               int rows_per_block, int M, int C,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, float eps,
+                                                               float momentum, float* __restrict__ mean_out,
+                                                               float* __restrict__ rstd_out,
+                                                               float* __restrict__ scale, float* __restrict__ shift,
+                                                               float* __restrict__ run_mean,
+                                                               float* __restrict__ run_var) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  if (c >= C) return;
+  float na = 0.f, ma = 0.f, m2 = 0.f;
+  for (int b = lane; b < nblk; b += 64) {
+    const float nb = (float)min(rows_per_block, M - b * rows_per_block);
+    chan_merge(na, ma, m2, nb, pmean[(size_t)b * C + c], pm2[(size_t)b * C + c]);
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float nb = __shfl_xor(na, o), mb = __shfl_xor(ma, o), m2b = __shfl_xor(m2, o);
+    // both partners compute the same merged value: order the operands by lane bit
+    if (lane & o) {
+      float n2 = nb, m_2 = mb, q2 = m2b;
+      chan_merge(n2, m_2, q2, na, ma, m2);
+      na = n2; ma = m_2; m2 = q2;
+    } else {
+      chan_merge(na, ma, m2, nb, mb, m2b);
+    }
+  }
+  if (lane == 0) {
+    const float var = m2 / (float)M;
+    const float rs = rsqrtf(var + eps);
+    const float sc = gamma[c] * rs;
+    mean_out[c] = ma;
+    rstd_out[c] = rs;
+    scale[c] = sc;
+    shift[c] = beta[c] - ma * sc;
+    if (run_mean) {
+      const float unb = M > 1 ? m2 / (float)(M - 1) : var;
+      run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * ma;
+      run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+    }
+  }
+}
+
+// y = act(x * scale + shift (+ res)); one thread per 8-channel vector
+template <bool kRes, bool kRelu>
+__global__ __launch_bounds__(kThreads) void bn_apply_kernel(const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ res,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift,
+                                                            uint16_t* __restrict__ y, int64_t nvec, int c8) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const int c = 8 * (int)(v % c8);
+    float a[8], r[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[v], a);
+    if (kRes) unpack8(reinterpret_cast<const uint4*>(res)[v], r);
+    const float4 s0 = *reinterpret_cast<const float4*>(scale + c), s1 = *reinterpret_cast<const float4*>(scale + c + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(shift + c), h1 = *reinterpret_cast<const float4*>(shift + c + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = __builtin_fmaf(a[j], sc[j], sh[j]);
+      if (kRes) t += r[j];
+      a[j] = kRelu ? fmaxf(t, 0.f) : t;
+    }
+    reinterpret_cast<uint4*>(y)[v] = pack8(a);
+  }
+}
+
+// backward statistics: per-block column sums of dz and dz * xhat, partial [nblk][2][C]
+template <bool kRelu>
+__global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const uint16_t* __restrict__ dy,
+                                                                const uint16_t* __restrict__ y,
+                                                                const uint16_t* __restrict__ x,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd, int M, int C,
+                                                                int rows_per_block, float* __restrict__ partial) {
+  const RowGeo g(C);
+  const int vc = blockIdx.x * g.cv + g.tv;
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  __shared__ float sm[2][kThreads][8];
+  float sd[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (vc < g.c8) {
+    float mu[8], rs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mu[j] = mean[8 * vc + j];
+      rs[j] = rstd[8 * vc + j];
+    }
+    for (int r = r0 + g.tr; r < r1; r += g.rpi) {
+      float d[8], a[8];
+      const size_t off = (size_t)r * C;
+      unpack8(reinterpret_cast<const uint4*>(dy + off)[vc], d);
+      unpack8(reinterpret_cast<const uint4*>(x + off)[vc], a);
+      if (kRelu) {
+        float o[8];
+        unpack8(reinterpret_cast<const uint4*>(y + off)[vc], o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = o[j] > 0.f ? d[j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sd[j] += d[j];
+        sx[j] = __builtin_fmaf(d[j], (a[j] - mu[j]) * rs[j], sx[j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sm[0][threadIdx.x][j] = sd[j];
+    sm[1][threadIdx.x][j] = sx[j];
+  }
+  __syncthreads();
+  if (g.tr == 0 && vc < g.c8) {
+    for (int k = 1; k < g.rpi; ++k) {
+      const int t = k * g.cv + g.tv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sd[j] += sm[0][t][j];
+        sx[j] += sm[1][t][j];
+      }
+    }
+    float* p0 = partial + (size_t)blockIdx.y * 2 * C + 8 * vc;
+    float* p1 = p0 + C;
+#pragma unroll
+    for (int j = 0; j < 8; j += 4) {
+      *reinterpret_cast<float4*>(p0 + j) = make_float4(sd[j], sd[j + 1], sd[j + 2], sd[j + 3]);
+      *reinterpret_cast<float4*>(p1 + j) = make_float4(sx[j], sx[j + 1], sx[j + 2], sx[j + 3]);
+    }
+  }
+}
+
+// dbeta / dgamma (fp32, written or accumulated) and the dx coefficients:
+// coef[0][c] = gamma rstd, coef[1][c] = dbeta / M, coef[2][c] = dgamma / M
+__global__ __launch_bounds__(kThreads) void bn_bwd_finalize_kernel(const float* __restrict__ partial, int nblk,
+                                                                   int M, int C, const float* __restrict__ gamma,
+                                                                   const float* __restrict__ rstd,
+                                                                   float* __restrict__ dgamma,
+                                                                   float* __restrict__ dbeta, int accumulate,
+                                                                   float* __restrict__ coef) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  if (c >= C) return;
+  float sd = 0.f, sx = 0.f;
+  for (int b = lane; b < nblk; b += 64) {
+    sd += partial[(size_t)b * 2 * C + c];
+    sx += partial[(size_t)b * 2 * C + C + c];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {   // fixed tree: every lane ends with the same sums
+    sd += __shfl_xor(sd, o);
+    sx += __shfl_xor(sx, o);
+  }
+  if (lane == 0) {
+    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + sd : sd;
+    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + sx : sx;
+    coef[c] = gamma[c] * rstd[c];
+    coef[C + c] = sd / (float)M;
+    coef[2 * C + c] = sx / (float)M;
+  }
+}
+
+template <bool kRelu, bool kRes>
+__global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dy,
+                                                                const uint16_t* __restrict__ y,
+                                                                const uint16_t* __restrict__ x,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd,
+                                                                const float* __restrict__ coef,
+                                                                uint16_t* __restrict__ dx, uint16_t* __restrict__ dres,
+                                                                int64_t nvec, int C) {
+  const int c8 = C / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const int c = 8 * (int)(v % c8);
+    float d[8], a[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[v], d);
+    unpack8(reinterpret_cast<const uint4*>(x)[v], a);
+    if (kRelu) {
+      float o[8];
+      unpack8(reinterpret_cast<const uint4*>(y)[v], o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = o[j] > 0.f ? d[j] : 0.f;
+    }
+    if (kRes) reinterpret_cast<uint4*>(dres)[v] = pack8(d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (a[j] - mean[c + j]) * rstd[c + j];
+      a[j] = coef[c + j] * (d[j] - coef[C + c + j] - xh * coef[2 * C + c + j]);
+    }
+    reinterpret_cast<uint4*>(dx)[v] = pack8(a);
+  }
+}
+
+int rows_per_block(int M) {
+  int r = (M + 511) / 512;   // <= 512 row blocks: the finalize merges <= 8 partials per lane
+  return r < 64 ? 64 : r;
+}
+
+int elem_grid(int64_t nvec) {
+  int64_t g = (nvec + kThreads - 1) / kThreads;
+  return (int)(g < 4096 ? (g < 1 ? 1 : g) : 4096);
+}
+
+}  // namespace
+
+// partial scratch (floats) the forward / backward need for M rows x C channels
+MX_EXPORT int64_t mx_bn_scratch(int M, int C) {
+  const int nblk = (M + rows_per_block(M) - 1) / rows_per_block(M);
+  return (int64_t)nblk * 2 * C + 3 * (int64_t)C + 2 * (int64_t)C;
+}
+
+// Training forward.  x, res, y: [M][C] bf16 (res may be null); gamma / beta fp32 [C];
+// mean / rstd out fp32 [C] (saved for backward); run_mean / run_var fp32 [C] updated in
+// place (null: not tracked); scratch: mx_bn_scratch floats.
+MX_EXPORT int mx_bn_fwd(const void* x, const void* res, void* y, const float* gamma, const float* beta, float* mean,
+                        float* rstd, float* run_mean, float* run_var, int M, int C, float eps, float momentum,
+                        int relu, float* scratch, hipStream_t s) {
+  if (C % 8 || C <= 0 || M <= 0 || C > 8 * 65535 * kThreads) return hipErrorInvalidValue;
+  const int rpb = rows_per_block(M), nblk = (M + rpb - 1) / rpb;
+  const int c8 = C / 8, cv = c8 < kThreads ? c8 : kThreads;
+  float* pmean = scratch;
+  float* pm2 = scratch + (size_t)nblk * C;
+  float* scale = pm2 + (size_t)nblk * C;
+  float* shift = scale + C;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3((c8 + cv - 1) / cv, nblk), dim3(kThreads), 0, s, (const uint16_t*)x, M,
+                     C, rpb, pmean, pm2);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 3) / 4), dim3(kThreads), 0, s, pmean, pm2, nblk, rpb, M, C,
+                     gamma, beta, eps, momentum, mean, rstd, scale, shift, run_mean, run_var);
+  const int64_t nvec = (int64_t)M * c8;
+  const dim3 gr(elem_grid(nvec));
+  if (res) {
+    if (relu) hipLaunchKernelGGL((bn_apply_kernel<true, true>), gr, dim3(kThreads), 0, s, (const uint16_t*)x,
+                                 (const uint16_t*)res, scale, shift, (uint16_t*)y, nvec, c8);
+    else hipLaunchKernelGGL((bn_apply_kernel<true, false>), gr, dim3(kThreads), 0, s, (const uint16_t*)x,
+                            (const uint16_t*)res, scale, shift, (uint16_t*)y, nvec, c8);
+  } else {
+    if (relu) hipLaunchKernelGGL((bn_apply_kernel<false, true>), gr, dim3(kThreads), 0, s, (const uint16_t*)x,
+                                 nullptr, scale, shift, (uint16_t*)y, nvec, c8);
+    else hipLaunchKernelGGL((bn_apply_kernel<false, false>), gr, dim3(kThreads), 0, s, (const uint16_t*)x,
+                            nullptr, scale, shift, (uint16_t*)y, nvec, c8);
+  }
+  return hipGetLastError();
+}
+
+// Evaluation / frozen-statistics forward with a caller-provided per-channel scale / shift
+MX_EXPORT int mx_bn_apply(const void* x, const void* res, void* y, const float* scale, const float* shift, int M,
+                          int C, int relu, hipStream_t s) {
+  if (C % 8 || C <= 0 || M <= 0) return hipErrorInvalidValue;
+  const int c8 = C / 8;
+  const int64_t nvec = (int64_t)M * c8;
+  const dim3 gr(elem_grid(nvec));
+  if (res) {
+    if (relu) hipLaunchKernelGGL((bn_apply_kernel<true, true>), gr, dim3(kThreads), 0, s, (const uint16_t*)x,
+                                 (const uint16_t*)res, scale, shift, (uint16_t*)y, nvec, c8);
+    else hipLaunchKernelGGL((bn_apply_kernel<true, false>), gr, dim3(kThreads), 0, s, (const uint16_t*)x,
+                            (const uint16_t*)res, scale, shift, (uint16_t*)y, nvec, c8);
+  } else {
+    if (relu) hipLaunchKernelGGL((bn_apply_kernel<false, true>), gr, dim3(kThreads), 0, s, (const uint16_t*)x,
+                                 nullptr, scale, shift, (uint16_t*)y, nvec, c8);
+    else hipLaunchKernelGGL((bn_apply_kernel<false, false>), gr, dim3(kThreads), 0, s, (const uint16_t*)x,
+                            nullptr, scale, shift, (uint16_t*)y, nvec, c8);
+  }
+  return hipGetLastError();
+}
+
+// Backward.  dy, y (forward output: the ReLU mask), x (forward input): [M][C] bf16;
+// dx out, dres out (null: no residual); dgamma / dbeta fp32 [C] written (accumulate = 0) or
+// added to; scratch: mx_bn_scratch floats.
+MX_EXPORT int mx_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd,
+                        const float* gamma, void* dx, void* dres, float* dgamma, float* dbeta, int accumulate, int M,
+                        int C, int relu, float* scratch, hipStream_t s) {
+  if (C % 8 || C <= 0 || M <= 0) return hipErrorInvalidValue;
+  const int rpb = rows_per_block(M), nblk = (M + rpb - 1) / rpb;
+  const int c8 = C / 8, cv = c8 < kThreads ? c8 : kThreads;
+  float* partial = scratch;
+  float* coef = scratch + (size_t)nblk * 2 * C;
+  const dim3 sg((c8 + cv - 1) / cv, nblk);
+  if (relu) hipLaunchKernelGGL(bn_bwd_stats_kernel<true>, sg, dim3(kThreads), 0, s, (const uint16_t*)dy,
+                               (const uint16_t*)y, (const uint16_t*)x, mean, rstd, M, C, rpb, partial);
+  else hipLaunchKernelGGL(bn_bwd_stats_kernel<false>, sg, dim3(kThreads), 0, s, (const uint16_t*)dy, nullptr,
+                          (const uint16_t*)x, mean, rstd, M, C, rpb, partial);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(kThreads), 0, s, partial, nblk, M, C, gamma,
+                     rstd, dgamma, dbeta, accumulate, coef);
+  const int64_t nvec = (int64_t)M * c8;
+  const dim3 gr(elem_grid(nvec));
+#define MX_BN_BWD(RL, RS)                                                                                   \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, RS>), gr, dim3(kThreads), 0, s, (const uint16_t*)dy,          \
+                     (const uint16_t*)y, (const uint16_t*)x, mean, rstd, coef, (uint16_t*)dx, (uint16_t*)dres, \
+                     nvec, C)
+  if (relu) {
+    if (dres) MX_BN_BWD(true, true);
+    else MX_BN_BWD(true, false);
+  } else {
+    if (dres) MX_BN_BWD(false, true);
+    else MX_BN_BWD(false, false);
+  }
+#undef MX_BN_BWD
+  return hipGetLastError();
+}

@@ -19,7 +19,23 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import compute_weights as _cw
-from ..ops.epilogue import conv_bias_act
+from ..ops import convwg
+from ..ops.batchnorm import bn_act
+from ..ops.epilogue import ConvBiasActFn, conv_bias_act
+
+
+def _conv_nobias(x, w, stride, padding, dilation):
+    """conv2d without bias for the trainable-BN path: bf16 NHWC activations go through the
+    implicit-GEMM kernels where they tile (forward, input and weight gradients), then the
+    MIOpen-forward + implicit-GEMM-weight-gradient path, else torch (autocast / fp32)."""
+    if x.is_cuda and x.dtype == torch.bfloat16:
+        wb = w.to(torch.bfloat16)
+        if convwg.fwd_supported(x, wb, None, None, stride, padding, dilation):
+            return ConvBiasActFn.apply(x, wb, None, None, False, stride, padding, dilation)
+        if convwg.supported(x, wb, stride, padding, dilation):
+            return convwg.conv2d_wg(x, wb, stride, padding, dilation)
+        return F.conv2d(x, wb, None, stride, padding, dilation)
+    return F.conv2d(x, w.to(x.dtype), None, stride, padding, dilation)
 
 
 class FrozenBN(nn.Module):
@@ -71,10 +87,11 @@ class ConvNorm(nn.Module):
             # one MIOpen conv + one fused bias (+ residual) (+ ReLU) pass (ops/epilogue.py)
             return conv_bias_act(x, wf, bf, self.conv.stride, self.conv.padding, self.conv.dilation, relu=relu,
                                  residual=residual)
-        y = self.norm(F.conv2d(x, w.to(dt), None, self.conv.stride, self.conv.padding, self.conv.dilation))
-        if residual is not None:
-            y = y + residual
-        return F.relu(y, inplace=True) if relu else y
+        # trainable BatchNorm: the convolution on csrc/convwg.hip where it tiles (implicit-GEMM
+        # forward / input / weight gradients), then ONE fused BN (+ residual) (+ ReLU) node
+        # (ops/batchnorm.py, csrc/batchnorm.hip)
+        return bn_act(_conv_nobias(x, w, self.conv.stride, self.conv.padding, self.conv.dilation), self.norm,
+                      residual=residual, relu=relu)
 
     def _folded(self, w: torch.Tensor, dt: torch.dtype):
         """FrozenBN folded into the conv: weight * s (per output channel) and bias

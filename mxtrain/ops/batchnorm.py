@@ -1,0 +1,104 @@
+"""Training-mode BatchNorm fused with the residual add and ReLU, NHWC bf16 (csrc/batchnorm.hip).
+
+``bn_act(x, bn, residual, relu)`` computes ``act(BatchNorm(x) (+ residual))`` for an
+``nn.BatchNorm2d`` ``bn`` whose affine parameters / running statistics stay fp32 (AMP
+style): one statistics pass, a per-channel finalize (running statistics updated in place,
+deterministic two-stage reductions) and one apply pass forward; a statistics pass, a
+finalize and one pass producing dx (and the residual's gradient) backward.  The ResNet-50
+bottleneck's BN -> add -> ReLU tail is a single autograd node.  Evaluation mode (or the
+CPU) uses the running statistics through the same apply kernel / plain torch ops.
+
+Reference: the Ray Train Lightning ResNet-50 config (BASELINE.json config 5,
+/root/reference/charts/machine-learning/training/raytrain/templates/train.yaml:142-221).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+
+def _nhwc_ok(t: Optional[torch.Tensor]) -> bool:
+    return t is None or (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 4
+                         and t.is_contiguous(memory_format=torch.channels_last) and t.data_ptr() % 16 == 0)
+
+
+def supported(x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> bool:
+    return (_lib.use_hip(x) and _nhwc_ok(x) and _nhwc_ok(residual) and x.shape[1] % 8 == 0
+            and (residual is None or residual.shape == x.shape))
+
+
+def _scratch(M: int, C: int, device) -> torch.Tensor:
+    return torch.empty(_lib.query64("mx_bn_scratch", M, C), dtype=torch.float32, device=device)
+
+
+class BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, momentum: float, eps: float, relu: bool):
+        N, C, H, W = x.shape
+        M = N * H * W
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        g32 = gamma.detach().float().contiguous()
+        b32 = beta.detach().float().contiguous()
+        _lib.call("mx_bn_fwd", x.data_ptr(), _lib.ptr(residual), y.data_ptr(), g32.data_ptr(), b32.data_ptr(),
+                  mean.data_ptr(), rstd.data_ptr(), _lib.ptr(running_mean), _lib.ptr(running_var), M, C,
+                  float(eps), float(momentum), int(relu), _scratch(M, C, x.device).data_ptr(), _lib.stream())
+        ctx.relu, ctx.has_res = relu, residual is not None
+        ctx.save_for_backward(x, y, mean, rstd, g32)
+        ctx.pdtypes = (gamma.dtype, beta.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, rstd, g32 = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        N, C, H, W = x.shape
+        M = N * H * W
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+        dg = torch.empty(C, dtype=torch.float32, device=x.device)
+        db = torch.empty_like(dg)
+        _lib.call("mx_bn_bwd", dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                  g32.data_ptr(), dx.data_ptr(), _lib.ptr(dres), dg.data_ptr(), db.data_ptr(), 0, M, C,
+                  int(ctx.relu), _scratch(M, C, x.device).data_ptr(), _lib.stream())
+        return (dx, dg.to(ctx.pdtypes[0]), db.to(ctx.pdtypes[1]), dres, None, None, None, None, None)
+
+
+def bn_act_ref(x, gamma, beta, residual, running_mean, running_var, momentum, eps, relu, training=True):
+    """The same op in plain torch (fp32 math): the CPU path and the tests' reference."""
+    y = F.batch_norm(x.float(), running_mean, running_var, gamma.float(), beta.float(), training, momentum, eps)
+    if residual is not None:
+        y = y + residual.float()
+    if relu:
+        y = F.relu(y)
+    return y.to(x.dtype)
+
+
+def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, residual: Optional[torch.Tensor] = None,
+           relu: bool = False) -> torch.Tensor:
+    """act(bn(x) (+ residual)) for an ``nn.BatchNorm2d`` (training: batch statistics and
+    running-statistics update; eval: running statistics)."""
+    mom = bn.momentum if bn.momentum is not None else 0.1
+    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    if supported(x, residual):
+        if bn.training:
+            return BNActFn.apply(x, bn.weight, bn.bias, residual, bn.running_mean if bn.track_running_stats else None,
+                                 bn.running_var if bn.track_running_stats else None, mom, bn.eps, relu)
+        # eval: y = act(x * scale + shift (+ res)) with the running statistics
+        s = bn.weight.float() * torch.rsqrt(bn.running_var.float() + bn.eps)
+        h = bn.bias.float() - bn.running_mean.float() * s
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        N, C, H, W = x.shape
+        _lib.call("mx_bn_apply", x.data_ptr(), _lib.ptr(residual), y.data_ptr(), s.contiguous().data_ptr(),
+                  h.contiguous().data_ptr(), N * H * W, C, int(relu), _lib.stream())
+        return y
+    y = bn(x)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y

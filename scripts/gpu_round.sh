@@ -48,10 +48,12 @@ for s in $STEPS; do
       i=0
       for G in "$G1" "$G2" "$G3"; do
         i=$((i+1))
-        timeout -s KILL ${T_PMC:-120} rocprofv3 --pmc $G --kernel-include-regex "${PMC_REGEX:-.*}" -d "$GRAFT_REPO_ROOT/gpurun_out/pmc$i" -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/$PMC_CMD > "$GRAFT_REPO_ROOT/gpurun_out/pmc$i.log" 2>&1; rc=$?
-        echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || { cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/pmc$i.log; exit $rc; }
+        timeout -s KILL ${T_PMC:-120} rocprofv3 --pmc $G --kernel-include-regex "${PMC_REGEX:-.*}" -d "$GRAFT_REPO_ROOT/gpurun_out/${PMC_TAG:-pmc}$i" -o run -- python3 $GRAFT_REPO_ROOT/$PMC_CMD > "$GRAFT_REPO_ROOT/gpurun_out/${PMC_TAG:-pmc}$i.log" 2>&1; rc=$?
+        echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || { cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/${PMC_TAG:-pmc}$i.log; exit $rc; }
       done
-      cd "$GRAFT_REPO_ROOT" ;;
+      cd "$GRAFT_REPO_ROOT"
+      python3 scripts/rocpd_pmc.py $(find gpurun_out/${PMC_TAG:-pmc}[123] -name "*.db") > gpurun_out/${PMC_TAG:-pmc}_summary.txt 2>&1
+      find gpurun_out/${PMC_TAG:-pmc}[123] -name "*.db" -delete ;;
   esac
 done
 echo ALLDONE

