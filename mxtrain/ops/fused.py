@@ -253,13 +253,14 @@ def cross_entropy_fwd_bwd(logits, labels, grad_scale, ignore_index=-100, tp_grou
         return loss
     m, s, tgt = ce_stats(logits, labels, vocab_start)
     if tp_group is not None:
-        import torch.distributed as dist
-        gm = m.clone()
-        dist.all_reduce(gm, op=dist.ReduceOp.MAX, group=tp_group)
-        s = s * torch.exp(m - gm)
-        dist.all_reduce(s, group=tp_group)
-        dist.all_reduce(tgt, group=tp_group)
-        m = gm
+        # the row max as an all-gather + local max and (sum, target logit) as ONE sum
+        # all-reduce: both are collectives the xGMI kernels run, so a captured TP step keeps
+        # the CE inside the graph (a MAX reduction would need RCCL / gloo)
+        from ..parallel import collectives as C
+        gm = C.all_gather_dim0(m.float().reshape(1, -1).contiguous(), tp_group).amax(0)
+        st = torch.stack([s.float() * torch.exp(m - gm), tgt.float()])
+        C.all_reduce_(st, tp_group)
+        s, tgt, m = st[0], st[1], gm
     lse = lse_from_stats(m, s)
     return ce_grad_inplace(logits, labels, lse, tgt, grad_scale, vocab_start, ignore_index)
 

@@ -23,6 +23,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
+from . import collectives as _C
 from . import xgmi as _xgmi
 
 from ..ops import optim as optim_ops
@@ -247,7 +248,7 @@ class DistributedOptimizer:
             return
         for name in self._sp_names:
             if self.flat.unit_to_bucket[self.flat.spec_by_name[name].unit] == bucket.index:
-                dist.all_reduce(self.flat.grads[name], group=self.sp_group)
+                _C.all_reduce_(self.flat.grads[name], self.sp_group)
 
     def _start_bucket(self, bi: int):
         if bi in self.started:
@@ -283,7 +284,7 @@ class DistributedOptimizer:
         if self.embed_group is not None and dist.get_world_size(self.embed_group) > 1:
             for s in self.flat.specs:
                 if s.shared == "word_embeddings":
-                    dist.all_reduce(self.flat.grads[s.name], group=self.embed_group)
+                    _C.all_reduce_(self.flat.grads[s.name], self.embed_group)
         for bi in range(len(self.flat.buckets)):
             self._start_bucket(bi)
         if self.overlap:

@@ -30,16 +30,28 @@ for s in $STEPS; do
       timeout -k 10 ${T_MRCNN:-600} python scripts/bench_maskrcnn.py ${MRCNN_ARGS:-} > gpurun_out/mrcnn.log 2>&1; rc=$?
       tail -12 gpurun_out/mrcnn.log; echo "mrcnn rc=$rc"; ok $rc || exit $rc ;;
     mrprof)
+      # whole-step kernel census of Mask R-CNN (MRCNN_ARGS e.g. "--batch 4"), summarised on the box
       cd /tmp && export TMPDIR=/tmp
-      timeout -k 10 ${T_PROF:-500} rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/mrprof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/scripts/bench_maskrcnn.py" --steps 12 --warmup 6 ${MRCNN_ARGS:-} > "$GRAFT_REPO_ROOT/gpurun_out/mrprof.log" 2>&1; rc=$?
-      cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/mrprof.log; echo "mrprof rc=$rc"; ok $rc || exit $rc ;;
+      timeout -k 10 ${T_PROF:-500} rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/${PROF_TAG:-mrprof}" -o run -- python3 "$GRAFT_REPO_ROOT/scripts/bench_maskrcnn.py" --steps ${MR_STEPS:-12} --warmup 6 ${MRCNN_ARGS:-} > "$GRAFT_REPO_ROOT/gpurun_out/${PROF_TAG:-mrprof}.log" 2>&1; rc=$?
+      cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/${PROF_TAG:-mrprof}.log; echo "mrprof rc=$rc"; ok $rc || exit $rc
+      python3 scripts/prof_summary.py $(find gpurun_out/${PROF_TAG:-mrprof} -name "*.db" | head -1) $((${MR_STEPS:-12} + 6)) 60 > gpurun_out/${PROF_TAG:-mrprof}_summary.txt 2>&1
+      find gpurun_out/${PROF_TAG:-mrprof} -name "*.db" -delete ;;
     kbench)
       timeout -k 10 300 python scripts/kbench.py ${KBENCH_ARGS:-} > gpurun_out/kbench.log 2>&1; rc=$?
       cat gpurun_out/kbench.log | tail -40; echo "kbench rc=$rc"; ok $rc || exit $rc ;;
     prof)
       cd /tmp && export TMPDIR=/tmp
-      timeout -k 10 ${T_PROF:-400} rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --gpus 1 --steps 5 --warmup 3 ${PROF_ARGS:-} > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1; rc=$?
-      cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/prof.log; echo "prof rc=$rc"; ok $rc || exit $rc ;;
+      timeout -k 10 ${T_PROF:-400} rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/${PROF_TAG:-prof}" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --gpus 1 --steps ${P_STEPS:-10} --warmup 3 --no-maskrcnn ${PROF_ARGS:-} > "$GRAFT_REPO_ROOT/gpurun_out/${PROF_TAG:-prof}.log" 2>&1; rc=$?
+      cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/${PROF_TAG:-prof}.log; echo "prof rc=$rc"; ok $rc || exit $rc
+      python3 scripts/prof_summary.py $(find gpurun_out/${PROF_TAG:-prof} -name "*.db" | head -1) $((${P_STEPS:-10} + 6)) 60 > gpurun_out/${PROF_TAG:-prof}_summary.txt 2>&1
+      find gpurun_out/${PROF_TAG:-prof} -name "*.db" -delete ;;
+    gemm)
+      timeout -k 10 ${T_GEMM:-400} python scripts/gemm_nt_bench.py > gpurun_out/${GEMM_TAG:-gemm}.txt 2>&1; rc=$?
+      tail -20 gpurun_out/${GEMM_TAG:-gemm}.txt; echo "gemm rc=$rc"; ok $rc || exit $rc ;;
+    cmd)
+      # one arbitrary python command: CMD="scripts/x.py args" (output to gpurun_out/$CMD_TAG.txt)
+      timeout -k 10 ${T_CMD:-300} python $CMD > gpurun_out/${CMD_TAG:-cmd}.txt 2>&1; rc=$?
+      tail -${CMD_TAIL:-20} gpurun_out/${CMD_TAG:-cmd}.txt; echo "cmd rc=$rc"; ok $rc || exit $rc ;;
     pmc)
       cd /tmp && export TMPDIR=/tmp
       G1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES"
