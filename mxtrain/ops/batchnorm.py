@@ -26,8 +26,11 @@ def _nhwc_ok(t: Optional[torch.Tensor]) -> bool:
                          and t.is_contiguous(memory_format=torch.channels_last) and t.data_ptr() % 16 == 0)
 
 
+ENABLED = True   # module switch (A/B runs: scripts/resnet_ab.py)
+
+
 def supported(x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> bool:
-    return (_lib.use_hip(x) and _nhwc_ok(x) and _nhwc_ok(residual) and x.shape[1] % 8 == 0
+    return (ENABLED and _lib.use_hip(x) and _nhwc_ok(x) and _nhwc_ok(residual) and x.shape[1] % 8 == 0
             and (residual is None or residual.shape == x.shape))
 
 

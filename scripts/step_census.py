@@ -14,6 +14,7 @@ def main():
     ap.add_argument("--marker", default="nms_keep_kernel")
     ap.add_argument("--last", type=int, default=10)
     ap.add_argument("--top", type=int, default=80)
+    ap.add_argument("--sort", choices=("count", "time"), default="time")
     a = ap.parse_args()
     con = sqlite3.connect(a.db)
     cols = [r[1] for r in con.execute("PRAGMA table_info(kernels)")]
@@ -34,8 +35,9 @@ def main():
     busy = sum(v[1] for v in agg.values()) / steps
     print(f"== {a.db}: {n_tot:.0f} kernels/step, GPU busy {busy:.0f} us/step, "
           f"wall {(t1 - t0) / 1000 / steps:.0f} us/step (last {steps} steps)")
-    for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:a.top]:
-        print(f"{c / steps:7.1f}x {t / steps:9.1f} us  {k}")
+    key = (lambda kv: -kv[1][0]) if a.sort == "count" else (lambda kv: -kv[1][1])
+    for k, (c, t) in sorted(agg.items(), key=key)[:a.top]:
+        print(f"{c / steps:7.1f}x {t / steps:9.1f} us {100 * t / steps / busy:5.1f}%  {k}")
 
 
 if __name__ == "__main__":
