@@ -306,36 +306,65 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
 #pragma unroll
       for (int a = 0; a < FM; ++a) {
         const bf16x8 av = lds_read8(As, offA + 16 * a * R + cK[kk]);
+        // the weight fragment is the A operand: a lane ends with 4 consecutive output
+        // channels of one pixel (epilogue below)
 #pragma unroll
-        for (int u = 0; u < FN; ++u) acc[a][u] = mfma16(av, b[u], acc[a][u]);
+        for (int u = 0; u < FN; ++u) acc[a][u] = mfma16(b[u], av, acc[a][u]);
       }
     }
     slot ^= 1;
   }
   (void)PER;
 
-  // ---- epilogue: lane holds y[m0 + 16 (FM wm + a) + 4 G + e][n0 + 16 (FN wn + u) + i]
-  const int col = n0 + 16 * FN * wn + i;
-  float bv[FN];
+  // ---- epilogue: lane (G, i) holds y[m0 + 16 (FM wm + a) + i][n0 + 16 (FN wn + u) + 4 G + e];
+  // pairs of 16-channel subtiles are re-dealt (permlane swaps) so every lane stores 8
+  // consecutive channels: 16-B stores and 16-B residual loads (2-B scattered stores made
+  // the epilogue store-issue bound)
+  const int colw = n0 + 16 * FN * wn;
+  float bv[FN][4];
 #pragma unroll
-  for (int u = 0; u < FN; ++u) bv[u] = cp.bias ? bf2f(cp.bias[col + 16 * u]) : 0.f;
-#pragma unroll
-  for (int a = 0; a < FM; ++a)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int p = m0 + 16 * (FM * wm + a) + 4 * G + e;
-      if (p < cp.T) {
-        uint16_t* row = cp.y + (size_t)p * cp.ldy + col;
-        const uint16_t* rr = RES ? cp.res + (size_t)p * cp.ldy + col : nullptr;
-#pragma unroll
-        for (int u = 0; u < FN; ++u) {
-          float v = acc[a][u][e] + bv[u];
-          if (RES) v += bf2f(rr[16 * u]);
-          if (RELU) v = fmaxf(v, 0.f);
-          row[16 * u] = f2bf(v);
-        }
-      }
+  for (int u = 0; u < FN; ++u) {
+    if (cp.bias) {
+      const uint2 b2 = *reinterpret_cast<const uint2*>(cp.bias + colw + 16 * u + 4 * G);
+      bv[u][0] = lo_bf(b2.x); bv[u][1] = hi_bf(b2.x); bv[u][2] = lo_bf(b2.y); bv[u][3] = hi_bf(b2.y);
+    } else {
+      bv[u][0] = bv[u][1] = bv[u][2] = bv[u][3] = 0.f;
     }
+  }
+#pragma unroll
+  for (int a = 0; a < FM; ++a) {
+    const int p = m0 + 16 * (FM * wm + a) + i;
+    const size_t pr = (size_t)(p < cp.T ? p : cp.T - 1) * cp.ldy;   // every lane takes part in the swaps
+#pragma unroll
+    for (int up = 0; up < FN / 2; ++up) {
+      uint32_t c[2][2], h[2][2];
+      if (RES) {
+        const uint4 rv = *reinterpret_cast<const uint4*>(cp.res + pr + colw + 32 * up + 8 * G);
+        h[0][0] = rv.x; h[0][1] = rv.y; h[1][0] = rv.z; h[1][1] = rv.w;
+        undeal(h[0][0], h[0][1], h[1][0], h[1][1]);
+      }
+#pragma unroll
+      for (int hlf = 0; hlf < 2; ++hlf) {
+        const int u = 2 * up + hlf;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[a][u][e] + bv[u][e];
+        if (RES) {
+          v[0] += lo_bf(h[hlf][0]); v[1] += hi_bf(h[hlf][0]);
+          v[2] += lo_bf(h[hlf][1]); v[3] += hi_bf(h[hlf][1]);
+        }
+        if (RELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        c[hlf][0] = pack2(v[0], v[1]);
+        c[hlf][1] = pack2(v[2], v[3]);
+      }
+      deal(c[0][0], c[0][1], c[1][0], c[1][1]);
+      if (p < cp.T)
+        *reinterpret_cast<uint4*>(cp.y + pr + colw + 32 * up + 8 * G) = make_uint4(c[0][0], c[0][1], c[1][0], c[1][1]);
+    }
+  }
 }
 
 // ============================================================================ input gradient
@@ -353,6 +382,8 @@ struct ConvDg {
   const uint16_t* w;     // [Cout][taps][Cin]
   const uint16_t* zero;  // >= 256 zero bf16
   uint16_t* dx;          // [N * IH * IW][ldx]
+  const uint16_t* add;   // [N * IH * IW][ldx] or null: added to dX (a second gradient of X)
+  const uint16_t* mask;  // [N * IH * IW][ldx] or null: dX zeroed where mask <= 0 (X's ReLU)
   int ldy, ldx;
   int T, OH, OW, IH, IW;
   int KW, taps, stride, pad, dil;
@@ -468,25 +499,54 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
 #pragma unroll
       for (int a = 0; a < FM; ++a) {
         const bf16x8 av = lds_read8(As, offA + 16 * a * RA + cA[kk]);
+        // weight fragment as the A operand: 4 consecutive input channels per lane
 #pragma unroll
-        for (int u = 0; u < FN; ++u) acc[a][u] = mfma16(av, b[u], acc[a][u]);
+        for (int u = 0; u < FN; ++u) acc[a][u] = mfma16(b[u], av, acc[a][u]);
       }
     }
     if (++slot == NSLOT) slot = 0;
   }
 
-  // ---- epilogue: lane holds dX[m0 + 16 (FM wm + a) + 4 G + e][n0 + 16 (FN wn + u) + i]
+  // ---- epilogue: lane (G, i) holds dX[m0 + 16 (FM wm + a) + i][n0 + 16 (FN wn + u) + 4 G + e],
+  // re-dealt per subtile pair into 8 consecutive channels per lane (16-B stores)
+  const int colw = n0 + 16 * FN * wn;
 #pragma unroll
-  for (int a = 0; a < FM; ++a)
+  for (int a = 0; a < FM; ++a) {
+    const int p = m0 + 16 * (FM * wm + a) + i;
+    const size_t pr = (size_t)(p < cp.T ? p : cp.T - 1) * cp.ldx;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int p = m0 + 16 * (FM * wm + a) + 4 * G + e;
-      if (p < cp.T) {
-        uint16_t* row = cp.dx + (size_t)p * cp.ldx + n0 + 16 * FN * wn + i;
-#pragma unroll
-        for (int u = 0; u < FN; ++u) row[16 * u] = f2bf(acc[a][u][e]);
+    for (int up = 0; up < FN / 2; ++up) {
+      uint32_t c[2][2], ad[2][2], mk[2][2];
+      if (cp.add) {
+        const uint4 v = *reinterpret_cast<const uint4*>(cp.add + pr + colw + 32 * up + 8 * G);
+        ad[0][0] = v.x; ad[0][1] = v.y; ad[1][0] = v.z; ad[1][1] = v.w;
+        undeal(ad[0][0], ad[0][1], ad[1][0], ad[1][1]);
       }
+      if (cp.mask) {
+        const uint4 v = *reinterpret_cast<const uint4*>(cp.mask + pr + colw + 32 * up + 8 * G);
+        mk[0][0] = v.x; mk[0][1] = v.y; mk[1][0] = v.z; mk[1][1] = v.w;
+        undeal(mk[0][0], mk[0][1], mk[1][0], mk[1][1]);
+      }
+#pragma unroll
+      for (int hlf = 0; hlf < 2; ++hlf) {
+        const int u = 2 * up + hlf;
+        float v[4] = {acc[a][u][0], acc[a][u][1], acc[a][u][2], acc[a][u][3]};
+        if (cp.add) {
+          v[0] += lo_bf(ad[hlf][0]); v[1] += hi_bf(ad[hlf][0]);
+          v[2] += lo_bf(ad[hlf][1]); v[3] += hi_bf(ad[hlf][1]);
+        }
+        if (cp.mask) {
+          v[0] = lo_bf(mk[hlf][0]) > 0.f ? v[0] : 0.f; v[1] = hi_bf(mk[hlf][0]) > 0.f ? v[1] : 0.f;
+          v[2] = lo_bf(mk[hlf][1]) > 0.f ? v[2] : 0.f; v[3] = hi_bf(mk[hlf][1]) > 0.f ? v[3] : 0.f;
+        }
+        c[hlf][0] = pack2(v[0], v[1]);
+        c[hlf][1] = pack2(v[2], v[3]);
+      }
+      deal(c[0][0], c[0][1], c[1][0], c[1][1]);
+      if (p < cp.T)
+        *reinterpret_cast<uint4*>(cp.dx + pr + colw + 32 * up + 8 * G) = make_uint4(c[0][0], c[0][1], c[1][0], c[1][1]);
     }
+  }
 }
 
 // Split-K reduction: one thread per (tile, accumulator register group, lane) float4 column,
@@ -603,15 +663,19 @@ MX_EXPORT int mx_conv_wgrad_splits(int64_t T, int splits) {
   return (steps + nk - 1) / nk;
 }
 
-// d (int64[20]): {dy, w, zero, dx, 0, 0, ldy, ldx, N, OH, OW, IH, IW, KH, KW, stride, pad,
-// dil, Cout, Cin}: dX of conv2d for the output gradient dY, weight [Cout][KH][KW][Cin]
-// (channels_last).  Cout a multiple of 64, Cin of 128; 16-B aligned operands.
+// d (int64[20]): {dy, w, zero, dx, add, mask, ldy, ldx, N, OH, OW, IH, IW, KH, KW, stride,
+// pad, dil, Cout, Cin}: dX of conv2d for the output gradient dY, weight [Cout][KH][KW][Cin]
+// (channels_last), then (optional, null to skip) + add[p][c] and * (mask[p][c] > 0): X's
+// second gradient (a residual branch) and X's own ReLU folded into the one store.  Cout a
+// multiple of 64, Cin of 128; 16-B aligned operands (add / mask share dX's layout).
 MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   ConvDg cp{};
   cp.dy = reinterpret_cast<const uint16_t*>(d[0]);
   cp.w = reinterpret_cast<const uint16_t*>(d[1]);
   cp.zero = reinterpret_cast<const uint16_t*>(d[2]);
   cp.dx = reinterpret_cast<uint16_t*>(d[3]);
+  cp.add = reinterpret_cast<const uint16_t*>(d[4]);
+  cp.mask = reinterpret_cast<const uint16_t*>(d[5]);
   cp.ldy = (int)d[6];
   cp.ldx = (int)d[7];
   const int64_t N = d[8];
@@ -632,7 +696,7 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
     return (int)hipErrorInvalidValue;
   if (Cout % 64 || cp.Cin % 128 || cp.ldy < Cout || cp.ldx < cp.Cin || (cp.ldy & 7) || (cp.ldx & 7))
     return (int)hipErrorInvalidValue;
-  if ((d[0] | d[1] | d[2] | d[3]) & 15) return (int)hipErrorInvalidValue;
+  if ((d[0] | d[1] | d[2] | d[3] | d[4] | d[5]) & 15) return (int)hipErrorInvalidValue;
   cp.T = (int)T;
   cp.taps = KH * cp.KW;
   cp.cob = Cout / 64;

@@ -50,5 +50,34 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
 }
 
+// Epilogue re-deal of two 16-column MFMA subtiles: (x0, x1) = lane's 4 columns 4G..4G+3
+// of subtile u0 (bf16 pairs), (y0, y1) the same of u1.  permlane32_swap exchanges the
+// upper half of x with the lower half of y, permlane16_swap the odd 16-lane rows of x with
+// the even rows of y; afterwards lane group G holds the 8 consecutive columns 8G .. 8G + 7
+// of the 32-column pair as (x0, x1, y0, y1).  undeal is the inverse (each swap is an
+// involution, applied in reverse order).
+__device__ __forceinline__ void swap32(uint32_t& x, uint32_t& y) {
+  auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+  x = r[0];
+  y = r[1];
+}
+__device__ __forceinline__ void swap16(uint32_t& x, uint32_t& y) {
+  auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+  x = r[0];
+  y = r[1];
+}
+__device__ __forceinline__ void deal(uint32_t& x0, uint32_t& x1, uint32_t& y0, uint32_t& y1) {
+  swap32(x0, y0);
+  swap32(x1, y1);
+  swap16(x0, y0);
+  swap16(x1, y1);
+}
+__device__ __forceinline__ void undeal(uint32_t& x0, uint32_t& x1, uint32_t& y0, uint32_t& y1) {
+  swap16(x0, y0);
+  swap16(x1, y1);
+  swap32(x0, y0);
+  swap32(x1, y1);
+}
+
 }  // namespace gemm
 }  // namespace mx

@@ -21,7 +21,7 @@ import torch.nn.functional as F
 from . import compute_weights as _cw
 from ..ops import convwg
 from ..ops.batchnorm import bn_act
-from ..ops.epilogue import ConvBiasActFn, conv_bias_act
+from ..ops.epilogue import BlockLink, ConvBiasActFn, conv_bias_act, fused_conv_ok
 
 
 def _conv_nobias(x, w, stride, padding, dilation):
@@ -67,9 +67,11 @@ class ConvNorm(nn.Module):
 
     calibrating = False
 
-    def forward(self, x, residual=None, relu=None):
+    def forward(self, x, residual=None, relu=None, fuse=None):
         """act(conv(x) [+ folded FrozenBN] (+ residual)); ``relu`` overrides the module's
-        activation (the bottleneck applies its ReLU after the residual add)."""
+        activation (the bottleneck applies its ReLU after the residual add).  ``fuse`` =
+        (BlockLink, k, roles): the bottleneck's backward-fusion contract (ops/epilogue.py),
+        honoured only when this conv runs the all-implicit-GEMM ConvBiasActFn path."""
         relu = self.relu if relu is None else relu
         dt = x.dtype
         w = self.conv.weight
@@ -84,9 +86,18 @@ class ConvNorm(nn.Module):
                 self.norm.bias.zero_()
         if self.norm_kind == "frozen":
             wf, bf = self._folded(w, dt)
+            if fuse is not None:
+                link, k, roles = fuse
+                if fused_conv_ok(x, wf, bf, residual, self.conv.stride, self.conv.padding, self.conv.dilation):
+                    if "mask_in" in roles:
+                        link.premask[k - 1] = True     # conv k-1 leaves its ReLU mask to this dgrad
+                    if "take_res" in roles:
+                        link.taker = True
+                else:
+                    fuse = None
             # one MIOpen conv + one fused bias (+ residual) (+ ReLU) pass (ops/epilogue.py)
             return conv_bias_act(x, wf, bf, self.conv.stride, self.conv.padding, self.conv.dilation, relu=relu,
-                                 residual=residual)
+                                 residual=residual, fuse=fuse)
         # trainable BatchNorm: the convolution on csrc/convwg.hip where it tiles (implicit-GEMM
         # forward / input / weight gradients), then ONE fused BN (+ residual) (+ ReLU) node
         # (ops/batchnorm.py, csrc/batchnorm.hip)
@@ -146,9 +157,19 @@ class Bottleneck(nn.Module):
         if norm == "bn":
             nn.init.zeros_(self.conv3.norm.weight)   # zero-init last BN gamma (standard ResNet recipe)
 
+    # backward fusion inside the block (ops/epilogue.py BlockLink): the dgrads of conv2 /
+    # conv3 apply conv1's / conv2's ReLU in their stores, and an identity block's residual
+    # gradient is added in conv1's dgrad store instead of by autograd (FrozenBN path)
+    fuse_backward = True
+
     def forward(self, x):
-        idt = self.shortcut(x) if self.shortcut is not None else x
-        return self.conv3(self.conv2(self.conv1(x)), residual=idt, relu=True)
+        link = BlockLink() if self.fuse_backward and self.conv1.norm_kind == "frozen" else None
+        ident = self.shortcut is None
+        a1 = self.conv1(x, fuse=(link, 1, ("take_res",) if ident else ()) if link else None)
+        a2 = self.conv2(a1, fuse=(link, 2, ("mask_in",)) if link else None)
+        idt = x if ident else self.shortcut(x)
+        return self.conv3(a2, residual=idt, relu=True,
+                          fuse=(link, 3, ("mask_in", "stash_res") if ident else ("mask_in",)) if link else None)
 
 
 class ResNet(nn.Module):

@@ -105,9 +105,12 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dila
     return out
 
 
-def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride, padding, dilation) -> torch.Tensor:
+def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride, padding, dilation, add=None,
+               mask=None) -> torch.Tensor:
     """dX [N, Cin, IH, IW] (channels_last bf16) of conv2d(x, w) for the output gradient
-    ``dy``; ``w`` bf16 [Cout, Cin, KH, KW] (made channels_last if it is not)."""
+    ``dy``; ``w`` bf16 [Cout, Cin, KH, KW] (made channels_last if it is not).  In the same
+    store (optional): ``+ add`` (another gradient of X) and ``* (mask > 0)`` (X's ReLU; mask
+    = X itself when X is a ReLU output); both channels_last bf16 of X's shape."""
     Cout, Cin, KH, KW = w.shape
     N, _, IH, IW = x_shape
     _, _, OH, OW = dy.shape
@@ -117,8 +120,11 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride, padding, dila
         w = w.contiguous(memory_format=torch.channels_last)
     dx = torch.empty((N, IH, IW, Cin), dtype=torch.bfloat16, device=dy.device).permute(0, 3, 1, 2)
     _, zero = _workspace(dy.device, 1)
+    for t in (add, mask):
+        assert t is None or (_cl(t) and tuple(t.shape) == (N, Cin, IH, IW) and t.dtype == torch.bfloat16
+                             and t.data_ptr() % 16 == 0), "dgrad add / mask: X's channels_last shape"
     d = _DESC_T()
-    d[:20] = [dy.data_ptr(), w.data_ptr(), zero.data_ptr(), dx.data_ptr(), 0, 0,
+    d[:20] = [dy.data_ptr(), w.data_ptr(), zero.data_ptr(), dx.data_ptr(), _lib.ptr(add) or 0, _lib.ptr(mask) or 0,
             Cout, Cin, N, OH, OW, IH, IW, KH, KW, _sym(stride), _sym(padding), _sym(dilation), Cout, Cin]
     _lib.call("mx_conv_dgrad", d, _lib.stream())
     return dx
@@ -135,14 +141,16 @@ def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, paddi
             and _cl(x) and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
             and None not in (_sym(stride), _sym(padding), _sym(dilation))):
         return False
-    if b is not None and not (b.dtype == torch.bfloat16 and b.is_contiguous() and b.numel() == w.shape[0]):
+    if b is not None and not (b.dtype == torch.bfloat16 and b.is_contiguous() and b.numel() == w.shape[0]
+                              and b.data_ptr() % 8 == 0):   # 8-B bias loads (4 channels per lane)
         return False
     st, pd, dl = _sym(stride), _sym(padding), _sym(dilation)
     N, _, IH, IW = x.shape
     OH = (IH + 2 * pd - dl * (w.shape[2] - 1) - 1) // st + 1
     OW = (IW + 2 * pd - dl * (w.shape[3] - 1) - 1) // st + 1
     if residual is not None and not (residual.dtype == torch.bfloat16 and _cl(residual)
-                                     and tuple(residual.shape) == (N, w.shape[0], OH, OW)):
+                                     and tuple(residual.shape) == (N, w.shape[0], OH, OW)
+                                     and residual.data_ptr() % 16 == 0):   # 16-B residual loads
         return False
     return (N * OH * OW + 127) // 128 * (w.shape[0] // 128) >= FWD_MIN_TILES
 

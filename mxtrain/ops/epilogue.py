@@ -82,17 +82,41 @@ def _bias_act_bwd(g, out, relu: bool, want_db: bool):
     return dy, db
 
 
+class BlockLink:
+    """Backward-fusion contract between the convolutions of one bottleneck block (built by
+    models/resnet.py; every field is decided in the forward, read in the backward):
+
+    * ``premask[k]``: the consumer of conv k's output (conv k+1) multiplies its input
+      gradient by (its input > 0) in its dgrad store -- conv k's ReLU -- so conv k's
+      backward skips its own ReLU-mask pass;
+    * ``stash``: identity residual: conv3's backward puts the residual branch's gradient
+      here instead of returning it, and conv1's backward adds it in its dgrad store (conv1
+      always runs after conv3 in backward: data dependency), so autograd's separate add
+      of the block input's two gradients disappears."""
+
+    __slots__ = ("premask", "stash", "taker")
+
+    def __init__(self):
+        self.premask = {}
+        self.stash = []
+        self.taker = False    # conv1 runs ConvBiasActFn with role "take_res" (set in its forward)
+
+
 class ConvBiasActFn(torch.autograd.Function):
     """act(conv2d(x, w) + b (+ res)) with every direction on csrc/convwg.hip where it tiles:
     forward = one implicit-GEMM launch with the epilogue fused; backward = the ReLU mask +
-    bias-gradient pass, then the implicit-GEMM input and weight gradients."""
+    bias-gradient pass, then the implicit-GEMM input and weight gradients.  With a
+    ``BlockLink`` (``fuse`` = (link, k, role)): role "mask_in" folds the producer's ReLU
+    into this conv's dgrad, role "stash_res" hands the residual gradient to conv1, role
+    "take_res" adds it (see BlockLink)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, res, relu: bool, stride, padding, dilation):
+    def forward(ctx, x, w, b, res, relu: bool, stride, padding, dilation, fuse=None):
         y = convwg.conv_fwd(x, w, b, res, relu, stride, padding, dilation)
         ctx.conf = (list(convwg._pair(stride)), list(convwg._pair(padding)), list(convwg._pair(dilation)))
         ctx.relu, ctx.has_res = relu, res is not None
         ctx.bdtype = b.dtype if b is not None else None
+        ctx.fuse = fuse
         ctx.save_for_backward(x, w, y if relu else None)
         return y
 
@@ -101,23 +125,37 @@ class ConvBiasActFn(torch.autograd.Function):
         x, w, out = ctx.saved_tensors
         st, pd, dl = ctx.conf
         want_db = ctx.needs_input_grad[2]
-        dy, db = _bias_act_bwd(g, out, ctx.relu, want_db)
+        link, k, roles = ctx.fuse if ctx.fuse is not None else (None, -1, ())
+        relu = ctx.relu and not (link is not None and link.premask.get(k) and not want_db)
+        dy, db = _bias_act_bwd(g, out, relu, want_db)
         if db is not None and db.dtype != ctx.bdtype:
             db = db.to(ctx.bdtype)
+        dres = dy if ctx.has_res else None
+        if dres is not None and "stash_res" in roles and link.taker and ctx.needs_input_grad[3]:
+            link.stash.append(dres)
+            dres = None
+        add = link.stash.pop() if "take_res" in roles and link.stash else None
+        mask = x if "mask_in" in roles else None
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            if convwg.dgrad_supported(w, tuple(x.shape), st):
-                dx = convwg.conv_dgrad(dy, w, tuple(x.shape), st, pd, dl)
+            if convwg.dgrad_supported(w, tuple(x.shape), st) and (add is None or add.data_ptr() % 16 == 0):
+                dx = convwg.conv_dgrad(dy, w, tuple(x.shape), st, pd, dl, add=add, mask=mask)
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, st, pd, dl, False, [0, 0], 1,
                                                          [True, False, False])[0]
+                if add is not None:
+                    dx = dx + add
+                if mask is not None:
+                    dx = torch.where(mask > 0, dx, torch.zeros_like(dx))
+        elif add is not None:
+            raise RuntimeError("BlockLink: residual gradient stashed for a conv without an input gradient")
         if ctx.needs_input_grad[1]:
             if w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0:
                 dw = convwg.conv_wgrad(dy, x, tuple(w.shape), st, pd, dl)
             else:
                 dw = torch.ops.aten.convolution_backward(dy, x, w, None, st, pd, dl, False, [0, 0], 1,
                                                          [False, True, False])[1]
-        return dx, dw, db, (dy if ctx.has_res else None), None, None, None, None
+        return dx, dw, db, dres, None, None, None, None, None
 
 
 def _fused_ok(y, b, residual) -> bool:
@@ -142,14 +180,22 @@ def bias_act(y: torch.Tensor, b: Optional[torch.Tensor], residual: Optional[torc
 
 
 
+def fused_conv_ok(x, w, b=None, residual=None, stride=1, padding=0, dilation=1) -> bool:
+    """True when conv_bias_act runs ConvBiasActFn (every direction on csrc/convwg.hip)."""
+    return _fused_ok(x, b, residual) and x.shape[1] == w.shape[1] and \
+        convwg.fwd_supported(x, w, b, residual, stride, padding, dilation)
+
+
 def conv_bias_act(x, w, b=None, stride=1, padding=0, dilation=1, relu: bool = False,
-                  residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  residual: Optional[torch.Tensor] = None, fuse=None) -> torch.Tensor:
     """act(conv2d(x, w) + b (+ residual)) -- one conv (MIOpen forward and input gradient;
-    the weight gradient from csrc/convwg.hip where it tiles) + one fused epilogue pass."""
+    the weight gradient from csrc/convwg.hip where it tiles) + one fused epilogue pass.
+    ``fuse``: (BlockLink, index, roles) -- only honoured on the ConvBiasActFn path (the
+    caller checks fused_conv_ok before promising a role to a neighbour)."""
     if _fused_ok(x, b, residual) and x.shape[1] == w.shape[1]:
         if convwg.fwd_supported(x, w, b, residual, stride, padding, dilation):
             # forward, input and weight gradients all implicit GEMMs (ops/convwg.py)
-            return ConvBiasActFn.apply(x, w, b, residual, relu, stride, padding, dilation)
+            return ConvBiasActFn.apply(x, w, b, residual, relu, stride, padding, dilation, fuse)
         if convwg.supported(x, w, stride, padding, dilation):
             # MIOpen forward / input gradient, implicit-GEMM weight gradient (ops/convwg.py)
             return bias_act(convwg.conv2d_wg(x, w, stride, padding, dilation), b, residual, relu)

@@ -15,7 +15,7 @@ STEPS="${STEPS:-tests smoke bench}"
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 ${T_TESTS:-900} python -u -m pytest tests -m gpu ${PYTEST_X--x} -q --timeout ${T_TEST:-300} --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1; rc=$?
+      timeout -k 10 ${T_TESTS:-900} python -u -m pytest ${PYTEST_TARGET:-tests} -m gpu ${PYTEST_X--x} -q --timeout ${T_TEST:-300} --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1; rc=$?
       tail -30 gpurun_out/gpu_tests.log; echo "tests rc=$rc"; ok $rc || exit $rc ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?

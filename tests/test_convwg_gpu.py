@@ -169,3 +169,60 @@ def _fused_path_case(convwg, conv_bias_act):
                                                     [0, 0], 1, [True, True, False])
     for got, ref in ((xg.grad, dx), (wg.grad, dw), (bg.grad, dy.sum((0, 2, 3))), (rg.grad, dy)):
         _close(got, ref)
+
+
+@pytest.mark.parametrize("case", [(1, 128, 64, 13, 9, 3, 1, 1, 1), (2, 256, 128, 25, 42, 1, 1, 0, 1)])
+def test_conv_dgrad_add_and_relu_mask_epilogue(case):
+    """dX + add, then * (mask > 0), in the dgrad store (the bottleneck's residual gradient and
+    the producer's ReLU) against the fp32 reference of the same three ops."""
+    from mxtrain.ops import convwg
+    N, Cin, Cout, H, W, k, stride, pad, dil = case
+    x, dy = _inputs(*case, seed=17)
+    g = torch.Generator().manual_seed(19)
+    w = (torch.randn(Cout, k, k, Cin, generator=g) * 0.1).to(torch.bfloat16).cuda().permute(0, 3, 1, 2)
+    cl = torch.channels_last
+    add = torch.randn(x.shape, generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=cl)
+    mask = torch.randn(x.shape, generator=g).relu().to(torch.bfloat16).cuda().contiguous(memory_format=cl)
+    dx = convwg.conv_dgrad(dy, w, tuple(x.shape), stride, pad, dil, add=add, mask=mask)
+    ref = (_ref_dx(dy, w, tuple(x.shape), stride, pad, dil) + add.float().cpu()) * (mask.float().cpu() > 0)
+    _close(dx, ref)
+
+
+def test_bottleneck_backward_fusion_matches_unfused():
+    """models/resnet.py Bottleneck with the BlockLink backward fusion (ReLU masks in the
+    consumers' dgrad stores, identity residual gradient added in conv1's dgrad) against the
+    same blocks with fusion off: input and weight gradients agree to bf16 rounding (the
+    fused path rounds once where the unfused one rounds the dgrad, then adds)."""
+    from mxtrain.models.resnet import Bottleneck
+    from mxtrain.ops import convwg
+    fwd0, convwg.FWD = convwg.FWD, True
+    try:
+        torch.manual_seed(3)
+        blocks = torch.nn.Sequential(Bottleneck(512, 128, stride=1), Bottleneck(512, 128, stride=1),
+                                     Bottleneck(512, 256, stride=2)).cuda()
+        for m in blocks.modules():
+            if hasattr(m, "norm") and hasattr(m.norm, "running_var"):
+                m.norm.running_var.uniform_(0.5, 2.0)
+                m.norm.bias.uniform_(-0.2, 0.2)
+        x0 = torch.randn(2, 512, 40, 48, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        gy = None
+        out = {}
+        for fuse in (False, True):
+            for b in blocks:
+                b.fuse_backward = fuse
+            blocks.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_()
+            y = blocks(x)
+            if gy is None:
+                gy = torch.randn_like(y)
+            y.backward(gy)
+            torch.cuda.synchronize()
+            out[fuse] = (y.detach().float(), x.grad.float(),
+                         [p.grad.float() for p in blocks.parameters() if p.grad is not None])
+        assert torch.equal(out[False][0], out[True][0])
+        _close(out[True][1], out[False][1])
+        assert len(out[True][2]) == len(out[False][2]) > 0
+        for a, b in zip(out[True][2], out[False][2]):
+            _close(a, b)
+    finally:
+        convwg.FWD = fwd0
