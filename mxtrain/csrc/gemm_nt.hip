@@ -52,7 +52,6 @@ struct Args {
   int lda, ldb, ldc, ldx;
   int K, N;
   int tiles_n, gm;
-  int tiles_m;
 };
 
 __device__ __forceinline__ float dpp_rowsum16(float v) {
@@ -385,206 +384,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_nt_kernel(const Args 
   }
 }
 
-// ---- persistent form: the grid is (at most) one resident workgroup per CU x MINB and each
-// workgroup walks the tiles L = w, w + G, w + 2G, ... (w = its XCD-contiguous id) as ONE
-// continuous stream of K-steps through the LDS-DMA ring.  The look-ahead DMA of the ring
-// therefore crosses tile boundaries: while a tile's last K-steps and its epilogue run, the
-// next tile's first NSLOT - 1 K-steps are already in flight, and the epilogue's stores drain
-// while the next tile computes.  One-tile-per-CU launches pay both in full (profiles/r3_s2:
-// ~2.9k cycles to first data + ~8.8k of HBM-bound epilogue on a 46k-cycle loop at
-// 4096 x 4096 x 1024); here the tiles are smaller and every CU runs several.
-// The ring slot is a runtime value (a scalar add on the fragment and DMA addresses per
-// K-step), so the per-tile K-loop is a plain loop and the epilogue is emitted once.
-template <int NSLOT, int PER, int S>
-__device__ __forceinline__ void ring_wait(int later, bool post) {
-  // retire this step's pieces; `post`: the previous tile's epilogue issued >= S vector-memory
-  // instructions after them (C stores), which may stay in flight
-  if (post) {
-    if (NSLOT >= 4 && later >= 2) vm_wait<(NSLOT >= 4 ? 2 : 0) * PER + S>();
-    else if (NSLOT >= 3 && later >= 1) vm_wait<(NSLOT >= 3 ? 1 : 0) * PER + S>();
-    else vm_wait<S>();
-  } else {
-    if (NSLOT >= 4 && later >= 2) vm_wait<(NSLOT >= 4 ? 2 : 0) * PER>();
-    else if (NSLOT >= 3 && later >= 1) vm_wait<(NSLOT >= 3 ? 1 : 0) * PER>();
-    else vm_wait<0>();
-  }
-}
-
-template <bool BKC, int WM, int WN, int FM, int FN, int BKT, int NSLOT, int MINB, int EPI>
-__global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_pt_kernel(const Args g) {
-  using Gm = Geo<BKC, WM, WN, FM, FN, BKT, NSLOT>;
-  constexpr int BM = Gm::BM, BN = Gm::BN, RA = Gm::RA, RB = Gm::RB, IA = Gm::IA;
-  constexpr int PA = Gm::PA, PB = Gm::PB, SLOT = Gm::SLOT;
-  constexpr int PER = PA + PB;
-  constexpr int LPR = RA / 16;
-  static_assert(NSLOT <= 4, "the post-epilogue wait covers look-ahead <= 2 steps");
-  // C stores of one epilogue per wave (a lower bound of its vector-memory instructions: the
-  // wait after it is exact or conservative, never early)
-  constexpr int S_EPI = FM * (FN / 2) < 48 ? FM * (FN / 2) : 48;
-  __shared__ __attribute__((aligned(1024))) char smem[Gm::LDS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int Gw = gridDim.x;
-  const int w = xcd_remap(blockIdx.x, Gw);
-  const int T = g.tiles_m * g.tiles_n;
-  const int ntl = (T - w + Gw - 1) / Gw;
-  const int nk = g.K / BKT;
-  const int total = ntl * nk;
-  const int per_group = g.gm * g.tiles_n;
-  auto tile_mn = [&](int tl, int& tm, int& tn) __attribute__((always_inline)) {
-    const int L = tl * Gw + w;
-    const int grp = L / per_group, rem = L - grp * per_group;
-    tm = grp * g.gm + rem % g.gm;
-    tn = rem / g.gm;
-  };
-  auto base_a = [&](int tm) __attribute__((always_inline)) {
-    return reinterpret_cast<const char*>(g.a + (size_t)tm * BM * g.lda);
-  };
-  auto base_b = [&](int tn) __attribute__((always_inline)) {
-    return reinterpret_cast<const char*>(BKC ? g.b + (size_t)tn * BN * g.ldb : g.b + tn * BN);
-  };
-
-  uint32_t voA[PA], voB[PB];
-#pragma unroll
-  for (int j = 0; j < PA; ++j) {
-    const int row = (PA * wave + j) * (1024 / RA) + lane / LPR;
-    voA[j] = (uint32_t)(row * g.lda + 8 * ((lane % LPR) ^ kc_swz<RA>(row))) * 2u;
-  }
-  if constexpr (BKC) {
-#pragma unroll
-    for (int j = 0; j < PB; ++j) {
-      const int row = (PB * wave + j) * (1024 / RB) + lane / LPR;
-      voB[j] = (uint32_t)(row * g.ldb + 8 * ((lane % LPR) ^ kc_swz<RB>(row))) * 2u;
-    }
-  } else {
-    constexpr int CB = RB / 16;
-#pragma unroll
-    for (int j = 0; j < PB; ++j) {
-      const int k = (PB * wave + j) * (1024 / RB) + lane / CB;
-      voB[j] = (uint32_t)(k * g.ldb + 8 * pchunk(k, lane % CB)) * 2u;
-    }
-  }
-  const size_t stepA = (size_t)BKT * 2, stepB = BKC ? (size_t)BKT * 2 : (size_t)BKT * g.ldb * 2;
-
-  const int G = lane >> 4, i = lane & 15;
-  const int wm = wave / WN, wn = wave % WN;
-  const int offA = (16 * FM * wm + i) * RA;
-  int cA[BKT / 32];
-#pragma unroll
-  for (int kk = 0; kk < BKT / 32; ++kk) cA[kk] = 16 * ((4 * kk + G) ^ kc_swz<RA>(i));
-  int offBu[FN];
-#pragma unroll
-  for (int u = 0; u < FN; ++u) {
-    if constexpr (BKC) {
-      offBu[u] = (16 * FN * wn + i) * RB + 16 * u * RB;
-    } else {
-      const int krow = 8 * G + (i >> 2);
-      offBu[u] = krow * RB + ((((FN * wn + u) ^ gsw(krow)) << 1) | ((i & 3) >> 1)) * 16 + (i & 1) * 8;
-    }
-  }
-
-  const uint32_t lds0 = lds_addr(smem);
-  const uint32_t ldsA = __builtin_amdgcn_readfirstlane(lds0 + PA * wave * 1024);
-  const uint32_t ldsB = __builtin_amdgcn_readfirstlane(lds0 + IA + PB * wave * 1024);
-
-  // fetch cursor: global step fgs = (tile ftl, K-step fit) into ring slot fslot
-  int fgs = 0, fit = 0, ftl = 0, fslot = 0;
-  const char* fA;
-  const char* fB;
-  {
-    int tm, tn;
-    tile_mn(0, tm, tn);
-    fA = base_a(tm);
-    fB = base_b(tn);
-  }
-  auto piece = [&](int j) __attribute__((always_inline)) {
-    if (j < PA) dma16s(fA + fit * stepA, voA[j], ldsA + fslot * SLOT + j * 1024);
-    else dma16s(fB + fit * stepB, voB[j - PA], ldsB + fslot * SLOT + (j - PA) * 1024);
-  };
-  auto advance_fetch = [&]() __attribute__((always_inline)) {
-    ++fgs;
-    fslot = fslot + 1 == NSLOT ? 0 : fslot + 1;
-    if (++fit == nk) {
-      fit = 0;
-      if (++ftl < ntl) {
-        int tm, tn;
-        tile_mn(ftl, tm, tn);
-        fA = base_a(tm);
-        fB = base_b(tn);
-      }
-    }
-  };
-#pragma unroll
-  for (int q = 0; q < NSLOT - 1; ++q)
-    if (fgs < total) {
-#pragma unroll
-      for (int j = 0; j < PER; ++j) piece(j);
-      advance_fetch();
-    }
-
-  constexpr bool XRES = FM >= FN;
-  constexpr int NSTREAM = XRES ? FN : FM;
-  constexpr int NS = (BKT / 32) * NSTREAM;
-  constexpr int SPREAD = NS / 2 >= PER ? NS / 2 : NS;
-  int gs = 0, slot = 0;
-  for (int tl = 0; tl < ntl; ++tl) {
-    int tm, tn;
-    tile_mn(tl, tm, tn);
-    f32x4 acc[FM][FN];
-#pragma unroll
-    for (int s = 0; s < FM; ++s)
-#pragma unroll
-      for (int u = 0; u < FN; ++u) acc[s][u] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int it = 0; it < nk; ++it, ++gs) {
-      ring_wait<NSLOT, PER, S_EPI>(total - 1 - gs, tl > 0 && it < NSLOT - 1);
-      __builtin_amdgcn_s_barrier();
-      const bool fetch = fgs < total;
-      const char* As = smem + slot * SLOT;
-      const char* Bs = As + IA;
-      auto wfrag = [&](int u, int kk) __attribute__((always_inline)) {
-        if constexpr (BKC) return lds_read8(Bs, offBu[u] + cA[kk]);
-        else return cat(tr_read(Bs, offBu[u] + 32 * RB * kk), tr_read(Bs, offBu[u] + 32 * RB * kk + 4 * RB));
-      };
-      auto xfrag = [&](int s, int kk) __attribute__((always_inline)) {
-        return lds_read8(As, offA + 16 * s * RA + cA[kk]);
-      };
-#pragma unroll
-      for (int kk = 0; kk < BKT / 32; ++kk) {
-        if constexpr (XRES) {
-          bf16x8 x[FM];
-#pragma unroll
-          for (int s = 0; s < FM; ++s) x[s] = xfrag(s, kk);
-#pragma unroll
-          for (int u = 0; u < FN; ++u) {
-            const bf16x8 wv = wfrag(u, kk);
-            const int qq = kk * NSTREAM + u;
-#pragma unroll
-            for (int j = 0; j < PER; ++j)
-              if (qq < SPREAD && j * SPREAD / PER == qq && fetch) piece(j);
-#pragma unroll
-            for (int s = 0; s < FM; ++s) acc[s][u] = mfma16(wv, x[s], acc[s][u]);
-          }
-        } else {
-          bf16x8 wv[FN];
-#pragma unroll
-          for (int u = 0; u < FN; ++u) wv[u] = wfrag(u, kk);
-#pragma unroll
-          for (int s = 0; s < FM; ++s) {
-            const bf16x8 x = xfrag(s, kk);
-            const int qq = kk * NSTREAM + s;
-#pragma unroll
-            for (int j = 0; j < PER; ++j)
-              if (qq < SPREAD && j * SPREAD / PER == qq && fetch) piece(j);
-#pragma unroll
-            for (int u = 0; u < FN; ++u) acc[s][u] = mfma16(wv[u], x, acc[s][u]);
-          }
-        }
-      }
-      if (fetch) advance_fetch();
-      slot = slot + 1 == NSLOT ? 0 : slot + 1;
-    }
-    epilogue<WM, WN, FM, FN, EPI>(g, acc, tm, tm * BM, tn * BN, wave, lane);
-  }
-}
 
 template <bool BKC, int WM, int WN, int FM, int FN, int BKT, int NSLOT, int MINB, int EPI>
 int launch(Args a, int M, hipStream_t stream) {
@@ -600,38 +399,6 @@ int launch(Args a, int M, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-int cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
-
-template <bool BKC, int WM, int WN, int FM, int FN, int BKT, int NSLOT, int MINB, int EPI>
-int launch_pt(Args a, int M, hipStream_t stream) {
-  using Gm = Geo<BKC, WM, WN, FM, FN, BKT, NSLOT>;
-  if (M % Gm::BM || a.N % Gm::BN || a.K % BKT || a.K <= 0) return (int)hipErrorInvalidValue;
-  a.tiles_m = M / Gm::BM;
-  a.tiles_n = a.N / Gm::BN;
-  int gm = 8;
-  while (gm > 1 && a.tiles_m % gm) gm >>= 1;
-  a.gm = gm;
-  const int tiles = a.tiles_m * a.tiles_n;
-  const int resident = cu_count() * MINB;
-  // every workgroup the same number of tiles (+-1): the largest grid <= resident that
-  // leaves no workgroup a partial extra round where possible
-  int grid = tiles <= resident ? tiles : resident;
-  const int rounds = (tiles + grid - 1) / grid;
-  grid = (tiles + rounds - 1) / rounds;
-  hipLaunchKernelGGL((gemm_pt_kernel<BKC, WM, WN, FM, FN, BKT, NSLOT, MINB, EPI>), dim3(grid), dim3(Gm::NT), 0,
-                     stream, a);
-  return (int)hipGetLastError();
-}
-
-
 // variant -> {BM, BN, rows per column-partial block (16 FM), B may be K-major}
 struct Variant {
   int bm, bn, part_rows, kmajor_ok;
@@ -646,14 +413,6 @@ constexpr Variant kVariants[] = {
     {256, 256, 128, 1},   // 6: as 0 with BK 64 and a 2-slot ring
     {128, 128, 64, 1},    // 7: 8 waves 2 x 4 of 64 x 32, BK 32, 6-slot ring
     {256, 128, 64, 1},    // 8: 8 waves 4 x 2 of 64 x 64, BK 32, 5-slot ring (120 KiB)
-    // persistent (gemm_pt_kernel): several tiles per CU, look-ahead DMA across tiles
-    {256, 128, 64, 1},    // 9: 8 waves 4 x 2 of 64 x 64, BK 32, 4-slot ring (96 KiB)
-    {128, 256, 64, 1},    // 10: 8 waves 2 x 4 of 64 x 64, BK 32, 4-slot ring (96 KiB)
-    {128, 128, 64, 1},    // 11: 8 waves 2 x 4 of 64 x 32, BK 64, 4-slot ring (128 KiB)
-    {128, 128, 64, 1},    // 12: 4 waves 2 x 2 of 64 x 64, BK 64, 2-slot ring, two workgroups per CU
-    {256, 256, 128, 1},   // 13: 8 waves 2 x 4 of 128 x 64, BK 32, 4-slot ring (128 KiB)
-    {128, 64, 64, 0},     // 14: 4 waves 2 x 2 of 64 x 32, BK 64, 4-slot ring (96 KiB); forward only
-    {256, 192, 64, 0},    // 15: 8 waves 4 x 2 of 64 x 96, BK 64, 2-slot ring (112 KiB); forward only
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -671,17 +430,6 @@ int dispatch(int variant, const Args& a, int M, hipStream_t st) {
     case 6: return launch<BKC, 2, 4, 8, 4, 64, 2, 1, EPI>(a, M, st);
     case 7: return launch<BKC, 2, 4, 4, 2, 32, 6, 1, EPI>(a, M, st);
     case 8: return launch<BKC, 4, 2, 4, 4, 32, 5, 1, EPI>(a, M, st);
-    case 9: return launch_pt<BKC, 4, 2, 4, 4, 32, 4, 1, EPI>(a, M, st);
-    case 10: return launch_pt<BKC, 2, 4, 4, 4, 32, 4, 1, EPI>(a, M, st);
-    case 11: return launch_pt<BKC, 2, 4, 4, 2, 64, 4, 1, EPI>(a, M, st);
-    case 12: return launch_pt<BKC, 2, 2, 4, 4, 64, 2, 2, EPI>(a, M, st);
-    case 13: return launch_pt<BKC, 2, 4, 8, 4, 32, 4, 1, EPI>(a, M, st);
-    case 14:
-      if constexpr (BKC) return launch_pt<BKC, 2, 2, 4, 2, 64, 4, 1, EPI>(a, M, st);
-      else return (int)hipErrorInvalidValue;
-    case 15:
-      if constexpr (BKC) return launch_pt<BKC, 4, 2, 4, 6, 64, 2, 1, EPI>(a, M, st);
-      else return (int)hipErrorInvalidValue;
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -145,6 +145,100 @@ class RPNHead(nn.Module):
         # NHWC flatten -> [B, H*W*A] / [B, H*W*A, 4] (cell-major, anchor-minor)
         return lg.permute(0, 2, 3, 1).reshape(B, -1), bx.permute(0, 2, 3, 1).reshape(B, -1, 4)
 
+    def forward_levels(self, P: List[torch.Tensor]):
+        """The shared head over all FPN levels as ONE 3x3 conv and ONE 1x1 conv (cls and box
+        weights stacked, padded to 8 output channels) on a canvas holding every level
+        (``level_canvas``): 2 launches per direction instead of 15, and no gradient
+        accumulation of the shared weights across levels.  Same math as ``forward`` per
+        level: the levels sit 1 zero row / column apart, so the 3x3 window of a level
+        pixel sees exactly its level's zero-padded neighbourhood; canvas pixels outside
+        the levels get no gradient.  Returns ([B, H*W*A] logits, [B, H*W*A, 4] deltas)
+        per level."""
+        lay = level_canvas([(p.shape[2], p.shape[3]) for p in P])
+        if lay is None or not self.pack_levels:
+            return [self(p) for p in P]
+        dt = P[0].dtype
+        na = self.cls.weight.shape[0]
+        x = _PackLevels.apply(lay, *P)
+        t = conv_bias_act(x, cw(self.conv.weight, dt), cw(self.conv.bias, dt), padding=1, relu=True)
+        pad = (-5 * na) % 8
+        w = torch.cat([cw(self.cls.weight, dt), cw(self.box.weight, dt)]
+                      + ([cw(self.cls.weight, dt).new_zeros(pad, *self.cls.weight.shape[1:])] if pad else []))
+        b = torch.cat([cw(self.cls.bias, dt), cw(self.box.bias, dt)]
+                      + ([cw(self.cls.bias, dt).new_zeros(pad)] if pad else []))
+        o = conv_bias_act(t, w.contiguous(memory_format=torch.channels_last), b)
+        geo = [(y0, x0, p.shape[2], p.shape[3]) for (y0, x0), p in zip(lay[2], P)]
+        flat = _UnpackLevels.apply(o, geo, na)
+        return [(flat[2 * i], flat[2 * i + 1]) for i in range(len(P))]
+
+    pack_levels = True
+
+
+def level_canvas(shapes):
+    """Layout of FPN levels on one canvas: level 0 at the origin, the others left to right
+    on a shelf below it, one zero row / column between neighbours.  Returns (Hc, Wc,
+    [(y0, x0)] per level), or None when the shelf does not fit under level 0."""
+    (h0, w0), rest = shapes[0], shapes[1:]
+    if not rest:
+        return None
+    x, offs = 0, [(0, 0)]
+    for h, w in rest:
+        offs.append((h0 + 1, x))
+        x += w + 1
+    if x - 1 > w0:
+        return None
+    return h0 + 1 + max(h for h, _ in rest), w0, offs
+
+
+class _PackLevels(torch.autograd.Function):
+    """[B, C, Hc, Wc] canvas (channels_last, zero outside the levels) of the FPN levels;
+    backward hands each level its slice of the canvas gradient (views, no copies)."""
+
+    @staticmethod
+    def forward(ctx, lay, *levels):
+        Hc, Wc, offs = lay
+        p0 = levels[0]
+        c = torch.zeros(p0.shape[0], p0.shape[1], Hc, Wc, dtype=p0.dtype, device=p0.device,
+                        ).contiguous(memory_format=torch.channels_last)
+        for (y0, x0), p in zip(offs, levels):
+            c[:, :, y0:y0 + p.shape[2], x0:x0 + p.shape[3]].copy_(p)
+        ctx.geo = [(y0, x0, p.shape[2], p.shape[3]) for (y0, x0), p in zip(offs, levels)]
+        return c
+
+    @staticmethod
+    def backward(ctx, g):
+        return (None,) + tuple(g[:, :, y0:y0 + h, x0:x0 + w] for y0, x0, h, w in ctx.geo)
+
+
+class _UnpackLevels(torch.autograd.Function):
+    """Per level ([B, h*w*A] logits, [B, h*w*A, 4] deltas) out of the head's canvas output
+    [B, 5A(+pad), Hc, Wc]; backward writes every level's gradients into ONE zeroed canvas
+    gradient (instead of a full-size zero tensor per slice)."""
+
+    @staticmethod
+    def forward(ctx, o, geo, na):
+        ctx.geo, ctx.na, ctx.shape = geo, na, o.shape
+        B = o.shape[0]
+        out = []
+        for y0, x0, h, w in geo:
+            v = o[:, :, y0:y0 + h, x0:x0 + w].permute(0, 2, 3, 1)          # [B, h, w, 5A(+pad)]
+            out += [v[..., :na].reshape(B, -1), v[..., na:5 * na].reshape(B, -1, 4)]
+        return tuple(out)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        B, C, Hc, Wc = ctx.shape
+        na = ctx.na
+        ref = next(g for g in gs if g is not None)
+        d = torch.zeros(B, Hc, Wc, C, dtype=ref.dtype, device=ref.device)     # NHWC memory
+        for i, (y0, x0, h, w) in enumerate(ctx.geo):
+            gl, gb = gs[2 * i], gs[2 * i + 1]
+            if gl is not None:
+                d[:, y0:y0 + h, x0:x0 + w, :na].copy_(gl.reshape(B, h, w, na))
+            if gb is not None:
+                d[:, y0:y0 + h, x0:x0 + w, na:5 * na].copy_(gb.reshape(B, h, w, 4 * na))
+        return d.permute(0, 3, 1, 2), None, None
+
 
 class BoxHead(nn.Module):
     def __init__(self, c: int, fc: int, ncls: int):
@@ -376,7 +470,7 @@ class MaskRCNN(nn.Module):
         gt_mask_table int32 [B, G, 5]) the flat uint8 buffer of packed instance crops."""
         cfg = self.cfg
         P = self.features(images)
-        lv = [self.rpn(p) for p in P]
+        lv = self.rpn.forward_levels(P)
         logits_lv = [l for l, _ in lv]
         deltas_lv = [d for _, d in lv]
         anchors_lv = self.anchors([(p.shape[2], p.shape[3]) for p in P], images.device)

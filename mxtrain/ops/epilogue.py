@@ -180,10 +180,18 @@ def bias_act(y: torch.Tensor, b: Optional[torch.Tensor], residual: Optional[torc
 
 
 
+def _conv_in_ok(x, w, b, residual) -> bool:
+    """conv_bias_act's input-side conditions for the fused epilogues (the residual has the
+    OUTPUT's shape: convwg.fwd_supported / bias_act check it against the conv output)."""
+    return (_ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and _nhwc(x) and _nhwc(residual)
+            and x.shape[1] == w.shape[1] and w.shape[0] % 8 == 0 and w.shape[0] <= 2048
+            and (b is None or (b.dtype == torch.bfloat16 and b.is_contiguous()))
+            and (residual is None or residual.dtype == torch.bfloat16))
+
+
 def fused_conv_ok(x, w, b=None, residual=None, stride=1, padding=0, dilation=1) -> bool:
     """True when conv_bias_act runs ConvBiasActFn (every direction on csrc/convwg.hip)."""
-    return _fused_ok(x, b, residual) and x.shape[1] == w.shape[1] and \
-        convwg.fwd_supported(x, w, b, residual, stride, padding, dilation)
+    return _conv_in_ok(x, w, b, residual) and convwg.fwd_supported(x, w, b, residual, stride, padding, dilation)
 
 
 def conv_bias_act(x, w, b=None, stride=1, padding=0, dilation=1, relu: bool = False,
@@ -192,7 +200,7 @@ def conv_bias_act(x, w, b=None, stride=1, padding=0, dilation=1, relu: bool = Fa
     the weight gradient from csrc/convwg.hip where it tiles) + one fused epilogue pass.
     ``fuse``: (BlockLink, index, roles) -- only honoured on the ConvBiasActFn path (the
     caller checks fused_conv_ok before promising a role to a neighbour)."""
-    if _fused_ok(x, b, residual) and x.shape[1] == w.shape[1]:
+    if _conv_in_ok(x, w, b, residual):
         if convwg.fwd_supported(x, w, b, residual, stride, padding, dilation):
             # forward, input and weight gradients all implicit GEMMs (ops/convwg.py)
             return ConvBiasActFn.apply(x, w, b, residual, relu, stride, padding, dilation, fuse)

@@ -78,7 +78,7 @@ def main():
             if gelu:
                 ref = ref * Gm._gelu_grad_ref(hh.float())
         variants = []
-        for v in ([int(x) for x in os.environ["VARIANTS"].split(",")] if os.environ.get("VARIANTS") else range(16)):
+        for v in ([int(x) for x in os.environ["VARIANTS"].split(",")] if os.environ.get("VARIANTS") else range(9)):
             bm, bn, _, kok = Gm._nt_tile(v)
             if M % bm or N % bn or (kind.startswith("dg") and not kok):
                 continue

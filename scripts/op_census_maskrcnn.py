@@ -53,7 +53,8 @@ def main():
     for _ in range(5):
         step()
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True,
+                 record_shapes=True) as prof:
         step()
         torch.cuda.synchronize()
     # kernels per aten op (direct children), attributed to the innermost repo frame
@@ -85,6 +86,14 @@ def main():
         for k in getattr(e, "kernels", []) or []:
             if pat.search(k.name):
                 sel[(k.name[:60], e.name, where)] += 1
+    # gradient-accumulation / residual adds by operand shape (backward ops carry no stack)
+    shp = collections.Counter()
+    for e in evs:
+        if e.device_type.name == "CPU" and e.name in ("aten::add", "aten::add_") and getattr(e, "kernels", None):
+            shp[(e.name, str(e.input_shapes)[:90])] += len(e.kernels)
+    print("\nadd kernels by operand shapes:")
+    for (name, sh), n in shp.most_common(60):
+        print(f"{n:5d}  {name:10s} {sh}")
     print("\nselected kernels by launching op:")
     for (kn, name, where), n in sel.most_common(80):
         print(f"{n:5d}  {kn:60s} {name:32s} {where}")

@@ -188,41 +188,52 @@ def test_conv_dgrad_add_and_relu_mask_epilogue(case):
     _close(dx, ref)
 
 
-def test_bottleneck_backward_fusion_matches_unfused():
+def test_bottleneck_backward_fusion_matches_unfused(monkeypatch):
     """models/resnet.py Bottleneck with the BlockLink backward fusion (ReLU masks in the
     consumers' dgrad stores, identity residual gradient added in conv1's dgrad) against the
-    same blocks with fusion off: input and weight gradients agree to bf16 rounding (the
-    fused path rounds once where the unfused one rounds the dgrad, then adds)."""
+    same blocks with fusion off: identical forward, input and weight gradients equal to bf16
+    rounding (the fused path rounds once where the unfused one rounds the dgrad, then adds).
+    Shapes sized so every conv takes the implicit-GEMM path (>= 64 output tiles)."""
     from mxtrain.models.resnet import Bottleneck
     from mxtrain.ops import convwg
-    fwd0, convwg.FWD = convwg.FWD, True
-    try:
-        torch.manual_seed(3)
-        blocks = torch.nn.Sequential(Bottleneck(512, 128, stride=1), Bottleneck(512, 128, stride=1),
-                                     Bottleneck(512, 256, stride=2)).cuda()
-        for m in blocks.modules():
-            if hasattr(m, "norm") and hasattr(m.norm, "running_var"):
-                m.norm.running_var.uniform_(0.5, 2.0)
-                m.norm.bias.uniform_(-0.2, 0.2)
-        x0 = torch.randn(2, 512, 40, 48, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        gy = None
-        out = {}
-        for fuse in (False, True):
-            for b in blocks:
-                b.fuse_backward = fuse
-            blocks.zero_grad(set_to_none=True)
-            x = x0.clone().requires_grad_()
-            y = blocks(x)
-            if gy is None:
-                gy = torch.randn_like(y)
-            y.backward(gy)
-            torch.cuda.synchronize()
-            out[fuse] = (y.detach().float(), x.grad.float(),
-                         [p.grad.float() for p in blocks.parameters() if p.grad is not None])
-        assert torch.equal(out[False][0], out[True][0])
-        _close(out[True][1], out[False][1])
-        assert len(out[True][2]) == len(out[False][2]) > 0
-        for a, b in zip(out[True][2], out[False][2]):
-            _close(a, b)
-    finally:
-        convwg.FWD = fwd0
+    monkeypatch.setattr(convwg, "FWD", True)
+    monkeypatch.setattr(convwg, "DGRAD", True)
+    seen = {"add": 0, "mask": 0}
+    real = convwg.conv_dgrad
+
+    def spy(*a, add=None, mask=None, **k):
+        seen["add"] += add is not None
+        seen["mask"] += mask is not None
+        return real(*a, add=add, mask=mask, **k)
+
+    monkeypatch.setattr(convwg, "conv_dgrad", spy)
+    torch.manual_seed(3)
+    blocks = torch.nn.Sequential(Bottleneck(512, 128, stride=1), Bottleneck(512, 128, stride=1),
+                                 Bottleneck(512, 256, stride=2)).cuda()
+    for m in blocks.modules():
+        if hasattr(m, "norm") and hasattr(m.norm, "running_var"):
+            m.norm.running_var.uniform_(0.5, 2.0)
+            m.norm.bias.uniform_(-0.2, 0.2)
+    x0 = torch.randn(4, 512, 80, 96, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gy = None
+    out = {}
+    for fuse in (False, False, True):
+        for b in blocks:
+            b.fuse_backward = fuse
+        seen.update(add=0, mask=0)
+        blocks.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        y = blocks(x)
+        if gy is None:
+            gy = torch.randn_like(y)
+        y.backward(gy)
+        torch.cuda.synchronize()
+        out[fuse] = (y.detach().float(), x.grad.float(),
+                     [p.grad.float() for p in blocks.parameters() if p.grad is not None])
+    # fused: conv2 + conv3 of all three blocks mask their input, conv1 of the two identity blocks adds
+    assert seen == {"add": 2, "mask": 6}, seen
+    assert torch.equal(out[False][0], out[True][0])
+    _close(out[True][1], out[False][1].cpu())
+    assert len(out[True][2]) == len(out[False][2]) == 10
+    for a, b in zip(out[True][2], out[False][2]):
+        _close(a, b.cpu())

@@ -591,8 +591,7 @@ def test_dropmask_layers_match_per_layer_calls(monkeypatch):
 
 
 # ------------------------------------------------------------------ forward / dgrad GEMMs
-NT_VARIANTS = list(range(16))
-NT_PERSISTENT = [9, 10, 11, 12, 13, 14, 15]
+NT_VARIANTS = list(range(9))
 
 
 @pytest.mark.parametrize("variant", NT_VARIANTS)
@@ -616,7 +615,7 @@ def test_gemm_nt_forward_epilogues(variant, epi):
         _close(out, ref, 2e-2, 1e-2, "y")
 
 
-@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("gelu", [False, True])
 def test_gemm_nt_dgrad_epilogues(variant, gelu):
     """dgrad dx = dy w (w K-major) and the fused GeLU' + bias-gradient epilogue."""
@@ -634,36 +633,6 @@ def test_gemm_nt_dgrad_epilogues(variant, gelu):
     _close(out, ref, 2e-2, 1e-2, "dx")
     if gelu:
         _close(dbg, db, 0.25, 2e-2, "dbias")
-
-
-@pytest.mark.parametrize("variant", NT_PERSISTENT)
-def test_gemm_nt_persistent_many_tiles(variant):
-    """Persistent variants (gemm_pt_kernel) with more tiles than resident workgroups: every
-    workgroup walks several tiles, the look-ahead DMA crosses tile boundaries and the ring
-    slot wraps mid-tile (K-steps per tile not a multiple of the ring depth); uneven rounds
-    (tiles not a multiple of the grid).  Forward with the bias-GeLU epilogue and, where the
-    variant takes K-major weights, dgrad with the GeLU' + bias-gradient epilogue, against
-    fp32 references."""
-    from mxtrain.ops import gemm as Gm
-    bm, bn, _, kok = Gm._nt_tile(variant)
-    M, N, K = 4096, 20 * bn, 320
-    g = torch.Generator(device=DEV).manual_seed(variant)
-    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
-    w = (torch.randn(N, K, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
-    b = torch.randn(N, device=DEV, generator=g).to(torch.bfloat16)
-    y, h = Gm.linear_fwd(x, w, b, gelu=True, variant=variant)
-    h_ref = x.float() @ w.float().t() + b.float()
-    _close(h, h_ref, 2e-2, 1e-2, "pre-activation")
-    _close(y, Gm._gelu_ref(h_ref), 2e-2, 1e-2, "gelu")
-    if kok:
-        dy = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
-        wk = (torch.randn(K, N, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
-        aux = (torch.randn(M, N, device=DEV, generator=g) * 2).to(torch.bfloat16)
-        db = torch.zeros(N, device=DEV, dtype=torch.bfloat16)
-        dx = Gm.linear_dgrad(dy, wk, gelu_aux=aux, dbias=db, accumulate=False, variant=variant)
-        d_ref = (dy.float() @ wk.float()) * Gm._gelu_grad_ref(aux.float())
-        _close(dx, d_ref, 2e-2, 1e-2, "dx")
-        _close(db, d_ref.sum(0), 0.25, 2e-2, "dbias")
 
 
 def test_gemm_nt_strided_inputs_and_plan():

@@ -362,3 +362,37 @@ def test_compute_weights_batched_cast_matches_per_tensor_casts():
     for a, b in zip(ga[:2], gb[:2]):
         assert a.dtype == torch.float32 and torch.equal(a, b)
     assert gb[2].dtype == torch.float32 and torch.allclose(ga[2], gb[2], rtol=2e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("shapes", [[(16, 48), (8, 24), (4, 12), (2, 6), (1, 3)],    # landscape: one shelf
+                                    [(48, 16), (24, 8), (12, 4), (6, 2), (3, 1)]])   # no fit: per level
+def test_rpn_level_canvas_matches_per_level(shapes):
+    """models/maskrcnn.py RPNHead.forward_levels (all FPN levels on one canvas, cls + box as
+    one conv) against the per-level head, fp64: outputs and every gradient exact."""
+    from mxtrain.models.maskrcnn import RPNHead, level_canvas
+    torch.manual_seed(0)
+    h = RPNHead(32, 3).double()
+    for m in (h.conv, h.cls, h.box):
+        torch.nn.init.normal_(m.weight, std=0.1)
+        torch.nn.init.normal_(m.bias, std=0.1)
+    P = [torch.randn(2, 32, a, b, dtype=torch.float64).contiguous(memory_format=torch.channels_last).requires_grad_()
+         for a, b in shapes]
+    res = {}
+    try:
+        for pack in (False, True):
+            RPNHead.pack_levels = pack
+            h.zero_grad()
+            for p in P:
+                p.grad = None
+            lv = h.forward_levels(P)
+            g = torch.Generator().manual_seed(1)
+            loss = sum((l * torch.randn(l.shape, generator=g, dtype=l.dtype)).sum()
+                       + (d * torch.randn(d.shape, generator=g, dtype=d.dtype)).sum() for l, d in lv)
+            loss.backward()
+            res[pack] = [t for l, d in lv for t in (l, d)] + [p.grad for p in P] + [q.grad for q in h.parameters()]
+    finally:
+        RPNHead.pack_levels = True
+    assert (level_canvas(shapes) is None) == (shapes[0][0] > shapes[0][1])
+    for a, b in zip(res[False], res[True]):
+        assert a.shape == b.shape
+        torch.testing.assert_close(a, b, rtol=0, atol=1e-10)
