@@ -217,9 +217,11 @@ struct ConvFw {
   const uint16_t* zero;
   uint16_t* y;           // [N * OH * OW][ldy]
   const uint16_t* bias;  // [Cout] or null
-  const uint16_t* res;   // [N * OH * OW][ldy] or null
+  const uint16_t* res;   // [N * OH * OW][ldy] or null; res_up: [N * OH/2 * OW/2][ldy], read
+                         // nearest-upsampled (the FPN top-down join, res[n][oh/2][ow/2])
   int ldx, ldy;
   int T, OH, OW, IH, IW;
+  int res_up;
   int KW, taps, stride, pad, dil;
   int Cin, tiles_n, nk, cib;
   float invOW, invOH;
@@ -339,7 +341,14 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
     for (int up = 0; up < FN / 2; ++up) {
       uint32_t c[2][2], h[2][2];
       if (RES) {
-        const uint4 rv = *reinterpret_cast<const uint4*>(cp.res + pr + colw + 32 * up + 8 * G);
+        size_t rr = pr;
+        if (cp.res_up) {
+          int q, ow, n, oh;
+          divmod(p < cp.T ? p : cp.T - 1, cp.OW, cp.invOW, q, ow);
+          divmod(q, cp.OH, cp.invOH, n, oh);
+          rr = ((size_t)(n * (cp.OH >> 1) + (oh >> 1)) * (cp.OW >> 1) + (ow >> 1)) * cp.ldy;
+        }
+        const uint4 rv = *reinterpret_cast<const uint4*>(cp.res + rr + colw + 32 * up + 8 * G);
         h[0][0] = rv.x; h[0][1] = rv.y; h[1][0] = rv.z; h[1][1] = rv.w;
         undeal(h[0][0], h[0][1], h[1][0], h[1][1]);
       }
@@ -710,8 +719,9 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
 }
 
 // d (int64[24]): {x, w, zero, y, bias, res, ldx, ldy, N, OH, OW, IH, IW, KH, KW, stride, pad,
-// dil, Cout, Cin, relu}: y = act(conv2d(x, w) + bias (+ res)) in NHWC bf16, weight
-// [Cout][KH][KW][Cin] (channels_last).  Cout a multiple of 128, Cin of 64.
+// dil, Cout, Cin, relu, res_up}: y = act(conv2d(x, w) + bias (+ res, or with res_up the 2x
+// nearest upsampling of res)) in NHWC bf16, weight [Cout][KH][KW][Cin] (channels_last).
+// Cout a multiple of 128, Cin of 64; res_up needs even OH, OW.
 MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   ConvFw cp{};
   cp.x = reinterpret_cast<const uint16_t*>(d[0]);
@@ -735,7 +745,9 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   const int Cout = (int)d[18];
   cp.Cin = (int)d[19];
   const bool relu = d[20] != 0;
+  cp.res_up = cp.res && d[21] != 0;
   const int64_t T = N * cp.OH * cp.OW;
+  if (cp.res_up && ((cp.OH | cp.OW) & 1)) return (int)hipErrorInvalidValue;
   if (N <= 0 || cp.IH <= 0 || cp.IW <= 0 || cp.OH <= 0 || cp.OW <= 0 || KH <= 0 || cp.KW <= 0 || cp.stride <= 0 ||
       cp.dil <= 0 || cp.pad < 0 || T >= (1 << 23) || N * cp.IH * cp.IW >= ((int64_t)1 << 31))
     return (int)hipErrorInvalidValue;

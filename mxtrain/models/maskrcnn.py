@@ -118,9 +118,15 @@ class FPN(nn.Module):
 
     def forward(self, feats: List[torch.Tensor]) -> List[torch.Tensor]:
         dt = feats[0].dtype
-        lat = [conv_bias_act(f, cw(m.weight, dt), cw(m.bias, dt)) for f, m in zip(feats, self.lateral)]
-        for i in range(len(lat) - 2, -1, -1):
-            lat[i] = lat[i] + F.interpolate(lat[i + 1], scale_factor=2, mode="nearest")
+        # top-down: lateral_i(C_i) + up2(merged_{i+1}); the join is the lateral conv's
+        # residual, read nearest-upsampled by its epilogue (no upsampled tensor, no add pass)
+        L = len(feats)
+        lat = [None] * L
+        m = self.lateral[L - 1]
+        lat[L - 1] = conv_bias_act(feats[L - 1], cw(m.weight, dt), cw(m.bias, dt))
+        for i in range(L - 2, -1, -1):
+            m = self.lateral[i]
+            lat[i] = conv_bias_act(feats[i], cw(m.weight, dt), cw(m.bias, dt), residual=lat[i + 1], res_up=True)
         outs = [conv_bias_act(x, cw(m.weight, dt), cw(m.bias, dt), padding=1) for x, m in zip(lat, self.output)]
         outs.append(F.max_pool2d(outs[-1], 1, 2))   # P6
         return outs

@@ -133,9 +133,11 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride, padding, dila
 DGRAD_MIN_TILES = 64
 
 
-def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, padding=0, dilation=1) -> bool:
+def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, padding=0, dilation=1,
+                  res_up: bool = False) -> bool:
     """The implicit-GEMM forward: NHWC bf16, Cout a multiple of 128, Cin of 64, and at least
-    FWD_MIN_TILES 128 x 128 output tiles (smaller convs stay on MIOpen)."""
+    FWD_MIN_TILES 128 x 128 output tiles (smaller convs stay on MIOpen).  ``res_up``: the
+    residual is at half the output resolution, added nearest-upsampled."""
     if not (FWD and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
             and w.dim() == 4 and w.shape[0] % 128 == 0 and w.shape[1] % 64 == 0 and x.shape[1] == w.shape[1]
             and _cl(x) and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
@@ -148,16 +150,20 @@ def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, paddi
     N, _, IH, IW = x.shape
     OH = (IH + 2 * pd - dl * (w.shape[2] - 1) - 1) // st + 1
     OW = (IW + 2 * pd - dl * (w.shape[3] - 1) - 1) // st + 1
+    rshape = (N, w.shape[0], OH // 2, OW // 2) if res_up else (N, w.shape[0], OH, OW)
+    if res_up and (residual is None or OH % 2 or OW % 2):
+        return False
     if residual is not None and not (residual.dtype == torch.bfloat16 and _cl(residual)
-                                     and tuple(residual.shape) == (N, w.shape[0], OH, OW)
+                                     and tuple(residual.shape) == rshape
                                      and residual.data_ptr() % 16 == 0):   # 16-B residual loads
         return False
     return (N * OH * OW + 127) // 128 * (w.shape[0] // 128) >= FWD_MIN_TILES
 
 
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool = False, stride=1, padding=0,
-             dilation=1) -> torch.Tensor:
-    """act(conv2d(x, w) + b (+ residual)), NHWC bf16 in and out, one launch."""
+             dilation=1, res_up: bool = False) -> torch.Tensor:
+    """act(conv2d(x, w) + b (+ residual, nearest-upsampled 2x with ``res_up``)), NHWC bf16 in
+    and out, one launch."""
     Cout, Cin, KH, KW = w.shape
     N, _, IH, IW = x.shape
     st, pd, dl = _sym(stride), _sym(padding), _sym(dilation)
@@ -168,8 +174,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool
     y = torch.empty((N, OH, OW, Cout), dtype=torch.bfloat16, device=x.device).permute(0, 3, 1, 2)
     _, zero = _workspace(x.device, 1)
     d = _DESC_T()
-    d[:21] = [x.data_ptr(), w.data_ptr(), zero.data_ptr(), y.data_ptr(), _lib.ptr(b) or 0,
-              _lib.ptr(residual) or 0, Cin, Cout, N, OH, OW, IH, IW, KH, KW, st, pd, dl, Cout, Cin, int(relu)]
+    d[:22] = [x.data_ptr(), w.data_ptr(), zero.data_ptr(), y.data_ptr(), _lib.ptr(b) or 0,
+              _lib.ptr(residual) or 0, Cin, Cout, N, OH, OW, IH, IW, KH, KW, st, pd, dl, Cout, Cin, int(relu),
+              int(res_up)]
     _lib.call("mx_conv_fwd", d, _lib.stream())
     return y
 

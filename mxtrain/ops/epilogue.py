@@ -111,10 +111,10 @@ class ConvBiasActFn(torch.autograd.Function):
     "take_res" adds it (see BlockLink)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, res, relu: bool, stride, padding, dilation, fuse=None):
-        y = convwg.conv_fwd(x, w, b, res, relu, stride, padding, dilation)
+    def forward(ctx, x, w, b, res, relu: bool, stride, padding, dilation, fuse=None, res_up=False):
+        y = convwg.conv_fwd(x, w, b, res, relu, stride, padding, dilation, res_up=res_up)
         ctx.conf = (list(convwg._pair(stride)), list(convwg._pair(padding)), list(convwg._pair(dilation)))
-        ctx.relu, ctx.has_res = relu, res is not None
+        ctx.relu, ctx.has_res, ctx.res_up = relu, res is not None, res_up
         ctx.bdtype = b.dtype if b is not None else None
         ctx.fuse = fuse
         ctx.save_for_backward(x, w, y if relu else None)
@@ -131,6 +131,8 @@ class ConvBiasActFn(torch.autograd.Function):
         if db is not None and db.dtype != ctx.bdtype:
             db = db.to(ctx.bdtype)
         dres = dy if ctx.has_res else None
+        if dres is not None and ctx.res_up:
+            dres = down2_sum(dres)
         if dres is not None and "stash_res" in roles and link.taker and ctx.needs_input_grad[3]:
             link.stash.append(dres)
             dres = None
@@ -155,7 +157,14 @@ class ConvBiasActFn(torch.autograd.Function):
             else:
                 dw = torch.ops.aten.convolution_backward(dy, x, w, None, st, pd, dl, False, [0, 0], 1,
                                                          [False, True, False])[1]
-        return dx, dw, db, dres, None, None, None, None, None
+        return dx, dw, db, dres, None, None, None, None, None, None
+
+
+def down2_sum(g: torch.Tensor) -> torch.Tensor:
+    """Gradient of the 2x nearest upsampling: each 2 x 2 block summed (NHWC memory kept)."""
+    N, C, H, W = g.shape
+    t = g.permute(0, 2, 3, 1).reshape(N, H // 2, 2, W // 2, 2, C).sum((2, 4), dtype=torch.float32)
+    return t.to(g.dtype).permute(0, 3, 1, 2)
 
 
 def _fused_ok(y, b, residual) -> bool:
@@ -195,22 +204,28 @@ def fused_conv_ok(x, w, b=None, residual=None, stride=1, padding=0, dilation=1) 
 
 
 def conv_bias_act(x, w, b=None, stride=1, padding=0, dilation=1, relu: bool = False,
-                  residual: Optional[torch.Tensor] = None, fuse=None) -> torch.Tensor:
+                  residual: Optional[torch.Tensor] = None, fuse=None, res_up: bool = False) -> torch.Tensor:
     """act(conv2d(x, w) + b (+ residual)) -- one conv (MIOpen forward and input gradient;
     the weight gradient from csrc/convwg.hip where it tiles) + one fused epilogue pass.
     ``fuse``: (BlockLink, index, roles) -- only honoured on the ConvBiasActFn path (the
-    caller checks fused_conv_ok before promising a role to a neighbour)."""
+    caller checks fused_conv_ok before promising a role to a neighbour).  ``res_up``: the
+    residual is at half resolution and joins nearest-upsampled (FPN top-down pathway); the
+    implicit-GEMM forward reads it in place, elsewhere it is upsampled first."""
     if _conv_in_ok(x, w, b, residual):
+        if res_up and convwg.fwd_supported(x, w, b, residual, stride, padding, dilation, res_up=True):
+            return ConvBiasActFn.apply(x, w, b, residual, relu, stride, padding, dilation, fuse, True)
+        if res_up:
+            residual, res_up = F.interpolate(residual, scale_factor=2, mode="nearest"), False
         if convwg.fwd_supported(x, w, b, residual, stride, padding, dilation):
             # forward, input and weight gradients all implicit GEMMs (ops/convwg.py)
-            return ConvBiasActFn.apply(x, w, b, residual, relu, stride, padding, dilation, fuse)
+            return ConvBiasActFn.apply(x, w, b, residual, relu, stride, padding, dilation, fuse, False)
         if convwg.supported(x, w, stride, padding, dilation):
             # MIOpen forward / input gradient, implicit-GEMM weight gradient (ops/convwg.py)
             return bias_act(convwg.conv2d_wg(x, w, stride, padding, dilation), b, residual, relu)
         return bias_act(F.conv2d(x, w, None, stride, padding, dilation), b, residual, relu)
     y = F.conv2d(x, w, b, stride, padding, dilation)
     if residual is not None:
-        y = y + residual
+        y = y + (F.interpolate(residual, scale_factor=2, mode="nearest") if res_up else residual)
     return F.relu(y, inplace=True) if relu else y
 
 

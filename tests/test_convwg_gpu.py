@@ -237,3 +237,32 @@ def test_bottleneck_backward_fusion_matches_unfused(monkeypatch):
     assert len(out[True][2]) == len(out[False][2]) == 10
     for a, b in zip(out[True][2], out[False][2]):
         _close(a, b.cpu())
+
+
+@pytest.mark.parametrize("cin", [256, 512])
+def test_conv_bias_act_upsampled_residual_matches_fp32(cin):
+    """FPN top-down join in the conv epilogue (ops/epilogue.py conv_bias_act res_up):
+    conv1x1(x) + b + up2(r) against fp32 F.conv2d + F.interpolate, values and the input,
+    weight, bias and residual gradients (the residual's = 2 x 2 block sums)."""
+    import torch.nn.functional as F
+    from mxtrain.ops import convwg
+    from mxtrain.ops.epilogue import conv_bias_act
+    g = torch.Generator().manual_seed(cin)
+    cl = torch.channels_last
+    x = torch.randn(2, cin, 50, 84, generator=g).to(torch.bfloat16)
+    w = (torch.randn(256, cin, 1, 1, generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(256, generator=g).to(torch.bfloat16)
+    r = torch.randn(2, 256, 25, 42, generator=g).to(torch.bfloat16)
+    gy = torch.randn(2, 256, 50, 84, generator=g)
+    assert convwg.fwd_supported(x.cuda().contiguous(memory_format=cl), w.cuda().contiguous(memory_format=cl),
+                                b.cuda(), r.cuda().contiguous(memory_format=cl), res_up=True)
+    xs = [t.cuda().contiguous(memory_format=cl).requires_grad_() if t.dim() == 4 else t.cuda().requires_grad_()
+          for t in (x, w, b, r)]
+    y = conv_bias_act(xs[0], xs[1], xs[2], residual=xs[3], res_up=True)
+    y.backward(gy.to(torch.bfloat16).cuda().contiguous(memory_format=cl))
+    rs = [t.float().requires_grad_() for t in (x, w, b, r)]
+    yr = F.conv2d(rs[0], rs[1], rs[2]) + F.interpolate(rs[3], scale_factor=2, mode="nearest")
+    yr.backward(gy.to(torch.bfloat16).float())
+    _close(y, yr.detach())
+    for a, ref in zip(xs, rs):
+        _close(a.grad, ref.grad)
