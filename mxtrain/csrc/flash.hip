@@ -498,21 +498,19 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
     return row[(size_t)((tile_of(t) * BK) >> 7) * 64];
   };
 
-  auto compute = [&](const char* Kt, const char* Vt, int j) __attribute__((always_inline)) {
-    const int kv0 = j * BK;
-    int nsub = NSUB;
-    // (qw, kv0 are 32-aligned: subtiles up to and including the diagonal one)
-    if (CAUSAL) nsub = qw >= kv0 ? min(NSUB, (qw - kv0) / 32 + 1) : 0;
-    nsub = uni(row_ok ? nsub : 0);
-    if (nsub == 0) return;
-    // the subtile on the causal diagonal (qw is 32-aligned) and the padded-key tail
-    const int tdiag = CAUSAL ? uni((qw - kv0) >> 5) : -1;
-    const bool tail = uni(kv0 + BK > kl ? 1 : 0);
+  // FULL: every key of the tile is visible to every row of the wave (below the causal
+  // diagonal, no padded tail): the tile body is straight-line code with no per-subtile
+  // guards or masks, so the compiler can hoist the LDS reads ahead of their MFMAs and
+  // interleave one subtile's softmax VALU with the neighbouring subtile's MFMAs (the
+  // guarded form compiles to one basic block per subtile: read -> wait -> MFMA in series).
+  auto compute_body = [&](const char* Kt, const char* Vt, int kv0, int nsub, int tdiag, bool tail,
+                          auto fullc) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(fullc)::value;
     if constexpr (!DQ) {
       f32x16 sacc[NSUB];
 #pragma unroll
       for (int t = 0; t < NSUB; ++t) {
-        if (t < nsub) {
+        if (FULL || t < nsub) {
           bf16x8 kr[NKK];
 #pragma unroll
           for (int kk = 0; kk < NKK; ++kk) kr[kk] = lds8(Kt + 32 * t * RB, offK[kk]);
@@ -524,12 +522,12 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
 #pragma unroll
       for (int t = 0; t < NSUB; ++t) {
         // (a wave-uniform branch: only the diagonal subtile pays the per-element select)
-        if (CAUSAL && uni(t == tdiag ? 1 : 0)) {
+        if (!FULL && CAUSAL && uni(t == tdiag ? 1 : 0)) {
           asm volatile("" ::: "memory");   // a real branch, not per-element selects
 #pragma unroll
           for (int e = 0; e < 16; ++e) sacc[t][e] = crow(e, 0) > rr ? -INFINITY : sacc[t][e];
         }
-        if (!CAUSAL && tail && t < nsub) {
+        if (!FULL && !CAUSAL && tail && t < nsub) {
           const int lim = kl - kv0 - 32 * t - 4 * hh;
 #pragma unroll
           for (int e = 0; e < 16; ++e) sacc[t][e] = crow(e, 0) >= lim ? -INFINITY : sacc[t][e];
@@ -538,7 +536,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
       float mx = -INFINITY;
 #pragma unroll
       for (int t = 0; t < NSUB; ++t)
-        if (t < nsub) {
+        if (FULL || t < nsub) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sacc[t][e]);
         }
@@ -558,7 +556,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
       float rs = 0.f;
 #pragma unroll
       for (int t = 0; t < NSUB; ++t)
-        if (t < nsub) {
+        if (FULL || t < nsub) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[t][e], c, -mc));
@@ -569,7 +567,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
       l_i += rs;
 #pragma unroll
       for (int t = 0; t < NSUB; ++t)
-        if (t < nsub) {
+        if (FULL || t < nsub) {
           const uint32_t wd = (uint32_t)(dm_cur >> (32 * ((((kv0 >> 5) + t) >> 1) & 1)));
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
@@ -586,7 +584,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
     } else {
 #pragma unroll
       for (int t = 0; t < NSUB; ++t) {
-        if (t < nsub) {
+        if (FULL || t < nsub) {
           bf16x8 kr[NKK], vr[NKK];
 #pragma unroll
           for (int kk = 0; kk < NKK; ++kk) {
@@ -605,7 +603,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
 #pragma unroll
           for (int e = 0; e < 16; ++e) pv[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(s_[e], c, -lse2));
           // (only the diagonal / padded-tail subtile is masked: a wave-uniform branch)
-          if (uni((CAUSAL && t == tdiag) || (!CAUSAL && tail) ? 1 : 0)) {
+          if (!FULL && uni((CAUSAL && t == tdiag) || (!CAUSAL && tail) ? 1 : 0)) {
             asm volatile("" ::: "memory");   // a real branch, not per-element selects
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
@@ -635,6 +633,23 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
         }
       }
     }
+  };
+  auto compute = [&](const char* Kt, const char* Vt, int j) __attribute__((always_inline)) {
+    const int kv0 = j * BK;
+    int nsub = NSUB;
+    // (qw, kv0 are 32-aligned: subtiles up to and including the diagonal one)
+    if (CAUSAL) nsub = qw >= kv0 ? min(NSUB, (qw - kv0) / 32 + 1) : 0;
+    nsub = uni(row_ok ? nsub : 0);
+    if (nsub == 0) return;
+    // the subtile on the causal diagonal (qw is 32-aligned) and the padded-key tail
+    const int tdiag = CAUSAL ? uni((qw - kv0) >> 5) : -1;
+    const bool tail = uni(kv0 + BK > kl ? 1 : 0);
+    // forward only: the FULL dQ body measured slower at D = 64 (38.3 vs 36.0 us per GPT-2
+    // layer; profiles/r4_s2/) and spills at D = 128, so dQ keeps the guarded form
+    if (!DQ && uni((!CAUSAL || kv0 + BK <= qw) && !tail ? 1 : 0))
+      compute_body(Kt, Vt, kv0, NSUB, tdiag, false, std::integral_constant<bool, !DQ>{});
+    else
+      compute_body(Kt, Vt, kv0, nsub, tdiag, tail, std::false_type{});
   };
 
   // one step: wait for this step's tile, hand the other slot to the next step's DMA, compute
@@ -915,15 +930,18 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
   };
   uint32_t dm_cur = 0, dm_next = 0;
 
-  auto compute = [&](const char* Qt, const char* Ot, const float* Lt, const float* Dt, int t) __attribute__((always_inline)) {
-    int hq, qs;
-    decode(t, hq, qs);
-    (void)hq;
+  // FULL: every query subtile of the step active, none on the causal diagonal, no query
+  // tail -- straight-line code (see qmajor's compute_body)
+  auto compute_body = [&](const char* Qt, const char* Ot, const float* Lt, const float* Dt, int qs,
+                          auto fullc) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
     for (int u = 0; u < NQS; ++u) {
       const int qsu = qs + 32 * u;
-      const bool act = uni(wave_on && qsu < S && (!CAUSAL || qsu + 31 >= kw0) ? 1 : 0);
-      if (!act) continue;
+      if constexpr (!FULL) {
+        const bool act = uni(wave_on && qsu < S && (!CAUSAL || qsu + 31 >= kw0) ? 1 : 0);
+        if (!act) continue;
+      }
       f32x16 sacc = f32x16{}, dpacc = f32x16{};
       const char* Qu = Qt + 32 * u * RB;
       const char* Ou = Ot + 32 * u * RB;
@@ -935,8 +953,8 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
         sacc = mfma32(qa, kb_, sacc);
         dpacc = mfma32(oa, vf[kk], dpacc);
       }
-      const bool diag = CAUSAL && qsu == kw0;
-      const bool qtail = qsu + 32 > S;
+      const bool diag = !FULL && CAUSAL && qsu == kw0;
+      const bool qtail = !FULL && qsu + 32 > S;
       // P of the subtile, unmasked; the causal diagonal subtile (wave-uniform branch) and, in
       // RAGGED launches only, the query tail / invalid keys are zeroed afterwards
       float pv[16];
@@ -948,7 +966,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
         const float lse_e = (e & 3) == 0 ? lsq.x : (e & 3) == 1 ? lsq.y : (e & 3) == 2 ? lsq.z : lsq.w;
         pv[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[e], c, -lse_e));
       }
-      if (uni(diag ? 1 : 0)) {
+      if (!FULL && uni(diag ? 1 : 0)) {
         asm volatile("" ::: "memory");   // keeps this a real (scalar) branch: not if-converted into selects
 #pragma unroll
         for (int e = 0; e < 16; ++e) pv[e] = rr > crow(e, 0) ? 0.f : pv[e];
@@ -992,6 +1010,14 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
         }
       }
     }
+  };
+  auto compute = [&](const char* Qt, const char* Ot, const float* Lt, const float* Dt, int t) __attribute__((always_inline)) {
+    int hq, qs;
+    decode(t, hq, qs);
+    (void)hq;
+    // (the straight-line FULL body spills at D = 64 -- dK/dV accumulators plus hoisted
+    // operands exceed the two-waves-per-SIMD register budget -- so it is not instantiated)
+    compute_body(Qt, Ot, Lt, Dt, qs, std::false_type{});
   };
 
   auto step = [&](char* Qc, char* Oc, float* Lc, float* Dc, char* Qn, char* On, float* Ln, float* Dn,

@@ -29,7 +29,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.epilogue import conv_bias_act, conv_transpose_bias_act
+from ..ops.epilogue import BlockLink, conv_bias_act, conv_transpose_bias_act, fused_conv_ok
 from ..ops import detloss as D
 from ..ops import vision as V
 from .compute_weights import ComputeWeights, cw
@@ -287,8 +287,16 @@ class MaskHead(nn.Module):
     def forward(self, x):            # x: [R, 14, 14, C] NHWC -> [R, ncls, 28, 28]
         dt = x.dtype
         x = x.permute(0, 3, 1, 2)    # NCHW view of NHWC memory (channels_last)
-        for m in self.convs:
-            x = conv_bias_act(x, cw(m.weight, dt), cw(m.bias, dt), padding=1, relu=True)
+        # backward fusion along the conv chain (ops/epilogue.py BlockLink): conv i+1's dgrad
+        # store applies conv i's ReLU, so conv i skips its mask pass
+        link = BlockLink()
+        for i, m in enumerate(self.convs):
+            w, b = cw(m.weight, dt), cw(m.bias, dt)
+            roles = ()
+            if i > 0 and fused_conv_ok(x, w, b, None, 1, 1, 1):
+                link.premask[i] = True
+                roles = ("mask_in",)
+            x = conv_bias_act(x, w, b, padding=1, relu=True, fuse=(link, i + 1, roles))
         x = conv_transpose_bias_act(x, cw(self.deconv.weight, dt), cw(self.deconv.bias, dt), stride=2, relu=True)
         return conv_bias_act(x, cw(self.pred.weight, dt), cw(self.pred.bias, dt))
 

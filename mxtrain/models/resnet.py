@@ -93,6 +93,8 @@ class ConvNorm(nn.Module):
                         link.premask[k - 1] = True     # conv k-1 leaves its ReLU mask to this dgrad
                     if "take_res" in roles:
                         link.taker = True
+                    if "mask_prev" in roles:
+                        link.prev.premask[3] = True    # the previous block's conv3 likewise
                 else:
                     fuse = None
             # one MIOpen conv + one fused bias (+ residual) (+ ReLU) pass (ops/epilogue.py)
@@ -159,17 +161,28 @@ class Bottleneck(nn.Module):
 
     # backward fusion inside the block (ops/epilogue.py BlockLink): the dgrads of conv2 /
     # conv3 apply conv1's / conv2's ReLU in their stores, and an identity block's residual
-    # gradient is added in conv1's dgrad store instead of by autograd (FrozenBN path)
+    # gradient is added in conv1's dgrad store instead of by autograd (FrozenBN path).
+    # Across blocks: an identity block's input is the previous block's ReLU output and its
+    # conv1 dgrad store already holds that input's whole gradient (dgrad + residual), so it
+    # applies the previous block's ReLU too ("mask_prev") and the previous conv3 skips its
+    # mask pass.  The link travels on the output tensor (``_mx_link``).
     fuse_backward = True
 
     def forward(self, x):
         link = BlockLink() if self.fuse_backward and self.conv1.norm_kind == "frozen" else None
         ident = self.shortcut is None
-        a1 = self.conv1(x, fuse=(link, 1, ("take_res",) if ident else ()) if link else None)
+        prev = getattr(x, "_mx_link", None) if (link is not None and ident) else None
+        r1 = ("take_res", "mask_prev") if prev is not None else (("take_res",) if ident else ())
+        if prev is not None:
+            link.prev = prev
+        a1 = self.conv1(x, fuse=(link, 1, r1) if link else None)
         a2 = self.conv2(a1, fuse=(link, 2, ("mask_in",)) if link else None)
         idt = x if ident else self.shortcut(x)
-        return self.conv3(a2, residual=idt, relu=True,
-                          fuse=(link, 3, ("mask_in", "stash_res") if ident else ("mask_in",)) if link else None)
+        out = self.conv3(a2, residual=idt, relu=True,
+                         fuse=(link, 3, ("mask_in", "stash_res") if ident else ("mask_in",)) if link else None)
+        if link is not None:
+            out._mx_link = link
+        return out
 
 
 class ResNet(nn.Module):

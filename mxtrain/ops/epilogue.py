@@ -92,14 +92,19 @@ class BlockLink:
     * ``stash``: identity residual: conv3's backward puts the residual branch's gradient
       here instead of returning it, and conv1's backward adds it in its dgrad store (conv1
       always runs after conv3 in backward: data dependency), so autograd's separate add
-      of the block input's two gradients disappears."""
+      of the block input's two gradients disappears;
+    * role "mask_prev" (conv1 of an identity block whose input is the previous block's
+      ReLU output): its dgrad store, which then holds the input's whole gradient, also
+      applies that ReLU (``prev.premask[3]``).  Masking is idempotent, so a consumer that
+      masks a gradient its producer masks too is only wasted work, never wrong."""
 
-    __slots__ = ("premask", "stash", "taker")
+    __slots__ = ("premask", "stash", "taker", "prev")
 
     def __init__(self):
         self.premask = {}
         self.stash = []
         self.taker = False    # conv1 runs ConvBiasActFn with role "take_res" (set in its forward)
+        self.prev = None      # the previous block's link when conv1 has role "mask_prev"
 
 
 class ConvBiasActFn(torch.autograd.Function):
@@ -137,7 +142,7 @@ class ConvBiasActFn(torch.autograd.Function):
             link.stash.append(dres)
             dres = None
         add = link.stash.pop() if "take_res" in roles and link.stash else None
-        mask = x if "mask_in" in roles else None
+        mask = x if ("mask_in" in roles or "mask_prev" in roles) else None
         dx = dw = None
         if ctx.needs_input_grad[0]:
             if convwg.dgrad_supported(w, tuple(x.shape), st) and (add is None or add.data_ptr() % 16 == 0):

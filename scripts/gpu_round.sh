@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun session, parameterised (the one wrapper every GPU call goes through):
 #   STEPS="tests smoke bench"  (also: slice mrcnn mrprof kbench prof pmc)
-#   PYTEST_ARGS / BENCH_ARGS / MRCNN_ARGS / KBENCH_ARGS / PROF_ARGS / SLICE_ARGS
+#   PYTEST_K (a -k expression, may contain spaces) / PYTEST_ARGS / BENCH_ARGS / MRCNN_ARGS / KBENCH_ARGS / PROF_ARGS / SLICE_ARGS
 #   pmc: PMC_CMD (python script + args, run directly after rocprofv3's --), PMC_REGEX
 #        (kernel-name filter), one rocprofv3 pass per counter group (SQ <= 8 per pass)
 # Each GPU step has its own time limit; after a crash/timeout (exit >= 124 or signal)
@@ -15,7 +15,7 @@ STEPS="${STEPS:-tests smoke bench}"
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 ${T_TESTS:-900} python -u -m pytest ${PYTEST_TARGET:-tests} -m gpu ${PYTEST_X--x} -q --timeout ${T_TEST:-300} --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1; rc=$?
+      timeout -k 10 ${T_TESTS:-900} python -u -m pytest ${PYTEST_TARGET:-tests} -m gpu ${PYTEST_X--x} -q --timeout ${T_TEST:-300} --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1; rc=$?
       tail -30 gpurun_out/gpu_tests.log; echo "tests rc=$rc"; ok $rc || exit $rc ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?

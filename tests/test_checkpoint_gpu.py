@@ -41,7 +41,7 @@ def test_async_save_then_step_matches_sync_save(tmp_path):
     from mxtrain.parallel.state import ParallelState
     from mxtrain.training import GPTTrainer, TrainConfig, synthetic_batch
     dev = torch.device("cuda", 0)
-    cfg = GPTConfig(num_layers=2, hidden_size=128, num_attention_heads=4, seq_length=128,
+    cfg = GPTConfig(num_layers=2, hidden_size=128, num_attention_heads=2, seq_length=128,
                     max_position_embeddings=128, vocab_size=512, hidden_dropout=0.1, attention_dropout=0.1)
     tr = GPTTrainer(cfg, TrainConfig(micro_batch_size=2), ParallelState(device=dev))
     tok, lab = synthetic_batch(cfg, 1, 2, dev, torch.Generator().manual_seed(0))

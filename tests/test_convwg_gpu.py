@@ -230,8 +230,9 @@ def test_bottleneck_backward_fusion_matches_unfused(monkeypatch):
         torch.cuda.synchronize()
         out[fuse] = (y.detach().float(), x.grad.float(),
                      [p.grad.float() for p in blocks.parameters() if p.grad is not None])
-    # fused: conv2 + conv3 of all three blocks mask their input, conv1 of the two identity blocks adds
-    assert seen == {"add": 2, "mask": 6}, seen
+    # fused: conv2 + conv3 of all three blocks mask their input, conv1 of the two identity
+    # blocks adds, and the second block's conv1 also masks (the first block's ReLU)
+    assert seen == {"add": 2, "mask": 7}, seen
     assert torch.equal(out[False][0], out[True][0])
     _close(out[True][1], out[False][1].cpu())
     assert len(out[True][2]) == len(out[False][2]) == 10
@@ -266,3 +267,32 @@ def test_conv_bias_act_upsampled_residual_matches_fp32(cin):
     _close(y, yr.detach())
     for a, ref in zip(xs, rs):
         _close(a.grad, ref.grad)
+
+
+def test_mask_head_conv_chain_fusion_matches_fp32():
+    """models/maskrcnn.py MaskHead: conv i+1's dgrad store applies conv i's ReLU (BlockLink
+    chain); input and parameter gradients against the fp32 CPU head with the same weights."""
+    from mxtrain.models.maskrcnn import MaskHead
+    torch.manual_seed(5)
+    ref = MaskHead(256, 256, 80)
+    for m in ref.convs:
+        torch.nn.init.normal_(m.bias, std=0.1)
+    head = MaskHead(256, 256, 80)
+    head.load_state_dict(ref.state_dict())
+    head = head.cuda()
+    x0 = torch.randn(96, 14, 14, 256)
+    gy = torch.randn(96, 80, 28, 28)
+    x = x0.to(torch.bfloat16).cuda().requires_grad_()
+    y = head(x)
+    y.backward(gy.to(torch.bfloat16).cuda().contiguous(memory_format=torch.channels_last))
+    xr = x0.to(torch.bfloat16).float().requires_grad_()
+    yr = ref(xr)
+    yr.backward(gy.to(torch.bfloat16).float())
+    def close(a, b, what):   # five bf16 convs deep: 3 % of the reference's max magnitude
+        err = (a.float().cpu() - b).abs().max().item()
+        assert err <= 3e-2 * b.abs().max().item() + 1e-3, (what, err, b.abs().max().item())
+
+    close(y, yr.detach(), "y")
+    close(x.grad, xr.grad, "dx")
+    for (n, a), (_, b) in zip(head.named_parameters(), ref.named_parameters()):
+        close(a.grad, b.grad, n)
