@@ -284,19 +284,21 @@ class MaskHead(nn.Module):
         nn.init.normal_(self.pred.weight, std=0.001)
         nn.init.zeros_(self.pred.bias)
 
+    fuse_backward = True
+
     def forward(self, x):            # x: [R, 14, 14, C] NHWC -> [R, ncls, 28, 28]
         dt = x.dtype
         x = x.permute(0, 3, 1, 2)    # NCHW view of NHWC memory (channels_last)
         # backward fusion along the conv chain (ops/epilogue.py BlockLink): conv i+1's dgrad
         # store applies conv i's ReLU, so conv i skips its mask pass
-        link = BlockLink()
+        link = BlockLink() if self.fuse_backward else None
         for i, m in enumerate(self.convs):
             w, b = cw(m.weight, dt), cw(m.bias, dt)
             roles = ()
-            if i > 0 and fused_conv_ok(x, w, b, None, 1, 1, 1):
+            if link is not None and i > 0 and fused_conv_ok(x, w, b, None, 1, 1, 1):
                 link.premask[i] = True
                 roles = ("mask_in",)
-            x = conv_bias_act(x, w, b, padding=1, relu=True, fuse=(link, i + 1, roles))
+            x = conv_bias_act(x, w, b, padding=1, relu=True, fuse=(link, i + 1, roles) if link else None)
         x = conv_transpose_bias_act(x, cw(self.deconv.weight, dt), cw(self.deconv.bias, dt), stride=2, relu=True)
         return conv_bias_act(x, cw(self.pred.weight, dt), cw(self.pred.bias, dt))
 

@@ -269,30 +269,32 @@ def test_conv_bias_act_upsampled_residual_matches_fp32(cin):
         _close(a.grad, ref.grad)
 
 
-def test_mask_head_conv_chain_fusion_matches_fp32():
+def test_mask_head_conv_chain_fusion_matches_unfused():
     """models/maskrcnn.py MaskHead: conv i+1's dgrad store applies conv i's ReLU (BlockLink
-    chain); input and parameter gradients against the fp32 CPU head with the same weights."""
+    chain) -- identical forward, input and parameter gradients equal to the unfused head's
+    to bf16 rounding (same bf16 path; an fp32 reference differs wherever a pre-activation
+    near zero flips its ReLU mask under bf16, which max-error checks cannot tell from a bug)."""
     from mxtrain.models.maskrcnn import MaskHead
     torch.manual_seed(5)
-    ref = MaskHead(256, 256, 80)
-    for m in ref.convs:
-        torch.nn.init.normal_(m.bias, std=0.1)
     head = MaskHead(256, 256, 80)
-    head.load_state_dict(ref.state_dict())
+    for m in head.convs:
+        torch.nn.init.normal_(m.bias, std=0.1)
     head = head.cuda()
-    x0 = torch.randn(96, 14, 14, 256)
-    gy = torch.randn(96, 80, 28, 28)
-    x = x0.to(torch.bfloat16).cuda().requires_grad_()
-    y = head(x)
-    y.backward(gy.to(torch.bfloat16).cuda().contiguous(memory_format=torch.channels_last))
-    xr = x0.to(torch.bfloat16).float().requires_grad_()
-    yr = ref(xr)
-    yr.backward(gy.to(torch.bfloat16).float())
-    def close(a, b, what):   # five bf16 convs deep: 3 % of the reference's max magnitude
-        err = (a.float().cpu() - b).abs().max().item()
-        assert err <= 3e-2 * b.abs().max().item() + 1e-3, (what, err, b.abs().max().item())
-
-    close(y, yr.detach(), "y")
-    close(x.grad, xr.grad, "dx")
-    for (n, a), (_, b) in zip(head.named_parameters(), ref.named_parameters()):
-        close(a.grad, b.grad, n)
+    x0 = torch.randn(96, 14, 14, 256).to(torch.bfloat16).cuda()
+    gy = torch.randn(96, 80, 28, 28).to(torch.bfloat16).cuda().contiguous(memory_format=torch.channels_last)
+    out = {}
+    try:
+        for fuse in (False, True):
+            MaskHead.fuse_backward = fuse
+            head.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_()
+            y = head(x)
+            y.backward(gy)
+            torch.cuda.synchronize()
+            out[fuse] = (y.detach().float(), x.grad.float(), [p.grad.float() for p in head.parameters()])
+    finally:
+        MaskHead.fuse_backward = True
+    assert torch.equal(out[False][0], out[True][0])
+    _close(out[True][1], out[False][1].cpu())
+    for a, b in zip(out[True][2], out[False][2]):
+        _close(a, b.cpu())
