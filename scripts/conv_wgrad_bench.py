@@ -6,6 +6,7 @@ import torch
 from mxtrain.ops import convwg
 
 N = int(os.environ.get("IMGS", "1"))
+WGRAD_ONLY = os.environ.get("WGRAD_ONLY", "0") == "1"   # split sweeps: skip the dgrad / fwd columns
 # name, Cin, Cout, H_in, W_in, k, stride, pad, count per step
 SHAPES = [
     ("res3.conv1 s2", 256, 128, 200, 336, 1, 2, 0, 1),
@@ -80,6 +81,12 @@ for name, Cin, Cout, H, W, k, s, p, cnt in SHAPES:
     fl = 2.0 * n * OH * OW * Cout * Cin * k * k
     T = n * OH * OW
     ntiles = k * k * (Cout // 128) * (Cin // 128)
+    if WGRAD_ONLY:
+        print(f"{name:22s} {n:3d} {tm:10.1f} {th:10.1f} {fl / tm / 1e6:8.1f} {fl / th / 1e6:8.1f}  "
+              f"{convwg.plan_splits(T, ntiles):6d}  {rel:.2e}  x{cnt}", flush=True)
+        tot_m += cnt * tm
+        tot_h += cnt * th
+        continue
     dmi = lambda: torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                       [True, False, False])
     dwg = lambda: convwg.conv_dgrad(dy, w, tuple(x.shape), s, p, 1)
