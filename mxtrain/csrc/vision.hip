@@ -13,6 +13,7 @@
 //    (wave64 = one word per lane); the sequential keep pass runs in one wave per problem
 //    with the removed-bitmask distributed one word per lane.
 #include "common.h"
+#include "gemm_common.h"
 
 namespace {
 
@@ -437,7 +438,7 @@ __device__ __forceinline__ void write_tile_bf16(const float* acc, uint16_t* g, i
 
 // split tiles (kChunk < n <= kSortBig): sort the whole entry list once, so the chunks'
 // membership and order -- and so the result -- are deterministic
-constexpr int kSortBig = 4096;
+constexpr int kSortBig = 16384;   // 64 KB of keys in LDS
 __global__ __launch_bounds__(1024) void tile_sort_kernel(const int* __restrict__ offsets, int T,
                                                          int* __restrict__ entries) {
   __shared__ int keys[kSortBig];
@@ -599,6 +600,188 @@ __global__ __launch_bounds__(256) void roi_align_bwd_tile_kernel(Levels L, TileG
   float* dst = partial + (size_t)slot * kTile * kTile * C;
   for (int i = tid * 4; i < kTile * kTile * C; i += nt * 4)
     *reinterpret_cast<float4*>(dst + i) = *reinterpret_cast<const float4*>(acc + i);
+}
+
+// C = 256: the same chunk as roi_align_bwd_tile_kernel, accumulated on the matrix cores.
+// A chunk's contribution to its tile is a GEMM, out[px][c] = sum_e W[e][px] dY[e][c], with W
+// the entries' bilinear footprints (<= 16 nonzeros of 64 per entry) and dY their gradient
+// rows; per 32-entry K-step the rows are staged in LDS ([e][256 c], 16-B chunks swizzled by
+// gemm_common.h's pchunk: the transposed reads of the A fragments are conflict-free) and W
+// is scattered into an [px][e] image as bf16 hi + lo halves (w = hi + lo to ~2^-16, so the
+// weights keep fp32-level precision; dY is bf16 already), two 16x16x32 MFMAs per product.
+// The per-entry LDS read-modify-write loop of the scalar kernel (16 round trips per entry
+// and channel) measured ~1.2 us per entry on the concentrated RoIs of a random-init RPN
+// (scripts/roi_bwd_bench.py); here an entry costs 1/32 of a K-step.  Accumulation order is
+// fixed (sorted entries, K-steps in order): deterministic like the scalar kernel.
+constexpr int kMKS = 32;   // entries per K-step (the 16x16x32 MFMA depth)
+__global__ __launch_bounds__(256, 2) void roi_align_bwd_mfma_kernel(Levels L, TileGeo G, int T,
+                                                                    const uint16_t* __restrict__ dout,
+                                                                    const FootP* __restrict__ fp,
+                                                                    const int* __restrict__ offsets,
+                                                                    const int* __restrict__ coff,
+                                                                    const int* __restrict__ poff,
+                                                                    const int* __restrict__ ctile,
+                                                                    const int* __restrict__ entries, GOut gout,
+                                                                    float* __restrict__ partial, int pslots,
+                                                                    int* __restrict__ overflow,
+                                                                    long long* __restrict__ dbg) {
+  constexpr int C = 256, RB = C * 2;               // dY image row bytes
+  constexpr int DIMG = kMKS * RB;                  // 16 KB
+  constexpr int WIMG = kTile * kTile * kMKS * 2;   // [64 px][32 e] bf16 = 4 KB (hi, then lo)
+  // the fp32 output tile aliases the K-step images (used only after the last K-step)
+  __shared__ __attribute__((aligned(16))) char stage[kTile * kTile * C * 4];
+  __shared__ int keys[kChunk];
+  __shared__ FootP fs[kChunk];
+  const long long t_start = dbg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
+  char* const dimg = stage;
+  char* const whi = stage + DIMG;
+  char* const wlo = whi + WIMG;
+  float* const acc_t = reinterpret_cast<float*>(stage);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int k = blockIdx.x;
+  if (k >= coff[T]) return;
+  const int tile = ctile[k];
+  const int j = k - coff[tile], nch = coff[tile + 1] - coff[tile];
+  int lv, b, ty, tx;
+  decode_tile(L, G, tile, lv, b, ty, tx);
+  const int H = L.H[lv], W = L.W[lv];
+  const int y0 = ty * kTile, x0 = tx * kTile;
+  const int ebeg = offsets[tile] + j * kChunk;
+  const int n = min(kChunk, offsets[tile + 1] - ebeg);
+  if (n == 0) {
+    uint16_t* g = gout.p[lv];
+    for (int q = tid; q < kTile * kTile * (C / 8); q += 256) {
+      const int p = q / (C / 8), ch = (q % (C / 8)) * 8;
+      const int y = y0 + p / kTile, x = x0 + p % kTile;
+      if (y < H && x < W) *reinterpret_cast<uint4*>(g + (((size_t)b * H + y) * W + x) * C + ch) = make_uint4(0, 0, 0, 0);
+    }
+    return;
+  }
+  int np = 1;
+  while (np < n) np <<= 1;
+  for (int i = tid; i < np; i += 256) keys[i] = i < n ? entries[ebeg + i] : 0x7fffffff;
+  __syncthreads();
+  if (nch == 1)
+    for (int kk = 2; kk <= np; kk <<= 1)
+      for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+        for (int i = tid; i < np; i += 256) {
+          const int p = i ^ jj;
+          if (p > i) {
+            const int a = keys[i], c = keys[p];
+            if ((a > c) == ((i & kk) == 0)) { keys[i] = c; keys[p] = a; }
+          }
+        }
+        __syncthreads();
+      }
+  for (int i = tid; i < n; i += 256) fs[i] = fp[keys[i]];
+  __syncthreads();
+
+  // dY staging: thread t moves chunks q = t + 256 u (u < 4) of the K-step: row q / 32, logical
+  // 16-B chunk q % 32, stored at its swizzled position
+  uint4 dv[4];
+  auto load_rows = [&](int e0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = tid + 256 * u, e = e0 + (q >> 5), c = q & 31;
+      dv[u] = e < n ? *reinterpret_cast<const uint4*>(dout + (size_t)keys[e] * C + 8 * c) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_rows = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = tid + 256 * u, e = q >> 5, c = q & 31;
+      *reinterpret_cast<uint4*>(dimg + e * RB + gemm::pchunk(e, c) * 16) = dv[u];
+    }
+  };
+  // W image [px][e]: 64-B rows, 16-B chunk (e >> 3) at (e >> 3) ^ ((px >> 2) & 3)
+  auto woff = [](int px, int e) __attribute__((always_inline)) {
+    return px * (kMKS * 2) + (((e >> 3) ^ ((px >> 2) & 3)) << 4) + (e & 7) * 2;
+  };
+
+  // fragments: A = dY^T (16 channels x 32 entries) by transposed reads, B = W (32 entries x
+  // 16 pixels); lane (G, i) of the 16x16 output holds channels 4G .. 4G + 3 of pixel i
+  const int G4 = lane >> 4, i16 = lane & 15;
+  const int krow = 8 * G4 + (i16 >> 2);
+  int offA[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    const int pair = 4 * wave + cb;                 // 16-channel block = 32-B chunk pair
+    offA[cb] = krow * RB + (((pair ^ gemm::gsw(krow)) << 1) | ((i16 & 3) >> 1)) * 16 + (i16 & 1) * 8;
+  }
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int pb = 0; pb < 4; ++pb) acc[cb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_rows(0);
+  for (int e0 = 0; e0 < n; e0 += kMKS) {
+    store_rows();
+    // zero both W images (8 KB: two 16-B stores per thread)
+    reinterpret_cast<uint4*>(whi)[tid] = make_uint4(0, 0, 0, 0);
+    reinterpret_cast<uint4*>(whi)[tid + 256] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    // scatter the footprints: thread t takes entry e0 + (t & 31), slots (t >> 5) and + 8
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int el = tid & 31, slot = (tid >> 5) + 8 * h;
+      const int e = e0 + el;
+      if (e < n) {
+        const FootP& f = fs[e];
+        const int si = slot >> 2, sj = slot & 3;
+        const float w = f.wy[si] * f.wx[sj];
+        const int yy = f.ry[si] - y0, xx = f.rx[sj] - x0;
+        if (w != 0.f && (unsigned)yy < (unsigned)kTile && (unsigned)xx < (unsigned)kTile) {
+          const int px = yy * kTile + xx;
+          const __bf16 hi = (__bf16)w;
+          const __bf16 lo = (__bf16)(w - (float)hi);
+          *reinterpret_cast<__bf16*>(whi + woff(px, el)) = hi;
+          *reinterpret_cast<__bf16*>(wlo + woff(px, el)) = lo;
+        }
+      }
+    }
+    if (e0 + kMKS < n) load_rows(e0 + kMKS);      // next K-step's rows in flight during the MFMAs
+    __syncthreads();
+    bf16x8 a[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) a[cb] = gemm::cat(gemm::tr_read(dimg, offA[cb]), gemm::tr_read(dimg, offA[cb] + 4 * RB));
+#pragma unroll
+    for (int pb = 0; pb < 4; ++pb) {
+      const int px = 16 * pb + i16;
+      const int wo = px * (kMKS * 2) + ((G4 ^ ((px >> 2) & 3)) << 4);
+      const bf16x8 bh = gemm::lds_read8(whi, wo), bl = gemm::lds_read8(wlo, wo);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        acc[cb][pb] = gemm::mfma16(a[cb], bh, acc[cb][pb]);
+        acc[cb][pb] = gemm::mfma16(a[cb], bl, acc[cb][pb]);
+      }
+    }
+    __syncthreads();   // the next K-step rewrites the images
+  }
+  // accumulators -> fp32 tile [64 px][256 c] (aliases the images: every wave is past its last
+  // read -- the loop's final barrier)
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int pb = 0; pb < 4; ++pb)
+      *reinterpret_cast<f32x4*>(acc_t + (16 * pb + i16) * C + 64 * wave + 16 * cb + 4 * G4) = acc[cb][pb];
+  __syncthreads();
+  if (dbg && tid == 0) {
+    dbg[4 * k] = k; dbg[4 * k + 1] = tile; dbg[4 * k + 2] = n;
+    dbg[4 * k + 3] = (long long)__builtin_amdgcn_s_memrealtime() - t_start;
+  }
+  if (nch == 1) {
+    write_tile_bf16(acc_t, gout.p[lv], C, H, W, b, y0, x0, tid, 256);
+    return;
+  }
+  const int slot = poff[tile] + j;
+  if (slot >= pslots) {
+    if (tid == 0) atomicAdd(overflow, 1);
+    return;
+  }
+  float* dst = partial + (size_t)slot * kTile * kTile * C;
+  for (int i = tid * 4; i < kTile * kTile * C; i += 256 * 4)
+    *reinterpret_cast<float4*>(dst + i) = *reinterpret_cast<const float4*>(acc_t + i);
 }
 
 // split tiles: sum the chunk partials in chunk order -> bf16
@@ -1368,7 +1551,8 @@ MX_EXPORT int64_t mx_roi_align_bwd_tiled_ws(const int* H, const int* W, int n, i
 static long long* g_tile_dbg = nullptr;
 static int g_tile_dmode = 0;
 // debugging: per-workgroup timing records of the next tiled backward (4 x int64 per chunk);
-// mode bit 0 = skip the gradient loads, bit 1 = skip the LDS accumulation
+// mode bit 0 = skip the gradient loads, bit 1 = skip the LDS accumulation (scalar kernel);
+// bit 2 = the scalar per-entry kernel also for C = 256 (A/B against the MFMA kernel)
 MX_EXPORT void mx_roi_align_bwd_tiled_debug(long long* buf, int mode) {
   g_tile_dbg = buf;
   g_tile_dmode = mode;
@@ -1412,9 +1596,13 @@ MX_EXPORT int mx_roi_align_bwd_tiled(void* const* grads, const int* H, const int
   hipLaunchKernelGGL(tile_sort_kernel, dim3(T), dim3(1024), 0, s, offsets, T, entries);
   GOut go = {};
   for (int i = 0; i < n; ++i) go.p[i] = (uint16_t*)grads[i];
-  hipLaunchKernelGGL(roi_align_bwd_tile_kernel, dim3(grid), dim3(C), 0, s, L, G, T, C, (const uint16_t*)dout, fp,
-                     offsets, coff, poff, ctile, entries, go, partial, pslots, overflow, g_tile_dbg,
-                     g_tile_dmode);
+  if (C == 256 && !(g_tile_dmode & 4))
+    hipLaunchKernelGGL(roi_align_bwd_mfma_kernel, dim3(grid), dim3(256), 0, s, L, G, T, (const uint16_t*)dout, fp,
+                       offsets, coff, poff, ctile, entries, go, partial, pslots, overflow, g_tile_dbg);
+  else
+    hipLaunchKernelGGL(roi_align_bwd_tile_kernel, dim3(grid), dim3(C), 0, s, L, G, T, C, (const uint16_t*)dout, fp,
+                       offsets, coff, poff, ctile, entries, go, partial, pslots, overflow, g_tile_dbg,
+                       g_tile_dmode);
   hipLaunchKernelGGL(roi_align_bwd_combine_kernel, dim3(T), dim3(256), 0, s, L, G, C, coff, poff, partial, pslots, go);
   return hipGetLastError();
 }

@@ -81,7 +81,28 @@ def main():
         fn = V._lib.lib().mx_roi_align_bwd_tiled_debug
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
         fn.restype = None
-        for mode in (0, 1, 2, 3):
+        # the scalar per-entry kernel (debug mode bit 2) against the MFMA one, same inputs
+        fn2 = V._lib.lib().mx_roi_align_bwd_tiled_debug
+        fn2.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        fn2.restype = None
+        ab = {}
+        for mode in (4, 0):
+            fn2(None, mode)
+            for _ in range(3):
+                gg = torch.autograd.grad(out, fs, dout, retain_graph=True)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                gg = torch.autograd.grad(out, fs, dout, retain_graph=True)
+            e1.record()
+            torch.cuda.synchronize()
+            ab[mode] = (e0.elapsed_time(e1) * 1000 / a.iters, [t.float() for t in gg])
+        fn2(None, 0)
+        d_ab = max(float((x - y).abs().max() / (y.abs().max() + 1e-6)) for x, y in zip(ab[0][1], ab[4][1]))
+        print(f"[roi] call {ci}: tiled scalar-entry kernel {ab[4][0]:.1f} us, MFMA kernel {ab[0][0]:.1f} us, "
+              f"max rel diff {d_ab:.2e}", flush=True)
+        for mode in (0, 4):
             dbg = torch.full((200000, 4), -1, dtype=torch.int64, device=dev)
             fn(dbg.data_ptr(), mode)
             torch.autograd.grad(out, fs, dout, retain_graph=True)

@@ -97,19 +97,34 @@ def test_decode_inverts_encode():
     torch.testing.assert_close(V.decode_boxes(ref, V.encode_boxes(ref, gt, w), w), gt, rtol=1e-4, atol=1e-3)
 
 
+def _tiny_rois(R, B, gen):
+    """Concentrated small boxes (what a random-init RPN proposes): most entries land in a
+    few P2 tiles, which the tiled backward splits into several chunks + a combine pass."""
+    cx = 300 + torch.rand(R, generator=gen) * 40
+    cy = 200 + torch.rand(R, generator=gen) * 40
+    w = 4 + torch.rand(R, generator=gen) * 20
+    h = 4 + torch.rand(R, generator=gen) * 20
+    b = torch.randint(0, B, (R,), generator=gen).float()
+    return torch.stack([b, cx - w / 2, cy - h / 2, cx + w / 2, cy + h / 2], 1)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("tiled", [True, False])
 @pytest.mark.parametrize("out_hw", [7, 14])
-def test_roi_align_gpu_fwd_bwd(tiled, out_hw, monkeypatch):
-    """Forward and both backward kernels (tiled / fp32 atomics) vs the fp32 torch
-    reference; the tiled backward is also bitwise deterministic across runs."""
+@pytest.mark.parametrize("spread", ["spread", "tiny"])
+def test_roi_align_gpu_fwd_bwd(tiled, out_hw, spread, monkeypatch):
+    """Forward and both backward kernels (tiled -- the MFMA kernel at C = 256 -- / fp32
+    atomics) vs the fp32 torch reference, on spread-out boxes and on concentrated tiny ones
+    (split tiles); the tiled backward is also bitwise deterministic across runs."""
     monkeypatch.setattr(V, "_TILED", tiled)
     g = torch.Generator().manual_seed(3)
     B, C = 2, 256
     shapes = [(200, 336), (100, 168), (50, 84), (25, 42)]
     scales = [1 / 4, 1 / 8, 1 / 16, 1 / 32]
     feats = [torch.randn(B, h, w, C, generator=g).bfloat16() for h, w in shapes]
-    rois = _rand_rois(300, B, 800, 1344, g)
+    # (tiny: 9800 items -- 200 boxes at 7 x 7, 50 at 14 x 14 -- so no tile exceeds the
+    # 16384-entry sort that keeps split tiles deterministic)
+    rois = _rand_rois(300, B, 800, 1344, g) if spread == "spread" else _tiny_rois(9800 // (out_hw * out_hw), B, g)
     ref_in = [f.float().requires_grad_(True) for f in feats]
     ref = V._ref_roi_align(ref_in, scales, rois, out_hw, out_hw, 2, True, 2, 224.0, 4)
     fg = [f.cuda().requires_grad_(True) for f in feats]
@@ -119,8 +134,9 @@ def test_roi_align_gpu_fwd_bwd(tiled, out_hw, monkeypatch):
     (ref * dout).sum().backward()
     (out.float() * dout.cuda()).sum().backward()
     for a, b in zip(fg, ref_in):
-        err = (a.grad.float().cpu() - b.grad).norm() / (b.grad.norm() + 1e-6)
-        assert err < 2e-2, float(err)
+        bg = b.grad if b.grad is not None else torch.zeros_like(b)   # a level no RoI maps to
+        err = (a.grad.float().cpu() - bg).norm() / (bg.norm() + 1e-6)
+        assert err < 2e-2 or bg.norm() == 0 and a.grad.abs().max() == 0, float(err)
     if tiled:
         assert V.tiled_overflow() == 0
         first = [f.grad.clone() for f in fg]
