@@ -29,6 +29,8 @@
 //    (ds_read_b64_tr_b16) with the source-side XOR swizzle, as in gemm.hip.
 #include "gemm_common.h"
 
+#include <cstdlib>
+
 using namespace mx;
 using namespace mx::gemm;
 
@@ -227,9 +229,9 @@ struct ConvFw {
   float invOW, invOH;
 };
 
-template <bool RES, bool RELU>
+template <int NSLOT, bool RES, bool RELU>
 __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
-  constexpr int WN = 2, FM = 4, FN = 4, BKT = 64, NSLOT = 2;
+  constexpr int WN = 2, FM = 4, FN = 4, BKT = 64;
   constexpr int BM = 128, BN = 128, R = BKT * 2;
   constexpr int IA = BM * R, IB = BN * R;
   constexpr int PA = IA / 1024 / 4, PB = IB / 1024 / 4;
@@ -292,12 +294,23 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
     for (int j = 0; j < PB; ++j) dma16(srcB(j, tap, ci0), b1 + j * 1024);
   };
 
-  if (nk > 0) issue(0, 0);
+  // NSLOT-deep LDS-DMA ring, counted waits (the input gradient's scheme): with NSLOT > 2 the
+  // next steps' pieces stay in flight across the barrier
+#pragma unroll
+  for (int q = 0; q < NSLOT - 1; ++q)
+    if (q < nk) issue(q, q);
   int slot = 0;
   for (int it = 0; it < nk; ++it) {
-    vm_wait<0>();
+    const int later = nk - 1 - it;
+    if (NSLOT >= 4 && later >= 2) vm_wait<(NSLOT >= 4 ? 2 : 0) * PER>();
+    else if (NSLOT >= 3 && later >= 1) vm_wait<(NSLOT >= 3 ? 1 : 0) * PER>();
+    else vm_wait<0>();
     __builtin_amdgcn_s_barrier();
-    if (it + 1 < nk) issue(slot ^ 1, it + 1);
+    if (it + NSLOT - 1 < nk) {
+      int ns = slot + NSLOT - 1;
+      if (ns >= NSLOT) ns -= NSLOT;
+      issue(ns, it + NSLOT - 1);
+    }
     const char* As = smem + slot * SLOT;
     const char* Bs = As + IA;
 #pragma unroll
@@ -314,9 +327,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
         for (int u = 0; u < FN; ++u) acc[a][u] = mfma16(b[u], av, acc[a][u]);
       }
     }
-    slot ^= 1;
+    if (++slot == NSLOT) slot = 0;
   }
-  (void)PER;
 
   // ---- epilogue: lane (G, i) holds y[m0 + 16 (FM wm + a) + i][n0 + 16 (FN wn + u) + 4 G + e];
   // pairs of 16-channel subtiles are re-dealt (permlane swaps) so every lane stores 8
@@ -600,6 +612,19 @@ __global__ __launch_bounds__(64) void conv_wgrad_reduce_kernel(const ConvWg cp) 
 }  // namespace
 
 // Tile geometry for the host planner: what = 0 -> BM, 1 -> BN, 2 -> BK (pixel rows per K-step).
+// LDS-DMA ring depth of the forward (which = 0) / input-gradient (1) kernels: 2 (two
+// workgroups per CU, 64 KB each) unless MXTRAIN_CONV_FWD_SLOTS / MXTRAIN_CONV_DGRAD_SLOTS
+// pick 3 or 4 (one workgroup per CU, counted waits keep 1-2 steps in flight) -- A/B knob
+static int conv_slots(int which) {
+  static int v[2] = {-1, -1};
+  if (v[which] < 0) {
+    const char* e = getenv(which ? "MXTRAIN_CONV_DGRAD_SLOTS" : "MXTRAIN_CONV_FWD_SLOTS");
+    const int n = e ? atoi(e) : 2;
+    v[which] = (n == 3 || n == 4) ? n : 2;
+  }
+  return v[which];
+}
+
 MX_EXPORT int mx_conv_wgrad_tile(int what) { return what == 0 ? kBM : what == 1 ? kBN : kBK; }
 
 // d (int64[20]): {dy, x, zero, dw, slab, 0, ldy, ldx, N, OH, OW, IH, IW, KH, KW, stride,
@@ -714,7 +739,11 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   cp.invIW = 1.f / (float)cp.IW;
   cp.invIH = 1.f / (float)cp.IH;
   const int tiles_m = (int)((T + 127) / 128);
-  hipLaunchKernelGGL(conv_dgrad_kernel<2>, dim3(tiles_m * cp.tiles_n), dim3(256), 0, (hipStream_t)stream, cp);
+  switch (conv_slots(1)) {
+    case 3: hipLaunchKernelGGL(conv_dgrad_kernel<3>, dim3(tiles_m * cp.tiles_n), dim3(256), 0, (hipStream_t)stream, cp); break;
+    case 4: hipLaunchKernelGGL(conv_dgrad_kernel<4>, dim3(tiles_m * cp.tiles_n), dim3(256), 0, (hipStream_t)stream, cp); break;
+    default: hipLaunchKernelGGL(conv_dgrad_kernel<2>, dim3(tiles_m * cp.tiles_n), dim3(256), 0, (hipStream_t)stream, cp);
+  }
   return (int)hipGetLastError();
 }
 
@@ -763,12 +792,19 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   cp.invOH = 1.f / (float)cp.OH;
   const dim3 grid((unsigned)((T + 127) / 128) * cp.tiles_n), block(256);
   hipStream_t st = (hipStream_t)stream;
-  if (cp.res) {
-    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<true, true>), grid, block, 0, st, cp);
-    else hipLaunchKernelGGL((conv_fwd_kernel<true, false>), grid, block, 0, st, cp);
-  } else {
-    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<false, true>), grid, block, 0, st, cp);
-    else hipLaunchKernelGGL((conv_fwd_kernel<false, false>), grid, block, 0, st, cp);
+#define MX_CF(NS)                                                                      \
+  if (cp.res) {                                                                        \
+    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, true, true>), grid, block, 0, st, cp);   \
+    else hipLaunchKernelGGL((conv_fwd_kernel<NS, true, false>), grid, block, 0, st, cp);       \
+  } else {                                                                             \
+    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, false, true>), grid, block, 0, st, cp);  \
+    else hipLaunchKernelGGL((conv_fwd_kernel<NS, false, false>), grid, block, 0, st, cp);      \
   }
+  switch (conv_slots(0)) {
+    case 3: MX_CF(3) break;
+    case 4: MX_CF(4) break;
+    default: MX_CF(2) break;
+  }
+#undef MX_CF
   return (int)hipGetLastError();
 }

@@ -1643,6 +1643,34 @@ MX_EXPORT int mx_match(const float* anchors, int A, int per_image_anchors, const
   return hipGetLastError();
 }
 
+// Rows of an NHWC level into its place on a canvas (RPN level canvas, models/maskrcnn.py):
+// src [B][h][w*C] contiguous -> dst[(n * Hc + y0 + y) * pitch + x0 * C ...], 16-B vectors
+// (a strided-view copy_ ran PyTorch's non-vectorised elementwise kernel).  row_elems and
+// pitch multiples of 8, pointers 16-B aligned.
+__global__ __launch_bounds__(256) void copy_rows_kernel(uint16_t* __restrict__ dst, const uint16_t* __restrict__ src,
+                                                        int h, int row_vec, int Hc, int64_t pitch, int64_t dst_off,
+                                                        int64_t nvec) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = v / row_vec;
+    const int c = (int)(v - r * row_vec);
+    const int n = (int)(r / h), y = (int)(r - (int64_t)n * h);
+    reinterpret_cast<uint4*>(dst + dst_off + ((int64_t)n * Hc + y) * pitch)[c] =
+        reinterpret_cast<const uint4*>(src)[v];
+  }
+}
+
+MX_EXPORT int mx_copy_rows(void* dst, const void* src, int B, int h, int row_elems, int Hc, int64_t pitch,
+                           int64_t dst_off, hipStream_t s) {
+  if ((row_elems & 7) || (pitch & 7) || (dst_off & 7) || (((uintptr_t)dst | (uintptr_t)src) & 15))
+    return hipErrorInvalidValue;
+  const int64_t nvec = (int64_t)B * h * (row_elems / 8);
+  if (nvec == 0) return hipSuccess;
+  const int64_t want = (nvec + 255) / 256;
+  hipLaunchKernelGGL(copy_rows_kernel, dim3((unsigned)(want < 16384 ? want : 16384)), dim3(256), 0, s,
+                     (uint16_t*)dst, (const uint16_t*)src, h, row_elems / 8, Hc, pitch, dst_off, nvec);
+  return hipGetLastError();
+}
+
 MX_EXPORT int mx_decode_clip(const float* ref, const float* deltas, int N, int per_row_ref, float wx, float wy,
                              float ww, float wh, float clamp, const float* img_hw, int rows_per_img, float* out,
                              hipStream_t s) {

@@ -32,6 +32,7 @@ import torch.nn.functional as F
 from ..ops.epilogue import BlockLink, conv_bias_act, conv_transpose_bias_act, fused_conv_ok
 from ..ops import detloss as D
 from ..ops import vision as V
+from ..ops import _lib
 from .compute_weights import ComputeWeights, cw
 from .resnet import ConvNorm, resnet50
 
@@ -204,10 +205,16 @@ class _PackLevels(torch.autograd.Function):
     def forward(ctx, lay, *levels):
         Hc, Wc, offs = lay
         p0 = levels[0]
-        c = torch.zeros(p0.shape[0], p0.shape[1], Hc, Wc, dtype=p0.dtype, device=p0.device,
-                        ).contiguous(memory_format=torch.channels_last)
+        B, C = p0.shape[0], p0.shape[1]
+        c = torch.empty(B, C, Hc, Wc, dtype=p0.dtype, device=p0.device, memory_format=torch.channels_last).zero_()
         for (y0, x0), p in zip(offs, levels):
-            c[:, :, y0:y0 + p.shape[2], x0:x0 + p.shape[3]].copy_(p)
+            if (p.is_cuda and p.dtype == torch.bfloat16 and p.is_contiguous(memory_format=torch.channels_last)
+                    and C % 8 == 0 and p.data_ptr() % 16 == 0):
+                # one vectorised launch per level (csrc/vision.hip copy_rows_kernel)
+                _lib.call("mx_copy_rows", c.data_ptr(), p.data_ptr(), B, p.shape[2], p.shape[3] * C, Hc, Wc * C,
+                          (y0 * Wc + x0) * C, _lib.stream())
+            else:
+                c[:, :, y0:y0 + p.shape[2], x0:x0 + p.shape[3]].copy_(p)
         ctx.geo = [(y0, x0, p.shape[2], p.shape[3]) for (y0, x0), p in zip(offs, levels)]
         return c
 

@@ -85,7 +85,7 @@ def main():
         where = frames[0].split("mxtrain/")[-1] if frames else "?"
         for k in getattr(e, "kernels", []) or []:
             if pat.search(k.name):
-                sel[(k.name[:60], e.name, where)] += 1
+                sel[(k.name[:60], e.name, str(e.input_shapes)[:110])] += 1
     # gradient-accumulation / residual adds by operand shape (backward ops carry no stack)
     shp = collections.Counter()
     for e in evs:
@@ -96,7 +96,7 @@ def main():
         print(f"{n:5d}  {name:10s} {sh}")
     print("\nselected kernels by launching op:")
     for (kn, name, where), n in sel.most_common(80):
-        print(f"{n:5d}  {kn:60s} {name:32s} {where}")
+        print(f"{n:5d}  {kn:60s} {name:24s} {where}")
 
 
 if __name__ == "__main__":

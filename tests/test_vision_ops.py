@@ -375,3 +375,28 @@ def test_topk_rows_ties_early_larger_keys_late(n, k):
             assert i[r].unique().numel() == k
             # the tied part is the lowest indices, in order
             assert torch.equal(i[r, n_gt:].sort().values, torch.arange(k - n_gt, device="cuda"))
+
+
+@pytest.mark.gpu
+def test_rpn_level_canvas_pack_gpu():
+    """models/maskrcnn.py _PackLevels on the GPU (csrc/vision.hip copy_rows_kernel): the
+    canvas equals the levels placed by slicing, zeros elsewhere; the backward hands each
+    level its slice of the canvas gradient."""
+    from mxtrain.models.maskrcnn import _PackLevels, level_canvas
+    g = torch.Generator().manual_seed(11)
+    shapes = [(200, 336), (100, 168), (50, 84), (25, 42), (13, 21)]
+    lay = level_canvas(shapes)
+    assert lay is not None
+    cl = torch.channels_last
+    lv = [torch.randn(2, 256, h, w, generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=cl).requires_grad_()
+          for h, w in shapes]
+    c = _PackLevels.apply(lay, *lv)
+    Hc, Wc, offs = lay
+    ref = torch.zeros(2, 256, Hc, Wc, dtype=torch.bfloat16)
+    for (y0, x0), p in zip(offs, lv):
+        ref[:, :, y0:y0 + p.shape[2], x0:x0 + p.shape[3]] = p.detach().cpu()
+    assert torch.equal(c.detach().cpu(), ref)
+    gc = torch.randn(c.shape, generator=g).to(torch.bfloat16).cuda()
+    c.backward(gc)
+    for (y0, x0), p in zip(offs, lv):
+        assert torch.equal(p.grad.cpu(), gc[:, :, y0:y0 + p.shape[2], x0:x0 + p.shape[3]].cpu())
