@@ -29,8 +29,6 @@
 //    (ds_read_b64_tr_b16) with the source-side XOR swizzle, as in gemm.hip.
 #include "gemm_common.h"
 
-#include <cstdlib>
-
 using namespace mx;
 using namespace mx::gemm;
 
@@ -612,19 +610,6 @@ __global__ __launch_bounds__(64) void conv_wgrad_reduce_kernel(const ConvWg cp) 
 }  // namespace
 
 // Tile geometry for the host planner: what = 0 -> BM, 1 -> BN, 2 -> BK (pixel rows per K-step).
-// LDS-DMA ring depth of the forward (which = 0) / input-gradient (1) kernels: 2 (two
-// workgroups per CU, 64 KB each) unless MXTRAIN_CONV_FWD_SLOTS / MXTRAIN_CONV_DGRAD_SLOTS
-// pick 3 or 4 (one workgroup per CU, counted waits keep 1-2 steps in flight) -- A/B knob
-static int conv_slots(int which) {
-  static int v[2] = {-1, -1};
-  if (v[which] < 0) {
-    const char* e = getenv(which ? "MXTRAIN_CONV_DGRAD_SLOTS" : "MXTRAIN_CONV_FWD_SLOTS");
-    const int n = e ? atoi(e) : 2;
-    v[which] = (n == 3 || n == 4) ? n : 2;
-  }
-  return v[which];
-}
-
 MX_EXPORT int mx_conv_wgrad_tile(int what) { return what == 0 ? kBM : what == 1 ? kBN : kBK; }
 
 // d (int64[20]): {dy, x, zero, dw, slab, 0, ldy, ldx, N, OH, OW, IH, IW, KH, KW, stride,
@@ -739,11 +724,7 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   cp.invIW = 1.f / (float)cp.IW;
   cp.invIH = 1.f / (float)cp.IH;
   const int tiles_m = (int)((T + 127) / 128);
-  switch (conv_slots(1)) {
-    case 3: hipLaunchKernelGGL(conv_dgrad_kernel<3>, dim3(tiles_m * cp.tiles_n), dim3(256), 0, (hipStream_t)stream, cp); break;
-    case 4: hipLaunchKernelGGL(conv_dgrad_kernel<4>, dim3(tiles_m * cp.tiles_n), dim3(256), 0, (hipStream_t)stream, cp); break;
-    default: hipLaunchKernelGGL(conv_dgrad_kernel<2>, dim3(tiles_m * cp.tiles_n), dim3(256), 0, (hipStream_t)stream, cp);
-  }
+  hipLaunchKernelGGL(conv_dgrad_kernel<2>, dim3(tiles_m * cp.tiles_n), dim3(256), 0, (hipStream_t)stream, cp);
   return (int)hipGetLastError();
 }
 
@@ -800,11 +781,9 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
     if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, false, true>), grid, block, 0, st, cp);  \
     else hipLaunchKernelGGL((conv_fwd_kernel<NS, false, false>), grid, block, 0, st, cp);      \
   }
-  switch (conv_slots(0)) {
-    case 3: MX_CF(3) break;
-    case 4: MX_CF(4) break;
-    default: MX_CF(2) break;
-  }
+  // ring depth 2 at two workgroups per CU: 3 / 4 slots (one workgroup per CU, counted waits)
+  // measured 40 % slower on the Mask R-CNN shapes (profiles/r4_s2/conv_ring_depth_ab_4img.txt)
+  MX_CF(2)
 #undef MX_CF
   return (int)hipGetLastError();
 }

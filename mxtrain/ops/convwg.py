@@ -15,7 +15,6 @@ non-bf16 tensors, CPU) take plain ``F.conv2d`` -- part of the contract, not an e
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Dict, Tuple
 
 import torch
@@ -27,8 +26,8 @@ ENABLED = True          # module switch (A/B runs: scripts/conv_wgrad_bench.py)
 DGRAD = True            # input gradient from csrc/convwg.hip too (else MIOpen's backward-data)
 FWD = True              # forward with the fused bias / residual / ReLU epilogue (else MIOpen)
 FWD_MIN_TILES = 64
-TARGET_WGS = int(os.environ.get("MXTRAIN_WGRAD_TARGET_WGS", "512"))   # two 128 x 128 workgroups per CU
-MIN_STEPS = int(os.environ.get("MXTRAIN_WGRAD_MIN_STEPS", "8"))
+TARGET_WGS = 512        # two 128 x 128 workgroups per CU on 256 CUs (a 256 / 1024 x 4 / 16 sweep:
+MIN_STEPS = 8           # profiles/r4_s2/conv_wgrad_split_sweep.txt)
 _DESC_T = ctypes.c_int64 * 24
 _WS: Dict[torch.device, Tuple[torch.Tensor, torch.Tensor]] = {}
 _RETIRED = []           # outgrown slabs stay alive: a captured hipGraph may still write them

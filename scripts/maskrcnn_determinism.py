@@ -18,6 +18,9 @@ def main():
     from mxtrain.data.coco_synth import write_split
     from mxtrain.models.compute_weights import FlatMaster
     from mxtrain.models.maskrcnn import MaskRCNN, MaskRCNNConfig
+    if os.environ.get("MIOPEN_DET") == "1":   # MIOpen's deterministic solvers only
+        torch.backends.cudnn.deterministic = True
+        print("cudnn.deterministic = True")
     d = tempfile.mkdtemp()
     write_split(d, "train2017", 16, 0, 1)
     for (H, W, small) in ((256, 384, True), (800, 1333, False)):
@@ -30,8 +33,9 @@ def main():
         torch.manual_seed(0)
         ma = MaskRCNN(cfg).cuda().train()
         mb = copy.deepcopy(ma)
+        mw = copy.deepcopy(ma)   # warm-up copy: MIOpen's first call of a shape may run another solver
         hist = {}
-        for tag, m in (("a", ma), ("b", mb)):
+        for tag, m in (("warm", mw), ("a", ma), ("b", mb)):
             ps = [p for p in m.parameters() if p.requires_grad]
             opt = torch.optim.SGD(ps, lr=0.01, momentum=0.9)
             fm = FlatMaster(m, opt, 1.0)
@@ -48,6 +52,8 @@ def main():
             torch.cuda.synchronize()
             hist[tag] = (out, [p.detach().float().clone() for p in ps])
         print(f"== {H}x{W}")
+        for s, (lw, la) in enumerate(zip(hist["warm"][0], hist["a"][0])):
+            print(f"first-run copy vs a, step {s}: {'identical' if lw == la else 'differ'}")
         for s, (la, lb) in enumerate(zip(hist["a"][0], hist["b"][0])):
             diff = {k: (la[k], lb[k]) for k in la if la[k] != lb[k]}
             print(f"step {s}: {'identical' if not diff else 'DIFFER ' + str(diff)}")
