@@ -37,6 +37,7 @@ def _worker(rank, world, port, data_dir, q):
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
+        torch.backends.cudnn.deterministic = True   # as workloads/maskrcnn/train.py
         from mxtrain.data.coco import COCODetection, DetectionDataset, collate
         from mxtrain.models.compute_weights import FlatMaster
         from mxtrain.models.maskrcnn import MaskRCNN, MaskRCNNConfig
@@ -122,10 +123,11 @@ def test_dp_graphed_step_with_xgmi_allreduce_matches_eager(tmp_path):
     for r, info, ha, hb in res:
         assert info["captures"] == 1 and info["replays"] == 3 and info["eager"] == 0, info
         assert info["routes_a"] == ["xgmi"] and info["routes_b"] == ["xgmi"], info
-        assert info["rel"] < 1e-3, info
+        # MIOpen's deterministic solvers (set in the worker) + deterministic in-repo kernels and
+        # xGMI reductions: the graphed step reproduces the eager one
+        assert info["rel"] < 1e-6, info
         for s, (x, y) in enumerate(zip(info["la"], info["lb"])):
-            tol = 0.05
-            assert abs(x - y) <= tol * abs(x) + 1e-3, (r, s, info["la"], info["lb"])
+            assert abs(x - y) <= 1e-5 * abs(x), (r, s, info["la"], info["lb"])
     # every rank applied the same averaged gradients: identical parameters on both paths
     assert np.array_equal(res[0][2], res[1][2])
     assert np.array_equal(res[0][3], res[1][3])

@@ -41,6 +41,12 @@ def test_graphed_step_matches_eager(tmp_path):
     b1 = {k: (v.pin_memory() if torch.is_tensor(v) else v) for k, v in b1.items()}
     b2 = {k: (v.pin_memory() if torch.is_tensor(v) else v) for k, v in b2.items()}
     cfg = MaskRCNNConfig(train_per_level_topk=300, train_post_nms_topk=300, frcnn_batch_per_im=64)
+    # MIOpen's deterministic solvers: with its default (atomics-based) choices for the few
+    # convolutions it still runs, two identical eager steps already differ in the last bits
+    # and the random-init proposal sampling amplifies that (scripts/maskrcnn_determinism.py);
+    # every in-repo kernel is deterministic, so the graph must then reproduce eager exactly
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
     torch.manual_seed(0)
     ma = MaskRCNN(cfg).cuda().train()
     mb = copy.deepcopy(ma)
@@ -53,24 +59,17 @@ def test_graphed_step_matches_eager(tmp_path):
     torch.cuda.manual_seed(7)
     lb = [gs(b, lr) for b, lr in plan]
     torch.cuda.synchronize()
+    torch.backends.cudnn.deterministic = det
     assert gs.captures == 1 and gs.replays == 3
     num = sum(float((p - q).float().norm() ** 2) for p, q in zip(pa, pb)) ** 0.5
     den = sum(float(p.float().norm() ** 2) for p in pa) ** 0.5
-    # GEMM algorithms chosen under capture can differ from eager ones in rounding, and the
-    # discrete proposal / RoI sampling amplifies the difference, while the parameters stay
-    # within 1e-3.
     rel = [max(abs(float(x[k]) - float(y[k])) / (abs(float(x[k])) + 1e-6) for k in x) for x, y in zip(la, lb)]
-    print(f"graphed vs eager, max relative loss difference per step: {[round(r, 4) for r in rel]}; "
-          f"params {num / den:.2e}")
-    # (measured with the graph's memset nodes replayed as fill kernels: <= 3.3 % on every
-    # step, profiles/r3_s4/; 15 % was needed on later steps before)
+    print(f"graphed vs eager, max relative loss difference per step: {rel}; params {num / den:.2e}")
     for s, (x, y) in enumerate(zip(la, lb)):
-        tol = 0.05
         for k in x:
             assert torch.isfinite(y[k]), (s, k)
-            assert abs(float(x[k]) - float(y[k])) <= tol * abs(float(x[k])) + 1e-3, \
-                (s, k, float(x[k]), float(y[k]), num / den)
-    assert num / den < 1e-3, num / den
+            assert abs(float(x[k]) - float(y[k])) <= 1e-5 * abs(float(x[k])), (s, k, float(x[k]), float(y[k]))
+    assert num / den < 1e-6, num / den
 
 
 @pytest.mark.gpu
