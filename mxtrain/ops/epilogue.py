@@ -131,7 +131,9 @@ class ConvBiasActFn(torch.autograd.Function):
         st, pd, dl = ctx.conf
         want_db = ctx.needs_input_grad[2]
         link, k, roles = ctx.fuse if ctx.fuse is not None else (None, -1, ())
-        relu = ctx.relu and not (link is not None and link.premask.get(k) and not want_db)
+        # a premasked gradient already carries this conv's ReLU (the consumer's dgrad store
+        # applied it): only the bias gradient, if any, is left -- column sums of g itself
+        relu = ctx.relu and not (link is not None and link.premask.get(k))
         dy, db = _bias_act_bwd(g, out, relu, want_db)
         if db is not None and db.dtype != ctx.bdtype:
             db = db.to(ctx.bdtype)
