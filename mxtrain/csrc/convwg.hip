@@ -227,10 +227,13 @@ struct ConvFw {
   float invOW, invOH;
 };
 
-template <int NSLOT, bool RES, bool RELU>
+// FN = 4: 128 x 128 tiles (Cout % 128 == 0); FN = 2: 128 x 64 tiles for Cout % 128 == 64 (the
+// 64-channel res2 convolutions, which otherwise went to MIOpen)
+template <int NSLOT, int FN, bool RES, bool RELU>
 __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
-  constexpr int WN = 2, FM = 4, FN = 4, BKT = 64;
-  constexpr int BM = 128, BN = 128, R = BKT * 2;
+  constexpr int WN = 2, FM = 4, BKT = 64;
+  constexpr int BM = 128, BN = 16 * FN * WN, R = BKT * 2;
+  static_assert(FN == 2 || FN == 4, "tile width");
   constexpr int IA = BM * R, IB = BN * R;
   constexpr int PA = IA / 1024 / 4, PB = IB / 1024 / 4;
   constexpr int SLOT = IA + IB, PER = PA + PB;
@@ -731,7 +734,7 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
 // d (int64[24]): {x, w, zero, y, bias, res, ldx, ldy, N, OH, OW, IH, IW, KH, KW, stride, pad,
 // dil, Cout, Cin, relu, res_up}: y = act(conv2d(x, w) + bias (+ res, or with res_up the 2x
 // nearest upsampling of res)) in NHWC bf16, weight [Cout][KH][KW][Cin] (channels_last).
-// Cout a multiple of 128, Cin of 64; res_up needs even OH, OW.
+// Cout a multiple of 64 (128 x 64 tiles when not of 128), Cin of 64; res_up needs even OH, OW.
 MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   ConvFw cp{};
   cp.x = reinterpret_cast<const uint16_t*>(d[0]);
@@ -761,29 +764,29 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   if (N <= 0 || cp.IH <= 0 || cp.IW <= 0 || cp.OH <= 0 || cp.OW <= 0 || KH <= 0 || cp.KW <= 0 || cp.stride <= 0 ||
       cp.dil <= 0 || cp.pad < 0 || T >= (1 << 23) || N * cp.IH * cp.IW >= ((int64_t)1 << 31))
     return (int)hipErrorInvalidValue;
-  if (Cout % 128 || cp.Cin % 64 || cp.ldx < cp.Cin || cp.ldy < Cout || (cp.ldx & 7) || (cp.ldy & 7))
+  if (Cout % 64 || cp.Cin % 64 || cp.ldx < cp.Cin || cp.ldy < Cout || (cp.ldx & 7) || (cp.ldy & 7))
     return (int)hipErrorInvalidValue;
   if ((d[0] | d[1] | d[2]) & 15) return (int)hipErrorInvalidValue;
   cp.T = (int)T;
   cp.taps = KH * cp.KW;
   cp.cib = cp.Cin / 64;
   cp.nk = cp.taps * cp.cib;
-  cp.tiles_n = Cout / 128;
+  cp.tiles_n = Cout % 128 == 0 ? Cout / 128 : Cout / 64;
   cp.invOW = 1.f / (float)cp.OW;
   cp.invOH = 1.f / (float)cp.OH;
   const dim3 grid((unsigned)((T + 127) / 128) * cp.tiles_n), block(256);
   hipStream_t st = (hipStream_t)stream;
-#define MX_CF(NS)                                                                      \
-  if (cp.res) {                                                                        \
-    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, true, true>), grid, block, 0, st, cp);   \
-    else hipLaunchKernelGGL((conv_fwd_kernel<NS, true, false>), grid, block, 0, st, cp);       \
-  } else {                                                                             \
-    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, false, true>), grid, block, 0, st, cp);  \
-    else hipLaunchKernelGGL((conv_fwd_kernel<NS, false, false>), grid, block, 0, st, cp);      \
+#define MX_CF(NS, FN)                                                                         \
+  if (cp.res) {                                                                               \
+    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, true, true>), grid, block, 0, st, cp);   \
+    else hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, true, false>), grid, block, 0, st, cp);       \
+  } else {                                                                                    \
+    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, false, true>), grid, block, 0, st, cp);  \
+    else hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, false, false>), grid, block, 0, st, cp);      \
   }
   // ring depth 2 at two workgroups per CU: 3 / 4 slots (one workgroup per CU, counted waits)
   // measured 40 % slower on the Mask R-CNN shapes (profiles/r4_s2/conv_ring_depth_ab_4img.txt)
-  MX_CF(2)
+  if (Cout % 128 == 0) { MX_CF(2, 4) } else { MX_CF(2, 2) }
 #undef MX_CF
   return (int)hipGetLastError();
 }

@@ -135,11 +135,11 @@ DGRAD_MIN_TILES = 64
 
 def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, padding=0, dilation=1,
                   res_up: bool = False) -> bool:
-    """The implicit-GEMM forward: NHWC bf16, Cout a multiple of 128, Cin of 64, and at least
-    FWD_MIN_TILES 128 x 128 output tiles (smaller convs stay on MIOpen).  ``res_up``: the
+    """The implicit-GEMM forward: NHWC bf16, Cout a multiple of 64, Cin of 64, and at least
+    FWD_MIN_TILES output tiles (smaller convs stay on MIOpen).  ``res_up``: the
     residual is at half the output resolution, added nearest-upsampled."""
     if not (FWD and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
-            and w.dim() == 4 and w.shape[0] % 128 == 0 and w.shape[1] % 64 == 0 and x.shape[1] == w.shape[1]
+            and w.dim() == 4 and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and x.shape[1] == w.shape[1]
             and _cl(x) and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
             and None not in (_sym(stride), _sym(padding), _sym(dilation))):
         return False
@@ -157,7 +157,8 @@ def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, paddi
                                      and tuple(residual.shape) == rshape
                                      and residual.data_ptr() % 16 == 0):   # 16-B residual loads
         return False
-    return (N * OH * OW + 127) // 128 * (w.shape[0] // 128) >= FWD_MIN_TILES
+    # 128 x 128 tiles, or 128 x 64 when Cout is an odd multiple of 64 (csrc/convwg.hip)
+    return (N * OH * OW + 127) // 128 * (w.shape[0] // (128 if w.shape[0] % 128 == 0 else 64)) >= FWD_MIN_TILES
 
 
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool = False, stride=1, padding=0,

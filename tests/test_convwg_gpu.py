@@ -111,7 +111,10 @@ def test_conv_dgrad_matches_fp32(case):
 
 
 @pytest.mark.parametrize("case", [(1, 64, 256, 40, 48, 1, 1, 0, 1), (2, 128, 128, 25, 42, 3, 1, 1, 1),
-                                  (1, 256, 128, 50, 60, 1, 2, 0, 1), (1, 128, 256, 30, 33, 3, 1, 2, 2)])
+                                  (1, 256, 128, 50, 60, 1, 2, 0, 1), (1, 128, 256, 30, 33, 3, 1, 2, 2),
+                                  # 128 x 64 tiles (Cout an odd multiple of 64: res2)
+                                  (2, 64, 64, 50, 62, 3, 1, 1, 1), (1, 256, 64, 41, 37, 1, 1, 0, 1),
+                                  (1, 128, 192, 30, 33, 1, 1, 0, 1)])
 @pytest.mark.parametrize("res", [False, True])
 def test_conv_fwd_fused_epilogue_matches_fp32(case, res):
     from mxtrain.ops import convwg
