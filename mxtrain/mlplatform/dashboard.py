@@ -24,7 +24,9 @@ Replaces, per reference component:
   ``GET /api/runs/<run>``, ``POST /api/runs/<run>/terminate`` (asynchronous runs; with
   ``cache: true`` steps whose inputs succeeded before are served from the step cache),
   ``GET|POST /api/recurringruns``, ``POST /api/recurringruns/<name>/enable|disable``
-  (cron / interval schedules fired by the scheduler thread);
+  (cron / interval schedules fired by the scheduler thread), ``GET /api/runs/<run>/lineage``,
+  ``GET /api/artifacts/<id>/lineage`` (run metadata: MLMD executions / artifacts / events,
+  mxtrain/mlmd.py);
 * C48 profiles / KFAM -> ``GET /api/profiles``;
 * C22-C26 node view (Karpenter / device plugins) -> ``GET /api/node`` (GPUs, ledger,
   node profile, sysfs power/clock samples);
@@ -565,6 +567,12 @@ def route(path: str, q: Dict[str, str], method: str = "GET", body: bytes = b"", 
         if k == "runs" and len(rest) == 2:
             from ..pipeline import get_run
             return 200, js, json.dumps(get_run(rest[1]), default=str)
+        if k == "runs" and len(rest) == 3 and rest[2] == "lineage":
+            from ..mlmd import run_lineage
+            return 200, js, json.dumps(run_lineage(rest[1]), default=str)
+        if k == "artifacts" and len(rest) == 3 and rest[2] == "lineage":
+            from ..mlmd import artifact_lineage
+            return 200, js, json.dumps(artifact_lineage(int(rest[1])), default=str)
         if k == "profiles":
             return 200, js, json.dumps(profiles(), default=str)
         if k == "node":

@@ -227,6 +227,10 @@ def run_pipeline(chart_configs: List[Dict], log=print, run_name: Optional[str] =
         os.replace(tmp, os.path.join(runs_dir(), run_name + ".json"))
 
     _save()
+    # run metadata / lineage (MLMD, mxtrain/mlmd.py): contexts, one execution per step,
+    # input and output artifacts -- best-effort, never fails the run
+    from .mlmd import RunRecorder
+    md = RunRecorder(run_name, pipeline, log)
     result = "Success"
     for cfg in chart_configs:
         if cancel is not None and cancel.is_set():
@@ -235,11 +239,14 @@ def run_pipeline(chart_configs: List[Dict], log=print, run_name: Optional[str] =
         t0 = time.time()
         use_cache = bool(cfg.get("cache", cache))
         try:
+            chart_dir = resolve_chart(cfg)
             key = step_cache_key(cfg)
         except (FileNotFoundError, ValueError):
-            key = None
+            chart_dir = key = None
         step = {"release": cfg.get("release_name"), "namespace": cfg.get("namespace"),
                 "chart": cfg.get("chart") or cfg.get("path"), "cache_key": key, "cached": False}
+        eid = md.step_started(cfg, chart_dir, key)
+        step["execution_id"] = eid
         hit = cache_lookup(key, cfg.get("max_cache_staleness")) if (use_cache and key) else None
         if hit is not None:
             log(f"Step {cfg.get('release_name')}: cached (execution of run {hit.get('run')})")
@@ -250,6 +257,8 @@ def run_pipeline(chart_configs: List[Dict], log=print, run_name: Optional[str] =
             if rc == 0 and key:
                 cache_store(key, run_name, cfg, round(time.time() - t0, 2))
         step.update(exit_code=rc, seconds=round(time.time() - t0, 2))
+        md.step_finished(eid, cfg, rc, step["seconds"], cached_from=step.get("cached_from"), cache_key=key,
+                         canceled=cancel is not None and cancel.is_set())
         rec["steps"].append(step)
         _save()
         if rc > 0:

@@ -445,6 +445,47 @@ def test_pipeline_step_cache(home):
     assert rec["cache"] and rec["steps"][0]["cached"]
 
 
+def test_pipeline_run_metadata_lineage(home):
+    """KFP metadata store (MLMD, C46; mxtrain/mlmd.py): a run records a run context under its
+    pipeline context, one execution per step with its Chart / ChartValues inputs and a
+    ReleaseRecord output; a cached step is a CACHED execution pointing at (and outputting)
+    what the producing execution wrote; a failed step is FAILED; artifact lineage walks back
+    from an output to the producing execution and its inputs; served over the API."""
+    from mxtrain import mlmd
+    from mxtrain import pipeline as pl
+    from mxtrain.mlplatform import dashboard as db
+    dp = "charts/machine-learning/data-prep/data-process"
+    step = {"release_name": "m-a", "namespace": "default", "path": dp,
+            "values": {"process": {"command": ["echo"], "args": ["ok"]}}}
+    bad = {"release_name": "m-b", "namespace": "default", "path": dp,
+           "values": {"process": {"command": ["false"]}}}
+    assert pl.run_pipeline([step], run_name="m1", pipeline="pm", cache=True) == "Success"
+    assert pl.run_pipeline([step, bad], run_name="m2", pipeline="pm", cache=True) == "Failure"
+    l1, l2 = mlmd.run_lineage("m1"), mlmd.run_lineage("m2")
+    assert l1["run"]["parents"] == [{"type": "pipeline", "name": "pm"}]
+    (e1,) = l1["executions"]
+    assert e1["state"] == "COMPLETE" and e1["properties"]["exit_code"] == 0
+    assert sorted(a["type"] for a in e1["inputs"]) == ["Chart", "ChartValues"]
+    (out1,) = e1["outputs"]
+    assert out1["type"] == "ReleaseRecord"
+    c, f = l2["executions"]
+    assert c["state"] == "CACHED" and c["properties"]["cached_from_run"] == "m1"
+    assert c["properties"]["cached_from_execution"] == e1["id"]
+    assert [a["id"] for a in c["outputs"]] == [out1["id"]]          # the reused output
+    # identical inputs are shared artifacts
+    assert sorted(a["id"] for a in c["inputs"]) == sorted(a["id"] for a in e1["inputs"])
+    assert f["state"] == "FAILED" and f["properties"]["exit_code"] != 0
+    assert pl.get_run("m2")["steps"][0]["execution_id"] == c["id"]
+    lin = mlmd.artifact_lineage(out1["id"])
+    assert lin["produced_by"] == [e1["id"], c["id"]]                # the producer and the cache hit
+    assert lin["upstream"][0]["id"] == e1["id"] and len(lin["upstream"][0]["inputs"]) == 2
+    code, _, body = db.route("/api/runs/m2/lineage", {})
+    assert code == 200 and [e["state"] for e in json.loads(body)["executions"]] == ["CACHED", "FAILED"]
+    code, _, body = db.route(f"/api/artifacts/{out1['id']}/lineage", {})
+    assert code == 200 and json.loads(body)["artifact"]["type"] == "ReleaseRecord"
+    assert db.route("/api/runs/nope/lineage", {})[0] == 404
+
+
 def test_cron_expressions():
     import datetime as dt
     from mxtrain.pipeline import Cron
