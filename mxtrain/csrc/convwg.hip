@@ -225,6 +225,8 @@ struct ConvFw {
   int KW, taps, stride, pad, dil;
   int Cin, tiles_n, nk, cib;
   float invOW, invOH;
+  int splits, Cout;      // split-K (few output tiles): fp32 partials [splits][T][Cout] in part,
+  float* part;           // then conv_fwd_reduce_kernel applies the epilogue
 };
 
 // FN = 4: 128 x 128 tiles (Cout % 128 == 0); FN = 2: 128 x 64 tiles for Cout % 128 == 64 (the
@@ -240,9 +242,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
   __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = wg / cp.tiles_n, tn = wg - tm * cp.tiles_n;
+  // split-K: the splits of one tile are adjacent (same XCD: they share its operand rows)
+  const int sidx = wg % cp.splits, tile = wg / cp.splits;
+  const int tm = tile / cp.tiles_n, tn = tile - tm * cp.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = cp.nk;
+  const int kb = (int)((int64_t)sidx * cp.nk / cp.splits);
+  const int nk = (int)((int64_t)(sidx + 1) * cp.nk / cp.splits) - kb;   // this split's K-steps
   const size_t ldw = (size_t)cp.taps * cp.Cin;
 
   int an[PA], aoh[PA], aow[PA], ach[PA];
@@ -285,7 +290,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
     for (int u = 0; u < FN; ++u) acc[a][u] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const uint32_t lds0 = lds_addr(smem);
-  auto issue = [&](int slot, int it) __attribute__((always_inline)) {
+  auto issue = [&](int slot, int li) __attribute__((always_inline)) {
+    const int it = kb + li;
     const int tap = it / cp.cib, ci0 = (it - tap * cp.cib) * BKT;
     const uint32_t b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
     const uint32_t b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
@@ -336,6 +342,18 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
   // consecutive channels: 16-B stores and 16-B residual loads (2-B scattered stores made
   // the epilogue store-issue bound)
   const int colw = n0 + 16 * FN * wn;
+  if (cp.splits > 1) {   // split-K: raw fp32 partial sums, the epilogue runs in the reduction
+#pragma unroll
+    for (int a = 0; a < FM; ++a) {
+      const int p = m0 + 16 * (FM * wm + a) + i;
+      if (p < cp.T) {
+        float* dst = cp.part + ((size_t)sidx * cp.T + p) * cp.Cout + colw + 4 * G;
+#pragma unroll
+        for (int u = 0; u < FN; ++u) *reinterpret_cast<f32x4*>(dst + 16 * u) = acc[a][u];
+      }
+    }
+    return;
+  }
   float bv[FN][4];
 #pragma unroll
   for (int u = 0; u < FN; ++u) {
@@ -386,6 +404,48 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
       if (p < cp.T)
         *reinterpret_cast<uint4*>(cp.y + pr + colw + 32 * up + 8 * G) = make_uint4(c[0][0], c[0][1], c[1][0], c[1][1]);
     }
+  }
+}
+
+// split-K forward: y[p][c] = act(sum_s part[s][p][c] + b[c] (+ res)), splits summed in order
+// (deterministic); one thread per 8 channels of a pixel
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(256) void conv_fwd_reduce_kernel(const ConvFw cp) {
+  const int c8 = cp.Cout / 8;
+  const int64_t nvec = (int64_t)cp.T * c8;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const int p = (int)(v / c8), c = (int)(v - (int64_t)p * c8) * 8;
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int s2 = 0; s2 < cp.splits; ++s2) {
+      const float4* q = reinterpret_cast<const float4*>(cp.part + ((size_t)s2 * cp.T + p) * cp.Cout + c);
+      const float4 x0 = q[0], x1 = q[1];
+      o[0] += x0.x; o[1] += x0.y; o[2] += x0.z; o[3] += x0.w;
+      o[4] += x1.x; o[5] += x1.y; o[6] += x1.z; o[7] += x1.w;
+    }
+    if (cp.bias) {
+      float b[8];
+      unpack8(*reinterpret_cast<const uint4*>(cp.bias + c), b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += b[j];
+    }
+    if (RES) {
+      size_t rr = (size_t)p * cp.ldy;
+      if (cp.res_up) {
+        int q2, ow, n, oh;
+        divmod(p, cp.OW, cp.invOW, q2, ow);
+        divmod(q2, cp.OH, cp.invOH, n, oh);
+        rr = ((size_t)(n * (cp.OH >> 1) + (oh >> 1)) * (cp.OW >> 1) + (ow >> 1)) * cp.ldy;
+      }
+      float r[8];
+      unpack8(*reinterpret_cast<const uint4*>(cp.res + rr + c), r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += r[j];
+    }
+    if (RELU) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = fmaxf(o[j], 0.f);
+    }
+    *reinterpret_cast<uint4*>(cp.y + (size_t)p * cp.ldy + c) = pack8(o);
   }
 }
 
@@ -732,7 +792,7 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
 }
 
 // d (int64[24]): {x, w, zero, y, bias, res, ldx, ldy, N, OH, OW, IH, IW, KH, KW, stride, pad,
-// dil, Cout, Cin, relu, res_up}: y = act(conv2d(x, w) + bias (+ res, or with res_up the 2x
+// dil, Cout, Cin, relu, res_up, splits, part}: y = act(conv2d(x, w) + bias (+ res, or with res_up the 2x
 // nearest upsampling of res)) in NHWC bf16, weight [Cout][KH][KW][Cin] (channels_last).
 // Cout a multiple of 64 (128 x 64 tiles when not of 128), Cin of 64; res_up needs even OH, OW.
 MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
@@ -759,6 +819,9 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   cp.Cin = (int)d[19];
   const bool relu = d[20] != 0;
   cp.res_up = cp.res && d[21] != 0;
+  cp.splits = d[22] > 1 ? (int)d[22] : 1;
+  cp.part = reinterpret_cast<float*>(d[23]);
+  cp.Cout = (int)d[18];
   const int64_t T = N * cp.OH * cp.OW;
   if (cp.res_up && ((cp.OH | cp.OW) & 1)) return (int)hipErrorInvalidValue;
   if (N <= 0 || cp.IH <= 0 || cp.IW <= 0 || cp.OH <= 0 || cp.OW <= 0 || KH <= 0 || cp.KW <= 0 || cp.stride <= 0 ||
@@ -774,7 +837,9 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   cp.tiles_n = Cout % 128 == 0 ? Cout / 128 : Cout / 64;
   cp.invOW = 1.f / (float)cp.OW;
   cp.invOH = 1.f / (float)cp.OH;
-  const dim3 grid((unsigned)((T + 127) / 128) * cp.tiles_n), block(256);
+  if (cp.splits > cp.nk) cp.splits = cp.nk;
+  if (cp.splits > 1 && (!cp.part || (d[23] & 15))) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)((T + 127) / 128) * cp.tiles_n * cp.splits), block(256);
   hipStream_t st = (hipStream_t)stream;
 #define MX_CF(NS, FN)                                                                         \
   if (cp.res) {                                                                               \
@@ -788,5 +853,16 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   // measured 40 % slower on the Mask R-CNN shapes (profiles/r4_s2/conv_ring_depth_ab_4img.txt)
   if (Cout % 128 == 0) { MX_CF(2, 4) } else { MX_CF(2, 2) }
 #undef MX_CF
+  if (cp.splits > 1) {
+    const int64_t nvec = T * (Cout / 8);
+    const unsigned rg = (unsigned)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
+    if (cp.res) {
+      if (relu) hipLaunchKernelGGL((conv_fwd_reduce_kernel<true, true>), dim3(rg), block, 0, st, cp);
+      else hipLaunchKernelGGL((conv_fwd_reduce_kernel<true, false>), dim3(rg), block, 0, st, cp);
+    } else {
+      if (relu) hipLaunchKernelGGL((conv_fwd_reduce_kernel<false, true>), dim3(rg), block, 0, st, cp);
+      else hipLaunchKernelGGL((conv_fwd_reduce_kernel<false, false>), dim3(rg), block, 0, st, cp);
+    }
+  }
   return (int)hipGetLastError();
 }

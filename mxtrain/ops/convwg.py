@@ -157,8 +157,22 @@ def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, paddi
                                      and tuple(residual.shape) == rshape
                                      and residual.data_ptr() % 16 == 0):   # 16-B residual loads
         return False
-    # 128 x 128 tiles, or 128 x 64 when Cout is an odd multiple of 64 (csrc/convwg.hip)
-    return (N * OH * OW + 127) // 128 * (w.shape[0] // (128 if w.shape[0] % 128 == 0 else 64)) >= FWD_MIN_TILES
+    # 128 x 128 tiles, or 128 x 64 when Cout is an odd multiple of 64 (csrc/convwg.hip); fewer
+    # than FWD_MIN_TILES tiles split the reduction (fwd_splits)
+    tiles = (N * OH * OW + 127) // 128 * (w.shape[0] // (128 if w.shape[0] % 128 == 0 else 64))
+    return tiles >= FWD_MIN_TILES or fwd_splits(tiles, w.shape[2] * w.shape[3] * w.shape[1] // 64) > 1
+
+
+FWD_SPLIT_WGS = 256
+
+
+def fwd_splits(tiles: int, nk: int) -> int:
+    """Split-K of the forward for convolutions with few output tiles (res5 / P5 at one image:
+    9-36 tiles on 256 CUs): about FWD_SPLIT_WGS workgroups, each split >= 4 K-steps of 64;
+    the fp32 partials are summed in order by the reduction kernel, which applies the epilogue."""
+    if tiles >= FWD_MIN_TILES:
+        return 1
+    return max(1, min(FWD_SPLIT_WGS // max(tiles, 1), nk // 4))
 
 
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool = False, stride=1, padding=0,
@@ -173,11 +187,13 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool
     if not _cl(w):
         w = w.contiguous(memory_format=torch.channels_last)
     y = torch.empty((N, OH, OW, Cout), dtype=torch.bfloat16, device=x.device).permute(0, 3, 1, 2)
-    _, zero = _workspace(x.device, 1)
+    T = N * OH * OW
+    splits = fwd_splits((T + 127) // 128 * (Cout // (128 if Cout % 128 == 0 else 64)), KH * KW * Cin // 64)
+    slab, zero = _workspace(x.device, splits * T * Cout if splits > 1 else 1)
     d = _DESC_T()
-    d[:22] = [x.data_ptr(), w.data_ptr(), zero.data_ptr(), y.data_ptr(), _lib.ptr(b) or 0,
+    d[:24] = [x.data_ptr(), w.data_ptr(), zero.data_ptr(), y.data_ptr(), _lib.ptr(b) or 0,
               _lib.ptr(residual) or 0, Cin, Cout, N, OH, OW, IH, IW, KH, KW, st, pd, dl, Cout, Cin, int(relu),
-              int(res_up)]
+              int(res_up), splits, slab.data_ptr() if splits > 1 else 0]
     _lib.call("mx_conv_fwd", d, _lib.stream())
     return y
 

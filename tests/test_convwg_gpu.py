@@ -114,7 +114,10 @@ def test_conv_dgrad_matches_fp32(case):
                                   (1, 256, 128, 50, 60, 1, 2, 0, 1), (1, 128, 256, 30, 33, 3, 1, 2, 2),
                                   # 128 x 64 tiles (Cout an odd multiple of 64: res2)
                                   (2, 64, 64, 50, 62, 3, 1, 1, 1), (1, 256, 64, 41, 37, 1, 1, 0, 1),
-                                  (1, 128, 192, 30, 33, 1, 1, 0, 1)])
+                                  (1, 128, 192, 30, 33, 1, 1, 0, 1),
+                                  # split-K (few tiles: res5 / P5 at one image)
+                                  (1, 512, 512, 25, 42, 3, 1, 1, 1), (1, 1024, 512, 50, 84, 1, 2, 0, 1),
+                                  (1, 256, 256, 25, 42, 3, 1, 1, 1)])
 @pytest.mark.parametrize("res", [False, True])
 def test_conv_fwd_fused_epilogue_matches_fp32(case, res):
     from mxtrain.ops import convwg
@@ -243,8 +246,8 @@ def test_bottleneck_backward_fusion_matches_unfused(monkeypatch):
         _close(a, b.cpu())
 
 
-@pytest.mark.parametrize("cin", [256, 512])
-def test_conv_bias_act_upsampled_residual_matches_fp32(cin):
+@pytest.mark.parametrize("cin,hw", [(256, (50, 84)), (512, (50, 84)), (2048, (26, 42))])
+def test_conv_bias_act_upsampled_residual_matches_fp32(cin, hw):
     """FPN top-down join in the conv epilogue (ops/epilogue.py conv_bias_act res_up):
     conv1x1(x) + b + up2(r) against fp32 F.conv2d + F.interpolate, values and the input,
     weight, bias and residual gradients (the residual's = 2 x 2 block sums)."""
@@ -253,11 +256,12 @@ def test_conv_bias_act_upsampled_residual_matches_fp32(cin):
     from mxtrain.ops.epilogue import conv_bias_act
     g = torch.Generator().manual_seed(cin)
     cl = torch.channels_last
-    x = torch.randn(2, cin, 50, 84, generator=g).to(torch.bfloat16)
+    H, W = hw      # (26, 42) at 2048 input channels: 18 tiles -> the split-K forward
+    x = torch.randn(2 if H > 30 else 1, cin, H, W, generator=g).to(torch.bfloat16)
     w = (torch.randn(256, cin, 1, 1, generator=g) * 0.05).to(torch.bfloat16)
     b = torch.randn(256, generator=g).to(torch.bfloat16)
-    r = torch.randn(2, 256, 25, 42, generator=g).to(torch.bfloat16)
-    gy = torch.randn(2, 256, 50, 84, generator=g)
+    r = torch.randn(x.shape[0], 256, H // 2, W // 2, generator=g).to(torch.bfloat16)
+    gy = torch.randn(x.shape[0], 256, H, W, generator=g)
     assert convwg.fwd_supported(x.cuda().contiguous(memory_format=cl), w.cuda().contiguous(memory_format=cl),
                                 b.cuda(), r.cuda().contiguous(memory_format=cl), res_up=True)
     xs = [t.cuda().contiguous(memory_format=cl).requires_grad_() if t.dim() == 4 else t.cuda().requires_grad_()
