@@ -471,6 +471,8 @@ struct ConvDg {
   int KW, taps, stride, pad, dil;
   int Cin, tiles_n, nk, cob;
   float invIW, invIH;
+  int splits;            // split-K (few input-pixel tiles): fp32 partials [splits][T][Cin] in
+  float* part;           // part, reduced with the add / mask epilogue by conv_dgrad_reduce_kernel
 };
 
 template <int NSLOT>
@@ -483,10 +485,13 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
   __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  // Cin tiles of one pixel block adjacent (same XCD): they share the gathered dY rows in L2
-  const int tm = wg / cp.tiles_n, tn = wg - tm * cp.tiles_n;
+  // Cin tiles of one pixel block adjacent (same XCD): they share the gathered dY rows in L2;
+  // the splits of one tile adjacent too
+  const int sidx = wg % cp.splits, tile = wg / cp.splits;
+  const int tm = tile / cp.tiles_n, tn = tile - tm * cp.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = cp.nk;
+  const int kb = (int)((int64_t)sidx * cp.nk / cp.splits);
+  const int nk = (int)((int64_t)(sidx + 1) * cp.nk / cp.splits) - kb;
   const size_t ldw = (size_t)cp.taps * cp.Cin;
 
   // ---- A (gathered dY) rows of this lane: fixed input pixel per DMA piece
@@ -545,7 +550,8 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
     for (int u = 0; u < FN; ++u) acc[a][u] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const uint32_t lds0 = lds_addr(smem);
-  auto issue = [&](int slot, int it) __attribute__((always_inline)) {
+  auto issue = [&](int slot, int li) __attribute__((always_inline)) {
+    const int it = kb + li;
     const int tap = it / cp.cob, co0 = (it - tap * cp.cob) * BKT;
     const uint32_t b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
     const uint32_t b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
@@ -592,6 +598,18 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
   // ---- epilogue: lane (G, i) holds dX[m0 + 16 (FM wm + a) + i][n0 + 16 (FN wn + u) + 4 G + e],
   // re-dealt per subtile pair into 8 consecutive channels per lane (16-B stores)
   const int colw = n0 + 16 * FN * wn;
+  if (cp.splits > 1) {   // split-K: raw fp32 partials; add / mask / bf16 in the reduction
+#pragma unroll
+    for (int a = 0; a < FM; ++a) {
+      const int p = m0 + 16 * (FM * wm + a) + i;
+      if (p < cp.T) {
+        float* dst = cp.part + ((size_t)sidx * cp.T + p) * cp.Cin + colw + 4 * G;
+#pragma unroll
+        for (int u = 0; u < FN; ++u) *reinterpret_cast<f32x4*>(dst + 16 * u) = acc[a][u];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int a = 0; a < FM; ++a) {
     const int p = m0 + 16 * (FM * wm + a) + i;
@@ -745,6 +763,36 @@ MX_EXPORT int mx_conv_wgrad_splits(int64_t T, int splits) {
   return (steps + nk - 1) / nk;
 }
 
+// split-K input gradient: dX[p][c] = (sum_s part[s][p][c] (+ add)) * (mask > 0), splits in order
+__global__ __launch_bounds__(256) void conv_dgrad_reduce_kernel(const ConvDg cp) {
+  const int c8 = cp.Cin / 8;
+  const int64_t nvec = (int64_t)cp.T * c8;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const int p = (int)(v / c8), c = (int)(v - (int64_t)p * c8) * 8;
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int s2 = 0; s2 < cp.splits; ++s2) {
+      const float4* q = reinterpret_cast<const float4*>(cp.part + ((size_t)s2 * cp.T + p) * cp.Cin + c);
+      const float4 x0 = q[0], x1 = q[1];
+      o[0] += x0.x; o[1] += x0.y; o[2] += x0.z; o[3] += x0.w;
+      o[4] += x1.x; o[5] += x1.y; o[6] += x1.z; o[7] += x1.w;
+    }
+    const size_t off = (size_t)p * cp.ldx + c;
+    if (cp.add) {
+      float a[8];
+      unpack8(*reinterpret_cast<const uint4*>(cp.add + off), a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += a[j];
+    }
+    if (cp.mask) {
+      float m[8];
+      unpack8(*reinterpret_cast<const uint4*>(cp.mask + off), m);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = m[j] > 0.f ? o[j] : 0.f;
+    }
+    *reinterpret_cast<uint4*>(cp.dx + off) = pack8(o);
+  }
+}
+
 // d (int64[20]): {dy, w, zero, dx, add, mask, ldy, ldx, N, OH, OW, IH, IW, KH, KW, stride,
 // pad, dil, Cout, Cin}: dX of conv2d for the output gradient dY, weight [Cout][KH][KW][Cin]
 // (channels_last), then (optional, null to skip) + add[p][c] and * (mask[p][c] > 0): X's
@@ -787,7 +835,16 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   cp.invIW = 1.f / (float)cp.IW;
   cp.invIH = 1.f / (float)cp.IH;
   const int tiles_m = (int)((T + 127) / 128);
-  hipLaunchKernelGGL(conv_dgrad_kernel<2>, dim3(tiles_m * cp.tiles_n), dim3(256), 0, (hipStream_t)stream, cp);
+  cp.splits = d[20] > 1 ? (int)(d[20] < cp.nk ? d[20] : cp.nk) : 1;
+  cp.part = reinterpret_cast<float*>(d[21]);
+  if (cp.splits > 1 && (!cp.part || (d[21] & 15))) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(conv_dgrad_kernel<2>, dim3(tiles_m * cp.tiles_n * cp.splits), dim3(256), 0,
+                     (hipStream_t)stream, cp);
+  if (cp.splits > 1) {
+    const int64_t nvec = T * (cp.Cin / 8);
+    const unsigned rg = (unsigned)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
+    hipLaunchKernelGGL(conv_dgrad_reduce_kernel, dim3(rg), dim3(256), 0, (hipStream_t)stream, cp);
+  }
   return (int)hipGetLastError();
 }
 

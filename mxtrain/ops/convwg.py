@@ -119,18 +119,30 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride, padding, dila
     if not _cl(w):
         w = w.contiguous(memory_format=torch.channels_last)
     dx = torch.empty((N, IH, IW, Cin), dtype=torch.bfloat16, device=dy.device).permute(0, 3, 1, 2)
-    _, zero = _workspace(dy.device, 1)
+    T = N * IH * IW
+    splits = dgrad_splits((T + 127) // 128 * (Cin // 128), KH * KW * Cout // 64)
+    slab, zero = _workspace(dy.device, splits * T * Cin if splits > 1 else 1)
     for t in (add, mask):
         assert t is None or (_cl(t) and tuple(t.shape) == (N, Cin, IH, IW) and t.dtype == torch.bfloat16
                              and t.data_ptr() % 16 == 0), "dgrad add / mask: X's channels_last shape"
     d = _DESC_T()
-    d[:20] = [dy.data_ptr(), w.data_ptr(), zero.data_ptr(), dx.data_ptr(), _lib.ptr(add) or 0, _lib.ptr(mask) or 0,
-            Cout, Cin, N, OH, OW, IH, IW, KH, KW, _sym(stride), _sym(padding), _sym(dilation), Cout, Cin]
+    d[:22] = [dy.data_ptr(), w.data_ptr(), zero.data_ptr(), dx.data_ptr(), _lib.ptr(add) or 0, _lib.ptr(mask) or 0,
+              Cout, Cin, N, OH, OW, IH, IW, KH, KW, _sym(stride), _sym(padding), _sym(dilation), Cout, Cin,
+              splits, slab.data_ptr() if splits > 1 else 0]
     _lib.call("mx_conv_dgrad", d, _lib.stream())
     return dx
 
 
 DGRAD_MIN_TILES = 64
+
+
+def dgrad_splits(tiles: int, nk: int) -> int:
+    """Split-K of the input gradient below DGRAD_MIN_TILES output tiles (res5 at one image:
+    36 tiles, 72 K-steps): as fwd_splits -- about FWD_SPLIT_WGS workgroups, >= 4 K-steps
+    each, fp32 partials summed in order with the add / mask epilogue applied after."""
+    if tiles >= DGRAD_MIN_TILES:
+        return 1
+    return max(1, min(FWD_SPLIT_WGS // max(tiles, 1), nk // 4))
 
 
 def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, padding=0, dilation=1,
@@ -201,14 +213,17 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool
 def dgrad_supported(w: torch.Tensor, x_shape, stride) -> bool:
     """The implicit-GEMM input gradient where it beat MIOpen's backward-data solvers at the
     Mask R-CNN shapes (profiles/r3_s4/conv_dgrad_vs_miopen_graphed.txt): at least
-    DGRAD_MIN_TILES 128 x 128 output tiles (fewer: long latency-bound K loops on a mostly
-    idle chip -- res5 3x3 65 vs 40 us), and stride 1 or at most 256 output channels (a
-    strided conv's gathered dY has 3 of 4 rows zero, which costs MFMA time per K-step)."""
+    DGRAD_MIN_TILES 128 x 128 output tiles, or fewer with the reduction split (dgrad_splits;
+    unsplit, a few tiles run long latency-bound K loops on a mostly idle chip -- res5 3x3
+    65 vs 40 us), and stride 1 or at most 256 output channels (a strided conv's gathered dY
+    has 3 of 4 rows zero, which costs MFMA time per K-step)."""
     if not (DGRAD and w.shape[0] % 64 == 0 and w.shape[1] % 128 == 0 and w.data_ptr() % 16 == 0):
         return False
     N, Cin, IH, IW = x_shape
     tiles = (N * IH * IW + 127) // 128 * (Cin // 128)
-    return tiles >= DGRAD_MIN_TILES and (_sym(stride) == 1 or w.shape[0] <= 256)
+    nk = w.shape[2] * w.shape[3] * w.shape[0] // 64
+    return ((tiles >= DGRAD_MIN_TILES or dgrad_splits(tiles, nk) > 1)
+            and (_sym(stride) == 1 or w.shape[0] <= 256))
 
 
 class ConvWgFn(torch.autograd.Function):

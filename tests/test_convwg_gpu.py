@@ -67,10 +67,10 @@ def test_conv_wgrad_accumulates_and_is_deterministic():
     _close(acc.float() - base.float(), _ref(dy, x, (Cout, Cin, k, k), stride, pad, dil))
 
 
-@pytest.mark.parametrize("hw", [(20, 24), (64, 64)])   # input gradient: MIOpen / implicit GEMM
+@pytest.mark.parametrize("hw", [(20, 24), (64, 64)])   # input gradient: split-K / plain implicit GEMM
 def test_conv_wg_autograd_matches_conv2d(hw):
-    """The autograd Function: output and input gradient are MIOpen's (as F.conv2d's, up to
-    the solver MIOpen picks per call), the weight gradient matches the fp32 reference."""
+    """The autograd Function: output as F.conv2d's (MIOpen), the input gradient as MIOpen's
+    to bf16 rounding, the weight gradient matches the fp32 reference."""
     from mxtrain.ops import convwg
     torch.manual_seed(0)
     cl = torch.channels_last
@@ -79,7 +79,9 @@ def test_conv_wg_autograd_matches_conv2d(hw):
     x1, w1 = x.clone().requires_grad_(), w.detach().clone(memory_format=cl).requires_grad_()
     x2, w2 = x.clone().requires_grad_(), w.detach().clone(memory_format=cl).requires_grad_()
     assert convwg.supported(x1, w1, 1, 1, 1)
-    assert convwg.dgrad_supported(w1, tuple(x.shape), 1) == (hw == (64, 64))
+    assert convwg.dgrad_supported(w1, tuple(x.shape), 1)
+    tiles = (2 * hw[0] * hw[1] + 127) // 128
+    assert (convwg.dgrad_splits(tiles, 9 * 256 // 64) > 1) == (hw == (20, 24))
     y1 = convwg.conv2d_wg(x1, w1, 1, 1, 1)
     y2 = torch.nn.functional.conv2d(x2, w2, None, 1, 1, 1)
     _close(y1.detach(), y2.detach().float().cpu())
@@ -97,7 +99,10 @@ def _ref_dx(dy, w, x_shape, stride, pad, dil):
                                                [True, False, False])[0]
 
 
-@pytest.mark.parametrize("case", CASES + [(1, 128, 64, 13, 9, 3, 1, 1, 1)])
+@pytest.mark.parametrize("case", CASES + [(1, 128, 64, 13, 9, 3, 1, 1, 1),
+                                  # split-K (few tiles: res5 at one image) and a plain one
+                                  (1, 512, 512, 25, 42, 3, 1, 1, 1), (1, 512, 2048, 25, 42, 1, 1, 0, 1),
+                                  (2, 256, 256, 40, 52, 3, 1, 1, 1)])
 def test_conv_dgrad_matches_fp32(case):
     from mxtrain.ops import convwg
     N, Cin, Cout, H, W, k, stride, pad, dil = case
@@ -177,10 +182,12 @@ def _fused_path_case(convwg, conv_bias_act):
         _close(got, ref)
 
 
-@pytest.mark.parametrize("case", [(1, 128, 64, 13, 9, 3, 1, 1, 1), (2, 256, 128, 25, 42, 1, 1, 0, 1)])
+@pytest.mark.parametrize("case", [(1, 128, 64, 13, 9, 3, 1, 1, 1), (2, 256, 128, 25, 42, 1, 1, 0, 1),
+                                  (1, 512, 512, 25, 42, 3, 1, 1, 1)])
 def test_conv_dgrad_add_and_relu_mask_epilogue(case):
     """dX + add, then * (mask > 0), in the dgrad store (the bottleneck's residual gradient and
-    the producer's ReLU) against the fp32 reference of the same three ops."""
+    the producer's ReLU) against the fp32 reference of the same three ops; split-K cases
+    (first and last) apply them in the ordered reduction, and repeat bitwise."""
     from mxtrain.ops import convwg
     N, Cin, Cout, H, W, k, stride, pad, dil = case
     x, dy = _inputs(*case, seed=17)
@@ -192,6 +199,7 @@ def test_conv_dgrad_add_and_relu_mask_epilogue(case):
     dx = convwg.conv_dgrad(dy, w, tuple(x.shape), stride, pad, dil, add=add, mask=mask)
     ref = (_ref_dx(dy, w, tuple(x.shape), stride, pad, dil) + add.float().cpu()) * (mask.float().cpu() > 0)
     _close(dx, ref)
+    assert torch.equal(dx, convwg.conv_dgrad(dy, w, tuple(x.shape), stride, pad, dil, add=add, mask=mask))
 
 
 def test_bottleneck_backward_fusion_matches_unfused(monkeypatch):
