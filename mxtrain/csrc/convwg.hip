@@ -231,13 +231,13 @@ struct ConvFw {
 
 // FN = 4: 128 x 128 tiles (Cout % 128 == 0); FN = 2: 128 x 64 tiles for Cout % 128 == 64 (the
 // 64-channel res2 convolutions, which otherwise went to MIOpen)
-template <int NSLOT, int FN, bool RES, bool RELU>
-__global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
-  constexpr int WN = 2, FM = 4, BKT = 64;
-  constexpr int BM = 128, BN = 16 * FN * WN, R = BKT * 2;
+template <int NSLOT, int FN, bool RES, bool RELU, int WM = 2>
+__global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv_fwd_kernel(const ConvFw cp) {
+  constexpr int WN = 2, FM = 4, BKT = 64, NW = WM * WN;
+  constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN, R = BKT * 2;
   static_assert(FN == 2 || FN == 4, "tile width");
   constexpr int IA = BM * R, IB = BN * R;
-  constexpr int PA = IA / 1024 / 4, PB = IB / 1024 / 4;
+  constexpr int PA = IA / 1024 / NW, PB = IB / 1024 / NW;
   constexpr int SLOT = IA + IB, PER = PA + PB;
   __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -473,7 +473,22 @@ struct ConvDg {
   float invIW, invIH;
   int splits;            // split-K (few input-pixel tiles): fp32 partials [splits][T][Cin] in
   float* part;           // part, reduced with the add / mask epilogue by conv_dgrad_reduce_kernel
+  int ldw;               // weight row pitch (elements per output channel: taps * Cin)
+  const uint16_t* bias;  // [Cin] or null: + bias (the transposed convolution's forward)
+  int relu;              // max(., 0) after bias / add, before the mask
+  // parity class (xs > 0): this launch's pixels are the dX pixels (i * xs + xa, j * xs + xb)
+  // of an XH x XW image, enumerated as an IH x IW grid (stride-decomposed dgrad, below)
+  int xs, xa, xb, XH, XW;
 };
+
+// dX row of the launch's pixel p (identity unless a parity-class launch)
+__device__ __forceinline__ int dx_row(const ConvDg& cp, int p) {
+  if (!cp.xs) return p;
+  int q, j, n, i;
+  divmod(p, cp.IW, cp.invIW, q, j);
+  divmod(q, cp.IH, cp.invIH, n, i);
+  return (n * cp.XH + i * cp.xs + cp.xa) * cp.XW + j * cp.xs + cp.xb;
+}
 
 template <int NSLOT>
 __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
@@ -492,7 +507,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
   const int m0 = tm * BM, n0 = tn * BN;
   const int kb = (int)((int64_t)sidx * cp.nk / cp.splits);
   const int nk = (int)((int64_t)(sidx + 1) * cp.nk / cp.splits) - kb;
-  const size_t ldw = (size_t)cp.taps * cp.Cin;
+  const size_t ldw = (size_t)cp.ldw;
 
   // ---- A (gathered dY) rows of this lane: fixed input pixel per DMA piece
   int an[PA], aih[PA], aiw[PA], ach[PA];
@@ -610,10 +625,15 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
     }
     return;
   }
+  float bz[FN][4];
+#pragma unroll
+  for (int u = 0; u < FN; ++u)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bz[u][e] = cp.bias ? bf2f(cp.bias[colw + 16 * u + 4 * G + e]) : 0.f;
 #pragma unroll
   for (int a = 0; a < FM; ++a) {
     const int p = m0 + 16 * (FM * wm + a) + i;
-    const size_t pr = (size_t)(p < cp.T ? p : cp.T - 1) * cp.ldx;
+    const size_t pr = (size_t)dx_row(cp, p < cp.T ? p : cp.T - 1) * cp.ldx;
 #pragma unroll
     for (int up = 0; up < FN / 2; ++up) {
       uint32_t c[2][2], ad[2][2], mk[2][2];
@@ -630,10 +650,15 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
 #pragma unroll
       for (int hlf = 0; hlf < 2; ++hlf) {
         const int u = 2 * up + hlf;
-        float v[4] = {acc[a][u][0], acc[a][u][1], acc[a][u][2], acc[a][u][3]};
+        float v[4] = {acc[a][u][0] + bz[u][0], acc[a][u][1] + bz[u][1], acc[a][u][2] + bz[u][2],
+                      acc[a][u][3] + bz[u][3]};
         if (cp.add) {
           v[0] += lo_bf(ad[hlf][0]); v[1] += hi_bf(ad[hlf][0]);
           v[2] += lo_bf(ad[hlf][1]); v[3] += hi_bf(ad[hlf][1]);
+        }
+        if (cp.relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
         }
         if (cp.mask) {
           v[0] = lo_bf(mk[hlf][0]) > 0.f ? v[0] : 0.f; v[1] = hi_bf(mk[hlf][0]) > 0.f ? v[1] : 0.f;
@@ -776,12 +801,20 @@ __global__ __launch_bounds__(256) void conv_dgrad_reduce_kernel(const ConvDg cp)
       o[0] += x0.x; o[1] += x0.y; o[2] += x0.z; o[3] += x0.w;
       o[4] += x1.x; o[5] += x1.y; o[6] += x1.z; o[7] += x1.w;
     }
-    const size_t off = (size_t)p * cp.ldx + c;
+    const size_t off = (size_t)dx_row(cp, p) * cp.ldx + c;
+    if (cp.bias) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += bf2f(cp.bias[c + j]);
+    }
     if (cp.add) {
       float a[8];
       unpack8(*reinterpret_cast<const uint4*>(cp.add + off), a);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] += a[j];
+    }
+    if (cp.relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = fmaxf(o[j], 0.f);
     }
     if (cp.mask) {
       float m[8];
@@ -793,11 +826,63 @@ __global__ __launch_bounds__(256) void conv_dgrad_reduce_kernel(const ConvDg cp)
   }
 }
 
-// d (int64[20]): {dy, w, zero, dx, add, mask, ldy, ldx, N, OH, OW, IH, IW, KH, KW, stride,
-// pad, dil, Cout, Cin}: dX of conv2d for the output gradient dY, weight [Cout][KH][KW][Cin]
-// (channels_last), then (optional, null to skip) + add[p][c] and * (mask[p][c] > 0): X's
-// second gradient (a residual branch) and X's own ReLU folded into the one store.  Cout a
-// multiple of 64, Cin of 128; 16-B aligned operands (add / mask share dX's layout).
+// Stride-decomposed dgrad, the pixels no tap reaches ((ih mod s, iw mod s) outside the
+// filter, e.g. 3 of 4 pixels of a 1x1 stride-2 conv): the epilogue applied to a zero sum.
+__global__ __launch_bounds__(256) void conv_dgrad_fill_kernel(const ConvDg cp, int KH) {
+  const int c8 = cp.Cin / 8;
+  const int64_t nvec = (int64_t)cp.T * c8;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const int p = (int)(v / c8), c = (int)(v - (int64_t)p * c8) * 8;
+    const int iw = p % cp.IW, ih = (p / cp.IW) % cp.IH;
+    if (ih % cp.stride < KH && iw % cp.stride < cp.KW) continue;
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const size_t off = (size_t)p * cp.ldx + c;
+    if (cp.bias) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = bf2f(cp.bias[c + j]);
+    }
+    if (cp.add) {
+      float a[8];
+      unpack8(*reinterpret_cast<const uint4*>(cp.add + off), a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += a[j];
+    }
+    if (cp.relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = fmaxf(o[j], 0.f);
+    }
+    if (cp.mask) {
+      float m[8];
+      unpack8(*reinterpret_cast<const uint4*>(cp.mask + off), m);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = m[j] > 0.f ? o[j] : 0.f;
+    }
+    *reinterpret_cast<uint4*>(cp.dx + off) = pack8(o);
+  }
+}
+
+static void launch_dgrad(ConvDg cp, int splits, hipStream_t st) {
+  cp.splits = splits < 1 ? 1 : (splits > cp.nk ? cp.nk : splits);
+  const int tiles_m = (cp.T + 127) / 128;
+  hipLaunchKernelGGL(conv_dgrad_kernel<2>, dim3(tiles_m * cp.tiles_n * cp.splits), dim3(256), 0, st, cp);
+  if (cp.splits > 1) {
+    const int64_t nvec = (int64_t)cp.T * (cp.Cin / 8);
+    const unsigned rg = (unsigned)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
+    hipLaunchKernelGGL(conv_dgrad_reduce_kernel, dim3(rg), dim3(256), 0, st, cp);
+  }
+}
+
+// d (int64[24]): {dy, w, zero, dx, add, mask, ldy, ldx, N, OH, OW, IH, IW, KH, KW, stride,
+// pad, dil, Cout, Cin, splits, part, bias, flags}: dX of conv2d for the output gradient dY,
+// weight [Cout][KH][KW][Cin] (channels_last), then (optional, null to skip) + bias[c] +
+// add[p][c], max(., 0) (flags bit 0) and * (mask[p][c] > 0): X's second gradient (a residual
+// branch) and X's own ReLU folded into the one store; bias + ReLU make it the forward of a
+// transposed convolution.  flags bit 1: stride-decomposed (stride s > 1, no padding or
+// dilation, filter <= s x s): one launch per parity class (ih mod s, iw mod s) = (a, b), whose
+// pixels all take the single tap (a, b) from dY[ih / s][iw / s] -- a plain GEMM over a
+// quarter of the pixels instead of the gathered K loop whose rows are 3 of 4 zero -- and one
+// fill of the pixels no tap reaches.  Cout a multiple of 64, Cin of 128; 16-B aligned
+// operands (add / mask share dX's layout); splits > 1 needs part (fp32, splits x pixels x Cin).
 MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   ConvDg cp{};
   cp.dy = reinterpret_cast<const uint16_t*>(d[0]);
@@ -829,23 +914,54 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   if ((d[0] | d[1] | d[2] | d[3] | d[4] | d[5]) & 15) return (int)hipErrorInvalidValue;
   cp.T = (int)T;
   cp.taps = KH * cp.KW;
+  cp.ldw = cp.taps * cp.Cin;
   cp.cob = Cout / 64;
   cp.nk = cp.taps * cp.cob;
   cp.tiles_n = cp.Cin / 128;
   cp.invIW = 1.f / (float)cp.IW;
   cp.invIH = 1.f / (float)cp.IH;
-  const int tiles_m = (int)((T + 127) / 128);
-  cp.splits = d[20] > 1 ? (int)(d[20] < cp.nk ? d[20] : cp.nk) : 1;
+  cp.bias = reinterpret_cast<const uint16_t*>(d[22]);
+  cp.relu = (int)(d[23] & 1);
+  const bool decomp = (d[23] >> 1) & 1;
+  const int splits = d[20] > 1 ? (int)d[20] : 1;
   cp.part = reinterpret_cast<float*>(d[21]);
-  if (cp.splits > 1 && (!cp.part || (d[21] & 15))) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(conv_dgrad_kernel<2>, dim3(tiles_m * cp.tiles_n * cp.splits), dim3(256), 0,
-                     (hipStream_t)stream, cp);
-  if (cp.splits > 1) {
+  if (splits > 1 && (!cp.part || (d[21] & 15))) return (int)hipErrorInvalidValue;
+  if (d[22] & 7) return (int)hipErrorInvalidValue;
+  const hipStream_t st = (hipStream_t)stream;
+  if (!decomp) {
+    launch_dgrad(cp, splits, st);
+    return (int)hipGetLastError();
+  }
+  const int s = cp.stride;
+  if (s < 2 || cp.pad || cp.dil != 1 || KH > s || cp.KW > s) return (int)hipErrorInvalidValue;
+  for (int a = 0; a < KH; ++a)
+    for (int b = 0; b < cp.KW; ++b) {
+      ConvDg c = cp;
+      c.xs = s; c.xa = a; c.xb = b; c.XH = cp.IH; c.XW = cp.IW;
+      c.IH = (cp.IH - a + s - 1) / s;
+      c.IW = (cp.IW - b + s - 1) / s;
+      c.T = (int)(N * c.IH * c.IW);
+      c.invIW = 1.f / (float)c.IW;
+      c.invIH = 1.f / (float)c.IH;
+      c.stride = 1; c.KW = 1; c.taps = 1; c.nk = cp.cob;
+      c.w = cp.w + (size_t)(a * cp.KW + b) * cp.Cin;   // tap (a, b); rows keep the pitch ldw
+      launch_dgrad(c, splits, st);
+    }
+  if (KH < s || cp.KW < s) {
     const int64_t nvec = T * (cp.Cin / 8);
-    const unsigned rg = (unsigned)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
-    hipLaunchKernelGGL(conv_dgrad_reduce_kernel, dim3(rg), dim3(256), 0, (hipStream_t)stream, cp);
+    const unsigned rg = (unsigned)((nvec + 255) / 256 < 16384 ? (nvec + 255) / 256 : 16384);
+    hipLaunchKernelGGL(conv_dgrad_fill_kernel, dim3(rg), dim3(256), 0, st, cp, KH);
   }
   return (int)hipGetLastError();
+}
+
+// Tile A/B switch (diagnostic, scripts/conv_wgrad_bench.py): 0 = 128 x 128 tiles, two
+// workgroups of 4 waves per CU; 1 / 2 = 256 x 128 tiles, one workgroup of 8 waves, 2 / 3 slots.
+static int g_fwd_variant = 0;
+MX_EXPORT int mx_conv_fwd_variant(int v) {
+  const int old = g_fwd_variant;
+  if (v >= 0 && v <= 2) g_fwd_variant = v;
+  return old;
 }
 
 // d (int64[24]): {x, w, zero, y, bias, res, ldx, ldy, N, OH, OW, IH, IW, KH, KW, stride, pad,
@@ -896,19 +1012,24 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   cp.invOH = 1.f / (float)cp.OH;
   if (cp.splits > cp.nk) cp.splits = cp.nk;
   if (cp.splits > 1 && (!cp.part || (d[23] & 15))) return (int)hipErrorInvalidValue;
-  const dim3 grid((unsigned)((T + 127) / 128) * cp.tiles_n * cp.splits), block(256);
   hipStream_t st = (hipStream_t)stream;
-#define MX_CF(NS, FN)                                                                         \
-  if (cp.res) {                                                                               \
-    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, true, true>), grid, block, 0, st, cp);   \
-    else hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, true, false>), grid, block, 0, st, cp);       \
-  } else {                                                                                    \
-    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, false, true>), grid, block, 0, st, cp);  \
-    else hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, false, false>), grid, block, 0, st, cp);      \
+  const int wide = g_fwd_variant != 0 && Cout % 128 == 0 && cp.splits == 1;   // 256 x 128 tiles
+  const dim3 grid((unsigned)((T + (wide ? 255 : 127)) / (wide ? 256 : 128)) * cp.tiles_n * cp.splits),
+      block(wide ? 512 : 256);
+#define MX_CF(NS, FN, WM)                                                                             \
+  if (cp.res) {                                                                                       \
+    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, true, true, WM>), grid, block, 0, st, cp);   \
+    else hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, true, false, WM>), grid, block, 0, st, cp);       \
+  } else {                                                                                            \
+    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, false, true, WM>), grid, block, 0, st, cp);  \
+    else hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, false, false, WM>), grid, block, 0, st, cp);      \
   }
   // ring depth 2 at two workgroups per CU: 3 / 4 slots (one workgroup per CU, counted waits)
   // measured 40 % slower on the Mask R-CNN shapes (profiles/r4_s2/conv_ring_depth_ab_4img.txt)
-  if (Cout % 128 == 0) { MX_CF(2, 4) } else { MX_CF(2, 2) }
+  if (wide == 1) { MX_CF(2, 4, 4) }
+  else if (wide) { MX_CF(3, 4, 4) }
+  else if (Cout % 128 == 0) { MX_CF(2, 4, 2) }
+  else { MX_CF(2, 2, 2) }
 #undef MX_CF
   if (cp.splits > 1) {
     const int64_t nvec = T * (Cout / 8);

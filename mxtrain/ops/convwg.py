@@ -105,12 +105,21 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dila
     return out
 
 
+def decomposed(KH: int, KW: int, stride, padding, dilation) -> bool:
+    """Stride-decomposed dgrad (csrc/convwg.hip mx_conv_dgrad flags bit 1): stride > 1, no
+    padding / dilation and a filter within s x s (1x1 stride 2, the 2x2 stride-2 transposed
+    convolution) -- every input pixel takes at most one tap."""
+    st, pd, dl = _sym(stride), _sym(padding), _sym(dilation)
+    return st is not None and st > 1 and pd == 0 and dl == 1 and KH <= st and KW <= st
+
+
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride, padding, dilation, add=None,
-               mask=None) -> torch.Tensor:
+               mask=None, bias=None, relu: bool = False) -> torch.Tensor:
     """dX [N, Cin, IH, IW] (channels_last bf16) of conv2d(x, w) for the output gradient
     ``dy``; ``w`` bf16 [Cout, Cin, KH, KW] (made channels_last if it is not).  In the same
-    store (optional): ``+ add`` (another gradient of X) and ``* (mask > 0)`` (X's ReLU; mask
-    = X itself when X is a ReLU output); both channels_last bf16 of X's shape."""
+    store (optional): ``+ bias`` ([Cin]), ``+ add`` (another gradient of X), ``relu`` and
+    ``* (mask > 0)`` (X's ReLU; mask = X itself when X is a ReLU output); add / mask
+    channels_last bf16 of X's shape.  With bias + relu this is conv_transpose2d's forward."""
     Cout, Cin, KH, KW = w.shape
     N, _, IH, IW = x_shape
     _, _, OH, OW = dy.shape
@@ -119,16 +128,20 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride, padding, dila
     if not _cl(w):
         w = w.contiguous(memory_format=torch.channels_last)
     dx = torch.empty((N, IH, IW, Cin), dtype=torch.bfloat16, device=dy.device).permute(0, 3, 1, 2)
-    T = N * IH * IW
-    splits = dgrad_splits((T + 127) // 128 * (Cin // 128), KH * KW * Cout // 64)
+    dec = decomposed(KH, KW, stride, padding, dilation)
+    st = _sym(stride)
+    T = N * (-(-IH // st)) * (-(-IW // st)) if dec else N * IH * IW   # largest launch's pixels
+    splits = dgrad_splits((T + 127) // 128 * (Cin // 128), (1 if dec else KH * KW) * Cout // 64)
     slab, zero = _workspace(dy.device, splits * T * Cin if splits > 1 else 1)
+    assert bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == Cin
+                            and bias.data_ptr() % 8 == 0)
     for t in (add, mask):
         assert t is None or (_cl(t) and tuple(t.shape) == (N, Cin, IH, IW) and t.dtype == torch.bfloat16
                              and t.data_ptr() % 16 == 0), "dgrad add / mask: X's channels_last shape"
     d = _DESC_T()
-    d[:22] = [dy.data_ptr(), w.data_ptr(), zero.data_ptr(), dx.data_ptr(), _lib.ptr(add) or 0, _lib.ptr(mask) or 0,
-              Cout, Cin, N, OH, OW, IH, IW, KH, KW, _sym(stride), _sym(padding), _sym(dilation), Cout, Cin,
-              splits, slab.data_ptr() if splits > 1 else 0]
+    d[:24] = [dy.data_ptr(), w.data_ptr(), zero.data_ptr(), dx.data_ptr(), _lib.ptr(add) or 0, _lib.ptr(mask) or 0,
+              Cout, Cin, N, OH, OW, IH, IW, KH, KW, st, _sym(padding), _sym(dilation), Cout, Cin,
+              splits, slab.data_ptr() if splits > 1 else 0, _lib.ptr(bias) or 0, int(relu) | (int(dec) << 1)]
     _lib.call("mx_conv_dgrad", d, _lib.stream())
     return dx
 
@@ -210,20 +223,27 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool
     return y
 
 
-def dgrad_supported(w: torch.Tensor, x_shape, stride) -> bool:
+def dgrad_supported(w: torch.Tensor, x_shape, stride, padding=0, dilation=1) -> bool:
     """The implicit-GEMM input gradient where it beat MIOpen's backward-data solvers at the
     Mask R-CNN shapes (profiles/r3_s4/conv_dgrad_vs_miopen_graphed.txt): at least
     DGRAD_MIN_TILES 128 x 128 output tiles, or fewer with the reduction split (dgrad_splits;
     unsplit, a few tiles run long latency-bound K loops on a mostly idle chip -- res5 3x3
-    65 vs 40 us), and stride 1 or at most 256 output channels (a strided conv's gathered dY
+    65 vs 40 us), and stride 1, a stride-decomposed filter (1x1 stride 2: one GEMM over the
+    pixels of one parity class) or at most 256 output channels (a strided 3x3's gathered dY
     has 3 of 4 rows zero, which costs MFMA time per K-step)."""
     if not (DGRAD and w.shape[0] % 64 == 0 and w.shape[1] % 128 == 0 and w.data_ptr() % 16 == 0):
         return False
     N, Cin, IH, IW = x_shape
+    st = _sym(stride)
+    if st is None or _sym(padding) is None or _sym(dilation) is None:
+        return False
+    if decomposed(w.shape[2], w.shape[3], stride, padding, dilation):
+        tiles = (N * (-(-IH // st)) * (-(-IW // st)) + 127) // 128 * (Cin // 128)
+        return tiles >= DGRAD_MIN_TILES or dgrad_splits(tiles, w.shape[0] // 64) > 1
     tiles = (N * IH * IW + 127) // 128 * (Cin // 128)
     nk = w.shape[2] * w.shape[3] * w.shape[0] // 64
     return ((tiles >= DGRAD_MIN_TILES or dgrad_splits(tiles, nk) > 1)
-            and (_sym(stride) == 1 or w.shape[0] <= 256))
+            and (st == 1 or w.shape[0] <= 256))
 
 
 class ConvWgFn(torch.autograd.Function):
@@ -243,7 +263,7 @@ class ConvWgFn(torch.autograd.Function):
             g = g.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            if dgrad_supported(w, tuple(x.shape), st):
+            if dgrad_supported(w, tuple(x.shape), st, pd, dl):
                 dx = conv_dgrad(g, w, tuple(x.shape), st, pd, dl)
             else:
                 dx = torch.ops.aten.convolution_backward(g, x, w, None, st, pd, dl, False, [0, 0], 1,

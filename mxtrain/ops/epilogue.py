@@ -147,7 +147,7 @@ class ConvBiasActFn(torch.autograd.Function):
         mask = x if ("mask_in" in roles or "mask_prev" in roles) else None
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            if convwg.dgrad_supported(w, tuple(x.shape), st) and (add is None or add.data_ptr() % 16 == 0):
+            if convwg.dgrad_supported(w, tuple(x.shape), st, pd, dl) and (add is None or add.data_ptr() % 16 == 0):
                 dx = convwg.conv_dgrad(dy, w, tuple(x.shape), st, pd, dl, add=add, mask=mask)
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, st, pd, dl, False, [0, 0], 1,
@@ -236,7 +236,64 @@ def conv_bias_act(x, w, b=None, stride=1, padding=0, dilation=1, relu: bool = Fa
     return F.relu(y, inplace=True) if relu else y
 
 
+class ConvTransposeBiasActFn(torch.autograd.Function):
+    """act(conv_transpose2d(x, w, stride=s) + b) for a filter within s x s (windows do not
+    overlap: the mask head's 2x2 stride-2 upsampling, tensorpack
+    examples/FasterRCNN/modeling/model_mrcnn.py maskrcnn_upXconv_head) on csrc/convwg.hip.
+    A transposed convolution is the input gradient of conv2d(., w): forward = the
+    stride-decomposed dgrad kernel (one GEMM per output parity class) with bias + ReLU in its
+    store; backward = the ReLU-mask + bias-gradient pass, then dX = conv2d(dy, w, stride s)
+    on the implicit-GEMM forward and dW = the implicit-GEMM weight gradient of that conv2d
+    with x and dy in each other's roles."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride: int, relu: bool):
+        N, _, H, W = x.shape
+        _, Co, KH, KW = w.shape
+        w = w.contiguous(memory_format=torch.channels_last)
+        y = convwg.conv_dgrad(x, w, (N, Co, (H - 1) * stride + KH, (W - 1) * stride + KW), stride, 0, 1,
+                              bias=b, relu=relu)
+        ctx.stride, ctx.relu = stride, relu
+        ctx.bdtype = b.dtype if b is not None else None
+        ctx.save_for_backward(x, w, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, out = ctx.saved_tensors
+        st = ctx.stride
+        dy, db = _bias_act_bwd(g, out, ctx.relu, ctx.needs_input_grad[2])
+        if db is not None and db.dtype != ctx.bdtype:
+            db = db.to(ctx.bdtype)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if convwg.fwd_supported(dy, w, None, None, st, 0, 1):
+                dx = convwg.conv_fwd(dy, w, None, None, False, st, 0, 1)
+            else:
+                dx = F.conv2d(dy, w, None, st)
+        if ctx.needs_input_grad[1]:
+            dw = convwg.conv_wgrad(x, dy, tuple(w.shape), st, 0, 1)
+        return dx, dw, db, None, None
+
+
+def _deconv_ok(x, w, b, stride) -> bool:
+    """ConvTransposeBiasActFn's conditions: NHWC bf16, non-overlapping windows, channel
+    counts the weight-gradient tiles take (multiples of 128), enough output tiles."""
+    if not (_ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and _nhwc(x)
+            and x.dim() == 4 and w.dim() == 4 and x.shape[1] == w.shape[0] and x.data_ptr() % 16 == 0
+            and isinstance(stride, int) and w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0
+            and (b is None or (b.dtype == torch.bfloat16 and b.is_contiguous() and b.data_ptr() % 8 == 0))
+            and convwg.decomposed(w.shape[2], w.shape[3], stride, 0, 1)):
+        return False
+    N, _, H, W = x.shape
+    out_shape = (N, w.shape[1], (H - 1) * stride + w.shape[2], (W - 1) * stride + w.shape[3])
+    return convwg.dgrad_supported(w, out_shape, stride, 0, 1)
+
+
 def conv_transpose_bias_act(x, w, b=None, stride=1, relu: bool = False) -> torch.Tensor:
+    """act(conv_transpose2d(x, w, stride) + b); ConvTransposeBiasActFn where it applies."""
+    if _deconv_ok(x, w, b, stride):
+        return ConvTransposeBiasActFn.apply(x, w, b, stride, relu)
     if _fused_ok(x, b, None):
         return bias_act(F.conv_transpose2d(x, w, None, stride=stride), b, None, relu)
     y = F.conv_transpose2d(x, w, b, stride=stride)

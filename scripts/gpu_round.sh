@@ -34,7 +34,7 @@ for s in $STEPS; do
       cd /tmp && export TMPDIR=/tmp
       timeout -k 10 ${T_PROF:-500} rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/${PROF_TAG:-mrprof}" -o run -- python3 "$GRAFT_REPO_ROOT/scripts/bench_maskrcnn.py" --steps ${MR_STEPS:-12} --warmup 6 ${MRCNN_ARGS:-} > "$GRAFT_REPO_ROOT/gpurun_out/${PROF_TAG:-mrprof}.log" 2>&1; rc=$?
       cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/${PROF_TAG:-mrprof}.log; echo "mrprof rc=$rc"; ok $rc || exit $rc
-      python3 scripts/step_census.py $(find gpurun_out/${PROF_TAG:-mrprof} -name "*.db" | head -1) --last $((${MR_STEPS:-12} - 4)) --top 90 > gpurun_out/${PROF_TAG:-mrprof}_census.txt 2>&1
+      python3 scripts/step_census.py $(find gpurun_out/${PROF_TAG:-mrprof} -name "*.db" | head -1) --last $((${MR_STEPS:-12} - 4)) --top 90 ${CENSUS_DETAIL:+--detail "$CENSUS_DETAIL"} > gpurun_out/${PROF_TAG:-mrprof}_census.txt 2>&1
       find gpurun_out/${PROF_TAG:-mrprof} -name "*.db" -delete ;;
     kbench)
       timeout -k 10 300 python scripts/kbench.py ${KBENCH_ARGS:-} > gpurun_out/kbench.log 2>&1; rc=$?

@@ -97,6 +97,16 @@ def main():
     print("\nselected kernels by launching op:")
     for (kn, name, where), n in sel.most_common(80):
         print(f"{n:5d}  {kn:60s} {name:24s} {where}")
+    # convolutions still on MIOpen, by operand shapes, with their kernels' device time
+    conv = collections.defaultdict(lambda: [0, 0.0])
+    for e in evs:
+        if e.device_type.name == "CPU" and "convolution" in e.name and getattr(e, "kernels", None):
+            c = conv[(e.name, str(e.input_shapes)[:120])]
+            c[0] += 1
+            c[1] += sum(getattr(k, "duration", 0.0) for k in e.kernels)
+    print("\nMIOpen convolution ops by operand shapes (calls, kernel us):")
+    for (name, sh), (n, us) in sorted(conv.items(), key=lambda kv: -kv[1][1]):
+        print(f"{n:4d} {us:9.1f}  {name:36s} {sh}")
 
 
 if __name__ == "__main__":

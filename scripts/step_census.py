@@ -2,7 +2,8 @@
 """Per-step kernel census of a rocprofv3 SQLite trace: steps are delimited by a kernel that
 runs exactly once per training step (default: the RPN NMS keep pass); the last N intervals
 are averaged, so one-time work (MIOpen search, capture, warm-up) is excluded.
-    python scripts/step_census.py DB [--marker nms_keep_kernel] [--last 10] [--top 80]"""
+    python scripts/step_census.py DB [--marker nms_keep_kernel] [--last 10] [--top 80]
+        [--detail REGEX]   (every call of the matching kernels in the last step, in order)"""
 import argparse
 import sqlite3
 from collections import defaultdict
@@ -15,6 +16,7 @@ def main():
     ap.add_argument("--last", type=int, default=10)
     ap.add_argument("--top", type=int, default=80)
     ap.add_argument("--sort", choices=("count", "time"), default="time")
+    ap.add_argument("--detail", default="")
     a = ap.parse_args()
     con = sqlite3.connect(a.db)
     cols = [r[1] for r in con.execute("PRAGMA table_info(kernels)")]
@@ -38,6 +40,17 @@ def main():
     key = (lambda kv: -kv[1][0]) if a.sort == "count" else (lambda kv: -kv[1][1])
     for k, (c, t) in sorted(agg.items(), key=key)[:a.top]:
         print(f"{c / steps:7.1f}x {t / steps:9.1f} us {100 * t / steps / busy:5.1f}%  {k}")
+    if a.detail:
+        import re
+        pat = re.compile(a.detail)
+        gcol = [c for c in cols if "grid" in c.lower()]
+        sel = ", ".join([nc, "start", "end"] + gcol)
+        t0 = marks[-2]
+        print(f"\n== calls matching {a.detail!r} in the last step (us, {', '.join(gcol)})")
+        for r in con.execute(f"select {sel} from kernels where start >= ? and start < ? order by start", (t0, t1)):
+            if pat.search(r[0]):
+                name = r[0].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:40]
+                print(f"  {(r[2] - r[1]) / 1000.0:8.1f}  {name:40s} {' '.join(str(g) for g in r[3:])}")
 
 
 if __name__ == "__main__":

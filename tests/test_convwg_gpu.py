@@ -313,3 +313,55 @@ def test_mask_head_conv_chain_fusion_matches_unfused():
     _close(out[True][1], out[False][1].cpu())
     for a, b in zip(out[True][2], out[False][2]):
         _close(a, b.cpu())
+
+
+@pytest.mark.parametrize("case", [(1, 1024, 512, 50, 84, 1, 2, 0, 1), (1, 1024, 2048, 49, 83, 1, 2, 0, 1),
+                                  (2, 512, 256, 40, 40, 1, 2, 0, 1), (1, 256, 256, 28, 30, 2, 2, 0, 1),
+                                  (1, 128, 256, 31, 29, 2, 2, 0, 1), (1, 512, 1024, 30, 34, 1, 2, 0, 1)])
+@pytest.mark.parametrize("epi", [False, True])
+def test_conv_dgrad_stride_decomposed_matches_fp32(case, epi):
+    """Stride-decomposed input gradient (1x1 / 2x2 filters at stride 2, odd and even image
+    sizes): one GEMM per parity class plus the fill of the pixels no tap reaches, with and
+    without the add / ReLU-mask epilogue, against the fp32 reference."""
+    from mxtrain.ops import convwg
+    N, Cin, Cout, H, W, k, stride, pad, dil = case
+    assert convwg.decomposed(k, k, stride, pad, dil)
+    x, dy = _inputs(*case, seed=23)
+    g = torch.Generator().manual_seed(29)
+    w = (torch.randn(Cout, k, k, Cin, generator=g) * 0.1).to(torch.bfloat16).cuda().permute(0, 3, 1, 2)
+    cl = torch.channels_last
+    add = mask = None
+    if epi:
+        add = torch.randn(x.shape, generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=cl)
+        mask = torch.randn(x.shape, generator=g).relu().to(torch.bfloat16).cuda().contiguous(memory_format=cl)
+    dx = convwg.conv_dgrad(dy, w, tuple(x.shape), stride, pad, dil, add=add, mask=mask)
+    ref = _ref_dx(dy, w, tuple(x.shape), stride, pad, dil)
+    if epi:
+        ref = (ref + add.float().cpu()) * (mask.float().cpu() > 0)
+    _close(dx, ref)
+
+
+def test_conv_transpose_bias_relu_matches_fp32():
+    """Mask-head upsampling (2x2 stride-2 transposed conv + bias + ReLU) on
+    ops/epilogue.py ConvTransposeBiasActFn: output and the input, weight and bias gradients
+    against fp32 F.conv_transpose2d (gradients through the bf16 output's ReLU mask)."""
+    import torch.nn.functional as F
+    from mxtrain.ops.epilogue import ConvTransposeBiasActFn, _deconv_ok, conv_transpose_bias_act
+    g = torch.Generator().manual_seed(31)
+    cl = torch.channels_last
+    x = torch.randn(48, 256, 14, 14, generator=g).to(torch.bfloat16)
+    w = (torch.randn(256, 256, 2, 2, generator=g) * 0.05).to(torch.bfloat16)
+    b = (torch.randn(256, generator=g) * 0.1).to(torch.bfloat16)
+    gy = torch.randn(48, 256, 28, 28, generator=g).to(torch.bfloat16)
+    xg = x.cuda().contiguous(memory_format=cl).requires_grad_()
+    wg, bg = w.cuda().requires_grad_(), b.cuda().requires_grad_()
+    assert _deconv_ok(xg, wg, bg, 2)
+    y = conv_transpose_bias_act(xg, wg, bg, stride=2, relu=True)
+    assert isinstance(y.grad_fn, ConvTransposeBiasActFn._backward_cls), y.grad_fn
+    y.backward(gy.cuda().contiguous(memory_format=cl))
+    xr, wr, br = (t.float().requires_grad_() for t in (x, w, b))
+    yr = F.relu(F.conv_transpose2d(xr, wr, br, stride=2))
+    _close(y.detach(), yr.detach())
+    (F.conv_transpose2d(xr, wr, br, stride=2) * (y.detach().float().cpu() > 0)).backward(gy.float())
+    for got, ref in ((xg.grad, xr.grad), (wg.grad, wr.grad), (bg.grad, br.grad)):
+        _close(got, ref)
