@@ -231,9 +231,11 @@ struct ConvFw {
 
 // FN = 4: 128 x 128 tiles (Cout % 128 == 0); FN = 2: 128 x 64 tiles for Cout % 128 == 64 (the
 // 64-channel res2 convolutions, which otherwise went to MIOpen)
-template <int NSLOT, int FN, bool RES, bool RELU, int WM = 2>
-__global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv_fwd_kernel(const ConvFw cp) {
-  constexpr int WN = 2, FM = 4, BKT = 64, NW = WM * WN;
+// (256 x 128 tiles, one workgroup of 8 waves per CU, measured 3-8 % slower on the Mask R-CNN
+// shapes: profiles/r4_s2/conv_fwd_tiles_4img.txt)
+template <int NSLOT, int FN, bool RES, bool RELU>
+__global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
+  constexpr int WM = 2, WN = 2, FM = 4, BKT = 64, NW = WM * WN;
   constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN, R = BKT * 2;
   static_assert(FN == 2 || FN == 4, "tile width");
   constexpr int IA = BM * R, IB = BN * R;
@@ -492,10 +494,10 @@ __device__ __forceinline__ int dx_row(const ConvDg& cp, int p) {
 
 template <int NSLOT>
 __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
-  constexpr int WN = 2, FM = 4, FN = 4, BKT = 64;
-  constexpr int BM = 128, BN = 128, RA = BKT * 2, RB = BN * 2;
+  constexpr int WM = 2, WN = 2, FM = 4, FN = 4, BKT = 64, NW = WM * WN;
+  constexpr int BM = 16 * FM * WM, BN = 128, RA = BKT * 2, RB = BN * 2;
   constexpr int IA = BM * RA, IB = BKT * RB;
-  constexpr int PA = IA / 1024 / 4, PB = IB / 1024 / 4;
+  constexpr int PA = IA / 1024 / NW, PB = IB / 1024 / NW;
   constexpr int SLOT = IA + IB, PER = PA + PB;
   __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -955,15 +957,6 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   return (int)hipGetLastError();
 }
 
-// Tile A/B switch (diagnostic, scripts/conv_wgrad_bench.py): 0 = 128 x 128 tiles, two
-// workgroups of 4 waves per CU; 1 / 2 = 256 x 128 tiles, one workgroup of 8 waves, 2 / 3 slots.
-static int g_fwd_variant = 0;
-MX_EXPORT int mx_conv_fwd_variant(int v) {
-  const int old = g_fwd_variant;
-  if (v >= 0 && v <= 2) g_fwd_variant = v;
-  return old;
-}
-
 // d (int64[24]): {x, w, zero, y, bias, res, ldx, ldy, N, OH, OW, IH, IW, KH, KW, stride, pad,
 // dil, Cout, Cin, relu, res_up, splits, part}: y = act(conv2d(x, w) + bias (+ res, or with res_up the 2x
 // nearest upsampling of res)) in NHWC bf16, weight [Cout][KH][KW][Cin] (channels_last).
@@ -1013,23 +1006,18 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   if (cp.splits > cp.nk) cp.splits = cp.nk;
   if (cp.splits > 1 && (!cp.part || (d[23] & 15))) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  const int wide = g_fwd_variant != 0 && Cout % 128 == 0 && cp.splits == 1;   // 256 x 128 tiles
-  const dim3 grid((unsigned)((T + (wide ? 255 : 127)) / (wide ? 256 : 128)) * cp.tiles_n * cp.splits),
-      block(wide ? 512 : 256);
-#define MX_CF(NS, FN, WM)                                                                             \
-  if (cp.res) {                                                                                       \
-    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, true, true, WM>), grid, block, 0, st, cp);   \
-    else hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, true, false, WM>), grid, block, 0, st, cp);       \
-  } else {                                                                                            \
-    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, false, true, WM>), grid, block, 0, st, cp);  \
-    else hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, false, false, WM>), grid, block, 0, st, cp);      \
+  const dim3 grid((unsigned)((T + 127) / 128) * cp.tiles_n * cp.splits), block(256);
+#define MX_CF(NS, FN)                                                                         \
+  if (cp.res) {                                                                               \
+    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, true, true>), grid, block, 0, st, cp);   \
+    else hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, true, false>), grid, block, 0, st, cp);       \
+  } else {                                                                                    \
+    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, false, true>), grid, block, 0, st, cp);  \
+    else hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, false, false>), grid, block, 0, st, cp);      \
   }
   // ring depth 2 at two workgroups per CU: 3 / 4 slots (one workgroup per CU, counted waits)
   // measured 40 % slower on the Mask R-CNN shapes (profiles/r4_s2/conv_ring_depth_ab_4img.txt)
-  if (wide == 1) { MX_CF(2, 4, 4) }
-  else if (wide) { MX_CF(3, 4, 4) }
-  else if (Cout % 128 == 0) { MX_CF(2, 4, 2) }
-  else { MX_CF(2, 2, 2) }
+  if (Cout % 128 == 0) { MX_CF(2, 4) } else { MX_CF(2, 2) }
 #undef MX_CF
   if (cp.splits > 1) {
     const int64_t nvec = T * (Cout / 8);

@@ -104,7 +104,6 @@ SIGNATURES = {
     "mx_conv_wgrad_splits": [I64, I],
     "mx_conv_dgrad": [P, P],
     "mx_conv_fwd": [P, P],
-    "mx_conv_fwd_variant": [I],
     # gemm_nt.hip
     "mx_gemm_nt_tile": [I, I],
     "mx_gemm_nt": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],

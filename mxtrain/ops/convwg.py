@@ -150,12 +150,9 @@ DGRAD_MIN_TILES = 64
 
 
 def dgrad_splits(tiles: int, nk: int) -> int:
-    """Split-K of the input gradient below DGRAD_MIN_TILES output tiles (res5 at one image:
-    36 tiles, 72 K-steps): as fwd_splits -- about FWD_SPLIT_WGS workgroups, >= 4 K-steps
-    each, fp32 partials summed in order with the add / mask epilogue applied after."""
-    if tiles >= DGRAD_MIN_TILES:
-        return 1
-    return max(1, min(FWD_SPLIT_WGS // max(tiles, 1), nk // 4))
+    """Split-K of the input gradient (k_splits), the fp32 partials summed in order with the
+    add / mask epilogue applied after."""
+    return k_splits(tiles, nk)
 
 
 def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, padding=0, dilation=1,
@@ -188,16 +185,32 @@ def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, paddi
     return tiles >= FWD_MIN_TILES or fwd_splits(tiles, w.shape[2] * w.shape[3] * w.shape[1] // 64) > 1
 
 
-FWD_SPLIT_WGS = 256
+# split-K below SPLIT_TILES output tiles (the chip holds 512 workgroups of the 128 x 128
+# kernels: 256 CUs x 2) when the reduction is long (>= SPLIT_MIN_NK K-steps of 64): about
+# SPLIT_WGS workgroups (rounded down: one more would start a second, mostly idle wave of
+# workgroups -- 132 tiles x 4 splits = 528 ran 50 us where x 3 ran 39), at most SPLIT_MAX
+# slices of >= 4 K-steps.  Short reductions lose
+# more to the fp32 partial traffic than they gain (res3 3x3 at one image: 18 K-steps, 132
+# tiles, 18.9 -> 26.9 us split in two); long ones on a part-empty chip gain (res5 3x3 at
+# four images: 72 K-steps, 132 tiles, 60 -> 39 us in three) -- profiles/r4_s2/conv_split_ab_*.txt
+SPLIT_TILES = 256
+SPLIT_WGS = 512
+SPLIT_MAX = 8
+SPLIT_MIN_NK = 32
+
+
+def k_splits(tiles: int, nk: int) -> int:
+    """Reduction slices of a conv forward / input gradient with ``tiles`` output tiles and
+    ``nk`` 64-deep K-steps (res5 / P5 at one image: 9-36 tiles; at four images 66-132): the
+    fp32 partials ([splits][pixels][channels]) are summed in order (deterministic) by the
+    reduction kernel, which applies the epilogue."""
+    if tiles >= SPLIT_TILES or nk < SPLIT_MIN_NK:
+        return 1
+    return max(1, min(SPLIT_WGS // max(tiles, 1), nk // 4, SPLIT_MAX))
 
 
 def fwd_splits(tiles: int, nk: int) -> int:
-    """Split-K of the forward for convolutions with few output tiles (res5 / P5 at one image:
-    9-36 tiles on 256 CUs): about FWD_SPLIT_WGS workgroups, each split >= 4 K-steps of 64;
-    the fp32 partials are summed in order by the reduction kernel, which applies the epilogue."""
-    if tiles >= FWD_MIN_TILES:
-        return 1
-    return max(1, min(FWD_SPLIT_WGS // max(tiles, 1), nk // 4))
+    return k_splits(tiles, nk)
 
 
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool = False, stride=1, padding=0,

@@ -7,9 +7,9 @@ from mxtrain.ops import convwg
 
 N = int(os.environ.get("IMGS", "1"))
 WGRAD_ONLY = os.environ.get("WGRAD_ONLY", "0") == "1"   # split sweeps: skip the dgrad / fwd columns
-# forward tile A/B (csrc/convwg.hip mx_conv_fwd_variant): e.g. FWD_VARIANTS="0 1 2" times only
-# the forward under each variant
-FWD_VARIANTS = [int(v) for v in os.environ.get("FWD_VARIANTS", "").split()]
+# split-K planning A/B (ops/convwg.py k_splits): SPLIT_AB="TILES:WGS:MAX[:MIN_NK] ..." times
+# the forward and the input gradient under each setting of SPLIT_TILES / WGS / MAX / MIN_NK
+SPLIT_AB = [tuple(int(t) for t in c.split(":")) for c in os.environ.get("SPLIT_AB", "").split()]
 # name, Cin, Cout, H_in, W_in, k, stride, pad, count per step
 SHAPES = [
     ("res3.conv1 s2", 256, 128, 200, 336, 1, 2, 0, 1),
@@ -67,31 +67,31 @@ def timeit(fn, it=10, reps=5):
 
 tot_m = tot_h = tot_dm = tot_dh = tot_fm = tot_fh = 0.0
 cl = torch.channels_last
-if FWD_VARIANTS:
-    from mxtrain.ops import _lib
-    tot = [0.0] * len(FWD_VARIANTS)
-    print(f"{'conv (fwd + bias + relu)':26s} {'N':>3s} " + " ".join(f"{'v%d us' % v:>9s} {'TF/s':>6s}" for v in FWD_VARIANTS)
-          + "  maxdiff vs first")
+if SPLIT_AB:
+    tot = [[0.0, 0.0] for _ in SPLIT_AB]
+    print(f"{'split-K A/B (fwd | dgrad us)':26s} {'N':>3s} " + " ".join(f"{':'.join(map(str, c)):>17s}" for c in SPLIT_AB))
     for name, Cin, Cout, H, W, k, s, p, cnt in SHAPES:
-        if name.startswith("rpn P") or name in ("res3.conv1 s2",):
+        if name.startswith("rpn P") or name in ("res3.conv1 s2", "res3.short s2", "fpn.lat2"):
             continue
         n = 64 * N if name.startswith("mask") else N
         x = torch.randn(n, Cin, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
         w = (torch.randn(Cout, Cin, k, k, device="cuda") * 0.05).to(torch.bfloat16).contiguous(memory_format=cl)
         bias = torch.randn(Cout, device="cuda").to(torch.bfloat16)
         OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-        fl = 2.0 * n * OH * OW * Cout * Cin * k * k
-        cols, outs = [], []
-        for i, v in enumerate(FWD_VARIANTS):
-            _lib._fn("mx_conv_fwd_variant")(v)
-            t = timeit(lambda: convwg.conv_fwd(x, w, bias, None, True, s, p, 1))
-            outs.append(convwg.conv_fwd(x, w, bias, None, True, s, p, 1).float())
-            tot[i] += cnt * t
-            cols.append(f"{t:9.1f} {fl / t / 1e6:6.0f}")
-        _lib._fn("mx_conv_fwd_variant")(0)
-        diff = max((o - outs[0]).abs().max().item() for o in outs)
-        print(f"{name:26s} {n:3d} " + " ".join(cols) + f"  {diff:.3g}", flush=True)
-    print("per step (counts): " + ", ".join(f"v{v} {t:.0f} us" for v, t in zip(FWD_VARIANTS, tot)))
+        dy = torch.randn(n, Cout, OH, OW, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+        dg_ok = convwg.dgrad_supported(w, tuple(x.shape), s, p, 1)
+        cols = []
+        for i, c in enumerate(SPLIT_AB):
+            convwg.SPLIT_TILES, convwg.SPLIT_WGS, convwg.SPLIT_MAX = c[:3]
+            convwg.SPLIT_MIN_NK = c[3] if len(c) > 3 else 0
+            tf = timeit(lambda: convwg.conv_fwd(x, w, bias, None, True, s, p, 1))
+            td = timeit(lambda: convwg.conv_dgrad(dy, w, tuple(x.shape), s, p, 1)) if dg_ok else 0.0
+            tot[i][0] += cnt * tf
+            tot[i][1] += cnt * td
+            cols.append(f"{tf:8.1f} {td:8.1f}")
+        print(f"{name:26s} {n:3d} " + " ".join(cols), flush=True)
+    print("per step (counts, fwd / dgrad): " + ", ".join(f"{':'.join(map(str, c))} {a:.0f} / {b:.0f} us"
+                                                        for c, (a, b) in zip(SPLIT_AB, tot)))
     sys.exit(0)
 print(f"{'conv':22s} {'N':>3s} {'MIOpen us':>10s} {'convwg us':>10s} {'TF/s mi':>8s} {'TF/s wg':>8s}  splits  maxrel"
       f"   | dgrad: MIOpen us  convdg us  maxrel   | fwd+bias: MIOpen us  convfw us  maxrel")

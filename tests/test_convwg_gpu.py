@@ -80,8 +80,6 @@ def test_conv_wg_autograd_matches_conv2d(hw):
     x2, w2 = x.clone().requires_grad_(), w.detach().clone(memory_format=cl).requires_grad_()
     assert convwg.supported(x1, w1, 1, 1, 1)
     assert convwg.dgrad_supported(w1, tuple(x.shape), 1)
-    tiles = (2 * hw[0] * hw[1] + 127) // 128
-    assert (convwg.dgrad_splits(tiles, 9 * 256 // 64) > 1) == (hw == (20, 24))
     y1 = convwg.conv2d_wg(x1, w1, 1, 1, 1)
     y2 = torch.nn.functional.conv2d(x2, w2, None, 1, 1, 1)
     _close(y1.detach(), y2.detach().float().cpu())
