@@ -553,18 +553,23 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
           for (int e = 0; e < 16; ++e) acc[dt][e] *= alpha;
       }
       const float mc = m_i == -INFINITY ? 0.f : m_i * c;
-      float rs = 0.f;
+      // packed fp32 (v_pk_fma_f32 / v_pk_add_f32: two elements per issue) for the exponent
+      // argument and the row sum -- the forward is VALU-issue bound (profiles/r4_s1)
+      const f32x2_t c2 = {c, c}, nmc2 = {-mc, -mc};
+      f32x2_t rs2 = {0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < NSUB; ++t)
         if (FULL || t < nsub) {
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[t][e], c, -mc));
-            sacc[t][e] = p;
-            rs += p;
+          for (int e = 0; e < 16; e += 2) {
+            const f32x2_t a = __builtin_elementwise_fma((f32x2_t){sacc[t][e], sacc[t][e + 1]}, c2, nmc2);
+            const f32x2_t p = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+            sacc[t][e] = p.x;
+            sacc[t][e + 1] = p.y;
+            rs2 += p;
           }
         }
-      l_i += rs;
+      l_i += rs2.x + rs2.y;
 #pragma unroll
       for (int t = 0; t < NSUB; ++t)
         if (FULL || t < nsub) {
@@ -600,8 +605,13 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
           const uint32_t wd = (uint32_t)(dm_cur >> (32 * ((((kv0 >> 5) + t) >> 1) & 1)));
           const int lim = kl - kv0 - 32 * t - 4 * hh;
           float pv[16];
+          const f32x2_t c2 = {c, c}, nl2 = {-lse2, -lse2};
 #pragma unroll
-          for (int e = 0; e < 16; ++e) pv[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(s_[e], c, -lse2));
+          for (int e = 0; e < 16; e += 2) {   // packed exponent arguments (v_pk_fma_f32)
+            const f32x2_t a = __builtin_elementwise_fma((f32x2_t){s_[e], s_[e + 1]}, c2, nl2);
+            pv[e] = __builtin_amdgcn_exp2f(a.x);
+            pv[e + 1] = __builtin_amdgcn_exp2f(a.y);
+          }
           // (only the diagonal / padded-tail subtile is masked: a wave-uniform branch)
           if (!FULL && uni((CAUSAL && t == tdiag) || (!CAUSAL && tail) ? 1 : 0)) {
             asm volatile("" ::: "memory");   // a real branch, not per-element selects
@@ -611,14 +621,17 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
               else pv[e] = crow(e, 0) >= lim ? 0.f : pv[e];
             }
           }
+          const f32x2_t ndl2 = {-dl, -dl};
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            float x = dp[e];
+          for (int e = 0; e < 16; e += 2) {
+            f32x2_t x = {dp[e], dp[e + 1]};
             if (DROP) {   // (keep ? dP : 0) - delta
-              const uint32_t mk = elem_keep(wd, 8 * (t & 1), e);
-              x = __uint_as_float(__float_as_uint(x) & mk);
+              x.x = __uint_as_float(__float_as_uint(x.x) & elem_keep(wd, 8 * (t & 1), e));
+              x.y = __uint_as_float(__float_as_uint(x.y) & elem_keep(wd, 8 * (t & 1), e + 1));
             }
-            s_[e] = pv[e] * (x - dl);   // dS^T (the common 1/(1-p) is in oscale)
+            const f32x2_t d = (f32x2_t){pv[e], pv[e + 1]} * (x + ndl2);   // dS^T (1/(1-p) in oscale)
+            s_[e] = d.x;
+            s_[e + 1] = d.y;
           }
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
@@ -958,13 +971,18 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
       // P of the subtile, unmasked; the causal diagonal subtile (wave-uniform branch) and, in
       // RAGGED launches only, the query tail / invalid keys are zeroed afterwards
       float pv[16];
+      const f32x2_t c2 = {c, c};
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        // row constants of the lane's query rows, 4 consecutive per e >> 2 (one ds_read_b128)
-        float4 lsq;
-        if ((e & 3) == 0) lsq = *reinterpret_cast<const float4*>(Lt + 32 * u + 8 * (e >> 2) + 4 * hh);
-        const float lse_e = (e & 3) == 0 ? lsq.x : (e & 3) == 1 ? lsq.y : (e & 3) == 2 ? lsq.z : lsq.w;
-        pv[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[e], c, -lse_e));
+      for (int e = 0; e < 16; e += 4) {
+        // row constants of the lane's query rows, 4 consecutive per e >> 2 (one ds_read_b128);
+        // exponent arguments two at a time (v_pk_fma_f32)
+        const float4 lsq = *reinterpret_cast<const float4*>(Lt + 32 * u + 8 * (e >> 2) + 4 * hh);
+        const f32x2_t a0 = __builtin_elementwise_fma((f32x2_t){sacc[e], sacc[e + 1]}, c2, (f32x2_t){-lsq.x, -lsq.y});
+        const f32x2_t a1 = __builtin_elementwise_fma((f32x2_t){sacc[e + 2], sacc[e + 3]}, c2, (f32x2_t){-lsq.z, -lsq.w});
+        pv[e] = __builtin_amdgcn_exp2f(a0.x);
+        pv[e + 1] = __builtin_amdgcn_exp2f(a0.y);
+        pv[e + 2] = __builtin_amdgcn_exp2f(a1.x);
+        pv[e + 3] = __builtin_amdgcn_exp2f(a1.y);
       }
       if (!FULL && uni(diag ? 1 : 0)) {
         asm volatile("" ::: "memory");   // keeps this a real (scalar) branch: not if-converted into selects
@@ -979,22 +997,28 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
         }
       }
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
+      for (int e = 0; e < 16; e += 2) {
         float4 dlq;
         if ((e & 3) == 0) dlq = *reinterpret_cast<const float4*>(Dt + 32 * u + 8 * (e >> 2) + 4 * hh);
-        const float dl_e = (e & 3) == 0 ? dlq.x : (e & 3) == 1 ? dlq.y : (e & 3) == 2 ? dlq.z : dlq.w;
-        const float p = pv[e];
+        const f32x2_t ndl = (e & 3) == 0 ? (f32x2_t){-dlq.x, -dlq.y} : (f32x2_t){-dlq.z, -dlq.w};
+        const f32x2_t p = {pv[e], pv[e + 1]};
         // dS = P (keep ? dP - delta : -delta) = P ((keep ? dP : 0) - delta); the dropped P is 0
         // in dV's operand: one sign-extended bit-field extract serves both
-        float x = dpacc[e];
+        f32x2_t x = {dpacc[e], dpacc[e + 1]};
         if (DROP) {
-          const uint32_t mk = elem_keep(dm_cur, 8 * ((qsu >> 5) & 1), e);
-          x = __uint_as_float(__float_as_uint(x) & mk);
-          sacc[e] = __uint_as_float(__float_as_uint(p) & mk);
+          const uint32_t mk0 = elem_keep(dm_cur, 8 * ((qsu >> 5) & 1), e);
+          const uint32_t mk1 = elem_keep(dm_cur, 8 * ((qsu >> 5) & 1), e + 1);
+          x.x = __uint_as_float(__float_as_uint(x.x) & mk0);
+          x.y = __uint_as_float(__float_as_uint(x.y) & mk1);
+          sacc[e] = __uint_as_float(__float_as_uint(p.x) & mk0);
+          sacc[e + 1] = __uint_as_float(__float_as_uint(p.y) & mk1);
         } else {
-          sacc[e] = p;
+          sacc[e] = p.x;
+          sacc[e + 1] = p.y;
         }
-        dpacc[e] = p * (x - dl_e);   // dS (1/(1-p) in dkscale)
+        const f32x2_t d = p * (x + ndl);   // dS (1/(1-p) in dkscale), v_pk_add_f32 + v_pk_mul_f32
+        dpacc[e] = d.x;
+        dpacc[e + 1] = d.y;
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
