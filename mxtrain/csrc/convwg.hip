@@ -46,6 +46,7 @@ struct ConvWg {
   int Cin, tiles_n, tiles_tap, ntiles;
   int splits, nk;        // pixel slices, 64-row K-steps per slice
   float invOW, invOH, beta;
+  uint32_t xbytes, ybytes;   // sizes of x and dY (buffer resources; < 2 GiB)
 };
 
 __device__ __forceinline__ void divmod(int p, int d, float inv, int& q, int& r) {
@@ -89,23 +90,61 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
     kB[j] = (PB * wave + j) * (1024 / RB) + lane / CB;
     cB[j] = 8 * pchunk(kB[j], lane % CB);
   }
-  const int Tm1 = cp.T - 1;
-  auto srcA = [&](int j, int it) __attribute__((always_inline)) {
-    const int p = min(p0 + it * BKT + kA[j], Tm1);   // rows past T: any valid row (B is zero there)
-    return cp.dy + (size_t)p * cp.ldy + cA[j];
-  };
-  auto srcB = [&](int j, int it) __attribute__((always_inline)) {
-    const int p = p0 + it * BKT + kB[j];
-    if (IDENT) {
-      return p < cp.T ? cp.x + (size_t)p * cp.ldx + n0 + cB[j] : cp.zero + cB[j];
-    } else {
-      int q, ow, n, oh;
-      divmod(p, cp.OW, cp.invOW, q, ow);
-      divmod(q, cp.OH, cp.invOH, n, oh);
-      const int ih = oh * cp.stride + dh, iw = ow * cp.stride + dwc;
-      const bool ok = p < cp.T && (unsigned)ih < (unsigned)cp.IH && (unsigned)iw < (unsigned)cp.IW;
-      return ok ? cp.x + ((size_t)(n * cp.IH + ih) * cp.IW + iw) * cp.ldx + n0 + cB[j] : cp.zero + cB[j];
+  // Per-lane gather state, advanced by one 64-pixel K-step per issue (32-bit offsets, no
+  // per-step division or 64-bit math; the former per-step divmods and 64-bit addresses were
+  // ~210 VALU per 32 MFMAs, profiles/r4_s3/pmc_conv_rpn_canvas_4img.txt).  dY rows past T
+  // and input taps outside the image read zeros through out-of-range buffer offsets.
+  const i32x4_t yres = buffer_rsrc(cp.dy, cp.ybytes), xres = buffer_rsrc(cp.x, cp.xbytes);
+  uint32_t ya[PA];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) ya[j] = (uint32_t)((p0 + kA[j]) * cp.ldy + cA[j]) * 2u;
+  const uint32_t ystep = (uint32_t)(BKT * cp.ldy) * 2u;
+  // B: pixel p = p0 + it BKT + kB[j] -> (oh s, ow s) and xo = ((n IH + oh s) IW + ow s) ldx
+  int bp[PB], bohs[PB], bows[PB], bxo[PB];
+  const int S_ = cp.stride, X_ = cp.ldx;
+#pragma unroll
+  for (int j = 0; j < PB; ++j) {
+    const int p = p0 + kB[j];
+    int q, ow, n, oh;
+    divmod(p, cp.OW, cp.invOW, q, ow);
+    divmod(q, cp.OH, cp.invOH, n, oh);
+    bp[j] = p;
+    bohs[j] = oh * S_;
+    bows[j] = ow * S_;
+    bxo[j] = IDENT ? p * X_ : ((n * cp.IH + oh * S_) * cp.IW + ow * S_) * X_;
+  }
+  const int dq = BKT / cp.OW, dr = BKT - dq * cp.OW;   // per-step (rows, columns) advance
+  const int tapoff = (dh * cp.IW + dwc) * X_ + n0;    // this tile's tap and channel block
+  auto advance = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < PA; ++j) ya[j] += ystep;
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      bp[j] += BKT;
+      if (IDENT) {
+        bxo[j] += BKT * X_;
+      } else {
+        bows[j] += dr * S_;
+        bxo[j] += dr * S_ * X_;
+        if (bows[j] >= cp.OW * S_) {
+          bows[j] -= cp.OW * S_;
+          bohs[j] += S_;
+          bxo[j] += (S_ * cp.IW - cp.OW * S_) * X_;
+        }
+        bohs[j] += dq * S_;
+        bxo[j] += dq * S_ * cp.IW * X_;
+        while (bohs[j] >= cp.OH * S_) {   // next image (at most once when OH OW >= 64)
+          bohs[j] -= cp.OH * S_;
+          bxo[j] += (cp.IH - cp.OH * S_) * cp.IW * X_;
+        }
+      }
     }
+  };
+  auto boffB = [&](int j) __attribute__((always_inline)) {
+    bool ok = bp[j] < cp.T;
+    if (!IDENT)
+      ok = ok && (unsigned)(bohs[j] + dh) < (unsigned)cp.IH && (unsigned)(bows[j] + dwc) < (unsigned)cp.IW;
+    return ok ? (uint32_t)(bxo[j] + tapoff + cB[j]) * 2u : kOOB;
   };
 
   const int G = lane >> 4, i = lane & 15;
@@ -127,13 +166,14 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
     for (int u = 0; u < FN; ++u) acc[a][u] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const uint32_t lds0 = lds_addr(smem);
-  auto issue = [&](int slot, int it) __attribute__((always_inline)) {
+  auto issue = [&](int slot, int) __attribute__((always_inline)) {   // steps issued in order
     const uint32_t b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
     const uint32_t b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
 #pragma unroll
-    for (int j = 0; j < PA; ++j) dma16(srcA(j, it), b0 + j * 1024);
+    for (int j = 0; j < PA; ++j) dma16_buf(yres, ya[j], b0 + j * 1024);
 #pragma unroll
-    for (int j = 0; j < PB; ++j) dma16(srcB(j, it), b1 + j * 1024);
+    for (int j = 0; j < PB; ++j) dma16_buf(xres, boffB(j), b1 + j * 1024);
+    advance();
   };
   constexpr int PER = PA + PB;
 
@@ -227,6 +267,7 @@ struct ConvFw {
   float invOW, invOH;
   int splits, Cout;      // split-K (few output tiles): fp32 partials [splits][T][Cout] in part,
   float* part;           // then conv_fwd_reduce_kernel applies the epilogue
+  uint32_t xbytes;       // size of x (the gather's buffer resource; < 2 GiB)
 };
 
 // FN = 4: 128 x 128 tiles (Cout % 128 == 0); FN = 2: 128 x 64 tiles for Cout % 128 == 64 (the
@@ -252,32 +293,40 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
   const int nk = (int)((int64_t)(sidx + 1) * cp.nk / cp.splits) - kb;   // this split's K-steps
   const size_t ldw = (size_t)cp.taps * cp.Cin;
 
-  int an[PA], aoh[PA], aow[PA], ach[PA];
-  bool aok[PA];
+  // Per-lane constants of the gather, so a K-step's DMA addressing is 32-bit adds and one
+  // select per piece: each A piece's element offset at tap (0, 0) (negative in the padding)
+  // and a bit per filter tap that lands inside the image; padding taps read zeros through
+  // an out-of-range buffer offset.  (The former 64-bit address per piece and step cost
+  // ~80 VALU per K-step against 32 MFMAs: VALU:MFMA 4:1 in PMC,
+  // profiles/r4_s3/pmc_conv_rpn_canvas_4img.txt.)
+  int aoff[PA];
+  uint32_t amask[PA];
 #pragma unroll
   for (int j = 0; j < PA; ++j) {
     const int row = (PA * wave + j) * (1024 / R) + lane / (R / 16);
     const int p = m0 + row;
-    aok[j] = p < cp.T;
+    const bool ok = p < cp.T;
     int q, ow, n, oh;
-    divmod(aok[j] ? p : 0, cp.OW, cp.invOW, q, ow);
+    divmod(ok ? p : 0, cp.OW, cp.invOW, q, ow);
     divmod(q, cp.OH, cp.invOH, n, oh);
-    an[j] = n; aoh[j] = oh * cp.stride - cp.pad; aow[j] = ow * cp.stride - cp.pad;
-    ach[j] = 8 * ((lane % (R / 16)) ^ (row & 7));
+    const int ih0 = oh * cp.stride - cp.pad, iw0 = ow * cp.stride - cp.pad;
+    aoff[j] = ((n * cp.IH + ih0) * cp.IW + iw0) * cp.ldx + 8 * ((lane % (R / 16)) ^ (row & 7));
+    uint32_t m = 0u;
+    for (int r = 0, t = 0; r < cp.taps / cp.KW; ++r) {
+      const bool rin = ok && (unsigned)(ih0 + r * cp.dil) < (unsigned)cp.IH;
+      for (int c = 0; c < cp.KW; ++c, ++t)
+        m |= (rin && (unsigned)(iw0 + c * cp.dil) < (unsigned)cp.IW) ? 1u << t : 0u;
+    }
+    amask[j] = m;
+    asm volatile("" : "+v"(aoff[j]));   // keep the per-lane offset whole (no per-step re-multiply)
   }
-  int brow[PB];
+  uint32_t boff[PB];
 #pragma unroll
-  for (int j = 0; j < PB; ++j) brow[j] = n0 + (PB * wave + j) * (1024 / R) + lane / (R / 16);
-  auto srcA = [&](int j, int tap, int ci0) __attribute__((always_inline)) {
-    const int r = tap / cp.KW, s = tap - r * cp.KW;
-    const int ih = aoh[j] + r * cp.dil, iw = aow[j] + s * cp.dil;
-    const bool ok = aok[j] && (unsigned)ih < (unsigned)cp.IH && (unsigned)iw < (unsigned)cp.IW;
-    return ok ? cp.x + ((size_t)(an[j] * cp.IH + ih) * cp.IW + iw) * cp.ldx + ci0 + ach[j] : cp.zero + ach[j];
-  };
-  auto srcB = [&](int j, int tap, int ci0) __attribute__((always_inline)) {
-    return cp.w + (size_t)brow[j] * ldw + (size_t)tap * cp.Cin + ci0 + ach[j];   // same chunk swizzle
-  };
-
+  for (int j = 0; j < PB; ++j) {
+    const int brow = n0 + (PB * wave + j) * (1024 / R) + lane / (R / 16);
+    boff[j] = (uint32_t)(brow * (int)ldw + 8 * ((lane % (R / 16)) ^ (brow & 7))) * 2u;
+  }
+  const i32x4_t xres = buffer_rsrc(cp.x, cp.xbytes);
   const int G = lane >> 4, i = lane & 15;
   const int wm = wave / WN, wn = wave % WN;
   const int offA = (16 * FM * wm + i) * R, offB = (16 * FN * wn + i) * R;
@@ -292,15 +341,30 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
     for (int u = 0; u < FN; ++u) acc[a][u] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const uint32_t lds0 = lds_addr(smem);
-  auto issue = [&](int slot, int li) __attribute__((always_inline)) {
-    const int it = kb + li;
-    const int tap = it / cp.cib, ci0 = (it - tap * cp.cib) * BKT;
+  // K-step walk (wave-uniform, advanced once per issue: the steps are issued in order):
+  // channel block, tap, the tap's filter row / column and its element offset in x
+  int k_ci = kb % cp.cib, k_tap = kb / cp.cib;
+  int k_r = k_tap / cp.KW, k_c = k_tap - (k_tap / cp.KW) * cp.KW;
+  int k_toff = (k_r * cp.IW + k_c) * cp.dil * cp.ldx;
+  auto issue = [&](int slot, int) __attribute__((always_inline)) {
+    const int tap = k_tap, ci0 = k_ci * BKT;
+    const int delta = k_toff + ci0;
+    if (++k_ci == cp.cib) {
+      k_ci = 0;
+      ++k_tap;
+      k_toff += cp.dil * cp.ldx;
+      if (++k_c == cp.KW) { k_c = 0; k_toff += (cp.IW - cp.KW) * cp.dil * cp.ldx; }
+    }
     const uint32_t b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
     const uint32_t b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
 #pragma unroll
-    for (int j = 0; j < PA; ++j) dma16(srcA(j, tap, ci0), b0 + j * 1024);
+    for (int j = 0; j < PA; ++j) {
+      const bool in = (amask[j] >> tap) & 1u;
+      dma16_buf(xres, in ? (uint32_t)(aoff[j] + delta) * 2u : kOOB, b0 + j * 1024);
+    }
+    const uint16_t* wb = cp.w + (size_t)tap * cp.Cin + ci0;
 #pragma unroll
-    for (int j = 0; j < PB; ++j) dma16(srcB(j, tap, ci0), b1 + j * 1024);
+    for (int j = 0; j < PB; ++j) dma16_sbase(wb, boff[j], b1 + j * 1024);
   };
 
   // NSLOT-deep LDS-DMA ring, counted waits (the input gradient's scheme): with NSLOT > 2 the
@@ -481,6 +545,7 @@ struct ConvDg {
   // parity class (xs > 0): this launch's pixels are the dX pixels (i * xs + xa, j * xs + xb)
   // of an XH x XW image, enumerated as an IH x IW grid (stride-decomposed dgrad, below)
   int xs, xa, xb, XH, XW;
+  uint32_t ybytes;       // size of dY (the gather's buffer resource; < 2 GiB)
 };
 
 // dX row of the launch's pixel p (identity unless a parity-class launch)
@@ -511,41 +576,52 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
   const int nk = (int)((int64_t)(sidx + 1) * cp.nk / cp.splits) - kb;
   const size_t ldw = (size_t)cp.ldw;
 
-  // ---- A (gathered dY) rows of this lane: fixed input pixel per DMA piece
-  int an[PA], aih[PA], aiw[PA], ach[PA];
-  bool aok[PA];
+  // ---- A (gathered dY) rows of this lane: fixed input pixel per DMA piece.  As in the
+  // forward: the element offset of dY[(ih + pad) / s][(iw + pad) / s] and a bit per tap whose
+  // output pixel exists (in the image, on the stride grid); tap (r, c) then reads at the
+  // wave-uniform delta -((r dil / s) OW + c dil / s) ldy (exact on the grid: ih + pad and
+  // r dil have equal residues mod s there), padding through out-of-range buffer offsets.
+  int aoff[PA];
+  uint32_t amask[PA];
 #pragma unroll
   for (int j = 0; j < PA; ++j) {
     const int row = (PA * wave + j) * (1024 / RA) + lane / (RA / 16);
     const int p = m0 + row;
-    aok[j] = p < cp.T;
+    const bool ok = p < cp.T;
     int q, iw, n, ih;
-    divmod(aok[j] ? p : 0, cp.IW, cp.invIW, q, iw);
+    divmod(ok ? p : 0, cp.IW, cp.invIW, q, iw);
     divmod(q, cp.IH, cp.invIH, n, ih);
-    an[j] = n; aih[j] = ih; aiw[j] = iw;
-    ach[j] = 8 * ((lane % (RA / 16)) ^ (row & 7));
+    const int hh = ih + cp.pad, ww = iw + cp.pad, st = cp.stride, KHt = cp.taps / cp.KW;
+    const int sw = 8 * ((lane % (RA / 16)) ^ (row & 7));
+    uint32_t m = 0u;
+    if (st == 1) {   // (wave-uniform) no per-lane divisions on the common path
+      aoff[j] = ((n * cp.OH + hh) * cp.OW + ww) * cp.ldy + sw;
+      for (int r = 0, t = 0; r < KHt; ++r) {
+        const bool rin = ok && (unsigned)(hh - r * cp.dil) < (unsigned)cp.OH;
+        for (int c = 0; c < cp.KW; ++c, ++t)
+          m |= (rin && (unsigned)(ww - c * cp.dil) < (unsigned)cp.OW) ? 1u << t : 0u;
+      }
+    } else {
+      aoff[j] = ((n * cp.OH + hh / st) * cp.OW + ww / st) * cp.ldy + sw;
+      for (int r = 0, t = 0; r < KHt; ++r) {
+        const int ah = hh - r * cp.dil;
+        const bool rin = ok && ah >= 0 && ah % st == 0 && ah / st < cp.OH;
+        for (int c = 0; c < cp.KW; ++c, ++t) {
+          const int aw = ww - c * cp.dil;
+          m |= (rin && aw >= 0 && aw % st == 0 && aw / st < cp.OW) ? 1u << t : 0u;
+        }
+      }
+    }
+    amask[j] = m;
+    asm volatile("" : "+v"(aoff[j]));   // keep the per-lane offset whole
   }
-  int kB[PB], cB[PB];
+  uint32_t boff[PB];
 #pragma unroll
   for (int j = 0; j < PB; ++j) {
-    kB[j] = (PB * wave + j) * (1024 / RB) + lane / (RB / 16);
-    cB[j] = 8 * pchunk(kB[j], lane % (RB / 16));
+    const int kB = (PB * wave + j) * (1024 / RB) + lane / (RB / 16);
+    boff[j] = (uint32_t)(kB * (int)ldw + n0 + 8 * pchunk(kB, lane % (RB / 16))) * 2u;
   }
-  auto srcA = [&](int j, int tap, int co0) __attribute__((always_inline)) {
-    const int r = tap / cp.KW, s = tap - r * cp.KW;
-    int oh = aih[j] + cp.pad - r * cp.dil, ow = aiw[j] + cp.pad - s * cp.dil;
-    bool ok = aok[j];
-    if (cp.stride > 1) {
-      ok = ok && (oh % cp.stride) == 0 && (ow % cp.stride) == 0;
-      oh /= cp.stride;
-      ow /= cp.stride;
-    }
-    ok = ok && (unsigned)oh < (unsigned)cp.OH && (unsigned)ow < (unsigned)cp.OW;
-    return ok ? cp.dy + ((size_t)(an[j] * cp.OH + oh) * cp.OW + ow) * cp.ldy + co0 + ach[j] : cp.zero + ach[j];
-  };
-  auto srcB = [&](int j, int tap, int co0) __attribute__((always_inline)) {
-    return cp.w + (size_t)(co0 + kB[j]) * ldw + (size_t)tap * cp.Cin + n0 + cB[j];
-  };
+  const i32x4_t yres = buffer_rsrc(cp.dy, cp.ybytes);
 
   const int G = lane >> 4, i = lane & 15;
   const int wm = wave / WN, wn = wave % WN;
@@ -567,15 +643,34 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
     for (int u = 0; u < FN; ++u) acc[a][u] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const uint32_t lds0 = lds_addr(smem);
-  auto issue = [&](int slot, int li) __attribute__((always_inline)) {
-    const int it = kb + li;
-    const int tap = it / cp.cob, co0 = (it - tap * cp.cob) * BKT;
+  // K-step walk (wave-uniform, advanced once per issue): output-channel block, tap, its
+  // filter row / column and its dY element offset
+  int k_co = kb % cp.cob, k_tap = kb / cp.cob;
+  int k_r = k_tap / cp.KW, k_c = k_tap - (k_tap / cp.KW) * cp.KW;
+  auto tap_off = [&]() __attribute__((always_inline)) {
+    if (cp.stride == 1) return -(k_r * cp.OW + k_c) * cp.dil * cp.ldy;
+    return -((k_r * cp.dil / cp.stride) * cp.OW + k_c * cp.dil / cp.stride) * cp.ldy;
+  };
+  int k_toff = tap_off();
+  auto issue = [&](int slot, int) __attribute__((always_inline)) {
+    const int tap = k_tap, co0 = k_co * BKT;
+    const int delta = k_toff + co0;
+    if (++k_co == cp.cob) {
+      k_co = 0;
+      ++k_tap;
+      if (++k_c == cp.KW) { k_c = 0; ++k_r; }
+      k_toff = tap_off();
+    }
     const uint32_t b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
     const uint32_t b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
 #pragma unroll
-    for (int j = 0; j < PA; ++j) dma16(srcA(j, tap, co0), b0 + j * 1024);
+    for (int j = 0; j < PA; ++j) {
+      const bool in = (amask[j] >> tap) & 1u;
+      dma16_buf(yres, in ? (uint32_t)(aoff[j] + delta) * 2u : kOOB, b0 + j * 1024);
+    }
+    const uint16_t* wb = cp.w + (size_t)co0 * ldw + (size_t)tap * cp.Cin;
 #pragma unroll
-    for (int j = 0; j < PB; ++j) dma16(srcB(j, tap, co0), b1 + j * 1024);
+    for (int j = 0; j < PB; ++j) dma16_sbase(wb, boff[j], b1 + j * 1024);
   };
 
 #pragma unroll
@@ -755,6 +850,10 @@ MX_EXPORT int mx_conv_wgrad(const int64_t* d, float beta, int splits, void* stre
   if (splits < 1 || (splits > 1 && cp.slab == nullptr)) return (int)hipErrorInvalidValue;
   cp.T = (int)T;
   cp.taps = KH * cp.KW;
+  const int64_t xbytes = N * cp.IH * cp.IW * (int64_t)cp.ldx * 2, ybytes = T * (int64_t)cp.ldy * 2;
+  if (xbytes >= ((int64_t)1 << 31) || ybytes >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  cp.xbytes = (uint32_t)xbytes;
+  cp.ybytes = (uint32_t)ybytes;
   cp.tiles_n = cp.Cin / kBN;
   cp.tiles_tap = (Cout / kBM) * cp.tiles_n;
   cp.ntiles = cp.taps * cp.tiles_tap;
@@ -916,6 +1015,9 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   if ((d[0] | d[1] | d[2] | d[3] | d[4] | d[5]) & 15) return (int)hipErrorInvalidValue;
   cp.T = (int)T;
   cp.taps = KH * cp.KW;
+  const int64_t ybytes = N * cp.OH * cp.OW * (int64_t)cp.ldy * 2;
+  if (cp.taps > 32 || ybytes >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  cp.ybytes = (uint32_t)ybytes;
   cp.ldw = cp.taps * cp.Cin;
   cp.cob = Cout / 64;
   cp.nk = cp.taps * cp.cob;
@@ -998,6 +1100,9 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   if ((d[0] | d[1] | d[2]) & 15) return (int)hipErrorInvalidValue;
   cp.T = (int)T;
   cp.taps = KH * cp.KW;
+  const int64_t xbytes = N * cp.IH * cp.IW * (int64_t)cp.ldx * 2;
+  if (cp.taps > 32 || xbytes >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  cp.xbytes = (uint32_t)xbytes;
   cp.cib = cp.Cin / 64;
   cp.nk = cp.taps * cp.cib;
   cp.tiles_n = Cout % 128 == 0 ? Cout / 128 : Cout / 64;

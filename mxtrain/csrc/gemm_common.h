@@ -42,6 +42,24 @@ __device__ __forceinline__ void dma16(const void* g, uint32_t lds_base) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
                :: "v"(g), "s"(lds_base) : "memory", "m0");
 }
+// The same piece addressed as a 32-bit byte offset from a wave-uniform base (saddr form): the
+// per-lane address math stays 32-bit (no 64-bit adds / multiplies per piece).
+__device__ __forceinline__ void dma16_sbase(const void* sbase, uint32_t voff, uint32_t lds_base) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+               :: "v"(voff), "s"(sbase), "s"(lds_base) : "memory", "m0");
+}
+// Buffer-resource form: a byte offset >= the resource's size reads zeros (padding rows of an
+// implicit-GEMM gather without a select between two 64-bit addresses).  Raw buffer, stride 0.
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4_t buffer_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  return i32x4_t{(int)(uint32_t)b, (int)(uint32_t)(b >> 32), (int)bytes, 0x00020000};
+}
+constexpr uint32_t kOOB = 0x80000000u;   // out-of-range offset (resources stay < 2 GiB)
+__device__ __forceinline__ void dma16_buf(i32x4_t rsrc, uint32_t voff, uint32_t lds_base) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :: "v"(voff), "s"(rsrc), "s"(lds_base) : "memory", "m0");
+}
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
