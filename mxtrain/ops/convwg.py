@@ -26,8 +26,9 @@ ENABLED = True          # module switch (A/B runs: scripts/conv_wgrad_bench.py)
 DGRAD = True            # input gradient from csrc/convwg.hip too (else MIOpen's backward-data)
 FWD = True              # forward with the fused bias / residual / ReLU epilogue (else MIOpen)
 FWD_MIN_TILES = 64
-TARGET_WGS = 512        # two 128 x 128 workgroups per CU on 256 CUs (a 256 / 1024 x 4 / 16 sweep:
-MIN_STEPS = 8           # profiles/r4_s2/conv_wgrad_split_sweep.txt)
+TARGET_WGS = 512        # two 128 x 128 workgroups per CU on 256 CUs; >= 16 K-steps per slice since
+MIN_STEPS = 16          # the 32-bit gather made the slices cheaper than their fp32 partials
+                        # (profiles/r4_s3/wgrad_split_ab*_{1,4}img.txt; before: r4_s2 sweep, 8)
 _DESC_T = ctypes.c_int64 * 24
 _WS: Dict[torch.device, Tuple[torch.Tensor, torch.Tensor]] = {}
 _RETIRED = []           # outgrown slabs stay alive: a captured hipGraph may still write them

@@ -67,6 +67,25 @@ def timeit(fn, it=10, reps=5):
 
 tot_m = tot_h = tot_dm = tot_dh = tot_fm = tot_fh = 0.0
 cl = torch.channels_last
+# weight-gradient split planning A/B (ops/convwg.py plan_splits): WG_AB="TARGET_WGS:MIN_STEPS ..."
+WG_AB = [tuple(int(t) for t in c.split(":")) for c in os.environ.get("WG_AB", "").split()]
+if WG_AB:
+    tot = [0.0] * len(WG_AB)
+    print(f"{'wgrad split A/B (us)':24s} {'N':>3s} " + " ".join(f"{'%d:%d' % c:>9s}" for c in WG_AB))
+    for name, Cin, Cout, H, W, k, s, p, cnt in SHAPES:
+        n = 64 * N if name.startswith("mask") else N
+        x = torch.randn(n, Cin, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+        OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        dy = torch.randn(n, Cout, OH, OW, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+        cols = []
+        for i, (tw, ms) in enumerate(WG_AB):
+            convwg.TARGET_WGS, convwg.MIN_STEPS = tw, ms
+            t = timeit(lambda: convwg.conv_wgrad(dy, x, (Cout, Cin, k, k), s, p, 1))
+            tot[i] += cnt * t
+            cols.append(f"{t:9.1f}")
+        print(f"{name:24s} {n:3d} " + " ".join(cols), flush=True)
+    print("per step (counts): " + ", ".join(f"{'%d:%d' % c} {t:.0f} us" for c, t in zip(WG_AB, tot)))
+    sys.exit(0)
 if SPLIT_AB:
     tot = [[0.0, 0.0] for _ in SPLIT_AB]
     print(f"{'split-K A/B (fwd | dgrad us)':26s} {'N':>3s} " + " ".join(f"{':'.join(map(str, c)):>17s}" for c in SPLIT_AB))
