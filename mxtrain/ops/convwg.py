@@ -194,7 +194,7 @@ def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, paddi
 # more to the fp32 partial traffic than they gain (res3 3x3 at one image: 18 K-steps, 132
 # tiles, 18.9 -> 26.9 us split in two); long ones on a part-empty chip gain (res5 3x3 at
 # four images: 72 K-steps, 132 tiles, 60 -> 39 us in three) -- profiles/r4_s2/conv_split_ab_*.txt
-SPLIT_TILES = 256
+SPLIT_TILES = 512       # 256 before the 32-bit gather (profiles/r4_s3/split_ab3_*: 512 best at 1 and 4 img)
 SPLIT_WGS = 512
 SPLIT_MAX = 8
 SPLIT_MIN_NK = 32
