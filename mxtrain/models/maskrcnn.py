@@ -21,6 +21,7 @@ deltas (weights 10,10,5,5), mask sigmoid BCE.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -339,8 +340,19 @@ class MaskRCNN(nn.Module):
 
     def features(self, images: torch.Tensor):
         dt = self.compute_dtype(images.device)
-        x = ((images.float() - self.pixel_mean) / self.pixel_std).to(dt)
-        x = x.contiguous(memory_format=torch.channels_last)
+        x = None
+        if (images.is_cuda and images.dtype == torch.uint8 and dt == torch.bfloat16 and images.is_contiguous()
+                and (images.shape[2] * images.shape[3]) % 4 == 0 and _lib.use_hip(images)):
+            # one pass: uint8 NCHW -> normalised bf16 NHWC (csrc/vision.hip normalize_u8_nhwc_kernel)
+            B, _, H, W = images.shape
+            x = torch.empty(B, H, W, 3, dtype=dt, device=images.device).permute(0, 3, 1, 2)
+            _lib.call("mx_normalize_u8_nhwc", images.data_ptr(), x.data_ptr(), B, H, W,
+                      ctypes.cast((ctypes.c_float * 3)(*self.cfg.pixel_mean), ctypes.c_void_p),
+                      ctypes.cast((ctypes.c_float * 3)(*[1.0 / v for v in self.cfg.pixel_std]), ctypes.c_void_p),
+                      _lib.stream())
+        if x is None:
+            x = ((images.float() - self.pixel_mean) / self.pixel_std).to(dt)
+            x = x.contiguous(memory_format=torch.channels_last)
         c = self.backbone.forward_features(x)
         return self.fpn(c)      # P2..P6, NCHW views of channels_last memory
 

@@ -124,6 +124,7 @@ SIGNATURES = {
     "mx_match": [P, I, I, P, P, I, I, P, P, P, P, P],
     "mx_decode_clip": [P, P, I, I, F, F, F, F, F, P, I, P, P],
     "mx_copy_rows": [P, P, I, I, I, I, I64, I64, P],
+    "mx_normalize_u8_nhwc": [P, P, I, I, I, P, P, P],
     "mx_crop_resize_masks": [P, I, I, P, P, I, I, P, P],
     "mx_crop_resize_mask_crops": [P, P, I, I, P, P, I, I, P, P],
 }

@@ -106,3 +106,25 @@ def test_flat_master_gpu_matches_cpu():
         for a, b in zip(fg.compute_views(), fc.compute_views()):
             assert a.shape == b.shape
             torch.testing.assert_close(a.float().cpu(), b.float(), rtol=8e-3, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_input_normalisation_kernel_matches_reference():
+    """uint8 NCHW images -> normalised bf16 NHWC in one pass (csrc/vision.hip
+    normalize_u8_nhwc_kernel, models/maskrcnn.py MaskRCNN.features) against the fp32 chain."""
+    import ctypes
+    from mxtrain.models.maskrcnn import MaskRCNNConfig
+    from mxtrain.ops import _lib
+    cfg = MaskRCNNConfig()
+    g = torch.Generator().manual_seed(3)
+    img = torch.randint(0, 256, (2, 3, 40, 36), generator=g, dtype=torch.uint8).cuda()
+    x = torch.empty(2, 40, 36, 3, dtype=torch.bfloat16, device="cuda").permute(0, 3, 1, 2)
+    _lib.call("mx_normalize_u8_nhwc", img.data_ptr(), x.data_ptr(), 2, 40, 36,
+              ctypes.cast((ctypes.c_float * 3)(*cfg.pixel_mean), ctypes.c_void_p),
+              ctypes.cast((ctypes.c_float * 3)(*[1.0 / v for v in cfg.pixel_std]), ctypes.c_void_p), _lib.stream())
+    torch.cuda.synchronize()
+    mean = torch.tensor(cfg.pixel_mean).view(1, 3, 1, 1)
+    std = torch.tensor(cfg.pixel_std).view(1, 3, 1, 1)
+    ref = (img.cpu().float() - mean) / std
+    assert x.is_contiguous(memory_format=torch.channels_last)
+    assert (x.float().cpu() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
