@@ -328,7 +328,9 @@ def test_fused_detection_losses_match_torch():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("R,n,k,largest", [(2, 10000, 2000, True), (4, 2100, 512, True), (2, 2100, 128, False),
-                                           (1, 300, 300, True), (3, 32768, 2048, False), (8, 64, 1, True)])
+                                           (1, 300, 300, True), (3, 32768, 2048, False), (8, 64, 1, True),
+                                           # long rows: chunked two-stage (RPN anchor sampling)
+                                           (2, 268569, 256, False), (1, 100000, 512, True), (2, 40000, 2048, True)])
 def test_topk_rows_matches_torch(R, n, k, largest):
     """csrc/vision.hip topk_rows_kernel vs torch.topk: identical values; indices point at
     those values, are distinct, and order equal values by lower index (ties forced by
