@@ -24,7 +24,8 @@ weights, full training step incl. SGD; the in-repo MIOpen find-db skips the conv
 
 Both steps are whole-step hipGraph replays at every N: at N > 1 the captured GPT step holds
 its ZeRO-1 reduce-scatter / all-gather, and the Mask R-CNN step its bucketed gradient
-all-reduces (RCCL over xGMI by default; --xgmi selects the direct peer-to-peer kernels).
+all-reduces.  At N > 1 each collective runs on RCCL or on the direct 7-link xGMI kernels,
+whichever the autotune (--xgmi auto, the N > 1 default) measured faster for its size.
 """
 from __future__ import annotations
 
@@ -39,7 +40,7 @@ import time
 def _coll_summary(tr):
     comms = getattr(tr, "xgmi_comms", {}) or {}
     if not comms:
-        return "rccl"
+        return "rccl" if tr.device.type == "cuda" else "gloo"
     out = {}
     for name, c in comms.items():
         if c is None:
@@ -102,12 +103,105 @@ def run_maskrcnn(batch: int, steps: int, warmup: int, world: int = 1, rank: int 
             res["hipgraph"] = {k: rec["graph"][k] for k in ("captures", "replays", "eager")}
         if rec.get("dp_routes"):
             res["dp_routes"] = rec["dp_routes"]
+        for k in ("loader_wait_ms", "host_enqueue_ms"):   # host time per step (child rank 0)
+            if k in rec:
+                res[k] = rec[k]
         return res
     except Exception as e:  # noqa: BLE001 -- the GPT number must still be reported
         return {"error": f"rank {rank}: " + repr(e)[:300]}
     finally:
         if os.path.exists(out):
             os.remove(out)
+
+
+def gpt3_layout(world: int):
+    """BASELINE config 4 (GPT-3 6.7B, TP2 x PP2 x DP2 at 8 GPUs;
+    examples/megatron-deepspeed/gpt2_345m/pretrain-ddp-tp-pp-zero1.yaml:39-40) scaled to the
+    job: (tp, pp, global batch) with micro-batch 2 -- the whole model on one 288 GB GPU at
+    N = 1, TP2 at 2, TP2 x PP2 (4 micro-batches: the 1F1B pipeline filled) at 4, and DP over
+    that at 8."""
+    if world >= 4 and world % 4 == 0:
+        return 2, 2, 8 * (world // 4)
+    if world % 2 == 0:
+        return 2, 1, 2 * (world // 2)
+    return 1, 1, 2 * world
+
+
+def _run_child(cmd, world: int, rank: int, port: int, timeout: float):
+    """One child rank (never an exec: this process has initialised the GPU) -> (rc, stdout)."""
+    import subprocess
+    try:
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout,
+                           env=_child_env(world, rank, port))
+        return r.returncode, r.stdout
+    except subprocess.TimeoutExpired as e:
+        out = e.stdout.decode() if isinstance(e.stdout, bytes) else (e.stdout or "")
+        return 124, out + f"\n[timeout after {timeout:.0f} s]"
+
+
+def _last_json(text: str):
+    for line in reversed(text.splitlines()):
+        line = line.strip()
+        if line.startswith("{") and line.endswith("}"):
+            try:
+                return json.loads(line)
+            except ValueError:
+                continue
+    return None
+
+
+def run_gpt3(world: int, rank: int, port: int, steps: int, warmup: int, extra=(), timeout: float = 420.0) -> dict:
+    """BASELINE config 4 phase: every bench rank starts one child rank of a fresh N-rank
+    GPT-3 6.7B job (this file, --model gpt3-6.7b, no further phases); child rank 0's JSON
+    line is the result."""
+    tp, pp, gb = gpt3_layout(world)
+    here = os.path.dirname(os.path.abspath(__file__))
+    cmd = [sys.executable, os.path.join(here, "bench.py"), "--gpus", str(world), "--model", "gpt3-6.7b",
+           "--micro-batch-size", "2", "--global-batch-size", str(gb), "--tp", str(tp), "--pp", str(pp),
+           "--steps", str(steps), "--warmup", str(warmup), "--no-maskrcnn", "--no-extra-configs"] + list(extra)
+    t0 = time.time()
+    rc, out = _run_child(cmd, world, rank, port, timeout)
+    if rc != 0:
+        return {"error": f"rank {rank} rc={rc}: " + out[-400:]}
+    if rank != 0:
+        return {"rc": 0}
+    rec = _last_json(out)
+    if rec is None:
+        return {"error": "no result line: " + out[-300:]}
+    return {"tok_s": rec["value"], "ms_per_step": rec["ms_per_step"], "steps": steps, "warmup": warmup,
+            "tflops_per_gpu": rec.get("tflops_per_gpu"), "mfu_bf16_dense_2.5pf": rec.get("mfu_bf16_dense_2.5pf"),
+            "global_batch": gb, "micro_batch": 2, "seq_len": rec["config"]["seq_len"],
+            "parallelism": rec["config"]["parallelism"], "hipgraph": rec["config"].get("hipgraph"),
+            "loss": rec.get("loss"), "wall_s": round(time.time() - t0, 1)}
+
+
+def run_resnet(world: int, steps: int, extra=(), timeout: float = 420.0) -> dict:
+    """BASELINE config 5 phase (rank 0 only): the Ray-Train-style ResNet-50 launcher
+    (mxtrain/workloads/ray/train_resnet50.py, the raytrain chart's workload) with one worker
+    per GPU, batch 256 per worker, synthetic ImageNet 224^2; images/s over the steps after
+    the first three, as the launcher reports it (data loading included)."""
+    import tempfile
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = tempfile.mktemp(prefix="mx_resnet_", suffix=".jsonl")
+    store = tempfile.mkdtemp(prefix="mx_resnet_ckpt_")
+    cmd = [sys.executable, os.path.join(here, "mxtrain", "workloads", "ray", "train_resnet50.py"),
+           "--num-workers", str(world), "--batch-size", "256", "--epochs", "1", "--steps-per-epoch", str(steps),
+           "--storage-path", store, "--result-json", out] + list(extra)
+    t0 = time.time()
+    try:
+        rc, text = _run_child(cmd, 1, 0, 0, timeout)
+        if rc != 0:
+            return {"error": f"rc={rc}: " + text[-400:]}
+        rec = json.loads(open(out).read().splitlines()[-1]) if os.path.exists(out) else None
+        if rec is None or rec.get("value") is None:
+            return {"error": "no result record: " + text[-300:]}
+        return {"img_s": round(rec["value"], 1), "workers": world, "batch_per_worker": 256, "steps": steps,
+                "warmup": 3, "wall_s": round(time.time() - t0, 1)}
+    finally:
+        import shutil
+        if os.path.exists(out):
+            os.remove(out)
+        shutil.rmtree(store, ignore_errors=True)
 
 
 def _free_port() -> int:
@@ -159,13 +253,24 @@ def main():
     ap.add_argument("--maskrcnn-args", default="",
                     help="extra arguments for scripts/bench_maskrcnn.py, one shell-quoted string "
                          "(tests: a small synthetic set and image size on the CPU)")
-    ap.add_argument("--xgmi", choices=["0", "1", "auto"], default="0",
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="skip the BASELINE config 4 / 5 phases (GPT-3 6.7B tokens/s, Ray-Train ResNet-50 "
+                         "images/s) that follow the Mask R-CNN runs")
+    ap.add_argument("--extra-steps", default="8:3",
+                    help="timed:warmup steps of the GPT-3 6.7B phase")
+    ap.add_argument("--resnet-steps", type=int, default=40, help="steps of the ResNet-50 phase (3 warm-up)")
+    ap.add_argument("--gpt3-args", default="", help="extra bench.py arguments of the GPT-3 phase (tests)")
+    ap.add_argument("--resnet-args", default="", help="extra train_resnet50.py arguments (tests)")
+    ap.add_argument("--xgmi", choices=["0", "1", "auto"], default=None,
                     help="direct xGMI peer-to-peer collectives (csrc/comm/xgmi.hip) for the DP "
-                         "reduce-scatter / all-gather and TP all-reduce: 0 = RCCL only (default: the "
-                         "xGMI kernels have only been exercised by processes sharing one GPU, so the "
-                         "scaling runs use RCCL over xGMI), 1 = always, auto = verify against RCCL and "
-                         "keep the faster per message size (N > 1)")
+                         "reduce-scatter / all-gather, the TP all-reduce and the Mask R-CNN bucket "
+                         "all-reduce: 0 = RCCL only, 1 = always, auto (default at N > 1) = a fail-fast "
+                         "probe, then a bit-exact check against RCCL and a timing of both per message "
+                         "size on the live group, agreed on every rank; any failure -> RCCL everywhere. "
+                         "The per-size decision is recorded in the JSON line (config.collectives)")
     args = ap.parse_args()
+    if args.xgmi is None:
+        args.xgmi = "auto" if int(os.environ.get("WORLD_SIZE", "1")) > 1 else "0"
     os.environ.setdefault("MXTRAIN_XGMI", args.xgmi)
 
     import torch
@@ -285,6 +390,7 @@ def main():
                 "optimizer": "adamw",
                 "tuned_gemm_tables": n_tables,
                 "collectives": _coll_summary(tr),
+                "xgmi_mode": os.environ.get("MXTRAIN_XGMI", "0"),
                 "fused_linear": not args.no_fused_linear,
             },
             "tflops_per_gpu": round(flops / world / 1e12, 1),
@@ -337,6 +443,49 @@ def main():
                 "conv_search": "MIOpen find (in-repo find-db) + implicit-GEMM HIP convolutions",
                 "step": "whole-step hipGraph replay (gradient all-reduces captured at N > 1)",
                 **{f"{b}img": {k: v for k, v in res[b].items() if k != "img_s"} for b in batches}}
+    if not args.no_extra_configs:
+        # BASELINE.json configs 4 and 5, each a fresh child job on the same N GPUs after the
+        # headline phases (outside every timed window above)
+        if args.no_maskrcnn:   # (else the GPT-2 model was freed before the Mask R-CNN runs)
+            del tr, tokens, labels
+            import gc
+            gc.collect()
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+                torch.cuda.empty_cache()
+        ctrl = dist.new_group(backend="gloo") if world > 1 else None   # host-only waits
+        port = _free_port() if ps.rank == 0 else None
+        if world > 1:
+            box = [port]
+            dist.broadcast_object_list(box, src=0)
+            port = box[0]
+        st, wu = (int(v) for v in args.extra_steps.split(":"))
+        g3 = run_gpt3(world, ps.rank, port, st, wu, extra=shlex.split(args.gpt3_args))
+        if "error" in g3:
+            print(f"gpt3-6.7b: {g3['error']}", file=sys.stderr, flush=True)
+        if world > 1:
+            errs = [None] * world
+            dist.all_gather_object(errs, g3.get("error"), group=ctrl)
+            if ps.rank == 0 and "error" not in g3 and any(errs):
+                g3 = {"error": next(e for e in errs if e)}
+        rn = run_resnet(world, args.resnet_steps, extra=shlex.split(args.resnet_args)) if ps.rank == 0 else None
+        if rn is not None and "error" in rn:
+            print(f"resnet50: {rn['error']}", file=sys.stderr, flush=True)
+        if world > 1:
+            dist.barrier(group=ctrl)   # the other ranks idle on the host while rank 0's workers run
+        if out is not None:
+            tp, pp, gb = gpt3_layout(world)
+            out["gpt3_6.7b_tok_s"] = g3.get("tok_s")
+            out["gpt3_6.7b_config"] = {
+                "model": "gpt3-6.7b (32 x 4096, 32 heads, seq 2048)", "n_gpus": world, "dtype": "bf16",
+                "data": "synthetic tokens, random-init weights", "unit": "tokens/s (whole job)",
+                "optimizer": "ZeRO-1 AdamW + clip 1.0", "dropout": "0.1 / 0.1",
+                **{k: v for k, v in g3.items() if k != "tok_s"}}
+            out["resnet50_img_s"] = (rn or {}).get("img_s")
+            out["resnet50_config"] = {
+                "model": "ResNet-50 (BatchNorm), Ray-Train + Lightning launcher", "n_gpus": world,
+                "dtype": "bf16 autocast, channels_last", "data": "synthetic ImageNet 224x224, random-init weights",
+                "unit": "images/s (whole job)", **{k: v for k, v in (rn or {}).items() if k != "img_s"}}
     if out is not None:
         print(json.dumps(out), flush=True)
     if world > 1:

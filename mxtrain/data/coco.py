@@ -103,12 +103,14 @@ class DetectionDataset(torch.utils.data.Dataset):
 
     def __getitem__(self, i: int):
         from PIL import Image
+        # AspectGroupedSampler(repeat=True) folds the epoch into the index
+        epoch, i = divmod(i, len(self.coco)) if i >= len(self.coco) else (self.epoch, i)
         rec = self.coco.record(i)
         img = Image.open(rec["file"]).convert("RGB")
         w0, h0 = img.size
         h, w, scale = resize_shape(h0, w0, self.short, self.max)
         img = img.resize((w, h), Image.BILINEAR)
-        flip = self.training and random.Random(self.seed * 7919 + self.epoch * 1_000_003 + i).random() < 0.5
+        flip = self.training and random.Random(self.seed * 7919 + epoch * 1_000_003 + i).random() < 0.5
         if flip:
             img = img.transpose(Image.FLIP_LEFT_RIGHT)
         arr = torch.from_numpy(np.asarray(img, dtype=np.uint8).copy()).permute(2, 0, 1)     # [3, h, w]
@@ -228,12 +230,27 @@ def collate(batch: List[dict], short: int = 800, max_size: int = 1333, max_gt: i
 
 
 class AspectGroupedSampler(torch.utils.data.Sampler):
-    """Distributed, aspect-grouped, epoch-shuffled batch sampler: every batch holds
-    images of one orientation; rank r takes every world-th batch."""
+    """Distributed, aspect-grouped, epoch-shuffled batch sampler.
+
+    Every batch holds images of one orientation, and every GLOBAL step has one
+    orientation: batches are grouped ``world`` at a time within an orientation, the
+    groups are shuffled (one shared seed), and rank r takes batch r of each group.  So
+    all ranks meet the same canvas shape on the same step -- the whole-step hipGraph
+    (workloads/maskrcnn/graphed.py) captures a new shape on every rank together, and the
+    padded canvases of one step cost the same on every rank (no straggler from a mixed
+    landscape / portrait step).
+
+    ``repeat=True`` yields an endless stream of epochs (tensorpack's RepeatedData): the
+    DataLoader iterator then lives for the whole run and its workers never drain at an
+    epoch boundary.  The epoch is folded into the yielded indices (``e * len(ds) + i``;
+    DetectionDataset maps them back), so flips differ per epoch inside worker processes
+    too.
+    """
 
     def __init__(self, ds: DetectionDataset, batch_size: int, rank: int = 0, world: int = 1, seed: int = 0,
-                 drop_last: bool = True):
+                 drop_last: bool = True, repeat: bool = False):
         self.ds, self.bs, self.rank, self.world, self.seed, self.drop = ds, batch_size, rank, world, seed, drop_last
+        self.repeat = repeat
         self.epoch = 0
         self.groups = [[i for i in range(len(ds)) if ds.orientation(i) == o] for o in (0, 1)]
 
@@ -241,23 +258,44 @@ class AspectGroupedSampler(torch.utils.data.Sampler):
         self.epoch = e
         self.ds.epoch = e
 
-    def _batches(self):
-        r = random.Random(self.seed + self.epoch)
-        out = []
+    def _batches(self, epoch: int):
+        r = random.Random(self.seed + epoch)
+        steps, loose = [], []
         for g in self.groups:
             g = list(g)
             r.shuffle(g)
+            bl = []
             for k in range(0, len(g), self.bs):
                 b = g[k:k + self.bs]
                 if len(b) == self.bs or (b and not self.drop):
-                    out.append(b)
-        r.shuffle(out)
-        n = len(out) // self.world * self.world
-        return out[:n] if n else out
+                    bl.append(b)
+            n = len(bl) // self.world * self.world
+            steps += [bl[k:k + self.world] for k in range(0, n, self.world)]
+            loose += bl[n:]
+        r.shuffle(steps)
+        out = [b for st in steps for b in st]
+        if not out:
+            # fewer than ``world`` batches per orientation (tiny sets): mixed-orientation
+            # steps, which graphed.py's collective capture protocol also handles
+            n = len(loose) // self.world * self.world
+            out = loose[:n] if n else loose
+        return out
+
+    def _epoch_iter(self, epoch: int):
+        off = epoch * len(self.ds) if self.repeat else 0
+        for b in self._batches(epoch)[self.rank::self.world]:
+            yield [off + i for i in b]
 
     def __iter__(self):
-        bs = self._batches()
-        return iter(bs[self.rank::self.world])
+        if not self.repeat:
+            return self._epoch_iter(self.epoch)
+
+        def endless():
+            e = self.epoch
+            while True:
+                yield from self._epoch_iter(e)
+                e += 1
+        return endless()
 
     def __len__(self):
-        return max(1, len(self._batches()) // self.world)
+        return max(1, len(self._batches(self.epoch)) // self.world)

@@ -185,7 +185,7 @@ class FlatMaster:
     """
 
     def __init__(self, model, opt: torch.optim.SGD, clip: float, dt: torch.dtype = torch.bfloat16,
-                 group=None, bucket_bytes: int = 32 << 20):
+                 group=None, bucket_bytes: int = 32 << 20, force_dp: bool = False):
         from ..ops import _lib
         self.model, self.opt, self.dt = model, opt, dt
         mom = {g["momentum"] for g in opt.param_groups}
@@ -197,13 +197,17 @@ class FlatMaster:
         self.world = dist.get_world_size(group) if dist_on else 1
         # an explicit group object: the xGMI communicator registry is keyed on it
         self.group = group if (group is not None or not dist_on) else dist.group.WORLD
+        # the data-parallel machinery (buckets, per-bucket all-reduce, joined average) runs
+        # when world > 1; ``force_dp`` runs it on a one-rank group too (tests: the RCCL
+        # all-reduce captured inside the step graph on one GPU)
+        self.dp = self.world > 1 or (bool(force_dp) and dist_on)
         self.params, wdf = [], []
         for g in opt.param_groups:
             for p in g["params"]:
                 if p.requires_grad:
                     self.params.append(p)
                     wdf.append(1 if g["weight_decay"] else 0)
-        if self.world > 1:
+        if self.dp:
             # model order: backward finishes the last modules' gradients first
             order = {id(p): i for i, p in enumerate(model.parameters())}
             pairs = sorted(zip(self.params, wdf), key=lambda pw: order.get(id(pw[0]), len(order)))
@@ -217,7 +221,7 @@ class FlatMaster:
         # (256-B) aligned so every all-reduce message divides over 8 ranks in 16-B units
         self.offs, off = [], 0
         self.buckets: List[Tuple[int, int, int, int]] = []
-        cap = max(1, bucket_bytes // 4) if self.world > 1 else None
+        cap = max(1, bucket_bytes // 4) if self.dp else None
         tb, e0 = 0, 0
         for t, n in enumerate(self.sizes):
             self.offs.append(off)
@@ -272,7 +276,7 @@ class FlatMaster:
         self.zero_bf16 = torch.zeros(_align8(max(self.sizes)), dtype=dt, device=dev)
         self._wkey = None
         self._cw_specs = None
-        self._dp_stream = torch.cuda.Stream(device=dev) if (self.cuda and self.world > 1) else None
+        self._dp_stream = torch.cuda.Stream(device=dev) if (self.cuda and self.dp) else None
         self.dp_route = None     # route of the last bucket reduced: "xgmi" / "rccl" / "gloo"
         self.dp_routes = set()   # every route used so far
         self._dp_reset()
@@ -396,7 +400,7 @@ class FlatMaster:
             _lib.call("mx_mt_grad_in_range", self.tab.data_ptr(), self.bmap.data_ptr(), self.bstart.data_ptr(),
                       self.bstart_c, tb, te, ctypes.addressof(arr), self.G.data_ptr(), self.partial.data_ptr(),
                       _lib.stream())
-            if self.world == 1:
+            if not self.dp:
                 _lib.call("mx_mt_sumsq_fin", self.partial.data_ptr(), self.nblocks, self.normsq.data_ptr(),
                           _lib.stream())
         else:
@@ -410,9 +414,9 @@ class FlatMaster:
                         gv = gv * self.scales[t].view(-1, *([1] * (p.dim() - 1)))
                     self.G[o:o + n].copy_(gv.reshape(-1) if gv.is_contiguous() else gv.contiguous().reshape(-1))
                     acc = acc + gv.pow(2).sum()
-                if self.world == 1:
+                if not self.dp:
                     self.normsq.fill_(float(acc))
-        if self.world > 1:
+        if self.dp:
             self._dp_ready(k)
         return [self.G[self.offs[t]:self.offs[t] + self.sizes[t]].view(self.params[t].shape) for t in range(tb, te)]
 
@@ -453,7 +457,7 @@ class FlatMaster:
         """Data parallel: make sure every bucket was reduced (a bucket whose parameters
         got no gradient at all still contributes zeros), join the reductions, average and
         take ||g||^2 of the averaged gradient."""
-        if self.world == 1:
+        if not self.dp:
             return
         for k in range(self._next, -1, -1):
             if k not in self._ready:

@@ -86,10 +86,15 @@ def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, residual: Optional[torch.T
            relu: bool = False) -> torch.Tensor:
     """act(bn(x) (+ residual)) for an ``nn.BatchNorm2d`` (training: batch statistics and
     running-statistics update; eval: running statistics)."""
-    mom = bn.momentum if bn.momentum is not None else 0.1
-    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
-        bn.num_batches_tracked.add_(1)
     if supported(x, residual):
+        mom = bn.momentum
+        if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+            # (the torch fallback below counts the batch inside nn.BatchNorm2d.forward)
+            bn.num_batches_tracked.add_(1)
+            if mom is None:   # cumulative moving average, as nn.BatchNorm2d
+                mom = 1.0 / float(bn.num_batches_tracked)
+        if mom is None:
+            mom = 0.0
         if bn.training:
             return BNActFn.apply(x, bn.weight, bn.bias, residual, bn.running_mean if bn.track_running_stats else None,
                                  bn.running_var if bn.track_running_stats else None, mom, bn.eps, relu)

@@ -88,6 +88,15 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dila
     Cout, Cin, KH, KW = w_shape
     N, _, IH, IW = x.shape
     _, _, OH, OW = dy.shape
+    if not _fits(dy.numel(), x.numel()):
+        # beyond the kernel's 32-bit offsets: MIOpen's weight gradient
+        wz = torch.zeros((Cout, Cin, KH, KW), dtype=dy.dtype, device=dy.device)
+        dw = torch.ops.aten.convolution_backward(dy, x, wz, None, list(_pair(stride)), list(_pair(padding)),
+                                                 list(_pair(dilation)), False, [0, 0], 1,
+                                                 [False, True, False])[1]
+        if out is None:
+            return dw.contiguous(memory_format=torch.channels_last)
+        return out.add_(dw) if beta else out.copy_(dw)
     if not _cl(dy):
         dy = dy.contiguous(memory_format=torch.channels_last)
     if out is None:
@@ -156,6 +165,15 @@ def dgrad_splits(tiles: int, nk: int) -> int:
     return k_splits(tiles, nk)
 
 
+# the kernels address x / dY / y / residual with 32-bit buffer offsets (csrc/convwg.hip:
+# mx_conv_fwd / mx_conv_dgrad / mx_conv_wgrad reject larger tensors): bigger ones take MIOpen
+_MAX_BYTES = 1 << 31
+
+
+def _fits(*numels: int) -> bool:
+    return all(2 * int(n) < _MAX_BYTES for n in numels)
+
+
 def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, padding=0, dilation=1,
                   res_up: bool = False) -> bool:
     """The implicit-GEMM forward: NHWC bf16, Cout a multiple of 64, Cin of 64, and at least
@@ -175,6 +193,8 @@ def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, paddi
     OW = (IW + 2 * pd - dl * (w.shape[3] - 1) - 1) // st + 1
     rshape = (N, w.shape[0], OH // 2, OW // 2) if res_up else (N, w.shape[0], OH, OW)
     if res_up and (residual is None or OH % 2 or OW % 2):
+        return False
+    if OH <= 0 or OW <= 0 or not _fits(x.numel(), N * OH * OW * w.shape[0]):
         return False
     if residual is not None and not (residual.dtype == torch.bfloat16 and _cl(residual)
                                      and tuple(residual.shape) == rshape
@@ -250,6 +270,11 @@ def dgrad_supported(w: torch.Tensor, x_shape, stride, padding=0, dilation=1) -> 
     N, Cin, IH, IW = x_shape
     st = _sym(stride)
     if st is None or _sym(padding) is None or _sym(dilation) is None:
+        return False
+    pd, dl = _sym(padding), _sym(dilation)
+    OH = (IH + 2 * pd - dl * (w.shape[2] - 1) - 1) // st + 1
+    OW = (IW + 2 * pd - dl * (w.shape[3] - 1) - 1) // st + 1
+    if OH <= 0 or OW <= 0 or not _fits(N * Cin * IH * IW, N * w.shape[0] * OH * OW):
         return False
     if decomposed(w.shape[2], w.shape[3], stride, padding, dilation):
         tiles = (N * (-(-IH // st)) * (-(-IW // st)) + 127) // 128 * (Cin // 128)

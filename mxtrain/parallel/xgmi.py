@@ -437,6 +437,10 @@ class XGMICommunicator:
         timed-out barrier on any rank disables the kernel (prefer = {} -> RCCL)."""
         res = {}
         w = self.world
+        # the (op, size) grid is the same on every rank, so every collective below -- the
+        # RCCL side of each pair and the final max-reductions -- has the same shape everywhere
+        keys = [(op, nb) for op in ("all_reduce", "reduce_scatter", "all_gather") for nb in sizes
+                if nb <= self.max_bytes and nb % (16 * w) == 0]
         ok = True
         try:
             # fail fast: one small all-reduce with a short barrier bound, checked at once --
@@ -450,54 +454,58 @@ class XGMICommunicator:
             finally:
                 self.timeout_s = t_keep
             ok = bool((probe == w * (w + 1) / 2).all().item())
-            ops = ("all_reduce", "reduce_scatter", "all_gather") if ok else ()
-            for op in ops:
-                for nb in sizes:
-                    if nb > self.max_bytes or nb % (16 * w):
-                        continue
-                    n = nb // 4
-                    big = torch.arange(n, device=self.device, dtype=torch.float32).remainder(13)
-                    big.add_(self.rank)
-                    small = big[: n // w].clone()
-                    inp = big if op == "reduce_scatter" else (small if op == "all_gather" else None)
+        except Exception:
+            ok = False
+        # the probe's verdict is collective: with one-sided flag visibility one rank can time
+        # out while its peer passes, and a rank that skipped the timed loop would leave the
+        # peer's RCCL calls below unmatched
+        pflag = torch.tensor([1.0 if ok else 0.0], device=self.device)
+        dist.all_reduce(pflag, op=dist.ReduceOp.MIN, group=self.group)
+        ok = float(pflag.item()) == 1.0
+        try:
+            for op, nb in (keys if ok else ()):
+                n = nb // 4
+                big = torch.arange(n, device=self.device, dtype=torch.float32).remainder(13)
+                big.add_(self.rank)
+                small = big[: n // w].clone()
+                inp = big if op == "reduce_scatter" else (small if op == "all_gather" else None)
 
-                    def fresh():
-                        if op == "all_reduce":
-                            return big.clone()
-                        return torch.empty(n // w if op == "reduce_scatter" else n, device=self.device)
+                def fresh():
+                    if op == "all_reduce":
+                        return big.clone()
+                    return torch.empty(n // w if op == "reduce_scatter" else n, device=self.device)
 
-                    a, b = fresh(), fresh()
-                    self._mine(op, a, inp)
-                    self._rccl(op, b, inp)
+                a, b = fresh(), fresh()
+                self._mine(op, a, inp)
+                self._rccl(op, b, inp)
+                torch.cuda.synchronize(self.device)
+                ok = ok and torch.equal(a, b)
+                times = []
+                for fn in (self._mine, self._rccl):
+                    o = fresh()
+                    for _ in range(2):
+                        fn(op, o, inp)
                     torch.cuda.synchronize(self.device)
-                    ok = ok and torch.equal(a, b)
-                    times = []
-                    for fn in (self._mine, self._rccl):
-                        o = fresh()
-                        for _ in range(2):
-                            fn(op, o, inp)
-                        torch.cuda.synchronize(self.device)
-                        e0 = torch.cuda.Event(enable_timing=True)
-                        e1 = torch.cuda.Event(enable_timing=True)
-                        e0.record()
-                        for _ in range(iters):
-                            fn(op, o, inp)
-                        e1.record()
-                        torch.cuda.synchronize(self.device)
-                        times.append(e0.elapsed_time(e1) / iters)
-                    res[(op, nb)] = times
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(iters):
+                        fn(op, o, inp)
+                    e1.record()
+                    torch.cuda.synchronize(self.device)
+                    times.append(e0.elapsed_time(e1) / iters)
+                res[(op, nb)] = times
             self.check()
         except Exception:
             ok = False
         flag = torch.tensor([0.0 if ok else 1.0], device=self.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
-        keys = sorted(res)
-        tt = torch.tensor([res[k] for k in keys] or [[0.0, 0.0]], device=self.device,
+        tt = torch.tensor([res.get(k, [0.0, 0.0]) for k in keys] or [[0.0, 0.0]], device=self.device,
                           dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=self.group)
         prefer: Dict[str, List] = {"all_reduce": [], "reduce_scatter": [], "all_gather": []}
         self.autotune_ok = float(flag.item()) == 0.0
-        if self.autotune_ok:
+        if self.autotune_ok and keys:
             for k, (tx, tr) in zip(keys, tt.tolist()):
                 prefer[k[0]].append((k[1], tx < tr))
                 res[k] = (tx, tr)
@@ -616,6 +624,33 @@ class XGMIP2P:
             events.append(self.s_recv.record_event())
         return _P2PHandle(events, recv_buf, keep)
 
+    def selftest(self, timeout_s: float = 5.0) -> bool:
+        """Round-trip a known tensor with every peer (both directions at once: sends and
+        receives run on their own streams) under a short wait bound and compare; the verdict
+        is agreed over the group (MIN), so every rank keeps or drops the channels together.
+        Collective: call on every rank of the group, before any real traffic."""
+        ok = True
+        t_keep, self.timeout_s = self.timeout_s, min(self.timeout_s, timeout_s)
+        try:
+            n = min(self.slot_bytes // 4, 4096) // 4 * 4
+            hs = []
+            for p in self.peers:
+                src = torch.arange(n, device=self.device, dtype=torch.float32).add_(1000.0 * self.rank + 7 * p)
+                dst = torch.full((n,), -1.0, device=self.device)
+                hs.append((p, self.post(src, p, dst, p), dst))
+            for p, h, dst in hs:
+                got = h.wait()
+                exp = torch.arange(n, device=self.device, dtype=torch.float32).add_(1000.0 * p + 7 * self.rank)
+                ok = ok and bool(torch.equal(got, exp))
+            self.check()
+        except Exception:
+            ok = False
+        finally:
+            self.timeout_s = t_keep
+        flag = torch.tensor([1.0 if ok else 0.0], device=self.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        return float(flag.item()) == 1.0
+
     def check(self):
         """Raise if a send / receive wait timed out on this rank (synchronises)."""
         torch.cuda.synchronize(self.device)
@@ -651,15 +686,38 @@ def get_p2p(group, device, peers, slot_bytes: int) -> Optional[XGMIP2P]:
         return _P2PS[key]
     if torch.cuda.is_current_stream_capturing():
         return None
-    try:
-        c = XGMIP2P(group, device, peers, slot_bytes,
-                    timeout_s=float(os.environ.get("MXTRAIN_XGMI_TIMEOUT_S", "30")))
-    except XGMIUnavailable as e:
-        if dist.get_rank(group) == 0:
-            print(f"[mxtrain] {e}; pipeline p2p uses RCCL", flush=True)
-        c = None
+    c = None
+    if _single_node(group):
+        try:
+            c = XGMIP2P(group, device, peers, slot_bytes,
+                        timeout_s=float(os.environ.get("MXTRAIN_XGMI_TIMEOUT_S", "30")))
+        except XGMIUnavailable as e:
+            if dist.get_rank(group) == 0:
+                print(f"[mxtrain] {e}; pipeline p2p uses RCCL", flush=True)
+        # validated once against known data (agreed on every rank): a channel whose waits
+        # time out would otherwise leave the receive buffer unwritten and train on garbage
+        if c is not None and not c.selftest():
+            if dist.get_rank(group) == 0:
+                print("[mxtrain] xGMI p2p self-test failed; pipeline p2p uses RCCL", flush=True)
+            c.close()
+            c = None
     _P2PS[key] = c
     return c
+
+
+_NODE: Dict[int, bool] = {}
+
+
+def _single_node(group) -> bool:
+    """Whether every rank of ``group`` runs on this host (collective on first use): the
+    xGMI kernels map peer memory through IPC handles, which exist within one node only."""
+    key = id(group)
+    if key not in _NODE:
+        import socket
+        names: List = [None] * dist.get_world_size(group)
+        dist.all_gather_object(names, socket.gethostname(), group=group)
+        _NODE[key] = len(set(names)) == 1
+    return _NODE[key]
 
 
 _COMMS: Dict[int, Optional[XGMICommunicator]] = {}
@@ -694,6 +752,9 @@ def get_comm(group, device) -> Optional[XGMICommunicator]:
     key = id(group)
     if key in _COMMS:
         return _COMMS[key]
+    if not _single_node(group):
+        _COMMS[key] = None
+        return None
     max_mb = int(os.environ.get("MXTRAIN_XGMI_MAX_MB", "256"))
     try:
         c = XGMICommunicator(group, device, max_bytes=max_mb << 20,
@@ -730,3 +791,4 @@ def destroy_all():
             c.close()
     _COMMS.clear()
     _P2PS.clear()
+    _NODE.clear()

@@ -61,11 +61,14 @@ class DistributedOptimizer:
                  tp_group=None, sp_group=None, mp_group=None, embed_group=None,
                  pp_rank: int = 0, schedule: Optional[LRSchedule] = None,
                  overlap_param_gather: Optional[bool] = None,
-                 grad_scale_world: Optional[int] = None, norm_groups=()):
+                 grad_scale_world: Optional[int] = None, norm_groups=(), force_collectives: bool = False):
         self.flat = flat
         self.dp_group = dp_group
         self.world = dist.get_world_size(dp_group) if dp_group is not None else 1
         self.rank = dist.get_rank(dp_group) if dp_group is not None else 0
+        # sharded path (reduce-scatter / all-gather per bucket) at world > 1; forced on a
+        # one-rank group it runs the same collectives (tests: RCCL inside the step graph)
+        self.sharded = self.world > 1 or (bool(force_collectives) and dp_group is not None)
         self.betas, self.eps, self.wd, self.clip = betas, eps, weight_decay, clip_grad
         # gradients are sum-reduced over dp_group and divided by gs_world (= the number of
         # replicas whose losses are averaged; larger than dp_group for expert parameters)
@@ -85,7 +88,7 @@ class DistributedOptimizer:
             self.slices.append((b, b.start + self.rank * n, off, n))
             off += n
         self.shard_numel = off
-        if self.world == 1:
+        if not self.sharded:
             self.grad_shard = flat.grad
             self.param_shard = flat.data
         else:
@@ -124,7 +127,7 @@ class DistributedOptimizer:
         self.normsq = self._normsq_buf[:1]
         self.step_count = 0
         # ---- overlap bookkeeping
-        self.overlap = overlap and self.world > 1 and dev.type == "cuda"
+        self.overlap = overlap and self.sharded and dev.type == "cuda"
         self.comm_stream = torch.cuda.Stream(device=dev) if self.overlap else None
         self.units_left: Dict[int, int] = {}
         self._bucket_units = {b.index: set(b.units) for b in flat.buckets}
@@ -145,7 +148,7 @@ class DistributedOptimizer:
         # with its forward (bucket by bucket, in forward order); the layers wait on their
         # bucket's event (StepRuntime.before_unit -> wait_unit)
         self.overlap_param_gather = (self.overlap if overlap_param_gather is None
-                                     else bool(overlap_param_gather) and self.world > 1)
+                                     else bool(overlap_param_gather) and self.sharded)
         self.gather_pending = False
         self._gather_events: Dict[int, object] = {}
         self._last_event = None
@@ -158,7 +161,7 @@ class DistributedOptimizer:
     def _refresh_master(self):
         for (_, fs, so, n) in self.slices:
             self.master[so:so + n].copy_(self.flat.data[fs:fs + n].float())
-        if self.world > 1:
+        if self.sharded:
             for (_, fs, so, n) in self.slices:
                 self.param_shard[so:so + n].copy_(self.flat.data[fs:fs + n])
 
@@ -257,7 +260,7 @@ class DistributedOptimizer:
         b = self.flat.buckets[bi]
         if self.pre_reduce is not None:
             self.pre_reduce(bi)
-        if self.world == 1:
+        if not self.sharded:
             self._sp_allreduce(b)
             return
         (_, _, so, n) = self.slices[bi]
@@ -338,7 +341,7 @@ class DistributedOptimizer:
     def gather_params(self):
         """After the update: all-gather the new bf16 shards now, or (overlap mode) mark
         them pending for begin_param_gather() at the next step's start."""
-        if self.world == 1:
+        if not self.sharded:
             return
         if self.overlap_param_gather:
             self.gather_pending = True
@@ -350,7 +353,7 @@ class DistributedOptimizer:
         """Start the parameter all-gather deferred from the previous step
         (overlap_param_gather), per bucket in forward order.  On the GPU it runs on the comm
         stream and records one event per bucket for wait_unit(); on the CPU it runs inline."""
-        gat = self.gather_pending and self.world > 1
+        gat = self.gather_pending and self.sharded
         self.gather_pending = False
         if not gat:
             return
@@ -401,7 +404,7 @@ class DistributedOptimizer:
         # re-materialise bf16 params from the master shard
         for (b, fs, so, n) in self.slices:
             self.param_shard[so:so + n].copy_(self.master[so:so + n].to(self.flat.dtype))
-        if self.world > 1:
+        if self.sharded:
             for (b, fs, so, n) in self.slices:
                 self._ag(self.flat.data[b.start:b.end], self.param_shard[so:so + n])
 

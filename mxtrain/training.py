@@ -50,6 +50,9 @@ class TrainConfig:
     # Linear forward / dgrad GEMMs with fused bias / bias-GeLU / GeLU' epilogues
     # (csrc/gemm_nt.hip); False = hipBLASLt + separate bias-GeLU kernels
     fused_linear: bool = True
+    # run the ZeRO-1 reduce-scatter / all-gather even on a one-rank data group (tests: the
+    # RCCL collectives inside the captured step on one GPU)
+    force_dp_collectives: bool = False
 
 
 class GPTTrainer:
@@ -87,8 +90,11 @@ class GPTTrainer:
         self.eflat = self.eopt = None
         if cfg.num_experts > 1:
             self._setup_moe(cfg, tcfg, ps, dtype, sched)
+        dp_group = ps.grad_group if ps.grad_world > 1 else None
+        if dp_group is None and tcfg.force_dp_collectives and dist.is_initialized():
+            dp_group = dist.group.WORLD
         self.opt = DistributedOptimizer(
-            self.flat, dp_group=ps.grad_group if ps.grad_world > 1 else None, lr=tcfg.lr,
+            self.flat, dp_group=dp_group, lr=tcfg.lr, force_collectives=tcfg.force_dp_collectives,
             betas=(tcfg.adam_beta1, tcfg.adam_beta2), eps=tcfg.adam_eps,
             weight_decay=tcfg.weight_decay, clip_grad=tcfg.clip_grad,
             overlap=tcfg.overlap_grad_reduce, tp_rank=ps.tp_rank, tp_group=ps.tp_group,
@@ -104,7 +110,7 @@ class GPTTrainer:
                 and os.environ.get("MXTRAIN_DEFER_COLREDUCE", "1") != "0"):
             from .ops.norm import ColReduceQueue
             group_of = None
-            if ps.grad_world > 1:
+            if self.opt.sharded:
                 group_of = self.flat.bucket_of_grad_ptr
             self.stage.rt.colq = ColReduceQueue(self.device, group_of=group_of)
             if group_of is not None:
@@ -169,6 +175,23 @@ class GPTTrainer:
             if g is not None and n > 1:
                 self.xgmi_comms[name] = xgmi.get_comm(g, self.device)
 
+    @property
+    def _check_every(self) -> int:
+        """Steps between xGMI error-word checks (0 = never): only when xGMI kernels carry
+        this rank's traffic; each check synchronises the device once."""
+        from .parallel import xgmi
+        if not (xgmi._COMMS or xgmi._P2PS):
+            return 0
+        return int(os.environ.get("MXTRAIN_XGMI_CHECK_EVERY", "100"))
+
+    def check_comms(self) -> None:
+        """Raise if any xGMI collective barrier or p2p wait of this rank timed out since the
+        start (a timed-out kernel leaves its output unwritten: training must not go on)."""
+        from .parallel import xgmi
+        for c in list(xgmi._COMMS.values()) + list(xgmi._P2PS.values()):
+            if c is not None:
+                c.check()
+
     def _sync_initial_params(self):
         ps = self.ps
         # DP replicas start identical (same generator seed per (pp, tp) already); tied
@@ -213,6 +236,8 @@ class GPTTrainer:
         also under context parallelism).  Returns the mean loss over the step as a device
         scalar (last stage; 0 elsewhere)."""
         tokens, labels = self._local(tokens), self._local(labels)
+        if self._check_every and self.iteration and self.iteration % self._check_every == 0:
+            self.check_comms()
         if self._graph is not None:
             self._static[0].copy_(tokens)
             self._static[1].copy_(labels)

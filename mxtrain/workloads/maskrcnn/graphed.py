@@ -16,6 +16,17 @@ whole step is capturable:
 So there is one graph per (batch, canvas) shape -- two for COCO -- captured lazily the
 first time a shape is seen (that step runs eagerly: it also warms MIOpen/BLAS, the
 anchor caches and the momentum buffers, none of which may be created during capture).
+
+Data parallel, the capture decision is collective.  A capturing rank issues a different
+collective sequence than a replaying one (an eager step's bucket all-reduces, a capture
+that records but does not run them, an agreement), so every step starts with a host-side
+handshake on a gloo control group -- one all-reduce MAX of [needs a capture, mask bytes]
+(~0.1 ms of host time, no GPU synchronisation): when ANY rank meets a new shape, every
+rank runs the eager step (the capturing ranks also record their graph), and every rank
+grows the mask buffer to the largest payload together (dropping and recapturing its
+graphs).  Ranks whose orientation sequences differ therefore stay in collective lockstep;
+AspectGroupedSampler additionally gives every rank the same orientation per step, so in
+training the captures happen on the same steps anyway.
 Graphs share one memory pool (they never run concurrently and keep no state between
 replays except the parameters and optimizer buffers, which live outside the pool).
 The learning rate is a device scalar filled before each replay.
@@ -93,6 +104,25 @@ class GraphedTrainStep:
         self.debug = os.environ.get("MXTRAIN_GRAPH_DEBUG", "0") == "1"
         self.marker = None   # diagnostics hook: called around the capture window
         self.graph_info: Dict[tuple, dict] = {}   # per captured shape: node census
+        self.ctrl = self._control_group() if (flat_master is not None and flat_master.world > 1) else None
+        self.handshakes = 0
+        self.regrows = 0
+
+    def _control_group(self):
+        """Host-side control plane for the capture / capacity agreement: the data group
+        itself when it is gloo, else a gloo group over the same ranks (collective call:
+        every rank constructs its GraphedTrainStep at the same point)."""
+        import torch.distributed as dist
+        g = self.fm.group
+        if dist.get_backend(g) == "gloo":
+            return g
+        return dist.new_group(ranks=dist.get_process_group_ranks(g), backend="gloo")
+
+    def _agree(self, vals: List[int], op=None) -> List[int]:
+        import torch.distributed as dist
+        t = torch.tensor(vals, dtype=torch.int64)
+        dist.all_reduce(t, op=op or dist.ReduceOp.MAX, group=self.ctrl)
+        return [int(v) for v in t.tolist()]
 
     def _dbg(self, what: str, key) -> None:
         if self.debug:
@@ -123,6 +153,8 @@ class GraphedTrainStep:
         return dict(zip(LOSS_NAMES, out.unbind(0)))
 
     def _ensure_capacity(self, n: int) -> None:
+        """Grow the mask buffer to hold ``n`` bytes (data parallel: ``n`` is already the
+        MAX over ranks, so every rank grows -- and recaptures -- on the same step)."""
         if n <= self.flat.numel():
             return
         cap = self.flat.numel()
@@ -130,6 +162,7 @@ class GraphedTrainStep:
             cap *= 2
         # the graphs read the old buffer's address: drop them (recaptured on next use)
         self._drop_graphs()
+        self.regrows += 1
         self.flat = torch.zeros(cap, dtype=torch.uint8, device=self.device)
 
     def _drop_graphs(self) -> None:
@@ -149,56 +182,35 @@ class GraphedTrainStep:
 
     def __call__(self, batch: Dict[str, torch.Tensor], lr: float) -> Dict[str, torch.Tensor]:
         flat = batch["gt_mask_flat"]
-        self._ensure_capacity(flat.numel())
         key = tuple(tuple(batch[k].shape) for k in INPUT_KEYS)
+        need_bytes, any_need = flat.numel(), 0
+        if self.ctrl is not None and self.capturable:
+            # collective: [anyone needs a capture, largest mask payload]
+            need = int(self.capturable and (key not in self.graphs or need_bytes > self.flat.numel()))
+            any_need, need_bytes = self._agree([need, need_bytes])
+            self.handshakes += 1
+        self._ensure_capacity(need_bytes)
         cur = torch.cuda.current_stream(self.device)
         self.lr.fill_(lr)
         entry = self.graphs.get(key)
-        if entry is None and not self.capturable:
+        if not self.capturable:
             return self._eager(batch)
+        if self.ctrl is not None and any_need:
+            # capture round: the ranks that meet a new shape capture it, the others run the
+            # same step eagerly (the same collectives); then all agree on the outcome
+            if entry is None:
+                out, err = self._capture(batch, key, cur)
+            else:
+                out, err = self._eager(batch), None
+            import torch.distributed as dist
+            if self._agree([0 if err else 1], op=dist.ReduceOp.MIN)[0] == 0:
+                self._give_up(err or "capture failed on another rank")
+            return out
         if entry is None:
-            st = {k: batch[k].to(self.device, non_blocking=True) for k in INPUT_KEYS}
-            self.flat[:flat.numel()].copy_(flat, non_blocking=True)
-            self.stream.wait_stream(cur)
-            with torch.cuda.stream(self.stream):
-                # eager step with this batch (a real update): warms every lazy cache
-                self.opt.zero_grad(set_to_none=True)
-                out = self._body(st)
-                # capture: grads are allocated inside the graph's pool, never zeroed
-                self.opt.zero_grad(set_to_none=True)
-                g = torch.cuda.CUDAGraph(keep_graph=True)
-                if self.marker is not None:
-                    torch.cuda.synchronize(self.device)
-                    self.marker("capture-begin")
-                err = None
-                try:
-                    with torch.cuda.graph(g, pool=self.pool, stream=self.stream):
-                        sout = self._body(st)
-                    if self.marker is not None:
-                        self.marker("capture-end")
-                    self._finish_capture(g, key)
-                except Exception as e:  # noqa: BLE001 -- fall back to the eager step, loudly
-                    err = repr(e)[:300]
-            cur.wait_stream(self.stream)
-            if self.fm is not None and self.fm.world > 1:
-                # every rank takes the same path: a rank whose capture failed runs eager
-                # collectives that the others would otherwise replay from their graphs
-                import torch.distributed as dist
-                ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=self.device)
-                dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=self.fm.group)
-                if int(ok.item()) == 0 and err is None:
-                    err = "capture failed on another rank"
+            out, err = self._capture(batch, key, cur)
             if err is not None:
-                print(f"[graphed] capture failed, training eagerly: {err}", file=sys.stderr, flush=True)
-                self.capturable = False
-                self.eager_steps += 1
-                return dict(zip(LOSS_NAMES, out.unbind(0)))
-            self.graphs[key] = (g, st, sout)
-            self.captures += 1
-            self._dbg("captured", key)
-            if self.debug:
-                print(f"[graphed] graph {key}: {self.graph_info[key]}", file=sys.stderr, flush=True)
-            return dict(zip(LOSS_NAMES, out.unbind(0)))
+                self._give_up(err)
+            return out
         g, st, sout = entry
         for k in INPUT_KEYS:
             st[k].copy_(batch[k], non_blocking=True)
@@ -208,3 +220,46 @@ class GraphedTrainStep:
         self._dbg("replayed", key)
         # the pool is shared: copy the losses out before another graph can reuse it
         return dict(zip(LOSS_NAMES, sout.clone().unbind(0)))
+
+    def _capture(self, batch, key, cur):
+        """Eager step + capture of this shape -> (losses of the eager step, error or None)."""
+        flat = batch["gt_mask_flat"]
+        st = {k: batch[k].to(self.device, non_blocking=True) for k in INPUT_KEYS}
+        self.flat[:flat.numel()].copy_(flat, non_blocking=True)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            # eager step with this batch (a real update): warms every lazy cache
+            self.opt.zero_grad(set_to_none=True)
+            out = self._body(st)
+            # capture: grads are allocated inside the graph's pool, never zeroed
+            self.opt.zero_grad(set_to_none=True)
+            g = torch.cuda.CUDAGraph(keep_graph=True)
+            if self.marker is not None:
+                torch.cuda.synchronize(self.device)
+                self.marker("capture-begin")
+            err = None
+            try:
+                with torch.cuda.graph(g, pool=self.pool, stream=self.stream):
+                    sout = self._body(st)
+                if self.marker is not None:
+                    self.marker("capture-end")
+                self._finish_capture(g, key)
+            except Exception as e:  # noqa: BLE001 -- fall back to the eager step, loudly
+                err = repr(e)[:300]
+        cur.wait_stream(self.stream)
+        res = dict(zip(LOSS_NAMES, out.unbind(0)))
+        if err is not None:
+            self.eager_steps += 1
+            return res, err
+        self.graphs[key] = (g, st, sout)
+        self.captures += 1
+        self._dbg("captured", key)
+        if self.debug:
+            print(f"[graphed] graph {key}: {self.graph_info[key]}", file=sys.stderr, flush=True)
+        return res, None
+
+    def _give_up(self, err: str) -> None:
+        """Train eagerly from now on (every rank together: the caller agreed on it)."""
+        print(f"[graphed] capture failed, training eagerly: {err}", file=sys.stderr, flush=True)
+        self.capturable = False
+        self._drop_graphs()

@@ -305,7 +305,10 @@ def main(argv=None):
                           mask_format="crops")
     train_coll = functools.partial(collate, short=short, max_size=max_size, fixed_gt=use_graph)
     bs = int(cfg.TRAIN.BATCH_SIZE_PER_GPU)
-    sampler = AspectGroupedSampler(ds, bs, rank, world, seed=42)
+    # one endless loader stream for the whole run (tensorpack's RepeatedData): the workers
+    # and their prefetch queue never drain at a dataset-epoch boundary, and every global
+    # step has one orientation on all ranks
+    sampler = AspectGroupedSampler(ds, bs, rank, world, seed=42, repeat=True)
     nw = int(cfg.DATA.NUM_WORKERS)
     loader = torch.utils.data.DataLoader(ds, batch_sampler=sampler, num_workers=nw, collate_fn=train_coll,
                                          pin_memory=device.type == "cuda", persistent_workers=nw > 0,
@@ -350,25 +353,26 @@ def main(argv=None):
         dmodel = hvd.DistributedDataParallel(model)
     if use_graph:
         from mxtrain.workloads.maskrcnn.graphed import GraphedTrainStep
-        gstep = GraphedTrainStep(model, opt, params, clip, device, flat_master=fm)
+        from mxtrain.data.coco import canvas
+        ch, cw = canvas(short, max_size, 0)
+        # every mask crop lies inside its image: bs x max_gt x canvas bytes bound the packed
+        # payload, so the buffer (and the graphs that read its address) never regrows --
+        # 0.45 GB at 4 img/GPU, sized for 288 GB of HBM
+        gstep = GraphedTrainStep(model, opt, params, clip, device, flat_master=fm,
+                                 flat_capacity=bs * 100 * ch * cw)
         log("Training step runs as a hipGraph (one graph per input shape)")
     max_steps = args.mx_max_steps
     timed_imgs, t_timed = 0, None
     t_wait = t_enq = 0.0
     done = False
+    sampler.set_epoch(start_epoch)
+    it = iter(loader)
     for epoch in range(start_epoch, int(cfg.TRAIN.MAX_EPOCH) + 1):
-        sampler.set_epoch(epoch)
         log(f"Start Epoch {epoch} ...")
         t_ep = time.time()
-        it = iter(loader)
         for k in range(int(cfg.TRAIN.STEPS_PER_EPOCH)):
             t_a = time.time()
-            try:
-                batch = next(it)
-            except StopIteration:
-                sampler.set_epoch(epoch * 1000 + k)
-                it = iter(loader)
-                batch = next(it)
+            batch = next(it)
             t_b = time.time()
             lr = C.lr_at(cfg, step)
             for g in opt.param_groups:
@@ -446,6 +450,8 @@ def main(argv=None):
                                      "packet_capture": os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "runtime default"),
                                      "nodes": [v for v in gstep.graph_info.values()]},
                                     "flat_sgd": fm is not None,
+                                    "loader_wait_ms": round(1e3 * t_wait / max(1, step - args.mx_warmup_steps), 3),
+                                    "host_enqueue_ms": round(1e3 * t_enq / max(1, step - args.mx_warmup_steps), 3),
                                     "dp_routes": sorted(fm.dp_routes) if fm is not None else None}) + "\n")
     hvd.shutdown()
     return 0

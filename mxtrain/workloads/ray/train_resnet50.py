@@ -90,7 +90,7 @@ def train_loop_per_worker(cfg):
     ctx = train.get_context()
     bs = cfg["batch_size"]
     steps = cfg["steps_per_epoch"]
-    ds = SyntheticImageNet(bs * steps * ctx.get_world_size(), seed=cfg.get("seed", 0))
+    ds = SyntheticImageNet(bs * steps * ctx.get_world_size(), seed=cfg.get("seed", 0), size=cfg.get("image_size", 224))
     dl = torch.utils.data.DataLoader(ds, batch_size=bs, shuffle=True, num_workers=cfg.get("num_workers", 4),
                                      drop_last=True, persistent_workers=cfg.get("num_workers", 4) > 0)
     dl = prepare_data_loader(dl)
@@ -113,6 +113,7 @@ def main(argv=None):
     ap.add_argument("--steps-per-epoch", type=int, default=100)
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--loader-workers", type=int, default=4)
+    ap.add_argument("--image-size", type=int, default=224, help="synthetic image side (tests: small)")
     ap.add_argument("--storage-path", default=os.path.join(os.environ.get("HOME", "."), "ray_results"))
     ap.add_argument("--name", default="resnet50")
     ap.add_argument("--result-json", default=None)
@@ -121,7 +122,7 @@ def main(argv=None):
     trainer = TorchTrainer(train_loop_per_worker,
                            train_loop_config={"batch_size": a.batch_size, "epochs": a.epochs,
                                               "steps_per_epoch": a.steps_per_epoch, "lr": a.lr,
-                                              "num_workers": a.loader_workers},
+                                              "num_workers": a.loader_workers, "image_size": a.image_size},
                            scaling_config=ScalingConfig(num_workers=a.num_workers, use_gpu=use_gpu),
                            run_config=RunConfig(name=a.name, storage_path=a.storage_path))
     result = trainer.fit()

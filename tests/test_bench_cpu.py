@@ -14,7 +14,7 @@ def test_bench_two_ranks_gloo_json_line():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(REPO, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--model", "gpt-tiny", "--no-maskrcnn",
-           "--no-tuned-gemm"]
+           "--no-tuned-gemm", "--no-extra-configs"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -25,6 +25,8 @@ def test_bench_two_ranks_gloo_json_line():
         assert k in d, k
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
     assert d["config"]["parallelism"].startswith("dp2") and d["value"] > 0
+    # N > 1 default: xGMI autotune mode; on the CPU the collectives are gloo's
+    assert d["config"]["xgmi_mode"] == "auto" and d["config"]["collectives"] == "gloo", d["config"]
     # whole-job tokens/s: global batch x seq / step time
     tok = d["config"]["global_batch"] * d["config"]["seq_len"]
     assert abs(d["value"] - tok / (d["ms_per_step"] / 1000.0)) / d["value"] < 0.01
@@ -42,7 +44,7 @@ def test_bench_two_ranks_gloo_maskrcnn_fields(tmp_path):
            "--master-addr", "127.0.0.1", "--master-port", "29537", os.path.join(REPO, "bench.py"),
            "--gpus", "2", "--steps", "1", "--warmup", "1", "--model", "gpt-tiny", "--no-tuned-gemm",
            "--maskrcnn-batches", "1", "--maskrcnn-steps", "2:1", "--maskrcnn-workers", "0",
-           "--maskrcnn-args", small]
+           "--maskrcnn-args", small, "--no-extra-configs"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -52,3 +54,26 @@ def test_bench_two_ranks_gloo_maskrcnn_fields(tmp_path):
     assert d["maskrcnn_img_s_1img"] and d["maskrcnn_img_s_1img"] > 0, d.get("maskrcnn_config")
     mc = d["maskrcnn_config"]
     assert mc["n_gpus"] == 2 and mc["1img"]["n_gpus"] == 2 and mc["parallelism"].startswith("dp2")
+
+
+def test_bench_two_ranks_gloo_extra_config_fields():
+    """BASELINE configs 4 and 5 in the bench line: the GPT-3 phase (a fresh N-rank child job:
+    here a tiny GPT through the same --tp / --pp layout rule, TP2 at N = 2) and the
+    Ray-Train ResNet-50 phase (rank 0's launcher with N workers; here small CPU images)."""
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29541", os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "1", "--model", "gpt-tiny", "--no-tuned-gemm",
+           "--no-maskrcnn", "--extra-steps", "2:1", "--resnet-steps", "5",
+           "--gpt3-args", "--model gpt-tiny --no-tuned-gemm",
+           "--resnet-args", "--cpu --batch-size 2 --image-size 64 --loader-workers 0"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["gpt3_6.7b_tok_s"] and d["gpt3_6.7b_tok_s"] > 0, (d.get("gpt3_6.7b_config"), r.stderr[-2000:])
+    g = d["gpt3_6.7b_config"]
+    assert g["n_gpus"] == 2 and g["parallelism"].startswith("dp1_tp2"), g
+    assert d["resnet50_img_s"] and d["resnet50_img_s"] > 0, (d.get("resnet50_config"), r.stderr[-2000:])
+    assert d["resnet50_config"]["workers"] == 2

@@ -396,3 +396,38 @@ def test_rpn_level_canvas_matches_per_level(shapes):
     for a, b in zip(res[False], res[True]):
         assert a.shape == b.shape
         torch.testing.assert_close(a, b, rtol=0, atol=1e-10)
+
+
+def test_sampler_global_step_orientation_lockstep(tmp_path):
+    """Every global step has ONE orientation on all ranks (graphed.py captures a new canvas
+    shape on every rank together), ranks draw disjoint images, and the endless stream
+    (repeat=True) crosses epochs with the epoch folded into the indices."""
+    from mxtrain.data.coco import AspectGroupedSampler, COCODetection, DetectionDataset
+    from mxtrain.data.coco_synth import write_split
+    write_split(str(tmp_path), "train2017", 40, 0, 1)
+    ds = DetectionDataset(COCODetection(str(tmp_path), "coco_train2017"), 256, 384)
+    n = len(ds)
+    orients = {ds.orientation(i) for i in range(n)}
+    assert orients == {0, 1}
+    for world, bs in ((2, 1), (2, 2), (4, 1)):
+        streams = [AspectGroupedSampler(ds, bs, r, world, seed=42, repeat=True) for r in range(world)]
+        its = [iter(s) for s in streams]
+        per_epoch = len(streams[0])
+        seen = set()
+        for step in range(3 * per_epoch):
+            bl = [next(it) for it in its]
+            o = {ds.orientation(i % n) for b in bl for i in b}
+            assert len(o) == 1, (world, bs, step, bl)
+            flat = [i for b in bl for i in b]
+            assert len(flat) == len(set(flat)) == world * bs
+            if step < per_epoch:
+                assert all(i < n for i in flat)
+                seen.update(flat)
+            else:
+                assert all(i >= n * (step // per_epoch) for i in flat)
+        # an epoch covers all but the remainder batches of each orientation
+        assert len(seen) >= n - 2 * world * bs
+        # the finite (default) iterator yields exactly one epoch
+        assert len(list(AspectGroupedSampler(ds, bs, 0, world, seed=42))) == per_epoch
+    # the dataset maps a folded index back (epoch 2, image 3)
+    assert ds[2 * n + 3]["image_id"] == ds[3]["image_id"]
