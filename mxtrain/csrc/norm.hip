@@ -19,7 +19,7 @@ using namespace mx;
 
 namespace {
 
-template <int NV, bool RMS, bool HAS_BDA>
+template <int NV, bool RMS, bool HAS_BDA, int R = 1>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const uint16_t* __restrict__ x,        // [rows, cols]  (GEMM output if HAS_BDA)
     const uint16_t* __restrict__ bias,     // [cols] or null
@@ -31,10 +31,12 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     int rows, int cols, float eps, uint32_t thresh, float keep_scale,
     const uint32_t* __restrict__ seed_ptr, uint32_t salt, uint64_t elem0) {
   const int lane = threadIdx.x & 63;
-  const int row = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (row >= rows) return;
+  // R rows per wave: rows w, w + nw, ... (nw = waves in the grid); all R rows' loads are
+  // issued before any math, so each wave has R rows of reads in flight
+  const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int nw = gridDim.x * 4;
+  if (w >= rows) return;
   const uint32_t seed = HAS_BDA && seed_ptr ? (*seed_ptr + salt) : 0u;
-  const size_t base = (size_t)row * cols;
   // Every load of the row (x, bias, residual, gamma, beta) is issued before any math:
   // one memory round trip per row instead of one per 512-column vector plus one for the
   // affine parameters.  Columns are clamped into the row and the loads unconditional;
@@ -42,20 +44,29 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   // optional operands are zeroed through masks the optimiser cannot see through (a
   // `bias ? load : 0` select became a branch around a load issued last).
   constexpr bool EARLY = NV <= 4;  // wider rows load the affine parameters at use
-  uint4 xr[NV], br[NV], rr[NV], gr[NV], er[NV];
+  uint4 xr[R][NV], rr[R][NV], br[NV], gr[NV], er[NV];
   const uint16_t* bsrc = bias ? bias : gamma;
   const uint16_t* rsrc = residual ? residual : x;
   const uint16_t* esrc = beta ? beta : gamma;
   uint32_t bm = bias ? ~0u : 0u, rmk = residual ? ~0u : 0u, em = beta ? ~0u : 0u;
   asm volatile("" : "+v"(bm), "+v"(rmk), "+v"(em));
 #pragma unroll
+  for (int k = 0; k < R; ++k) {
+    // rows past the end reload the wave's own first row (its cache lines), never a
+    // shared clamp row
+    const int rl = (w + k * nw < rows) ? w + k * nw : w;
+    const size_t b_ = (size_t)rl * cols;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = min((lane + 64 * i) * 8, cols - 8);
+      xr[k][i] = *reinterpret_cast<const uint4*>(x + b_ + c);
+      if constexpr (HAS_BDA) rr[k][i] = *reinterpret_cast<const uint4*>(rsrc + b_ + c);
+    }
+  }
+#pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = min((lane + 64 * i) * 8, cols - 8);
-    xr[i] = *reinterpret_cast<const uint4*>(x + base + c);
-    if constexpr (HAS_BDA) {
-      br[i] = *reinterpret_cast<const uint4*>(bsrc + c);
-      rr[i] = *reinterpret_cast<const uint4*>(rsrc + base + c);
-    }
+    if constexpr (HAS_BDA) br[i] = *reinterpret_cast<const uint4*>(bsrc + c);
     if constexpr (EARLY) {
       gr[i] = *reinterpret_cast<const uint4*>(gamma + c);
       if constexpr (!RMS) er[i] = *reinterpret_cast<const uint4*>(esrc + c);
@@ -65,69 +76,75 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   auto and4 = [](uint4 a, uint32_t m) __attribute__((always_inline)) {
     return make_uint4(a.x & m, a.y & m, a.z & m, a.w & m);
   };
-  float v[NV][8];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = (lane + 64 * i) * 8;
-    const bool ok = c < cols;
-    unpack8(xr[i], v[i]);
-    if constexpr (HAS_BDA) {
-      float b[8], r[8];
-      unpack8(and4(br[i], bm), b);
-      unpack8(and4(rr[i], rmk), r);
-      bool km[8];
-      if (thresh) dropout_keep8(elem0 + base + c, seed, thresh, km);
+  for (int k = 0; k < R; ++k) {
+    const int row = w + k * nw;
+    if (row >= rows) break;
+    const size_t base = (size_t)row * cols;
+    float v[NV][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float t = v[i][j] + b[j];
-        if (thresh) t = km[j] ? t * keep_scale : 0.f;
-        v[i][j] = r[j] + t;
+    for (int i = 0; i < NV; ++i) {
+      const int c = (lane + 64 * i) * 8;
+      const bool ok = c < cols;
+      unpack8(xr[k][i], v[i]);
+      if constexpr (HAS_BDA) {
+        float b[8], r[8];
+        unpack8(and4(br[i], bm), b);
+        unpack8(and4(rr[k][i], rmk), r);
+        bool km[8];
+        if (thresh) dropout_keep8(elem0 + base + c, seed, thresh, km);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float t = v[i][j] + b[j];
+          if (thresh) t = km[j] ? t * keep_scale : 0.f;
+          v[i][j] = r[j] + t;
+        }
+        // the residual stream is stored in bf16; normalise the rounded value so that
+        // backward (which re-reads h_out) sees exactly the forward's input
+        uint4 packed = pack8(v[i]);
+        if (ok) *reinterpret_cast<uint4*>(h_out + base + c) = packed;
+        unpack8(packed, v[i]);
       }
-      // the residual stream is stored in bf16; normalise the rounded value so that
-      // backward (which re-reads h_out) sees exactly the forward's input
-      uint4 packed = pack8(v[i]);
-      if (ok) *reinterpret_cast<uint4*>(h_out + base + c) = packed;
-      unpack8(packed, v[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = ok ? v[i][j] : 0.f;
+    }
+    float mean = 0.f;
+    if constexpr (!RMS) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[i][j];
+      mean = wave_sum(s) / (float)cols;
+    }
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const bool ok = (lane + 64 * i) * 8 < cols;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { float d = v[i][j] - mean; ss += ok ? d * d : 0.f; }
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / (float)cols + eps);
+    if (lane == 0) {
+      if (!RMS) mean_out[row] = mean;
+      rstd_out[row] = rstd;
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[i][j] = ok ? v[i][j] : 0.f;
-  }
-  float mean = 0.f;
-  if constexpr (!RMS) {
-    float s = 0.f;
+    for (int i = 0; i < NV; ++i) {
+      const int c = (lane + 64 * i) * 8;
+      if (!EARLY && c >= cols) continue;
+      const int cc = min(c, cols - 8);
+      float g[8], bt[8], o[8];
+      unpack8(EARLY ? gr[i] : *reinterpret_cast<const uint4*>(gamma + cc), g);
+      if constexpr (!RMS) unpack8(and4(EARLY ? er[i] : *reinterpret_cast<const uint4*>(esrc + cc), em), bt);
+      else {
 #pragma unroll
-    for (int i = 0; i < NV; ++i)
+        for (int j = 0; j < 8; ++j) bt[j] = 0.f;
+      }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += v[i][j];
-    mean = wave_sum(s) / (float)cols;
-  }
-  float ss = 0.f;
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const bool ok = (lane + 64 * i) * 8 < cols;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { float d = v[i][j] - mean; ss += ok ? d * d : 0.f; }
-  }
-  const float rstd = rsqrtf(wave_sum(ss) / (float)cols + eps);
-  if (lane == 0) {
-    if (!RMS) mean_out[row] = mean;
-    rstd_out[row] = rstd;
-  }
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = (lane + 64 * i) * 8;
-    if (!EARLY && c >= cols) continue;
-    const int cc = min(c, cols - 8);
-    float g[8], bt[8], o[8];
-    unpack8(EARLY ? gr[i] : *reinterpret_cast<const uint4*>(gamma + cc), g);
-    if constexpr (!RMS) unpack8(and4(EARLY ? er[i] : *reinterpret_cast<const uint4*>(esrc + cc), em), bt);
-    else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) bt[j] = 0.f;
+      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + bt[j];
+      if (c < cols) *reinterpret_cast<uint4*>(y + base + c) = pack8(o);
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + bt[j];
-    if (c < cols) *reinterpret_cast<uint4*>(y + base + c) = pack8(o);
   }
 }
 
@@ -138,7 +155,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
 // (4-way LDS atomics, once per column).  Wider rows use per-row LDS atomics.
 // COLS=false: row-wise part only (dh, dx); the column sums of wide rows come from
 // ln_bwd_cols_kernel instead (per-element LDS atomics made cols >= 2560 ~10x slower).
-template <int NV, bool RMS, bool REG, bool COLS = true>
+template <int NV, bool RMS, bool REG, bool COLS = true, int G = (NV <= 2 ? 4 : (NV <= 4 ? 2 : 1))>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dres,
     const uint16_t* __restrict__ h, const float* __restrict__ mean_in,
@@ -177,7 +194,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   // one-row-ahead prefetch left only one row in flight at every wait).  Addresses are
   // clamped into the tensor and the loads unconditional: a `cond ? load : 0` select makes
   // the compiler wait for the load right where it is issued.
-  constexpr int G = NV <= 2 ? 4 : (NV <= 4 ? 2 : 1);
+  // G is the launch's rows per wave when that is smaller (a group wider than the wave's
+  // share loaded clamped duplicates of the LAST row: every wave of the grid hammering the
+  // same few cache lines)
   const uint16_t* rsrc = dres ? dres : h;
   // residual-gradient mask, opaque to the optimiser: `dres ? load : 0` was turned into a
   // branch around the load, issued last and waited for with vmcnt(0) before row 0's math
@@ -459,6 +478,8 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(
   for (int j = 0; j < 8; ++j) o[j] = acc[j];
 }
 
+int kFwdRowsPerWave = 1;   // rows per wave of the forward (1 or 2)
+
 template <bool RMS, bool BDA>
 hipError_t launch_fwd(const void* x, const void* bias, const void* residual,
                       const void* gamma, const void* beta, void* h_out, void* y,
@@ -468,14 +489,24 @@ hipError_t launch_fwd(const void* x, const void* bias, const void* residual,
   const int nv = (cols + 511) / 512;
   const uint32_t thresh = p > 0.f ? (uint32_t)((double)p * 4294967296.0) : 0u;
   const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  dim3 grid((rows + 3) / 4), block(256);
+  const int R = (nv <= 2 && kFwdRowsPerWave >= 2) ? 2 : 1;
+  dim3 grid((rows + 4 * R - 1) / (4 * R)), block(256);
 #define MX_LN_CASE(N)                                                                  \
   case N:                                                                              \
-    hipLaunchKernelGGL((ln_fwd_kernel<N, RMS, BDA>), grid, block, 0, s,                \
-                       (const uint16_t*)x, (const uint16_t*)bias,                      \
-                       (const uint16_t*)residual, (const uint16_t*)gamma,              \
-                       (const uint16_t*)beta, (uint16_t*)h_out, (uint16_t*)y, mean,    \
-                       rstd, rows, cols, eps, thresh, ks, seed, salt, elem0);          \
+    if (R == 2) {                                                                      \
+      if constexpr ((N) <= 2)                                                          \
+        hipLaunchKernelGGL((ln_fwd_kernel<N, RMS, BDA, 2>), grid, block, 0, s,         \
+                           (const uint16_t*)x, (const uint16_t*)bias,                  \
+                           (const uint16_t*)residual, (const uint16_t*)gamma,          \
+                           (const uint16_t*)beta, (uint16_t*)h_out, (uint16_t*)y, mean, \
+                           rstd, rows, cols, eps, thresh, ks, seed, salt, elem0);      \
+    } else {                                                                           \
+      hipLaunchKernelGGL((ln_fwd_kernel<N, RMS, BDA, 1>), grid, block, 0, s,           \
+                         (const uint16_t*)x, (const uint16_t*)bias,                    \
+                         (const uint16_t*)residual, (const uint16_t*)gamma,            \
+                         (const uint16_t*)beta, (uint16_t*)h_out, (uint16_t*)y, mean,  \
+                         rstd, rows, cols, eps, thresh, ks, seed, salt, elem0);        \
+    }                                                                                  \
     break;
   switch (nv) {
     MX_LN_CASE(1) MX_LN_CASE(2) MX_LN_CASE(3) MX_LN_CASE(4) MX_LN_CASE(5)
@@ -536,10 +567,11 @@ constexpr int kColsRowsPerBlock = 32;
 // scripts/ln_ab.py: 16.0 us at 2, 17.2 at 4, 16.2 at 1 -- with load groups, two waves per
 // SIMD hide each other's dropout-hash VALU better than the halved partials save)
 int kBwdRowsPerWave = 2;
+int kBwdMaxBlocks = 512;   // partial slabs: [blocks][3][cols] fp32
 int bwd_grid(int rows) {
   const int rpb = 4 * kBwdRowsPerWave;
   int g = (rows + rpb - 1) / rpb;
-  if (g > 512) g = 512;
+  if (g > kBwdMaxBlocks) g = kBwdMaxBlocks;
   if (g < 1) g = 1;
   return g;
 }
@@ -580,13 +612,18 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
     return hipGetLastError();
   }
   const size_t lds = (size_t)(nv <= 4 ? 12 : 3) * cols * sizeof(float);
-#define MX_LNB_CASE(N)                                                                 \
-  case N:                                                                              \
-    hipLaunchKernelGGL((ln_bwd_kernel<N, RMS, (N <= 4)>), grid, block, lds, s,         \
+  const int rpw = (rows + grid.x * 4 - 1) / (grid.x * 4);   // rows per wave of this launch
+#define MX_LNB_LAUNCH(N, GG)                                                           \
+    hipLaunchKernelGGL((ln_bwd_kernel<N, RMS, (N <= 4), true, GG>), grid, block, lds, s, \
                        (const uint16_t*)dy, (const uint16_t*)dres, (const uint16_t*)h, \
                        mean, rstd, (const uint16_t*)gamma, (uint16_t*)dh_out,          \
                        (uint16_t*)dx_drop, partial, rows, cols, thresh, ks, seed,      \
-                       salt, elem0);                                                   \
+                       salt, elem0);
+#define MX_LNB_CASE(N)                                                                 \
+  case N:                                                                              \
+    if ((N) <= 2 && rpw >= 4) { MX_LNB_LAUNCH(N, 4) }                                  \
+    else if ((N) <= 4 && rpw >= 2) { MX_LNB_LAUNCH(N, 2) }                             \
+    else { MX_LNB_LAUNCH(N, 1) }                                                       \
     break;
   switch (nv) {
     MX_LNB_CASE(1) MX_LNB_CASE(2) MX_LNB_CASE(3) MX_LNB_CASE(4) MX_LNB_CASE(5)
@@ -594,6 +631,7 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
     default: return hipErrorInvalidValue;
   }
 #undef MX_LNB_CASE
+#undef MX_LNB_LAUNCH
   return hipGetLastError();
 }
 
@@ -605,6 +643,18 @@ MX_EXPORT int mx_norm_bwd_nparts(int rows) { return bwd_grid(rows); }
 MX_EXPORT int mx_norm_bwd_rows_per_wave(int r) {
   const int old = kBwdRowsPerWave;
   if (r > 0) kBwdRowsPerWave = r;
+  return old;
+}
+// rows per wave of the norm forward (1, or 2 for rows <= 1024 columns); returns the old value
+MX_EXPORT int mx_norm_fwd_rows_per_wave(int r) {
+  const int old = kFwdRowsPerWave;
+  if (r > 0) kFwdRowsPerWave = r;
+  return old;
+}
+// cap on the fused backward's workgroups (= partial slabs); returns the old value
+MX_EXPORT int mx_norm_bwd_max_blocks(int b) {
+  const int old = kBwdMaxBlocks;
+  if (b > 0) kBwdMaxBlocks = b;
   return old;
 }
 // rows wider than this use the split (row + column) backward; returns the old value

@@ -591,7 +591,7 @@ def test_dropmask_layers_match_per_layer_calls(monkeypatch):
 
 
 # ------------------------------------------------------------------ forward / dgrad GEMMs
-NT_VARIANTS = list(range(9))
+NT_VARIANTS = list(range(13))   # 9-12: two k-groups per workgroup (intra-workgroup split-K)
 
 
 @pytest.mark.parametrize("variant", NT_VARIANTS)
@@ -615,7 +615,7 @@ def test_gemm_nt_forward_epilogues(variant, epi):
         _close(out, ref, 2e-2, 1e-2, "y")
 
 
-@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("gelu", [False, True])
 def test_gemm_nt_dgrad_epilogues(variant, gelu):
     """dgrad dx = dy w (w K-major) and the fused GeLU' + bias-gradient epilogue."""
