@@ -166,32 +166,20 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
     for (int u = 0; u < FN; ++u) acc[a][u] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const uint32_t lds0 = lds_addr(smem);
-  // prep(): the step's LDS bases and per-piece source offsets, then the walk advances;
-  // piece(j) issues one of them.  In the main loop the pieces are spread over the step's
-  // MFMA groups (the forward's scheme: no burst of LDS-DMA issues after the barrier)
-  uint32_t p_b0 = 0, p_b1 = 0, p_ya[PA], p_xb[PB];
-  auto prep = [&](int slot) __attribute__((always_inline)) {   // steps prepared in order
-    p_b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
-    p_b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
+  auto issue = [&](int slot, int) __attribute__((always_inline)) {   // steps issued in order
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
+    const uint32_t b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
 #pragma unroll
-    for (int j = 0; j < PA; ++j) p_ya[j] = ya[j];
+    for (int j = 0; j < PA; ++j) dma16_buf(yres, ya[j], b0 + j * 1024);
 #pragma unroll
-    for (int j = 0; j < PB; ++j) p_xb[j] = boffB(j);
+    for (int j = 0; j < PB; ++j) dma16_buf(xres, boffB(j), b1 + j * 1024);
     advance();
-  };
-  auto piece = [&](int j) __attribute__((always_inline)) {
-    if (j < PA) dma16_buf(yres, p_ya[j], p_b0 + j * 1024);
-    else dma16_buf(xres, p_xb[j - PA], p_b1 + (j - PA) * 1024);
   };
   constexpr int PER = PA + PB;
 
 #pragma unroll
   for (int q = 0; q < NSLOT - 1; ++q)
-    if (q < nk) {
-      prep(q);
-#pragma unroll
-      for (int j = 0; j < PER; ++j) piece(j);
-    }
+    if (q < nk) issue(q, q);
   int slot = 0;
   for (int it = 0; it < nk; ++it) {
     const int later = nk - 1 - it;
@@ -200,11 +188,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
     else if (NSLOT >= 3 && later >= 1) vm_wait<(NSLOT >= 3 ? 1 : 0) * PER>();
     else vm_wait<0>();
     __builtin_amdgcn_s_barrier();
-    const bool fetch = it + NSLOT - 1 < nk;
-    if (fetch) {
+    if (it + NSLOT - 1 < nk) {
       int ns = slot + NSLOT - 1;
       if (ns >= NSLOT) ns -= NSLOT;
-      prep(ns);
+      issue(ns, it + NSLOT - 1);
     }
     const char* As = smem + slot * SLOT;
     const char* Bs = As + IA;
@@ -216,13 +203,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
         b[u] = cat(tr_read(Bs, offB[u] + 32 * RB * kk), tr_read(Bs, offB[u] + 32 * RB * kk + 4 * RB));
 #pragma unroll
       for (int a = 0; a < FM; ++a) {
-        {
-          constexpr int NG = (BKT / 32) * FM;
-          const int grp = kk * FM + a;
-#pragma unroll
-          for (int j = 0; j < PER; ++j)
-            if (fetch && j * NG / PER == grp) piece(j);
-        }
         const bf16x8 av = cat(tr_read(As, offA[a] + 32 * RA * kk), tr_read(As, offA[a] + 32 * RA * kk + 4 * RA));
 #pragma unroll
         for (int u = 0; u < FN; ++u) acc[a][u] = mfma16(av, b[u], acc[a][u]);
@@ -366,45 +346,32 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
   int k_ci = kb % cp.cib, k_tap = kb / cp.cib;
   int k_r = k_tap / cp.KW, k_c = k_tap - (k_tap / cp.KW) * cp.KW;
   int k_toff = (k_r * cp.IW + k_c) * cp.dil * cp.ldx;
-  // one K-step's DMA: prep() advances the walk and fixes the step's bases, piece(j) issues
-  // piece j (A pieces first).  In the main loop the pieces of step it + NSLOT - 1 are spread
-  // over step it's MFMA groups, one per group: a burst of PER LDS-DMA issues right after the
-  // barrier held the wave's issue slot for most of a K-step's MFMA time (gemm_nt.hip)
-  int p_tap = 0, p_delta = 0;
-  uint32_t p_b0 = 0, p_b1 = 0;
-  const uint16_t* p_wb = cp.w;
-  auto prep = [&](int slot) __attribute__((always_inline)) {
-    p_tap = k_tap;
-    const int ci0 = k_ci * BKT;
-    p_delta = k_toff + ci0;
+  auto issue = [&](int slot, int) __attribute__((always_inline)) {
+    const int tap = k_tap, ci0 = k_ci * BKT;
+    const int delta = k_toff + ci0;
     if (++k_ci == cp.cib) {
       k_ci = 0;
       ++k_tap;
       k_toff += cp.dil * cp.ldx;
       if (++k_c == cp.KW) { k_c = 0; k_toff += (cp.IW - cp.KW) * cp.dil * cp.ldx; }
     }
-    p_b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
-    p_b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
-    p_wb = cp.w + (size_t)p_tap * cp.Cin + ci0;
-  };
-  auto piece = [&](int j) __attribute__((always_inline)) {
-    if (j < PA) {
-      const bool in = (amask[j] >> p_tap) & 1u;
-      dma16_buf(xres, in ? (uint32_t)(aoff[j] + p_delta) * 2u : kOOB, p_b0 + j * 1024);
-    } else {
-      dma16_sbase(p_wb, boff[j - PA], p_b1 + (j - PA) * 1024);
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
+    const uint32_t b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const bool in = (amask[j] >> tap) & 1u;
+      dma16_buf(xres, in ? (uint32_t)(aoff[j] + delta) * 2u : kOOB, b0 + j * 1024);
     }
+    const uint16_t* wb = cp.w + (size_t)tap * cp.Cin + ci0;
+#pragma unroll
+    for (int j = 0; j < PB; ++j) dma16_sbase(wb, boff[j], b1 + j * 1024);
   };
 
   // NSLOT-deep LDS-DMA ring, counted waits (the input gradient's scheme): with NSLOT > 2 the
   // next steps' pieces stay in flight across the barrier
 #pragma unroll
   for (int q = 0; q < NSLOT - 1; ++q)
-    if (q < nk) {
-      prep(q);
-#pragma unroll
-      for (int j = 0; j < PER; ++j) piece(j);
-    }
+    if (q < nk) issue(q, q);
   int slot = 0;
   for (int it = 0; it < nk; ++it) {
     const int later = nk - 1 - it;
@@ -412,11 +379,10 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
     else if (NSLOT >= 3 && later >= 1) vm_wait<(NSLOT >= 3 ? 1 : 0) * PER>();
     else vm_wait<0>();
     __builtin_amdgcn_s_barrier();
-    const bool fetch = it + NSLOT - 1 < nk;
-    if (fetch) {
+    if (it + NSLOT - 1 < nk) {
       int ns = slot + NSLOT - 1;
       if (ns >= NSLOT) ns -= NSLOT;
-      prep(ns);
+      issue(ns, it + NSLOT - 1);
     }
     const char* As = smem + slot * SLOT;
     const char* Bs = As + IA;
@@ -428,11 +394,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
 #pragma unroll
       for (int a = 0; a < FM; ++a) {
         const bf16x8 av = lds_read8(As, offA + 16 * a * R + cK[kk]);
-        constexpr int NG = (BKT / 32) * FM;   // MFMA groups per K-step
-        const int grp = kk * FM + a;
-#pragma unroll
-        for (int j = 0; j < PER; ++j)
-          if (fetch && j * NG / PER == grp) piece(j);
         // the weight fragment is the A operand: a lane ends with 4 consecutive output
         // channels of one pixel (epilogue below)
 #pragma unroll
@@ -691,40 +652,30 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
     return -((k_r * cp.dil / cp.stride) * cp.OW + k_c * cp.dil / cp.stride) * cp.ldy;
   };
   int k_toff = tap_off();
-  // prep / piece: the forward's spread DMA issue (one piece per MFMA group of the step before)
-  int p_tap = 0, p_delta = 0;
-  uint32_t p_b0 = 0, p_b1 = 0;
-  const uint16_t* p_wb = cp.w;
-  auto prep = [&](int slot) __attribute__((always_inline)) {
-    p_tap = k_tap;
-    const int co0 = k_co * BKT;
-    p_delta = k_toff + co0;
+  auto issue = [&](int slot, int) __attribute__((always_inline)) {
+    const int tap = k_tap, co0 = k_co * BKT;
+    const int delta = k_toff + co0;
     if (++k_co == cp.cob) {
       k_co = 0;
       ++k_tap;
       if (++k_c == cp.KW) { k_c = 0; ++k_r; }
       k_toff = tap_off();
     }
-    p_b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
-    p_b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
-    p_wb = cp.w + (size_t)co0 * ldw + (size_t)p_tap * cp.Cin;
-  };
-  auto piece = [&](int j) __attribute__((always_inline)) {
-    if (j < PA) {
-      const bool in = (amask[j] >> p_tap) & 1u;
-      dma16_buf(yres, in ? (uint32_t)(aoff[j] + p_delta) * 2u : kOOB, p_b0 + j * 1024);
-    } else {
-      dma16_sbase(p_wb, boff[j - PA], p_b1 + (j - PA) * 1024);
+    const uint32_t b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
+    const uint32_t b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const bool in = (amask[j] >> tap) & 1u;
+      dma16_buf(yres, in ? (uint32_t)(aoff[j] + delta) * 2u : kOOB, b0 + j * 1024);
     }
+    const uint16_t* wb = cp.w + (size_t)co0 * ldw + (size_t)tap * cp.Cin;
+#pragma unroll
+    for (int j = 0; j < PB; ++j) dma16_sbase(wb, boff[j], b1 + j * 1024);
   };
 
 #pragma unroll
   for (int q = 0; q < NSLOT - 1; ++q)
-    if (q < nk) {
-      prep(q);
-#pragma unroll
-      for (int j = 0; j < PER; ++j) piece(j);
-    }
+    if (q < nk) issue(q, q);
   int slot = 0;
   for (int it = 0; it < nk; ++it) {
     const int later = nk - 1 - it;
@@ -732,11 +683,10 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
     else if (NSLOT >= 3 && later >= 1) vm_wait<(NSLOT >= 3 ? 1 : 0) * PER>();
     else vm_wait<0>();
     __builtin_amdgcn_s_barrier();
-    const bool fetch = it + NSLOT - 1 < nk;
-    if (fetch) {
+    if (it + NSLOT - 1 < nk) {
       int ns = slot + NSLOT - 1;
       if (ns >= NSLOT) ns -= NSLOT;
-      prep(ns);
+      issue(ns, it + NSLOT - 1);
     }
     const char* As = smem + slot * SLOT;
     const char* Bs = As + IA;
@@ -748,13 +698,6 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
         b[u] = cat(tr_read(Bs, offB[u] + 32 * RB * kk), tr_read(Bs, offB[u] + 32 * RB * kk + 4 * RB));
 #pragma unroll
       for (int a = 0; a < FM; ++a) {
-        {
-          constexpr int NG = (BKT / 32) * FM;
-          const int grp = kk * FM + a;
-#pragma unroll
-          for (int j = 0; j < PER; ++j)
-            if (fetch && j * NG / PER == grp) piece(j);
-        }
         const bf16x8 av = lds_read8(As, offA + 16 * a * RA + cA[kk]);
         // weight fragment as the A operand: 4 consecutive input channels per lane
 #pragma unroll
