@@ -296,6 +296,77 @@ __global__ __launch_bounds__(256) void flash_dropmask_kernel(
   }
 }
 
+// The same images from a fixed grid of waves that walk the LIVE 64x64 groups of every
+// (layer, batch x head) -- a causal mask has NB2 (NB2 + 1) / 2 of NB2^2 -- instead of one
+// 4-wave workgroup per (query group, 4 key groups, layer x head): that grid launched ~98k
+// workgroups per GPT-2 step, half of them dead above the diagonal, each running ~600
+// instructions -- dispatch-bound at ~3x the VALU time of the hashing (312 us per step,
+// profiles/r4_s1/gpt2_kernel_table.txt).  Bit-identical images: the same per-group code.
+__global__ __launch_bounds__(256) void flash_dropmask_waves_kernel(
+    const uint32_t* __restrict__ seed_ptr, uint32_t salt0, uint32_t thr16, int S, int Hq,
+    int h_off, int Hg, int NB, int NKT, int NQT, int causal, uint32_t* __restrict__ fwd_bits0,
+    uint32_t* __restrict__ bwd_bits0, int BH, int L, long long fwd_stride, long long bwd_stride) {
+  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
+  __shared__ uint32_t fwl[4][2][64];
+  const int NB2 = (NB + 1) >> 1;
+  const int per = causal ? NB2 * (NB2 + 1) / 2 : NB2 * NB2;   // live groups per (layer, bh)
+  const long long total = (long long)L * BH * per;
+  const int r = lane & 31, hh = lane >> 5;
+  const uint32_t seed0 = *seed_ptr;
+  // bwd-image gather constants (see flash_dropmask_kernel)
+  const int kl = r;
+  const int ef = (kl & 3) + 4 * (kl >> 3), fhi = 32 * ((kl >> 2) & 1);
+  const int fpos = 16 * (ef & 1) + (ef >> 1);
+  for (long long it = (long long)blockIdx.x * 4 + w; it < total; it += (long long)gridDim.x * 4) {
+    const int z = uni((int)(it / per));
+    const int pi = uni((int)(it - (long long)z * per));
+    int qb2, kb2;
+    if (causal) {   // row qb2 of the lower triangle holds qb2 + 1 groups
+      int q = (int)((sqrtf(8.f * (float)pi + 1.f) - 1.f) * 0.5f);
+      while ((q + 1) * (q + 2) / 2 <= pi) ++q;
+      while (q * (q + 1) / 2 > pi) --q;
+      qb2 = uni(q);
+      kb2 = uni(pi - q * (q + 1) / 2);
+    } else {
+      qb2 = uni(pi / NB2);
+      kb2 = uni(pi - (pi / NB2) * NB2);
+    }
+    const int layer = z / BH, bh = z - layer * BH;
+    uint32_t* fwd_bits = fwd_bits0 + (size_t)layer * fwd_stride;
+    uint32_t* bwd_bits = bwd_bits0 + (size_t)layer * bwd_stride;
+    const uint32_t seed = seed0 + salt0 + (uint32_t)layer;
+    const int b = bh / Hq, h = bh - b * Hq;
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      const uint32_t row = (uint32_t)(((long long)b * Hg + h_off + h) * S + (2 * qb2 + qq) * 32 + r);
+      const uint32_t rbase = row * 0x85EBCA6Bu;
+      uint32_t fb0 = drop_stream_bits(rbase, (uint32_t)(2 * kb2), hh, seed, thr16);
+      uint32_t fb1 = drop_stream_bits(rbase, (uint32_t)(2 * kb2 + 1), hh, seed, thr16);
+      const int qb = 2 * qb2 + qq;
+      const uint32_t word = fb0 | (fb1 << 8);
+      if (qb < NB) fwd_bits[(((size_t)bh * NB + qb) * NKT + (kb2 >> 1)) * 128 + lane * 2 + (kb2 & 1)] = word;
+      fwl[w][qq][lane] = word;
+    }
+    __builtin_amdgcn_wave_barrier();   // (LDS ops of one wave run in order; keep the compiler's too)
+    uint32_t wb[2] = {0u, 0u};
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const uint32_t src = fwl[w][u][crow(e, hh) + fhi];
+        const int pos = 8 * u + 16 * (e & 1) + (e >> 1);
+        wb[0] |= __builtin_amdgcn_ubfe(src, (uint32_t)fpos, 1u) << pos;
+        wb[1] |= __builtin_amdgcn_ubfe(src, (uint32_t)(8 + fpos), 1u) << pos;
+      }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int kb = 2 * kb2 + kk;
+      if (kb < NB) bwd_bits[(((size_t)bh * NB + kb) * NQT + qb2) * 64 + lane] = wb[kk];
+    }
+    __builtin_amdgcn_wave_barrier();   // this group's reads before the next group's writes
+  }
+}
+
 // ============================================================================ query-major
 // DQ false: forward (o, lse out).  DQ true: dQ (o, dout, lse in; delta, dq out).
 //
@@ -1497,6 +1568,38 @@ MX_EXPORT int mx_flash_kmajor128_variant(int variant) {
   return old;
 }
 
+namespace {
+// 0: the per-group grid (flash_dropmask_kernel), 1 (default): the wave-walk kernel
+int g_dropmask_variant = 1;
+int launch_dropmask(const uint32_t* seed, uint32_t salt, uint32_t thr16, int S, int Hq, int h_off, int Hg, int NB,
+                    int NKT, int NQT, int causal, void* fwd_bits, void* bwd_bits, int BH, int L, long long fwd_words,
+                    long long bwd_words, hipStream_t s) {
+  const int NB2 = (NB + 1) / 2;
+  if (g_dropmask_variant == 0) {
+    if ((long long)BH * L > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(flash_dropmask_kernel, dim3(NB2, (NB2 + 3) / 4, BH * L), dim3(256), 0, s, seed, salt, thr16,
+                       S, Hq, h_off, Hg, NB, NKT, NQT, causal, (uint32_t*)fwd_bits, (uint32_t*)bwd_bits, BH,
+                       fwd_words, bwd_words);
+    return hipGetLastError();
+  }
+  const long long per = causal ? (long long)NB2 * (NB2 + 1) / 2 : (long long)NB2 * NB2;
+  const long long waves = per * BH * L;
+  long long blocks = (waves + 3) / 4;
+  if (blocks > 2048) blocks = 2048;   // 8 waves per CU, each walking its share of the groups
+  hipLaunchKernelGGL(flash_dropmask_waves_kernel, dim3((unsigned)blocks), dim3(256), 0, s, seed, salt, thr16, S, Hq,
+                     h_off, Hg, NB, NKT, NQT, causal, (uint32_t*)fwd_bits, (uint32_t*)bwd_bits, BH, L, fwd_words,
+                     bwd_words);
+  return hipGetLastError();
+}
+}  // namespace
+
+// dropout-mask kernel choice (0 per-group grid, 1 wave walk); returns the previous setting
+MX_EXPORT int mx_flash_dropmask_variant(int v) {
+  const int old = g_dropmask_variant;
+  if (v >= 0) g_dropmask_variant = v;
+  return old;
+}
+
 // Dropout keep-mask images for one attention call (layouts in flash_dropmask_kernel).
 // fwd_bits: u64 [B*Hq][NB][NKT][64]; bwd_bits: u32 [B*Hq][NB][NQT][64], NB = ceil(S/32),
 // NKT = ceil(S/128), NQT = ceil(S/64).  h_off / Hg: this rank's first global head / the
@@ -1507,10 +1610,8 @@ MX_EXPORT int mx_flash_dropmask(const uint32_t* seed, uint32_t salt, float p, in
   const int NB = (S + 31) / 32, NKT = (S + 127) / 128, NQT = (S + 63) / 64;
   const int NB2 = (NB + 1) / 2;
   const uint32_t thr16 = (uint32_t)(p * 65536.0f + 0.5f);
-  hipLaunchKernelGGL(flash_dropmask_kernel, dim3(NB2, (NB2 + 3) / 4, B * Hq), dim3(256), 0, s, seed,
-                     salt, thr16, S, Hq, h_off, Hg, NB, NKT, NQT, causal, (uint32_t*)fwd_bits,
-                     (uint32_t*)bwd_bits, B * Hq, 0ll, 0ll);
-  return hipGetLastError();
+  return launch_dropmask(seed, salt, thr16, S, Hq, h_off, Hg, NB, NKT, NQT, causal, fwd_bits, bwd_bits, B * Hq, 1,
+                         0ll, 0ll, s);
 }
 
 // the images of L layers (salts salt, salt + 1, ...) in one launch; layer l's images start
@@ -1518,14 +1619,12 @@ MX_EXPORT int mx_flash_dropmask(const uint32_t* seed, uint32_t salt, float p, in
 MX_EXPORT int mx_flash_dropmask_layers(const uint32_t* seed, uint32_t salt, float p, int B, int S, int Hq,
                                        int h_off, int Hg, int causal, int L, void* fwd_bits, void* bwd_bits,
                                        long long fwd_words, long long bwd_words, hipStream_t s) {
-  if (L < 1 || (long long)B * Hq * L > 65535) return hipErrorInvalidValue;
+  if (L < 1) return hipErrorInvalidValue;
   const int NB = (S + 31) / 32, NKT = (S + 127) / 128, NQT = (S + 63) / 64;
   const int NB2 = (NB + 1) / 2;
   const uint32_t thr16 = (uint32_t)(p * 65536.0f + 0.5f);
-  hipLaunchKernelGGL(flash_dropmask_kernel, dim3(NB2, (NB2 + 3) / 4, B * Hq * L), dim3(256), 0, s, seed,
-                     salt, thr16, S, Hq, h_off, Hg, NB, NKT, NQT, causal, (uint32_t*)fwd_bits,
-                     (uint32_t*)bwd_bits, B * Hq, fwd_words, bwd_words);
-  return hipGetLastError();
+  return launch_dropmask(seed, salt, thr16, S, Hq, h_off, Hg, NB, NKT, NQT, causal, fwd_bits, bwd_bits, B * Hq, L,
+                         fwd_words, bwd_words, s);
 }
 
 // Q/K/V/O bf16 with token strides ld*; head h at column h*D.  lse: fp32 [B, Hq, S] (base 2).

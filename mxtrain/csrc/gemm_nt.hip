@@ -62,11 +62,9 @@ __device__ __forceinline__ float dpp_rowsum16(float v) {
   return v;
 }
 
-template <bool BKC, int WM, int WN, int FM, int FN, int BKT, int NSLOT, int KS = 1>
+template <bool BKC, int WM, int WN, int FM, int FN, int BKT, int NSLOT>
 struct Geo {
-  // KS k-groups of WM x WN compute waves: group g multiplies k-slice g of every K-step
-  // (intra-workgroup split-K), all KS * WM * WN waves share the DMA
-  static constexpr int NW = WM * WN * KS, NT = 64 * NW;
+  static constexpr int NW = WM * WN, NT = 64 * NW;
   static constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
   static constexpr int RA = BKT * 2;                   // [m][k] image row bytes (64 or 128)
   static constexpr int IA = BM * RA;
@@ -78,8 +76,6 @@ struct Geo {
   static_assert(PA * NW * 1024 == IA && PB * NW * 1024 == IB, "DMA pieces per wave");
   static_assert(BKC || (RB >= 256 && (BN & (BN - 1)) == 0), "K-major weight image needs BN = 2^k >= 128");
   static_assert(LDS <= 160 * 1024, "LDS");
-  static_assert(KS == 1 || (BKT / 32) % KS == 0, "k-groups split the K-step's 32-deep slices");
-  static_assert(KS == 1 || (size_t)WM * WN * FM * FN * 64 * 16 <= (size_t)LDS, "k-group exchange fits the ring");
 };
 
 // XOR swizzle of the 16-B chunks of a K-contiguous image row r (the same involution on the
@@ -202,19 +198,15 @@ __device__ __forceinline__ void epilogue(const Args& g, f32x4 (&acc)[FM][FN], in
 // STAMP (diagnostic build, mx_gemm_nt_stamps only): lane 0 of wave 0 records s_memtime /
 // s_memrealtime at tile start, after the first K-step's data landed, after the main loop
 // and after the epilogue into g.part ([tile][8] uint64); no output value depends on them
-template <bool BKC, int WM, int WN, int FM, int FN, int BKT, int NSLOT, int MINB, int EPI, bool STAMP = false,
-          int KS = 1>
-__global__ __launch_bounds__(64 * WM * WN * KS, MINB) void gemm_nt_kernel(const Args g) {
-  using Gm = Geo<BKC, WM, WN, FM, FN, BKT, NSLOT, KS>;
-  constexpr int NKQ = BKT / 32 / KS;   // 32-deep slices per K-step of one k-group
+template <bool BKC, int WM, int WN, int FM, int FN, int BKT, int NSLOT, int MINB, int EPI, bool STAMP = false>
+__global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_nt_kernel(const Args g) {
+  using Gm = Geo<BKC, WM, WN, FM, FN, BKT, NSLOT>;
   constexpr int BM = Gm::BM, BN = Gm::BN, RA = Gm::RA, RB = Gm::RB, IA = Gm::IA;
   constexpr int PA = Gm::PA, PB = Gm::PB, SLOT = Gm::SLOT;
   constexpr int PER = PA + PB;   // DMA instructions per wave per K-step
   constexpr int LPR = RA / 16;   // lanes per K-contiguous image row in a DMA piece
   __shared__ __attribute__((aligned(1024))) char smem[Gm::LDS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;   // wave: DMA role
-  const int kg = KS > 1 ? __builtin_amdgcn_readfirstlane(wave / (WM * WN)) : 0;   // k-group
-  const int cw = KS > 1 ? wave - kg * (WM * WN) : wave;                            // compute wave
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // grouped, XCD-contiguous tile order: consecutive logical ids walk gm row-tiles first
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int per_group = g.gm * g.tiles_n;
@@ -262,12 +254,11 @@ __global__ __launch_bounds__(64 * WM * WN * KS, MINB) void gemm_nt_kernel(const 
 
   // ---- fragment offsets: lane (G, i) reads row i of a 16-row subtile, k 8G .. 8G + 7 (+32 kk)
   const int G = lane >> 4, i = lane & 15;
-  const int wm = cw / WN, wn = cw % WN;
+  const int wm = wave / WN, wn = wave % WN;
   const int offA = (16 * FM * wm + i) * RA;          // + 16 s RA (compile-time) per subtile
-  // this k-group's slices kk = NKQ kg + kq of every K-step
-  int cA[NKQ];
+  int cA[BKT / 32];
 #pragma unroll
-  for (int kq = 0; kq < NKQ; ++kq) cA[kq] = 16 * ((4 * (NKQ * kg + kq) + G) ^ kc_swz<RA>(i));
+  for (int kk = 0; kk < BKT / 32; ++kk) cA[kk] = 16 * ((4 * kk + G) ^ kc_swz<RA>(i));
   int offB;
   if constexpr (BKC) {
     offB = (16 * FN * wn + i) * RB;
@@ -320,7 +311,7 @@ __global__ __launch_bounds__(64 * WM * WN * KS, MINB) void gemm_nt_kernel(const 
   // its latency exposed: one lgkmcnt stall per MFMA group in the ISA)
   constexpr bool XRES = FM >= FN;
   constexpr int NSTREAM = XRES ? FN : FM;
-  constexpr int NS = NKQ * NSTREAM;               // streamed-fragment steps per K-step
+  constexpr int NS = (BKT / 32) * NSTREAM;       // streamed-fragment steps per K-step
   constexpr int SPREAD = NS / 2 >= PER ? NS / 2 : NS;
   // the K-loop is unrolled by the ring depth, so every ring slot (LDS offset, M0 value) is
   // a compile-time constant
@@ -342,18 +333,15 @@ __global__ __launch_bounds__(64 * WM * WN * KS, MINB) void gemm_nt_kernel(const 
       constexpr int ns = (q + NSLOT - 1) % NSLOT;
       const char* As = smem + q * SLOT;
       const char* Bs = As + IA;
-      auto wfrag = [&](int u, int kq) __attribute__((always_inline)) {
-        if constexpr (BKC) return lds_read8(Bs, offBu[u] + cA[kq]);
-        else {
-          const int kk = NKQ * kg + kq;
-          return cat(tr_read(Bs, offBu[u] + 32 * RB * kk), tr_read(Bs, offBu[u] + 32 * RB * kk + 4 * RB));
-        }
+      auto wfrag = [&](int u, int kk) __attribute__((always_inline)) {
+        if constexpr (BKC) return lds_read8(Bs, offBu[u] + cA[kk]);
+        else return cat(tr_read(Bs, offBu[u] + 32 * RB * kk), tr_read(Bs, offBu[u] + 32 * RB * kk + 4 * RB));
       };
-      auto xfrag = [&](int s, int kq) __attribute__((always_inline)) {
-        return lds_read8(As, offA + 16 * s * RA + cA[kq]);
+      auto xfrag = [&](int s, int kk) __attribute__((always_inline)) {
+        return lds_read8(As, offA + 16 * s * RA + cA[kk]);
       };
 #pragma unroll
-      for (int kk = 0; kk < NKQ; ++kk) {
+      for (int kk = 0; kk < BKT / 32; ++kk) {
         if constexpr (XRES) {
           bf16x8 x[FM];
 #pragma unroll
@@ -388,29 +376,7 @@ __global__ __launch_bounds__(64 * WM * WN * KS, MINB) void gemm_nt_kernel(const 
   }
 
   stamp(2);
-  if constexpr (KS == 2) {
-    // fold k-group 1's partial tile into group 0's through the (now idle) ring: every wave
-    // is past its last fragment read, then group 1 stores lane-linear (1 KiB per f32x4),
-    // group 0 adds and runs the epilogue alone
-    __builtin_amdgcn_s_barrier();
-    f32x4* x = reinterpret_cast<f32x4*>(smem) + (size_t)cw * FM * FN * 64 + lane;
-    if (kg == 1) {
-#pragma unroll
-      for (int s = 0; s < FM; ++s)
-#pragma unroll
-        for (int u = 0; u < FN; ++u) x[(s * FN + u) * 64] = acc[s][u];
-    }
-    __syncthreads();
-    if (kg == 1) return;
-#pragma unroll
-    for (int s = 0; s < FM; ++s)
-#pragma unroll
-      for (int u = 0; u < FN; ++u) {
-        const f32x4 o = x[(s * FN + u) * 64];
-        acc[s][u] += o;
-      }
-  }
-  epilogue<WM, WN, FM, FN, EPI>(g, acc, tm, m0, n0, cw, lane);
+  epilogue<WM, WN, FM, FN, EPI>(g, acc, tm, m0, n0, wave, lane);
   if constexpr (STAMP) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -419,17 +385,17 @@ __global__ __launch_bounds__(64 * WM * WN * KS, MINB) void gemm_nt_kernel(const 
 }
 
 
-template <bool BKC, int WM, int WN, int FM, int FN, int BKT, int NSLOT, int MINB, int EPI, int KS = 1>
+template <bool BKC, int WM, int WN, int FM, int FN, int BKT, int NSLOT, int MINB, int EPI>
 int launch(Args a, int M, hipStream_t stream) {
-  using Gm = Geo<BKC, WM, WN, FM, FN, BKT, NSLOT, KS>;
+  using Gm = Geo<BKC, WM, WN, FM, FN, BKT, NSLOT>;
   if (M % Gm::BM || a.N % Gm::BN || a.K % BKT || a.K <= 0) return (int)hipErrorInvalidValue;
   const int tiles_m = M / Gm::BM;
   a.tiles_n = a.N / Gm::BN;
   int gm = 8;
   while (gm > 1 && tiles_m % gm) gm >>= 1;
   a.gm = gm;
-  hipLaunchKernelGGL((gemm_nt_kernel<BKC, WM, WN, FM, FN, BKT, NSLOT, MINB, EPI, false, KS>),
-                     dim3(tiles_m * a.tiles_n), dim3(Gm::NT), 0, stream, a);
+  hipLaunchKernelGGL((gemm_nt_kernel<BKC, WM, WN, FM, FN, BKT, NSLOT, MINB, EPI>), dim3(tiles_m * a.tiles_n),
+                     dim3(Gm::NT), 0, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -447,10 +413,6 @@ constexpr Variant kVariants[] = {
     {256, 256, 128, 1},   // 6: as 0 with BK 64 and a 2-slot ring
     {128, 128, 64, 1},    // 7: 8 waves 2 x 4 of 64 x 32, BK 32, 6-slot ring
     {256, 128, 64, 1},    // 8: 8 waves 4 x 2 of 64 x 64, BK 32, 5-slot ring (120 KiB)
-    {128, 128, 64, 1},    // 9: 8 waves = 2 k-groups x (2 x 2 of 64 x 64), BK 64, 4-slot ring
-    {128, 128, 64, 1},    // 10: as 9 with a 3-slot ring
-    {128, 256, 64, 1},    // 11: 8 waves = 2 k-groups x (2 x 2 of 64 x 128), BK 64, 3-slot ring (144 KiB)
-    {256, 128, 128, 1},   // 12: 8 waves = 2 k-groups x (2 x 2 of 128 x 64), BK 64, 3-slot ring (144 KiB)
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -468,10 +430,6 @@ int dispatch(int variant, const Args& a, int M, hipStream_t st) {
     case 6: return launch<BKC, 2, 4, 8, 4, 64, 2, 1, EPI>(a, M, st);
     case 7: return launch<BKC, 2, 4, 4, 2, 32, 6, 1, EPI>(a, M, st);
     case 8: return launch<BKC, 4, 2, 4, 4, 32, 5, 1, EPI>(a, M, st);
-    case 9: return launch<BKC, 2, 2, 4, 4, 64, 4, 1, EPI, 2>(a, M, st);
-    case 10: return launch<BKC, 2, 2, 4, 4, 64, 3, 1, EPI, 2>(a, M, st);
-    case 11: return launch<BKC, 2, 2, 4, 8, 64, 3, 1, EPI, 2>(a, M, st);
-    case 12: return launch<BKC, 2, 2, 8, 4, 64, 3, 1, EPI, 2>(a, M, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -19,7 +19,7 @@ using namespace mx;
 
 namespace {
 
-template <int NV, bool RMS, bool HAS_BDA, int R = 1>
+template <int NV, bool RMS, bool HAS_BDA>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const uint16_t* __restrict__ x,        // [rows, cols]  (GEMM output if HAS_BDA)
     const uint16_t* __restrict__ bias,     // [cols] or null
@@ -31,12 +31,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     int rows, int cols, float eps, uint32_t thresh, float keep_scale,
     const uint32_t* __restrict__ seed_ptr, uint32_t salt, uint64_t elem0) {
   const int lane = threadIdx.x & 63;
-  // R rows per wave: rows w, w + nw, ... (nw = waves in the grid); all R rows' loads are
-  // issued before any math, so each wave has R rows of reads in flight
-  const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  const int nw = gridDim.x * 4;
-  if (w >= rows) return;
+  const int row = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (row >= rows) return;
   const uint32_t seed = HAS_BDA && seed_ptr ? (*seed_ptr + salt) : 0u;
+  const size_t base = (size_t)row * cols;
   // Every load of the row (x, bias, residual, gamma, beta) is issued before any math:
   // one memory round trip per row instead of one per 512-column vector plus one for the
   // affine parameters.  Columns are clamped into the row and the loads unconditional;
@@ -44,29 +42,20 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   // optional operands are zeroed through masks the optimiser cannot see through (a
   // `bias ? load : 0` select became a branch around a load issued last).
   constexpr bool EARLY = NV <= 4;  // wider rows load the affine parameters at use
-  uint4 xr[R][NV], rr[R][NV], br[NV], gr[NV], er[NV];
+  uint4 xr[NV], br[NV], rr[NV], gr[NV], er[NV];
   const uint16_t* bsrc = bias ? bias : gamma;
   const uint16_t* rsrc = residual ? residual : x;
   const uint16_t* esrc = beta ? beta : gamma;
   uint32_t bm = bias ? ~0u : 0u, rmk = residual ? ~0u : 0u, em = beta ? ~0u : 0u;
   asm volatile("" : "+v"(bm), "+v"(rmk), "+v"(em));
 #pragma unroll
-  for (int k = 0; k < R; ++k) {
-    // rows past the end reload the wave's own first row (its cache lines), never a
-    // shared clamp row
-    const int rl = (w + k * nw < rows) ? w + k * nw : w;
-    const size_t b_ = (size_t)rl * cols;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = min((lane + 64 * i) * 8, cols - 8);
-      xr[k][i] = *reinterpret_cast<const uint4*>(x + b_ + c);
-      if constexpr (HAS_BDA) rr[k][i] = *reinterpret_cast<const uint4*>(rsrc + b_ + c);
-    }
-  }
-#pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = min((lane + 64 * i) * 8, cols - 8);
-    if constexpr (HAS_BDA) br[i] = *reinterpret_cast<const uint4*>(bsrc + c);
+    xr[i] = *reinterpret_cast<const uint4*>(x + base + c);
+    if constexpr (HAS_BDA) {
+      br[i] = *reinterpret_cast<const uint4*>(bsrc + c);
+      rr[i] = *reinterpret_cast<const uint4*>(rsrc + base + c);
+    }
     if constexpr (EARLY) {
       gr[i] = *reinterpret_cast<const uint4*>(gamma + c);
       if constexpr (!RMS) er[i] = *reinterpret_cast<const uint4*>(esrc + c);
@@ -76,75 +65,69 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   auto and4 = [](uint4 a, uint32_t m) __attribute__((always_inline)) {
     return make_uint4(a.x & m, a.y & m, a.z & m, a.w & m);
   };
+  float v[NV][8];
 #pragma unroll
-  for (int k = 0; k < R; ++k) {
-    const int row = w + k * nw;
-    if (row >= rows) break;
-    const size_t base = (size_t)row * cols;
-    float v[NV][8];
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    const bool ok = c < cols;
+    unpack8(xr[i], v[i]);
+    if constexpr (HAS_BDA) {
+      float b[8], r[8];
+      unpack8(and4(br[i], bm), b);
+      unpack8(and4(rr[i], rmk), r);
+      bool km[8];
+      if (thresh) dropout_keep8(elem0 + base + c, seed, thresh, km);
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = (lane + 64 * i) * 8;
-      const bool ok = c < cols;
-      unpack8(xr[k][i], v[i]);
-      if constexpr (HAS_BDA) {
-        float b[8], r[8];
-        unpack8(and4(br[i], bm), b);
-        unpack8(and4(rr[k][i], rmk), r);
-        bool km[8];
-        if (thresh) dropout_keep8(elem0 + base + c, seed, thresh, km);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float t = v[i][j] + b[j];
-          if (thresh) t = km[j] ? t * keep_scale : 0.f;
-          v[i][j] = r[j] + t;
-        }
-        // the residual stream is stored in bf16; normalise the rounded value so that
-        // backward (which re-reads h_out) sees exactly the forward's input
-        uint4 packed = pack8(v[i]);
-        if (ok) *reinterpret_cast<uint4*>(h_out + base + c) = packed;
-        unpack8(packed, v[i]);
+      for (int j = 0; j < 8; ++j) {
+        float t = v[i][j] + b[j];
+        if (thresh) t = km[j] ? t * keep_scale : 0.f;
+        v[i][j] = r[j] + t;
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[i][j] = ok ? v[i][j] : 0.f;
-    }
-    float mean = 0.f;
-    if constexpr (!RMS) {
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < NV; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s += v[i][j];
-      mean = wave_sum(s) / (float)cols;
-    }
-    float ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const bool ok = (lane + 64 * i) * 8 < cols;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { float d = v[i][j] - mean; ss += ok ? d * d : 0.f; }
-    }
-    const float rstd = rsqrtf(wave_sum(ss) / (float)cols + eps);
-    if (lane == 0) {
-      if (!RMS) mean_out[row] = mean;
-      rstd_out[row] = rstd;
+      // the residual stream is stored in bf16; normalise the rounded value so that
+      // backward (which re-reads h_out) sees exactly the forward's input
+      uint4 packed = pack8(v[i]);
+      if (ok) *reinterpret_cast<uint4*>(h_out + base + c) = packed;
+      unpack8(packed, v[i]);
     }
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = (lane + 64 * i) * 8;
-      if (!EARLY && c >= cols) continue;
-      const int cc = min(c, cols - 8);
-      float g[8], bt[8], o[8];
-      unpack8(EARLY ? gr[i] : *reinterpret_cast<const uint4*>(gamma + cc), g);
-      if constexpr (!RMS) unpack8(and4(EARLY ? er[i] : *reinterpret_cast<const uint4*>(esrc + cc), em), bt);
-      else {
+    for (int j = 0; j < 8; ++j) v[i][j] = ok ? v[i][j] : 0.f;
+  }
+  float mean = 0.f;
+  if constexpr (!RMS) {
+    float s = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) bt[j] = 0.f;
-      }
+    for (int i = 0; i < NV; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + bt[j];
-      if (c < cols) *reinterpret_cast<uint4*>(y + base + c) = pack8(o);
+      for (int j = 0; j < 8; ++j) s += v[i][j];
+    mean = wave_sum(s) / (float)cols;
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const bool ok = (lane + 64 * i) * 8 < cols;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { float d = v[i][j] - mean; ss += ok ? d * d : 0.f; }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / (float)cols + eps);
+  if (lane == 0) {
+    if (!RMS) mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    if (!EARLY && c >= cols) continue;
+    const int cc = min(c, cols - 8);
+    float g[8], bt[8], o[8];
+    unpack8(EARLY ? gr[i] : *reinterpret_cast<const uint4*>(gamma + cc), g);
+    if constexpr (!RMS) unpack8(and4(EARLY ? er[i] : *reinterpret_cast<const uint4*>(esrc + cc), em), bt);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bt[j] = 0.f;
     }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + bt[j];
+    if (c < cols) *reinterpret_cast<uint4*>(y + base + c) = pack8(o);
   }
 }
 
@@ -478,8 +461,6 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(
   for (int j = 0; j < 8; ++j) o[j] = acc[j];
 }
 
-int kFwdRowsPerWave = 1;   // rows per wave of the forward (1 or 2)
-
 template <bool RMS, bool BDA>
 hipError_t launch_fwd(const void* x, const void* bias, const void* residual,
                       const void* gamma, const void* beta, void* h_out, void* y,
@@ -489,24 +470,14 @@ hipError_t launch_fwd(const void* x, const void* bias, const void* residual,
   const int nv = (cols + 511) / 512;
   const uint32_t thresh = p > 0.f ? (uint32_t)((double)p * 4294967296.0) : 0u;
   const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const int R = (nv <= 2 && kFwdRowsPerWave >= 2) ? 2 : 1;
-  dim3 grid((rows + 4 * R - 1) / (4 * R)), block(256);
+  dim3 grid((rows + 3) / 4), block(256);
 #define MX_LN_CASE(N)                                                                  \
   case N:                                                                              \
-    if (R == 2) {                                                                      \
-      if constexpr ((N) <= 2)                                                          \
-        hipLaunchKernelGGL((ln_fwd_kernel<N, RMS, BDA, 2>), grid, block, 0, s,         \
-                           (const uint16_t*)x, (const uint16_t*)bias,                  \
-                           (const uint16_t*)residual, (const uint16_t*)gamma,          \
-                           (const uint16_t*)beta, (uint16_t*)h_out, (uint16_t*)y, mean, \
-                           rstd, rows, cols, eps, thresh, ks, seed, salt, elem0);      \
-    } else {                                                                           \
-      hipLaunchKernelGGL((ln_fwd_kernel<N, RMS, BDA, 1>), grid, block, 0, s,           \
-                         (const uint16_t*)x, (const uint16_t*)bias,                    \
-                         (const uint16_t*)residual, (const uint16_t*)gamma,            \
-                         (const uint16_t*)beta, (uint16_t*)h_out, (uint16_t*)y, mean,  \
-                         rstd, rows, cols, eps, thresh, ks, seed, salt, elem0);        \
-    }                                                                                  \
+    hipLaunchKernelGGL((ln_fwd_kernel<N, RMS, BDA>), grid, block, 0, s,                \
+                       (const uint16_t*)x, (const uint16_t*)bias,                      \
+                       (const uint16_t*)residual, (const uint16_t*)gamma,              \
+                       (const uint16_t*)beta, (uint16_t*)h_out, (uint16_t*)y, mean,    \
+                       rstd, rows, cols, eps, thresh, ks, seed, salt, elem0);          \
     break;
   switch (nv) {
     MX_LN_CASE(1) MX_LN_CASE(2) MX_LN_CASE(3) MX_LN_CASE(4) MX_LN_CASE(5)
@@ -643,12 +614,6 @@ MX_EXPORT int mx_norm_bwd_nparts(int rows) { return bwd_grid(rows); }
 MX_EXPORT int mx_norm_bwd_rows_per_wave(int r) {
   const int old = kBwdRowsPerWave;
   if (r > 0) kBwdRowsPerWave = r;
-  return old;
-}
-// rows per wave of the norm forward (1, or 2 for rows <= 1024 columns); returns the old value
-MX_EXPORT int mx_norm_fwd_rows_per_wave(int r) {
-  const int old = kFwdRowsPerWave;
-  if (r > 0) kFwdRowsPerWave = r;
   return old;
 }
 // cap on the fused backward's workgroups (= partial slabs); returns the old value

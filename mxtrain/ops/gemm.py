@@ -187,12 +187,6 @@ def nt_plan(M: int, N: int, K: int, kmajor: bool) -> int:
         if M % bm or N % bn or (kmajor and not kok):
             continue
         if (M // bm) * (N // bn) >= 224:
-            # long reductions on 128 x 128 tiles: two k-groups of 4 waves (64 x 64 each, a
-            # third less LDS read traffic per MFMA) instead of 8 waves of 64 x 32 -- 3-4 %
-            # faster at K >= 3072 (fc2 fwd / fc1 dgrad 4096 x 1024 x 4096: 32.3 -> 31.3 us),
-            # 1-2 % slower at K = 1024 (profiles/r5_s1/gemm_ks.txt)
-            if v == 3 and K >= 2048:
-                return 10
             return v
         if fallback < 0 or (M // bm) * (N // bn) > (M // _nt_tile(fallback)[0]) * (N // _nt_tile(fallback)[1]):
             fallback = v
