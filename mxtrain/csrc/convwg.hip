@@ -242,6 +242,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
 }
 
 constexpr int kBM = 128, kBN = 128, kBK = 64, kNT = 256;
+int g_conv_fwd_bk32 = 0;   // forward K-step depth 32 (up to four workgroups per CU) instead of 64
 
 // ================================================================================= forward
 // y[p][co] = act(sum over taps (r, s) and ci of X[pix(p, r, s)][ci] * W[co][r][s][ci] + b[co]
@@ -274,9 +275,20 @@ struct ConvFw {
 // 64-channel res2 convolutions, which otherwise went to MIOpen)
 // (256 x 128 tiles, one workgroup of 8 waves per CU, measured 3-8 % slower on the Mask R-CNN
 // shapes: profiles/r4_s2/conv_fwd_tiles_4img.txt)
-template <int NSLOT, int FN, bool RES, bool RELU>
+// K-contiguous image row swizzle: 128-B rows (BKT 64): chunk ^ (row & 7); 64-B rows
+// (BKT 32, four rows per 256-B bank row): chunk ^ f((row >> 2) & 3), f = {0, 2, 3, 1}
+// (gemm_nt.hip kc_swz): conflict-free ds_read_b128 over every 16-lane group either way
+template <int R>
+__device__ __forceinline__ int row_swz(int r) {
+  if constexpr (R == 128) return r & 7;
+  else return (0x78 >> (2 * ((r >> 2) & 3))) & 3;
+}
+
+// BKT 64: 2-slot ring of 32 KiB slots, two workgroups per CU (LDS-bound); BKT 32: 16 KiB
+// slots, up to four workgroups per CU (VGPR-bound), twice the barriers per unit of K
+template <int NSLOT, int FN, bool RES, bool RELU, int BKT = 64>
 __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
-  constexpr int WM = 2, WN = 2, FM = 4, BKT = 64, NW = WM * WN;
+  constexpr int WM = 2, WN = 2, FM = 4, NW = WM * WN;
   constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN, R = BKT * 2;
   static_assert(FN == 2 || FN == 4, "tile width");
   constexpr int IA = BM * R, IB = BN * R;
@@ -310,7 +322,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
     divmod(ok ? p : 0, cp.OW, cp.invOW, q, ow);
     divmod(q, cp.OH, cp.invOH, n, oh);
     const int ih0 = oh * cp.stride - cp.pad, iw0 = ow * cp.stride - cp.pad;
-    aoff[j] = ((n * cp.IH + ih0) * cp.IW + iw0) * cp.ldx + 8 * ((lane % (R / 16)) ^ (row & 7));
+    aoff[j] = ((n * cp.IH + ih0) * cp.IW + iw0) * cp.ldx + 8 * ((lane % (R / 16)) ^ row_swz<R>(row));
     uint32_t m = 0u;
     for (int r = 0, t = 0; r < cp.taps / cp.KW; ++r) {
       const bool rin = ok && (unsigned)(ih0 + r * cp.dil) < (unsigned)cp.IH;
@@ -324,7 +336,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
 #pragma unroll
   for (int j = 0; j < PB; ++j) {
     const int brow = n0 + (PB * wave + j) * (1024 / R) + lane / (R / 16);
-    boff[j] = (uint32_t)(brow * (int)ldw + 8 * ((lane % (R / 16)) ^ (brow & 7))) * 2u;
+    boff[j] = (uint32_t)(brow * (int)ldw + 8 * ((lane % (R / 16)) ^ row_swz<R>(brow))) * 2u;
   }
   const i32x4_t xres = buffer_rsrc(cp.x, cp.xbytes);
   const int G = lane >> 4, i = lane & 15;
@@ -332,7 +344,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
   const int offA = (16 * FM * wm + i) * R, offB = (16 * FN * wn + i) * R;
   int cK[BKT / 32];
 #pragma unroll
-  for (int kk = 0; kk < BKT / 32; ++kk) cK[kk] = 16 * ((4 * kk + G) ^ (i & 7));
+  for (int kk = 0; kk < BKT / 32; ++kk) cK[kk] = 16 * ((4 * kk + G) ^ row_swz<R>(i));
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -1103,7 +1115,8 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   const int64_t xbytes = N * cp.IH * cp.IW * (int64_t)cp.ldx * 2;
   if (cp.taps > 32 || xbytes >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   cp.xbytes = (uint32_t)xbytes;
-  cp.cib = cp.Cin / 64;
+  const int bkt = g_conv_fwd_bk32 && cp.Cin % 32 == 0 ? 32 : 64;
+  cp.cib = cp.Cin / bkt;
   cp.nk = cp.taps * cp.cib;
   cp.tiles_n = Cout % 128 == 0 ? Cout / 128 : Cout / 64;
   cp.invOW = 1.f / (float)cp.OW;
@@ -1112,17 +1125,21 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   if (cp.splits > 1 && (!cp.part || (d[23] & 15))) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)((T + 127) / 128) * cp.tiles_n * cp.splits), block(256);
-#define MX_CF(NS, FN)                                                                         \
+#define MX_CF(NS, FN, BK)                                                                     \
   if (cp.res) {                                                                               \
-    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, true, true>), grid, block, 0, st, cp);   \
-    else hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, true, false>), grid, block, 0, st, cp);       \
+    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, true, true, BK>), grid, block, 0, st, cp);   \
+    else hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, true, false, BK>), grid, block, 0, st, cp);       \
   } else {                                                                                    \
-    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, false, true>), grid, block, 0, st, cp);  \
-    else hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, false, false>), grid, block, 0, st, cp);      \
+    if (relu) hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, false, true, BK>), grid, block, 0, st, cp);  \
+    else hipLaunchKernelGGL((conv_fwd_kernel<NS, FN, false, false, BK>), grid, block, 0, st, cp);      \
   }
   // ring depth 2 at two workgroups per CU: 3 / 4 slots (one workgroup per CU, counted waits)
   // measured 40 % slower on the Mask R-CNN shapes (profiles/r4_s2/conv_ring_depth_ab_4img.txt)
-  if (Cout % 128 == 0) { MX_CF(2, 4) } else { MX_CF(2, 2) }
+  if (bkt == 32) {
+    if (Cout % 128 == 0) { MX_CF(2, 4, 32) } else { MX_CF(2, 2, 32) }
+  } else {
+    if (Cout % 128 == 0) { MX_CF(2, 4, 64) } else { MX_CF(2, 2, 64) }
+  }
 #undef MX_CF
   if (cp.splits > 1) {
     const int64_t nvec = T * (Cout / 8);
@@ -1136,4 +1153,11 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
     }
   }
   return (int)hipGetLastError();
+}
+
+// forward K-step depth: 1 -> 32 (16-KiB ring slots), 0 -> 64; negative: query.  Returns the old value.
+MX_EXPORT int mx_conv_fwd_bk32(int on) {
+  const int old = g_conv_fwd_bk32;
+  if (on >= 0) g_conv_fwd_bk32 = on;
+  return old;
 }

@@ -1220,15 +1220,22 @@ __device__ __forceinline__ uint32_t tkr_key(float f, bool largest) {
   return largest ? k : ~k;
 }
 
+// nc > 0 (chunk stage of a long row): workgroup r takes chunk r % nc (columns (r % nc) c ..
+// + c, clipped to n_orig) of row r / nc and reports row-global indices.  imap (merge stage):
+// the reported index is imap[r][local index] (the candidates' original positions).
 __global__ __launch_bounds__(1024) void topk_rows_kernel(const float* __restrict__ x, int n, int ld, int k, int largest,
-                                                         float* __restrict__ ov, int64_t* __restrict__ oi) {
+                                                         float* __restrict__ ov, int64_t* __restrict__ oi, int nc,
+                                                         int n_orig, const int64_t* __restrict__ imap) {
   __shared__ int hist[256];
   __shared__ int sel[2];
   __shared__ int wc[16];
   __shared__ int ngt;
   __shared__ unsigned long long cand[kTkrMaxK];
   const int r = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const float* row = x + (size_t)r * ld;
+  const int chunk = nc > 0 ? r % nc : 0;
+  const float* row = nc > 0 ? x + (size_t)(r / nc) * ld + (size_t)chunk * n : x + (size_t)r * ld;
+  const int n_in = n;
+  if (nc > 0) n = min(n, n_orig - chunk * n_in);   // (the host keeps every chunk >= k long)
   const bool lg = largest != 0;
   uint32_t prefix = 0u, pmask = 0u;
   int rem = k;
@@ -1326,7 +1333,7 @@ __global__ __launch_bounds__(1024) void topk_rows_kernel(const float* __restrict
   for (int i = t; i < k; i += 1024) {
     const int idx = (int)(~(uint32_t)cand[i]);
     ov[(size_t)r * k + i] = row[idx];
-    oi[(size_t)r * k + i] = idx;
+    oi[(size_t)r * k + i] = imap ? imap[(size_t)r * n_in + idx] : (int64_t)chunk * n_in + idx;
   }
 }
 
@@ -1755,7 +1762,23 @@ MX_EXPORT int mx_topk_chunk() { return kTkChunk; }
 MX_EXPORT int mx_topk_rows(const float* x, int R, int n, int ld, int k, int largest, float* ov, int64_t* oi,
                            hipStream_t s) {
   if (R <= 0 || k <= 0 || k > n || k > kTkrMaxK || ld < n || n >= (1 << 30)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(topk_rows_kernel, dim3(R), dim3(1024), 0, s, x, n, ld, k, largest, ov, oi);
+  hipLaunchKernelGGL(topk_rows_kernel, dim3(R), dim3(1024), 0, s, x, n, ld, k, largest, ov, oi, 0, 0,
+                     (const int64_t*)nullptr);
+  return hipGetLastError();
+}
+// Long rows in two launches (ops/vision.py topk_rows): the k best of each of nc chunks of c
+// columns of every row (row-global indices, ragged last chunk read in place -- no padded
+// copy), then the k best of the R x (nc k) candidates with their original indices (no
+// index arithmetic / gather launches in between).  cand_v / cand_i: R * nc * k scratch.
+MX_EXPORT int mx_topk_rows_long(const float* x, int R, int n, int ld, int nc, int c, int k, int largest,
+                                float* cand_v, int64_t* cand_i, float* ov, int64_t* oi, hipStream_t s) {
+  if (R <= 0 || k <= 0 || k > kTkrMaxK || nc < 1 || c < k || (int64_t)nc * c < n || n - (nc - 1) * c < k ||
+      (int64_t)nc * k > (1 << 30) || ld < n)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(topk_rows_kernel, dim3(R * nc), dim3(1024), 0, s, x, c, ld, k, largest, cand_v, cand_i, nc, n,
+                     (const int64_t*)nullptr);
+  hipLaunchKernelGGL(topk_rows_kernel, dim3(R), dim3(1024), 0, s, (const float*)cand_v, nc * k, nc * k, k, largest,
+                     ov, oi, 0, 0, (const int64_t*)cand_i);
   return hipGetLastError();
 }
 MX_EXPORT int mx_topk_rows_max_k() { return kTkrMaxK; }

@@ -176,7 +176,23 @@ class RPNHead(nn.Module):
                       + ([cw(self.cls.bias, dt).new_zeros(pad)] if pad else []))
         o = conv_bias_act(t, w.contiguous(memory_format=torch.channels_last), b)
         geo = [(y0, x0, p.shape[2], p.shape[3]) for (y0, x0), p in zip(lay[2], P)]
+        if (o.is_cuda and o.dtype == torch.bfloat16 and o.is_contiguous(memory_format=torch.channels_last)
+                and _lib.use_hip(o) and len(geo) <= 8):
+            # flat [B, A] / [B, A, 4] of all levels in one launch; the per-level pairs are views
+            geo5, off = [], 0
+            for y0, x0, h, w in geo:
+                geo5 += [y0, x0, h, w, off]
+                off += h * w * na
+            lg, dl = _UnpackFlat.apply(o, tuple(geo5), na, off)
+            self.last_flat = (lg, dl)
+            out, off = [], 0
+            for _, _, h, w in geo:
+                n = h * w * na
+                out.append((lg[:, off:off + n], dl[:, off:off + n]))
+                off += n
+            return out
         flat = _UnpackLevels.apply(o, geo, na)
+        self.last_flat = None
         return [(flat[2 * i], flat[2 * i + 1]) for i in range(len(P))]
 
     pack_levels = True
@@ -252,6 +268,37 @@ class _UnpackLevels(torch.autograd.Function):
             if gb is not None:
                 d[:, y0:y0 + h, x0:x0 + w, na:5 * na].copy_(gb.reshape(B, h, w, 4 * na))
         return d.permute(0, 3, 1, 2), None, None
+
+
+class _UnpackFlat(torch.autograd.Function):
+    """The head's canvas output [B, C, Hc, Wc] (channels_last bf16) -> flat per-image anchor
+    order of ALL levels: logits [B, A], deltas [B, A, 4] (level l at anchor offset off_l) in
+    one launch (csrc/dettarget.hip rpn_unpack_kernel); backward builds the whole canvas
+    gradient in one launch too.  The loss takes the flat tensors as they are and the
+    proposal top-k per-level views of them: no per-level copies, no concatenation."""
+
+    @staticmethod
+    def forward(ctx, o, geo5, na, A):
+        B, C, Hc, Wc = o.shape
+        lg = torch.empty(B, A, dtype=o.dtype, device=o.device)
+        dl = torch.empty(B, A, 4, dtype=o.dtype, device=o.device)
+        arr = (ctypes.c_int * len(geo5))(*geo5)
+        _lib.call("mx_rpn_unpack", o.data_ptr(), B, Hc, Wc, C, na, arr, len(geo5) // 5, A, lg.data_ptr(), dl.data_ptr(),
+                  _lib.stream())
+        ctx.geo5, ctx.na, ctx.A, ctx.shape = geo5, na, A, o.shape
+        return lg, dl
+
+    @staticmethod
+    def backward(ctx, glg, gdl):
+        B, C, Hc, Wc = ctx.shape
+        ref = glg if glg is not None else gdl
+        glg = glg.contiguous() if glg is not None else None
+        gdl = gdl.contiguous() if gdl is not None else None
+        d = torch.empty(B, Hc, Wc, C, dtype=ref.dtype, device=ref.device)
+        arr = (ctypes.c_int * len(ctx.geo5))(*ctx.geo5)
+        _lib.call("mx_rpn_pack_grad", _lib.ptr(glg), _lib.ptr(gdl), B, Hc, Wc, C, ctx.na, arr, len(ctx.geo5) // 5,
+                  ctx.A, d.data_ptr(), _lib.stream())
+        return d.permute(0, 3, 1, 2), None, None, None
 
 
 class BoxHead(nn.Module):
@@ -338,6 +385,13 @@ class MaskRCNN(nn.Module):
             self._anchor_cache[key] = lv
         return self._anchor_cache[key]
 
+    def _all_anchors(self, anchors_lv):
+        """All levels' anchors [A, 4] (concatenated once per level-shape set)."""
+        key = ("all", tuple(a.data_ptr() for a in anchors_lv))
+        if key not in self._anchor_cache:
+            self._anchor_cache[key] = torch.cat(anchors_lv, 0)
+        return self._anchor_cache[key]
+
     def features(self, images: torch.Tensor):
         dt = self.compute_dtype(images.device)
         x = None
@@ -363,6 +417,8 @@ class MaskRCNN(nn.Module):
 
     # ------------------------------------------------------------------ RPN
     def rpn_targets(self, anchors: torch.Tensor, gt_boxes, gt_count, img_hw):
+        """(sel_pos, sel_neg [B, A] bool, encoded regression targets [B, A, 4] fp32) -- the
+        PyTorch definition; the GPU path is _rpn_targets_fused (same draws, same math)."""
         cfg = self.cfg
         B = gt_boxes.shape[0]
         mi, am, lq = V.match_boxes(anchors, gt_boxes, gt_count)
@@ -377,13 +433,50 @@ class MaskRCNN(nn.Module):
         sel_neg = _rank_select(g, cfg.rpn_batch_per_im - npos, neg, cfg.rpn_batch_per_im)
         matched = torch.where(lq >= 0, lq, am).clamp(min=0)
         tgt_boxes = torch.gather(gt_boxes, 1, matched[..., None].expand(-1, -1, 4))
-        return sel_pos, sel_neg, tgt_boxes
+        enc = V.encode_boxes(anchors[None].expand(B, -1, -1).reshape(-1, 4), tgt_boxes.reshape(-1, 4)).view(B, -1, 4)
+        return sel_pos, sel_neg, enc
+
+    def _rpn_targets_fused(self, anchors, gt_boxes, gt_count, img_hw):
+        """rpn_targets in 8 launches (csrc/dettarget.hip): match, the random keys, one
+        labelling pass (inside / pos / neg keys + regression targets), two bounded top-k
+        selections and the selection scatter -- instead of ~40 PyTorch kernels."""
+        cfg = self.cfg
+        B, G = gt_boxes.shape[:2]
+        A = anchors.shape[0]
+        dev = anchors.device
+        gtf = gt_boxes.float().contiguous()
+        mi, am, lq = V.match_boxes(anchors, gtf, gt_count, int32=True)
+        g = torch.rand((B, A), device=dev)
+        kpos = torch.empty(B, A, dtype=torch.float32, device=dev)
+        kneg = torch.empty_like(kpos)
+        enc = torch.empty(B, A, 4, dtype=torch.float32, device=dev)
+        sel_pos = torch.empty(B, A, dtype=torch.bool, device=dev)
+        sel_neg = torch.empty_like(sel_pos)
+        an = anchors.float().contiguous()
+        hw = img_hw.float().contiguous()
+        _lib.call("mx_rpn_keys", _lib.ptr(an), A, B, _lib.ptr(mi), _lib.ptr(am), _lib.ptr(lq), _lib.ptr(hw),
+                  _lib.ptr(g), _lib.ptr(gtf), G, float(cfg.rpn_fg_thresh), float(cfg.rpn_bg_thresh), _lib.ptr(kpos),
+                  _lib.ptr(kneg), _lib.ptr(enc), _lib.ptr(sel_pos), _lib.ptr(sel_neg), _lib.stream())
+        nfg_max = min(int(cfg.rpn_batch_per_im * cfg.rpn_fg_ratio), A)
+        nb = min(cfg.rpn_batch_per_im, A)
+        vp, ip = V.topk_rows(kpos, nfg_max, largest=False)
+        vn, ineg = V.topk_rows(kneg, nb, largest=False)
+        _lib.call("mx_rpn_select", _lib.ptr(vp), _lib.ptr(ip), nfg_max, _lib.ptr(vn), _lib.ptr(ineg), nb,
+                  int(cfg.rpn_batch_per_im), A, B, _lib.ptr(sel_pos), _lib.ptr(sel_neg), _lib.stream())
+        return sel_pos, sel_neg, enc
+
+    def _fused_targets_ok(self, t: torch.Tensor) -> bool:
+        return self.fused_targets and _lib.use_hip(t)
+
+    fused_targets = True
 
     def rpn_losses(self, logits, deltas, anchors, gt_boxes, gt_count, img_hw):
         cfg = self.cfg
-        sel_pos, sel_neg, tgt = self.rpn_targets(anchors, gt_boxes, gt_count, img_hw)
         B = logits.shape[0]
-        enc = V.encode_boxes(anchors[None].expand(B, -1, -1).reshape(-1, 4), tgt.reshape(-1, 4)).view(B, -1, 4)
+        if self._fused_targets_ok(logits) and gt_boxes.shape[1] > 0:
+            sel_pos, sel_neg, enc = self._rpn_targets_fused(anchors, gt_boxes, gt_count, img_hw)
+        else:
+            sel_pos, sel_neg, enc = self.rpn_targets(anchors, gt_boxes, gt_count, img_hw)
         # BCE over the sampled anchors / #sampled, huber(1/9) over the positives / (B * 256)
         return D.rpn_loss(logits, deltas, enc, sel_pos, sel_neg, B * cfg.rpn_batch_per_im)
 
@@ -419,7 +512,8 @@ class MaskRCNN(nn.Module):
     @torch.no_grad()
     def sample_rois(self, props, gt_boxes, gt_labels, gt_count):
         """Returns rois [B, N, 4] (fg first), labels [B, N] (0 = bg), matched gt [B, N],
-        regression targets [B, N, 4], fg mask [B, N]; N = frcnn_batch_per_im."""
+        regression targets [B, N, 4], fg mask [B, N]; N = frcnn_batch_per_im.  The PyTorch
+        definition; the GPU path is _sample_rois_fused (same draws, same math)."""
         cfg = self.cfg
         B, G = gt_boxes.shape[:2]
         gvalid = torch.arange(G, device=props.device)[None] < gt_count[:, None]
@@ -442,6 +536,52 @@ class MaskRCNN(nn.Module):
         mgt = torch.gather(gt_boxes, 1, g[..., None].expand(-1, -1, 4))
         tgt = V.encode_boxes(rois.reshape(-1, 4), mgt.reshape(-1, 4), cfg.bbox_reg_weights).view(B, N, 4)
         return rois, labels, g, tgt, is_fg
+
+    @torch.no_grad()
+    def _sample_rois_fused(self, props, gt_boxes, gt_labels, gt_count):
+        """sample_rois in 8 launches (csrc/dettarget.hip): candidates (proposals + valid gt),
+        match, the random keys, fg keys, bounded top-k of the fg, the ordering keys, top-k of
+        the N slots and one gather pass (RoI, fg flag, matched gt, label, regression target,
+        and the [batch, box] RoIAlign rows of all slots / of the fg slots) -- instead of ~45
+        PyTorch kernels.  Returns sample_rois' tuple + (rois5, rois5_fg)."""
+        cfg = self.cfg
+        B, K = props.shape[:2]
+        G = gt_boxes.shape[1]
+        C = K + G
+        N = cfg.frcnn_batch_per_im
+        nfg = int(N * cfg.frcnn_fg_ratio)
+        dev = props.device
+        gtf = gt_boxes.float().contiguous()
+        gc = gt_count.to(torch.int32).contiguous()
+        cand = torch.empty(B, C, 4, dtype=torch.float32, device=dev)
+        cvalid = torch.empty(B, C, dtype=torch.uint8, device=dev)
+        _lib.call("mx_roi_candidates", _lib.ptr(props.float().contiguous()), K, _lib.ptr(gtf), _lib.ptr(gc), G, B,
+                  _lib.ptr(cand), _lib.ptr(cvalid), _lib.stream())
+        mi, am, _ = V.match_boxes(cand, gtf, gc, low_quality=False, int32=True)
+        r = torch.rand((B, C), device=dev)
+        fgk = torch.empty(B, C, dtype=torch.float32, device=dev)
+        _lib.call("mx_roi_fgkey", _lib.ptr(mi), _lib.ptr(cvalid), _lib.ptr(r), B * C, float(cfg.frcnn_fg_thresh),
+                  _lib.ptr(fgk), _lib.stream())
+        kf = min(nfg, C)
+        vf, i_f = V.topk_rows(fgk, kf, largest=False)
+        sel_fg = torch.empty(B, C, dtype=torch.bool, device=dev)
+        key = torch.empty(B, C, dtype=torch.float32, device=dev)
+        _lib.call("mx_roi_order", _lib.ptr(vf), _lib.ptr(i_f), kf, _lib.ptr(mi), _lib.ptr(cvalid), _lib.ptr(r), C, B,
+                  float(cfg.frcnn_fg_thresh), _lib.ptr(sel_fg), _lib.ptr(key), _lib.stream())
+        _, idx = V.topk_rows(key, N)
+        rois = torch.empty(B, N, 4, dtype=torch.float32, device=dev)
+        labels = torch.empty(B, N, dtype=torch.int64, device=dev)
+        gidx = torch.empty(B, N, dtype=torch.int64, device=dev)
+        tgt = torch.empty(B, N, 4, dtype=torch.float32, device=dev)
+        is_fg = torch.empty(B, N, dtype=torch.bool, device=dev)
+        rois5 = torch.empty(B * N, 5, dtype=torch.float32, device=dev)
+        rois5_fg = torch.empty(B * nfg, 5, dtype=torch.float32, device=dev)
+        wx, wy, ww, wh = cfg.bbox_reg_weights
+        _lib.call("mx_roi_gather", _lib.ptr(idx), N, nfg, B, _lib.ptr(cand), C, _lib.ptr(sel_fg), _lib.ptr(am),
+                  _lib.ptr(gt_labels.long().contiguous()), _lib.ptr(gtf), G, float(wx), float(wy), float(ww), float(wh),
+                  _lib.ptr(rois), _lib.ptr(labels), _lib.ptr(gidx), _lib.ptr(tgt), _lib.ptr(is_fg), _lib.ptr(rois5),
+                  _lib.ptr(rois5_fg), _lib.stream())
+        return rois, labels, gidx, tgt, is_fg, rois5, rois5_fg
 
     @staticmethod
     def _with_batch(boxes: torch.Tensor) -> torch.Tensor:
@@ -512,15 +652,22 @@ class MaskRCNN(nn.Module):
         img_hw = img_hw.float()
         if not self.training:
             return self.inference(P, logits_lv, deltas_lv, anchors_lv, img_hw)
-        anchors = torch.cat(anchors_lv, 0)
-        rpn_cls, rpn_box = self.rpn_losses(torch.cat(logits_lv, 1), torch.cat(deltas_lv, 1), anchors,
-                                           gt_boxes, gt_count, img_hw)
+        anchors = self._all_anchors(anchors_lv)
+        flat = getattr(self.rpn, "last_flat", None)
+        self.rpn.last_flat = None
+        lg_all, dl_all = flat if flat is not None else (torch.cat(logits_lv, 1), torch.cat(deltas_lv, 1))
+        rpn_cls, rpn_box = self.rpn_losses(lg_all, dl_all, anchors, gt_boxes, gt_count, img_hw)
         props, _ = self.proposals(logits_lv, deltas_lv, anchors_lv, img_hw, True)
-        rois, labels, gidx, tgt, is_fg = self.sample_rois(props, gt_boxes.float(), gt_labels, gt_count)
+        rois5 = rois5_fg = None
+        if self._fused_targets_ok(props) and gt_boxes.shape[1] > 0:
+            rois, labels, gidx, tgt, is_fg, rois5, rois5_fg = self._sample_rois_fused(props, gt_boxes, gt_labels,
+                                                                                       gt_count)
+        else:
+            rois, labels, gidx, tgt, is_fg = self.sample_rois(props, gt_boxes.float(), gt_labels, gt_count)
         B, N = labels.shape
         feats = [self._nhwc(p) for p in P[:4]]
         scales = [1.0 / s for s in cfg.anchor_strides[:4]]
-        roi_feat = V.roi_align(feats, self._with_batch(rois), (7, 7), scales)
+        roi_feat = V.roi_align(feats, rois5 if rois5 is not None else self._with_batch(rois), (7, 7), scales)
         cls_logits, box_deltas = self.box_head(roi_feat)
         lab = labels.reshape(-1)
         # softmax CE (mean) + huber(1) of the labelled class's deltas over the fg RoIs / (B * N)
@@ -532,7 +679,8 @@ class MaskRCNN(nn.Module):
             fg_rois = rois[:, :nfg]
             fg_valid = is_fg[:, :nfg].reshape(-1).float()
             fg_lab = labels[:, :nfg].reshape(-1)
-            mf = V.roi_align(feats, self._with_batch(fg_rois), (14, 14), scales)
+            mf = V.roi_align(feats, rois5_fg if rois5_fg is not None else self._with_batch(fg_rois), (14, 14),
+                             scales)
             ml = self.mask_head(mf)                                               # [R, 80, 28, 28]
             G = (gt_mask_table if gt_mask_table is not None else gt_masks).shape[1]
             flat_gid = (torch.arange(B, device=images.device)[:, None] * G + gidx[:, :nfg]).reshape(-1)

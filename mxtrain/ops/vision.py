@@ -262,10 +262,12 @@ def nms(boxes: torch.Tensor, scores: torch.Tensor, thr: float, max_out: Optional
 
 
 # ============================================================================ matching
-def match_boxes(anchors: torch.Tensor, gt: torch.Tensor, gcount: torch.Tensor, low_quality: bool = True):
+def match_boxes(anchors: torch.Tensor, gt: torch.Tensor, gcount: torch.Tensor, low_quality: bool = True,
+                int32: bool = False):
     """anchors [A, 4] (shared) or [B, A, 4]; gt [B, G, 4] (rows >= gcount[b] ignored).
     Returns (max_iou [B, A], argmax [B, A] (-1 if no gt), lowq [B, A] gt index forced by
-    the low-quality rule or -1)."""
+    the low-quality rule or -1); ``int32``: the index tensors as the kernel writes them
+    (GPU; no int64 conversion launches)."""
     per_image = anchors.dim() == 3
     B, G = gt.shape[0], gt.shape[1]
     A = anchors.shape[-2]
@@ -279,6 +281,8 @@ def match_boxes(anchors: torch.Tensor, gt: torch.Tensor, gcount: torch.Tensor, l
         lq = torch.empty(B, A, dtype=torch.int32, device=anchors.device) if low_quality else None
         _lib.call("mx_match", _lib.ptr(an), A, int(per_image), _lib.ptr(g), _lib.ptr(gc), B, G, _lib.ptr(mi),
                   _lib.ptr(am), _lib.ptr(gb), _lib.ptr(lq), _lib.stream())
+        if int32:
+            return mi, am, lq
         return mi, am.long(), (lq.long() if lq is not None else None)
     mis, ams, lqs = [], [], []
     for b in range(B):
@@ -338,7 +342,16 @@ def decode_boxes(ref: torch.Tensor, deltas: torch.Tensor, weights=(1.0, 1.0, 1.0
 
 
 def encode_boxes(ref: torch.Tensor, gt: torch.Tensor, weights=(1.0, 1.0, 1.0, 1.0)) -> torch.Tensor:
+    """Box-regression targets of gt [N, 4] w.r.t. ref [N, 4] (fp32 [N, 4]); one launch on the
+    GPU (csrc/dettarget.hip), the PyTorch formula below otherwise."""
     wx, wy, ww, wh = weights
+    if _lib.use_hip(gt) and gt.dim() == 2 and ref.shape[-1] == 4 and gt.shape[0] > 0:
+        r = ref.float().contiguous()
+        g = gt.float().contiguous()
+        out = torch.empty(g.shape[0], 4, dtype=torch.float32, device=g.device)
+        _lib.call("mx_encode_boxes", _lib.ptr(r), int(r.numel() == 4 and g.shape[0] != 1), _lib.ptr(g), g.shape[0],
+                  float(wx), float(wy), float(ww), float(wh), _lib.ptr(out), _lib.stream())
+        return out
     rw = (ref[:, 2] - ref[:, 0]).clamp(min=1e-6)
     rh = (ref[:, 3] - ref[:, 1]).clamp(min=1e-6)
     rcx = ref[:, 0] + 0.5 * rw
@@ -431,14 +444,18 @@ def topk_rows(x: torch.Tensor, k: int, largest: bool = True):
         # workgroup per row), each <= 32k
         nc = max(-(-n // 32768), min(int(math.sqrt(n / k)) + 1, 32768 // k))
         c = -(-n // nc)
+        while nc > 1 and n - (nc - 1) * c < k:   # every chunk, the ragged last one too, >= k long
+            nc -= 1
+            c = -(-n // nc)
         if k > c or c > 32768 or nc * k > 32768:
             return x.topk(k, dim=1, largest=largest)
-        xx = x if (x.stride(0) == n and nc * c == n) else torch.cat(
-            [x, x.new_full((R, nc * c - n), float("-inf") if largest else float("inf"))], 1)
-        v1, i1 = topk_rows(xx.view(R * nc, c), k, largest)
-        i1 = i1.view(R, nc, k) + torch.arange(0, nc * c, c, device=x.device).view(1, nc, 1)
-        v2, j = topk_rows(v1.view(R, nc * k), k, largest)
-        return v2, torch.gather(i1.view(R, nc * k), 1, j)
+        cv = torch.empty((R * nc, k), dtype=torch.float32, device=x.device)
+        ci = torch.empty((R * nc, k), dtype=torch.int64, device=x.device)
+        ov = torch.empty((R, k), dtype=torch.float32, device=x.device)
+        oi = torch.empty((R, k), dtype=torch.int64, device=x.device)
+        _lib.call("mx_topk_rows_long", x.data_ptr(), R, n, x.stride(0), nc, c, k, int(largest), cv.data_ptr(),
+                  ci.data_ptr(), ov.data_ptr(), oi.data_ptr(), _lib.stream())
+        return ov, oi
     ov = torch.empty((R, k), dtype=torch.float32, device=x.device)
     oi = torch.empty((R, k), dtype=torch.int64, device=x.device)
     _lib.call("mx_topk_rows", x.data_ptr(), R, n, x.stride(0), k, int(largest), ov.data_ptr(), oi.data_ptr(),
@@ -475,8 +492,9 @@ def level_topk_decode(logits_lv: Sequence[torch.Tensor], deltas_lv: Sequence[tor
     B = logits_lv[0].shape[0]
     lg0 = logits_lv[0]
     ok = (_lib.use_hip(lg0) and k <= 2048 and B * L <= _lib.query("mx_topk_max_rows")
-          and all(t.dtype == torch.bfloat16 and t.is_contiguous() for t in logits_lv)
-          and all(t.dtype == torch.bfloat16 and t.is_contiguous() for t in deltas_lv)
+          and all(t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1 for t in logits_lv)
+          and all(t.dtype == torch.bfloat16 and t.dim() == 3 and t.stride(2) == 1 and t.stride(1) == 4
+                  for t in deltas_lv)
           and all(t.dtype == torch.float32 and t.is_contiguous() for t in anchors_lv))
     if not ok:
         return _level_topk_decode_ref(logits_lv, deltas_lv, anchors_lv, img_hw, k)
@@ -486,7 +504,8 @@ def level_topk_decode(logits_lv: Sequence[torch.Tensor], deltas_lv: Sequence[tor
     for b in range(B):
         for lg, dl, an in zip(logits_lv, deltas_lv, anchors_lv):
             n = lg.shape[1]
-            rows += [lg.data_ptr() + 2 * b * n, dl.data_ptr() + 2 * 4 * b * n, an.data_ptr(), n, b, 0]
+            # (rows may be views of the flat all-level tensors: row stride, not n)
+            rows += [lg.data_ptr() + 2 * b * lg.stride(0), dl.data_ptr() + 2 * b * dl.stride(0), an.data_ptr(), n, b, 0]
     chunk = _lib.query("mx_topk_chunk")
     nchunks = sum((lg.shape[1] + chunk - 1) // chunk for lg in logits_lv) * B
     key = (str(dev), R)

@@ -6,7 +6,8 @@ per library per round (A, B, A, B, ...); each child times forward, input gradien
 weight gradient of every shape over ITERS calls after warm-up (events), and checks both
 builds produce the same outputs (max relative difference printed).
     python scripts/conv_ab.py --a mxtrain/lib/ab/libmxkernels_a.so [--b mxtrain/lib/libmxkernels.so]
-        [--rounds 3] [--imgs 4]"""
+        [--rounds 3] [--imgs 4]
+    python scripts/conv_ab.py --toggle mx_conv_fwd_bk32     # one library, A = setter(0), B = setter(1)"""
 import argparse
 import json
 import os
@@ -28,12 +29,15 @@ SHAPES = [
 ]
 
 
-def child(lib, imgs, iters, out_path):
+def child(lib, imgs, iters, out_path, setting=None):
     sys.path.insert(0, REPO)
     import torch
     from mxtrain.ops import _lib
     _lib.LIB_PATH = os.path.abspath(lib)
     from mxtrain.ops import convwg
+    if setting:
+        fn, val = setting.split("=")
+        _lib._fn(fn)(int(val))
     cl = torch.channels_last
     torch.manual_seed(0)
     res = {}
@@ -72,7 +76,9 @@ def child(lib, imgs, iters, out_path):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--a", required=True)
+    ap.add_argument("--a", default=None)
+    ap.add_argument("--toggle", default=None, help="exported setter: A runs it with 0, B with 1 (same library)")
+    ap.add_argument("--set", default=None)
     ap.add_argument("--b", default=os.path.join(REPO, "mxtrain", "lib", "libmxkernels.so"))
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--imgs", type=int, default=4)
@@ -81,8 +87,10 @@ def main():
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     if a.child:
-        child(a.child, a.imgs, a.iters, a.out)
+        child(a.child, a.imgs, a.iters, a.out, a.set)
         return
+    if a.toggle:
+        a.a = a.b
     import statistics
     import tempfile
     times = {"A": {}, "B": {}}
@@ -90,8 +98,9 @@ def main():
     for r in range(a.rounds):
         for tag, lib in (("A", a.a), ("B", a.b)):
             out = tempfile.mktemp(suffix=".json")
-            subprocess.run([sys.executable, __file__, "--a", a.a, "--child", lib, "--out", out, "--imgs",
-                            str(a.imgs), "--iters", str(a.iters)], check=True)
+            extra = ["--set", f"{a.toggle}={0 if tag == 'A' else 1}"] if a.toggle else []
+            subprocess.run([sys.executable, __file__, "--child", lib, "--out", out, "--imgs",
+                            str(a.imgs), "--iters", str(a.iters)] + extra, check=True)
             for k, v in json.load(open(out)).items():
                 times[tag].setdefault(k, []).append(v)
             if r == 0:
@@ -99,7 +108,8 @@ def main():
                 outs[tag] = torch.load(out + ".pt", weights_only=True)
             os.remove(out)
             os.remove(out + ".pt")
-    print(f"conv A/B at {a.imgs} images: A = {a.a}, B = {a.b}; median us over {a.rounds} rounds")
+    what = f"{a.toggle} 0 / 1" if a.toggle else f"A = {a.a}, B = {a.b}"
+    print(f"conv A/B at {a.imgs} images: {what}; median us over {a.rounds} rounds")
     ta = tb = 0.0
     for k in times["A"]:
         ma, mb = statistics.median(times["A"][k]), statistics.median(times["B"].get(k, [float("nan")]))

@@ -1,0 +1,157 @@
+"""Fused Mask R-CNN training targets (csrc/dettarget.hip) against their PyTorch definitions
+(models/maskrcnn.py rpn_targets / sample_rois) on the same random draws: the sampled anchors
+and RoIs must be identical, the regression targets equal to fp32 rounding.  Also the
+two-launch long-row top-k (ragged last chunk, indices mapped in the merge stage) against
+torch.topk, and the fused box encoder against the PyTorch formula."""
+import types
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _fake_model():
+    from mxtrain.models.maskrcnn import MaskRCNNConfig
+    return types.SimpleNamespace(cfg=MaskRCNNConfig())
+
+
+def _anchors(H, W):
+    from mxtrain.models.maskrcnn import MaskRCNNConfig, level_anchors
+    cfg = MaskRCNNConfig()
+    lv = [level_anchors(s, z, cfg.anchor_ratios, (H + s - 1) // s, (W + s - 1) // s, DEV)
+          for s, z in zip(cfg.anchor_strides, cfg.anchor_sizes)]
+    return torch.cat(lv, 0)
+
+
+def _gt(B, G, H, W, counts, seed):
+    g = torch.Generator().manual_seed(seed)
+    xy = torch.rand(B, G, 2, generator=g) * torch.tensor([W * 0.8, H * 0.8])
+    wh = 8 + torch.rand(B, G, 2, generator=g) * torch.tensor([W * 0.4, H * 0.4])
+    boxes = torch.cat([xy, xy + wh], -1)
+    for b, c in enumerate(counts):
+        boxes[b, c:] = 0
+    return boxes.to(DEV), torch.tensor(counts, dtype=torch.int32, device=DEV)
+
+
+@pytest.mark.parametrize("counts", [[5, 17], [0, 3, 30]])
+def test_rpn_targets_fused_matches_torch(counts):
+    from mxtrain.models.maskrcnn import MaskRCNN
+    H, W = 320, 448
+    B, G = len(counts), 32
+    m = _fake_model()
+    anchors = _anchors(H, W)
+    gt, gc = _gt(B, G, H, W, counts, 1)
+    hw = torch.tensor([[H - 13.0, W - 7.0]] * B, device=DEV)
+    torch.cuda.manual_seed(11)
+    ref = MaskRCNN.rpn_targets(m, anchors, gt, gc, hw)
+    torch.cuda.manual_seed(11)
+    got = MaskRCNN._rpn_targets_fused(m, anchors, gt, gc, hw)
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+    assert int(got[0].sum()) > 0 and int(got[1].sum()) > 0
+    assert (got[0].sum(1) + got[1].sum(1) <= 256).all()
+    torch.testing.assert_close(got[2], ref[2], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("counts", [[5, 17], [0, 3, 30]])
+def test_sample_rois_fused_matches_torch(counts):
+    from mxtrain.models.maskrcnn import MaskRCNN
+    H, W = 320, 448
+    B, G, K = len(counts), 32, 1000
+    m = _fake_model()
+    gt, gc = _gt(B, G, H, W, counts, 2)
+    labels = torch.randint(1, 81, (B, G), device=DEV)
+    g = torch.Generator().manual_seed(3)
+    # proposals: jittered copies of the gt boxes (enough foreground) and random boxes
+    base = gt.cpu()[:, torch.randint(0, G, (K,), generator=g)]
+    props = (base + torch.randn(B, K, 4, generator=g) * 6).to(DEV)
+    rnd = torch.rand(B, K, 2, generator=g) * torch.tensor([W, H]) * 0.9
+    props[:, K // 2:] = torch.cat([rnd, rnd + 20], -1)[:, K // 2:].to(DEV)
+    torch.cuda.manual_seed(5)
+    ref = MaskRCNN.sample_rois(m, props, gt.float(), labels, gc)
+    torch.cuda.manual_seed(5)
+    got = MaskRCNN._sample_rois_fused(m, props, gt, labels, gc)
+    rois, lab, gidx, tgt, is_fg, rois5, rois5_fg = got
+    assert torch.equal(rois, ref[0]) and torch.equal(lab, ref[1]) and torch.equal(gidx, ref[2])
+    assert torch.equal(is_fg, ref[4])
+    torch.testing.assert_close(tgt, ref[3], rtol=1e-5, atol=1e-4)
+    N = rois.shape[1]
+    nfg = rois5_fg.shape[0] // B
+    bi = torch.arange(B, device=DEV, dtype=torch.float32)
+    assert torch.equal(rois5, torch.cat([bi[:, None, None].expand(B, N, 1), rois], -1).reshape(-1, 5))
+    assert torch.equal(rois5_fg, torch.cat([bi[:, None, None].expand(B, nfg, 1), rois[:, :nfg]], -1).reshape(-1, 5))
+    if sum(counts) > 0:
+        assert int(is_fg.sum()) > 0
+
+
+@pytest.mark.parametrize("n,k,largest", [(268_569, 128, False), (268_569, 256, False), (70_001, 100, True),
+                                         (40_000, 2048, True)])
+def test_topk_rows_long_matches_torch(n, k, largest):
+    from mxtrain.ops import vision as V
+    g = torch.Generator().manual_seed(n + k)
+    x = torch.rand(3, n, generator=g)
+    x[:, ::7] = 2.0                       # many ties (the rank-select keys)
+    x = x.to(DEV)
+    v, i = V.topk_rows(x, k, largest=largest)
+    rv, _ = x.topk(k, dim=1, largest=largest)
+    assert torch.equal(v, rv)
+    assert torch.equal(torch.gather(x, 1, i), v)
+    assert all(len(set(r.tolist())) == k for r in i.cpu())
+
+
+def test_encode_boxes_fused_matches_torch():
+    from mxtrain.ops import _lib
+    from mxtrain.ops import vision as V
+    g = torch.Generator().manual_seed(9)
+    a = torch.rand(5000, 2, generator=g) * 500
+    ref = torch.cat([a, a + 1 + torch.rand(5000, 2, generator=g) * 100], -1).to(DEV)
+    b = torch.rand(5000, 2, generator=g) * 500
+    gt = torch.cat([b, b + 1 + torch.rand(5000, 2, generator=g) * 100], -1).to(DEV)
+    out = V.encode_boxes(ref, gt, (10.0, 10.0, 5.0, 5.0))
+    _lib_on = _lib.use_hip(gt)
+    assert _lib_on
+    wx, wy, ww, wh = 10.0, 10.0, 5.0, 5.0
+    rw = (ref[:, 2] - ref[:, 0]).clamp(min=1e-6)
+    rh = (ref[:, 3] - ref[:, 1]).clamp(min=1e-6)
+    gw = (gt[:, 2] - gt[:, 0]).clamp(min=1e-6)
+    gh = (gt[:, 3] - gt[:, 1]).clamp(min=1e-6)
+    exp = torch.stack([wx * (gt[:, 0] + 0.5 * gw - ref[:, 0] - 0.5 * rw) / rw,
+                       wy * (gt[:, 1] + 0.5 * gh - ref[:, 1] - 0.5 * rh) / rh,
+                       ww * torch.log(gw / rw), wh * torch.log(gh / rh)], 1)
+    torch.testing.assert_close(out, exp, rtol=1e-5, atol=1e-4)
+
+
+def test_rpn_canvas_unpack_flat_matches_per_level():
+    """The one-launch flat unpack of the RPN head's canvas output (and its one-launch
+    canvas gradient) equals the per-level slices (and their scattered gradients)."""
+    from mxtrain.models.maskrcnn import _UnpackFlat, _UnpackLevels, level_canvas
+    B, na, C = 2, 3, 16
+    shapes = [(50, 84), (25, 42), (13, 21), (7, 11), (4, 6)]
+    lay = level_canvas(shapes)
+    Hc, Wc, offs = lay
+    geo = [(y0, x0, h, w) for (y0, x0), (h, w) in zip(offs, shapes)]
+    g = torch.Generator().manual_seed(4)
+    o = torch.randn(B, C, Hc, Wc, generator=g).to(torch.bfloat16).to(DEV).contiguous(memory_format=torch.channels_last)
+    o1 = o.detach().clone().requires_grad_(True)
+    o2 = o.detach().clone().requires_grad_(True)
+    ref = _UnpackLevels.apply(o1, geo, na)
+    geo5, off = [], 0
+    for y0, x0, h, w in geo:
+        geo5 += [y0, x0, h, w, off]
+        off += h * w * na
+    lg, dl = _UnpackFlat.apply(o2, tuple(geo5), na, off)
+    assert torch.equal(lg, torch.cat(ref[0::2], 1)) and torch.equal(dl, torch.cat(ref[1::2], 1))
+    glg = torch.randn(lg.shape, generator=g).to(torch.bfloat16).to(DEV)
+    gdl = torch.randn(dl.shape, generator=g).to(torch.bfloat16).to(DEV)
+    (lg.float() * glg.float()).sum().backward(retain_graph=True)
+    (dl.float() * gdl.float()).sum().backward()
+    gl_lv, gd_lv, off = [], [], 0
+    for _, _, h, w in geo:
+        n = h * w * na
+        gl_lv.append(glg[:, off:off + n])
+        gd_lv.append(gdl[:, off:off + n])
+        off += n
+    loss = sum((r.float() * t.float()).sum() for r, t in zip(ref, [x for pair in zip(gl_lv, gd_lv) for x in pair]))
+    loss.backward()
+    assert torch.equal(o2.grad, o1.grad)
