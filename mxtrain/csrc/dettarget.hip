@@ -310,3 +310,97 @@ MX_EXPORT int mx_rpn_pack_grad(const void* dlogits, const void* ddeltas, int B, 
                      (const uint16_t*)ddeltas, Hc, Wc, C, na, g, A, (uint16_t*)d);
   return hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------ FPN fan-in
+// The gradient of an FPN level that feeds the RPN canvas, the box RoIAlign and the mask
+// RoIAlign: out = a + b + c in ONE pass (NHWC bf16, 8 channels per thread, fp32 sum), a
+// read through its canvas pitch (a strided slice of the canvas gradient), b / c contiguous
+// (null = absent).  Autograd summed them with two adds, one of them PyTorch's
+// non-vectorised strided kernel: 6 passes over the level instead of 4.
+namespace {
+__global__ __launch_bounds__(256) void add3_nhwc_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ a,
+                                                        int64_t a_img, int64_t a_row, const uint16_t* __restrict__ b,
+                                                        const uint16_t* __restrict__ c, int H, int W, int C8,
+                                                        int64_t nvec) {
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const int64_t pix = v / C8;
+    const int c8 = (int)(v - pix * C8);
+    const int64_t n = pix / ((int64_t)H * W);
+    const int rem = (int)(pix - n * H * W);
+    const int y = rem / W, x = rem - (rem / W) * W;
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t[8];
+    if (a) {
+      unpack8(reinterpret_cast<const uint4*>(a + n * a_img + (int64_t)y * a_row + (int64_t)x * C8 * 8)[c8], t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += t[j];
+    }
+    if (b) {
+      unpack8(reinterpret_cast<const uint4*>(b)[v], t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += t[j];
+    }
+    if (c) {
+      unpack8(reinterpret_cast<const uint4*>(c)[v], t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += t[j];
+    }
+    reinterpret_cast<uint4*>(out)[v] = pack8(s);
+  }
+}
+}  // namespace
+
+// out [B][H][W][C] = a + b + c; a: element strides (a_img, a_row) per image / row, channels
+// and pixels of a row contiguous; C % 8 == 0, every pointer 16-B aligned
+MX_EXPORT int mx_add3_nhwc(void* out, const void* a, int64_t a_img, int64_t a_row, const void* b, const void* c, int B,
+                           int H, int W, int C, hipStream_t s) {
+  if (C % 8 || B <= 0) return (int)hipErrorInvalidValue;
+  const int64_t nvec = (int64_t)B * H * W * (C / 8);
+  const int64_t blocks = (nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192;
+  hipLaunchKernelGGL(add3_nhwc_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (uint16_t*)out, (const uint16_t*)a,
+                     a_img, a_row, (const uint16_t*)b, (const uint16_t*)c, H, W, C / 8, nvec);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ RPN canvas pack
+// The FPN levels (NHWC bf16, level l [B][h_l][w_l][C]) onto the RPN canvas [B][Hc][Wc][C]
+// in ONE pass over the canvas: level pixels copied, everything between them zero (the
+// former zero-fill of the whole canvas + one row-copy launch per level wrote most of it
+// twice).  16-B vectors; srcs: device pointer array (host-built, passed by value).
+namespace {
+struct PackSrc {
+  const uint16_t* p[kMaxLevels];
+};
+__global__ __launch_bounds__(256) void rpn_pack_kernel(uint16_t* __restrict__ dst, PackSrc src, LevelGeo g, int Hc,
+                                                       int Wc, int C8, int64_t nvec) {
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const int64_t pix = v / C8;
+    const int c8 = (int)(v - pix * C8);
+    const int64_t n = pix / ((int64_t)Hc * Wc);
+    const int rem = (int)(pix - n * Hc * Wc);
+    const int cy = rem / Wc, cx = rem - (rem / Wc) * Wc;
+    uint4 val = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = 0; i < g.L; ++i) {
+      const int y = cy - g.y0[i], x = cx - g.x0[i];
+      if (y >= 0 && y < g.h[i] && x >= 0 && x < g.w[i]) {
+        val = reinterpret_cast<const uint4*>(src.p[i] + (((int64_t)n * g.h[i] + y) * g.w[i] + x) * C8 * 8)[c8];
+        break;
+      }
+    }
+    reinterpret_cast<uint4*>(dst)[v] = val;
+  }
+}
+}  // namespace
+
+// srcs: host array of L device pointers; geo: host int32 [L][5] (y0, x0, h, w, unused)
+MX_EXPORT int mx_rpn_pack(void* dst, const void* const* srcs, const int* geo, int L, int B, int Hc, int Wc, int C,
+                          hipStream_t s) {
+  LevelGeo g;
+  if (!make_geo(geo, L, g) || C % 8 || B <= 0) return (int)hipErrorInvalidValue;
+  PackSrc ps = {};
+  for (int i = 0; i < L; ++i) ps.p[i] = (const uint16_t*)srcs[i];
+  const int64_t nvec = (int64_t)B * Hc * Wc * (C / 8);
+  const int64_t blocks = (nvec + 255) / 256 < 16384 ? (nvec + 255) / 256 : 16384;
+  hipLaunchKernelGGL(rpn_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (uint16_t*)dst, ps, g, Hc, Wc, C / 8,
+                     nvec);
+  return hipGetLastError();
+}

@@ -223,14 +223,21 @@ class _PackLevels(torch.autograd.Function):
         Hc, Wc, offs = lay
         p0 = levels[0]
         B, C = p0.shape[0], p0.shape[1]
-        c = torch.empty(B, C, Hc, Wc, dtype=p0.dtype, device=p0.device, memory_format=torch.channels_last).zero_()
-        for (y0, x0), p in zip(offs, levels):
-            if (p.is_cuda and p.dtype == torch.bfloat16 and p.is_contiguous(memory_format=torch.channels_last)
-                    and C % 8 == 0 and p.data_ptr() % 16 == 0):
-                # one vectorised launch per level (csrc/vision.hip copy_rows_kernel)
-                _lib.call("mx_copy_rows", c.data_ptr(), p.data_ptr(), B, p.shape[2], p.shape[3] * C, Hc, Wc * C,
-                          (y0 * Wc + x0) * C, _lib.stream())
-            else:
+        c = torch.empty(B, C, Hc, Wc, dtype=p0.dtype, device=p0.device, memory_format=torch.channels_last)
+        if (all(p.is_cuda and p.dtype == torch.bfloat16 and p.is_contiguous(memory_format=torch.channels_last)
+                and p.data_ptr() % 16 == 0 for p in levels) and C % 8 == 0 and len(levels) <= 8
+                and _lib.use_hip(p0)):
+            # every canvas pixel written once: the levels copied, the gaps zeroed
+            # (csrc/dettarget.hip rpn_pack_kernel)
+            geo = []
+            for (y0, x0), p in zip(offs, levels):
+                geo += [y0, x0, p.shape[2], p.shape[3], 0]
+            srcs = (ctypes.c_void_p * len(levels))(*[p.data_ptr() for p in levels])
+            _lib.call("mx_rpn_pack", c.data_ptr(), srcs, (ctypes.c_int * len(geo))(*geo), len(levels), B, Hc, Wc, C,
+                      _lib.stream())
+        else:
+            c.zero_()
+            for (y0, x0), p in zip(offs, levels):
                 c[:, :, y0:y0 + p.shape[2], x0:x0 + p.shape[3]].copy_(p)
         ctx.geo = [(y0, x0, p.shape[2], p.shape[3]) for (y0, x0), p in zip(offs, levels)]
         return c
@@ -299,6 +306,41 @@ class _UnpackFlat(torch.autograd.Function):
         _lib.call("mx_rpn_pack_grad", _lib.ptr(glg), _lib.ptr(gdl), B, Hc, Wc, C, ctx.na, arr, len(ctx.geo5) // 5,
                   ctx.A, d.data_ptr(), _lib.stream())
         return d.permute(0, 3, 1, 2), None, None, None
+
+
+class _FanOut3(torch.autograd.Function):
+    """An FPN level (NCHW view of channels_last bf16) handed to its three consumers -- the
+    RPN canvas, the box RoIAlign and the mask RoIAlign -- as three aliases, so backward gets
+    their gradients separately and sums them in ONE pass (csrc/dettarget.hip add3_nhwc,
+    the canvas slice read through its pitch) instead of autograd's two adds."""
+
+    @staticmethod
+    def forward(ctx, p):
+        ctx.set_materialize_grads(False)
+        ctx.shape = p.shape
+        return p.view_as(p), p.view_as(p), p.view_as(p)
+
+    @staticmethod
+    def backward(ctx, ga, gb, gc):
+        B, C, H, W = ctx.shape
+        ref = next((g for g in (ga, gb, gc) if g is not None), None)
+        if ref is None:
+            return None
+        cl = torch.channels_last
+        a = ga
+        if a is not None and not (a.stride(1) == 1 and a.stride(3) == C and a.data_ptr() % 16 == 0):
+            a = a.contiguous(memory_format=cl)
+        b = gb.contiguous(memory_format=cl) if gb is not None else None
+        c = gc.contiguous(memory_format=cl) if gc is not None else None
+        out = torch.empty(B, H, W, C, dtype=ref.dtype, device=ref.device)
+        _lib.call("mx_add3_nhwc", out.data_ptr(), _lib.ptr(a), a.stride(0) if a is not None else 0,
+                  a.stride(2) if a is not None else 0, _lib.ptr(b), _lib.ptr(c), B, H, W, C, _lib.stream())
+        return out.permute(0, 3, 1, 2)
+
+
+def _fanout_ok(p: torch.Tensor) -> bool:
+    return (p.is_cuda and p.dtype == torch.bfloat16 and p.is_contiguous(memory_format=torch.channels_last)
+            and p.shape[1] % 8 == 0 and p.data_ptr() % 16 == 0 and _lib.use_hip(p))
 
 
 class BoxHead(nn.Module):
@@ -645,7 +687,18 @@ class MaskRCNN(nn.Module):
         gt_mask_table int32 [B, G, 5]) the flat uint8 buffer of packed instance crops."""
         cfg = self.cfg
         P = self.features(images)
-        lv = self.rpn.forward_levels(P)
+        # training: the RoIAlign levels reach the FPN through _FanOut3 (one fused gradient sum
+        # per level for the canvas / box / mask consumers)
+        fan = (self.training and self.fused_targets and torch.is_grad_enabled()
+               and all(_fanout_ok(p) for p in P[:4]))
+        if fan:
+            f3 = [_FanOut3.apply(p) for p in P[:4]]
+            P_rpn = [f[0] for f in f3] + list(P[4:])
+            P_box = [f[1] for f in f3]
+            P_mask = [f[2] for f in f3]
+        else:
+            P_rpn = P_box = P_mask = P
+        lv = self.rpn.forward_levels(P_rpn)
         logits_lv = [l for l, _ in lv]
         deltas_lv = [d for _, d in lv]
         anchors_lv = self.anchors([(p.shape[2], p.shape[3]) for p in P], images.device)
@@ -665,7 +718,7 @@ class MaskRCNN(nn.Module):
         else:
             rois, labels, gidx, tgt, is_fg = self.sample_rois(props, gt_boxes.float(), gt_labels, gt_count)
         B, N = labels.shape
-        feats = [self._nhwc(p) for p in P[:4]]
+        feats = [self._nhwc(p) for p in P_box[:4]]
         scales = [1.0 / s for s in cfg.anchor_strides[:4]]
         roi_feat = V.roi_align(feats, rois5 if rois5 is not None else self._with_batch(rois), (7, 7), scales)
         cls_logits, box_deltas = self.box_head(roi_feat)
@@ -679,7 +732,8 @@ class MaskRCNN(nn.Module):
             fg_rois = rois[:, :nfg]
             fg_valid = is_fg[:, :nfg].reshape(-1).float()
             fg_lab = labels[:, :nfg].reshape(-1)
-            mf = V.roi_align(feats, rois5_fg if rois5_fg is not None else self._with_batch(fg_rois), (14, 14),
+            mfeats = [self._nhwc(p) for p in P_mask[:4]]
+            mf = V.roi_align(mfeats, rois5_fg if rois5_fg is not None else self._with_batch(fg_rois), (14, 14),
                              scales)
             ml = self.mask_head(mf)                                               # [R, 80, 28, 28]
             G = (gt_mask_table if gt_mask_table is not None else gt_masks).shape[1]

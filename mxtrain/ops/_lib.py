@@ -127,6 +127,23 @@ SIGNATURES = {
     "mx_normalize_u8_nhwc": [P, P, I, I, I, P, P, P],
     "mx_crop_resize_masks": [P, I, I, P, P, I, I, P, P],
     "mx_crop_resize_mask_crops": [P, P, I, I, P, P, I, I, P, P],
+    "mx_topk_rows_long": [P, I, I, I, I, I, I, I, P, P, P, P, P],
+    # dettarget.hip
+    "mx_encode_boxes": [P, I, P, I, F, F, F, F, P, P],
+    "mx_rpn_keys": [P, I, I, P, P, P, P, P, P, I, F, F, P, P, P, P, P, P],
+    "mx_rpn_select": [P, P, I, P, P, I, I, I, I, P, P, P],
+    "mx_roi_candidates": [P, I, P, P, I, I, P, P, P],
+    "mx_roi_fgkey": [P, P, P, I, F, P, P],
+    "mx_roi_order": [P, P, I, P, P, P, I, I, F, P, P, P],
+    "mx_roi_gather": [P, I, I, I, P, I, P, P, P, P, I, F, F, F, F, P, P, P, P, P, P, P, P],
+    "mx_rpn_unpack": [P, I, I, I, I, I, P, I, I, P, P, P],
+    "mx_rpn_pack_grad": [P, P, I, I, I, I, I, P, I, I, P, P],
+    "mx_add3_nhwc": [P, P, I64, I64, P, P, I, I, I, I, P],
+    "mx_rpn_pack": [P, P, P, I, I, I, I, I, P],
+    # knobs (one int; return the previous setting)
+    "mx_flash_dropmask_variant": [I],
+    "mx_conv_fwd_bk32": [I],
+    "mx_norm_bwd_max_blocks": [I],
 }
 
 

@@ -155,3 +155,25 @@ def test_rpn_canvas_unpack_flat_matches_per_level():
     loss = sum((r.float() * t.float()).sum() for r, t in zip(ref, [x for pair in zip(gl_lv, gd_lv) for x in pair]))
     loss.backward()
     assert torch.equal(o2.grad, o1.grad)
+
+
+def test_fpn_fanout_gradient_sum():
+    """_FanOut3: the three consumers' gradients of an FPN level (a strided canvas slice, two
+    contiguous NHWC RoIAlign gradients, any of them absent) summed in one pass."""
+    from mxtrain.models.maskrcnn import _FanOut3
+    B, C, H, W = 2, 256, 25, 42
+    cl = torch.channels_last
+    g = torch.Generator().manual_seed(8)
+    bf = lambda *s: torch.randn(*s, generator=g).to(torch.bfloat16).to(DEV)  # noqa: E731
+    p = bf(B, C, H, W).contiguous(memory_format=cl).requires_grad_(True)
+    canvas = bf(B, C, H + 30, W + 7).contiguous(memory_format=cl)
+    ga = canvas[:, :, 10:10 + H, 3:3 + W]                   # canvas-gradient slice (strided)
+    gb = bf(B, H, W, C).permute(0, 3, 1, 2)
+    gc = bf(B, H, W, C).permute(0, 3, 1, 2)
+    for use in ((1, 1, 1), (1, 1, 0), (0, 1, 1), (1, 0, 0)):
+        p.grad = None
+        a, b, c = _FanOut3.apply(p)
+        loss = sum((o.float() * t.float()).sum() for o, t, u in zip((a, b, c), (ga, gb, gc), use) if u)
+        loss.backward()
+        exp = sum(t.float() for t, u in zip((ga, gb, gc), use) if u)
+        torch.testing.assert_close(p.grad.float(), exp, rtol=1e-2, atol=2e-2)
