@@ -11,7 +11,6 @@ CPU / non-channels_last tensors take the plain PyTorch ops (same math).
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Optional
 
 import torch
@@ -20,9 +19,9 @@ import torch.nn.functional as F
 from . import _lib
 from . import convwg
 
-_ENABLED = os.environ.get("MXTRAIN_CONV_EPILOGUE", "1") == "1"
+_ENABLED = True
 # narrow 1x1 heads (Cout not a multiple of 64) as hipBLASLt GEMMs over the NHWC pixels
-_GEMM1X1 = os.environ.get("MXTRAIN_GEMM1X1", "1") == "1"
+_GEMM1X1 = True
 
 
 def _rows_cols(y: torch.Tensor):

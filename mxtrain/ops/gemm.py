@@ -13,7 +13,6 @@ error fallback; CPU tensors always use it.
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import List, Sequence, Tuple
 
 import torch
@@ -94,7 +93,7 @@ def _tile(variant):
 
 
 NUM_CU = 256
-_FORCE = os.environ.get("MXTRAIN_GEMM_VARIANT")
+_FORCE = None      # "variant[:splits]": benchmarking scripts pin the wgrad plan
 
 
 def plan(items, T: int):
@@ -144,7 +143,7 @@ def wgrad(gbuf, dy, x, accumulate: bool = True):
 # GeLU' + bias-gradient column partials).  Shapes the kernel does not tile go through
 # torch (part of the contract, like wgrad above); CPU tensors always do.
 _NT_TILE = {}
-_NT_FORCE = os.environ.get("MXTRAIN_GEMM_NT_VARIANT")
+_NT_FORCE = None   # benchmarking scripts pin the gemm_nt variant
 # preference order: big tiles first (less L2 traffic per FLOP), as long as one launch still
 # has >= ~one tile per CU
 _NT_ORDER = (0, 1, 4, 5, 3, 2)

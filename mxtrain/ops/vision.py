@@ -7,7 +7,6 @@ Conventions: boxes are fp32 ``[x1, y1, x2, y2]`` in input-image pixels; RoIs are
 from __future__ import annotations
 
 import ctypes
-import os
 import math
 from typing import List, Optional, Sequence, Tuple
 
@@ -95,9 +94,9 @@ def _ptr_array(ts, ctype=ctypes.c_void_p):
     return arr
 
 
-# MXTRAIN_ROIALIGN_TILED=0: the fp32-atomic backward (roi_align_bwd_kernel) instead of the
-# tiled one (roi_align_bwd_tile_kernel)
-_TILED = os.environ.get("MXTRAIN_ROIALIGN_TILED", "1") == "1"
+# the tiled backward (roi_align_bwd_tile_kernel) handles sr <= 2, C % 64 == 0, C <= 256; other
+# shapes take the fp32-atomic one (roi_align_bwd_kernel).  Tests flip this to compare the two.
+_TILED = True
 
 
 _WS_CACHE = {}

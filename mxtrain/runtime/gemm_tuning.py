@@ -27,8 +27,8 @@ def tuned_tables():
 
 def use_tuned_gemms(tune: bool = False, tables=None) -> int:
     """Enable TunableOp with the checked-in solution tables.  Returns the number of
-    tables accepted (0 on CPU / when disabled with MXTRAIN_TUNED_GEMM=0)."""
-    if not torch.cuda.is_available() or os.environ.get("MXTRAIN_TUNED_GEMM", "1") == "0":
+    tables accepted (0 on CPU)."""
+    if not torch.cuda.is_available():
         return 0
     import torch.cuda.tunable as tn
     tn.enable(True)

@@ -225,9 +225,6 @@ def main(argv=None):
     C.finalize(cfg, world, args.images_per_epoch)
     if device.type == "cuda" and hasattr(torch.backends.cuda, "preferred_blas_library"):
         torch.backends.cuda.preferred_blas_library("hipblaslt")
-    # MXTRAIN_MIOPEN=0: convolutions through torch's native GEMM path instead of MIOpen
-    if os.environ.get("MXTRAIN_MIOPEN", "1") == "0":
-        torch.backends.cudnn.enabled = False
     os.makedirs(args.logdir, exist_ok=True)
     log(f"Config: world {world} x {cfg.TRAIN.BATCH_SIZE_PER_GPU} img/GPU, device {device}, "
         f"lr {cfg.TRAIN.LR:.5f}, steps/epoch {cfg.TRAIN.STEPS_PER_EPOCH}, epochs {cfg.TRAIN.MAX_EPOCH}")
@@ -280,10 +277,10 @@ def main(argv=None):
     # found solver.  MIOPEN_FIND_MODE=FAST keeps the search to the fast candidates.
     # Measured on one MI355X: 1 img/GPU 51 -> 66 img/s, 4 img/GPU 108 -> 129 img/s; the
     # one-time search costs ~4 minutes on a fresh node (MIOpen's user find-db keeps it for
-    # later runs).  MXTRAIN_CONV_BENCHMARK=0 returns to immediate mode.
+    # later runs).
     # Training only: the fixed training canvases make the search a one-time cost; predict /
     # evaluate see arbitrary image sizes and stay in immediate mode (evaluate_epoch too).
-    torch.backends.cudnn.benchmark = os.environ.get("MXTRAIN_CONV_BENCHMARK", "1") == "1"
+    torch.backends.cudnn.benchmark = True
     if torch.backends.cudnn.benchmark:
         os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
         db = use_shipped_find_db()
@@ -295,7 +292,7 @@ def main(argv=None):
     prof = StepProfiler(rank, out_dir=os.path.join(args.logdir, "profile") if os.environ.get("MXTRAIN_PROFILE") else None)
     debug_finite = check_finite_enabled()
     train_sets = [COCODetection(cfg.DATA.BASEDIR, n, training=True) for n in cfg.DATA.TRAIN]
-    flat_sgd = device.type == "cuda" and os.environ.get("MXTRAIN_FLAT_SGD", "1") != "0"
+    flat_sgd = device.type == "cuda"
     # whole-step hipGraph: 1 GPU, or world > 1 with the fused flat SGD, whose bucketed
     # gradient all-reduces are captured into the graph -- RCCL by default, or the direct
     # xGMI kernel with MXTRAIN_XGMI=1/auto (checked against RCCL and timed on the live group)
