@@ -242,7 +242,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
 }
 
 constexpr int kBM = 128, kBN = 128, kBK = 64, kNT = 256;
-int g_conv_fwd_bk32 = 0;   // forward K-step depth 32 (up to four workgroups per CU) instead of 64
+// forward K-step depth: 0 -> 64, 1 -> 32 (16-KiB ring slots, up to four workgroups per CU),
+// 2 (default) -> 32 for 1x1 convolutions and Cin <= 128, where the reduction is a few K-steps
+// and the ring's fill dominates (scripts/conv_ab.py --toggle: 1x1 / Cin 128 forwards 5-15 %
+// faster, the 3x3 Cin 256 ones at P2 and the RPN canvas 14-16 % slower,
+// profiles/r5_s1/conv_ab_bk32.txt)
+int g_conv_fwd_bk32 = 2;
 
 // ================================================================================= forward
 // y[p][co] = act(sum over taps (r, s) and ci of X[pix(p, r, s)][ci] * W[co][r][s][ci] + b[co]
@@ -1115,7 +1120,8 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   const int64_t xbytes = N * cp.IH * cp.IW * (int64_t)cp.ldx * 2;
   if (cp.taps > 32 || xbytes >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   cp.xbytes = (uint32_t)xbytes;
-  const int bkt = g_conv_fwd_bk32 && cp.Cin % 32 == 0 ? 32 : 64;
+  const bool bk32 = g_conv_fwd_bk32 == 1 || (g_conv_fwd_bk32 == 2 && (cp.taps == 1 || cp.Cin <= 128));
+  const int bkt = bk32 && cp.Cin % 32 == 0 ? 32 : 64;
   cp.cib = cp.Cin / bkt;
   cp.nk = cp.taps * cp.cib;
   cp.tiles_n = Cout % 128 == 0 ? Cout / 128 : Cout / 64;
@@ -1155,7 +1161,8 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   return (int)hipGetLastError();
 }
 
-// forward K-step depth: 1 -> 32 (16-KiB ring slots), 0 -> 64; negative: query.  Returns the old value.
+// forward K-step depth: 1 -> 32 (16-KiB ring slots), 0 -> 64, 2 -> by shape (default);
+// negative: query.  Returns the old value.
 MX_EXPORT int mx_conv_fwd_bk32(int on) {
   const int old = g_conv_fwd_bk32;
   if (on >= 0) g_conv_fwd_bk32 = on;

@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--graph", choices=("auto", "0", "1"), default="auto",
                     help="whole-step hipGraph replay (train.py --mx-graph; auto = on for 1 GPU)")
+    ap.add_argument("--set", action="append", default=[],
+                    help="A/B hook: module:attr=int (e.g. mxtrain.ops.epilogue:_GEMM1X1=0) or "
+                         "lib:setter=int (a kernel-library setter, e.g. lib:mx_conv_fwd_bk32=0)")
     ap.add_argument("extra", nargs="*")
     a = ap.parse_args()
     rank = int(os.environ.get("RANK", os.environ.get("OMPI_COMM_WORLD_RANK", "0")))
@@ -37,6 +40,19 @@ def main():
         import time
         while not os.path.exists(os.path.join(a.data, "annotations", "instances_val2017.json")):
             time.sleep(0.5)
+    for kv in a.set:
+        import importlib
+        target, val = kv.split("=")
+        mod, attr = target.split(":")
+        if mod == "lib":
+            from mxtrain.ops import _lib
+            _lib._fn(attr)(int(val))
+        else:
+            obj = importlib.import_module(mod)
+            *path, last = attr.split(".")          # module:Class.attr reaches class attributes
+            for n in path:
+                obj = getattr(obj, n)
+            setattr(obj, last, type(getattr(obj, last))(int(val)))
     from mxtrain.workloads.maskrcnn import train
     out = a.out or os.path.join(REPO, "gpurun_out", "maskrcnn_bench.jsonl")
     os.makedirs(os.path.dirname(out), exist_ok=True)

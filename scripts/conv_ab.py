@@ -78,6 +78,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--a", default=None)
     ap.add_argument("--toggle", default=None, help="exported setter: A runs it with 0, B with 1 (same library)")
+    ap.add_argument("--vals", default="0,1", help="setter arguments of A and B with --toggle")
     ap.add_argument("--set", default=None)
     ap.add_argument("--b", default=os.path.join(REPO, "mxtrain", "lib", "libmxkernels.so"))
     ap.add_argument("--rounds", type=int, default=3)
@@ -98,7 +99,8 @@ def main():
     for r in range(a.rounds):
         for tag, lib in (("A", a.a), ("B", a.b)):
             out = tempfile.mktemp(suffix=".json")
-            extra = ["--set", f"{a.toggle}={0 if tag == 'A' else 1}"] if a.toggle else []
+            va, vb = a.vals.split(",")
+            extra = ["--set", f"{a.toggle}={va if tag == 'A' else vb}"] if a.toggle else []
             subprocess.run([sys.executable, __file__, "--child", lib, "--out", out, "--imgs",
                             str(a.imgs), "--iters", str(a.iters)] + extra, check=True)
             for k, v in json.load(open(out)).items():
@@ -108,7 +110,7 @@ def main():
                 outs[tag] = torch.load(out + ".pt", weights_only=True)
             os.remove(out)
             os.remove(out + ".pt")
-    what = f"{a.toggle} 0 / 1" if a.toggle else f"A = {a.a}, B = {a.b}"
+    what = f"{a.toggle} {a.vals.replace(',', ' / ')}" if a.toggle else f"A = {a.a}, B = {a.b}"
     print(f"conv A/B at {a.imgs} images: {what}; median us over {a.rounds} rounds")
     ta = tb = 0.0
     for k in times["A"]:

@@ -52,6 +52,9 @@ for s in $STEPS; do
       # one arbitrary python command: CMD="scripts/x.py args" (output to gpurun_out/$CMD_TAG.txt)
       timeout -k 10 ${T_CMD:-300} python $CMD > gpurun_out/${CMD_TAG:-cmd}.txt 2>&1; rc=$?
       tail -${CMD_TAIL:-20} gpurun_out/${CMD_TAG:-cmd}.txt; echo "cmd rc=$rc"; ok $rc || exit $rc ;;
+    cmd2)
+      timeout -k 10 ${T_CMD2:-300} python $CMD2 > gpurun_out/${CMD2_TAG:-cmd2}.txt 2>&1; rc=$?
+      tail -${CMD_TAIL:-20} gpurun_out/${CMD2_TAG:-cmd2}.txt; echo "cmd2 rc=$rc"; ok $rc || exit $rc ;;
     pmc)
       cd /tmp && export TMPDIR=/tmp
       G1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES"
