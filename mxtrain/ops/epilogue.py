@@ -20,8 +20,6 @@ from . import _lib
 from . import convwg
 
 _ENABLED = True
-# narrow 1x1 heads (Cout not a multiple of 64) as hipBLASLt GEMMs over the NHWC pixels
-_GEMM1X1 = True
 
 
 def _rows_cols(y: torch.Tensor):
@@ -195,58 +193,6 @@ def bias_act(y: torch.Tensor, b: Optional[torch.Tensor], residual: Optional[torc
         y = y + residual
     return F.relu(y) if relu else y
 
-
-
-class Conv1x1GemmFn(torch.autograd.Function):
-    """act(conv1x1(x, w) + b) for the narrow heads the implicit-GEMM tiles do not take
-    (Cout not a multiple of 64: the RPN objectness / box 1x1 on the level canvas, 16
-    channels; the mask predictor, 80): an NHWC 1x1 convolution IS a GEMM over the pixels,
-    [M, Cin] x [Cin, Cout], so forward, input and weight gradient are three hipBLASLt GEMMs on
-    views of the activations (no im2col, no layout change) instead of MIOpen's solvers
-    (142.9 + 33.8 us and 188.6 + 61.9 us per 4-img step there, ~90 TFLOP/s:
-    profiles/r5_s1/maskrcnn_4img_op_census.txt).  The bias gradient comes from the
-    column-sum pass of csrc/epilogue.hip."""
-
-    @staticmethod
-    def forward(ctx, x, w, b, relu: bool):
-        N, C, H, W = x.shape
-        Co = w.shape[0]
-        xf = x.permute(0, 2, 3, 1).reshape(-1, C)                 # [M, Cin] view (NHWC)
-        wf = w.reshape(Co, C)
-        yf = torch.addmm(b, xf, wf.t()) if b is not None else torch.mm(xf, wf.t())
-        if relu:
-            yf = F.relu(yf, inplace=True)
-        ctx.relu = relu
-        ctx.bdtype = b.dtype if b is not None else None
-        ctx.save_for_backward(x, w, yf if relu else None)
-        return yf.view(N, H, W, Co).permute(0, 3, 1, 2)
-
-    @staticmethod
-    def backward(ctx, g):
-        x, w, yf = ctx.saved_tensors
-        N, C, H, W = x.shape
-        Co = w.shape[0]
-        dy, db = _bias_act_bwd(g, None if yf is None else yf.view(N, H, W, Co).permute(0, 3, 1, 2), ctx.relu,
-                               ctx.needs_input_grad[2])
-        gf = dy.permute(0, 2, 3, 1).reshape(-1, Co)               # [M, Cout] view
-        dx = dw = None
-        if ctx.needs_input_grad[0]:
-            dx = torch.mm(gf, w.reshape(Co, C)).view(N, H, W, C).permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1]:
-            xf = x.permute(0, 2, 3, 1).reshape(-1, C)
-            dw = torch.mm(gf.t(), xf).view(Co, C, 1, 1)
-        if db is not None and db.dtype != ctx.bdtype:
-            db = db.to(ctx.bdtype)
-        return dx, dw, db, None
-
-
-def _gemm1x1_ok(x, w, b, residual, stride, padding, dilation) -> bool:
-    return (residual is None and w.dim() == 4 and w.shape[2] == 1 and w.shape[3] == 1 and w.shape[0] % 64 != 0
-            and w.shape[0] % 8 == 0 and x.shape[1] % 8 == 0 and convwg._sym(stride) == 1
-            and convwg._sym(padding) == 0 and convwg._sym(dilation) == 1 and w.dtype == torch.bfloat16
-            and (b is None or b.dtype == torch.bfloat16))
-
-
 def _conv_in_ok(x, w, b, residual) -> bool:
     """conv_bias_act's input-side conditions for the fused epilogues (the residual has the
     OUTPUT's shape: convwg.fwd_supported / bias_act check it against the conv output)."""
@@ -255,11 +201,9 @@ def _conv_in_ok(x, w, b, residual) -> bool:
             and (b is None or (b.dtype == torch.bfloat16 and b.is_contiguous()))
             and (residual is None or residual.dtype == torch.bfloat16))
 
-
 def fused_conv_ok(x, w, b=None, residual=None, stride=1, padding=0, dilation=1) -> bool:
     """True when conv_bias_act runs ConvBiasActFn (every direction on csrc/convwg.hip)."""
     return _conv_in_ok(x, w, b, residual) and convwg.fwd_supported(x, w, b, residual, stride, padding, dilation)
-
 
 def conv_bias_act(x, w, b=None, stride=1, padding=0, dilation=1, relu: bool = False,
                   residual: Optional[torch.Tensor] = None, fuse=None, res_up: bool = False) -> torch.Tensor:
@@ -277,8 +221,6 @@ def conv_bias_act(x, w, b=None, stride=1, padding=0, dilation=1, relu: bool = Fa
         if convwg.fwd_supported(x, w, b, residual, stride, padding, dilation):
             # forward, input and weight gradients all implicit GEMMs (ops/convwg.py)
             return ConvBiasActFn.apply(x, w, b, residual, relu, stride, padding, dilation, fuse, False)
-        if _GEMM1X1 and _gemm1x1_ok(x, w, b, residual, stride, padding, dilation):
-            return Conv1x1GemmFn.apply(x, w, b, relu)
         if convwg.supported(x, w, stride, padding, dilation):
             # MIOpen forward / input gradient, implicit-GEMM weight gradient (ops/convwg.py)
             return bias_act(convwg.conv2d_wg(x, w, stride, padding, dilation), b, residual, relu)
@@ -287,7 +229,6 @@ def conv_bias_act(x, w, b=None, stride=1, padding=0, dilation=1, relu: bool = Fa
     if residual is not None:
         y = y + (F.interpolate(residual, scale_factor=2, mode="nearest") if res_up else residual)
     return F.relu(y, inplace=True) if relu else y
-
 
 class ConvTransposeBiasActFn(torch.autograd.Function):
     """act(conv_transpose2d(x, w, stride=s) + b) for a filter within s x s (windows do not
@@ -328,7 +269,6 @@ class ConvTransposeBiasActFn(torch.autograd.Function):
             dw = convwg.conv_wgrad(x, dy, tuple(w.shape), st, 0, 1)
         return dx, dw, db, None, None
 
-
 def _deconv_ok(x, w, b, stride) -> bool:
     """ConvTransposeBiasActFn's conditions: NHWC bf16, non-overlapping windows, channel
     counts the weight-gradient tiles take (multiples of 128), enough output tiles."""
@@ -341,7 +281,6 @@ def _deconv_ok(x, w, b, stride) -> bool:
     N, _, H, W = x.shape
     out_shape = (N, w.shape[1], (H - 1) * stride + w.shape[2], (W - 1) * stride + w.shape[3])
     return convwg.dgrad_supported(w, out_shape, stride, 0, 1)
-
 
 def conv_transpose_bias_act(x, w, b=None, stride=1, relu: bool = False) -> torch.Tensor:
     """act(conv_transpose2d(x, w, stride) + b); ConvTransposeBiasActFn where it applies."""

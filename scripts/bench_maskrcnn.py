@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--graph", choices=("auto", "0", "1"), default="auto",
                     help="whole-step hipGraph replay (train.py --mx-graph; auto = on for 1 GPU)")
     ap.add_argument("--set", action="append", default=[],
-                    help="A/B hook: module:attr=int (e.g. mxtrain.ops.epilogue:_GEMM1X1=0) or "
+                    help="A/B hook: module:attr=int (e.g. mxtrain.models.maskrcnn:MaskRCNN.fused_targets=0) or "
                          "lib:setter=int (a kernel-library setter, e.g. lib:mx_conv_fwd_bk32=0)")
     ap.add_argument("extra", nargs="*")
     a = ap.parse_args()

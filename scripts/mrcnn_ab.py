@@ -2,7 +2,7 @@
 """Interleaved same-box A/B of Mask R-CNN training throughput: ROUNDS x (A, B) child runs of
 scripts/bench_maskrcnn.py, A with the --set hooks of --a, B with those of --b (each a
 comma-separated list of module:attr=int / lib:setter=int), median img/s per arm.
-    python scripts/mrcnn_ab.py --a "" --b "mxtrain.ops.epilogue:_GEMM1X1=0" --batch 4 --rounds 3"""
+    python scripts/mrcnn_ab.py --a "" --b "mxtrain.models.maskrcnn:MaskRCNN.fused_targets=0" --batch 4 --rounds 3"""
 import argparse
 import json
 import os

@@ -373,31 +373,3 @@ def test_conv_transpose_bias_relu_matches_fp32():
     (F.conv_transpose2d(xr, wr, br, stride=2) * (y.detach().float().cpu() > 0)).backward(gy.float())
     for got, ref in ((xg.grad, xr.grad), (wg.grad, wr.grad), (bg.grad, br.grad)):
         _close(got, ref)
-
-
-@pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 256, 16, 37, 41), (64, 256, 80, 14, 14)])
-def test_conv1x1_gemm_heads_match_fp32(N, Cin, Cout, H, W):
-    """The narrow 1x1 heads (RPN objectness / box: 16 channels, mask predictor: 80) routed by
-    conv_bias_act through Conv1x1GemmFn -- forward, input, weight and bias gradients as GEMMs
-    over the NHWC pixels -- against the fp32 PyTorch convolution."""
-    from mxtrain.ops import epilogue as E
-    g = torch.Generator().manual_seed(3)
-    cl = torch.channels_last
-    x = torch.randn(N, Cin, H, W, generator=g).to(torch.bfloat16)
-    w = (torch.randn(Cout, Cin, 1, 1, generator=g) * 0.05).to(torch.bfloat16)
-    b = torch.randn(Cout, generator=g).to(torch.bfloat16)
-    dy = torch.randn(N, Cout, H, W, generator=g).to(torch.bfloat16)
-    xd = x.cuda().contiguous(memory_format=cl).requires_grad_(True)
-    wd = w.cuda().contiguous(memory_format=cl).requires_grad_(True)
-    bd = b.cuda().requires_grad_(True)
-    assert E._gemm1x1_ok(xd, wd, bd, None, 1, 0, 1)
-    y = E.conv_bias_act(xd, wd, bd)
-    assert y.grad_fn is not None and "Conv1x1Gemm" in type(y.grad_fn).__name__, type(y.grad_fn)
-    y.backward(dy.cuda().contiguous(memory_format=cl))
-    xr, wr, br = (t.float().requires_grad_(True) for t in (x, w, b))
-    yr = torch.nn.functional.conv2d(xr, wr, br)
-    yr.backward(dy.float())
-    _close(y.detach(), yr.detach())
-    _close(xd.grad, xr.grad)
-    _close(wd.grad, wr.grad)
-    assert (bd.grad.float().cpu() - br.grad).abs().max().item() <= 2e-2 * br.grad.abs().max().item() + 1e-2
