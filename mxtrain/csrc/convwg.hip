@@ -563,6 +563,7 @@ struct ConvDg {
   // of an XH x XW image, enumerated as an IH x IW grid (stride-decomposed dgrad, below)
   int xs, xa, xb, XH, XW;
   uint32_t ybytes;       // size of dY (the gather's buffer resource; < 2 GiB)
+  int bkt;               // K-step depth (output channels per step): 64 or 32 (host-side choice)
 };
 
 // dX row of the launch's pixel p (identity unless a parity-class launch)
@@ -574,9 +575,9 @@ __device__ __forceinline__ int dx_row(const ConvDg& cp, int p) {
   return (n * cp.XH + i * cp.xs + cp.xa) * cp.XW + j * cp.xs + cp.xb;
 }
 
-template <int NSLOT>
+template <int NSLOT, int BKT = 64>
 __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
-  constexpr int WM = 2, WN = 2, FM = 4, FN = 4, BKT = 64, NW = WM * WN;
+  constexpr int WM = 2, WN = 2, FM = 4, FN = 4, NW = WM * WN;
   constexpr int BM = 16 * FM * WM, BN = 128, RA = BKT * 2, RB = BN * 2;
   constexpr int IA = BM * RA, IB = BKT * RB;
   constexpr int PA = IA / 1024 / NW, PB = IB / 1024 / NW;
@@ -609,7 +610,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
     divmod(ok ? p : 0, cp.IW, cp.invIW, q, iw);
     divmod(q, cp.IH, cp.invIH, n, ih);
     const int hh = ih + cp.pad, ww = iw + cp.pad, st = cp.stride, KHt = cp.taps / cp.KW;
-    const int sw = 8 * ((lane % (RA / 16)) ^ (row & 7));
+    const int sw = 8 * ((lane % (RA / 16)) ^ row_swz<RA>(row));
     uint32_t m = 0u;
     if (st == 1) {   // (wave-uniform) no per-lane divisions on the common path
       aoff[j] = ((n * cp.OH + hh) * cp.OW + ww) * cp.ldy + sw;
@@ -645,7 +646,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
   const int offA = (16 * FM * wm + i) * RA;
   int cA[BKT / 32];
 #pragma unroll
-  for (int kk = 0; kk < BKT / 32; ++kk) cA[kk] = 16 * ((4 * kk + G) ^ (i & 7));
+  for (int kk = 0; kk < BKT / 32; ++kk) cA[kk] = 16 * ((4 * kk + G) ^ row_swz<RA>(i));
   const int krow = 8 * G + (i >> 2);
   const int gq = gsw(krow);
   int offB[FN];
@@ -979,10 +980,21 @@ __global__ __launch_bounds__(256) void conv_dgrad_fill_kernel(const ConvDg cp, i
   }
 }
 
+// input-gradient K-step depth: 0 -> 64, 1 -> 32, 2 -> 32 when the reduction (taps x Cout)
+// is <= 256 deep; ring4: the 32-deep steps in a 4-slot ring (three in flight)
+int g_conv_dgrad_bk32 = 0;
+int g_conv_dgrad_ring4 = 0;
+
 static void launch_dgrad(ConvDg cp, int splits, hipStream_t st) {
   cp.splits = splits < 1 ? 1 : (splits > cp.nk ? cp.nk : splits);
   const int tiles_m = (cp.T + 127) / 128;
-  hipLaunchKernelGGL(conv_dgrad_kernel<2>, dim3(tiles_m * cp.tiles_n * cp.splits), dim3(256), 0, st, cp);
+  const dim3 grid(tiles_m * cp.tiles_n * cp.splits);
+  if (cp.bkt == 32 && g_conv_dgrad_ring4)
+    hipLaunchKernelGGL((conv_dgrad_kernel<4, 32>), grid, dim3(256), 0, st, cp);
+  else if (cp.bkt == 32)
+    hipLaunchKernelGGL((conv_dgrad_kernel<2, 32>), grid, dim3(256), 0, st, cp);
+  else
+    hipLaunchKernelGGL((conv_dgrad_kernel<2, 64>), grid, dim3(256), 0, st, cp);
   if (cp.splits > 1) {
     const int64_t nvec = (int64_t)cp.T * (cp.Cin / 8);
     const unsigned rg = (unsigned)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
@@ -1036,7 +1048,10 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   if (cp.taps > 32 || ybytes >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   cp.ybytes = (uint32_t)ybytes;
   cp.ldw = cp.taps * cp.Cin;
-  cp.cob = Cout / 64;
+  // K-step depth as in the forward (mx_conv_dgrad_bk32): 32 for short reductions
+  const bool small_k = cp.taps * Cout <= 256;
+  cp.bkt = (g_conv_dgrad_bk32 == 1 || (g_conv_dgrad_bk32 == 2 && small_k)) ? 32 : 64;
+  cp.cob = Cout / cp.bkt;
   cp.nk = cp.taps * cp.cob;
   cp.tiles_n = cp.Cin / 128;
   cp.invIW = 1.f / (float)cp.IW;
@@ -1120,7 +1135,12 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   const int64_t xbytes = N * cp.IH * cp.IW * (int64_t)cp.ldx * 2;
   if (cp.taps > 32 || xbytes >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   cp.xbytes = (uint32_t)xbytes;
-  const bool bk32 = g_conv_fwd_bk32 == 1 || (g_conv_fwd_bk32 == 2 && (cp.taps == 1 || cp.Cin <= 128));
+  const bool small_k = cp.taps == 1 || cp.Cin <= 128;
+  const bool bk32 = g_conv_fwd_bk32 == 1 || g_conv_fwd_bk32 == 3 || g_conv_fwd_bk32 == 4 ||
+                    (g_conv_fwd_bk32 == 2 && small_k);
+  // 3: 32-deep steps in a 4-slot ring everywhere (three steps in flight, 64 KiB per
+  // workgroup); 4: that ring for the long reductions, the 2-slot one for small_k
+  const bool ring4 = g_conv_fwd_bk32 == 3 || (g_conv_fwd_bk32 == 4 && !small_k);
   const int bkt = bk32 && cp.Cin % 32 == 0 ? 32 : 64;
   cp.cib = cp.Cin / bkt;
   cp.nk = cp.taps * cp.cib;
@@ -1141,7 +1161,9 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   }
   // ring depth 2 at two workgroups per CU: 3 / 4 slots (one workgroup per CU, counted waits)
   // measured 40 % slower on the Mask R-CNN shapes (profiles/r4_s2/conv_ring_depth_ab_4img.txt)
-  if (bkt == 32) {
+  if (bkt == 32 && ring4) {
+    if (Cout % 128 == 0) { MX_CF(4, 4, 32) } else { MX_CF(4, 2, 32) }
+  } else if (bkt == 32) {
     if (Cout % 128 == 0) { MX_CF(2, 4, 32) } else { MX_CF(2, 2, 32) }
   } else {
     if (Cout % 128 == 0) { MX_CF(2, 4, 64) } else { MX_CF(2, 2, 64) }
@@ -1166,5 +1188,14 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
 MX_EXPORT int mx_conv_fwd_bk32(int on) {
   const int old = g_conv_fwd_bk32;
   if (on >= 0) g_conv_fwd_bk32 = on;
+  return old;
+}
+
+// input-gradient K-step depth (g_conv_dgrad_bk32 above; ring4 >= 0 sets the 32-deep ring
+// depth flag, negative leaves it); negative mode: query.  Returns the old mode.
+MX_EXPORT int mx_conv_dgrad_bk32(int mode, int ring4) {
+  const int old = g_conv_dgrad_bk32;
+  if (mode >= 0) g_conv_dgrad_bk32 = mode;
+  if (ring4 >= 0) g_conv_dgrad_ring4 = ring4;
   return old;
 }

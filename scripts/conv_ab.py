@@ -37,7 +37,7 @@ def child(lib, imgs, iters, out_path, setting=None):
     from mxtrain.ops import convwg
     if setting:
         fn, val = setting.split("=")
-        _lib._fn(fn)(int(val))
+        _lib._fn(fn)(*[int(v) for v in val.split(":")])   # setter arguments, ':'-separated
     cl = torch.channels_last
     torch.manual_seed(0)
     res = {}

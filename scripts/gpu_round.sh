@@ -52,6 +52,14 @@ for s in $STEPS; do
       # one arbitrary python command: CMD="scripts/x.py args" (output to gpurun_out/$CMD_TAG.txt)
       timeout -k 10 ${T_CMD:-300} python $CMD > gpurun_out/${CMD_TAG:-cmd}.txt 2>&1; rc=$?
       tail -${CMD_TAIL:-20} gpurun_out/${CMD_TAG:-cmd}.txt; echo "cmd rc=$rc"; ok $rc || exit $rc ;;
+    cmds)
+      # several python commands: CMDS="a.py args|b.py args", outputs gpurun_out/${CMDS_TAG}_<i>.txt
+      IFS='|' read -ra _CMDS <<< "$CMDS"; i=0
+      for c in "${_CMDS[@]}"; do
+        i=$((i+1))
+        timeout -k 10 ${T_CMD:-300} python $c > gpurun_out/${CMDS_TAG:-cmds}_$i.txt 2>&1; rc=$?
+        tail -${CMD_TAIL:-20} gpurun_out/${CMDS_TAG:-cmds}_$i.txt; echo "cmds[$i] rc=$rc"; ok $rc || exit $rc
+      done ;;
     cmd2)
       timeout -k 10 ${T_CMD2:-300} python $CMD2 > gpurun_out/${CMD2_TAG:-cmd2}.txt 2>&1; rc=$?
       tail -${CMD_TAIL:-20} gpurun_out/${CMD2_TAG:-cmd2}.txt; echo "cmd2 rc=$rc"; ok $rc || exit $rc ;;
