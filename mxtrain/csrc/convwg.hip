@@ -980,18 +980,15 @@ __global__ __launch_bounds__(256) void conv_dgrad_fill_kernel(const ConvDg cp, i
   }
 }
 
-// input-gradient K-step depth: 0 -> 64, 1 -> 32, 2 -> 32 when the reduction (taps x Cout)
-// is <= 256 deep; ring4: the 32-deep steps in a 4-slot ring (three in flight)
-int g_conv_dgrad_bk32 = 0;
-int g_conv_dgrad_ring4 = 0;
+// input-gradient K-step depth: 0 -> 64, 1 -> 32, 2 -> by shape (mx_conv_dgrad, default).
+// (A 4-slot ring of 32-deep steps was 2-11 % slower: profiles/r5_s1/conv_ab_ring_4.txt)
+int g_conv_dgrad_bk32 = 2;
 
 static void launch_dgrad(ConvDg cp, int splits, hipStream_t st) {
   cp.splits = splits < 1 ? 1 : (splits > cp.nk ? cp.nk : splits);
   const int tiles_m = (cp.T + 127) / 128;
   const dim3 grid(tiles_m * cp.tiles_n * cp.splits);
-  if (cp.bkt == 32 && g_conv_dgrad_ring4)
-    hipLaunchKernelGGL((conv_dgrad_kernel<4, 32>), grid, dim3(256), 0, st, cp);
-  else if (cp.bkt == 32)
+  if (cp.bkt == 32)
     hipLaunchKernelGGL((conv_dgrad_kernel<2, 32>), grid, dim3(256), 0, st, cp);
   else
     hipLaunchKernelGGL((conv_dgrad_kernel<2, 64>), grid, dim3(256), 0, st, cp);
@@ -1048,9 +1045,12 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   if (cp.taps > 32 || ybytes >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   cp.ybytes = (uint32_t)ybytes;
   cp.ldw = cp.taps * cp.Cin;
-  // K-step depth as in the forward (mx_conv_dgrad_bk32): 32 for short reductions
-  const bool small_k = cp.taps * Cout <= 256;
-  cp.bkt = (g_conv_dgrad_bk32 == 1 || (g_conv_dgrad_bk32 == 2 && small_k)) ? 32 : 64;
+  // K-step depth (mx_conv_dgrad_bk32): 32 for the narrow reductions -- 3x3 with Cout <= 128,
+  // 1x1 with Cout <= 512 -- where scripts/conv_ab.py measured the 16-KiB slots 16-20 % faster
+  // (res3.conv2, res3.conv3, fpn.lat2 at 4 images); the 3x3 Cout 256 convs and res4.conv3
+  // (1x1, Cout 1024) are 3-23 % slower with them (profiles/r5_s1/conv_ab_ring_3.txt)
+  const bool narrow = Cout <= 128 || (cp.taps == 1 && Cout <= 512);
+  cp.bkt = (g_conv_dgrad_bk32 == 1 || (g_conv_dgrad_bk32 == 2 && narrow)) ? 32 : 64;
   cp.cob = Cout / cp.bkt;
   cp.nk = cp.taps * cp.cob;
   cp.tiles_n = cp.Cin / 128;
@@ -1135,12 +1135,9 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   const int64_t xbytes = N * cp.IH * cp.IW * (int64_t)cp.ldx * 2;
   if (cp.taps > 32 || xbytes >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   cp.xbytes = (uint32_t)xbytes;
-  const bool small_k = cp.taps == 1 || cp.Cin <= 128;
-  const bool bk32 = g_conv_fwd_bk32 == 1 || g_conv_fwd_bk32 == 3 || g_conv_fwd_bk32 == 4 ||
-                    (g_conv_fwd_bk32 == 2 && small_k);
-  // 3: 32-deep steps in a 4-slot ring everywhere (three steps in flight, 64 KiB per
-  // workgroup); 4: that ring for the long reductions, the 2-slot one for small_k
-  const bool ring4 = g_conv_fwd_bk32 == 3 || (g_conv_fwd_bk32 == 4 && !small_k);
+  // (32-deep steps in a 4-slot ring -- three in flight -- measured 4-5 % slower overall,
+  // profiles/r5_s1/conv_ab_ring_1.txt)
+  const bool bk32 = g_conv_fwd_bk32 == 1 || (g_conv_fwd_bk32 == 2 && (cp.taps == 1 || cp.Cin <= 128));
   const int bkt = bk32 && cp.Cin % 32 == 0 ? 32 : 64;
   cp.cib = cp.Cin / bkt;
   cp.nk = cp.taps * cp.cib;
@@ -1161,9 +1158,7 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   }
   // ring depth 2 at two workgroups per CU: 3 / 4 slots (one workgroup per CU, counted waits)
   // measured 40 % slower on the Mask R-CNN shapes (profiles/r4_s2/conv_ring_depth_ab_4img.txt)
-  if (bkt == 32 && ring4) {
-    if (Cout % 128 == 0) { MX_CF(4, 4, 32) } else { MX_CF(4, 2, 32) }
-  } else if (bkt == 32) {
+  if (bkt == 32) {
     if (Cout % 128 == 0) { MX_CF(2, 4, 32) } else { MX_CF(2, 2, 32) }
   } else {
     if (Cout % 128 == 0) { MX_CF(2, 4, 64) } else { MX_CF(2, 2, 64) }
@@ -1191,11 +1186,9 @@ MX_EXPORT int mx_conv_fwd_bk32(int on) {
   return old;
 }
 
-// input-gradient K-step depth (g_conv_dgrad_bk32 above; ring4 >= 0 sets the 32-deep ring
-// depth flag, negative leaves it); negative mode: query.  Returns the old mode.
-MX_EXPORT int mx_conv_dgrad_bk32(int mode, int ring4) {
+// input-gradient K-step depth (g_conv_dgrad_bk32 above); negative: query.  Returns the old mode.
+MX_EXPORT int mx_conv_dgrad_bk32(int mode) {
   const int old = g_conv_dgrad_bk32;
   if (mode >= 0) g_conv_dgrad_bk32 = mode;
-  if (ring4 >= 0) g_conv_dgrad_ring4 = ring4;
   return old;
 }

@@ -133,6 +133,25 @@ __device__ __forceinline__ void bias_partial_store(const f32x16 (&acc)[N], float
 }
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
+// One 32-column group of a row-per-lane 32x32 MFMA result (lane r and r + 32 hold row r:
+// columns 8 k + 4 hh .. +3 of each group k) stored as bf16 with 16-B stores: for each pair of
+// groups (k, k + 1) one v_permlane32_swap per dword gives the lower half-wave columns
+// 8 k .. 8 k + 7 and the upper one 8 k + 8 .. 8 k + 15 -- 2 dwordx4 stores per lane instead of
+// 4 dwordx2 (the epilogue store tail is issue-bound: MI355X guide T21).  Both lanes of a row
+// must be active.
+__device__ __forceinline__ void store_row32(uint16_t* rowp, const f32x16& acc, float sc, int hh) {
+#pragma unroll
+  for (int k = 0; k < 4; k += 2) {
+    const uint32_t ax = pack2(acc[4 * k + 0] * sc, acc[4 * k + 1] * sc);
+    const uint32_t ay = pack2(acc[4 * k + 2] * sc, acc[4 * k + 3] * sc);
+    const uint32_t bx = pack2(acc[4 * k + 4] * sc, acc[4 * k + 5] * sc);
+    const uint32_t by = pack2(acc[4 * k + 6] * sc, acc[4 * k + 7] * sc);
+    const auto rx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+    const auto ry = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+    *reinterpret_cast<uint4*>(rowp + 8 * k + 8 * hh) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+  }
+}
+
 // one 1-KiB LDS-DMA piece: lane i's 16 B from `g` land at lds_base + 16 i.  Issued from
 // inline asm: for the builtin, the compiler cannot prove that a later ds_read of another
 // ring slot does not alias the in-flight DMA (no alias-scope info on either access) and
@@ -508,15 +527,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
     }
     uint16_t* op = DQ ? dq + (size_t)(b * S + qrow) * lddq + hq * D : o + (size_t)(b * S + qrow) * ldo + hq * D;
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = 32 * dt + 8 * g4 + 4 * hh;
-        uint2 u;
-        u.x = pack2(acc[dt][4 * g4 + 0] * sc, acc[dt][4 * g4 + 1] * sc);
-        u.y = pack2(acc[dt][4 * g4 + 2] * sc, acc[dt][4 * g4 + 3] * sc);
-        *reinterpret_cast<uint2*>(op + d) = u;
-      }
+    for (int dt = 0; dt < NDT; ++dt) store_row32(op + 32 * dt, acc[dt], sc, hh);
     // dQ's bias-gradient column partials (S % 32 == 0: every row of the wave is valid)
     if (DQ && bpart) bias_partial_store<NDT>(acc, sc, bpart, ldbp, (b * S + qw) >> 5, hq * D, 0, lane);
   };
@@ -927,18 +938,10 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
     uint16_t* dkp = dk + (size_t)(b * S + key) * lddk + hk * D;
     uint16_t* dvp = dv + (size_t)(b * S + key) * lddv + hk * D;
 #pragma unroll
-    for (int dt = 0; dt < NDL; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = 32 * (dt + DT0) + 8 * g4 + 4 * hh;
-        uint2 u;
-        u.x = pack2(dkacc[dt][4 * g4 + 0] * dkscale, dkacc[dt][4 * g4 + 1] * dkscale);
-        u.y = pack2(dkacc[dt][4 * g4 + 2] * dkscale, dkacc[dt][4 * g4 + 3] * dkscale);
-        *reinterpret_cast<uint2*>(dkp + d) = u;
-        u.x = pack2(dvacc[dt][4 * g4 + 0] * dvscale, dvacc[dt][4 * g4 + 1] * dvscale);
-        u.y = pack2(dvacc[dt][4 * g4 + 2] * dvscale, dvacc[dt][4 * g4 + 3] * dvscale);
-        *reinterpret_cast<uint2*>(dvp + d) = u;
-      }
+    for (int dt = 0; dt < NDL; ++dt) {
+      store_row32(dkp + 32 * (dt + DT0), dkacc[dt], dkscale, hh);
+      store_row32(dvp + 32 * (dt + DT0), dvacc[dt], dvscale, hh);
+    }
     // dK / dV bias-gradient column partials (S % 32 == 0: every key of the wave is valid)
     if (bpart) {
       bias_partial_store<NDL>(dkacc, dkscale, bpart, ldbp, (b * S + kw0) >> 5, bcol + hk * D, DT0, lane);
@@ -1430,18 +1433,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   uint16_t* dkp = dk + (size_t)(b * S + key) * lddk + hk * D;
   uint16_t* dvp = dv + (size_t)(b * S + key) * lddv + hk * D;
 #pragma unroll
-  for (int dt = 0; dt < NDL; ++dt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int d = 32 * (dt + DT0) + 8 * g4 + 4 * hh;
-      uint2 u;
-      u.x = pack2(dkacc[dt][4 * g4 + 0] * dkscale, dkacc[dt][4 * g4 + 1] * dkscale);
-      u.y = pack2(dkacc[dt][4 * g4 + 2] * dkscale, dkacc[dt][4 * g4 + 3] * dkscale);
-      *reinterpret_cast<uint2*>(dkp + d) = u;
-      u.x = pack2(dvacc[dt][4 * g4 + 0] * dvscale, dvacc[dt][4 * g4 + 1] * dvscale);
-      u.y = pack2(dvacc[dt][4 * g4 + 2] * dvscale, dvacc[dt][4 * g4 + 3] * dvscale);
-      *reinterpret_cast<uint2*>(dvp + d) = u;
-    }
+  for (int dt = 0; dt < NDL; ++dt) {
+    store_row32(dkp + 32 * (dt + DT0), dkacc[dt], dkscale, hh);
+    store_row32(dvp + 32 * (dt + DT0), dvacc[dt], dvscale, hh);
+  }
   if (bpart) {   // dK / dV bias-gradient column partials (S % 32 == 0)
     bias_partial_store<NDL>(dkacc, dkscale, bpart, ldbp, (b * S + kw0) >> 5, bcol + hk * D, DT0, lane);
     bias_partial_store<NDL>(dvacc, dvscale, bpart, ldbp, (b * S + kw0) >> 5, bcol + (Hkv + hk) * D, DT0, lane);

@@ -143,7 +143,7 @@ SIGNATURES = {
     # knobs (one int; return the previous setting)
     "mx_flash_dropmask_variant": [I],
     "mx_conv_fwd_bk32": [I],
-    "mx_conv_dgrad_bk32": [I, I],
+    "mx_conv_dgrad_bk32": [I],
     "mx_norm_bwd_max_blocks": [I],
 }
 
