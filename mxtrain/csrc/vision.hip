@@ -825,9 +825,12 @@ __device__ __forceinline__ float iou4(const float4 a, const float4 b) {
 
 // boxes: [P, N, 4] sorted by score (desc) per problem; counts[P] valid boxes.
 // mask: [P, N, NB] uint64, bit j of word (i, cb) set when box cb*64+j (> i) overlaps i.
+// colmask (nullable): [P, N] uint64, bit j set when box (i & ~63) + j (< i) overlaps i -- the
+// transposed diagonal block, for the parallel in-chunk scan of nms_keep_par_kernel
 __global__ __launch_bounds__(64) void nms_mask_kernel(const float4* __restrict__ boxes, const int* __restrict__ counts,
                                                       int N, int NB, float thr,
-                                                      unsigned long long* __restrict__ mask) {
+                                                      unsigned long long* __restrict__ mask,
+                                                      unsigned long long* __restrict__ colmask) {
   const int cb = blockIdx.x, rb = blockIdx.y, p = blockIdx.z;
   const int n = counts ? counts[p] : N;
   const int t = threadIdx.x;
@@ -839,12 +842,15 @@ __global__ __launch_bounds__(64) void nms_mask_kernel(const float4* __restrict__
   __syncthreads();
   if (i >= n) return;
   const float4 bi = boxes[(size_t)p * N + i];
-  unsigned long long bits = 0ull;
+  unsigned long long bits = 0ull, col = 0ull;
   const int jn = min(64, n - j0);
   for (int j = 0; j < jn; ++j) {
-    if (j0 + j > i && iou4(bi, cbox[j]) > thr) bits |= (1ull << j);
+    const bool ov = iou4(bi, cbox[j]) > thr;
+    if (j0 + j > i && ov) bits |= (1ull << j);
+    if (j0 + j < i && ov) col |= (1ull << j);
   }
   mask[((size_t)p * N + i) * NB + cb] = bits;
+  if (colmask && cb == rb) colmask[(size_t)p * N + i] = col;
 }
 
 // one wave per problem; lane w owns removed-word w (NB <= NBM <= 64 -> N <= 64 NBM)
@@ -931,6 +937,88 @@ __global__ __launch_bounds__(64) void nms_keep_kernel(const unsigned long long* 
       // batches of 8 independent LDS reads, then the masked OR (kept bit ii: all-ones select;
       // never set for ii >= cn, whose LDS rows are stale); a guarded read per row had the
       // compiler wait for each one
+#pragma unroll
+      for (int i0 = 0; i0 < 64; i0 += 8) {
+        unsigned long long v8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v8[j] = rows[(i0 + j) * NB + lane];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc |= v8[j] & (0ull - ((kept >> (i0 + j)) & 1ull));
+      }
+      removed = acc;
+    }
+    __syncthreads();
+  }
+  if (lane == 0) nkeep[p] = out;
+  for (int k = out + lane; k < max_out; k += 64) keep[(size_t)p * max_out + k] = -1;
+}
+
+// nms_keep_kernel with the in-chunk greedy decided in parallel: box i of a chunk is kept iff it
+// is not suppressed by earlier chunks (avail) and no KEPT box j < i of the chunk overlaps it.
+// Lane i holds the transposed diagonal block (colmask: its earlier overlapping boxes), and
+// the kept set K is iterated to its fixed point, K' = ballot(avail_i && !(col_i & K)) from
+// K = avail: the greedy set is the map's only fixed point and box t's status is final after
+// t + 1 rounds, so the loop ends (typically after a few rounds, not 64 serial steps with two
+// v_readlane each).  The fetch (one chunk ahead), the staging and the suppression OR-pass are
+// those of nms_keep_kernel.
+template <int NBM>
+__global__ __launch_bounds__(64) void nms_keep_par_kernel(const unsigned long long* __restrict__ mask,
+                                                          const unsigned long long* __restrict__ colmask,
+                                                          const int* __restrict__ counts, int N, int NB,
+                                                          int max_out, int* __restrict__ keep,
+                                                          int* __restrict__ nkeep) {
+  const int p = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int n = counts ? counts[p] : N;
+  __shared__ unsigned long long rows[64 * NBM];
+  unsigned long long removed = 0ull;
+  int out = 0;
+  const unsigned long long* m = mask + (size_t)p * N * NB;
+  const unsigned long long* cm = colmask + (size_t)p * N;
+  unsigned long long pre[NBM];
+  unsigned long long pcol = 0ull;
+  const float inv_nb = 1.f / (float)NB;
+  unsigned long long valid = 0ull;
+  auto fetch = [&](int c0) __attribute__((always_inline)) {
+    const int cn = min(64, n - c0), cw = c0 >> 6;
+    valid = 0ull;
+#pragma unroll
+    for (int q = 0; q < NBM; ++q) {
+      const int k = lane + 64 * q;
+      const int r = (int)(((float)k + 0.5f) * inv_nb), w = k - r * NB;
+      const bool ok = q < NB && r < cn && w > cw;   // (the diagonal word comes from colmask)
+      valid |= (ok ? 1ull : 0ull) << q;
+      pre[q] = m[ok ? (size_t)c0 * NB + k : 0];
+    }
+    pcol = cm[c0 + min(lane, cn - 1)];
+  };
+  if (n > 0) fetch(0);
+  for (int c0 = 0; c0 < n && out < max_out; c0 += 64) {
+    const int cn = min(64, n - c0);
+#pragma unroll
+    for (int q = 0; q < NBM; ++q)
+      if (q < NB) rows[lane + 64 * q] = ((valid >> q) & 1ull) ? pre[q] : 0ull;
+    const unsigned long long col = lane < cn ? pcol : 0ull;
+    __syncthreads();
+    if (c0 + 64 < n) fetch(c0 + 64);      // next chunk in flight during this one's scan
+    const int cw = c0 >> 6;
+    const unsigned long long word = __shfl(removed, cw);
+    const bool av = lane < cn && !((word >> lane) & 1ull);
+    unsigned long long K = __ballot(av);
+    for (;;) {
+      const unsigned long long Kn = __ballot(av && (col & K) == 0ull);
+      if (Kn == K) break;
+      K = Kn;
+    }
+    const int room = max_out - out;
+    unsigned long long kept = K;
+    if (__popcll(K) > room)   // greedy order is index order: the first `room` kept boxes
+      kept = __ballot(((K >> lane) & 1ull) && __popcll(K & ((1ull << lane) - 1ull)) < room);
+    if ((kept >> lane) & 1ull)
+      keep[(size_t)p * max_out + out + __popcll(kept & ((1ull << lane) - 1ull))] = c0 + lane;
+    out += __popcll(kept);
+    if (lane < NB && lane > cw) {
+      unsigned long long acc = removed;
 #pragma unroll
       for (int i0 = 0; i0 < 64; i0 += 8) {
         unsigned long long v8[8];
@@ -1614,16 +1702,37 @@ MX_EXPORT int mx_roi_align_bwd_tiled(void* const* grads, const int* H, const int
   return hipGetLastError();
 }
 
-MX_EXPORT int mx_nms_workspace_words(int N) { return (N + 63) / 64; }
+// uint64 words of mask_ws per box: the [N][NB] mask and one colmask word
+MX_EXPORT int mx_nms_workspace_words(int N) { return (N + 63) / 64 + 1; }
 
-// batched NMS over P independent problems (boxes sorted by score desc per problem)
+int g_nms_par = 1;   // in-chunk scan: 1 = parallel fixed point (nms_keep_par_kernel), 0 = serial
+
+MX_EXPORT int mx_nms_par(int on) {
+  const int old = g_nms_par;
+  if (on >= 0) g_nms_par = on;
+  return old;
+}
+
+// batched NMS over P independent problems (boxes sorted by score desc per problem);
+// mask_ws holds P * N * mx_nms_workspace_words(N) uint64
 MX_EXPORT int mx_nms(const float* boxes, const int* counts, int P, int N, float thr, int max_out, void* mask_ws,
                      int* keep, int* nkeep, hipStream_t s) {
   const int NB = (N + 63) / 64;
   if (NB > 64) return hipErrorInvalidValue;
   if (P == 0 || N == 0) return hipSuccess;
+  unsigned long long* mw = (unsigned long long*)mask_ws;
+  unsigned long long* colw = mw + (size_t)P * N * NB;
   hipLaunchKernelGGL(nms_mask_kernel, dim3(NB, NB, P), dim3(64), 0, s, (const float4*)boxes, counts, N, NB, thr,
-                     (unsigned long long*)mask_ws);
+                     mw, g_nms_par ? colw : (unsigned long long*)nullptr);
+  if (g_nms_par) {
+    if (NB <= 16)
+      hipLaunchKernelGGL(nms_keep_par_kernel<16>, dim3(P), dim3(64), 0, s, mw, colw, counts, N, NB, max_out, keep, nkeep);
+    else if (NB <= 32)
+      hipLaunchKernelGGL(nms_keep_par_kernel<32>, dim3(P), dim3(64), 0, s, mw, colw, counts, N, NB, max_out, keep, nkeep);
+    else
+      hipLaunchKernelGGL(nms_keep_par_kernel<64>, dim3(P), dim3(64), 0, s, mw, colw, counts, N, NB, max_out, keep, nkeep);
+    return hipGetLastError();
+  }
   if (NB <= 16)
     hipLaunchKernelGGL(nms_keep_kernel<16>, dim3(P), dim3(64), 0, s, (const unsigned long long*)mask_ws, counts, N,
                        NB, max_out, keep, nkeep);

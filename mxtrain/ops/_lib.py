@@ -115,6 +115,7 @@ SIGNATURES = {
     "mx_roi_align_bwd": [P, P, P, P, I, I, F, I, P, I, I, I, I, I, I, P, P],
     "mx_roi_align_bwd_tiled": [P, P, P, P, I, I, F, I, I, P, I, I, I, I, I, I, P, P, P, P],
     "mx_nms_workspace_words": [I],
+    "mx_nms_par": [I],
     "mx_topk_chunk": [],
     "mx_topk_rows": [P, I, I, I, I, I, P, P, P],
     "mx_topk_rows_max_k": [],

@@ -234,7 +234,7 @@ def batched_nms_sorted(boxes: torch.Tensor, counts: Optional[torch.Tensor], thr:
     if _lib.use_hip(boxes) and N <= 4096:
         b = boxes.float().contiguous()
         cnt = counts.to(torch.int32).contiguous() if counts is not None else None
-        nb = (N + 63) // 64
+        nb = (N + 63) // 64 + 1   # mask words + the transposed diagonal word (mx_nms_workspace_words)
         ws = torch.empty(P * N * nb, dtype=torch.int64, device=boxes.device)
         keep = torch.empty(P, max_out, dtype=torch.int32, device=boxes.device)
         nk = torch.empty(P, dtype=torch.int32, device=boxes.device)

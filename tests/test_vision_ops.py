@@ -402,3 +402,30 @@ def test_rpn_level_canvas_pack_gpu():
     c.backward(gc)
     for (y0, x0), p in zip(offs, lv):
         assert torch.equal(p.grad.cpu(), gc[:, :, y0:y0 + p.shape[2], x0:x0 + p.shape[3]].cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,max_out", [(2000, 2000), (2000, 300), (130, 17), (4096, 1000)])
+def test_nms_parallel_scan_matches_serial(N, max_out):
+    """Boxes clustered around a few objects (long suppression chains inside a 64-box chunk):
+    the fixed-point in-chunk scan (nms_keep_par_kernel) and the serial one give the greedy
+    CPU result, including the max_out cut inside a chunk."""
+    from mxtrain.ops import _lib
+    g = torch.Generator().manual_seed(N + max_out)
+    P = 4
+    ctr = torch.rand(P, 12, 2, generator=g) * 600
+    pick = torch.randint(0, 12, (P, N), generator=g)
+    c = torch.gather(ctr, 1, pick[..., None].expand(P, N, 2)) + torch.randn(P, N, 2, generator=g) * 6
+    wh = 30 + torch.rand(P, N, 2, generator=g) * 40
+    boxes = torch.cat([c - wh / 2, c + wh / 2], -1)
+    counts = torch.tensor([N, max(1, N - 77), 64, 0])
+    kc, nc = V.batched_nms_sorted(boxes, counts, 0.7, max_out)
+    old = _lib._fn("mx_nms_par")(-1)
+    try:
+        for par in (1, 0):
+            _lib._fn("mx_nms_par")(par)
+            kg, ng = V.batched_nms_sorted(boxes.cuda(), counts.cuda(), 0.7, max_out)
+            assert ng.cpu().tolist() == nc.tolist(), par
+            assert torch.equal(kg.cpu(), kc), par
+    finally:
+        _lib._fn("mx_nms_par")(old)
