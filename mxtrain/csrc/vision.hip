@@ -967,41 +967,45 @@ __global__ __launch_bounds__(64) void nms_keep_par_kernel(const unsigned long lo
                                                           const int* __restrict__ counts, int N, int NB,
                                                           int max_out, int* __restrict__ keep,
                                                           int* __restrict__ nkeep) {
+  // LDS-DMA ring of DEPTH chunks (DEPTH - 1 in flight during a chunk's scan): a chunk's mask
+  // rows are one contiguous [64][NB] block, its transposed diagonal words [64] another; both
+  // land by buffer_load ... lds (reads past the problem's last row return zeros), so no
+  // register staging and no load latency per chunk once the ring is full (the one-ahead
+  // register prefetch left most of a ~3.7 us chunk waiting on it: profiles/r5_s1/nms_*.txt)
+  constexpr int DEPTH = 4;
+  constexpr int RB = 64 * NBM * 8;                 // row bytes of a slot
+  constexpr int SLOTB = RB + 1024;                 // + 1 KiB for the colmask words
+  constexpr int PER = NBM / 2 + 1;                 // DMA pieces per chunk
+  __shared__ __attribute__((aligned(1024))) char ring[DEPTH * SLOTB];
   const int p = blockIdx.x;
   const int lane = threadIdx.x;
   const int n = counts ? counts[p] : N;
-  __shared__ unsigned long long rows[64 * NBM];
   unsigned long long removed = 0ull;
   int out = 0;
-  const unsigned long long* m = mask + (size_t)p * N * NB;
-  const unsigned long long* cm = colmask + (size_t)p * N;
-  unsigned long long pre[NBM];
-  unsigned long long pcol = 0ull;
-  const float inv_nb = 1.f / (float)NB;
-  unsigned long long valid = 0ull;
-  auto fetch = [&](int c0) __attribute__((always_inline)) {
-    const int cn = min(64, n - c0), cw = c0 >> 6;
-    valid = 0ull;
+  const gemm::i32x4_t mres = gemm::buffer_rsrc(mask + (size_t)p * N * NB, (uint32_t)((size_t)n * NB * 8));
+  const gemm::i32x4_t cres = gemm::buffer_rsrc(colmask + (size_t)p * N, (uint32_t)((size_t)n * 8));
+  const uint32_t ring0 = gemm::lds_addr(ring);
+  const int nchunks = (n + 63) >> 6;
+  auto issue = [&](int c) __attribute__((always_inline)) {
+    const uint32_t base = __builtin_amdgcn_readfirstlane(ring0 + (c % DEPTH) * SLOTB);
+    const uint32_t src = (uint32_t)c * 64u * (uint32_t)NB * 8u;
 #pragma unroll
-    for (int q = 0; q < NBM; ++q) {
-      const int k = lane + 64 * q;
-      const int r = (int)(((float)k + 0.5f) * inv_nb), w = k - r * NB;
-      const bool ok = q < NB && r < cn && w > cw;   // (the diagonal word comes from colmask)
-      valid |= (ok ? 1ull : 0ull) << q;
-      pre[q] = m[ok ? (size_t)c0 * NB + k : 0];
-    }
-    pcol = cm[c0 + min(lane, cn - 1)];
+    for (int q = 0; q < NBM / 2; ++q)
+      gemm::dma16_buf(mres, 2 * q < NB ? src + 1024u * q + 16u * lane : gemm::kOOB, base + 1024 * q);
+    gemm::dma16_buf(cres, (uint32_t)c * 512u + 16u * lane, base + RB);
   };
-  if (n > 0) fetch(0);
-  for (int c0 = 0; c0 < n && out < max_out; c0 += 64) {
-    const int cn = min(64, n - c0);
-#pragma unroll
-    for (int q = 0; q < NBM; ++q)
-      if (q < NB) rows[lane + 64 * q] = ((valid >> q) & 1ull) ? pre[q] : 0ull;
-    const unsigned long long col = lane < cn ? pcol : 0ull;
-    __syncthreads();
-    if (c0 + 64 < n) fetch(c0 + 64);      // next chunk in flight during this one's scan
-    const int cw = c0 >> 6;
+  for (int c = 0; c < DEPTH - 1; ++c)
+    if (c < nchunks) issue(c);
+  for (int c = 0; c < nchunks && out < max_out; ++c) {
+    const int later = min(nchunks - 1 - c, DEPTH - 2);   // chunks issued after this one
+    // (counts above the 6-bit field's 63 wait for more than needed: still correct)
+    if (later >= 2) gemm::vm_wait<(2 * PER < 63 ? 2 * PER : 63)>();
+    else if (later == 1) gemm::vm_wait<(PER < 63 ? PER : 63)>();
+    else gemm::vm_wait<0>();
+    const int c0 = c << 6, cn = min(64, n - c0), cw = c;
+    const char* slot = ring + (c % DEPTH) * SLOTB;
+    const unsigned long long* rows = reinterpret_cast<const unsigned long long*>(slot);
+    const unsigned long long col = lane < cn ? reinterpret_cast<const unsigned long long*>(slot + RB)[lane] : 0ull;
     const unsigned long long word = __shfl(removed, cw);
     const bool av = lane < cn && !((word >> lane) & 1ull);
     unsigned long long K = __ballot(av);
@@ -1019,6 +1023,7 @@ __global__ __launch_bounds__(64) void nms_keep_par_kernel(const unsigned long lo
     out += __popcll(kept);
     if (lane < NB && lane > cw) {
       unsigned long long acc = removed;
+      // rows beyond cn are never kept (their bits of `kept` are 0), so their contents do not matter
 #pragma unroll
       for (int i0 = 0; i0 < 64; i0 += 8) {
         unsigned long long v8[8];
@@ -1029,8 +1034,11 @@ __global__ __launch_bounds__(64) void nms_keep_par_kernel(const unsigned long lo
       }
       removed = acc;
     }
-    __syncthreads();
+    // this slot's reads are complete before the DMA that reuses it is issued
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+    if (c + DEPTH - 1 < nchunks) issue(c + DEPTH - 1);
   }
+  gemm::vm_wait<0>();   // no LDS-DMA outstanding at exit (early max_out stop)
   if (lane == 0) nkeep[p] = out;
   for (int k = out + lane; k < max_out; k += 64) keep[(size_t)p * max_out + k] = -1;
 }
