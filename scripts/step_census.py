@@ -2,7 +2,7 @@
 """Per-step kernel census of a rocprofv3 SQLite trace: steps are delimited by a kernel that
 runs exactly once per training step (default: the RPN NMS keep pass); the last N intervals
 are averaged, so one-time work (MIOpen search, capture, warm-up) is excluded.
-    python scripts/step_census.py DB [--marker nms_keep_kernel] [--last 10] [--top 80]
+    python scripts/step_census.py DB [--marker nms_keep] [--last 10] [--top 80]
         [--detail REGEX]   (every call of the matching kernels in the last step, in order)"""
 import argparse
 import sqlite3
@@ -12,7 +12,7 @@ from collections import defaultdict
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
-    ap.add_argument("--marker", default="nms_keep_kernel")
+    ap.add_argument("--marker", default="nms_keep")
     ap.add_argument("--last", type=int, default=10)
     ap.add_argument("--top", type=int, default=80)
     ap.add_argument("--sort", choices=("count", "time"), default="time")
