@@ -962,25 +962,30 @@ __global__ __launch_bounds__(64) void nms_keep_kernel(const unsigned long long* 
 // v_readlane each).  The fetch (one chunk ahead), the staging and the suppression OR-pass are
 // those of nms_keep_kernel.
 template <int NBM>
-__global__ __launch_bounds__(64) void nms_keep_par_kernel(const unsigned long long* __restrict__ mask,
-                                                          const unsigned long long* __restrict__ colmask,
-                                                          const int* __restrict__ counts, int N, int NB,
-                                                          int max_out, int* __restrict__ keep,
-                                                          int* __restrict__ nkeep) {
+__global__ __launch_bounds__(256) void nms_keep_par_kernel(const unsigned long long* __restrict__ mask,
+                                                           const unsigned long long* __restrict__ colmask,
+                                                           const int* __restrict__ counts, int N, int NB,
+                                                           int max_out, int* __restrict__ keep,
+                                                           int* __restrict__ nkeep) {
   // LDS-DMA ring of DEPTH chunks (DEPTH - 1 in flight during a chunk's scan): a chunk's mask
   // rows are one contiguous [64][NB] block, its transposed diagonal words [64] another; both
-  // land by buffer_load ... lds (reads past the problem's last row return zeros), so no
-  // register staging and no load latency per chunk once the ring is full (the one-ahead
-  // register prefetch left most of a ~3.7 us chunk waiting on it: profiles/r5_s1/nms_*.txt)
+  // land by buffer_load ... lds (reads past the problem's last row return zeros).  Four waves
+  // per problem: each issues a quarter of the DMA pieces and ORs a quarter of the kept rows
+  // into the suppression words (LDS ds_or_b64); every wave evaluates the (wave-uniform, cheap)
+  // fixed-point scan itself.  One wave doing all of it spent ~2.5 us per chunk in DMA issue
+  // and the 64-row OR pass (profiles/r5_s1/nms_lds_ring.txt).
   constexpr int DEPTH = 4;
   constexpr int RB = 64 * NBM * 8;                 // row bytes of a slot
   constexpr int SLOTB = RB + 1024;                 // + 1 KiB for the colmask words
-  constexpr int PER = NBM / 2 + 1;                 // DMA pieces per chunk
+  constexpr int NP = NBM / 2 + 1;                  // DMA pieces per chunk
+  constexpr int PW = (NP + 3) / 4;                 // pieces per wave
   __shared__ __attribute__((aligned(1024))) char ring[DEPTH * SLOTB];
+  __shared__ unsigned long long sremoved[NBM];
   const int p = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR LDS bases)
   const int n = counts ? counts[p] : N;
-  unsigned long long removed = 0ull;
+  if (tid < NBM) sremoved[tid] = 0ull;
   int out = 0;
   const gemm::i32x4_t mres = gemm::buffer_rsrc(mask + (size_t)p * N * NB, (uint32_t)((size_t)n * NB * 8));
   const gemm::i32x4_t cres = gemm::buffer_rsrc(colmask + (size_t)p * N, (uint32_t)((size_t)n * 8));
@@ -990,23 +995,30 @@ __global__ __launch_bounds__(64) void nms_keep_par_kernel(const unsigned long lo
     const uint32_t base = __builtin_amdgcn_readfirstlane(ring0 + (c % DEPTH) * SLOTB);
     const uint32_t src = (uint32_t)c * 64u * (uint32_t)NB * 8u;
 #pragma unroll
-    for (int q = 0; q < NBM / 2; ++q)
-      gemm::dma16_buf(mres, 2 * q < NB ? src + 1024u * q + 16u * lane : gemm::kOOB, base + 1024 * q);
-    gemm::dma16_buf(cres, (uint32_t)c * 512u + 16u * lane, base + RB);
+    for (int k = 0; k < PW; ++k) {
+      const int q = wv + 4 * k;                    // piece q of the chunk (NP - 1: colmask)
+      if (q < NP - 1)
+        gemm::dma16_buf(mres, 2 * q < NB ? src + 1024u * q + 16u * lane : gemm::kOOB, base + 1024 * q);
+      else if (q == NP - 1)
+        gemm::dma16_buf(cres, (uint32_t)c * 512u + 16u * lane, base + RB);
+      else   // (keeps the per-wave piece count uniform for the counted waits)
+        gemm::dma16_buf(cres, gemm::kOOB + 0u * lane, base + RB);
+    }
   };
   for (int c = 0; c < DEPTH - 1; ++c)
     if (c < nchunks) issue(c);
+  __syncthreads();   // sremoved initialised
   for (int c = 0; c < nchunks && out < max_out; ++c) {
     const int later = min(nchunks - 1 - c, DEPTH - 2);   // chunks issued after this one
-    // (counts above the 6-bit field's 63 wait for more than needed: still correct)
-    if (later >= 2) gemm::vm_wait<(2 * PER < 63 ? 2 * PER : 63)>();
-    else if (later == 1) gemm::vm_wait<(PER < 63 ? PER : 63)>();
+    if (later >= 2) gemm::vm_wait<2 * PW>();
+    else if (later == 1) gemm::vm_wait<PW>();
     else gemm::vm_wait<0>();
+    __syncthreads();   // every wave's pieces of chunk c have landed
     const int c0 = c << 6, cn = min(64, n - c0), cw = c;
     const char* slot = ring + (c % DEPTH) * SLOTB;
     const unsigned long long* rows = reinterpret_cast<const unsigned long long*>(slot);
     const unsigned long long col = lane < cn ? reinterpret_cast<const unsigned long long*>(slot + RB)[lane] : 0ull;
-    const unsigned long long word = __shfl(removed, cw);
+    const unsigned long long word = sremoved[cw];
     const bool av = lane < cn && !((word >> lane) & 1ull);
     unsigned long long K = __ballot(av);
     for (;;) {
@@ -1018,29 +1030,29 @@ __global__ __launch_bounds__(64) void nms_keep_par_kernel(const unsigned long lo
     unsigned long long kept = K;
     if (__popcll(K) > room)   // greedy order is index order: the first `room` kept boxes
       kept = __ballot(((K >> lane) & 1ull) && __popcll(K & ((1ull << lane) - 1ull)) < room);
-    if ((kept >> lane) & 1ull)
+    if (wv == 0 && ((kept >> lane) & 1ull))
       keep[(size_t)p * max_out + out + __popcll(kept & ((1ull << lane) - 1ull))] = c0 + lane;
     out += __popcll(kept);
-    if (lane < NB && lane > cw) {
-      unsigned long long acc = removed;
-      // rows beyond cn are never kept (their bits of `kept` are 0), so their contents do not matter
+    // this wave's 16 rows of the chunk (rows past cn are never kept)
+    const unsigned long long mine = (kept >> (16 * wv)) & 0xFFFFull;
+    if (mine && lane < NB && lane > cw) {
+      unsigned long long acc = 0ull;
 #pragma unroll
-      for (int i0 = 0; i0 < 64; i0 += 8) {
+      for (int i0 = 0; i0 < 16; i0 += 8) {
         unsigned long long v8[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v8[j] = rows[(i0 + j) * NB + lane];
+        for (int j = 0; j < 8; ++j) v8[j] = rows[(16 * wv + i0 + j) * NB + lane];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc |= v8[j] & (0ull - ((kept >> (i0 + j)) & 1ull));
+        for (int j = 0; j < 8; ++j) acc |= v8[j] & (0ull - ((mine >> (i0 + j)) & 1ull));
       }
-      removed = acc;
+      if (acc) atomicOr(&sremoved[lane], acc);
     }
-    // this slot's reads are complete before the DMA that reuses it is issued
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+    __syncthreads();   // the slot's reads and the suppression words are complete
     if (c + DEPTH - 1 < nchunks) issue(c + DEPTH - 1);
   }
   gemm::vm_wait<0>();   // no LDS-DMA outstanding at exit (early max_out stop)
-  if (lane == 0) nkeep[p] = out;
-  for (int k = out + lane; k < max_out; k += 64) keep[(size_t)p * max_out + k] = -1;
+  if (tid == 0) nkeep[p] = out;
+  for (int k = out + tid; k < max_out; k += 256) keep[(size_t)p * max_out + k] = -1;
 }
 
 // ------------------------------------------------------------------ RPN level top-k + decode
@@ -1734,11 +1746,11 @@ MX_EXPORT int mx_nms(const float* boxes, const int* counts, int P, int N, float 
                      mw, g_nms_par ? colw : (unsigned long long*)nullptr);
   if (g_nms_par) {
     if (NB <= 16)
-      hipLaunchKernelGGL(nms_keep_par_kernel<16>, dim3(P), dim3(64), 0, s, mw, colw, counts, N, NB, max_out, keep, nkeep);
+      hipLaunchKernelGGL(nms_keep_par_kernel<16>, dim3(P), dim3(256), 0, s, mw, colw, counts, N, NB, max_out, keep, nkeep);
     else if (NB <= 32)
-      hipLaunchKernelGGL(nms_keep_par_kernel<32>, dim3(P), dim3(64), 0, s, mw, colw, counts, N, NB, max_out, keep, nkeep);
+      hipLaunchKernelGGL(nms_keep_par_kernel<32>, dim3(P), dim3(256), 0, s, mw, colw, counts, N, NB, max_out, keep, nkeep);
     else
-      hipLaunchKernelGGL(nms_keep_par_kernel<64>, dim3(P), dim3(64), 0, s, mw, colw, counts, N, NB, max_out, keep, nkeep);
+      hipLaunchKernelGGL(nms_keep_par_kernel<64>, dim3(P), dim3(256), 0, s, mw, colw, counts, N, NB, max_out, keep, nkeep);
     return hipGetLastError();
   }
   if (NB <= 16)
