@@ -976,7 +976,10 @@ __global__ __launch_bounds__(256) void nms_keep_par_kernel(const unsigned long l
   // and the 64-row OR pass (profiles/r5_s1/nms_lds_ring.txt).
   constexpr int DEPTH = 4;
   constexpr int RB = 64 * NBM * 8;                 // row bytes of a slot
-  constexpr int SLOTB = RB + 1024;                 // + 1 KiB for the colmask words
+  // + 1 KiB for the colmask words + 1 KiB that the padding pieces fill with zeros (an
+  // out-of-range buffer_load ... lds still WRITES its zeros: aimed at the colmask words, a
+  // padding piece raced the real one)
+  constexpr int SLOTB = RB + 2048;
   constexpr int NP = NBM / 2 + 1;                  // DMA pieces per chunk
   constexpr int PW = (NP + 3) / 4;                 // pieces per wave
   __shared__ __attribute__((aligned(1024))) char ring[DEPTH * SLOTB];
@@ -1002,7 +1005,7 @@ __global__ __launch_bounds__(256) void nms_keep_par_kernel(const unsigned long l
       else if (q == NP - 1)
         gemm::dma16_buf(cres, (uint32_t)c * 512u + 16u * lane, base + RB);
       else   // (keeps the per-wave piece count uniform for the counted waits)
-        gemm::dma16_buf(cres, gemm::kOOB + 0u * lane, base + RB);
+        gemm::dma16_buf(cres, gemm::kOOB + 0u * lane, base + RB + 1024);
     }
   };
   for (int c = 0; c < DEPTH - 1; ++c)
