@@ -234,16 +234,9 @@ class FlatMaster:
             off = _align(max(off, 8), 64)
         self.buckets.append((tb, len(self.sizes), e0, max(off, 8)))
         total = max(off, 8)
-        self.P = torch.zeros(total, dtype=torch.float32, device=dev)
-        self.G = torch.zeros(total, dtype=torch.float32, device=dev)
-        self.M = torch.zeros(total, dtype=torch.float32, device=dev)
-        self.W = torch.zeros(total, dtype=dt, device=dev)
-        with torch.no_grad():
-            for p, o, n in zip(self.params, self.offs, self.sizes):
-                self.P[o:o + n].copy_(p.detach().reshape(-1))
-                p.data = self.P[o:o + n].view(p.shape)
-        self.rebind_state()
-        # layout: fp32 [d0, d1, inner]; bf16 copy channels_last for 4-D weights
+        # layout: 4-D (conv) weights channels_last [d0, kh, kw, d1] in the fp32 buffers too,
+        # i.e. the bf16 copy's order, so every multi-tensor pass (gradient in, SGD + copy out)
+        # is a linear vector stream; the parameters are channels_last-strided views of it
         self.geo = []
         for p in self.params:
             s = p.shape
@@ -251,6 +244,16 @@ class FlatMaster:
             d1 = s[1] if p.dim() >= 2 else 1
             inner = int(torch.Size(s[2:]).numel()) if p.dim() >= 3 else 1
             self.geo.append((d0, d1, inner, 1 if p.dim() == 4 else 0))
+        self.P = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.G = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.M = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.W = torch.zeros(total, dtype=dt, device=dev)
+        with torch.no_grad():
+            for t, p in enumerate(self.params):
+                v = self._fview(self.P, t)
+                v.copy_(p.detach())
+                p.data = v
+        self.rebind_state()
         nb = [(n + self.chunk - 1) // self.chunk for n in self.sizes]
         self.bstart_host = [0]
         for k in nb:
@@ -281,15 +284,25 @@ class FlatMaster:
         self.dp_routes = set()   # every route used so far
         self._dp_reset()
 
+    def _fview(self, buf: torch.Tensor, t: int) -> torch.Tensor:
+        """Parameter t's slice of a flat fp32 buffer as a tensor of the parameter's shape
+        (channels_last-strided for 4-D weights: the buffer holds them in [d0, kh, kw, d1] order)."""
+        p, o, n = self.params[t], self.offs[t], self.sizes[t]
+        d0, d1, inner, cl = self.geo[t]
+        v = buf[o:o + n]
+        if cl and inner > 1:
+            return v.view(d0, p.shape[2], p.shape[3], d1).permute(0, 3, 1, 2)
+        return v.view(p.shape)
+
     # -------------------------------------------------------------- optimizer state
     def rebind_state(self) -> None:
         """Momentum buffers as views of the flat buffer (after construction or after
         ``opt.load_state_dict``, which installs fresh tensors)."""
         with torch.no_grad():
-            for p, o, n in zip(self.params, self.offs, self.sizes):
+            for t, p in enumerate(self.params):
                 st = self.opt.state[p]
                 buf = st.get("momentum_buffer")
-                view = self.M[o:o + n].view(p.shape)
+                view = self._fview(self.M, t)
                 if buf is not None and buf.data_ptr() != view.data_ptr():
                     view.copy_(buf)
                 st["momentum_buffer"] = view
@@ -310,7 +323,8 @@ class FlatMaster:
         for t, (p, o, n) in enumerate(zip(self.params, self.offs, self.sizes)):
             d0, d1, inner, cl = self.geo[t]
             sp = scales[t].data_ptr() if (scales[t] is not None and self.cuda) else 0
-            rows.append([o, n, d0, d1, inner, cl, sp, self.wdf[t]])
+            # cl = 0 for the kernels: the fp32 buffers already hold the copy's order
+            rows.append([o, n, d0, d1, inner, 0, sp, self.wdf[t]])
         self.tab.copy_(torch.tensor(rows, dtype=torch.int64))
         self._scale_key = object()   # new identity: the copies must be re-cast
 
@@ -408,17 +422,16 @@ class FlatMaster:
                 acc = torch.zeros((), dtype=torch.float32)
                 for t, s in zip(range(tb, te), srcs):
                     p = self.params[t]
-                    o, n = self.offs[t], self.sizes[t]
                     gv = torch.zeros(p.shape) if s is None else s.float()
                     if self.scales[t] is not None:
                         gv = gv * self.scales[t].view(-1, *([1] * (p.dim() - 1)))
-                    self.G[o:o + n].copy_(gv.reshape(-1) if gv.is_contiguous() else gv.contiguous().reshape(-1))
+                    self._fview(self.G, t).copy_(gv)
                     acc = acc + gv.pow(2).sum()
                 if not self.dp:
                     self.normsq.fill_(float(acc))
         if self.dp:
             self._dp_ready(k)
-        return [self.G[self.offs[t]:self.offs[t] + self.sizes[t]].view(self.params[t].shape) for t in range(tb, te)]
+        return [self._fview(self.G, t) for t in range(tb, te)]
 
     # -------------------------------------------------------------- data parallel
     def _dp_reset(self) -> None:
