@@ -1324,6 +1324,7 @@ __global__ __launch_bounds__(1024) void tk_sort_decode_kernel(const int64_t* __r
 //      prefix sums) until the need is met;
 //   3. bitonic sort of the <= 2048 (key, ~index) pairs in LDS, values re-read from the row.
 constexpr int kTkrMaxK = 2048;
+constexpr int kTkrLds = 12288;   // rows up to this long keep their keys in LDS for the passes
 
 __device__ __forceinline__ uint32_t tkr_key(float f, bool largest) {
   const uint32_t u = __float_as_uint(f);
@@ -1342,21 +1343,47 @@ __global__ __launch_bounds__(1024) void topk_rows_kernel(const float* __restrict
   __shared__ int wc[16];
   __shared__ int ngt;
   __shared__ unsigned long long cand[kTkrMaxK];
+  __shared__ uint32_t kbuf[kTkrLds];
   const int r = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int chunk = nc > 0 ? r % nc : 0;
   const float* row = nc > 0 ? x + (size_t)(r / nc) * ld + (size_t)chunk * n : x + (size_t)r * ld;
   const int n_in = n;
   if (nc > 0) n = min(n, n_orig - chunk * n_in);   // (the host keeps every chunk >= k long)
   const bool lg = largest != 0;
+  const bool in_lds = n <= kTkrLds;   // (uniform)
+  if (in_lds) {
+    for (int e = t; e < n; e += 1024) kbuf[e] = tkr_key(row[e], lg);
+  }
+  auto key_at = [&](int e) __attribute__((always_inline)) -> uint32_t {
+    return in_lds ? kbuf[e] : tkr_key(row[e], lg);
+  };
+  const unsigned long long below = (1ull << lane) - 1ull;
   uint32_t prefix = 0u, pmask = 0u;
   int rem = k;
   for (int pass = 0; pass < 4; ++pass) {
     const int shift = 24 - 8 * pass;
     if (t < 256) hist[t] = 0;
     __syncthreads();
-    for (int e = t; e < n; e += 1024) {
-      const uint32_t key = tkr_key(row[e], lg);
-      if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1);
+    for (int e0 = 0; e0 < n; e0 += 1024) {
+      const int e = e0 + t;
+      const uint32_t key = e < n ? key_at(e) : 0u;
+      const uint32_t bin = (key >> shift) & 255u;
+      // Keys that share a prefix are concentrated (scores of one range, uniform draws in
+      // [0, 1) share their exponent byte): same-address LDS atomics serialise per lane, so
+      // the bins of the first two still-active lanes are counted with one atomic per wave
+      // (ballot + popcount), the stragglers one by one.
+      bool done = !(e < n && (key & pmask) == prefix);
+#pragma unroll
+      for (int pe = 0; pe < 2; ++pe) {
+        const unsigned long long left = __ballot(!done);
+        if (left == 0ull) break;
+        const int first = __builtin_ctzll(left);
+        const uint32_t b0 = (uint32_t)__shfl((int)bin, first);
+        const unsigned long long same = __ballot(!done && bin == b0);
+        if (lane == first) atomicAdd(&hist[b0], __popcll(same));
+        done = done || bin == b0;
+      }
+      if (!done) atomicAdd(&hist[bin], 1);
     }
     __syncthreads();
     if (w == 0) {
@@ -1394,15 +1421,17 @@ __global__ __launch_bounds__(1024) void topk_rows_kernel(const float* __restrict
   const int need_eq = rem, n_gt = k - need_eq;
   if (t == 0) ngt = 0;
   __syncthreads();
-  const unsigned long long below = (1ull << lane) - 1ull;
   int eq_base = 0;
   for (int e0 = 0; e0 < n; e0 += 1024) {
     const int e = e0 + t;
-    const uint32_t key = e < n ? tkr_key(row[e], lg) : 0u;
+    const uint32_t key = e < n ? key_at(e) : 0u;
     const bool gt = e < n && key > T, eq = e < n && key == T;
-    if (gt) {
-      const int pos = atomicAdd(&ngt, 1);
-      cand[pos] = ((unsigned long long)key << 32) | (uint32_t)(~(uint32_t)e);
+    const unsigned long long bgt = __ballot(gt);   // one slot-claiming atomic per wave
+    if (bgt) {
+      int b_ = 0;
+      if (lane == 0) b_ = atomicAdd(&ngt, __popcll(bgt));
+      b_ = __shfl(b_, 0);
+      if (gt) cand[b_ + __popcll(bgt & below)] = ((unsigned long long)key << 32) | (uint32_t)(~(uint32_t)e);
     }
     const unsigned long long bq = __ballot(eq);
     if (lane == 0) wc[w] = __popcll(bq);
