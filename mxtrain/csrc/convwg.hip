@@ -792,15 +792,16 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
 // Split-K reduction: one thread per (tile, accumulator register group, lane) float4 column,
 // summed over the slices in slice order (deterministic), written to dW with the main
 // kernel's epilogue mapping (4 waves of 64 x 64: WM = WN = 2, FM = FN = 4).
-__global__ __launch_bounds__(64) void conv_wgrad_reduce_kernel(const ConvWg cp) {
+__device__ __forceinline__ void wgrad_reduce_one(const float* slab, uint16_t* dw, int ntiles, int splits,
+                                                 int tiles_tap, int tiles_n, int taps, int Cin, float beta,
+                                                 int gid) {
   constexpr int FM = 4, FN = 4, WN = 2, NR = FM * FN, NT = kNT;
-  const int gid = blockIdx.x * 64 + threadIdx.x;           // < ntiles * NR * NT
-  const int tid = gid % NT, rg = (gid / NT) % NR, t = gid / (NT * NR);
-  if (t >= cp.ntiles) return;
-  const float4* src = reinterpret_cast<const float4*>(cp.slab) + ((size_t)t * cp.splits * NR + rg) * NT + tid;
+  const int tid = gid % NT, rg = (gid / NT) % NR, t = gid / (NT * NR);   // gid < ntiles * NR * NT
+  if (t >= ntiles) return;
+  const float4* src = reinterpret_cast<const float4*>(slab) + ((size_t)t * splits * NR + rg) * NT + tid;
   float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
   int q = 0;
-  for (; q + 4 <= cp.splits; q += 4) {
+  for (; q + 4 <= splits; q += 4) {
     const float4 a0 = src[(size_t)(q + 0) * NR * NT], a1 = src[(size_t)(q + 1) * NR * NT];
     const float4 a2 = src[(size_t)(q + 2) * NR * NT], a3 = src[(size_t)(q + 3) * NR * NT];
     v.x += a0.x; v.y += a0.y; v.z += a0.z; v.w += a0.w;
@@ -808,24 +809,51 @@ __global__ __launch_bounds__(64) void conv_wgrad_reduce_kernel(const ConvWg cp) 
     v.x += a2.x; v.y += a2.y; v.z += a2.z; v.w += a2.w;
     v.x += a3.x; v.y += a3.y; v.z += a3.z; v.w += a3.w;
   }
-  for (; q < cp.splits; ++q) {
+  for (; q < splits; ++q) {
     const float4 a0 = src[(size_t)q * NR * NT];
     v.x += a0.x; v.y += a0.y; v.z += a0.z; v.w += a0.w;
   }
-  const int tap = t / cp.tiles_tap, lt = t - tap * cp.tiles_tap;
-  const int m0 = (lt / cp.tiles_n) * kBM, n0 = (lt % cp.tiles_n) * kBN;
+  const int tap = t / tiles_tap, lt = t - tap * tiles_tap;
+  const int m0 = (lt / tiles_n) * kBM, n0 = (lt % tiles_n) * kBN;
   const int lane = tid & 63, wave = tid >> 6, G = lane >> 4, i = lane & 15;
   const int wm = wave / WN, wn = wave % WN, a = rg / FN, u = rg % FN;
-  const size_t ldc = (size_t)cp.taps * cp.Cin;
-  uint16_t* C = cp.dw + (size_t)(m0 + 16 * FM * wm + 4 * G + 16 * a) * ldc + (size_t)tap * cp.Cin + n0 +
+  const size_t ldc = (size_t)taps * Cin;
+  uint16_t* C = dw + (size_t)(m0 + 16 * FM * wm + 4 * G + 16 * a) * ldc + (size_t)tap * Cin + n0 +
                 16 * FN * wn + 16 * u + i;
   const float e4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     float o = e4[e];
-    if (cp.beta != 0.f) o += cp.beta * bf2f(C[(size_t)e * ldc]);
+    if (beta != 0.f) o += beta * bf2f(C[(size_t)e * ldc]);
     C[(size_t)e * ldc] = f2bf(o);
   }
+}
+
+__global__ __launch_bounds__(64) void conv_wgrad_reduce_kernel(const ConvWg cp) {
+  wgrad_reduce_one(cp.slab, cp.dw, cp.ntiles, cp.splits, cp.tiles_tap, cp.tiles_n, cp.taps, cp.Cin, cp.beta,
+                   blockIdx.x * 64 + threadIdx.x);
+}
+
+// The split-K reductions of up to kWgJobs weight gradients in ONE launch (the deferred
+// reductions of a backward pass, ops/convwg.py): job j owns blocks b0[j] .. b0[j + 1] - 1.
+// The job list travels by value (kernel arguments), so a captured launch replays it as is.
+constexpr int kWgJobs = 40;
+struct WgJob {
+  const float* slab;
+  uint16_t* dw;
+  int ntiles, splits, tiles_tap, tiles_n, taps, Cin, b0;
+  float beta;
+};
+struct WgJobs {
+  WgJob j[kWgJobs];
+};
+__global__ __launch_bounds__(64) void conv_wgrad_reduce_batched_kernel(const WgJobs js, int njobs) {
+  const int b = blockIdx.x;
+  int q = 0;
+  while (q + 1 < njobs && js.j[q + 1].b0 <= b) ++q;   // (wave-uniform)
+  const WgJob& J = js.j[q];
+  wgrad_reduce_one(J.slab, J.dw, J.ntiles, J.splits, J.tiles_tap, J.tiles_n, J.taps, J.Cin, J.beta,
+                   (b - J.b0) * 64 + threadIdx.x);
 }
 
 }  // namespace
@@ -883,6 +911,7 @@ MX_EXPORT int mx_conv_wgrad(const int64_t* d, float beta, int splits, void* stre
   cp.invOW = 1.f / (float)cp.OW;
   cp.invOH = 1.f / (float)cp.OH;
   cp.beta = beta;
+  const bool defer = (d[5] & 1) != 0;   // the caller batches the split-K reduction (mx_conv_wgrad_reduce_batched)
   const bool ident = cp.taps == 1 && cp.stride == 1 && cp.pad == 0 && cp.OH == cp.IH && cp.OW == cp.IW;
   const dim3 grid(cp.ntiles * splits);
   hipStream_t st = (hipStream_t)stream;
@@ -890,10 +919,35 @@ MX_EXPORT int mx_conv_wgrad(const int64_t* d, float beta, int splits, void* stre
     hipLaunchKernelGGL((conv_wgrad_kernel<2, 2, 4, 4, kBK, 2, 2, true>), grid, dim3(kNT), 0, st, cp);
   else
     hipLaunchKernelGGL((conv_wgrad_kernel<2, 2, 4, 4, kBK, 2, 2, false>), grid, dim3(kNT), 0, st, cp);
-  if (splits > 1) {
+  if (splits > 1 && !defer) {
     const int e = hipGetLastError();
     if (e) return e;
     hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(cp.ntiles * 16 * kNT / 64), dim3(64), 0, st, cp);
+  }
+  return (int)hipGetLastError();
+}
+
+// Deferred split-K reductions of several mx_conv_wgrad launches (flag bit 0 of d[5]): jobs =
+// host int64 [njobs][9] {slab, dw, ntiles, splits, tiles_tap, tiles_n, taps, Cin, beta != 0},
+// launched kWgJobs at a time.
+MX_EXPORT int mx_conv_wgrad_reduce_batched(const int64_t* jobs, int njobs, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  for (int j0 = 0; j0 < njobs; j0 += kWgJobs) {
+    const int nj = njobs - j0 < kWgJobs ? njobs - j0 : kWgJobs;
+    WgJobs js{};
+    int blocks = 0;
+    for (int q = 0; q < nj; ++q) {
+      const int64_t* r = jobs + (size_t)(j0 + q) * 9;
+      WgJob& J = js.j[q];
+      J.slab = reinterpret_cast<const float*>(r[0]);
+      J.dw = reinterpret_cast<uint16_t*>(r[1]);
+      J.ntiles = (int)r[2]; J.splits = (int)r[3]; J.tiles_tap = (int)r[4]; J.tiles_n = (int)r[5];
+      J.taps = (int)r[6]; J.Cin = (int)r[7]; J.beta = r[8] ? 1.f : 0.f;
+      if (J.splits < 2 || J.ntiles <= 0 || !J.slab || !J.dw) return (int)hipErrorInvalidValue;
+      J.b0 = blocks;
+      blocks += J.ntiles * 16 * kNT / 64;
+    }
+    hipLaunchKernelGGL(conv_wgrad_reduce_batched_kernel, dim3(blocks), dim3(64), 0, st, js, nj);
   }
   return (int)hipGetLastError();
 }

@@ -368,6 +368,9 @@ class FlatMaster:
             def __enter__(self_):
                 if torch.is_grad_enabled():
                     fm._dp_reset()
+                    if fm.cuda:
+                        from ..ops import convwg
+                        convwg.defer_begin()   # the step's weight-gradient reductions: one launch
                     outs = []
                     for k, (tb, te, _, _) in enumerate(fm.buckets):
                         outs.extend(_FlatCast.apply(fm, k, *fm.params[tb:te]))
@@ -389,6 +392,9 @@ class FlatMaster:
         """Gradients of bucket k's compute copies (bf16, copy layout; None = no gradient)
         -> its slice of the flat fp32 buffer (x fold scale), with sum-of-squares partials."""
         tb, te, _, _ = self.buckets[k]
+        if self.cuda:
+            from ..ops import convwg
+            convwg.defer_flush(keep_on=self.dp and len(self._ready) + 1 < len(self.buckets))
         srcs = []
         keep = []
         for t, g in zip(range(tb, te), grads):

@@ -102,6 +102,7 @@ SIGNATURES = {
     "mx_conv_wgrad_tile": [I],
     "mx_conv_wgrad": [P, F, I, P],
     "mx_conv_wgrad_splits": [I64, I],
+    "mx_conv_wgrad_reduce_batched": [P, I, P],
     "mx_conv_dgrad": [P, P],
     "mx_conv_fwd": [P, P],
     # gemm_nt.hip

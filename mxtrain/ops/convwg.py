@@ -81,6 +81,54 @@ def _workspace(device, slab_elems: int):
     return ws
 
 
+# Deferred split-K reductions (FlatMaster, models/compute_weights.py): between
+# ``defer_begin()`` (forward of a training step) and ``defer_flush()`` (right before the
+# optimizer reads the gradients) every split weight gradient keeps its fp32 partials in its
+# own region of a persistent arena and the reductions run as ONE launch
+# (mx_conv_wgrad_reduce_batched) instead of one small launch per convolution (44 per 1-img
+# Mask R-CNN step at ~5-7 us each, profiles/r5_s1/maskrcnn_1img_census_nms_par.txt).  The
+# arena is sized by the eager steps; a capture that would outgrow it reduces immediately.
+DEFER_WGRAD = True      # module switch (A/B)
+_DEF = {"on": False, "jobs": [], "arena": None, "cursor": 0}
+_DEF_RETIRED = []
+
+
+def defer_begin():
+    _DEF["on"] = DEFER_WGRAD
+    _DEF["jobs"] = []
+    _DEF["cursor"] = 0
+
+
+def defer_flush(keep_on: bool = False):
+    """Launch the pending reductions; deferral stays on only if ``keep_on`` (more gradient
+    buckets of this backward still to come)."""
+    _DEF["on"] = _DEF["on"] and keep_on
+    jobs = _DEF["jobs"]
+    if jobs:
+        flat = [v for j in jobs for v in j]
+        arr = (ctypes.c_int64 * len(flat))(*flat)
+        _lib.call("mx_conv_wgrad_reduce_batched", ctypes.addressof(arr), len(jobs), _lib.stream())
+    _DEF["jobs"] = []
+    _DEF["cursor"] = 0
+
+
+def _defer_slab(device, elems: int):
+    """fp32 region of the deferral arena for one weight gradient's partials, or None."""
+    need = (elems + 63) // 64 * 64
+    a = _DEF["arena"]
+    cur = _DEF["cursor"]
+    if a is None or a.device != device or a.numel() < cur + need:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        if a is not None:
+            _DEF_RETIRED.append(a)   # earlier jobs of this step (and captured graphs) still use it
+        a = _DEF["arena"] = torch.empty(max(2 * (a.numel() if a is not None else 0), need, 1 << 22),
+                                        device=device, dtype=torch.float32)
+        cur = 0
+    _DEF["cursor"] = cur + need
+    return a[cur:cur + need]
+
+
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dilation, out=None,
                beta: float = 0.0, splits: int = 0) -> torch.Tensor:
     """dW [Cout, Cin, KH, KW] (channels_last bf16) of conv2d(x, w) for the output gradient
@@ -108,8 +156,16 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dila
         splits = plan_splits(T, ntiles)
     splits = int(_lib.query("mx_conv_wgrad_splits", T, splits))
     slab, zero = _workspace(x.device, ntiles * splits * 128 * 128 if splits > 1 else 1)
+    defer = 0
+    # (only from inside an autograd backward: a direct call never waits for a flush)
+    if splits > 1 and _DEF["on"] and torch._C._current_autograd_node() is not None:
+        reg = _defer_slab(x.device, ntiles * splits * 128 * 128)
+        if reg is not None:
+            slab, defer = reg, 1
+            _DEF["jobs"].append([reg.data_ptr(), out.data_ptr(), ntiles, splits, (Cout // 128) * (Cin // 128),
+                                 Cin // 128, KH * KW, Cin, 1 if beta else 0])
     d = _DESC_T()
-    d[:20] = [dy.data_ptr(), x.data_ptr(), zero.data_ptr(), out.data_ptr(), slab.data_ptr(), 0,
+    d[:20] = [dy.data_ptr(), x.data_ptr(), zero.data_ptr(), out.data_ptr(), slab.data_ptr(), defer,
             Cout, Cin, N, OH, OW, IH, IW, KH, KW, _sym(stride), _sym(padding), _sym(dilation), Cout, Cin]
     _lib.call("mx_conv_wgrad", d, float(beta), splits, _lib.stream())
     return out
