@@ -67,16 +67,17 @@ __global__ __launch_bounds__(256) void rpn_keys_kernel(const float4* __restrict_
 // (_rank_select twice, the second one's quota from the first's count).
 __global__ __launch_bounds__(256) void rpn_select_kernel(const float* __restrict__ vpos, const int64_t* __restrict__ ipos,
                                                          int kp, const float* __restrict__ vneg,
-                                                         const int64_t* __restrict__ ineg, int kn, int batch, int A,
-                                                         uint8_t* __restrict__ sel_pos, uint8_t* __restrict__ sel_neg) {
+                                                         const int64_t* __restrict__ ineg, int kn, int ld, int batch,
+                                                         int A, uint8_t* __restrict__ sel_pos,
+                                                         uint8_t* __restrict__ sel_neg) {
   __shared__ int cnt;
   const int b = blockIdx.x, t = threadIdx.x;
   if (t == 0) cnt = 0;
   __syncthreads();
   int mine = 0;
   for (int r = t; r < kp; r += 256) {
-    if (vpos[(size_t)b * kp + r] < 2.f) {
-      sel_pos[(size_t)b * A + ipos[(size_t)b * kp + r]] = 1;
+    if (vpos[(size_t)b * ld + r] < 2.f) {
+      sel_pos[(size_t)b * A + ipos[(size_t)b * ld + r]] = 1;
       ++mine;
     }
   }
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(256) void rpn_select_kernel(const float* __restrict
   __syncthreads();
   const int want = batch - cnt;
   for (int r = t; r < kn && r < want; r += 256)
-    if (vneg[(size_t)b * kn + r] < 2.f) sel_neg[(size_t)b * A + ineg[(size_t)b * kn + r]] = 1;
+    if (vneg[(size_t)b * ld + r] < 2.f) sel_neg[(size_t)b * A + ineg[(size_t)b * ld + r]] = 1;
 }
 
 // Fast R-CNN RoI sampling, candidates = K proposals + G gt boxes per image (gt rows past
@@ -187,11 +188,14 @@ MX_EXPORT int mx_rpn_keys(const float* anchors, int A, int B, const float* mi, c
   return hipGetLastError();
 }
 
+// vpos / ipos, vneg / ineg: [B][ld] sorted key / index rows (the first kp / kn used)
 MX_EXPORT int mx_rpn_select(const float* vpos, const int64_t* ipos, int kp, const float* vneg, const int64_t* ineg,
-                            int kn, int batch, int A, int B, uint8_t* sel_pos, uint8_t* sel_neg, hipStream_t s) {
+                            int kn, int ld, int batch, int A, int B, uint8_t* sel_pos, uint8_t* sel_neg,
+                            hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  hipLaunchKernelGGL(rpn_select_kernel, dim3(B), dim3(256), 0, s, vpos, ipos, kp, vneg, ineg, kn, batch, A, sel_pos,
-                     sel_neg);
+  if (ld < kp || ld < kn) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rpn_select_kernel, dim3(B), dim3(256), 0, s, vpos, ipos, kp, vneg, ineg, kn, ld, batch, A,
+                     sel_pos, sel_neg);
   return hipGetLastError();
 }
 

@@ -489,8 +489,8 @@ class MaskRCNN(nn.Module):
         gtf = gt_boxes.float().contiguous()
         mi, am, lq = V.match_boxes(anchors, gtf, gt_count, int32=True)
         g = torch.rand((B, A), device=dev)
-        kpos = torch.empty(B, A, dtype=torch.float32, device=dev)
-        kneg = torch.empty_like(kpos)
+        keys = torch.empty(2 * B, A, dtype=torch.float32, device=dev)   # positive rows, then negative rows
+        kpos, kneg = keys[:B], keys[B:]
         enc = torch.empty(B, A, 4, dtype=torch.float32, device=dev)
         sel_pos = torch.empty(B, A, dtype=torch.bool, device=dev)
         sel_neg = torch.empty_like(sel_pos)
@@ -501,9 +501,11 @@ class MaskRCNN(nn.Module):
                   _lib.ptr(kneg), _lib.ptr(enc), _lib.ptr(sel_pos), _lib.ptr(sel_neg), _lib.stream())
         nfg_max = min(int(cfg.rpn_batch_per_im * cfg.rpn_fg_ratio), A)
         nb = min(cfg.rpn_batch_per_im, A)
-        vp, ip = V.topk_rows(kpos, nfg_max, largest=False)
-        vn, ineg = V.topk_rows(kneg, nb, largest=False)
-        _lib.call("mx_rpn_select", _lib.ptr(vp), _lib.ptr(ip), nfg_max, _lib.ptr(vn), _lib.ptr(ineg), nb,
+        # both selections in one (two-launch) long-row top-k: the nfg_max smallest positive
+        # keys are the first nfg_max of that row's nb smallest (sorted, ties by index)
+        kk = max(nfg_max, nb)
+        v2, i2 = V.topk_rows(keys, kk, largest=False)
+        _lib.call("mx_rpn_select", _lib.ptr(v2), _lib.ptr(i2), nfg_max, _lib.ptr(v2[B:]), _lib.ptr(i2[B:]), nb, kk,
                   int(cfg.rpn_batch_per_im), A, B, _lib.ptr(sel_pos), _lib.ptr(sel_neg), _lib.stream())
         return sel_pos, sel_neg, enc
 
@@ -544,9 +546,8 @@ class MaskRCNN(nn.Module):
         kb = torch.gather(boxes, 1, ki[..., None].expand(-1, -1, 4))
         ks = torch.where(valid, torch.gather(scores, 1, ki), torch.full_like(scores, -float("inf")))
         kb = kb.view(B, L * pre, 4)
-        ks = ks.view(B, L * pre)
-        top = min(post, ks.shape[1])
-        s, i = V.topk_rows(ks, top)
+        top = min(post, L * pre)
+        s, i = V.merge_sorted_topk(ks.view(B, L, pre), top)   # (each level's survivors are sorted)
         b = torch.gather(kb, 1, i[..., None].expand(-1, -1, 4))
         return b.detach(), s.detach()
 

@@ -133,7 +133,8 @@ SIGNATURES = {
     # dettarget.hip
     "mx_encode_boxes": [P, I, P, I, F, F, F, F, P, P],
     "mx_rpn_keys": [P, I, I, P, P, P, P, P, P, I, F, F, P, P, P, P, P, P],
-    "mx_rpn_select": [P, P, I, P, P, I, I, I, I, P, P, P],
+    "mx_rpn_select": [P, P, I, P, P, I, I, I, I, I, P, P, P],
+    "mx_merge_sorted_topk": [P, I, I, I, I, P, P, P],
     "mx_roi_candidates": [P, I, P, P, I, I, P, P, P],
     "mx_roi_fgkey": [P, P, P, I, F, P, P],
     "mx_roi_order": [P, P, I, P, P, P, I, I, F, P, P, P],

@@ -423,6 +423,20 @@ def crop_resize_mask_crops(flat: torch.Tensor, table: torch.Tensor, H: int, W: i
 _TK_CACHE = {}
 
 
+def merge_sorted_topk(ks: torch.Tensor, top: int):
+    """topk_rows(ks.view(B, L * pre), top) for ks [B, L, pre] whose L lists are each sorted
+    non-increasing (the per-level NMS survivors): one rank-by-binary-search pass
+    (csrc/vision.hip merge_topk_kernel) instead of a radix select + sort."""
+    B, L, pre = ks.shape
+    if _lib.use_hip(ks) and ks.dtype == torch.float32 and L * pre <= 16384 and top <= L * pre:
+        k = ks.contiguous()
+        ov = torch.empty(B, top, dtype=torch.float32, device=ks.device)
+        oi = torch.empty(B, top, dtype=torch.int64, device=ks.device)
+        _lib.call("mx_merge_sorted_topk", _lib.ptr(k), B, L, pre, top, _lib.ptr(ov), _lib.ptr(oi), _lib.stream())
+        return ov, oi
+    return topk_rows(ks.reshape(B, L * pre), top)
+
+
 def topk_rows(x: torch.Tensor, k: int, largest: bool = True):
     """(values, int64 indices) of the k largest / smallest entries of each row of a 2-D
     fp32 tensor, sorted, ties by lower index -- torch.topk(x, k, dim=1, largest) semantics

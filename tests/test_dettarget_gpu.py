@@ -177,3 +177,20 @@ def test_fpn_fanout_gradient_sum():
         loss.backward()
         exp = sum(t.float() for t, u in zip((ga, gb, gc), use) if u)
         torch.testing.assert_close(p.grad.float(), exp, rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("B,L,pre,top", [(1, 5, 2000, 2000), (4, 5, 2000, 2000), (2, 3, 700, 1000), (3, 8, 64, 100)])
+def test_merge_sorted_topk_matches_topk_rows(B, L, pre, top):
+    """The post-NMS merge of L sorted level lists (with duplicated scores across and within
+    lists and -inf tails) equals topk_rows over the flattened lists: values and indices."""
+    from mxtrain.ops import vision as V
+    g = torch.Generator().manual_seed(B * 100 + L)
+    x = (torch.rand(B, L, pre, generator=g) * 50).round() / 50     # many ties
+    x = torch.sort(x, dim=-1, descending=True)[0]
+    nvalid = torch.randint(pre // 3, pre + 1, (B, L), generator=g)
+    x[torch.arange(pre)[None, None] >= nvalid[..., None]] = -float("inf")
+    x = x.to(DEV)
+    v, i = V.merge_sorted_topk(x, top)
+    rv, ri = V.topk_rows(x.reshape(B, L * pre), top)
+    assert torch.equal(v, rv)
+    assert torch.equal(i, ri)
