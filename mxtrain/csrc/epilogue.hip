@@ -95,6 +95,42 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const uint16_t* __res
   }
 }
 
+// Gradient of a 2x nearest upsampling (NHWC): out[n][y][x][c] = sum of g over the 2 x 2 block
+// at (2y, 2x) (+ add[n][y][x][c]) -- fp32 sum, one bf16 rounding.  The FPN top-down join's
+// residual gradient, with the joined level's other gradient folded in (ops/epilogue.py
+// JoinLink); thread = 8 channels of one output pixel, 16-B loads / store.
+__global__ __launch_bounds__(256) void down2_add_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ add,
+                                                        uint16_t* __restrict__ out, int N, int H, int W, int C) {
+  const int C8 = C >> 3;
+  const int64_t total = (int64_t)N * H * W * C8;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+    const int c = (int)(q % C8) * 8;
+    const int64_t pix = q / C8;
+    const int x = (int)(pix % W);
+    const int64_t ny = pix / W;
+    const int y = (int)(ny % H);
+    const int n = (int)(ny / H);
+    const size_t r0 = (((size_t)n * 2 * H + 2 * y) * 2 * W + 2 * x) * C + c;
+    const size_t r1 = r0 + (size_t)2 * W * C;
+    float a[8], b[8], d[8], e[8];
+    unpack8(*reinterpret_cast<const uint4*>(g + r0), a);
+    unpack8(*reinterpret_cast<const uint4*>(g + r0 + C), b);
+    unpack8(*reinterpret_cast<const uint4*>(g + r1), d);
+    unpack8(*reinterpret_cast<const uint4*>(g + r1 + C), e);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (a[j] + b[j]) + (d[j] + e[j]);
+    const size_t op = (size_t)pix * C + c;
+    if (add) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(add + op), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += f[j];
+    }
+    *reinterpret_cast<uint4*>(out + op) = pack8(o);
+  }
+}
+
 }  // namespace
 
 // colreduce (norm.hip): fold fp32 partials [P][C] into a bf16 vector
@@ -151,5 +187,17 @@ MX_EXPORT int mx_bias_act_bwd(const void* g, const void* out, void* dy, void* db
   }
 #undef MX_BB
   if (db) return mx_colsum_finalize(partial, nparts, C, 1, db, nullptr, nullptr, accumulate, nullptr, s);
+  return hipGetLastError();
+}
+
+// g [N][2H][2W][C], add (nullable) / out [N][H][W][C], all NHWC contiguous bf16, C % 8 == 0,
+// 16-B aligned
+MX_EXPORT int mx_down2_add(const void* g, const void* add, void* out, int N, int H, int W, int C, hipStream_t s) {
+  if (N <= 0 || H <= 0 || W <= 0) return hipSuccess;
+  if ((C & 7) || (((uintptr_t)g | (uintptr_t)add | (uintptr_t)out) & 15)) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  const unsigned blocks = (unsigned)((total + 255) / 256 < 16384 ? (total + 255) / 256 : 16384);
+  hipLaunchKernelGGL(down2_add_kernel, dim3(blocks), dim3(256), 0, s, (const uint16_t*)g, (const uint16_t*)add,
+                     (uint16_t*)out, N, H, W, C);
   return hipGetLastError();
 }

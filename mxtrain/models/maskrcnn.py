@@ -30,10 +30,11 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.epilogue import BlockLink, conv_bias_act, conv_transpose_bias_act, fused_conv_ok
+from ..ops.epilogue import BlockLink, JoinLink, _conv_in_ok, conv_bias_act, conv_transpose_bias_act, fused_conv_ok
 from ..ops import detloss as D
 from ..ops import vision as V
 from ..ops import _lib
+from ..ops import convwg
 from .compute_weights import ComputeWeights, cw
 from .resnet import ConvNorm, resnet50
 
@@ -110,6 +111,8 @@ def huber(x: torch.Tensor, delta: float) -> torch.Tensor:
 
 # ---------------------------------------------------------------------------- modules
 class FPN(nn.Module):
+    join_backward = True   # JoinLink fusion of the top-down join gradients (A/B switch)
+
     def __init__(self, in_channels: Sequence[int], out: int = 256):
         super().__init__()
         self.lateral = nn.ModuleList([nn.Conv2d(c, out, 1) for c in in_channels])
@@ -126,10 +129,23 @@ class FPN(nn.Module):
         lat = [None] * L
         m = self.lateral[L - 1]
         lat[L - 1] = conv_bias_act(feats[L - 1], cw(m.weight, dt), cw(m.bias, dt))
+        # backward: level i's two gradients (output conv, next lateral's residual) summed inside
+        # the kernels (ops/epilogue.py JoinLink) when both convs run the fused path
+        link = JoinLink() if (torch.is_grad_enabled() and self.join_backward) else None
+        joined = set()
         for i in range(L - 2, -1, -1):
             m = self.lateral[i]
-            lat[i] = conv_bias_act(feats[i], cw(m.weight, dt), cw(m.bias, dt), residual=lat[i + 1], res_up=True)
-        outs = [conv_bias_act(x, cw(m.weight, dt), cw(m.bias, dt), padding=1) for x, m in zip(lat, self.output)]
+            wl, bl, wo, bo = cw(m.weight, dt), cw(m.bias, dt), cw(self.output[i + 1].weight, dt), cw(self.output[i + 1].bias, dt)
+            fuse = None
+            if (link is not None and _conv_in_ok(feats[i], wl, bl, lat[i + 1])
+                    and convwg.fwd_supported(feats[i], wl, bl, lat[i + 1], 1, 0, 1, res_up=True)
+                    and fused_conv_ok(lat[i + 1], wo, bo, None, 1, 1, 1)):
+                fuse = (link, i + 1, ("join_res",))
+                joined.add(i + 1)
+            lat[i] = conv_bias_act(feats[i], wl, bl, residual=lat[i + 1], res_up=True, fuse=fuse)
+        outs = [conv_bias_act(x, cw(m.weight, dt), cw(m.bias, dt), padding=1,
+                              fuse=(link, i, ("join_dx",)) if i in joined else None)
+                for i, (x, m) in enumerate(zip(lat, self.output))]
         outs.append(F.max_pool2d(outs[-1], 1, 2))   # P6
         return outs
 

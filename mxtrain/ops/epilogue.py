@@ -106,6 +106,22 @@ class BlockLink:
         self.prev = None      # the previous block's link when conv1 has role "mask_prev"
 
 
+class JoinLink(BlockLink):
+    """FPN top-down join (models/maskrcnn.py FPN): merged level i has two consumers, its 3 x 3
+    output conv (role "join_dx", key i) and the next lateral conv, which reads it
+    nearest-upsampled as its residual (role "join_res", key i).  Whichever backward runs
+    first parks its gradient of the level in ``join[i]`` and returns None for it; the second
+    folds it in -- into its dgrad store (output conv) or into the 2 x 2 block sum of the
+    residual gradient (lateral conv) -- so autograd's separate add of the two gradients, and
+    the upsampling gradient's reduce + cast passes, disappear."""
+
+    __slots__ = ("join",)
+
+    def __init__(self):
+        super().__init__()
+        self.join = {}
+
+
 class ConvBiasActFn(torch.autograd.Function):
     """act(conv2d(x, w) + b (+ res)) with every direction on csrc/convwg.hip where it tiles:
     forward = one implicit-GEMM launch with the epilogue fused; backward = the ReLU mask +
@@ -138,11 +154,23 @@ class ConvBiasActFn(torch.autograd.Function):
             db = db.to(ctx.bdtype)
         dres = dy if ctx.has_res else None
         if dres is not None and ctx.res_up:
-            dres = down2_sum(dres)
+            if "join_res" in roles and k in link.join:     # the level's other gradient came first
+                dres = down2_sum(dres, link.join.pop(k))
+            else:
+                dres = down2_sum(dres)
+                if "join_res" in roles:
+                    link.join[k] = dres
+                    dres = None
         if dres is not None and "stash_res" in roles and link.taker and ctx.needs_input_grad[3]:
             link.stash.append(dres)
             dres = None
         add = link.stash.pop() if "take_res" in roles and link.stash else None
+        join_first = False
+        if "join_dx" in roles:
+            if k in link.join:
+                add = link.join.pop(k)
+            else:
+                join_first = True
         mask = x if ("mask_in" in roles or "mask_prev" in roles) else None
         dx = dw = None
         if ctx.needs_input_grad[0]:
@@ -155,6 +183,9 @@ class ConvBiasActFn(torch.autograd.Function):
                     dx = dx + add
                 if mask is not None:
                     dx = torch.where(mask > 0, dx, torch.zeros_like(dx))
+            if join_first:
+                link.join[k] = dx
+                dx = None
         elif add is not None:
             raise RuntimeError("BlockLink: residual gradient stashed for a conv without an input gradient")
         if ctx.needs_input_grad[1]:
@@ -166,11 +197,19 @@ class ConvBiasActFn(torch.autograd.Function):
         return dx, dw, db, dres, None, None, None, None, None, None
 
 
-def down2_sum(g: torch.Tensor) -> torch.Tensor:
-    """Gradient of the 2x nearest upsampling: each 2 x 2 block summed (NHWC memory kept)."""
+def down2_sum(g: torch.Tensor, add: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Gradient of the 2x nearest upsampling: each 2 x 2 block summed (+ ``add``, a second
+    gradient of the same tensor), NHWC memory kept -- one pass (csrc/epilogue.hip
+    mx_down2_add) on the GPU path."""
     N, C, H, W = g.shape
+    if (_lib.use_hip(g) and g.dtype == torch.bfloat16 and _nhwc(g) and C % 8 == 0 and H % 2 == 0 and W % 2 == 0
+            and (add is None or (add.dtype == torch.bfloat16 and _nhwc(add) and add.shape == (N, C, H // 2, W // 2)))):
+        out = torch.empty((N, H // 2, W // 2, C), dtype=g.dtype, device=g.device)
+        _lib.call("mx_down2_add", _lib.ptr(g), _lib.ptr(add), _lib.ptr(out), N, H // 2, W // 2, C, _lib.stream())
+        return out.permute(0, 3, 1, 2)
     t = g.permute(0, 2, 3, 1).reshape(N, H // 2, 2, W // 2, 2, C).sum((2, 4), dtype=torch.float32)
-    return t.to(g.dtype).permute(0, 3, 1, 2)
+    t = t.to(g.dtype).permute(0, 3, 1, 2)
+    return t if add is None else t + add
 
 
 def _fused_ok(y, b, residual) -> bool:

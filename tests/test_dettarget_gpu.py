@@ -194,3 +194,31 @@ def test_merge_sorted_topk_matches_topk_rows(B, L, pre, top):
     rv, ri = V.topk_rows(x.reshape(B, L * pre), top)
     assert torch.equal(v, rv)
     assert torch.equal(i, ri)
+
+
+def test_fpn_join_backward_matches_autograd_add():
+    """FPN top-down join with the two gradients of each merged level summed inside the kernels
+    (JoinLink: output conv dgrad store / 2x2 block-sum kernel) equals the unfused backward
+    (autograd's add of the output conv's input gradient and the upsampling gradient)."""
+    from mxtrain.models.maskrcnn import FPN
+    torch.manual_seed(0)
+    chans = [256, 512, 1024, 2048]
+    shapes = [(48, 64), (24, 32), (12, 16), (6, 8)]
+    fpn = FPN(chans, 256).to(DEV).to(torch.bfloat16)
+    feats = [torch.randn(2, c, h, w, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+             for c, (h, w) in zip(chans, shapes)]
+    gouts = None
+    res = []
+    for join in (False, True):
+        FPN.join_backward = join
+        fs = [f.detach().clone().requires_grad_(True) for f in feats]
+        for p in fpn.parameters():
+            p.grad = None
+        outs = fpn(fs)
+        if gouts is None:
+            gouts = [torch.randn_like(o) for o in outs]
+        sum((o.float() * g.float()).sum() for o, g in zip(outs, gouts)).backward()
+        res.append([f.grad.float() for f in fs] + [p.grad.float() for p in fpn.parameters()])
+    FPN.join_backward = True
+    for a, b in zip(*res):
+        torch.testing.assert_close(b, a, rtol=3e-2, atol=3e-2 * float(a.abs().max()) + 1e-3)
