@@ -89,7 +89,7 @@ def _workspace(device, slab_elems: int):
 # Mask R-CNN step at ~5-7 us each, profiles/r5_s1/maskrcnn_1img_census_nms_par.txt).  The
 # arena is sized by the eager steps; a capture that would outgrow it reduces immediately.
 DEFER_WGRAD = True      # module switch (A/B)
-_DEF = {"on": False, "jobs": [], "arena": None, "cursor": 0}
+_DEF = {"on": False, "jobs": [], "arena": None, "cursor": 0, "total": 0, "peak": 0}
 _DEF_RETIRED = []
 
 
@@ -97,6 +97,7 @@ def defer_begin():
     _DEF["on"] = DEFER_WGRAD
     _DEF["jobs"] = []
     _DEF["cursor"] = 0
+    _DEF["total"] = 0
 
 
 def defer_flush(keep_on: bool = False):
@@ -110,11 +111,19 @@ def defer_flush(keep_on: bool = False):
         _lib.call("mx_conv_wgrad_reduce_batched", ctypes.addressof(arr), len(jobs), _lib.stream())
     _DEF["jobs"] = []
     _DEF["cursor"] = 0
+    # an arena outgrown mid-step held only the later jobs: size it for the whole step now
+    # (eager), so the capture that follows this shape's eager step defers every reduction
+    a = _DEF["arena"]
+    _DEF["peak"] = max(_DEF["peak"], _DEF["total"])
+    if a is not None and a.numel() < _DEF["peak"] and not torch.cuda.is_current_stream_capturing():
+        _DEF_RETIRED.append(a)
+        _DEF["arena"] = torch.empty(_DEF["peak"], device=a.device, dtype=torch.float32)
 
 
 def _defer_slab(device, elems: int):
     """fp32 region of the deferral arena for one weight gradient's partials, or None."""
     need = (elems + 63) // 64 * 64
+    _DEF["total"] += need
     a = _DEF["arena"]
     cur = _DEF["cursor"]
     if a is None or a.device != device or a.numel() < cur + need:
