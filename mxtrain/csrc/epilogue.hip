@@ -131,6 +131,52 @@ __global__ __launch_bounds__(256) void down2_add_kernel(const uint16_t* __restri
   }
 }
 
+// Deferred bias-gradient column sums of a backward (ops/convwg.py defer_flush): job j folds
+// its fp32 partial rows [nparts][C] into the bf16 vector out[C] (written, or added to);
+// a block = 16 columns of one job, thread t sums column t & 15 over the rows t >> 4,
+// (t >> 4) + 16, ... (eight loads in flight), the 16 row-phase sums folded in LDS in a fixed
+// order (deterministic).  The job list travels by value.
+constexpr int kCsJobs = 64;
+struct CsJob {
+  const float* part;
+  uint16_t* out;
+  int nparts, C, acc, b0;
+};
+struct CsJobs {
+  CsJob j[kCsJobs];
+};
+__global__ __launch_bounds__(256) void colsum_jobs_kernel(const CsJobs js, int njobs) {
+  __shared__ float red[16][17];
+  const int b = blockIdx.x;
+  int q = 0;
+  while (q + 1 < njobs && js.j[q + 1].b0 <= b) ++q;
+  const CsJob& J = js.j[q];
+  const int t = threadIdx.x, ci = t & 15, ph = t >> 4;
+  const int c = (b - J.b0) * 16 + ci;
+  float s = 0.f;
+  if (c < J.C) {
+    int r = ph;
+    for (; r + 7 * 16 < J.nparts; r += 8 * 16) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = J.part[(size_t)(r + 16 * u) * J.C + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; r < J.nparts; r += 16) s += J.part[(size_t)r * J.C + c];
+  }
+  red[ph][ci] = s;
+  __syncthreads();
+  if (t < 16 && (b - J.b0) * 16 + t < J.C) {
+    float tot = 0.f;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) tot += red[p][t];
+    uint16_t* o = J.out + (b - J.b0) * 16 + t;
+    if (J.acc) tot += bf2f(*o);
+    *o = f2bf(tot);
+  }
+}
+
 }  // namespace
 
 // colreduce (norm.hip): fold fp32 partials [P][C] into a bf16 vector
@@ -186,7 +232,30 @@ MX_EXPORT int mx_bias_act_bwd(const void* g, const void* out, void* dy, void* db
     MX_BB(false, true);
   }
 #undef MX_BB
-  if (db) return mx_colsum_finalize(partial, nparts, C, 1, db, nullptr, nullptr, accumulate, nullptr, s);
+  // accumulate bit 1: the caller folds the partials later (mx_colsum_jobs)
+  if (db && !(accumulate & 2))
+    return mx_colsum_finalize(partial, nparts, C, 1, db, nullptr, nullptr, accumulate & 1, nullptr, s);
+  return hipGetLastError();
+}
+
+// jobs: host int64 [njobs][5] {partial, out, nparts, C, accumulate}; kCsJobs per launch
+MX_EXPORT int mx_colsum_jobs(const int64_t* jobs, int njobs, hipStream_t s) {
+  for (int j0 = 0; j0 < njobs; j0 += kCsJobs) {
+    const int nj = njobs - j0 < kCsJobs ? njobs - j0 : kCsJobs;
+    CsJobs js{};
+    int blocks = 0;
+    for (int q = 0; q < nj; ++q) {
+      const int64_t* r = jobs + (size_t)(j0 + q) * 5;
+      CsJob& J = js.j[q];
+      J.part = reinterpret_cast<const float*>(r[0]);
+      J.out = reinterpret_cast<uint16_t*>(r[1]);
+      J.nparts = (int)r[2]; J.C = (int)r[3]; J.acc = (int)r[4];
+      if (!J.part || !J.out || J.C <= 0 || J.nparts <= 0) return hipErrorInvalidValue;
+      J.b0 = blocks;
+      blocks += (J.C + 15) / 16;
+    }
+    hipLaunchKernelGGL(colsum_jobs_kernel, dim3(blocks), dim3(256), 0, s, js, nj);
+  }
   return hipGetLastError();
 }
 

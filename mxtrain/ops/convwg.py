@@ -89,13 +89,14 @@ def _workspace(device, slab_elems: int):
 # Mask R-CNN step at ~5-7 us each, profiles/r5_s1/maskrcnn_1img_census_nms_par.txt).  The
 # arena is sized by the eager steps; a capture that would outgrow it reduces immediately.
 DEFER_WGRAD = True      # module switch (A/B)
-_DEF = {"on": False, "jobs": [], "arena": None, "cursor": 0, "total": 0, "peak": 0}
+_DEF = {"on": False, "jobs": [], "cjobs": [], "arena": None, "cursor": 0, "total": 0, "peak": 0}
 _DEF_RETIRED = []
 
 
 def defer_begin():
     _DEF["on"] = DEFER_WGRAD
     _DEF["jobs"] = []
+    _DEF["cjobs"] = []
     _DEF["cursor"] = 0
     _DEF["total"] = 0
 
@@ -104,12 +105,13 @@ def defer_flush(keep_on: bool = False):
     """Launch the pending reductions; deferral stays on only if ``keep_on`` (more gradient
     buckets of this backward still to come)."""
     _DEF["on"] = _DEF["on"] and keep_on
-    jobs = _DEF["jobs"]
-    if jobs:
-        flat = [v for j in jobs for v in j]
-        arr = (ctypes.c_int64 * len(flat))(*flat)
-        _lib.call("mx_conv_wgrad_reduce_batched", ctypes.addressof(arr), len(jobs), _lib.stream())
-    _DEF["jobs"] = []
+    for key, fn, width in (("jobs", "mx_conv_wgrad_reduce_batched", 9), ("cjobs", "mx_colsum_jobs", 5)):
+        jobs = _DEF[key]
+        if jobs:
+            flat = [v for j in jobs for v in j]
+            arr = (ctypes.c_int64 * len(flat))(*flat)
+            _lib.call(fn, ctypes.addressof(arr), len(jobs), _lib.stream())
+        _DEF[key] = []
     _DEF["cursor"] = 0
     # an arena outgrown mid-step held only the later jobs: size it for the whole step now
     # (eager), so the capture that follows this shape's eager step defers every reduction
@@ -118,6 +120,22 @@ def defer_flush(keep_on: bool = False):
     if a is not None and a.numel() < _DEF["peak"] and not torch.cuda.is_current_stream_capturing():
         _DEF_RETIRED.append(a)
         _DEF["arena"] = torch.empty(_DEF["peak"], device=a.device, dtype=torch.float32)
+
+
+def deferring() -> bool:
+    """Deferral is on and the caller runs inside an autograd backward."""
+    return _DEF["on"] and torch._C._current_autograd_node() is not None
+
+
+def defer_colsum(device, nparts: int, C: int, out: torch.Tensor):
+    """fp32 [nparts * C] arena region for a bias gradient's column partials, reduced into the
+    bf16 ``out`` at the flush; None when deferral is off (reduce immediately)."""
+    if not deferring():
+        return None
+    reg = _defer_slab(device, nparts * C)
+    if reg is not None:
+        _DEF["cjobs"].append([reg.data_ptr(), out.data_ptr(), nparts, C, 0])
+    return reg
 
 
 def _defer_slab(device, elems: int):

@@ -55,16 +55,16 @@ class BiasActFn(torch.autograd.Function):
         dy = torch.empty_like(g) if relu else g
         db = torch.empty(C, dtype=torch.bfloat16, device=g.device) if want_db else None
         nparts = _lib.query("mx_bias_act_bwd_parts", M, C)
-        partial = torch.empty(nparts * C, dtype=torch.float32, device=g.device) if want_db else None
+        partial, flags = _colsum_partial(g.device, nparts, C, db, ctx.bdtype)
         out = ctx.saved_tensors[0] if relu else None
         _lib.call("mx_bias_act_bwd", _lib.ptr(g), _lib.ptr(out), _lib.ptr(dy), _lib.ptr(db), _lib.ptr(partial),
-                  M, C, int(relu), 0, _lib.stream())
+                  M, C, int(relu), flags, _lib.stream())
         if db is not None and db.dtype != ctx.bdtype:
             db = db.to(ctx.bdtype)
         return dy, db, (dy if ctx.has_res else None), None
 
 
-def _bias_act_bwd(g, out, relu: bool, want_db: bool):
+def _bias_act_bwd(g, out, relu: bool, want_db: bool, bdtype=torch.bfloat16):
     """(dy, db) of y = act(conv + b (+ res)): the ReLU mask and the bias-gradient column sums
     in one pass (csrc/epilogue.hip)."""
     if not _nhwc(g):
@@ -75,10 +75,24 @@ def _bias_act_bwd(g, out, relu: bool, want_db: bool):
     dy = torch.empty_like(g) if relu else g
     db = torch.empty(C, dtype=torch.bfloat16, device=g.device) if want_db else None
     nparts = _lib.query("mx_bias_act_bwd_parts", M, C)
-    partial = torch.empty(nparts * C, dtype=torch.float32, device=g.device) if want_db else None
+    partial, flags = _colsum_partial(g.device, nparts, C, db, bdtype)
     _lib.call("mx_bias_act_bwd", _lib.ptr(g), _lib.ptr(out), _lib.ptr(dy), _lib.ptr(db), _lib.ptr(partial),
-              M, C, int(relu), 0, _lib.stream())
+              M, C, int(relu), flags, _lib.stream())
     return dy, db
+
+
+def _colsum_partial(device, nparts: int, C: int, db: Optional[torch.Tensor], bdtype=torch.bfloat16):
+    """(fp32 partial buffer, mx_bias_act_bwd flags): the bias gradient's column sums are
+    deferred to the step's batched flush (ops/convwg.py) when that is on, else reduced at once
+    (also when the caller casts db right away: a deferred db is only final after the flush)."""
+    if db is None:
+        return None, 0
+    if bdtype != torch.bfloat16:
+        return torch.empty(nparts * C, dtype=torch.float32, device=device), 0
+    reg = convwg.defer_colsum(device, nparts, C, db)
+    if reg is not None:
+        return reg, 2
+    return torch.empty(nparts * C, dtype=torch.float32, device=device), 0
 
 
 class BlockLink:
@@ -149,7 +163,7 @@ class ConvBiasActFn(torch.autograd.Function):
         # a premasked gradient already carries this conv's ReLU (the consumer's dgrad store
         # applied it): only the bias gradient, if any, is left -- column sums of g itself
         relu = ctx.relu and not (link is not None and link.premask.get(k))
-        dy, db = _bias_act_bwd(g, out, relu, want_db)
+        dy, db = _bias_act_bwd(g, out, relu, want_db, ctx.bdtype)
         if db is not None and db.dtype != ctx.bdtype:
             db = db.to(ctx.bdtype)
         dres = dy if ctx.has_res else None
@@ -295,7 +309,7 @@ class ConvTransposeBiasActFn(torch.autograd.Function):
     def backward(ctx, g):
         x, w, out = ctx.saved_tensors
         st = ctx.stride
-        dy, db = _bias_act_bwd(g, out, ctx.relu, ctx.needs_input_grad[2])
+        dy, db = _bias_act_bwd(g, out, ctx.relu, ctx.needs_input_grad[2], getattr(ctx, "bdtype", torch.bfloat16))
         if db is not None and db.dtype != ctx.bdtype:
             db = db.to(ctx.bdtype)
         dx = dw = None
