@@ -274,7 +274,32 @@ struct ConvFw {
   int splits, Cout;      // split-K (few output tiles): fp32 partials [splits][T][Cout] in part,
   float* part;           // then conv_fwd_reduce_kernel applies the epilogue
   uint32_t xbytes;       // size of x (the gather's buffer resource; < 2 GiB)
+  uint32_t* ticket;      // non-null: the last-arriving split of a tile sums the partials and
+                         // runs the epilogue itself (no reduction launch); [tiles], zero
 };
+
+// Split-K without a reduction launch: after publishing its fp32 partial tile, each split
+// takes a ticket; the last one of the tile (a counter it resets) reads the others' partials
+// back and runs the epilogue.  The partial stores are complete (vmcnt) and released at agent
+// scope before the ticket, the last arriver acquires after it -- as gemm.hip's split-K.
+// A per-convolution reduction launch cost ~5-7 us each, ~26 per 1-img Mask R-CNN step.
+__device__ __forceinline__ bool split_last_arriver(uint32_t* ticket, int tile, int splits) {
+  __shared__ uint32_t last_flag;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint32_t prev = __hip_atomic_fetch_add(ticket + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t is_last = prev == (uint32_t)(splits - 1);
+    if (is_last) {
+      __hip_atomic_store(ticket + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    last_flag = is_last;
+  }
+  __syncthreads();
+  return last_flag != 0u;
+}
 
 // FN = 4: 128 x 128 tiles (Cout % 128 == 0); FN = 2: 128 x 64 tiles for Cout % 128 == 64 (the
 // 64-channel res2 convolutions, which otherwise went to MIOpen)
@@ -435,7 +460,20 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
         for (int u = 0; u < FN; ++u) *reinterpret_cast<f32x4*>(dst + 16 * u) = acc[a][u];
       }
     }
-    return;
+    if (!cp.ticket || !split_last_arriver(cp.ticket, tile, cp.splits)) return;
+    // the tile's sum over the splits in split order (deterministic whichever arrives last)
+#pragma unroll
+    for (int a = 0; a < FM; ++a) {
+      const int p = m0 + 16 * (FM * wm + a) + i;
+      const float* src = cp.part + ((size_t)(p < cp.T ? p : 0)) * cp.Cout + colw + 4 * G;
+#pragma unroll
+      for (int u = 0; u < FN; ++u) {
+        f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int q = 0; q < cp.splits; ++q)
+          tot += q == sidx ? acc[a][u] : *reinterpret_cast<const f32x4*>(src + (size_t)q * cp.T * cp.Cout + 16 * u);
+        acc[a][u] = tot;
+      }
+    }
   }
   float bv[FN][4];
 #pragma unroll
@@ -564,6 +602,7 @@ struct ConvDg {
   int xs, xa, xb, XH, XW;
   uint32_t ybytes;       // size of dY (the gather's buffer resource; < 2 GiB)
   int bkt;               // K-step depth (output channels per step): 64 or 32 (host-side choice)
+  uint32_t* ticket;      // as ConvFw::ticket
 };
 
 // dX row of the launch's pixel p (identity unless a parity-class launch)
@@ -738,7 +777,19 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
         for (int u = 0; u < FN; ++u) *reinterpret_cast<f32x4*>(dst + 16 * u) = acc[a][u];
       }
     }
-    return;
+    if (!cp.ticket || !split_last_arriver(cp.ticket, tile, cp.splits)) return;
+#pragma unroll
+    for (int a = 0; a < FM; ++a) {
+      const int p = m0 + 16 * (FM * wm + a) + i;
+      const float* src = cp.part + ((size_t)(p < cp.T ? p : 0)) * cp.Cin + colw + 4 * G;
+#pragma unroll
+      for (int u = 0; u < FN; ++u) {
+        f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int q = 0; q < cp.splits; ++q)
+          tot += q == sidx ? acc[a][u] : *reinterpret_cast<const f32x4*>(src + (size_t)q * cp.T * cp.Cin + 16 * u);
+        acc[a][u] = tot;
+      }
+    }
   }
   float bz[FN][4];
 #pragma unroll
@@ -1046,7 +1097,7 @@ static void launch_dgrad(ConvDg cp, int splits, hipStream_t st) {
     hipLaunchKernelGGL((conv_dgrad_kernel<2, 32>), grid, dim3(256), 0, st, cp);
   else
     hipLaunchKernelGGL((conv_dgrad_kernel<2, 64>), grid, dim3(256), 0, st, cp);
-  if (cp.splits > 1) {
+  if (cp.splits > 1 && !cp.ticket) {
     const int64_t nvec = (int64_t)cp.T * (cp.Cin / 8);
     const unsigned rg = (unsigned)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
     hipLaunchKernelGGL(conv_dgrad_reduce_kernel, dim3(rg), dim3(256), 0, st, cp);
@@ -1112,6 +1163,7 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   cp.invIH = 1.f / (float)cp.IH;
   cp.bias = reinterpret_cast<const uint16_t*>(d[22]);
   cp.relu = (int)(d[23] & 1);
+  cp.ticket = reinterpret_cast<uint32_t*>(d[24]);   // (d has >= 25 entries: ops/convwg.py _DESC_T)
   const bool decomp = (d[23] >> 1) & 1;
   const int splits = d[20] > 1 ? (int)d[20] : 1;
   cp.part = reinterpret_cast<float*>(d[21]);
@@ -1175,6 +1227,7 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   cp.res_up = cp.res && d[21] != 0;
   cp.splits = d[22] > 1 ? (int)d[22] : 1;
   cp.part = reinterpret_cast<float*>(d[23]);
+  cp.ticket = reinterpret_cast<uint32_t*>(d[24]);
   cp.Cout = (int)d[18];
   const int64_t T = N * cp.OH * cp.OW;
   if (cp.res_up && ((cp.OH | cp.OW) & 1)) return (int)hipErrorInvalidValue;
@@ -1218,7 +1271,7 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
     if (Cout % 128 == 0) { MX_CF(2, 4, 64) } else { MX_CF(2, 2, 64) }
   }
 #undef MX_CF
-  if (cp.splits > 1) {
+  if (cp.splits > 1 && !cp.ticket) {
     const int64_t nvec = T * (Cout / 8);
     const unsigned rg = (unsigned)((nvec + 255) / 256 < 8192 ? (nvec + 255) / 256 : 8192);
     if (cp.res) {

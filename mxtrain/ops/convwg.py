@@ -29,7 +29,7 @@ FWD_MIN_TILES = 64
 TARGET_WGS = 512        # two 128 x 128 workgroups per CU on 256 CUs; >= 16 K-steps per slice since
 MIN_STEPS = 16          # the 32-bit gather made the slices cheaper than their fp32 partials
                         # (profiles/r4_s3/wgrad_split_ab*_{1,4}img.txt; before: r4_s2 sweep, 8)
-_DESC_T = ctypes.c_int64 * 24
+_DESC_T = ctypes.c_int64 * 32
 _WS: Dict[torch.device, Tuple[torch.Tensor, torch.Tensor]] = {}
 _RETIRED = []           # outgrown slabs stay alive: a captured hipGraph may still write them
 
@@ -66,6 +66,20 @@ def plan_splits(T: int, ntiles: int) -> int:
     steps = (T + bk - 1) // bk
     s = max(1, min(TARGET_WGS // max(ntiles, 1), steps // MIN_STEPS))
     return int(_lib.query("mx_conv_wgrad_splits", T, max(s, 1)))
+
+
+# split-K forward / input gradient: the last-arriving split of each tile sums the partials and
+# runs the epilogue (csrc/convwg.hip split_last_arriver) instead of a reduction launch
+SPLIT_IN_KERNEL = True
+_TICKETS: Dict[torch.device, torch.Tensor] = {}
+
+
+def _tickets(device) -> int:
+    """Per-tile arrival counters (uint32, zero between launches: the last arriver resets its own)."""
+    t = _TICKETS.get(device)
+    if t is None:
+        t = _TICKETS[device] = torch.zeros(1 << 16, dtype=torch.int32, device=device)
+    return t.data_ptr()
 
 
 def _workspace(device, slab_elems: int):
@@ -235,6 +249,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride, padding, dila
     d[:24] = [dy.data_ptr(), w.data_ptr(), zero.data_ptr(), dx.data_ptr(), _lib.ptr(add) or 0, _lib.ptr(mask) or 0,
               Cout, Cin, N, OH, OW, IH, IW, KH, KW, st, _sym(padding), _sym(dilation), Cout, Cin,
               splits, slab.data_ptr() if splits > 1 else 0, _lib.ptr(bias) or 0, int(relu) | (int(dec) << 1)]
+    d[24] = _tickets(dy.device) if (splits > 1 and SPLIT_IN_KERNEL) else 0
     _lib.call("mx_conv_dgrad", d, _lib.stream())
     return dx
 
@@ -336,6 +351,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool
     d[:24] = [x.data_ptr(), w.data_ptr(), zero.data_ptr(), y.data_ptr(), _lib.ptr(b) or 0,
               _lib.ptr(residual) or 0, Cin, Cout, N, OH, OW, IH, IW, KH, KW, st, pd, dl, Cout, Cin, int(relu),
               int(res_up), splits, slab.data_ptr() if splits > 1 else 0]
+    d[24] = _tickets(x.device) if (splits > 1 and SPLIT_IN_KERNEL) else 0
     _lib.call("mx_conv_fwd", d, _lib.stream())
     return y
 

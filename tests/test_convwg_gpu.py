@@ -384,3 +384,28 @@ def test_conv_transpose_bias_relu_matches_fp32():
     (F.conv_transpose2d(xr, wr, br, stride=2) * (y.detach().float().cpu() > 0)).backward(gy.float())
     for got, ref in ((xg.grad, xr.grad), (wg.grad, wr.grad), (bg.grad, br.grad)):
         _close(got, ref)
+
+
+@pytest.mark.parametrize("case", [(1, 512, 512, 25, 42, 3, 1, 1, 1), (1, 1024, 512, 50, 84, 1, 2, 0, 1),
+                                  (1, 256, 256, 25, 42, 3, 1, 1, 1)])
+def test_split_k_last_arriver_matches_reduce_launch(case, monkeypatch):
+    """Split-K forward / input gradient with the last-arriving split summing the partials in
+    the kernel (split_last_arriver) is bit-identical to the separate reduction launch (same
+    split-order fp32 sums, same epilogue)."""
+    from mxtrain.ops import convwg
+    N, Cin, Cout, H, W, k, stride, pad, dil = case
+    x, dy = _inputs(*case, seed=21)
+    g = torch.Generator().manual_seed(23)
+    w = (torch.randn(Cout, k, k, Cin, generator=g) * 0.1).to(torch.bfloat16).cuda().permute(0, 3, 1, 2)
+    b = (torch.randn(Cout, generator=g) * 0.1).to(torch.bfloat16).cuda()
+    outs = []
+    for in_kernel in (False, True):
+        monkeypatch.setattr(convwg, "SPLIT_IN_KERNEL", in_kernel)
+        y = convwg.conv_fwd(x, w, b, None, True, stride, pad, dil)
+        dx = convwg.conv_dgrad(dy, w, tuple(x.shape), stride, pad, dil) if convwg.dgrad_supported(
+            w, tuple(x.shape), stride, pad, dil) else None
+        torch.cuda.synchronize()
+        outs.append((y, dx))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if outs[0][1] is not None:
+        assert torch.equal(outs[0][1], outs[1][1])
