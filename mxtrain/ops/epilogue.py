@@ -124,10 +124,11 @@ class JoinLink(BlockLink):
     """FPN top-down join (models/maskrcnn.py FPN): merged level i has two consumers, its 3 x 3
     output conv (role "join_dx", key i) and the next lateral conv, which reads it
     nearest-upsampled as its residual (role "join_res", key i).  Whichever backward runs
-    first parks its gradient of the level in ``join[i]`` and returns None for it; the second
-    folds it in -- into its dgrad store (output conv) or into the 2 x 2 block sum of the
-    residual gradient (lateral conv) -- so autograd's separate add of the two gradients, and
-    the upsampling gradient's reduce + cast passes, disappear."""
+    first parks its gradient in ``join[i]`` (the output conv its dX, the lateral conv its
+    full-resolution residual gradient) and returns None for the level; the second returns
+    the level's whole gradient from one pass, fp32 2 x 2 block sum + dX, rounded once -- the
+    same arithmetic in either order (eager and captured steps must agree bit for bit) -- so
+    autograd's separate add and the upsampling gradient's reduce + cast passes disappear."""
 
     __slots__ = ("join",)
 
@@ -168,21 +169,21 @@ class ConvBiasActFn(torch.autograd.Function):
             db = db.to(ctx.bdtype)
         dres = dy if ctx.has_res else None
         if dres is not None and ctx.res_up:
-            if "join_res" in roles and k in link.join:     # the level's other gradient came first
+            if "join_res" in roles and k in link.join:     # the output conv's dX came first
                 dres = down2_sum(dres, link.join.pop(k))
+            elif "join_res" in roles:                      # park the full-resolution gradient
+                link.join[k] = dres
+                dres = None
             else:
                 dres = down2_sum(dres)
-                if "join_res" in roles:
-                    link.join[k] = dres
-                    dres = None
         if dres is not None and "stash_res" in roles and link.taker and ctx.needs_input_grad[3]:
             link.stash.append(dres)
             dres = None
         add = link.stash.pop() if "take_res" in roles and link.stash else None
-        join_first = False
-        if "join_dx" in roles:
+        join_first = join_last = None
+        if "join_dx" in roles:   # (the same sum, fp32 2 x 2 block + bf16 dX, whichever comes first)
             if k in link.join:
-                add = link.join.pop(k)
+                join_last = link.join.pop(k)
             else:
                 join_first = True
         mask = x if ("mask_in" in roles or "mask_prev" in roles) else None
@@ -200,6 +201,8 @@ class ConvBiasActFn(torch.autograd.Function):
             if join_first:
                 link.join[k] = dx
                 dx = None
+            elif join_last is not None:
+                dx = down2_sum(join_last, dx)
         elif add is not None:
             raise RuntimeError("BlockLink: residual gradient stashed for a conv without an input gradient")
         if ctx.needs_input_grad[1]:

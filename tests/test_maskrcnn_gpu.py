@@ -27,10 +27,12 @@ def _sgd(model):
 
 
 @pytest.mark.gpu
-def test_graphed_step_matches_eager(tmp_path):
+@pytest.mark.parametrize("join", [True, False])
+def test_graphed_step_matches_eager(tmp_path, join, monkeypatch):
     from mxtrain.data.coco import COCODetection, DetectionDataset, collate
     from mxtrain.data.coco_synth import write_split
-    from mxtrain.models.maskrcnn import MaskRCNN, MaskRCNNConfig
+    from mxtrain.models.maskrcnn import FPN, MaskRCNN, MaskRCNNConfig
+    monkeypatch.setattr(FPN, "join_backward", join)
     from mxtrain.workloads.maskrcnn.graphed import GraphedTrainStep
     write_split(str(tmp_path), "train2017", 24, 0, 1)
     ds = DetectionDataset(COCODetection(str(tmp_path), "coco_train2017"), 256, 384, mask_format="crops")
