@@ -27,7 +27,7 @@ def _sgd(model):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("join", [True, False])
+@pytest.mark.parametrize("join", [False, True])
 def test_graphed_step_matches_eager(tmp_path, join, monkeypatch):
     from mxtrain.data.coco import COCODetection, DetectionDataset, collate
     from mxtrain.data.coco_synth import write_split
