@@ -47,6 +47,8 @@ struct ConvWg {
   int splits, nk;        // pixel slices, 64-row K-steps per slice
   float invOW, invOH, beta;
   uint32_t xbytes, ybytes;   // sizes of x and dY (buffer resources; < 2 GiB)
+  int Cout;              // < the tiles' rows for the narrow 1x1 heads: dY columns past it read
+                         // zeros, dW rows past it are not written
 };
 
 __device__ __forceinline__ void divmod(int p, int d, float inv, int& q, int& r) {
@@ -96,8 +98,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
   // and input taps outside the image read zeros through out-of-range buffer offsets.
   const i32x4_t yres = buffer_rsrc(cp.dy, cp.ybytes), xres = buffer_rsrc(cp.x, cp.xbytes);
   uint32_t ya[PA];
+  bool aok[PA];   // this lane's dY column exists (false only past a narrow Cout)
 #pragma unroll
-  for (int j = 0; j < PA; ++j) ya[j] = (uint32_t)((p0 + kA[j]) * cp.ldy + cA[j]) * 2u;
+  for (int j = 0; j < PA; ++j) {
+    ya[j] = (uint32_t)((p0 + kA[j]) * cp.ldy + cA[j]) * 2u;
+    aok[j] = cA[j] < cp.Cout;
+  }
   const uint32_t ystep = (uint32_t)(BKT * cp.ldy) * 2u;
   // B: pixel p = p0 + it BKT + kB[j] -> (oh s, ow s) and xo = ((n IH + oh s) IW + ow s) ldx
   int bp[PB], bohs[PB], bows[PB], bxo[PB];
@@ -170,7 +176,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
     const uint32_t b0 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + PA * wave * 1024);
     const uint32_t b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
 #pragma unroll
-    for (int j = 0; j < PA; ++j) dma16_buf(yres, ya[j], b0 + j * 1024);
+    for (int j = 0; j < PA; ++j) dma16_buf(yres, aok[j] ? ya[j] : kOOB, b0 + j * 1024);
 #pragma unroll
     for (int j = 0; j < PB; ++j) dma16_buf(xres, boffB(j), b1 + j * 1024);
     advance();
@@ -225,12 +231,14 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
 
   // ---- epilogue: lane holds dW[m0 + 16 a + 4 G + e][tap][n0 + 16 u + i] of its wave's block
   const size_t ldc = (size_t)cp.taps * cp.Cin;
-  uint16_t* C = cp.dw + (size_t)(m0 + 16 * FM * wm + 4 * G) * ldc + (size_t)tap * cp.Cin + n0 + 16 * FN * wn + i;
+  const int mrow = m0 + 16 * FM * wm + 4 * G;
+  uint16_t* C = cp.dw + (size_t)mrow * ldc + (size_t)tap * cp.Cin + n0 + 16 * FN * wn + i;
   const bool acc_in = cp.beta != 0.f;
 #pragma unroll
   for (int a = 0; a < FM; ++a)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
+      if (mrow + 16 * a + e >= cp.Cout) continue;
       uint16_t* row = C + (size_t)(16 * a + e) * ldc;
 #pragma unroll
       for (int u = 0; u < FN; ++u) {
@@ -363,12 +371,16 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
     asm volatile("" : "+v"(aoff[j]));   // keep the per-lane offset whole (no per-step re-multiply)
   }
   uint32_t boff[PB];
+  bool bok[PB];   // the weight row exists (false only past a narrow Cout)
 #pragma unroll
   for (int j = 0; j < PB; ++j) {
     const int brow = n0 + (PB * wave + j) * (1024 / R) + lane / (R / 16);
+    bok[j] = brow < cp.Cout;
     boff[j] = (uint32_t)(brow * (int)ldw + 8 * ((lane % (R / 16)) ^ row_swz<R>(brow))) * 2u;
   }
   const i32x4_t xres = buffer_rsrc(cp.x, cp.xbytes);
+  const bool narrow = cp.Cout % 64 != 0;   // (the 1x1 heads: weight rows past Cout read zeros)
+  const i32x4_t wres = buffer_rsrc(cp.w, (uint32_t)(cp.Cout * ldw * 2));
   const int G = lane >> 4, i = lane & 15;
   const int wm = wave / WN, wn = wave % WN;
   const int offA = (16 * FM * wm + i) * R, offB = (16 * FN * wn + i) * R;
@@ -404,9 +416,15 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
       const bool in = (amask[j] >> tap) & 1u;
       dma16_buf(xres, in ? (uint32_t)(aoff[j] + delta) * 2u : kOOB, b0 + j * 1024);
     }
-    const uint16_t* wb = cp.w + (size_t)tap * cp.Cin + ci0;
+    if (narrow) {
+      const uint32_t wo = (uint32_t)((size_t)tap * cp.Cin + ci0) * 2u;
 #pragma unroll
-    for (int j = 0; j < PB; ++j) dma16_sbase(wb, boff[j], b1 + j * 1024);
+      for (int j = 0; j < PB; ++j) dma16_buf(wres, bok[j] ? wo + boff[j] : kOOB, b1 + j * 1024);
+    } else {
+      const uint16_t* wb = cp.w + (size_t)tap * cp.Cin + ci0;
+#pragma unroll
+      for (int j = 0; j < PB; ++j) dma16_sbase(wb, boff[j], b1 + j * 1024);
+    }
   };
 
   // NSLOT-deep LDS-DMA ring, counted waits (the input gradient's scheme): with NSLOT > 2 the
@@ -478,7 +496,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
   float bv[FN][4];
 #pragma unroll
   for (int u = 0; u < FN; ++u) {
-    if (cp.bias) {
+    if (cp.bias && colw + 16 * u + 4 * G < cp.Cout) {
       const uint2 b2 = *reinterpret_cast<const uint2*>(cp.bias + colw + 16 * u + 4 * G);
       bv[u][0] = lo_bf(b2.x); bv[u][1] = hi_bf(b2.x); bv[u][2] = lo_bf(b2.y); bv[u][3] = hi_bf(b2.y);
     } else {
@@ -500,7 +518,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
           divmod(q, cp.OH, cp.invOH, n, oh);
           rr = ((size_t)(n * (cp.OH >> 1) + (oh >> 1)) * (cp.OW >> 1) + (ow >> 1)) * cp.ldy;
         }
-        const uint4 rv = *reinterpret_cast<const uint4*>(cp.res + rr + colw + 32 * up + 8 * G);
+        const uint4 rv = colw + 32 * up + 8 * G < cp.Cout ? *reinterpret_cast<const uint4*>(cp.res + rr + colw + 32 * up + 8 * G)
+                                                         : make_uint4(0u, 0u, 0u, 0u);
         h[0][0] = rv.x; h[0][1] = rv.y; h[1][0] = rv.z; h[1][1] = rv.w;
         undeal(h[0][0], h[0][1], h[1][0], h[1][1]);
       }
@@ -522,7 +541,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
         c[hlf][1] = pack2(v[2], v[3]);
       }
       deal(c[0][0], c[0][1], c[1][0], c[1][1]);
-      if (p < cp.T)
+      if (p < cp.T && colw + 32 * up + 8 * G < cp.Cout)
         *reinterpret_cast<uint4*>(cp.y + pr + colw + 32 * up + 8 * G) = make_uint4(c[0][0], c[0][1], c[1][0], c[1][1]);
     }
   }
@@ -595,6 +614,7 @@ struct ConvDg {
   int splits;            // split-K (few input-pixel tiles): fp32 partials [splits][T][Cin] in
   float* part;           // part, reduced with the add / mask epilogue by conv_dgrad_reduce_kernel
   int ldw;               // weight row pitch (elements per output channel: taps * Cin)
+  int Cout;              // output channels (a multiple of 8; K-steps past it read zeros)
   const uint16_t* bias;  // [Cin] or null: + bias (the transposed convolution's forward)
   int relu;              // max(., 0) after bias / add, before the mask
   // parity class (xs > 0): this launch's pixels are the dX pixels (i * xs + xa, j * xs + xb)
@@ -638,7 +658,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
   // output pixel exists (in the image, on the stride grid); tap (r, c) then reads at the
   // wave-uniform delta -((r dil / s) OW + c dil / s) ldy (exact on the grid: ih + pad and
   // r dil have equal residues mod s there), padding through out-of-range buffer offsets.
-  int aoff[PA];
+  int aoff[PA], acol[PA];   // acol: the lane's dY column within a K-step (narrow Cout check)
   uint32_t amask[PA];
 #pragma unroll
   for (int j = 0; j < PA; ++j) {
@@ -650,6 +670,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
     divmod(q, cp.IH, cp.invIH, n, ih);
     const int hh = ih + cp.pad, ww = iw + cp.pad, st = cp.stride, KHt = cp.taps / cp.KW;
     const int sw = 8 * ((lane % (RA / 16)) ^ row_swz<RA>(row));
+    acol[j] = sw;
     uint32_t m = 0u;
     if (st == 1) {   // (wave-uniform) no per-lane divisions on the common path
       aoff[j] = ((n * cp.OH + hh) * cp.OW + ww) * cp.ldy + sw;
@@ -673,12 +694,17 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
     asm volatile("" : "+v"(aoff[j]));   // keep the per-lane offset whole
   }
   uint32_t boff[PB];
+  int bkrow[PB];
 #pragma unroll
   for (int j = 0; j < PB; ++j) {
     const int kB = (PB * wave + j) * (1024 / RB) + lane / (RB / 16);
+    bkrow[j] = kB;
     boff[j] = (uint32_t)(kB * (int)ldw + n0 + 8 * pchunk(kB, lane % (RB / 16))) * 2u;
   }
   const i32x4_t yres = buffer_rsrc(cp.dy, cp.ybytes);
+  // narrow Cout (the 1x1 heads, Cout % BKT != 0): dY columns and weight rows past Cout read zeros
+  const bool narrow = cp.Cout % BKT != 0;
+  const i32x4_t wres = buffer_rsrc(cp.w, (uint32_t)(cp.Cout * cp.ldw * 2));
 
   const int G = lane >> 4, i = lane & 15;
   const int wm = wave / WN, wn = wave % WN;
@@ -722,12 +748,18 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
     const uint32_t b1 = __builtin_amdgcn_readfirstlane(lds0 + slot * SLOT + IA + PB * wave * 1024);
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
-      const bool in = (amask[j] >> tap) & 1u;
+      const bool in = ((amask[j] >> tap) & 1u) && (!narrow || co0 + acol[j] < cp.Cout);
       dma16_buf(yres, in ? (uint32_t)(aoff[j] + delta) * 2u : kOOB, b0 + j * 1024);
     }
-    const uint16_t* wb = cp.w + (size_t)co0 * ldw + (size_t)tap * cp.Cin;
+    if (narrow) {
+      const uint32_t wo = (uint32_t)((size_t)co0 * ldw + (size_t)tap * cp.Cin) * 2u;
 #pragma unroll
-    for (int j = 0; j < PB; ++j) dma16_sbase(wb, boff[j], b1 + j * 1024);
+      for (int j = 0; j < PB; ++j) dma16_buf(wres, co0 + bkrow[j] < cp.Cout ? wo + boff[j] : kOOB, b1 + j * 1024);
+    } else {
+      const uint16_t* wb = cp.w + (size_t)co0 * ldw + (size_t)tap * cp.Cin;
+#pragma unroll
+      for (int j = 0; j < PB; ++j) dma16_sbase(wb, boff[j], b1 + j * 1024);
+    }
   };
 
 #pragma unroll
@@ -844,8 +876,8 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
 // summed over the slices in slice order (deterministic), written to dW with the main
 // kernel's epilogue mapping (4 waves of 64 x 64: WM = WN = 2, FM = FN = 4).
 __device__ __forceinline__ void wgrad_reduce_one(const float* slab, uint16_t* dw, int ntiles, int splits,
-                                                 int tiles_tap, int tiles_n, int taps, int Cin, float beta,
-                                                 int gid) {
+                                                 int tiles_tap, int tiles_n, int taps, int Cin, int Cout,
+                                                 float beta, int gid) {
   constexpr int FM = 4, FN = 4, WN = 2, NR = FM * FN, NT = kNT;
   const int tid = gid % NT, rg = (gid / NT) % NR, t = gid / (NT * NR);   // gid < ntiles * NR * NT
   if (t >= ntiles) return;
@@ -872,8 +904,10 @@ __device__ __forceinline__ void wgrad_reduce_one(const float* slab, uint16_t* dw
   uint16_t* C = dw + (size_t)(m0 + 16 * FM * wm + 4 * G + 16 * a) * ldc + (size_t)tap * Cin + n0 +
                 16 * FN * wn + 16 * u + i;
   const float e4[4] = {v.x, v.y, v.z, v.w};
+  const int mrow = m0 + 16 * FM * wm + 4 * G + 16 * a;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
+    if (mrow + e >= Cout) continue;
     float o = e4[e];
     if (beta != 0.f) o += beta * bf2f(C[(size_t)e * ldc]);
     C[(size_t)e * ldc] = f2bf(o);
@@ -881,8 +915,8 @@ __device__ __forceinline__ void wgrad_reduce_one(const float* slab, uint16_t* dw
 }
 
 __global__ __launch_bounds__(64) void conv_wgrad_reduce_kernel(const ConvWg cp) {
-  wgrad_reduce_one(cp.slab, cp.dw, cp.ntiles, cp.splits, cp.tiles_tap, cp.tiles_n, cp.taps, cp.Cin, cp.beta,
-                   blockIdx.x * 64 + threadIdx.x);
+  wgrad_reduce_one(cp.slab, cp.dw, cp.ntiles, cp.splits, cp.tiles_tap, cp.tiles_n, cp.taps, cp.Cin, cp.Cout,
+                   cp.beta, blockIdx.x * 64 + threadIdx.x);
 }
 
 // The split-K reductions of up to kWgJobs weight gradients in ONE launch (the deferred
@@ -892,7 +926,7 @@ constexpr int kWgJobs = 40;
 struct WgJob {
   const float* slab;
   uint16_t* dw;
-  int ntiles, splits, tiles_tap, tiles_n, taps, Cin, b0;
+  int ntiles, splits, tiles_tap, tiles_n, taps, Cin, Cout, b0;
   float beta;
 };
 struct WgJobs {
@@ -903,7 +937,7 @@ __global__ __launch_bounds__(64) void conv_wgrad_reduce_batched_kernel(const WgJ
   int q = 0;
   while (q + 1 < njobs && js.j[q + 1].b0 <= b) ++q;   // (wave-uniform)
   const WgJob& J = js.j[q];
-  wgrad_reduce_one(J.slab, J.dw, J.ntiles, J.splits, J.tiles_tap, J.tiles_n, J.taps, J.Cin, J.beta,
+  wgrad_reduce_one(J.slab, J.dw, J.ntiles, J.splits, J.tiles_tap, J.tiles_n, J.taps, J.Cin, J.Cout, J.beta,
                    (b - J.b0) * 64 + threadIdx.x);
 }
 
@@ -941,8 +975,10 @@ MX_EXPORT int mx_conv_wgrad(const int64_t* d, float beta, int splits, void* stre
   if (N <= 0 || cp.OH <= 0 || cp.OW <= 0 || KH <= 0 || cp.KW <= 0 || cp.stride <= 0 || cp.dil <= 0 ||
       cp.pad < 0 || T >= (1 << 23) || N * cp.IH * cp.IW >= ((int64_t)1 << 31))
     return (int)hipErrorInvalidValue;
-  if (Cout % kBM || cp.Cin % kBN || cp.ldy < Cout || cp.ldx < cp.Cin || (cp.ldy & 7) || (cp.ldx & 7))
+  // Cout: a multiple of 128, or of 8 (the narrow 1x1 heads: 128-row tiles, zero-padded)
+  if ((Cout % kBM && Cout % 8) || cp.Cin % kBN || cp.ldy < Cout || cp.ldx < cp.Cin || (cp.ldy & 7) || (cp.ldx & 7))
     return (int)hipErrorInvalidValue;
+  cp.Cout = Cout;
   if ((d[0] | d[1] | d[2]) & 15) return (int)hipErrorInvalidValue;
   if (splits < 1 || (splits > 1 && cp.slab == nullptr)) return (int)hipErrorInvalidValue;
   cp.T = (int)T;
@@ -952,7 +988,7 @@ MX_EXPORT int mx_conv_wgrad(const int64_t* d, float beta, int splits, void* stre
   cp.xbytes = (uint32_t)xbytes;
   cp.ybytes = (uint32_t)ybytes;
   cp.tiles_n = cp.Cin / kBN;
-  cp.tiles_tap = (Cout / kBM) * cp.tiles_n;
+  cp.tiles_tap = ((Cout + kBM - 1) / kBM) * cp.tiles_n;
   cp.ntiles = cp.taps * cp.tiles_tap;
   const int steps = (int)((T + kBK - 1) / kBK);
   if (splits > steps) splits = steps;
@@ -979,7 +1015,7 @@ MX_EXPORT int mx_conv_wgrad(const int64_t* d, float beta, int splits, void* stre
 }
 
 // Deferred split-K reductions of several mx_conv_wgrad launches (flag bit 0 of d[5]): jobs =
-// host int64 [njobs][9] {slab, dw, ntiles, splits, tiles_tap, tiles_n, taps, Cin, beta != 0},
+// host int64 [njobs][10] {slab, dw, ntiles, splits, tiles_tap, tiles_n, taps, Cin, beta != 0, Cout},
 // launched kWgJobs at a time.
 MX_EXPORT int mx_conv_wgrad_reduce_batched(const int64_t* jobs, int njobs, void* stream) {
   hipStream_t st = (hipStream_t)stream;
@@ -988,12 +1024,12 @@ MX_EXPORT int mx_conv_wgrad_reduce_batched(const int64_t* jobs, int njobs, void*
     WgJobs js{};
     int blocks = 0;
     for (int q = 0; q < nj; ++q) {
-      const int64_t* r = jobs + (size_t)(j0 + q) * 9;
+      const int64_t* r = jobs + (size_t)(j0 + q) * 10;
       WgJob& J = js.j[q];
       J.slab = reinterpret_cast<const float*>(r[0]);
       J.dw = reinterpret_cast<uint16_t*>(r[1]);
       J.ntiles = (int)r[2]; J.splits = (int)r[3]; J.tiles_tap = (int)r[4]; J.tiles_n = (int)r[5];
-      J.taps = (int)r[6]; J.Cin = (int)r[7]; J.beta = r[8] ? 1.f : 0.f;
+      J.taps = (int)r[6]; J.Cin = (int)r[7]; J.beta = r[8] ? 1.f : 0.f; J.Cout = (int)r[9];
       if (J.splits < 2 || J.ntiles <= 0 || !J.slab || !J.dw) return (int)hipErrorInvalidValue;
       J.b0 = blocks;
       blocks += J.ntiles * 16 * kNT / 64;
@@ -1141,7 +1177,7 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   if (N <= 0 || cp.IH <= 0 || cp.IW <= 0 || cp.OH <= 0 || cp.OW <= 0 || KH <= 0 || cp.KW <= 0 || cp.stride <= 0 ||
       cp.dil <= 0 || cp.pad < 0 || T >= (1 << 23) || N * cp.OH * cp.OW >= ((int64_t)1 << 31))
     return (int)hipErrorInvalidValue;
-  if (Cout % 64 || cp.Cin % 128 || cp.ldy < Cout || cp.ldx < cp.Cin || (cp.ldy & 7) || (cp.ldx & 7))
+  if (Cout % 8 || cp.Cin % 128 || cp.ldy < Cout || cp.ldx < cp.Cin || (cp.ldy & 7) || (cp.ldx & 7))
     return (int)hipErrorInvalidValue;
   if ((d[0] | d[1] | d[2] | d[3] | d[4] | d[5]) & 15) return (int)hipErrorInvalidValue;
   cp.T = (int)T;
@@ -1156,7 +1192,8 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   // (1x1, Cout 1024) are 3-23 % slower with them (profiles/r5_s1/conv_ab_ring_3.txt)
   const bool narrow = Cout <= 128 || (cp.taps == 1 && Cout <= 512);
   cp.bkt = (g_conv_dgrad_bk32 == 1 || (g_conv_dgrad_bk32 == 2 && narrow)) ? 32 : 64;
-  cp.cob = Cout / cp.bkt;
+  cp.cob = (Cout + cp.bkt - 1) / cp.bkt;
+  cp.Cout = Cout;
   cp.nk = cp.taps * cp.cob;
   cp.tiles_n = cp.Cin / 128;
   cp.invIW = 1.f / (float)cp.IW;
@@ -1234,7 +1271,7 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   if (N <= 0 || cp.IH <= 0 || cp.IW <= 0 || cp.OH <= 0 || cp.OW <= 0 || KH <= 0 || cp.KW <= 0 || cp.stride <= 0 ||
       cp.dil <= 0 || cp.pad < 0 || T >= (1 << 23) || N * cp.IH * cp.IW >= ((int64_t)1 << 31))
     return (int)hipErrorInvalidValue;
-  if (Cout % 64 || cp.Cin % 64 || cp.ldx < cp.Cin || cp.ldy < Cout || (cp.ldx & 7) || (cp.ldy & 7))
+  if (Cout % 8 || cp.Cin % 64 || cp.ldx < cp.Cin || cp.ldy < Cout || (cp.ldx & 7) || (cp.ldy & 7))
     return (int)hipErrorInvalidValue;
   if ((d[0] | d[1] | d[2]) & 15) return (int)hipErrorInvalidValue;
   cp.T = (int)T;
@@ -1248,7 +1285,8 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   const int bkt = bk32 && cp.Cin % 32 == 0 ? 32 : 64;
   cp.cib = cp.Cin / bkt;
   cp.nk = cp.taps * cp.cib;
-  cp.tiles_n = Cout % 128 == 0 ? Cout / 128 : Cout / 64;
+  cp.tiles_n = Cout % 128 == 0 ? Cout / 128 : (Cout + 63) / 64;   // (narrow Cout: zero-padded tiles)
+  if (Cout % 64 && cp.splits > 1) return (int)hipErrorInvalidValue;   // partial planes assume whole tiles
   cp.invOW = 1.f / (float)cp.OW;
   cp.invOH = 1.f / (float)cp.OH;
   if (cp.splits > cp.nk) cp.splits = cp.nk;

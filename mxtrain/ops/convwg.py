@@ -119,7 +119,7 @@ def defer_flush(keep_on: bool = False):
     """Launch the pending reductions; deferral stays on only if ``keep_on`` (more gradient
     buckets of this backward still to come)."""
     _DEF["on"] = _DEF["on"] and keep_on
-    for key, fn, width in (("jobs", "mx_conv_wgrad_reduce_batched", 9), ("cjobs", "mx_colsum_jobs", 5)):
+    for key, fn, width in (("jobs", "mx_conv_wgrad_reduce_batched", 10), ("cjobs", "mx_colsum_jobs", 5)):
         jobs = _DEF[key]
         if jobs:
             flat = [v for j in jobs for v in j]
@@ -192,7 +192,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dila
         out = torch.empty((Cout, KH, KW, Cin), dtype=torch.bfloat16, device=x.device).permute(0, 3, 1, 2)
     assert tuple(out.shape) == (Cout, Cin, KH, KW) and out.stride(1) == 1 and out.stride(0) == KH * KW * Cin
     T = N * OH * OW
-    ntiles = KH * KW * (Cout // 128) * (Cin // 128)
+    ntiles = KH * KW * (-(-Cout // 128)) * (Cin // 128)   # (a narrow Cout: one zero-padded row tile)
     if splits <= 0:
         splits = plan_splits(T, ntiles)
     splits = int(_lib.query("mx_conv_wgrad_splits", T, splits))
@@ -203,8 +203,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dila
         reg = _defer_slab(x.device, ntiles * splits * 128 * 128)
         if reg is not None:
             slab, defer = reg, 1
-            _DEF["jobs"].append([reg.data_ptr(), out.data_ptr(), ntiles, splits, (Cout // 128) * (Cin // 128),
-                                 Cin // 128, KH * KW, Cin, 1 if beta else 0])
+            _DEF["jobs"].append([reg.data_ptr(), out.data_ptr(), ntiles, splits, (-(-Cout // 128)) * (Cin // 128),
+                                 Cin // 128, KH * KW, Cin, 1 if beta else 0, Cout])
     d = _DESC_T()
     d[:20] = [dy.data_ptr(), x.data_ptr(), zero.data_ptr(), out.data_ptr(), slab.data_ptr(), defer,
             Cout, Cin, N, OH, OW, IH, IW, KH, KW, _sym(stride), _sym(padding), _sym(dilation), Cout, Cin]
@@ -238,7 +238,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride, padding, dila
     dec = decomposed(KH, KW, stride, padding, dilation)
     st = _sym(stride)
     T = N * (-(-IH // st)) * (-(-IW // st)) if dec else N * IH * IW   # largest launch's pixels
-    splits = dgrad_splits((T + 127) // 128 * (Cin // 128), (1 if dec else KH * KW) * Cout // 64)
+    splits = dgrad_splits((T + 127) // 128 * (Cin // 128), (1 if dec else KH * KW) * -(-Cout // 64))
     slab, zero = _workspace(dy.device, splits * T * Cin if splits > 1 else 1)
     assert bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == Cin
                             and bias.data_ptr() % 8 == 0)
@@ -277,8 +277,9 @@ def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, paddi
     """The implicit-GEMM forward: NHWC bf16, Cout a multiple of 64, Cin of 64, and at least
     FWD_MIN_TILES output tiles (smaller convs stay on MIOpen).  ``res_up``: the
     residual is at half the output resolution, added nearest-upsampled."""
+    # (Cout a multiple of 8: the narrow 1x1 heads -- RPN 16, mask logits 80 -- run zero-padded tiles)
     if not (FWD and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
-            and w.dim() == 4 and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and x.shape[1] == w.shape[1]
+            and w.dim() == 4 and w.shape[0] % 8 == 0 and w.shape[1] % 64 == 0 and x.shape[1] == w.shape[1]
             and _cl(x) and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
             and None not in (_sym(stride), _sym(padding), _sym(dilation))):
         return False
@@ -300,7 +301,9 @@ def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, paddi
         return False
     # 128 x 128 tiles, or 128 x 64 when Cout is an odd multiple of 64 (csrc/convwg.hip); fewer
     # than FWD_MIN_TILES tiles split the reduction (fwd_splits)
-    tiles = (N * OH * OW + 127) // 128 * (w.shape[0] // (128 if w.shape[0] % 128 == 0 else 64))
+    tiles = (N * OH * OW + 127) // 128 * (w.shape[0] // 128 if w.shape[0] % 128 == 0 else -(-w.shape[0] // 64))
+    if w.shape[0] % 64:   # narrow Cout: no split-K (whole-tile partial planes)
+        return tiles >= FWD_MIN_TILES
     return tiles >= FWD_MIN_TILES or fwd_splits(tiles, w.shape[2] * w.shape[3] * w.shape[1] // 64) > 1
 
 
@@ -345,7 +348,8 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool
         w = w.contiguous(memory_format=torch.channels_last)
     y = torch.empty((N, OH, OW, Cout), dtype=torch.bfloat16, device=x.device).permute(0, 3, 1, 2)
     T = N * OH * OW
-    splits = fwd_splits((T + 127) // 128 * (Cout // (128 if Cout % 128 == 0 else 64)), KH * KW * Cin // 64)
+    splits = 1 if Cout % 64 else fwd_splits((T + 127) // 128 * (Cout // (128 if Cout % 128 == 0 else 64)),
+                                             KH * KW * Cin // 64)
     slab, zero = _workspace(x.device, splits * T * Cout if splits > 1 else 1)
     d = _DESC_T()
     d[:24] = [x.data_ptr(), w.data_ptr(), zero.data_ptr(), y.data_ptr(), _lib.ptr(b) or 0,
@@ -364,7 +368,7 @@ def dgrad_supported(w: torch.Tensor, x_shape, stride, padding=0, dilation=1) -> 
     65 vs 40 us), and stride 1, a stride-decomposed filter (1x1 stride 2: one GEMM over the
     pixels of one parity class) or at most 256 output channels (a strided 3x3's gathered dY
     has 3 of 4 rows zero, which costs MFMA time per K-step)."""
-    if not (DGRAD and w.shape[0] % 64 == 0 and w.shape[1] % 128 == 0 and w.data_ptr() % 16 == 0):
+    if not (DGRAD and w.shape[0] % 8 == 0 and w.shape[1] % 128 == 0 and w.data_ptr() % 16 == 0):
         return False
     N, Cin, IH, IW = x_shape
     st = _sym(stride)
@@ -377,9 +381,9 @@ def dgrad_supported(w: torch.Tensor, x_shape, stride, padding=0, dilation=1) -> 
         return False
     if decomposed(w.shape[2], w.shape[3], stride, padding, dilation):
         tiles = (N * (-(-IH // st)) * (-(-IW // st)) + 127) // 128 * (Cin // 128)
-        return tiles >= DGRAD_MIN_TILES or dgrad_splits(tiles, w.shape[0] // 64) > 1
+        return tiles >= DGRAD_MIN_TILES or dgrad_splits(tiles, -(-w.shape[0] // 64)) > 1
     tiles = (N * IH * IW + 127) // 128 * (Cin // 128)
-    nk = w.shape[2] * w.shape[3] * w.shape[0] // 64
+    nk = -(-(w.shape[2] * w.shape[3] * w.shape[0]) // 64)
     return ((tiles >= DGRAD_MIN_TILES or dgrad_splits(tiles, nk) > 1)
             and (st == 1 or w.shape[0] <= 256))
 

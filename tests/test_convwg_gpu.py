@@ -4,6 +4,7 @@ plain PyTorch fp32 weight gradient of the same convolution (CPU), for 1x1 / stri
 fixed and planned split counts and accumulation into an existing gradient."""
 import pytest
 import torch
+import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
@@ -409,3 +410,42 @@ def test_split_k_last_arriver_matches_reduce_launch(case, monkeypatch):
     assert torch.equal(outs[0][0], outs[1][0])
     if outs[0][1] is not None:
         assert torch.equal(outs[0][1], outs[1][1])
+
+
+NARROW = [(2, 256, 16, 40, 52, 1, 1, 0, 1), (48, 256, 80, 28, 28, 1, 1, 0, 1), (1, 128, 24, 33, 17, 1, 1, 0, 1)]
+
+
+@pytest.mark.parametrize("case", NARROW)
+def test_narrow_cout_convs_match_fp32(case):
+    """The narrow 1x1 heads (RPN objectness + box: 16 channels, mask logits: 80) on the
+    implicit-GEMM kernels with zero-padded tiles: forward (+ bias), input gradient and weight
+    gradient (split and unsplit) against fp32 PyTorch, and the fused autograd path."""
+    from mxtrain.ops import convwg
+    from mxtrain.ops.epilogue import conv_bias_act
+    N, Cin, Cout, H, W, k, stride, pad, dil = case
+    x, dy = _inputs(*case, seed=31)
+    g = torch.Generator().manual_seed(37)
+    w = (torch.randn(Cout, k, k, Cin, generator=g) * 0.1).to(torch.bfloat16).cuda().permute(0, 3, 1, 2)
+    b = (torch.randn(Cout, generator=g) * 0.1).to(torch.bfloat16).cuda()
+    assert convwg.fwd_supported(x, w, b, None, stride, pad, dil)
+    y = convwg.conv_fwd(x, w, b, None, False, stride, pad, dil)
+    yr = F.conv2d(x.float().cpu(), w.float().cpu(), b.float().cpu(), stride, pad, dil)
+    _close(y, yr)
+    assert convwg.dgrad_supported(w, tuple(x.shape), stride, pad, dil)
+    _close(convwg.conv_dgrad(dy, w, tuple(x.shape), stride, pad, dil), _ref_dx(dy, w, tuple(x.shape), stride, pad, dil))
+    for splits in (1, 4, 0):
+        _close(convwg.conv_wgrad(dy, x, (Cout, Cin, k, k), stride, pad, dil, splits=splits),
+               _ref(dy, x, (Cout, Cin, k, k), stride, pad, dil))
+    xg = x.detach().clone().requires_grad_(True)
+    wg = w.detach().clone().requires_grad_(True)
+    bg = b.detach().clone().requires_grad_(True)
+    out = conv_bias_act(xg, wg, bg, stride, pad, dil)
+    assert "ConvBiasAct" in type(out.grad_fn).__name__, type(out.grad_fn)
+    (out.float() * dy.float()).sum().backward()
+    xr = x.float().cpu().requires_grad_(True)
+    wr = w.float().cpu().requires_grad_(True)
+    br = b.float().cpu().requires_grad_(True)
+    (F.conv2d(xr, wr, br, stride, pad, dil) * dy.float().cpu()).sum().backward()
+    _close(xg.grad, xr.grad)
+    _close(wg.grad, wr.grad)
+    _close(bg.grad, br.grad)
