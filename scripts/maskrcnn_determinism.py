@@ -35,20 +35,32 @@ def main():
         mb = copy.deepcopy(ma)
         mw = copy.deepcopy(ma)   # warm-up copy: MIOpen's first call of a shape may run another solver
         hist = {}
+        plain = os.environ.get("PLAIN") == "1"     # torch SGD + clip instead of FlatMaster
+        side = torch.cuda.Stream()
         for tag, m in (("warm", mw), ("a", ma), ("b", mb)):
             ps = [p for p in m.parameters() if p.requires_grad]
             opt = torch.optim.SGD(ps, lr=0.01, momentum=0.9)
-            fm = FlatMaster(m, opt, 1.0)
-            m.__dict__["_flat_master"] = fm
+            fm = None if plain else FlatMaster(m, opt, 1.0)
+            if fm is not None:
+                m.__dict__["_flat_master"] = fm
             torch.cuda.manual_seed(7)
             out = []
+            # SIDE=1: copy b runs on a side stream (as the graphed step's eager warm-up does)
+            stream = side if (tag == "b" and os.environ.get("SIDE") == "1") else torch.cuda.current_stream()
+            stream.wait_stream(torch.cuda.current_stream())
             for s in range(3):
-                opt.zero_grad(set_to_none=True)
-                losses = m(x["images"], x["hw"], x["gt_boxes"], x["gt_labels"], x["gt_count"], x["gt_mask_flat"],
-                           x["gt_mask_table"])
-                losses["total_loss"].backward()
-                fm.step(0.01)
+                with torch.cuda.stream(stream):
+                    opt.zero_grad(set_to_none=True)
+                    losses = m(x["images"], x["hw"], x["gt_boxes"], x["gt_labels"], x["gt_count"], x["gt_mask_flat"],
+                               x["gt_mask_table"])
+                    losses["total_loss"].backward()
+                    if fm is not None:
+                        fm.step(0.01)
+                    else:
+                        torch.nn.utils.clip_grad_norm_(ps, 1.0)
+                        opt.step()
                 out.append({k: float(v.detach()) for k, v in losses.items()})
+            torch.cuda.current_stream().wait_stream(stream)
             torch.cuda.synchronize()
             hist[tag] = (out, [p.detach().float().clone() for p in ps])
         print(f"== {H}x{W}")

@@ -412,7 +412,7 @@ def test_split_k_last_arriver_matches_reduce_launch(case, monkeypatch):
         assert torch.equal(outs[0][1], outs[1][1])
 
 
-NARROW = [(2, 256, 16, 40, 52, 1, 1, 0, 1), (48, 256, 80, 28, 28, 1, 1, 0, 1), (1, 128, 24, 33, 17, 1, 1, 0, 1)]
+NARROW = [(2, 256, 16, 80, 104, 1, 1, 0, 1), (48, 256, 80, 28, 28, 1, 1, 0, 1), (4, 128, 24, 66, 68, 1, 1, 0, 1)]
 
 
 @pytest.mark.parametrize("case", NARROW)

@@ -222,3 +222,43 @@ def test_fpn_join_backward_matches_autograd_add():
     FPN.join_backward = True
     for a, b in zip(*res):
         torch.testing.assert_close(b, a, rtol=3e-2, atol=3e-2 * float(a.abs().max()) + 1e-3)
+
+
+def test_fpn_join_graph_replay_matches_eager():
+    """The FPN forward + backward with JoinLink captured in a hipGraph and replayed gives the
+    eager gradients bit for bit (the parked-gradient protocol is host-side, fixed at capture)."""
+    from mxtrain.models.maskrcnn import FPN
+    torch.manual_seed(0)
+    chans = [256, 512, 1024, 2048]
+    shapes = [(96, 128), (48, 64), (24, 32), (12, 16)]
+    fpn = FPN(chans, 256).to(DEV).to(torch.bfloat16)
+    params = list(fpn.parameters())
+    feats = [torch.randn(2, c, h, w, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+             .requires_grad_(True) for c, (h, w) in zip(chans, shapes)]
+    with torch.no_grad():
+        gouts = [torch.randn_like(o) for o in fpn(feats)]
+
+    def step():
+        for p in params + feats:
+            p.grad = None
+        outs = fpn(feats)
+        torch.autograd.backward(outs, gouts)
+        return [t.grad for t in feats + params]
+
+    ref = [g.clone() for g in step()]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    for p in params + feats:
+        p.grad = None
+    with torch.cuda.graph(g):
+        outs = fpn(feats)
+        torch.autograd.backward(outs, gouts)
+    grads = [t.grad for t in feats + params]
+    g.replay()
+    torch.cuda.synchronize()
+    for a, b in zip(ref, grads):
+        assert torch.equal(a, b)
