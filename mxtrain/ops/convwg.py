@@ -275,11 +275,11 @@ def _fits(*numels: int) -> bool:
 def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, padding=0, dilation=1,
                   res_up: bool = False) -> bool:
     """The implicit-GEMM forward: NHWC bf16, Cout a multiple of 64, Cin of 64, and at least
-    FWD_MIN_TILES output tiles (smaller convs stay on MIOpen).  ``res_up``: the
+    FWD_MIN_TILES output tiles or a split reduction (any size unless SMALL_ON_MIOPEN).  ``res_up``: the
     residual is at half the output resolution, added nearest-upsampled."""
     # (Cout a multiple of 8: the narrow 1x1 heads -- RPN 16, mask logits 80 -- run zero-padded tiles)
     if not (FWD and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
-            and w.dim() == 4 and w.shape[0] % 8 == 0 and w.shape[1] % 64 == 0 and x.shape[1] == w.shape[1]
+            and w.dim() == 4 and cout_ok(w.shape[0]) and w.shape[1] % 64 == 0 and x.shape[1] == w.shape[1]
             and _cl(x) and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
             and None not in (_sym(stride), _sym(padding), _sym(dilation))):
         return False
@@ -302,6 +302,8 @@ def fwd_supported(x: torch.Tensor, w: torch.Tensor, b, residual, stride=1, paddi
     # 128 x 128 tiles, or 128 x 64 when Cout is an odd multiple of 64 (csrc/convwg.hip); fewer
     # than FWD_MIN_TILES tiles split the reduction (fwd_splits)
     tiles = (N * OH * OW + 127) // 128 * (w.shape[0] // 128 if w.shape[0] % 128 == 0 else -(-w.shape[0] // 64))
+    if not SMALL_ON_MIOPEN:
+        return True
     if w.shape[0] % 64:   # narrow Cout: no split-K (whole-tile partial planes)
         return tiles >= FWD_MIN_TILES
     return tiles >= FWD_MIN_TILES or fwd_splits(tiles, w.shape[2] * w.shape[3] * w.shape[1] // 64) > 1
@@ -321,12 +323,30 @@ SPLIT_MAX = 8
 SPLIT_MIN_NK = 32
 
 
+# Convolutions with fewer than FWD_MIN_TILES / DGRAD_MIN_TILES output tiles once went to
+# MIOpen unless their reduction was long enough to split.  MIOpen's split-K solvers for
+# these (the coarse FPN levels and heads at small images) accumulate with atomics: two
+# identical steps differed in the last bits even with cudnn.deterministic, so a graphed
+# step could not reproduce the eager one (scripts/fpn_graph_probe.py).  Now every small
+# convolution stays on the implicit GEMM, split when it has >= 8 K-steps (slices >= 4).
+SMALL_ON_MIOPEN = False   # A/B switch (the former routing)
+
+# Cout a multiple of 8 but not of 64 (the RPN head's 16 and the mask logits' 80 channels)
+# runs zero-padded tiles; NARROW = False sends those convs back to MIOpen (A/B switch)
+NARROW = True
+
+
+def cout_ok(cout: int) -> bool:
+    return cout % 64 == 0 or (NARROW and cout % 8 == 0)
+
+
 def k_splits(tiles: int, nk: int) -> int:
     """Reduction slices of a conv forward / input gradient with ``tiles`` output tiles and
     ``nk`` 64-deep K-steps (res5 / P5 at one image: 9-36 tiles; at four images 66-132): the
     fp32 partials ([splits][pixels][channels]) are summed in order (deterministic) by the
-    reduction kernel, which applies the epilogue."""
-    if tiles >= SPLIT_TILES or nk < SPLIT_MIN_NK:
+    last-arriving slice of each tile (or the reduction kernel), which applies the epilogue."""
+    small = tiles < FWD_MIN_TILES and not SMALL_ON_MIOPEN
+    if tiles >= SPLIT_TILES or (nk < SPLIT_MIN_NK and not small):
         return 1
     return max(1, min(SPLIT_WGS // max(tiles, 1), nk // 4, SPLIT_MAX))
 
@@ -368,7 +388,7 @@ def dgrad_supported(w: torch.Tensor, x_shape, stride, padding=0, dilation=1) -> 
     65 vs 40 us), and stride 1, a stride-decomposed filter (1x1 stride 2: one GEMM over the
     pixels of one parity class) or at most 256 output channels (a strided 3x3's gathered dY
     has 3 of 4 rows zero, which costs MFMA time per K-step)."""
-    if not (DGRAD and w.shape[0] % 8 == 0 and w.shape[1] % 128 == 0 and w.data_ptr() % 16 == 0):
+    if not (DGRAD and cout_ok(w.shape[0]) and w.shape[1] % 128 == 0 and w.data_ptr() % 16 == 0):
         return False
     N, Cin, IH, IW = x_shape
     st = _sym(stride)
@@ -381,10 +401,10 @@ def dgrad_supported(w: torch.Tensor, x_shape, stride, padding=0, dilation=1) -> 
         return False
     if decomposed(w.shape[2], w.shape[3], stride, padding, dilation):
         tiles = (N * (-(-IH // st)) * (-(-IW // st)) + 127) // 128 * (Cin // 128)
-        return tiles >= DGRAD_MIN_TILES or dgrad_splits(tiles, -(-w.shape[0] // 64)) > 1
+        return tiles >= DGRAD_MIN_TILES or dgrad_splits(tiles, -(-w.shape[0] // 64)) > 1 or not SMALL_ON_MIOPEN
     tiles = (N * IH * IW + 127) // 128 * (Cin // 128)
     nk = -(-(w.shape[2] * w.shape[3] * w.shape[0]) // 64)
-    return ((tiles >= DGRAD_MIN_TILES or dgrad_splits(tiles, nk) > 1)
+    return ((tiles >= DGRAD_MIN_TILES or dgrad_splits(tiles, nk) > 1 or not SMALL_ON_MIOPEN)
             and (st == 1 or w.shape[0] <= 256))
 
 

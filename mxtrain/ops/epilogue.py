@@ -206,7 +206,7 @@ class ConvBiasActFn(torch.autograd.Function):
         elif add is not None:
             raise RuntimeError("BlockLink: residual gradient stashed for a conv without an input gradient")
         if ctx.needs_input_grad[1]:
-            if w.shape[0] % 8 == 0 and w.shape[1] % 128 == 0:   # (narrow Cout: zero-padded row tile)
+            if convwg.cout_ok(w.shape[0]) and w.shape[1] % 128 == 0:   # (narrow Cout: zero-padded row tile)
                 dw = convwg.conv_wgrad(dy, x, tuple(w.shape), st, pd, dl)
             else:
                 dw = torch.ops.aten.convolution_backward(dy, x, w, None, st, pd, dl, False, [0, 0], 1,
