@@ -69,8 +69,11 @@ def plan_splits(T: int, ntiles: int) -> int:
 
 
 # split-K forward / input gradient: the last-arriving split of each tile sums the partials and
-# runs the epilogue (csrc/convwg.hip split_last_arriver) instead of a reduction launch
-SPLIT_IN_KERNEL = True
+# runs the epilogue (csrc/convwg.hip split_last_arriver) instead of a reduction launch.  OFF:
+# its agent-scope release is a whole-L2 write-back (buffer_wbl2) per workgroup, and the step
+# ran 130.3 img/s with it vs 152.4 with the reduction launches at one image
+# (profiles/r5_s1/mrcnn_ab_split_in_kernel_1img.txt)
+SPLIT_IN_KERNEL = False
 _TICKETS: Dict[torch.device, torch.Tensor] = {}
 
 
