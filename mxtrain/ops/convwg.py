@@ -30,7 +30,7 @@ TARGET_WGS = 512        # two 128 x 128 workgroups per CU on 256 CUs; >= 16 K-st
 MIN_STEPS = 16          # the 32-bit gather made the slices cheaper than their fp32 partials
                         # (profiles/r4_s3/wgrad_split_ab*_{1,4}img.txt; before: r4_s2 sweep, 8)
 _DESC_T = ctypes.c_int64 * 32
-_WS: Dict[torch.device, Tuple[torch.Tensor, torch.Tensor]] = {}
+_WS: Dict[Tuple[torch.device, int], Tuple[torch.Tensor, torch.Tensor]] = {}
 _RETIRED = []           # outgrown slabs stay alive: a captured hipGraph may still write them
 
 
@@ -88,12 +88,13 @@ def _tickets(device) -> int:
 def _workspace(device, slab_elems: int):
     """(fp32 split-K slab, 256 zero bf16): grown on demand, so the first (eager) steps size
     it before a hipGraph capture records its address."""
-    ws = _WS.get(device)
+    key = (device, _lib.stream())   # per stream: the side-stream weight gradients run concurrently
+    ws = _WS.get(key)
     if ws is None or ws[0].numel() < slab_elems:
         if ws is not None:
             _RETIRED.append(ws)
         s = max(slab_elems, ws[0].numel() if ws else 0, 1)
-        ws = _WS[device] = (torch.empty(s, device=device, dtype=torch.float32),
+        ws = _WS[key] = (torch.empty(s, device=device, dtype=torch.float32),
                             torch.zeros(256, device=device, dtype=torch.bfloat16))
     return ws
 
@@ -106,11 +107,50 @@ def _workspace(device, slab_elems: int):
 # Mask R-CNN step at ~5-7 us each, profiles/r5_s1/maskrcnn_1img_census_nms_par.txt).  The
 # arena is sized by the eager steps; a capture that would outgrow it reduces immediately.
 DEFER_WGRAD = True      # module switch (A/B)
-_DEF = {"on": False, "jobs": [], "cjobs": [], "arena": None, "cursor": 0, "total": 0, "peak": 0}
+_DEF = {"on": False, "jobs": [], "cjobs": [], "arena": None, "cursor": 0, "total": 0, "peak": 0,
+        "side": None, "side_keep": []}
 _DEF_RETIRED = []
 
 
+# Weight gradients on a side stream (FlatMaster steps, i.e. while deferring): a conv's dW
+# GEMM is independent of its dX GEMM and of the earlier layers' backward, and at one image
+# most Mask R-CNN convs fill a fraction of the chip (10-30 us launches), so the two chains
+# overlap (graph branches run concurrently, profiles/r5_s1/graph_branch_probe.txt).  The
+# side stream forks after the conv's output gradient is ready and joins the main stream at
+# the flush, before the optimizer pass reads any gradient; the operands stay referenced
+# until then (their memory must not be reused under the side stream's kernels).
+# OFF: measured slower in the graphed step -- 143.1 vs 153.2 img/s at one image, 288.2 vs
+# 291.5 at four (profiles/r5_s1/mrcnn_ab_wgrad_side_*.txt); the ~60 fork edges cost more
+# than the overlap recovers.
+WGRAD_SIDE = False       # A/B switch
+_SIDE: Dict[torch.device, "torch.cuda.Stream"] = {}
+
+
+def wgrad_side(device):
+    """The side stream for this backward's weight gradients, or None (run inline)."""
+    if not (WGRAD_SIDE and deferring()):
+        return None
+    st = _SIDE.get(device)
+    if st is None:
+        st = _SIDE[device] = torch.cuda.Stream(device=device)
+    _DEF["side"] = st
+    return st
+
+
+def side_keep(*ts):
+    _DEF["side_keep"].extend(ts)
+
+
+def _side_join():
+    st = _DEF.get("side")
+    if st is not None:
+        torch.cuda.current_stream(st.device).wait_stream(st)
+        _DEF["side"] = None
+    _DEF["side_keep"] = []
+
+
 def defer_begin():
+    _side_join()
     _DEF["on"] = DEFER_WGRAD
     _DEF["jobs"] = []
     _DEF["cjobs"] = []
@@ -121,6 +161,7 @@ def defer_begin():
 def defer_flush(keep_on: bool = False):
     """Launch the pending reductions; deferral stays on only if ``keep_on`` (more gradient
     buckets of this backward still to come)."""
+    _side_join()
     _DEF["on"] = _DEF["on"] and keep_on
     for key, fn, width in (("jobs", "mx_conv_wgrad_reduce_batched", 10), ("cjobs", "mx_colsum_jobs", 5)):
         jobs = _DEF[key]
