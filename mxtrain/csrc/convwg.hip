@@ -1234,8 +1234,8 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   return (int)hipGetLastError();
 }
 
-// d (int64[24]): {x, w, zero, y, bias, res, ldx, ldy, N, OH, OW, IH, IW, KH, KW, stride, pad,
-// dil, Cout, Cin, relu, res_up, splits, part}: y = act(conv2d(x, w) + bias (+ res, or with res_up the 2x
+// d (int64[26]): {x, w, zero, y, bias, res, ldx, ldy, N, OH, OW, IH, IW, KH, KW, stride, pad,
+// dil, Cout, Cin, relu, res_up, splits, part, ticket, half}: y = act(conv2d(x, w) + bias (+ res, or with res_up the 2x
 // nearest upsampling of res)) in NHWC bf16, weight [Cout][KH][KW][Cin] (channels_last).
 // Cout a multiple of 64 (128 x 64 tiles when not of 128), Cin of 64; res_up needs even OH, OW.
 MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
@@ -1285,7 +1285,10 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   const int bkt = bk32 && cp.Cin % 32 == 0 ? 32 : 64;
   cp.cib = cp.Cin / bkt;
   cp.nk = cp.taps * cp.cib;
-  cp.tiles_n = Cout % 128 == 0 ? Cout / 128 : (Cout + 63) / 64;   // (narrow Cout: zero-padded tiles)
+  // d[25] != 0: 128 x 64 tiles even when Cout is a multiple of 128 (twice the tiles for a small
+  // convolution instead of a deeper K split: no fp32 partial round trip)
+  const bool half = d[25] != 0 && Cout % 64 == 0;
+  cp.tiles_n = Cout % 128 == 0 && !half ? Cout / 128 : (Cout + 63) / 64;   // (narrow Cout: zero-padded tiles)
   if (Cout % 64 && cp.splits > 1) return (int)hipErrorInvalidValue;   // partial planes assume whole tiles
   cp.invOW = 1.f / (float)cp.OW;
   cp.invOH = 1.f / (float)cp.OH;
@@ -1304,9 +1307,9 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   // ring depth 2 at two workgroups per CU: 3 / 4 slots (one workgroup per CU, counted waits)
   // measured 40 % slower on the Mask R-CNN shapes (profiles/r4_s2/conv_ring_depth_ab_4img.txt)
   if (bkt == 32) {
-    if (Cout % 128 == 0) { MX_CF(2, 4, 32) } else { MX_CF(2, 2, 32) }
+    if (Cout % 128 == 0 && !half) { MX_CF(2, 4, 32) } else { MX_CF(2, 2, 32) }
   } else {
-    if (Cout % 128 == 0) { MX_CF(2, 4, 64) } else { MX_CF(2, 2, 64) }
+    if (Cout % 128 == 0 && !half) { MX_CF(2, 4, 64) } else { MX_CF(2, 2, 64) }
   }
 #undef MX_CF
   if (cp.splits > 1 && !cp.ticket) {

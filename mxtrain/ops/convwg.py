@@ -26,6 +26,9 @@ ENABLED = True          # module switch (A/B runs: scripts/conv_wgrad_bench.py)
 DGRAD = True            # input gradient from csrc/convwg.hip too (else MIOpen's backward-data)
 FWD = True              # forward with the fused bias / residual / ReLU epilogue (else MIOpen)
 FWD_MIN_TILES = 64
+# forward convs with fewer 128 x 128 output tiles than this run 128 x 64 tiles (twice the
+# workgroups, so a shallower K split or none)
+FWD_HALF_TILES = 128
 TARGET_WGS = 512        # two 128 x 128 workgroups per CU on 256 CUs; >= 16 K-steps per slice since
 MIN_STEPS = 16          # the 32-bit gather made the slices cheaper than their fp32 partials
                         # (profiles/r4_s3/wgrad_split_ab*_{1,4}img.txt; before: r4_s2 sweep, 8)
@@ -395,8 +398,14 @@ def k_splits(tiles: int, nk: int) -> int:
     return max(1, min(SPLIT_WGS // max(tiles, 1), nk // 4, SPLIT_MAX))
 
 
+# the forward's own cap: at >= FWD_SPLIT_TILES tiles (128 x 64 ones included) an unsplit
+# launch beat every split at the 1-img shapes (mask head 196 tiles: 28.5 us unsplit vs 35.4
+# in two; res4 3x3 132 half tiles: 23.6 vs 25.0 -- profiles/r5_s1/conv_fwd_sweep_1img.txt)
+FWD_SPLIT_TILES = 160
+
+
 def fwd_splits(tiles: int, nk: int) -> int:
-    return k_splits(tiles, nk)
+    return 1 if tiles >= FWD_SPLIT_TILES else k_splits(tiles, nk)
 
 
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool = False, stride=1, padding=0,
@@ -412,14 +421,18 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool
         w = w.contiguous(memory_format=torch.channels_last)
     y = torch.empty((N, OH, OW, Cout), dtype=torch.bfloat16, device=x.device).permute(0, 3, 1, 2)
     T = N * OH * OW
-    splits = 1 if Cout % 64 else fwd_splits((T + 127) // 128 * (Cout // (128 if Cout % 128 == 0 else 64)),
-                                             KH * KW * Cin // 64)
+    tiles = (T + 127) // 128 * (Cout // (128 if Cout % 128 == 0 else 64))
+    half = Cout % 128 == 0 and tiles < FWD_HALF_TILES
+    if half:
+        tiles *= 2
+    splits = 1 if Cout % 64 else fwd_splits(tiles, KH * KW * Cin // 64)
     slab, zero = _workspace(x.device, splits * T * Cout if splits > 1 else 1)
     d = _DESC_T()
     d[:24] = [x.data_ptr(), w.data_ptr(), zero.data_ptr(), y.data_ptr(), _lib.ptr(b) or 0,
               _lib.ptr(residual) or 0, Cin, Cout, N, OH, OW, IH, IW, KH, KW, st, pd, dl, Cout, Cin, int(relu),
               int(res_up), splits, slab.data_ptr() if splits > 1 else 0]
     d[24] = _tickets(x.device) if (splits > 1 and SPLIT_IN_KERNEL) else 0
+    d[25] = int(half)
     _lib.call("mx_conv_fwd", d, _lib.stream())
     return y
 
