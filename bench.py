@@ -268,6 +268,8 @@ def main():
                          "probe, then a bit-exact check against RCCL and a timing of both per message "
                          "size on the live group, agreed on every rank; any failure -> RCCL everywhere. "
                          "The per-size decision is recorded in the JSON line (config.collectives)")
+    ap.add_argument("--lib-set", action="append", default=[], metavar="SETTER=INT",
+                    help="call a kernel-library A/B setter before the run (e.g. mx_gemm_nt_prio=1)")
     args = ap.parse_args()
     if args.xgmi is None:
         args.xgmi = "auto" if int(os.environ.get("WORLD_SIZE", "1")) > 1 else "0"
@@ -296,6 +298,11 @@ def main():
     except Exception:
         pass
     from mxtrain.runtime.gemm_tuning import use_tuned_gemms
+    if args.lib_set:
+        from mxtrain.ops import _lib
+        for kv in args.lib_set:
+            name, val = kv.split("=")
+            _lib._fn(name)(int(val))
     n_tables = 0 if args.no_tuned_gemm else use_tuned_gemms(tune=args.tune_gemm,
                                                                tables=[] if args.tune_gemm else None)
     mcfg = dict(GPT_CONFIGS[args.model])

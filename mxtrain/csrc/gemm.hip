@@ -51,7 +51,11 @@ struct Batch {
   float beta;
   float* slab;          // split-K partials: [ntiles][splits][NT / 64][acc regs / 4][64] float4
   uint32_t* ticket;     // [ntiles], zero between launches (the last arriver resets its word)
+  int prio;             // 8-wave tiles, bit 0: s_setprio 1 for waves 4-7; bit 1: their half-step stagger
 };
+
+// as gemm_nt.hip g_gemm_nt_prio (MI355X_MICROARCH.md "Two waves per SIMD", items 4 and 9)
+int g_gemm_kk_prio = 3;
 
 __device__ __forceinline__ Prob pick(const Batch& bt, int t) {
   // constant indices only: a runtime index into the by-value kernel argument would copy it
@@ -146,6 +150,21 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kk_kernel(const Batch
 #pragma unroll
   for (int q = 0; q < NSLOT - 1; ++q)
     if (q < nk) issue(q, q);
+  // stagger (bt.prio bit 1): waves 4-7 read all of step it's fragments before the barrier that
+  // frees its slot but run only the first half of its (kk, s) MFMA groups there; the rest runs
+  // from registers after the next barrier, beside the partner wave's LDS read burst.  Same
+  // MFMAs per accumulator in the same order: bit-identical output.
+  constexpr int KK = BKT / 32, NQ = KK * FM, NH1 = NQ / 2;
+  const bool stag = C_::NW == 8 && (bt.prio & 2) && wave >= 4;
+  if (C_::NW == 8 && (bt.prio & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  bf16x8 sa[NQ], sb[KK][FN];
+  bool pend = false;
+  auto run_h2 = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = NH1; p < NQ; ++p)
+#pragma unroll
+      for (int u = 0; u < FN; ++u) acc[p % FM][u] = mfma16(sa[p], sb[p / FM][u], acc[p % FM][u]);
+  };
   int slot = 0;
   for (int it = 0; it < nk; ++it) {
     // retire step it's pieces (the later steps' stay in flight), then one barrier: every
@@ -163,6 +182,27 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kk_kernel(const Batch
     }
     const char* As = smem + slot * SLOT;
     const char* Bs = As + IA;
+    if (stag) {
+      if (pend) run_h2();
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+        for (int u = 0; u < FN; ++u)
+          sb[kk][u] = cat(tr_read(Bs, offB[u] + 32 * RB * kk), tr_read(Bs, offB[u] + 32 * RB * kk + 4 * RB));
+#pragma unroll
+      for (int p = 0; p < NQ; ++p) {
+        const int kk = p / FM, s2 = p % FM;
+        sa[p] = cat(tr_read(As, offA[s2] + 32 * RA * kk), tr_read(As, offA[s2] + 32 * RA * kk + 4 * RA));
+        if (p < NH1) {
+#pragma unroll
+          for (int u = 0; u < FN; ++u) acc[s2][u] = mfma16(sa[p], sb[kk][u], acc[s2][u]);
+        }
+      }
+      pend = true;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot is freed at the next barrier
+      if (++slot == NSLOT) slot = 0;
+      continue;
+    }
 #pragma unroll
     for (int kk = 0; kk < BKT / 32; ++kk) {
       bf16x8 b[FN];
@@ -178,6 +218,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kk_kernel(const Batch
     }
     if (++slot == NSLOT) slot = 0;
   }
+  if (stag && pend) run_h2();
 
   // ---- split-K: every slice publishes its partial tile; the last arriver sums them
   if (bt.splits > 1) {
@@ -247,6 +288,7 @@ int launch(const int64_t* desc, int np, int K, float beta, int splits, float* sl
   bt.splits = splits;
   bt.slab = slab;
   bt.ticket = ticket;
+  bt.prio = g_gemm_kk_prio;
   int total = 0;
   for (int q = 0; q < np; ++q) {
     const int64_t* d = desc + 8 * q;
@@ -316,4 +358,12 @@ MX_EXPORT int mx_gemm_kk(int np, const int64_t* desc, int K, float beta, int var
     case 6: return launch<2, 4, 4, 2, 64, 4, 1>(desc, np, K, beta, splits, sl, tk, st);
     default: return launch<2, 2, 4, 4, 64, 2, 2>(desc, np, K, beta, splits, sl, tk, st);
   }
+}
+
+// A/B: priority / stagger of the 8-wave weight-gradient tiles (g_gemm_kk_prio bits); negative:
+// query.  Returns the old value.
+MX_EXPORT int mx_gemm_kk_prio(int on) {
+  const int old = g_gemm_kk_prio;
+  if (on >= 0) g_gemm_kk_prio = on;
+  return old;
 }

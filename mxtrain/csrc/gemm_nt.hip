@@ -52,7 +52,13 @@ struct Args {
   int lda, ldb, ldc, ldx;
   int K, N;
   int tiles_n, gm;
+  int prio;              // 8-wave tiles, bit 0: s_setprio 1 for waves 4-7; bit 1: their half-step stagger
 };
+
+// Waves 4-7 of an 8-wave workgroup are the VALU-arbitration losers against their SIMD partners
+// (waves 0-3) at equal priority: one static s_setprio 1 for that half before the K-loop
+// (MI355X_MICROARCH.md "Two waves per SIMD", item 4).  A/B switch, read at launch.
+int g_gemm_nt_prio = 3;
 
 __device__ __forceinline__ float dpp_rowsum16(float v) {
   v += MX_DPP(v, 0xB1);   // quad_perm [1,0,3,2]
@@ -313,6 +319,24 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_nt_kernel(const Args 
   constexpr int NSTREAM = XRES ? FN : FM;
   constexpr int NS = (BKT / 32) * NSTREAM;       // streamed-fragment steps per K-step
   constexpr int SPREAD = NS / 2 >= PER ? NS / 2 : NS;
+  // Stagger (g.prio bit 1, 8-wave resident-x tiles): waves 4-7 run half a K-step behind their
+  // SIMD partners (waves 0-3).  They read ALL of step it's fragments before barrier it + 1 but
+  // issue only the first half of its (kk, u) MFMA pairs there; the second half runs from
+  // registers right after the next barrier, while the partner is in its LDS read burst
+  // (MI355X_MICROARCH.md "Two waves per SIMD", item 9).  Same arithmetic in the same order
+  // per accumulator, so the output is bit-identical.
+  constexpr int KK = BKT / 32, NQ = KK * FN, NH1 = NQ / 2;
+  const bool stag = XRES && WM * WN == 8 && (g.prio & 2) && wave >= 4;
+  bf16x8 dx[KK][FM], dw[NQ - NH1 > 0 ? NQ - NH1 : 1];
+  bool pend = false;
+  auto run_h2 = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = NH1; p < NQ; ++p)
+#pragma unroll
+      for (int s2 = 0; s2 < FM; ++s2)
+        acc[s2][p % FN] = mfma16(dw[p - NH1], dx[p / FN][s2], acc[s2][p % FN]);
+  };
+  if (WM * WN == 8 && (g.prio & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
   // the K-loop is unrolled by the ring depth, so every ring slot (LDS offset, M0 value) is
   // a compile-time constant
   for (int it0 = 0; it0 < nk; it0 += NSLOT) {
@@ -340,6 +364,28 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_nt_kernel(const Args 
       auto xfrag = [&](int s, int kk) __attribute__((always_inline)) {
         return lds_read8(As, offA + 16 * s * RA + cA[kk]);
       };
+      if (XRES && stag) {
+        if (pend) run_h2();
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+          for (int s2 = 0; s2 < FM; ++s2) dx[kk][s2] = xfrag(s2, kk);
+#pragma unroll
+        for (int p = 0; p < NH1; ++p) {
+          const bf16x8 w = wfrag(p % FN, p / FN);
+#pragma unroll
+          for (int j = 0; j < PER; ++j)
+            if (j * NH1 / PER == p && fetch) piece(ns, it + NSLOT - 1, j);
+#pragma unroll
+          for (int s2 = 0; s2 < FM; ++s2) acc[s2][p % FN] = mfma16(w, dx[p / FN][s2], acc[s2][p % FN]);
+        }
+#pragma unroll
+        for (int p = NH1; p < NQ; ++p) dw[p - NH1] = wfrag(p % FN, p / FN);
+        pend = true;
+        // every fragment of this slot is in registers before the barrier that frees the slot
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        return;
+      }
 #pragma unroll
       for (int kk = 0; kk < BKT / 32; ++kk) {
         if constexpr (XRES) {
@@ -375,6 +421,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_nt_kernel(const Args 
     });
   }
 
+  if (stag && pend) run_h2();
   stamp(2);
   epilogue<WM, WN, FM, FN, EPI>(g, acc, tm, m0, n0, wave, lane);
   if constexpr (STAMP) {
@@ -514,6 +561,7 @@ MX_EXPORT int mx_gemm_nt(const void* a, const void* b, void* c, void* aux, const
   g.ldx = ldx;
   g.K = K;
   g.N = N;
+  g.prio = g_gemm_nt_prio;
   hipStream_t st = (hipStream_t)stream;
   if (!b_kmajor) {
     switch (epi) {
@@ -528,4 +576,12 @@ MX_EXPORT int mx_gemm_nt(const void* a, const void* b, void* c, void* aux, const
     case 3: return dispatch<false, 3>(variant, g, M, st);
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+// A/B: static priority for the second half of the 8-wave tiles (g_gemm_nt_prio); negative:
+// query.  Returns the old value.
+MX_EXPORT int mx_gemm_nt_prio(int on) {
+  const int old = g_gemm_nt_prio;
+  if (on >= 0) g_gemm_nt_prio = on;
+  return old;
 }

@@ -108,6 +108,8 @@ SIGNATURES = {
     # gemm_nt.hip
     "mx_gemm_nt_tile": [I, I],
     "mx_gemm_nt": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
+    "mx_gemm_nt_prio": [I],
+    "mx_gemm_kk_prio": [I],
     "mx_gemm_nt_stamps": [P, P, P, P, I, I, I, I, I, I, I, P],
     # rope.hip
     "mx_rope": [P, I64, I, I, I, I, I, I, I, P, P, P, I, P],
