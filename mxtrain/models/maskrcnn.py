@@ -35,6 +35,7 @@ from ..ops import detloss as D
 from ..ops import vision as V
 from ..ops import _lib
 from ..ops import convwg
+from ..ops import stem as stem_ops
 from .compute_weights import ComputeWeights, cw
 from .resnet import ConvNorm, resnet50
 
@@ -450,8 +451,19 @@ class MaskRCNN(nn.Module):
             self._anchor_cache[key] = torch.cat(anchors_lv, 0)
         return self._anchor_cache[key]
 
+    # frozen stem + pool0 as one kernel straight from the uint8 image (ops/stem.py); A/B switch
+    fused_stem = True
+
     def features(self, images: torch.Tensor):
         dt = self.compute_dtype(images.device)
+        stem = self.backbone.stem
+        if (self.fused_stem and images.is_cuda and images.dtype == torch.uint8 and dt == torch.bfloat16
+                and stem.norm_kind == "frozen" and not stem.conv.weight.requires_grad and not ConvNorm.calibrating
+                and _lib.use_hip(images)):
+            wf, bf = stem._folded(stem.conv.weight, dt)
+            if stem_ops.supported(images, wf, bf):
+                x = stem_ops.stem_pool(images, wf, bf, self.cfg.pixel_mean, self.cfg.pixel_std)
+                return self.fpn(self.backbone.forward_features(x, stem_done=True))
         x = None
         if (images.is_cuda and images.dtype == torch.uint8 and dt == torch.bfloat16 and images.is_contiguous()
                 and (images.shape[2] * images.shape[3]) % 4 == 0 and _lib.use_hip(images)):

@@ -210,9 +210,11 @@ class ResNet(nn.Module):
             for p in self.stages[0].parameters():
                 p.requires_grad_(False)
 
-    def forward_features(self, x) -> List[torch.Tensor]:
-        x = self.stem(x)
-        x = F.max_pool2d(x, 3, 2, 1)
+    def forward_features(self, x, stem_done: bool = False) -> List[torch.Tensor]:
+        """C2..C5; ``stem_done``: x is already the pooled stem output (ops/stem.py)."""
+        if not stem_done:
+            x = self.stem(x)
+            x = F.max_pool2d(x, 3, 2, 1)
         outs = []
         for st in self.stages:
             x = st(x)

@@ -1,0 +1,64 @@
+"""Fused frozen ResNet stem (csrc/stem.hip): uint8 NCHW image -> normalise -> conv 7x7/2
+(FrozenBN folded) -> ReLU -> max-pool 3x3/2 in one launch, bf16 NHWC out.  The torch path
+below is the fp32 reference of the same op (the CPU path and the kernel test's oracle).
+Reference: tensorpack's ResNet conv0 + pool0 with FREEZE_AT=2."""
+import ctypes
+from typing import Sequence
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+_PACK = {}
+
+
+def pack_weight(wf: torch.Tensor) -> torch.Tensor:
+    """[64, 3, 7, 7] -> bf16 [64, 192], K = (channel, kernel row 0..7, kernel column 0..7), the
+    eighth row / column zero (csrc/stem.hip's MFMA K layout); cached against the weight's
+    storage and version (the folded frozen weight only changes by in-place writes)."""
+    key = (wf.data_ptr(), wf._version, wf.device)
+    hit = _PACK.get(key)
+    if hit is not None:
+        return hit
+    co = wf.shape[0]
+    wp = torch.zeros(co, 3, 8, 8, dtype=torch.float32, device=wf.device)
+    wp[:, :, :7, :7] = wf.float()
+    wp = wp.reshape(co, 192).to(torch.bfloat16).contiguous()
+    _PACK.clear()
+    _PACK[key] = wp
+    return wp
+
+
+def supported(images: torch.Tensor, wf: torch.Tensor, bf) -> bool:
+    return (images.is_cuda and images.dtype == torch.uint8 and images.dim() == 4 and images.shape[1] == 3
+            and images.is_contiguous() and tuple(wf.shape) == (64, 3, 7, 7) and bf is not None
+            and bf.dtype == torch.bfloat16 and bf.is_contiguous() and bf.data_ptr() % 8 == 0
+            and images.shape[2] >= 2 and images.shape[3] >= 2 and _lib.use_hip(images))
+
+
+def stem_pool(images: torch.Tensor, wf: torch.Tensor, bf: torch.Tensor, mean: Sequence[float],
+              std: Sequence[float]) -> torch.Tensor:
+    """max_pool2d(relu(conv2d((images - mean) / std, wf, bf, stride 2, pad 3)), 3, 2, 1) as a
+    channels_last bf16 [N, 64, PH, PW] (NCHW view of NHWC memory)."""
+    N, _, H, W = images.shape
+    if not supported(images, wf, bf):
+        return stem_pool_ref(images, wf, bf, mean, std)
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    PH, PW = (OH - 1) // 2 + 1, (OW - 1) // 2 + 1
+    y = torch.empty((N, PH, PW, 64), dtype=torch.bfloat16, device=images.device)
+    wp = pack_weight(wf)
+    _lib.call("mx_stem_pool", images.data_ptr(), wp.data_ptr(), bf.data_ptr(), y.data_ptr(), N, H, W,
+              ctypes.cast((ctypes.c_float * 3)(*mean), ctypes.c_void_p),
+              ctypes.cast((ctypes.c_float * 3)(*[1.0 / v for v in std]), ctypes.c_void_p), _lib.stream())
+    return y.permute(0, 3, 1, 2)
+
+
+def stem_pool_ref(images, wf, bf, mean, std) -> torch.Tensor:
+    """fp32 torch reference (inputs normalised and rounded to bf16, as the kernel does)."""
+    m = torch.tensor(list(mean), dtype=torch.float32, device=images.device).view(1, 3, 1, 1)
+    inv = torch.tensor([1.0 / v for v in std], dtype=torch.float32, device=images.device).view(1, 3, 1, 1)
+    x = ((images.float() - m) * inv).to(torch.bfloat16).float()
+    y = F.relu(F.conv2d(x, wf.float(), bf.float() if bf is not None else None, 2, 3))
+    y = F.max_pool2d(y, 3, 2, 1)
+    return y.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)

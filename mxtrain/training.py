@@ -317,7 +317,7 @@ class GPTTrainer:
         # the optimizer step counter / hyper-parameters are host-driven: set_hyper copies
         # from a pinned buffer that the captured memcpy re-reads on every replay
         step0 = [o.step_count for o in self._opts]
-        with torch.cuda.graph(g, stream=s):
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
             loss = self._graph_body()
         for o, c in zip(self._opts, step0):
             o.step_count = c

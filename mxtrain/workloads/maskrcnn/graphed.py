@@ -239,13 +239,20 @@ class GraphedTrainStep:
                 self.marker("capture-begin")
             err = None
             try:
-                with torch.cuda.graph(g, pool=self.pool, stream=self.stream):
+                # thread-local capture mode: the loader's threads keep pinning and copying host
+                # buffers while this thread captures; under the default global mode such a
+                # call from ANY thread invalidates the capture (seen at 4 img/GPU once the
+                # fused stem shortened the forward: hipErrorStreamCaptureInvalidated)
+                with torch.cuda.graph(g, pool=self.pool, stream=self.stream, capture_error_mode="thread_local"):
                     sout = self._body(st)
                 if self.marker is not None:
                     self.marker("capture-end")
                 self._finish_capture(g, key)
             except Exception as e:  # noqa: BLE001 -- fall back to the eager step, loudly
                 err = repr(e)[:300]
+                if self.debug:
+                    import traceback
+                    traceback.print_exc()
         cur.wait_stream(self.stream)
         res = dict(zip(LOSS_NAMES, out.unbind(0)))
         if err is not None:
