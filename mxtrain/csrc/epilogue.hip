@@ -270,3 +270,41 @@ MX_EXPORT int mx_down2_add(const void* g, const void* add, void* out, int N, int
                      (uint16_t*)out, N, H, W, C);
   return hipGetLastError();
 }
+
+// FPN P6 = max_pool2d(P5, kernel 1, stride 2), i.e. every second row / column of P5 (NHWC bf16,
+// 8 channels per thread), and its gradient: the P6 gradient at the even positions of a
+// P5-shaped tensor, zeros elsewhere (one pass, no zero fill).  torch's NHWC max-pool kernels
+// took ~10 us forward and ~37 us backward on these few-KB tensors (profiles/r5_s1 census).
+namespace {
+__global__ __launch_bounds__(256) void subsample2_kernel(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst,
+                                                         int H, int W, int h, int w, int C8, int64_t nvec, int grad) {
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const int64_t pix = v / C8;
+    const int c8 = (int)(v - pix * C8);
+    if (!grad) {   // v indexes P6 [N][h][w]
+      const int64_t n = pix / ((int64_t)h * w);
+      const int rem = (int)(pix - n * h * w), y = rem / w, x = rem - (rem / w) * w;
+      reinterpret_cast<uint4*>(dst)[v] =
+          reinterpret_cast<const uint4*>(src)[((n * H + 2 * y) * W + 2 * x) * C8 + c8];
+    } else {       // v indexes the P5-shaped gradient [N][H][W]; src is the P6 gradient
+      const int64_t n = pix / ((int64_t)H * W);
+      const int rem = (int)(pix - n * H * W), y = rem / W, x = rem - (rem / W) * W;
+      uint4 val = make_uint4(0u, 0u, 0u, 0u);
+      if (!((y | x) & 1)) val = reinterpret_cast<const uint4*>(src)[((n * h + y / 2) * w + x / 2) * C8 + c8];
+      reinterpret_cast<uint4*>(dst)[v] = val;
+    }
+  }
+}
+}  // namespace
+
+// grad = 0: dst [N][ceil(H/2)][ceil(W/2)][C] = src [N][H][W][C] at even (y, x); grad = 1: dst [N][H][W][C]
+// = src [N][ceil(H/2)][ceil(W/2)][C] at even positions, zero elsewhere.  C % 8 == 0, 16-B aligned.
+MX_EXPORT int mx_subsample2(const void* src, void* dst, int N, int H, int W, int C, int grad, hipStream_t s) {
+  if (N <= 0 || H <= 0 || W <= 0 || C % 8 || (((uintptr_t)src | (uintptr_t)dst) & 15)) return (int)hipErrorInvalidValue;
+  const int h = (H + 1) / 2, w = (W + 1) / 2;
+  const int64_t nvec = (int64_t)N * (grad ? (int64_t)H * W : (int64_t)h * w) * (C / 8);
+  const int64_t blocks = (nvec + 255) / 256 < 4096 ? (nvec + 255) / 256 : 4096;
+  hipLaunchKernelGGL(subsample2_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint16_t*)src, (uint16_t*)dst, H,
+                     W, h, w, C / 8, nvec, grad);
+  return hipGetLastError();
+}

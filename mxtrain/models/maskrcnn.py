@@ -30,7 +30,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.epilogue import BlockLink, JoinLink, _conv_in_ok, conv_bias_act, conv_transpose_bias_act, fused_conv_ok
+from ..ops.epilogue import (BlockLink, JoinLink, _conv_in_ok, conv_bias_act, conv_transpose_bias_act, fused_conv_ok,
+                            subsample2)
 from ..ops import detloss as D
 from ..ops import vision as V
 from ..ops import _lib
@@ -113,6 +114,7 @@ def huber(x: torch.Tensor, delta: float) -> torch.Tensor:
 # ---------------------------------------------------------------------------- modules
 class FPN(nn.Module):
     join_backward = True   # JoinLink fusion of the top-down join gradients (A/B switch)
+    fast_p6 = True         # P6 subsample on csrc/epilogue.hip mx_subsample2 (A/B switch)
 
     def __init__(self, in_channels: Sequence[int], out: int = 256):
         super().__init__()
@@ -147,7 +149,8 @@ class FPN(nn.Module):
         outs = [conv_bias_act(x, cw(m.weight, dt), cw(m.bias, dt), padding=1,
                               fuse=(link, i, ("join_dx",)) if i in joined else None)
                 for i, (x, m) in enumerate(zip(lat, self.output))]
-        outs.append(F.max_pool2d(outs[-1], 1, 2))   # P6
+        # P6 = max_pool2d(P5, 1, 2)
+        outs.append(subsample2(outs[-1]) if self.fast_p6 else F.max_pool2d(outs[-1], 1, 2))
         return outs
 
 

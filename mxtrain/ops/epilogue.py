@@ -223,6 +223,37 @@ class ConvBiasActFn(torch.autograd.Function):
         return dx, dw, db, dres, None, None, None, None, None, None
 
 
+class Subsample2Fn(torch.autograd.Function):
+    """max_pool2d(x, 1, 2) of an NHWC bf16 tensor -- FPN P6 = every second row / column of P5 --
+    on csrc/epilogue.hip mx_subsample2 in both directions (torch's max-pool kernels: ~10 us
+    forward, ~37 us backward on these few-KB tensors)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N, C, H, W = x.shape
+        ctx.shape = (N, C, H, W)
+        y = torch.empty((N, (H + 1) // 2, (W + 1) // 2, C), dtype=x.dtype, device=x.device)
+        _lib.call("mx_subsample2", x.data_ptr(), y.data_ptr(), N, H, W, C, 0, _lib.stream())
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        N, C, H, W = ctx.shape
+        if not _nhwc(g) or g.data_ptr() % 16:
+            g = g.contiguous(memory_format=torch.channels_last)
+        dx = torch.empty((N, H, W, C), dtype=g.dtype, device=g.device)
+        _lib.call("mx_subsample2", g.data_ptr(), dx.data_ptr(), N, H, W, C, 1, _lib.stream())
+        return dx.permute(0, 3, 1, 2)
+
+
+def subsample2(x: torch.Tensor) -> torch.Tensor:
+    """F.max_pool2d(x, 1, 2) (kernel 1: a plain stride-2 subsample)."""
+    if (_lib.use_hip(x) and x.dtype == torch.bfloat16 and _nhwc(x) and x.shape[1] % 8 == 0
+            and x.data_ptr() % 16 == 0):
+        return Subsample2Fn.apply(x)
+    return F.max_pool2d(x, 1, 2)
+
+
 def down2_sum(g: torch.Tensor, add: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Gradient of the 2x nearest upsampling: each 2 x 2 block summed (+ ``add``, a second
     gradient of the same tensor), NHWC memory kept -- one pass (csrc/epilogue.hip

@@ -7,6 +7,7 @@ import types
 
 import pytest
 import torch
+import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -286,3 +287,18 @@ def test_fused_stem_pool_matches_fp32(N, H, W):
     assert got.shape == ref.shape
     err = (got - ref).abs().max().item()
     assert err <= 0.02 * ref.abs().max().item() + 1e-2, err
+
+
+@pytest.mark.parametrize("H,W", [(25, 42), (13, 21), (24, 40)])
+def test_subsample2_matches_maxpool_1x1_stride2(H, W):
+    """FPN P6 (mx_subsample2) forward and backward bit-identical to F.max_pool2d(x, 1, 2)."""
+    from mxtrain.ops.epilogue import subsample2
+    torch.manual_seed(0)
+    x = torch.randn(2, 256, H, W, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ya, yb = subsample2(xa), F.max_pool2d(xb, 1, 2)
+    assert torch.equal(ya, yb)
+    g = torch.randn_like(yb)
+    ya.backward(g)
+    yb.backward(g)
+    assert torch.equal(xa.grad, xb.grad)
