@@ -17,16 +17,16 @@ def pack_weight(wf: torch.Tensor) -> torch.Tensor:
     """[64, 3, 7, 7] -> bf16 [64, 192], K = (channel, kernel row 0..7, kernel column 0..7), the
     eighth row / column zero (csrc/stem.hip's MFMA K layout); cached against the weight's
     storage and version (the folded frozen weight only changes by in-place writes)."""
-    key = (wf.data_ptr(), wf._version, wf.device)
-    hit = _PACK.get(key)
-    if hit is not None:
-        return hit
+    # the cache holds the source tensor itself: an address + version key went stale when a
+    # new weight was allocated where a freed one had been (same address, version 0)
+    hit = _PACK.get("w")
+    if hit is not None and hit[0] is wf and hit[1] == wf._version:
+        return hit[2]
     co = wf.shape[0]
     wp = torch.zeros(co, 3, 8, 8, dtype=torch.float32, device=wf.device)
     wp[:, :, :7, :7] = wf.float()
     wp = wp.reshape(co, 192).to(torch.bfloat16).contiguous()
-    _PACK.clear()
-    _PACK[key] = wp
+    _PACK["w"] = (wf, wf._version, wp)
     return wp
 
 
