@@ -188,13 +188,23 @@ class RPNHead(nn.Module):
         dt = P[0].dtype
         na = self.cls.weight.shape[0]
         x = _PackLevels.apply(lay, *P)
-        t = conv_bias_act(x, cw(self.conv.weight, dt), cw(self.conv.bias, dt), padding=1, relu=True)
+        # the 3x3 conv's ReLU mask is applied by the 1x1's input-gradient store (BlockLink
+        # "mask_in"), so its backward has no mask pass -- and, with the bias gradient summed by
+        # the weight-gradient kernel, no pass over the canvas gradient at all
+        link = BlockLink() if (self.fold_relu and torch.is_grad_enabled()) else None
+        t = conv_bias_act(x, cw(self.conv.weight, dt), cw(self.conv.bias, dt), padding=1, relu=True,
+                          fuse=(link, 0, ()) if link is not None else None)
         pad = (-5 * na) % 8
         w = torch.cat([cw(self.cls.weight, dt), cw(self.box.weight, dt)]
                       + ([cw(self.cls.weight, dt).new_zeros(pad, *self.cls.weight.shape[1:])] if pad else []))
         b = torch.cat([cw(self.cls.bias, dt), cw(self.box.bias, dt)]
                       + ([cw(self.cls.bias, dt).new_zeros(pad)] if pad else []))
-        o = conv_bias_act(t, w.contiguous(memory_format=torch.channels_last), b)
+        w = w.contiguous(memory_format=torch.channels_last)
+        fuse_o = None
+        if link is not None and fused_conv_ok(t, w, b):
+            link.premask[0] = True
+            fuse_o = (link, 1, ("mask_in",))
+        o = conv_bias_act(t, w, b, fuse=fuse_o)
         geo = [(y0, x0, p.shape[2], p.shape[3]) for (y0, x0), p in zip(lay[2], P)]
         if (o.is_cuda and o.dtype == torch.bfloat16 and o.is_contiguous(memory_format=torch.channels_last)
                 and _lib.use_hip(o) and len(geo) <= 8):
@@ -216,6 +226,7 @@ class RPNHead(nn.Module):
         return [(flat[2 * i], flat[2 * i + 1]) for i in range(len(P))]
 
     pack_levels = True
+    fold_relu = True   # A/B switch for the ReLU fold above
 
 
 def level_canvas(shapes):

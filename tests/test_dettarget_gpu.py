@@ -302,3 +302,30 @@ def test_subsample2_matches_maxpool_1x1_stride2(H, W):
     ya.backward(g)
     yb.backward(g)
     assert torch.equal(xa.grad, xb.grad)
+
+
+def test_rpn_head_relu_fold_matches_unfolded():
+    """RPNHead.forward_levels with the 3x3 conv's ReLU applied in the 1x1's input-gradient
+    store (BlockLink mask_in) gives the same gradients as the unfolded head."""
+    from mxtrain.models.maskrcnn import RPNHead
+    torch.manual_seed(0)
+    head = RPNHead(256, 3).to(DEV).to(torch.bfloat16)
+    shapes = [(64, 96), (32, 48), (16, 24), (8, 12), (4, 6)]
+    P = [torch.randn(2, 256, h, w, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+         for h, w in shapes]
+    outs = []
+    for fold in (False, True):
+        head.fold_relu = fold
+        for p in head.parameters():
+            p.grad = None
+        Pg = [p.clone().requires_grad_(True) for p in P]
+        lv = head.forward_levels(Pg)
+        g = torch.Generator(device=DEV).manual_seed(3)
+        loss = sum((l.float() * torch.randn(l.shape, device=DEV, generator=g)).sum()
+                   + (d.float() * torch.randn(d.shape, device=DEV, generator=g)).sum() for l, d in lv)
+        loss.backward()
+        torch.cuda.synchronize()
+        outs.append([p.grad.float().clone() for p in head.parameters()] + [p.grad.float().clone() for p in Pg])
+    head.fold_relu = True
+    for a, b in zip(*outs):
+        assert (a - b).abs().max().item() <= 0.02 * a.abs().max().item() + 1e-3
