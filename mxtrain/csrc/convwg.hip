@@ -49,9 +49,6 @@ struct ConvWg {
   uint32_t xbytes, ybytes;   // sizes of x and dY (buffer resources; < 2 GiB)
   int Cout;              // < the tiles' rows for the narrow 1x1 heads: dY columns past it read
                          // zeros, dW rows past it are not written
-  float* dbp;            // non-null: the bias gradient's partial column sums of dY, [splits][Cout]
-                         // fp32, accumulated by the (tap 0, first Cin block) tiles from the dY
-                         // fragments they already read (no separate column-sum pass over dY)
 };
 
 __device__ __forceinline__ void divmod(int p, int d, float inv, int& q, int& r) {
@@ -173,11 +170,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
   for (int a = 0; a < FM; ++a)
 #pragma unroll
     for (int u = 0; u < FN; ++u) acc[a][u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // bias gradient: the waves of the first Cin column block of tap 0 sum their dY fragments
-  const bool do_db = cp.dbp != nullptr && tap == 0 && n0 == 0 && wn == 0;
-  float dbs[FM];
-#pragma unroll
-  for (int a = 0; a < FM; ++a) dbs[a] = 0.f;
 
   const uint32_t lds0 = lds_addr(smem);
   auto issue = [&](int slot, int) __attribute__((always_inline)) {   // steps issued in order
@@ -220,30 +212,11 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
         const bf16x8 av = cat(tr_read(As, offA[a] + 32 * RA * kk), tr_read(As, offA[a] + 32 * RA * kk + 4 * RA));
 #pragma unroll
         for (int u = 0; u < FN; ++u) acc[a][u] = mfma16(av, b[u], acc[a][u]);
-        if (do_db) {   // row 16 a + i of this wave's dY^T block, 8 of the K-step's pixels
-          float t = 0.f;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) t += __uint_as_float(((uint32_t)(uint16_t)av[j]) << 16);
-          dbs[a] += t;
-        }
       }
     }
     if (++slot == NSLOT) slot = 0;
   }
 
-  if (do_db) {
-    // the 4 lane rows G hold disjoint pixels of row i: sum them, lanes G == 0 store
-#pragma unroll
-    for (int a = 0; a < FM; ++a) {
-      float v = dbs[a];
-      auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-      v = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
-      auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-      v = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
-      const int row = m0 + 16 * FM * wm + 16 * a + i;
-      if (G == 0 && row < cp.Cout) cp.dbp[(size_t)slice * cp.Cout + row] = v;
-    }
-  }
   if (cp.splits > 1) {
     // publish the partial tile; conv_wgrad_reduce sums the slices (spread over the chip)
     constexpr int NR = FM * FN;
@@ -1026,7 +999,6 @@ MX_EXPORT int mx_conv_wgrad(const int64_t* d, float beta, int splits, void* stre
   cp.invOH = 1.f / (float)cp.OH;
   cp.beta = beta;
   const bool defer = (d[5] & 1) != 0;   // the caller batches the split-K reduction (mx_conv_wgrad_reduce_batched)
-  cp.dbp = reinterpret_cast<float*>(d[20]);   // optional bias-gradient partials [splits][Cout]
   const bool ident = cp.taps == 1 && cp.stride == 1 && cp.pad == 0 && cp.OH == cp.IH && cp.OW == cp.IW;
   const dim3 grid(cp.ntiles * splits);
   hipStream_t st = (hipStream_t)stream;

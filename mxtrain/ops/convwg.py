@@ -15,7 +15,7 @@ non-bf16 tensors, CPU) take plain ``F.conv2d`` -- part of the contract, not an e
 from __future__ import annotations
 
 import ctypes
-from typing import Dict, Optional, Tuple
+from typing import Dict, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -218,12 +218,9 @@ def _defer_slab(device, elems: int):
 
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dilation, out=None,
-               beta: float = 0.0, splits: int = 0, db: Optional[torch.Tensor] = None) -> torch.Tensor:
+               beta: float = 0.0, splits: int = 0) -> torch.Tensor:
     """dW [Cout, Cin, KH, KW] (channels_last bf16) of conv2d(x, w) for the output gradient
-    ``dy`` (NHWC bf16); ``out`` given: written (beta 0) or accumulated (beta 1) in place.
-    ``db`` (bf16 [Cout]): also the bias gradient, the column sums of dy, accumulated by the
-    weight-gradient tiles from the dY fragments they read anyway (their [splits][Cout]
-    partials reduced at the step's flush, or right away outside one)."""
+    ``dy`` (NHWC bf16); ``out`` given: written (beta 0) or accumulated (beta 1) in place."""
     Cout, Cin, KH, KW = w_shape
     N, _, IH, IW = x.shape
     _, _, OH, OW = dy.shape
@@ -233,8 +230,6 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dila
         dw = torch.ops.aten.convolution_backward(dy, x, wz, None, list(_pair(stride)), list(_pair(padding)),
                                                  list(_pair(dilation)), False, [0, 0], 1,
                                                  [False, True, False])[1]
-        if db is not None:
-            db.copy_(dy.float().sum((0, 2, 3)).to(db.dtype))
         if out is None:
             return dw.contiguous(memory_format=torch.channels_last)
         return out.add_(dw) if beta else out.copy_(dw)
@@ -260,18 +255,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dila
     d = _DESC_T()
     d[:20] = [dy.data_ptr(), x.data_ptr(), zero.data_ptr(), out.data_ptr(), slab.data_ptr(), defer,
             Cout, Cin, N, OH, OW, IH, IW, KH, KW, _sym(stride), _sym(padding), _sym(dilation), Cout, Cin]
-    part = None
-    if db is not None:
-        assert db.dtype == torch.bfloat16 and db.numel() == Cout and db.is_contiguous()
-        part = defer_colsum(x.device, splits, Cout, db)
-        now = part is None
-        if now:
-            part = torch.empty(splits * Cout, dtype=torch.float32, device=x.device)
-        d[20] = part.data_ptr()
     _lib.call("mx_conv_wgrad", d, float(beta), splits, _lib.stream())
-    if db is not None and now:
-        job = (ctypes.c_int64 * 5)(part.data_ptr(), db.data_ptr(), splits, Cout, 0)
-        _lib.call("mx_colsum_jobs", ctypes.addressof(job), 1, _lib.stream())
     return out
 
 
@@ -393,10 +377,6 @@ SPLIT_MIN_NK = 32
 # step could not reproduce the eager one (scripts/fpn_graph_probe.py).  Now every small
 # convolution stays on the implicit GEMM, split when it has >= 8 K-steps (slices >= 4).
 SMALL_ON_MIOPEN = False   # A/B switch (the former routing)
-
-# bias gradients of ReLU-free convs from the weight-gradient kernel (conv_wgrad ``db``)
-# instead of a separate column-sum pass over dY (A/B switch)
-WGRAD_DB = True
 
 # Cout a multiple of 8 but not of 64 (the RPN head's 16 and the mask logits' 80 channels)
 # runs zero-padded tiles; NARROW = False sends those convs back to MIOpen (A/B switch)

@@ -164,15 +164,7 @@ class ConvBiasActFn(torch.autograd.Function):
         # a premasked gradient already carries this conv's ReLU (the consumer's dgrad store
         # applied it): only the bias gradient, if any, is left -- column sums of g itself
         relu = ctx.relu and not (link is not None and link.premask.get(k))
-        wg_hip = ctx.needs_input_grad[1] and convwg.cout_ok(w.shape[0]) and w.shape[1] % 128 == 0
-        # no ReLU to mask: the weight-gradient kernel also sums the bias gradient from dY
-        fuse_db = (convwg.WGRAD_DB and want_db and not relu and wg_hip and ctx.bdtype == torch.bfloat16
-                   and convwg.deferring())
-        if fuse_db:
-            dy = g if _nhwc(g) else g.contiguous(memory_format=torch.channels_last)
-            db = torch.empty(w.shape[0], dtype=torch.bfloat16, device=g.device)
-        else:
-            dy, db = _bias_act_bwd(g, out, relu, want_db, ctx.bdtype)
+        dy, db = _bias_act_bwd(g, out, relu, want_db, ctx.bdtype)
         if db is not None and db.dtype != ctx.bdtype:
             db = db.to(ctx.bdtype)
         dres = dy if ctx.has_res else None
@@ -196,13 +188,14 @@ class ConvBiasActFn(torch.autograd.Function):
                 join_first = True
         mask = x if ("mask_in" in roles or "mask_prev" in roles) else None
         dx = dw = None
+        wg_hip = ctx.needs_input_grad[1] and convwg.cout_ok(w.shape[0]) and w.shape[1] % 128 == 0
         side = convwg.wgrad_side(dy.device) if wg_hip else None
         if side is not None:   # dW on the side stream, concurrent with dX (joined at the flush)
             Cout, Cin, KH, KW = w.shape
             dw = torch.empty((Cout, KH, KW, Cin), dtype=torch.bfloat16, device=dy.device).permute(0, 3, 1, 2)
             side.wait_stream(torch.cuda.current_stream(dy.device))
             with torch.cuda.stream(side):
-                convwg.conv_wgrad(dy, x, tuple(w.shape), st, pd, dl, out=dw, db=db if fuse_db else None)
+                convwg.conv_wgrad(dy, x, tuple(w.shape), st, pd, dl, out=dw)
             convwg.side_keep(dy, x, dw)
         if ctx.needs_input_grad[0]:
             if convwg.dgrad_supported(w, tuple(x.shape), st, pd, dl) and (add is None or add.data_ptr() % 16 == 0):
@@ -223,7 +216,7 @@ class ConvBiasActFn(torch.autograd.Function):
             raise RuntimeError("BlockLink: residual gradient stashed for a conv without an input gradient")
         if ctx.needs_input_grad[1] and side is None:
             if wg_hip:   # (narrow Cout: zero-padded row tile)
-                dw = convwg.conv_wgrad(dy, x, tuple(w.shape), st, pd, dl, db=db if fuse_db else None)
+                dw = convwg.conv_wgrad(dy, x, tuple(w.shape), st, pd, dl)
             else:
                 dw = torch.ops.aten.convolution_backward(dy, x, w, None, st, pd, dl, False, [0, 0], 1,
                                                          [False, True, False])[1]
