@@ -189,8 +189,7 @@ class RPNHead(nn.Module):
         na = self.cls.weight.shape[0]
         x = _PackLevels.apply(lay, *P)
         # the 3x3 conv's ReLU mask is applied by the 1x1's input-gradient store (BlockLink
-        # "mask_in"), so its backward has no mask pass -- and, with the bias gradient summed by
-        # the weight-gradient kernel, no pass over the canvas gradient at all
+        # "mask_in"), so its backward has no mask pass (only the bias-gradient column sums)
         link = BlockLink() if (self.fold_relu and torch.is_grad_enabled()) else None
         t = conv_bias_act(x, cw(self.conv.weight, dt), cw(self.conv.bias, dt), padding=1, relu=True,
                           fuse=(link, 0, ()) if link is not None else None)
