@@ -106,6 +106,13 @@ class ConvNorm(nn.Module):
         return bn_act(_conv_nobias(x, w, self.conv.stride, self.conv.padding, self.conv.dilation), self.norm,
                       residual=residual, relu=relu)
 
+    def fused_ok(self, x) -> bool:
+        """This conv (frozen norm) would run ConvBiasActFn on input x, honouring a BlockLink."""
+        if self.norm_kind != "frozen" or ConvNorm.calibrating:
+            return False
+        wf, bf = self._folded(self.conv.weight, x.dtype)
+        return fused_conv_ok(x, wf, bf, None, self.conv.stride, self.conv.padding, self.conv.dilation)
+
     def _folded(self, w: torch.Tensor, dt: torch.dtype):
         """FrozenBN folded into the conv: weight * s (per output channel) and bias
         b - mean * s.  The frozen statistics change only through in-place writes
@@ -168,16 +175,27 @@ class Bottleneck(nn.Module):
     # mask pass.  The link travels on the output tensor (``_mx_link``).
     fuse_backward = True
 
+    # projection blocks: the shortcut conv's input gradient is parked too ("stash_dx") and
+    # added in conv1's dgrad store, which then holds the block input's whole gradient and can
+    # apply the previous block's ReLU as in an identity block (autograd's add of the two
+    # input gradients and the previous conv3's mask pass disappear).  The shortcut's backward
+    # always runs before conv1's: both become ready after conv3's, and the engine takes the
+    # later-created node (the shortcut) first; conv1 checks it (ops/epilogue.py).
+    fuse_projection = True
+
     def forward(self, x):
         link = BlockLink() if self.fuse_backward and self.conv1.norm_kind == "frozen" else None
         ident = self.shortcut is None
-        prev = getattr(x, "_mx_link", None) if (link is not None and ident) else None
-        r1 = ("take_res", "mask_prev") if prev is not None else (("take_res",) if ident else ())
+        proj = link is not None and not ident and self.fuse_projection and self.shortcut.fused_ok(x)
+        prev = getattr(x, "_mx_link", None) if (link is not None and (ident or proj)) else None
+        r1 = ("take_res", "mask_prev") if prev is not None else (("take_res",) if (ident or proj) else ())
+        if proj:
+            r1 = r1 + ("take_dx",)
         if prev is not None:
             link.prev = prev
         a1 = self.conv1(x, fuse=(link, 1, r1) if link else None)
         a2 = self.conv2(a1, fuse=(link, 2, ("mask_in",)) if link else None)
-        idt = x if ident else self.shortcut(x)
+        idt = x if ident else self.shortcut(x, fuse=(link, 0, ("stash_dx",)) if proj else None)
         out = self.conv3(a2, residual=idt, relu=True,
                          fuse=(link, 3, ("mask_in", "stash_res") if ident else ("mask_in",)) if link else None)
         if link is not None:

@@ -179,6 +179,9 @@ class ConvBiasActFn(torch.autograd.Function):
         if dres is not None and "stash_res" in roles and link.taker and ctx.needs_input_grad[3]:
             link.stash.append(dres)
             dres = None
+        if "take_dx" in roles and ctx.needs_input_grad[0] and link.taker and not link.stash:
+            # (the projection shortcut's dX must already be parked: see models/resnet.py)
+            raise RuntimeError("BlockLink: conv1 ran before the projection shortcut's backward")
         add = link.stash.pop() if "take_res" in roles and link.stash else None
         join_first = join_last = None
         if "join_dx" in roles:   # (the same sum, fp32 2 x 2 block + bf16 dX, whichever comes first)
@@ -207,6 +210,9 @@ class ConvBiasActFn(torch.autograd.Function):
                     dx = dx + add
                 if mask is not None:
                     dx = torch.where(mask > 0, dx, torch.zeros_like(dx))
+            if "stash_dx" in roles and link.taker and dx is not None:
+                link.stash.append(dx)   # conv1's dgrad store adds it (role "take_dx")
+                dx = None
             if join_first:
                 link.join[k] = dx
                 dx = None

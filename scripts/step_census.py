@@ -47,10 +47,14 @@ def main():
         sel = ", ".join([nc, "start", "end"] + gcol)
         t0 = marks[-2]
         print(f"\n== calls matching {a.detail!r} in the last step (us, {', '.join(gcol)})")
-        for r in con.execute(f"select {sel} from kernels where start >= ? and start < ? order by start", (t0, t1)):
+        rows = list(con.execute(f"select {sel} from kernels where start >= ? and start < ? order by start", (t0, t1)))
+        short = lambda n: n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:40]
+        for idx, r in enumerate(rows):
             if pat.search(r[0]):
-                name = r[0].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:40]
-                print(f"  {(r[2] - r[1]) / 1000.0:8.1f}  {name:40s} {' '.join(str(g) for g in r[3:])}")
+                ctx = " <- ".join(short(rows[j][0])[:28] for j in range(idx - 1, max(idx - 3, -1), -1))
+                nxt = short(rows[idx + 1][0])[:28] if idx + 1 < len(rows) else ""
+                print(f"  {(r[2] - r[1]) / 1000.0:8.1f}  {short(r[0]):40s} {' '.join(str(g) for g in r[3:])}"
+                      f"   [after: {ctx}] [next: {nxt}]")
 
 
 if __name__ == "__main__":

@@ -265,10 +265,22 @@ def test_bottleneck_backward_fusion_matches_unfused(monkeypatch):
         out[fuse] = (y.detach().float(), x.grad.float(),
                      [p.grad.float() for p in blocks.parameters() if p.grad is not None])
     # fused: conv2 + conv3 of all three blocks mask their input, conv1 of the two identity
-    # blocks adds, and the second block's conv1 also masks (the first block's ReLU)
-    assert seen == {"add": 2, "mask": 7}, seen
+    # blocks adds, and the second block's conv1 also masks (the first block's ReLU); the
+    # projection block's conv1 adds its shortcut's dX and masks the second block's ReLU
+    assert seen == {"add": 3, "mask": 8}, seen
     assert torch.equal(out[False][0], out[True][0])
-    _close(out[True][1], out[False][1].cpu())
+    # the input gradient crosses all three blocks, and the fused path rounds each join once
+    # where autograd rounds the dgrad and the add: judge both against an fp32 run of the same
+    # blocks -- the fused gradient must be as close to it as the unfused one
+    import copy
+    b32 = copy.deepcopy(blocks).float()
+    for b in b32:
+        b.fuse_backward = False
+    x32 = x0.float().requires_grad_()
+    b32(x32).backward(gy.float())
+    e_f = (out[True][1] - x32.grad).abs().max().item()
+    e_u = (out[False][1] - x32.grad).abs().max().item()
+    assert e_f <= 1.25 * e_u + 1e-3 * x32.grad.abs().max().item(), (e_f, e_u)
     assert len(out[True][2]) == len(out[False][2]) == 10
     for a, b in zip(out[True][2], out[False][2]):
         _close(a, b.cpu())
@@ -449,3 +461,33 @@ def test_narrow_cout_convs_match_fp32(case):
     _close(xg.grad, xr.grad)
     _close(wg.grad, wr.grad)
     _close(bg.grad, br.grad)
+
+
+def test_projection_block_dx_fold_matches_autograd_add():
+    """Bottleneck.fuse_projection: the projection shortcut's input gradient added in conv1's
+    dgrad store (with the previous block's ReLU applied there too) gives the gradients of
+    autograd's separate add + mask pass."""
+    from mxtrain.models.resnet import Bottleneck
+    torch.manual_seed(0)
+    blk_a = Bottleneck(256, 64).cuda().to(torch.bfloat16)            # identity block
+    blk_b = Bottleneck(256, 128, stride=2).cuda().to(torch.bfloat16)  # projection block
+    x0 = torch.randn(2, 256, 48, 64, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gout = None
+    res = []
+    for fold in (False, True):
+        Bottleneck.fuse_projection = fold
+        for m in (blk_a, blk_b):
+            for p in m.parameters():
+                p.grad = None
+        x = x0.clone().requires_grad_(True)
+        y = blk_b(blk_a(x))
+        if gout is None:
+            gout = torch.randn_like(y)
+        y.backward(gout)
+        torch.cuda.synchronize()
+        res.append([x.grad.float()] + [p.grad.float() for m in (blk_a, blk_b) for p in m.parameters()
+                                       if p.grad is not None])
+    Bottleneck.fuse_projection = True
+    assert len(res[0]) == len(res[1])
+    for a, b in zip(*res):
+        assert (a - b).abs().max().item() <= 0.02 * a.abs().max().item() + 1e-3
