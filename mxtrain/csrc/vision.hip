@@ -1515,6 +1515,49 @@ __global__ __launch_bounds__(256) void merge_topk_kernel(const float* __restrict
   }
 }
 
+// The proposal tail in one launch: per (image, level) problem p = b L + l, NMS survivor j is
+// keep[p][j] (a row of the problem's score-sorted boxes, -1 padded); its score (-inf when
+// padded) and box are read straight from the NMS inputs, ranked across the image's L sorted
+// survivor lists as in merge_topk_kernel (same tie order), and the top `top` written as
+// scores + boxes.  Replaces keep.long(), the validity mask, clamp, two gathers, the -inf fill
+// / select, the merge and the final box gather (9 launches).
+__global__ __launch_bounds__(256) void merge_keep_topk_kernel(const int* __restrict__ keep,
+                                                              const float* __restrict__ scores,
+                                                              const float4* __restrict__ boxes, int L, int pre,
+                                                              int top, float* __restrict__ ov,
+                                                              float4* __restrict__ ob) {
+  __shared__ float lst[kMergeMax];
+  const int b = blockIdx.y, n = L * pre;
+  const size_t p0 = (size_t)b * L * pre;   // this image's first (problem, slot)
+  for (int e = threadIdx.x; e < n; e += 256) {
+    const int l = e / pre;
+    const int k = keep[p0 + e];
+    lst[e] = k >= 0 ? scores[p0 + (size_t)l * pre + k] : -INFINITY;
+  }
+  __syncthreads();
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  const int l = e / pre, j = e - l * pre;
+  const float sv = lst[e];
+  int rank = j;
+  for (int m = 0; m < L; ++m) {
+    if (m == l) continue;
+    const float* a = lst + m * pre;
+    int lo = 0, hi = pre;
+    if (m < l) {
+      while (lo < hi) { const int mid = (lo + hi) >> 1; if (a[mid] >= sv) lo = mid + 1; else hi = mid; }
+    } else {
+      while (lo < hi) { const int mid = (lo + hi) >> 1; if (a[mid] > sv) lo = mid + 1; else hi = mid; }
+    }
+    rank += lo;
+  }
+  if (rank < top) {
+    const int k = keep[p0 + e];
+    ov[(size_t)b * top + rank] = sv;
+    ob[(size_t)b * top + rank] = boxes[p0 + (size_t)l * pre + (k > 0 ? k : 0)];
+  }
+}
+
 // ------------------------------------------------------------------------------ matching
 // per (image, anchor): max IoU over that image's gt boxes and its argmax; per gt: the
 // best IoU over anchors (atomicMax on the float bits -- IoU >= 0).
@@ -2014,6 +2057,18 @@ MX_EXPORT int mx_level_topk_decode(const int64_t* host_rows, int R, int K, const
 
 // ks [B][L][pre]: per (image, list) scores sorted non-increasing; out [B][top] values and
 // flat indices (l * pre + j), ordered as topk_rows(ks.view(B, L * pre), top).  L * pre <= 16384.
+// keep int32 [B * L][pre], scores fp32 [B * L][pre], boxes fp32 [B * L][pre][4] -> ov [B][top],
+// ob [B][top][4] (merge_keep_topk_kernel)
+MX_EXPORT int mx_merge_keep_topk(const int* keep, const float* scores, const void* boxes, int B, int L, int pre,
+                                 int top, float* ov, void* ob, hipStream_t s) {
+  const int n = L * pre;
+  if (B <= 0 || n <= 0) return hipSuccess;
+  if (n > kMergeMax || top > n || (((uintptr_t)boxes | (uintptr_t)ob) & 15)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(merge_keep_topk_kernel, dim3((n + 255) / 256, B), dim3(256), 0, s, keep, scores,
+                     (const float4*)boxes, L, pre, top, ov, (float4*)ob);
+  return hipGetLastError();
+}
+
 MX_EXPORT int mx_merge_sorted_topk(const float* ks, int B, int L, int pre, int top, float* ov, int64_t* oi,
                                    hipStream_t s) {
   const int n = L * pre;

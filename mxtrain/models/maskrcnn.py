@@ -581,15 +581,9 @@ class MaskRCNN(nn.Module):
         if ck not in self._anchor_cache:   # (no host->device copy inside a captured step)
             self._anchor_cache[ck] = torch.tensor(counts, dtype=torch.int32, device=boxes.device).repeat(B)
         cnt = self._anchor_cache[ck]
-        keep, nk = V.batched_nms_sorted(boxes, cnt, cfg.rpn_nms_thresh, pre)
-        valid = keep >= 0
-        ki = keep.clamp(min=0)
-        kb = torch.gather(boxes, 1, ki[..., None].expand(-1, -1, 4))
-        ks = torch.where(valid, torch.gather(scores, 1, ki), torch.full_like(scores, -float("inf")))
-        kb = kb.view(B, L * pre, 4)
-        top = min(post, L * pre)
-        s, i = V.merge_sorted_topk(ks.view(B, L, pre), top)   # (each level's survivors are sorted)
-        b = torch.gather(kb, 1, i[..., None].expand(-1, -1, 4))
+        keep, _ = V.batched_nms_sorted(boxes, cnt, cfg.rpn_nms_thresh, pre, raw=True)
+        # each image's top `post` survivors over its levels (every level's list is sorted)
+        b, s = V.nms_merge_topk(keep, scores, boxes, B, L, min(post, L * pre))
         return b.detach(), s.detach()
 
     # ------------------------------------------------------------------ RoI sampling

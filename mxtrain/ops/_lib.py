@@ -139,6 +139,7 @@ SIGNATURES = {
     "mx_rpn_keys": [P, I, I, P, P, P, P, P, P, I, F, F, P, P, P, P, P, P],
     "mx_rpn_select": [P, P, I, P, P, I, I, I, I, I, P, P, P],
     "mx_merge_sorted_topk": [P, I, I, I, I, P, P, P],
+    "mx_merge_keep_topk": [P, P, P, I, I, I, I, P, P, P],
     "mx_down2_add": [P, P, P, I, I, I, I, P],
     "mx_subsample2": [P, P, I, I, I, I, I, P],
     "mx_colsum_jobs": [P, I, P],

@@ -227,9 +227,11 @@ def _ref_nms_one(boxes, thr, max_out):
     return torch.tensor(keep, dtype=torch.long)
 
 
-def batched_nms_sorted(boxes: torch.Tensor, counts: Optional[torch.Tensor], thr: float, max_out: int):
+def batched_nms_sorted(boxes: torch.Tensor, counts: Optional[torch.Tensor], thr: float, max_out: int,
+                       raw: bool = False):
     """boxes [P, N, 4] sorted by descending score per problem (rows >= counts[p] ignored).
-    Returns (keep [P, max_out] int64 row indices, -1 padded; nkeep [P])."""
+    Returns (keep [P, max_out] int64 row indices, -1 padded; nkeep [P]); ``raw``: the
+    kernel's int32 tensors as they are (no conversion launches)."""
     P, N, _ = boxes.shape
     if _lib.use_hip(boxes) and N <= 4096:
         b = boxes.float().contiguous()
@@ -240,7 +242,7 @@ def batched_nms_sorted(boxes: torch.Tensor, counts: Optional[torch.Tensor], thr:
         nk = torch.empty(P, dtype=torch.int32, device=boxes.device)
         _lib.call("mx_nms", _lib.ptr(b), _lib.ptr(cnt), P, N, float(thr), max_out, _lib.ptr(ws), _lib.ptr(keep),
                   _lib.ptr(nk), _lib.stream())
-        return keep.long(), nk.long()
+        return (keep, nk) if raw else (keep.long(), nk.long())
     keep = torch.full((P, max_out), -1, dtype=torch.long)
     nk = torch.zeros(P, dtype=torch.long)
     for p in range(P):
@@ -421,6 +423,30 @@ def crop_resize_mask_crops(flat: torch.Tensor, table: torch.Tensor, H: int, W: i
 
 # ------------------------------------------------------------------ RPN level top-k + decode
 _TK_CACHE = {}
+
+
+def nms_merge_topk(keep: torch.Tensor, scores: torch.Tensor, boxes: torch.Tensor, B: int, L: int, top: int):
+    """The proposal tail after a batched NMS of B x L score-sorted problems: each image's
+    top ``top`` survivors over its L levels, as (boxes [B, top, 4], scores [B, top]); padded
+    survivors score -inf with the problem's first box.  ``keep`` int32 [B L, pre] (the
+    kernel's raw NMS output, ``batched_nms_sorted(..., raw=True)``); one launch
+    (csrc/vision.hip merge_keep_topk_kernel)."""
+    P, pre = keep.shape
+    if (_lib.use_hip(keep) and keep.dtype == torch.int32 and scores.dtype == torch.float32
+            and boxes.dtype == torch.float32 and L * pre <= 16384 and top <= L * pre and P == B * L):
+        k, sc, bx = keep.contiguous(), scores.contiguous(), boxes.contiguous()
+        ov = torch.empty(B, top, dtype=torch.float32, device=keep.device)
+        ob = torch.empty(B, top, 4, dtype=torch.float32, device=keep.device)
+        _lib.call("mx_merge_keep_topk", _lib.ptr(k), _lib.ptr(sc), _lib.ptr(bx), B, L, pre, top, _lib.ptr(ov),
+                  _lib.ptr(ob), _lib.stream())
+        return ob, ov
+    keep = keep.long()
+    valid = keep >= 0
+    ki = keep.clamp(min=0)
+    kb = torch.gather(boxes, 1, ki[..., None].expand(-1, -1, 4)).view(B, L * pre, 4)
+    ks = torch.where(valid, torch.gather(scores, 1, ki), torch.full_like(scores, -float("inf")))
+    s, i = merge_sorted_topk(ks.view(B, L, pre), top)
+    return torch.gather(kb, 1, i[..., None].expand(-1, -1, 4)), s
 
 
 def merge_sorted_topk(ks: torch.Tensor, top: int):

@@ -329,3 +329,30 @@ def test_rpn_head_relu_fold_matches_unfolded():
     head.fold_relu = True
     for a, b in zip(*outs):
         assert (a - b).abs().max().item() <= 0.02 * a.abs().max().item() + 1e-3
+
+
+def test_nms_merge_topk_matches_torch_tail():
+    """ops/vision.py nms_merge_topk (one launch) against the torch tail it replaces: gathers of
+    the NMS survivors' scores and boxes, -inf padding, the sorted-list merge and the final
+    box gather -- bit-identical."""
+    from mxtrain.ops import vision as V
+    torch.manual_seed(0)
+    B, L, pre, top = 2, 5, 300, 400
+    P = B * L
+    scores = torch.rand(P, pre, device=DEV).sort(1, descending=True).values
+    scores[3, 250:] = -float("inf")
+    c = torch.rand(P, pre, 2, device=DEV) * 500
+    wh = 10 + torch.rand(P, pre, 2, device=DEV) * 60
+    boxes = torch.cat([c, c + wh], -1).contiguous()
+    cnt = torch.full((P,), pre, dtype=torch.int32, device=DEV)
+    keep, _ = V.batched_nms_sorted(boxes, cnt, 0.7, pre, raw=True)
+    b, s = V.nms_merge_topk(keep, scores, boxes, B, L, top)
+    k64 = keep.long()
+    valid = k64 >= 0
+    ki = k64.clamp(min=0)
+    kb = torch.gather(boxes, 1, ki[..., None].expand(-1, -1, 4)).view(B, L * pre, 4)
+    ks = torch.where(valid, torch.gather(scores, 1, ki), torch.full_like(scores, -float("inf")))
+    s_ref, i_ref = V.merge_sorted_topk(ks.view(B, L, pre), top)
+    b_ref = torch.gather(kb, 1, i_ref[..., None].expand(-1, -1, 4))
+    assert torch.equal(s, s_ref)
+    assert torch.equal(b, b_ref)
