@@ -766,14 +766,17 @@ class MaskRCNN(nn.Module):
         if self.mask_head is not None:
             nfg = int(N * cfg.frcnn_fg_ratio)
             fg_rois = rois[:, :nfg]
-            fg_valid = is_fg[:, :nfg].reshape(-1).float()
+            fg_valid = is_fg[:, :nfg].float().reshape(-1)   # (one strided cast, then a view)
             fg_lab = labels[:, :nfg].reshape(-1)
             mfeats = [self._nhwc(p) for p in P_mask[:4]]
             mf = V.roi_align(mfeats, rois5_fg if rois5_fg is not None else self._with_batch(fg_rois), (14, 14),
                              scales)
             ml = self.mask_head(mf)                                               # [R, 80, 28, 28]
             G = (gt_mask_table if gt_mask_table is not None else gt_masks).shape[1]
-            flat_gid = (torch.arange(B, device=images.device)[:, None] * G + gidx[:, :nfg]).reshape(-1)
+            ck = ("gt_base", B, G, str(images.device))
+            if ck not in self._anchor_cache:   # (constant per shape: no arange / mul in the step)
+                self._anchor_cache[ck] = torch.arange(B, device=images.device)[:, None] * G
+            flat_gid = (self._anchor_cache[ck] + gidx[:, :nfg]).reshape(-1)
             if gt_mask_table is not None:
                 tgt_m = V.crop_resize_mask_crops(gt_masks, gt_mask_table.reshape(-1, 5), images.shape[2],
                                                  images.shape[3], fg_rois.reshape(-1, 4), flat_gid, cfg.mask_size)
@@ -782,7 +785,8 @@ class MaskRCNN(nn.Module):
                                             flat_gid, cfg.mask_size)
             # per-RoI mean BCE of the labelled class's mask vs (target >= 0.5), over valid fg RoIs
             out["maskrcnn_loss"] = D.mask_loss(ml, fg_lab, tgt_m, fg_valid)
-        out["total_loss"] = sum(out.values())
+        # one stack + one reduction instead of a chain of scalar adds
+        out["total_loss"] = torch.stack([v.float() for v in out.values()]).sum()
         return out
 
     @torch.no_grad()
