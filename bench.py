@@ -72,7 +72,7 @@ def _child_env(world: int, rank: int, port: int) -> dict:
 
 
 def run_maskrcnn(batch: int, steps: int, warmup: int, world: int = 1, rank: int = 0, port: int = 0,
-                 extra=(), workers: int = 6, timeout: float = 600.0) -> dict:
+                 extra=(), workers: int = 6, timeout: float = 300.0) -> dict:
     """One Mask R-CNN training throughput run -> {"img_s": .., ...} (rank 0) / {"rc": 0} (others).
 
     Every bench rank starts ONE child process (``scripts/bench_maskrcnn.py``) with its own
@@ -80,7 +80,6 @@ def run_maskrcnn(batch: int, steps: int, warmup: int, world: int = 1, rank: int 
     ``port``) -- the reference's Horovod MPIJob shape, one rank per GPU
     (examples/maskrcnn/train-maskrcnn-tensorpack.yaml:7,34).  A child, never an exec: this
     process has initialised the GPU.  The whole-job images/s comes from child rank 0."""
-    import subprocess
     import tempfile
     here = os.path.dirname(os.path.abspath(__file__))
     out = tempfile.mktemp(prefix=f"mx_mrcnn_r{rank}_", suffix=".jsonl")
@@ -88,15 +87,14 @@ def run_maskrcnn(batch: int, steps: int, warmup: int, world: int = 1, rank: int 
            "--steps", str(steps), "--warmup", str(warmup), "--out", out, "--workers", str(workers)] + list(extra)
     t0 = time.time()
     try:
-        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout,
-                           env=_child_env(world, rank, port))
-        if r.returncode != 0:
-            return {"error": f"rank {rank} rc={r.returncode}: " + r.stdout[-400:]}
+        rc, text = _run_child(cmd, world, rank, port, timeout)
+        if rc != 0:
+            return {"error": f"rank {rank} rc={rc}: " + text[-400:]}
         if rank != 0:
             return {"rc": 0}
         rec = json.loads(open(out).read().splitlines()[-1]) if os.path.exists(out) else None
         if rec is None:
-            return {"error": "no result record: " + r.stdout[-300:]}
+            return {"error": "no result record: " + text[-300:]}
         res = {"img_s": rec["value"], "n_gpus": rec.get("n_gpus", world), "steps": steps, "warmup": warmup,
                "wall_s": round(time.time() - t0, 1)}
         if rec.get("graph"):
@@ -127,16 +125,30 @@ def gpt3_layout(world: int):
     return 1, 1, 2 * world
 
 
-def _run_child(cmd, world: int, rank: int, port: int, timeout: float):
-    """One child rank (never an exec: this process has initialised the GPU) -> (rc, stdout)."""
+_CHILDREN: set = set()   # live child processes (the deadline kills their process groups)
+
+
+def _run_child(cmd, world: int, rank: int, port: int, timeout: float, env=None):
+    """One child rank (never an exec: this process has initialised the GPU) -> (rc, stdout).
+    The child leads its own session, so a timeout or the bench deadline ends the child and
+    everything it started (loader workers, Ray-style workers)."""
+    import signal
     import subprocess
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                         env=env if env is not None else _child_env(world, rank, port), start_new_session=True)
+    _CHILDREN.add(p)
     try:
-        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout,
-                           env=_child_env(world, rank, port))
-        return r.returncode, r.stdout
-    except subprocess.TimeoutExpired as e:
-        out = e.stdout.decode() if isinstance(e.stdout, bytes) else (e.stdout or "")
-        return 124, out + f"\n[timeout after {timeout:.0f} s]"
+        out, _ = p.communicate(timeout=max(1.0, timeout))
+        return p.returncode, out
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except OSError:
+            pass
+        out, _ = p.communicate()
+        return 124, (out or "") + f"\n[timeout after {timeout:.0f} s]"
+    finally:
+        _CHILDREN.discard(p)
 
 
 def _last_json(text: str):
@@ -150,7 +162,7 @@ def _last_json(text: str):
     return None
 
 
-def run_gpt3(world: int, rank: int, port: int, steps: int, warmup: int, extra=(), timeout: float = 420.0) -> dict:
+def run_gpt3(world: int, rank: int, port: int, steps: int, warmup: int, extra=(), timeout: float = 300.0) -> dict:
     """BASELINE config 4 phase: every bench rank starts one child rank of a fresh N-rank
     GPT-3 6.7B job (this file, --model gpt3-6.7b, no further phases); child rank 0's JSON
     line is the result."""
@@ -175,7 +187,7 @@ def run_gpt3(world: int, rank: int, port: int, steps: int, warmup: int, extra=()
             "loss": rec.get("loss"), "wall_s": round(time.time() - t0, 1)}
 
 
-def run_resnet(world: int, steps: int, extra=(), timeout: float = 420.0) -> dict:
+def run_resnet(world: int, steps: int, extra=(), timeout: float = 300.0) -> dict:
     """BASELINE config 5 phase (rank 0 only): the Ray-Train-style ResNet-50 launcher
     (mxtrain/workloads/ray/train_resnet50.py, the raytrain chart's workload) with one worker
     per GPU, batch 256 per worker, synthetic ImageNet 224^2; images/s over the steps after
@@ -213,6 +225,84 @@ def _free_port() -> int:
     return p
 
 
+_T_START = time.monotonic()
+_LINE = {"out": None, "printed": False, "rank": 0}   # the one JSON line (rank 0) and whether it went out
+_LINE_LOCK = None
+
+
+def _emit(final: bool = True):
+    """Print the JSON line once (rank 0).  The deadline thread / SIGTERM handler call this
+    with whatever has been measured so far, so a phase that overruns never erases the
+    numbers of the phases before it."""
+    with _LINE_LOCK:
+        if _LINE["printed"] or _LINE["rank"] != 0 or _LINE["out"] is None:
+            return
+        _LINE["printed"] = True
+        if not final:
+            _LINE["out"]["deadline"] = "bench wall budget reached: later phases cut short"
+        print(json.dumps(_LINE["out"]), flush=True)
+
+
+def _deadline(reason: str):
+    """Budget exhausted (or SIGTERM): emit the line, end every child process group, exit."""
+    import signal
+    print(f"[bench] {reason}: printing the measured fields and exiting", file=sys.stderr, flush=True)
+    _emit(final=False)
+    for p in list(_CHILDREN):
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except OSError:
+            pass
+    os._exit(0)
+
+
+def _arm_deadline(budget_s: float):
+    """Hard stop at the wall budget (a thread, so it fires while the main thread sits in a
+    child wait or a collective) and on SIGTERM from the driver."""
+    import signal
+    import threading
+    global _LINE_LOCK
+    _LINE_LOCK = threading.Lock()
+    left = budget_s - (time.monotonic() - _T_START)
+    t = threading.Timer(max(1.0, left), _deadline, args=("wall budget reached",))
+    t.daemon = True
+    t.start()
+    try:
+        signal.signal(signal.SIGTERM, lambda *_: _deadline("SIGTERM"))
+    except ValueError:   # (not the main thread)
+        pass
+
+
+class _Phases:
+    """Per-phase wall budget: rank 0 decides each phase's child timeout (its own limit, cut
+    to what is left of --budget-s minus a reserve for the phases' result exchange) and
+    every rank follows that decision (host-only gloo group), so all ranks skip or run a
+    phase together."""
+
+    def __init__(self, budget_s: float, world: int, rank: int, ctrl, min_s=None):
+        self.budget_s, self.world, self.rank, self.ctrl = budget_s, world, rank, ctrl
+        self.min_s = min_s
+        self.skipped = {}
+
+    def left(self) -> float:
+        return self.budget_s - (time.monotonic() - _T_START)
+
+    def timeout(self, name: str, own: float, minimum: float, reserve: float = 15.0):
+        """-> the child timeout for this phase, or None to skip it (agreed on all ranks)."""
+        import torch.distributed as dist
+        minimum = self.min_s if self.min_s is not None else minimum
+        t = min(own, self.left() - reserve)
+        t = t if t >= minimum else -1.0
+        if self.world > 1:
+            box = [t]
+            dist.broadcast_object_list(box, src=0, group=self.ctrl)
+            t = box[0]
+        if t < 0:
+            self.skipped[name] = f"skipped: budget ({max(0.0, self.left()):.0f} s left of {self.budget_s:.0f})"
+            return None
+        return t
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,6 +318,8 @@ def main():
     ap.add_argument("--pp", type=int, default=1)
     ap.add_argument("--cp", type=int, default=1, help="Ulysses context-parallel size (sequence split)")
     ap.add_argument("--seq-length", type=int, default=None, help="override the model's sequence length")
+    ap.add_argument("--num-layers", type=int, default=None,
+                    help="override the model's depth (tests / memory rehearsals; the bench line says so)")
     ap.add_argument("--num-experts", type=int, default=0, help="MoE: experts per MoE layer (every 2nd layer)")
     ap.add_argument("--ep", type=int, default=1, help="MoE expert-parallel size")
     ap.add_argument("--topk", type=int, default=1)
@@ -268,12 +360,37 @@ def main():
                          "probe, then a bit-exact check against RCCL and a timing of both per message "
                          "size on the live group, agreed on every rank; any failure -> RCCL everywhere. "
                          "The per-size decision is recorded in the JSON line (config.collectives)")
+    ap.add_argument("--budget-s", type=float, default=float(os.environ.get("MXTRAIN_BENCH_BUDGET_S", "540")),
+                    help="whole-run wall budget (s, from process start).  Each child phase gets "
+                         "min(its own timeout, what is left); phases that no longer fit are recorded as "
+                         "'skipped: budget'; at the budget the line is printed with what was measured")
+    ap.add_argument("--preflight-timeout", type=float, default=150.0,
+                    help="wall limit of the xGMI preflight children (N > 1, --xgmi 1/auto)")
+    ap.add_argument("--min-phase-s", type=float, default=None, help=argparse.SUPPRESS)   # tests
+    ap.add_argument("--test-hang", choices=["start", "after-gpt"], default=None, help=argparse.SUPPRESS)
     ap.add_argument("--lib-set", action="append", default=[], metavar="SETTER=INT",
                     help="call a kernel-library A/B setter before the run (e.g. mx_gemm_nt_prio=1)")
     args = ap.parse_args()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    rank_env = int(os.environ.get("RANK", "0"))
+    _LINE["rank"] = rank_env
+    _arm_deadline(args.budget_s)
+    if args.test_hang == "start":   # (tests: a phase child that never finishes)
+        time.sleep(3600)
     if args.xgmi is None:
-        args.xgmi = "auto" if int(os.environ.get("WORLD_SIZE", "1")) > 1 else "0"
+        args.xgmi = "auto" if world_env > 1 else "0"
     os.environ.setdefault("MXTRAIN_XGMI", args.xgmi)
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    # xGMI preflight: the direct peer-memory kernels are proven in throwaway children
+    # BEFORE this process touches its GPU (mxtrain/parallel/preflight.py); any failure on
+    # any rank -> MXTRAIN_XGMI=0 (RCCL) on every rank, with the reason in the line
+    from mxtrain.parallel import preflight as _pre
+    pre = None
+    if _pre.should_run(world_env, os.environ["MXTRAIN_XGMI"]):
+        pre = _pre.run_preflight(world_env, rank_env, timeout_s=args.preflight_timeout)
+        if rank_env == 0:
+            print(f"[bench] xGMI preflight: {pre}", file=sys.stderr, flush=True)
 
     import torch
     import torch.distributed as dist
@@ -282,7 +399,6 @@ def main():
         if torch.cuda.is_available():   # (CPU / gloo rehearsal runs: tests/test_bench_cpu.py)
             torch.cuda.synchronize()
 
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from mxtrain.models.gpt import GPT_CONFIGS, GPTConfig
     from mxtrain.parallel import state as pstate
     from mxtrain.training import GPTTrainer, TrainConfig, synthetic_batch
@@ -292,6 +408,13 @@ def main():
     world = ps.world_size
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    ctrl = dist.new_group(backend="gloo") if world > 1 else None   # host-only phase decisions / waits
+    phases = _Phases(args.budget_s, world, ps.rank, ctrl, args.min_phase_s)
+    if ps.rank == 0:   # what the deadline prints if the headline phase itself never ends
+        _LINE["out"] = {"metric": "tokens/sec Megatron-DeepSpeed GPT-2 345M pretrain (DP+ZeRO-1)", "value": None,
+                        "unit": "tokens/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+                        "error": "GPT phase did not finish within the budget"}
     torch.backends.cuda.matmul.allow_tf32 = False
     try:
         torch.backends.cuda.preferred_blas_library("hipblaslt")
@@ -309,6 +432,8 @@ def main():
     if args.seq_length:
         mcfg.update(seq_length=args.seq_length,
                     max_position_embeddings=max(args.seq_length, mcfg.get("max_position_embeddings", 0)))
+    if args.num_layers:
+        mcfg.update(num_layers=args.num_layers)
     if args.num_experts > 1:
         mcfg.update(num_experts=args.num_experts, moe_topk=args.topk)
     cfg = GPTConfig(**mcfg)
@@ -404,21 +529,33 @@ def main():
             "mfu_bf16_dense_2.5pf": round(flops / world / 2.5e15, 4),
             "loss": round(float(loss.item()), 4) if loss is not None else None,
         }
+        if args.num_layers:
+            out["config"]["num_layers"] = cfg.num_layers
+        if pre is not None:
+            out["config"]["xgmi_preflight"] = pre
         if graph_err:
             out["graph_error"] = graph_err
         if use_graph and getattr(tr, "graph_census", None):
             out["graph_nodes"] = tr.graph_census
     else:
         out = None
-    if not args.no_maskrcnn:
-        # BASELINE.json metric, part 2: Mask R-CNN images/s with the same N GPUs, outside
-        # the GPT timed window.  The GPT model is freed first; every rank then runs one child.
-        del tr, tokens, labels
+    _LINE["out"] = out   # from here on the deadline prints at least the headline fields
+    if args.test_hang == "after-gpt":   # (tests: a stuck later phase; the deadline must print)
+        time.sleep(3600)
+
+    def _free_gpt():
+        nonlocal tr, tokens, labels
+        tr = tokens = labels = None
         import gc
         gc.collect()
         if torch.cuda.is_available():
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
+
+    if not args.no_maskrcnn:
+        # BASELINE.json metric, part 2: Mask R-CNN images/s with the same N GPUs, outside
+        # the GPT timed window.  The GPT model is freed first; every rank then runs one child.
+        _free_gpt()
         batches = [int(b) for b in args.maskrcnn_batches.split(",") if b]
         sw = [tuple(int(v) for v in p.split(":")) for p in args.maskrcnn_steps.split(",")]
         ports = [_free_port() for _ in batches] if ps.rank == 0 else None
@@ -429,74 +566,81 @@ def main():
         res = {}
         for i, b in enumerate(batches):
             st, wu = sw[min(i, len(sw) - 1)]
+            tmo = phases.timeout(f"maskrcnn_{b}img", 300.0, 45.0)
+            if tmo is None:
+                res[b] = {"error": phases.skipped[f"maskrcnn_{b}img"]}
+                continue
             res[b] = run_maskrcnn(b, st, wu, world=world, rank=ps.rank, port=ports[i],
-                                  extra=shlex.split(args.maskrcnn_args), workers=args.maskrcnn_workers)
+                                  extra=shlex.split(args.maskrcnn_args), workers=args.maskrcnn_workers,
+                                  timeout=tmo)
             if "error" in res[b]:
                 print(f"maskrcnn {b} img/GPU: {res[b]['error']}", file=sys.stderr, flush=True)
-        if world > 1:   # a failed child on any rank is reported by rank 0
-            errs = [None] * world
-            dist.all_gather_object(errs, {b: r.get("error") for b, r in res.items() if r.get("error")})
-            for r_, e in enumerate(errs):
-                for b, msg in (e or {}).items():
-                    if ps.rank == 0 and "error" not in res[b]:
-                        res[b] = {"error": msg}
-        if out is not None:
-            for b in batches:
+            if world > 1:   # a failed child on any rank is reported by rank 0
+                errs = [None] * world
+                dist.all_gather_object(errs, res[b].get("error"), group=ctrl)
+                if ps.rank == 0 and "error" not in res[b] and any(errs):
+                    res[b] = {"error": next(e for e in errs if e)}
+            if out is not None:
                 out[f"maskrcnn_img_s_{b}img"] = res[b].get("img_s")
-            out["maskrcnn_config"] = {
-                "model": "Mask R-CNN R50-FPN (tensorpack layout)", "n_gpus": world, "dtype": "bf16",
-                "data": "synthetic COCO-shaped 800x<=1333, random-init weights", "unit": "images/s (whole job)",
-                "parallelism": f"dp{world} (one child rank per GPU, bucketed gradient all-reduce)",
-                "conv_search": "MIOpen find (in-repo find-db) + implicit-GEMM HIP convolutions",
-                "step": "whole-step hipGraph replay (gradient all-reduces captured at N > 1)",
-                **{f"{b}img": {k: v for k, v in res[b].items() if k != "img_s"} for b in batches}}
+                out.setdefault("maskrcnn_config", {
+                    "model": "Mask R-CNN R50-FPN (tensorpack layout)", "n_gpus": world, "dtype": "bf16",
+                    "data": "synthetic COCO-shaped 800x<=1333, random-init weights", "unit": "images/s (whole job)",
+                    "parallelism": f"dp{world} (one child rank per GPU, bucketed gradient all-reduce)",
+                    "conv_search": "MIOpen find (in-repo find-db) + implicit-GEMM HIP convolutions",
+                    "step": "whole-step hipGraph replay (gradient all-reduces captured at N > 1)"})
+                out["maskrcnn_config"][f"{b}img"] = {k: v for k, v in res[b].items() if k != "img_s"}
     if not args.no_extra_configs:
         # BASELINE.json configs 4 and 5, each a fresh child job on the same N GPUs after the
         # headline phases (outside every timed window above)
-        if args.no_maskrcnn:   # (else the GPT-2 model was freed before the Mask R-CNN runs)
-            del tr, tokens, labels
-            import gc
-            gc.collect()
-            if torch.cuda.is_available():
-                torch.cuda.synchronize()
-                torch.cuda.empty_cache()
-        ctrl = dist.new_group(backend="gloo") if world > 1 else None   # host-only waits
+        if tr is not None:
+            _free_gpt()
         port = _free_port() if ps.rank == 0 else None
         if world > 1:
             box = [port]
-            dist.broadcast_object_list(box, src=0)
+            dist.broadcast_object_list(box, src=0, group=ctrl)
             port = box[0]
         st, wu = (int(v) for v in args.extra_steps.split(":"))
-        g3 = run_gpt3(world, ps.rank, port, st, wu, extra=shlex.split(args.gpt3_args))
-        if "error" in g3:
-            print(f"gpt3-6.7b: {g3['error']}", file=sys.stderr, flush=True)
-        if world > 1:
-            errs = [None] * world
-            dist.all_gather_object(errs, g3.get("error"), group=ctrl)
-            if ps.rank == 0 and "error" not in g3 and any(errs):
-                g3 = {"error": next(e for e in errs if e)}
-        rn = run_resnet(world, args.resnet_steps, extra=shlex.split(args.resnet_args)) if ps.rank == 0 else None
-        if rn is not None and "error" in rn:
-            print(f"resnet50: {rn['error']}", file=sys.stderr, flush=True)
-        if world > 1:
-            dist.barrier(group=ctrl)   # the other ranks idle on the host while rank 0's workers run
+        tmo = phases.timeout("gpt3", 300.0, 60.0)
+        if tmo is None:
+            g3 = {"error": phases.skipped["gpt3"]}
+        else:
+            g3 = run_gpt3(world, ps.rank, port, st, wu, extra=shlex.split(args.gpt3_args), timeout=tmo)
+            if "error" in g3:
+                print(f"gpt3-6.7b: {g3['error']}", file=sys.stderr, flush=True)
+            if world > 1:
+                errs = [None] * world
+                dist.all_gather_object(errs, g3.get("error"), group=ctrl)
+                if ps.rank == 0 and "error" not in g3 and any(errs):
+                    g3 = {"error": next(e for e in errs if e)}
         if out is not None:
-            tp, pp, gb = gpt3_layout(world)
             out["gpt3_6.7b_tok_s"] = g3.get("tok_s")
             out["gpt3_6.7b_config"] = {
                 "model": "gpt3-6.7b (32 x 4096, 32 heads, seq 2048)", "n_gpus": world, "dtype": "bf16",
                 "data": "synthetic tokens, random-init weights", "unit": "tokens/s (whole job)",
                 "optimizer": "ZeRO-1 AdamW + clip 1.0", "dropout": "0.1 / 0.1",
                 **{k: v for k, v in g3.items() if k != "tok_s"}}
+        tmo = phases.timeout("resnet50", 300.0, 45.0)
+        rn = None
+        if tmo is None:
+            rn = {"error": phases.skipped["resnet50"]}
+        elif ps.rank == 0:
+            rn = run_resnet(world, args.resnet_steps, extra=shlex.split(args.resnet_args), timeout=tmo)
+            if "error" in rn:
+                print(f"resnet50: {rn['error']}", file=sys.stderr, flush=True)
+        if world > 1 and tmo is not None:
+            dist.barrier(group=ctrl)   # the other ranks idle on the host while rank 0's workers run
+        if out is not None:
             out["resnet50_img_s"] = (rn or {}).get("img_s")
             out["resnet50_config"] = {
                 "model": "ResNet-50 (BatchNorm), Ray-Train + Lightning launcher", "n_gpus": world,
                 "dtype": "bf16 autocast, channels_last", "data": "synthetic ImageNet 224x224, random-init weights",
                 "unit": "images/s (whole job)", **{k: v for k, v in (rn or {}).items() if k != "img_s"}}
     if out is not None:
-        print(json.dumps(out), flush=True)
+        out["bench_wall_s"] = round(time.monotonic() - _T_START, 1)
+        out["budget_s"] = args.budget_s
+    _emit()
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=ctrl)
         dist.destroy_process_group()
 
 

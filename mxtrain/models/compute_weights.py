@@ -368,12 +368,12 @@ class FlatMaster:
             def __enter__(self_):
                 if torch.is_grad_enabled():
                     fm._dp_reset()
-                    if fm.cuda:
-                        from ..ops import convwg
-                        convwg.defer_begin()   # the step's weight-gradient reductions: one launch
                     outs = []
                     for k, (tb, te, _, _) in enumerate(fm.buckets):
                         outs.extend(_FlatCast.apply(fm, k, *fm.params[tb:te]))
+                    if fm.cuda:   # the step's weight-gradient reductions: one launch
+                        from ..ops import convwg
+                        convwg.defer_begin([o.data_ptr() for o in outs])
                 else:
                     fm.ensure_fresh()
                     outs = fm.compute_views()
@@ -505,6 +505,9 @@ class FlatMaster:
         device scalar ``self.lr`` was filled already -- graph replay)."""
         if lr is not None:
             self.lr.fill_(float(lr))
+        if self.cuda:   # every deferred reduction launched, deferral off until the next step
+            from ..ops import convwg
+            convwg.defer_flush(keep_on=False)
         self.finish_grads()
         if self.cuda:
             from ..ops import _lib

@@ -362,6 +362,12 @@ class _FanOut3(torch.autograd.Function):
             a = a.contiguous(memory_format=cl)
         b = gb.contiguous(memory_format=cl) if gb is not None else None
         c = gc.contiguous(memory_format=cl) if gc is not None else None
+        # (.contiguous returns an already-contiguous view as is, whatever its storage offset:
+        # the kernel's 16-B vector loads need aligned b / c as well)
+        if b is not None and b.data_ptr() % 16:
+            b = b.clone(memory_format=cl)
+        if c is not None and c.data_ptr() % 16:
+            c = c.clone(memory_format=cl)
         out = torch.empty(B, H, W, C, dtype=ref.dtype, device=ref.device)
         _lib.call("mx_add3_nhwc", out.data_ptr(), _lib.ptr(a), a.stride(0) if a is not None else 0,
                   a.stride(2) if a is not None else 0, _lib.ptr(b), _lib.ptr(c), B, H, W, C, _lib.stream())

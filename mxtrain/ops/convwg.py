@@ -111,7 +111,7 @@ def _workspace(device, slab_elems: int):
 # arena is sized by the eager steps; a capture that would outgrow it reduces immediately.
 DEFER_WGRAD = True      # module switch (A/B)
 _DEF = {"on": False, "jobs": [], "cjobs": [], "arena": None, "cursor": 0, "total": 0, "peak": 0,
-        "side": None, "side_keep": []}
+        "side": None, "side_keep": [], "uses": {}}
 _DEF_RETIRED = []
 
 
@@ -152,13 +152,34 @@ def _side_join():
     _DEF["side_keep"] = []
 
 
-def defer_begin():
+def defer_begin(keys=()):
+    """Start a deferring step.  ``keys`` are the data pointers of the FlatMaster compute
+    copies: only a gradient of one of those, used by exactly ONE op of this forward
+    (``note_use``), is deferred -- its unfinished dW / db then reaches _FlatCast.backward
+    untouched.  A weight used twice (autograd would sum two unfinished gradients) or one
+    outside the FlatMaster (AccumulateGrad, hooks) is reduced at once."""
     _side_join()
+    if _DEF["jobs"] or _DEF["cjobs"]:   # (a backward that never reached its flush)
+        defer_flush(keep_on=False)
     _DEF["on"] = DEFER_WGRAD
+    _DEF["uses"] = {int(k): 0 for k in keys}
     _DEF["jobs"] = []
     _DEF["cjobs"] = []
     _DEF["cursor"] = 0
     _DEF["total"] = 0
+
+
+def note_use(t) -> None:
+    """Forward of an op whose weight / bias gradient may be deferred: count the use."""
+    if _DEF["on"] and t is not None:
+        k = t.data_ptr()
+        if k in _DEF["uses"]:
+            _DEF["uses"][k] += 1
+
+
+def _deferrable(key) -> bool:
+    return (_DEF["on"] and key is not None and _DEF["uses"].get(key) == 1
+            and torch._C._current_autograd_node() is not None)
 
 
 def defer_flush(keep_on: bool = False):
@@ -188,10 +209,11 @@ def deferring() -> bool:
     return _DEF["on"] and torch._C._current_autograd_node() is not None
 
 
-def defer_colsum(device, nparts: int, C: int, out: torch.Tensor):
+def defer_colsum(device, nparts: int, C: int, out: torch.Tensor, key=None):
     """fp32 [nparts * C] arena region for a bias gradient's column partials, reduced into the
-    bf16 ``out`` at the flush; None when deferral is off (reduce immediately)."""
-    if not deferring():
+    bf16 ``out`` at the flush; None when deferral is off or the bias (``key``: its data
+    pointer) is not a single-use FlatMaster copy (reduce immediately)."""
+    if not _deferrable(key):
         return None
     reg = _defer_slab(device, nparts * C)
     if reg is not None:
@@ -218,9 +240,10 @@ def _defer_slab(device, elems: int):
 
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dilation, out=None,
-               beta: float = 0.0, splits: int = 0) -> torch.Tensor:
+               beta: float = 0.0, splits: int = 0, key=None) -> torch.Tensor:
     """dW [Cout, Cin, KH, KW] (channels_last bf16) of conv2d(x, w) for the output gradient
-    ``dy`` (NHWC bf16); ``out`` given: written (beta 0) or accumulated (beta 1) in place."""
+    ``dy`` (NHWC bf16); ``out`` given: written (beta 0) or accumulated (beta 1) in place.
+    ``key`` (the weight's data pointer, from a backward) allows a deferred split-K reduction."""
     Cout, Cin, KH, KW = w_shape
     N, _, IH, IW = x.shape
     _, _, OH, OW = dy.shape
@@ -245,8 +268,9 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dila
     splits = int(_lib.query("mx_conv_wgrad_splits", T, splits))
     slab, zero = _workspace(x.device, ntiles * splits * 128 * 128 if splits > 1 else 1)
     defer = 0
-    # (only from inside an autograd backward: a direct call never waits for a flush)
-    if splits > 1 and _DEF["on"] and torch._C._current_autograd_node() is not None:
+    # (only from inside an autograd backward, for a single-use FlatMaster weight: a direct
+    # call never waits for a flush, and autograd must never sum an unfinished gradient)
+    if splits > 1 and _deferrable(key):
         reg = _defer_slab(x.device, ntiles * splits * 128 * 128)
         if reg is not None:
             slab, defer = reg, 1
@@ -471,6 +495,8 @@ class ConvWgFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, padding, dilation):
         ctx.conf = (list(_pair(stride)), list(_pair(padding)), list(_pair(dilation)))
+        note_use(w)
+        ctx.wkey = w.data_ptr()
         ctx.save_for_backward(x, w)
         return F.conv2d(x, w, None, stride, padding, dilation)
 
@@ -488,7 +514,7 @@ class ConvWgFn(torch.autograd.Function):
                 dx = torch.ops.aten.convolution_backward(g, x, w, None, st, pd, dl, False, [0, 0], 1,
                                                          [True, False, False])[0]
         if ctx.needs_input_grad[1]:
-            dw = conv_wgrad(g, x, tuple(w.shape), st, pd, dl)
+            dw = conv_wgrad(g, x, tuple(w.shape), st, pd, dl, key=ctx.wkey)
         return dx, dw, None, None, None
 
 

@@ -40,6 +40,8 @@ class BiasActFn(torch.autograd.Function):
         ctx.mark_dirty(y)
         ctx.relu, ctx.has_res, ctx.want_db = relu, res is not None, b is not None and b.requires_grad
         ctx.bdtype = b.dtype if b is not None else None
+        convwg.note_use(b)
+        ctx.bkey = b.data_ptr() if b is not None else None
         if relu:
             ctx.save_for_backward(y)
         return y
@@ -55,7 +57,7 @@ class BiasActFn(torch.autograd.Function):
         dy = torch.empty_like(g) if relu else g
         db = torch.empty(C, dtype=torch.bfloat16, device=g.device) if want_db else None
         nparts = _lib.query("mx_bias_act_bwd_parts", M, C)
-        partial, flags = _colsum_partial(g.device, nparts, C, db, ctx.bdtype)
+        partial, flags = _colsum_partial(g.device, nparts, C, db, ctx.bdtype, ctx.bkey)
         out = ctx.saved_tensors[0] if relu else None
         _lib.call("mx_bias_act_bwd", _lib.ptr(g), _lib.ptr(out), _lib.ptr(dy), _lib.ptr(db), _lib.ptr(partial),
                   M, C, int(relu), flags, _lib.stream())
@@ -64,7 +66,7 @@ class BiasActFn(torch.autograd.Function):
         return dy, db, (dy if ctx.has_res else None), None
 
 
-def _bias_act_bwd(g, out, relu: bool, want_db: bool, bdtype=torch.bfloat16):
+def _bias_act_bwd(g, out, relu: bool, want_db: bool, bdtype=torch.bfloat16, bkey=None):
     """(dy, db) of y = act(conv + b (+ res)): the ReLU mask and the bias-gradient column sums
     in one pass (csrc/epilogue.hip)."""
     if not _nhwc(g):
@@ -75,13 +77,13 @@ def _bias_act_bwd(g, out, relu: bool, want_db: bool, bdtype=torch.bfloat16):
     dy = torch.empty_like(g) if relu else g
     db = torch.empty(C, dtype=torch.bfloat16, device=g.device) if want_db else None
     nparts = _lib.query("mx_bias_act_bwd_parts", M, C)
-    partial, flags = _colsum_partial(g.device, nparts, C, db, bdtype)
+    partial, flags = _colsum_partial(g.device, nparts, C, db, bdtype, bkey)
     _lib.call("mx_bias_act_bwd", _lib.ptr(g), _lib.ptr(out), _lib.ptr(dy), _lib.ptr(db), _lib.ptr(partial),
               M, C, int(relu), flags, _lib.stream())
     return dy, db
 
 
-def _colsum_partial(device, nparts: int, C: int, db: Optional[torch.Tensor], bdtype=torch.bfloat16):
+def _colsum_partial(device, nparts: int, C: int, db: Optional[torch.Tensor], bdtype=torch.bfloat16, key=None):
     """(fp32 partial buffer, mx_bias_act_bwd flags): the bias gradient's column sums are
     deferred to the step's batched flush (ops/convwg.py) when that is on, else reduced at once
     (also when the caller casts db right away: a deferred db is only final after the flush)."""
@@ -89,7 +91,7 @@ def _colsum_partial(device, nparts: int, C: int, db: Optional[torch.Tensor], bdt
         return None, 0
     if bdtype != torch.bfloat16:
         return torch.empty(nparts * C, dtype=torch.float32, device=device), 0
-    reg = convwg.defer_colsum(device, nparts, C, db)
+    reg = convwg.defer_colsum(device, nparts, C, db, key)
     if reg is not None:
         return reg, 2
     return torch.empty(nparts * C, dtype=torch.float32, device=device), 0
@@ -152,6 +154,9 @@ class ConvBiasActFn(torch.autograd.Function):
         ctx.relu, ctx.has_res, ctx.res_up = relu, res is not None, res_up
         ctx.bdtype = b.dtype if b is not None else None
         ctx.fuse = fuse
+        convwg.note_use(w)
+        convwg.note_use(b)
+        ctx.wkey, ctx.bkey = w.data_ptr(), (b.data_ptr() if b is not None else None)
         ctx.save_for_backward(x, w, y if relu else None)
         return y
 
@@ -164,7 +169,7 @@ class ConvBiasActFn(torch.autograd.Function):
         # a premasked gradient already carries this conv's ReLU (the consumer's dgrad store
         # applied it): only the bias gradient, if any, is left -- column sums of g itself
         relu = ctx.relu and not (link is not None and link.premask.get(k))
-        dy, db = _bias_act_bwd(g, out, relu, want_db, ctx.bdtype)
+        dy, db = _bias_act_bwd(g, out, relu, want_db, ctx.bdtype, ctx.bkey)
         if db is not None and db.dtype != ctx.bdtype:
             db = db.to(ctx.bdtype)
         dres = dy if ctx.has_res else None
@@ -198,7 +203,7 @@ class ConvBiasActFn(torch.autograd.Function):
             dw = torch.empty((Cout, KH, KW, Cin), dtype=torch.bfloat16, device=dy.device).permute(0, 3, 1, 2)
             side.wait_stream(torch.cuda.current_stream(dy.device))
             with torch.cuda.stream(side):
-                convwg.conv_wgrad(dy, x, tuple(w.shape), st, pd, dl, out=dw)
+                convwg.conv_wgrad(dy, x, tuple(w.shape), st, pd, dl, out=dw, key=ctx.wkey)
             convwg.side_keep(dy, x, dw)
         if ctx.needs_input_grad[0]:
             if convwg.dgrad_supported(w, tuple(x.shape), st, pd, dl) and (add is None or add.data_ptr() % 16 == 0):
@@ -222,7 +227,7 @@ class ConvBiasActFn(torch.autograd.Function):
             raise RuntimeError("BlockLink: residual gradient stashed for a conv without an input gradient")
         if ctx.needs_input_grad[1] and side is None:
             if wg_hip:   # (narrow Cout: zero-padded row tile)
-                dw = convwg.conv_wgrad(dy, x, tuple(w.shape), st, pd, dl)
+                dw = convwg.conv_wgrad(dy, x, tuple(w.shape), st, pd, dl, key=ctx.wkey)
             else:
                 dw = torch.ops.aten.convolution_backward(dy, x, w, None, st, pd, dl, False, [0, 0], 1,
                                                          [False, True, False])[1]
@@ -346,6 +351,9 @@ class ConvTransposeBiasActFn(torch.autograd.Function):
     def forward(ctx, x, w, b, stride: int, relu: bool):
         N, _, H, W = x.shape
         _, Co, KH, KW = w.shape
+        convwg.note_use(w)
+        convwg.note_use(b)
+        ctx.wkey, ctx.bkey = w.data_ptr(), (b.data_ptr() if b is not None else None)
         w = w.contiguous(memory_format=torch.channels_last)
         y = convwg.conv_dgrad(x, w, (N, Co, (H - 1) * stride + KH, (W - 1) * stride + KW), stride, 0, 1,
                               bias=b, relu=relu)
@@ -358,7 +366,8 @@ class ConvTransposeBiasActFn(torch.autograd.Function):
     def backward(ctx, g):
         x, w, out = ctx.saved_tensors
         st = ctx.stride
-        dy, db = _bias_act_bwd(g, out, ctx.relu, ctx.needs_input_grad[2], getattr(ctx, "bdtype", torch.bfloat16))
+        dy, db = _bias_act_bwd(g, out, ctx.relu, ctx.needs_input_grad[2], getattr(ctx, "bdtype", torch.bfloat16),
+                               ctx.bkey)
         if db is not None and db.dtype != ctx.bdtype:
             db = db.to(ctx.bdtype)
         dx = dw = None
@@ -368,7 +377,7 @@ class ConvTransposeBiasActFn(torch.autograd.Function):
             else:
                 dx = F.conv2d(dy, w, None, st)
         if ctx.needs_input_grad[1]:
-            dw = convwg.conv_wgrad(x, dy, tuple(w.shape), st, 0, 1)
+            dw = convwg.conv_wgrad(x, dy, tuple(w.shape), st, 0, 1, key=ctx.wkey)
         return dx, dw, db, None, None
 
 def _deconv_ok(x, w, b, stride) -> bool:

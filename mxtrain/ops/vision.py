@@ -346,7 +346,8 @@ def encode_boxes(ref: torch.Tensor, gt: torch.Tensor, weights=(1.0, 1.0, 1.0, 1.
     """Box-regression targets of gt [N, 4] w.r.t. ref [N, 4] (fp32 [N, 4]); one launch on the
     GPU (csrc/dettarget.hip), the PyTorch formula below otherwise."""
     wx, wy, ww, wh = weights
-    if _lib.use_hip(gt) and gt.dim() == 2 and ref.shape[-1] == 4 and gt.shape[0] > 0:
+    if (_lib.use_hip(gt) and gt.dim() == 2 and gt.shape[-1] == 4 and ref.dim() == 2 and ref.shape[-1] == 4
+            and ref.shape[0] in (1, gt.shape[0]) and gt.shape[0] > 0):
         r = ref.float().contiguous()
         g = gt.float().contiguous()
         out = torch.empty(g.shape[0], 4, dtype=torch.float32, device=g.device)
@@ -433,7 +434,10 @@ def nms_merge_topk(keep: torch.Tensor, scores: torch.Tensor, boxes: torch.Tensor
     (csrc/vision.hip merge_keep_topk_kernel)."""
     P, pre = keep.shape
     if (_lib.use_hip(keep) and keep.dtype == torch.int32 and scores.dtype == torch.float32
-            and boxes.dtype == torch.float32 and L * pre <= 16384 and top <= L * pre and P == B * L):
+            and boxes.dtype == torch.float32 and L * pre <= 16384 and top <= L * pre and P == B * L
+            # (the kernel indexes scores / boxes with keep's row length: NMS inputs of
+            # exactly [B L, pre]; any other width takes the gather path)
+            and tuple(scores.shape) == tuple(keep.shape) and tuple(boxes.shape[:2]) == tuple(keep.shape)):
         k, sc, bx = keep.contiguous(), scores.contiguous(), boxes.contiguous()
         ov = torch.empty(B, top, dtype=torch.float32, device=keep.device)
         ob = torch.empty(B, top, 4, dtype=torch.float32, device=keep.device)

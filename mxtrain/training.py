@@ -92,6 +92,11 @@ class GPTTrainer:
             self._setup_moe(cfg, tcfg, ps, dtype, sched)
         dp_group = ps.grad_group if ps.grad_world > 1 else None
         if dp_group is None and tcfg.force_dp_collectives and dist.is_initialized():
+            # (WORLD is the data group only when there is nothing but data parallelism:
+            # with TP / PP ranks it would reduce gradients across different shards)
+            if dist.get_world_size() != 1:
+                raise ValueError("force_dp_collectives with grad_world == 1 needs a 1-rank job "
+                                 f"(world {dist.get_world_size()}: tp {ps.tp}, pp {ps.pp}, cp {ps.cp})")
             dp_group = dist.group.WORLD
         self.opt = DistributedOptimizer(
             self.flat, dp_group=dp_group, lr=tcfg.lr, force_collectives=tcfg.force_dp_collectives,

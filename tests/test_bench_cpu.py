@@ -77,3 +77,64 @@ def test_bench_two_ranks_gloo_extra_config_fields():
     assert g["n_gpus"] == 2 and g["parallelism"].startswith("dp1_tp2"), g
     assert d["resnet50_img_s"] and d["resnet50_img_s"] > 0, (d.get("resnet50_config"), r.stderr[-2000:])
     assert d["resnet50_config"]["workers"] == 2
+
+
+def _run2(args, env_extra=None, timeout=600, port=29545):
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="2", **(env_extra or {}))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "1", "--model", "gpt-tiny", "--no-tuned-gemm"] + args
+    import time
+    t0 = time.time()
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=REPO)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    return r, lines, time.time() - t0
+
+
+def test_bench_xgmi_preflight_failure_falls_back_to_rccl():
+    """The xGMI preflight runs in throwaway children before the bench ranks touch a GPU; a
+    child that exits non-zero on ONE rank (rank 1 here) must turn the direct kernels off on
+    EVERY rank (MXTRAIN_XGMI=0), with the reason in the line (gloo stand-in children)."""
+    r, lines, _ = _run2(["--no-maskrcnn", "--no-extra-configs"],
+                        {"MXTRAIN_PREFLIGHT_CPU": "1", "MXTRAIN_PREFLIGHT_FAIL_RANK": "1"}, port=29547)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    pre = d["config"]["xgmi_preflight"]
+    assert d["config"]["xgmi_mode"] == "0", d["config"]
+    assert pre["ok"] is False and "rank 1" in pre["reason"] and "rc=3" in pre["reason"], pre
+
+
+def test_bench_xgmi_preflight_success_keeps_auto():
+    r, lines, _ = _run2(["--no-maskrcnn", "--no-extra-configs"], {"MXTRAIN_PREFLIGHT_CPU": "1"}, port=29549)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(lines[0])
+    assert d["config"]["xgmi_preflight"]["ok"] is True and d["config"]["xgmi_mode"] == "auto", d["config"]
+
+
+def test_bench_hung_phase_cannot_erase_headline():
+    """A GPT-3 child that never finishes is cut at the budget: the headline line still comes
+    out (once), the GPT-3 field carries the timeout, and the ResNet phase that no longer
+    fits is recorded as skipped."""
+    r, lines, wall = _run2(["--no-maskrcnn", "--budget-s", "45", "--min-phase-s", "3", "--extra-steps", "1:1",
+                            "--gpt3-args", "--model gpt-tiny --no-tuned-gemm --test-hang start",
+                            "--resnet-args", "--cpu --batch-size 2 --image-size 32 --loader-workers 0"],
+                           port=29551)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["value"] and d["value"] > 0
+    assert d["gpt3_6.7b_tok_s"] is None and "timeout" in d["gpt3_6.7b_config"]["error"], d["gpt3_6.7b_config"]
+    assert "skipped: budget" in d["resnet50_config"]["error"], d["resnet50_config"]
+    assert wall < 45 + 40, wall
+
+
+def test_bench_deadline_prints_measured_fields():
+    """A stuck phase inside the bench ranks themselves: the wall-budget thread prints the
+    line with what was measured (the GPT-2 headline) and ends the job."""
+    r, lines, wall = _run2(["--no-maskrcnn", "--no-extra-configs", "--budget-s", "30", "--test-hang", "after-gpt"],
+                           port=29553)
+    assert len(lines) == 1, (r.stdout, r.stderr[-2000:])
+    d = json.loads(lines[0])
+    assert d["value"] and d["value"] > 0 and "deadline" in d
+    assert wall < 30 + 40, wall

@@ -491,3 +491,62 @@ def test_projection_block_dx_fold_matches_autograd_add():
     assert len(res[0]) == len(res[1])
     for a, b in zip(*res):
         assert (a - b).abs().max().item() <= 0.02 * a.abs().max().item() + 1e-3
+
+
+@pytest.mark.gpu
+def test_deferred_wgrad_shared_weight_matches_undeferred(monkeypatch):
+    """a deferred split-K dW / db is unfinished until the FlatMaster flush, so it
+    must never reach autograd's accumulation.  One FlatMaster compute copy (weight AND bias)
+    feeds two convolutions (autograd sums their gradients) next to a single-use conv that
+    may defer: the flat gradients after the step must match DEFER_WGRAD=False."""
+    import copy
+    from mxtrain.models.compute_weights import FlatMaster, cw
+    from mxtrain.ops import convwg
+    from mxtrain.ops.epilogue import conv_bias_act
+
+    class Shared(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = torch.nn.Conv2d(256, 256, 3, padding=1)
+            self.b = torch.nn.Conv2d(256, 256, 3, padding=1)
+
+        def compute_weight_specs(self):
+            return [(p, None) for p in self.parameters()]
+
+        def forward(self, x):
+            wa, ba = cw(self.a.weight, torch.bfloat16), cw(self.a.bias, torch.bfloat16)
+            wb, bb = cw(self.b.weight, torch.bfloat16), cw(self.b.bias, torch.bfloat16)
+            y1 = conv_bias_act(x, wa, ba, padding=1, relu=True)     # shared: used twice
+            y2 = conv_bias_act(y1, wa, ba, padding=1, relu=True)
+            y3 = conv_bias_act(y2, wb, bb, padding=1, relu=False)   # single use: may defer
+            return y3.float().pow(2).mean()
+
+    torch.manual_seed(0)
+    base = Shared().cuda()
+    x = (torch.randn(2, 256, 64, 96, device="cuda") * 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    grads = {}
+    jobs = {}
+    real_flush = convwg.defer_flush
+
+    def spy(keep_on=False):
+        jobs[cur[0]] = jobs.get(cur[0], 0) + len(convwg._DEF["jobs"]) + len(convwg._DEF["cjobs"])
+        return real_flush(keep_on)
+
+    monkeypatch.setattr(convwg, "defer_flush", spy)
+    cur = [None]
+    for defer in (False, True):
+        cur[0] = defer
+        monkeypatch.setattr(convwg, "DEFER_WGRAD", defer)
+        m = copy.deepcopy(base)
+        opt = torch.optim.SGD(m.parameters(), lr=0.0, momentum=0.0)
+        fm = FlatMaster(m, opt, 0.0)
+        with fm.compute_weights():
+            loss = m(x)
+        loss.backward()
+        fm.step(0.0)
+        torch.cuda.synchronize()
+        grads[defer] = fm.G.detach().clone()
+        assert not convwg._DEF["on"], "deferral must be off after the step"
+    assert jobs[False] == 0 and jobs[True] >= 1, jobs   # the single-use conv did defer
+    torch.testing.assert_close(grads[True], grads[False], rtol=0, atol=0)
