@@ -34,6 +34,8 @@ SIGNATURES = {
     "mx_norm_bwd_rows_per_wave": [I],
     "mx_flash_qmajor_bk": [I, I],
     "mx_flash_kmajor128_variant": [I],
+    # membw.hip (HBM roofline probe, scripts/hbm_probe.py)
+    "mx_membw": [I, I, I, P, P, I64, I, P],
     # graph.hip (host-side hipGraph inspection; no stream argument)
     "mx_graph_census": [P, P, I],
     "mx_graph_memsets_to_kernels": [P],

@@ -24,7 +24,9 @@ charts/machine-learning/training/mpijob-horovod-tensorflow-gpu/values.yaml:64-65
 
 Test hooks (CPU): ``MXTRAIN_PREFLIGHT_CPU=1`` runs the children on gloo (the agreement
 plumbing without a GPU); ``MXTRAIN_PREFLIGHT_FAIL_RANK=r`` makes child rank r exit 3;
-``MXTRAIN_PREFLIGHT_HANG_RANK=r`` makes it sleep past its timeout.
+``MXTRAIN_PREFLIGHT_HANG_RANK=r`` makes it sleep past its timeout.  GPU tests on a one-GPU
+box: ``MXTRAIN_PREFLIGHT_EMU=1`` puts every child on device 0 with the RCCL side of the
+checks emulated on gloo (RCCL refuses two ranks on one GPU).
 """
 from __future__ import annotations
 
@@ -179,6 +181,27 @@ def run_preflight(world: int, rank: int, timeout_s: float = 150.0) -> Dict:
 
 
 # ----------------------------------------------------------------------------- child side
+def _emulated_rccl(world: int, rank: int):
+    import torch
+    import torch.distributed as dist
+
+    def emu(self, op, o, i):
+        if op == "all_reduce":
+            c = o.cpu()
+            dist.all_reduce(c)
+        elif op == "reduce_scatter":
+            parts = [x.clone() for x in i.cpu().chunk(world)]
+            for x in parts:
+                dist.all_reduce(x)
+            c = parts[rank]
+        else:
+            lst = [torch.empty_like(i.cpu()) for _ in range(world)]
+            dist.all_gather(lst, i.cpu())
+            c = torch.cat(lst)
+        o.copy_(c)
+    return emu
+
+
 def _child(out: str) -> int:
     import torch
     import torch.distributed as dist
@@ -198,10 +221,17 @@ def _child(out: str) -> int:
         res["why"] = "" if res["ok"] else "gloo all-reduce mismatch"
     else:
         from . import xgmi as X
-        local = int(os.environ.get("LOCAL_RANK", rank))
+        emu = os.environ.get("MXTRAIN_PREFLIGHT_EMU") == "1"
+        local = 0 if emu else int(os.environ.get("LOCAL_RANK", rank))
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if emu:
+            # (tests on a one-GPU box: the ranks share the GPU, which RCCL refuses -- the
+            # reference side of the checks runs on gloo over host copies)
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            X.XGMICommunicator._rccl = _emulated_rccl(world, rank)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         g = dist.group.WORLD
         # RCCL itself first: a failure here is not the xGMI kernels' and is reported as such
         t = torch.full((1024,), float(rank + 1), device=dev)
