@@ -369,7 +369,7 @@ def main():
     ap.add_argument("--min-phase-s", type=float, default=None, help=argparse.SUPPRESS)   # tests
     ap.add_argument("--test-hang", choices=["start", "after-gpt"], default=None, help=argparse.SUPPRESS)
     ap.add_argument("--lib-set", action="append", default=[], metavar="SETTER=INT",
-                    help="call a kernel-library A/B setter before the run (e.g. mx_gemm_nt_prio=1)")
+                    help="call a kernel-library A/B setter before the run (e.g. mx_flash_dropmask_variant=0)")
     args = ap.parse_args()
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rank_env = int(os.environ.get("RANK", "0"))

@@ -255,7 +255,7 @@ constexpr int kBM = 128, kBN = 128, kBK = 64, kNT = 256;
 // and the ring's fill dominates (scripts/conv_ab.py --toggle: 1x1 / Cin 128 forwards 5-15 %
 // faster, the 3x3 Cin 256 ones at P2 and the RPN canvas 14-16 % slower,
 // profiles/r5_s1/conv_ab_bk32.txt)
-int g_conv_fwd_bk32 = 2;
+constexpr int g_conv_fwd_bk32 = 2;
 
 // ================================================================================= forward
 // y[p][co] = act(sum over taps (r, s) and ci of X[pix(p, r, s)][ci] * W[co][r][s][ci] + b[co]
@@ -1123,7 +1123,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_fill_kernel(const ConvDg cp, i
 
 // input-gradient K-step depth: 0 -> 64, 1 -> 32, 2 -> by shape (mx_conv_dgrad, default).
 // (A 4-slot ring of 32-deep steps was 2-11 % slower: profiles/r5_s1/conv_ab_ring_4.txt)
-int g_conv_dgrad_bk32 = 2;
+constexpr int g_conv_dgrad_bk32 = 2;
 
 static void launch_dgrad(ConvDg cp, int splits, hipStream_t st) {
   cp.splits = splits < 1 ? 1 : (splits > cp.nk ? cp.nk : splits);
@@ -1326,17 +1326,3 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   return (int)hipGetLastError();
 }
 
-// forward K-step depth: 1 -> 32 (16-KiB ring slots), 0 -> 64, 2 -> by shape (default);
-// negative: query.  Returns the old value.
-MX_EXPORT int mx_conv_fwd_bk32(int on) {
-  const int old = g_conv_fwd_bk32;
-  if (on >= 0) g_conv_fwd_bk32 = on;
-  return old;
-}
-
-// input-gradient K-step depth (g_conv_dgrad_bk32 above); negative: query.  Returns the old mode.
-MX_EXPORT int mx_conv_dgrad_bk32(int mode) {
-  const int old = g_conv_dgrad_bk32;
-  if (mode >= 0) g_conv_dgrad_bk32 = mode;
-  return old;
-}

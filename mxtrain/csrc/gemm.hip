@@ -55,7 +55,7 @@ struct Batch {
 };
 
 // as gemm_nt.hip g_gemm_nt_prio (MI355X_MICROARCH.md "Two waves per SIMD", items 4 and 9)
-int g_gemm_kk_prio = 3;
+constexpr int g_gemm_kk_prio = 3;
 
 __device__ __forceinline__ Prob pick(const Batch& bt, int t) {
   // constant indices only: a runtime index into the by-value kernel argument would copy it
@@ -360,10 +360,3 @@ MX_EXPORT int mx_gemm_kk(int np, const int64_t* desc, int K, float beta, int var
   }
 }
 
-// A/B: priority / stagger of the 8-wave weight-gradient tiles (g_gemm_kk_prio bits); negative:
-// query.  Returns the old value.
-MX_EXPORT int mx_gemm_kk_prio(int on) {
-  const int old = g_gemm_kk_prio;
-  if (on >= 0) g_gemm_kk_prio = on;
-  return old;
-}

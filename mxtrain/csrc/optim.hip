@@ -163,21 +163,16 @@ __global__ __launch_bounds__(256) void adamw_kernel(
   }
 }
 
-int g_adam_unroll = 1;
-int g_adam_blocks = 1 << 20;   // one 8-element vector per thread (no grid-stride loop): scripts/adam_sweep.py, 355M elements: 1.95 ms at 16384 blocks, 1.85 at 131072
+// one 8-element vector per thread (no grid-stride loop, U = 1): 355M elements 1.95 ms at 16384
+// blocks, 1.85 at 131072; at 5.22 TB/s it sits on the measured 3-read / 3-write HBM roofline
+// (profiles/r6/hbm_roofline.txt)
+constexpr int g_adam_blocks = 1 << 20;
 
 }  // namespace
 
 constexpr int kSumsqParts = 2048;   // blocks of sumsq_kernel = partial slots
 MX_EXPORT int mx_sumsq_nparts() { return kSumsqParts; }
 
-// launch shape of mx_adamw_step (unroll 1|2 vectors per thread-iteration, max blocks)
-MX_EXPORT int mx_adamw_config(int unroll, int blocks) {
-  if (unroll != 1 && unroll != 2) return hipErrorInvalidValue;
-  g_adam_unroll = unroll;
-  if (blocks > 0) g_adam_blocks = blocks;
-  return hipSuccess;
-}
 
 // normsq_out[0] (+)= sum((g*scale)^2); partial must hold mx_sumsq_nparts() floats
 MX_EXPORT int mx_sumsq_bf16(const void* g, int64_t n, float scale, const uint8_t* flags,
@@ -200,11 +195,7 @@ MX_EXPORT int mx_adamw_step(float* master, float* m, float* v, const void* grad,
   int64_t blocks = (n / 8 + 255) / 256;
   if (blocks > g_adam_blocks) blocks = g_adam_blocks;
   if (blocks < 1) blocks = 1;
-  if (g_adam_unroll == 2)
-    hipLaunchKernelGGL(adamw_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, s, master, m, v,
-                       (const uint16_t*)grad, (uint16_t*)param_out, wd_flags, n, hyper, normsq);
-  else
-    hipLaunchKernelGGL(adamw_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, master, m, v,
+  hipLaunchKernelGGL(adamw_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, master, m, v,
                        (const uint16_t*)grad, (uint16_t*)param_out, wd_flags, n, hyper, normsq);
   return hipGetLastError();
 }

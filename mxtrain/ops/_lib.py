@@ -85,7 +85,6 @@ SIGNATURES = {
     # optim.hip
     "mx_sumsq_nparts": [],
     "mx_sumsq_bf16": [P, I64, F, P, P, P, I, P],
-    "mx_adamw_config": [I, I],
     "mx_adamw_step": [P, P, P, P, P, P, I64, P, P, P],
     # flash.hip
     "mx_flash_dropmask": [P, U32, F, I, I, I, I, I, I, P, P, P],
@@ -110,8 +109,6 @@ SIGNATURES = {
     # gemm_nt.hip
     "mx_gemm_nt_tile": [I, I],
     "mx_gemm_nt": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
-    "mx_gemm_nt_prio": [I],
-    "mx_gemm_kk_prio": [I],
     "mx_gemm_nt_stamps": [P, P, P, P, I, I, I, I, I, I, I, P],
     # rope.hip
     "mx_rope": [P, I64, I, I, I, I, I, I, I, P, P, P, I, P],
@@ -155,8 +152,6 @@ SIGNATURES = {
     "mx_rpn_pack": [P, P, P, I, I, I, I, I, P],
     # knobs (one int; return the previous setting)
     "mx_flash_dropmask_variant": [I],
-    "mx_conv_fwd_bk32": [I],
-    "mx_conv_dgrad_bk32": [I],
     "mx_norm_bwd_max_blocks": [I],
 }
 

@@ -91,7 +91,7 @@ def _tickets(device) -> int:
 def _workspace(device, slab_elems: int):
     """(fp32 split-K slab, 256 zero bf16): grown on demand, so the first (eager) steps size
     it before a hipGraph capture records its address."""
-    key = (device, _lib.stream())   # per stream: the side-stream weight gradients run concurrently
+    key = (device, _lib.stream())   # per stream: kernels on two streams never share a workspace
     ws = _WS.get(key)
     if ws is None or ws[0].numel() < slab_elems:
         if ws is not None:
@@ -111,45 +111,8 @@ def _workspace(device, slab_elems: int):
 # arena is sized by the eager steps; a capture that would outgrow it reduces immediately.
 DEFER_WGRAD = True      # module switch (A/B)
 _DEF = {"on": False, "jobs": [], "cjobs": [], "arena": None, "cursor": 0, "total": 0, "peak": 0,
-        "side": None, "side_keep": [], "uses": {}}
+        "uses": {}}
 _DEF_RETIRED = []
-
-
-# Weight gradients on a side stream (FlatMaster steps, i.e. while deferring): a conv's dW
-# GEMM is independent of its dX GEMM and of the earlier layers' backward, and at one image
-# most Mask R-CNN convs fill a fraction of the chip (10-30 us launches), so the two chains
-# overlap (graph branches run concurrently, profiles/r5_s1/graph_branch_probe.txt).  The
-# side stream forks after the conv's output gradient is ready and joins the main stream at
-# the flush, before the optimizer pass reads any gradient; the operands stay referenced
-# until then (their memory must not be reused under the side stream's kernels).
-# OFF: measured slower in the graphed step -- 143.1 vs 153.2 img/s at one image, 288.2 vs
-# 291.5 at four (profiles/r5_s1/mrcnn_ab_wgrad_side_*.txt); the ~60 fork edges cost more
-# than the overlap recovers.
-WGRAD_SIDE = False       # A/B switch
-_SIDE: Dict[torch.device, "torch.cuda.Stream"] = {}
-
-
-def wgrad_side(device):
-    """The side stream for this backward's weight gradients, or None (run inline)."""
-    if not (WGRAD_SIDE and deferring()):
-        return None
-    st = _SIDE.get(device)
-    if st is None:
-        st = _SIDE[device] = torch.cuda.Stream(device=device)
-    _DEF["side"] = st
-    return st
-
-
-def side_keep(*ts):
-    _DEF["side_keep"].extend(ts)
-
-
-def _side_join():
-    st = _DEF.get("side")
-    if st is not None:
-        torch.cuda.current_stream(st.device).wait_stream(st)
-        _DEF["side"] = None
-    _DEF["side_keep"] = []
 
 
 def defer_begin(keys=()):
@@ -158,7 +121,6 @@ def defer_begin(keys=()):
     (``note_use``), is deferred -- its unfinished dW / db then reaches _FlatCast.backward
     untouched.  A weight used twice (autograd would sum two unfinished gradients) or one
     outside the FlatMaster (AccumulateGrad, hooks) is reduced at once."""
-    _side_join()
     if _DEF["jobs"] or _DEF["cjobs"]:   # (a backward that never reached its flush)
         defer_flush(keep_on=False)
     _DEF["on"] = DEFER_WGRAD
@@ -185,7 +147,6 @@ def _deferrable(key) -> bool:
 def defer_flush(keep_on: bool = False):
     """Launch the pending reductions; deferral stays on only if ``keep_on`` (more gradient
     buckets of this backward still to come)."""
-    _side_join()
     _DEF["on"] = _DEF["on"] and keep_on
     for key, fn, width in (("jobs", "mx_conv_wgrad_reduce_batched", 10), ("cjobs", "mx_colsum_jobs", 5)):
         jobs = _DEF[key]

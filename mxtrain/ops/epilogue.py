@@ -197,14 +197,6 @@ class ConvBiasActFn(torch.autograd.Function):
         mask = x if ("mask_in" in roles or "mask_prev" in roles) else None
         dx = dw = None
         wg_hip = ctx.needs_input_grad[1] and convwg.cout_ok(w.shape[0]) and w.shape[1] % 128 == 0
-        side = convwg.wgrad_side(dy.device) if wg_hip else None
-        if side is not None:   # dW on the side stream, concurrent with dX (joined at the flush)
-            Cout, Cin, KH, KW = w.shape
-            dw = torch.empty((Cout, KH, KW, Cin), dtype=torch.bfloat16, device=dy.device).permute(0, 3, 1, 2)
-            side.wait_stream(torch.cuda.current_stream(dy.device))
-            with torch.cuda.stream(side):
-                convwg.conv_wgrad(dy, x, tuple(w.shape), st, pd, dl, out=dw, key=ctx.wkey)
-            convwg.side_keep(dy, x, dw)
         if ctx.needs_input_grad[0]:
             if convwg.dgrad_supported(w, tuple(x.shape), st, pd, dl) and (add is None or add.data_ptr() % 16 == 0):
                 dx = convwg.conv_dgrad(dy, w, tuple(x.shape), st, pd, dl, add=add, mask=mask)
@@ -225,7 +217,7 @@ class ConvBiasActFn(torch.autograd.Function):
                 dx = down2_sum(join_last, dx)
         elif add is not None:
             raise RuntimeError("BlockLink: residual gradient stashed for a conv without an input gradient")
-        if ctx.needs_input_grad[1] and side is None:
+        if ctx.needs_input_grad[1]:
             if wg_hip:   # (narrow Cout: zero-padded row tile)
                 dw = convwg.conv_wgrad(dy, x, tuple(w.shape), st, pd, dl, key=ctx.wkey)
             else:

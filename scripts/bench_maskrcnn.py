@@ -27,7 +27,7 @@ def main():
                     help="whole-step hipGraph replay (train.py --mx-graph; auto = on for 1 GPU)")
     ap.add_argument("--set", action="append", default=[],
                     help="A/B hook: module:attr=int (e.g. mxtrain.models.maskrcnn:MaskRCNN.fused_targets=0) or "
-                         "lib:setter=int (a kernel-library setter, e.g. lib:mx_conv_fwd_bk32=0)")
+                         "lib:setter=int (a kernel-library setter, e.g. lib:mx_flash_dropmask_variant=0)")
     ap.add_argument("extra", nargs="*")
     a = ap.parse_args()
     rank = int(os.environ.get("RANK", os.environ.get("OMPI_COMM_WORLD_RANK", "0")))

@@ -7,7 +7,7 @@ weight gradient of every shape over ITERS calls after warm-up (events), and chec
 builds produce the same outputs (max relative difference printed).
     python scripts/conv_ab.py --a mxtrain/lib/ab/libmxkernels_a.so [--b mxtrain/lib/libmxkernels.so]
         [--rounds 3] [--imgs 4]
-    python scripts/conv_ab.py --toggle mx_conv_fwd_bk32     # one library, A = setter(0), B = setter(1)"""
+    python scripts/conv_ab.py --toggle SETTER     # one library, A = setter(0), B = setter(1)"""
 import argparse
 import json
 import os

@@ -169,11 +169,6 @@ def main():
         ns = O.sumsq_bf16(gg)
         rec("sumsq 355M", timeit(lambda: O.sumsq_bf16(gg, out=ns)), n * 2)
         rec("adamw 355M", timeit(lambda: O.adamw_step(master, m, v_, gg, p, hyper, ns)), n * 28)
-        from mxtrain.ops import _lib
-        for u, b in ((1, 2048), (1, 8192), (2, 2048), (2, 4096), (2, 8192), (1, 16384)):
-            _lib.call("mx_adamw_config", u, b)
-            rec(f"adamw 355M u{u} b{b}", timeit(lambda: O.adamw_step(master, m, v_, gg, p, hyper, ns)), n * 28)
-        _lib.call("mx_adamw_config", 1, 4096)
     if want("gemm"):
         shapes = [("qkv fwd", T, 3 * h, h), ("proj fwd", T, h, h), ("fc1 fwd", T, 4 * h, h),
                   ("fc2 fwd", T, h, 4 * h), ("logits", T, 50304, h)]

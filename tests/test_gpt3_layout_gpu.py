@@ -59,15 +59,25 @@ def _trainer(ps, init_sd, n_local):
 
 
 def _worker(rank, world, port, paths, q):
+    import time
+    t0 = time.time()
+    os.makedirs(paths["logdir"], exist_ok=True)
+    logf = open(os.path.join(paths["logdir"], f"gpt3_layout_r{rank}.log"), "a", buffering=1)
+
+    def log(msg):   # per-rank progress (a long silent run looks hung to the box's watchdog)
+        logf.write(f"[{time.time() - t0:7.1f}s] {msg}\n")
+
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                          LOCAL_RANK="0", MXTRAIN_XGMI="1", MXTRAIN_XGMI_TIMEOUT_S="60", MXTRAIN_XGMI_MAX_MB="256",
+                          LOCAL_RANK="0", MXTRAIN_XGMI="1", MXTRAIN_XGMI_TIMEOUT_S="30", MXTRAIN_XGMI_MAX_MB="256",
                           MXTRAIN_TP_OVERLAP="1")
         from mxtrain.models.gpt import shard_gpt_state
         from mxtrain.parallel import state as pstate
         from mxtrain.parallel import xgmi
         ps = pstate.initialize_model_parallel(tp=2, pp=2, backend="gloo", device_type="cuda")
+        log(f"initialised: tp {ps.tp_rank} pp {ps.pp_rank} dp {ps.dp_rank}")
         init_sd = torch.load(paths["init"], weights_only=True)
+        log("init loaded")
         tok, lab = _data()
         per = N_MICRO // ps.dp
         tok = tok[ps.dp_rank * per:(ps.dp_rank + 1) * per].to(ps.device)
@@ -75,8 +85,11 @@ def _worker(rank, world, port, paths, q):
         torch.cuda.reset_peak_memory_stats()
         # eager
         cfg, tr = _trainer(ps, init_sd, per)
+        la = []
+        for i in range(STEPS):
+            la.append(float(tr.train_step(tok, lab)))
+            log(f"eager step {i}: loss {la[-1]}")
         assert tr.pipeline is not None and tr.pipeline._xp is not None, "1F1B must run on the xGMI p2p channels"
-        la = [float(tr.train_step(tok, lab)) for _ in range(STEPS)]
         tr.sync_params()
         torch.cuda.synchronize()
         pa = {n: p.detach().float().cpu() for n, p in tr.flat.params.items()}
@@ -87,7 +100,10 @@ def _worker(rank, world, port, paths, q):
         _, tg = _trainer(ps, init_sd, per)
         lg = [float(tg.capture(tok, lab, warmup=1))]
         assert tg._graph is not None
-        lg += [float(tg.train_step(tok, lab)) for _ in range(STEPS - 1)]
+        log(f"captured: loss {lg[-1]}")
+        for i in range(STEPS - 1):
+            lg.append(float(tg.train_step(tok, lab)))
+            log(f"replay {i}: loss {lg[-1]}")
         tg.sync_params()
         torch.cuda.synchronize()
         same = all(torch.equal(pa[n], p.detach().float().cpu()) for n, p in tg.flat.params.items())
@@ -102,6 +118,7 @@ def _worker(rank, world, port, paths, q):
         num = sum(float(((pa[n] - t.float()) ** 2).sum()) for n, t in exp.items()) ** 0.5
         den = sum(float(((t.float() - ini[n].float()) ** 2).sum()) for n, t in exp.items()) ** 0.5
         nparams = sum(p.numel() for p in pa.values())
+        log(f"drift {num / max(den, 1e-30):.4f}, bit-identical graph {same}")
         q.put((rank, dict(eager=la, graph=lg, same=same, drift=num / max(den, 1e-30), tp=ps.tp_rank, pp=ps.pp_rank,
                           dp=ps.dp_rank, last=ps.is_last_stage, peak_gib=round(max(peak_eager, torch.cuda.max_memory_allocated()) / 2**30, 2),
                           params_m=round(nparams / 1e6, 1), census=census)))
@@ -111,6 +128,7 @@ def _worker(rank, world, port, paths, q):
         pstate.destroy()
     except Exception:
         import traceback
+        log(traceback.format_exc())
         q.put((rank, {"error": traceback.format_exc()[-3000:]}))
         raise
 
@@ -125,7 +143,8 @@ def test_gpt3_tp2_pp2_dp2_real_shapes(tmp_path):
     ps = ParallelState(device=torch.device("cuda"))
     tr = GPTTrainer(cfg, TrainConfig(micro_batch_size=MICRO, global_batch_size=N_MICRO * MICRO, lr=1e-4), ps)
     init = {k: v.detach().cpu().clone() for k, v in tr.flat.state_dict().items()}
-    paths = {"init": str(tmp_path / "init.pt"), "final": str(tmp_path / "final.pt")}
+    paths = {"init": str(tmp_path / "init.pt"), "final": str(tmp_path / "final.pt"),
+             "logdir": os.path.join(os.environ.get("GRAFT_REPO_ROOT", str(tmp_path)), "gpurun_out")}
     torch.save(init, paths["init"])
     tok, lab = _data()
     ref = [float(tr.train_step(tok.cuda(), lab.cuda())) for _ in range(STEPS)]

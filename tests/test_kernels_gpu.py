@@ -616,32 +616,6 @@ def test_dropmask_layers_match_per_layer_calls(monkeypatch):
     assert runs[0][0] == runs[1][0] and torch.equal(runs[0][1], runs[1][1])
 
 
-@pytest.mark.parametrize("variant,splits", [(0, 1), (6, 1), (2, 2), (6, 2)])
-@pytest.mark.parametrize("mode", [1, 2, 3])
-def test_gemm_wgrad_priority_and_stagger_bit_identical(variant, splits, mode):
-    """mx_gemm_kk_prio (static priority / half-step stagger of waves 4-7) leaves the grouped
-    weight gradient bit-identical."""
-    from mxtrain.ops import _lib
-    from mxtrain.ops.gemm import wgrad_group
-    g = torch.Generator(device="cuda").manual_seed(1)
-    T = 1024
-    dys = [torch.randn(T, M, device="cuda", generator=g).to(torch.bfloat16) for M in (1024, 512)]
-    xs = [torch.randn(T, N, device="cuda", generator=g).to(torch.bfloat16) for N in (1024, 1536)]
-    outs = []
-    old = _lib._fn("mx_gemm_kk_prio")(-1)
-    try:
-        for m in (0, mode):
-            _lib._fn("mx_gemm_kk_prio")(m)
-            gbs = [torch.zeros(dy.shape[1], x.shape[1], device="cuda", dtype=torch.bfloat16) for dy, x in zip(dys, xs)]
-            wgrad_group(list(zip(gbs, dys, xs)), accumulate=False, variant=variant, splits=splits)
-            torch.cuda.synchronize()
-            outs.append(gbs)
-    finally:
-        _lib._fn("mx_gemm_kk_prio")(old)
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
-
-
 # ------------------------------------------------------------------ forward / dgrad GEMMs
 NT_VARIANTS = list(range(9))
 
@@ -685,33 +659,6 @@ def test_gemm_nt_dgrad_epilogues(variant, gelu):
     _close(out, ref, 2e-2, 1e-2, "dx")
     if gelu:
         _close(dbg, db, 0.25, 2e-2, "dbias")
-
-
-@pytest.mark.parametrize("variant", NT_VARIANTS)
-@pytest.mark.parametrize("mode", [1, 2, 3])
-def test_gemm_nt_priority_and_stagger_bit_identical(variant, mode):
-    """mx_gemm_nt_prio: static priority (1) and the half-step stagger of waves 4-7 (2) leave
-    every forward / dgrad output bit-identical (same MFMAs per accumulator, same order)."""
-    from mxtrain.ops import _lib
-    from mxtrain.ops import gemm as Gm
-    bm, bn, _, kok = Gm._nt_tile(variant)
-    M, N, K = 2 * bm, 2 * bn, 448
-    x, w = _bf(torch.randn(M, K)).to(DEV), _bf(torch.randn(N, K) * 0.1).to(DEV)
-    wk = _bf(torch.randn(K, N) * 0.1).to(DEV)
-    b = _bf(torch.randn(N)).to(DEV)
-    outs = []
-    old = _lib._fn("mx_gemm_nt_prio")(-1)
-    try:
-        for m in (0, mode):
-            _lib._fn("mx_gemm_nt_prio")(m)
-            y = Gm.linear_fwd(x, w, b, gelu=True, variant=variant)
-            dx = Gm.linear_dgrad(x[:, :K] @ torch.eye(K, device=DEV, dtype=x.dtype), wk, variant=variant) if kok else None
-            torch.cuda.synchronize()
-            outs.append((y[0].clone(), y[1].clone(), None if dx is None else dx.clone()))
-    finally:
-        _lib._fn("mx_gemm_nt_prio")(old)
-    for a, c in zip(outs[0], outs[1]):
-        assert a is None or torch.equal(a, c)
 
 
 def test_gemm_nt_strided_inputs_and_plan():
