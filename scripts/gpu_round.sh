@@ -45,6 +45,13 @@ for s in $STEPS; do
       cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/${PROF_TAG:-prof}.log; echo "prof rc=$rc"; ok $rc || exit $rc
       python3 scripts/prof_summary.py $(find gpurun_out/${PROF_TAG:-prof} -name "*.db" | head -1) $((${P_STEPS:-10} + 6)) 60 > gpurun_out/${PROF_TAG:-prof}_summary.txt 2>&1
       find gpurun_out/${PROF_TAG:-prof} -name "*.db" -delete ;;
+    rprof)
+      # kernel census of any python script: RPROF_CMD="script.py args", RPROF_STEPS (divisor), RPROF_TAG
+      cd /tmp && export TMPDIR=/tmp
+      timeout -k 10 ${T_PROF:-400} rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/${RPROF_TAG:-rprof}" -o run -- python3 $GRAFT_REPO_ROOT/$RPROF_CMD > "$GRAFT_REPO_ROOT/gpurun_out/${RPROF_TAG:-rprof}.log" 2>&1; rc=$?
+      cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/${RPROF_TAG:-rprof}.log; echo "rprof rc=$rc"; ok $rc || exit $rc
+      python3 scripts/prof_summary.py $(find gpurun_out/${RPROF_TAG:-rprof} -name "*.db" | head -1) ${RPROF_STEPS:-10} 60 > gpurun_out/${RPROF_TAG:-rprof}_summary.txt 2>&1
+      find gpurun_out/${RPROF_TAG:-rprof} -name "*.db" -delete ;;
     gemm)
       timeout -k 10 ${T_GEMM:-400} python scripts/gemm_nt_bench.py > gpurun_out/${GEMM_TAG:-gemm}.txt 2>&1; rc=$?
       tail -20 gpurun_out/${GEMM_TAG:-gemm}.txt; echo "gemm rc=$rc"; ok $rc || exit $rc ;;

@@ -69,7 +69,7 @@ def _worker(rank, world, port, paths, q):
 
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                          LOCAL_RANK="0", MXTRAIN_XGMI="1", MXTRAIN_XGMI_TIMEOUT_S="30", MXTRAIN_XGMI_MAX_MB="256",
+                          LOCAL_RANK="0", MXTRAIN_XGMI="1", MXTRAIN_XGMI_TIMEOUT_S="30", MXTRAIN_XGMI_MAX_MB="640",
                           MXTRAIN_TP_OVERLAP="1")
         from mxtrain.models.gpt import shard_gpt_state
         from mxtrain.parallel import state as pstate
