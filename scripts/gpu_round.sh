@@ -44,10 +44,11 @@ for s in $STEPS; do
       timeout -k 10 ${T_PROF:-400} rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/${PROF_TAG:-prof}" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --gpus 1 --steps ${P_STEPS:-10} --warmup 3 --no-maskrcnn ${PROF_ARGS:-} > "$GRAFT_REPO_ROOT/gpurun_out/${PROF_TAG:-prof}.log" 2>&1; rc=$?
       cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/${PROF_TAG:-prof}.log; echo "prof rc=$rc"; ok $rc || exit $rc
       python3 scripts/prof_summary.py $(find gpurun_out/${PROF_TAG:-prof} -name "*.db" | head -1) $((${P_STEPS:-10} + 6)) 60 > gpurun_out/${PROF_TAG:-prof}_summary.txt 2>&1
+      [ -n "$CENSUS_MARKER" ] && python3 scripts/step_census.py $(find gpurun_out/${PROF_TAG:-prof} -name "*.db" | head -1) --marker "$CENSUS_MARKER" --last $((${P_STEPS:-10} - 2)) --top 60 ${CENSUS_DETAIL:+--detail "$CENSUS_DETAIL"} > gpurun_out/${PROF_TAG:-prof}_census.txt 2>&1
       find gpurun_out/${PROF_TAG:-prof} -name "*.db" -delete ;;
     rprof)
       # kernel census of any python script: RPROF_CMD="script.py args", RPROF_STEPS (divisor), RPROF_TAG
-      cd /tmp && export TMPDIR=/tmp
+      cd /tmp && export TMPDIR=/tmp && export PYTHONPATH="$GRAFT_REPO_ROOT${PYTHONPATH:+:$PYTHONPATH}"
       timeout -k 10 ${T_PROF:-400} rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/${RPROF_TAG:-rprof}" -o run -- python3 $GRAFT_REPO_ROOT/$RPROF_CMD > "$GRAFT_REPO_ROOT/gpurun_out/${RPROF_TAG:-rprof}.log" 2>&1; rc=$?
       cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/${RPROF_TAG:-rprof}.log; echo "rprof rc=$rc"; ok $rc || exit $rc
       python3 scripts/prof_summary.py $(find gpurun_out/${RPROF_TAG:-rprof} -name "*.db" | head -1) ${RPROF_STEPS:-10} 60 > gpurun_out/${RPROF_TAG:-rprof}_summary.txt 2>&1
