@@ -398,7 +398,16 @@ __global__ __launch_bounds__(256) void flash_dropmask_waves_kernel(
 // t takes block 2i+t whole.  The critical path is ~half the heaviest block's tiles.
 // !PAIR (D = 128): one 4-wave workgroup per block (two per CU), heaviest block first.
 
-template <int D, bool CAUSAL, bool DROP, bool DQ, bool PAIR, int BKT = 64>
+// In-kernel keep bits (DGEN, forward only; the measured alternative to the mask pre-pass,
+// profiles/r6/attn_inkernel_dropout_ab.txt): every wave hashes its own 32 rows x 128 keys per
+// tile with drop_stream_bits, bit-identical to the pre-pass images.
+struct DGen {
+  const uint32_t* seed;
+  uint32_t salt, thr16;
+  int hoff, hg;
+};
+
+template <int D, bool CAUSAL, bool DROP, bool DQ, bool PAIR, int BKT = 64, bool DGEN = false>
 __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_eu(2, 2))) void flash_qmajor_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
     const uint16_t* __restrict__ v, int ldq, int ldk, int ldv,
@@ -406,7 +415,7 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
     float* __restrict__ lse, float* __restrict__ delta, uint16_t* __restrict__ dq, int lddq,
     int S, int Hq, int Hkv, const int* __restrict__ klen, float c,
     float oscale /* FWD 1/(1-p); DQ scale/(1-p) */, float dkeep /* 1-p */,
-    const uint64_t* __restrict__ dbits, int NB, int NKT, float* __restrict__ bpart, int ldbp) {
+    const uint64_t* __restrict__ dbits, int NB, int NKT, float* __restrict__ bpart, int ldbp, DGen dg) {
   constexpr int BQ = 128, BK = BKT, NSUB = BK / 32, NKK = D / 16, NDT = D / 32;
   constexpr int RB = D * 2, CPR = D / 8, RPP = 64 / CPR;
   constexpr int TILE = BK * RB, PIECES = TILE / 1024, PPW = PIECES / 4;
@@ -576,6 +585,16 @@ __global__ __launch_bounds__(PAIR ? 512 : 256) __attribute__((amdgpu_waves_per_e
     const int qb_ = (PAIR && CAUSAL && team == 1 && t >= sw) ? blk1 : blk0;
     const int qw_ = qb_ * BQ + 32 * wl;
     if (qw_ >= S) return 0;
+    if constexpr (DGEN) {   // the pre-pass's words for (row block qw_, 128-key tile j), hashed here
+      const uint32_t j = (uint32_t)((tile_of(t) * BK) >> 7);
+      const uint32_t row = (uint32_t)(((long long)b * dg.hg + dg.hoff + hq) * S + qw_ + r);
+      const uint32_t rbase = row * 0x85EBCA6Bu, seed = *dg.seed + dg.salt;
+      const uint32_t lo = drop_stream_bits(rbase, 4 * j, hh, seed, dg.thr16) |
+                          (drop_stream_bits(rbase, 4 * j + 1, hh, seed, dg.thr16) << 8);
+      const uint32_t hi = drop_stream_bits(rbase, 4 * j + 2, hh, seed, dg.thr16) |
+                          (drop_stream_bits(rbase, 4 * j + 3, hh, seed, dg.thr16) << 8);
+      return (uint64_t)lo | ((uint64_t)hi << 32);
+    }
     const uint64_t* row = dbits + ((size_t)(b * Hq + hq) * NB + (qw_ >> 5)) * NKT * 64 + lane;
     return row[(size_t)((tile_of(t) * BK) >> 7) * 64];
   };
@@ -1462,14 +1481,27 @@ hipError_t launch_qmajor(bool causal, bool drop, int S, int B, hipStream_t s,
                          int ldv, const uint16_t* dout, int lddo, uint16_t* o, int ldo, float* lse,
                          float* delta, uint16_t* dq, int lddq, int Hq, int Hkv,
                          const int* klen, float c, float oscale, float dkeep,
-                         const uint64_t* dbits, int NB, int NKT, float* bpart = nullptr, int ldbp = 0) {
+                         const uint64_t* dbits, int NB, int NKT, float* bpart = nullptr, int ldbp = 0,
+                         const DGen* dgen = nullptr) {
   constexpr bool PAIR = D == 64;
   const int nqb = (S + 127) / 128;
   const dim3 grid((PAIR ? (nqb + 1) / 2 : nqb) * Hq * B);
+  const DGen dg = dgen ? *dgen : DGen{nullptr, 0u, 0u, 0, 0};
 #define MX_QM(C, DR, BKT)                                                                              \
-  hipLaunchKernelGGL((flash_qmajor_kernel<D, C, DR, DQ, PAIR, BKT>), grid, dim3(PAIR ? 512 : 256), 0, s, \
-                     q, k, v, ldq, ldk, ldv, dout, lddo, o, ldo, lse, delta, dq, lddq, S, Hq, Hkv,       \
-                     klen, c, oscale, dkeep, dbits, NB, NKT, bpart, ldbp)
+  do {                                                                                                 \
+    if constexpr (!DQ && DR && D == 64) {                                                              \
+      if (dgen) {                                                                                      \
+        hipLaunchKernelGGL((flash_qmajor_kernel<D, C, DR, DQ, PAIR, BKT, true>), grid,                 \
+                           dim3(PAIR ? 512 : 256), 0, s, q, k, v, ldq, ldk, ldv, dout, lddo, o, ldo,     \
+                           lse, delta, dq, lddq, S, Hq, Hkv, klen, c, oscale, dkeep, dbits, NB, NKT,     \
+                           bpart, ldbp, dg);                                                           \
+        break;                                                                                         \
+      }                                                                                                \
+    }                                                                                                  \
+    hipLaunchKernelGGL((flash_qmajor_kernel<D, C, DR, DQ, PAIR, BKT>), grid, dim3(PAIR ? 512 : 256),    \
+                       0, s, q, k, v, ldq, ldk, ldv, dout, lddo, o, ldo, lse, delta, dq, lddq, S, Hq,    \
+                       Hkv, klen, c, oscale, dkeep, dbits, NB, NKT, bpart, ldbp, dg);                  \
+  } while (0)
 #define MX_QM_B(BKT)                                                          \
   {                                                                           \
     if (causal) { if (drop) MX_QM(true, true, BKT); else MX_QM(true, false, BKT); } \
@@ -1645,6 +1677,23 @@ MX_EXPORT int mx_flash_fwd(const void* q, const void* k, const void* v, int ldq,
                                      lse, nullptr, nullptr, 0, Hq, Hkv, klen, c, osc, 1.f,
                                      (const uint64_t*)fwd_bits, NB, NKT);
   return hipErrorInvalidValue;
+}
+
+// A/B only (profiles/r6/attn_inkernel_dropout_ab.txt): the forward with its keep bits hashed
+// in-kernel from (seed, salt, p, h_off, Hg) instead of read from the pre-pass image.  Output
+// bit-identical to mx_flash_fwd with the image of mx_flash_dropmask(seed, salt, p, ...).
+MX_EXPORT int mx_flash_fwd_dgen(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv,
+                                void* o, int ldo, float* lse, int B, int S, int Hq, int Hkv, int D, int causal,
+                                const int* klen, float scale, const uint32_t* seed, uint32_t salt, float p,
+                                int h_off, int Hg, hipStream_t s) {
+  if (Hq % Hkv || S <= 0 || D != 64 || !(p > 0.f) || seed == nullptr) return hipErrorInvalidValue;
+  const float c = scale * 1.4426950408889634f;
+  const int NB = (S + 31) / 32, NKT = (S + 127) / 128;
+  const DGen dg{seed, salt, (uint32_t)(p * 65536.0f + 0.5f), h_off, Hg};
+  return launch_qmajor<64, false>(causal, true, S, B, s, (const uint16_t*)q, (const uint16_t*)k,
+                                  (const uint16_t*)v, ldq, ldk, ldv, nullptr, 0, (uint16_t*)o, ldo, lse, nullptr,
+                                  nullptr, 0, Hq, Hkv, klen, c, (float)(65536.0 / (65536.0 - dg.thr16)), 1.f, nullptr, NB, NKT, nullptr,
+                                  0, &dg);
 }
 
 // delta: fp32 [B, Hq, S] workspace (written by the dQ kernel, read by the dK/dV kernel).

@@ -220,6 +220,70 @@ __global__ __launch_bounds__(128) void embed_bwd_kernel(
   }
 }
 
+// Sort-free deterministic form (no torch.sort of the ids every step: the radix sort, its
+// index copies and an arange cost ~60 us of the GPT-2 step against ~7 us for the scatter,
+// profiles/r6/gpt2_step_census_small_kernels.txt).  A block stages every id in LDS; one wave
+// per token scans them in 64-id chunks with a ballot: a token that has an EARLIER duplicate
+// returns, the first occurrence sums its own row and every later duplicate's row in token
+// order (fixed order: bit-reproducible) into fp32 registers, then adds them to dW once.
+// Random tokens over a 50k vocabulary have ~1 duplicate pair per 25 tokens, so nearly every
+// wave writes one row.  NV 16-B vectors per lane per 512 columns (hidden = 512 NV).
+template <int NV>
+__global__ __launch_bounds__(256) void embed_bwd_scan_kernel(
+    const int64_t* __restrict__ ids, const uint16_t* __restrict__ dout, uint16_t* __restrict__ dw,
+    int ntok, int hidden, int tok_per_block, int64_t vocab_start, int64_t vocab_end) {
+  extern __shared__ int64_t sid[];   // [ntok]
+  for (int t = threadIdx.x; t < ntok; t += blockDim.x) sid[t] = ids[t];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int t0 = blockIdx.x * tok_per_block;
+  const int t1 = min(ntok, t0 + tok_per_block);
+  for (int i = t0 + w; i < t1; i += 4) {
+    const int64_t id = sid[i];
+    if (id < vocab_start || id >= vocab_end) continue;
+    // an earlier duplicate owns this id
+    bool dup = false;
+    for (int c = 0; c < i && !dup; c += 64) {
+      const int k = c + lane;
+      dup = __ballot(k < i && sid[k] == id) != 0ull;
+    }
+    if (dup) continue;
+    float acc[NV][8];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[v][j] = 0.f;
+    for (int c = i & ~63; c < ntok; c += 64) {
+      const int k = c + lane;
+      uint64_t m = __ballot(k >= i && k < ntok && sid[k] == id);
+      while (m) {   // this chunk's duplicates, ascending token order
+        const int kk = c + __builtin_ctzll(m);
+        m &= m - 1;
+        const uint16_t* row = dout + (size_t)kk * hidden + lane * 8;
+        uint4 x[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) x[v] = *reinterpret_cast<const uint4*>(row + 512 * v);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          float f[8];
+          unpack8(x[v], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[v][j] += f[j];
+        }
+      }
+    }
+    uint16_t* drow = dw + (size_t)(id - vocab_start) * hidden + lane * 8;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      float d[8];
+      unpack8(*reinterpret_cast<const uint4*>(drow + 512 * v), d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] += acc[v][j];
+      *reinterpret_cast<uint4*>(drow + 512 * v) = pack8(d);
+    }
+  }
+}
+
 // dwpe[s] += sum_b dout[b*seq + s]
 __global__ __launch_bounds__(256) void pos_bwd_kernel(const uint16_t* __restrict__ dout,
                                                       uint16_t* __restrict__ dwpe, int batch,
@@ -488,6 +552,28 @@ MX_EXPORT int mx_embed_bwd(const int64_t* sorted_ids, const int64_t* perm, const
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(ntok), dim3(128), 0, s, sorted_ids, perm,
                      (const uint16_t*)dout, (uint16_t*)dw, ntok, hidden, vocab_start,
                      vocab_end);
+  return hipGetLastError();
+}
+
+// Sort-free embedding backward (embed_bwd_scan_kernel): ids [ntok] int64 as given.  Returns
+// hipErrorInvalidValue (nothing launched) when the shape is outside the kernel's range
+// (hidden not 512, 1024, 2048 or 4096; ids beyond the LDS stage): the caller sorts instead.
+MX_EXPORT int mx_embed_bwd_scan(const int64_t* ids, const void* dout, void* dw, int ntok, int hidden,
+                                int64_t vocab_start, int64_t vocab_end, hipStream_t s) {
+  if (ntok <= 0 || (size_t)ntok * 8 > 64 * 1024) return hipErrorInvalidValue;
+  constexpr int TPB = 16;   // tokens per block: 4096 tokens -> 256 blocks
+  const dim3 grid((ntok + TPB - 1) / TPB);
+  const size_t lds = (size_t)ntok * 8;
+#define MX_EB(NV) hipLaunchKernelGGL(embed_bwd_scan_kernel<NV>, grid, dim3(256), lds, s, ids, (const uint16_t*)dout, \
+                                     (uint16_t*)dw, ntok, hidden, TPB, vocab_start, vocab_end)
+  switch (hidden) {
+    case 512: MX_EB(1); break;
+    case 1024: MX_EB(2); break;
+    case 2048: MX_EB(4); break;
+    case 4096: MX_EB(8); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef MX_EB
   return hipGetLastError();
 }
 

@@ -60,6 +60,8 @@ SIGNATURES = {
     "mx_bias_swiglu_bwd": [P, P, P, P, P, I, P, I, I, P],
     "mx_embed_fwd": [P, P, P, P, I, I, I, I64, I64, I, P],
     "mx_embed_bwd": [P, P, P, P, I, I, I64, I64, P],
+    "mx_embed_bwd_scan": [P, P, P, I, I, I64, I64, P],
+    "mx_flash_fwd_dgen": [P, P, P, I, I, I, P, I, P, I, I, I, I, I, I, P, F, P, U32, F, I, I, P],
     "mx_pos_embed_bwd": [P, P, I, I, I, P],
     "mx_ce_stats": [P, P, I, I, I64, P, P, P, P],
     "mx_ce_lse": [P, P, P, I, P],

@@ -156,6 +156,12 @@ def embed_bwd(ids, dout, dwte, vocab_start=0):
         acc.index_add_(0, loc[inside], dout.float()[inside])
         dwte.copy_(acc.to(dwte.dtype))
         return dwte
+    if (ids.dtype == torch.int64 and ids.is_contiguous() and dout.is_contiguous() and dwte.is_contiguous()
+            and ids.numel() * 8 <= 64 * 1024 and H in (512, 1024, 2048, 4096)):
+        # one launch, no sort (csrc/fused.hip embed_bwd_scan_kernel)
+        _lib.call("mx_embed_bwd_scan", _lib.ptr(ids), _lib.ptr(dout), _lib.ptr(dwte), ntok, H, vocab_start,
+                  vocab_start + V, _lib.stream())
+        return dwte
     sorted_ids, perm = torch.sort(ids)
     _lib.call("mx_embed_bwd", _lib.ptr(sorted_ids), _lib.ptr(perm), _lib.ptr(dout), _lib.ptr(dwte),
               ntok, H, vocab_start, vocab_start + V, _lib.stream())

@@ -52,6 +52,7 @@ for s in $STEPS; do
       timeout -k 10 ${T_PROF:-400} rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/${RPROF_TAG:-rprof}" -o run -- python3 $GRAFT_REPO_ROOT/$RPROF_CMD > "$GRAFT_REPO_ROOT/gpurun_out/${RPROF_TAG:-rprof}.log" 2>&1; rc=$?
       cd "$GRAFT_REPO_ROOT"; tail -5 gpurun_out/${RPROF_TAG:-rprof}.log; echo "rprof rc=$rc"; ok $rc || exit $rc
       python3 scripts/prof_summary.py $(find gpurun_out/${RPROF_TAG:-rprof} -name "*.db" | head -1) ${RPROF_STEPS:-10} 60 > gpurun_out/${RPROF_TAG:-rprof}_summary.txt 2>&1
+      [ -n "$CENSUS_MARKER" ] && python3 scripts/step_census.py $(find gpurun_out/${RPROF_TAG:-rprof} -name "*.db" | head -1) --marker "$CENSUS_MARKER" --last ${CENSUS_LAST:-10} --top 60 ${CENSUS_DETAIL:+--detail "$CENSUS_DETAIL"} > gpurun_out/${RPROF_TAG:-rprof}_census.txt 2>&1
       find gpurun_out/${RPROF_TAG:-rprof} -name "*.db" -delete ;;
     gemm)
       timeout -k 10 ${T_GEMM:-400} python scripts/gemm_nt_bench.py > gpurun_out/${GEMM_TAG:-gemm}.txt 2>&1; rc=$?

@@ -132,6 +132,39 @@ def test_embedding_fwd_bwd():
     _close(dp, dpr, 3e-2, 1e-2, "pos bwd")
 
 
+@pytest.mark.parametrize("H,ntok,vocab_start", [(1024, 4096, 0), (4096, 2048, 0), (512, 1000, 300), (1024, 8192, 0)])
+def test_embedding_bwd_sort_free(H, ntok, vocab_start):
+    """csrc/fused.hip embed_bwd_scan_kernel (no torch.sort): repeated ids -- in runs, spread
+    over the whole batch, across the 64-id scan chunks -- and ids outside a vocab shard,
+    against the fp32 index_add reference; bit-reproducible from run to run; and the sort
+    path it replaced (accumulation order may differ: bf16 tolerance)."""
+    from mxtrain.ops import _lib
+    V = 3000
+    g = torch.Generator().manual_seed(H + ntok)
+    ids = torch.randint(0, V + vocab_start, (ntok,), generator=g)
+    ids[:70] = 5 + vocab_start            # a run across a chunk boundary
+    ids[100::97] = 11 + vocab_start       # spread duplicates
+    ids[-1] = 5 + vocab_start
+    dout = _bf(torch.randn(ntok, H, generator=g))
+    dw0 = _bf(torch.randn(V, H, generator=g) * 0.1)
+    ref = dw0.clone()
+    Fu.embed_bwd(ids, dout, ref, vocab_start=vocab_start)
+    runs = []
+    for _ in range(2):
+        dw = dw0.to(DEV).clone()
+        Fu.embed_bwd(ids.to(DEV), dout.to(DEV), dw, vocab_start=vocab_start)
+        torch.cuda.synchronize()
+        runs.append(dw.cpu())
+    assert torch.equal(runs[0], runs[1])
+    _close(runs[0], ref, 5e-2, 2e-2, "embed bwd (scan)")
+    # the sort path (still used beyond the scan kernel's range)
+    sdw = dw0.to(DEV).clone()
+    sids, perm = torch.sort(ids.to(DEV))
+    _lib.call("mx_embed_bwd", _lib.ptr(sids), _lib.ptr(perm), _lib.ptr(dout.to(DEV)), _lib.ptr(sdw), ntok, H,
+              vocab_start, vocab_start + V, _lib.stream())
+    _close(runs[0], sdw.cpu(), 5e-2, 2e-2, "scan vs sort")
+
+
 def test_cross_entropy():
     rows, V = 256, 50304
     logits = _bf(3 * torch.randn(rows, V))
@@ -674,3 +707,26 @@ def test_gemm_nt_strided_inputs_and_plan():
     for (M, N, K, km) in [(4096, 3072, 1024, False), (4096, 4096, 1024, False), (4096, 1024, 4096, False),
                           (4096, 1024, 1024, False), (4096, 1024, 3072, True), (4096, 4096, 1024, True)]:
         assert Gm.nt_plan(M, N, K, km) >= 0, (M, N, K, km)
+
+
+@pytest.mark.parametrize("S,causal,hoff", [(1024, True, 0), (200, False, 3), (384, True, 2)])
+def test_flash_fwd_inkernel_dropout_bits_identical(S, causal, hoff):
+    """The A/B variant of the attention forward that hashes its keep bits in-kernel
+    (mx_flash_fwd_dgen) gives exactly the output and lse of the shipping forward fed the
+    pre-pass image (mx_flash_dropmask) for the same (seed, salt, p, head offset)."""
+    from mxtrain.ops import _lib
+    from mxtrain.ops import attention as A
+    B, H, D, p, salt, Hg = 2, 4, 64, 0.1, 77, 9
+    g = torch.Generator(device=DEV).manual_seed(S)
+    qkv = torch.randn(B * S, 3 * H * D, device=DEV, generator=g).to(torch.bfloat16)
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    seed = torch.tensor([4242], dtype=torch.int32, device=DEV)
+    dm = A.dropmask(B, S, H, p, seed, salt, hoff, Hg, causal)
+    o1, lse1, _ = A.attn_fwd(q, k, v, B, S, H, H, D, causal, dmask=dm)
+    o2 = torch.empty_like(o1)
+    lse2 = torch.empty_like(lse1)
+    _lib.call("mx_flash_fwd_dgen", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), q.stride(0), k.stride(0), v.stride(0),
+              _lib.ptr(o2), o2.stride(0), _lib.ptr(lse2), B, S, H, H, D, int(causal), None, 1.0 / D ** 0.5,
+              _lib.ptr(seed), salt, p, hoff, Hg, _lib.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2) and torch.equal(lse1, lse2)
