@@ -202,13 +202,23 @@ def run_resnet(world: int, steps: int, extra=(), timeout: float = 300.0) -> dict
     t0 = time.time()
     try:
         rc, text = _run_child(cmd, 1, 0, 0, timeout)
+        graphed = True
+        if rc != 0 and time.time() - t0 < timeout / 2:
+            # the launcher's hipGraph step failed hard (a crash is not catchable inside the
+            # worker): once more with eager steps, in what is left of the phase's time
+            print(f"resnet50: graphed run failed (rc={rc}), retrying eagerly: {text[-300:]}", file=sys.stderr,
+                  flush=True)
+            env = _child_env(1, 0, 0)
+            env["MXTRAIN_LIGHTNING_GRAPH"] = "0"
+            graphed = False
+            rc, text = _run_child(cmd, 1, 0, 0, timeout - (time.time() - t0), env=env)
         if rc != 0:
             return {"error": f"rc={rc}: " + text[-400:]}
         rec = json.loads(open(out).read().splitlines()[-1]) if os.path.exists(out) else None
         if rec is None or rec.get("value") is None:
             return {"error": "no result record: " + text[-300:]}
         return {"img_s": round(rec["value"], 1), "workers": world, "batch_per_worker": 256, "steps": steps,
-                "warmup": 3, "wall_s": round(time.time() - t0, 1)}
+                "warmup": 3, "hipgraph": graphed and world == 1, "wall_s": round(time.time() - t0, 1)}
     finally:
         import shutil
         if os.path.exists(out):

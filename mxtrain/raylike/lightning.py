@@ -43,7 +43,13 @@ class LightningModule(nn.Module):
             v = v.to(self.device)
             dist.all_reduce(v)
             v = v / dist.get_world_size()
-        self._logged[name] = float(v)
+        # kept as a (device) tensor and read only when the metrics are (epoch end, progress
+        # lines): a float() here synchronised the host with the GPU on every step, so the
+        # next step's launches could never run ahead of the GPU
+        self._logged[name] = v
+
+    def logged_metrics(self) -> Dict[str, float]:
+        return {k: float(v) for k, v in self._logged.items()}
 
     def log_dict(self, d: Dict[str, Any], **kw):
         for k, v in d.items():
@@ -107,8 +113,14 @@ class Trainer:
     def __init__(self, max_epochs: int = 1, max_steps: int = -1, devices="auto", accelerator="auto", strategy=None,
                  plugins=None, callbacks: Optional[List[Callback]] = None, enable_progress_bar: bool = True,
                  limit_train_batches=None, limit_val_batches=None, precision="32", log_every_n_steps: int = 50,
-                 enable_checkpointing: bool = False, num_sanity_val_steps: int = 0, default_root_dir=None, **kw):
+                 enable_checkpointing: bool = False, num_sanity_val_steps: int = 0, default_root_dir=None,
+                 hipgraph: Optional[bool] = None, **kw):
         self.max_epochs, self.max_steps = max_epochs, max_steps
+        # hipGraph replay of the training step (forward, backward, SGD) after GRAPH_WARMUP
+        # eager steps: None = on when it applies (one GPU worker, torch.optim.SGD without
+        # dampening; MXTRAIN_LIGHTNING_GRAPH=0 turns it off)
+        self.hipgraph = hipgraph
+        self.graph_info: Dict[str, Any] = {}
         self.strategy = strategy
         self.callbacks = callbacks or []
         self.limit_train, self.limit_val = limit_train_batches, limit_val_batches
@@ -157,6 +169,7 @@ class Trainer:
             opt = opt_cfg
         rank = get_context().get_world_rank()
         world = get_context().get_world_size()
+        graph = None
         done = False
         for epoch in range(self.max_epochs):
             self.current_epoch = epoch
@@ -165,16 +178,26 @@ class Trainer:
                 sampler.set_epoch(epoch)
             model.train()
             t0, nsamp = None, 0
+            loss = out = None
             for i, batch in enumerate(train_dataloaders):
                 if self.limit_train is not None and i >= self.limit_train:
                     break
                 batch = self._to(batch, dev)
-                with self._autocast(dev):
-                    out = ddp("training_step", batch, i)
-                loss = out["loss"] if isinstance(out, dict) else out
-                opt.zero_grad(set_to_none=True)
-                loss.backward()
-                opt.step()
+                if graph is None and self.global_step >= GRAPH_WARMUP and self._graph_ok(dev, opt, world):
+                    # the last eager step's loss keeps its autograd graph (and AccumulateGrad
+                    # nodes bound to the default stream) alive: a capture that reaches them
+                    # waits across streams and the runtime crashes at capture end
+                    loss = out = None
+                    graph = self._capture(ddp, opt, batch, i, dev)
+                if graph is not None and graph.matches(batch):
+                    loss = graph.replay(batch)
+                else:
+                    with self._autocast(dev):
+                        out = ddp("training_step", batch, i)
+                    loss = out["loss"] if isinstance(out, dict) else out
+                    opt.zero_grad(set_to_none=True)
+                    loss.backward()
+                    opt.step()
                 if sched is not None:
                     sched.step()
                 self.global_step += 1
@@ -206,7 +229,7 @@ class Trainer:
                             model.validation_step(self._to(batch, dev), i)
                 model.on_validation_epoch_end()
             model.on_train_epoch_end()
-            self.callback_metrics = dict(model._logged)
+            self.callback_metrics = model.logged_metrics()
             if rank == 0:
                 print(f"Epoch {epoch}: " + " ".join(f"{k}={v:.4f}" for k, v in self.callback_metrics.items()),
                       flush=True)
@@ -215,6 +238,127 @@ class Trainer:
             if done:
                 break
         return self
+
+
+    # ------------------------------------------------------------------ hipGraph step
+    def _graph_ok(self, dev, opt, world) -> bool:
+        on = self.hipgraph if self.hipgraph is not None else os.environ.get("MXTRAIN_LIGHTNING_GRAPH", "1") != "0"
+        if not on or dev.type != "cuda" or world != 1 or type(opt) is not torch.optim.SGD:
+            return False
+        return all(not g.get("dampening") and not g.get("maximize") for g in opt.param_groups)
+
+    def _capture(self, ddp, opt, batch, idx, dev):
+        """Capture one training step (forward under autocast, backward, SGD with device
+        learning rates) into a hipGraph; None (eager from here on) if anything fails."""
+        try:
+            step = _GraphedStep(self, ddp, opt, batch, idx, dev)
+            self.graph_info = {"captured_at_step": self.global_step, "nodes": step.census}
+            return step
+        except Exception as e:   # noqa: BLE001 -- keep training eagerly
+            self.hipgraph = False
+            self.graph_info = {"error": repr(e)[:300]}
+            print(f"[mxtrain.lightning] hipGraph capture failed, eager steps: {e!r}"[:400], flush=True)
+            return None
+
+
+@torch.no_grad()
+def sgd_step_device_lr(opt: torch.optim.SGD, lrs: List[torch.Tensor]) -> None:
+    """torch.optim.SGD.step (momentum, Nesterov, weight decay; dampening 0) with each
+    group's learning rate read from a device scalar, so the update can live inside a
+    captured graph while an LR scheduler changes the rate every step.  Momentum buffers
+    start at zero, which gives torch's first-step buf = d."""
+    for g, lr in zip(opt.param_groups, lrs):
+        ps = [p for p in g["params"] if p.grad is not None]
+        if not ps:
+            continue
+        grads = [p.grad for p in ps]
+        if g["weight_decay"]:
+            grads = torch._foreach_add(grads, ps, alpha=g["weight_decay"])
+        mom = g["momentum"]
+        if mom:
+            bufs = []
+            for p in ps:
+                st = opt.state[p]
+                if st.get("momentum_buffer") is None:
+                    st["momentum_buffer"] = torch.zeros_like(p)
+                bufs.append(st["momentum_buffer"])
+            torch._foreach_mul_(bufs, mom)
+            torch._foreach_add_(bufs, grads)
+            upd = torch._foreach_add(grads, bufs, alpha=mom) if g["nesterov"] else bufs
+        else:
+            upd = grads
+        torch._foreach_add_(ps, torch._foreach_mul(upd, lr), alpha=-1.0)
+
+
+GRAPH_WARMUP = 3   # eager steps before the capture (lazy state, momentum buffers, MIOpen / GEMM choices)
+
+
+class _GraphedStep:
+    def __init__(self, trainer, ddp, opt, batch, idx, dev):
+        from ..runtime.graphfix import census, memsets_to_kernels
+        self.opt = opt
+        self.lrs = [torch.tensor(float(g["lr"]), dtype=torch.float32, device=dev) for g in opt.param_groups]
+        for g in opt.param_groups:   # buffers exist before capture (allocated outside the pool)
+            for p in g["params"]:
+                if g["momentum"] and opt.state[p].get("momentum_buffer") is None:
+                    opt.state[p]["momentum_buffer"] = torch.zeros_like(p)
+        self.static = _clone(batch)
+        opt.zero_grad(set_to_none=True)
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph(keep_graph=True)
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+            with trainer._autocast(dev):
+                out = ddp("training_step", self.static, idx)
+            loss = out["loss"] if isinstance(out, dict) else out
+            loss.backward()
+            sgd_step_device_lr(opt, self.lrs)
+        self.loss = loss
+        # memset nodes (MIOpen zeroes workspaces with hipMemsetAsync) replay wrong under this
+        # runtime's graph packet capture: fill-kernel nodes instead (runtime/graphfix.py)
+        self.census = census(self.graph)
+        self.census["memsets_as_kernels"] = memsets_to_kernels(self.graph)
+        self.graph.instantiate()
+
+    def matches(self, batch) -> bool:
+        return _shapes(self.static) == _shapes(batch)
+
+    def replay(self, batch):
+        _copy_into(self.static, batch)
+        for t, g in zip(self.lrs, self.opt.param_groups):
+            t.fill_(float(g["lr"]))
+        self.graph.replay()
+        return self.loss
+
+
+def _shapes(b):
+    if torch.is_tensor(b):
+        return (tuple(b.shape), b.dtype, b.device)
+    if isinstance(b, dict):
+        return tuple((k, _shapes(v)) for k, v in sorted(b.items()))
+    if isinstance(b, (list, tuple)):
+        return tuple(_shapes(v) for v in b)
+    return None
+
+
+def _clone(b):
+    if torch.is_tensor(b):
+        return b.clone()
+    if isinstance(b, dict):
+        return {k: _clone(v) for k, v in b.items()}
+    if isinstance(b, (list, tuple)):
+        return type(b)(_clone(v) for v in b)
+    return b
+
+
+def _copy_into(dst, src):
+    if torch.is_tensor(dst):
+        dst.copy_(src, non_blocking=True)
+    elif isinstance(dst, dict):
+        for k in dst:
+            _copy_into(dst[k], src[k])
+    elif isinstance(dst, (list, tuple)):
+        for a, b in zip(dst, src):
+            _copy_into(a, b)
 
 
 class _StepWrapper(nn.Module):

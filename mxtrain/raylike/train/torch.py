@@ -50,6 +50,11 @@ def prepare_model(model: torch.nn.Module, move_to_device: bool = True, parallel_
 
 
 class _DeviceLoader:
+    """Moves each batch to the device one batch AHEAD, on a copy stream from pinned host
+    memory: batch i + 1's host-to-device copy overlaps step i's kernels instead of
+    blocking the host in front of them (a pageable ``.to(non_blocking=True)`` is a
+    synchronous staged copy).  The consumer's stream waits for the copy's event."""
+
     def __init__(self, dl, device):
         self.dl, self.device = dl, device
 
@@ -57,12 +62,57 @@ class _DeviceLoader:
         return len(self.dl)
 
     def __iter__(self):
-        for b in self.dl:
-            yield _to(b, self.device)
+        if self.device.type != "cuda":
+            for b in self.dl:
+                yield _to(b, self.device)
+            return
+        stream = torch.cuda.Stream(device=self.device)
+        it = iter(self.dl)
+
+        def fetch():
+            try:
+                b = next(it)
+            except StopIteration:
+                return None
+            b = _pin(b)
+            with torch.cuda.stream(stream):
+                d = _to(b, self.device)
+            return d, stream.record_event(), b
+
+        nxt = fetch()
+        while nxt is not None:
+            d, ev, host = nxt
+            torch.cuda.current_stream(self.device).wait_event(ev)
+            _record(d, torch.cuda.current_stream(self.device))   # allocator: used on the compute stream
+            nxt = fetch()
+            yield d
+            del host
 
     @property
     def sampler(self):
         return self.dl.sampler
+
+
+def _pin(b):
+    if torch.is_tensor(b):
+        return b if b.is_pinned() else b.pin_memory()
+    if isinstance(b, dict):
+        return {k: _pin(v) for k, v in b.items()}
+    if isinstance(b, (list, tuple)):
+        return type(b)(_pin(v) for v in b)
+    return b
+
+
+def _record(b, stream):
+    if torch.is_tensor(b):
+        if b.is_cuda:
+            b.record_stream(stream)
+    elif isinstance(b, dict):
+        for v in b.values():
+            _record(v, stream)
+    elif isinstance(b, (list, tuple)):
+        for v in b:
+            _record(v, stream)
 
 
 def _to(b, dev):
@@ -85,4 +135,12 @@ def prepare_data_loader(dl: torch.utils.data.DataLoader, add_dist_sampler: bool 
         dl = torch.utils.data.DataLoader(dl.dataset, batch_size=dl.batch_size, sampler=sampler,
                                          num_workers=dl.num_workers, collate_fn=dl.collate_fn,
                                          pin_memory=get_device().type == "cuda", drop_last=dl.drop_last)
+    elif move_to_device and get_device().type == "cuda" and not dl.pin_memory:
+        # pinned batches (pinned by the loader's own pin thread, off the training loop) so the
+        # device copies below are truly asynchronous
+        kw = dict(batch_size=dl.batch_size, sampler=dl.sampler, num_workers=dl.num_workers,
+                  collate_fn=dl.collate_fn, pin_memory=True, drop_last=dl.drop_last)
+        if dl.num_workers > 0:
+            kw.update(persistent_workers=dl.persistent_workers, prefetch_factor=dl.prefetch_factor)
+        dl = torch.utils.data.DataLoader(dl.dataset, **kw)
     return _DeviceLoader(dl, get_device()) if move_to_device else dl

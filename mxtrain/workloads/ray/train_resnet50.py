@@ -47,17 +47,17 @@ class SyntheticImageNet(torch.utils.data.Dataset):
 
 
 class ResNet50Module(L.LightningModule):
-    MEAN = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1) * 255
-    STD = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1) * 255
-
     def __init__(self, lr: float, weight_decay: float = 5e-5, warmup: int = 50, total: int = 1000):
         super().__init__()
         from mxtrain.models.resnet import resnet50
         self.net = resnet50(norm="bn", num_classes=1000).to(memory_format=torch.channels_last)
         self.lr, self.wd, self.warmup, self.total = lr, weight_decay, warmup, total
+        # device-resident normalisation constants (no host copies inside the step: capturable)
+        self.register_buffer("mean", torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1) * 255, persistent=False)
+        self.register_buffer("std", torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1) * 255, persistent=False)
 
     def forward(self, x):
-        x = (x.float() - self.MEAN.to(x.device)) / self.STD.to(x.device)
+        x = (x.float() - self.mean) / self.std
         return self.net(x.contiguous(memory_format=torch.channels_last))
 
     def training_step(self, batch, idx):
