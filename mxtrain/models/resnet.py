@@ -24,14 +24,18 @@ from ..ops.batchnorm import bn_act
 from ..ops.epilogue import BlockLink, ConvBiasActFn, conv_bias_act, fused_conv_ok
 
 
-def _conv_nobias(x, w, stride, padding, dilation):
+def _conv_nobias(x, w, stride, padding, dilation, fuse=None):
     """conv2d without bias for the trainable-BN path: bf16 NHWC activations go through the
     implicit-GEMM kernels where they tile (forward, input and weight gradients), then the
-    MIOpen-forward + implicit-GEMM-weight-gradient path, else torch (autocast / fp32)."""
+    MIOpen-forward + implicit-GEMM-weight-gradient path, else torch (autocast / fp32).
+    ``fuse`` (BlockLink, k, ("take_res",)): honoured on the first path only; sets the link's
+    taker so the block's last BN hands its residual gradient to this conv's dgrad."""
     if x.is_cuda and x.dtype == torch.bfloat16:
         wb = w.to(torch.bfloat16)
         if convwg.fwd_supported(x, wb, None, None, stride, padding, dilation):
-            return ConvBiasActFn.apply(x, wb, None, None, False, stride, padding, dilation)
+            if fuse is not None:
+                fuse[0].taker = True
+            return ConvBiasActFn.apply(x, wb, None, None, False, stride, padding, dilation, fuse)
         if convwg.supported(x, wb, stride, padding, dilation):
             return convwg.conv2d_wg(x, wb, stride, padding, dilation)
         return F.conv2d(x, wb, None, stride, padding, dilation)
@@ -103,8 +107,12 @@ class ConvNorm(nn.Module):
         # trainable BatchNorm: the convolution on csrc/convwg.hip where it tiles (implicit-GEMM
         # forward / input / weight gradients), then ONE fused BN (+ residual) (+ ReLU) node
         # (ops/batchnorm.py, csrc/batchnorm.hip)
-        return bn_act(_conv_nobias(x, w, self.conv.stride, self.conv.padding, self.conv.dilation), self.norm,
-                      residual=residual, relu=relu)
+        # (identity blocks: conv1 role "take_res" adds the residual gradient that conv3's BN
+        # backward stashes, role "stash_res" -- see Bottleneck.forward)
+        link, roles = (fuse[0], fuse[2]) if fuse is not None else (None, ())
+        y = _conv_nobias(x, w, self.conv.stride, self.conv.padding, self.conv.dilation,
+                         fuse=fuse if "take_res" in roles else None)
+        return bn_act(y, self.norm, residual=residual, relu=relu, link=link if "stash_res" in roles else None)
 
     def fused_ok(self, x) -> bool:
         """This conv (frozen norm) would run ConvBiasActFn on input x, honouring a BlockLink."""
@@ -184,8 +192,20 @@ class Bottleneck(nn.Module):
     fuse_projection = True
 
     def forward(self, x):
-        link = BlockLink() if self.fuse_backward and self.conv1.norm_kind == "frozen" else None
         ident = self.shortcut is None
+        if self.conv1.norm_kind == "bn":
+            # trainable BatchNorm, identity block: the residual's gradient (conv3's BN backward)
+            # is added in conv1's dgrad store instead of by a separate autograd add
+            if self.fuse_backward and ident and torch.is_grad_enabled():
+                link = BlockLink()
+                a1 = self.conv1(x, fuse=(link, 1, ("take_res",)))
+                a2 = self.conv2(a1)
+                return self.conv3(a2, residual=x, relu=True, fuse=(link, 3, ("stash_res",)))
+            a1 = self.conv1(x)
+            a2 = self.conv2(a1)
+            idt = x if ident else self.shortcut(x)
+            return self.conv3(a2, residual=idt, relu=True)
+        link = BlockLink() if self.fuse_backward and self.conv1.norm_kind == "frozen" else None
         proj = link is not None and not ident and self.fuse_projection and self.shortcut.fused_ok(x)
         prev = getattr(x, "_mx_link", None) if (link is not None and (ident or proj)) else None
         r1 = ("take_res", "mask_prev") if prev is not None else (("take_res",) if (ident or proj) else ())

@@ -40,7 +40,8 @@ def _scratch(M: int, C: int, device) -> torch.Tensor:
 
 class BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, momentum: float, eps: float, relu: bool):
+    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, momentum: float, eps: float, relu: bool,
+                link=None):
         N, C, H, W = x.shape
         M = N * H * W
         y = torch.empty_like(x, memory_format=torch.channels_last)
@@ -52,6 +53,7 @@ class BNActFn(torch.autograd.Function):
                   mean.data_ptr(), rstd.data_ptr(), _lib.ptr(running_mean), _lib.ptr(running_var), M, C,
                   float(eps), float(momentum), int(relu), _scratch(M, C, x.device).data_ptr(), _lib.stream())
         ctx.relu, ctx.has_res = relu, residual is not None
+        ctx.link = link
         ctx.save_for_backward(x, y, mean, rstd, g32)
         ctx.pdtypes = (gamma.dtype, beta.dtype)
         return y
@@ -69,7 +71,13 @@ class BNActFn(torch.autograd.Function):
         _lib.call("mx_bn_bwd", dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                   g32.data_ptr(), dx.data_ptr(), _lib.ptr(dres), dg.data_ptr(), db.data_ptr(), 0, M, C,
                   int(ctx.relu), _scratch(M, C, x.device).data_ptr(), _lib.stream())
-        return (dx, dg.to(ctx.pdtypes[0]), db.to(ctx.pdtypes[1]), dres, None, None, None, None, None)
+        link = ctx.link
+        if dres is not None and link is not None and link.taker and ctx.needs_input_grad[3]:
+            # identity residual (ops/epilogue.py BlockLink): conv1's dgrad store adds it to the
+            # block input's gradient, so autograd's add of the input's two gradients disappears
+            link.stash.append(dres)
+            dres = None
+        return (dx, dg.to(ctx.pdtypes[0]), db.to(ctx.pdtypes[1]), dres, None, None, None, None, None, None)
 
 
 def bn_act_ref(x, gamma, beta, residual, running_mean, running_var, momentum, eps, relu, training=True):
@@ -83,9 +91,10 @@ def bn_act_ref(x, gamma, beta, residual, running_mean, running_var, momentum, ep
 
 
 def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, residual: Optional[torch.Tensor] = None,
-           relu: bool = False) -> torch.Tensor:
+           relu: bool = False, link=None) -> torch.Tensor:
     """act(bn(x) (+ residual)) for an ``nn.BatchNorm2d`` (training: batch statistics and
-    running-statistics update; eval: running statistics)."""
+    running-statistics update; eval: running statistics).  ``link``: a BlockLink whose taker
+    (the block's conv1) adds the residual's gradient in its dgrad store."""
     if supported(x, residual):
         mom = bn.momentum
         if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
@@ -97,7 +106,7 @@ def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, residual: Optional[torch.T
             mom = 0.0
         if bn.training:
             return BNActFn.apply(x, bn.weight, bn.bias, residual, bn.running_mean if bn.track_running_stats else None,
-                                 bn.running_var if bn.track_running_stats else None, mom, bn.eps, relu)
+                                 bn.running_var if bn.track_running_stats else None, mom, bn.eps, relu, link)
         # eval: y = act(x * scale + shift (+ res)) with the running statistics
         s = bn.weight.float() * torch.rsqrt(bn.running_var.float() + bn.eps)
         h = bn.bias.float() - bn.running_mean.float() * s

@@ -94,3 +94,58 @@ def test_resnet50_bn_step_uses_fused_paths():
     gn = sum(float(p.grad.float().norm() ** 2) for p in net.parameters() if p.grad is not None) ** 0.5
     assert gn > 0 and gn == gn
     assert all(p.grad is not None for p in net.parameters() if p.requires_grad)
+
+
+def test_bn_bottleneck_residual_gradient_fused_into_conv1_dgrad(monkeypatch):
+    """Trainable-BN identity blocks: conv3's BN backward stashes the residual gradient and
+    conv1's implicit-GEMM dgrad adds it in its store (one rounding) instead of autograd's
+    separate add.  Against the unfused blocks and an fp32 run: same forward, gradients as
+    close to fp32 as the unfused ones; the fused dgrad actually received the addend."""
+    import copy
+    from mxtrain.models.resnet import Bottleneck
+    from mxtrain.ops import convwg
+    seen = {"add": 0}
+    real = convwg.conv_dgrad
+
+    def spy(*a, add=None, **k):
+        seen["add"] += add is not None
+        return real(*a, add=add, **k)
+
+    monkeypatch.setattr(convwg, "conv_dgrad", spy)
+    torch.manual_seed(5)
+    blocks = torch.nn.Sequential(Bottleneck(512, 128, norm="bn"), Bottleneck(512, 128, norm="bn")).to(DEV)
+    blocks = blocks.to(memory_format=torch.channels_last)
+    for m in blocks.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+    x0 = torch.randn(4, 512, 48, 64, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    out = {}
+    gy = None
+    for fuse in (False, True):
+        b2 = copy.deepcopy(blocks)
+        for b in b2:
+            b.fuse_backward = fuse
+        seen["add"] = 0
+        x = x0.clone().requires_grad_()
+        y = b2(x)
+        if gy is None:
+            gy = torch.randn_like(y)
+        y.backward(gy)
+        torch.cuda.synchronize()
+        out[fuse] = (y.detach().float(), x.grad.float(), [p.grad.float() for p in b2.parameters()], seen["add"])
+    assert out[True][3] == 2 and out[False][3] == 0, (out[True][3], out[False][3])
+    assert torch.equal(out[False][0], out[True][0])
+    b32 = copy.deepcopy(blocks).float()
+    for b in b32:
+        b.fuse_backward = False
+    x32 = x0.float().requires_grad_()
+    b32(x32).backward(gy.float())
+    e_f = (out[True][1] - x32.grad).abs().max().item()
+    e_u = (out[False][1] - x32.grad).abs().max().item()
+    assert e_f <= 1.25 * e_u + 1e-3 * x32.grad.abs().max().item(), (e_f, e_u)
+    # weight gradients: as close to the fp32 run as the unfused ones (relative norm error)
+    for a, c, r in zip(out[True][2], out[False][2], [p.grad.float() for p in b32.parameters()]):
+        rn = float(r.norm()) + 1e-12
+        ef, eu = float((a - r).norm()) / rn, float((c - r).norm()) / rn
+        assert ef <= 1.25 * eu + 1e-3, (ef, eu)
