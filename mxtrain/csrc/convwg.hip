@@ -147,7 +147,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
     }
   };
   auto boffB = [&](int j) __attribute__((always_inline)) {
-    bool ok = bp[j] < cp.T;
+    // (a narrow Cin -- 64 channels, the ResNet res2 convolutions -- reads zeros past it)
+    bool ok = bp[j] < cp.T && n0 + cB[j] < cp.Cin;
     if (!IDENT)
       ok = ok && (unsigned)(bohs[j] + dh) < (unsigned)cp.IH && (unsigned)(bows[j] + dwc) < (unsigned)cp.IW;
     return ok ? (uint32_t)(bxo[j] + tapoff + cB[j]) * 2u : kOOB;
@@ -242,6 +243,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void conv_wgrad_kernel(const Co
       uint16_t* row = C + (size_t)(16 * a + e) * ldc;
 #pragma unroll
       for (int u = 0; u < FN; ++u) {
+        if (n0 + 16 * FN * wn + 16 * u + i >= cp.Cin) continue;   // (narrow Cin: padded columns)
         float v = acc[a][u][e];
         if (acc_in) v += cp.beta * bf2f(row[16 * u]);
         row[16 * u] = f2bf(v);
@@ -695,15 +697,19 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
   }
   uint32_t boff[PB];
   int bkrow[PB];
+  bool bcol[PB];   // this lane's weight columns exist (false only past a narrow Cin)
 #pragma unroll
   for (int j = 0; j < PB; ++j) {
     const int kB = (PB * wave + j) * (1024 / RB) + lane / (RB / 16);
     bkrow[j] = kB;
+    bcol[j] = n0 + 8 * pchunk(kB, lane % (RB / 16)) < cp.Cin;
     boff[j] = (uint32_t)(kB * (int)ldw + n0 + 8 * pchunk(kB, lane % (RB / 16))) * 2u;
   }
   const i32x4_t yres = buffer_rsrc(cp.dy, cp.ybytes);
-  // narrow Cout (the 1x1 heads, Cout % BKT != 0): dY columns and weight rows past Cout read zeros
-  const bool narrow = cp.Cout % BKT != 0;
+  // narrow Cout (the 1x1 heads, Cout % BKT != 0): dY columns and weight rows past Cout read
+  // zeros; narrow Cin (64 channels: the ResNet res2 convolutions, 128-column tiles half
+  // padded): weight columns past Cin read zeros and the padded dX columns are not written
+  const bool narrow = cp.Cout % BKT != 0 || cp.Cin % BN != 0;
   const i32x4_t wres = buffer_rsrc(cp.w, (uint32_t)(cp.Cout * cp.ldw * 2));
 
   const int G = lane >> 4, i = lane & 15;
@@ -754,7 +760,8 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
     if (narrow) {
       const uint32_t wo = (uint32_t)((size_t)co0 * ldw + (size_t)tap * cp.Cin) * 2u;
 #pragma unroll
-      for (int j = 0; j < PB; ++j) dma16_buf(wres, co0 + bkrow[j] < cp.Cout ? wo + boff[j] : kOOB, b1 + j * 1024);
+      for (int j = 0; j < PB; ++j)
+        dma16_buf(wres, (co0 + bkrow[j] < cp.Cout && bcol[j]) ? wo + boff[j] : kOOB, b1 + j * 1024);
     } else {
       const uint16_t* wb = cp.w + (size_t)co0 * ldw + (size_t)tap * cp.Cin;
 #pragma unroll
@@ -799,17 +806,21 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
   // ---- epilogue: lane (G, i) holds dX[m0 + 16 (FM wm + a) + i][n0 + 16 (FN wn + u) + 4 G + e],
   // re-dealt per subtile pair into 8 consecutive channels per lane (16-B stores)
   const int colw = n0 + 16 * FN * wn;
+  // (narrow Cin: a wave whose 64 columns are all padding stores nothing; the split-K ticket
+  // below is taken by the whole workgroup, so such a wave still joins it)
+  const bool cols_live = colw < cp.Cin;
   if (cp.splits > 1) {   // split-K: raw fp32 partials; add / mask / bf16 in the reduction
 #pragma unroll
     for (int a = 0; a < FM; ++a) {
       const int p = m0 + 16 * (FM * wm + a) + i;
-      if (p < cp.T) {
+      if (p < cp.T && cols_live) {
         float* dst = cp.part + ((size_t)sidx * cp.T + p) * cp.Cin + colw + 4 * G;
 #pragma unroll
         for (int u = 0; u < FN; ++u) *reinterpret_cast<f32x4*>(dst + 16 * u) = acc[a][u];
       }
     }
     if (!cp.ticket || !split_last_arriver(cp.ticket, tile, cp.splits)) return;
+    if (!cols_live) return;
 #pragma unroll
     for (int a = 0; a < FM; ++a) {
       const int p = m0 + 16 * (FM * wm + a) + i;
@@ -823,6 +834,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
       }
     }
   }
+  if (!cols_live) return;
   float bz[FN][4];
 #pragma unroll
   for (int u = 0; u < FN; ++u)
@@ -905,6 +917,7 @@ __device__ __forceinline__ void wgrad_reduce_one(const float* slab, uint16_t* dw
                 16 * FN * wn + 16 * u + i;
   const float e4[4] = {v.x, v.y, v.z, v.w};
   const int mrow = m0 + 16 * FM * wm + 4 * G + 16 * a;
+  if (n0 + 16 * FN * wn + 16 * u + i >= Cin) return;   // (narrow Cin: padded columns)
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     if (mrow + e >= Cout) continue;
@@ -947,7 +960,7 @@ __global__ __launch_bounds__(64) void conv_wgrad_reduce_batched_kernel(const WgJ
 MX_EXPORT int mx_conv_wgrad_tile(int what) { return what == 0 ? kBM : what == 1 ? kBN : kBK; }
 
 // d (int64[20]): {dy, x, zero, dw, slab, 0, ldy, ldx, N, OH, OW, IH, IW, KH, KW, stride,
-// pad, dil, Cout, Cin}.  Cout and Cin multiples of 128; dy / x / zero 16-B aligned with
+// pad, dil, Cout, Cin}.  Cout a multiple of 128 (or 8: narrow), Cin of 64; dy / x / zero 16-B aligned with
 // ldy / ldx multiples of 8; dW is written (beta 0) or accumulated (beta 1) in bf16.
 // splits > 1 needs slab (ntiles x splits x 128 x 128 fp32) and adds the reduction launch.
 MX_EXPORT int mx_conv_wgrad(const int64_t* d, float beta, int splits, void* stream) {
@@ -975,8 +988,9 @@ MX_EXPORT int mx_conv_wgrad(const int64_t* d, float beta, int splits, void* stre
   if (N <= 0 || cp.OH <= 0 || cp.OW <= 0 || KH <= 0 || cp.KW <= 0 || cp.stride <= 0 || cp.dil <= 0 ||
       cp.pad < 0 || T >= (1 << 23) || N * cp.IH * cp.IW >= ((int64_t)1 << 31))
     return (int)hipErrorInvalidValue;
-  // Cout: a multiple of 128, or of 8 (the narrow 1x1 heads: 128-row tiles, zero-padded)
-  if ((Cout % kBM && Cout % 8) || cp.Cin % kBN || cp.ldy < Cout || cp.ldx < cp.Cin || (cp.ldy & 7) || (cp.ldx & 7))
+  // Cout: a multiple of 128, or of 8 (the narrow 1x1 heads: 128-row tiles, zero-padded);
+  // Cin: a multiple of 64 (an odd multiple: the last column tile half zero-padded)
+  if ((Cout % kBM && Cout % 8) || cp.Cin % 64 || cp.ldy < Cout || cp.ldx < cp.Cin || (cp.ldy & 7) || (cp.ldx & 7))
     return (int)hipErrorInvalidValue;
   cp.Cout = Cout;
   if ((d[0] | d[1] | d[2]) & 15) return (int)hipErrorInvalidValue;
@@ -987,7 +1001,7 @@ MX_EXPORT int mx_conv_wgrad(const int64_t* d, float beta, int splits, void* stre
   if (xbytes >= ((int64_t)1 << 31) || ybytes >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   cp.xbytes = (uint32_t)xbytes;
   cp.ybytes = (uint32_t)ybytes;
-  cp.tiles_n = cp.Cin / kBN;
+  cp.tiles_n = (cp.Cin + kBN - 1) / kBN;
   cp.tiles_tap = ((Cout + kBM - 1) / kBM) * cp.tiles_n;
   cp.ntiles = cp.taps * cp.tiles_tap;
   const int steps = (int)((T + kBK - 1) / kBK);
@@ -1149,7 +1163,7 @@ static void launch_dgrad(ConvDg cp, int splits, hipStream_t st) {
 // dilation, filter <= s x s): one launch per parity class (ih mod s, iw mod s) = (a, b), whose
 // pixels all take the single tap (a, b) from dY[ih / s][iw / s] -- a plain GEMM over a
 // quarter of the pixels instead of the gathered K loop whose rows are 3 of 4 zero -- and one
-// fill of the pixels no tap reaches.  Cout a multiple of 64, Cin of 128; 16-B aligned
+// fill of the pixels no tap reaches.  Cout a multiple of 8, Cin of 64; 16-B aligned
 // operands (add / mask share dX's layout); splits > 1 needs part (fp32, splits x pixels x Cin).
 MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   ConvDg cp{};
@@ -1177,7 +1191,7 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   if (N <= 0 || cp.IH <= 0 || cp.IW <= 0 || cp.OH <= 0 || cp.OW <= 0 || KH <= 0 || cp.KW <= 0 || cp.stride <= 0 ||
       cp.dil <= 0 || cp.pad < 0 || T >= (1 << 23) || N * cp.OH * cp.OW >= ((int64_t)1 << 31))
     return (int)hipErrorInvalidValue;
-  if (Cout % 8 || cp.Cin % 128 || cp.ldy < Cout || cp.ldx < cp.Cin || (cp.ldy & 7) || (cp.ldx & 7))
+  if (Cout % 8 || cp.Cin % 64 || cp.ldy < Cout || cp.ldx < cp.Cin || (cp.ldy & 7) || (cp.ldx & 7))
     return (int)hipErrorInvalidValue;
   if ((d[0] | d[1] | d[2] | d[3] | d[4] | d[5]) & 15) return (int)hipErrorInvalidValue;
   cp.T = (int)T;
@@ -1195,7 +1209,7 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   cp.cob = (Cout + cp.bkt - 1) / cp.bkt;
   cp.Cout = Cout;
   cp.nk = cp.taps * cp.cob;
-  cp.tiles_n = cp.Cin / 128;
+  cp.tiles_n = (cp.Cin + 127) / 128;   // (Cin % 128 == 64: the last column tile half padded)
   cp.invIW = 1.f / (float)cp.IW;
   cp.invIH = 1.f / (float)cp.IH;
   cp.bias = reinterpret_cast<const uint16_t*>(d[22]);

@@ -223,7 +223,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dila
         out = torch.empty((Cout, KH, KW, Cin), dtype=torch.bfloat16, device=x.device).permute(0, 3, 1, 2)
     assert tuple(out.shape) == (Cout, Cin, KH, KW) and out.stride(1) == 1 and out.stride(0) == KH * KW * Cin
     T = N * OH * OW
-    ntiles = KH * KW * (-(-Cout // 128)) * (Cin // 128)   # (a narrow Cout: one zero-padded row tile)
+    ntiles = KH * KW * (-(-Cout // 128)) * (-(-Cin // 128))   # (narrow Cout / Cin: zero-padded tiles)
     if splits <= 0:
         splits = plan_splits(T, ntiles)
     splits = int(_lib.query("mx_conv_wgrad_splits", T, splits))
@@ -235,8 +235,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, dila
         reg = _defer_slab(x.device, ntiles * splits * 128 * 128)
         if reg is not None:
             slab, defer = reg, 1
-            _DEF["jobs"].append([reg.data_ptr(), out.data_ptr(), ntiles, splits, (-(-Cout // 128)) * (Cin // 128),
-                                 Cin // 128, KH * KW, Cin, 1 if beta else 0, Cout])
+            _DEF["jobs"].append([reg.data_ptr(), out.data_ptr(), ntiles, splits, (-(-Cout // 128)) * (-(-Cin // 128)),
+                                 -(-Cin // 128), KH * KW, Cin, 1 if beta else 0, Cout])
     d = _DESC_T()
     d[:20] = [dy.data_ptr(), x.data_ptr(), zero.data_ptr(), out.data_ptr(), slab.data_ptr(), defer,
             Cout, Cin, N, OH, OW, IH, IW, KH, KW, _sym(stride), _sym(padding), _sym(dilation), Cout, Cin]
@@ -270,7 +270,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride, padding, dila
     dec = decomposed(KH, KW, stride, padding, dilation)
     st = _sym(stride)
     T = N * (-(-IH // st)) * (-(-IW // st)) if dec else N * IH * IW   # largest launch's pixels
-    splits = dgrad_splits((T + 127) // 128 * (Cin // 128), (1 if dec else KH * KW) * -(-Cout // 64))
+    splits = dgrad_splits((T + 127) // 128 * -(-Cin // 128), (1 if dec else KH * KW) * -(-Cout // 64))
     slab, zero = _workspace(dy.device, splits * T * Cin if splits > 1 else 1)
     assert bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == Cin
                             and bias.data_ptr() % 8 == 0)
@@ -430,6 +430,8 @@ def dgrad_supported(w: torch.Tensor, x_shape, stride, padding=0, dilation=1) -> 
     65 vs 40 us), and stride 1, a stride-decomposed filter (1x1 stride 2: one GEMM over the
     pixels of one parity class) or at most 256 output channels (a strided 3x3's gathered dY
     has 3 of 4 rows zero, which costs MFMA time per K-step)."""
+    # (the kernel also takes Cin = 64 -- half-padded 128-column tiles -- but at the ResNet res2
+    # shapes that ran 1.4 ms per step vs MIOpen's 0.93 ms, profiles/r6/resnet50_census_cin64.txt)
     if not (DGRAD and cout_ok(w.shape[0]) and w.shape[1] % 128 == 0 and w.data_ptr() % 16 == 0):
         return False
     N, Cin, IH, IW = x_shape
@@ -442,9 +444,9 @@ def dgrad_supported(w: torch.Tensor, x_shape, stride, padding=0, dilation=1) -> 
     if OH <= 0 or OW <= 0 or not _fits(N * Cin * IH * IW, N * w.shape[0] * OH * OW):
         return False
     if decomposed(w.shape[2], w.shape[3], stride, padding, dilation):
-        tiles = (N * (-(-IH // st)) * (-(-IW // st)) + 127) // 128 * (Cin // 128)
+        tiles = (N * (-(-IH // st)) * (-(-IW // st)) + 127) // 128 * -(-Cin // 128)
         return tiles >= DGRAD_MIN_TILES or dgrad_splits(tiles, -(-w.shape[0] // 64)) > 1 or not SMALL_ON_MIOPEN
-    tiles = (N * IH * IW + 127) // 128 * (Cin // 128)
+    tiles = (N * IH * IW + 127) // 128 * -(-Cin // 128)
     nk = -(-(w.shape[2] * w.shape[3] * w.shape[0]) // 64)
     return ((tiles >= DGRAD_MIN_TILES or dgrad_splits(tiles, nk) > 1 or not SMALL_ON_MIOPEN)
             and (st == 1 or w.shape[0] <= 256))

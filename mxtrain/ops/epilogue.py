@@ -196,6 +196,7 @@ class ConvBiasActFn(torch.autograd.Function):
                 join_first = True
         mask = x if ("mask_in" in roles or "mask_prev" in roles) else None
         dx = dw = None
+        # (Cin = 64 tiles half padded: even with MIOpen at the ResNet res2 shapes, so MIOpen keeps them)
         wg_hip = ctx.needs_input_grad[1] and convwg.cout_ok(w.shape[0]) and w.shape[1] % 128 == 0
         if ctx.needs_input_grad[0]:
             if convwg.dgrad_supported(w, tuple(x.shape), st, pd, dl) and (add is None or add.data_ptr() % 16 == 0):

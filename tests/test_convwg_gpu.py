@@ -16,6 +16,11 @@ CASES = [
     (3, 256, 256, 14, 14, 3, 1, 1, 1),
     (1, 128, 128, 19, 21, 3, 1, 2, 2),
     (2, 128, 256, 9, 11, 3, 2, 1, 1),
+    # Cin an odd multiple of 64 (ResNet res2 inputs: the last 128-column tile half padded)
+    (2, 64, 64, 28, 30, 3, 1, 1, 1),
+    (1, 64, 256, 20, 22, 1, 1, 0, 1),
+    (2, 64, 128, 17, 19, 1, 2, 0, 1),
+    (1, 192, 128, 15, 16, 3, 1, 1, 1),
 ]
 
 
