@@ -116,9 +116,12 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(const float* __re
                                                                float* __restrict__ rstd_out,
                                                                float* __restrict__ scale, float* __restrict__ shift,
                                                                float* __restrict__ run_mean,
-                                                               float* __restrict__ run_var) {
+                                                               float* __restrict__ run_var,
+                                                               int64_t* __restrict__ nbt) {
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  // nn.BatchNorm2d's num_batches_tracked += 1 (a separate 5-us launch per layer otherwise)
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
   if (c >= C) return;
   float na = 0.f, ma = 0.f, m2 = 0.f;
   for (int b = lane; b < nblk; b += 64) {
@@ -138,6 +141,74 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(const float* __re
     }
   }
   if (lane == 0) {
+    const float var = m2 / (float)M;
+    const float rs = rsqrtf(var + eps);
+    const float sc = gamma[c] * rs;
+    mean_out[c] = ma;
+    rstd_out[c] = rs;
+    scale[c] = sc;
+    shift[c] = beta[c] - ma * sc;
+    if (run_mean) {
+      const float unb = M > 1 ? m2 / (float)(M - 1) : var;
+      run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * ma;
+      run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+    }
+  }
+}
+
+// Finalize from the statistics a convolution's epilogue wrote (csrc/convwg.hip ConvFw::bnp):
+// channel-major [C][nblk] means and M2 of 64-row blocks (up to ~12.5k blocks at the ResNet-50
+// res2 shapes).  One workgroup per channel: thread t merges blocks t, t + 256, ... (coalesced
+// loads, four in flight), then a fixed butterfly in each wave and the four waves in order
+// (deterministic); outputs as bn_finalize_kernel.
+__global__ __launch_bounds__(kThreads) void bn_finalize_cm_kernel(const float* __restrict__ pmean,
+                                                                  const float* __restrict__ pm2, int nblk, int rpb,
+                                                                  int M, int C, const float* __restrict__ gamma,
+                                                                  const float* __restrict__ beta, float eps,
+                                                                  float momentum, float* __restrict__ mean_out,
+                                                                  float* __restrict__ rstd_out,
+                                                                  float* __restrict__ scale, float* __restrict__ shift,
+                                                                  float* __restrict__ run_mean,
+                                                                  float* __restrict__ run_var,
+                                                                  int64_t* __restrict__ nbt) {
+  const int c = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (nbt && c == 0 && t == 0) nbt[0] += 1;
+  const float* pmr = pmean + (size_t)c * nblk;
+  const float* pqr = pm2 + (size_t)c * nblk;
+  float na = 0.f, ma = 0.f, m2 = 0.f;
+  int b = t;
+  for (; b + 3 * kThreads < nblk; b += 4 * kThreads) {
+    float mb[4], qb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      mb[k] = pmr[b + k * kThreads];
+      qb[k] = pqr[b + k * kThreads];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      chan_merge(na, ma, m2, (float)min(rpb, M - (b + k * kThreads) * rpb), mb[k], qb[k]);
+  }
+  for (; b < nblk; b += kThreads) chan_merge(na, ma, m2, (float)min(rpb, M - b * rpb), pmr[b], pqr[b]);
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float nb = __shfl_xor(na, o), mb = __shfl_xor(ma, o), m2b = __shfl_xor(m2, o);
+    if (lane & o) {
+      float n2 = nb, m_2 = mb, q2 = m2b;
+      chan_merge(n2, m_2, q2, na, ma, m2);
+      na = n2; ma = m_2; m2 = q2;
+    } else {
+      chan_merge(na, ma, m2, nb, mb, m2b);
+    }
+  }
+  __shared__ float sw[3][kThreads / 64];
+  if (lane == 0) {
+    sw[0][wave] = na;
+    sw[1][wave] = ma;
+    sw[2][wave] = m2;
+  }
+  __syncthreads();
+  if (t == 0) {
+    for (int w = 1; w < kThreads / 64; ++w) chan_merge(na, ma, m2, sw[0][w], sw[1][w], sw[2][w]);
     const float var = m2 / (float)M;
     const float rs = rsqrtf(var + eps);
     const float sc = gamma[c] * rs;
@@ -310,6 +381,8 @@ int rows_per_block(int M) {
   return r < 64 ? 64 : r;
 }
 
+constexpr int kPreRows = 64;   // rows per block of the convolution epilogue's statistics
+
 int elem_grid(int64_t nvec) {
   int64_t g = (nvec + kThreads - 1) / kThreads;
   return (int)(g < 4096 ? (g < 1 ? 1 : g) : 4096);
@@ -323,23 +396,37 @@ MX_EXPORT int64_t mx_bn_scratch(int M, int C) {
   return (int64_t)nblk * 2 * C + 3 * (int64_t)C + 2 * (int64_t)C;
 }
 
+// floats of the per-64-row-block statistics the convolution forward writes (ConvFw::bnp)
+MX_EXPORT int64_t mx_bn_pre_size(int M, int C) {
+  return (int64_t)((M + kPreRows - 1) / kPreRows) * 2 * C;
+}
+
 // Training forward.  x, res, y: [M][C] bf16 (res may be null); gamma / beta fp32 [C];
 // mean / rstd out fp32 [C] (saved for backward); run_mean / run_var fp32 [C] updated in
 // place (null: not tracked); scratch: mx_bn_scratch floats.
+// nbt: num_batches_tracked (int64, incremented by the finalize) or null.
+// pre: null, or the per-64-row-block statistics of x the producing convolution's epilogue
+// wrote (mx_bn_pre_size floats): then no statistics pass reads x.
 MX_EXPORT int mx_bn_fwd(const void* x, const void* res, void* y, const float* gamma, const float* beta, float* mean,
                         float* rstd, float* run_mean, float* run_var, int M, int C, float eps, float momentum,
-                        int relu, float* scratch, hipStream_t s) {
+                        int relu, float* scratch, int64_t* nbt, const float* pre, hipStream_t s) {
   if (C % 8 || C <= 0 || M <= 0 || C > 8 * 65535 * kThreads) return hipErrorInvalidValue;
-  const int rpb = rows_per_block(M), nblk = (M + rpb - 1) / rpb;
   const int c8 = C / 8, cv = c8 < kThreads ? c8 : kThreads;
-  float* pmean = scratch;
-  float* pm2 = scratch + (size_t)nblk * C;
-  float* scale = pm2 + (size_t)nblk * C;
+  const int rpb = rows_per_block(M), nblk = (M + rpb - 1) / rpb;
+  float* scale = scratch + (size_t)2 * nblk * C;
   float* shift = scale + C;
-  hipLaunchKernelGGL(bn_stats_kernel, dim3((c8 + cv - 1) / cv, nblk), dim3(kThreads), 0, s, (const uint16_t*)x, M,
-                     C, rpb, pmean, pm2);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 3) / 4), dim3(kThreads), 0, s, pmean, pm2, nblk, rpb, M, C,
-                     gamma, beta, eps, momentum, mean, rstd, scale, shift, run_mean, run_var);
+  if (!pre) {
+    float* pmean = scratch;
+    float* pm2 = scratch + (size_t)nblk * C;
+    hipLaunchKernelGGL(bn_stats_kernel, dim3((c8 + cv - 1) / cv, nblk), dim3(kThreads), 0, s, (const uint16_t*)x, M,
+                       C, rpb, pmean, pm2);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 3) / 4), dim3(kThreads), 0, s, pmean, pm2, nblk, rpb, M, C,
+                       gamma, beta, eps, momentum, mean, rstd, scale, shift, run_mean, run_var, nbt);
+  } else {
+    const int nb = (M + kPreRows - 1) / kPreRows;
+    hipLaunchKernelGGL(bn_finalize_cm_kernel, dim3(C), dim3(kThreads), 0, s, pre, pre + (size_t)nb * C, nb,
+                       kPreRows, M, C, gamma, beta, eps, momentum, mean, rstd, scale, shift, run_mean, run_var, nbt);
+  }
   const int64_t nvec = (int64_t)M * c8;
   const dim3 gr(elem_grid(nvec));
   if (res) {

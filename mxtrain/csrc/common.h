@@ -68,6 +68,14 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 // norm kernels latency-bound: SQ_WAIT_INST_LDS dominated their wave cycles.)
 #define MX_DPP(v, ctrl) \
   __uint_as_float(__builtin_amdgcn_update_dpp(0u, __float_as_uint(v), (ctrl), 0xf, 0xf, false))
+// sum over the 16 lanes of each row (every lane of the row ends with it)
+__device__ __forceinline__ float row_sum16(float v) {
+  v += MX_DPP(v, 0xB1);   // quad_perm [1,0,3,2]
+  v += MX_DPP(v, 0x4E);   // quad_perm [2,3,0,1]
+  v += MX_DPP(v, 0x124);  // row_ror:4
+  v += MX_DPP(v, 0x128);  // row_ror:8
+  return v;
+}
 __device__ __forceinline__ float wave_sum(float v) {
   v += MX_DPP(v, 0xB1);   // quad_perm [1,0,3,2]
   v += MX_DPP(v, 0x4E);   // quad_perm [2,3,0,1]

@@ -286,6 +286,11 @@ struct ConvFw {
   uint32_t xbytes;       // size of x (the gather's buffer resource; < 2 GiB)
   uint32_t* ticket;      // non-null: the last-arriving split of a tile sums the partials and
                          // runs the epilogue itself (no reduction launch); [tiles], zero
+  float* bnp;            // non-null (unsplit launches): BatchNorm statistics of y from the
+                         // epilogue -- per 64-row block b (one wave's rows) and channel c the
+                         // mean at bnp[c][b] and M2 at bnp[Cout + c][b], nblk = ceil(T / 64)
+                         // blocks per row, channel-major so the finalize's loads coalesce
+                         // (csrc/batchnorm.hip: no statistics pass over y)
 };
 
 // Split-K without a reduction launch: after publishing its fp32 partial tile, each split
@@ -496,8 +501,11 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
     }
   }
   float bv[FN][4];
+  float bs[FN][4], bq[FN][4];   // BatchNorm statistics: this lane's sum / sum of squares
 #pragma unroll
   for (int u = 0; u < FN; ++u) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bs[u][e] = bq[u][e] = 0.f;
     if (cp.bias && colw + 16 * u + 4 * G < cp.Cout) {
       const uint2 b2 = *reinterpret_cast<const uint2*>(cp.bias + colw + 16 * u + 4 * G);
       bv[u][0] = lo_bf(b2.x); bv[u][1] = hi_bf(b2.x); bv[u][2] = lo_bf(b2.y); bv[u][3] = hi_bf(b2.y);
@@ -541,10 +549,46 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvFw cp) {
         }
         c[hlf][0] = pack2(v[0], v[1]);
         c[hlf][1] = pack2(v[2], v[3]);
+        if (cp.bnp && p < cp.T) {   // the statistics of the stored (rounded) values
+          const float r[4] = {lo_bf(c[hlf][0]), hi_bf(c[hlf][0]), lo_bf(c[hlf][1]), hi_bf(c[hlf][1])};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            bs[u][e] += r[e];
+            bq[u][e] = __builtin_fmaf(r[e], r[e], bq[u][e]);
+          }
+        }
       }
       deal(c[0][0], c[0][1], c[1][0], c[1][1]);
       if (p < cp.T && colw + 32 * up + 8 * G < cp.Cout)
         *reinterpret_cast<uint4*>(cp.y + pr + colw + 32 * up + 8 * G) = make_uint4(c[0][0], c[0][1], c[1][0], c[1][1]);
+    }
+  }
+  if (cp.bnp) {
+    // the wave's 64 rows (16 lanes x FM fragments per channel): row sums over the lanes, then
+    // (mean, M2) = (s / n, q - s * mean) -- the per-thread form of bn_stats_kernel
+    const int rb = m0 + 64 * wm, n = cp.T - rb < 64 ? cp.T - rb : 64;
+    if (n > 0) {
+      const float inv = 1.f / (float)n;
+      const size_t nblk = (size_t)((cp.T + 63) / 64);
+      float* pm = cp.bnp + (size_t)(rb / 64);
+#pragma unroll
+      for (int u = 0; u < FN; ++u) {
+        float mo[4], qo[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float s1 = row_sum16(bs[u][e]), q1 = row_sum16(bq[u][e]);
+          mo[e] = s1 * inv;
+          qo[e] = fmaxf(q1 - s1 * mo[e], 0.f);
+        }
+        // every lane of the row holds the sums: lane i < 4 stores channel col + i
+        const int col = colw + 16 * u + 4 * G + (i & 3);
+        const float mv = i == 0 ? mo[0] : i == 1 ? mo[1] : i == 2 ? mo[2] : mo[3];
+        const float qv = i == 0 ? qo[0] : i == 1 ? qo[1] : i == 2 ? qo[2] : qo[3];
+        if (i < 4 && col < cp.Cout) {
+          pm[(size_t)col * nblk] = mv;
+          pm[(size_t)(cp.Cout + col) * nblk] = qv;
+        }
+      }
     }
   }
 }
@@ -1248,8 +1292,8 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   return (int)hipGetLastError();
 }
 
-// d (int64[26]): {x, w, zero, y, bias, res, ldx, ldy, N, OH, OW, IH, IW, KH, KW, stride, pad,
-// dil, Cout, Cin, relu, res_up, splits, part, ticket, half}: y = act(conv2d(x, w) + bias (+ res, or with res_up the 2x
+// d (int64[27]): {x, w, zero, y, bias, res, ldx, ldy, N, OH, OW, IH, IW, KH, KW, stride, pad,
+// dil, Cout, Cin, relu, res_up, splits, part, ticket, half, bnp}: y = act(conv2d(x, w) + bias (+ res, or with res_up the 2x
 // nearest upsampling of res)) in NHWC bf16, weight [Cout][KH][KW][Cin] (channels_last).
 // Cout a multiple of 64 (128 x 64 tiles when not of 128), Cin of 64; res_up needs even OH, OW.
 MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
@@ -1280,6 +1324,7 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   cp.part = reinterpret_cast<float*>(d[23]);
   cp.ticket = reinterpret_cast<uint32_t*>(d[24]);
   cp.Cout = (int)d[18];
+  cp.bnp = reinterpret_cast<float*>(d[26]);
   const int64_t T = N * cp.OH * cp.OW;
   if (cp.res_up && ((cp.OH | cp.OW) & 1)) return (int)hipErrorInvalidValue;
   if (N <= 0 || cp.IH <= 0 || cp.IW <= 0 || cp.OH <= 0 || cp.OW <= 0 || KH <= 0 || cp.KW <= 0 || cp.stride <= 0 ||
@@ -1308,6 +1353,7 @@ MX_EXPORT int mx_conv_fwd(const int64_t* d, void* stream) {
   cp.invOH = 1.f / (float)cp.OH;
   if (cp.splits > cp.nk) cp.splits = cp.nk;
   if (cp.splits > 1 && (!cp.part || (d[23] & 15))) return (int)hipErrorInvalidValue;
+  if (cp.bnp && (cp.splits > 1 || Cout % 64 || (d[26] & 3))) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)((T + 127) / 128) * cp.tiles_n * cp.splits), block(256);
 #define MX_CF(NS, FN, BK)                                                                     \

@@ -61,14 +61,6 @@ struct Args {
 // +0.6-0.75 % per GPT-2 step in same-box A/Bs (profiles/r5_s1/bench_ab_gemm_*.txt).
 constexpr int g_gemm_nt_prio = 3;
 
-__device__ __forceinline__ float dpp_rowsum16(float v) {
-  v += MX_DPP(v, 0xB1);   // quad_perm [1,0,3,2]
-  v += MX_DPP(v, 0x4E);   // quad_perm [2,3,0,1]
-  v += MX_DPP(v, 0x124);  // row_ror:4
-  v += MX_DPP(v, 0x128);  // row_ror:8  -> every lane of a 16-lane row holds the row sum
-  return v;
-}
-
 template <bool BKC, int WM, int WN, int FM, int FN, int BKT, int NSLOT>
 struct Geo {
   static constexpr int NW = WM * WN, NT = 64 * NW;
@@ -196,7 +188,7 @@ __device__ __forceinline__ void epilogue(const Args& g, f32x4 (&acc)[FM][FN], in
     for (int u = 0; u < FN; ++u) {
       float t[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) t[e] = dpp_rowsum16(csum[u][e]);
+      for (int e = 0; e < 4; ++e) t[e] = row_sum16(csum[u][e]);
       if (i == 0) *reinterpret_cast<float4*>(prow + 16 * u) = make_float4(t[0], t[1], t[2], t[3]);
     }
   }

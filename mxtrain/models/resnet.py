@@ -24,18 +24,24 @@ from ..ops.batchnorm import bn_act
 from ..ops.epilogue import BlockLink, ConvBiasActFn, conv_bias_act, fused_conv_ok
 
 
-def _conv_nobias(x, w, stride, padding, dilation, fuse=None):
+# trainable BN: batch statistics from the producing conv's epilogue (A/B switch, scripts/resnet_ab.py)
+BN_EPILOGUE_STATS = True
+
+
+def _conv_nobias(x, w, stride, padding, dilation, fuse=None, bnpre=None):
     """conv2d without bias for the trainable-BN path: bf16 NHWC activations go through the
     implicit-GEMM kernels where they tile (forward, input and weight gradients), then the
     MIOpen-forward + implicit-GEMM-weight-gradient path, else torch (autocast / fp32).
-    ``fuse`` (BlockLink, k, ("take_res",)): honoured on the first path only; sets the link's
-    taker so the block's last BN hands its residual gradient to this conv's dgrad."""
+    ``fuse`` (BlockLink, k, roles): honoured on the first path only; role "take_res" sets
+    the link's taker so the block's last BN hands its residual gradient to this conv's dgrad.
+    ``bnpre`` (list): on the first path receives the epilogue's BatchNorm statistics of the
+    output (ops/batchnorm.py bn_act ``pre``)."""
     if x.is_cuda and x.dtype == torch.bfloat16:
         wb = w.to(torch.bfloat16)
         if convwg.fwd_supported(x, wb, None, None, stride, padding, dilation):
-            if fuse is not None:
+            if fuse is not None and "take_res" in fuse[2]:
                 fuse[0].taker = True
-            return ConvBiasActFn.apply(x, wb, None, None, False, stride, padding, dilation, fuse)
+            return ConvBiasActFn.apply(x, wb, None, None, False, stride, padding, dilation, fuse, False, bnpre)
         if convwg.supported(x, wb, stride, padding, dilation):
             return convwg.conv2d_wg(x, wb, stride, padding, dilation)
         return F.conv2d(x, wb, None, stride, padding, dilation)
@@ -109,10 +115,13 @@ class ConvNorm(nn.Module):
         # (ops/batchnorm.py, csrc/batchnorm.hip)
         # (identity blocks: conv1 role "take_res" adds the residual gradient that conv3's BN
         # backward stashes, role "stash_res" -- see Bottleneck.forward)
+        # (the BN statistics of the conv output come from the conv's epilogue: bnpre)
         link, roles = (fuse[0], fuse[2]) if fuse is not None else (None, ())
+        pre = [] if self.norm.training and BN_EPILOGUE_STATS else None
         y = _conv_nobias(x, w, self.conv.stride, self.conv.padding, self.conv.dilation,
-                         fuse=fuse if "take_res" in roles else None)
-        return bn_act(y, self.norm, residual=residual, relu=relu, link=link if "stash_res" in roles else None)
+                         fuse=fuse if ("take_res" in roles or "stash_dx" in roles) else None, bnpre=pre)
+        return bn_act(y, self.norm, residual=residual, relu=relu, link=link if "stash_res" in roles else None,
+                      pre=pre[0] if pre else None)
 
     def fused_ok(self, x) -> bool:
         """This conv (frozen norm) would run ConvBiasActFn on input x, honouring a BlockLink."""
@@ -201,6 +210,14 @@ class Bottleneck(nn.Module):
                 a1 = self.conv1(x, fuse=(link, 1, ("take_res",)))
                 a2 = self.conv2(a1)
                 return self.conv3(a2, residual=x, relu=True, fuse=(link, 3, ("stash_res",)))
+            # projection block: the shortcut conv's input gradient is parked and added in conv1's
+            # dgrad store (the same contract as the FrozenBN path below)
+            if self.fuse_backward and self.fuse_projection and torch.is_grad_enabled() and self._bn_proj_ok(x):
+                link = BlockLink()
+                a1 = self.conv1(x, fuse=(link, 1, ("take_res", "take_dx")))
+                a2 = self.conv2(a1)
+                idt = self.shortcut(x, fuse=(link, 0, ("stash_dx",)))
+                return self.conv3(a2, residual=idt, relu=True)
             a1 = self.conv1(x)
             a2 = self.conv2(a1)
             idt = x if ident else self.shortcut(x)
@@ -221,6 +238,18 @@ class Bottleneck(nn.Module):
         if link is not None:
             out._mx_link = link
         return out
+
+
+    def _bn_proj_ok(self, x) -> bool:
+        """Both convs reading x (conv1, shortcut) take the implicit-GEMM forward (so conv1's
+        backward finds the shortcut's parked dX); shape-only check with bf16 meta weights."""
+        if self.shortcut is None or not (x.is_cuda and x.dtype == torch.bfloat16):
+            return False
+        for cn in (self.conv1, self.shortcut):
+            wm = torch.empty(cn.conv.weight.shape, dtype=torch.bfloat16, device="meta")
+            if not convwg.fwd_supported(x, wm, None, None, cn.conv.stride, cn.conv.padding, cn.conv.dilation):
+                return False
+        return True
 
 
 class ResNet(nn.Module):

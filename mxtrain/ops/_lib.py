@@ -99,7 +99,7 @@ SIGNATURES = {
     "mx_gemm_kk": [I, P, I, F, I, I, P, P, P],
     # convwg.hip
     # batchnorm.hip
-    "mx_bn_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, F, I, P, P],
+    "mx_bn_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, F, I, P, P, P, P],
     "mx_bn_apply": [P, P, P, P, P, I, I, I, P],
     "mx_bn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, P, P],
     "mx_conv_wgrad_tile": [I],

@@ -3,8 +3,10 @@
 ``bn_act(x, bn, residual, relu)`` computes ``act(BatchNorm(x) (+ residual))`` for an
 ``nn.BatchNorm2d`` ``bn`` whose affine parameters / running statistics stay fp32 (AMP
 style): one statistics pass, a per-channel finalize (running statistics updated in place,
-deterministic two-stage reductions) and one apply pass forward; a statistics pass, a
-finalize and one pass producing dx (and the residual's gradient) backward.  The ResNet-50
+deterministic two-stage reductions) and one apply pass forward -- after a convolution on
+csrc/convwg.hip the statistics come from that convolution's epilogue instead of a pass over
+x; a statistics pass, a finalize and one pass producing dx (and the residual's gradient)
+backward.  The ResNet-50
 bottleneck's BN -> add -> ReLU tail is a single autograd node.  Evaluation mode (or the
 CPU) uses the running statistics through the same apply kernel / plain torch ops.
 
@@ -41,7 +43,7 @@ def _scratch(M: int, C: int, device) -> torch.Tensor:
 class BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, running_mean, running_var, momentum: float, eps: float, relu: bool,
-                link=None):
+                link=None, nbt=None, pre=None):
         N, C, H, W = x.shape
         M = N * H * W
         y = torch.empty_like(x, memory_format=torch.channels_last)
@@ -51,7 +53,8 @@ class BNActFn(torch.autograd.Function):
         b32 = beta.detach().float().contiguous()
         _lib.call("mx_bn_fwd", x.data_ptr(), _lib.ptr(residual), y.data_ptr(), g32.data_ptr(), b32.data_ptr(),
                   mean.data_ptr(), rstd.data_ptr(), _lib.ptr(running_mean), _lib.ptr(running_var), M, C,
-                  float(eps), float(momentum), int(relu), _scratch(M, C, x.device).data_ptr(), _lib.stream())
+                  float(eps), float(momentum), int(relu), _scratch(M, C, x.device).data_ptr(), _lib.ptr(nbt),
+                  _lib.ptr(pre), _lib.stream())
         ctx.relu, ctx.has_res = relu, residual is not None
         ctx.link = link
         ctx.save_for_backward(x, y, mean, rstd, g32)
@@ -77,7 +80,8 @@ class BNActFn(torch.autograd.Function):
             # block input's gradient, so autograd's add of the input's two gradients disappears
             link.stash.append(dres)
             dres = None
-        return (dx, dg.to(ctx.pdtypes[0]), db.to(ctx.pdtypes[1]), dres, None, None, None, None, None, None)
+        return (dx, dg.to(ctx.pdtypes[0]), db.to(ctx.pdtypes[1]), dres, None, None, None, None, None, None, None,
+                None)
 
 
 def bn_act_ref(x, gamma, beta, residual, running_mean, running_var, momentum, eps, relu, training=True):
@@ -91,22 +95,28 @@ def bn_act_ref(x, gamma, beta, residual, running_mean, running_var, momentum, ep
 
 
 def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, residual: Optional[torch.Tensor] = None,
-           relu: bool = False, link=None) -> torch.Tensor:
+           relu: bool = False, link=None, pre: Optional[torch.Tensor] = None) -> torch.Tensor:
     """act(bn(x) (+ residual)) for an ``nn.BatchNorm2d`` (training: batch statistics and
     running-statistics update; eval: running statistics).  ``link``: a BlockLink whose taker
-    (the block's conv1) adds the residual's gradient in its dgrad store."""
+    (the block's conv1) adds the residual's gradient in its dgrad store.  ``pre``: x's
+    per-64-row statistics from the producing convolution's epilogue (ops/convwg.py
+    conv_fwd ``bn_stats``): the forward then never re-reads x for them."""
     if supported(x, residual):
         mom = bn.momentum
+        nbt = None
         if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
             # (the torch fallback below counts the batch inside nn.BatchNorm2d.forward)
-            bn.num_batches_tracked.add_(1)
             if mom is None:   # cumulative moving average, as nn.BatchNorm2d
+                bn.num_batches_tracked.add_(1)
                 mom = 1.0 / float(bn.num_batches_tracked)
+            else:             # counted by the statistics finalize kernel
+                nbt = bn.num_batches_tracked
         if mom is None:
             mom = 0.0
         if bn.training:
             return BNActFn.apply(x, bn.weight, bn.bias, residual, bn.running_mean if bn.track_running_stats else None,
-                                 bn.running_var if bn.track_running_stats else None, mom, bn.eps, relu, link)
+                                 bn.running_var if bn.track_running_stats else None, mom, bn.eps, relu, link, nbt,
+                                 pre)
         # eval: y = act(x * scale + shift (+ res)) with the running statistics
         s = bn.weight.float() * torch.rsqrt(bn.running_var.float() + bn.eps)
         h = bn.bias.float() - bn.running_mean.float() * s

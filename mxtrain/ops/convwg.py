@@ -394,9 +394,11 @@ def fwd_splits(tiles: int, nk: int) -> int:
 
 
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool = False, stride=1, padding=0,
-             dilation=1, res_up: bool = False) -> torch.Tensor:
+             dilation=1, res_up: bool = False, bn_stats: bool = False):
     """act(conv2d(x, w) + b (+ residual, nearest-upsampled 2x with ``res_up``)), NHWC bf16 in
-    and out, one launch."""
+    and out, one launch.  ``bn_stats``: returns (y, pre) where ``pre`` holds the per-64-row
+    BatchNorm statistics of y from the epilogue (csrc/batchnorm.hip mx_bn_fwd's ``pre``), or
+    None when the launch splits its reduction (the statistics pass then reads y)."""
     Cout, Cin, KH, KW = w.shape
     N, _, IH, IW = x.shape
     st, pd, dl = _sym(stride), _sym(padding), _sym(dilation)
@@ -418,8 +420,12 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, b=None, residual=None, relu: bool
               int(res_up), splits, slab.data_ptr() if splits > 1 else 0]
     d[24] = _tickets(x.device) if (splits > 1 and SPLIT_IN_KERNEL) else 0
     d[25] = int(half)
+    pre = None
+    if bn_stats and splits == 1 and Cout % 64 == 0:
+        pre = torch.empty(_lib.query64("mx_bn_pre_size", T, Cout), dtype=torch.float32, device=x.device)
+        d[26] = pre.data_ptr()
     _lib.call("mx_conv_fwd", d, _lib.stream())
-    return y
+    return (y, pre) if bn_stats else y
 
 
 def dgrad_supported(w: torch.Tensor, x_shape, stride, padding=0, dilation=1) -> bool:

@@ -148,8 +148,14 @@ class ConvBiasActFn(torch.autograd.Function):
     "take_res" adds it (see BlockLink)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, res, relu: bool, stride, padding, dilation, fuse=None, res_up=False):
-        y = convwg.conv_fwd(x, w, b, res, relu, stride, padding, dilation, res_up=res_up)
+    def forward(ctx, x, w, b, res, relu: bool, stride, padding, dilation, fuse=None, res_up=False, bnpre=None):
+        # bnpre: a list that receives the epilogue's BatchNorm statistics of y (or None) for
+        # the trainable-BN ResNet (ops/batchnorm.py bn_act ``pre``)
+        if bnpre is not None:
+            y, pre = convwg.conv_fwd(x, w, b, res, relu, stride, padding, dilation, res_up=res_up, bn_stats=True)
+            bnpre.append(pre)
+        else:
+            y = convwg.conv_fwd(x, w, b, res, relu, stride, padding, dilation, res_up=res_up)
         ctx.conf = (list(convwg._pair(stride)), list(convwg._pair(padding)), list(convwg._pair(dilation)))
         ctx.relu, ctx.has_res, ctx.res_up = relu, res is not None, res_up
         ctx.bdtype = b.dtype if b is not None else None
@@ -224,7 +230,7 @@ class ConvBiasActFn(torch.autograd.Function):
             else:
                 dw = torch.ops.aten.convolution_backward(dy, x, w, None, st, pd, dl, False, [0, 0], 1,
                                                          [False, True, False])[1]
-        return dx, dw, db, dres, None, None, None, None, None, None
+        return dx, dw, db, dres, None, None, None, None, None, None, None
 
 
 class Subsample2Fn(torch.autograd.Function):

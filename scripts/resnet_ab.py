@@ -4,8 +4,11 @@ bf16 autocast, SGD-Nesterov) A/B in one process, interleaved rounds on the same 
   fused   csrc/batchnorm.hip BN + residual + ReLU nodes and the implicit-GEMM convolutions
   bn      the fused BN nodes, convolutions on MIOpen (ops/convwg.py switched off)
   torch   nn.BatchNorm2d + add + ReLU on MIOpen (the round-3 path)
+  any other arm: "name:module.attr=value,..." on top of fused (e.g.
+  "noepi:mxtrain.models.resnet.BN_EPILOGUE_STATS=0")
 Prints images/s per arm (median over rounds).
-    python scripts/resnet_ab.py [--batch 256] [--steps 10] [--rounds 3]"""
+    python scripts/resnet_ab.py [--batch 256] [--steps 10] [--rounds 3] [--arms fused,bn,torch]"""
+import importlib
 import argparse
 import os
 import statistics
@@ -21,9 +24,27 @@ from mxtrain.ops import batchnorm as BN  # noqa: E402
 from mxtrain.ops import convwg  # noqa: E402
 
 
+_SAVED = {}
+
+
 def set_arm(arm):
-    convwg.ENABLED = convwg.FWD = convwg.DGRAD = arm == "fused"
-    BN.ENABLED = arm in ("fused", "bn")
+    for (mod, attr), v in _SAVED.items():
+        setattr(mod, attr, v)
+    name, _, spec = arm.partition(":")
+    base = "fused" if spec else name
+    convwg.ENABLED = convwg.FWD = convwg.DGRAD = base == "fused"
+    BN.ENABLED = base in ("fused", "bn")
+    for item in filter(None, spec.split(",")):
+        path, val = item.split("=")
+        modname, attr = path.rsplit(".", 1)
+        try:
+            mod = importlib.import_module(modname)
+        except ModuleNotFoundError:   # a class attribute: module.Class.attr
+            modname, cls = modname.rsplit(".", 1)
+            mod = getattr(importlib.import_module(modname), cls)
+        _SAVED.setdefault((mod, attr), getattr(mod, attr))
+        cur = getattr(mod, attr)
+        setattr(mod, attr, type(cur)(int(val)) if isinstance(cur, (bool, int)) else type(cur)(val))
 
 
 def main():
@@ -31,6 +52,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--arms", default="fused,bn,torch")
     a = ap.parse_args()
     torch.manual_seed(0)
     net = R.resnet50(norm="bn", num_classes=1000).cuda().to(memory_format=torch.channels_last)
@@ -46,7 +68,7 @@ def main():
         opt.step()
         return loss
 
-    res = {arm: [] for arm in ("fused", "bn", "torch")}
+    res = {arm: [] for arm in a.arms.split(";" if ":" in a.arms else ",")}
     for arm in res:   # warm-up (MIOpen immediate-mode solution lookups, allocator)
         set_arm(arm)
         for _ in range(3):
@@ -63,7 +85,7 @@ def main():
             torch.cuda.synchronize()
             res[arm].append(a.batch * a.steps / (time.time() - t0))
     for arm, v in res.items():
-        print(f"{arm:6s} {statistics.median(v):8.1f} images/s  (rounds {[round(t) for t in v]})  loss {float(loss):.3f}")
+        print(f"{arm.partition(':')[0]:6s} {statistics.median(v):8.1f} images/s  (rounds {[round(t) for t in v]})  loss {float(loss):.3f}")
 
 
 if __name__ == "__main__":

@@ -96,11 +96,65 @@ def test_resnet50_bn_step_uses_fused_paths():
     assert all(p.grad is not None for p in net.parameters() if p.requires_grad)
 
 
-def test_bn_bottleneck_residual_gradient_fused_into_conv1_dgrad(monkeypatch):
+@pytest.mark.parametrize("N,Cin,Cout,H,W,k,stride,split", [(2, 64, 64, 7, 7, 3, 1, True),
+                                                          (32, 64, 256, 56, 56, 1, 1, False),
+                                                          (64, 256, 128, 28, 28, 3, 2, False),
+                                                          (16, 1024, 2048, 14, 14, 1, 2, False),
+                                                          (3, 128, 192, 10, 13, 1, 1, False)])
+def test_conv_epilogue_bn_statistics(N, Cin, Cout, H, W, k, stride, split):
+    """The implicit-GEMM forward's epilogue writes per-64-row BatchNorm statistics of its
+    (rounded) output: they match the block statistics of y in fp32, the stored y is the same
+    bits as without them, and bn_act fed with them (merged to <= 512 blocks when there are
+    more) matches bn_act's own statistics pass -- output, running statistics, batch count."""
+    from mxtrain.ops import convwg
+    from mxtrain.ops.batchnorm import bn_act
+    g = torch.Generator(device=DEV).manual_seed(Cin + Cout + H)
+    x = torch.randn(N, Cin, H, W, device=DEV, generator=g).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(Cout, Cin, k, k, device=DEV, generator=g) / (Cin * k * k) ** 0.5 + 0.02).to(
+        torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert convwg.fwd_supported(x, w, None, None, stride, k // 2, 1)
+    y0 = convwg.conv_fwd(x, w, None, None, False, stride, k // 2, 1)
+    y, pre = convwg.conv_fwd(x, w, None, None, False, stride, k // 2, 1, bn_stats=True)
+    assert torch.equal(y0, y)
+    if split:   # split-K launch: no epilogue statistics, bn_act runs its own pass
+        assert pre is None
+        return
+    T = y.shape[0] * y.shape[2] * y.shape[3]
+    nb = (T + 63) // 64
+    assert pre.numel() == nb * 2 * Cout
+    rows = y.permute(0, 2, 3, 1).reshape(T, Cout).float()
+    pad = torch.full((nb * 64 - T, Cout), float("nan"), device=DEV)
+    blk = torch.cat([rows, pad]).view(nb, 64, Cout)
+    cnt = (~blk.isnan()).sum(1).float()
+    mean = torch.nansum(blk, 1) / cnt
+    m2 = torch.nansum((blk - mean[:, None]) ** 2, 1)
+    pm, pq = pre.view(2, Cout, nb)   # channel-major [C][blocks]
+    _close(pm.t(), mean, 1e-4, 1e-4, "block means")
+    _close(pq.t(), m2, 1e-3 * 64, 2e-3, "block M2")
+    gamma = torch.empty(Cout, device=DEV).uniform_(0.5, 1.5, generator=g)
+    beta = torch.empty(Cout, device=DEV).uniform_(-0.5, 0.5, generator=g)
+    outs = []
+    for p in (None, pre):
+        bn = torch.nn.BatchNorm2d(Cout).to(DEV)
+        with torch.no_grad():
+            bn.weight.copy_(gamma)
+            bn.bias.copy_(beta)
+        outs.append((bn_act(y, bn, None, True, pre=p), bn))
+    (ya, bna), (yb, bnb) = outs
+    _close(yb, ya, 2e-2, 1e-2, "bn_act with epilogue statistics")
+    _close(bnb.running_mean, bna.running_mean, 1e-5, 1e-4, "running_mean")
+    _close(bnb.running_var, bna.running_var, 1e-5, 1e-4, "running_var")
+    assert int(bna.num_batches_tracked) == 1 and int(bnb.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("proj", [False, True])
+def test_bn_bottleneck_residual_gradient_fused_into_conv1_dgrad(monkeypatch, proj):
     """Trainable-BN identity blocks: conv3's BN backward stashes the residual gradient and
     conv1's implicit-GEMM dgrad adds it in its store (one rounding) instead of autograd's
-    separate add.  Against the unfused blocks and an fp32 run: same forward, gradients as
-    close to fp32 as the unfused ones; the fused dgrad actually received the addend."""
+    separate add; projection blocks (``proj``): the shortcut conv's input gradient is parked
+    and added the same way.  Against the unfused blocks and an fp32 run: same forward,
+    gradients as close to fp32 as the unfused ones; the fused dgrad received the addend."""
     import copy
     from mxtrain.models.resnet import Bottleneck
     from mxtrain.ops import convwg
@@ -113,13 +167,15 @@ def test_bn_bottleneck_residual_gradient_fused_into_conv1_dgrad(monkeypatch):
 
     monkeypatch.setattr(convwg, "conv_dgrad", spy)
     torch.manual_seed(5)
-    blocks = torch.nn.Sequential(Bottleneck(512, 128, norm="bn"), Bottleneck(512, 128, norm="bn")).to(DEV)
+    first = Bottleneck(256, 128, stride=2, norm="bn") if proj else Bottleneck(512, 128, norm="bn")
+    blocks = torch.nn.Sequential(first, Bottleneck(512, 128, norm="bn")).to(DEV)
     blocks = blocks.to(memory_format=torch.channels_last)
     for m in blocks.modules():
         if isinstance(m, torch.nn.BatchNorm2d):
             m.weight.data.uniform_(0.5, 1.5)
             m.bias.data.uniform_(-0.2, 0.2)
-    x0 = torch.randn(4, 512, 48, 64, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    cin = 256 if proj else 512
+    x0 = torch.randn(4, cin, 48, 64, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     out = {}
     gy = None
     for fuse in (False, True):
