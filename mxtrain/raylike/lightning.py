@@ -183,12 +183,14 @@ class Trainer:
                 if self.limit_train is not None and i >= self.limit_train:
                     break
                 batch = self._to(batch, dev)
+                captured = False
                 if graph is None and self.global_step >= GRAPH_WARMUP and self._graph_ok(dev, opt, world):
                     # the last eager step's loss keeps its autograd graph (and AccumulateGrad
                     # nodes bound to the default stream) alive: a capture that reaches them
                     # waits across streams and the runtime crashes at capture end
                     loss = out = None
                     graph = self._capture(ddp, opt, batch, i, dev)
+                    captured = True
                 if graph is not None and graph.matches(batch):
                     loss = graph.replay(batch)
                 else:
@@ -201,7 +203,7 @@ class Trainer:
                 if sched is not None:
                     sched.step()
                 self.global_step += 1
-                if i == 2:          # exclude warm-up batches from the throughput figure
+                if i == 2 or captured:   # exclude warm-up batches (and the capture) from the throughput
                     if dev.type == "cuda":
                         torch.cuda.synchronize()
                     t0, nsamp = time.time(), 0

@@ -2,7 +2,8 @@
 """Interleaved same-box A/B of the GPT-2 bench step: ROUNDS x (A, B) child runs of
 `bench.py --no-maskrcnn --no-extra-configs` with the extra flags of --a / --b, median
 tokens/s and ms/step per arm.
-    python scripts/bench_ab.py --b "--no-wgrad-stream" --rounds 3 --steps 20"""
+    python scripts/bench_ab.py --b "--no-wgrad-stream" --rounds 3 --steps 20
+(a "+" in --a / --b separates arguments too: --b=--model=gpt3-6.7b+--no-defer-update)"""
 import argparse
 import json
 import os
@@ -26,7 +27,7 @@ def main():
     for r in range(a.rounds):
         for tag, extra in (("A", a.a), ("B", a.b)):
             cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", "--steps", str(a.steps),
-                   "--warmup", str(a.warmup), "--no-maskrcnn", "--no-extra-configs"] + shlex.split(extra)
+                   "--warmup", str(a.warmup), "--no-maskrcnn", "--no-extra-configs"] + shlex.split(extra.replace("+", " "))
             out = subprocess.run(cmd, check=True, stdout=subprocess.PIPE, text=True).stdout
             rec = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
             res[tag].append((rec["value"], rec["ms_per_step"]))
