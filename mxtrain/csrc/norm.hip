@@ -531,6 +531,87 @@ __global__ __launch_bounds__(256) void ln_bwd_cols_kernel(
   }
 }
 
+// Row-wise part of the backward for wide rows (cols > kSplitCols: GPT-3 6.7B's h = 4096), the
+// column sums coming from ln_bwd_cols_kernel.  One row per wave.  h / dy / dres / gamma stay
+// packed bf16 in registers (4 VGPRs per 8 columns) and xhat, gamma * dy are recomputed in the
+// second pass: ln_bwd_kernel holds them as fp32 row arrays, 256 VGPRs at NV = 8 -- one wave
+// per SIMD, so a wave's loads and its stores never overlapped another wave's (~60 % of the
+// HBM bandwidth at 4096 x 4096).
+template <int NV, bool RMS>
+__global__ __launch_bounds__(256) void ln_bwd_wide_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dres,
+    const uint16_t* __restrict__ h, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const uint16_t* __restrict__ gamma,
+    uint16_t* __restrict__ dh_out, uint16_t* __restrict__ dx_drop, int rows, int cols,
+    uint32_t thresh, float keep_scale, const uint32_t* __restrict__ seed_ptr, uint32_t salt,
+    uint64_t elem0) {
+  const int lane = threadIdx.x & 63;
+  const int row = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (row >= rows) return;
+  const uint32_t seed = seed_ptr ? (*seed_ptr + salt) : 0u;
+  const size_t base = (size_t)row * cols;
+  const uint16_t* rsrc = dres ? dres : h;
+  uint32_t rm = dres ? ~0u : 0u;   // (opaque mask: see ln_bwd_kernel)
+  asm volatile("" : "+v"(rm));
+  uint4 hb[NV], db[NV], rb[NV], gb[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = min((lane + 64 * i) * 8, cols - 8);
+    hb[i] = *reinterpret_cast<const uint4*>(h + base + c);
+    db[i] = *reinterpret_cast<const uint4*>(dy + base + c);
+    gb[i] = *reinterpret_cast<const uint4*>(gamma + c);
+    rb[i] = *reinterpret_cast<const uint4*>(rsrc + base + c);
+  }
+  const float mean = RMS ? 0.f : mean_in[row];
+  const float rstd = rstd_in[row];
+  __builtin_amdgcn_sched_barrier(0);
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const bool ok = (lane + 64 * i) * 8 < cols;
+    float hv[8], dv[8], g[8];
+    unpack8(hb[i], hv);
+    unpack8(db[i], dv);
+    unpack8(gb[i], g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gy = ok ? dv[j] * g[j] : 0.f;
+      s1 += gy;
+      s2 += gy * ((hv[j] - mean) * rstd);
+    }
+  }
+  const float m1 = RMS ? 0.f : wave_sum(s1) / (float)cols;
+  const float m2 = wave_sum(s2) / (float)cols;
+  // opaque to the optimiser: otherwise it keeps the first pass's unpacked fp32 values alive
+  // across the reductions for reuse below (256 VGPRs again) instead of re-unpacking
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    asm volatile("" : "+v"(hb[i].x), "+v"(hb[i].y), "+v"(hb[i].z), "+v"(hb[i].w));
+    asm volatile("" : "+v"(db[i].x), "+v"(db[i].y), "+v"(db[i].z), "+v"(db[i].w));
+    asm volatile("" : "+v"(gb[i].x), "+v"(gb[i].y), "+v"(gb[i].z), "+v"(gb[i].w));
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 8;
+    const bool ok = c < cols;
+    float hv[8], dv[8], g[8], r[8], o[8];
+    unpack8(hb[i], hv);
+    unpack8(db[i], dv);
+    unpack8(gb[i], g);
+    unpack8(make_uint4(rb[i].x & rm, rb[i].y & rm, rb[i].z & rm, rb[i].w & rm), r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = r[j] + rstd * (dv[j] * g[j] - m1 - ((hv[j] - mean) * rstd) * m2);
+    if (ok) *reinterpret_cast<uint4*>(dh_out + base + c) = pack8(o);
+    if (dx_drop) {
+      bool km[8];
+      if (thresh) dropout_keep8(elem0 + base + c, seed, thresh, km);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = thresh ? (km[j] ? o[j] * keep_scale : 0.f) : o[j];
+      if (ok) *reinterpret_cast<uint4*>(dx_drop + base + c) = pack8(o);
+    }
+  }
+}
+
 int kSplitCols = 2048;   // wider rows: row kernel without column sums + column kernel
 constexpr int kColsRowsPerBlock = 32;
 
@@ -558,19 +639,18 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
   const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
   dim3 grid(bwd_grid(rows)), block(256);
   if (cols > kSplitCols) {
-    // row-wise pass (no LDS), then the column sums in a column-parallel pass
+    // row-wise pass (no LDS, one row per wave), then the column sums in a column-parallel pass
 #define MX_LNB_SPLIT(N)                                                                \
   case N:                                                                              \
-    hipLaunchKernelGGL((ln_bwd_kernel<N, RMS, false, false>), grid, block, 0, s,       \
+    hipLaunchKernelGGL((ln_bwd_wide_kernel<N, RMS>), dim3((rows + 3) / 4), block, 0, s, \
                        (const uint16_t*)dy, (const uint16_t*)dres, (const uint16_t*)h, \
                        mean, rstd, (const uint16_t*)gamma, (uint16_t*)dh_out,          \
-                       (uint16_t*)dx_drop, partial, rows, cols, thresh, ks, seed,      \
-                       salt, elem0);                                                   \
+                       (uint16_t*)dx_drop, rows, cols, thresh, ks, seed, salt, elem0); \
     break;
     switch (nv) {
       MX_LNB_SPLIT(1) MX_LNB_SPLIT(2) MX_LNB_SPLIT(3) MX_LNB_SPLIT(4)
-      MX_LNB_SPLIT(5) MX_LNB_SPLIT(6) MX_LNB_SPLIT(8) MX_LNB_SPLIT(10) MX_LNB_SPLIT(12)
-      MX_LNB_SPLIT(16)
+      MX_LNB_SPLIT(5) MX_LNB_SPLIT(6) MX_LNB_SPLIT(7) MX_LNB_SPLIT(8) MX_LNB_SPLIT(10)
+      MX_LNB_SPLIT(12) MX_LNB_SPLIT(16)
       default: return hipErrorInvalidValue;
     }
 #undef MX_LNB_SPLIT

@@ -38,7 +38,8 @@ def _seed():
     assert torch.cuda.is_available()
 
 
-@pytest.mark.parametrize("rows,cols", [(512, 768), (512, 1024), (4100, 1024), (512, 4096), (512, 8192)])
+@pytest.mark.parametrize("rows,cols", [(512, 768), (512, 1024), (4100, 1024), (512, 4096), (512, 8192),
+                                       (256, 2600)])
 def test_layernorm_fwd_bwd(rows, cols):
     x = _bf(torch.randn(rows, cols))
     g = _bf(1 + 0.1 * torch.randn(cols))
