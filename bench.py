@@ -218,7 +218,9 @@ def run_resnet(world: int, steps: int, extra=(), timeout: float = 300.0) -> dict
         if rec is None or rec.get("value") is None:
             return {"error": "no result record: " + text[-300:]}
         return {"img_s": round(rec["value"], 1), "workers": world, "batch_per_worker": 256, "steps": steps,
-                "warmup": 3, "hipgraph": graphed and world == 1, "wall_s": round(time.time() - t0, 1)}
+                "warmup": "3 eager steps + the hipGraph capture step" if graphed and world == 1 else 3,
+                "timed_steps": steps - (4 if graphed and world == 1 else 3),
+                "hipgraph": graphed and world == 1, "wall_s": round(time.time() - t0, 1)}
     finally:
         import shutil
         if os.path.exists(out):
