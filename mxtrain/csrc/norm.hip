@@ -612,14 +612,14 @@ __global__ __launch_bounds__(256) void ln_bwd_wide_kernel(
   }
 }
 
-int kSplitCols = 2048;   // wider rows: row kernel without column sums + column kernel
+constexpr int kSplitCols = 2048;   // wider rows: row kernel without column sums + column kernel
 constexpr int kColsRowsPerBlock = 32;
 
 // rows per wave of the fused backward: 2 (BDA-LN at 4096 x 1024 with its column reduction,
-// scripts/ln_ab.py: 16.0 us at 2, 17.2 at 4, 16.2 at 1 -- with load groups, two waves per
+// profiles/r5_s1/ln_ab_rows_per_wave.txt: 16.0 us at 2, 17.2 at 4, 16.2 at 1 -- with load groups, two waves per
 // SIMD hide each other's dropout-hash VALU better than the halved partials save)
-int kBwdRowsPerWave = 2;
-int kBwdMaxBlocks = 512;   // partial slabs: [blocks][3][cols] fp32
+constexpr int kBwdRowsPerWave = 2;
+constexpr int kBwdMaxBlocks = 512;   // partial slabs: [blocks][3][cols] fp32
 int bwd_grid(int rows) {
   const int rpb = 4 * kBwdRowsPerWave;
   int g = (rows + rpb - 1) / rpb;
@@ -690,24 +690,6 @@ hipError_t launch_bwd(const void* dy, const void* dres, const void* h, const flo
 
 // number of partial slabs the norm backward writes (caller sizes `partial`)
 MX_EXPORT int mx_norm_bwd_nparts(int rows) { return bwd_grid(rows); }
-// rows per wave of the fused (register-partial) backward; returns the old value
-MX_EXPORT int mx_norm_bwd_rows_per_wave(int r) {
-  const int old = kBwdRowsPerWave;
-  if (r > 0) kBwdRowsPerWave = r;
-  return old;
-}
-// cap on the fused backward's workgroups (= partial slabs); returns the old value
-MX_EXPORT int mx_norm_bwd_max_blocks(int b) {
-  const int old = kBwdMaxBlocks;
-  if (b > 0) kBwdMaxBlocks = b;
-  return old;
-}
-// rows wider than this use the split (row + column) backward; returns the old value
-MX_EXPORT int mx_norm_split_cols(int c) {
-  const int old = kSplitCols;
-  if (c > 0) kSplitCols = c;
-  return old;
-}
 MX_EXPORT int mx_norm_bwd_nparts2(int rows, int cols) {
   return cols > kSplitCols ? (rows + kColsRowsPerBlock - 1) / kColsRowsPerBlock : bwd_grid(rows);
 }

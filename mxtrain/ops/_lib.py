@@ -30,8 +30,6 @@ SIGNATURES = {
     # norm.hip
     "mx_norm_bwd_nparts": [I],
     "mx_norm_bwd_nparts2": [I, I],
-    "mx_norm_split_cols": [I],
-    "mx_norm_bwd_rows_per_wave": [I],
     "mx_flash_qmajor_bk": [I, I],
     "mx_flash_kmajor128_variant": [I],
     # membw.hip (HBM roofline probe, scripts/hbm_probe.py)
@@ -154,7 +152,6 @@ SIGNATURES = {
     "mx_rpn_pack": [P, P, P, I, I, I, I, I, P],
     # knobs (one int; return the previous setting)
     "mx_flash_dropmask_variant": [I],
-    "mx_norm_bwd_max_blocks": [I],
 }
 
 

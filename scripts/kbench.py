@@ -103,8 +103,7 @@ def main():
         rec("ln_bwd 4096x4096 (bda)", timeit(lambda: N.norm_bwd(x, x, hh_, mean_, rstd_, g, want_dx=True, p=0.1,
                                                                  seed_t=seed, dgamma=dg, dbeta=db, dbias=dbi,
                                                                  accumulate=True)), rows * cols * 2 * 5)
-    if want("lnsplit"):   # GPT-2 345M LN backward: fused (register partials) vs split
-        from mxtrain.ops import _lib
+    if want("lnsplit"):   # GPT-2 345M LN backward (fused: register column partials) and BDA forward
         rows, cols = 4096, 1024
         x = torch.randn(rows, cols, device=dev).to(bf)
         g = torch.ones(cols, device=dev, dtype=bf)
@@ -112,22 +111,11 @@ def main():
         seed = torch.tensor([1], dtype=torch.int32, device=dev)
         hh_, y_, mean_, rstd_ = N.bda_norm_fwd(x, bb, x, g, bb, p=0.1, seed_t=seed)
         dg, db, dbi = (torch.zeros(cols, device=dev, dtype=bf) for _ in range(3))
-        fn = lambda: N.norm_bwd(x, x, hh_, mean_, rstd_, g, want_dx=True, p=0.1, seed_t=seed,  # noqa: E731
-                                dgamma=dg, dbeta=db, dbias=dbi, accumulate=True)
-        for thr in (2048, 512):
-            old = _lib._fn("mx_norm_split_cols")(thr)   # a setter: never through the memoised query
-            _lib._QCACHE.clear()
-            rec(f"ln_bwd 4096x1024 split>{thr}", timeit(fn), rows * cols * 2 * 5)
-            _lib._fn("mx_norm_split_cols")(old)
-            _lib._QCACHE.clear()
+        rec("ln_bwd 4096x1024", timeit(lambda: N.norm_bwd(x, x, hh_, mean_, rstd_, g, want_dx=True, p=0.1,
+                                                          seed_t=seed, dgamma=dg, dbeta=db, dbias=dbi,
+                                                          accumulate=True)), rows * cols * 2 * 5)
         rec("bda_ln_fwd 4096x1024", timeit(lambda: N.bda_norm_fwd(x, bb, x, g, bb, p=0.1, seed_t=seed)),
             rows * cols * 2 * 4)
-        for rpw in (2, 4, 8):   # rows per wave of the fused backward (row pipeline + partials)
-            old = _lib._fn("mx_norm_bwd_rows_per_wave")(rpw)
-            _lib._QCACHE.clear()
-            rec(f"ln_bwd 4096x1024 rpw{rpw}", timeit(fn), rows * cols * 2 * 5)
-            _lib._fn("mx_norm_bwd_rows_per_wave")(old)
-            _lib._QCACHE.clear()
     if want("norm"):
         x = torch.randn(T, h, device=dev).to(bf)
         r_ = torch.randn(T, h, device=dev).to(bf)
