@@ -31,7 +31,7 @@ namespace {
 constexpr int kPH = 7, kPW = 8;                      // pooled outputs per workgroup
 constexpr int kSH = 2 * kPH + 1, kSW = 2 * kPW + 1;  // stem pixels per workgroup (15 x 17 = 255)
 constexpr int kLdsRow = 72;                          // bf16 per LDS pixel row (64 + 8 pad)
-int g_stem_grid = 512;                               // persistent workgroups (two per CU)
+constexpr int g_stem_grid = 512;                     // persistent workgroups (two per CU)
 
 struct StemArgs {
   const uint8_t* img;     // [N][3][H][W]
@@ -242,9 +242,3 @@ MX_EXPORT int mx_stem_pool(const void* img, const void* w, const void* bias, voi
   return (int)hipGetLastError();
 }
 
-// A/B: persistent grid of the stem kernel; negative: query.  Returns the old value.
-MX_EXPORT int mx_stem_grid(int g) {
-  const int old = g_stem_grid;
-  if (g > 0) g_stem_grid = g;
-  return old;
-}

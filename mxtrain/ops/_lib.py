@@ -129,7 +129,6 @@ SIGNATURES = {
     "mx_copy_rows": [P, P, I, I, I, I, I64, I64, P],
     "mx_normalize_u8_nhwc": [P, P, I, I, I, P, P, P],
     "mx_stem_pool": [P, P, P, P, I, I, I, P, P, P],
-    "mx_stem_grid": [I],
     "mx_crop_resize_masks": [P, I, I, P, P, I, I, P, P],
     "mx_crop_resize_mask_crops": [P, P, I, I, P, P, I, I, P, P],
     "mx_topk_rows_long": [P, I, I, I, I, I, I, I, P, P, P, P, P],
