@@ -1,0 +1,130 @@
+// 3x3 / stride-2 / pad-1 max-pool of an NHWC bf16 tensor -- the ResNet-50 stem's pool0
+// (BASELINE config 5: conv -> BN -> ReLU -> max-pool at 112 x 112 x 64 per image).
+//
+// torch's NHWC max-pool saves an int64 index per output element and its backward scatters:
+// 250 + 632 us per step at batch 256 (profiles/r6/resnet50_census_final_tree.txt), against
+// ~110 us each for the bytes that have to move.  Here the forward stores the argmax as one
+// byte per output element (its position 0..8 in the window) and the backward GATHERS: every
+// input pixel visits the <= 2 x 2 windows that contain it and adds the gradients of those
+// whose argmax is that pixel, in a fixed order (deterministic, no atomics, no zero fill).
+// Ties keep the first maximum in window order, as torch (strict >); padding never wins.
+// One thread per 8 channels of a pixel: 16-B loads / stores, 8-B argmax words.
+#include "common.h"
+
+using namespace mx;
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__global__ __launch_bounds__(kThreads) void maxpool3s2_fwd_kernel(const uint16_t* __restrict__ x,
+                                                                  uint16_t* __restrict__ y, uint8_t* __restrict__ arg,
+                                                                  int N, int H, int W, int C, int OH, int OW) {
+  const int c8 = C / 8;
+  const int64_t total = (int64_t)N * OH * OW * c8;
+  for (int64_t v = (int64_t)blockIdx.x * kThreads + threadIdx.x; v < total; v += (int64_t)gridDim.x * kThreads) {
+    const int cv = (int)(v % c8);
+    int64_t p = v / c8;
+    const int ow = (int)(p % OW);
+    p /= OW;
+    const int oh = (int)(p % OH);
+    const int n = (int)(p / OH);
+    float m[8];
+    uint32_t idx[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      m[j] = -INFINITY;
+      idx[j] = 0u;
+    }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = 2 * oh - 1 + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = 2 * ow - 1 + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        float f[8];
+        unpack8(reinterpret_cast<const uint4*>(x + (((size_t)n * H + ih) * W + iw) * C)[cv], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (f[j] > m[j] || f[j] != f[j]) {   // (NaN propagates, as torch)
+            m[j] = f[j];
+            idx[j] = (uint32_t)(kh * 3 + kw);
+          }
+      }
+    }
+    const size_t o = (((size_t)n * OH + oh) * OW + ow) * C + 8 * cv;
+    *reinterpret_cast<uint4*>(y + o) = pack8(m);
+    uint2 a;
+    a.x = idx[0] | (idx[1] << 8) | (idx[2] << 16) | (idx[3] << 24);
+    a.y = idx[4] | (idx[5] << 8) | (idx[6] << 16) | (idx[7] << 24);
+    *reinterpret_cast<uint2*>(arg + o) = a;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void maxpool3s2_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                                  const uint8_t* __restrict__ arg,
+                                                                  uint16_t* __restrict__ dx, int N, int H, int W,
+                                                                  int C, int OH, int OW) {
+  const int c8 = C / 8;
+  const int64_t total = (int64_t)N * H * W * c8;
+  for (int64_t v = (int64_t)blockIdx.x * kThreads + threadIdx.x; v < total; v += (int64_t)gridDim.x * kThreads) {
+    const int cv = (int)(v % c8);
+    int64_t p = v / c8;
+    const int w = (int)(p % W);
+    p /= W;
+    const int h = (int)(p % H);
+    const int n = (int)(p / H);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // the windows containing row h: oh in {(h + 1) / 2 - 1, (h + 1) / 2} with kh = h - 2 oh + 1 in [0, 2]
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int oh = (h + 1) / 2 - 1 + a;
+      const int kh = h - 2 * oh + 1;
+      if ((unsigned)oh >= (unsigned)OH || (unsigned)kh > 2u) continue;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int ow = (w + 1) / 2 - 1 + b;
+        const int kw = w - 2 * ow + 1;
+        if ((unsigned)ow >= (unsigned)OW || (unsigned)kw > 2u) continue;
+        const size_t o = (((size_t)n * OH + oh) * OW + ow) * C + 8 * cv;
+        const uint2 am = *reinterpret_cast<const uint2*>(arg + o);
+        const uint32_t me = (uint32_t)(kh * 3 + kw);
+        float g[8];
+        unpack8(*reinterpret_cast<const uint4*>(dy + o), g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t aj = ((j < 4 ? am.x : am.y) >> (8 * (j & 3))) & 0xffu;
+          if (aj == me) acc[j] += g[j];
+        }
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + (((size_t)n * H + h) * W + w) * C + 8 * cv) = pack8(acc);
+  }
+}
+
+int grid_for(int64_t nvec) {
+  const int64_t g = (nvec + kThreads - 1) / kThreads;
+  return (int)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
+}
+
+}  // namespace
+
+// x [N][H][W][C] -> y [N][OH][OW][C] (+ argmax bytes [N][OH][OW][C]); OH = (H - 1) / 2 + 1
+MX_EXPORT int mx_maxpool3s2_fwd(const void* x, void* y, void* arg, int N, int H, int W, int C, hipStream_t s) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8) return hipErrorInvalidValue;
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  hipLaunchKernelGGL(maxpool3s2_fwd_kernel, dim3(grid_for((int64_t)N * OH * OW * (C / 8))), dim3(kThreads), 0, s,
+                     (const uint16_t*)x, (uint16_t*)y, (uint8_t*)arg, N, H, W, C, OH, OW);
+  return hipGetLastError();
+}
+
+// dy [N][OH][OW][C] + argmax -> dx [N][H][W][C] (every element written)
+MX_EXPORT int mx_maxpool3s2_bwd(const void* dy, const void* arg, void* dx, int N, int H, int W, int C, hipStream_t s) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8) return hipErrorInvalidValue;
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  hipLaunchKernelGGL(maxpool3s2_bwd_kernel, dim3(grid_for((int64_t)N * H * W * (C / 8))), dim3(kThreads), 0, s,
+                     (const uint16_t*)dy, (const uint8_t*)arg, (uint16_t*)dx, N, H, W, C, OH, OW);
+  return hipGetLastError();
+}

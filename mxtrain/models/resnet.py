@@ -21,7 +21,7 @@ import torch.nn.functional as F
 from . import compute_weights as _cw
 from ..ops import convwg
 from ..ops.batchnorm import bn_act
-from ..ops.epilogue import BlockLink, ConvBiasActFn, conv_bias_act, fused_conv_ok
+from ..ops.epilogue import BlockLink, ConvBiasActFn, conv_bias_act, fused_conv_ok, maxpool3s2
 
 
 # trainable BN: batch statistics from the producing conv's epilogue (A/B switch, scripts/resnet_ab.py)
@@ -281,7 +281,7 @@ class ResNet(nn.Module):
         """C2..C5; ``stem_done``: x is already the pooled stem output (ops/stem.py)."""
         if not stem_done:
             x = self.stem(x)
-            x = F.max_pool2d(x, 3, 2, 1)
+            x = maxpool3s2(x)   # (NHWC bf16: csrc/pool.hip; else F.max_pool2d(x, 3, 2, 1))
         outs = []
         for st in self.stages:
             x = st(x)

@@ -140,6 +140,8 @@ SIGNATURES = {
     "mx_merge_keep_topk": [P, P, P, I, I, I, I, P, P, P],
     "mx_down2_add": [P, P, P, I, I, I, I, P],
     "mx_subsample2": [P, P, I, I, I, I, I, P],
+    "mx_maxpool3s2_fwd": [P, P, P, I, I, I, I, P],
+    "mx_maxpool3s2_bwd": [P, P, P, I, I, I, I, P],
     "mx_colsum_jobs": [P, I, P],
     "mx_roi_candidates": [P, I, P, P, I, I, P, P, P],
     "mx_roi_fgkey": [P, P, P, I, F, P, P],

@@ -264,6 +264,41 @@ def subsample2(x: torch.Tensor) -> torch.Tensor:
     return F.max_pool2d(x, 1, 2)
 
 
+class MaxPool3s2Fn(torch.autograd.Function):
+    """max_pool2d(x, 3, 2, 1) of an NHWC bf16 tensor (the ResNet stem's pool0) on csrc/pool.hip:
+    a one-byte window argmax instead of torch's int64 indices, and a gathering backward (each
+    input pixel sums the <= 4 windows that picked it: deterministic, no zero fill)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N, C, H, W = x.shape
+        OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y = torch.empty((N, OH, OW, C), dtype=x.dtype, device=x.device)
+        arg = torch.empty((N, OH, OW, C), dtype=torch.uint8, device=x.device)
+        _lib.call("mx_maxpool3s2_fwd", x.data_ptr(), y.data_ptr(), arg.data_ptr(), N, H, W, C, _lib.stream())
+        ctx.save_for_backward(arg)
+        ctx.shape = (N, C, H, W)
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        (arg,) = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        if not _nhwc(g) or g.data_ptr() % 16:
+            g = g.contiguous(memory_format=torch.channels_last)
+        dx = torch.empty((N, H, W, C), dtype=g.dtype, device=g.device)
+        _lib.call("mx_maxpool3s2_bwd", g.data_ptr(), arg.data_ptr(), dx.data_ptr(), N, H, W, C, _lib.stream())
+        return dx.permute(0, 3, 1, 2)
+
+
+def maxpool3s2(x: torch.Tensor) -> torch.Tensor:
+    """F.max_pool2d(x, 3, 2, 1)."""
+    if (_lib.use_hip(x) and x.dtype == torch.bfloat16 and _nhwc(x) and x.shape[1] % 8 == 0
+            and x.data_ptr() % 16 == 0):
+        return MaxPool3s2Fn.apply(x)
+    return F.max_pool2d(x, 3, 2, 1)
+
+
 def down2_sum(g: torch.Tensor, add: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Gradient of the 2x nearest upsampling: each 2 x 2 block summed (+ ``add``, a second
     gradient of the same tensor), NHWC memory kept -- one pass (csrc/epilogue.hip

@@ -205,3 +205,26 @@ def test_bn_bottleneck_residual_gradient_fused_into_conv1_dgrad(monkeypatch, pro
         rn = float(r.norm()) + 1e-12
         ef, eu = float((a - r).norm()) / rn, float((c - r).norm()) / rn
         assert ef <= 1.25 * eu + 1e-3, (ef, eu)
+
+
+@pytest.mark.parametrize("N,C,H,W,relu", [(4, 64, 112, 112, True), (2, 8, 7, 9, False), (3, 24, 10, 13, True),
+                                          (1, 16, 1, 1, False)])
+def test_maxpool3s2_matches_torch(N, C, H, W, relu):
+    """The stem's 3x3 / 2 / pad-1 max-pool (csrc/pool.hip: one-byte window argmax, gathering
+    backward) against F.max_pool2d: the same output bits and, with ReLU ties (many zeros per
+    window: the first maximum in window order wins in both), the same input gradient."""
+    from mxtrain.ops.epilogue import maxpool3s2
+    g = torch.Generator(device=DEV).manual_seed(C + H)
+    x = torch.randn(N, C, H, W, device=DEV, generator=g)
+    if relu:
+        x = torch.relu(x)
+    x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xa = x.clone().requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    y = maxpool3s2(xa)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    assert y.shape == yr.shape and torch.equal(y, yr)
+    dy = torch.randn(y.shape, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y.backward(dy)
+    yr.backward(dy)
+    _close(xa.grad, xr.grad, 1e-2, 1e-2, "dx")
