@@ -128,6 +128,79 @@ class ComputeWeights:
         return False
 
 
+def _cast_dense(t: torch.Tensor) -> bool:
+    return (t.is_cuda and t.numel() % 8 == 0 and t.data_ptr() % 16 == 0
+            and (t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))))
+
+
+def _cast_launch(pairs, to_bf16: bool) -> None:
+    """One csrc/cast.hip launch per <= 96 (src, dst) pairs of equal memory order."""
+    from ..ops import _lib
+    for i in range(0, len(pairs), 96):
+        chunk = pairs[i:i + 96]
+        d = ctypes_int64_array([v for s, t in chunk for v in (s.data_ptr(), t.data_ptr(), s.numel())])
+        _lib.call("mx_cast_multi", d, len(chunk), int(to_bf16), _lib.stream())
+
+
+class _CastGroup(torch.autograd.Function):
+    """bf16 compute copies of fp32 weights in ONE launch (csrc/cast.hip), each copy with its
+    weight's strides; the backward casts their bf16 gradients to fp32 in one launch too
+    (gradients in another memory order fall back to a plain cast)."""
+
+    @staticmethod
+    def forward(ctx, *params):
+        sizes = [p.numel() for p in params]
+        flat = torch.empty(sum(sizes), dtype=torch.bfloat16, device=params[0].device)
+        outs, off = [], 0
+        for p, n in zip(params, sizes):
+            outs.append(flat[off:off + n].as_strided(p.shape, p.stride()))
+            off += n
+        _cast_launch(list(zip(params, outs)), True)
+        ctx.meta = [(p.shape, p.stride()) for p in params]
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        out: List[Optional[torch.Tensor]] = [None] * len(grads)
+        pairs = []
+        for i, g in enumerate(grads):
+            if g is None:
+                continue
+            shape, stride = ctx.meta[i]
+            if g.stride() == stride and _cast_dense(g):
+                out[i] = torch.empty_strided(shape, stride, dtype=torch.float32, device=g.device)
+                pairs.append((g, out[i]))
+            else:
+                out[i] = torch.empty_strided(shape, stride, dtype=torch.float32, device=g.device).copy_(g)
+        if pairs:
+            _cast_launch(pairs, False)
+        return tuple(out)
+
+
+class CastGroup:
+    """Context manager: bf16 compute copies of ``params`` (fp32, dense, numel % 8 == 0) from
+    one launch per group, visible to cw() -- the one-launch form of per-module weight casts
+    under bf16 autocast.  ``groups`` > 1 cuts them into contiguous chunks (data parallel:
+    their fp32 gradients, and DDP's bucket hooks, then become ready during backward)."""
+
+    def __init__(self, params, groups: int = 1):
+        self.params = [p for p in params if p.requires_grad and _cast_dense(p) and p.dtype == torch.float32]
+        self.groups = max(1, int(groups))
+
+    def __enter__(self):
+        if self.params and torch.is_grad_enabled():
+            for chunk in ComputeWeights.split([(p, None) for p in self.params], self.groups):
+                ps = [p for p, _ in chunk]
+                for p, o in zip(ps, _CastGroup.apply(*ps)):
+                    _ACTIVE[id(p)] = o
+        return self
+
+    def __exit__(self, *exc):
+        for p in self.params:
+            _ACTIVE.pop(id(p), None)
+        return False
+
+
 # ------------------------------------------------------------------------- flat master
 def _align8(n: int) -> int:
     return (n + 7) // 8 * 8

@@ -12,6 +12,7 @@ parameters stay fp32 masters (cast per forward, AMP style).
 """
 from __future__ import annotations
 
+import contextlib
 from typing import List, Optional
 
 import torch
@@ -26,6 +27,7 @@ from ..ops.epilogue import BlockLink, ConvBiasActFn, conv_bias_act, fused_conv_o
 
 # trainable BN: batch statistics from the producing conv's epilogue (A/B switch, scripts/resnet_ab.py)
 BN_EPILOGUE_STATS = True
+BN_CASTS = __import__("os").environ.get("MXTRAIN_BN_CASTS", "1") != "0"   # (A/B)
 
 
 def _conv_nobias(x, w, stride, padding, dilation, fuse=None, bnpre=None):
@@ -37,7 +39,7 @@ def _conv_nobias(x, w, stride, padding, dilation, fuse=None, bnpre=None):
     ``bnpre`` (list): on the first path receives the epilogue's BatchNorm statistics of the
     output (ops/batchnorm.py bn_act ``pre``)."""
     if x.is_cuda and x.dtype == torch.bfloat16:
-        wb = w.to(torch.bfloat16)
+        wb = _cw.cw(w, torch.bfloat16)   # (one-launch compute copies under ResNet.forward)
         if convwg.fwd_supported(x, wb, None, None, stride, padding, dilation):
             if fuse is not None and "take_res" in fuse[2]:
                 fuse[0].taker = True
@@ -288,8 +290,20 @@ class ResNet(nn.Module):
             outs.append(x)
         return outs   # C2..C5 (strides 4..32)
 
+    def _casts(self, x):
+        """Trainable-BN model under bf16 autocast: every conv weight's bf16 copy from one
+        launch (and their fp32 gradients from one), instead of a cast kernel per weight each
+        way (models/compute_weights.py CastGroup)."""
+        if (not BN_CASTS or self.stem.norm_kind != "bn" or not x.is_cuda or not torch.is_grad_enabled()
+                or not torch.is_autocast_enabled("cuda") or torch.get_autocast_dtype("cuda") != torch.bfloat16):
+            return contextlib.nullcontext()
+        dp = torch.distributed.is_available() and torch.distributed.is_initialized()
+        return _cw.CastGroup([m.conv.weight for m in self.modules() if isinstance(m, ConvNorm)],
+                             groups=8 if dp else 1)
+
     def forward(self, x):
-        c = self.forward_features(x)
+        with self._casts(x):
+            c = self.forward_features(x)
         if self.fc is None:
             return c
         pooled = c[-1].float().mean(dim=(2, 3))

@@ -228,3 +228,28 @@ def test_maxpool3s2_matches_torch(N, C, H, W, relu):
     y.backward(dy)
     yr.backward(dy)
     _close(xa.grad, xr.grad, 1e-2, 1e-2, "dx")
+
+
+def test_cast_group_one_launch_copies_and_grads():
+    """models/compute_weights.py CastGroup: bf16 compute copies of fp32 weights (channels_last
+    and contiguous) from one csrc/cast.hip launch equal w.to(bf16) bit for bit, keep each
+    weight's strides, and their fp32 gradients (one launch back) equal g.float()."""
+    from mxtrain.models import compute_weights as cw
+    ws = [torch.randn(64, 32, 3, 3, device=DEV).contiguous(memory_format=torch.channels_last),
+          torch.randn(128, 64, 1, 1, device=DEV).contiguous(memory_format=torch.channels_last),
+          torch.randn(24, 16, device=DEV), torch.randn(64, 3, 7, 7, device=DEV).contiguous(memory_format=torch.channels_last)]
+    ws = [w.requires_grad_(True) for w in ws]
+    gs = []
+    with cw.CastGroup(ws):
+        for w in ws:
+            c = cw.cw(w, torch.bfloat16)
+            assert c.dtype == torch.bfloat16 and c.stride() == w.stride()
+            assert torch.equal(c, w.detach().to(torch.bfloat16))
+            g = torch.randn(w.shape, device=DEV).to(torch.bfloat16).contiguous(
+                memory_format=torch.channels_last if w.dim() == 4 else torch.contiguous_format)
+            gs.append(g)
+        loss = sum((cw.cw(w, torch.bfloat16).float() * g.float()).sum() for w, g in zip(ws, gs))
+    loss.backward()
+    for w, g in zip(ws, gs):
+        assert w.grad.dtype == torch.float32 and w.grad.stride() == w.stride()
+        torch.testing.assert_close(w.grad, g.float(), rtol=0, atol=0)
