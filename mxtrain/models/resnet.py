@@ -27,7 +27,6 @@ from ..ops.epilogue import BlockLink, ConvBiasActFn, conv_bias_act, fused_conv_o
 
 # trainable BN: batch statistics from the producing conv's epilogue (A/B switch, scripts/resnet_ab.py)
 BN_EPILOGUE_STATS = True
-BN_CASTS = __import__("os").environ.get("MXTRAIN_BN_CASTS", "1") != "0"   # (A/B)
 
 
 def _conv_nobias(x, w, stride, padding, dilation, fuse=None, bnpre=None):
@@ -294,7 +293,7 @@ class ResNet(nn.Module):
         """Trainable-BN model under bf16 autocast: every conv weight's bf16 copy from one
         launch (and their fp32 gradients from one), instead of a cast kernel per weight each
         way (models/compute_weights.py CastGroup)."""
-        if (not BN_CASTS or self.stem.norm_kind != "bn" or not x.is_cuda or not torch.is_grad_enabled()
+        if (self.stem.norm_kind != "bn" or not x.is_cuda or not torch.is_grad_enabled()
                 or not torch.is_autocast_enabled("cuda") or torch.get_autocast_dtype("cuda") != torch.bfloat16):
             return contextlib.nullcontext()
         dp = torch.distributed.is_available() and torch.distributed.is_initialized()
