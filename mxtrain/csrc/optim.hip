@@ -199,3 +199,82 @@ MX_EXPORT int mx_adamw_step(float* master, float* m, float* v, const void* grad,
                        (const uint16_t*)grad, (uint16_t*)param_out, wd_flags, n, hyper, normsq);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------- multi-tensor SGD
+// torch.optim.SGD's update (weight decay, momentum, Nesterov; dampening 0) over a list of
+// fp32 parameters in ONE launch, the learning rate read from a device scalar (so the step can
+// be captured in a hipGraph while an LR scheduler moves it): per element
+//   d = g + wd p;  buf = mom buf + d;  u = nesterov ? d + mom buf : buf;  p -= lr u
+// -- the Ray-Lightning ResNet-50 step (raylike/lightning.py), where torch's multi-tensor
+// kernels took 19 launches and ~420 us for ~510 MB (1.2 TB/s) per step.  Jobs by value,
+// 4-element vectors (numel % 4 == 0, 16-byte aligned).
+namespace {
+constexpr int kSgdJobs = 96;
+struct SgdJob {
+  float* p;
+  const float* g;
+  float* buf;
+  int64_t v0;   // first float4 of this job in the launch's flat vector space
+};
+struct SgdJobs {
+  SgdJob j[kSgdJobs];
+};
+
+__global__ __launch_bounds__(256) void sgd_multi_kernel(const SgdJobs js, int njobs, int64_t nvec, const float* lr_p,
+                                                        float wd, float mom, int nesterov) {
+  const float lr = *lr_p;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (js.j[mid].v0 <= v) lo = mid;
+      else hi = mid - 1;
+    }
+    const SgdJob& J = js.j[lo];
+    const int64_t e = v - J.v0;
+    float4 p = reinterpret_cast<const float4*>(J.p)[e];
+    const float4 g = reinterpret_cast<const float4*>(J.g)[e];
+    float pv[4] = {p.x, p.y, p.z, p.w};
+    const float gv[4] = {g.x, g.y, g.z, g.w};
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    float4 b;
+    if (J.buf) {
+      b = reinterpret_cast<const float4*>(J.buf)[e];
+      bv[0] = b.x; bv[1] = b.y; bv[2] = b.z; bv[3] = b.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float d = gv[k] + wd * pv[k];
+      float u = d;
+      if (J.buf) {
+        bv[k] = bv[k] * mom + d;
+        u = nesterov ? d + mom * bv[k] : bv[k];
+      }
+      pv[k] = pv[k] - u * lr;
+    }
+    reinterpret_cast<float4*>(J.p)[e] = make_float4(pv[0], pv[1], pv[2], pv[3]);
+    if (J.buf) reinterpret_cast<float4*>(J.buf)[e] = make_float4(bv[0], bv[1], bv[2], bv[3]);
+  }
+}
+}  // namespace
+
+// d (int64[4 * njobs]): {param, grad, momentum buffer (0: no momentum), numel} per job
+MX_EXPORT int mx_sgd_multi(const int64_t* d, int njobs, const float* lr, float wd, float mom, int nesterov,
+                           hipStream_t s) {
+  if (njobs <= 0 || njobs > kSgdJobs || !lr) return hipErrorInvalidValue;
+  SgdJobs js{};
+  int64_t nvec = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const int64_t n = d[4 * i + 3];
+    if (n <= 0 || n % 4 || ((d[4 * i] | d[4 * i + 1] | d[4 * i + 2]) & 15)) return hipErrorInvalidValue;
+    js.j[i].p = reinterpret_cast<float*>(d[4 * i]);
+    js.j[i].g = reinterpret_cast<const float*>(d[4 * i + 1]);
+    js.j[i].buf = reinterpret_cast<float*>(d[4 * i + 2]);
+    js.j[i].v0 = nvec;
+    nvec += n / 4;
+  }
+  int64_t g = (nvec + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(sgd_multi_kernel, dim3((unsigned)g), dim3(256), 0, s, js, njobs, nvec, lr, wd, mom, nesterov);
+  return hipGetLastError();
+}

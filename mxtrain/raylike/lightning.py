@@ -273,6 +273,9 @@ def sgd_step_device_lr(opt: torch.optim.SGD, lrs: List[torch.Tensor]) -> None:
         ps = [p for p in g["params"] if p.grad is not None]
         if not ps:
             continue
+        ps = _sgd_multi(opt, g, ps, lr)   # one HIP launch for the dense fp32 ones; the rest below
+        if not ps:
+            continue
         grads = [p.grad for p in ps]
         if g["weight_decay"]:
             grads = torch._foreach_add(grads, ps, alpha=g["weight_decay"])
@@ -290,6 +293,38 @@ def sgd_step_device_lr(opt: torch.optim.SGD, lrs: List[torch.Tensor]) -> None:
         else:
             upd = grads
         torch._foreach_add_(ps, torch._foreach_mul(upd, lr), alpha=-1.0)
+
+
+def _sgd_dense(p, gr, buf) -> bool:
+    return (p.is_cuda and p.dtype == torch.float32 and gr.dtype == torch.float32 and p.numel() % 4 == 0
+            and p.stride() == gr.stride() and (buf is None or buf.stride() == p.stride())
+            and (p.is_contiguous() or (p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last)))
+            and all(t is None or t.data_ptr() % 16 == 0 for t in (p, gr, buf)))
+
+
+def _sgd_multi(opt, g, ps, lr):
+    """The group's update for its dense fp32 parameters in one csrc/optim.hip mx_sgd_multi
+    launch per 96 (torch's multi-tensor kernels: ~19 launches per ResNet-50 step); returns the
+    parameters left for the torch path."""
+    from ..ops import _lib
+    if not ps[0].is_cuda or not _lib.use_hip(ps[0]) or g.get("dampening", 0):
+        return ps
+    mom = g["momentum"]
+    jobs, rest = [], []
+    for p in ps:
+        buf = opt.state[p].get("momentum_buffer") if mom else None
+        if mom and buf is None:
+            buf = opt.state[p]["momentum_buffer"] = torch.zeros_like(p)
+        (jobs if _sgd_dense(p, p.grad, buf) else rest).append((p, buf))
+    from ..models.compute_weights import ctypes_int64_array
+    for i in range(0, len(jobs), 96):
+        chunk = jobs[i:i + 96]
+        d = ctypes_int64_array([v for p, b in chunk
+                                for v in (p.data_ptr(), p.grad.data_ptr(), b.data_ptr() if b is not None else 0,
+                                          p.numel())])
+        _lib.call("mx_sgd_multi", d, len(chunk), lr.data_ptr(), float(g["weight_decay"]), float(mom),
+                  int(bool(g["nesterov"])), _lib.stream())
+    return [p for p, _ in rest]
 
 
 GRAPH_WARMUP = 3   # eager steps before the capture (lazy state, momentum buffers, MIOpen / GEMM choices)

@@ -55,3 +55,31 @@ def _init_state():
     from mxtrain.workloads.ray.train_resnet50 import ResNet50Module
     torch.manual_seed(0)
     return ResNet50Module(0.05, total=8).state_dict()
+
+
+def test_sgd_multi_matches_torch_sgd():
+    """raylike/lightning.py sgd_step_device_lr on the one-launch HIP update (csrc/optim.hip
+    mx_sgd_multi: weight decay, momentum, Nesterov, LR from a device scalar) against
+    torch.optim.SGD over three steps: channels_last conv weights, vectors, a matrix."""
+    import torch
+    from mxtrain.raylike.lightning import sgd_step_device_lr
+    torch.manual_seed(0)
+    shapes = [(64, 32, 3, 3), (256,), (100, 48), (128, 64, 1, 1)]
+    mk = lambda: [torch.nn.Parameter(torch.randn(s, device="cuda").contiguous(  # noqa: E731
+        memory_format=torch.channels_last if len(s) == 4 else torch.contiguous_format)) for s in shapes]
+    a, b = mk(), mk()
+    for x, y in zip(a, b):
+        y.data.copy_(x.data)
+    kw = dict(lr=0.05, momentum=0.9, nesterov=True, weight_decay=1e-3)
+    oa, ob = torch.optim.SGD(a, **kw), torch.optim.SGD(b, **kw)
+    lrs = [torch.tensor(0.05, device="cuda")]
+    for _ in range(3):
+        gs = [torch.randn(s, device="cuda") for s in shapes]
+        for x, y, g in zip(a, b, gs):
+            x.grad = g.clone().contiguous(memory_format=torch.channels_last if g.dim() == 4 else torch.contiguous_format)
+            y.grad = x.grad.clone()
+        oa.step()
+        sgd_step_device_lr(ob, lrs)
+    for x, y in zip(a, b):
+        torch.testing.assert_close(y, x, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(ob.state[y]["momentum_buffer"], oa.state[x]["momentum_buffer"], rtol=1e-6, atol=1e-6)
