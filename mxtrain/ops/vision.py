@@ -199,6 +199,27 @@ def roi_align(feats: List[torch.Tensor], rois: torch.Tensor, output_size: Tuple[
 
 
 # ============================================================================ box utils
+def normalize_u8_nhwc(images: torch.Tensor, mean: Sequence[float], std: Sequence[float],
+                      dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """(images - mean) / std of a uint8 NCHW RGB batch as a channels_last ``dtype`` tensor: one
+    pass on the GPU (csrc/vision.hip normalize_u8_nhwc_kernel: uint8 in, bf16 NHWC out)
+    instead of float / subtract / divide / layout-change / autocast-cast passes over fp32
+    copies; the torch expression otherwise."""
+    if (images.is_cuda and images.dtype == torch.uint8 and dtype == torch.bfloat16 and images.dim() == 4
+            and images.shape[1] == 3 and images.is_contiguous() and (images.shape[2] * images.shape[3]) % 4 == 0
+            and _lib.use_hip(images)):
+        B, _, H, W = images.shape
+        x = torch.empty(B, H, W, 3, dtype=dtype, device=images.device).permute(0, 3, 1, 2)
+        _lib.call("mx_normalize_u8_nhwc", images.data_ptr(), x.data_ptr(), B, H, W,
+                  ctypes.cast((ctypes.c_float * 3)(*[float(v) for v in mean]), ctypes.c_void_p),
+                  ctypes.cast((ctypes.c_float * 3)(*[1.0 / float(v) for v in std]), ctypes.c_void_p),
+                  _lib.stream())
+        return x
+    m = torch.tensor(list(mean), dtype=torch.float32, device=images.device).view(1, -1, 1, 1)
+    sd = torch.tensor(list(std), dtype=torch.float32, device=images.device).view(1, -1, 1, 1)
+    return ((images.float() - m) / sd).to(dtype).contiguous(memory_format=torch.channels_last)
+
+
 def box_iou(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     area_a = (a[:, 2] - a[:, 0]).clamp(min=0) * (a[:, 3] - a[:, 1]).clamp(min=0)
     area_b = (b[:, 2] - b[:, 0]).clamp(min=0) * (b[:, 3] - b[:, 1]).clamp(min=0)

@@ -56,7 +56,15 @@ class ResNet50Module(L.LightningModule):
         self.register_buffer("mean", torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1) * 255, persistent=False)
         self.register_buffer("std", torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1) * 255, persistent=False)
 
+    MEAN = (0.485 * 255, 0.456 * 255, 0.406 * 255)
+    STD = (0.229 * 255, 0.224 * 255, 0.225 * 255)
+
     def forward(self, x):
+        if (x.is_cuda and x.dtype == torch.uint8 and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+            # uint8 NCHW -> normalised bf16 NHWC in one kernel (the autocast conv input)
+            from mxtrain.ops.vision import normalize_u8_nhwc
+            return self.net(normalize_u8_nhwc(x, self.MEAN, self.STD))
         x = (x.float() - self.mean) / self.std
         return self.net(x.contiguous(memory_format=torch.channels_last))
 

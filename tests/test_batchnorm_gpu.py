@@ -253,3 +253,15 @@ def test_cast_group_one_launch_copies_and_grads():
     for w, g in zip(ws, gs):
         assert w.grad.dtype == torch.float32 and w.grad.stride() == w.stride()
         torch.testing.assert_close(w.grad, g.float(), rtol=0, atol=0)
+
+
+def test_normalize_u8_nhwc_helper_matches_torch():
+    """ops/vision.py normalize_u8_nhwc (the ResNet-50 workload's input pass): uint8 NCHW ->
+    normalised bf16 channels_last in one kernel, against the fp32 torch expression."""
+    from mxtrain.ops.vision import normalize_u8_nhwc
+    img = torch.randint(0, 256, (4, 3, 32, 48), dtype=torch.uint8, device=DEV)
+    mean, std = (123.7, 116.3, 103.5), (58.4, 57.1, 57.4)
+    x = normalize_u8_nhwc(img, mean, std)
+    assert x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)
+    ref = (img.float() - torch.tensor(mean, device=DEV).view(1, 3, 1, 1)) / torch.tensor(std, device=DEV).view(1, 3, 1, 1)
+    _close(x, ref, 1e-2, 1e-2, "normalised")
