@@ -252,19 +252,50 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const uint16_t* __re
 }
 
 // backward statistics: per-block column sums of dz and dz * xhat, partial [nblk][2][C]
-template <bool kRelu>
+// kRecon (ReLU, no residual): xhat recovered from the output where the ReLU passed,
+// xhat = (y - beta) / gamma -- exactly where dz can be nonzero -- so x is not read (a third
+// of this pass's bytes); a thread whose channels include |gamma| < 1e-6 reads x instead.
+template <bool kRelu, bool kRecon = false>
 __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const uint16_t* __restrict__ dy,
                                                                 const uint16_t* __restrict__ y,
                                                                 const uint16_t* __restrict__ x,
                                                                 const float* __restrict__ mean,
                                                                 const float* __restrict__ rstd, int M, int C,
-                                                                int rows_per_block, float* __restrict__ partial) {
+                                                                int rows_per_block, float* __restrict__ partial,
+                                                                const float* __restrict__ gamma = nullptr,
+                                                                const float* __restrict__ beta = nullptr) {
   const RowGeo g(C);
   const int vc = blockIdx.x * g.cv + g.tv;
   const int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
   __shared__ float sm[2][kThreads][8];
   float sd[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (vc < g.c8) {
+  float ig[8], bt[8];
+  bool recon = kRecon && vc < g.c8;
+  if (recon) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gm = gamma[8 * vc + j];
+      recon = recon && fabsf(gm) >= 1e-6f;
+      ig[j] = 1.f / gm;
+      bt[j] = beta[8 * vc + j];
+    }
+  }
+  if (recon) {
+    {
+      for (int r = r0 + g.tr; r < r1; r += g.rpi) {
+        float d[8], o[8];
+        const size_t off = (size_t)r * C;
+        unpack8(reinterpret_cast<const uint4*>(dy + off)[vc], d);
+        unpack8(reinterpret_cast<const uint4*>(y + off)[vc], o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float dz = o[j] > 0.f ? d[j] : 0.f;
+          sd[j] += dz;
+          sx[j] = __builtin_fmaf(dz, o[j] > 0.f ? (o[j] - bt[j]) * ig[j] : 0.f, sx[j]);
+        }
+      }
+    }
+  } else if (vc < g.c8) {
     float mu[8], rs[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -469,17 +500,21 @@ MX_EXPORT int mx_bn_apply(const void* x, const void* res, void* y, const float* 
 // added to; scratch: mx_bn_scratch floats.
 MX_EXPORT int mx_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd,
                         const float* gamma, void* dx, void* dres, float* dgamma, float* dbeta, int accumulate, int M,
-                        int C, int relu, float* scratch, hipStream_t s) {
+                        int C, int relu, float* scratch, const float* beta, int recon, hipStream_t s) {
   if (C % 8 || C <= 0 || M <= 0) return hipErrorInvalidValue;
+  if (recon && (!relu || dres || !beta)) return hipErrorInvalidValue;
   const int rpb = rows_per_block(M), nblk = (M + rpb - 1) / rpb;
   const int c8 = C / 8, cv = c8 < kThreads ? c8 : kThreads;
   float* partial = scratch;
   float* coef = scratch + (size_t)nblk * 2 * C;
   const dim3 sg((c8 + cv - 1) / cv, nblk);
-  if (relu) hipLaunchKernelGGL(bn_bwd_stats_kernel<true>, sg, dim3(kThreads), 0, s, (const uint16_t*)dy,
-                               (const uint16_t*)y, (const uint16_t*)x, mean, rstd, M, C, rpb, partial);
+  if (recon) hipLaunchKernelGGL((bn_bwd_stats_kernel<true, true>), sg, dim3(kThreads), 0, s, (const uint16_t*)dy,
+                                (const uint16_t*)y, (const uint16_t*)x, mean, rstd, M, C, rpb, partial, gamma, beta);
+  else if (relu) hipLaunchKernelGGL(bn_bwd_stats_kernel<true>, sg, dim3(kThreads), 0, s, (const uint16_t*)dy,
+                                    (const uint16_t*)y, (const uint16_t*)x, mean, rstd, M, C, rpb, partial,
+                                    nullptr, nullptr);
   else hipLaunchKernelGGL(bn_bwd_stats_kernel<false>, sg, dim3(kThreads), 0, s, (const uint16_t*)dy, nullptr,
-                          (const uint16_t*)x, mean, rstd, M, C, rpb, partial);
+                          (const uint16_t*)x, mean, rstd, M, C, rpb, partial, nullptr, nullptr);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(kThreads), 0, s, partial, nblk, M, C, gamma,
                      rstd, dgamma, dbeta, accumulate, coef);
   const int64_t nvec = (int64_t)M * c8;

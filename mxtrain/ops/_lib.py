@@ -99,7 +99,7 @@ SIGNATURES = {
     # batchnorm.hip
     "mx_bn_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, F, I, P, P, P, P],
     "mx_bn_apply": [P, P, P, P, P, I, I, I, P],
-    "mx_bn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, P, P],
+    "mx_bn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, P, P, I, P],
     "mx_conv_wgrad_tile": [I],
     "mx_conv_wgrad": [P, F, I, P],
     "mx_conv_wgrad_splits": [I64, I],

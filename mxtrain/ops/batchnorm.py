@@ -29,6 +29,9 @@ def _nhwc_ok(t: Optional[torch.Tensor]) -> bool:
 
 
 ENABLED = True   # module switch (A/B runs: scripts/resnet_ab.py)
+# backward statistics of BN + ReLU (no residual) from the output: xhat = (y - beta) / gamma
+# where the ReLU passed (csrc/batchnorm.hip bn_bwd_stats_kernel kRecon), x not re-read
+RECON = True   # (the test compares both passes)
 
 
 def supported(x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> bool:
@@ -57,13 +60,13 @@ class BNActFn(torch.autograd.Function):
                   _lib.ptr(pre), _lib.stream())
         ctx.relu, ctx.has_res = relu, residual is not None
         ctx.link = link
-        ctx.save_for_backward(x, y, mean, rstd, g32)
+        ctx.save_for_backward(x, y, mean, rstd, g32, b32)
         ctx.pdtypes = (gamma.dtype, beta.dtype)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, mean, rstd, g32 = ctx.saved_tensors
+        x, y, mean, rstd, g32, b32 = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
         N, C, H, W = x.shape
         M = N * H * W
@@ -73,7 +76,8 @@ class BNActFn(torch.autograd.Function):
         db = torch.empty_like(dg)
         _lib.call("mx_bn_bwd", dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                   g32.data_ptr(), dx.data_ptr(), _lib.ptr(dres), dg.data_ptr(), db.data_ptr(), 0, M, C,
-                  int(ctx.relu), _scratch(M, C, x.device).data_ptr(), _lib.stream())
+                  int(ctx.relu), _scratch(M, C, x.device).data_ptr(), b32.data_ptr(),
+                  int(RECON and ctx.relu and not ctx.has_res), _lib.stream())
         link = ctx.link
         if dres is not None and link is not None and link.taker and ctx.needs_input_grad[3]:
             # identity residual (ops/epilogue.py BlockLink): conv1's dgrad store adds it to the

@@ -265,3 +265,31 @@ def test_normalize_u8_nhwc_helper_matches_torch():
     assert x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)
     ref = (img.float() - torch.tensor(mean, device=DEV).view(1, 3, 1, 1)) / torch.tensor(std, device=DEV).view(1, 3, 1, 1)
     _close(x, ref, 1e-2, 1e-2, "normalised")
+
+
+def test_bn_relu_backward_stats_from_output_match_reading_x(monkeypatch):
+    """BN + ReLU without a residual takes its backward statistics from the output
+    (xhat = (y - beta) / gamma where the ReLU passed; x not re-read): the same dx / dgamma /
+    dbeta as the pass that reads x, including channels whose gamma is zero (those threads
+    read x)."""
+    from mxtrain.ops import batchnorm as BN
+    g = torch.Generator(device=DEV).manual_seed(7)
+    x = (torch.randn(16, 64, 20, 20, device=DEV, generator=g) * 2 + 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    dy = torch.randn(x.shape, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for recon in (False, True):
+        monkeypatch.setattr(BN, "RECON", recon)
+        bn = torch.nn.BatchNorm2d(64).to(DEV)
+        with torch.no_grad():
+            bn.weight.copy_(torch.linspace(0.3, 1.7, 64))
+            bn.weight[:8] = 0.0
+            bn.bias.copy_(torch.linspace(-0.4, 0.4, 64))
+        xa = x.clone().requires_grad_(True)
+        y = BN.bn_act(xa, bn, None, True)
+        y.backward(dy)
+        outs.append((y, xa.grad.float(), bn.weight.grad.clone(), bn.bias.grad.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    _close(outs[1][1], outs[0][1], 2e-2, 2e-2, "dx")
+    _close(outs[1][2], outs[0][2], 0.5, 1e-2, "dgamma")
+    assert torch.equal(outs[1][3], outs[0][3])   # dbeta does not use xhat
