@@ -52,7 +52,11 @@ def test_bn_act_matches_fp32(N, C, H, W, res, relu):
     # of zero (batch statistics summed in another order) agree
     yr_pre.backward(torch.where(y.float() > 0, dy.float(), 0.0) if relu else dy.float())
     _close(xa.grad, xr.grad, 3e-2, 3e-2, "dx")
-    _close(bn.weight.grad, ref_bn.weight.grad, 0.05 + 1e-3 * (N * H * W) ** 0.5, 1e-2, "dgamma")
+    # BN + ReLU without a residual recovers xhat from the bf16 output (ops/batchnorm.py RECON):
+    # dgamma = sum dz xhat then carries the output's rounding, std ~ 2^-9 sqrt(sum (dz y)^2) / gamma
+    # ~ 0.04 at these sizes, where the reference reads the same bf16 x exactly
+    k = 5e-3 if (relu and not res) else 1e-3
+    _close(bn.weight.grad, ref_bn.weight.grad, 0.05 + k * (N * H * W) ** 0.5, 1e-2, "dgamma")
     _close(bn.bias.grad, ref_bn.bias.grad, 0.05 + 1e-3 * (N * H * W) ** 0.5, 1e-2, "dbeta")
     if res:
         _close(ra.grad, rr.grad, 1e-2, 1e-2, "dres")
