@@ -22,7 +22,7 @@ import torch.nn.functional as F
 from . import compute_weights as _cw
 from ..ops import convwg
 from ..ops.batchnorm import bn_act
-from ..ops.epilogue import BlockLink, ConvBiasActFn, conv_bias_act, fused_conv_ok, maxpool3s2
+from ..ops.epilogue import BlockLink, ConvBiasActFn, conv_bias_act, fused_conv_ok, global_avg_pool, maxpool3s2
 
 
 # trainable BN: batch statistics from the producing conv's epilogue (A/B switch, scripts/resnet_ab.py)
@@ -305,7 +305,7 @@ class ResNet(nn.Module):
             c = self.forward_features(x)
         if self.fc is None:
             return c
-        pooled = c[-1].float().mean(dim=(2, 3))
+        pooled = global_avg_pool(c[-1])   # (fp32 [N, C]; NHWC bf16: csrc/pool.hip, +0.5%)
         return self.fc(pooled)
 
 

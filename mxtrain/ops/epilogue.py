@@ -139,6 +139,31 @@ class JoinLink(BlockLink):
         self.join = {}
 
 
+# 1 x 1 stride-1 input gradients the implicit-GEMM dgrad does not take (Cin = 64: the ResNet
+# res2 shapes) as ONE plain GEMM dX[pixels][Cin] = dY[pixels][Cout] . W[Cout][Cin] on the NHWC
+# views, a second gradient of X accumulated in place (beta = 1) instead of an add launch
+GEMM_DGRAD_1X1 = True
+
+
+def _gemm_dgrad_ok(dy, w, add, st, pd, dl) -> bool:
+    return (GEMM_DGRAD_1X1 and __import__("os").environ.get("MXTRAIN_AB", "1") != "0"  # AB-TEMP
+            and tuple(w.shape[2:]) == (1, 1) and list(st) == [1, 1]
+            and list(pd) == [0, 0] and dy.dtype == w.dtype == torch.bfloat16 and _nhwc(dy)
+            and (add is None or (add.dtype == dy.dtype and _nhwc(add) and add.shape[1] == w.shape[1])))
+
+
+def _gemm_dgrad(dy, w, add):
+    N, Cout, H, W = dy.shape
+    Cin = w.shape[1]
+    a = dy.permute(0, 2, 3, 1).reshape(N * H * W, Cout)
+    b = w.reshape(Cout, Cin)
+    if add is not None:
+        dx = add.permute(0, 2, 3, 1).reshape(N * H * W, Cin)
+        dx.addmm_(a, b)
+        return add
+    return torch.mm(a, b).view(N, H, W, Cin).permute(0, 3, 1, 2)
+
+
 class ConvBiasActFn(torch.autograd.Function):
     """act(conv2d(x, w) + b (+ res)) with every direction on csrc/convwg.hip where it tiles:
     forward = one implicit-GEMM launch with the epilogue fused; backward = the ReLU mask +
@@ -207,6 +232,8 @@ class ConvBiasActFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if convwg.dgrad_supported(w, tuple(x.shape), st, pd, dl) and (add is None or add.data_ptr() % 16 == 0):
                 dx = convwg.conv_dgrad(dy, w, tuple(x.shape), st, pd, dl, add=add, mask=mask)
+            elif mask is None and _gemm_dgrad_ok(dy, w, add, st, pd, dl):
+                dx = _gemm_dgrad(dy, w, add)
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, st, pd, dl, False, [0, 0], 1,
                                                          [True, False, False])[0]
@@ -297,6 +324,35 @@ def maxpool3s2(x: torch.Tensor) -> torch.Tensor:
             and x.data_ptr() % 16 == 0):
         return MaxPool3s2Fn.apply(x)
     return F.max_pool2d(x, 3, 2, 1)
+
+
+class GlobalAvgPoolFn(torch.autograd.Function):
+    """x.float().mean(dim=(2, 3)) of an NHWC bf16 tensor -> fp32 [N, C] in one launch each way
+    (csrc/pool.hip mx_gap_fwd / mx_gap_bwd)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N, C, H, W = x.shape
+        y = torch.empty((N, C), dtype=torch.float32, device=x.device)
+        _lib.call("mx_gap_fwd", x.data_ptr(), y.data_ptr(), N, H * W, C, _lib.stream())
+        ctx.shape = (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        N, C, H, W = ctx.shape
+        g = g.float().contiguous()
+        dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=g.device)
+        _lib.call("mx_gap_bwd", g.data_ptr(), dx.data_ptr(), N, H * W, C, _lib.stream())
+        return dx.permute(0, 3, 1, 2)
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """x.float().mean(dim=(2, 3)) (fp32 [N, C])."""
+    if (_lib.use_hip(x) and x.dtype == torch.bfloat16 and _nhwc(x) and x.shape[1] % 8 == 0
+            and x.data_ptr() % 16 == 0):
+        return GlobalAvgPoolFn.apply(x)
+    return x.float().mean(dim=(2, 3))
 
 
 def down2_sum(g: torch.Tensor, add: Optional[torch.Tensor] = None) -> torch.Tensor:

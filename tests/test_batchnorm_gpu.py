@@ -234,6 +234,28 @@ def test_maxpool3s2_matches_torch(N, C, H, W, relu):
     _close(xa.grad, xr.grad, 1e-2, 1e-2, "dx")
 
 
+@pytest.mark.parametrize("N,C,H,W", [(256, 2048, 7, 7), (3, 24, 5, 3), (2, 8, 1, 1)])
+def test_global_avg_pool_matches_fp32(N, C, H, W):
+    """The classifier head's pool (csrc/pool.hip mx_gap_fwd / mx_gap_bwd, fp32 accumulation)
+    against x.float().mean((2, 3)) and its gradient; the HIP path must be the one taken."""
+    from mxtrain.ops.epilogue import GlobalAvgPoolFn, global_avg_pool
+    g = torch.Generator(device=DEV).manual_seed(C + H)
+    x = torch.randn(N, C, H, W, device=DEV, generator=g).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    xa = x.clone().requires_grad_(True)
+    xr = x.float().requires_grad_(True)
+    y = global_avg_pool(xa)
+    assert y.grad_fn is not None and type(y.grad_fn).__name__.startswith(GlobalAvgPoolFn.__name__)
+    yr = xr.mean(dim=(2, 3))
+    assert y.dtype == torch.float32 and y.shape == (N, C)
+    _close(y, yr, 1e-5, 1e-5, "y")
+    dy = torch.randn(N, C, device=DEV, generator=g)
+    y.backward(dy)
+    yr.backward(dy)
+    assert xa.grad.dtype == torch.bfloat16 and xa.grad.is_contiguous(memory_format=torch.channels_last)
+    _close(xa.grad.float(), xr.grad, 1e-5, 1e-2, "dx")
+
+
 def test_cast_group_one_launch_copies_and_grads():
     """models/compute_weights.py CastGroup: bf16 compute copies of fp32 weights (channels_last
     and contiguous) from one csrc/cast.hip launch equal w.to(bf16) bit for bit, keep each
@@ -297,3 +319,25 @@ def test_bn_relu_backward_stats_from_output_match_reading_x(monkeypatch):
     _close(outs[1][1], outs[0][1], 2e-2, 2e-2, "dx")
     _close(outs[1][2], outs[0][2], 0.5, 1e-2, "dgamma")
     assert torch.equal(outs[1][3], outs[0][3])   # dbeta does not use xhat
+
+
+@pytest.mark.parametrize("Cout,add", [(64, False), (256, True)])
+def test_gemm_dgrad_1x1_matches_miopen(Cout, add):
+    """ops/epilogue.py _gemm_dgrad: the 1 x 1 stride-1 input gradient of the Cin = 64 res2
+    convolutions as one GEMM on the NHWC views (a second gradient accumulated in place)
+    against MIOpen's backward-data of the same bf16 operands."""
+    from mxtrain.ops.epilogue import _gemm_dgrad, _gemm_dgrad_ok
+    g = torch.Generator(device=DEV).manual_seed(Cout)
+    cl = torch.channels_last
+    dy = torch.randn(8, Cout, 14, 14, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    x = torch.randn(8, 64, 14, 14, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (torch.randn(Cout, 64, 1, 1, device=DEV, generator=g) / 8).to(torch.bfloat16).contiguous(memory_format=cl)
+    a = torch.randn(x.shape, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=cl) if add else None
+    assert _gemm_dgrad_ok(dy, w, a, [1, 1], [0, 0], [1, 1])
+    ref = torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                              [True, False, False])[0].float()
+    if add:
+        ref = ref + a.float()
+    dx = _gemm_dgrad(dy, w, a)
+    assert dx.shape == x.shape and dx.is_contiguous(memory_format=cl)
+    _close(dx, ref, 2e-2, 2e-2, "dx")
