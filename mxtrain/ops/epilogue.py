@@ -139,31 +139,6 @@ class JoinLink(BlockLink):
         self.join = {}
 
 
-# 1 x 1 stride-1 input gradients the implicit-GEMM dgrad does not take (Cin = 64: the ResNet
-# res2 shapes) as ONE plain GEMM dX[pixels][Cin] = dY[pixels][Cout] . W[Cout][Cin] on the NHWC
-# views, a second gradient of X accumulated in place (beta = 1) instead of an add launch
-GEMM_DGRAD_1X1 = True
-
-
-def _gemm_dgrad_ok(dy, w, add, st, pd, dl) -> bool:
-    return (GEMM_DGRAD_1X1 and __import__("os").environ.get("MXTRAIN_AB", "1") != "0"  # AB-TEMP
-            and tuple(w.shape[2:]) == (1, 1) and list(st) == [1, 1]
-            and list(pd) == [0, 0] and dy.dtype == w.dtype == torch.bfloat16 and _nhwc(dy)
-            and (add is None or (add.dtype == dy.dtype and _nhwc(add) and add.shape[1] == w.shape[1])))
-
-
-def _gemm_dgrad(dy, w, add):
-    N, Cout, H, W = dy.shape
-    Cin = w.shape[1]
-    a = dy.permute(0, 2, 3, 1).reshape(N * H * W, Cout)
-    b = w.reshape(Cout, Cin)
-    if add is not None:
-        dx = add.permute(0, 2, 3, 1).reshape(N * H * W, Cin)
-        dx.addmm_(a, b)
-        return add
-    return torch.mm(a, b).view(N, H, W, Cin).permute(0, 3, 1, 2)
-
-
 class ConvBiasActFn(torch.autograd.Function):
     """act(conv2d(x, w) + b (+ res)) with every direction on csrc/convwg.hip where it tiles:
     forward = one implicit-GEMM launch with the epilogue fused; backward = the ReLU mask +
@@ -227,13 +202,13 @@ class ConvBiasActFn(torch.autograd.Function):
                 join_first = True
         mask = x if ("mask_in" in roles or "mask_prev" in roles) else None
         dx = dw = None
-        # (Cin = 64 tiles half padded: even with MIOpen at the ResNet res2 shapes, so MIOpen keeps them)
+        # (Cin = 64 tiles half padded: even with MIOpen at the ResNet res2 shapes, so MIOpen keeps them;
+        # a plain hipBLASLt GEMM on the NHWC views loses to MIOpen there too, dgrad 92 vs 59 us,
+        # wgrad 1017 vs 47 us: profiles/r6/resnet_gemm_dgrad_1x1_rejected.txt)
         wg_hip = ctx.needs_input_grad[1] and convwg.cout_ok(w.shape[0]) and w.shape[1] % 128 == 0
         if ctx.needs_input_grad[0]:
             if convwg.dgrad_supported(w, tuple(x.shape), st, pd, dl) and (add is None or add.data_ptr() % 16 == 0):
                 dx = convwg.conv_dgrad(dy, w, tuple(x.shape), st, pd, dl, add=add, mask=mask)
-            elif mask is None and _gemm_dgrad_ok(dy, w, add, st, pd, dl):
-                dx = _gemm_dgrad(dy, w, add)
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, st, pd, dl, False, [0, 0], 1,
                                                          [True, False, False])[0]

@@ -320,24 +320,3 @@ def test_bn_relu_backward_stats_from_output_match_reading_x(monkeypatch):
     _close(outs[1][2], outs[0][2], 0.5, 1e-2, "dgamma")
     assert torch.equal(outs[1][3], outs[0][3])   # dbeta does not use xhat
 
-
-@pytest.mark.parametrize("Cout,add", [(64, False), (256, True)])
-def test_gemm_dgrad_1x1_matches_miopen(Cout, add):
-    """ops/epilogue.py _gemm_dgrad: the 1 x 1 stride-1 input gradient of the Cin = 64 res2
-    convolutions as one GEMM on the NHWC views (a second gradient accumulated in place)
-    against MIOpen's backward-data of the same bf16 operands."""
-    from mxtrain.ops.epilogue import _gemm_dgrad, _gemm_dgrad_ok
-    g = torch.Generator(device=DEV).manual_seed(Cout)
-    cl = torch.channels_last
-    dy = torch.randn(8, Cout, 14, 14, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
-    x = torch.randn(8, 64, 14, 14, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
-    w = (torch.randn(Cout, 64, 1, 1, device=DEV, generator=g) / 8).to(torch.bfloat16).contiguous(memory_format=cl)
-    a = torch.randn(x.shape, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=cl) if add else None
-    assert _gemm_dgrad_ok(dy, w, a, [1, 1], [0, 0], [1, 1])
-    ref = torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-                                              [True, False, False])[0].float()
-    if add:
-        ref = ref + a.float()
-    dx = _gemm_dgrad(dy, w, a)
-    assert dx.shape == x.shape and dx.is_contiguous(memory_format=cl)
-    _close(dx, ref, 2e-2, 2e-2, "dx")
