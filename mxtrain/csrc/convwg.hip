@@ -669,6 +669,7 @@ struct ConvDg {
   uint32_t ybytes;       // size of dY (the gather's buffer resource; < 2 GiB)
   int bkt;               // K-step depth (output channels per step): 64 or 32 (host-side choice)
   uint32_t* ticket;      // as ConvFw::ticket
+  int add_rows;          // add indexed by the launch's pixel (add holds only this parity class)
 };
 
 // dX row of the launch's pixel p (identity unless a parity-class launch)
@@ -888,11 +889,12 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const ConvDg cp) {
   for (int a = 0; a < FM; ++a) {
     const int p = m0 + 16 * (FM * wm + a) + i;
     const size_t pr = (size_t)dx_row(cp, p < cp.T ? p : cp.T - 1) * cp.ldx;
+    const size_t ar = cp.add_rows ? (size_t)(p < cp.T ? p : cp.T - 1) * cp.ldx : pr;
 #pragma unroll
     for (int up = 0; up < FN / 2; ++up) {
       uint32_t c[2][2], ad[2][2], mk[2][2];
       if (cp.add) {
-        const uint4 v = *reinterpret_cast<const uint4*>(cp.add + pr + colw + 32 * up + 8 * G);
+        const uint4 v = *reinterpret_cast<const uint4*>(cp.add + ar + colw + 32 * up + 8 * G);
         ad[0][0] = v.x; ad[0][1] = v.y; ad[1][0] = v.z; ad[1][1] = v.w;
         undeal(ad[0][0], ad[0][1], ad[1][0], ad[1][1]);
       }
@@ -1126,7 +1128,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_reduce_kernel(const ConvDg cp)
     }
     if (cp.add) {
       float a[8];
-      unpack8(*reinterpret_cast<const uint4*>(cp.add + off), a);
+      unpack8(*reinterpret_cast<const uint4*>(cp.add + (cp.add_rows ? (size_t)p * cp.ldx + c : off)), a);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] += a[j];
     }
@@ -1145,7 +1147,8 @@ __global__ __launch_bounds__(256) void conv_dgrad_reduce_kernel(const ConvDg cp)
 }
 
 // Stride-decomposed dgrad, the pixels no tap reaches ((ih mod s, iw mod s) outside the
-// filter, e.g. 3 of 4 pixels of a 1x1 stride-2 conv): the epilogue applied to a zero sum.
+// filter, e.g. 3 of 4 pixels of a 1x1 stride-2 conv): the epilogue applied to a zero sum
+// (an add holding only the filter's parity class contributes nothing here).
 __global__ __launch_bounds__(256) void conv_dgrad_fill_kernel(const ConvDg cp, int KH) {
   const int c8 = cp.Cin / 8;
   const int64_t nvec = (int64_t)cp.T * c8;
@@ -1159,7 +1162,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_fill_kernel(const ConvDg cp, i
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = bf2f(cp.bias[c + j]);
     }
-    if (cp.add) {
+    if (cp.add && !cp.add_rows) {
       float a[8];
       unpack8(*reinterpret_cast<const uint4*>(cp.add + off), a);
 #pragma unroll
@@ -1271,6 +1274,26 @@ MX_EXPORT int mx_conv_dgrad(const int64_t* d, void* stream) {
   }
   const int s = cp.stride;
   if (s < 2 || cp.pad || cp.dil != 1 || KH > s || cp.KW > s) return (int)hipErrorInvalidValue;
+  // flags bit 2 (class_out): a 1 x 1 filter's only parity class (0, 0) written compact as
+  // [N][ceil(IH / s)][ceil(IW / s)][ldx] -- no zero fill of the other s^2 - 1 classes (the
+  // ResNet projection shortcut's parked dX, ops/epilogue.py); bit 3 (add_class): ``add`` is
+  // such a compact class tensor, added to the class pixels only
+  const bool class_out = (d[23] >> 2) & 1, add_class = (d[23] >> 3) & 1;
+  if ((class_out || add_class) && (KH != 1 || cp.KW != 1)) return (int)hipErrorInvalidValue;
+  if (class_out && (cp.add || cp.mask || cp.bias || cp.relu)) return (int)hipErrorInvalidValue;
+  if (add_class && !cp.add) return (int)hipErrorInvalidValue;
+  cp.add_rows = add_class ? 1 : 0;
+  if (class_out) {
+    ConvDg c = cp;
+    c.IH = (cp.IH + s - 1) / s;
+    c.IW = (cp.IW + s - 1) / s;
+    c.T = (int)(N * c.IH * c.IW);
+    c.invIW = 1.f / (float)c.IW;
+    c.invIH = 1.f / (float)c.IH;
+    c.stride = 1; c.taps = 1; c.nk = cp.cob;   // (xs = 0: dX rows are the launch's pixels)
+    launch_dgrad(c, splits, st);
+    return (int)hipGetLastError();
+  }
   for (int a = 0; a < KH; ++a)
     for (int b = 0; b < cp.KW; ++b) {
       ConvDg c = cp;

@@ -253,12 +253,17 @@ def decomposed(KH: int, KW: int, stride, padding, dilation) -> bool:
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride, padding, dilation, add=None,
-               mask=None, bias=None, relu: bool = False) -> torch.Tensor:
+               mask=None, bias=None, relu: bool = False, class_out: bool = False,
+               add_class: bool = False) -> torch.Tensor:
     """dX [N, Cin, IH, IW] (channels_last bf16) of conv2d(x, w) for the output gradient
     ``dy``; ``w`` bf16 [Cout, Cin, KH, KW] (made channels_last if it is not).  In the same
     store (optional): ``+ bias`` ([Cin]), ``+ add`` (another gradient of X), ``relu`` and
     ``* (mask > 0)`` (X's ReLU; mask = X itself when X is a ReLU output); add / mask
-    channels_last bf16 of X's shape.  With bias + relu this is conv_transpose2d's forward."""
+    channels_last bf16 of X's shape.  With bias + relu this is conv_transpose2d's forward.
+    A 1 x 1 stride-s filter (stride-decomposed, class_ok) reaches only the pixels
+    (s i, s j): ``class_out`` returns just those, dX[:, :, ::s, ::s] as a compact
+    [N, Cin, ceil(IH / s), ceil(IW / s)] tensor (no add / mask / bias / relu), and ``add_class``
+    takes such a compact tensor as ``add`` (added to those pixels only)."""
     Cout, Cin, KH, KW = w.shape
     N, _, IH, IW = x_shape
     _, _, OH, OW = dy.shape
@@ -266,24 +271,40 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride, padding, dila
         dy = dy.contiguous(memory_format=torch.channels_last)
     if not _cl(w):
         w = w.contiguous(memory_format=torch.channels_last)
-    dx = torch.empty((N, IH, IW, Cin), dtype=torch.bfloat16, device=dy.device).permute(0, 3, 1, 2)
     dec = decomposed(KH, KW, stride, padding, dilation)
     st = _sym(stride)
+    if class_out or add_class:
+        assert dec and KH == KW == 1, "class_out / add_class: a stride-decomposed 1 x 1 filter"
+    cshape = (N, Cin, -(-IH // st), -(-IW // st))
+    if class_out:
+        assert add is None and mask is None and bias is None and not relu
+        dx = torch.empty((N, cshape[2], cshape[3], Cin), dtype=torch.bfloat16, device=dy.device).permute(0, 3, 1, 2)
+    else:
+        dx = torch.empty((N, IH, IW, Cin), dtype=torch.bfloat16, device=dy.device).permute(0, 3, 1, 2)
     T = N * (-(-IH // st)) * (-(-IW // st)) if dec else N * IH * IW   # largest launch's pixels
     splits = dgrad_splits((T + 127) // 128 * -(-Cin // 128), (1 if dec else KH * KW) * -(-Cout // 64))
     slab, zero = _workspace(dy.device, splits * T * Cin if splits > 1 else 1)
     assert bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == Cin
                             and bias.data_ptr() % 8 == 0)
-    for t in (add, mask):
-        assert t is None or (_cl(t) and tuple(t.shape) == (N, Cin, IH, IW) and t.dtype == torch.bfloat16
+    for t, shp in ((add, cshape if add_class else (N, Cin, IH, IW)), (mask, (N, Cin, IH, IW))):
+        assert t is None or (_cl(t) and tuple(t.shape) == shp and t.dtype == torch.bfloat16
                              and t.data_ptr() % 16 == 0), "dgrad add / mask: X's channels_last shape"
+    assert not add_class or add is not None
     d = _DESC_T()
     d[:24] = [dy.data_ptr(), w.data_ptr(), zero.data_ptr(), dx.data_ptr(), _lib.ptr(add) or 0, _lib.ptr(mask) or 0,
               Cout, Cin, N, OH, OW, IH, IW, KH, KW, st, _sym(padding), _sym(dilation), Cout, Cin,
-              splits, slab.data_ptr() if splits > 1 else 0, _lib.ptr(bias) or 0, int(relu) | (int(dec) << 1)]
+              splits, slab.data_ptr() if splits > 1 else 0, _lib.ptr(bias) or 0,
+              int(relu) | (int(dec) << 1) | (int(class_out) << 2) | (int(add_class) << 3)]
     d[24] = _tickets(dy.device) if (splits > 1 and SPLIT_IN_KERNEL) else 0
     _lib.call("mx_conv_dgrad", d, _lib.stream())
     return dx
+
+
+def class_ok(w: torch.Tensor, x_shape, stride, padding, dilation) -> bool:
+    """conv_dgrad's class_out / add_class apply: the implicit-GEMM dgrad of a 1 x 1 filter
+    with stride > 1 and no padding (stride-decomposed into a single parity class)."""
+    return (tuple(w.shape[2:]) == (1, 1) and decomposed(1, 1, stride, padding, dilation)
+            and dgrad_supported(w, x_shape, stride, padding, dilation))
 
 
 DGRAD_MIN_TILES = 64

@@ -139,6 +139,19 @@ class JoinLink(BlockLink):
         self.join = {}
 
 
+# projection blocks with 1 x 1 stride-2 convs (A/B switch): the shortcut's parked input
+# gradient holds only the (0, 0) parity class (ops/convwg.py conv_dgrad class_out)
+# (+1.4 % ResNet-50 img/s: profiles/r6/resnet_launcher_ab_class_stash.txt)
+CLASS_STASH = True
+
+
+def _class_spread(c: torch.Tensor, x_shape, s: int) -> torch.Tensor:
+    """A compact parity-class gradient [N, C, ceil(H / s), ceil(W / s)] at its pixels of X's shape."""
+    full = torch.zeros(x_shape, dtype=c.dtype, device=c.device, memory_format=torch.channels_last)
+    full[:, :, ::s, ::s] = c
+    return full
+
+
 class ConvBiasActFn(torch.autograd.Function):
     """act(conv2d(x, w) + b (+ res)) with every direction on csrc/convwg.hip where it tiles:
     forward = one implicit-GEMM launch with the epilogue fused; backward = the ReLU mask +
@@ -207,8 +220,22 @@ class ConvBiasActFn(torch.autograd.Function):
         # wgrad 1017 vs 47 us: profiles/r6/resnet_gemm_dgrad_1x1_rejected.txt)
         wg_hip = ctx.needs_input_grad[1] and convwg.cout_ok(w.shape[0]) and w.shape[1] % 128 == 0
         if ctx.needs_input_grad[0]:
-            if convwg.dgrad_supported(w, tuple(x.shape), st, pd, dl) and (add is None or add.data_ptr() % 16 == 0):
-                dx = convwg.conv_dgrad(dy, w, tuple(x.shape), st, pd, dl, add=add, mask=mask)
+            # a 1 x 1 stride-2 projection shortcut parks only the pixels its filter reaches
+            # (compact parity class, no zero fill); conv1 adds them in its own class launch when
+            # it is such a conv too (stride_in_1x1), else they are spread to X's shape first
+            cls_out = (CLASS_STASH and "stash_dx" in roles and link.taker and add is None and mask is None
+                       and convwg.class_ok(w, tuple(x.shape), st, pd, dl))
+            add_cls = add is not None and getattr(add, "_mx_class", 0)
+            if add_cls:
+                s = add._mx_class
+                if not (convwg.class_ok(w, tuple(x.shape), st, pd, dl) and list(st) == [s, s]):
+                    add = _class_spread(add, tuple(x.shape), s)
+                    add_cls = 0
+            if cls_out:
+                dx = convwg.conv_dgrad(dy, w, tuple(x.shape), st, pd, dl, class_out=True)
+                dx._mx_class = st[0]
+            elif convwg.dgrad_supported(w, tuple(x.shape), st, pd, dl) and (add is None or add.data_ptr() % 16 == 0):
+                dx = convwg.conv_dgrad(dy, w, tuple(x.shape), st, pd, dl, add=add, mask=mask, add_class=bool(add_cls))
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, st, pd, dl, False, [0, 0], 1,
                                                          [True, False, False])[0]

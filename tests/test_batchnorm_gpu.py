@@ -162,11 +162,12 @@ def test_bn_bottleneck_residual_gradient_fused_into_conv1_dgrad(monkeypatch, pro
     import copy
     from mxtrain.models.resnet import Bottleneck
     from mxtrain.ops import convwg
-    seen = {"add": 0}
+    seen = {"add": 0, "cls": 0}
     real = convwg.conv_dgrad
 
     def spy(*a, add=None, **k):
         seen["add"] += add is not None
+        seen["cls"] += bool(k.get("class_out")) + bool(k.get("add_class"))
         return real(*a, add=add, **k)
 
     monkeypatch.setattr(convwg, "conv_dgrad", spy)
@@ -186,15 +187,21 @@ def test_bn_bottleneck_residual_gradient_fused_into_conv1_dgrad(monkeypatch, pro
         b2 = copy.deepcopy(blocks)
         for b in b2:
             b.fuse_backward = fuse
-        seen["add"] = 0
+        seen["add"] = seen["cls"] = 0
         x = x0.clone().requires_grad_()
         y = b2(x)
         if gy is None:
             gy = torch.randn_like(y)
         y.backward(gy)
         torch.cuda.synchronize()
-        out[fuse] = (y.detach().float(), x.grad.float(), [p.grad.float() for p in b2.parameters()], seen["add"])
+        out[fuse] = (y.detach().float(), x.grad.float(), [p.grad.float() for p in b2.parameters()], seen["add"],
+                     seen["cls"])
     assert out[True][3] == 2 and out[False][3] == 0, (out[True][3], out[False][3])
+    # 1 x 1 stride-2 conv1 and shortcut (stride_in_1x1): the parked dX is the compact parity class
+    ws = first.shortcut.conv.weight.to(torch.bfloat16) if proj else None
+    if proj and convwg.class_ok(ws, tuple(x0.shape), 2, 0, 1) and convwg.class_ok(
+            first.conv1.conv.weight.to(torch.bfloat16), tuple(x0.shape), 2, 0, 1):
+        assert out[True][4] == 2, out[True][4]
     assert torch.equal(out[False][0], out[True][0])
     b32 = copy.deepcopy(blocks).float()
     for b in b32:

@@ -367,6 +367,30 @@ def test_conv_dgrad_stride_decomposed_matches_fp32(case, epi):
     _close(dx, ref)
 
 
+@pytest.mark.parametrize("case", [(2, 512, 256, 40, 40, 1, 2, 0, 1), (1, 256, 512, 31, 29, 1, 2, 0, 1)])
+def test_conv_dgrad_parity_class_compact(case):
+    """1 x 1 stride-2 input gradient as the compact parity class (class_out: dX[:, :, ::2, ::2]
+    without the zero fill) and a compact class gradient as the add (add_class: added to the
+    class pixels only) against the full-shape launches (ResNet projection blocks)."""
+    from mxtrain.ops import convwg
+    N, Cin, Cout, H, W, k, stride, pad, dil = case
+    x, dy = _inputs(*case, seed=41)
+    g = torch.Generator().manual_seed(43)
+    w = (torch.randn(Cout, 1, 1, Cin, generator=g) * 0.1).to(torch.bfloat16).cuda().permute(0, 3, 1, 2)
+    cl = torch.channels_last
+    assert convwg.class_ok(w, tuple(x.shape), stride, pad, dil)
+    full = convwg.conv_dgrad(dy, w, tuple(x.shape), stride, pad, dil)
+    c = convwg.conv_dgrad(dy, w, tuple(x.shape), stride, pad, dil, class_out=True)
+    assert c.shape == (N, Cin, (H + 1) // 2, (W + 1) // 2) and c.is_contiguous(memory_format=cl)
+    assert torch.equal(c, full[:, :, ::2, ::2])
+    mask = torch.randn(x.shape, generator=g).relu().to(torch.bfloat16).cuda().contiguous(memory_format=cl)
+    spread = torch.zeros(x.shape, dtype=torch.bfloat16, device="cuda").contiguous(memory_format=cl)
+    spread[:, :, ::2, ::2] = c
+    a = convwg.conv_dgrad(dy, w, tuple(x.shape), stride, pad, dil, add=c, mask=mask, add_class=True)
+    b = convwg.conv_dgrad(dy, w, tuple(x.shape), stride, pad, dil, add=spread, mask=mask)
+    assert torch.equal(a, b)
+
+
 def test_conv_transpose_bias_relu_matches_fp32():
     """Mask-head upsampling (2x2 stride-2 transposed conv + bias + ReLU) on
     ops/epilogue.py ConvTransposeBiasActFn: output and the input, weight and bias gradients
