@@ -145,10 +145,13 @@ def _cast_launch(pairs, to_bf16: bool) -> None:
 class _CastGroup(torch.autograd.Function):
     """bf16 compute copies of fp32 weights in ONE launch (csrc/cast.hip), each copy with its
     weight's strides; the backward casts their bf16 gradients to fp32 in one launch too
-    (gradients in another memory order fall back to a plain cast)."""
+    (gradients in another memory order fall back to a plain cast).  ``state`` (a dict shared
+    by the groups of one forward): ``left`` groups whose backward has not run -- the
+    implicit-GEMM weight gradients' deferred split-K reductions (ops/convwg.py) are flushed
+    before each group's cast, deferral staying on while groups remain."""
 
     @staticmethod
-    def forward(ctx, *params):
+    def forward(ctx, state, *params):
         sizes = [p.numel() for p in params]
         flat = torch.empty(sum(sizes), dtype=torch.bfloat16, device=params[0].device)
         outs, off = [], 0
@@ -157,10 +160,16 @@ class _CastGroup(torch.autograd.Function):
             off += n
         _cast_launch(list(zip(params, outs)), True)
         ctx.meta = [(p.shape, p.stride()) for p in params]
+        ctx.state = state
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, *grads):
+        st = ctx.state
+        if st is not None and st.get("defer"):
+            from ..ops import convwg
+            st["left"] -= 1
+            convwg.defer_flush(keep_on=st["left"] > 0)
         out: List[Optional[torch.Tensor]] = [None] * len(grads)
         pairs = []
         for i, g in enumerate(grads):
@@ -174,7 +183,7 @@ class _CastGroup(torch.autograd.Function):
                 out[i] = torch.empty_strided(shape, stride, dtype=torch.float32, device=g.device).copy_(g)
         if pairs:
             _cast_launch(pairs, False)
-        return tuple(out)
+        return (None,) + tuple(out)
 
 
 class CastGroup:
@@ -183,16 +192,31 @@ class CastGroup:
     under bf16 autocast.  ``groups`` > 1 cuts them into contiguous chunks (data parallel:
     their fp32 gradients, and DDP's bucket hooks, then become ready during backward)."""
 
+    # the split-K weight-gradient reductions of the convolutions using these copies run as one
+    # batched launch per group backward (ops/convwg.py defer_begin / defer_flush) instead of
+    # one launch per convolution (44 per ResNet-50 step)
+    # (44 launches / 427 us -> 2 / 283 us per step; launcher A/B within noise:
+    # profiles/r6/resnet_launcher_ab_deferred_wgrad_reduce.txt)
+    DEFER = True
+
     def __init__(self, params, groups: int = 1):
         self.params = [p for p in params if p.requires_grad and _cast_dense(p) and p.dtype == torch.float32]
         self.groups = max(1, int(groups))
 
     def __enter__(self):
         if self.params and torch.is_grad_enabled():
-            for chunk in ComputeWeights.split([(p, None) for p in self.params], self.groups):
+            chunks = ComputeWeights.split([(p, None) for p in self.params], self.groups)
+            defer = CastGroup.DEFER and self.params[0].is_cuda
+            state = {"left": len(chunks), "defer": defer}
+            keys = []
+            for chunk in chunks:
                 ps = [p for p, _ in chunk]
-                for p, o in zip(ps, _CastGroup.apply(*ps)):
+                for p, o in zip(ps, _CastGroup.apply(state, *ps)):
                     _ACTIVE[id(p)] = o
+                    keys.append(o.data_ptr())
+            if defer:
+                from ..ops import convwg
+                convwg.defer_begin(keys)
         return self
 
     def __exit__(self, *exc):

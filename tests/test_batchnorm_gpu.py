@@ -327,3 +327,39 @@ def test_bn_relu_backward_stats_from_output_match_reading_x(monkeypatch):
     _close(outs[1][2], outs[0][2], 0.5, 1e-2, "dgamma")
     assert torch.equal(outs[1][3], outs[0][3])   # dbeta does not use xhat
 
+
+
+def test_cast_group_deferred_wgrad_reductions_bit_identical(monkeypatch):
+    """Under CastGroup the implicit-GEMM weight gradients' split-K reductions are deferred and
+    run as one batched launch before the group's fp32 cast (ops/convwg.py defer_*): the same
+    gradient bits as reducing each at once, and the batched launch actually ran."""
+    import copy
+    from mxtrain.models import compute_weights as cw
+    from mxtrain.models.resnet import Bottleneck
+    from mxtrain.ops import convwg
+    torch.manual_seed(7)
+    blocks = torch.nn.Sequential(Bottleneck(256, 128, stride=2, norm="bn"), Bottleneck(512, 128, norm="bn"))
+    blocks = blocks.to(DEV).to(memory_format=torch.channels_last)
+    x0 = torch.randn(8, 256, 32, 32, device=DEV).contiguous(memory_format=torch.channels_last)
+    flushed = {"n": 0}
+    real = convwg.defer_flush
+
+    def spy(*a, **k):
+        flushed["n"] += len(convwg._DEF["jobs"])
+        return real(*a, **k)
+
+    monkeypatch.setattr(convwg, "defer_flush", spy)
+    grads = {}
+    for defer in (False, True):
+        monkeypatch.setattr(cw.CastGroup, "DEFER", defer)
+        b = copy.deepcopy(blocks)
+        flushed["n"] = 0
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            with cw.CastGroup([m.weight for m in b.modules() if isinstance(m, torch.nn.Conv2d)]):
+                y = b(x0.to(torch.bfloat16))
+        y.float().square().mean().backward()
+        torch.cuda.synchronize()
+        grads[defer] = ([p.grad.clone() for p in b.parameters()], flushed["n"])
+    assert grads[True][1] > 0 and grads[False][1] == 0, (grads[True][1], grads[False][1])
+    for a, c in zip(grads[True][0], grads[False][0]):
+        assert torch.equal(a, c)
