@@ -20,15 +20,12 @@ constexpr int kThreads = 256;
 __global__ __launch_bounds__(kThreads) void maxpool3s2_fwd_kernel(const uint16_t* __restrict__ x,
                                                                   uint16_t* __restrict__ y, uint8_t* __restrict__ arg,
                                                                   int N, int H, int W, int C, int OH, int OW) {
+  // one workgroup per output row (n, oh): 32-bit index math only (the 64-bit divisions of a
+  // flat index cost more VALU time than the pass's memory traffic)
   const int c8 = C / 8;
-  const int64_t total = (int64_t)N * OH * OW * c8;
-  for (int64_t v = (int64_t)blockIdx.x * kThreads + threadIdx.x; v < total; v += (int64_t)gridDim.x * kThreads) {
-    const int cv = (int)(v % c8);
-    int64_t p = v / c8;
-    const int ow = (int)(p % OW);
-    p /= OW;
-    const int oh = (int)(p % OH);
-    const int n = (int)(p / OH);
+  const int n = blockIdx.x / OH, oh = blockIdx.x - (blockIdx.x / OH) * OH;
+  for (int e = threadIdx.x; e < OW * c8; e += kThreads) {
+    const int ow = e / c8, cv = e - (e / c8) * c8;
     float m[8];
     uint32_t idx[8];
 #pragma unroll
@@ -68,14 +65,9 @@ __global__ __launch_bounds__(kThreads) void maxpool3s2_bwd_kernel(const uint16_t
                                                                   uint16_t* __restrict__ dx, int N, int H, int W,
                                                                   int C, int OH, int OW) {
   const int c8 = C / 8;
-  const int64_t total = (int64_t)N * H * W * c8;
-  for (int64_t v = (int64_t)blockIdx.x * kThreads + threadIdx.x; v < total; v += (int64_t)gridDim.x * kThreads) {
-    const int cv = (int)(v % c8);
-    int64_t p = v / c8;
-    const int w = (int)(p % W);
-    p /= W;
-    const int h = (int)(p % H);
-    const int n = (int)(p / H);
+  const int n = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H;   // one input row per workgroup
+  for (int e = threadIdx.x; e < W * c8; e += kThreads) {
+    const int w = e / c8, cv = e - (e / c8) * c8;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     // the windows containing row h: oh in {(h + 1) / 2 - 1, (h + 1) / 2} with kh = h - 2 oh + 1 in [0, 2]
 #pragma unroll
@@ -104,18 +96,14 @@ __global__ __launch_bounds__(kThreads) void maxpool3s2_bwd_kernel(const uint16_t
   }
 }
 
-int grid_for(int64_t nvec) {
-  const int64_t g = (nvec + kThreads - 1) / kThreads;
-  return (int)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
-}
-
 }  // namespace
 
 // x [N][H][W][C] -> y [N][OH][OW][C] (+ argmax bytes [N][OH][OW][C]); OH = (H - 1) / 2 + 1
 MX_EXPORT int mx_maxpool3s2_fwd(const void* x, void* y, void* arg, int N, int H, int W, int C, hipStream_t s) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8) return hipErrorInvalidValue;
   const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
-  hipLaunchKernelGGL(maxpool3s2_fwd_kernel, dim3(grid_for((int64_t)N * OH * OW * (C / 8))), dim3(kThreads), 0, s,
+  if ((int64_t)N * OH >= ((int64_t)1 << 31) || (int64_t)OW * (C / 8) >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(maxpool3s2_fwd_kernel, dim3((unsigned)(N * OH)), dim3(kThreads), 0, s,
                      (const uint16_t*)x, (uint16_t*)y, (uint8_t*)arg, N, H, W, C, OH, OW);
   return hipGetLastError();
 }
@@ -124,7 +112,8 @@ MX_EXPORT int mx_maxpool3s2_fwd(const void* x, void* y, void* arg, int N, int H,
 MX_EXPORT int mx_maxpool3s2_bwd(const void* dy, const void* arg, void* dx, int N, int H, int W, int C, hipStream_t s) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8) return hipErrorInvalidValue;
   const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
-  hipLaunchKernelGGL(maxpool3s2_bwd_kernel, dim3(grid_for((int64_t)N * H * W * (C / 8))), dim3(kThreads), 0, s,
+  if ((int64_t)N * H >= ((int64_t)1 << 31) || (int64_t)W * (C / 8) >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(maxpool3s2_bwd_kernel, dim3((unsigned)(N * H)), dim3(kThreads), 0, s,
                      (const uint16_t*)dy, (const uint8_t*)arg, (uint16_t*)dx, N, H, W, C, OH, OW);
   return hipGetLastError();
 }
@@ -157,15 +146,15 @@ __global__ __launch_bounds__(256) void gap_fwd_kernel(const uint16_t* __restrict
 __global__ __launch_bounds__(256) void gap_bwd_kernel(const float* __restrict__ g, uint16_t* __restrict__ dx, int N,
                                                       int HW, int C) {
   const int c8 = C / 8;
-  const int64_t total = (int64_t)N * HW * c8;
   const float inv = 1.f / (float)HW;
-  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < total; v += (int64_t)gridDim.x * 256) {
-    const int cv = (int)(v % c8);
-    const int n = (int)(v / ((int64_t)HW * c8));
+  const int n = blockIdx.x;   // image n, a 1 / gridDim.y share of its pixels
+  uint4* dst = reinterpret_cast<uint4*>(dx) + (size_t)n * HW * c8;
+  for (int e = blockIdx.y * 256 + threadIdx.x; e < HW * c8; e += 256 * gridDim.y) {
+    const int cv = e % c8;
     const float4* s = reinterpret_cast<const float4*>(g + (size_t)n * C + 8 * cv);
     const float4 a = s[0], b = s[1];
     const float f[8] = {a.x * inv, a.y * inv, a.z * inv, a.w * inv, b.x * inv, b.y * inv, b.z * inv, b.w * inv};
-    reinterpret_cast<uint4*>(dx)[v] = pack8(f);
+    dst[e] = pack8(f);
   }
 }
 }  // namespace
@@ -180,7 +169,8 @@ MX_EXPORT int mx_gap_fwd(const void* x, float* y, int N, int HW, int C, hipStrea
 
 MX_EXPORT int mx_gap_bwd(const float* g, void* dx, int N, int HW, int C, hipStream_t s) {
   if (N <= 0 || HW <= 0 || C <= 0 || C % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(gap_bwd_kernel, dim3((unsigned)grid_for((int64_t)N * HW * (C / 8))), dim3(256), 0, s, g,
+  if ((int64_t)HW * (C / 8) >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3((unsigned)N, 8), dim3(256), 0, s, g,
                      (uint16_t*)dx, N, HW, C);
   return hipGetLastError();
 }
