@@ -251,15 +251,24 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const uint16_t* __re
                                                             const float* __restrict__ shift,
                                                             uint16_t* __restrict__ y, int64_t nvec, int c8) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
-    const int c = 8 * (int)(v % c8);
+  float sc[8], sh[8];
+  auto coefs = [&](int c) __attribute__((always_inline)) {
+    const float4 s0 = *reinterpret_cast<const float4*>(scale + c), s1 = *reinterpret_cast<const float4*>(scale + c + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(shift + c), h1 = *reinterpret_cast<const float4*>(shift + c + 4);
+    sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+    sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+  };
+  // the grid stride is a multiple of c8 (c8 divides the 256-thread block: C a power-of-two
+  // multiple of 8 up to 2048): a thread's channels never change -- the coefficients are
+  // loaded once and no per-vector 64-bit modulo runs
+  const bool fixed = (kThreads % c8) == 0;
+  const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (fixed) coefs(8 * (int)((uint32_t)v0 % (uint32_t)c8));
+  for (int64_t v = v0; v < nvec; v += stride) {
+    if (!fixed) coefs(8 * (int)(v % c8));
     float a[8], r[8];
     unpack8(reinterpret_cast<const uint4*>(x)[v], a);
     if (kRes) unpack8(reinterpret_cast<const uint4*>(res)[v], r);
-    const float4 s0 = *reinterpret_cast<const float4*>(scale + c), s1 = *reinterpret_cast<const float4*>(scale + c + 4);
-    const float4 h0 = *reinterpret_cast<const float4*>(shift + c), h1 = *reinterpret_cast<const float4*>(shift + c + 4);
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float t = __builtin_fmaf(a[j], sc[j], sh[j]);
@@ -405,8 +414,24 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const uint16_t* 
                                                                 int64_t nvec, int C) {
   const int c8 = C / 8;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
-    const int c = 8 * (int)(v % c8);
+  // per-channel terms of dx = k0 (dz - k1 - (x - mean) rstd k2) = A (x - mean) + B dz + D,
+  // held in registers when the thread's channels are fixed (as bn_apply_kernel)
+  float A[8], B[8], D[8], Mn[8];
+  auto coefs = [&](int c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float k0 = coef[c + j];
+      A[j] = -k0 * rstd[c + j] * coef[2 * C + c + j];
+      B[j] = k0;
+      D[j] = -k0 * coef[C + c + j];
+      Mn[j] = mean[c + j];
+    }
+  };
+  const bool fixed = (kThreads % c8) == 0;
+  const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (fixed) coefs(8 * (int)((uint32_t)v0 % (uint32_t)c8));
+  for (int64_t v = v0; v < nvec; v += stride) {
+    if (!fixed) coefs(8 * (int)(v % c8));
     float d[8], a[8];
     unpack8(reinterpret_cast<const uint4*>(dy)[v], d);
     unpack8(reinterpret_cast<const uint4*>(x)[v], a);
@@ -418,10 +443,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const uint16_t* 
     }
     if (kRes) reinterpret_cast<uint4*>(dres)[v] = pack8(d);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float xh = (a[j] - mean[c + j]) * rstd[c + j];
-      a[j] = coef[c + j] * (d[j] - coef[C + c + j] - xh * coef[2 * C + c + j]);
-    }
+    for (int j = 0; j < 8; ++j) a[j] = __builtin_fmaf(A[j], a[j] - Mn[j], __builtin_fmaf(B[j], d[j], D[j]));
     reinterpret_cast<uint4*>(dx)[v] = pack8(a);
   }
 }
