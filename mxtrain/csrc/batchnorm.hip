@@ -196,15 +196,17 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_cm_kernel(const float* _
   const float* pqr = pm2 + (size_t)c * nblk;
   float na = 0.f, ma = 0.f, m2 = 0.f;
   int b = t;
-  for (; b + 3 * kThreads < nblk; b += 4 * kThreads) {
-    float mb[4], qb[4];
+  // 8 + 8 loads in flight per thread (latency-bound: 12,544 partials per channel at the
+  // ResNet res2 shapes); the merge order is the plain b = t, t + 256, ... sequence
+  for (; b + 7 * kThreads < nblk; b += 8 * kThreads) {
+    float mb[8], qb[8];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 8; ++k) {
       mb[k] = pmr[b + k * kThreads];
       qb[k] = pqr[b + k * kThreads];
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < 8; ++k)
       chan_merge(na, ma, m2, (float)min(rpb, M - (b + k * kThreads) * rpb), mb[k], qb[k]);
   }
   for (; b < nblk; b += kThreads) chan_merge(na, ma, m2, (float)min(rpb, M - b * rpb), pmr[b], pqr[b]);
