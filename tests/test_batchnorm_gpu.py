@@ -359,6 +359,7 @@ def test_cast_group_deferred_wgrad_reductions_bit_identical(monkeypatch):
                 y = b(x0.to(torch.bfloat16))
         y.float().square().mean().backward()
         torch.cuda.synchronize()
+        assert not convwg._DEF["on"], "deferral must be off after the last group's backward"
         grads[defer] = ([p.grad.clone() for p in b.parameters()], flushed["n"])
     assert grads[True][1] > 0 and grads[False][1] == 0, (grads[True][1], grads[False][1])
     for a, c in zip(grads[True][0], grads[False][0]):
