@@ -501,6 +501,7 @@ MX_EXPORT int mx_bn_fwd(const void* x, const void* res, void* y, const float* ga
     hipLaunchKernelGGL(bn_finalize_cm_kernel, dim3(C), dim3(kThreads), 0, s, pre, pre + (size_t)nb * C, nb,
                        kPreRows, M, C, gamma, beta, eps, momentum, mean, rstd, scale, shift, run_mean, run_var, nbt);
   }
+  if (!y) return hipGetLastError();   // statistics only (mx_bn2_apply applies them)
   const int64_t nvec = (int64_t)M * c8;
   const dim3 gr(elem_grid(nvec));
   if (res) {
@@ -574,5 +575,205 @@ MX_EXPORT int mx_bn_bwd(const void* dy, const void* y, const void* x, const floa
     else MX_BN_BWD(false, false);
   }
 #undef MX_BN_BWD
+  return hipGetLastError();
+}
+
+// ============================================================ two BatchNorms into one ReLU
+// The ResNet projection block's tail  y = relu(BN_a(xa) + BN_b(xb))  (conv3's BN plus the
+// shortcut's BN) without the shortcut BN's own output tensor: forward one apply pass reading
+// xa, xb (the statistics of both come from mx_bn_fwd with y = null); backward one statistics
+// pass (dz = dy (y > 0) shared: sum dz, sum dz xhat_a, sum dz xhat_b) and one apply pass
+// writing both input gradients -- 5 of the 18 tensor passes of the two separate BN layers
+// disappear.  Per-channel terms live in registers (the grid stride is a multiple of C / 8).
+namespace {
+
+struct Bn2P {
+  const float *mean_a, *rstd_a, *gamma_a, *beta_a, *mean_b, *rstd_b, *gamma_b, *beta_b;
+};
+
+__global__ __launch_bounds__(kThreads) void bn2_apply_kernel(const uint16_t* __restrict__ xa,
+                                                             const uint16_t* __restrict__ xb, const Bn2P p,
+                                                             uint16_t* __restrict__ y, int64_t nvec, int c8) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  float sa[8], sb[8], hh[8];
+  auto coefs = [&](int c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sa[j] = p.gamma_a[c + j] * p.rstd_a[c + j];
+      sb[j] = p.gamma_b[c + j] * p.rstd_b[c + j];
+      hh[j] = p.beta_a[c + j] - p.mean_a[c + j] * sa[j] + p.beta_b[c + j] - p.mean_b[c + j] * sb[j];
+    }
+  };
+  const bool fixed = (kThreads % c8) == 0;
+  const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (fixed) coefs(8 * (int)((uint32_t)v0 % (uint32_t)c8));
+  for (int64_t v = v0; v < nvec; v += stride) {
+    if (!fixed) coefs(8 * (int)(v % c8));
+    float a[8], b[8];
+    unpack8(reinterpret_cast<const uint4*>(xa)[v], a);
+    unpack8(reinterpret_cast<const uint4*>(xb)[v], b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = fmaxf(__builtin_fmaf(a[j], sa[j], __builtin_fmaf(b[j], sb[j], hh[j])), 0.f);
+    reinterpret_cast<uint4*>(y)[v] = pack8(a);
+  }
+}
+
+// partial_a / partial_b: [nblk][2][C] = (sum dz, sum dz xhat) of each BN
+__global__ __launch_bounds__(kThreads) void bn2_bwd_stats_kernel(const uint16_t* __restrict__ dy,
+                                                                 const uint16_t* __restrict__ y,
+                                                                 const uint16_t* __restrict__ xa,
+                                                                 const uint16_t* __restrict__ xb, const Bn2P p,
+                                                                 int M, int C, int rows_per_block,
+                                                                 float* __restrict__ partial_a,
+                                                                 float* __restrict__ partial_b) {
+  const RowGeo g(C);
+  const int vc = blockIdx.x * g.cv + g.tv;
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  __shared__ float sm[3][kThreads][8];
+  float sd[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sx[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (vc < g.c8) {
+    float ma[8], ra[8], mb[8], rb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ma[j] = p.mean_a[8 * vc + j];
+      ra[j] = p.rstd_a[8 * vc + j];
+      mb[j] = p.mean_b[8 * vc + j];
+      rb[j] = p.rstd_b[8 * vc + j];
+    }
+    for (int r = r0 + g.tr; r < r1; r += g.rpi) {
+      float d[8], o[8], a[8], b[8];
+      const size_t off = (size_t)r * C;
+      unpack8(reinterpret_cast<const uint4*>(dy + off)[vc], d);
+      unpack8(reinterpret_cast<const uint4*>(y + off)[vc], o);
+      unpack8(reinterpret_cast<const uint4*>(xa + off)[vc], a);
+      unpack8(reinterpret_cast<const uint4*>(xb + off)[vc], b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float dz = o[j] > 0.f ? d[j] : 0.f;
+        sd[j] += dz;
+        sx[j] = __builtin_fmaf(dz, (a[j] - ma[j]) * ra[j], sx[j]);
+        sz[j] = __builtin_fmaf(dz, (b[j] - mb[j]) * rb[j], sz[j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sm[0][threadIdx.x][j] = sd[j];
+    sm[1][threadIdx.x][j] = sx[j];
+    sm[2][threadIdx.x][j] = sz[j];
+  }
+  __syncthreads();
+  if (g.tr == 0 && vc < g.c8) {
+    for (int k = 1; k < g.rpi; ++k) {
+      const int t = k * g.cv + g.tv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sd[j] += sm[0][t][j];
+        sx[j] += sm[1][t][j];
+        sz[j] += sm[2][t][j];
+      }
+    }
+    float* pa = partial_a + (size_t)blockIdx.y * 2 * C + 8 * vc;
+    float* pb = partial_b + (size_t)blockIdx.y * 2 * C + 8 * vc;
+#pragma unroll
+    for (int j = 0; j < 8; j += 4) {
+      const float4 d4 = make_float4(sd[j], sd[j + 1], sd[j + 2], sd[j + 3]);
+      *reinterpret_cast<float4*>(pa + j) = d4;
+      *reinterpret_cast<float4*>(pb + j) = d4;
+      *reinterpret_cast<float4*>(pa + C + j) = make_float4(sx[j], sx[j + 1], sx[j + 2], sx[j + 3]);
+      *reinterpret_cast<float4*>(pb + C + j) = make_float4(sz[j], sz[j + 1], sz[j + 2], sz[j + 3]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void bn2_bwd_apply_kernel(const uint16_t* __restrict__ dy,
+                                                                 const uint16_t* __restrict__ y,
+                                                                 const uint16_t* __restrict__ xa,
+                                                                 const uint16_t* __restrict__ xb, const Bn2P p,
+                                                                 const float* __restrict__ coef_a,
+                                                                 const float* __restrict__ coef_b,
+                                                                 uint16_t* __restrict__ dxa, uint16_t* __restrict__ dxb,
+                                                                 int64_t nvec, int C) {
+  const int c8 = C / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // dx = k0 (dz - k1 - (x - mean) rstd k2) = A (x - mean) + B dz + D, per BN
+  float Aa[8], Ba[8], Da[8], Ma[8], Ab[8], Bb[8], Db[8], Mb[8];
+  auto coefs = [&](int c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float ka = coef_a[c + j], kb = coef_b[c + j];
+      Aa[j] = -ka * p.rstd_a[c + j] * coef_a[2 * C + c + j];
+      Ba[j] = ka;
+      Da[j] = -ka * coef_a[C + c + j];
+      Ma[j] = p.mean_a[c + j];
+      Ab[j] = -kb * p.rstd_b[c + j] * coef_b[2 * C + c + j];
+      Bb[j] = kb;
+      Db[j] = -kb * coef_b[C + c + j];
+      Mb[j] = p.mean_b[c + j];
+    }
+  };
+  const bool fixed = (kThreads % c8) == 0;
+  const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (fixed) coefs(8 * (int)((uint32_t)v0 % (uint32_t)c8));
+  for (int64_t v = v0; v < nvec; v += stride) {
+    if (!fixed) coefs(8 * (int)(v % c8));
+    float d[8], o[8], a[8], b[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[v], d);
+    unpack8(reinterpret_cast<const uint4*>(y)[v], o);
+    unpack8(reinterpret_cast<const uint4*>(xa)[v], a);
+    unpack8(reinterpret_cast<const uint4*>(xb)[v], b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float dz = o[j] > 0.f ? d[j] : 0.f;
+      a[j] = __builtin_fmaf(Aa[j], a[j] - Ma[j], __builtin_fmaf(Ba[j], dz, Da[j]));
+      b[j] = __builtin_fmaf(Ab[j], b[j] - Mb[j], __builtin_fmaf(Bb[j], dz, Db[j]));
+    }
+    reinterpret_cast<uint4*>(dxa)[v] = pack8(a);
+    reinterpret_cast<uint4*>(dxb)[v] = pack8(b);
+  }
+}
+
+}  // namespace
+
+// stats: float[8] pointers {mean_a, rstd_a, gamma_a, beta_a, mean_b, rstd_b, gamma_b, beta_b}
+// (fp32 [C] each; the statistics from mx_bn_fwd with y = null).  xa, xb, y: [M][C] bf16.
+MX_EXPORT int mx_bn2_apply(const void* xa, const void* xb, void* y, const int64_t* stats, int M, int C,
+                           hipStream_t s) {
+  if (C % 8 || C <= 0 || M <= 0) return hipErrorInvalidValue;
+  const Bn2P p{(const float*)stats[0], (const float*)stats[1], (const float*)stats[2], (const float*)stats[3],
+               (const float*)stats[4], (const float*)stats[5], (const float*)stats[6], (const float*)stats[7]};
+  const int64_t nvec = (int64_t)M * (C / 8);
+  hipLaunchKernelGGL(bn2_apply_kernel, dim3(elem_grid(nvec)), dim3(kThreads), 0, s, (const uint16_t*)xa,
+                     (const uint16_t*)xb, p, (uint16_t*)y, nvec, C / 8);
+  return hipGetLastError();
+}
+
+// floats of scratch mx_bn2_bwd needs
+MX_EXPORT int64_t mx_bn2_scratch(int M, int C) { return 2 * mx_bn_scratch(M, C); }
+
+// dy, y (the forward output), xa, xb -> dxa, dxb (bf16 [M][C]); dgamma / dbeta of both (fp32 [C])
+MX_EXPORT int mx_bn2_bwd(const void* dy, const void* y, const void* xa, const void* xb, const int64_t* stats,
+                         void* dxa, void* dxb, float* dgamma_a, float* dbeta_a, float* dgamma_b, float* dbeta_b,
+                         int M, int C, float* scratch, hipStream_t s) {
+  if (C % 8 || C <= 0 || M <= 0) return hipErrorInvalidValue;
+  const Bn2P p{(const float*)stats[0], (const float*)stats[1], (const float*)stats[2], (const float*)stats[3],
+               (const float*)stats[4], (const float*)stats[5], (const float*)stats[6], (const float*)stats[7]};
+  const int rpb = rows_per_block(M), nblk = (M + rpb - 1) / rpb;
+  const int c8 = C / 8, cv = c8 < kThreads ? c8 : kThreads;
+  float* part_a = scratch;
+  float* part_b = part_a + (size_t)nblk * 2 * C;
+  float* coef_a = part_b + (size_t)nblk * 2 * C;
+  float* coef_b = coef_a + 3 * (size_t)C;
+  hipLaunchKernelGGL(bn2_bwd_stats_kernel, dim3((c8 + cv - 1) / cv, nblk), dim3(kThreads), 0, s,
+                     (const uint16_t*)dy, (const uint16_t*)y, (const uint16_t*)xa, (const uint16_t*)xb, p, M, C, rpb,
+                     part_a, part_b);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(kThreads), 0, s, part_a, nblk, M, C, p.gamma_a,
+                     p.rstd_a, dgamma_a, dbeta_a, 0, coef_a);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(kThreads), 0, s, part_b, nblk, M, C, p.gamma_b,
+                     p.rstd_b, dgamma_b, dbeta_b, 0, coef_b);
+  const int64_t nvec = (int64_t)M * c8;
+  hipLaunchKernelGGL(bn2_bwd_apply_kernel, dim3(elem_grid(nvec)), dim3(kThreads), 0, s, (const uint16_t*)dy,
+                     (const uint16_t*)y, (const uint16_t*)xa, (const uint16_t*)xb, p, coef_a, coef_b,
+                     (uint16_t*)dxa, (uint16_t*)dxb, nvec, C);
   return hipGetLastError();
 }

@@ -21,7 +21,7 @@ import torch.nn.functional as F
 
 from . import compute_weights as _cw
 from ..ops import convwg
-from ..ops.batchnorm import bn_act
+from ..ops.batchnorm import bn2_add_relu, bn_act
 from ..ops.epilogue import BlockLink, ConvBiasActFn, conv_bias_act, fused_conv_ok, global_avg_pool, maxpool3s2
 
 
@@ -124,6 +124,14 @@ class ConvNorm(nn.Module):
         return bn_act(y, self.norm, residual=residual, relu=relu, link=link if "stash_res" in roles else None,
                       pre=pre[0] if pre else None)
 
+    def conv_pre(self, x, fuse=None):
+        """The trainable-BN path's convolution alone: (conv output, its epilogue BN statistics
+        or None) -- for a consumer applying this BN itself (ops/batchnorm.py bn2_add_relu)."""
+        pre = [] if self.norm.training and BN_EPILOGUE_STATS else None
+        y = _conv_nobias(x, self.conv.weight, self.conv.stride, self.conv.padding, self.conv.dilation,
+                         fuse=fuse, bnpre=pre)
+        return y, (pre[0] if pre else None)
+
     def fused_ok(self, x) -> bool:
         """This conv (frozen norm) would run ConvBiasActFn on input x, honouring a BlockLink."""
         if self.norm_kind != "frozen" or ConvNorm.calibrating:
@@ -217,8 +225,12 @@ class Bottleneck(nn.Module):
                 link = BlockLink()
                 a1 = self.conv1(x, fuse=(link, 1, ("take_res", "take_dx")))
                 a2 = self.conv2(a1)
-                idt = self.shortcut(x, fuse=(link, 0, ("stash_dx",)))
-                return self.conv3(a2, residual=idt, relu=True)
+                # (the shortcut conv is created after conv2 and before conv3, so its backward
+                # still runs before conv1's: see fuse_projection)
+                yd, pd = self.shortcut.conv_pre(x, fuse=(link, 0, ("stash_dx",)))
+                y3, p3 = self.conv3.conv_pre(a2)
+                # conv3's BN + the shortcut's BN + ReLU as one node (no shortcut BN output tensor)
+                return bn2_add_relu(y3, self.conv3.norm, yd, self.shortcut.norm, p3, pd)
             a1 = self.conv1(x)
             a2 = self.conv2(a1)
             idt = x if ident else self.shortcut(x)

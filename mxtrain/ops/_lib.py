@@ -99,6 +99,8 @@ SIGNATURES = {
     # batchnorm.hip
     "mx_bn_fwd": [P, P, P, P, P, P, P, P, P, I, I, F, F, I, P, P, P, P],
     "mx_bn_apply": [P, P, P, P, P, I, I, I, P],
+    "mx_bn2_apply": [P, P, P, P, I, I, P],
+    "mx_bn2_bwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, P, P],
     "mx_bn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, P, P, I, P],
     "mx_conv_wgrad_tile": [I],
     "mx_conv_wgrad": [P, F, I, P],

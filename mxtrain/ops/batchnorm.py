@@ -88,6 +88,86 @@ class BNActFn(torch.autograd.Function):
                 None)
 
 
+def _stat_ptrs(*ts) -> "ctypes.Array":
+    import ctypes
+    return (ctypes.c_int64 * len(ts))(*[t.data_ptr() for t in ts])
+
+
+class BN2AddReluFn(torch.autograd.Function):
+    """relu(BN_a(xa) + BN_b(xb)) in training mode (csrc/batchnorm.hip mx_bn2_*): the ResNet
+    projection block's tail -- conv3's BN and the shortcut's BN -- without the shortcut BN's
+    output tensor.  Each BN's statistics / running statistics / batch count as ``bn_act``
+    (mx_bn_fwd with y = null, from the convs' epilogue statistics when given); one apply
+    pass forward; backward one statistics pass (the shared dz) and one apply pass writing
+    both input gradients."""
+
+    @staticmethod
+    def forward(ctx, xa, ga, ba, xb, gb, bb, bufs_a, bufs_b):
+        N, C, H, W = xa.shape
+        M = N * H * W
+        dev = xa.device
+        stats = []
+        for x, g, b, (rm, rv, mom, eps, nbt, pre) in ((xa, ga, ba, bufs_a), (xb, gb, bb, bufs_b)):
+            mean = torch.empty(C, dtype=torch.float32, device=dev)
+            rstd = torch.empty_like(mean)
+            g32 = g.detach().float().contiguous()
+            b32 = b.detach().float().contiguous()
+            _lib.call("mx_bn_fwd", x.data_ptr(), 0, 0, g32.data_ptr(), b32.data_ptr(), mean.data_ptr(),
+                      rstd.data_ptr(), _lib.ptr(rm), _lib.ptr(rv), M, C, float(eps), float(mom), 0,
+                      _scratch(M, C, dev).data_ptr(), _lib.ptr(nbt), _lib.ptr(pre), _lib.stream())
+            stats += [mean, rstd, g32, b32]
+        y = torch.empty_like(xa, memory_format=torch.channels_last)
+        ptrs = _stat_ptrs(*stats)
+        _lib.call("mx_bn2_apply", xa.data_ptr(), xb.data_ptr(), y.data_ptr(), ptrs, M, C, _lib.stream())
+        ctx.save_for_backward(xa, xb, y, *stats)
+        ctx.pdtypes = (ga.dtype, ba.dtype, gb.dtype, bb.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xa, xb, y, *stats = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        N, C, H, W = xa.shape
+        M = N * H * W
+        dxa = torch.empty_like(xa, memory_format=torch.channels_last)
+        dxb = torch.empty_like(xb, memory_format=torch.channels_last)
+        grads = [torch.empty(C, dtype=torch.float32, device=xa.device) for _ in range(4)]
+        scratch = torch.empty(2 * _lib.query64("mx_bn_scratch", M, C), dtype=torch.float32, device=xa.device)
+        _lib.call("mx_bn2_bwd", dy.data_ptr(), y.data_ptr(), xa.data_ptr(), xb.data_ptr(), _stat_ptrs(*stats),
+                  dxa.data_ptr(), dxb.data_ptr(), *[t.data_ptr() for t in grads], M, C, scratch.data_ptr(),
+                  _lib.stream())
+        dga, dba, dgb, dbb = (t.to(d) for t, d in zip(grads, ctx.pdtypes))
+        return dxa, dga, dba, dxb, dgb, dbb, None, None
+
+
+def _bufs(bn: torch.nn.BatchNorm2d, pre):
+    mom = bn.momentum
+    nbt = None
+    if bn.track_running_stats and bn.num_batches_tracked is not None:
+        if mom is None:
+            bn.num_batches_tracked.add_(1)
+            mom = 1.0 / float(bn.num_batches_tracked)
+        else:
+            nbt = bn.num_batches_tracked
+    return (bn.running_mean if bn.track_running_stats else None, bn.running_var if bn.track_running_stats else None,
+            0.0 if mom is None else mom, bn.eps, nbt, pre)
+
+
+def bn2_add_relu(xa: torch.Tensor, bn_a: torch.nn.BatchNorm2d, xb: torch.Tensor, bn_b: torch.nn.BatchNorm2d,
+                 pre_a: Optional[torch.Tensor] = None, pre_b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """relu(bn_a(xa) + bn_b(xb)); one fused node when both BNs train on the HIP path, else
+    the two-layer form (bn_b's output as bn_a's residual)."""
+    if (DUAL and bn_a.training and bn_b.training and supported(xa, xb) and xa.shape == xb.shape
+            and xb.data_ptr() % 16 == 0 and xa.data_ptr() % 16 == 0):
+        return BN2AddReluFn.apply(xa, bn_a.weight, bn_a.bias, xb, bn_b.weight, bn_b.bias, _bufs(bn_a, pre_a),
+                                  _bufs(bn_b, pre_b))
+    return bn_act(xa, bn_a, residual=bn_act(xb, bn_b, None, False, pre=pre_b), relu=True, pre=pre_a)
+
+
+# (+2.9 % ResNet-50 img/s through the launcher: profiles/r6/resnet_launcher_ab_bn2_add_relu.txt)
+DUAL = True
+
+
 def bn_act_ref(x, gamma, beta, residual, running_mean, running_var, momentum, eps, relu, training=True):
     """The same op in plain torch (fp32 math): the CPU path and the tests' reference."""
     y = F.batch_norm(x.float(), running_mean, running_var, gamma.float(), beta.float(), training, momentum, eps)

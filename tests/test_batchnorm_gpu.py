@@ -202,12 +202,17 @@ def test_bn_bottleneck_residual_gradient_fused_into_conv1_dgrad(monkeypatch, pro
     if proj and convwg.class_ok(ws, tuple(x0.shape), 2, 0, 1) and convwg.class_ok(
             first.conv1.conv.weight.to(torch.bfloat16), tuple(x0.shape), 2, 0, 1):
         assert out[True][4] == 2, out[True][4]
-    assert torch.equal(out[False][0], out[True][0])
+    if not proj:   # (fused BN pair: the shortcut BN's output is not rounded to bf16 before the add)
+        assert torch.equal(out[False][0], out[True][0])
     b32 = copy.deepcopy(blocks).float()
     for b in b32:
         b.fuse_backward = False
     x32 = x0.float().requires_grad_()
-    b32(x32).backward(gy.float())
+    y32 = b32(x32)
+    y32.backward(gy.float())
+    ey_f = (out[True][0] - y32.detach()).abs().max().item()
+    ey_u = (out[False][0] - y32.detach()).abs().max().item()
+    assert ey_f <= 1.25 * ey_u + 1e-2, (ey_f, ey_u)
     e_f = (out[True][1] - x32.grad).abs().max().item()
     e_u = (out[False][1] - x32.grad).abs().max().item()
     assert e_f <= 1.25 * e_u + 1e-3 * x32.grad.abs().max().item(), (e_f, e_u)
@@ -364,3 +369,43 @@ def test_cast_group_deferred_wgrad_reductions_bit_identical(monkeypatch):
     assert grads[True][1] > 0 and grads[False][1] == 0, (grads[True][1], grads[False][1])
     for a, c in zip(grads[True][0], grads[False][0]):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("N,C,H,W", [(16, 256, 14, 14), (4, 2048, 7, 7), (3, 64, 9, 11)])
+def test_bn2_add_relu_matches_fp32(N, C, H, W):
+    """ops/batchnorm.py bn2_add_relu (csrc/batchnorm.hip mx_bn2_*): relu(BN_a(xa) + BN_b(xb))
+    as one node against fp32 torch -- output, both BNs' running statistics and batch counts,
+    both input gradients and both BNs' dgamma / dbeta."""
+    from mxtrain.ops.batchnorm import BN2AddReluFn, bn2_add_relu
+    g = torch.Generator(device=DEV).manual_seed(C + H)
+    cl = torch.channels_last
+    xa = (torch.randn(N, C, H, W, device=DEV, generator=g) * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+    xb = (torch.randn(N, C, H, W, device=DEV, generator=g) - 0.3).to(torch.bfloat16).contiguous(memory_format=cl)
+    bns = [torch.nn.BatchNorm2d(C).to(DEV) for _ in range(2)]
+    for bn in bns:
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5, generator=g)
+            bn.bias.uniform_(-0.5, 0.5, generator=g)
+    refs = [torch.nn.BatchNorm2d(C).to(DEV) for _ in range(2)]
+    for r, bn in zip(refs, bns):
+        r.load_state_dict(bn.state_dict())
+    a, b = xa.clone().requires_grad_(True), xb.clone().requires_grad_(True)
+    y = bn2_add_relu(a, bns[0], b, bns[1])
+    assert type(y.grad_fn).__name__.startswith(BN2AddReluFn.__name__)
+    ar, br = xa.float().requires_grad_(True), xb.float().requires_grad_(True)
+    pre = refs[0](ar) + refs[1](br)
+    yr = torch.relu(pre)
+    _close(y, yr, 3e-2, 1e-2, "y")
+    for bn, r in zip(bns, refs):
+        _close(bn.running_mean, r.running_mean, 1e-4, 1e-4, "running_mean")
+        _close(bn.running_var, r.running_var, 1e-3, 1e-3, "running_var")
+        assert int(bn.num_batches_tracked) == 1
+    dy = torch.randn(y.shape, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    y.backward(dy)
+    pre.backward(torch.where(y.float() > 0, dy.float(), 0.0))
+    _close(a.grad, ar.grad, 3e-2, 3e-2, "dxa")
+    _close(b.grad, br.grad, 3e-2, 3e-2, "dxb")
+    M = N * H * W
+    for bn, r in zip(bns, refs):
+        _close(bn.weight.grad, r.weight.grad, 0.05 + 1e-3 * M ** 0.5, 1e-2, "dgamma")
+        _close(bn.bias.grad, r.bias.grad, 0.05 + 1e-3 * M ** 0.5, 1e-2, "dbeta")
