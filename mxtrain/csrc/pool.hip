@@ -19,13 +19,25 @@ constexpr int kThreads = 256;
 
 __global__ __launch_bounds__(kThreads) void maxpool3s2_fwd_kernel(const uint16_t* __restrict__ x,
                                                                   uint16_t* __restrict__ y, uint8_t* __restrict__ arg,
-                                                                  int N, int H, int W, int C, int OH, int OW) {
+                                                                  int N, int H, int W, int C, int OH, int OW,
+                                                                  const float* __restrict__ bn_scale,
+                                                                  const float* __restrict__ bn_shift) {
   // one workgroup per output row (n, oh): 32-bit index math only (the 64-bit divisions of a
   // flat index cost more VALU time than the pass's memory traffic)
   const int c8 = C / 8;
   const int n = blockIdx.x / OH, oh = blockIdx.x - (blockIdx.x / OH) * OH;
   for (int e = threadIdx.x; e < OW * c8; e += kThreads) {
     const int ow = e / c8, cv = e - (e / c8) * c8;
+    // (bn_scale: the input is a BN's raw input, relu(x scale + shift) applied on load -- the
+    // stem's BN + ReLU output tensor is never written)
+    float sc[8], sh[8];
+    if (bn_scale) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sc[j] = bn_scale[8 * cv + j];
+        sh[j] = bn_shift[8 * cv + j];
+      }
+    }
     float m[8];
     uint32_t idx[8];
 #pragma unroll
@@ -43,6 +55,10 @@ __global__ __launch_bounds__(kThreads) void maxpool3s2_fwd_kernel(const uint16_t
         if ((unsigned)iw >= (unsigned)W) continue;
         float f[8];
         unpack8(reinterpret_cast<const uint4*>(x + (((size_t)n * H + ih) * W + iw) * C)[cv], f);
+        if (bn_scale) {   // (rounded to bf16 as the separate BN pass would store it)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = bf2f(f2bf(fmaxf(__builtin_fmaf(f[j], sc[j], sh[j]), 0.f)));
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (f[j] > m[j] || f[j] != f[j]) {   // (NaN propagates, as torch)
@@ -63,7 +79,8 @@ __global__ __launch_bounds__(kThreads) void maxpool3s2_fwd_kernel(const uint16_t
 __global__ __launch_bounds__(kThreads) void maxpool3s2_bwd_kernel(const uint16_t* __restrict__ dy,
                                                                   const uint8_t* __restrict__ arg,
                                                                   uint16_t* __restrict__ dx, int N, int H, int W,
-                                                                  int C, int OH, int OW) {
+                                                                  int C, int OH, int OW,
+                                                                  const uint16_t* __restrict__ ypool) {
   const int c8 = C / 8;
   const int n = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H;   // one input row per workgroup
   for (int e = threadIdx.x; e < W * c8; e += kThreads) {
@@ -85,6 +102,12 @@ __global__ __launch_bounds__(kThreads) void maxpool3s2_bwd_kernel(const uint16_t
         const uint32_t me = (uint32_t)(kh * 3 + kw);
         float g[8];
         unpack8(*reinterpret_cast<const uint4*>(dy + o), g);
+        if (ypool) {   // the fused ReLU's gradient: zero where the window's max (the ReLU output) is 0
+          float yv[8];
+          unpack8(*reinterpret_cast<const uint4*>(ypool + o), yv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const uint32_t aj = ((j < 4 ? am.x : am.y) >> (8 * (j & 3))) & 0xffu;
@@ -104,7 +127,18 @@ MX_EXPORT int mx_maxpool3s2_fwd(const void* x, void* y, void* arg, int N, int H,
   const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
   if ((int64_t)N * OH >= ((int64_t)1 << 31) || (int64_t)OW * (C / 8) >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(maxpool3s2_fwd_kernel, dim3((unsigned)(N * OH)), dim3(kThreads), 0, s,
-                     (const uint16_t*)x, (uint16_t*)y, (uint8_t*)arg, N, H, W, C, OH, OW);
+                     (const uint16_t*)x, (uint16_t*)y, (uint8_t*)arg, N, H, W, C, OH, OW, nullptr, nullptr);
+  return hipGetLastError();
+}
+
+// the same pool of relu(x scale[c] + shift[c]) (fp32 [C] each): a training BN + ReLU folded in
+MX_EXPORT int mx_maxpool3s2_fwd_bn(const void* x, void* y, void* arg, int N, int H, int W, int C, const float* scale,
+                                   const float* shift, hipStream_t s) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || !scale || !shift) return hipErrorInvalidValue;
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  if ((int64_t)N * OH >= ((int64_t)1 << 31) || (int64_t)OW * (C / 8) >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(maxpool3s2_fwd_kernel, dim3((unsigned)(N * OH)), dim3(kThreads), 0, s, (const uint16_t*)x,
+                     (uint16_t*)y, (uint8_t*)arg, N, H, W, C, OH, OW, scale, shift);
   return hipGetLastError();
 }
 
@@ -114,7 +148,18 @@ MX_EXPORT int mx_maxpool3s2_bwd(const void* dy, const void* arg, void* dx, int N
   const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
   if ((int64_t)N * H >= ((int64_t)1 << 31) || (int64_t)W * (C / 8) >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(maxpool3s2_bwd_kernel, dim3((unsigned)(N * H)), dim3(kThreads), 0, s,
-                     (const uint16_t*)dy, (const uint8_t*)arg, (uint16_t*)dx, N, H, W, C, OH, OW);
+                     (const uint16_t*)dy, (const uint8_t*)arg, (uint16_t*)dx, N, H, W, C, OH, OW, nullptr);
+  return hipGetLastError();
+}
+
+// the backward through mx_maxpool3s2_fwd_bn's ReLU as well: ypool = its output
+MX_EXPORT int mx_maxpool3s2_bwd_relu(const void* dy, const void* arg, const void* ypool, void* dx, int N, int H,
+                                     int W, int C, hipStream_t s) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || !ypool) return hipErrorInvalidValue;
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  if ((int64_t)N * H >= ((int64_t)1 << 31) || (int64_t)W * (C / 8) >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(maxpool3s2_bwd_kernel, dim3((unsigned)(N * H)), dim3(kThreads), 0, s, (const uint16_t*)dy,
+                     (const uint8_t*)arg, (uint16_t*)dx, N, H, W, C, OH, OW, (const uint16_t*)ypool);
   return hipGetLastError();
 }
 

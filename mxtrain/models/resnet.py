@@ -21,7 +21,7 @@ import torch.nn.functional as F
 
 from . import compute_weights as _cw
 from ..ops import convwg
-from ..ops.batchnorm import bn2_add_relu, bn_act
+from ..ops.batchnorm import bn2_add_relu, bn_act, bn_relu_maxpool
 from ..ops.epilogue import BlockLink, ConvBiasActFn, conv_bias_act, fused_conv_ok, global_avg_pool, maxpool3s2
 
 
@@ -293,8 +293,13 @@ class ResNet(nn.Module):
     def forward_features(self, x, stem_done: bool = False) -> List[torch.Tensor]:
         """C2..C5; ``stem_done``: x is already the pooled stem output (ops/stem.py)."""
         if not stem_done:
-            x = self.stem(x)
-            x = maxpool3s2(x)   # (NHWC bf16: csrc/pool.hip; else F.max_pool2d(x, 3, 2, 1))
+            if self.stem.norm_kind == "bn" and self.stem.norm.training:
+                # stem BN + ReLU folded into pool0 (ops/batchnorm.py bn_relu_maxpool)
+                y, pre = self.stem.conv_pre(x)
+                x = bn_relu_maxpool(y, self.stem.norm, pre)
+            else:
+                x = self.stem(x)
+                x = maxpool3s2(x)   # (NHWC bf16: csrc/pool.hip; else F.max_pool2d(x, 3, 2, 1))
         outs = []
         for st in self.stages:
             x = st(x)

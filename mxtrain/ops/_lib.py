@@ -144,6 +144,8 @@ SIGNATURES = {
     "mx_subsample2": [P, P, I, I, I, I, I, P],
     "mx_maxpool3s2_fwd": [P, P, P, I, I, I, I, P],
     "mx_cast_multi": [P, I, I, P],
+    "mx_maxpool3s2_fwd_bn": [P, P, P, I, I, I, I, P, P, P],
+    "mx_maxpool3s2_bwd_relu": [P, P, P, P, I, I, I, I, P],
     "mx_gap_fwd": [P, P, I, I, I, P],
     "mx_gap_bwd": [P, P, I, I, I, P],
     "mx_sgd_multi": [P, I, P, F, F, I, P],

@@ -168,6 +168,71 @@ def bn2_add_relu(xa: torch.Tensor, bn_a: torch.nn.BatchNorm2d, xb: torch.Tensor,
 DUAL = True
 
 
+def _rows_per_block(M: int) -> int:   # (csrc/batchnorm.hip rows_per_block)
+    return max(64, (M + 511) // 512)
+
+
+class BNReluMaxPoolFn(torch.autograd.Function):
+    """max_pool2d(relu(BN(x)), 3, 2, 1) in training mode -- the ResNet stem's BN, ReLU and pool0
+    -- without the BN + ReLU output tensor: the statistics pass and finalize (mx_bn_fwd with
+    y = null), then the pool reads x and applies relu(x scale + shift) on load
+    (csrc/pool.hip mx_maxpool3s2_fwd_bn); backward the pool's gather masks the ReLU from the
+    pooled output (mx_maxpool3s2_bwd_relu) and a plain BN backward reads dz and x."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, bufs):
+        rm, rv, mom, eps, nbt, pre = bufs
+        N, C, H, W = x.shape
+        M = N * H * W
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        g32 = gamma.detach().float().contiguous()
+        b32 = beta.detach().float().contiguous()
+        scratch = _scratch(M, C, x.device)
+        _lib.call("mx_bn_fwd", x.data_ptr(), 0, 0, g32.data_ptr(), b32.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                  _lib.ptr(rm), _lib.ptr(rv), M, C, float(eps), float(mom), 0, scratch.data_ptr(), _lib.ptr(nbt),
+                  _lib.ptr(pre), _lib.stream())
+        rpb = _rows_per_block(M)
+        off = 2 * ((M + rpb - 1) // rpb) * C   # scale, shift follow the partials (mx_bn_fwd)
+        OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y = torch.empty((N, OH, OW, C), dtype=x.dtype, device=x.device)
+        arg = torch.empty((N, OH, OW, C), dtype=torch.uint8, device=x.device)
+        _lib.call("mx_maxpool3s2_fwd_bn", x.data_ptr(), y.data_ptr(), arg.data_ptr(), N, H, W, C,
+                  scratch[off:].data_ptr(), scratch[off + C:].data_ptr(), _lib.stream())
+        ctx.save_for_backward(x, y, arg, mean, rstd, g32, b32)
+        ctx.pdtypes = (gamma.dtype, beta.dtype)
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y, arg, mean, rstd, g32, b32 = ctx.saved_tensors
+        N, C, H, W = x.shape
+        M = N * H * W
+        g = g.contiguous(memory_format=torch.channels_last)
+        dz = torch.empty((N, H, W, C), dtype=x.dtype, device=x.device)
+        _lib.call("mx_maxpool3s2_bwd_relu", g.data_ptr(), arg.data_ptr(), y.data_ptr(), dz.data_ptr(), N, H, W, C,
+                  _lib.stream())
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dg = torch.empty(C, dtype=torch.float32, device=x.device)
+        db = torch.empty_like(dg)
+        _lib.call("mx_bn_bwd", dz.data_ptr(), 0, x.data_ptr(), mean.data_ptr(), rstd.data_ptr(), g32.data_ptr(),
+                  dx.data_ptr(), 0, dg.data_ptr(), db.data_ptr(), 0, M, C, 0, _scratch(M, C, x.device).data_ptr(),
+                  b32.data_ptr(), 0, _lib.stream())
+        return dx, dg.to(ctx.pdtypes[0]), db.to(ctx.pdtypes[1]), None
+
+
+def bn_relu_maxpool(x: torch.Tensor, bn: torch.nn.BatchNorm2d, pre: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """max_pool2d(relu(bn(x)), 3, 2, 1): one fused node in training mode on the HIP path."""
+    from .epilogue import maxpool3s2
+    if POOL_FOLD and bn.training and supported(x) and x.dtype == torch.bfloat16 and x.data_ptr() % 16 == 0:
+        return BNReluMaxPoolFn.apply(x, bn.weight, bn.bias, _bufs(bn, pre))
+    return maxpool3s2(bn_act(x, bn, None, True, pre=pre))
+
+
+# (+0.9 % ResNet-50 img/s through the launcher: profiles/r6/resnet_launcher_ab_stem_bn_pool_fold.txt)
+POOL_FOLD = True
+
+
 def bn_act_ref(x, gamma, beta, residual, running_mean, running_var, momentum, eps, relu, training=True):
     """The same op in plain torch (fp32 math): the CPU path and the tests' reference."""
     y = F.batch_norm(x.float(), running_mean, running_var, gamma.float(), beta.float(), training, momentum, eps)

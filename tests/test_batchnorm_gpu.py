@@ -409,3 +409,41 @@ def test_bn2_add_relu_matches_fp32(N, C, H, W):
     for bn, r in zip(bns, refs):
         _close(bn.weight.grad, r.weight.grad, 0.05 + 1e-3 * M ** 0.5, 1e-2, "dgamma")
         _close(bn.bias.grad, r.bias.grad, 0.05 + 1e-3 * M ** 0.5, 1e-2, "dbeta")
+
+
+@pytest.mark.parametrize("N,C,H,W", [(8, 64, 56, 56), (3, 16, 13, 11)])
+def test_bn_relu_maxpool_fold_matches_separate(N, C, H, W):
+    """ops/batchnorm.py bn_relu_maxpool (the stem's BN + ReLU folded into pool0, csrc/pool.hip
+    mx_maxpool3s2_fwd_bn / _bwd_relu): the same output bits and running statistics as
+    bn_act + maxpool3s2, input / gamma / beta gradients as close to fp32 as theirs."""
+    from mxtrain.ops.batchnorm import BNReluMaxPoolFn, bn_act, bn_relu_maxpool
+    from mxtrain.ops.epilogue import maxpool3s2
+    g = torch.Generator(device=DEV).manual_seed(C + H)
+    x = (torch.randn(N, C, H, W, device=DEV, generator=g) * 2 - 0.3).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    bn = torch.nn.BatchNorm2d(C).to(DEV)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5, generator=g)
+        bn.bias.uniform_(-0.5, 0.5, generator=g)
+    bns = [copy_bn for copy_bn in (torch.nn.BatchNorm2d(C).to(DEV) for _ in range(3))]
+    for b in bns:
+        b.load_state_dict(bn.state_dict())
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ya = bn_relu_maxpool(xa, bns[0])
+    assert type(ya.grad_fn).__name__.startswith(BNReluMaxPoolFn.__name__)
+    yb = maxpool3s2(bn_act(xb, bns[1], None, True))
+    assert torch.equal(ya, yb)
+    assert torch.equal(bns[0].running_mean, bns[1].running_mean) and torch.equal(bns[0].running_var, bns[1].running_var)
+    assert int(bns[0].num_batches_tracked) == 1
+    xr = x.float().requires_grad_(True)
+    yr = F.max_pool2d(torch.relu(bns[2](xr)), 3, 2, 1)
+    dy = torch.randn(ya.shape, device=DEV, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ya.backward(dy)
+    yb.backward(dy)
+    yr.backward(dy.float())
+    for name, a, b, r in (("dx", xa.grad, xb.grad, xr.grad), ("dgamma", bns[0].weight.grad, bns[1].weight.grad,
+                                                                bns[2].weight.grad),
+                          ("dbeta", bns[0].bias.grad, bns[1].bias.grad, bns[2].bias.grad)):
+        ea = (a.float() - r).abs().max().item()
+        eb = (b.float() - r).abs().max().item()
+        assert ea <= 1.25 * eb + 1e-3 * r.abs().max().item(), (name, ea, eb)
