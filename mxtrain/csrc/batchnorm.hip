@@ -61,14 +61,14 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const uint16_t* __re
   int n = 0;
   if (vc < g.c8) {
     int r = r0 + g.tr;
-    // four rows' loads in flight per thread (narrow C -- the ResNet stem's 64 channels --
+    // eight rows' loads in flight per thread (narrow C -- the ResNet stem's 64 channels --
     // leaves one 16-B load per row group: one at a time the pass ran at ~2.4 TB/s)
-    for (; r + 3 * g.rpi < r1; r += 4 * g.rpi) {
-      uint4 w[4];
+    for (; r + 7 * g.rpi < r1; r += 8 * g.rpi) {
+      uint4 w[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) w[u] = reinterpret_cast<const uint4*>(x + (size_t)(r + u * g.rpi) * C)[vc];
+      for (int u = 0; u < 8; ++u) w[u] = reinterpret_cast<const uint4*>(x + (size_t)(r + u * g.rpi) * C)[vc];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         float v[8];
         unpack8(w[u], v);
 #pragma unroll
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const uint16_t* __re
           q[j] = __builtin_fmaf(v[j], v[j], q[j]);
         }
       }
-      n += 4;
+      n += 8;
     }
     for (; r < r1; r += g.rpi) {
       float v[8];

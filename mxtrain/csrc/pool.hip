@@ -176,6 +176,7 @@ __global__ __launch_bounds__(256) void gap_fwd_kernel(const uint16_t* __restrict
   const int n = (int)(v / c8), cv = (int)(v % c8);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const uint4* src = reinterpret_cast<const uint4*>(x + (size_t)n * HW * C) + cv;
+#pragma unroll 7
   for (int p = 0; p < HW; ++p) {
     float f[8];
     unpack8(src[(size_t)p * c8], f);
